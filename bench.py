@@ -1,0 +1,297 @@
+#!/usr/bin/env python3
+"""bench.py — publish-routing match throughput on MI355X.
+
+One "step" = one TopicsIndex.Subscribers pass (topics.go:484-555) of the HIP
+path over a batch of publish topics already resident in HBM, through the C ABI
+(mqm_match_device): tokenize -> walk -> dedupe -> CSR deliveries + shared
+candidates.  Workload (BASELINE.json `metric` is quoted "at 10M filters"):
+configs[2], 10M wildcard-heavy filters (40% '+', 10% '#', topics Zipf(1.2)
+over filter rank), 10M-topic batch, synthetic (tools/mqgen, seed 0x4D510003).
+
+N > 1 (torchrun, one rank per GPU, RCCL): --mode replicas (default) gives
+every rank the full trie and its own 10M-topic batch (weak scaling, no
+data-path collective); --mode sharded splits the subscribers by client range,
+RCCL-broadcasts rank 0's batch and gathers per-topic delivery counts back.
+
+Rank 0 prints ONE JSON line.  `roofline.achieved` = algorithmic bytes of the
+emit kernel (B = T + 8N + 8P + 8V + 8S + 8D, per-topic walk
+counters from the oracle on the CPU sample) / its average HIP-event time.
+`cpu_baseline` = oracle/mochi_ref.c (C restatement of the reference matcher,
+kind "port") on this host's cores over a time-bounded sample of the batch.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", type=int, default=3, help="BASELINE configs index + 1 (mqgen config)")
+    ap.add_argument("--filters", type=int, default=0, help="override n_filters")
+    ap.add_argument("--topics", type=int, default=0, help="override n_topics")
+    ap.add_argument("--mode", choices=["replicas", "sharded"], default="replicas")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="PMC-derived HBM bytes per emit launch (profiles/run_pmc.sh)")
+    return ap.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    args = parse()
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    import maxmq_amd
+    from tools import mqgen
+
+    overrides = {}
+    if args.filters:
+        overrides["n_filters"] = args.filters
+    if args.topics:
+        overrides["n_topics"] = args.topics
+    t0 = time.time()
+    w = mqgen.generate(args.config, **overrides)
+    n = len(w.topics)
+    log(f"[rank {rank}] generated {len(w.filters)} filters / {n} topics in {time.time() - t0:.1f}s")
+
+    # ---- build the index (host store -> snapshot -> HBM) -------------------------------
+    t0 = time.time()
+    idx = maxmq_amd.TopicsIndex(device=local, autocommit=False)
+    if args.mode == "sharded" and world > 1:
+        ncl = int(w.client_ids.max()) + 1
+        lo, hi = rank * ncl // world, (rank + 1) * ncl // world
+        keep = np.nonzero((w.client_ids >= lo) & (w.client_ids < hi))[0]
+        shard = _subset_workload(w, keep)
+        idx.subscribe_workload(shard)
+    else:
+        idx.subscribe_workload(w)
+    idx.commit()
+    snap = idx.snapshot_stats()
+    log(f"[rank {rank}] index built in {time.time() - t0:.1f}s: {snap}")
+
+    tb = torch.from_numpy(w.topics.data).to(dev)
+    to = torch.from_numpy(w.topics.offs.view(np.int64)).to(dev)
+    stream = torch.cuda.current_stream(dev)
+    counts = None
+    if args.mode == "sharded" and world > 1:
+        counts = torch.zeros(n, dtype=torch.int64, device=dev)
+
+    def step():
+        if args.mode == "sharded" and world > 1:
+            # the publish batch enters at rank 0 and is broadcast over xGMI
+            dist.broadcast(tb, src=0)
+            dist.broadcast(to, src=0)
+        r = idx.match_device(tb.data_ptr(), to.data_ptr(), n, stream.cuda_stream)
+        if args.mode == "sharded" and world > 1:
+            # per-topic delivery counts of every shard, gathered at rank 0
+            offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+            _dev_to_tensor(r.offsets, offs)
+            torch.diff(offs, out=counts)
+            dist.reduce(counts, dst=0)
+        return r
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    idx.profile(True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    deliveries = 0
+    shared = 0
+    fallback = 0
+    for _ in range(args.steps):
+        r = step()
+        deliveries += int(r.n_deliveries)
+        shared += int(r.n_shared)
+        fallback = int(r.n_fallback)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    prof = idx.profile_read()
+    idx.profile(False)
+    if dist:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        dsum = torch.tensor([deliveries, shared], dtype=torch.float64, device=dev)
+        dist.all_reduce(dsum)
+        deliveries, shared = int(dsum[0].item()), int(dsum[1].item())
+
+    if args.mode == "sharded" and world > 1:
+        topics_total = n * args.steps  # every shard walks the same batch
+    else:
+        topics_total = n * args.steps * world
+    value = topics_total / dt
+    out = None
+    if rank == 0:
+        emit_ms = prof["emit_ms"] / max(prof["calls"], 1)
+        count_ms = prof["count_ms"] / max(prof["calls"], 1)
+        cpu = None
+        stats = None
+        if not args.no_cpu_baseline:
+            cpu, stats = cpu_baseline(w, args)
+        roof = roofline(stats, n, emit_ms, args.traffic_json)
+        out = {
+            "metric": "publish topics matched/sec (node) + matched deliveries/sec at 10M filters",
+            "value": value,
+            "unit": "topics/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak" if args.mode == "replicas" else "strong",
+            "vs_baseline": None,
+            "dtype": "u8/u32 (byte+integer matching)",
+            "data": "synthetic (tools/mqgen, deterministic seed); inputs resident in HBM",
+            "config": {
+                "workload": f"mqgen config {args.config}: {len(w.filters)} filters "
+                            f"({w.params['p_plus']:.0%} '+', {w.params['p_hash']:.0%} '#', "
+                            f"topic Zipf s={w.params['topic_zipf_s']}), {n}-topic batch, depth<={w.params['max_depth']}",
+                "filters": len(w.filters),
+                "topics_per_batch": n,
+                "parallelism": f"{args.mode}{world}",
+            },
+            "deliveries_per_s": deliveries / dt,
+            "shared_candidates_per_s": shared / dt,
+            "deliveries_per_topic": deliveries / max(topics_total, 1),
+            "fallback_topics_per_batch": fallback,
+            "kernel_ms": {"count": count_ms, "emit": emit_ms, "between": prof["between_ms"] / max(prof["calls"], 1),
+                          "total": prof["total_ms"] / max(prof["calls"], 1)},
+            "snapshot": snap,
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _subset_workload(w, keep):
+    from tools.mqgen import Strings
+
+    def sub_strings(s):
+        items = [bytes(s.data[s.offs[i]:s.offs[i + 1]]) for i in keep]
+        return Strings.from_list(items)
+
+    class W:
+        pass
+
+    o = W()
+    o.filters, o.clients = sub_strings(w.filters), sub_strings(w.clients)
+    for k in ("qos", "no_local", "rap", "rh", "ident", "client_ids"):
+        setattr(o, k, getattr(w, k)[keep])
+    return o
+
+
+def _dev_to_tensor(ptr, t):
+    """copy a device buffer owned by the library into tensor t (device to device)."""
+    import ctypes
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    nbytes = t.numel() * t.element_size()
+    rc = hip.hipMemcpy(ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(ptr), ctypes.c_size_t(nbytes),
+                       ctypes.c_int(3))
+    if rc != 0:
+        raise RuntimeError(f"hipMemcpy D2D failed: {rc}")
+
+
+def cpu_baseline(w, args):
+    """oracle/mochi_ref.c over a time-bounded sample (chunks of the same batch,
+    from the front) on this host's cores; index build excluded."""
+    from oracle.binding import OracleIndex
+
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    t0 = time.time()
+    ora = OracleIndex()
+    ora.subscribe_workload(w)
+    build_s = time.time() - t0
+    data, offs = w.topics.data, w.topics.offs
+    n = len(offs) - 1
+    chunk = 20000
+    done = 0
+    busy = 0.0
+    tot = None
+    while done < n and busy < args.cpu_seconds:
+        hi = min(n, done + chunk)
+        o = (offs[done:hi + 1] - offs[done]).astype(np.uint64)
+        d = data[int(offs[done]):int(offs[hi])]
+        t1 = time.perf_counter()
+        _, _, st = ora.match_counts(d, o, nthreads=threads)
+        busy += time.perf_counter() - t1
+        tot = st if tot is None else {k: tot[k] + st[k] for k in tot}
+        done = hi
+        chunk = min(chunk * 2, 400000)
+    ora.close()
+    cpu = {
+        "value": done / busy,
+        "unit": "topics/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"first {done} topics of the batch ({busy:.1f}s of matching, index build {build_s:.0f}s "
+                  f"excluded); C restatement of mochi v2.2.12 TopicsIndex (oracle/mochi_ref.c); Go toolchain "
+                  f"unavailable",
+        "deliveries_per_s": tot["deliveries"] / busy,
+    }
+    return cpu, tot
+
+
+def roofline(stats, n, emit_ms, traffic_json):
+    """B = T + 8N + 8P + 8V + 8S + 8D algorithmic bytes."""
+    if not stats or not stats["topics"] or emit_ms <= 0:
+        return {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+                "traffic": None}
+    k = stats["topics"]
+    per_topic = (stats["topic_bytes"] + 8 * k + 8 * stats["probes"] + 8 * stats["visits"] + 8 * stats["gathered"] +
+                 8 * stats["deliveries"]) / k
+    bytes_per_launch = per_topic * n
+    achieved = bytes_per_launch / (emit_ms * 1e-3) / 1e9
+    traffic = None
+    if traffic_json and os.path.exists(traffic_json):
+        try:
+            with open(traffic_json) as fh:
+                traffic = json.load(fh).get("hbm_bytes_per_emit_launch")
+        except Exception:
+            traffic = None
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "algorithmic_bytes_per_topic": per_topic, "kernel": "k_match<emit>"}
+
+
+if __name__ == "__main__":
+    main()

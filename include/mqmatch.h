@@ -1,0 +1,180 @@
+/*
+ * mqmatch.h — C ABI of the MI355X-native MQTT publish-routing matcher.
+ *
+ * Drop-in boundary for mochi-co/mqtt v2.2.12 `TopicsIndex` as vendored by
+ * gsalomao/maxmq (reference paths below are relative to
+ * vendor/github.com/mochi-co/mqtt/v2/).  The reference exposes a concrete Go
+ * type reached through `Server.Topics *TopicsIndex` (server.go:111, created at
+ * server.go:149); a cgo shim implements that type's method set over these
+ * functions.
+ *
+ * Conventions
+ *   - Every function returns an int status (MQM_OK == 0, < 0 on error) and
+ *     never aborts across the ABI.  Boolean/int64 results of the reference
+ *     methods come back through out-parameters.
+ *   - Strings are (pointer, length) byte ranges, borrowed for the call.
+ *   - Client ids and filter ids are dense uint32 values assigned in order of
+ *     first appearance in mqm_subscribe (stable for the index's lifetime).
+ *   - Mutations go to the host-authoritative store; matching reads the last
+ *     committed GPU snapshot (mqm_commit).  With MQM_CFG_AUTOCOMMIT a match
+ *     first commits pending mutations, giving the reference's
+ *     read-your-writes visibility (topics.go takes no snapshot at all).
+ *   - The match path runs on the GPU only.  There is no CPU fallback: without
+ *     a usable HIP device mqm_create fails with MQM_ENODEV.
+ */
+#ifndef MQMATCH_H
+#define MQMATCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MQM_OK 0
+#define MQM_EINVAL -1  /* bad handle / argument                               */
+#define MQM_ENOMEM -2  /* host or device allocation failed                      */
+#define MQM_EHIP -3    /* HIP runtime error                                     */
+#define MQM_ELIMIT -4  /* a documented capacity limit was exceeded              */
+#define MQM_ENODEV -5  /* no HIP device                                         */
+
+#define MQM_CFG_AUTOCOMMIT 1u
+/* device value for a host-only index: the store and its mutation API work,
+ * mqm_commit / mqm_match_* return MQM_ENODEV (there is no CPU match path). */
+#define MQM_DEVICE_NONE (-1)
+
+typedef struct mqm_index mqm_index;   /* replaces *TopicsIndex               */
+typedef struct mqm_result mqm_result; /* one batch's host-side match result   */
+
+typedef struct {
+  int device;     /* HIP device ordinal, or MQM_DEVICE_NONE                    */
+  uint32_t flags; /* MQM_CFG_*                                                 */
+} mqm_config;
+
+/* packets.Subscription fields the index reads (packets/packets.go:168-178) */
+typedef struct {
+  uint8_t qos;                 /* 0..2 (SubscribeDecode enforces, :953)        */
+  uint8_t no_local;            /* MQTT 5 No Local                              */
+  uint8_t retain_as_published; /* MQTT 5 RAP                                   */
+  uint8_t retain_handling;     /* MQTT 5 RH (0..2)                             */
+  int32_t identifier;          /* subscription identifier (0 = none)          */
+} mqm_subscription;
+
+/* One merged non-shared delivery (topics.go:531-536 + packets.go:250-270).
+ *   client   : interned client id
+ *   packed   : first_sub (bits 0..27) | qos << 28 (2 bits) | no_local << 30
+ *              first_sub names the first-merged subscription; resolve it with
+ *              mqm_result_sub_info. */
+typedef struct {
+  uint32_t client;
+  uint32_t packed;
+} mqm_delivery;
+
+#define MQM_DELIVERY_SUB(p) ((p) & 0x0FFFFFFFu)
+#define MQM_DELIVERY_QOS(p) (((p) >> 28) & 3u)
+#define MQM_DELIVERY_NOLOCAL(p) (((p) >> 30) & 1u)
+
+typedef struct {
+  uint32_t filter;             /* filter id                                    */
+  uint32_t client;             /* client id                                    */
+  int32_t identifier;
+  uint8_t qos, no_local, retain_as_published, retain_handling;
+} mqm_sub_info;
+
+/* Device-resident result of mqm_match_device (library-owned; valid until the
+ * next match call on the same index). */
+typedef struct {
+  uint32_t n_topics;
+  uint64_t n_deliveries;
+  uint64_t n_shared;
+  const uint64_t *offsets;        /* device, n_topics + 1                       */
+  const mqm_delivery *deliveries; /* device                                     */
+  const uint64_t *shared_offsets; /* device, n_topics + 1                       */
+  const uint32_t *shared;         /* device: shared-subscription ids            */
+  uint32_t n_fallback;            /* topics routed through the unbounded path   */
+} mqm_device_result;
+
+/* ---- lifecycle: NewTopicsIndex (topics.go:291-299) ---------------------- */
+int mqm_create(const mqm_config *cfg, mqm_index **out);
+int mqm_destroy(mqm_index *h);
+
+/* ---- mutation ----------------------------------------------------------- */
+/* TopicsIndex.Subscribe (topics.go:303-321): *is_new = !existed */
+int mqm_subscribe(mqm_index *h, const char *client, size_t client_len, const char *filter, size_t filter_len,
+                  const mqm_subscription *sub, int *is_new);
+/* bulk form of the above for store reload (server.go:1377-1393); is_new may be NULL */
+int mqm_subscribe_many(mqm_index *h, size_t n, const char *client_bytes, const uint64_t *client_offs,
+                       const char *filter_bytes, const uint64_t *filter_offs, const mqm_subscription *subs,
+                       uint8_t *is_new);
+/* TopicsIndex.Unsubscribe (topics.go:325-349): *existed = the reference's bool */
+int mqm_unsubscribe(mqm_index *h, const char *filter, size_t filter_len, const char *client, size_t client_len,
+                    int *existed);
+/* TopicsIndex.RetainMessage (topics.go:354-377); message_ref is the caller's
+ * handle for the packet; payload_len == 0 deletes.  *result = 1 / 0 / -1. */
+int mqm_retain_message(mqm_index *h, const char *topic, size_t topic_len, uint64_t message_ref,
+                       uint32_t payload_len, int retain_flag, int64_t *result);
+/* Retained.Len() (packets.go:103) */
+int mqm_retained_len(mqm_index *h, uint64_t *out);
+
+/* publish the current store as the GPU snapshot (double-buffered) */
+int mqm_commit(mqm_index *h);
+
+/* ---- forward match: TopicsIndex.Subscribers (topics.go:484-555) --------- */
+/* Host in / host out.  Topic i is bytes[offsets[i] .. offsets[i+1]). */
+int mqm_match_batch(mqm_index *h, const char *topic_bytes, const uint64_t *topic_offsets, uint32_t n_topics,
+                    mqm_result **out);
+/* single-topic convenience == Subscribers(topic) */
+int mqm_subscribers(mqm_index *h, const char *topic, size_t topic_len, mqm_result **out);
+/* Device in / device out on `hip_stream` (hipStream_t, NULL = default stream). */
+int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t *d_topic_offsets,
+                     uint32_t n_topics, void *hip_stream, mqm_device_result *out);
+
+/* ---- result accessors --------------------------------------------------- */
+uint32_t mqm_result_num_topics(const mqm_result *r);
+const uint64_t *mqm_result_offsets(const mqm_result *r);          /* n + 1          */
+const mqm_delivery *mqm_result_deliveries(const mqm_result *r);
+const uint64_t *mqm_result_shared_offsets(const mqm_result *r);   /* n + 1          */
+const uint32_t *mqm_result_shared(const mqm_result *r);           /* shared sub ids */
+/* resolve a delivery's first_sub / a shared sub id (snapshot-relative) */
+int mqm_result_sub_info(const mqm_result *r, uint32_t sub, mqm_sub_info *out);
+int mqm_result_shared_info(const mqm_result *r, uint32_t shared_sub, mqm_sub_info *out);
+/* batch forms: resolve n ids at once (shared != 0 selects the shared table) */
+int mqm_result_sub_infos(const mqm_result *r, int shared, const uint32_t *subs, size_t n, mqm_sub_info *out);
+void mqm_result_free(mqm_result *r);
+
+/* ---- names -------------------------------------------------------------- */
+/* copy up to cap bytes of the name into buf; *len = full length */
+int mqm_client_name(mqm_index *h, uint32_t client, char *buf, size_t cap, size_t *len);
+int mqm_filter_name(mqm_index *h, uint32_t filter, char *buf, size_t cap, size_t *len);
+int mqm_num_clients(mqm_index *h, uint32_t *out);
+
+/* ---- admission helpers (topics.go:580-624) ------------------------------ */
+int mqm_is_valid_filter(const char *filter, size_t len, int for_publish); /* IsValidFilter  */
+int mqm_is_shared_filter(const char *filter, size_t len);                  /* IsSharedFilter */
+
+/* ---- stats for the roofline (per committed snapshot) -------------------- */
+typedef struct {
+  uint64_t nodes, edges, edge_buckets, subs, shared, height;
+  uint64_t device_bytes; /* HBM bytes held by the current snapshot */
+} mqm_snapshot_stats;
+int mqm_snapshot_stats_get(mqm_index *h, mqm_snapshot_stats *out);
+
+/* ---- kernel timing (HIP events on the launch stream) --------------------- */
+typedef struct {
+  uint64_t calls;           /* match calls while enabled                        */
+  uint64_t fallback_topics; /* topics that took the unbounded path              */
+  double count_ms;          /* walk + dedupe, count pass (k_match<false>)        */
+  double emit_ms;           /* walk + dedupe + write pass (k_match<true>)        */
+  double between_ms;        /* scans, fallback phases 0-2 and host syncs between */
+  double total_ms;          /* first to last kernel of each call, summed          */
+} mqm_profile;
+int mqm_profile_enable(mqm_index *h, int on); /* resets the accumulators */
+int mqm_profile_read(mqm_index *h, mqm_profile *out);
+
+const char *mqm_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MQMATCH_H */

@@ -1,0 +1,298 @@
+"""maxmq_amd — MI355X-native MQTT publish-routing matcher.
+
+Python host mirror of the reference's ``TopicsIndex`` API
+(vendor/github.com/mochi-co/mqtt/v2/topics.go:284-624 in gsalomao/maxmq) over
+the C ABI in include/mqmatch.h.  Method names, argument meaning and return
+values follow the reference:
+
+    idx = TopicsIndex()                       # NewTopicsIndex  (topics.go:291)
+    idx.subscribe("cl1", Subscription("a/+", qos=1))   -> bool (topics.go:303)
+    idx.unsubscribe("a/+", "cl1")             -> bool           (topics.go:325)
+    idx.retain_message(topic, ref, payload_len, retain=True) -> 1/0/-1 (:354)
+    idx.subscribers("a/b")                    -> Subscribers    (topics.go:484)
+    idx.match_batch(bytes, offsets)           -> BatchResult    (GPU batch)
+
+Matching runs only on the GPU (libmqmatch.so); there is no Python or CPU
+match path.  Without a device, ``TopicsIndex(device=None)`` still offers the
+host store (mutation semantics) and raises on matching.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import capi
+from .capi import MqmError, b, check, lib
+
+__all__ = ["TopicsIndex", "Subscription", "Subscribers", "BatchResult", "MqmError", "is_valid_filter",
+           "is_shared_filter"]
+
+
+@dataclass
+class Subscription:
+    """packets.Subscription (packets/packets.go:168-178)."""
+
+    filter: str
+    qos: int = 0
+    identifier: int = 0
+    no_local: bool = False
+    retain_as_published: bool = False
+    retain_handling: int = 0
+    identifiers: dict | None = None
+
+    def _c(self):
+        return capi.Subscription(self.qos, int(self.no_local), int(self.retain_as_published),
+                                 self.retain_handling, self.identifier)
+
+
+@dataclass
+class Subscribers:
+    """Subscribers (topics.go:248-252): merged non-shared subscriptions keyed by
+    client, and shared subscriptions keyed by filter then client."""
+
+    subscriptions: dict = field(default_factory=dict)
+    shared: dict = field(default_factory=dict)
+    shared_selected: dict = field(default_factory=dict)
+
+    def select_shared(self):
+        """SelectShared (topics.go:255-268) with a deterministic policy: the
+        lowest client id of each shared filter (the reference picks the first
+        Go-map iteration entry, i.e. an arbitrary one)."""
+        self.shared_selected = {}
+        for filt in sorted(self.shared):
+            subs = self.shared[filt]
+            client = min(subs)
+            sub = subs[client]
+            cur = self.shared_selected.get(client, sub)
+            self.shared_selected[client] = _merge(cur, sub)
+
+    def merge_shared_selected(self):
+        """MergeSharedSelected (topics.go:273-282)."""
+        for client, sub in self.shared_selected.items():
+            cur = self.subscriptions.get(client, sub)
+            self.subscriptions[client] = _merge(cur, sub)
+
+
+def _merge(s: Subscription, n: Subscription) -> Subscription:
+    """Subscription.Merge (packets/packets.go:250-270)."""
+    out = Subscription(s.filter, s.qos, s.identifier, s.no_local, s.retain_as_published, s.retain_handling,
+                       dict(s.identifiers) if s.identifiers is not None else {s.filter: s.identifier})
+    if n.identifier > 0:
+        out.identifiers[n.filter] = n.identifier
+    out.qos = max(out.qos, n.qos)
+    out.no_local = out.no_local or n.no_local
+    return out
+
+
+class BatchResult:
+    """Host copy of one batch's CSR result (mqm_result)."""
+
+    def __init__(self, index: "TopicsIndex", handle):
+        L = lib()
+        self._index = index
+        self._h = handle
+        n = L.mqm_result_num_topics(handle)
+        self.n = n
+
+        def arr(ptr, count, dtype):
+            if count == 0 or not ptr:
+                return np.zeros(0, dtype)
+            return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_uint8)),
+                                         shape=(count * np.dtype(dtype).itemsize,)).view(dtype).copy()
+
+        self.offsets = arr(L.mqm_result_offsets(handle), n + 1, np.uint64)
+        self.shared_offsets = arr(L.mqm_result_shared_offsets(handle), n + 1, np.uint64)
+        nd = int(self.offsets[-1]) if n else 0
+        ns = int(self.shared_offsets[-1]) if n else 0
+        self.deliveries = arr(L.mqm_result_deliveries(handle), nd, capi.DELIVERY_DTYPE)
+        self.shared = arr(L.mqm_result_shared(handle), ns, np.uint32)
+
+    def close(self):
+        if self._h:
+            lib().mqm_result_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sub_info(self, sub: int) -> capi.SubInfo:
+        info = capi.SubInfo()
+        check("mqm_result_sub_info", lib().mqm_result_sub_info(self._h, sub, C.byref(info)))
+        return info
+
+    def shared_info(self, sub: int) -> capi.SubInfo:
+        info = capi.SubInfo()
+        check("mqm_result_shared_info", lib().mqm_result_shared_info(self._h, sub, C.byref(info)))
+        return info
+
+    def sub_infos(self, subs: np.ndarray, shared: bool = False) -> np.ndarray:
+        """Vectorised sub_info: -> structured array (capi.SUB_INFO_DTYPE)."""
+        subs = np.ascontiguousarray(subs, dtype=np.uint32)
+        out = np.zeros(len(subs), capi.SUB_INFO_DTYPE)
+        check("mqm_result_sub_infos", lib().mqm_result_sub_infos(
+            self._h, int(shared), subs.ctypes.data_as(C.c_void_p), len(subs), out.ctypes.data_as(C.c_void_p)))
+        return out
+
+    def subscribers(self, i: int) -> Subscribers:
+        """Topic i's result in the reference's Subscribers shape (names
+        resolved; Identifiers holds the first-merged filter's identifier)."""
+        out = Subscribers()
+        first, qos, nl = capi.delivery_fields(self.deliveries["packed"][self.offsets[i]:self.offsets[i + 1]])
+        clients = self.deliveries["client"][self.offsets[i]:self.offsets[i + 1]]
+        for c, f, q, n in zip(clients, first, qos, nl):
+            info = self.sub_info(int(f))
+            fname = self._index.filter_name(info.filter)
+            out.subscriptions[self._index.client_name(int(c))] = Subscription(
+                fname, int(q), info.identifier, bool(n), bool(info.retain_as_published), info.retain_handling,
+                {fname: info.identifier})
+        for sid in self.shared[self.shared_offsets[i]:self.shared_offsets[i + 1]]:
+            info = self.shared_info(int(sid))
+            fname = self._index.filter_name(info.filter)
+            out.shared.setdefault(fname, {})[self._index.client_name(info.client)] = Subscription(
+                fname, info.qos, info.identifier, bool(info.no_local), bool(info.retain_as_published),
+                info.retain_handling)
+        return out
+
+
+class TopicsIndex:
+    """TopicsIndex (topics.go:285) backed by the MI355X matcher."""
+
+    def __init__(self, device: int | None = 0, autocommit: bool = True):
+        L = lib()
+        cfg = capi.Config(capi.MQM_DEVICE_NONE if device is None else device,
+                          capi.MQM_CFG_AUTOCOMMIT if autocommit else 0)
+        h = C.c_void_p()
+        check("mqm_create", L.mqm_create(C.byref(cfg), C.byref(h)))
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().mqm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- mutation -------------------------------------------------------------
+    def subscribe(self, client: str, sub: Subscription) -> bool:
+        c, f = b(client), b(sub.filter)
+        out = C.c_int()
+        cs = sub._c()
+        check("mqm_subscribe", lib().mqm_subscribe(self._h, c, len(c), f, len(f), C.byref(cs), C.byref(out)))
+        return bool(out.value)
+
+    def subscribe_workload(self, w) -> np.ndarray:
+        """Bulk Subscribe of a tools.mqgen.Workload in filter order; -> is_new[]."""
+        n = len(w.filters)
+        subs = np.zeros(n, dtype=np.dtype([("qos", "u1"), ("nl", "u1"), ("rap", "u1"), ("rh", "u1"),
+                                           ("ident", "<i4")]))
+        subs["qos"], subs["nl"], subs["rap"], subs["rh"], subs["ident"] = w.qos, w.no_local, w.rap, w.rh, w.ident
+        is_new = np.zeros(n, np.uint8)
+        p = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+        check("mqm_subscribe_many", lib().mqm_subscribe_many(
+            self._h, n, p(w.clients.data), p(w.clients.offs), p(w.filters.data), p(w.filters.offs), p(subs),
+            p(is_new)))
+        return is_new
+
+    def unsubscribe(self, filt: str, client: str) -> bool:
+        f, c = b(filt), b(client)
+        out = C.c_int()
+        check("mqm_unsubscribe", lib().mqm_unsubscribe(self._h, f, len(f), c, len(c), C.byref(out)))
+        return bool(out.value)
+
+    def retain_message(self, topic: str, message_ref: int, payload_len: int, retain: bool = True) -> int:
+        t = b(topic)
+        out = C.c_int64()
+        check("mqm_retain_message",
+              lib().mqm_retain_message(self._h, t, len(t), message_ref, payload_len, int(retain), C.byref(out)))
+        return int(out.value)
+
+    def retained_len(self) -> int:
+        out = C.c_uint64()
+        check("mqm_retained_len", lib().mqm_retained_len(self._h, C.byref(out)))
+        return int(out.value)
+
+    def commit(self):
+        check("mqm_commit", lib().mqm_commit(self._h))
+
+    # -- names ------------------------------------------------------------------
+    def _name(self, fn, i):
+        n = C.c_size_t()
+        check(fn, getattr(lib(), fn)(self._h, i, None, 0, C.byref(n)))
+        buf = C.create_string_buffer(max(n.value, 1))
+        check(fn, getattr(lib(), fn)(self._h, i, buf, n.value, C.byref(n)))
+        return buf.raw[: n.value].decode("utf-8", "surrogateescape")
+
+    def client_name(self, i: int) -> str:
+        return self._name("mqm_client_name", i)
+
+    def filter_name(self, i: int) -> str:
+        return self._name("mqm_filter_name", i)
+
+    def num_clients(self) -> int:
+        out = C.c_uint32()
+        check("mqm_num_clients", lib().mqm_num_clients(self._h, C.byref(out)))
+        return out.value
+
+    def profile(self, on: bool):
+        check("mqm_profile_enable", lib().mqm_profile_enable(self._h, int(on)))
+
+    def profile_read(self) -> dict:
+        p = capi.Profile()
+        check("mqm_profile_read", lib().mqm_profile_read(self._h, C.byref(p)))
+        return {n: getattr(p, n) for n, _ in capi.Profile._fields_}
+
+    def snapshot_stats(self) -> dict:
+        st = capi.SnapshotStats()
+        check("mqm_snapshot_stats_get", lib().mqm_snapshot_stats_get(self._h, C.byref(st)))
+        return {n: int(getattr(st, n)) for n, _ in capi.SnapshotStats._fields_}
+
+    # -- matching -------------------------------------------------------------------
+    def match_batch(self, data: np.ndarray, offs: np.ndarray) -> BatchResult:
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        h = C.c_void_p()
+        check("mqm_match_batch", lib().mqm_match_batch(
+            self._h, data.ctypes.data_as(C.c_void_p), offs.ctypes.data_as(C.c_void_p), len(offs) - 1,
+            C.byref(h)))
+        return BatchResult(self, h)
+
+    def subscribers(self, topic: str) -> Subscribers:
+        t = b(topic)
+        h = C.c_void_p()
+        check("mqm_subscribers", lib().mqm_subscribers(self._h, t, len(t), C.byref(h)))
+        r = BatchResult(self, h)
+        try:
+            return r.subscribers(0)
+        finally:
+            r.close()
+
+    def match_device(self, d_bytes_ptr: int, d_offs_ptr: int, n: int, stream_ptr: int = 0) -> capi.DeviceResult:
+        """Device-resident batch (pointers from e.g. torch tensors); the result's
+        device buffers are owned by the index and valid until the next match."""
+        out = capi.DeviceResult()
+        check("mqm_match_device", lib().mqm_match_device(self._h, C.c_void_p(d_bytes_ptr), C.c_void_p(d_offs_ptr),
+                                                         n, C.c_void_p(stream_ptr), C.byref(out)))
+        return out
+
+
+def is_valid_filter(filt: str, for_publish: bool) -> bool:
+    """IsValidFilter (topics.go:586-624)."""
+    f = b(filt)
+    return bool(lib().mqm_is_valid_filter(f, len(f), int(for_publish)))
+
+
+def is_shared_filter(filt: str) -> bool:
+    """IsSharedFilter (topics.go:580-583)."""
+    f = b(filt)
+    return bool(lib().mqm_is_shared_filter(f, len(f)))

@@ -1,0 +1,146 @@
+"""ctypes binding of the C ABI in include/mqmatch.h (maxmq_amd/_lib/libmqmatch.so).
+
+This is the binding a Python host would add (the Go host would use the cgo
+stub in INTEGRATION.md).  It loads the in-tree library and fails loudly if it
+is missing: there is no Python or CPU implementation of the match path.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libmqmatch.so")
+
+MQM_OK = 0
+MQM_EINVAL = -1
+MQM_ENOMEM = -2
+MQM_EHIP = -3
+MQM_ELIMIT = -4
+MQM_ENODEV = -5
+MQM_CFG_AUTOCOMMIT = 1
+MQM_DEVICE_NONE = -1
+
+ERRORS = {MQM_EINVAL: "EINVAL", MQM_ENOMEM: "ENOMEM", MQM_EHIP: "EHIP", MQM_ELIMIT: "ELIMIT",
+          MQM_ENODEV: "ENODEV"}
+
+# every function include/mqmatch.h declares (checked by tests/test_capi_symbols.py)
+EXPORTED = [
+    "mqm_create", "mqm_destroy", "mqm_subscribe", "mqm_subscribe_many", "mqm_unsubscribe",
+    "mqm_retain_message", "mqm_retained_len", "mqm_commit", "mqm_match_batch", "mqm_subscribers",
+    "mqm_match_device", "mqm_result_num_topics", "mqm_result_offsets", "mqm_result_deliveries",
+    "mqm_result_shared_offsets", "mqm_result_shared", "mqm_result_sub_info", "mqm_result_shared_info",
+    "mqm_result_sub_infos", "mqm_result_free", "mqm_client_name", "mqm_filter_name", "mqm_num_clients", "mqm_is_valid_filter",
+    "mqm_is_shared_filter", "mqm_snapshot_stats_get", "mqm_profile_enable", "mqm_profile_read", "mqm_version",
+]
+
+
+class MqmError(RuntimeError):
+    def __init__(self, fn, rc):
+        super().__init__(f"{fn} failed: {ERRORS.get(rc, rc)}")
+        self.rc = rc
+
+
+class Config(C.Structure):
+    _fields_ = [("device", C.c_int), ("flags", C.c_uint32)]
+
+
+class Subscription(C.Structure):
+    _fields_ = [("qos", C.c_uint8), ("no_local", C.c_uint8), ("retain_as_published", C.c_uint8),
+                ("retain_handling", C.c_uint8), ("identifier", C.c_int32)]
+
+
+class SubInfo(C.Structure):
+    _fields_ = [("filter", C.c_uint32), ("client", C.c_uint32), ("identifier", C.c_int32), ("qos", C.c_uint8),
+                ("no_local", C.c_uint8), ("retain_as_published", C.c_uint8), ("retain_handling", C.c_uint8)]
+
+
+class DeviceResult(C.Structure):
+    _fields_ = [("n_topics", C.c_uint32), ("n_deliveries", C.c_uint64), ("n_shared", C.c_uint64),
+                ("offsets", C.c_void_p), ("deliveries", C.c_void_p), ("shared_offsets", C.c_void_p),
+                ("shared", C.c_void_p), ("n_fallback", C.c_uint32)]
+
+
+class SnapshotStats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("nodes", "edges", "edge_buckets", "subs", "shared", "height",
+                                          "device_bytes")]
+
+
+class Profile(C.Structure):
+    _fields_ = [("calls", C.c_uint64), ("fallback_topics", C.c_uint64), ("count_ms", C.c_double),
+                ("emit_ms", C.c_double), ("between_ms", C.c_double), ("total_ms", C.c_double)]
+
+
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
+                           "(there is no non-HIP implementation of the match path)")
+    L = C.CDLL(LIB_PATH)
+    vp, sz, u32, u64, i32, cp = C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint64, C.c_int32, C.c_char_p
+    sigs = {
+        "mqm_create": ([C.POINTER(Config), C.POINTER(vp)], C.c_int),
+        "mqm_destroy": ([vp], C.c_int),
+        "mqm_subscribe": ([vp, cp, sz, cp, sz, C.POINTER(Subscription), C.POINTER(C.c_int)], C.c_int),
+        "mqm_subscribe_many": ([vp, sz, vp, vp, vp, vp, vp, vp], C.c_int),
+        "mqm_unsubscribe": ([vp, cp, sz, cp, sz, C.POINTER(C.c_int)], C.c_int),
+        "mqm_retain_message": ([vp, cp, sz, u64, u32, C.c_int, C.POINTER(C.c_int64)], C.c_int),
+        "mqm_retained_len": ([vp, C.POINTER(u64)], C.c_int),
+        "mqm_commit": ([vp], C.c_int),
+        "mqm_match_batch": ([vp, vp, vp, u32, C.POINTER(vp)], C.c_int),
+        "mqm_subscribers": ([vp, cp, sz, C.POINTER(vp)], C.c_int),
+        "mqm_match_device": ([vp, vp, vp, u32, vp, C.POINTER(DeviceResult)], C.c_int),
+        "mqm_result_num_topics": ([vp], u32),
+        "mqm_result_offsets": ([vp], vp),
+        "mqm_result_deliveries": ([vp], vp),
+        "mqm_result_shared_offsets": ([vp], vp),
+        "mqm_result_shared": ([vp], vp),
+        "mqm_result_sub_info": ([vp, u32, C.POINTER(SubInfo)], C.c_int),
+        "mqm_result_shared_info": ([vp, u32, C.POINTER(SubInfo)], C.c_int),
+        "mqm_result_sub_infos": ([vp, C.c_int, vp, sz, vp], C.c_int),
+        "mqm_result_free": ([vp], None),
+        "mqm_client_name": ([vp, u32, C.c_char_p, sz, C.POINTER(sz)], C.c_int),
+        "mqm_filter_name": ([vp, u32, C.c_char_p, sz, C.POINTER(sz)], C.c_int),
+        "mqm_num_clients": ([vp, C.POINTER(u32)], C.c_int),
+        "mqm_is_valid_filter": ([cp, sz, C.c_int], C.c_int),
+        "mqm_is_shared_filter": ([cp, sz], C.c_int),
+        "mqm_snapshot_stats_get": ([vp, C.POINTER(SnapshotStats)], C.c_int),
+        "mqm_profile_enable": ([vp, C.c_int], C.c_int),
+        "mqm_profile_read": ([vp, C.POINTER(Profile)], C.c_int),
+        "mqm_version": ([], C.c_char_p),
+    }
+    for name, (args, res) in sigs.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _LIB = L
+    return L
+
+
+def check(fn, rc):
+    if rc != MQM_OK:
+        raise MqmError(fn, rc)
+    return rc
+
+
+def b(s) -> bytes:
+    return s.encode("utf-8", "surrogateescape") if isinstance(s, str) else bytes(s)
+
+
+DELIVERY_DTYPE = np.dtype([("client", "<u4"), ("packed", "<u4")])
+SUB_INFO_DTYPE = np.dtype([("filter", "<u4"), ("client", "<u4"), ("identifier", "<i4"), ("qos", "u1"),
+                           ("no_local", "u1"), ("rap", "u1"), ("rh", "u1")])
+
+
+def delivery_fields(packed: np.ndarray):
+    """-> (first_sub, qos, no_local) arrays from the packed word (mqmatch.h)."""
+    packed = packed.astype(np.uint32, copy=False)
+    return packed & 0x0FFFFFFF, (packed >> 28) & 3, (packed >> 30) & 1

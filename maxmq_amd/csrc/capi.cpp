@@ -1,0 +1,365 @@
+// maxmq_amd/csrc/capi.cpp — the C ABI (include/mqmatch.h) over the host
+// store, the snapshot builder and the HIP match pipeline.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <string_view>
+#include <vector>
+
+#include "../../include/mqmatch.h"
+#include "flatten.h"
+#include "match.h"
+#include "store.h"
+
+using namespace mqm;
+
+struct mqm_index {
+  mqm_config cfg{};
+  std::mutex mu;  // serialises mutations, commits and matches on this index
+  Store store;
+  std::unique_ptr<GpuSnapshot> snap;
+  uint64_t snap_version = ~0ull;
+  Workspace ws;
+  hipStream_t stream = nullptr;
+};
+
+struct mqm_result {
+  uint32_t n = 0;
+  std::vector<uint64_t> offsets, shared_offsets;
+  std::vector<mqm_delivery> deliveries;
+  std::vector<uint32_t> shared;
+  std::shared_ptr<const HostSnapshot> snap;
+};
+
+namespace {
+
+template <class F>
+int guarded(F &&f) {
+  try {
+    return f();
+  } catch (const std::bad_alloc &) {
+    return MQM_ENOMEM;
+  } catch (...) {
+    return MQM_EINVAL;
+  }
+}
+
+std::string_view sv(const char *p, size_t n) { return std::string_view(p ? p : "", p ? n : 0); }
+
+int commit_locked(mqm_index *h) {
+  if (h->snap && h->snap_version == h->store.version()) return MQM_OK;
+  auto hs = std::make_shared<HostSnapshot>();
+  int rc = flatten(h->store, hs.get());
+  if (rc != MQM_OK) return rc;
+  std::unique_ptr<GpuSnapshot> g;
+  rc = upload(std::move(hs), h->cfg.device, &g);
+  if (rc != MQM_OK) return rc;
+  // the previous snapshot may still be read by kernels queued on any stream
+  if (h->snap && hipDeviceSynchronize() != hipSuccess) return MQM_EHIP;
+  h->snap = std::move(g);
+  h->snap_version = h->store.version();
+  return MQM_OK;
+}
+
+int ensure_snapshot(mqm_index *h) {
+  if (!h->snap || (h->cfg.flags & MQM_CFG_AUTOCOMMIT)) return commit_locked(h);
+  return MQM_OK;
+}
+
+int fill_info(const SubInfo &s, mqm_sub_info *out) {
+  out->filter = s.filter;
+  out->client = s.client;
+  out->identifier = s.ident;
+  out->qos = s.qos;
+  out->no_local = s.no_local;
+  out->retain_as_published = s.rap;
+  out->retain_handling = s.rh;
+  return MQM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *mqm_version(void) { return "mqmatch 0.1 (gfx950)"; }
+
+int mqm_profile_enable(mqm_index *h, int on) {
+  if (!h) return MQM_EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  h->ws.profile = on != 0;
+  h->ws.reset_profile();
+  return MQM_OK;
+}
+
+int mqm_profile_read(mqm_index *h, mqm_profile *out) {
+  if (!h || !out) return MQM_EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  out->calls = h->ws.prof_calls;
+  out->fallback_topics = h->ws.prof_fallback_topics;
+  out->count_ms = h->ws.prof_count_ms;
+  out->emit_ms = h->ws.prof_emit_ms;
+  out->between_ms = h->ws.prof_between_ms;
+  out->total_ms = h->ws.prof_total_ms;
+  return MQM_OK;
+}
+
+int mqm_create(const mqm_config *cfg, mqm_index **out) {
+  if (!out) return MQM_EINVAL;
+  *out = nullptr;
+  return guarded([&] {
+    auto h = std::make_unique<mqm_index>();
+    if (cfg) h->cfg = *cfg;
+    if (h->cfg.device == MQM_DEVICE_NONE) {  // host-only store: mutations, no matching
+      *out = h.release();
+      return MQM_OK;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return MQM_ENODEV;
+    if (h->cfg.device < 0 || h->cfg.device >= ndev) return MQM_EINVAL;
+    if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) return MQM_EHIP;
+    *out = h.release();
+    return MQM_OK;
+  });
+}
+
+int mqm_destroy(mqm_index *h) {
+  if (!h) return MQM_EINVAL;
+  if (h->cfg.device != MQM_DEVICE_NONE) {
+    (void)hipSetDevice(h->cfg.device);
+    (void)hipDeviceSynchronize();
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+  }
+  delete h;
+  return MQM_OK;
+}
+
+int mqm_subscribe(mqm_index *h, const char *client, size_t client_len, const char *filter, size_t filter_len,
+                  const mqm_subscription *sub, int *is_new) {
+  if (!h || !sub) return MQM_EINVAL;
+  return guarded([&] {
+    std::lock_guard<std::mutex> g(h->mu);
+    bool n = h->store.subscribe(sv(client, client_len), sv(filter, filter_len), sub->qos, sub->no_local,
+                                sub->retain_as_published, sub->retain_handling, sub->identifier);
+    if (is_new) *is_new = n ? 1 : 0;
+    return MQM_OK;
+  });
+}
+
+int mqm_subscribe_many(mqm_index *h, size_t n, const char *client_bytes, const uint64_t *client_offs,
+                       const char *filter_bytes, const uint64_t *filter_offs, const mqm_subscription *subs,
+                       uint8_t *is_new) {
+  if (!h || !client_offs || !filter_offs || !subs) return MQM_EINVAL;
+  return guarded([&] {
+    std::lock_guard<std::mutex> g(h->mu);
+    for (size_t i = 0; i < n; i++) {
+      const mqm_subscription &s = subs[i];
+      bool r = h->store.subscribe(sv(client_bytes + client_offs[i], client_offs[i + 1] - client_offs[i]),
+                                  sv(filter_bytes + filter_offs[i], filter_offs[i + 1] - filter_offs[i]), s.qos,
+                                  s.no_local, s.retain_as_published, s.retain_handling, s.identifier);
+      if (is_new) is_new[i] = r ? 1 : 0;
+    }
+    return MQM_OK;
+  });
+}
+
+int mqm_unsubscribe(mqm_index *h, const char *filter, size_t filter_len, const char *client, size_t client_len,
+                    int *existed) {
+  if (!h) return MQM_EINVAL;
+  return guarded([&] {
+    std::lock_guard<std::mutex> g(h->mu);
+    bool r = h->store.unsubscribe(sv(filter, filter_len), sv(client, client_len));
+    if (existed) *existed = r ? 1 : 0;
+    return MQM_OK;
+  });
+}
+
+int mqm_retain_message(mqm_index *h, const char *topic, size_t topic_len, uint64_t message_ref,
+                       uint32_t payload_len, int retain_flag, int64_t *result) {
+  if (!h) return MQM_EINVAL;
+  return guarded([&] {
+    std::lock_guard<std::mutex> g(h->mu);
+    int64_t r = h->store.retain_message(sv(topic, topic_len), message_ref, payload_len, retain_flag != 0);
+    if (result) *result = r;
+    return MQM_OK;
+  });
+}
+
+int mqm_retained_len(mqm_index *h, uint64_t *out) {
+  if (!h || !out) return MQM_EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  *out = h->store.retained_len();
+  return MQM_OK;
+}
+
+int mqm_commit(mqm_index *h) {
+  if (!h) return MQM_EINVAL;
+  return guarded([&] {
+    std::lock_guard<std::mutex> g(h->mu);
+    if (h->cfg.device == MQM_DEVICE_NONE) return MQM_ENODEV;
+    if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
+    return commit_locked(h);
+  });
+}
+
+int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t *d_topic_offsets, uint32_t n_topics,
+                     void *hip_stream, mqm_device_result *out) {
+  if (!h || !out || (n_topics && (!d_topic_bytes || !d_topic_offsets))) return MQM_EINVAL;
+  return guarded([&] {
+    std::lock_guard<std::mutex> g(h->mu);
+    if (h->cfg.device == MQM_DEVICE_NONE) return MQM_ENODEV;
+    if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
+    int rc = ensure_snapshot(h);
+    if (rc != MQM_OK) return rc;
+    MatchOutput mo;
+    rc = match_device(h->snap->dev, h->ws, d_topic_bytes, d_topic_offsets, n_topics, (hipStream_t)hip_stream, &mo);
+    if (rc != 0) return rc;
+    out->n_topics = mo.n_topics;
+    out->n_deliveries = mo.n_deliveries;
+    out->n_shared = mo.n_shared;
+    out->offsets = mo.offsets;
+    out->deliveries = reinterpret_cast<const mqm_delivery *>(mo.deliveries);
+    out->shared_offsets = mo.shared_offsets;
+    out->shared = mo.shared;
+    out->n_fallback = mo.n_fallback;
+    return MQM_OK;
+  });
+}
+
+int mqm_match_batch(mqm_index *h, const char *topic_bytes, const uint64_t *topic_offsets, uint32_t n_topics,
+                    mqm_result **out) {
+  if (!h || !out || !topic_offsets || (n_topics && !topic_bytes)) return MQM_EINVAL;
+  *out = nullptr;
+  return guarded([&] {
+    std::lock_guard<std::mutex> g(h->mu);
+    if (h->cfg.device == MQM_DEVICE_NONE) return MQM_ENODEV;
+    if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
+    int rc = ensure_snapshot(h);
+    if (rc != MQM_OK) return rc;
+    const uint64_t base = topic_offsets[0];
+    const uint64_t nbytes = topic_offsets[n_topics] - base;
+    Workspace &ws = h->ws;
+    if (ws.get(Workspace::kInBytes, nbytes + 16) || ws.get(Workspace::kInOffs, sizeof(uint64_t) * (n_topics + 1)))
+      return MQM_ENOMEM;
+    auto *d_bytes = (uint8_t *)ws.ptr(Workspace::kInBytes);
+    auto *d_offs = (uint64_t *)ws.ptr(Workspace::kInOffs);
+    std::vector<uint64_t> offs(topic_offsets, topic_offsets + n_topics + 1);
+    for (auto &o : offs) o -= base;
+    if (nbytes && hipMemcpyAsync(d_bytes, topic_bytes + base, nbytes, hipMemcpyHostToDevice, h->stream) != hipSuccess)
+      return MQM_EHIP;
+    if (hipMemcpyAsync(d_offs, offs.data(), sizeof(uint64_t) * (n_topics + 1), hipMemcpyHostToDevice, h->stream) !=
+        hipSuccess)
+      return MQM_EHIP;
+    MatchOutput mo;
+    rc = match_device(h->snap->dev, ws, d_bytes, d_offs, n_topics, h->stream, &mo);
+    if (rc != 0) return rc;
+    auto r = std::make_unique<mqm_result>();
+    r->n = n_topics;
+    r->offsets.resize(n_topics + 1);
+    r->shared_offsets.resize(n_topics + 1);
+    r->deliveries.resize(mo.n_deliveries);
+    r->shared.resize(mo.n_shared);
+    r->snap = h->snap->host;
+    if (hipMemcpyAsync(r->offsets.data(), mo.offsets, sizeof(uint64_t) * (n_topics + 1), hipMemcpyDeviceToHost,
+                       h->stream) != hipSuccess ||
+        hipMemcpyAsync(r->shared_offsets.data(), mo.shared_offsets, sizeof(uint64_t) * (n_topics + 1),
+                       hipMemcpyDeviceToHost, h->stream) != hipSuccess)
+      return MQM_EHIP;
+    if (mo.n_deliveries && hipMemcpyAsync(r->deliveries.data(), mo.deliveries, sizeof(uint64_t) * mo.n_deliveries,
+                                          hipMemcpyDeviceToHost, h->stream) != hipSuccess)
+      return MQM_EHIP;
+    if (mo.n_shared && hipMemcpyAsync(r->shared.data(), mo.shared, sizeof(uint32_t) * mo.n_shared,
+                                      hipMemcpyDeviceToHost, h->stream) != hipSuccess)
+      return MQM_EHIP;
+    if (hipStreamSynchronize(h->stream) != hipSuccess) return MQM_EHIP;
+    *out = r.release();
+    return MQM_OK;
+  });
+}
+
+int mqm_subscribers(mqm_index *h, const char *topic, size_t topic_len, mqm_result **out) {
+  uint64_t offs[2] = {0, topic_len};
+  return mqm_match_batch(h, topic ? topic : "", offs, 1, out);
+}
+
+uint32_t mqm_result_num_topics(const mqm_result *r) { return r ? r->n : 0; }
+const uint64_t *mqm_result_offsets(const mqm_result *r) { return r ? r->offsets.data() : nullptr; }
+const mqm_delivery *mqm_result_deliveries(const mqm_result *r) { return r ? r->deliveries.data() : nullptr; }
+const uint64_t *mqm_result_shared_offsets(const mqm_result *r) { return r ? r->shared_offsets.data() : nullptr; }
+const uint32_t *mqm_result_shared(const mqm_result *r) { return r ? r->shared.data() : nullptr; }
+
+int mqm_result_sub_info(const mqm_result *r, uint32_t sub, mqm_sub_info *out) {
+  if (!r || !out || !r->snap || sub >= r->snap->sub_info.size()) return MQM_EINVAL;
+  return fill_info(r->snap->sub_info[sub], out);
+}
+
+int mqm_result_shared_info(const mqm_result *r, uint32_t shared_sub, mqm_sub_info *out) {
+  if (!r || !out || !r->snap || shared_sub >= r->snap->shared_info.size()) return MQM_EINVAL;
+  return fill_info(r->snap->shared_info[shared_sub], out);
+}
+
+int mqm_result_sub_infos(const mqm_result *r, int shared, const uint32_t *subs, size_t n, mqm_sub_info *out) {
+  if (!r || !r->snap || (n && (!subs || !out))) return MQM_EINVAL;
+  const auto &tab = shared ? r->snap->shared_info : r->snap->sub_info;
+  for (size_t i = 0; i < n; i++) {
+    if (subs[i] >= tab.size()) return MQM_EINVAL;
+    fill_info(tab[subs[i]], &out[i]);
+  }
+  return MQM_OK;
+}
+
+void mqm_result_free(mqm_result *r) { delete r; }
+
+static int copy_name(const std::string &s, char *buf, size_t cap, size_t *len) {
+  if (len) *len = s.size();
+  if (buf && cap) memcpy(buf, s.data(), s.size() < cap ? s.size() : cap);
+  return MQM_OK;
+}
+
+int mqm_client_name(mqm_index *h, uint32_t client, char *buf, size_t cap, size_t *len) {
+  if (!h) return MQM_EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  if (client >= h->store.clients().size()) return MQM_EINVAL;
+  return copy_name(h->store.clients().name(client), buf, cap, len);
+}
+
+int mqm_filter_name(mqm_index *h, uint32_t filter, char *buf, size_t cap, size_t *len) {
+  if (!h) return MQM_EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  if (filter >= h->store.filters().size()) return MQM_EINVAL;
+  return copy_name(h->store.filters().name(filter), buf, cap, len);
+}
+
+int mqm_num_clients(mqm_index *h, uint32_t *out) {
+  if (!h || !out) return MQM_EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  *out = h->store.clients().size();
+  return MQM_OK;
+}
+
+int mqm_is_valid_filter(const char *filter, size_t len, int for_publish) {
+  return is_valid_filter(sv(filter, len), for_publish != 0) ? 1 : 0;
+}
+
+int mqm_is_shared_filter(const char *filter, size_t len) { return is_shared_filter(sv(filter, len)) ? 1 : 0; }
+
+int mqm_snapshot_stats_get(mqm_index *h, mqm_snapshot_stats *out) {
+  if (!h || !out) return MQM_EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  memset(out, 0, sizeof(*out));
+  if (!h->snap) return MQM_OK;
+  const HostSnapshot &hs = *h->snap->host;
+  out->nodes = hs.nodes.size();
+  out->edges = hs.n_edges;
+  out->edge_buckets = hs.bucket_mask + 1;
+  out->subs = hs.sub_info.size();
+  out->shared = hs.shared_info.size();
+  out->height = hs.height;
+  out->device_bytes = h->snap->device_bytes;
+  return MQM_OK;
+}
+
+}  // extern "C"

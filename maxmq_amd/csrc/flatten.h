@@ -1,0 +1,48 @@
+// maxmq_amd/csrc/flatten.h — host store -> GPU-resident CSR level-trie.
+#pragma once
+#include <stdint.h>
+
+#include <memory>
+#include <vector>
+
+#include "snapshot.h"
+#include "store.h"
+
+namespace mqm {
+
+// per-subscription side information, kept on the host to resolve result ids
+struct SubInfo {
+  uint32_t filter;
+  uint32_t client;
+  int32_t ident;
+  uint8_t qos, no_local, rap, rh;
+};
+
+struct HostSnapshot {
+  std::vector<NodeDesc> nodes;
+  std::vector<EdgeEntry> edges;  // (bucket_mask + 1) * kEdgesPerBucket
+  std::vector<SubEnt> subs;
+  std::vector<SubInfo> sub_info;     // by non-shared sid
+  std::vector<SubInfo> shared_info;  // by shared sid
+  std::vector<uint8_t> tok_pool;
+  uint64_t bucket_mask = 0;
+  uint32_t height = 0;
+  uint64_t n_edges = 0;
+};
+
+// Build the snapshot; returns MQM_OK or MQM_ELIMIT.
+int flatten(const Store &st, HostSnapshot *out);
+
+// Device copy of a HostSnapshot.  Host side tables stay shared with results
+// (shared_ptr) so a result can outlive the next commit.
+struct GpuSnapshot {
+  DeviceSnapshot dev{};
+  std::shared_ptr<const HostSnapshot> host;
+  void *buffers[4] = {nullptr, nullptr, nullptr, nullptr};
+  uint64_t device_bytes = 0;
+  ~GpuSnapshot();
+};
+
+int upload(std::shared_ptr<const HostSnapshot> hs, int device, std::unique_ptr<GpuSnapshot> *out);
+
+}  // namespace mqm

@@ -1,0 +1,86 @@
+// maxmq_amd/csrc/keys.h — level-token keys and hashes shared by the host
+// snapshot builder and the gfx950 kernels (compiled by both g++ and hipcc).
+//
+// A topic/filter level ("particle", topics.go:558-577) becomes a 128-bit key:
+//   * len <= 15 : the bytes themselves, little-endian in k0 | k1[0..55], and
+//                 the length in k1's top byte (0..15).  Exact: no collisions.
+//   * len >= 16 : a 120-bit hash with k1's top byte = 0xFF; a probe hit is
+//                 verified against the token byte pool, so matching stays exact.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define MQM_HD __host__ __device__ __forceinline__
+#else
+#define MQM_HD inline
+#endif
+
+namespace mqm {
+
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr uint32_t kInlineMax = 15;
+
+struct Key {
+  uint64_t k0, k1;
+};
+
+MQM_HD uint64_t fmix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+
+MQM_HD uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+
+// 128-bit hash of a long token (>= 16 bytes); reads whole 8-byte words through
+// the caller-supplied byte accessor so host and device share one definition.
+template <class ByteAt>
+MQM_HD Key hash_long_token(ByteAt at, uint32_t len) {
+  uint64_t h0 = 0x9E3779B97F4A7C15ull ^ len, h1 = 0xC2B2AE3D27D4EB4Full ^ ((uint64_t)len << 32);
+  uint32_t i = 0;
+  for (; i + 8 <= len; i += 8) {
+    uint64_t w = 0;
+    for (int b = 0; b < 8; b++) w |= (uint64_t)at(i + b) << (8 * b);
+    h0 = rotl64(h0 ^ (w * 0x87c37b91114253d5ull), 31) * 0x4cf5ad432745937full;
+    h1 = rotl64(h1 + (w * 0x4cf5ad432745937full), 33) * 0x87c37b91114253d5ull;
+  }
+  uint64_t w = 0;
+  for (uint32_t b = 0; i + b < len; b++) w |= (uint64_t)at(i + b) << (8 * b);
+  h0 ^= w * 0x9E3779B97F4A7C15ull;
+  h1 ^= rotl64(w, 17) * 0xC2B2AE3D27D4EB4Full;
+  h0 = fmix64(h0 + h1);
+  h1 = fmix64(h1 + h0);
+  Key k;
+  k.k0 = h0;
+  k.k1 = (h1 & 0x00FFFFFFFFFFFFFFull) | (0xFFull << 56);
+  return k;
+}
+
+template <class ByteAt>
+MQM_HD Key make_key(ByteAt at, uint32_t len) {
+  if (len > kInlineMax) return hash_long_token(at, len);
+  Key k;
+  k.k0 = 0;
+  k.k1 = (uint64_t)len << 56;
+  for (uint32_t i = 0; i < len; i++) {
+    uint64_t b = (uint64_t)at(i);
+    if (i < 8)
+      k.k0 |= b << (8 * i);
+    else
+      k.k1 |= b << (8 * (i - 8));
+  }
+  return k;
+}
+
+MQM_HD bool key_is_long(const Key &k) { return (k.k1 >> 56) == 0xFF; }
+
+// bucket hash of an edge (parent node, child key)
+MQM_HD uint64_t edge_hash(uint32_t parent, const Key &k) {
+  uint64_t h = fmix64(k.k0 ^ rotl64(k.k1, 29) ^ ((uint64_t)parent * 0x9E3779B97F4A7C15ull));
+  return h ^ (h >> 29);
+}
+
+}  // namespace mqm

@@ -1,0 +1,764 @@
+// maxmq_amd/csrc/match.hip — gfx950 kernels for TopicsIndex.Subscribers
+// (vendor/github.com/mochi-co/mqtt/v2/topics.go:484-555) over a batch of
+// publish topics, against the GPU-resident CSR level-trie (snapshot.h).
+//
+// Main path: one wavefront per topic (grid-stride over topics).
+//   1. tokenize   : 64 lanes scan the topic bytes, ballot the '/' positions,
+//                   lane k builds level k's 128-bit key (keys.h) into LDS.
+//   2. walk       : level-synchronous over the frontier; each frontier node
+//                   fans out to 3 lanes (literal edge probe / '+' child /
+//                   '#' child) so one level costs one dependent memory round
+//                   trip (the literal child's descriptor is inline in the
+//                   edge entry).  Hits and the next frontier are compacted
+//                   with ballot + popcount into LDS.
+//   3. gather     : hits are sorted by rank (= reference emission order, see
+//                   snapshot.h) in registers (bitonic, shuffles); the
+//                   subscription ranges are flattened over the 64 lanes.
+//   4. dedupe     : per-topic LDS hash table keyed by client; one atomicOr
+//                   folds max-QoS (one-hot), NoLocal and the hit's rank
+//                   (one-hot) — Subscription.Merge (packets.go:250-270).
+//   5. emit       : the entry whose hit is its client's lowest rank is the
+//                   client's first-merged subscription; winners are
+//                   compacted (ballot) and written at the topic's offset.
+// The pipeline is two-pass (count -> device scan -> emit).  Topics that
+// exceed a per-wave LDS capacity (frontier, hits, raw entries, levels) are
+// re-run by an unbounded fallback: a wave-cooperative DFS with an LDS stack
+// and a global-memory dedupe table.  Nothing runs on the CPU.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstdio>
+
+#include "match.h"
+
+namespace mqm {
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kWavesPerBlock = 4;
+constexpr int kLMax = 16;    // levels cached per topic on the main path
+constexpr int kFCap = 32;    // frontier nodes per level
+constexpr int kHCap = 28;    // non-shared hits (rank one-hot uses bits 4..31)
+constexpr int kShCap = 32;   // shared hits
+constexpr int kTCap = 512;   // dedupe table slots
+constexpr int kSMax = 384;   // raw entries (table load <= 0.75)
+
+enum : uint8_t { kStatusOk = 0, kStatusFallback = 1 };
+
+struct WaveLds {
+  uint64_t key0[kLMax];
+  uint64_t key1[kLMax];
+  uint32_t sep[kLMax];           // position of the '/' ending level k
+  uint32_t front[2][3][kFCap];   // (node, plus, hash) of the frontier
+  uint32_t hit_rank[32];
+  uint32_t hit_off[32];
+  uint32_t hit_pre[33];
+  uint32_t sh_off[kShCap];
+  uint32_t sh_cnt[kShCap];
+  uint32_t tkey[kTCap];
+  uint32_t tval[kTCap];
+};
+
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ uint64_t lanemask_lt(int lane) { return (1ull << lane) - 1ull; }
+
+__device__ __forceinline__ NodeDesc load_desc(const NodeDesc *p) {
+  const uint4 *q = reinterpret_cast<const uint4 *>(p);
+  uint4 a = q[0], b = q[1];
+  NodeDesc d;
+  d.plus = a.x;
+  d.hash = a.y;
+  d.sub_off = a.z;
+  d.sub_cnt = a.w;
+  d.hsub_off = b.x;
+  d.hsub_cnt = b.y;
+  d.sh_off = b.z;
+  d.sh_cnt_flags = b.w;
+  return d;
+}
+
+// Literal child lookup: open-addressed edge table, 2 entries per 128-B bucket.
+// Long keys (>= 16 bytes) are verified byte-for-byte against the token pool.
+__device__ uint32_t probe_edge(const DeviceSnapshot &s, uint32_t parent, uint64_t k0, uint64_t k1,
+                               const uint8_t *tok, uint32_t tok_len, NodeDesc *desc) {
+  const uint64_t nslots = (s.bucket_mask + 1) * kEdgesPerBucket;
+  Key key{k0, k1};
+  uint64_t slot = (edge_hash(parent, key) & s.bucket_mask) * kEdgesPerBucket;
+  for (;;) {
+    const EdgeEntry *e = s.edges + slot;
+    const ulonglong2 kk = *reinterpret_cast<const ulonglong2 *>(e);
+    const uint4 pc = *reinterpret_cast<const uint4 *>(&e->parent);
+    if (pc.x == kNone) return kNone;
+    if (pc.x == parent && kk.x == k0 && kk.y == k1) {
+      bool ok = true;
+      if (key_is_long(key)) {
+        ok = pc.w == tok_len;
+        for (uint32_t i = 0; ok && i < tok_len; i++) ok = s.tok_pool[pc.z + i] == tok[i];
+      }
+      if (ok) {
+        *desc = load_desc(&e->desc);
+        return pc.y;
+      }
+    }
+    slot = (slot + 1) & (nslots - 1);
+  }
+}
+
+__device__ __forceinline__ uint32_t table_slot(uint32_t client, uint32_t lg) {
+  return (uint32_t)(((uint64_t)(client * 2654435769u) << lg) >> 32);
+}
+
+__device__ __forceinline__ uint64_t pack_delivery(uint32_t client, uint32_t sid, uint32_t qos, uint32_t nl) {
+  return (uint64_t)client | ((uint64_t)(sid | (qos << 28) | (nl << 30)) << 32);
+}
+
+// Bitonic sort of 32 (rank, off, cnt) triples held by lanes 0..31 (lanes
+// 32..63 sort their own copy, harmlessly).  Ascending by rank.
+__device__ __forceinline__ void sort32(int lane, uint32_t &rank, uint32_t &off, uint32_t &cnt) {
+  for (int k = 2; k <= 32; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      uint32_t r2 = __shfl_xor(rank, j, 64);
+      uint32_t o2 = __shfl_xor(off, j, 64);
+      uint32_t c2 = __shfl_xor(cnt, j, 64);
+      const bool up = (lane & k) == 0;
+      const bool lower = (lane & j) == 0;
+      const bool take_other = (lower == up) ? (r2 < rank) : (r2 > rank);
+      if (take_other) {
+        rank = r2;
+        off = o2;
+        cnt = c2;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// main path
+// ---------------------------------------------------------------------------
+template <bool kEmit>
+__global__ __launch_bounds__(kWave *kWavesPerBlock) void k_match(
+    DeviceSnapshot s, const uint8_t *__restrict__ tbytes, const uint64_t *__restrict__ toffs, uint32_t n,
+    uint32_t *__restrict__ dcount, uint32_t *__restrict__ hcount, uint8_t *__restrict__ status,
+    uint32_t *__restrict__ ovf_list, uint32_t *__restrict__ ovf_n, const uint64_t *__restrict__ doffs,
+    const uint64_t *__restrict__ hoffs, uint64_t *__restrict__ dout, uint32_t *__restrict__ hout) {
+  __shared__ WaveLds lds_all[kWavesPerBlock];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wib = threadIdx.x / kWave;
+  WaveLds &L = lds_all[wib];
+  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+
+  for (uint32_t t = blockIdx.x * kWavesPerBlock + wib; t < n; t += nwaves) {
+    if (kEmit && status[t] != kStatusOk) continue;
+    const uint64_t off = toffs[t];
+    const uint32_t len = (uint32_t)(toffs[t + 1] - off);
+    const uint8_t *tp = tbytes + off;
+    if (len == 0) {  // scanSubscribers returns at once (topics.go:498-500)
+      if (!kEmit && lane == 0) {
+        dcount[t] = 0;
+        hcount[t] = 0;
+        status[t] = kStatusOk;
+      }
+      continue;
+    }
+    bool overflow = false;
+
+    // ---- 1. tokenize ------------------------------------------------------
+    uint32_t nsep = 0;
+    bool dollar = false;
+    for (uint32_t base = 0; base < len && nsep < (uint32_t)kLMax; base += kWave) {
+      const uint32_t p = base + lane;
+      const uint8_t b = p < len ? tp[p] : 0;
+      if (base == 0) dollar = __shfl(b, 0, 64) == '$';
+      const uint64_t m = __ballot(p < len && b == '/');
+      if (b == '/' && p < len) {
+        const uint32_t idx = nsep + __popcll(m & lanemask_lt(lane));
+        if (idx < (uint32_t)kLMax) L.sep[idx] = p;
+      }
+      nsep += __popcll(m);
+    }
+    // levels known: 0 .. nlev-1, with nlev capped at kLMax + 1
+    const uint32_t nlev = nsep >= (uint32_t)kLMax ? kLMax + 1 : nsep + 1;
+    wave_lds_sync();
+    if (lane < kLMax && (uint32_t)lane < nlev) {
+      const uint32_t st = lane == 0 ? 0 : L.sep[lane - 1] + 1;
+      const uint32_t en = ((uint32_t)lane < nsep) ? L.sep[lane] : len;
+      Key k = make_key([&](uint32_t i) { return tp[st + i]; }, en - st);
+      L.key0[lane] = k.k0;
+      L.key1[lane] = k.k1;
+    }
+    wave_lds_sync();
+
+    // ---- 2. walk ----------------------------------------------------------
+    uint32_t nf = 1, nh = 0, nsh = 0;
+    int cur = 0;
+    if (lane == 0) {
+      const NodeDesc r = load_desc(s.nodes);
+      L.front[0][0][0] = 0;
+      L.front[0][1][0] = r.plus;
+      L.front[0][2][0] = r.hash;
+    }
+    wave_lds_sync();
+    for (uint32_t d = 0; d < nlev && nf > 0 && !overflow; d++) {
+      if (d >= (uint32_t)kLMax) {
+        overflow = true;
+        break;
+      }
+      const uint64_t k0 = L.key0[d], k1 = L.key1[d];
+      const bool has_next = d + 1 < nlev;
+      // key == "+" / "#": the literal probe is the wildcard probe (collapse the
+      // reference's duplicate visit; no parent probe: topics.go:507 excludes it)
+      const bool lit_is_wild = (k1 == (1ull << 56)) && (k0 == '+' || k0 == '#');
+      const uint32_t tst = d == 0 ? 0 : L.sep[d - 1] + 1;
+      const uint32_t tln = ((d < nsep) ? L.sep[d] : len) - tst;
+      uint32_t nnext = 0;
+      for (uint32_t base = 0; base < nf * 3 && !overflow; base += kWave) {
+        const uint32_t item = base + lane;
+        const uint32_t fi = item / 3, type = item % 3;
+        uint32_t c = kNone;
+        NodeDesc dc;
+        if (item < nf * 3) {
+          const uint32_t node = L.front[cur][0][fi];
+          if (type == 0) {
+            if (!lit_is_wild) c = probe_edge(s, node, k0, k1, tp + tst, tln, &dc);
+          } else {
+            c = L.front[cur][type][fi];
+            if (c != kNone) dc = load_desc(s.nodes + c);
+          }
+        }
+        const bool found = c != kNone;
+        const uint32_t fl = found ? dc.sh_cnt_flags >> 24 : 0;
+        const bool skip_dollar = dollar && (fl & kFlagDollarWild);
+        const bool h_own = found && dc.sub_cnt > 0 && !skip_dollar;
+        const bool h_par = found && type == 0 && dc.hsub_cnt > 0 && !skip_dollar;
+        const bool h_sh = found && (dc.sh_cnt_flags & kShCntMask) > 0;
+        const bool push = found && has_next && (fl & kFlagHasChildren);
+        const uint64_t m_own = __ballot(h_own), m_par = __ballot(h_par), m_sh = __ballot(h_sh),
+                       m_push = __ballot(push);
+        const uint64_t lt = lanemask_lt(lane);
+        const uint32_t n_own = __popcll(m_own), n_par = __popcll(m_par);
+        if (nh + n_own + n_par > (uint32_t)kHCap || nsh + __popcll(m_sh) > (uint32_t)kShCap ||
+            nnext + __popcll(m_push) > (uint32_t)kFCap) {
+          overflow = true;
+          break;
+        }
+        if (h_own) {
+          const uint32_t i = nh + __popcll(m_own & lt);
+          L.hit_rank[i] = 2 * c;
+          L.hit_off[i] = dc.sub_off;
+          L.hit_pre[i] = dc.sub_cnt;
+        }
+        if (h_par) {
+          const uint32_t i = nh + n_own + __popcll(m_par & lt);
+          L.hit_rank[i] = 2 * c + 1;
+          L.hit_off[i] = dc.hsub_off;
+          L.hit_pre[i] = dc.hsub_cnt;
+        }
+        if (h_sh) {
+          const uint32_t i = nsh + __popcll(m_sh & lt);
+          L.sh_off[i] = dc.sh_off;
+          L.sh_cnt[i] = dc.sh_cnt_flags & kShCntMask;
+        }
+        if (push) {
+          const uint32_t i = nnext + __popcll(m_push & lt);
+          L.front[cur ^ 1][0][i] = c;
+          L.front[cur ^ 1][1][i] = dc.plus;
+          L.front[cur ^ 1][2][i] = dc.hash;
+        }
+        nh += n_own + n_par;
+        nsh += __popcll(m_sh);
+        nnext += __popcll(m_push);
+      }
+      wave_lds_sync();
+      cur ^= 1;
+      nf = nnext;
+    }
+
+    // ---- 3. order hits by rank, prefix their range sizes -------------------
+    uint32_t S = 0;
+    if (!overflow) {
+      uint32_t rank = 0xFFFFFFFFu, hoff = 0, hcnt = 0;
+      if ((uint32_t)(lane & 31) < nh) {
+        rank = L.hit_rank[lane & 31];
+        hoff = L.hit_off[lane & 31];
+        hcnt = L.hit_pre[lane & 31];
+      }
+      sort32(lane, rank, hoff, hcnt);
+      // inclusive scan of hcnt over lanes 0..31
+      uint32_t inc = hcnt;
+      for (int o = 1; o < 32; o <<= 1) {
+        const uint32_t v = __shfl_up(inc, o, 64);
+        if ((lane & 31) >= o) inc += v;
+      }
+      S = __shfl(inc, 31, 64);
+      wave_lds_sync();
+      if (lane < 32) {
+        L.hit_rank[lane] = rank;
+        L.hit_off[lane] = hoff;
+        L.hit_pre[lane + 1] = inc;
+      }
+      if (lane == 0) L.hit_pre[0] = 0;
+      if (S > (uint32_t)kSMax) overflow = true;
+      wave_lds_sync();
+    }
+
+    if (overflow) {
+      if (!kEmit && lane == 0) {
+        status[t] = kStatusFallback;
+        dcount[t] = 0;
+        hcount[t] = 0;
+        ovf_list[atomicAdd(ovf_n, 1u)] = t;
+      }
+      continue;
+    }
+
+    // ---- 4. dedupe in the LDS table ---------------------------------------
+    uint32_t lg = 6;
+    while ((1u << lg) < 2 * S) lg++;
+    const uint32_t tsize = 1u << lg;
+    for (uint32_t i = lane; i < tsize; i += kWave) L.tkey[i] = 0, L.tval[i] = 0;
+    wave_lds_sync();
+    for (uint32_t r = lane; r < S; r += kWave) {
+      uint32_t h = 0;  // hit with hit_pre[h] <= r < hit_pre[h+1]
+      for (uint32_t step = 16; step > 0; step >>= 1)
+        if (h + step < nh && L.hit_pre[h + step] <= r) h += step;
+      const SubEnt e = s.subs[L.hit_off[h] + (r - L.hit_pre[h])];
+      uint32_t slot = table_slot(e.client, lg);
+      for (;;) {
+        const uint32_t prev = atomicCAS(&L.tkey[slot], 0u, e.client + 1);
+        if (prev == 0 || prev == e.client + 1) break;
+        slot = (slot + 1) & (tsize - 1);
+      }
+      atomicOr(&L.tval[slot], (1u << (4 + h)) | (1u << (e.meta & 3)) | (((e.meta >> 2) & 1) << 3));
+    }
+    wave_lds_sync();
+
+    // ---- 5. winners -> deliveries -----------------------------------------
+    uint32_t D = 0;
+    const uint64_t dbase = kEmit ? doffs[t] : 0;
+    for (uint32_t r0 = 0; r0 < S; r0 += kWave) {
+      const uint32_t r = r0 + lane;
+      bool win = false;
+      uint64_t ent = 0;
+      if (r < S) {
+        uint32_t h = 0;
+        for (uint32_t step = 16; step > 0; step >>= 1)
+          if (h + step < nh && L.hit_pre[h + step] <= r) h += step;
+        const uint32_t sid = L.hit_off[h] + (r - L.hit_pre[h]);
+        const uint32_t client = s.subs[sid].client;
+        uint32_t slot = table_slot(client, lg);
+        while (L.tkey[slot] != client + 1) slot = (slot + 1) & (tsize - 1);
+        const uint32_t v = L.tval[slot];
+        win = (uint32_t)__builtin_ctz(v >> 4) == h;
+        if (kEmit && win) ent = pack_delivery(client, sid, 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
+      }
+      const uint64_t m = __ballot(win);
+      if (kEmit && win) dout[dbase + D + __popcll(m & lanemask_lt(lane))] = ent;
+      D += __popcll(m);
+    }
+
+    // ---- shared candidates (gatherSharedSubscriptions, topics.go:541-555) ---
+    uint32_t H = 0;
+    const uint64_t hbase = kEmit ? hoffs[t] : 0;
+    for (uint32_t i = 0; i < nsh; i++) {
+      const uint32_t so = L.sh_off[i], sc = L.sh_cnt[i];
+      if (kEmit)
+        for (uint32_t j = lane; j < sc; j += kWave) hout[hbase + H + j] = so + j;
+      H += sc;
+    }
+    if (!kEmit && lane == 0) {
+      dcount[t] = D;
+      hcount[t] = H;
+      status[t] = kStatusOk;
+    }
+    wave_lds_sync();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// fallback: unbounded wave-cooperative DFS for the topics the main path
+// flagged.  Phase 0 counts raw entries / shared candidates, phase 1 inserts
+// into a per-topic global table and writes shared candidates, phase 2 counts
+// distinct clients, phase 3 emits deliveries.
+// ---------------------------------------------------------------------------
+struct GEnt {  // global dedupe slot (16 B)
+  unsigned long long keybits;  // (client + 1) | bits << 32
+  unsigned long long first;    // (rank << 32) | sid, atomicMin
+};
+
+template <int kPhase>
+__global__ __launch_bounds__(kWave) void k_fallback(
+    DeviceSnapshot s, const uint8_t *__restrict__ tbytes, const uint64_t *__restrict__ toffs,
+    const uint32_t *__restrict__ ovf_list, const uint32_t *__restrict__ ovf_n, uint64_t *__restrict__ raw_cnt,
+    uint32_t *__restrict__ hcount, uint32_t *__restrict__ dcount, const uint64_t *__restrict__ tab_off,
+    GEnt *__restrict__ tab, const uint64_t *__restrict__ hoffs, uint32_t *__restrict__ hout,
+    const uint64_t *__restrict__ doffs, uint64_t *__restrict__ dout, uint32_t max_levels) {
+  extern __shared__ uint32_t dyn[];
+  // layout: sep[max_levels] | key0/key1 (u64 x max_levels each) | stack (4 x u32) x (2*max_levels + 8)
+  uint32_t *sep = dyn;
+  uint64_t *key0 = reinterpret_cast<uint64_t *>(dyn + ((max_levels + 1) & ~1u));
+  uint64_t *key1 = key0 + max_levels;
+  uint32_t *stk = reinterpret_cast<uint32_t *>(key1 + max_levels);
+  const int lane = threadIdx.x;
+  const uint32_t cnt = *ovf_n;
+  for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+    const uint32_t t = ovf_list[i];
+    const uint64_t off = toffs[t];
+    const uint32_t len = (uint32_t)(toffs[t + 1] - off);
+    const uint8_t *tp = tbytes + off;
+    const uint64_t tsz = kPhase >= 1 ? tab_off[i + 1] - tab_off[i] : 0;
+    GEnt *T = kPhase >= 1 ? tab + tab_off[i] : nullptr;
+
+    if (kPhase == 2 || kPhase == 3) {
+      uint32_t D = 0;
+      const uint64_t dbase = kPhase == 3 ? doffs[t] : 0;
+      for (uint64_t b = 0; b < tsz; b += kWave) {
+        const uint64_t j = b + lane;
+        bool occ = false;
+        GEnt g{0, 0};
+        if (j < tsz) {
+          g = T[j];
+          occ = (uint32_t)g.keybits != 0;
+        }
+        const uint64_t m = __ballot(occ);
+        if (kPhase == 3 && occ) {
+          const uint32_t bits = (uint32_t)(g.keybits >> 32);
+          dout[dbase + D + __popcll(m & lanemask_lt(lane))] =
+              pack_delivery((uint32_t)g.keybits - 1, (uint32_t)g.first, 31u - __builtin_clz(bits & 7u),
+                            (bits >> 3) & 1u);
+        }
+        D += __popcll(m);
+      }
+      if (kPhase == 2 && lane == 0) dcount[t] = D;
+      continue;
+    }
+
+    // tokenize up to max_levels levels
+    uint32_t nsep = 0;
+    bool dollar = false;
+    for (uint32_t base = 0; base < len && nsep < max_levels; base += kWave) {
+      const uint32_t p = base + lane;
+      const uint8_t b = p < len ? tp[p] : 0;
+      if (base == 0) dollar = __shfl(b, 0, 64) == '$';
+      const uint64_t m = __ballot(p < len && b == '/');
+      if (b == '/' && p < len) {
+        const uint32_t idx = nsep + __popcll(m & lanemask_lt(lane));
+        if (idx < max_levels) sep[idx] = p;
+      }
+      nsep += __popcll(m);
+    }
+    const uint32_t nlev = len == 0 ? 0 : (nsep >= max_levels ? max_levels + 1 : nsep + 1);
+    wave_lds_sync();
+    const uint32_t nkeys = nlev < max_levels ? nlev : max_levels;
+    for (uint32_t k = lane; k < nkeys; k += kWave) {
+      const uint32_t st = k == 0 ? 0 : sep[k - 1] + 1;
+      const uint32_t en = (k < nsep) ? sep[k] : len;
+      Key kk = make_key([&](uint32_t j) { return tp[st + j]; }, en - st);
+      key0[k] = kk.k0;
+      key1[k] = kk.k1;
+    }
+    wave_lds_sync();
+
+    uint64_t S = 0;
+    uint32_t H = 0;
+    const uint64_t hbase = kPhase == 1 ? hoffs[t] : 0;
+    uint32_t lg = 0;
+    if (kPhase == 1)
+      while ((1ull << lg) < tsz) lg++;
+    // DFS stack of (node, plus, hash, depth)
+    int sp = 0;
+    if (nlev > 0) {
+      if (lane == 0) {
+        const NodeDesc r = load_desc(s.nodes);
+        stk[0] = 0;
+        stk[1] = r.plus;
+        stk[2] = r.hash;
+        stk[3] = 0;
+      }
+      sp = 1;
+    }
+    wave_lds_sync();
+    while (sp > 0) {
+      sp--;
+      const uint32_t node = stk[4 * sp], pl = stk[4 * sp + 1], hs = stk[4 * sp + 2], d = stk[4 * sp + 3];
+      wave_lds_sync();
+      const uint64_t k0 = key0[d], k1 = key1[d];
+      const bool has_next = d + 1 < nlev;
+      const bool lit_is_wild = (k1 == (1ull << 56)) && (k0 == '+' || k0 == '#');
+      const uint32_t tst = d == 0 ? 0 : sep[d - 1] + 1;
+      const uint32_t tln = ((d < nsep) ? sep[d] : len) - tst;
+      uint32_t c = kNone;
+      NodeDesc dc;
+      if (lane == 0 && !lit_is_wild) c = probe_edge(s, node, k0, k1, tp + tst, tln, &dc);
+      if (lane == 1 && pl != kNone) {
+        c = pl;
+        dc = load_desc(s.nodes + c);
+      }
+      if (lane == 2 && hs != kNone) {
+        c = hs;
+        dc = load_desc(s.nodes + c);
+      }
+      // hits: process the 3 lanes' results one by one, wave-uniformly
+      for (int src = 0; src < 3; src++) {
+        const uint32_t cc = __shfl(c, src, 64);
+        if (cc == kNone) continue;
+        NodeDesc e;
+        e.plus = __shfl(dc.plus, src, 64);
+        e.hash = __shfl(dc.hash, src, 64);
+        e.sub_off = __shfl(dc.sub_off, src, 64);
+        e.sub_cnt = __shfl(dc.sub_cnt, src, 64);
+        e.hsub_off = __shfl(dc.hsub_off, src, 64);
+        e.hsub_cnt = __shfl(dc.hsub_cnt, src, 64);
+        e.sh_off = __shfl(dc.sh_off, src, 64);
+        e.sh_cnt_flags = __shfl(dc.sh_cnt_flags, src, 64);
+        const uint32_t fl = e.sh_cnt_flags >> 24;
+        const bool skip_dollar = dollar && (fl & kFlagDollarWild);
+        for (int part = 0; part < 2; part++) {
+          if (part == 1 && src != 0) break;
+          const uint32_t roff = part ? e.hsub_off : e.sub_off;
+          const uint32_t rcnt = skip_dollar ? 0 : (part ? e.hsub_cnt : e.sub_cnt);
+          const uint32_t rank = 2 * cc + part;
+          S += rcnt;
+          if (kPhase == 1) {
+            for (uint32_t j = lane; j < rcnt; j += kWave) {
+              const uint32_t sid = roff + j;
+              const SubEnt se = s.subs[sid];
+              uint64_t slot = ((uint64_t)(se.client * 2654435769u) << lg) >> 32;
+              for (;;) {
+                const unsigned long long prev =
+                    atomicCAS(reinterpret_cast<unsigned long long *>(&T[slot].keybits), 0ull,
+                              (unsigned long long)(se.client + 1));
+                if (prev == 0 || (uint32_t)prev == se.client + 1) break;
+                slot = (slot + 1) & (tsz - 1);
+              }
+              const uint32_t bits = (1u << (se.meta & 3)) | (((se.meta >> 2) & 1) << 3);
+              atomicOr(&T[slot].keybits, (unsigned long long)bits << 32);
+              atomicMin(&T[slot].first, ((unsigned long long)rank << 32) | sid);
+            }
+          }
+        }
+        const uint32_t shc = e.sh_cnt_flags & kShCntMask;
+        if (kPhase == 1)
+          for (uint32_t j = lane; j < shc; j += kWave) hout[hbase + H + j] = e.sh_off + j;
+        H += shc;
+        if (has_next && (fl & kFlagHasChildren)) {
+          if (lane == 0) {
+            stk[4 * sp] = cc;
+            stk[4 * sp + 1] = e.plus;
+            stk[4 * sp + 2] = e.hash;
+            stk[4 * sp + 3] = d + 1;
+          }
+          sp++;
+        }
+      }
+      wave_lds_sync();
+    }
+    if (lane == 0) {
+      if (kPhase == 0) {
+        raw_cnt[i] = S;
+        hcount[t] = H;
+      }
+    }
+  }
+}
+
+__global__ void k_table_sizes(const uint64_t *__restrict__ raw_cnt, const uint32_t *__restrict__ ovf_n,
+                              uint64_t *__restrict__ sizes) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= *ovf_n) return;
+  uint64_t sz = 64;
+  while (sz < 2 * raw_cnt[i]) sz <<= 1;
+  sizes[i] = sz;
+}
+
+#define HIP_TRY(x)                                                                         \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess) {                                                                \
+      fprintf(stderr, "mqmatch: %s failed: %s (%s:%d)\n", #x, hipGetErrorString(e_), __FILE__, \
+              __LINE__);                                                                   \
+      return -3;                                                                           \
+    }                                                                                      \
+  } while (0)
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// workspace / orchestration
+// ---------------------------------------------------------------------------
+int Workspace::reserve(void **p, size_t *cap, size_t need) {
+  if (*cap >= need && *p) return 0;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  size_t n = std::max<size_t>(need, 256);
+  n = n + n / 4;
+  if (hipMalloc(p, n) != hipSuccess) {
+    *cap = 0;
+    return -2;
+  }
+  *cap = n;
+  return 0;
+}
+
+Workspace::~Workspace() {
+  for (auto &b : bufs)
+    if (b.p) (void)hipFree(b.p);
+  if (host_pinned) (void)hipHostFree(host_pinned);
+  for (auto &e : ev)
+    if (e) (void)hipEventDestroy(e);
+}
+
+static void mark(Workspace &ws, int i, hipStream_t st) {
+  if (!ws.profile) return;
+  if (!ws.ev[i] && hipEventCreate(&ws.ev[i]) != hipSuccess) {
+    ws.profile = false;
+    return;
+  }
+  (void)hipEventRecord(ws.ev[i], st);
+}
+
+static float elapsed(Workspace &ws, int a, int b) {
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, ws.ev[a], ws.ev[b]) != hipSuccess) return 0;
+  return ms;
+}
+
+// inclusive-sum counts (u32, n) into offs + 1, offs[0] = 0  => exclusive offsets
+static int scan_offsets(Workspace &ws, const uint32_t *counts, uint64_t *offs, uint32_t n, hipStream_t st) {
+  HIP_TRY(hipMemsetAsync(offs, 0, sizeof(uint64_t), st));
+  if (n == 0) return 0;
+  size_t tmp = 0;
+  HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, tmp, counts, offs + 1, n, st));
+  if (ws.get(Workspace::kScanTmp, tmp)) return -2;
+  HIP_TRY(hipcub::DeviceScan::InclusiveSum(ws.ptr(Workspace::kScanTmp), tmp, counts, offs + 1, n, st));
+  return 0;
+}
+
+static int scan_offsets64(Workspace &ws, const uint64_t *counts, uint64_t *offs, uint32_t n, hipStream_t st) {
+  HIP_TRY(hipMemsetAsync(offs, 0, sizeof(uint64_t), st));
+  if (n == 0) return 0;
+  size_t tmp = 0;
+  HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, tmp, counts, offs + 1, n, st));
+  if (ws.get(Workspace::kScanTmp, tmp)) return -2;
+  HIP_TRY(hipcub::DeviceScan::InclusiveSum(ws.ptr(Workspace::kScanTmp), tmp, counts, offs + 1, n, st));
+  return 0;
+}
+
+int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes, const uint64_t *d_offs,
+                 uint32_t n, hipStream_t st, MatchOutput *out) {
+  using W = Workspace;
+  if (ws.get(W::kDCount, sizeof(uint32_t) * (n + 1)) || ws.get(W::kHCount, sizeof(uint32_t) * (n + 1)) ||
+      ws.get(W::kStatus, n + 1) || ws.get(W::kOvfList, sizeof(uint32_t) * (n + 1)) ||
+      ws.get(W::kOvfN, 64) || ws.get(W::kDOffs, sizeof(uint64_t) * (n + 1)) ||
+      ws.get(W::kHOffs, sizeof(uint64_t) * (n + 1)))
+    return -2;
+  if (!ws.host_pinned && hipHostMalloc(&ws.host_pinned, 64, hipHostMallocDefault) != hipSuccess) return -2;
+  uint64_t *hp = reinterpret_cast<uint64_t *>(ws.host_pinned);
+  auto *dcount = (uint32_t *)ws.ptr(W::kDCount);
+  auto *hcount = (uint32_t *)ws.ptr(W::kHCount);
+  auto *status = (uint8_t *)ws.ptr(W::kStatus);
+  auto *ovf_list = (uint32_t *)ws.ptr(W::kOvfList);
+  auto *ovf_n = (uint32_t *)ws.ptr(W::kOvfN);
+  auto *doffs = (uint64_t *)ws.ptr(W::kDOffs);
+  auto *hoffs = (uint64_t *)ws.ptr(W::kHOffs);
+  HIP_TRY(hipMemsetAsync(ovf_n, 0, 64, st));
+
+  const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + kWavesPerBlock - 1) / kWavesPerBlock,
+                                                                   ws.max_blocks));
+  mark(ws, 0, st);
+  if (n > 0)
+    hipLaunchKernelGGL(k_match<false>, dim3(blocks), dim3(kWave * kWavesPerBlock), 0, st, s, d_bytes, d_offs, n,
+                       dcount, hcount, status, ovf_list, ovf_n, nullptr, nullptr, nullptr, nullptr);
+  HIP_TRY(hipGetLastError());
+  mark(ws, 1, st);
+  HIP_TRY(hipMemcpyAsync(hp, ovf_n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  const uint32_t n_ovf = (uint32_t)(hp[0] & 0xFFFFFFFFu);
+  out->n_fallback = n_ovf;
+
+  const uint32_t max_levels = s.height + 1;
+  const size_t fb_lds = sizeof(uint32_t) * (((max_levels + 1) & ~1u) + 4 * (2 * max_levels + 8)) +
+                        sizeof(uint64_t) * 2 * max_levels;
+  const uint32_t fb_blocks = std::max<uint32_t>(1, std::min<uint32_t>(n_ovf, ws.max_blocks * kWavesPerBlock));
+  GEnt *tab = nullptr;
+  uint64_t *tab_off = nullptr;
+  if (n_ovf) {
+    if (ws.get(W::kRawCnt, sizeof(uint64_t) * (n_ovf + 1)) || ws.get(W::kTabOff, sizeof(uint64_t) * (n_ovf + 2)) ||
+        ws.get(W::kTabSize, sizeof(uint64_t) * (n_ovf + 1)))
+      return -2;
+    auto *raw_cnt = (uint64_t *)ws.ptr(W::kRawCnt);
+    tab_off = (uint64_t *)ws.ptr(W::kTabOff);
+    auto *tab_size = (uint64_t *)ws.ptr(W::kTabSize);
+    hipLaunchKernelGGL(k_fallback<0>, dim3(fb_blocks), dim3(kWave), fb_lds, st, s, d_bytes, d_offs, ovf_list, ovf_n,
+                       raw_cnt, hcount, dcount, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, max_levels);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_table_sizes, dim3((n_ovf + 255) / 256), dim3(256), 0, st, raw_cnt, ovf_n, tab_size);
+    HIP_TRY(hipGetLastError());
+    if (scan_offsets64(ws, tab_size, tab_off, n_ovf, st)) return -3;
+    HIP_TRY(hipMemcpyAsync(hp, tab_off + n_ovf, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    const uint64_t tab_total = hp[0];
+    if (ws.get(W::kTable, sizeof(GEnt) * (tab_total + 1))) return -2;
+    tab = (GEnt *)ws.ptr(W::kTable);
+    HIP_TRY(hipMemsetAsync(tab, 0, sizeof(GEnt) * tab_total, st));
+  }
+  if (scan_offsets(ws, hcount, hoffs, n, st)) return -3;
+  if (n_ovf) {
+    if (ws.get(W::kHOut, sizeof(uint32_t) * 1)) return -2;
+    // shared output must exist before phase 1 writes it: size it now
+    HIP_TRY(hipMemcpyAsync(hp + 1, hoffs + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (ws.get(W::kHOut, sizeof(uint32_t) * (hp[1] + 1))) return -2;
+    hipLaunchKernelGGL(k_fallback<1>, dim3(fb_blocks), dim3(kWave), fb_lds, st, s, d_bytes, d_offs, ovf_list, ovf_n,
+                       nullptr, hcount, dcount, tab_off, tab, hoffs, (uint32_t *)ws.ptr(W::kHOut), nullptr, nullptr,
+                       max_levels);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_fallback<2>, dim3(fb_blocks), dim3(kWave), fb_lds, st, s, d_bytes, d_offs, ovf_list, ovf_n,
+                       nullptr, hcount, dcount, tab_off, tab, nullptr, nullptr, nullptr, nullptr, max_levels);
+    HIP_TRY(hipGetLastError());
+  }
+  if (scan_offsets(ws, dcount, doffs, n, st)) return -3;
+  HIP_TRY(hipMemcpyAsync(hp, doffs + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(hp + 1, hoffs + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  const uint64_t D = hp[0], H = hp[1];
+  if (ws.get(W::kDOut, sizeof(uint64_t) * (D + 1)) || ws.get(W::kHOut, sizeof(uint32_t) * (H + 1))) return -2;
+  auto *dout = (uint64_t *)ws.ptr(W::kDOut);
+  auto *hout = (uint32_t *)ws.ptr(W::kHOut);
+  mark(ws, 2, st);
+  if (n > 0)
+    hipLaunchKernelGGL(k_match<true>, dim3(blocks), dim3(kWave * kWavesPerBlock), 0, st, s, d_bytes, d_offs, n,
+                       dcount, hcount, status, ovf_list, ovf_n, doffs, hoffs, dout, hout);
+  HIP_TRY(hipGetLastError());
+  mark(ws, 3, st);
+  if (n_ovf) {
+    hipLaunchKernelGGL(k_fallback<3>, dim3(fb_blocks), dim3(kWave), fb_lds, st, s, d_bytes, d_offs, ovf_list, ovf_n,
+                       nullptr, hcount, dcount, tab_off, tab, nullptr, nullptr, doffs, dout, max_levels);
+    HIP_TRY(hipGetLastError());
+  }
+  mark(ws, 4, st);
+  if (ws.profile) {
+    HIP_TRY(hipEventSynchronize(ws.ev[4]));
+    ws.prof_calls++;
+    ws.prof_fallback_topics += n_ovf;
+    ws.prof_count_ms += elapsed(ws, 0, 1);
+    ws.prof_between_ms += elapsed(ws, 1, 2);
+    ws.prof_emit_ms += elapsed(ws, 2, 3);
+    ws.prof_total_ms += elapsed(ws, 0, 4);
+  }
+  out->n_topics = n;
+  out->n_deliveries = D;
+  out->n_shared = H;
+  out->offsets = doffs;
+  out->deliveries = dout;
+  out->shared_offsets = hoffs;
+  out->shared = hout;
+  return 0;
+}
+
+}  // namespace mqm

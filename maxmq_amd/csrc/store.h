@@ -1,0 +1,106 @@
+// maxmq_amd/csrc/store.h — host-authoritative subscription/retained store.
+//
+// The mutable side of the drop-in: it keeps the reference's trie SHAPE and
+// mutation semantics (vendor/github.com/mochi-co/mqtt/v2/topics.go:303-423)
+// so Subscribe/Unsubscribe/RetainMessage return exactly what the reference
+// returns, and it is what the snapshot builder (flatten.cpp) turns into the
+// GPU-resident CSR level-trie.  Strings are interned: tokens (level keys),
+// clients and filters each get dense u32 ids in first-appearance order.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <string_view>
+#include <unordered_map>
+#include <vector>
+
+namespace mqm {
+
+struct SubRec {       // packets.Subscription (packets.go:168-178), interned
+  uint32_t client;
+  uint32_t filter;
+  int32_t ident;
+  uint8_t qos, no_local, rap, rh;
+};
+
+struct SharedRec {
+  uint32_t group;     // token id of the $SHARE group name
+  SubRec sub;
+};
+
+struct HNode {        // particle (topics.go:627-635)
+  uint32_t key = 0;   // token id
+  uint32_t parent = 0xFFFFFFFFu;
+  uint32_t first_child = 0xFFFFFFFFu, next_sibling = 0xFFFFFFFFu, prev_sibling = 0xFFFFFFFFu;
+  uint32_t n_children = 0;
+  uint32_t depth = 0;
+  bool retain_path = false;      // retainPath != ""
+  bool live = false;
+  std::vector<SubRec> subs;      // particle.subscriptions, unique by client
+  std::vector<SharedRec> shared; // particle.shared, unique by (group, client)
+};
+
+class Interner {
+ public:
+  uint32_t intern(std::string_view s);
+  uint32_t find(std::string_view s) const;  // kNone if absent
+  const std::string &name(uint32_t id) const { return names_[id]; }
+  uint32_t size() const { return (uint32_t)names_.size(); }
+
+ private:
+  std::unordered_map<std::string, uint32_t> ids_;
+  std::vector<std::string> names_;
+};
+
+struct RetainedRec {
+  uint64_t msg_ref;
+  uint32_t payload_len;
+  bool retain_flag;
+};
+
+class Store {
+ public:
+  Store();
+
+  bool subscribe(std::string_view client, std::string_view filter, uint8_t qos, uint8_t no_local, uint8_t rap,
+                 uint8_t rh, int32_t ident);                                   // topics.go:303-321
+  bool unsubscribe(std::string_view filter, std::string_view client);         // topics.go:325-349
+  int64_t retain_message(std::string_view topic, uint64_t msg_ref, uint32_t payload_len,
+                         bool retain_flag);                                    // topics.go:354-377
+  uint64_t retained_len() const { return retained_.size(); }
+
+  const Interner &tokens() const { return tokens_; }
+  const Interner &clients() const { return clients_; }
+  const Interner &filters() const { return filters_; }
+  const std::vector<HNode> &nodes() const { return nodes_; }
+  uint32_t root() const { return 0; }
+  uint32_t plus_token() const { return plus_tok_; }
+  uint32_t hash_token() const { return hash_tok_; }
+  uint32_t child(uint32_t parent, uint32_t tok) const;
+  uint64_t version() const { return version_; }
+  const std::unordered_map<std::string, RetainedRec> &retained() const { return retained_; }
+
+ private:
+  uint32_t set_path(std::string_view s, int d);          // set  (topics.go:380-397)
+  uint32_t seek_path(std::string_view s, int d) const;   // seek (topics.go:400-414)
+  void trim(uint32_t n);                                 // trim (topics.go:417-423)
+  uint32_t new_node(uint32_t parent, uint32_t tok);
+  void unlink(uint32_t n);
+
+  std::vector<HNode> nodes_;
+  std::vector<uint32_t> free_;
+  std::unordered_map<uint64_t, uint32_t> children_;  // (parent << 32 | token) -> child
+  Interner tokens_, clients_, filters_;
+  std::unordered_map<std::string, RetainedRec> retained_;  // packets.Packets (Retained)
+  uint32_t plus_tok_, hash_tok_;
+  uint64_t version_ = 0;
+};
+
+// isolateParticle (topics.go:558-577) over a byte string: level d and hasNext.
+bool isolate_particle(std::string_view s, int d, std::string_view *out);
+// strings.EqualFold(level, "$SHARE") with Go's simple folding (U+017F ~ 's')
+bool equal_fold_share(std::string_view s);
+bool is_valid_filter(std::string_view f, bool for_publish);  // topics.go:586-624
+bool is_shared_filter(std::string_view f);                   // topics.go:580-583
+
+}  // namespace mqm

@@ -1,0 +1,58 @@
+"""Helpers shared by the GPU parity tests: canonical (sorted) forms of the
+product's and the oracle's batch results so they compare bit-for-bit."""
+
+import numpy as np
+
+from maxmq_amd import capi
+
+CANON = np.dtype([("topic", "<u4"), ("client", "<u4"), ("qos", "u1"), ("no_local", "u1"), ("filter", "<u4"),
+                  ("ident", "<i4"), ("rap", "u1"), ("rh", "u1")])
+SHARED = np.dtype([("topic", "<u4"), ("filter", "<u4"), ("client", "<u4")])
+
+
+def _sort(a, keys):
+    return a[np.lexsort(tuple(a[k] for k in reversed(keys)))]
+
+
+def canon_gpu(res):
+    n = res.n
+    cnt = np.diff(res.offsets).astype(np.int64)
+    out = np.zeros(int(cnt.sum()), CANON)
+    out["topic"] = np.repeat(np.arange(n, dtype=np.uint32), cnt)
+    out["client"] = res.deliveries["client"]
+    first, qos, nl = capi.delivery_fields(res.deliveries["packed"])
+    out["qos"], out["no_local"] = qos, nl
+    info = res.sub_infos(first)
+    out["filter"], out["ident"], out["rap"], out["rh"] = info["filter"], info["identifier"], info["rap"], info["rh"]
+    scnt = np.diff(res.shared_offsets).astype(np.int64)
+    sh = np.zeros(int(scnt.sum()), SHARED)
+    sh["topic"] = np.repeat(np.arange(n, dtype=np.uint32), scnt)
+    sinfo = res.sub_infos(res.shared, shared=True)
+    sh["filter"], sh["client"] = sinfo["filter"], sinfo["client"]
+    return _sort(out, ["topic", "client"]), _sort(sh, ["topic", "filter", "client"])
+
+
+def canon_oracle(doffs, dout, soffs, sout):
+    n = len(doffs) - 1
+    cnt = np.diff(doffs).astype(np.int64)
+    out = np.zeros(int(cnt.sum()), CANON)
+    out["topic"] = np.repeat(np.arange(n, dtype=np.uint32), cnt)
+    out["client"] = dout["client"]
+    out["qos"], out["no_local"] = dout["qos"], dout["no_local"]
+    out["filter"], out["ident"], out["rap"], out["rh"] = dout["first_filter"], dout["first_ident"], dout["rap"], dout["rh"]
+    scnt = np.diff(soffs).astype(np.int64)
+    sh = np.zeros(int(scnt.sum()), SHARED)
+    sh["topic"] = np.repeat(np.arange(n, dtype=np.uint32), scnt)
+    sh["filter"], sh["client"] = sout["filter"], sout["client"]
+    return _sort(out, ["topic", "client"]), _sort(sh, ["topic", "filter", "client"])
+
+
+def assert_same(gpu, ref, what=""):
+    g, r = gpu, ref
+    if len(g) != len(r) or not np.array_equal(g, r):
+        # locate the first differing topic for a readable failure
+        n = min(len(g), len(r))
+        bad = np.nonzero(g[:n] != r[:n])[0]
+        i = int(bad[0]) if len(bad) else n
+        raise AssertionError(f"{what}: {len(g)} vs {len(r)} rows; first difference at row {i}: "
+                             f"gpu={g[i] if i < len(g) else None} ref={r[i] if i < len(r) else None}")

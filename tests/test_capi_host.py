@@ -1,0 +1,93 @@
+"""CPU tests of the product library without a GPU: the C-ABI loads and
+exports every function include/mqmatch.h declares, and the host-authoritative
+store (host-only index, MQM_DEVICE_NONE) reproduces the reference's
+Subscribe / Unsubscribe / RetainMessage return values and filter admission
+rules.  No compute (match) calls: those need the GPU."""
+
+import ctypes as C
+import os
+import random
+import re
+
+import pytest
+
+import maxmq_amd
+from maxmq_amd import capi
+from oracle import mochi_ref as pyref
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_exports_every_declared_symbol():
+    with open(os.path.join(ROOT, "include", "mqmatch.h")) as fh:
+        hdr = fh.read()
+    declared = set(re.findall(r"\b(mqm_[a-z0-9_]+)\s*\(", hdr))
+    declared -= {"mqm_index", "mqm_result"}
+    assert declared == set(capi.EXPORTED)
+    L = capi.lib()
+    for name in declared:
+        assert hasattr(L, name), name
+    assert L.mqm_version().startswith(b"mqmatch")
+
+
+def test_host_only_index_refuses_to_match():
+    idx = maxmq_amd.TopicsIndex(device=None)
+    assert idx.subscribe("c", maxmq_amd.Subscription("a/b"))
+    with pytest.raises(maxmq_amd.MqmError) as e:
+        idx.subscribers("a/b")
+    assert e.value.rc == capi.MQM_ENODEV
+    with pytest.raises(maxmq_amd.MqmError):
+        idx.commit()
+
+
+def test_mutation_kat(kat):
+    idx = maxmq_amd.TopicsIndex(device=None)
+    for op in kat["mutations"]:
+        if op[0] == "sub":
+            r = idx.subscribe(op[1], maxmq_amd.Subscription(op[2]))
+        elif op[0] == "unsub":
+            r = idx.unsubscribe(op[1], op[2])
+        else:
+            r = idx.retain_message(op[1], 1, op[2], True)
+        assert r == op[3], op
+
+
+def test_valid_and_shared_filter_kat(kat):
+    for row in kat["valid"]:
+        assert maxmq_amd.is_valid_filter(row["filter"], row["for_publish"]) == row["valid"], row
+    for f in ["$SHARE/g/a", "$share/g/a", "$ſhare/g/a", "$SHAREx/a", "a/$SHARE", "$SHARE"]:
+        assert maxmq_amd.is_shared_filter(f) == pyref.is_shared_filter(f), f
+
+
+def _level(rng):
+    return rng.choice(["a", "b", "", "+", "#", "$SYS", "$SHARE", "$share", "$ſhare", "g", "x" * 20])
+
+
+def test_random_mutations_match_python_oracle():
+    rng = random.Random(7)
+    for trial in range(20):
+        idx = maxmq_amd.TopicsIndex(device=None)
+        py = pyref.TopicsIndex()
+        for step in range(300):
+            f = "/".join(_level(rng) for _ in range(rng.randint(1, 4)))
+            c = f"k{rng.randint(0, 4)}"
+            op = rng.random()
+            if op < 0.55:
+                r1 = idx.subscribe(c, maxmq_amd.Subscription(f, qos=rng.randint(0, 2)))
+                r2 = py.subscribe(c, pyref.Sub(f))
+            elif op < 0.85:
+                r1, r2 = idx.unsubscribe(f, c), py.unsubscribe(f, c)
+            else:
+                t = f.replace("+", "p").replace("#", "h")
+                pl = rng.choice([0, 0, 4])
+                r1, r2 = idx.retain_message(t, step, pl), py.retain_message(t, step, pl)
+            assert r1 == r2, (trial, step, f, c, op)
+        assert idx.retained_len() == len(py.retained)
+
+
+def test_interning_order_is_first_appearance():
+    idx = maxmq_amd.TopicsIndex(device=None)
+    for c, f in [("zed", "a"), ("amy", "b"), ("zed", "c")]:
+        idx.subscribe(c, maxmq_amd.Subscription(f))
+    assert [idx.client_name(i) for i in range(idx.num_clients())] == ["zed", "amy"]
+    assert [idx.filter_name(i) for i in range(3)] == ["a", "b", "c"]

@@ -1,0 +1,223 @@
+"""GPU parity tests (MI355X): the HIP match path, called through the C ABI,
+against the hand-derived known-answer table, the frozen golden fixture, the C
+oracle on the same seeded inputs, and size-independent properties at the
+BASELINE sizes.  Bit-exact: every (topic, client, max QoS, NoLocal, first
+filter, its identifier, RAP, RH) row and every shared (topic, filter, client)
+candidate must be identical."""
+
+import os
+import random
+
+import numpy as np
+import pytest
+
+import maxmq_amd
+from maxmq_amd import capi
+from oracle import mochi_ref as pyref
+from oracle.binding import OracleIndex
+from tests.gpu_util import assert_same, canon_gpu, canon_oracle
+from tools import mqgen
+from tools.mqgen import Strings
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _gpu_and_oracle(filters, topics, clients=None, subs=None):
+    idx = maxmq_amd.TopicsIndex(0)
+    ora = OracleIndex()
+    for i, f in enumerate(filters):
+        c = clients[i] if clients else f"c{i}"
+        q, nl, rap, rh, ident = subs[i] if subs else (i % 3, 0, 0, 0, 0)
+        idx.subscribe(c, maxmq_amd.Subscription(f, q, ident, bool(nl), bool(rap), rh))
+        ora.subscribe(c, f, q, nl, rap, rh, ident)
+    s = Strings.from_list(topics)
+    res = idx.match_batch(s.data, s.offs)
+    g, gs = canon_gpu(res)
+    r, rs = canon_oracle(*ora.match(s.data, s.offs)[:4])
+    return (g, gs), (r, rs), res
+
+
+def test_kat_forward(kat):
+    for case in kat["forward"]:
+        idx = maxmq_amd.TopicsIndex(0)
+        for i, f in enumerate(case["filters"]):
+            idx.subscribe(f"c{i}", maxmq_amd.Subscription(f, qos=1))
+        got = idx.subscribers(case["topic"])
+        assert sorted(s.filter for s in got.subscriptions.values()) == sorted(case["subs"]), case
+        assert sorted(got.shared) == sorted(case["shared"]), case
+
+
+def test_kat_merge(kat):
+    for case in kat["merge"]:
+        idx = maxmq_amd.TopicsIndex(0)
+        for c, f, q, nl, rap, rh, ident in case["subs"]:
+            idx.subscribe(c, maxmq_amd.Subscription(f, q, ident, bool(nl), bool(rap), rh))
+        got = idx.subscribers(case["topic"])
+        out = {c: dict(qos=s.qos, no_local=int(s.no_local), first=s.filter, first_ident=s.identifier,
+                       rap=int(s.retain_as_published), rh=s.retain_handling) for c, s in got.subscriptions.items()}
+        assert out == case["expect"], case
+
+
+def test_golden_fixture():
+    z = np.load(os.path.join(ROOT, "tests", "golden", "c1_fixture.npz"))
+    idx = maxmq_amd.TopicsIndex(0)
+    fs, cs = Strings(z["filters_data"], z["filters_offs"]), Strings(z["clients_data"], z["clients_offs"])
+
+    class W:  # the subset of tools.mqgen.Workload subscribe_workload reads
+        filters, clients = fs, cs
+        qos, no_local, rap, rh, ident = z["qos"], z["no_local"], z["rap"], z["rh"], z["ident"]
+
+    idx.subscribe_workload(W)
+    res = idx.match_batch(z["topics_data"], z["topics_offs"])
+    g, gs = canon_gpu(res)
+    dout = np.zeros(len(z["dclient"]), dtype=[("client", "<u4"), ("first_filter", "<u4"), ("first_ident", "<i4"),
+                                              ("qos", "u1"), ("no_local", "u1"), ("rap", "u1"), ("rh", "u1")])
+    dout["client"], dout["first_filter"], dout["first_ident"] = z["dclient"], z["dfilter"], z["dident"]
+    dout["qos"], dout["no_local"], dout["rap"], dout["rh"] = z["dqos"], z["dno_local"], z["drap"], z["drh"]
+    sout = np.zeros(len(z["sclient"]), dtype=[("filter", "<u4"), ("client", "<u4")])
+    sout["filter"], sout["client"] = z["sfilter"], z["sclient"]
+    r, rs = canon_oracle(z["doffs"], dout, z["soffs"], sout)
+    assert_same(g, r, "deliveries")
+    assert_same(gs, rs, "shared")
+
+
+@pytest.mark.parametrize("config,overrides", [
+    (1, {}),                                   # BASELINE configs[0]: 10k filters, 100k topics
+    (5, dict(n_filters=200000, n_topics=200000)),  # shared subscriptions + MQTT 5 options
+])
+def test_config_vs_oracle(config, overrides):
+    w = mqgen.generate(config, **overrides)
+    idx = maxmq_amd.TopicsIndex(0)
+    idx.subscribe_workload(w)
+    ora = OracleIndex()
+    ora.subscribe_workload(w)
+    res = idx.match_batch(w.topics.data, w.topics.offs)
+    g, gs = canon_gpu(res)
+    r, rs = canon_oracle(*ora.match(w.topics.data, w.topics.offs, nthreads=16)[:4])
+    assert len(r) > 0
+    assert_same(g, r, "deliveries")
+    assert_same(gs, rs, "shared")
+
+
+def test_edge_cases_and_fallback_paths():
+    filters, clients, topics = [], [], []
+    # hub: 1000 clients on a/# and a/b -> S > 384 per topic (global dedupe path)
+    for i in range(1000):
+        filters += ["hub/#", "hub/x"]
+        clients += [f"h{i}", f"h{i}"]
+    topics += ["hub/x", "hub", "hub/x/y"]
+    # deep topics (> 16 levels) and deep filters (walk beyond the LDS level cache)
+    deep = "/".join(f"l{i}" for i in range(40))
+    filters += [deep, "/".join(["+"] * 20) + "/#", "l0/#", "/".join(f"l{i}" for i in range(25)) + "/#"]
+    clients += ["d1", "d2", "d3", "d4"]
+    topics += [deep, deep + "/z", "/".join(f"l{i}" for i in range(18))]
+    # long tokens (>= 16 bytes: hashed key + byte verification)
+    lt = "x" * 40
+    filters += [f"{lt}/a", f"{lt}/+", "y" * 16, "z" * 15]
+    clients += ["t1", "t2", "t3", "t4"]
+    topics += [f"{lt}/a", f"{lt[:-1]}y/a", "y" * 16, "y" * 17, "z" * 15]
+    # frontier blow-up: every {a, +} combination over 6 levels under w/
+    for m in range(64):
+        filters.append("w/" + "/".join("+" if (m >> k) & 1 else "a" for k in range(6)))
+        clients.append(f"f{m % 7}")
+    topics += ["w/a/a/a/a/a/a", "w/a/a/a/a/a/a/a"]
+    # many shared groups on one node (> 32 shared hits is not a thing: one node
+    # -> one hit; but many nodes with shared subs along a wildcard walk)
+    for g in range(50):
+        filters += [f"$SHARE/g{g}/s/+", f"$share/g{g}/s/#"]
+        clients += [f"s{g}", f"s{g}"]
+    topics += ["s/q", "s", "$SYS/s"]
+    # '$' rules, empty levels, unicode
+    filters += ["#", "+/+", "$SYS/#", "+", "/", "é/ü/+", "$SHARE/g/#"]
+    clients += ["u1", "u2", "u3", "u4", "u5", "u6", "u7"]
+    topics += ["$SYS/x", "$x", "/", "//", "", "é/ü/ß", "a", "$", "a/+", "a/#"]
+    (g, gs), (r, rs), res = _gpu_and_oracle(filters, topics, clients)
+    assert_same(g, r, "deliveries")
+    assert_same(gs, rs, "shared")
+
+
+def test_random_ops_with_autocommit():
+    rng = random.Random(99)
+    levels = ["a", "b", "", "+", "#", "$SYS", "$x", "c" * 18]
+    for trial in range(8):
+        idx = maxmq_amd.TopicsIndex(0)
+        py = pyref.TopicsIndex()
+        for step in range(400):
+            f = "/".join(rng.choice(levels) for _ in range(rng.randint(1, 5)))
+            c = f"k{rng.randint(0, 7)}"
+            if rng.random() < 0.7:
+                q = rng.randint(0, 2)
+                assert idx.subscribe(c, maxmq_amd.Subscription(f, q)) == py.subscribe(c, pyref.Sub(f, q))
+            else:
+                assert idx.unsubscribe(f, c) == py.unsubscribe(f, c)
+            if step % 50 == 49:
+                topics = ["/".join(rng.choice(["a", "b", "", "$SYS", "$x", "c" * 18]) for _ in range(rng.randint(1, 6)))
+                          for _ in range(50)]
+                s = Strings.from_list(topics)
+                res = idx.match_batch(s.data, s.offs)
+                for i, t in enumerate(topics):
+                    subs, shared = py.subscribers(t)
+                    lo, hi = res.offsets[i], res.offsets[i + 1]
+                    _, qos, _ = capi.delivery_fields(res.deliveries["packed"][lo:hi])
+                    got = sorted((idx.client_name(int(cl)), int(q)) for cl, q in zip(res.deliveries["client"][lo:hi], qos))
+                    assert got == sorted((k, v.qos) for k, v in subs.items()), (trial, step, t)
+
+
+def test_full_size_c2_properties():
+    """BASELINE configs[1] at full size (1M filters, 10M topics): exact
+    agreement with the oracle on a 100k-topic sample, and size-independent
+    properties over the whole batch (CSR monotone, per-topic clients unique and
+    within range, QoS <= 2, deterministic across two runs)."""
+    w = mqgen.generate(2)
+    idx = maxmq_amd.TopicsIndex(0)
+    idx.subscribe_workload(w)
+    idx.commit()
+    import torch
+
+    dev = torch.device("cuda:0")
+    tb = torch.from_numpy(w.topics.data).to(dev)
+    to = torch.from_numpy(w.topics.offs.view(np.int64)).to(dev)
+    n = len(w.topics)
+    r1 = idx.match_device(tb.data_ptr(), to.data_ptr(), n)
+    torch.cuda.synchronize()
+    nd = int(r1.n_deliveries)
+    offs = _dev_copy(r1.offsets, (n + 1) * 8).view(np.uint64)
+    ents = _dev_copy(r1.deliveries, nd * 8).view(np.uint64)
+    r2 = idx.match_device(tb.data_ptr(), to.data_ptr(), n)
+    torch.cuda.synchronize()
+    assert int(r2.n_deliveries) == nd
+    assert np.array_equal(_dev_copy(r2.deliveries, nd * 8).view(np.uint64), ents)
+    assert offs[0] == 0 and offs[-1] == nd and np.all(np.diff(offs.astype(np.int64)) >= 0)
+    clients = (ents & 0xFFFFFFFF).astype(np.uint32)
+    assert clients.max() < idx.num_clients()
+    assert np.all(((ents >> 60) & 3) <= 2)
+    tid = np.repeat(np.arange(n, dtype=np.uint64), np.diff(offs.astype(np.int64)))
+    key = (tid << np.uint64(32)) | clients.astype(np.uint64)
+    assert len(np.unique(key)) == nd, "a client appears twice in one topic"
+    # exact agreement on a deterministic sample of topics
+    rng = np.random.default_rng(5)
+    sample = np.sort(rng.choice(n, size=100000, replace=False))
+    sub = Strings.from_list([w.topics[int(i)] for i in sample])
+    ora = OracleIndex()
+    ora.subscribe_workload(w)
+    r, rs = canon_oracle(*ora.match(sub.data, sub.offs, nthreads=16)[:4])
+    res = idx.match_batch(sub.data, sub.offs)
+    g, gs = canon_gpu(res)
+    assert_same(g, r, "deliveries (sample)")
+    assert_same(gs, rs, "shared (sample)")
+
+
+def _dev_copy(ptr, nbytes):
+    import ctypes
+
+    import torch
+
+    out = np.empty(nbytes, np.uint8)
+    if nbytes:
+        torch.cuda.synchronize()
+        hip = ctypes.CDLL("libamdhip64.so")
+        rc = hip.hipMemcpy(ctypes.c_void_p(out.ctypes.data), ctypes.c_void_p(ptr), ctypes.c_size_t(nbytes),
+                           ctypes.c_int(2))
+        assert rc == 0
+    return out
