@@ -84,6 +84,16 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
                            "(there is no non-HIP implementation of the match path)")
+    # One HIP runtime per process.  PyTorch-ROCm ships its own libamdhip64 /
+    # libhsa-runtime64 (same SONAMEs as /opt/rocm's).  If libmqmatch loaded
+    # /opt/rocm's copy first, a later `import torch` would map a second HSA
+    # runtime and torch would see no GPU.  Importing torch first makes the
+    # dynamic linker bind libmqmatch to torch's copy (SONAME match), so torch
+    # tensors, streams and torch.distributed/RCCL share the device with us.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     vp, sz, u32, u64, i32, cp = C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint64, C.c_int32, C.c_char_p
     sigs = {

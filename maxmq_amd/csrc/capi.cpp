@@ -313,7 +313,7 @@ int mqm_result_sub_infos(const mqm_result *r, int shared, const uint32_t *subs, 
 
 void mqm_result_free(mqm_result *r) { delete r; }
 
-static int copy_name(const std::string &s, char *buf, size_t cap, size_t *len) {
+static int copy_name(std::string_view s, char *buf, size_t cap, size_t *len) {
   if (len) *len = s.size();
   if (buf && cap) memcpy(buf, s.data(), s.size() < cap ? s.size() : cap);
   return MQM_OK;

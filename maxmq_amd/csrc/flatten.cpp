@@ -78,7 +78,7 @@ int flatten(const Store &st, HostSnapshot *out) {
     if (i > 0) {
       const uint32_t parent_new = new_id[h.parent];
       if (parent_new == 0) {  // root child: Filter[0] of every sub stored below it
-        const std::string &k = st.tokens().name(h.key);
+        const std::string_view k = st.tokens().name(h.key);
         if (!k.empty() && (k[0] == '+' || k[0] == '#')) f |= kFlagDollarWild;
       } else {
         f |= flags[parent_new] & kFlagDollarWild;
@@ -115,7 +115,7 @@ int flatten(const Store &st, HostSnapshot *out) {
     for (uint32_t c = nodes[order[i]].first_child; c != kNone; c = nodes[c].next_sibling) {
       const uint32_t cn = new_id[c];
       if (cn == pc || cn == hc) continue;
-      const std::string &tok = st.tokens().name(nodes[c].key);
+      const std::string_view tok = st.tokens().name(nodes[c].key);
       Key k = make_key([&](uint32_t j) { return (uint8_t)tok[j]; }, (uint32_t)tok.size());
       EdgeEntry e;
       e.k0 = k.k0;

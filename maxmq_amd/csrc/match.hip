@@ -318,9 +318,11 @@ __global__ __launch_bounds__(kWave *kWavesPerBlock) void k_match(
     }
 
     // ---- 4. dedupe in the LDS table ---------------------------------------
+    // load <= 0.5 up to kTCap/2 entries, <= 0.75 above (kSMax = 3/4 kTCap)
     uint32_t lg = 6;
-    while ((1u << lg) < 2 * S) lg++;
+    while ((1u << lg) < 2 * S && (1u << lg) < (uint32_t)kTCap) lg++;
     const uint32_t tsize = 1u << lg;
+    static_assert(kSMax * 4 <= kTCap * 3, "dedupe table load factor");
     for (uint32_t i = lane; i < tsize; i += kWave) L.tkey[i] = 0, L.tval[i] = 0;
     wave_lds_sync();
     for (uint32_t r = lane; r < S; r += kWave) {
@@ -388,7 +390,7 @@ __global__ __launch_bounds__(kWave *kWavesPerBlock) void k_match(
 // ---------------------------------------------------------------------------
 struct GEnt {  // global dedupe slot (16 B)
   unsigned long long keybits;  // (client + 1) | bits << 32
-  unsigned long long first;    // (rank << 32) | sid, atomicMin
+  unsigned long long first;    // ~((rank << 32) | sid), atomicMax: the table starts zeroed
 };
 
 template <int kPhase>
@@ -429,7 +431,7 @@ __global__ __launch_bounds__(kWave) void k_fallback(
         if (kPhase == 3 && occ) {
           const uint32_t bits = (uint32_t)(g.keybits >> 32);
           dout[dbase + D + __popcll(m & lanemask_lt(lane))] =
-              pack_delivery((uint32_t)g.keybits - 1, (uint32_t)g.first, 31u - __builtin_clz(bits & 7u),
+              pack_delivery((uint32_t)g.keybits - 1, (uint32_t)~g.first, 31u - __builtin_clz(bits & 7u),
                             (bits >> 3) & 1u);
         }
         D += __popcll(m);
@@ -538,7 +540,7 @@ __global__ __launch_bounds__(kWave) void k_fallback(
               }
               const uint32_t bits = (1u << (se.meta & 3)) | (((se.meta >> 2) & 1) << 3);
               atomicOr(&T[slot].keybits, (unsigned long long)bits << 32);
-              atomicMin(&T[slot].first, ((unsigned long long)rank << 32) | sid);
+              atomicMax(&T[slot].first, ~(((unsigned long long)rank << 32) | sid));
             }
           }
         }

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cstddef>
+#include <cstring>
 
 #include "keys.h"
 
@@ -84,18 +85,59 @@ bool is_valid_filter(std::string_view f, bool for_publish) {
   return true;
 }
 
+static uint64_t hash_sv(std::string_view s) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ (s.size() * 0xff51afd7ed558ccdull);
+  size_t i = 0;
+  for (; i + 8 <= s.size(); i += 8) {
+    uint64_t w;
+    memcpy(&w, s.data() + i, 8);
+    h = fmix64(h ^ w) * 0x87c37b91114253d5ull;
+  }
+  uint64_t w = 0;
+  memcpy(&w, s.data() + i, s.size() - i);
+  return fmix64(h ^ w ^ 0x4cf5ad432745937full);
+}
+
+// slot holding s, or the empty slot where it would go
+uint64_t Interner::slot_of(std::string_view s, uint64_t h) const {
+  const uint64_t mask = table_.size() - 1;
+  const uint64_t tag = h >> 32;
+  for (uint64_t i = h & mask;; i = (i + 1) & mask) {
+    const uint64_t e = table_[i];
+    if (e == 0) return i;
+    if ((e >> 32) == tag && name((uint32_t)(e & 0xFFFFFFFFu) - 1) == s) return i;
+  }
+}
+
+void Interner::grow() {
+  std::vector<uint64_t> old;
+  old.swap(table_);
+  table_.assign(old.empty() ? 1024 : old.size() * 2, 0);
+  const uint64_t mask = table_.size() - 1;
+  for (uint64_t e : old) {
+    if (!e) continue;
+    uint64_t i = hash_sv(name((uint32_t)(e & 0xFFFFFFFFu) - 1)) & mask;
+    while (table_[i]) i = (i + 1) & mask;
+    table_[i] = e;
+  }
+}
+
 uint32_t Interner::intern(std::string_view s) {
-  auto it = ids_.find(std::string(s));
-  if (it != ids_.end()) return it->second;
-  uint32_t id = (uint32_t)names_.size();
-  names_.emplace_back(s);
-  ids_.emplace(names_.back(), id);
+  if ((size() + 1) * 2 > table_.size()) grow();
+  const uint64_t h = hash_sv(s);
+  const uint64_t i = slot_of(s, h);
+  if (table_[i]) return (uint32_t)(table_[i] & 0xFFFFFFFFu) - 1;
+  const uint32_t id = size();
+  arena_.insert(arena_.end(), s.begin(), s.end());
+  offs_.push_back(arena_.size());
+  table_[i] = ((h >> 32) << 32) | (uint64_t)(id + 1);
   return id;
 }
 
 uint32_t Interner::find(std::string_view s) const {
-  auto it = ids_.find(std::string(s));
-  return it == ids_.end() ? kNone : it->second;
+  if (table_.empty()) return kNone;
+  const uint64_t i = slot_of(s, hash_sv(s));
+  return table_[i] ? (uint32_t)(table_[i] & 0xFFFFFFFFu) - 1 : kNone;
 }
 
 Store::Store() {

@@ -40,16 +40,24 @@ struct HNode {        // particle (topics.go:627-635)
   std::vector<SharedRec> shared; // particle.shared, unique by (group, client)
 };
 
+// string -> dense id, first-appearance order.  Bytes live in one arena; the
+// index is an open-addressed table of (hash, id) probed with string_views, so
+// lookups allocate nothing.
 class Interner {
  public:
   uint32_t intern(std::string_view s);
   uint32_t find(std::string_view s) const;  // kNone if absent
-  const std::string &name(uint32_t id) const { return names_[id]; }
-  uint32_t size() const { return (uint32_t)names_.size(); }
+  std::string_view name(uint32_t id) const {
+    return std::string_view(arena_.data() + offs_[id], offs_[id + 1] - offs_[id]);
+  }
+  uint32_t size() const { return (uint32_t)(offs_.size() - 1); }
 
  private:
-  std::unordered_map<std::string, uint32_t> ids_;
-  std::vector<std::string> names_;
+  uint64_t slot_of(std::string_view s, uint64_t h) const;
+  void grow();
+  std::vector<char> arena_;
+  std::vector<uint64_t> offs_{0};
+  std::vector<uint64_t> table_;  // (hash high 32 bits << 32) | (id + 1); 0 = empty
 };
 
 struct RetainedRec {
