@@ -93,6 +93,7 @@ typedef struct {
   const uint64_t *shared_offsets; /* device, n_topics + 1                       */
   const uint32_t *shared;         /* device: shared-subscription ids            */
   uint32_t n_fallback;            /* topics routed through the unbounded path   */
+  uint32_t n_big;                 /* topics deduplicated by the workgroup tier  */
 } mqm_device_result;
 
 /* ---- lifecycle: NewTopicsIndex (topics.go:291-299) ---------------------- */
@@ -164,9 +165,9 @@ int mqm_snapshot_stats_get(mqm_index *h, mqm_snapshot_stats *out);
 typedef struct {
   uint64_t calls;           /* match calls while enabled                        */
   uint64_t fallback_topics; /* topics that took the unbounded path              */
-  double count_ms;          /* walk + dedupe, count pass (k_match<false>)        */
-  double emit_ms;           /* walk + dedupe + write pass (k_match<true>)        */
-  double between_ms;        /* scans, fallback phases 0-2 and host syncs between */
+  double walk_ms;           /* k_walk: tokenize + walk + per-wave dedupe/emit     */
+  double dedupe_ms;         /* k_big + DFS path (+ one host sync), after k_walk   */
+  double compact_ms;        /* k_compact: raw chunks -> topic-ordered CSR         */
   double total_ms;          /* first to last kernel of each call, summed          */
 } mqm_profile;
 int mqm_profile_enable(mqm_index *h, int on); /* resets the accumulators */

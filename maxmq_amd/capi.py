@@ -61,7 +61,7 @@ class SubInfo(C.Structure):
 class DeviceResult(C.Structure):
     _fields_ = [("n_topics", C.c_uint32), ("n_deliveries", C.c_uint64), ("n_shared", C.c_uint64),
                 ("offsets", C.c_void_p), ("deliveries", C.c_void_p), ("shared_offsets", C.c_void_p),
-                ("shared", C.c_void_p), ("n_fallback", C.c_uint32)]
+                ("shared", C.c_void_p), ("n_fallback", C.c_uint32), ("n_big", C.c_uint32)]
 
 
 class SnapshotStats(C.Structure):
@@ -70,8 +70,8 @@ class SnapshotStats(C.Structure):
 
 
 class Profile(C.Structure):
-    _fields_ = [("calls", C.c_uint64), ("fallback_topics", C.c_uint64), ("count_ms", C.c_double),
-                ("emit_ms", C.c_double), ("between_ms", C.c_double), ("total_ms", C.c_double)]
+    _fields_ = [("calls", C.c_uint64), ("fallback_topics", C.c_uint64), ("walk_ms", C.c_double),
+                ("dedupe_ms", C.c_double), ("compact_ms", C.c_double), ("total_ms", C.c_double)]
 
 
 _LIB = None

@@ -99,9 +99,9 @@ int mqm_profile_read(mqm_index *h, mqm_profile *out) {
   std::lock_guard<std::mutex> g(h->mu);
   out->calls = h->ws.prof_calls;
   out->fallback_topics = h->ws.prof_fallback_topics;
-  out->count_ms = h->ws.prof_count_ms;
-  out->emit_ms = h->ws.prof_emit_ms;
-  out->between_ms = h->ws.prof_between_ms;
+  out->walk_ms = h->ws.prof_walk_ms;
+  out->dedupe_ms = h->ws.prof_big_ms;
+  out->compact_ms = h->ws.prof_compact_ms;
   out->total_ms = h->ws.prof_total_ms;
   return MQM_OK;
 }
@@ -225,6 +225,7 @@ int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t 
     out->shared_offsets = mo.shared_offsets;
     out->shared = mo.shared;
     out->n_fallback = mo.n_fallback;
+    out->n_big = mo.n_big;
     return MQM_OK;
   });
 }

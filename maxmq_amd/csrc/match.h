@@ -11,8 +11,8 @@ namespace mqm {
 // Grow-only device buffers reused across batches (no allocation in steady state).
 struct Workspace {
   enum Slot {
-    kDCount, kHCount, kStatus, kOvfList, kOvfN, kDOffs, kHOffs, kDOut, kHOut,
-    kScanTmp, kRawCnt, kTabOff, kTabSize, kTable, kInBytes, kInOffs, kNumSlots
+    kDCount, kHCount, kDStart, kHStart, kTier, kDfsList, kCounters, kDBuf, kHBuf, kBigRecs,
+    kDOffs, kHOffs, kDOut, kHOut, kScanTmp, kRawCnt, kTabOff, kTabSize, kTable, kInBytes, kInOffs, kNumSlots
   };
   struct Buf {
     void *p = nullptr;
@@ -20,16 +20,18 @@ struct Workspace {
   };
   Buf bufs[kNumSlots];
   void *host_pinned = nullptr;
-  uint32_t max_blocks = 2048;  // main-path grid cap (grid-stride beyond)
+  uint32_t max_blocks = 2048;  // walk-kernel grid cap (grid-stride beyond)
+  // capacities (entries) of the chunk-allocated raw buffers; grown on overflow
+  uint64_t dcap = 0, hcap = 0, bcap = 0;
 
   // optional kernel timing (mqm_profile_*): events on the launch stream
   bool profile = false;
-  hipEvent_t ev[5] = {};  // 0 start, 1 count done, 2 emit start, 3 emit done, 4 end
+  hipEvent_t ev[5] = {};  // 0 start, 1 walk done, 2 big/fallback done, 3 compaction start, 4 end
   uint64_t prof_calls = 0, prof_fallback_topics = 0;
-  double prof_count_ms = 0, prof_emit_ms = 0, prof_between_ms = 0, prof_total_ms = 0;
+  double prof_walk_ms = 0, prof_big_ms = 0, prof_compact_ms = 0, prof_total_ms = 0;
   void reset_profile() {
     prof_calls = prof_fallback_topics = 0;
-    prof_count_ms = prof_emit_ms = prof_between_ms = prof_total_ms = 0;
+    prof_walk_ms = prof_big_ms = prof_compact_ms = prof_total_ms = 0;
   }
 
   static int reserve(void **p, size_t *cap, size_t need);
@@ -45,10 +47,12 @@ struct MatchOutput {
   const uint64_t *deliveries = nullptr;  // device, packed (snapshot.h)
   const uint64_t *shared_offsets = nullptr;
   const uint32_t *shared = nullptr;
-  uint32_t n_fallback = 0;
+  uint32_t n_fallback = 0;  // topics on the unbounded DFS path
+  uint32_t n_big = 0;       // topics deduplicated by the workgroup tier
 };
 
-// Runs count -> scan -> emit on `st`; returns 0 or a negative MQM_E* code.
+// Runs walk -> big-topic dedupe -> (DFS fallback) -> scan -> compaction on
+// `st`; returns 0 or a negative MQM_E* code.
 int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes, const uint64_t *d_offs,
                  uint32_t n, hipStream_t st, MatchOutput *out);
 

@@ -129,9 +129,10 @@ extern "C" void mqgen_default_params(int config, mqgen_params *p) {
       p->p_plus = 0.40;
       p->p_hash = 0.10;
       p->topic_zipf_s = 1.2;
-      p->vocab[0] = 256;
-      p->vocab[1] = 4096;
-      for (int i = 2; i < 8; i++) p->vocab[i] = 16384;
+      p->token_zipf_s = 0.8;
+      p->vocab[0] = 4096;
+      p->vocab[1] = 16384;
+      for (int i = 2; i < 8; i++) p->vocab[i] = 65536;
       break;
     case 4:
       p->n_filters = 100000000;
@@ -196,7 +197,7 @@ extern "C" int mqgen_generate(const mqgen_params *p, mqgen_workload *out) {
     } else {
       uint32_t m = draw_depth(rng);
       for (uint32_t d = 0; d < m; d++) lv.push_back(voc.tok[d][voc.z[d].draw(rng)]);
-      if (rng.uniform() < p->p_plus) {
+      if (m >= 2 && rng.uniform() < p->p_plus) {  // a depth-1 "+" would match every topic
         int nplus = (m >= 4 && rng.uniform() < p->p_plus) ? 2 : 1;  // "a/+/+"-style filters only when deep
         for (int k = 0; k < nplus; k++) {
           // level 0 becomes '+' rarely (a root '+' matches every topic)
