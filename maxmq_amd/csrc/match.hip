@@ -65,6 +65,7 @@ struct Counters {              // zeroed before every batch
   unsigned long long dpos;     // deliveries bump pointer (entries)
   unsigned long long hpos;     // shared candidates bump pointer
   unsigned long long bpos;     // big-topic records bump pointer
+  unsigned long long miss[3];  // entries requested after a buffer ran out (sizes the retry)
   unsigned int n_dfs;          // topics appended to the DFS list
   unsigned int overflow;       // 1: deliveries, 2: shared, 4: records
 };
@@ -163,14 +164,16 @@ __device__ __forceinline__ uint32_t find_hit(const uint32_t *pre, uint32_t nh, u
 }
 
 // Per-wave bump allocation from a global counter in chunks (wave-uniform).
+// Once the buffer is exhausted the wave only tallies what it still needed.
 struct WaveAlloc {
   uint64_t cur = 0, end = 0;
+  bool dead = false;
 };
 
 __device__ uint64_t wave_alloc(WaveAlloc &a, uint64_t need, unsigned long long *counter, uint64_t cap, uint32_t chunk,
-                               unsigned int *overflow, unsigned int bit, int lane) {
+                               Counters *ctr, unsigned int which, int lane) {
   if (need == 0) return 0;
-  if (a.cur + need > a.end) {
+  if (!a.dead && a.cur + need > a.end) {
     const uint64_t grab = need > chunk ? need : chunk;
     uint64_t base = 0;
     if (lane == 0) base = atomicAdd(counter, (unsigned long long)grab);
@@ -178,10 +181,13 @@ __device__ uint64_t wave_alloc(WaveAlloc &a, uint64_t need, unsigned long long *
     a.cur = base;
     a.end = base + grab;
     if (a.end > cap) {
-      if (lane == 0) atomicOr(overflow, bit);
-      a.cur = a.end;  // stay exhausted; every later request retries and fails
-      return kNoSpace;
+      if (lane == 0) atomicOr(&ctr->overflow, 1u << which);
+      a.dead = true;
     }
+  }
+  if (a.dead) {
+    if (lane == 0) atomicAdd(&ctr->miss[which], (unsigned long long)need);
+    return kNoSpace;
   }
   const uint64_t r = a.cur;
   a.cur += need;
@@ -400,7 +406,7 @@ __global__ __launch_bounds__(kWave *kWavesPerBlock, 6) void k_walk(DeviceSnapsho
     // ---- shared candidates (gatherSharedSubscriptions, topics.go:541-555) ---
     uint32_t H = 0;
     for (uint32_t i = 0; i < nsh; i++) H += L.sh_cnt[i];
-    const uint64_t hb = wave_alloc(ha, H, &o.ctr->hpos, caps.hcap, caps.hchunk, &o.ctr->overflow, 2, lane);
+    const uint64_t hb = wave_alloc(ha, H, &o.ctr->hpos, caps.hcap, caps.hchunk, o.ctr, 1, lane);
     if (hb != kNoSpace) {
       uint32_t w = 0;
       for (uint32_t i = 0; i < nsh; i++) {
@@ -415,7 +421,7 @@ __global__ __launch_bounds__(kWave *kWavesPerBlock, 6) void k_walk(DeviceSnapsho
     }
 
     if (S > (uint32_t)kSMax) {  // -> workgroup tier: leave the ordered hit list in a record
-      const uint64_t rb = wave_alloc(ba, 1, &o.ctr->bpos, caps.bcap, caps.bchunk, &o.ctr->overflow, 4, lane);
+      const uint64_t rb = wave_alloc(ba, 1, &o.ctr->bpos, caps.bcap, caps.bchunk, o.ctr, 2, lane);
       if (rb != kNoSpace) {
         uint32_t *rec = o.recs + rb * kRecWords;
         uint32_t v = 0;
@@ -455,7 +461,7 @@ __global__ __launch_bounds__(kWave *kWavesPerBlock, 6) void k_walk(DeviceSnapsho
     wave_lds_sync();
 
     // ---- 5. winners -> deliveries (space for S reserved, D <= S used) -------
-    const uint64_t db = wave_alloc(da, S, &o.ctr->dpos, caps.dcap, caps.dchunk, &o.ctr->overflow, 1, lane);
+    const uint64_t db = wave_alloc(da, S, &o.ctr->dpos, caps.dcap, caps.dchunk, o.ctr, 0, lane);
     uint32_t D = 0;
     for (uint32_t r0 = 0; r0 < S; r0 += kWave) {
       const uint32_t r = r0 + lane;
@@ -496,6 +502,7 @@ __global__ __launch_bounds__(kBigThreads) void k_big(DeviceSnapshot s, Outputs o
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
   const uint64_t nrec = o.ctr->bpos < caps.bcap ? o.ctr->bpos : caps.bcap;
   uint64_t cur = 0, end = 0;  // block chunk allocator (thread 0)
+  bool dead = false;
   for (uint64_t ri = blockIdx.x; ri < nrec; ri += gridDim.x) {
     if (tid < kRecWords) rec[tid] = o.recs[ri * kRecWords + tid];
     __syncthreads();
@@ -524,17 +531,18 @@ __global__ __launch_bounds__(kBigThreads) void k_big(DeviceSnapshot s, Outputs o
     }
     // space for S entries from the block's chunk
     if (tid == 0) {
-      if (cur + S > end) {
+      if (!dead && cur + S > end) {
         const uint64_t grab = S > caps.dchunk ? S : caps.dchunk;
         cur = atomicAdd(&o.ctr->dpos, (unsigned long long)grab);
         end = cur + grab;
         if (end > caps.dcap) {
           atomicOr(&o.ctr->overflow, 1u);
-          cur = end;
+          dead = true;
         }
       }
-      blk_base = (cur + S <= end && end <= caps.dcap) ? cur : kNoSpace;
-      if (blk_base != kNoSpace) cur += S;
+      if (dead) atomicAdd(&o.ctr->miss[0], (unsigned long long)S);
+      blk_base = dead ? kNoSpace : cur;
+      if (!dead) cur += S;
     }
     __syncthreads();
     const uint64_t db = blk_base;
@@ -613,7 +621,10 @@ __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *
       if (lane == 0 && D) db = atomicAdd(&o.ctr->dpos, (unsigned long long)D);
       db = shfl64(db, 0);
       const bool ok = db + D <= caps.dcap;
-      if (!ok && lane == 0) atomicOr(&o.ctr->overflow, 1u);
+      if (!ok && lane == 0) {
+        atomicOr(&o.ctr->overflow, 1u);
+        atomicAdd(&o.ctr->miss[0], (unsigned long long)D);
+      }
       uint32_t w = 0;
       for (uint64_t b = 0; b < tsz; b += kWave) {
         const uint64_t j = b + lane;
@@ -670,7 +681,10 @@ __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *
       if (lane == 0 && H) hb = atomicAdd(&o.ctr->hpos, (unsigned long long)H);
       hb = shfl64(hb, 0);
       hok = hb + H <= caps.hcap;
-      if (!hok && lane == 0) atomicOr(&o.ctr->overflow, 2u);
+      if (!hok && lane == 0) {
+        atomicOr(&o.ctr->overflow, 2u);
+        atomicAdd(&o.ctr->miss[1], (unsigned long long)H);
+      }
       if (lane == 0) o.hstart[t] = hok ? hb : kNoSpace;
       H = 0;
     }
@@ -869,6 +883,14 @@ static int scan_offsets(Workspace &ws, const T *counts, uint64_t *offs, uint32_t
   return 0;
 }
 
+// capacity for a redo: what was handed out before the buffer ran out, what
+// was still requested after, and one chunk of slack per wave
+static void grow_caps(Workspace &ws, const Counters &c, uint32_t waves, const Caps &caps) {
+  if (c.overflow & 1) ws.dcap = (std::min<uint64_t>(c.dpos, ws.dcap) + c.miss[0] + waves * (uint64_t)caps.dchunk) * 5 / 4;
+  if (c.overflow & 2) ws.hcap = (std::min<uint64_t>(c.hpos, ws.hcap) + c.miss[1] + waves * (uint64_t)caps.hchunk) * 5 / 4;
+  if (c.overflow & 4) ws.bcap = (std::min<uint64_t>(c.bpos, ws.bcap) + c.miss[2] + waves * (uint64_t)caps.bchunk) * 5 / 4;
+}
+
 static uint32_t chunk_for(uint64_t cap, uint32_t waves, uint32_t lo, uint32_t hi) {
   uint64_t c = cap / (8ull * waves);
   return (uint32_t)std::max<uint64_t>(lo, std::min<uint64_t>(hi, c));
@@ -925,9 +947,7 @@ static int match_once(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_b
   out->n_fallback = n_dfs;
   out->n_big = (uint32_t)std::min<uint64_t>(hc->bpos, ws.bcap);
   if (hc->overflow) {  // grow to the measured need and redo the batch
-    if (hc->overflow & 1) ws.dcap = (hc->dpos + waves * (uint64_t)caps.dchunk) * 5 / 4;
-    if (hc->overflow & 2) ws.hcap = (hc->hpos + waves * (uint64_t)caps.hchunk) * 5 / 4;
-    if (hc->overflow & 4) ws.bcap = (hc->bpos + waves * (uint64_t)caps.bchunk) * 5 / 4;
+    grow_caps(ws, *hc, waves, caps);
     *retry = true;
     return 0;
   }
@@ -987,8 +1007,7 @@ static int match_once(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_b
   HIP_TRY(hipMemcpyAsync(hp + 1, hoffs + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   if (hc->overflow) {
-    if (hc->overflow & 1) ws.dcap = (hc->dpos + waves * (uint64_t)caps.dchunk) * 5 / 4;
-    if (hc->overflow & 2) ws.hcap = (hc->hpos + waves * (uint64_t)caps.hchunk) * 5 / 4;
+    grow_caps(ws, *hc, waves, caps);
     *retry = true;
     return 0;
   }
