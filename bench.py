@@ -133,12 +133,14 @@ def main():
     shared = 0
     fallback = 0
     big = 0
+    why = {}
     for _ in range(args.steps):
         r = step()
         deliveries += int(r.n_deliveries)
         shared += int(r.n_shared)
         fallback = int(r.n_fallback)
         big = int(r.n_big)
+        why = dict(zip(["frontier", "hits", "levels", "shared_hits", "raw_entries"], list(r.fallback_why)))
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
@@ -193,6 +195,7 @@ def main():
             "deliveries_per_topic": deliveries / max(topics_total, 1),
             "fallback_topics_per_batch": fallback,
             "big_topics_per_batch": big,
+            "fallback_reasons": why,
             "kernel_ms": kms,
             "snapshot": snap,
             "roofline": roof,

@@ -94,6 +94,8 @@ typedef struct {
   const uint32_t *shared;         /* device: shared-subscription ids            */
   uint32_t n_fallback;            /* topics routed through the unbounded path   */
   uint32_t n_big;                 /* topics deduplicated by the workgroup tier  */
+  uint32_t fallback_why[5];       /* why topics took the unbounded path: frontier,
+                                     hits, cached levels, shared hits, raw entries */
 } mqm_device_result;
 
 /* ---- lifecycle: NewTopicsIndex (topics.go:291-299) ---------------------- */

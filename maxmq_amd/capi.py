@@ -61,7 +61,8 @@ class SubInfo(C.Structure):
 class DeviceResult(C.Structure):
     _fields_ = [("n_topics", C.c_uint32), ("n_deliveries", C.c_uint64), ("n_shared", C.c_uint64),
                 ("offsets", C.c_void_p), ("deliveries", C.c_void_p), ("shared_offsets", C.c_void_p),
-                ("shared", C.c_void_p), ("n_fallback", C.c_uint32), ("n_big", C.c_uint32)]
+                ("shared", C.c_void_p), ("n_fallback", C.c_uint32), ("n_big", C.c_uint32),
+                ("fallback_why", C.c_uint32 * 5)]
 
 
 class SnapshotStats(C.Structure):

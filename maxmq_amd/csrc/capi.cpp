@@ -226,6 +226,7 @@ int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t 
     out->shared = mo.shared;
     out->n_fallback = mo.n_fallback;
     out->n_big = mo.n_big;
+    for (int i = 0; i < 5; i++) out->fallback_why[i] = h->ws.why[i];
     return MQM_OK;
   });
 }

@@ -11,7 +11,7 @@ namespace mqm {
 // Grow-only device buffers reused across batches (no allocation in steady state).
 struct Workspace {
   enum Slot {
-    kDCount, kHCount, kDStart, kHStart, kTier, kDfsList, kCounters, kDBuf, kHBuf, kBigRecs,
+    kDCount, kHCount, kDStart, kHStart, kCls, kDfsList, kBigList, kRecs, kCounters, kDBuf, kHBuf,
     kDOffs, kHOffs, kDOut, kHOut, kScanTmp, kRawCnt, kTabOff, kTabSize, kTable, kInBytes, kInOffs, kNumSlots
   };
   struct Buf {
@@ -23,6 +23,9 @@ struct Workspace {
   uint32_t max_blocks = 2048;  // walk-kernel grid cap (grid-stride beyond)
   // capacities (entries) of the chunk-allocated raw buffers; grown on overflow
   uint64_t dcap = 0, hcap = 0, bcap = 0;
+  // why the last batch's DFS topics left the bounded path:
+  // frontier, hits, cached levels, shared hits, raw entries
+  uint32_t why[5] = {0, 0, 0, 0, 0};
 
   // optional kernel timing (mqm_profile_*): events on the launch stream
   bool profile = false;

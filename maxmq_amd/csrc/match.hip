@@ -2,31 +2,32 @@
 // (vendor/github.com/mochi-co/mqtt/v2/topics.go:484-555) over a batch of
 // publish topics, against the GPU-resident CSR level-trie (snapshot.h).
 //
-// One pass over the trie per topic:
-//   k_walk    one wavefront per topic (grid-stride).
-//     1. tokenize : 64 lanes scan the topic bytes and ballot the '/'
-//                   positions; lane k builds level k's 128-bit key (keys.h).
+// One pass over the trie per topic, then deduplication sized to the topic:
+//   k_walk    a 16-lane group per topic, 4 topics per wavefront.
+//     1. tokenize : the group scans the topic 16 bytes at a time and ballots
+//                   the '/' positions; lane k builds level k's 128-bit key.
 //     2. walk     : level-synchronous over the frontier; each frontier node
 //                   fans out to 3 lanes (literal edge probe / '+' child /
-//                   '#' child) so a level costs one dependent memory round
+//                   '#' child), so a level costs one dependent memory round
 //                   trip (the literal child's descriptor is inline in its
 //                   edge entry).  Hits and the next frontier are compacted
 //                   with ballot + popcount into LDS.
-//     3. order    : hits sorted by rank (= the reference's emission order,
-//                   snapshot.h) with a 32-lane bitonic network in registers.
-//     4. dedupe   : small topics (<= kSMax raw entries) in a per-wave LDS
-//                   hash table keyed by client; one atomicOr folds max QoS
-//                   (one-hot), NoLocal and the hit's rank (one-hot), i.e.
-//                   Subscription.Merge (packets.go:250-270).  The entry whose
-//                   hit is its client's lowest rank is the first-merged sub.
-//                   Winners are compacted with ballot and written through a
-//                   per-wave chunk allocator (no per-topic atomics).
-//                   Bigger topics leave their sorted hit list in a record.
-//   k_big     one 256-thread workgroup per record: the same dedupe in a
-//             64 KiB LDS table shared by 4 waves.
-//   k_dfs<P>  the unbounded path for topics that exceed a capacity (frontier,
-//             hits, cached levels, raw entries): a wave-cooperative DFS with an
-//             LDS stack and a global-memory dedupe table.
+//     3. order    : hits ranked by counting (rank = the reference's emission
+//                   order, snapshot.h) and their range sizes prefix-summed into
+//                   a per-topic record; shared candidates are written directly
+//                   (the reference does not merge them).
+//   k_small   a wavefront per topic with <= kSMax raw entries: per-wave LDS
+//             hash table keyed by client; atomicOr folds QoS (one-hot) and
+//             NoLocal, atomicMin keeps the lowest hit index; an entry is its
+//             client's winner iff its hit is that minimum — exactly
+//             Subscription.Merge (packets.go:250-270) with the first-merged
+//             subscription's fields.  Winners are compacted with ballot and
+//             written through a per-wave chunk allocator.
+//   k_big     a 256-thread workgroup per topic with <= kBigMax raw entries:
+//             the same dedupe in a 48 KiB LDS table shared by 4 waves.
+//   k_dfs<P>  the unbounded path for topics past a capacity (frontier, hits,
+//             cached levels, raw entries): wave-cooperative DFS with an LDS
+//             stack and a global-memory dedupe table.
 //   k_compact raw chunks -> topic-ordered CSR at the scanned offsets.
 // Nothing runs on the CPU.
 #include <hip/hip_runtime.h>
@@ -42,32 +43,42 @@ namespace mqm {
 namespace {
 
 constexpr int kWave = 64;
-constexpr int kWavesPerBlock = 4;
-constexpr int kLMax = 16;      // levels cached per topic on the wave path
-constexpr int kFCap = 32;      // frontier nodes per level
-constexpr int kHCap = 28;      // non-shared hits (rank one-hot uses bits 4..31)
-constexpr int kShCap = 32;     // shared hits
-constexpr int kTCap = 512;     // per-wave dedupe table slots
-constexpr int kSMax = 384;     // raw entries deduplicated per wave (load <= 0.75)
+constexpr int kG = 16;                   // lanes per topic in k_walk
+constexpr int kGroups = kWave / kG;      // topics per wavefront
+constexpr int kWalkWaves = 4;            // wavefronts per k_walk block
+constexpr int kLMax = 16;                // levels cached per topic (one per lane)
+constexpr int kFCap = 16;                // frontier nodes per level
+constexpr int kHCap = 48;                // non-shared hits per topic (3 per lane)
+constexpr int kShCap = 16;               // shared hits per topic
+constexpr int kRecStride = 100;          // record words: nh, S, off[kHCap], pre[kHCap + 1], pad
+constexpr int kRecPre = 2 + kHCap;
+constexpr int kTCap = 512;               // k_small table slots
+constexpr int kSMax = 384;               // raw entries per k_small topic (load <= 0.75)
+constexpr int kSmallWaves = 4;
 constexpr int kBigThreads = 256;
-constexpr int kBigSlots = 8192;   // per-workgroup table: 64 KiB of LDS
-constexpr int kBigMax = 6144;     // raw entries deduplicated per workgroup (load <= 0.75)
-constexpr int kRecWords = 64;     // big-topic record: t, nh, S, -, off[28], pre[29]
-constexpr uint32_t kNoTopic = 0xFFFFFFFFu;
+constexpr int kBigSlots = 4096;          // k_big table: 48 KiB of LDS
+constexpr int kBigMax = 3072;            // raw entries per k_big topic (load <= 0.75)
 constexpr uint64_t kNoSpace = ~0ull;
+constexpr uint32_t kNoWhy = 0xFFFFFFFFu;
 
-static_assert(kSMax * 4 <= kTCap * 3, "wave dedupe table load factor");
-static_assert(kBigMax * 4 <= kBigSlots * 3, "workgroup dedupe table load factor");
+static_assert(kLMax == kG, "one lane per cached level");
+static_assert(kHCap == 3 * kG, "three ranked hits per lane");
+static_assert(kRecPre + kHCap + 1 <= kRecStride, "record layout");
+static_assert(kSMax * 4 <= kTCap * 3, "k_small table load factor");
+static_assert(kBigMax * 4 <= kBigSlots * 3, "k_big table load factor");
 
-enum : uint8_t { kTierDone = 0, kTierBig = 1, kTierDfs = 2 };
+enum : uint8_t { kClsDone = 0, kClsSmall = 1, kClsBig = 2, kClsDfs = 3 };
+enum : uint32_t { kWhyFrontier = 0, kWhyHits = 1, kWhyLevels = 2, kWhyShared = 3, kWhyEntries = 4 };
 
 struct Counters {              // zeroed before every batch
   unsigned long long dpos;     // deliveries bump pointer (entries)
   unsigned long long hpos;     // shared candidates bump pointer
-  unsigned long long bpos;     // big-topic records bump pointer
-  unsigned long long miss[3];  // entries requested after a buffer ran out (sizes the retry)
+  unsigned long long bpos;     // big-topic list bump pointer
+  unsigned long long miss[3];  // entries requested after a buffer ran out (sizes the redo)
   unsigned int n_dfs;          // topics appended to the DFS list
-  unsigned int overflow;       // 1: deliveries, 2: shared, 4: records
+  unsigned int overflow;       // 1: deliveries, 2: shared, 4: big list
+  unsigned int why[5];         // DFS routing reasons (kWhy*)
+  unsigned int pad;
 };
 
 struct Caps {
@@ -75,18 +86,29 @@ struct Caps {
   uint32_t dchunk, hchunk, bchunk;
 };
 
-struct WaveLds {
+struct Outputs {
+  uint32_t *dcount, *hcount;
+  uint64_t *dstart, *hstart;
+  uint8_t *cls;
+  uint32_t *dfs_list;
+  uint32_t *big_list;
+  uint32_t *recs;  // kRecStride words per topic
+  Counters *ctr;
+  uint64_t *dbuf;
+  uint32_t *hbuf;
+};
+
+struct TopicLds {              // k_walk context of one topic (one 16-lane group)
   uint64_t key0[kLMax];
   uint64_t key1[kLMax];
-  uint32_t sep[kLMax];           // position of the '/' ending level k
-  uint32_t front[2][3][kFCap];   // (node, plus, hash) of the frontier
-  uint32_t hit_rank[32];
-  uint32_t hit_off[32];
-  uint32_t hit_pre[33];
+  uint32_t sep[kLMax];         // position of the '/' ending level k
+  uint32_t front[2][3][kFCap]; // (node, plus, hash) of the frontier
+  uint32_t hit_rank[kHCap];
+  uint32_t hit_off[kHCap];
+  uint32_t hit_cnt[kHCap];
+  uint32_t s_cnt[kHCap];       // counts in rank order
   uint32_t sh_off[kShCap];
   uint32_t sh_cnt[kShCap];
-  uint32_t tkey[kTCap];
-  uint32_t tval[kTCap];
 };
 
 __device__ __forceinline__ void wave_lds_sync() {
@@ -151,20 +173,19 @@ __device__ __forceinline__ uint64_t pack_delivery(uint32_t client, uint32_t sid,
   return (uint64_t)client | ((uint64_t)(sid | (qos << 28) | (nl << 30)) << 32);
 }
 
-__device__ __forceinline__ uint32_t merge_bits(uint32_t h, uint32_t meta) {
-  return (1u << (4 + h)) | (1u << (meta & 3)) | (((meta >> 2) & 1) << 3);
-}
+// QoS one-hot (bits 0..2) | NoLocal (bit 3): OR-merged, max QoS = top set bit
+__device__ __forceinline__ uint32_t qos_bits(uint32_t meta) { return (1u << (meta & 3)) | (((meta >> 2) & 1) << 3); }
 
 // hit h with pre[h] <= r < pre[h+1] (pre strictly increasing: empty hits are never recorded)
 __device__ __forceinline__ uint32_t find_hit(const uint32_t *pre, uint32_t nh, uint32_t r) {
   uint32_t h = 0;
-  for (uint32_t step = 16; step > 0; step >>= 1)
+  for (uint32_t step = 32; step > 0; step >>= 1)
     if (h + step < nh && pre[h + step] <= r) h += step;
   return h;
 }
 
-// Per-wave bump allocation from a global counter in chunks (wave-uniform).
-// Once the buffer is exhausted the wave only tallies what it still needed.
+// Wave-uniform bump allocation from a global counter in chunks.  Once the
+// buffer is exhausted the wave only tallies what it still needed.
 struct WaveAlloc {
   uint64_t cur = 0, end = 0;
   bool dead = false;
@@ -194,106 +215,70 @@ __device__ uint64_t wave_alloc(WaveAlloc &a, uint64_t need, unsigned long long *
   return r;
 }
 
-// Bitonic sort of 32 (rank, off, cnt) triples held by lanes 0..31 (lanes
-// 32..63 sort their own copy, harmlessly).  Ascending by rank.
-__device__ __forceinline__ void sort32(int lane, uint32_t &rank, uint32_t &off, uint32_t &cnt) {
-  for (int k = 2; k <= 32; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      uint32_t r2 = __shfl_xor(rank, j, 64);
-      uint32_t o2 = __shfl_xor(off, j, 64);
-      uint32_t c2 = __shfl_xor(cnt, j, 64);
-      const bool up = (lane & k) == 0;
-      const bool lower = (lane & j) == 0;
-      const bool take_other = (lower == up) ? (r2 < rank) : (r2 > rank);
-      if (take_other) {
-        rank = r2;
-        off = o2;
-        cnt = c2;
-      }
-    }
-  }
-}
-
-struct Outputs {
-  uint32_t *dcount, *hcount;
-  uint64_t *dstart, *hstart;
-  uint8_t *tier;
-  uint32_t *dfs_list;
-  Counters *ctr;
-  uint64_t *dbuf;
-  uint32_t *hbuf;
-  uint32_t *recs;
-};
-
 // ---------------------------------------------------------------------------
-// k_walk: tokenize + walk + (small topics) dedupe, one wavefront per topic
+// k_walk: tokenize + walk + order hits, a 16-lane group per topic
 // ---------------------------------------------------------------------------
-// 6 blocks/CU (LDS: 6 x 23 KiB) => 6 waves per SIMD => <= 80 VGPRs
-__global__ __launch_bounds__(kWave *kWavesPerBlock, 6) void k_walk(DeviceSnapshot s, const uint8_t *__restrict__ tbytes,
-                                                               const uint64_t *__restrict__ toffs, uint32_t n,
-                                                               Outputs o, Caps caps) {
-  __shared__ WaveLds lds_all[kWavesPerBlock];
+__global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, const uint8_t *__restrict__ tbytes,
+                                                           const uint64_t *__restrict__ toffs, uint32_t n, Outputs o,
+                                                           Caps caps) {
+  __shared__ TopicLds lds_all[kWalkWaves * kGroups];
   const int lane = threadIdx.x & (kWave - 1);
-  const int wib = threadIdx.x / kWave;
-  WaveLds &L = lds_all[wib];
-  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
-  WaveAlloc da, ha, ba;
+  const int g = lane / kG, gl = lane & (kG - 1), gbase = g * kG;
+  TopicLds &L = lds_all[(threadIdx.x / kWave) * kGroups + g];
+  const uint32_t gmask_lt = (1u << gl) - 1u;
+  const uint64_t stride = (uint64_t)gridDim.x * kWalkWaves * kGroups;
+  WaveAlloc ha, ba;
+  const NodeDesc root = load_desc(s.nodes);
 
-  for (uint32_t t = blockIdx.x * kWavesPerBlock + wib; t < n; t += nwaves) {
-    const uint64_t off = toffs[t];
-    const uint32_t len = (uint32_t)(toffs[t + 1] - off);
-    const uint8_t *tp = tbytes + off;
-    if (len == 0) {  // scanSubscribers returns at once (topics.go:498-500)
-      if (lane == 0) {
-        o.dcount[t] = 0;
-        o.hcount[t] = 0;
-        o.dstart[t] = 0;
-        o.hstart[t] = 0;
-        o.tier[t] = kTierDone;
-      }
-      continue;
+  for (uint64_t tb = ((uint64_t)blockIdx.x * kWalkWaves + threadIdx.x / kWave) * kGroups; tb < n; tb += stride) {
+    const uint32_t t = (uint32_t)(tb + g);
+    const bool active = t < n;
+    uint32_t len = 0;
+    const uint8_t *tp = tbytes;
+    if (active) {
+      const uint64_t off = toffs[t];
+      len = (uint32_t)(toffs[t + 1] - off);
+      tp = tbytes + off;
     }
-    bool overflow = false;
+    uint32_t why = kNoWhy;
 
     // ---- 1. tokenize ------------------------------------------------------
     uint32_t nsep = 0;
     bool dollar = false;
-    for (uint32_t base = 0; base < len && nsep < (uint32_t)kLMax; base += kWave) {
-      const uint32_t p = base + lane;
+    for (uint32_t base = 0; base < len && nsep < (uint32_t)kLMax; base += kG) {
+      const uint32_t p = base + gl;
       const uint8_t b = p < len ? tp[p] : 0;
-      if (base == 0) dollar = __shfl(b, 0, 64) == '$';
-      const uint64_t m = __ballot(p < len && b == '/');
+      if (base == 0) dollar = __shfl(b, gbase, 64) == '$';
+      const uint32_t m = (uint32_t)(__ballot(p < len && b == '/') >> gbase) & 0xFFFFu;
       if (b == '/' && p < len) {
-        const uint32_t idx = nsep + __popcll(m & lanemask_lt(lane));
+        const uint32_t idx = nsep + __popc(m & gmask_lt);
         if (idx < (uint32_t)kLMax) L.sep[idx] = p;
       }
-      nsep += __popcll(m);
+      nsep += __popc(m);
     }
     // levels known: 0 .. nlev-1, with nlev capped at kLMax + 1
-    const uint32_t nlev = nsep >= (uint32_t)kLMax ? kLMax + 1 : nsep + 1;
+    const uint32_t nlev = len == 0 ? 0 : (nsep >= (uint32_t)kLMax ? kLMax + 1 : nsep + 1);
     wave_lds_sync();
-    if (lane < kLMax && (uint32_t)lane < nlev) {
-      const uint32_t st = lane == 0 ? 0 : L.sep[lane - 1] + 1;
-      const uint32_t en = ((uint32_t)lane < nsep) ? L.sep[lane] : len;
+    if ((uint32_t)gl < nlev) {
+      const uint32_t st = gl == 0 ? 0 : L.sep[gl - 1] + 1;
+      const uint32_t en = ((uint32_t)gl < nsep) ? L.sep[gl] : len;
       Key k = make_key([&](uint32_t i) { return tp[st + i]; }, en - st);
-      L.key0[lane] = k.k0;
-      L.key1[lane] = k.k1;
+      L.key0[gl] = k.k0;
+      L.key1[gl] = k.k1;
+    }
+    if (gl == 0) {
+      L.front[0][0][0] = 0;
+      L.front[0][1][0] = root.plus;
+      L.front[0][2][0] = root.hash;
     }
     wave_lds_sync();
 
     // ---- 2. walk ----------------------------------------------------------
-    uint32_t nf = 1, nh = 0, nsh = 0;
+    uint32_t nf = nlev > 0 ? 1 : 0, nh = 0, nsh = 0;
     int cur = 0;
-    if (lane == 0) {
-      const NodeDesc r = load_desc(s.nodes);
-      L.front[0][0][0] = 0;
-      L.front[0][1][0] = r.plus;
-      L.front[0][2][0] = r.hash;
-    }
-    wave_lds_sync();
-    for (uint32_t d = 0; d < nlev && nf > 0 && !overflow; d++) {
+    for (uint32_t d = 0; d < nlev && nf > 0; d++) {
       if (d >= (uint32_t)kLMax) {
-        overflow = true;
+        why = kWhyLevels;
         break;
       }
       const uint64_t k0 = L.key0[d], k1 = L.key1[d];
@@ -304,8 +289,8 @@ __global__ __launch_bounds__(kWave *kWavesPerBlock, 6) void k_walk(DeviceSnapsho
       const uint32_t tst = d == 0 ? 0 : L.sep[d - 1] + 1;
       const uint32_t tln = ((d < nsep) ? L.sep[d] : len) - tst;
       uint32_t nnext = 0;
-      for (uint32_t base = 0; base < nf * 3 && !overflow; base += kWave) {
-        const uint32_t item = base + lane;
+      for (uint32_t base = 0; base < nf * 3; base += kG) {
+        const uint32_t item = base + gl;
         const uint32_t fi = item / 3, type = item % 3;
         uint32_t c = kNone;
         NodeDesc dc;
@@ -325,142 +310,178 @@ __global__ __launch_bounds__(kWave *kWavesPerBlock, 6) void k_walk(DeviceSnapsho
         const bool h_par = found && type == 0 && dc.hsub_cnt > 0 && !skip_dollar;  // topics.go:507-509
         const bool h_sh = found && (dc.sh_cnt_flags & kShCntMask) > 0;
         const bool push = found && has_next && (fl & kFlagHasChildren);
-        const uint64_t m_own = __ballot(h_own), m_par = __ballot(h_par), m_sh = __ballot(h_sh),
-                       m_push = __ballot(push);
-        const uint64_t lt = lanemask_lt(lane);
-        const uint32_t n_own = __popcll(m_own), n_par = __popcll(m_par);
-        if (nh + n_own + n_par > (uint32_t)kHCap || nsh + __popcll(m_sh) > (uint32_t)kShCap ||
-            nnext + __popcll(m_push) > (uint32_t)kFCap) {
-          overflow = true;
-          break;
-        }
+        const uint32_t m_own = (uint32_t)(__ballot(h_own) >> gbase) & 0xFFFFu;
+        const uint32_t m_par = (uint32_t)(__ballot(h_par) >> gbase) & 0xFFFFu;
+        const uint32_t m_sh = (uint32_t)(__ballot(h_sh) >> gbase) & 0xFFFFu;
+        const uint32_t m_push = (uint32_t)(__ballot(push) >> gbase) & 0xFFFFu;
+        const uint32_t n_own = __popc(m_own), n_par = __popc(m_par);
+        if (nh + n_own + n_par > (uint32_t)kHCap) why = kWhyHits;
+        if (nsh + __popc(m_sh) > (uint32_t)kShCap) why = kWhyShared;
+        if (nnext + __popc(m_push) > (uint32_t)kFCap) why = kWhyFrontier;
+        if (why != kNoWhy) break;
         if (h_own) {
-          const uint32_t i = nh + __popcll(m_own & lt);
+          const uint32_t i = nh + __popc(m_own & gmask_lt);
           L.hit_rank[i] = 2 * c;
           L.hit_off[i] = dc.sub_off;
-          L.hit_pre[i] = dc.sub_cnt;
+          L.hit_cnt[i] = dc.sub_cnt;
         }
         if (h_par) {
-          const uint32_t i = nh + n_own + __popcll(m_par & lt);
+          const uint32_t i = nh + n_own + __popc(m_par & gmask_lt);
           L.hit_rank[i] = 2 * c + 1;
           L.hit_off[i] = dc.hsub_off;
-          L.hit_pre[i] = dc.hsub_cnt;
+          L.hit_cnt[i] = dc.hsub_cnt;
         }
         if (h_sh) {
-          const uint32_t i = nsh + __popcll(m_sh & lt);
+          const uint32_t i = nsh + __popc(m_sh & gmask_lt);
           L.sh_off[i] = dc.sh_off;
           L.sh_cnt[i] = dc.sh_cnt_flags & kShCntMask;
         }
         if (push) {
-          const uint32_t i = nnext + __popcll(m_push & lt);
+          const uint32_t i = nnext + __popc(m_push & gmask_lt);
           L.front[cur ^ 1][0][i] = c;
           L.front[cur ^ 1][1][i] = dc.plus;
           L.front[cur ^ 1][2][i] = dc.hash;
         }
         nh += n_own + n_par;
-        nsh += __popcll(m_sh);
-        nnext += __popcll(m_push);
+        nsh += __popc(m_sh);
+        nnext += __popc(m_push);
       }
       wave_lds_sync();
+      if (why != kNoWhy) break;
       cur ^= 1;
       nf = nnext;
     }
 
-    // ---- 3. order hits by rank, prefix their range sizes -------------------
+    // ---- 3. rank hits, prefix-sum their sizes into the record ---------------
+    // record: [0] nh, [1] S, [2 + r] off of rank r, [kRecPre + r] pre[r], r <= nh
+    uint32_t *rec = o.recs + (uint64_t)(active ? t : 0) * kRecStride;
+    const bool ok = active && why == kNoWhy;
+    if (ok) {
+      for (uint32_t i = gl; i < nh; i += kG) {
+        const uint32_t r = L.hit_rank[i];
+        uint32_t pos = 0;
+        for (uint32_t j = 0; j < nh; j++) pos += L.hit_rank[j] < r;  // ranks are distinct
+        rec[2 + pos] = L.hit_off[i];
+        L.s_cnt[pos] = L.hit_cnt[i];
+      }
+    }
+    wave_lds_sync();
     uint32_t S = 0;
-    if (!overflow) {
-      uint32_t rank = 0xFFFFFFFFu, hoff = 0, hcnt = 0;
-      if ((uint32_t)(lane & 31) < nh) {
-        rank = L.hit_rank[lane & 31];
-        hoff = L.hit_off[lane & 31];
-        hcnt = L.hit_pre[lane & 31];
+    if (ok) {
+      uint32_t c3[3], local = 0;
+      for (int k = 0; k < 3; k++) {
+        const uint32_t i = 3 * gl + k;
+        c3[k] = i < nh ? L.s_cnt[i] : 0;
+        local += c3[k];
       }
-      sort32(lane, rank, hoff, hcnt);
-      uint32_t inc = hcnt;  // inclusive scan over lanes 0..31
-      for (int o2 = 1; o2 < 32; o2 <<= 1) {
-        const uint32_t v = __shfl_up(inc, o2, 64);
-        if ((lane & 31) >= o2) inc += v;
+      uint32_t inc = local;  // inclusive scan over the group's 16 lanes
+      for (int d = 1; d < kG; d <<= 1) {
+        const uint32_t v = __shfl_up(inc, d, kG);
+        if (gl >= d) inc += v;
       }
-      S = __shfl(inc, 31, 64);
-      wave_lds_sync();
-      if (lane < 32) {
-        L.hit_rank[lane] = rank;
-        L.hit_off[lane] = hoff;
-        L.hit_pre[lane + 1] = inc;
+      S = __shfl(inc, gbase + kG - 1, 64);
+      uint32_t p = inc - local;
+      for (int k = 0; k < 3; k++) {
+        const uint32_t i = 3 * gl + k;
+        if (i <= nh) rec[kRecPre + i] = p;
+        p += c3[k];
       }
-      if (lane == 0) L.hit_pre[0] = 0;
-      if (S > (uint32_t)kBigMax) overflow = true;
-      wave_lds_sync();
+      if (gl == 0) {
+        rec[0] = nh;
+        rec[1] = S;
+        rec[kRecPre + nh] = S;
+      }
+      if (S > (uint32_t)kBigMax) why = kWhyEntries;
     }
-
-    if (overflow) {  // -> unbounded DFS path (it also produces the shared candidates)
-      if (lane == 0) {
-        o.tier[t] = kTierDfs;
-        o.dcount[t] = 0;
-        o.hcount[t] = 0;
-        o.dfs_list[atomicAdd(&o.ctr->n_dfs, 1u)] = t;
-      }
-      continue;
-    }
+    const bool dfs = active && why != kNoWhy;
+    const uint8_t cls = !active ? kClsDone : dfs ? kClsDfs : S == 0 ? kClsDone : S <= (uint32_t)kSMax ? kClsSmall : kClsBig;
 
     // ---- shared candidates (gatherSharedSubscriptions, topics.go:541-555) ---
     uint32_t H = 0;
-    for (uint32_t i = 0; i < nsh; i++) H += L.sh_cnt[i];
-    const uint64_t hb = wave_alloc(ha, H, &o.ctr->hpos, caps.hcap, caps.hchunk, o.ctr, 1, lane);
-    if (hb != kNoSpace) {
+    if (active && !dfs)
+      for (uint32_t i = 0; i < nsh; i++) H += L.sh_cnt[i];
+    // one allocation per wavefront for its 4 topics (converged here)
+    const uint32_t h0 = __shfl(H, 0, 64), h1 = __shfl(H, 16, 64), h2 = __shfl(H, 32, 64), h3 = __shfl(H, 48, 64);
+    const uint32_t hbefore = (g > 0 ? h0 : 0) + (g > 1 ? h1 : 0) + (g > 2 ? h2 : 0);
+    const uint64_t hwave = wave_alloc(ha, (uint64_t)h0 + h1 + h2 + h3, &o.ctr->hpos, caps.hcap, caps.hchunk, o.ctr, 1,
+                                      lane);
+    const uint64_t hb = hwave == kNoSpace ? kNoSpace : hwave + hbefore;
+    if (H && hb != kNoSpace) {
       uint32_t w = 0;
       for (uint32_t i = 0; i < nsh; i++) {
         const uint32_t so = L.sh_off[i], sc = L.sh_cnt[i];
-        for (uint32_t j = lane; j < sc; j += kWave) o.hbuf[hb + w + j] = so + j;
+        for (uint32_t j = gl; j < sc; j += kG) o.hbuf[hb + w + j] = so + j;
         w += sc;
       }
     }
-    if (lane == 0) {
-      o.hcount[t] = H;
+    // big topics: one list slot each, one allocation per wavefront
+    const uint32_t isbig = cls == kClsBig ? 1u : 0u;
+    const uint32_t b0 = __shfl(isbig, 0, 64), b1 = __shfl(isbig, 16, 64), b2 = __shfl(isbig, 32, 64),
+                   b3 = __shfl(isbig, 48, 64);
+    const uint64_t bwave = wave_alloc(ba, b0 + b1 + b2 + b3, &o.ctr->bpos, caps.bcap, caps.bchunk, o.ctr, 2, lane);
+    if (isbig && gl == 0 && bwave != kNoSpace)
+      o.big_list[bwave + (g > 0 ? b0 : 0) + (g > 1 ? b1 : 0) + (g > 2 ? b2 : 0)] = t;
+    if (active && gl == 0) {
+      o.cls[t] = cls;
+      o.hcount[t] = dfs ? 0 : H;
       o.hstart[t] = hb;
-    }
-
-    if (S > (uint32_t)kSMax) {  // -> workgroup tier: leave the ordered hit list in a record
-      const uint64_t rb = wave_alloc(ba, 1, &o.ctr->bpos, caps.bcap, caps.bchunk, o.ctr, 2, lane);
-      if (rb != kNoSpace) {
-        uint32_t *rec = o.recs + rb * kRecWords;
-        uint32_t v = 0;
-        if (lane == 0) v = t;
-        else if (lane == 1) v = nh;
-        else if (lane == 2) v = S;
-        else if (lane >= 4 && lane < 32) v = L.hit_off[lane - 4];
-        else if (lane >= 32 && lane <= 60) v = L.hit_pre[lane - 32];
-        rec[lane] = v;
+      o.dcount[t] = 0;
+      o.dstart[t] = 0;
+      if (dfs) {
+        o.dfs_list[atomicAdd(&o.ctr->n_dfs, 1u)] = t;
+        atomicAdd(&o.ctr->why[why], 1u);
       }
-      if (lane == 0) {
-        o.tier[t] = kTierBig;
-        o.dcount[t] = 0;
-        o.dstart[t] = 0;
-      }
-      wave_lds_sync();
-      continue;
     }
+    wave_lds_sync();
+  }
+}
 
-    // ---- 4. dedupe in the per-wave LDS table --------------------------------
+// ---------------------------------------------------------------------------
+// k_small: a wavefront per topic with <= kSMax raw entries (per-wave LDS table)
+// ---------------------------------------------------------------------------
+struct SmallLds {
+  uint32_t rec[kRecStride];
+  uint32_t tkey[kTCap];
+  uint32_t tbits[kTCap];
+  uint32_t tmin[kTCap];
+};
+
+__global__ __launch_bounds__(kWave *kSmallWaves) void k_small(DeviceSnapshot s, uint32_t n, Outputs o, Caps caps) {
+  __shared__ SmallLds lds_all[kSmallWaves];
+  const int lane = threadIdx.x & (kWave - 1);
+  SmallLds &L = lds_all[threadIdx.x / kWave];
+  const uint32_t nwaves = gridDim.x * kSmallWaves;
+  WaveAlloc da;
+  for (uint32_t t = blockIdx.x * kSmallWaves + threadIdx.x / kWave; t < n; t += nwaves) {
+    if (o.cls[t] != kClsSmall) continue;
+    const uint32_t *rec = o.recs + (uint64_t)t * kRecStride;
+    const uint32_t nh = rec[0], S = rec[1];
+    for (uint32_t i = lane; i < 2 + nh; i += kWave) L.rec[i] = rec[i];
+    for (uint32_t i = lane; i <= nh; i += kWave) L.rec[kRecPre + i] = rec[kRecPre + i];
     uint32_t lg = 6;  // load <= 0.5 up to kTCap/2 entries, <= 0.75 above
     while ((1u << lg) < 2 * S && (1u << lg) < (uint32_t)kTCap) lg++;
     const uint32_t tsize = 1u << lg;
-    for (uint32_t i = lane; i < tsize; i += kWave) L.tkey[i] = 0, L.tval[i] = 0;
+    for (uint32_t i = lane; i < tsize; i += kWave) {
+      L.tkey[i] = 0;
+      L.tbits[i] = 0;
+      L.tmin[i] = 0xFFFFFFFFu;
+    }
     wave_lds_sync();
+    const uint32_t *off = L.rec + 2, *pre = L.rec + kRecPre;
     for (uint32_t r = lane; r < S; r += kWave) {
-      const uint32_t h = find_hit(L.hit_pre, nh, r);
-      const SubEnt e = s.subs[L.hit_off[h] + (r - L.hit_pre[h])];
+      const uint32_t h = find_hit(pre, nh, r);
+      const SubEnt e = s.subs[off[h] + (r - pre[h])];
       uint32_t slot = table_slot(e.client, lg);
       for (;;) {
         const uint32_t prev = atomicCAS(&L.tkey[slot], 0u, e.client + 1);
         if (prev == 0 || prev == e.client + 1) break;
         slot = (slot + 1) & (tsize - 1);
       }
-      atomicOr(&L.tval[slot], merge_bits(h, e.meta));
+      atomicOr(&L.tbits[slot], qos_bits(e.meta));
+      atomicMin(&L.tmin[slot], h);
     }
     wave_lds_sync();
-
-    // ---- 5. winners -> deliveries (space for S reserved, D <= S used) -------
+    // space for S entries (D <= S are used)
     const uint64_t db = wave_alloc(da, S, &o.ctr->dpos, caps.dcap, caps.dchunk, o.ctr, 0, lane);
     uint32_t D = 0;
     for (uint32_t r0 = 0; r0 < S; r0 += kWave) {
@@ -468,13 +489,13 @@ __global__ __launch_bounds__(kWave *kWavesPerBlock, 6) void k_walk(DeviceSnapsho
       bool win = false;
       uint64_t ent = 0;
       if (r < S) {
-        const uint32_t h = find_hit(L.hit_pre, nh, r);
-        const uint32_t sid = L.hit_off[h] + (r - L.hit_pre[h]);
+        const uint32_t h = find_hit(pre, nh, r);
+        const uint32_t sid = off[h] + (r - pre[h]);
         const uint32_t client = s.subs[sid].client;
         uint32_t slot = table_slot(client, lg);
         while (L.tkey[slot] != client + 1) slot = (slot + 1) & (tsize - 1);
-        const uint32_t v = L.tval[slot];
-        win = (uint32_t)__builtin_ctz(v >> 4) == h;
+        win = L.tmin[slot] == h;
+        const uint32_t v = L.tbits[slot];
         ent = pack_delivery(client, sid, 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
       }
       const uint64_t m = __ballot(win);
@@ -484,53 +505,53 @@ __global__ __launch_bounds__(kWave *kWavesPerBlock, 6) void k_walk(DeviceSnapsho
     if (lane == 0) {
       o.dcount[t] = D;
       o.dstart[t] = db;
-      o.tier[t] = kTierDone;
     }
     wave_lds_sync();
   }
 }
 
 // ---------------------------------------------------------------------------
-// k_big: 256-thread workgroup per big-topic record, 64 KiB LDS dedupe table
+// k_big: a 256-thread workgroup per listed topic, 48 KiB LDS dedupe table
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBigThreads) void k_big(DeviceSnapshot s, Outputs o, Caps caps) {
-  extern __shared__ uint32_t big_tab[];  // tkey[kBigSlots] | tval[kBigSlots]
-  uint32_t *tkey = big_tab, *tval = big_tab + kBigSlots;
-  __shared__ uint32_t rec[kRecWords];
+  __shared__ uint32_t tkey[kBigSlots], tbits[kBigSlots], tmin[kBigSlots];
+  __shared__ uint32_t rec[kRecStride];
   __shared__ uint32_t wsum[kBigThreads / kWave];
   __shared__ unsigned long long blk_base;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
-  const uint64_t nrec = o.ctr->bpos < caps.bcap ? o.ctr->bpos : caps.bcap;
+  const uint64_t nbig = o.ctr->bpos < caps.bcap ? o.ctr->bpos : caps.bcap;
   uint64_t cur = 0, end = 0;  // block chunk allocator (thread 0)
   bool dead = false;
-  for (uint64_t ri = blockIdx.x; ri < nrec; ri += gridDim.x) {
-    if (tid < kRecWords) rec[tid] = o.recs[ri * kRecWords + tid];
+  for (uint64_t bi = blockIdx.x; bi < nbig; bi += gridDim.x) {
+    const uint32_t t = o.big_list[bi];
+    if (t == kNone) continue;  // unused slot of some wave's last chunk (block-uniform)
+    const uint32_t *grec = o.recs + (uint64_t)t * kRecStride;
+    if (tid < kRecStride) rec[tid] = grec[tid];
     __syncthreads();
-    const uint32_t t = rec[0];
-    if (t == kNoTopic) {  // unused record of some wave's last chunk
-      __syncthreads();
-      continue;
-    }
-    const uint32_t nh = rec[1], S = rec[2];
-    const uint32_t *hoff = rec + 4, *pre = rec + 32;
+    const uint32_t nh = rec[0], S = rec[1];
+    const uint32_t *off = rec + 2, *pre = rec + kRecPre;
     uint32_t lg = 6;
     while ((1u << lg) < 2 * S && (1u << lg) < (uint32_t)kBigSlots) lg++;
     const uint32_t tsize = 1u << lg;
-    for (uint32_t i = tid; i < tsize; i += kBigThreads) tkey[i] = 0, tval[i] = 0;
+    for (uint32_t i = tid; i < tsize; i += kBigThreads) {
+      tkey[i] = 0;
+      tbits[i] = 0;
+      tmin[i] = 0xFFFFFFFFu;
+    }
     __syncthreads();
     for (uint32_t r = tid; r < S; r += kBigThreads) {
       const uint32_t h = find_hit(pre, nh, r);
-      const SubEnt e = s.subs[hoff[h] + (r - pre[h])];
+      const SubEnt e = s.subs[off[h] + (r - pre[h])];
       uint32_t slot = table_slot(e.client, lg);
       for (;;) {
         const uint32_t prev = atomicCAS(&tkey[slot], 0u, e.client + 1);
         if (prev == 0 || prev == e.client + 1) break;
         slot = (slot + 1) & (tsize - 1);
       }
-      atomicOr(&tval[slot], merge_bits(h, e.meta));
+      atomicOr(&tbits[slot], qos_bits(e.meta));
+      atomicMin(&tmin[slot], h);
     }
-    // space for S entries from the block's chunk
-    if (tid == 0) {
+    if (tid == 0) {  // space for S entries from the block's chunk
       if (!dead && cur + S > end) {
         const uint64_t grab = S > caps.dchunk ? S : caps.dchunk;
         cur = atomicAdd(&o.ctr->dpos, (unsigned long long)grab);
@@ -553,21 +574,22 @@ __global__ __launch_bounds__(kBigThreads) void k_big(DeviceSnapshot s, Outputs o
       uint64_t ent = 0;
       if (r < S) {
         const uint32_t h = find_hit(pre, nh, r);
-        const uint32_t sid = hoff[h] + (r - pre[h]);
+        const uint32_t sid = off[h] + (r - pre[h]);
         const uint32_t client = s.subs[sid].client;
         uint32_t slot = table_slot(client, lg);
         while (tkey[slot] != client + 1) slot = (slot + 1) & (tsize - 1);
-        const uint32_t v = tval[slot];
-        win = (uint32_t)__builtin_ctz(v >> 4) == h;
+        win = tmin[slot] == h;
+        const uint32_t v = tbits[slot];
         ent = pack_delivery(client, sid, 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
       }
       const uint64_t m = __ballot(win);
       if (lane == 0) wsum[wid] = __popcll(m);
       __syncthreads();
-      uint32_t before = D;
-      for (int w = 0; w < wid; w++) before += wsum[w];
-      uint32_t round = 0;
-      for (int w = 0; w < kBigThreads / kWave; w++) round += wsum[w];
+      uint32_t before = D, round = 0;
+      for (int w = 0; w < kBigThreads / kWave; w++) {
+        if (w < wid) before += wsum[w];
+        round += wsum[w];
+      }
       if (win && db != kNoSpace) o.dbuf[db + before + __popcll(m & lanemask_lt(lane))] = ent;
       D += round;
       __syncthreads();
@@ -628,14 +650,14 @@ __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *
       uint32_t w = 0;
       for (uint64_t b = 0; b < tsz; b += kWave) {
         const uint64_t j = b + lane;
-        GEnt g{0, 0};
-        if (j < tsz) g = T[j];
-        const bool occ = (uint32_t)g.keybits != 0;
+        GEnt gg{0, 0};
+        if (j < tsz) gg = T[j];
+        const bool occ = (uint32_t)gg.keybits != 0;
         const uint64_t m = __ballot(occ);
         if (occ && ok) {
-          const uint32_t bits = (uint32_t)(g.keybits >> 32);
+          const uint32_t bits = (uint32_t)(gg.keybits >> 32);
           o.dbuf[db + w + __popcll(m & lanemask_lt(lane))] = pack_delivery(
-              (uint32_t)g.keybits - 1, (uint32_t)~g.first, 31u - __builtin_clz(bits & 7u), (bits >> 3) & 1u);
+              (uint32_t)gg.keybits - 1, (uint32_t)~gg.first, 31u - __builtin_clz(bits & 7u), (bits >> 3) & 1u);
         }
         w += __popcll(m);
       }
@@ -756,8 +778,7 @@ __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *
                 if (prev == 0 || (uint32_t)prev == se.client + 1) break;
                 slot = (slot + 1) & (tsz - 1);
               }
-              const uint32_t bits = (1u << (se.meta & 3)) | (((se.meta >> 2) & 1) << 3);
-              atomicOr(&T[slot].keybits, (unsigned long long)bits << 32);
+              atomicOr(&T[slot].keybits, (unsigned long long)qos_bits(se.meta) << 32);
               atomicMax(&T[slot].first, ~(((unsigned long long)rank << 32) | sid));
             }
           }
@@ -794,8 +815,8 @@ __global__ void k_table_sizes(const uint64_t *__restrict__ raw_cnt, const Counte
   sizes[i] = sz;
 }
 
-// raw chunks -> topic-ordered CSR (one wavefront per topic)
-// (a batch whose chunk allocators overflowed is redone: skip what has no space)
+// raw chunks -> topic-ordered CSR (one wavefront per topic).  A batch whose
+// chunk allocators overflowed is redone, so what has no space is skipped.
 __global__ __launch_bounds__(256) void k_compact(uint32_t n, const uint32_t *__restrict__ dcount,
                                                 const uint64_t *__restrict__ dstart,
                                                 const uint64_t *__restrict__ doffs, const uint64_t *__restrict__ dbuf,
@@ -820,13 +841,13 @@ __global__ __launch_bounds__(256) void k_compact(uint32_t n, const uint32_t *__r
   }
 }
 
-#define HIP_TRY(x)                                                                                  \
-  do {                                                                                              \
-    hipError_t e_ = (x);                                                                            \
-    if (e_ != hipSuccess) {                                                                         \
+#define HIP_TRY(x)                                                                                        \
+  do {                                                                                                    \
+    hipError_t e_ = (x);                                                                                  \
+    if (e_ != hipSuccess) {                                                                               \
       fprintf(stderr, "mqmatch: %s failed: %s (%s:%d)\n", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
-      return -3;                                                                                    \
-    }                                                                                               \
+      return -3;                                                                                          \
+    }                                                                                                     \
   } while (0)
 
 }  // namespace
@@ -871,7 +892,7 @@ static float elapsed(Workspace &ws, int a, int b) {
   return ms;
 }
 
-// counts (u32, n) -> exclusive offsets (u64, n + 1)
+// counts (n) -> exclusive offsets (u64, n + 1)
 template <class T>
 static int scan_offsets(Workspace &ws, const T *counts, uint64_t *offs, uint32_t n, hipStream_t st) {
   HIP_TRY(hipMemsetAsync(offs, 0, sizeof(uint64_t), st));
@@ -902,62 +923,67 @@ static int match_once(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_b
   *retry = false;
   if (ws.get(W::kDCount, sizeof(uint32_t) * (n + 1)) || ws.get(W::kHCount, sizeof(uint32_t) * (n + 1)) ||
       ws.get(W::kDStart, sizeof(uint64_t) * (n + 1)) || ws.get(W::kHStart, sizeof(uint64_t) * (n + 1)) ||
-      ws.get(W::kTier, n + 1) || ws.get(W::kDfsList, sizeof(uint32_t) * (n + 1)) ||
+      ws.get(W::kCls, n + 1) || ws.get(W::kDfsList, sizeof(uint32_t) * (n + 1)) ||
+      ws.get(W::kRecs, sizeof(uint32_t) * kRecStride * ((uint64_t)n + 1)) ||
       ws.get(W::kCounters, sizeof(Counters)) || ws.get(W::kDOffs, sizeof(uint64_t) * (n + 1)) ||
       ws.get(W::kHOffs, sizeof(uint64_t) * (n + 1)) || ws.get(W::kDBuf, sizeof(uint64_t) * (ws.dcap + 1)) ||
-      ws.get(W::kHBuf, sizeof(uint32_t) * (ws.hcap + 1)) ||
-      ws.get(W::kBigRecs, sizeof(uint32_t) * kRecWords * (ws.bcap + 1)) ||
+      ws.get(W::kHBuf, sizeof(uint32_t) * (ws.hcap + 1)) || ws.get(W::kBigList, sizeof(uint32_t) * (ws.bcap + 1)) ||
       ws.get(W::kDOut, sizeof(uint64_t) * (ws.dcap + 1)) || ws.get(W::kHOut, sizeof(uint32_t) * (ws.hcap + 1)))
     return -2;
   if (!ws.host_pinned && hipHostMalloc(&ws.host_pinned, 256, hipHostMallocDefault) != hipSuccess) return -2;
   Counters *hc = reinterpret_cast<Counters *>(ws.host_pinned);
   uint64_t *hp = reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(ws.host_pinned) + 128);
+  static_assert(sizeof(Counters) <= 128, "pinned layout");
 
-  const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + kWavesPerBlock - 1) / kWavesPerBlock,
-                                                                   ws.max_blocks));
-  const uint32_t waves = blocks * kWavesPerBlock;
+  const uint32_t walk_blocks = std::max<uint32_t>(
+      1, std::min<uint32_t>((n + kWalkWaves * kGroups - 1) / (kWalkWaves * kGroups), ws.max_blocks));
+  const uint32_t waves = walk_blocks * kWalkWaves;
+  const uint32_t small_blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + kSmallWaves - 1) / kSmallWaves, 2048));
+  const uint32_t alloc_waves = std::max(waves, small_blocks * kSmallWaves);
   Outputs o;
   o.dcount = (uint32_t *)ws.ptr(W::kDCount);
   o.hcount = (uint32_t *)ws.ptr(W::kHCount);
   o.dstart = (uint64_t *)ws.ptr(W::kDStart);
   o.hstart = (uint64_t *)ws.ptr(W::kHStart);
-  o.tier = (uint8_t *)ws.ptr(W::kTier);
+  o.cls = (uint8_t *)ws.ptr(W::kCls);
   o.dfs_list = (uint32_t *)ws.ptr(W::kDfsList);
+  o.big_list = (uint32_t *)ws.ptr(W::kBigList);
+  o.recs = (uint32_t *)ws.ptr(W::kRecs);
   o.ctr = (Counters *)ws.ptr(W::kCounters);
   o.dbuf = (uint64_t *)ws.ptr(W::kDBuf);
   o.hbuf = (uint32_t *)ws.ptr(W::kHBuf);
-  o.recs = (uint32_t *)ws.ptr(W::kBigRecs);
   Caps caps;
   caps.dcap = ws.dcap;
   caps.hcap = ws.hcap;
   caps.bcap = ws.bcap;
-  caps.dchunk = chunk_for(ws.dcap, waves, 256, 8192);
-  caps.hchunk = chunk_for(ws.hcap, waves, 64, 4096);
-  caps.bchunk = chunk_for(ws.bcap, waves, 1, 16);
+  caps.dchunk = chunk_for(ws.dcap, alloc_waves, 256, 8192);
+  caps.hchunk = chunk_for(ws.hcap, alloc_waves, 64, 4096);
+  caps.bchunk = chunk_for(ws.bcap, alloc_waves, 4, 64);
 
   HIP_TRY(hipMemsetAsync(o.ctr, 0, sizeof(Counters), st));
-  HIP_TRY(hipMemsetAsync(o.recs, 0xFF, sizeof(uint32_t) * kRecWords * ws.bcap, st));
+  HIP_TRY(hipMemsetAsync(o.big_list, 0xFF, sizeof(uint32_t) * ws.bcap, st));
   mark(ws, 0, st);
-  if (n > 0) hipLaunchKernelGGL(k_walk, dim3(blocks), dim3(kWave * kWavesPerBlock), 0, st, s, d_bytes, d_offs, n, o, caps);
+  if (n > 0)
+    hipLaunchKernelGGL(k_walk, dim3(walk_blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o, caps);
   HIP_TRY(hipGetLastError());
   mark(ws, 1, st);
+  if (n > 0) hipLaunchKernelGGL(k_small, dim3(small_blocks), dim3(kWave * kSmallWaves), 0, st, s, n, o, caps);
+  HIP_TRY(hipGetLastError());
+  // k_big grid-strides over the big list (its length is read on the device)
+  hipLaunchKernelGGL(k_big, dim3(256 * 3), dim3(kBigThreads), 0, st, s, o, caps);
+  HIP_TRY(hipGetLastError());
+  mark(ws, 2, st);
   HIP_TRY(hipMemcpyAsync(hc, o.ctr, sizeof(Counters), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   const uint32_t n_dfs = hc->n_dfs;
   out->n_fallback = n_dfs;
   out->n_big = (uint32_t)std::min<uint64_t>(hc->bpos, ws.bcap);
+  for (int i = 0; i < 5; i++) ws.why[i] = hc->why[i];
   if (hc->overflow) {  // grow to the measured need and redo the batch
-    grow_caps(ws, *hc, waves, caps);
+    grow_caps(ws, *hc, alloc_waves, caps);
     *retry = true;
     return 0;
   }
-
-  // workgroup tier (grid-strides over the records; count read on the device)
-  const size_t big_lds = sizeof(uint32_t) * 2 * kBigSlots;
-  if (hc->bpos)
-    hipLaunchKernelGGL(k_big, dim3(std::min<uint64_t>(hc->bpos, 256 * 2)), dim3(kBigThreads), big_lds, st, s, o,
-                       caps);
-  HIP_TRY(hipGetLastError());
 
   if (n_dfs) {
     const uint32_t max_levels = s.height + 1;
@@ -989,7 +1015,6 @@ static int match_once(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_b
                        tab_off, tab, max_levels);
     HIP_TRY(hipGetLastError());
   }
-  mark(ws, 2, st);
 
   auto *doffs = (uint64_t *)ws.ptr(W::kDOffs);
   auto *hoffs = (uint64_t *)ws.ptr(W::kHOffs);
@@ -1007,7 +1032,7 @@ static int match_once(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_b
   HIP_TRY(hipMemcpyAsync(hp + 1, hoffs + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   if (hc->overflow) {
-    grow_caps(ws, *hc, waves, caps);
+    grow_caps(ws, *hc, alloc_waves, caps);
     *retry = true;
     return 0;
   }
