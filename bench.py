@@ -105,7 +105,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
     counts = None
     if args.mode == "sharded" and world > 1:
-        counts = torch.zeros(n, dtype=torch.int64, device=dev)
+        counts = torch.zeros(n, dtype=torch.int32, device=dev)
 
     def step():
         if args.mode == "sharded" and world > 1:
@@ -114,10 +114,8 @@ def main():
             dist.broadcast(to, src=0)
         r = idx.match_device(tb.data_ptr(), to.data_ptr(), n, stream.cuda_stream)
         if args.mode == "sharded" and world > 1:
-            # per-topic delivery counts of every shard, gathered at rank 0
-            offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
-            _dev_to_tensor(r.offsets, offs)
-            torch.diff(offs, out=counts)
+            # per-topic delivery counts of every shard, summed at rank 0
+            _dev_to_tensor(r.counts, counts)
             dist.reduce(counts, dst=0)
         return r
 
@@ -163,7 +161,7 @@ def main():
     out = None
     if rank == 0:
         calls = max(prof["calls"], 1)
-        kms = {k: prof[f"{k}_ms"] / calls for k in ("walk", "dedupe", "compact", "total")}
+        kms = {k: prof[f"{k}_ms"] / calls for k in ("walk", "dedupe", "total")}
         cpu = None
         stats = None
         if not args.no_cpu_baseline:

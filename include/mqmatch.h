@@ -83,14 +83,20 @@ typedef struct {
 } mqm_sub_info;
 
 /* Device-resident result of mqm_match_device (library-owned; valid until the
- * next match call on the same index). */
+ * next match call on the same index).  Topic t's deliveries are
+ * deliveries[starts[t] .. starts[t] + counts[t]) and its shared candidates
+ * shared[shared_starts[t] .. + shared_counts[t]).  Segments are in topic
+ * order but may leave gaps (a topic reserves its raw-entry count before
+ * deduplication); mqm_match_batch returns the dense form. */
 typedef struct {
   uint32_t n_topics;
-  uint64_t n_deliveries;
-  uint64_t n_shared;
-  const uint64_t *offsets;        /* device, n_topics + 1                       */
+  uint64_t n_deliveries;          /* sum of counts                              */
+  uint64_t n_shared;              /* sum of shared_counts                       */
+  const uint64_t *starts;         /* device, n_topics                           */
+  const uint32_t *counts;         /* device, n_topics                           */
   const mqm_delivery *deliveries; /* device                                     */
-  const uint64_t *shared_offsets; /* device, n_topics + 1                       */
+  const uint64_t *shared_starts;  /* device, n_topics                           */
+  const uint32_t *shared_counts;  /* device, n_topics                           */
   const uint32_t *shared;         /* device: shared-subscription ids            */
   uint32_t n_fallback;            /* topics routed through the unbounded path   */
   uint32_t n_big;                 /* topics deduplicated by the workgroup tier  */
@@ -167,10 +173,10 @@ int mqm_snapshot_stats_get(mqm_index *h, mqm_snapshot_stats *out);
 typedef struct {
   uint64_t calls;           /* match calls while enabled                        */
   uint64_t fallback_topics; /* topics that took the unbounded path              */
-  double walk_ms;           /* k_walk: tokenize + walk + per-wave dedupe/emit     */
-  double dedupe_ms;         /* k_big + DFS path (+ one host sync), after k_walk   */
-  double compact_ms;        /* k_compact: raw chunks -> topic-ordered CSR         */
-  double total_ms;          /* first to last kernel of each call, summed          */
+  double walk_ms;           /* k_walk: tokenize + walk + hit records              */
+  double dedupe_ms;         /* k_small + k_big + DFS phases 1-2                   */
+  double total_ms;          /* first to last kernel of each call (incl. scans and
+                               the one host sync that sizes the outputs), summed  */
 } mqm_profile;
 int mqm_profile_enable(mqm_index *h, int on); /* resets the accumulators */
 int mqm_profile_read(mqm_index *h, mqm_profile *out);

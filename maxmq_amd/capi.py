@@ -60,7 +60,8 @@ class SubInfo(C.Structure):
 
 class DeviceResult(C.Structure):
     _fields_ = [("n_topics", C.c_uint32), ("n_deliveries", C.c_uint64), ("n_shared", C.c_uint64),
-                ("offsets", C.c_void_p), ("deliveries", C.c_void_p), ("shared_offsets", C.c_void_p),
+                ("starts", C.c_void_p), ("counts", C.c_void_p), ("deliveries", C.c_void_p),
+                ("shared_starts", C.c_void_p), ("shared_counts", C.c_void_p),
                 ("shared", C.c_void_p), ("n_fallback", C.c_uint32), ("n_big", C.c_uint32),
                 ("fallback_why", C.c_uint32 * 5)]
 
@@ -72,7 +73,7 @@ class SnapshotStats(C.Structure):
 
 class Profile(C.Structure):
     _fields_ = [("calls", C.c_uint64), ("fallback_topics", C.c_uint64), ("walk_ms", C.c_double),
-                ("dedupe_ms", C.c_double), ("compact_ms", C.c_double), ("total_ms", C.c_double)]
+                ("dedupe_ms", C.c_double), ("total_ms", C.c_double)]
 
 
 _LIB = None

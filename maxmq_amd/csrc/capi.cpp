@@ -100,8 +100,7 @@ int mqm_profile_read(mqm_index *h, mqm_profile *out) {
   out->calls = h->ws.prof_calls;
   out->fallback_topics = h->ws.prof_fallback_topics;
   out->walk_ms = h->ws.prof_walk_ms;
-  out->dedupe_ms = h->ws.prof_big_ms;
-  out->compact_ms = h->ws.prof_compact_ms;
+  out->dedupe_ms = h->ws.prof_dedupe_ms;
   out->total_ms = h->ws.prof_total_ms;
   return MQM_OK;
 }
@@ -220,9 +219,11 @@ int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t 
     out->n_topics = mo.n_topics;
     out->n_deliveries = mo.n_deliveries;
     out->n_shared = mo.n_shared;
-    out->offsets = mo.offsets;
+    out->starts = mo.starts;
+    out->counts = mo.counts;
     out->deliveries = reinterpret_cast<const mqm_delivery *>(mo.deliveries);
-    out->shared_offsets = mo.shared_offsets;
+    out->shared_starts = mo.shared_starts;
+    out->shared_counts = mo.shared_counts;
     out->shared = mo.shared;
     out->n_fallback = mo.n_fallback;
     out->n_big = mo.n_big;
@@ -258,6 +259,9 @@ int mqm_match_batch(mqm_index *h, const char *topic_bytes, const uint64_t *topic
     MatchOutput mo;
     rc = match_device(h->snap->dev, ws, d_bytes, d_offs, n_topics, h->stream, &mo);
     if (rc != 0) return rc;
+    DenseOutput dn;
+    rc = densify(ws, mo, h->stream, &dn);
+    if (rc != 0) return rc;
     auto r = std::make_unique<mqm_result>();
     r->n = n_topics;
     r->offsets.resize(n_topics + 1);
@@ -265,15 +269,15 @@ int mqm_match_batch(mqm_index *h, const char *topic_bytes, const uint64_t *topic
     r->deliveries.resize(mo.n_deliveries);
     r->shared.resize(mo.n_shared);
     r->snap = h->snap->host;
-    if (hipMemcpyAsync(r->offsets.data(), mo.offsets, sizeof(uint64_t) * (n_topics + 1), hipMemcpyDeviceToHost,
+    if (hipMemcpyAsync(r->offsets.data(), dn.offsets, sizeof(uint64_t) * (n_topics + 1), hipMemcpyDeviceToHost,
                        h->stream) != hipSuccess ||
-        hipMemcpyAsync(r->shared_offsets.data(), mo.shared_offsets, sizeof(uint64_t) * (n_topics + 1),
+        hipMemcpyAsync(r->shared_offsets.data(), dn.shared_offsets, sizeof(uint64_t) * (n_topics + 1),
                        hipMemcpyDeviceToHost, h->stream) != hipSuccess)
       return MQM_EHIP;
-    if (mo.n_deliveries && hipMemcpyAsync(r->deliveries.data(), mo.deliveries, sizeof(uint64_t) * mo.n_deliveries,
+    if (mo.n_deliveries && hipMemcpyAsync(r->deliveries.data(), dn.deliveries, sizeof(uint64_t) * mo.n_deliveries,
                                           hipMemcpyDeviceToHost, h->stream) != hipSuccess)
       return MQM_EHIP;
-    if (mo.n_shared && hipMemcpyAsync(r->shared.data(), mo.shared, sizeof(uint32_t) * mo.n_shared,
+    if (mo.n_shared && hipMemcpyAsync(r->shared.data(), dn.shared, sizeof(uint32_t) * mo.n_shared,
                                       hipMemcpyDeviceToHost, h->stream) != hipSuccess)
       return MQM_EHIP;
     if (hipStreamSynchronize(h->stream) != hipSuccess) return MQM_EHIP;

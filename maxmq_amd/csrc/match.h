@@ -11,8 +11,9 @@ namespace mqm {
 // Grow-only device buffers reused across batches (no allocation in steady state).
 struct Workspace {
   enum Slot {
-    kDCount, kHCount, kDStart, kHStart, kCls, kDfsList, kBigList, kRecs, kCounters, kDBuf, kHBuf,
-    kDOffs, kHOffs, kDOut, kHOut, kScanTmp, kRawCnt, kTabOff, kTabSize, kTable, kInBytes, kInOffs, kNumSlots
+    kSCount, kHCount, kDCount, kDStart, kHStart, kCls, kDfsList, kRecs, kCounters, kDOut, kHOut,
+    kDense, kDenseShared, kDenseOffs, kDenseHOffs, kScanTmp, kRawCnt, kTabOff, kTabSize, kTable,
+    kInBytes, kInOffs, kNumSlots
   };
   struct Buf {
     void *p = nullptr;
@@ -21,20 +22,18 @@ struct Workspace {
   Buf bufs[kNumSlots];
   void *host_pinned = nullptr;
   uint32_t max_blocks = 2048;  // walk-kernel grid cap (grid-stride beyond)
-  // capacities (entries) of the chunk-allocated raw buffers; grown on overflow
-  uint64_t dcap = 0, hcap = 0, bcap = 0;
   // why the last batch's DFS topics left the bounded path:
   // frontier, hits, cached levels, shared hits, raw entries
   uint32_t why[5] = {0, 0, 0, 0, 0};
 
   // optional kernel timing (mqm_profile_*): events on the launch stream
   bool profile = false;
-  hipEvent_t ev[5] = {};  // 0 start, 1 walk done, 2 big/fallback done, 3 compaction start, 4 end
+  hipEvent_t ev[4] = {};  // 0 start, 1 walk done, 2 dedupe start, 3 end
   uint64_t prof_calls = 0, prof_fallback_topics = 0;
-  double prof_walk_ms = 0, prof_big_ms = 0, prof_compact_ms = 0, prof_total_ms = 0;
+  double prof_walk_ms = 0, prof_dedupe_ms = 0, prof_total_ms = 0;
   void reset_profile() {
     prof_calls = prof_fallback_topics = 0;
-    prof_walk_ms = prof_big_ms = prof_compact_ms = prof_total_ms = 0;
+    prof_walk_ms = prof_dedupe_ms = prof_total_ms = 0;
   }
 
   static int reserve(void **p, size_t *cap, size_t need);
@@ -43,20 +42,30 @@ struct Workspace {
   ~Workspace();
 };
 
+// Per-topic segments (starts/counts; see mqm_device_result).
 struct MatchOutput {
   uint32_t n_topics = 0;
   uint64_t n_deliveries = 0, n_shared = 0;
-  const uint64_t *offsets = nullptr;     // device, n + 1
+  const uint64_t *starts = nullptr;      // device, n
+  const uint32_t *counts = nullptr;      // device, n
   const uint64_t *deliveries = nullptr;  // device, packed (snapshot.h)
-  const uint64_t *shared_offsets = nullptr;
+  const uint64_t *shared_starts = nullptr;
+  const uint32_t *shared_counts = nullptr;
   const uint32_t *shared = nullptr;
   uint32_t n_fallback = 0;  // topics on the unbounded DFS path
   uint32_t n_big = 0;       // topics deduplicated by the workgroup tier
 };
 
-// Runs walk -> big-topic dedupe -> (DFS fallback) -> scan -> compaction on
-// `st`; returns 0 or a negative MQM_E* code.
+// Runs walk -> scan -> dedupe (small / big / DFS) on `st`; returns 0 or a
+// negative MQM_E* code.
 int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes, const uint64_t *d_offs,
                  uint32_t n, hipStream_t st, MatchOutput *out);
+
+// Dense CSR of a MatchOutput (offsets n+1, entries back to back) on `st`.
+struct DenseOutput {
+  const uint64_t *offsets = nullptr, *deliveries = nullptr, *shared_offsets = nullptr;
+  const uint32_t *shared = nullptr;
+};
+int densify(Workspace &ws, const MatchOutput &m, hipStream_t st, DenseOutput *out);
 
 }  // namespace mqm

@@ -13,28 +13,32 @@
 //                   edge entry).  Hits and the next frontier are compacted
 //                   with ballot + popcount into LDS.
 //     3. order    : hits ranked by counting (rank = the reference's emission
-//                   order, snapshot.h) and their range sizes prefix-summed into
-//                   a per-topic record; shared candidates are written directly
-//                   (the reference does not merge them).
+//                   order, snapshot.h); the ordered hit list, the prefix of
+//                   its range sizes and the shared hits go to a per-topic
+//                   record; S (raw entries) and H (shared candidates) counted.
+//   scan      S and H -> each topic's segment start (S is the upper bound of
+//             its deliveries, so every later kernel writes final positions).
 //   k_small   a wavefront per topic with <= kSMax raw entries: per-wave LDS
 //             hash table keyed by client; atomicOr folds QoS (one-hot) and
 //             NoLocal, atomicMin keeps the lowest hit index; an entry is its
 //             client's winner iff its hit is that minimum — exactly
 //             Subscription.Merge (packets.go:250-270) with the first-merged
-//             subscription's fields.  Winners are compacted with ballot and
-//             written through a per-wave chunk allocator.
+//             subscription's fields.  Winners are compacted with ballot.
+//             Also writes every topic's shared candidates.
 //   k_big     a 256-thread workgroup per topic with <= kBigMax raw entries:
-//             the same dedupe in a 48 KiB LDS table shared by 4 waves.
+//             the same dedupe in a 48 KiB LDS table shared by 4 waves, the
+//             entries held in registers between the two passes.
 //   k_dfs<P>  the unbounded path for topics past a capacity (frontier, hits,
-//             cached levels, raw entries): wave-cooperative DFS with an LDS
-//             stack and a global-memory dedupe table.
-//   k_compact raw chunks -> topic-ordered CSR at the scanned offsets.
+//             cached levels, shared hits, raw entries): wave-cooperative DFS
+//             with an LDS stack and a global-memory dedupe table, writing to
+//             a tail region after the scanned segments.
 // Nothing runs on the CPU.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstdio>
+#include <vector>
 
 #include "match.h"
 
@@ -50,52 +54,48 @@ constexpr int kLMax = 16;                // levels cached per topic (one per lan
 constexpr int kFCap = 16;                // frontier nodes per level
 constexpr int kHCap = 48;                // non-shared hits per topic (3 per lane)
 constexpr int kShCap = 16;               // shared hits per topic
-constexpr int kRecStride = 100;          // record words: nh, S, off[kHCap], pre[kHCap + 1], pad
+// record: [0] nh, [1] S, [2 + r] off of rank r, [kRecPre + r] pre[r] (r <= nh),
+//         [kRecSh] nsh, [kRecSh + 1 + 2i] shared (off, cnt)
 constexpr int kRecPre = 2 + kHCap;
+constexpr int kRecSh = kRecPre + kHCap + 1;
+constexpr int kRecStride = kRecSh + 1 + 2 * kShCap + 4;  // 136 words
 constexpr int kTCap = 512;               // k_small table slots
 constexpr int kSMax = 384;               // raw entries per k_small topic (load <= 0.75)
+constexpr int kSmallPer = kSMax / kWave; // entries per lane
 constexpr int kSmallWaves = 4;
 constexpr int kBigThreads = 256;
 constexpr int kBigSlots = 4096;          // k_big table: 48 KiB of LDS
 constexpr int kBigMax = 3072;            // raw entries per k_big topic (load <= 0.75)
-constexpr uint64_t kNoSpace = ~0ull;
+constexpr int kBigPer = kBigMax / kBigThreads;
 constexpr uint32_t kNoWhy = 0xFFFFFFFFu;
 
 static_assert(kLMax == kG, "one lane per cached level");
 static_assert(kHCap == 3 * kG, "three ranked hits per lane");
-static_assert(kRecPre + kHCap + 1 <= kRecStride, "record layout");
+static_assert(kRecStride % 4 == 0, "16-B aligned records");
 static_assert(kSMax * 4 <= kTCap * 3, "k_small table load factor");
 static_assert(kBigMax * 4 <= kBigSlots * 3, "k_big table load factor");
+static_assert(kSMax % kWave == 0 && kBigMax % kBigThreads == 0, "register tiles");
 
 enum : uint8_t { kClsDone = 0, kClsSmall = 1, kClsBig = 2, kClsDfs = 3 };
 enum : uint32_t { kWhyFrontier = 0, kWhyHits = 1, kWhyLevels = 2, kWhyShared = 3, kWhyEntries = 4 };
 
 struct Counters {              // zeroed before every batch
-  unsigned long long dpos;     // deliveries bump pointer (entries)
-  unsigned long long hpos;     // shared candidates bump pointer
-  unsigned long long bpos;     // big-topic list bump pointer
-  unsigned long long miss[3];  // entries requested after a buffer ran out (sizes the redo)
+  unsigned long long dtail;    // DFS deliveries: next free entry after the scanned segments
+  unsigned long long htail;    // DFS shared candidates: likewise
   unsigned int n_dfs;          // topics appended to the DFS list
-  unsigned int overflow;       // 1: deliveries, 2: shared, 4: big list
   unsigned int why[5];         // DFS routing reasons (kWhy*)
-  unsigned int pad;
-};
-
-struct Caps {
-  uint64_t dcap, hcap, bcap;
-  uint32_t dchunk, hchunk, bchunk;
 };
 
 struct Outputs {
-  uint32_t *dcount, *hcount;
-  uint64_t *dstart, *hstart;
+  uint32_t *scount, *hcount, *dcount;
+  uint64_t *dstart, *hstart;  // n + 1 (exclusive scans; DFS topics overwritten)
   uint8_t *cls;
   uint32_t *dfs_list;
-  uint32_t *big_list;
+  uint32_t *big_list, *n_big;
   uint32_t *recs;  // kRecStride words per topic
   Counters *ctr;
-  uint64_t *dbuf;
-  uint32_t *hbuf;
+  uint64_t *dout;
+  uint32_t *hout;
 };
 
 struct TopicLds {              // k_walk context of one topic (one 16-lane group)
@@ -184,50 +184,18 @@ __device__ __forceinline__ uint32_t find_hit(const uint32_t *pre, uint32_t nh, u
   return h;
 }
 
-// Wave-uniform bump allocation from a global counter in chunks.  Once the
-// buffer is exhausted the wave only tallies what it still needed.
-struct WaveAlloc {
-  uint64_t cur = 0, end = 0;
-  bool dead = false;
-};
-
-__device__ uint64_t wave_alloc(WaveAlloc &a, uint64_t need, unsigned long long *counter, uint64_t cap, uint32_t chunk,
-                               Counters *ctr, unsigned int which, int lane) {
-  if (need == 0) return 0;
-  if (!a.dead && a.cur + need > a.end) {
-    const uint64_t grab = need > chunk ? need : chunk;
-    uint64_t base = 0;
-    if (lane == 0) base = atomicAdd(counter, (unsigned long long)grab);
-    base = shfl64(base, 0);
-    a.cur = base;
-    a.end = base + grab;
-    if (a.end > cap) {
-      if (lane == 0) atomicOr(&ctr->overflow, 1u << which);
-      a.dead = true;
-    }
-  }
-  if (a.dead) {
-    if (lane == 0) atomicAdd(&ctr->miss[which], (unsigned long long)need);
-    return kNoSpace;
-  }
-  const uint64_t r = a.cur;
-  a.cur += need;
-  return r;
-}
-
 // ---------------------------------------------------------------------------
 // k_walk: tokenize + walk + order hits, a 16-lane group per topic
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, const uint8_t *__restrict__ tbytes,
-                                                           const uint64_t *__restrict__ toffs, uint32_t n, Outputs o,
-                                                           Caps caps) {
+                                                           const uint64_t *__restrict__ toffs, uint32_t n,
+                                                           Outputs o) {
   __shared__ TopicLds lds_all[kWalkWaves * kGroups];
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / kG, gl = lane & (kG - 1), gbase = g * kG;
   TopicLds &L = lds_all[(threadIdx.x / kWave) * kGroups + g];
   const uint32_t gmask_lt = (1u << gl) - 1u;
   const uint64_t stride = (uint64_t)gridDim.x * kWalkWaves * kGroups;
-  WaveAlloc ha, ba;
   const NodeDesc root = load_desc(s.nodes);
 
   for (uint64_t tb = ((uint64_t)blockIdx.x * kWalkWaves + threadIdx.x / kWave) * kGroups; tb < n; tb += stride) {
@@ -353,7 +321,6 @@ __global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, co
     }
 
     // ---- 3. rank hits, prefix-sum their sizes into the record ---------------
-    // record: [0] nh, [1] S, [2 + r] off of rank r, [kRecPre + r] pre[r], r <= nh
     uint32_t *rec = o.recs + (uint64_t)(active ? t : 0) * kRecStride;
     const bool ok = active && why == kNoWhy;
     if (ok) {
@@ -366,7 +333,7 @@ __global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, co
       }
     }
     wave_lds_sync();
-    uint32_t S = 0;
+    uint32_t S = 0, H = 0;
     if (ok) {
       uint32_t c3[3], local = 0;
       for (int k = 0; k < 3; k++) {
@@ -383,50 +350,28 @@ __global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, co
       uint32_t p = inc - local;
       for (int k = 0; k < 3; k++) {
         const uint32_t i = 3 * gl + k;
-        if (i <= nh) rec[kRecPre + i] = p;
+        if (i < nh) rec[kRecPre + i] = p;
         p += c3[k];
       }
+      if ((uint32_t)gl < nsh) {
+        rec[kRecSh + 1 + 2 * gl] = L.sh_off[gl];
+        rec[kRecSh + 2 + 2 * gl] = L.sh_cnt[gl];
+      }
+      for (uint32_t i = 0; i < nsh; i++) H += L.sh_cnt[i];
       if (gl == 0) {
         rec[0] = nh;
         rec[1] = S;
         rec[kRecPre + nh] = S;
+        rec[kRecSh] = nsh;
       }
       if (S > (uint32_t)kBigMax) why = kWhyEntries;
     }
-    const bool dfs = active && why != kNoWhy;
-    const uint8_t cls = !active ? kClsDone : dfs ? kClsDfs : S == 0 ? kClsDone : S <= (uint32_t)kSMax ? kClsSmall : kClsBig;
-
-    // ---- shared candidates (gatherSharedSubscriptions, topics.go:541-555) ---
-    uint32_t H = 0;
-    if (active && !dfs)
-      for (uint32_t i = 0; i < nsh; i++) H += L.sh_cnt[i];
-    // one allocation per wavefront for its 4 topics (converged here)
-    const uint32_t h0 = __shfl(H, 0, 64), h1 = __shfl(H, 16, 64), h2 = __shfl(H, 32, 64), h3 = __shfl(H, 48, 64);
-    const uint32_t hbefore = (g > 0 ? h0 : 0) + (g > 1 ? h1 : 0) + (g > 2 ? h2 : 0);
-    const uint64_t hwave = wave_alloc(ha, (uint64_t)h0 + h1 + h2 + h3, &o.ctr->hpos, caps.hcap, caps.hchunk, o.ctr, 1,
-                                      lane);
-    const uint64_t hb = hwave == kNoSpace ? kNoSpace : hwave + hbefore;
-    if (H && hb != kNoSpace) {
-      uint32_t w = 0;
-      for (uint32_t i = 0; i < nsh; i++) {
-        const uint32_t so = L.sh_off[i], sc = L.sh_cnt[i];
-        for (uint32_t j = gl; j < sc; j += kG) o.hbuf[hb + w + j] = so + j;
-        w += sc;
-      }
-    }
-    // big topics: one list slot each, one allocation per wavefront
-    const uint32_t isbig = cls == kClsBig ? 1u : 0u;
-    const uint32_t b0 = __shfl(isbig, 0, 64), b1 = __shfl(isbig, 16, 64), b2 = __shfl(isbig, 32, 64),
-                   b3 = __shfl(isbig, 48, 64);
-    const uint64_t bwave = wave_alloc(ba, b0 + b1 + b2 + b3, &o.ctr->bpos, caps.bcap, caps.bchunk, o.ctr, 2, lane);
-    if (isbig && gl == 0 && bwave != kNoSpace)
-      o.big_list[bwave + (g > 0 ? b0 : 0) + (g > 1 ? b1 : 0) + (g > 2 ? b2 : 0)] = t;
     if (active && gl == 0) {
-      o.cls[t] = cls;
+      const bool dfs = why != kNoWhy;
+      o.cls[t] = dfs ? kClsDfs : S == 0 ? kClsDone : S <= (uint32_t)kSMax ? kClsSmall : kClsBig;
+      o.scount[t] = dfs ? 0 : S;
       o.hcount[t] = dfs ? 0 : H;
-      o.hstart[t] = hb;
       o.dcount[t] = 0;
-      o.dstart[t] = 0;
       if (dfs) {
         o.dfs_list[atomicAdd(&o.ctr->n_dfs, 1u)] = t;
         atomicAdd(&o.ctr->why[why], 1u);
@@ -437,7 +382,8 @@ __global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, co
 }
 
 // ---------------------------------------------------------------------------
-// k_small: a wavefront per topic with <= kSMax raw entries (per-wave LDS table)
+// k_small: a wavefront per topic with <= kSMax raw entries (per-wave LDS
+// table); also writes every bounded topic's shared candidates
 // ---------------------------------------------------------------------------
 struct SmallLds {
   uint32_t rec[kRecStride];
@@ -446,15 +392,28 @@ struct SmallLds {
   uint32_t tmin[kTCap];
 };
 
-__global__ __launch_bounds__(kWave *kSmallWaves) void k_small(DeviceSnapshot s, uint32_t n, Outputs o, Caps caps) {
+__global__ __launch_bounds__(kWave *kSmallWaves) void k_small(DeviceSnapshot s, uint32_t n, Outputs o) {
   __shared__ SmallLds lds_all[kSmallWaves];
   const int lane = threadIdx.x & (kWave - 1);
   SmallLds &L = lds_all[threadIdx.x / kWave];
   const uint32_t nwaves = gridDim.x * kSmallWaves;
-  WaveAlloc da;
   for (uint32_t t = blockIdx.x * kSmallWaves + threadIdx.x / kWave; t < n; t += nwaves) {
-    if (o.cls[t] != kClsSmall) continue;
+    const uint8_t cls = o.cls[t];
+    if (cls == kClsDfs) continue;
+    const uint32_t H = o.hcount[t];
+    if (cls != kClsSmall && H == 0) continue;
     const uint32_t *rec = o.recs + (uint64_t)t * kRecStride;
+    if (H) {  // shared candidates (gatherSharedSubscriptions, topics.go:541-555)
+      const uint32_t nsh = rec[kRecSh];
+      const uint64_t hb = o.hstart[t];
+      uint32_t w = 0;
+      for (uint32_t i = 0; i < nsh; i++) {
+        const uint32_t so = rec[kRecSh + 1 + 2 * i], sc = rec[kRecSh + 2 + 2 * i];
+        for (uint32_t j = lane; j < sc; j += kWave) o.hout[hb + w + j] = so + j;
+        w += sc;
+      }
+    }
+    if (cls != kClsSmall) continue;
     const uint32_t nh = rec[0], S = rec[1];
     for (uint32_t i = lane; i < 2 + nh; i += kWave) L.rec[i] = rec[i];
     for (uint32_t i = lane; i <= nh; i += kWave) L.rec[kRecPre + i] = rec[kRecPre + i];
@@ -468,44 +427,44 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(DeviceSnapshot s, 
     }
     wave_lds_sync();
     const uint32_t *off = L.rec + 2, *pre = L.rec + kRecPre;
-    for (uint32_t r = lane; r < S; r += kWave) {
-      const uint32_t h = find_hit(pre, nh, r);
-      const SubEnt e = s.subs[off[h] + (r - pre[h])];
-      uint32_t slot = table_slot(e.client, lg);
-      for (;;) {
-        const uint32_t prev = atomicCAS(&L.tkey[slot], 0u, e.client + 1);
-        if (prev == 0 || prev == e.client + 1) break;
-        slot = (slot + 1) & (tsize - 1);
+    uint32_t cl[kSmallPer], sid[kSmallPer], hh[kSmallPer], slot[kSmallPer];
+#pragma unroll
+    for (int k = 0; k < kSmallPer; k++) {
+      const uint32_t r = lane + k * kWave;
+      if (r < S) {
+        hh[k] = find_hit(pre, nh, r);
+        sid[k] = off[hh[k]] + (r - pre[hh[k]]);
+        const SubEnt e = s.subs[sid[k]];
+        cl[k] = e.client;
+        uint32_t sl = table_slot(e.client, lg);
+        for (;;) {
+          const uint32_t prev = atomicCAS(&L.tkey[sl], 0u, e.client + 1);
+          if (prev == 0 || prev == e.client + 1) break;
+          sl = (sl + 1) & (tsize - 1);
+        }
+        slot[k] = sl;
+        atomicOr(&L.tbits[sl], qos_bits(e.meta));
+        atomicMin(&L.tmin[sl], hh[k]);
       }
-      atomicOr(&L.tbits[slot], qos_bits(e.meta));
-      atomicMin(&L.tmin[slot], h);
     }
     wave_lds_sync();
-    // space for S entries (D <= S are used)
-    const uint64_t db = wave_alloc(da, S, &o.ctr->dpos, caps.dcap, caps.dchunk, o.ctr, 0, lane);
+    const uint64_t db = o.dstart[t];
     uint32_t D = 0;
-    for (uint32_t r0 = 0; r0 < S; r0 += kWave) {
-      const uint32_t r = r0 + lane;
+#pragma unroll
+    for (int k = 0; k < kSmallPer; k++) {
+      const uint32_t r = lane + k * kWave;
       bool win = false;
       uint64_t ent = 0;
       if (r < S) {
-        const uint32_t h = find_hit(pre, nh, r);
-        const uint32_t sid = off[h] + (r - pre[h]);
-        const uint32_t client = s.subs[sid].client;
-        uint32_t slot = table_slot(client, lg);
-        while (L.tkey[slot] != client + 1) slot = (slot + 1) & (tsize - 1);
-        win = L.tmin[slot] == h;
-        const uint32_t v = L.tbits[slot];
-        ent = pack_delivery(client, sid, 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
+        win = L.tmin[slot[k]] == hh[k];
+        const uint32_t v = L.tbits[slot[k]];
+        ent = pack_delivery(cl[k], sid[k], 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
       }
       const uint64_t m = __ballot(win);
-      if (win && db != kNoSpace) o.dbuf[db + D + __popcll(m & lanemask_lt(lane))] = ent;
+      if (win) o.dout[db + D + __popcll(m & lanemask_lt(lane))] = ent;
       D += __popcll(m);
     }
-    if (lane == 0) {
-      o.dcount[t] = D;
-      o.dstart[t] = db;
-    }
+    if (lane == 0) o.dcount[t] = D;
     wave_lds_sync();
   }
 }
@@ -513,20 +472,16 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(DeviceSnapshot s, 
 // ---------------------------------------------------------------------------
 // k_big: a 256-thread workgroup per listed topic, 48 KiB LDS dedupe table
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kBigThreads) void k_big(DeviceSnapshot s, Outputs o, Caps caps) {
+__global__ __launch_bounds__(kBigThreads) void k_big(DeviceSnapshot s, Outputs o) {
   __shared__ uint32_t tkey[kBigSlots], tbits[kBigSlots], tmin[kBigSlots];
   __shared__ uint32_t rec[kRecStride];
   __shared__ uint32_t wsum[kBigThreads / kWave];
-  __shared__ unsigned long long blk_base;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
-  const uint64_t nbig = o.ctr->bpos < caps.bcap ? o.ctr->bpos : caps.bcap;
-  uint64_t cur = 0, end = 0;  // block chunk allocator (thread 0)
-  bool dead = false;
-  for (uint64_t bi = blockIdx.x; bi < nbig; bi += gridDim.x) {
+  const uint32_t nbig = *o.n_big;
+  for (uint32_t bi = blockIdx.x; bi < nbig; bi += gridDim.x) {
     const uint32_t t = o.big_list[bi];
-    if (t == kNone) continue;  // unused slot of some wave's last chunk (block-uniform)
     const uint32_t *grec = o.recs + (uint64_t)t * kRecStride;
-    if (tid < kRecStride) rec[tid] = grec[tid];
+    if (tid < kRecPre + kHCap + 1) rec[tid] = grec[tid];
     __syncthreads();
     const uint32_t nh = rec[0], S = rec[1];
     const uint32_t *off = rec + 2, *pre = rec + kRecPre;
@@ -539,48 +494,39 @@ __global__ __launch_bounds__(kBigThreads) void k_big(DeviceSnapshot s, Outputs o
       tmin[i] = 0xFFFFFFFFu;
     }
     __syncthreads();
-    for (uint32_t r = tid; r < S; r += kBigThreads) {
-      const uint32_t h = find_hit(pre, nh, r);
-      const SubEnt e = s.subs[off[h] + (r - pre[h])];
-      uint32_t slot = table_slot(e.client, lg);
-      for (;;) {
-        const uint32_t prev = atomicCAS(&tkey[slot], 0u, e.client + 1);
-        if (prev == 0 || prev == e.client + 1) break;
-        slot = (slot + 1) & (tsize - 1);
-      }
-      atomicOr(&tbits[slot], qos_bits(e.meta));
-      atomicMin(&tmin[slot], h);
-    }
-    if (tid == 0) {  // space for S entries from the block's chunk
-      if (!dead && cur + S > end) {
-        const uint64_t grab = S > caps.dchunk ? S : caps.dchunk;
-        cur = atomicAdd(&o.ctr->dpos, (unsigned long long)grab);
-        end = cur + grab;
-        if (end > caps.dcap) {
-          atomicOr(&o.ctr->overflow, 1u);
-          dead = true;
+    uint32_t cl[kBigPer], sid[kBigPer], hh[kBigPer], slot[kBigPer];
+#pragma unroll
+    for (int k = 0; k < kBigPer; k++) {
+      const uint32_t r = tid + k * kBigThreads;
+      if (r < S) {
+        hh[k] = find_hit(pre, nh, r);
+        sid[k] = off[hh[k]] + (r - pre[hh[k]]);
+        const SubEnt e = s.subs[sid[k]];
+        cl[k] = e.client;
+        uint32_t sl = table_slot(e.client, lg);
+        for (;;) {
+          const uint32_t prev = atomicCAS(&tkey[sl], 0u, e.client + 1);
+          if (prev == 0 || prev == e.client + 1) break;
+          sl = (sl + 1) & (tsize - 1);
         }
+        slot[k] = sl;
+        atomicOr(&tbits[sl], qos_bits(e.meta));
+        atomicMin(&tmin[sl], hh[k]);
       }
-      if (dead) atomicAdd(&o.ctr->miss[0], (unsigned long long)S);
-      blk_base = dead ? kNoSpace : cur;
-      if (!dead) cur += S;
     }
     __syncthreads();
-    const uint64_t db = blk_base;
+    const uint64_t db = o.dstart[t];
     uint32_t D = 0;
-    for (uint32_t r0 = 0; r0 < S; r0 += kBigThreads) {
-      const uint32_t r = r0 + tid;
+#pragma unroll
+    for (int k = 0; k < kBigPer; k++) {
+      if ((uint32_t)(k * kBigThreads) >= S) break;  // block-uniform
+      const uint32_t r = tid + k * kBigThreads;
       bool win = false;
       uint64_t ent = 0;
       if (r < S) {
-        const uint32_t h = find_hit(pre, nh, r);
-        const uint32_t sid = off[h] + (r - pre[h]);
-        const uint32_t client = s.subs[sid].client;
-        uint32_t slot = table_slot(client, lg);
-        while (tkey[slot] != client + 1) slot = (slot + 1) & (tsize - 1);
-        win = tmin[slot] == h;
-        const uint32_t v = tbits[slot];
-        ent = pack_delivery(client, sid, 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
+        win = tmin[slot[k]] == hh[k];
+        const uint32_t v = tbits[slot[k]];
+        ent = pack_delivery(cl[k], sid[k], 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
       }
       const uint64_t m = __ballot(win);
       if (lane == 0) wsum[wid] = __popcll(m);
@@ -590,22 +536,25 @@ __global__ __launch_bounds__(kBigThreads) void k_big(DeviceSnapshot s, Outputs o
         if (w < wid) before += wsum[w];
         round += wsum[w];
       }
-      if (win && db != kNoSpace) o.dbuf[db + before + __popcll(m & lanemask_lt(lane))] = ent;
+      if (win) o.dout[db + before + __popcll(m & lanemask_lt(lane))] = ent;
       D += round;
       __syncthreads();
     }
-    if (tid == 0) {
-      o.dcount[t] = D;
-      o.dstart[t] = db;
-    }
+    if (tid == 0) o.dcount[t] = D;
     __syncthreads();
   }
 }
 
+struct IsBig {
+  const uint8_t *cls;
+  __host__ __device__ bool operator()(uint32_t t) const { return cls[t] == kClsBig; }
+};
+
 // ---------------------------------------------------------------------------
 // k_dfs<P>: the unbounded path.  P0 counts raw entries / shared candidates;
 // P1 inserts into a per-topic global table and writes the shared candidates;
-// P2 counts the table's clients and writes the deliveries.
+// P2 counts the table's clients and writes the deliveries.  Output goes to
+// the tail regions after the scanned segments.
 // ---------------------------------------------------------------------------
 struct GEnt {                  // global dedupe slot (16 B)
   unsigned long long keybits;  // (client + 1) | bits << 32
@@ -614,9 +563,10 @@ struct GEnt {                  // global dedupe slot (16 B)
 
 template <int kPhase>
 __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *__restrict__ tbytes,
-                                              const uint64_t *__restrict__ toffs, Outputs o, Caps caps,
-                                              uint64_t *__restrict__ raw_cnt, const uint64_t *__restrict__ tab_off,
-                                              GEnt *__restrict__ tab, uint32_t max_levels) {
+                                              const uint64_t *__restrict__ toffs, Outputs o,
+                                              uint64_t *__restrict__ raw_cnt, uint64_t *__restrict__ raw_h,
+                                              const uint64_t *__restrict__ tab_off, GEnt *__restrict__ tab,
+                                              uint32_t max_levels) {
   extern __shared__ uint32_t dyn[];
   // layout: sep[max_levels] | key0/key1 (u64 x max_levels each) | stack (4 x u32) x (2*max_levels + 8)
   uint32_t *sep = dyn;
@@ -640,13 +590,8 @@ __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *
         D += __popcll(__ballot(j < tsz && (uint32_t)T[j].keybits != 0));
       }
       uint64_t db = 0;
-      if (lane == 0 && D) db = atomicAdd(&o.ctr->dpos, (unsigned long long)D);
+      if (lane == 0 && D) db = atomicAdd(&o.ctr->dtail, (unsigned long long)D);
       db = shfl64(db, 0);
-      const bool ok = db + D <= caps.dcap;
-      if (!ok && lane == 0) {
-        atomicOr(&o.ctr->overflow, 1u);
-        atomicAdd(&o.ctr->miss[0], (unsigned long long)D);
-      }
       uint32_t w = 0;
       for (uint64_t b = 0; b < tsz; b += kWave) {
         const uint64_t j = b + lane;
@@ -654,16 +599,16 @@ __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *
         if (j < tsz) gg = T[j];
         const bool occ = (uint32_t)gg.keybits != 0;
         const uint64_t m = __ballot(occ);
-        if (occ && ok) {
+        if (occ) {
           const uint32_t bits = (uint32_t)(gg.keybits >> 32);
-          o.dbuf[db + w + __popcll(m & lanemask_lt(lane))] = pack_delivery(
+          o.dout[db + w + __popcll(m & lanemask_lt(lane))] = pack_delivery(
               (uint32_t)gg.keybits - 1, (uint32_t)~gg.first, 31u - __builtin_clz(bits & 7u), (bits >> 3) & 1u);
         }
         w += __popcll(m);
       }
       if (lane == 0) {
         o.dcount[t] = D;
-        o.dstart[t] = ok ? db : kNoSpace;
+        o.dstart[t] = db;
       }
       continue;
     }
@@ -697,18 +642,14 @@ __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *
     uint64_t S = 0;
     uint32_t H = 0;
     uint64_t hb = 0;
-    bool hok = true;
     if (kPhase == 1) {
-      H = o.hcount[t];  // counted by phase 0
-      if (lane == 0 && H) hb = atomicAdd(&o.ctr->hpos, (unsigned long long)H);
+      const uint32_t hn = (uint32_t)raw_h[i];  // counted by phase 0
+      if (lane == 0 && hn) hb = atomicAdd(&o.ctr->htail, (unsigned long long)hn);
       hb = shfl64(hb, 0);
-      hok = hb + H <= caps.hcap;
-      if (!hok && lane == 0) {
-        atomicOr(&o.ctr->overflow, 2u);
-        atomicAdd(&o.ctr->miss[1], (unsigned long long)H);
+      if (lane == 0) {
+        o.hstart[t] = hb;
+        o.hcount[t] = hn;
       }
-      if (lane == 0) o.hstart[t] = hok ? hb : kNoSpace;
-      H = 0;
     }
     uint32_t lg = 0;
     if (kPhase == 1)
@@ -784,8 +725,8 @@ __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *
           }
         }
         const uint32_t shc = e.sh_cnt_flags & kShCntMask;
-        if (kPhase == 1 && hok)
-          for (uint32_t j = lane; j < shc; j += kWave) o.hbuf[hb + H + j] = e.sh_off + j;
+        if (kPhase == 1)
+          for (uint32_t j = lane; j < shc; j += kWave) o.hout[hb + H + j] = e.sh_off + j;
         H += shc;
         if (has_next && (fl & kFlagHasChildren)) {
           if (lane == 0) {
@@ -801,7 +742,7 @@ __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *
     }
     if (lane == 0 && kPhase == 0) {
       raw_cnt[i] = S;
-      o.hcount[t] = H;
+      raw_h[i] = H;
     }
   }
 }
@@ -815,29 +756,21 @@ __global__ void k_table_sizes(const uint64_t *__restrict__ raw_cnt, const Counte
   sizes[i] = sz;
 }
 
-// raw chunks -> topic-ordered CSR (one wavefront per topic).  A batch whose
-// chunk allocators overflowed is redone, so what has no space is skipped.
-__global__ __launch_bounds__(256) void k_compact(uint32_t n, const uint32_t *__restrict__ dcount,
+// segments -> dense CSR (one wavefront per topic)
+__global__ __launch_bounds__(256) void k_densify(uint32_t n, const uint32_t *__restrict__ dcount,
                                                 const uint64_t *__restrict__ dstart,
-                                                const uint64_t *__restrict__ doffs, const uint64_t *__restrict__ dbuf,
-                                                uint64_t *__restrict__ dout, const uint32_t *__restrict__ hcount,
+                                                const uint64_t *__restrict__ doffs, const uint64_t *__restrict__ dsrc,
+                                                uint64_t *__restrict__ ddst, const uint32_t *__restrict__ hcount,
                                                 const uint64_t *__restrict__ hstart,
-                                                const uint64_t *__restrict__ hoffs, const uint32_t *__restrict__ hbuf,
-                                                uint32_t *__restrict__ hout, Caps caps) {
+                                                const uint64_t *__restrict__ hoffs, const uint32_t *__restrict__ hsrc,
+                                                uint32_t *__restrict__ hdst) {
   const int lane = threadIdx.x & (kWave - 1);
   const uint32_t nwaves = gridDim.x * (blockDim.x / kWave);
   for (uint32_t t = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave; t < n; t += nwaves) {
     const uint32_t D = dcount[t], H = hcount[t];
-    if (D) {
-      const uint64_t src = dstart[t], dst = doffs[t];
-      if (src != kNoSpace && src + D <= caps.dcap && dst + D <= caps.dcap)
-        for (uint32_t j = lane; j < D; j += kWave) dout[dst + j] = dbuf[src + j];
-    }
-    if (H) {
-      const uint64_t src = hstart[t], dst = hoffs[t];
-      if (src != kNoSpace && src + H <= caps.hcap && dst + H <= caps.hcap)
-        for (uint32_t j = lane; j < H; j += kWave) hout[dst + j] = hbuf[src + j];
-    }
+    const uint64_t ds = dstart[t], dd = doffs[t], hs = hstart[t], hd = hoffs[t];
+    for (uint32_t j = lane; j < D; j += kWave) ddst[dd + j] = dsrc[ds + j];
+    for (uint32_t j = lane; j < H; j += kWave) hdst[hd + j] = hsrc[hs + j];
   }
 }
 
@@ -904,167 +837,172 @@ static int scan_offsets(Workspace &ws, const T *counts, uint64_t *offs, uint32_t
   return 0;
 }
 
-// capacity for a redo: what was handed out before the buffer ran out, what
-// was still requested after, and one chunk of slack per wave
-static void grow_caps(Workspace &ws, const Counters &c, uint32_t waves, const Caps &caps) {
-  if (c.overflow & 1) ws.dcap = (std::min<uint64_t>(c.dpos, ws.dcap) + c.miss[0] + waves * (uint64_t)caps.dchunk) * 5 / 4;
-  if (c.overflow & 2) ws.hcap = (std::min<uint64_t>(c.hpos, ws.hcap) + c.miss[1] + waves * (uint64_t)caps.hchunk) * 5 / 4;
-  if (c.overflow & 4) ws.bcap = (std::min<uint64_t>(c.bpos, ws.bcap) + c.miss[2] + waves * (uint64_t)caps.bchunk) * 5 / 4;
-}
-
-static uint32_t chunk_for(uint64_t cap, uint32_t waves, uint32_t lo, uint32_t hi) {
-  uint64_t c = cap / (8ull * waves);
-  return (uint32_t)std::max<uint64_t>(lo, std::min<uint64_t>(hi, c));
-}
-
-static int match_once(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes, const uint64_t *d_offs,
-                      uint32_t n, hipStream_t st, MatchOutput *out, bool *retry) {
+int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes, const uint64_t *d_offs,
+                 uint32_t n, hipStream_t st, MatchOutput *out) {
   using W = Workspace;
-  *retry = false;
-  if (ws.get(W::kDCount, sizeof(uint32_t) * (n + 1)) || ws.get(W::kHCount, sizeof(uint32_t) * (n + 1)) ||
-      ws.get(W::kDStart, sizeof(uint64_t) * (n + 1)) || ws.get(W::kHStart, sizeof(uint64_t) * (n + 1)) ||
-      ws.get(W::kCls, n + 1) || ws.get(W::kDfsList, sizeof(uint32_t) * (n + 1)) ||
-      ws.get(W::kRecs, sizeof(uint32_t) * kRecStride * ((uint64_t)n + 1)) ||
-      ws.get(W::kCounters, sizeof(Counters)) || ws.get(W::kDOffs, sizeof(uint64_t) * (n + 1)) ||
-      ws.get(W::kHOffs, sizeof(uint64_t) * (n + 1)) || ws.get(W::kDBuf, sizeof(uint64_t) * (ws.dcap + 1)) ||
-      ws.get(W::kHBuf, sizeof(uint32_t) * (ws.hcap + 1)) || ws.get(W::kBigList, sizeof(uint32_t) * (ws.bcap + 1)) ||
-      ws.get(W::kDOut, sizeof(uint64_t) * (ws.dcap + 1)) || ws.get(W::kHOut, sizeof(uint32_t) * (ws.hcap + 1)))
+  if (ws.get(W::kSCount, sizeof(uint32_t) * (n + 1)) || ws.get(W::kHCount, sizeof(uint32_t) * (n + 1)) ||
+      ws.get(W::kDCount, sizeof(uint32_t) * (n + 1)) || ws.get(W::kDStart, sizeof(uint64_t) * (n + 1)) ||
+      ws.get(W::kHStart, sizeof(uint64_t) * (n + 1)) || ws.get(W::kCls, n + 1) ||
+      ws.get(W::kDfsList, sizeof(uint32_t) * (n + 2)) ||
+      ws.get(W::kRecs, sizeof(uint32_t) * kRecStride * ((uint64_t)n + 1)) || ws.get(W::kCounters, 256))
     return -2;
   if (!ws.host_pinned && hipHostMalloc(&ws.host_pinned, 256, hipHostMallocDefault) != hipSuccess) return -2;
   Counters *hc = reinterpret_cast<Counters *>(ws.host_pinned);
   uint64_t *hp = reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(ws.host_pinned) + 128);
   static_assert(sizeof(Counters) <= 128, "pinned layout");
 
-  const uint32_t walk_blocks = std::max<uint32_t>(
-      1, std::min<uint32_t>((n + kWalkWaves * kGroups - 1) / (kWalkWaves * kGroups), ws.max_blocks));
-  const uint32_t waves = walk_blocks * kWalkWaves;
-  const uint32_t small_blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + kSmallWaves - 1) / kSmallWaves, 2048));
-  const uint32_t alloc_waves = std::max(waves, small_blocks * kSmallWaves);
   Outputs o;
-  o.dcount = (uint32_t *)ws.ptr(W::kDCount);
+  o.scount = (uint32_t *)ws.ptr(W::kSCount);
   o.hcount = (uint32_t *)ws.ptr(W::kHCount);
+  o.dcount = (uint32_t *)ws.ptr(W::kDCount);
   o.dstart = (uint64_t *)ws.ptr(W::kDStart);
   o.hstart = (uint64_t *)ws.ptr(W::kHStart);
   o.cls = (uint8_t *)ws.ptr(W::kCls);
   o.dfs_list = (uint32_t *)ws.ptr(W::kDfsList);
-  o.big_list = (uint32_t *)ws.ptr(W::kBigList);
   o.recs = (uint32_t *)ws.ptr(W::kRecs);
   o.ctr = (Counters *)ws.ptr(W::kCounters);
-  o.dbuf = (uint64_t *)ws.ptr(W::kDBuf);
-  o.hbuf = (uint32_t *)ws.ptr(W::kHBuf);
-  Caps caps;
-  caps.dcap = ws.dcap;
-  caps.hcap = ws.hcap;
-  caps.bcap = ws.bcap;
-  caps.dchunk = chunk_for(ws.dcap, alloc_waves, 256, 8192);
-  caps.hchunk = chunk_for(ws.hcap, alloc_waves, 64, 4096);
-  caps.bchunk = chunk_for(ws.bcap, alloc_waves, 4, 64);
+  // the big-topic list reuses the DFS list's tail? no: its own region after the record array
+  const uint32_t walk_blocks = std::max<uint32_t>(
+      1, std::min<uint32_t>((n + kWalkWaves * kGroups - 1) / (kWalkWaves * kGroups), ws.max_blocks));
 
   HIP_TRY(hipMemsetAsync(o.ctr, 0, sizeof(Counters), st));
-  HIP_TRY(hipMemsetAsync(o.big_list, 0xFF, sizeof(uint32_t) * ws.bcap, st));
   mark(ws, 0, st);
-  if (n > 0)
-    hipLaunchKernelGGL(k_walk, dim3(walk_blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o, caps);
+  if (n > 0) hipLaunchKernelGGL(k_walk, dim3(walk_blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o);
   HIP_TRY(hipGetLastError());
   mark(ws, 1, st);
-  if (n > 0) hipLaunchKernelGGL(k_small, dim3(small_blocks), dim3(kWave * kSmallWaves), 0, st, s, n, o, caps);
-  HIP_TRY(hipGetLastError());
-  // k_big grid-strides over the big list (its length is read on the device)
-  hipLaunchKernelGGL(k_big, dim3(256 * 3), dim3(kBigThreads), 0, st, s, o, caps);
-  HIP_TRY(hipGetLastError());
-  mark(ws, 2, st);
+  if (scan_offsets(ws, o.scount, o.dstart, n, st) || scan_offsets(ws, o.hcount, o.hstart, n, st)) return -3;
   HIP_TRY(hipMemcpyAsync(hc, o.ctr, sizeof(Counters), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(hp, o.dstart + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(hp + 1, o.hstart + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   const uint32_t n_dfs = hc->n_dfs;
-  out->n_fallback = n_dfs;
-  out->n_big = (uint32_t)std::min<uint64_t>(hc->bpos, ws.bcap);
+  const uint64_t s_total = hp[0], h_total = hp[1];
   for (int i = 0; i < 5; i++) ws.why[i] = hc->why[i];
-  if (hc->overflow) {  // grow to the measured need and redo the batch
-    grow_caps(ws, *hc, alloc_waves, caps);
-    *retry = true;
-    return 0;
-  }
 
+  // DFS phase 0: exact raw / shared counts size the tail regions
+  uint64_t dfs_raw = 0, dfs_h = 0, tab_total = 0;
+  const uint32_t max_levels = s.height + 1;
+  const size_t fb_lds = sizeof(uint32_t) * (((max_levels + 1) & ~1u) + 4 * (2 * max_levels + 8)) +
+                        sizeof(uint64_t) * 2 * max_levels;
+  const uint32_t fb_blocks = std::max<uint32_t>(1, std::min<uint32_t>(n_dfs, 4096));
+  uint64_t *raw_cnt = nullptr, *raw_h = nullptr, *tab_off = nullptr;
   if (n_dfs) {
-    const uint32_t max_levels = s.height + 1;
-    const size_t fb_lds = sizeof(uint32_t) * (((max_levels + 1) & ~1u) + 4 * (2 * max_levels + 8)) +
-                          sizeof(uint64_t) * 2 * max_levels;
-    const uint32_t fb_blocks = std::max<uint32_t>(1, std::min<uint32_t>(n_dfs, 4096));
-    if (ws.get(W::kRawCnt, sizeof(uint64_t) * (n_dfs + 1)) || ws.get(W::kTabOff, sizeof(uint64_t) * (n_dfs + 2)) ||
+    if (ws.get(W::kRawCnt, sizeof(uint64_t) * 2 * (n_dfs + 1)) || ws.get(W::kTabOff, sizeof(uint64_t) * (n_dfs + 2)) ||
         ws.get(W::kTabSize, sizeof(uint64_t) * (n_dfs + 1)))
       return -2;
-    auto *raw_cnt = (uint64_t *)ws.ptr(W::kRawCnt);
-    auto *tab_off = (uint64_t *)ws.ptr(W::kTabOff);
+    raw_cnt = (uint64_t *)ws.ptr(W::kRawCnt);
+    raw_h = raw_cnt + n_dfs + 1;
+    tab_off = (uint64_t *)ws.ptr(W::kTabOff);
     auto *tab_size = (uint64_t *)ws.ptr(W::kTabSize);
-    hipLaunchKernelGGL(k_dfs<0>, dim3(fb_blocks), dim3(kWave), fb_lds, st, s, d_bytes, d_offs, o, caps, raw_cnt,
+    hipLaunchKernelGGL(k_dfs<0>, dim3(fb_blocks), dim3(kWave), fb_lds, st, s, d_bytes, d_offs, o, raw_cnt, raw_h,
                        nullptr, nullptr, max_levels);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_table_sizes, dim3((n_dfs + 255) / 256), dim3(256), 0, st, raw_cnt, o.ctr, tab_size);
     HIP_TRY(hipGetLastError());
     if (scan_offsets(ws, tab_size, tab_off, n_dfs, st)) return -3;
+    std::vector<uint64_t> rc(2 * (n_dfs + 1));
+    HIP_TRY(hipMemcpyAsync(rc.data(), raw_cnt, sizeof(uint64_t) * 2 * (n_dfs + 1), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(hp, tab_off + n_dfs, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    const uint64_t tab_total = hp[0];
+    tab_total = hp[0];
+    for (uint32_t i = 0; i < n_dfs; i++) {
+      dfs_raw += rc[i];
+      dfs_h += rc[n_dfs + 1 + i];
+    }
+  }
+  // outputs: scanned segments, then the DFS tails
+  if (ws.get(W::kDOut, sizeof(uint64_t) * (s_total + dfs_raw + 1)) ||
+      ws.get(W::kHOut, sizeof(uint32_t) * (h_total + dfs_h + 1)) ||
+      ws.get(W::kDense, sizeof(uint32_t) * (n + 1)))  // big list
+    return -2;
+  o.dout = (uint64_t *)ws.ptr(W::kDOut);
+  o.hout = (uint32_t *)ws.ptr(W::kHOut);
+  o.big_list = (uint32_t *)ws.ptr(W::kDense);
+  o.n_big = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(o.ctr) + 128);
+
+  mark(ws, 2, st);
+  const uint32_t small_blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + kSmallWaves - 1) / kSmallWaves, 4096));
+  if (n > 0) hipLaunchKernelGGL(k_small, dim3(small_blocks), dim3(kWave * kSmallWaves), 0, st, s, n, o);
+  HIP_TRY(hipGetLastError());
+  if (n > 0) {  // list the big topics (count stays on the device)
+    size_t tmp = 0;
+    hipcub::CountingInputIterator<uint32_t> it(0);
+    HIP_TRY(hipcub::DeviceSelect::If(nullptr, tmp, it, o.big_list, o.n_big, n, IsBig{o.cls}, st));
+    if (ws.get(W::kScanTmp, tmp)) return -2;
+    HIP_TRY(hipcub::DeviceSelect::If(ws.ptr(W::kScanTmp), tmp, it, o.big_list, o.n_big, n, IsBig{o.cls}, st));
+    hipLaunchKernelGGL(k_big, dim3(256 * 3), dim3(kBigThreads), 0, st, s, o);
+    HIP_TRY(hipGetLastError());
+  }
+  if (n_dfs) {
+    hp[4] = s_total;  // Counters::dtail, Counters::htail (pinned staging)
+    hp[5] = h_total;
+    HIP_TRY(hipMemcpyAsync(o.ctr, hp + 4, 2 * sizeof(unsigned long long), hipMemcpyHostToDevice, st));
     if (ws.get(W::kTable, sizeof(GEnt) * (tab_total + 1))) return -2;
     GEnt *tab = (GEnt *)ws.ptr(W::kTable);
     HIP_TRY(hipMemsetAsync(tab, 0, sizeof(GEnt) * tab_total, st));
-    hipLaunchKernelGGL(k_dfs<1>, dim3(fb_blocks), dim3(kWave), fb_lds, st, s, d_bytes, d_offs, o, caps, raw_cnt,
+    hipLaunchKernelGGL(k_dfs<1>, dim3(fb_blocks), dim3(kWave), fb_lds, st, s, d_bytes, d_offs, o, raw_cnt, raw_h,
                        tab_off, tab, max_levels);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_dfs<2>, dim3(fb_blocks), dim3(kWave), fb_lds, st, s, d_bytes, d_offs, o, caps, raw_cnt,
+    hipLaunchKernelGGL(k_dfs<2>, dim3(fb_blocks), dim3(kWave), fb_lds, st, s, d_bytes, d_offs, o, raw_cnt, raw_h,
                        tab_off, tab, max_levels);
     HIP_TRY(hipGetLastError());
   }
-
-  auto *doffs = (uint64_t *)ws.ptr(W::kDOffs);
-  auto *hoffs = (uint64_t *)ws.ptr(W::kHOffs);
-  if (scan_offsets(ws, o.dcount, doffs, n, st) || scan_offsets(ws, o.hcount, hoffs, n, st)) return -3;
-  auto *dout = (uint64_t *)ws.ptr(W::kDOut);
-  auto *hout = (uint32_t *)ws.ptr(W::kHOut);
   mark(ws, 3, st);
-  if (n > 0)
-    hipLaunchKernelGGL(k_compact, dim3(std::min<uint32_t>((n + 3) / 4, 8192)), dim3(256), 0, st, n, o.dcount, o.dstart,
-                       doffs, o.dbuf, dout, o.hcount, o.hstart, hoffs, o.hbuf, hout, caps);
-  HIP_TRY(hipGetLastError());
-  mark(ws, 4, st);
-  HIP_TRY(hipMemcpyAsync(hc, o.ctr, sizeof(Counters), hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipMemcpyAsync(hp, doffs + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipMemcpyAsync(hp + 1, hoffs + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
-  if (hc->overflow) {
-    grow_caps(ws, *hc, alloc_waves, caps);
-    *retry = true;
-    return 0;
+  // totals for the caller: sum of counts
+  {
+    size_t tmp = 0;
+    uint64_t *sums = reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(o.ctr) + 192);
+    HIP_TRY(hipcub::DeviceReduce::Sum(nullptr, tmp, o.dcount, sums, n, st));
+    if (ws.get(W::kScanTmp, tmp)) return -2;
+    HIP_TRY(hipcub::DeviceReduce::Sum(ws.ptr(W::kScanTmp), tmp, o.dcount, sums, n, st));
+    HIP_TRY(hipcub::DeviceReduce::Sum(ws.ptr(W::kScanTmp), tmp, o.hcount, sums + 1, n, st));
+    HIP_TRY(hipMemcpyAsync(hp, sums, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(hp + 2, o.n_big, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
   }
   if (ws.profile) {
     ws.prof_calls++;
     ws.prof_fallback_topics += n_dfs;
     ws.prof_walk_ms += elapsed(ws, 0, 1);
-    ws.prof_big_ms += elapsed(ws, 1, 2);
-    ws.prof_compact_ms += elapsed(ws, 3, 4);
-    ws.prof_total_ms += elapsed(ws, 0, 4);
+    ws.prof_dedupe_ms += elapsed(ws, 2, 3);
+    ws.prof_total_ms += elapsed(ws, 0, 3);
   }
   out->n_topics = n;
   out->n_deliveries = hp[0];
   out->n_shared = hp[1];
-  out->offsets = doffs;
-  out->deliveries = dout;
-  out->shared_offsets = hoffs;
-  out->shared = hout;
+  out->n_big = (uint32_t)hp[2];
+  out->n_fallback = n_dfs;
+  out->starts = o.dstart;
+  out->counts = o.dcount;
+  out->deliveries = o.dout;
+  out->shared_starts = o.hstart;
+  out->shared_counts = o.hcount;
+  out->shared = o.hout;
   return 0;
 }
 
-int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes, const uint64_t *d_offs,
-                 uint32_t n, hipStream_t st, MatchOutput *out) {
-  if (ws.dcap == 0) ws.dcap = std::max<uint64_t>(1u << 20, 64ull * n);
-  if (ws.hcap == 0) ws.hcap = std::max<uint64_t>(1u << 16, 4ull * n);
-  if (ws.bcap == 0) ws.bcap = std::max<uint64_t>(1u << 12, n / 4 + 1);
-  for (int attempt = 0; attempt < 4; attempt++) {
-    bool retry = false;
-    int rc = match_once(s, ws, d_bytes, d_offs, n, st, out, &retry);
-    if (rc != 0 || !retry) return rc;
-  }
-  return -4;  // MQM_ELIMIT: capacities kept growing
+int densify(Workspace &ws, const MatchOutput &m, hipStream_t st, DenseOutput *out) {
+  using W = Workspace;
+  const uint32_t n = m.n_topics;
+  if (ws.get(W::kDenseOffs, sizeof(uint64_t) * (n + 1)) || ws.get(W::kDenseHOffs, sizeof(uint64_t) * (n + 1)) ||
+      ws.get(W::kTable, std::max(sizeof(uint64_t) * (m.n_deliveries + 1), sizeof(uint32_t) * (m.n_shared + 1))))
+    return -2;
+  auto *doffs = (uint64_t *)ws.ptr(W::kDenseOffs);
+  auto *hoffs = (uint64_t *)ws.ptr(W::kDenseHOffs);
+  if (scan_offsets(ws, m.counts, doffs, n, st) || scan_offsets(ws, m.shared_counts, hoffs, n, st)) return -3;
+  // dense deliveries in kTable; dense shared after them in kDenseShared
+  if (ws.get(W::kDenseShared, sizeof(uint32_t) * (m.n_shared + 1))) return -2;
+  auto *dd = (uint64_t *)ws.ptr(W::kTable);
+  auto *hd = (uint32_t *)ws.ptr(W::kDenseShared);
+  if (n > 0)
+    hipLaunchKernelGGL(k_densify, dim3(std::min<uint32_t>((n + 3) / 4, 8192)), dim3(256), 0, st, n, m.counts,
+                       m.starts, doffs, m.deliveries, dd, m.shared_counts, m.shared_starts, hoffs, m.shared, hd);
+  HIP_TRY(hipGetLastError());
+  out->offsets = doffs;
+  out->deliveries = dd;
+  out->shared_offsets = hoffs;
+  out->shared = hd;
+  return 0;
 }
 
 }  // namespace mqm

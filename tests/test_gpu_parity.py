@@ -179,21 +179,31 @@ def test_full_size_c2_properties():
     tb = torch.from_numpy(w.topics.data).to(dev)
     to = torch.from_numpy(w.topics.offs.view(np.int64)).to(dev)
     n = len(w.topics)
+    def segments(r):
+        starts = _dev_copy(r.starts, n * 8).view(np.uint64).astype(np.int64)
+        counts = _dev_copy(r.counts, n * 4).view(np.uint32).astype(np.int64)
+        end = int((starts + counts).max()) if n else 0
+        buf = _dev_copy(r.deliveries, end * 8).view(np.uint64)
+        tid = np.repeat(np.arange(n, dtype=np.int64), counts)
+        pos = np.repeat(starts - np.concatenate([[0], np.cumsum(counts)[:-1]]), counts) + np.arange(counts.sum())
+        return starts, counts, buf[pos], tid
+
     r1 = idx.match_device(tb.data_ptr(), to.data_ptr(), n)
     torch.cuda.synchronize()
     nd = int(r1.n_deliveries)
-    offs = _dev_copy(r1.offsets, (n + 1) * 8).view(np.uint64)
-    ents = _dev_copy(r1.deliveries, nd * 8).view(np.uint64)
+    starts, counts, ents, tid = segments(r1)
     r2 = idx.match_device(tb.data_ptr(), to.data_ptr(), n)
     torch.cuda.synchronize()
     assert int(r2.n_deliveries) == nd
-    assert np.array_equal(_dev_copy(r2.deliveries, nd * 8).view(np.uint64), ents)
-    assert offs[0] == 0 and offs[-1] == nd and np.all(np.diff(offs.astype(np.int64)) >= 0)
+    s2, c2, e2, _ = segments(r2)
+    assert np.array_equal(c2, counts) and np.array_equal(s2, starts) and np.array_equal(e2, ents)
+    assert counts.sum() == nd
+    # segments in topic order, non-overlapping
+    assert np.all(np.diff(starts) >= counts[:-1])
     clients = (ents & 0xFFFFFFFF).astype(np.uint32)
     assert clients.max() < idx.num_clients()
     assert np.all(((ents >> 60) & 3) <= 2)
-    tid = np.repeat(np.arange(n, dtype=np.uint64), np.diff(offs.astype(np.int64)))
-    key = (tid << np.uint64(32)) | clients.astype(np.uint64)
+    key = (tid.astype(np.uint64) << np.uint64(32)) | clients.astype(np.uint64)
     assert len(np.unique(key)) == nd, "a client appears twice in one topic"
     # exact agreement on a deterministic sample of topics
     rng = np.random.default_rng(5)
