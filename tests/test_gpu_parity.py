@@ -196,10 +196,15 @@ def test_full_size_c2_properties():
     torch.cuda.synchronize()
     assert int(r2.n_deliveries) == nd
     s2, c2, e2, _ = segments(r2)
-    assert np.array_equal(c2, counts) and np.array_equal(s2, starts) and np.array_equal(e2, ents)
+    # same per-topic results run to run (DFS-path topics live in a tail whose
+    # placement and internal order follow atomics: compare as sets)
+    assert np.array_equal(c2, counts)
+    order1, order2 = np.lexsort((ents, tid)), np.lexsort((e2, tid))
+    assert np.array_equal(ents[order1], e2[order2])
     assert counts.sum() == nd
-    # segments in topic order, non-overlapping
-    assert np.all(np.diff(starts) >= counts[:-1])
+    # segments never overlap
+    o = np.argsort(starts, kind="stable")
+    assert np.all(starts[o][1:] >= (starts + counts)[o][:-1])
     clients = (ents & 0xFFFFFFFF).astype(np.uint32)
     assert clients.max() < idx.num_clients()
     assert np.all(((ents >> 60) & 3) <= 2)
