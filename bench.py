@@ -73,6 +73,7 @@ def main():
     dev = torch.device("cuda", local)
 
     import maxmq_amd
+    from maxmq_amd import shard
     from tools import mqgen
 
     overrides = {}
@@ -89,11 +90,7 @@ def main():
     t0 = time.time()
     idx = maxmq_amd.TopicsIndex(device=local, autocommit=False)
     if args.mode == "sharded" and world > 1:
-        ncl = int(w.client_ids.max()) + 1
-        lo, hi = rank * ncl // world, (rank + 1) * ncl // world
-        keep = np.nonzero((w.client_ids >= lo) & (w.client_ids < hi))[0]
-        shard = _subset_workload(w, keep)
-        idx.subscribe_workload(shard)
+        idx.subscribe_workload(shard.shard_workload(w, world, rank))
     else:
         idx.subscribe_workload(w)
     idx.commit()
@@ -109,14 +106,13 @@ def main():
 
     def step():
         if args.mode == "sharded" and world > 1:
-            # the publish batch enters at rank 0 and is broadcast over xGMI
-            dist.broadcast(tb, src=0)
-            dist.broadcast(to, src=0)
+            # the publish batch enters at rank 0 and is broadcast over xGMI (RCCL)
+            shard.broadcast_batch(dist, tb, to, src=0)
         r = idx.match_device(tb.data_ptr(), to.data_ptr(), n, stream.cuda_stream)
         if args.mode == "sharded" and world > 1:
             # per-topic delivery counts of every shard, summed at rank 0
             _dev_to_tensor(r.counts, counts)
-            dist.reduce(counts, dst=0)
+            shard.reduce_counts(dist, counts, dst=0)
         return r
 
     for _ in range(args.warmup):
@@ -203,23 +199,6 @@ def main():
     if dist:
         dist.barrier()
         dist.destroy_process_group()
-
-
-def _subset_workload(w, keep):
-    from tools.mqgen import Strings
-
-    def sub_strings(s):
-        items = [bytes(s.data[s.offs[i]:s.offs[i + 1]]) for i in keep]
-        return Strings.from_list(items)
-
-    class W:
-        pass
-
-    o = W()
-    o.filters, o.clients = sub_strings(w.filters), sub_strings(w.clients)
-    for k in ("qos", "no_local", "rap", "rh", "ident", "client_ids"):
-        setattr(o, k, getattr(w, k)[keep])
-    return o
 
 
 def _dev_to_tensor(ptr, t):
