@@ -54,6 +54,7 @@ constexpr int kLMax = 16;                // levels cached per topic (one per lan
 constexpr int kFCap = 16;                // frontier nodes per level
 constexpr int kHCap = 48;                // non-shared hits per topic (3 per lane)
 constexpr int kShCap = 16;               // shared hits per topic
+constexpr int kStage = 64;               // topic bytes staged in LDS (4 per lane, one round trip)
 // record: [0] nh, [1] S, [2 + r] off of rank r, [kRecPre + r] pre[r] (r <= nh),
 //         [kRecSh] nsh, [kRecSh + 1 + 2i] shared (off, cnt)
 constexpr int kRecPre = 2 + kHCap;
@@ -109,6 +110,7 @@ struct TopicLds {              // k_walk context of one topic (one 16-lane group
   uint32_t s_cnt[kHCap];       // counts in rank order
   uint32_t sh_off[kShCap];
   uint32_t sh_cnt[kShCap];
+  uint8_t stage[kStage];       // the topic's first kStage bytes
 };
 
 __device__ __forceinline__ void wave_lds_sync() {
@@ -146,18 +148,25 @@ __device__ uint32_t probe_edge(const DeviceSnapshot &s, uint32_t parent, uint64_
   Key key{k0, k1};
   uint64_t slot = (edge_hash(parent, key) & s.bucket_mask) * kEdgesPerBucket;
   for (;;) {
-    const EdgeEntry *e = s.edges + slot;
-    const ulonglong2 kk = *reinterpret_cast<const ulonglong2 *>(e);
-    const uint4 pc = *reinterpret_cast<const uint4 *>(&e->parent);
+    // the whole 64-B entry in one round trip: key, header and the child's descriptor
+    const uint4 *q = reinterpret_cast<const uint4 *>(s.edges + slot);
+    const uint4 kk = q[0], pc = q[1], d0 = q[2], d1 = q[3];
     if (pc.x == kNone) return kNone;
-    if (pc.x == parent && kk.x == k0 && kk.y == k1) {
+    if (pc.x == parent && (((uint64_t)kk.y << 32) | kk.x) == k0 && (((uint64_t)kk.w << 32) | kk.z) == k1) {
       bool ok = true;
       if (key_is_long(key)) {
         ok = pc.w == tok_len;
         for (uint32_t i = 0; ok && i < tok_len; i++) ok = s.tok_pool[pc.z + i] == tok[i];
       }
       if (ok) {
-        *desc = load_desc(&e->desc);
+        desc->plus = d0.x;
+        desc->hash = d0.y;
+        desc->sub_off = d0.z;
+        desc->sub_cnt = d0.w;
+        desc->hsub_off = d1.x;
+        desc->hsub_cnt = d1.y;
+        desc->sh_off = d1.z;
+        desc->sh_cnt_flags = d1.w;
         return pc.y;
       }
     }
@@ -211,18 +220,33 @@ __global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, co
     uint32_t why = kNoWhy;
 
     // ---- 1. tokenize ------------------------------------------------------
+    // each lane issues kStage/kG independent byte loads per chunk (one round
+    // trip); the first chunk is kept in LDS for the key build below
     uint32_t nsep = 0;
     bool dollar = false;
-    for (uint32_t base = 0; base < len && nsep < (uint32_t)kLMax; base += kG) {
-      const uint32_t p = base + gl;
-      const uint8_t b = p < len ? tp[p] : 0;
-      if (base == 0) dollar = __shfl(b, gbase, 64) == '$';
-      const uint32_t m = (uint32_t)(__ballot(p < len && b == '/') >> gbase) & 0xFFFFu;
-      if (b == '/' && p < len) {
-        const uint32_t idx = nsep + __popc(m & gmask_lt);
-        if (idx < (uint32_t)kLMax) L.sep[idx] = p;
+    for (uint32_t base = 0; base < len && nsep < (uint32_t)kLMax; base += kStage) {
+      uint8_t b[kStage / kG];
+#pragma unroll
+      for (int j = 0; j < kStage / kG; j++) {
+        const uint32_t p = base + j * kG + gl;
+        b[j] = p < len ? tp[p] : 0;
       }
-      nsep += __popc(m);
+      if (base == 0) {
+#pragma unroll
+        for (int j = 0; j < kStage / kG; j++) L.stage[j * kG + gl] = b[j];
+        dollar = __shfl(b[0], gbase, 64) == '$';
+      }
+#pragma unroll
+      for (int j = 0; j < kStage / kG; j++) {
+        const uint32_t p = base + j * kG + gl;
+        const bool sep = p < len && b[j] == '/';
+        const uint32_t m = (uint32_t)(__ballot(sep) >> gbase) & 0xFFFFu;
+        if (sep) {
+          const uint32_t idx = nsep + __popc(m & gmask_lt);
+          if (idx < (uint32_t)kLMax) L.sep[idx] = p;
+        }
+        nsep += __popc(m);
+      }
     }
     // levels known: 0 .. nlev-1, with nlev capped at kLMax + 1
     const uint32_t nlev = len == 0 ? 0 : (nsep >= (uint32_t)kLMax ? kLMax + 1 : nsep + 1);
@@ -230,7 +254,8 @@ __global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, co
     if ((uint32_t)gl < nlev) {
       const uint32_t st = gl == 0 ? 0 : L.sep[gl - 1] + 1;
       const uint32_t en = ((uint32_t)gl < nsep) ? L.sep[gl] : len;
-      Key k = make_key([&](uint32_t i) { return tp[st + i]; }, en - st);
+      Key k = en <= (uint32_t)kStage ? make_key([&](uint32_t i) { return L.stage[st + i]; }, en - st)
+                                     : make_key([&](uint32_t i) { return tp[st + i]; }, en - st);
       L.key0[gl] = k.k0;
       L.key1[gl] = k.k1;
     }
@@ -427,7 +452,8 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(DeviceSnapshot s, 
     }
     wave_lds_sync();
     const uint32_t *off = L.rec + 2, *pre = L.rec + kRecPre;
-    uint32_t cl[kSmallPer], sid[kSmallPer], hh[kSmallPer], slot[kSmallPer];
+    uint32_t cl[kSmallPer], sid[kSmallPer], hh[kSmallPer], slot[kSmallPer], meta[kSmallPer];
+    // all subscription loads first (independent, in flight together), then the LDS inserts
 #pragma unroll
     for (int k = 0; k < kSmallPer; k++) {
       const uint32_t r = lane + k * kWave;
@@ -436,14 +462,21 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(DeviceSnapshot s, 
         sid[k] = off[hh[k]] + (r - pre[hh[k]]);
         const SubEnt e = s.subs[sid[k]];
         cl[k] = e.client;
-        uint32_t sl = table_slot(e.client, lg);
+        meta[k] = e.meta;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kSmallPer; k++) {
+      const uint32_t r = lane + k * kWave;
+      if (r < S) {
+        uint32_t sl = table_slot(cl[k], lg);
         for (;;) {
-          const uint32_t prev = atomicCAS(&L.tkey[sl], 0u, e.client + 1);
-          if (prev == 0 || prev == e.client + 1) break;
+          const uint32_t prev = atomicCAS(&L.tkey[sl], 0u, cl[k] + 1);
+          if (prev == 0 || prev == cl[k] + 1) break;
           sl = (sl + 1) & (tsize - 1);
         }
         slot[k] = sl;
-        atomicOr(&L.tbits[sl], qos_bits(e.meta));
+        atomicOr(&L.tbits[sl], qos_bits(meta[k]));
         atomicMin(&L.tmin[sl], hh[k]);
       }
     }
@@ -494,7 +527,8 @@ __global__ __launch_bounds__(kBigThreads) void k_big(DeviceSnapshot s, Outputs o
       tmin[i] = 0xFFFFFFFFu;
     }
     __syncthreads();
-    uint32_t cl[kBigPer], sid[kBigPer], hh[kBigPer], slot[kBigPer];
+    uint32_t cl[kBigPer], sid[kBigPer], hh[kBigPer], slot[kBigPer], meta[kBigPer];
+    // all subscription loads first (independent, in flight together), then the LDS inserts
 #pragma unroll
     for (int k = 0; k < kBigPer; k++) {
       const uint32_t r = tid + k * kBigThreads;
@@ -503,14 +537,21 @@ __global__ __launch_bounds__(kBigThreads) void k_big(DeviceSnapshot s, Outputs o
         sid[k] = off[hh[k]] + (r - pre[hh[k]]);
         const SubEnt e = s.subs[sid[k]];
         cl[k] = e.client;
-        uint32_t sl = table_slot(e.client, lg);
+        meta[k] = e.meta;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kBigPer; k++) {
+      const uint32_t r = tid + k * kBigThreads;
+      if (r < S) {
+        uint32_t sl = table_slot(cl[k], lg);
         for (;;) {
-          const uint32_t prev = atomicCAS(&tkey[sl], 0u, e.client + 1);
-          if (prev == 0 || prev == e.client + 1) break;
+          const uint32_t prev = atomicCAS(&tkey[sl], 0u, cl[k] + 1);
+          if (prev == 0 || prev == cl[k] + 1) break;
           sl = (sl + 1) & (tsize - 1);
         }
         slot[k] = sl;
-        atomicOr(&tbits[sl], qos_bits(e.meta));
+        atomicOr(&tbits[sl], qos_bits(meta[k]));
         atomicMin(&tmin[sl], hh[k]);
       }
     }
