@@ -166,6 +166,7 @@ int mqm_is_shared_filter(const char *filter, size_t len);                  /* Is
 typedef struct {
   uint64_t nodes, edges, edge_buckets, subs, shared, height;
   uint64_t device_bytes; /* HBM bytes held by the current snapshot */
+  uint64_t solo_subs;    /* subscriptions that skip the per-topic merge (snapshot.h kMetaMulti) */
 } mqm_snapshot_stats;
 int mqm_snapshot_stats_get(mqm_index *h, mqm_snapshot_stats *out);
 

@@ -68,7 +68,7 @@ class DeviceResult(C.Structure):
 
 class SnapshotStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("nodes", "edges", "edge_buckets", "subs", "shared", "height",
-                                          "device_bytes")]
+                                          "device_bytes", "solo_subs")]
 
 
 class Profile(C.Structure):

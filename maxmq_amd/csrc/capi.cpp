@@ -365,6 +365,7 @@ int mqm_snapshot_stats_get(mqm_index *h, mqm_snapshot_stats *out) {
   out->shared = hs.shared_info.size();
   out->height = hs.height;
   out->device_bytes = h->snap->device_bytes;
+  out->solo_subs = hs.n_solo;
   return MQM_OK;
 }
 

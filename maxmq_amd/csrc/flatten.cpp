@@ -22,6 +22,93 @@ static uint64_t next_pow2(uint64_t x) {
   return p;
 }
 
+// kMetaMulti (snapshot.h).  Levels of a filter are the keys on its node's
+// path; two filters of one client can be gathered for the same topic only if
+// the levels both have are pairwise equal or wildcards (a topic level cannot
+// equal two different literals), so a subscription whose client has no such
+// partner — and which the parent-'#' probe cannot emit twice — is solo.
+static constexpr uint32_t kMaxPairwise = 64;  // clients with more subscriptions: all multi
+
+static void mark_multi(const Store &st, const std::vector<uint32_t> &order, HostSnapshot &hs) {
+  const auto &nodes = st.nodes();
+  const uint32_t plus_tok = st.plus_token(), hash_tok = st.hash_token();
+  const uint64_t nsub = hs.sub_info.size();
+  std::vector<uint32_t> sub_node(nsub);
+  for (uint64_t i = 0; i < hs.nodes.size(); i++)
+    for (uint32_t j = 0; j < hs.nodes[i].sub_cnt; j++) sub_node[hs.nodes[i].sub_off + j] = order[i];
+  const uint32_t nc = st.clients().size();
+  std::vector<uint32_t> cstart(nc + 2, 0), by_client(nsub);
+  for (uint64_t s = 0; s < nsub; s++) cstart[hs.subs[s].client + 2]++;
+  for (uint32_t c = 0; c < nc; c++) cstart[c + 2] += cstart[c + 1];
+  for (uint64_t s = 0; s < nsub; s++) by_client[cstart[hs.subs[s].client + 1]++] = (uint32_t)s;
+  auto wild = [&](uint32_t tok) { return tok == plus_tok || tok == hash_tok; };
+  auto compatible = [&](uint32_t a, uint32_t b) {
+    while (nodes[a].depth > nodes[b].depth) a = nodes[a].parent;
+    while (nodes[b].depth > nodes[a].depth) b = nodes[b].parent;
+    for (; a != b; a = nodes[a].parent, b = nodes[b].parent) {  // common ancestor: same levels above
+      const uint32_t ka = nodes[a].key, kb = nodes[b].key;
+      if (ka != kb && !wild(ka) && !wild(kb)) return false;
+    }
+    return true;
+  };
+  for (uint32_t c = 0; c < nc; c++) {
+    const uint32_t lo = cstart[c], hi = cstart[c + 1];
+    for (uint32_t x = lo; x < hi; x++) {
+      const uint32_t sx = by_client[x], nx = sub_node[sx], px = nodes[nx].parent;
+      // the parent probe emits a '#' node's subscriptions after a literal hit on its parent
+      bool multi = hi - lo > kMaxPairwise ||
+                   (nodes[nx].key == hash_tok && px != st.root() && !wild(nodes[px].key));
+      for (uint32_t y = lo; !multi && y < hi; y++) multi = y != x && compatible(nx, sub_node[by_client[y]]);
+      if (multi) hs.subs[sx].meta |= kMetaMulti;
+      else hs.n_solo++;
+    }
+  }
+}
+
+// DeviceRetained arrays (snapshot.h) over the preorder ids
+static void build_retained(const Store &st, const std::vector<uint32_t> &order, const std::vector<uint32_t> &new_id,
+                           HostSnapshot &hs) {
+  const auto &nodes = st.nodes();
+  const uint64_t nn = order.size();
+  std::vector<uint32_t> parent(nn, kNone);
+  for (uint64_t i = 1; i < nn; i++) parent[i] = new_id[nodes[order[i]].parent];
+  hs.subtree.assign(nn, 1);
+  for (uint64_t i = nn - 1; i >= 1; i--) hs.subtree[parent[i]] += hs.subtree[i];
+  hs.child_off.assign(nn + 1, 0);
+  for (uint64_t i = 1; i < nn; i++) hs.child_off[parent[i] + 1]++;
+  for (uint64_t i = 0; i < nn; i++) hs.child_off[i + 1] += hs.child_off[i];
+  hs.child_ids.resize(nn ? nn - 1 : 0);
+  {
+    std::vector<uint32_t> cur(hs.child_off.begin(), hs.child_off.end() - 1);
+    for (uint64_t i = 1; i < nn; i++) hs.child_ids[cur[parent[i]]++] = (uint32_t)i;  // increasing ids
+  }
+  const uint32_t sys_tok = st.tokens().find("$SYS");
+  const uint32_t sys = sys_tok == kNone ? kNone : st.child(st.root(), sys_tok);
+  hs.sys_child = sys == kNone ? kNone : new_id[sys];
+  hs.cum.assign(nn + 1, 0);
+  hs.refs.clear();
+  hs.rch_off.assign(nn + 1, 0);
+  for (uint64_t i = 0; i < nn; i++) {
+    const HNode &h = nodes[order[i]];
+    hs.cum[i + 1] = hs.cum[i] + (h.retain_path ? 1u : 0u);
+    if (h.retain_path) {
+      hs.refs.push_back(h.ret_ref);
+      if (i > 0 && (uint32_t)i != hs.sys_child) hs.rch_off[parent[i] + 1]++;
+    }
+  }
+  for (uint64_t i = 0; i < nn; i++) hs.rch_off[i + 1] += hs.rch_off[i];
+  hs.rch_refs.resize(hs.rch_off[nn]);
+  {
+    std::vector<uint32_t> cur(hs.rch_off.begin(), hs.rch_off.end() - 1);
+    for (uint64_t i = 1; i < nn; i++)
+      if (nodes[order[i]].retain_path && (uint32_t)i != hs.sys_child)
+        hs.rch_refs[cur[parent[i]]++] = nodes[order[i]].ret_ref;
+  }
+  auto it = st.retained().find(std::string());
+  hs.has_empty = it != st.retained().end();
+  hs.refs.push_back(hs.has_empty ? it->second.msg_ref : 0);
+}
+
 int flatten(const Store &st, HostSnapshot *out) {
   const auto &nodes = st.nodes();
   const uint32_t plus_tok = st.plus_token(), hash_tok = st.hash_token();
@@ -88,6 +175,8 @@ int flatten(const Store &st, HostSnapshot *out) {
     d.sh_cnt_flags = (uint32_t)h.shared.size() | ((uint32_t)f << 24);
     hs.height = std::max(hs.height, h.depth);
   }
+  mark_multi(st, order, hs);
+  if (st.retained_len() > 0) build_retained(st, order, new_id, hs);
   for (uint64_t i = 0; i < nn; i++) {
     NodeDesc &d = hs.nodes[i];
     if (d.hash != kNone) {
@@ -152,13 +241,35 @@ GpuSnapshot::~GpuSnapshot() {
 int upload(std::shared_ptr<const HostSnapshot> hs, int device, std::unique_ptr<GpuSnapshot> *out) {
   if (hipSetDevice(device) != hipSuccess) return MQM_EHIP;
   auto g = std::make_unique<GpuSnapshot>();
-  const void *src[4] = {hs->nodes.data(), hs->edges.data(), hs->subs.data(), hs->tok_pool.data()};
-  const size_t sz[4] = {hs->nodes.size() * sizeof(NodeDesc), hs->edges.size() * sizeof(EdgeEntry),
-                        hs->subs.size() * sizeof(SubEnt), hs->tok_pool.size()};
-  for (int i = 0; i < 4; i++) {
+  const bool ret = !hs->cum.empty();
+  const void *src[GpuSnapshot::kNumBuffers] = {hs->nodes.data(),     hs->edges.data(),     hs->subs.data(),
+                                               hs->tok_pool.data(),  hs->subtree.data(),   hs->child_off.data(),
+                                               hs->child_ids.data(), hs->cum.data(),       hs->refs.data(),
+                                               hs->rch_off.data(),   hs->rch_refs.data()};
+  const size_t sz[GpuSnapshot::kNumBuffers] = {
+      hs->nodes.size() * sizeof(NodeDesc), hs->edges.size() * sizeof(EdgeEntry), hs->subs.size() * sizeof(SubEnt),
+      hs->tok_pool.size(),                 hs->subtree.size() * 4,                hs->child_off.size() * 4,
+      hs->child_ids.size() * 4,            hs->cum.size() * 4,                    hs->refs.size() * 8,
+      hs->rch_off.size() * 4,              hs->rch_refs.size() * 8};
+  for (int i = 0; i < GpuSnapshot::kNumBuffers; i++) {
+    if (i >= 4 && !ret) break;
     if (hipMalloc(&g->buffers[i], sz[i] ? sz[i] : 16) != hipSuccess) return MQM_ENOMEM;
     if (sz[i] && hipMemcpy(g->buffers[i], src[i], sz[i], hipMemcpyHostToDevice) != hipSuccess) return MQM_EHIP;
     g->device_bytes += sz[i];
+  }
+  if (ret) {
+    g->has_retained = true;
+    g->ret.subtree = (const uint32_t *)g->buffers[4];
+    g->ret.child_off = (const uint32_t *)g->buffers[5];
+    g->ret.child_ids = (const uint32_t *)g->buffers[6];
+    g->ret.cum = (const uint32_t *)g->buffers[7];
+    g->ret.refs = (const uint64_t *)g->buffers[8];
+    g->ret.rch_off = (const uint32_t *)g->buffers[9];
+    g->ret.rch_refs = (const uint64_t *)g->buffers[10];
+    g->ret.n_ret = hs->refs.size() - 1;
+    g->ret.n_nodes = (uint32_t)hs->nodes.size();
+    g->ret.sys_child = hs->sys_child;
+    g->ret.has_empty = hs->has_empty ? 1u : 0u;
   }
   g->dev.nodes = (const NodeDesc *)g->buffers[0];
   g->dev.edges = (const EdgeEntry *)g->buffers[1];

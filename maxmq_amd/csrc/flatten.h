@@ -28,6 +28,12 @@ struct HostSnapshot {
   uint64_t bucket_mask = 0;
   uint32_t height = 0;
   uint64_t n_edges = 0;
+  uint64_t n_solo = 0;  // subscriptions without kMetaMulti
+  // retained side (DeviceRetained), empty when nothing is retained
+  std::vector<uint32_t> subtree, child_off, child_ids, cum, rch_off;
+  std::vector<uint64_t> refs, rch_refs;
+  uint32_t sys_child = kNone;
+  bool has_empty = false;
 };
 
 // Build the snapshot; returns MQM_OK or MQM_ELIMIT.
@@ -38,7 +44,10 @@ int flatten(const Store &st, HostSnapshot *out);
 struct GpuSnapshot {
   DeviceSnapshot dev{};
   std::shared_ptr<const HostSnapshot> host;
-  void *buffers[4] = {nullptr, nullptr, nullptr, nullptr};
+  static constexpr int kNumBuffers = 11;
+  void *buffers[kNumBuffers] = {};
+  DeviceRetained ret{};
+  bool has_retained = false;
   uint64_t device_bytes = 0;
   ~GpuSnapshot();
 };

@@ -13,7 +13,7 @@ struct Workspace {
   enum Slot {
     kSCount, kHCount, kDCount, kDStart, kHStart, kCls, kDfsList, kRecs, kCounters, kDOut, kHOut,
     kDense, kDenseShared, kDenseOffs, kDenseHOffs, kScanTmp, kRawCnt, kTabOff, kTabSize, kTable,
-    kInBytes, kInOffs, kNumSlots
+    kInBytes, kInOffs, kOvfList, kNumSlots
   };
   struct Buf {
     void *p = nullptr;
@@ -22,6 +22,7 @@ struct Workspace {
   Buf bufs[kNumSlots];
   void *host_pinned = nullptr;
   uint32_t max_blocks = 2048;  // walk-kernel grid cap (grid-stride beyond)
+  uint32_t resident[3] = {0, 0, 0};  // k_big tiers, k_small: resident blocks on the device
   // why the last batch's DFS topics left the bounded path:
   // frontier, hits, cached levels, shared hits, raw entries
   uint32_t why[5] = {0, 0, 0, 0, 0};

@@ -55,26 +55,29 @@ constexpr int kFCap = 16;                // frontier nodes per level
 constexpr int kHCap = 48;                // non-shared hits per topic (3 per lane)
 constexpr int kShCap = 16;               // shared hits per topic
 constexpr int kStage = 64;               // topic bytes staged in LDS (4 per lane, one round trip)
-// record: [0] nh, [1] S, [2 + r] off of rank r, [kRecPre + r] pre[r] (r <= nh),
-//         [kRecSh] nsh, [kRecSh + 1 + 2i] shared (off, cnt)
-constexpr int kRecPre = 2 + kHCap;
-constexpr int kRecSh = kRecPre + kHCap + 1;
-constexpr int kRecStride = kRecSh + 1 + 2 * kShCap + 4;  // 136 words
-constexpr int kTCap = 512;               // k_small table slots
-constexpr int kSMax = 384;               // raw entries per k_small topic (load <= 0.75)
+// record (compact, so one 64-lane load usually fetches it whole):
+//   [0] nh | nsh << 8, [1] S,
+//   [2 + 2r] off, [3 + 2r] pre of the hit of rank r (r < nh),
+//   [2 + 2nh + 2i] off, [3 + 2nh + 2i] cnt of shared hit i (i < nsh)
+constexpr int kRecStride = 2 + 2 * kHCap + 2 * kShCap;  // 130 words (max)
+constexpr int kRecStrideAlloc = 132;                    // 16-B aligned per topic
+constexpr int kSMax = 384;               // raw entries per k_small topic
 constexpr int kSmallPer = kSMax / kWave; // entries per lane
+constexpr int kSmallSlots = 256;         // k_small merge table slots (per wave)
+constexpr int kSmallMulti = 192;         // multi entries it holds (load <= 0.75)
 constexpr int kSmallWaves = 4;
 constexpr int kBigThreads = 256;
-constexpr int kBigSlots = 4096;          // k_big table: 48 KiB of LDS
-constexpr int kBigMax = 3072;            // raw entries per k_big topic (load <= 0.75)
+constexpr int kBigSlotsA = 2048;         // k_big first tier: 24 KiB table
+constexpr int kBigSlotsB = 4096;         // overflow tier: 48 KiB, holds any bounded topic
+constexpr int kBigMax = 3072;            // raw entries per k_big topic
 constexpr int kBigPer = kBigMax / kBigThreads;
 constexpr uint32_t kNoWhy = 0xFFFFFFFFu;
 
 static_assert(kLMax == kG, "one lane per cached level");
 static_assert(kHCap == 3 * kG, "three ranked hits per lane");
-static_assert(kRecStride % 4 == 0, "16-B aligned records");
-static_assert(kSMax * 4 <= kTCap * 3, "k_small table load factor");
-static_assert(kBigMax * 4 <= kBigSlots * 3, "k_big table load factor");
+static_assert(kRecStrideAlloc % 4 == 0 && kRecStrideAlloc >= kRecStride, "16-B aligned records");
+static_assert(kSmallMulti * 4 <= kSmallSlots * 3, "k_small table load factor");
+static_assert(kBigMax * 4 <= kBigSlotsB * 3, "the overflow tier holds every bounded topic");
 static_assert(kSMax % kWave == 0 && kBigMax % kBigThreads == 0, "register tiles");
 
 enum : uint8_t { kClsDone = 0, kClsSmall = 1, kClsBig = 2, kClsDfs = 3 };
@@ -85,6 +88,7 @@ struct Counters {              // zeroed before every batch
   unsigned long long htail;    // DFS shared candidates: likewise
   unsigned int n_dfs;          // topics appended to the DFS list
   unsigned int why[5];         // DFS routing reasons (kWhy*)
+  unsigned int n_ovf;          // topics k_big<kBigSlotsA> passed to the 4096-slot tier
 };
 
 struct Outputs {
@@ -93,7 +97,7 @@ struct Outputs {
   uint8_t *cls;
   uint32_t *dfs_list;
   uint32_t *big_list, *n_big;
-  uint32_t *recs;  // kRecStride words per topic
+  uint32_t *recs;  // kRecStrideAlloc words per topic
   Counters *ctr;
   uint64_t *dout;
   uint32_t *hout;
@@ -185,12 +189,33 @@ __device__ __forceinline__ uint64_t pack_delivery(uint32_t client, uint32_t sid,
 // QoS one-hot (bits 0..2) | NoLocal (bit 3): OR-merged, max QoS = top set bit
 __device__ __forceinline__ uint32_t qos_bits(uint32_t meta) { return (1u << (meta & 3)) | (((meta >> 2) & 1) << 3); }
 
-// hit h with pre[h] <= r < pre[h+1] (pre strictly increasing: empty hits are never recorded)
-__device__ __forceinline__ uint32_t find_hit(const uint32_t *pre, uint32_t nh, uint32_t r) {
+// hit h with pre(h) <= r < pre(h+1), pre(h) = rec[3 + 2h] (strictly
+// increasing: empty hits are never recorded)
+__device__ __forceinline__ uint32_t find_hit(const uint32_t *rec, uint32_t nh, uint32_t r) {
   uint32_t h = 0;
   for (uint32_t step = 32; step > 0; step >>= 1)
-    if (h + step < nh && pre[h + step] <= r) h += step;
+    if (h + step < nh && rec[3 + 2 * (h + step)] <= r) h += step;
   return h;
+}
+
+// per-topic merge table in LDS (linear probing, key = client + 1):
+// QoS one-hot | NoLocal OR-folded, lowest hit rank kept (first-merged)
+__device__ __forceinline__ void table_insert(uint32_t *tkey, uint32_t *tbits, uint32_t *tmin, uint32_t mask,
+                                             uint32_t lg, uint32_t client, uint32_t meta, uint32_t hit) {
+  uint32_t sl = table_slot(client, lg);
+  for (;;) {
+    const uint32_t prev = atomicCAS(&tkey[sl], 0u, client + 1);
+    if (prev == 0 || prev == client + 1) break;
+    sl = (sl + 1) & mask;
+  }
+  atomicOr(&tbits[sl], qos_bits(meta));
+  atomicMin(&tmin[sl], hit);
+}
+
+__device__ __forceinline__ uint32_t table_find(const uint32_t *tkey, uint32_t mask, uint32_t lg, uint32_t client) {
+  uint32_t sl = table_slot(client, lg);
+  while (tkey[sl] != client + 1) sl = (sl + 1) & mask;
+  return sl;
 }
 
 // ---------------------------------------------------------------------------
@@ -346,14 +371,14 @@ __global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, co
     }
 
     // ---- 3. rank hits, prefix-sum their sizes into the record ---------------
-    uint32_t *rec = o.recs + (uint64_t)(active ? t : 0) * kRecStride;
+    uint32_t *rec = o.recs + (uint64_t)(active ? t : 0) * kRecStrideAlloc;
     const bool ok = active && why == kNoWhy;
     if (ok) {
       for (uint32_t i = gl; i < nh; i += kG) {
         const uint32_t r = L.hit_rank[i];
         uint32_t pos = 0;
         for (uint32_t j = 0; j < nh; j++) pos += L.hit_rank[j] < r;  // ranks are distinct
-        rec[2 + pos] = L.hit_off[i];
+        rec[2 + 2 * pos] = L.hit_off[i];
         L.s_cnt[pos] = L.hit_cnt[i];
       }
     }
@@ -375,19 +400,17 @@ __global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, co
       uint32_t p = inc - local;
       for (int k = 0; k < 3; k++) {
         const uint32_t i = 3 * gl + k;
-        if (i < nh) rec[kRecPre + i] = p;
+        if (i < nh) rec[3 + 2 * i] = p;
         p += c3[k];
       }
       if ((uint32_t)gl < nsh) {
-        rec[kRecSh + 1 + 2 * gl] = L.sh_off[gl];
-        rec[kRecSh + 2 + 2 * gl] = L.sh_cnt[gl];
+        rec[2 + 2 * nh + 2 * gl] = L.sh_off[gl];
+        rec[3 + 2 * nh + 2 * gl] = L.sh_cnt[gl];
       }
       for (uint32_t i = 0; i < nsh; i++) H += L.sh_cnt[i];
       if (gl == 0) {
-        rec[0] = nh;
+        rec[0] = nh | (nsh << 8);
         rec[1] = S;
-        rec[kRecPre + nh] = S;
-        rec[kRecSh] = nsh;
       }
       if (S > (uint32_t)kBigMax) why = kWhyEntries;
     }
@@ -407,14 +430,19 @@ __global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, co
 }
 
 // ---------------------------------------------------------------------------
-// k_small: a wavefront per topic with <= kSMax raw entries (per-wave LDS
-// table); also writes every bounded topic's shared candidates
+// k_small: a wavefront per topic with <= kSMax raw entries; also writes every
+// bounded topic's shared candidates.  The next topic's header (class, counts,
+// segment starts, the first 64 record words) is in flight while the current
+// one is processed, so a topic costs about one dependent round trip (its
+// subscription loads).  Topics whose entries are all solo (kMetaMulti clear)
+// are copied; the others merge their multi entries in a per-wave LDS table,
+// and topics with more multi entries than it holds move up to k_big.
 // ---------------------------------------------------------------------------
 struct SmallLds {
-  uint32_t rec[kRecStride];
-  uint32_t tkey[kTCap];
-  uint32_t tbits[kTCap];
-  uint32_t tmin[kTCap];
+  uint32_t rec[kRecStrideAlloc];
+  uint32_t tkey[kSmallSlots];
+  uint32_t tbits[kSmallSlots];
+  uint32_t tmin[kSmallSlots];
 };
 
 __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(DeviceSnapshot s, uint32_t n, Outputs o) {
@@ -422,80 +450,102 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(DeviceSnapshot s, 
   const int lane = threadIdx.x & (kWave - 1);
   SmallLds &L = lds_all[threadIdx.x / kWave];
   const uint32_t nwaves = gridDim.x * kSmallWaves;
-  for (uint32_t t = blockIdx.x * kSmallWaves + threadIdx.x / kWave; t < n; t += nwaves) {
-    const uint8_t cls = o.cls[t];
-    if (cls == kClsDfs) continue;
-    const uint32_t H = o.hcount[t];
-    if (cls != kClsSmall && H == 0) continue;
-    const uint32_t *rec = o.recs + (uint64_t)t * kRecStride;
+  uint32_t t = blockIdx.x * kSmallWaves + threadIdx.x / kWave;
+  uint32_t n_cls = kClsDone, n_H = 0, n_rw = 0;
+  uint64_t n_db = 0, n_hb = 0;
+  auto fetch = [&](uint32_t u) {
+    n_cls = o.cls[u];
+    n_H = o.hcount[u];
+    n_db = o.dstart[u];
+    n_hb = o.hstart[u];
+    n_rw = o.recs[(uint64_t)u * kRecStrideAlloc + lane];
+  };
+  if (t < n) fetch(t);
+  for (; t < n; t += nwaves) {
+    const uint32_t cls = n_cls, H = n_H, rw = n_rw;
+    const uint64_t db = n_db, hb = n_hb;
+    if (t + nwaves < n) fetch(t + nwaves);
+    if (cls == kClsDfs || (cls != kClsSmall && H == 0)) continue;
+    const uint32_t w0 = __shfl(rw, 0, 64), S = __shfl(rw, 1, 64);
+    const uint32_t nh = w0 & 0xFFu, nsh = w0 >> 8;
+    const uint32_t words = 2 + 2 * nh + 2 * nsh;
+    L.rec[lane] = rw;
+    for (uint32_t i = kWave + lane; i < words; i += kWave) L.rec[i] = o.recs[(uint64_t)t * kRecStrideAlloc + i];
+    wave_lds_sync();
     if (H) {  // shared candidates (gatherSharedSubscriptions, topics.go:541-555)
-      const uint32_t nsh = rec[kRecSh];
-      const uint64_t hb = o.hstart[t];
       uint32_t w = 0;
       for (uint32_t i = 0; i < nsh; i++) {
-        const uint32_t so = rec[kRecSh + 1 + 2 * i], sc = rec[kRecSh + 2 + 2 * i];
+        const uint32_t so = L.rec[2 + 2 * nh + 2 * i], sc = L.rec[3 + 2 * nh + 2 * i];
         for (uint32_t j = lane; j < sc; j += kWave) o.hout[hb + w + j] = so + j;
         w += sc;
       }
     }
-    if (cls != kClsSmall) continue;
-    const uint32_t nh = rec[0], S = rec[1];
-    for (uint32_t i = lane; i < 2 + nh; i += kWave) L.rec[i] = rec[i];
-    for (uint32_t i = lane; i <= nh; i += kWave) L.rec[kRecPre + i] = rec[kRecPre + i];
-    uint32_t lg = 6;  // load <= 0.5 up to kTCap/2 entries, <= 0.75 above
-    while ((1u << lg) < 2 * S && (1u << lg) < (uint32_t)kTCap) lg++;
-    const uint32_t tsize = 1u << lg;
-    for (uint32_t i = lane; i < tsize; i += kWave) {
-      L.tkey[i] = 0;
-      L.tbits[i] = 0;
-      L.tmin[i] = 0xFFFFFFFFu;
+    if (cls != kClsSmall) {
+      wave_lds_sync();
+      continue;
     }
-    wave_lds_sync();
-    const uint32_t *off = L.rec + 2, *pre = L.rec + kRecPre;
-    uint32_t cl[kSmallPer], sid[kSmallPer], hh[kSmallPer], slot[kSmallPer], meta[kSmallPer];
-    // all subscription loads first (independent, in flight together), then the LDS inserts
+    uint32_t cl[kSmallPer], sid[kSmallPer], hh[kSmallPer], meta[kSmallPer];
+    // all subscription loads first (independent, in flight together)
 #pragma unroll
     for (int k = 0; k < kSmallPer; k++) {
       const uint32_t r = lane + k * kWave;
+      meta[k] = 0;
       if (r < S) {
-        hh[k] = find_hit(pre, nh, r);
-        sid[k] = off[hh[k]] + (r - pre[hh[k]]);
+        hh[k] = find_hit(L.rec, nh, r);
+        sid[k] = L.rec[2 + 2 * hh[k]] + (r - L.rec[3 + 2 * hh[k]]);
         const SubEnt e = s.subs[sid[k]];
         cl[k] = e.client;
         meta[k] = e.meta;
       }
     }
+    uint32_t M = 0;  // entries that need the merge table (kMetaMulti)
 #pragma unroll
-    for (int k = 0; k < kSmallPer; k++) {
-      const uint32_t r = lane + k * kWave;
-      if (r < S) {
-        uint32_t sl = table_slot(cl[k], lg);
-        for (;;) {
-          const uint32_t prev = atomicCAS(&L.tkey[sl], 0u, cl[k] + 1);
-          if (prev == 0 || prev == cl[k] + 1) break;
-          sl = (sl + 1) & (tsize - 1);
-        }
-        slot[k] = sl;
-        atomicOr(&L.tbits[sl], qos_bits(meta[k]));
-        atomicMin(&L.tmin[sl], hh[k]);
-      }
-    }
-    wave_lds_sync();
-    const uint64_t db = o.dstart[t];
+    for (int k = 0; k < kSmallPer; k++) M += __popcll(__ballot(meta[k] & kMetaMulti));
     uint32_t D = 0;
+    if (M == 0) {  // every entry is its client's merged delivery: a straight copy
 #pragma unroll
-    for (int k = 0; k < kSmallPer; k++) {
-      const uint32_t r = lane + k * kWave;
-      bool win = false;
-      uint64_t ent = 0;
-      if (r < S) {
-        win = L.tmin[slot[k]] == hh[k];
-        const uint32_t v = L.tbits[slot[k]];
-        ent = pack_delivery(cl[k], sid[k], 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
+      for (int k = 0; k < kSmallPer; k++) {
+        const uint32_t r = lane + k * kWave;
+        if (r < S) o.dout[db + r] = pack_delivery(cl[k], sid[k], meta[k] & 3u, (meta[k] >> 2) & 1u);
       }
-      const uint64_t m = __ballot(win);
-      if (win) o.dout[db + D + __popcll(m & lanemask_lt(lane))] = ent;
-      D += __popcll(m);
+      D = S;
+    } else if (M > (uint32_t)kSmallMulti) {  // the workgroup tier takes it (k_big list is built after this kernel)
+      if (lane == 0) o.cls[t] = kClsBig;
+      wave_lds_sync();
+      continue;
+    } else {
+      uint32_t lg = 6;
+      while ((1u << lg) < 2 * M && (1u << lg) < (uint32_t)kSmallSlots) lg++;
+      const uint32_t mask = (1u << lg) - 1;
+      for (uint32_t i = lane; i <= mask; i += kWave) {
+        L.tkey[i] = 0;
+        L.tbits[i] = 0;
+        L.tmin[i] = 0xFFFFFFFFu;
+      }
+      wave_lds_sync();
+#pragma unroll
+      for (int k = 0; k < kSmallPer; k++)
+        if (meta[k] & kMetaMulti) table_insert(L.tkey, L.tbits, L.tmin, mask, lg, cl[k], meta[k], hh[k]);
+      wave_lds_sync();
+#pragma unroll
+      for (int k = 0; k < kSmallPer; k++) {
+        const uint32_t r = lane + k * kWave;
+        bool win = false;
+        uint64_t ent = 0;
+        if (r < S) {
+          uint32_t v = qos_bits(meta[k]);
+          win = true;
+          if (meta[k] & kMetaMulti) {
+            const uint32_t sl = table_find(L.tkey, mask, lg, cl[k]);
+            win = L.tmin[sl] == hh[k];
+            v = L.tbits[sl];
+          }
+          ent = pack_delivery(cl[k], sid[k], 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
+        }
+        const uint64_t m = __ballot(win);
+        if (win) o.dout[db + D + __popcll(m & lanemask_lt(lane))] = ent;
+        D += __popcll(m);
+      }
     }
     if (lane == 0) o.dcount[t] = D;
     wave_lds_sync();
@@ -503,60 +553,98 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(DeviceSnapshot s, 
 }
 
 // ---------------------------------------------------------------------------
-// k_big: a 256-thread workgroup per listed topic, 48 KiB LDS dedupe table
+// k_big<kSlots>: a 256-thread workgroup per listed topic (<= kBigMax raw
+// entries), LDS merge table of kSlots slots.  Topic ids are prefetched two
+// topics ahead and the record / segment start one topic ahead.  Topics with
+// more multi entries than the table holds go to `ovf` (the 4096-slot tier,
+// which holds any bounded topic).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kBigThreads) void k_big(DeviceSnapshot s, Outputs o) {
-  __shared__ uint32_t tkey[kBigSlots], tbits[kBigSlots], tmin[kBigSlots];
-  __shared__ uint32_t rec[kRecStride];
+template <int kSlots>
+__global__ __launch_bounds__(kBigThreads) void k_big(DeviceSnapshot s, Outputs o, const uint32_t *__restrict__ list,
+                                                    const uint32_t *__restrict__ count, uint32_t *__restrict__ ovf,
+                                                    unsigned int *__restrict__ n_ovf) {
+  __shared__ uint32_t tkey[kSlots], tbits[kSlots], tmin[kSlots];
+  __shared__ uint32_t rec[kRecStrideAlloc];
   __shared__ uint32_t wsum[kBigThreads / kWave];
+  constexpr uint32_t kMCap = kSlots * 3 / 4;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
-  const uint32_t nbig = *o.n_big;
-  for (uint32_t bi = blockIdx.x; bi < nbig; bi += gridDim.x) {
-    const uint32_t t = o.big_list[bi];
-    const uint32_t *grec = o.recs + (uint64_t)t * kRecStride;
-    if (tid < kRecPre + kHCap + 1) rec[tid] = grec[tid];
-    __syncthreads();
-    const uint32_t nh = rec[0], S = rec[1];
-    const uint32_t *off = rec + 2, *pre = rec + kRecPre;
-    uint32_t lg = 6;
-    while ((1u << lg) < 2 * S && (1u << lg) < (uint32_t)kBigSlots) lg++;
-    const uint32_t tsize = 1u << lg;
-    for (uint32_t i = tid; i < tsize; i += kBigThreads) {
-      tkey[i] = 0;
-      tbits[i] = 0;
-      tmin[i] = 0xFFFFFFFFu;
+  const uint32_t nb = *count, G = gridDim.x;
+  uint32_t bi = blockIdx.x;
+  uint32_t t_cur = bi < nb ? list[bi] : 0;
+  uint32_t t_nxt = bi + G < nb ? list[bi + G] : 0;
+  uint32_t rw = 0;
+  uint64_t db_nxt = 0;
+  if (bi < nb) {
+    if (tid < kWave) rw = o.recs[(uint64_t)t_cur * kRecStrideAlloc + tid];
+    db_nxt = o.dstart[t_cur];
+  }
+  for (; bi < nb; bi += G) {
+    const uint32_t t = t_cur;
+    const uint64_t db = db_nxt;
+    if (tid < kWave) rec[tid] = rw;
+    const uint32_t t_nn = bi + 2 * G < nb ? list[bi + 2 * G] : 0;
+    if (bi + G < nb) {
+      if (tid < kWave) rw = o.recs[(uint64_t)t_nxt * kRecStrideAlloc + tid];
+      db_nxt = o.dstart[t_nxt];
     }
+    t_cur = t_nxt;
+    t_nxt = t_nn;
     __syncthreads();
-    uint32_t cl[kBigPer], sid[kBigPer], hh[kBigPer], slot[kBigPer], meta[kBigPer];
-    // all subscription loads first (independent, in flight together), then the LDS inserts
+    const uint32_t nh = rec[0] & 0xFFu, S = rec[1];
+    if (2 + 2 * nh > (uint32_t)kWave) {  // block-uniform
+      for (uint32_t i = kWave + tid; i < 2 + 2 * nh; i += kBigThreads)
+        rec[i] = o.recs[(uint64_t)t * kRecStrideAlloc + i];
+      __syncthreads();
+    }
+    uint32_t cl[kBigPer], sid[kBigPer], hh[kBigPer], meta[kBigPer];
+    // all subscription loads first (independent, in flight together)
 #pragma unroll
     for (int k = 0; k < kBigPer; k++) {
       const uint32_t r = tid + k * kBigThreads;
+      meta[k] = 0;
       if (r < S) {
-        hh[k] = find_hit(pre, nh, r);
-        sid[k] = off[hh[k]] + (r - pre[hh[k]]);
+        hh[k] = find_hit(rec, nh, r);
+        sid[k] = rec[2 + 2 * hh[k]] + (r - rec[3 + 2 * hh[k]]);
         const SubEnt e = s.subs[sid[k]];
         cl[k] = e.client;
         meta[k] = e.meta;
       }
     }
+    uint32_t mw = 0;  // entries that need the merge table (kMetaMulti)
 #pragma unroll
-    for (int k = 0; k < kBigPer; k++) {
-      const uint32_t r = tid + k * kBigThreads;
-      if (r < S) {
-        uint32_t sl = table_slot(cl[k], lg);
-        for (;;) {
-          const uint32_t prev = atomicCAS(&tkey[sl], 0u, cl[k] + 1);
-          if (prev == 0 || prev == cl[k] + 1) break;
-          sl = (sl + 1) & (tsize - 1);
-        }
-        slot[k] = sl;
-        atomicOr(&tbits[sl], qos_bits(meta[k]));
-        atomicMin(&tmin[sl], hh[k]);
+    for (int k = 0; k < kBigPer; k++) mw += __popcll(__ballot(meta[k] & kMetaMulti));
+    if (lane == 0) wsum[wid] = mw;
+    __syncthreads();
+    uint32_t M = 0;
+    for (int w = 0; w < kBigThreads / kWave; w++) M += wsum[w];
+    if (M == 0) {  // every entry is its client's merged delivery: a straight copy
+#pragma unroll
+      for (int k = 0; k < kBigPer; k++) {
+        const uint32_t r = tid + k * kBigThreads;
+        if (r < S) o.dout[db + r] = pack_delivery(cl[k], sid[k], meta[k] & 3u, (meta[k] >> 2) & 1u);
       }
+      if (tid == 0) o.dcount[t] = S;
+      __syncthreads();
+      continue;
+    }
+    if (M > kMCap) {  // block-uniform; unreachable for the tier that holds kBigMax
+      if (tid == 0) ovf[atomicAdd(n_ovf, 1u)] = t;
+      __syncthreads();
+      continue;
+    }
+    uint32_t lg = 6;
+    while ((1u << lg) < 2 * M && (1u << lg) < (uint32_t)kSlots) lg++;
+    const uint32_t mask = (1u << lg) - 1;
+    for (uint32_t i = tid; i <= mask; i += kBigThreads) {
+      tkey[i] = 0;
+      tbits[i] = 0;
+      tmin[i] = 0xFFFFFFFFu;
     }
     __syncthreads();
-    const uint64_t db = o.dstart[t];
+#pragma unroll
+    for (int k = 0; k < kBigPer; k++)
+      if (meta[k] & kMetaMulti) table_insert(tkey, tbits, tmin, mask, lg, cl[k], meta[k], hh[k]);
+    __syncthreads();
     uint32_t D = 0;
 #pragma unroll
     for (int k = 0; k < kBigPer; k++) {
@@ -565,8 +653,13 @@ __global__ __launch_bounds__(kBigThreads) void k_big(DeviceSnapshot s, Outputs o
       bool win = false;
       uint64_t ent = 0;
       if (r < S) {
-        win = tmin[slot[k]] == hh[k];
-        const uint32_t v = tbits[slot[k]];
+        uint32_t v = qos_bits(meta[k]);
+        win = true;
+        if (meta[k] & kMetaMulti) {
+          const uint32_t sl = table_find(tkey, mask, lg, cl[k]);
+          win = tmin[sl] == hh[k];
+          v = tbits[sl];
+        }
         ent = pack_delivery(cl[k], sid[k], 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
       }
       const uint64_t m = __ballot(win);
@@ -866,6 +959,20 @@ static float elapsed(Workspace &ws, int a, int b) {
   return ms;
 }
 
+// grid = the blocks of `kern` that fit on the device at once (cached per slot)
+template <class K>
+static uint32_t resident_blocks(Workspace &ws, int slot, K kern) {
+  if (!ws.resident[slot]) {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, kBigThreads, 0) != hipSuccess || per < 1)
+      per = 2, cus = 256;
+    ws.resident[slot] = (uint32_t)(per * cus);
+  }
+  return ws.resident[slot];
+}
+
 // counts (n) -> exclusive offsets (u64, n + 1)
 template <class T>
 static int scan_offsets(Workspace &ws, const T *counts, uint64_t *offs, uint32_t n, hipStream_t st) {
@@ -885,7 +992,7 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
       ws.get(W::kDCount, sizeof(uint32_t) * (n + 1)) || ws.get(W::kDStart, sizeof(uint64_t) * (n + 1)) ||
       ws.get(W::kHStart, sizeof(uint64_t) * (n + 1)) || ws.get(W::kCls, n + 1) ||
       ws.get(W::kDfsList, sizeof(uint32_t) * (n + 2)) ||
-      ws.get(W::kRecs, sizeof(uint32_t) * kRecStride * ((uint64_t)n + 1)) || ws.get(W::kCounters, 256))
+      ws.get(W::kRecs, sizeof(uint32_t) * kRecStrideAlloc * ((uint64_t)n + 1)) || ws.get(W::kCounters, 256))
     return -2;
   if (!ws.host_pinned && hipHostMalloc(&ws.host_pinned, 256, hipHostMallocDefault) != hipSuccess) return -2;
   Counters *hc = reinterpret_cast<Counters *>(ws.host_pinned);
@@ -962,7 +1069,9 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   o.n_big = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(o.ctr) + 128);
 
   mark(ws, 2, st);
-  const uint32_t small_blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + kSmallWaves - 1) / kSmallWaves, 4096));
+  static_assert(kWave * kSmallWaves == kBigThreads, "resident_blocks assumes 256-thread blocks");
+  const uint32_t small_blocks = std::max<uint32_t>(
+      1, std::min<uint32_t>((n + kSmallWaves - 1) / kSmallWaves, resident_blocks(ws, 2, k_small)));
   if (n > 0) hipLaunchKernelGGL(k_small, dim3(small_blocks), dim3(kWave * kSmallWaves), 0, st, s, n, o);
   HIP_TRY(hipGetLastError());
   if (n > 0) {  // list the big topics (count stays on the device)
@@ -971,7 +1080,13 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
     HIP_TRY(hipcub::DeviceSelect::If(nullptr, tmp, it, o.big_list, o.n_big, n, IsBig{o.cls}, st));
     if (ws.get(W::kScanTmp, tmp)) return -2;
     HIP_TRY(hipcub::DeviceSelect::If(ws.ptr(W::kScanTmp), tmp, it, o.big_list, o.n_big, n, IsBig{o.cls}, st));
-    hipLaunchKernelGGL(k_big, dim3(256 * 3), dim3(kBigThreads), 0, st, s, o);
+    if (ws.get(W::kOvfList, sizeof(uint32_t) * (n + 1))) return -2;
+    auto *ovf = (uint32_t *)ws.ptr(W::kOvfList);
+    hipLaunchKernelGGL(k_big<kBigSlotsA>, dim3(resident_blocks(ws, 0, k_big<kBigSlotsA>)), dim3(kBigThreads), 0, st,
+                       s, o, o.big_list, o.n_big, ovf, &o.ctr->n_ovf);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_big<kBigSlotsB>, dim3(resident_blocks(ws, 1, k_big<kBigSlotsB>)), dim3(kBigThreads), 0, st,
+                       s, o, ovf, &o.ctr->n_ovf, nullptr, nullptr);
     HIP_TRY(hipGetLastError());
   }
   if (n_dfs) {

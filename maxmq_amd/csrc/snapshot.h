@@ -49,8 +49,19 @@ constexpr uint32_t kEdgesPerBucket = 2;
 // non-shared subscription entry; sid = index into the array
 struct SubEnt {
   uint32_t client;
-  uint32_t meta;          // qos[1:0] | no_local[2] | rap[3] | rh[5:4]
+  uint32_t meta;          // qos[1:0] | no_local[2] | rap[3] | rh[5:4] | multi[6]
 };
+
+// meta bit 6 ("multi"): this entry may meet another entry of the same client
+// in one topic's gather, so it must go through the per-topic merge
+// (packets.go:250-270).  Clear ("solo") only when the flattener proved that
+// no topic emits it twice (it is not on a '#' node, whose subscriptions the
+// parent probe of topics.go:507-509 can emit a second time) and that none of
+// the client's other filters is level-compatible with it (two filters can
+// both be gathered for one topic only if, at every level both have, the
+// levels are equal or one is a wildcard).  A solo entry is its client's
+// merged delivery as is.
+constexpr uint32_t kMetaMulti = 1u << 6;
 
 // delivery written by the matcher (one per (topic, client)):
 //   bits  0..31 client id
@@ -69,6 +80,27 @@ struct DeviceSnapshot {
   uint32_t n_subs;
   uint32_t n_shared;
   uint32_t height;        // max node depth (root = 0)
+};
+
+// Retained-message side of the snapshot (TopicsIndex.Messages, topics.go:426-480),
+// built only when the store holds retained messages.  Preorder ids make every
+// subtree the contiguous id range [i, i + subtree[i]), so "all retained
+// messages below a node" ('#') is a range of `refs`, located with `cum`.
+struct DeviceRetained {
+  const uint32_t *subtree;    // n_nodes: nodes in the subtree of i, i included
+  const uint32_t *child_off;  // n_nodes + 1: children of i = child_ids[child_off[i] ..)
+  const uint32_t *child_ids;  // in preorder
+  const uint32_t *cum;        // n_nodes + 1: retained nodes with id < i
+  const uint64_t *refs;       // n_ret + 1: message refs in preorder; refs[n_ret] = the
+                              //   message retained at topic "" (has_empty), see below
+  const uint32_t *rch_off;    // n_nodes + 1: retained children of i = rch_refs[rch_off[i] ..)
+  const uint64_t *rch_refs;   // (the root's list leaves out the root child "$SYS")
+  uint64_t n_ret;
+  uint32_t n_nodes;
+  uint32_t sys_child;         // the root child named exactly "$SYS", or kNone
+  uint32_t has_empty;         // a message is retained at topic "": its retainPath is ""
+                              //   (topics.go:362), so Retained.Get(particle.retainPath) of
+                              //   every literal-final node without one returns it (:474)
 };
 
 }  // namespace mqm

@@ -303,6 +303,7 @@ int64_t Store::retain_message(std::string_view topic, uint64_t msg_ref, uint32_t
   std::string key(topic);
   if (payload_len > 0) {
     nodes_[n].retain_path = !topic.empty();  // retainPath = pk.TopicName
+    nodes_[n].ret_ref = msg_ref;
     retained_[key] = RetainedRec{msg_ref, payload_len, retain_flag};
     return 1;
   }

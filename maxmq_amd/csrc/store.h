@@ -35,6 +35,7 @@ struct HNode {        // particle (topics.go:627-635)
   uint32_t n_children = 0;
   uint32_t depth = 0;
   bool retain_path = false;      // retainPath != ""
+  uint64_t ret_ref = 0;          // caller's message ref of the retained packet (retain_path)
   bool live = false;
   std::vector<SubRec> subs;      // particle.subscriptions, unique by client
   std::vector<SharedRec> shared; // particle.shared, unique by (group, client)

@@ -107,6 +107,15 @@ def test_edge_cases_and_fallback_paths():
         filters += ["hub/#", "hub/x"]
         clients += [f"h{i}", f"h{i}"]
     topics += ["hub/x", "hub", "hub/x/y"]
+    # 300 raw entries, all multi: the wave tier's table is too small -> workgroup tier
+    for i in range(100):
+        filters += ["m/#", "m/y"]
+        clients += [f"m{i}", f"m{i}"]
+    topics += ["m/y", "m", "m/z"]
+    # a client whose filters cannot co-match (solo entries) next to one whose can
+    filters += ["p/q/r", "p/s/r", "p/+/r", "p/q/#"]
+    clients += ["solo", "solo", "multi", "multi"]
+    topics += ["p/q/r", "p/s/r", "p/q"]
     # deep topics (> 16 levels) and deep filters (walk beyond the LDS level cache)
     deep = "/".join(f"l{i}" for i in range(40))
     filters += [deep, "/".join(["+"] * 20) + "/#", "l0/#", "/".join(f"l{i}" for i in range(25)) + "/#"]
