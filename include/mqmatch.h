@@ -46,6 +46,7 @@ extern "C" {
 
 typedef struct mqm_index mqm_index;   /* replaces *TopicsIndex               */
 typedef struct mqm_result mqm_result; /* one batch's host-side match result   */
+typedef struct mqm_messages mqm_messages; /* one batch's retained-message result */
 
 typedef struct {
   int device;     /* HIP device ordinal, or MQM_DEVICE_NONE                    */
@@ -123,6 +124,11 @@ int mqm_unsubscribe(mqm_index *h, const char *filter, size_t filter_len, const c
  * handle for the packet; payload_len == 0 deletes.  *result = 1 / 0 / -1. */
 int mqm_retain_message(mqm_index *h, const char *topic, size_t topic_len, uint64_t message_ref,
                        uint32_t payload_len, int retain_flag, int64_t *result);
+/* n RetainMessage calls in order (retained-store reload, server.go:1430-1434);
+ * retain_flags NULL = all set; results may be NULL */
+int mqm_retain_many(mqm_index *h, size_t n, const char *topic_bytes, const uint64_t *topic_offs,
+                    const uint64_t *message_refs, const uint32_t *payload_lens, const uint8_t *retain_flags,
+                    int64_t *results);
 /* Retained.Len() (packets.go:103) */
 int mqm_retained_len(mqm_index *h, uint64_t *out);
 
@@ -138,6 +144,32 @@ int mqm_subscribers(mqm_index *h, const char *topic, size_t topic_len, mqm_resul
 /* Device in / device out on `hip_stream` (hipStream_t, NULL = default stream). */
 int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t *d_topic_offsets,
                      uint32_t n_topics, void *hip_stream, mqm_device_result *out);
+
+/* ---- reverse match: TopicsIndex.Messages (topics.go:426-480) ------------ */
+/* The message refs retained under each filter (the message_ref given to
+ * mqm_retain_message).  Within a filter the order is unspecified (the
+ * reference returns Go map iteration order).  Filter i is
+ * bytes[offsets[i] .. offsets[i+1]); the reference's callers pass one filter
+ * per SUBSCRIBE topic (server.go:870-885). */
+int mqm_messages_batch(mqm_index *h, const char *filter_bytes, const uint64_t *filter_offsets, uint32_t n_filters,
+                       mqm_messages **out);
+/* single-filter convenience == Messages(filter) */
+int mqm_messages_one(mqm_index *h, const char *filter, size_t filter_len, mqm_messages **out);
+uint32_t mqm_messages_num_filters(const mqm_messages *m);
+const uint64_t *mqm_messages_offsets(const mqm_messages *m); /* n + 1 */
+const uint64_t *mqm_messages_refs(const mqm_messages *m);
+void mqm_messages_free(mqm_messages *m);
+
+/* Device in / device out (library-owned; valid until the next call on the index). */
+typedef struct {
+  uint32_t n_filters;
+  uint64_t n_refs;
+  const uint64_t *offsets; /* device, n_filters + 1 */
+  const uint64_t *refs;    /* device */
+  uint64_t n_ranges;       /* emitted ranges (roofline bookkeeping)      */
+} mqm_device_messages;
+int mqm_messages_device(mqm_index *h, const uint8_t *d_filter_bytes, const uint64_t *d_filter_offsets,
+                        uint32_t n_filters, void *hip_stream, mqm_device_messages *out);
 
 /* ---- result accessors --------------------------------------------------- */
 uint32_t mqm_result_num_topics(const mqm_result *r);

@@ -11,6 +11,8 @@ values follow the reference:
     idx.retain_message(topic, ref, payload_len, retain=True) -> 1/0/-1 (:354)
     idx.subscribers("a/b")                    -> Subscribers    (topics.go:484)
     idx.match_batch(bytes, offsets)           -> BatchResult    (GPU batch)
+    idx.messages("a/#")                       -> [message refs] (topics.go:426)
+    idx.messages_batch(bytes, offsets)        -> (offsets, refs) (GPU batch)
 
 Matching runs only on the GPU (libmqmatch.so); there is no Python or CPU
 match path.  Without a device, ``TopicsIndex(device=None)`` still offers the
@@ -217,6 +219,19 @@ class TopicsIndex:
               lib().mqm_retain_message(self._h, t, len(t), message_ref, payload_len, int(retain), C.byref(out)))
         return int(out.value)
 
+    def retain_many(self, topics, refs: np.ndarray, payload_lens: np.ndarray | None = None,
+                    retain_flags: np.ndarray | None = None) -> np.ndarray:
+        """Bulk RetainMessage of topics (a tools.mqgen.Strings) in order; -> results[]."""
+        n = len(topics)
+        refs = np.ascontiguousarray(refs, dtype=np.uint64)
+        pl = np.ones(n, np.uint32) if payload_lens is None else np.ascontiguousarray(payload_lens, dtype=np.uint32)
+        rf = None if retain_flags is None else np.ascontiguousarray(retain_flags, dtype=np.uint8)
+        out = np.zeros(n, np.int64)
+        p = lambda a: None if a is None else a.ctypes.data_as(C.c_void_p)  # noqa: E731
+        check("mqm_retain_many", lib().mqm_retain_many(
+            self._h, n, p(topics.data), p(topics.offs), p(refs), p(pl), p(rf), p(out)))
+        return out
+
     def retained_len(self) -> int:
         out = C.c_uint64()
         check("mqm_retained_len", lib().mqm_retained_len(self._h, C.byref(out)))
@@ -276,6 +291,43 @@ class TopicsIndex:
             return r.subscribers(0)
         finally:
             r.close()
+
+    def messages_batch(self, data: np.ndarray, offs: np.ndarray):
+        """Messages (topics.go:426-480) for a batch of filters on the GPU ->
+        (offsets[n+1], refs): filter i's retained message refs are
+        refs[offsets[i]:offsets[i+1]] (order within a filter unspecified)."""
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        h = C.c_void_p()
+        L = lib()
+        check("mqm_messages_batch", L.mqm_messages_batch(
+            self._h, data.ctypes.data_as(C.c_void_p), offs.ctypes.data_as(C.c_void_p), len(offs) - 1, C.byref(h)))
+        try:
+            n = L.mqm_messages_num_filters(h)
+
+            def arr(ptr, count):
+                if count == 0 or not ptr:
+                    return np.zeros(0, np.uint64)
+                return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_uint64)), shape=(count,)).copy()
+
+            o = arr(L.mqm_messages_offsets(h), n + 1)
+            r = arr(L.mqm_messages_refs(h), int(o[-1]) if n else 0)
+            return o, r
+        finally:
+            L.mqm_messages_free(h)
+
+    def messages(self, filt: str) -> list:
+        """Messages(filter) (topics.go:426): the retained message refs, sorted."""
+        f = b(filt)
+        o, r = self.messages_batch(np.frombuffer(f, np.uint8) if f else np.zeros(0, np.uint8),
+                                   np.array([0, len(f)], np.uint64))
+        return sorted(int(x) for x in r)
+
+    def messages_device(self, d_bytes_ptr: int, d_offs_ptr: int, n: int, stream_ptr: int = 0) -> capi.DeviceMessages:
+        out = capi.DeviceMessages()
+        check("mqm_messages_device", lib().mqm_messages_device(
+            self._h, C.c_void_p(d_bytes_ptr), C.c_void_p(d_offs_ptr), n, C.c_void_p(stream_ptr), C.byref(out)))
+        return out
 
     def match_device(self, d_bytes_ptr: int, d_offs_ptr: int, n: int, stream_ptr: int = 0) -> capi.DeviceResult:
         """Device-resident batch (pointers from e.g. torch tensors); the result's

@@ -35,6 +35,8 @@ EXPORTED = [
     "mqm_result_shared_offsets", "mqm_result_shared", "mqm_result_sub_info", "mqm_result_shared_info",
     "mqm_result_sub_infos", "mqm_result_free", "mqm_client_name", "mqm_filter_name", "mqm_num_clients", "mqm_is_valid_filter",
     "mqm_is_shared_filter", "mqm_snapshot_stats_get", "mqm_profile_enable", "mqm_profile_read", "mqm_version",
+    "mqm_retain_many", "mqm_messages_batch", "mqm_messages_one", "mqm_messages_num_filters", "mqm_messages_offsets",
+    "mqm_messages_refs", "mqm_messages_free", "mqm_messages_device",
 ]
 
 
@@ -64,6 +66,11 @@ class DeviceResult(C.Structure):
                 ("shared_starts", C.c_void_p), ("shared_counts", C.c_void_p),
                 ("shared", C.c_void_p), ("n_fallback", C.c_uint32), ("n_big", C.c_uint32),
                 ("fallback_why", C.c_uint32 * 5)]
+
+
+class DeviceMessages(C.Structure):
+    _fields_ = [("n_filters", C.c_uint32), ("n_refs", C.c_uint64), ("offsets", C.c_void_p), ("refs", C.c_void_p),
+                ("n_ranges", C.c_uint64)]
 
 
 class SnapshotStats(C.Structure):
@@ -128,6 +135,14 @@ def lib():
         "mqm_profile_enable": ([vp, C.c_int], C.c_int),
         "mqm_profile_read": ([vp, C.POINTER(Profile)], C.c_int),
         "mqm_version": ([], C.c_char_p),
+        "mqm_retain_many": ([vp, sz, vp, vp, vp, vp, vp, vp], C.c_int),
+        "mqm_messages_batch": ([vp, vp, vp, u32, C.POINTER(vp)], C.c_int),
+        "mqm_messages_one": ([vp, cp, sz, C.POINTER(vp)], C.c_int),
+        "mqm_messages_num_filters": ([vp], u32),
+        "mqm_messages_offsets": ([vp], vp),
+        "mqm_messages_refs": ([vp], vp),
+        "mqm_messages_free": ([vp], None),
+        "mqm_messages_device": ([vp, vp, vp, u32, vp, C.POINTER(DeviceMessages)], C.c_int),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

@@ -12,6 +12,7 @@
 #include "../../include/mqmatch.h"
 #include "flatten.h"
 #include "match.h"
+#include "retained.h"
 #include "store.h"
 
 using namespace mqm;
@@ -24,6 +25,11 @@ struct mqm_index {
   uint64_t snap_version = ~0ull;
   Workspace ws;
   hipStream_t stream = nullptr;
+};
+
+struct mqm_messages {
+  uint32_t n = 0;
+  std::vector<uint64_t> offsets, refs;
 };
 
 struct mqm_result {
@@ -187,6 +193,21 @@ int mqm_retain_message(mqm_index *h, const char *topic, size_t topic_len, uint64
   });
 }
 
+int mqm_retain_many(mqm_index *h, size_t n, const char *topic_bytes, const uint64_t *topic_offs,
+                    const uint64_t *message_refs, const uint32_t *payload_lens, const uint8_t *retain_flags,
+                    int64_t *results) {
+  if (!h || !topic_offs || !message_refs || !payload_lens || (n && !topic_bytes)) return MQM_EINVAL;
+  return guarded([&] {
+    std::lock_guard<std::mutex> g(h->mu);
+    for (size_t i = 0; i < n; i++) {
+      int64_t r = h->store.retain_message(sv(topic_bytes + topic_offs[i], topic_offs[i + 1] - topic_offs[i]),
+                                          message_refs[i], payload_lens[i], retain_flags ? retain_flags[i] != 0 : true);
+      if (results) results[i] = r;
+    }
+    return MQM_OK;
+  });
+}
+
 int mqm_retained_len(mqm_index *h, uint64_t *out) {
   if (!h || !out) return MQM_EINVAL;
   std::lock_guard<std::mutex> g(h->mu);
@@ -285,6 +306,82 @@ int mqm_match_batch(mqm_index *h, const char *topic_bytes, const uint64_t *topic
     return MQM_OK;
   });
 }
+
+int mqm_messages_device(mqm_index *h, const uint8_t *d_filter_bytes, const uint64_t *d_filter_offsets,
+                        uint32_t n_filters, void *hip_stream, mqm_device_messages *out) {
+  if (!h || !out || (n_filters && (!d_filter_bytes || !d_filter_offsets))) return MQM_EINVAL;
+  return guarded([&] {
+    std::lock_guard<std::mutex> g(h->mu);
+    if (h->cfg.device == MQM_DEVICE_NONE) return MQM_ENODEV;
+    if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
+    int rc = ensure_snapshot(h);
+    if (rc != MQM_OK) return rc;
+    MessagesOutput mo;
+    rc = messages_device(h->snap->dev, h->snap->has_retained ? &h->snap->ret : nullptr, h->ws, d_filter_bytes,
+                         d_filter_offsets, n_filters, (hipStream_t)hip_stream, &mo);
+    if (rc != 0) return rc;
+    out->n_filters = mo.n_filters;
+    out->n_refs = mo.n_refs;
+    out->offsets = mo.offsets;
+    out->refs = mo.refs;
+    out->n_ranges = mo.n_emissions;
+    return MQM_OK;
+  });
+}
+
+int mqm_messages_batch(mqm_index *h, const char *filter_bytes, const uint64_t *filter_offsets, uint32_t n_filters,
+                       mqm_messages **out) {
+  if (!h || !out || !filter_offsets || (n_filters && !filter_bytes)) return MQM_EINVAL;
+  *out = nullptr;
+  return guarded([&] {
+    std::lock_guard<std::mutex> g(h->mu);
+    if (h->cfg.device == MQM_DEVICE_NONE) return MQM_ENODEV;
+    if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
+    int rc = ensure_snapshot(h);
+    if (rc != MQM_OK) return rc;
+    const uint64_t base = filter_offsets[0];
+    const uint64_t nbytes = filter_offsets[n_filters] - base;
+    Workspace &ws = h->ws;
+    if (ws.get(Workspace::kRInBytes, nbytes + 16) || ws.get(Workspace::kRInOffs, sizeof(uint64_t) * (n_filters + 1)))
+      return MQM_ENOMEM;
+    auto *d_bytes = (uint8_t *)ws.ptr(Workspace::kRInBytes);
+    auto *d_offs = (uint64_t *)ws.ptr(Workspace::kRInOffs);
+    std::vector<uint64_t> offs(filter_offsets, filter_offsets + n_filters + 1);
+    for (auto &o : offs) o -= base;
+    if (nbytes && hipMemcpyAsync(d_bytes, filter_bytes + base, nbytes, hipMemcpyHostToDevice, h->stream) != hipSuccess)
+      return MQM_EHIP;
+    if (hipMemcpyAsync(d_offs, offs.data(), sizeof(uint64_t) * (n_filters + 1), hipMemcpyHostToDevice, h->stream) !=
+        hipSuccess)
+      return MQM_EHIP;
+    MessagesOutput mo;
+    rc = messages_device(h->snap->dev, h->snap->has_retained ? &h->snap->ret : nullptr, ws, d_bytes, d_offs,
+                         n_filters, h->stream, &mo);
+    if (rc != 0) return rc;
+    auto m = std::make_unique<mqm_messages>();
+    m->n = n_filters;
+    m->offsets.resize(n_filters + 1);
+    m->refs.resize(mo.n_refs);
+    if (hipMemcpyAsync(m->offsets.data(), mo.offsets, sizeof(uint64_t) * (n_filters + 1), hipMemcpyDeviceToHost,
+                       h->stream) != hipSuccess)
+      return MQM_EHIP;
+    if (mo.n_refs && hipMemcpyAsync(m->refs.data(), mo.refs, sizeof(uint64_t) * mo.n_refs, hipMemcpyDeviceToHost,
+                                    h->stream) != hipSuccess)
+      return MQM_EHIP;
+    if (hipStreamSynchronize(h->stream) != hipSuccess) return MQM_EHIP;
+    *out = m.release();
+    return MQM_OK;
+  });
+}
+
+int mqm_messages_one(mqm_index *h, const char *filter, size_t filter_len, mqm_messages **out) {
+  uint64_t offs[2] = {0, filter_len};
+  return mqm_messages_batch(h, filter ? filter : "", offs, 1, out);
+}
+
+uint32_t mqm_messages_num_filters(const mqm_messages *m) { return m ? m->n : 0; }
+const uint64_t *mqm_messages_offsets(const mqm_messages *m) { return m ? m->offsets.data() : nullptr; }
+const uint64_t *mqm_messages_refs(const mqm_messages *m) { return m ? m->refs.data() : nullptr; }
+void mqm_messages_free(mqm_messages *m) { delete m; }
 
 int mqm_subscribers(mqm_index *h, const char *topic, size_t topic_len, mqm_result **out) {
   uint64_t offs[2] = {0, topic_len};

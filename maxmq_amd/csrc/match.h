@@ -13,7 +13,10 @@ struct Workspace {
   enum Slot {
     kSCount, kHCount, kDCount, kDStart, kHStart, kCls, kDfsList, kRecs, kCounters, kDOut, kHOut,
     kDense, kDenseShared, kDenseOffs, kDenseHOffs, kScanTmp, kRawCnt, kTabOff, kTabSize, kTable,
-    kInBytes, kInOffs, kOvfList, kNumSlots
+    kInBytes, kInOffs, kOvfList,
+    // reverse match (retained.hip)
+    kROffs, kRNLev, kRWild, kRLOff, kRFCount, kRFCur, kRLevels, kRNCount, kRNOff, kRItemF0, kRItemN0, kRItemF1,
+    kRItemN1, kRChild, kRECount, kREOff, kREmit, kRPos, kRChunks, kRCOff, kROut, kRInBytes, kRInOffs, kNumSlots
   };
   struct Buf {
     void *p = nullptr;
@@ -39,6 +42,10 @@ struct Workspace {
 
   static int reserve(void **p, size_t *cap, size_t need);
   int get(Slot s, size_t need) { return reserve(&bufs[s].p, &bufs[s].cap, need); }
+  // like get(), but a reallocation keeps the first `used` bytes (copied on `st`)
+  int grow_keep(Slot s, size_t used, size_t need, hipStream_t st);
+  // 256 B of pinned host memory for small read-backs (nullptr on failure)
+  uint64_t *pinned_u64();
   void *ptr(Slot s) const { return bufs[s].p; }
   ~Workspace();
 };

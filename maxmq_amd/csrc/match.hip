@@ -40,6 +40,7 @@
 #include <cstdio>
 #include <vector>
 
+#include "device.h"
 #include "match.h"
 
 namespace mqm {
@@ -127,55 +128,6 @@ __device__ __forceinline__ uint64_t lanemask_lt(int lane) { return (1ull << lane
 __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
   const uint32_t lo = __shfl((uint32_t)v, src, 64), hi = __shfl((uint32_t)(v >> 32), src, 64);
   return ((uint64_t)hi << 32) | lo;
-}
-
-__device__ __forceinline__ NodeDesc load_desc(const NodeDesc *p) {
-  const uint4 *q = reinterpret_cast<const uint4 *>(p);
-  uint4 a = q[0], b = q[1];
-  NodeDesc d;
-  d.plus = a.x;
-  d.hash = a.y;
-  d.sub_off = a.z;
-  d.sub_cnt = a.w;
-  d.hsub_off = b.x;
-  d.hsub_cnt = b.y;
-  d.sh_off = b.z;
-  d.sh_cnt_flags = b.w;
-  return d;
-}
-
-// Literal child lookup: open-addressed edge table, 2 entries per 128-B bucket.
-// Long keys (>= 16 bytes) are verified byte-for-byte against the token pool.
-__device__ uint32_t probe_edge(const DeviceSnapshot &s, uint32_t parent, uint64_t k0, uint64_t k1,
-                               const uint8_t *tok, uint32_t tok_len, NodeDesc *desc) {
-  const uint64_t nslots = (s.bucket_mask + 1) * kEdgesPerBucket;
-  Key key{k0, k1};
-  uint64_t slot = (edge_hash(parent, key) & s.bucket_mask) * kEdgesPerBucket;
-  for (;;) {
-    // the whole 64-B entry in one round trip: key, header and the child's descriptor
-    const uint4 *q = reinterpret_cast<const uint4 *>(s.edges + slot);
-    const uint4 kk = q[0], pc = q[1], d0 = q[2], d1 = q[3];
-    if (pc.x == kNone) return kNone;
-    if (pc.x == parent && (((uint64_t)kk.y << 32) | kk.x) == k0 && (((uint64_t)kk.w << 32) | kk.z) == k1) {
-      bool ok = true;
-      if (key_is_long(key)) {
-        ok = pc.w == tok_len;
-        for (uint32_t i = 0; ok && i < tok_len; i++) ok = s.tok_pool[pc.z + i] == tok[i];
-      }
-      if (ok) {
-        desc->plus = d0.x;
-        desc->hash = d0.y;
-        desc->sub_off = d0.z;
-        desc->sub_cnt = d0.w;
-        desc->hsub_off = d1.x;
-        desc->hsub_cnt = d1.y;
-        desc->sh_off = d1.z;
-        desc->sh_cnt_flags = d1.w;
-        return pc.y;
-      }
-    }
-    slot = (slot + 1) & (nslots - 1);
-  }
 }
 
 __device__ __forceinline__ uint32_t table_slot(uint32_t client, uint32_t lg) {
@@ -924,7 +876,10 @@ __global__ __launch_bounds__(256) void k_densify(uint32_t n, const uint32_t *__r
 // ---------------------------------------------------------------------------
 int Workspace::reserve(void **p, size_t *cap, size_t need) {
   if (*cap >= need && *p) return 0;
-  if (*p) (void)hipFree(*p);
+  if (*p) {
+    (void)hipDeviceSynchronize();  // queued kernels may still read the old buffer
+    (void)hipFree(*p);
+  }
   *p = nullptr;
   size_t n = std::max<size_t>(need, 256);
   n = n + n / 4;
@@ -934,6 +889,28 @@ int Workspace::reserve(void **p, size_t *cap, size_t need) {
   }
   *cap = n;
   return 0;
+}
+
+int Workspace::grow_keep(Slot s, size_t used, size_t need, hipStream_t st) {
+  Buf &b = bufs[s];
+  if (b.cap >= need && b.p) return 0;
+  void *p = nullptr;
+  size_t cap = 0;
+  if (reserve(&p, &cap, need)) return -2;
+  if (used && (hipMemcpyAsync(p, b.p, used, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+               hipStreamSynchronize(st) != hipSuccess)) {
+    (void)hipFree(p);
+    return -3;
+  }
+  if (b.p) (void)hipFree(b.p);
+  b.p = p;
+  b.cap = cap;
+  return 0;
+}
+
+uint64_t *Workspace::pinned_u64() {
+  if (!host_pinned && hipHostMalloc(&host_pinned, 256, hipHostMallocDefault) != hipSuccess) return nullptr;
+  return reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(host_pinned) + 128);
 }
 
 Workspace::~Workspace() {

@@ -118,6 +118,9 @@ class OracleIndex:
         t = _b(topic)
         return int(self._L.oref_retain(self._h, t, len(t), msg_ref, payload_len, int(retain_flag)))
 
+    def retained_len(self) -> int:
+        return int(self._L.oref_retained_len(self._h))
+
     def num_clients(self):
         return int(self._L.oref_num_clients(self._h))
 
