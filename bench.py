@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", choices=["forward", "reverse"], default="forward",
+                    help="forward: Subscribers (headline); reverse: Messages over retained topics (config 5)")
+    ap.add_argument("--retained", type=int, default=50000000, help="reverse: retained topics")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per emit launch (profiles/run_pmc.sh)")
     return ap.parse_args()
@@ -57,8 +60,24 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def _heartbeat(period=60.0):
+    """a progress line every `period` s while long host phases (generation,
+    index build, CPU baseline) run, so a watchdog never mistakes them for a hang"""
+    import threading
+
+    t0 = time.time()
+
+    def beat():
+        while True:
+            time.sleep(period)
+            log(f"[heartbeat] {time.time() - t0:.0f}s")
+
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main():
     args = parse()
+    _heartbeat()
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -75,6 +94,9 @@ def main():
     import maxmq_amd
     from maxmq_amd import shard
     from tools import mqgen
+
+    if args.workload == "reverse":
+        return run_reverse(args, dist, rank, world, local, dev)
 
     overrides = {}
     if args.filters:
@@ -199,6 +221,131 @@ def main():
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def run_reverse(args, dist, rank, world, local, dev):
+    """Messages (topics.go:426-480) for a batch of subscription filters against
+    the retained topics (BASELINE configs[4]): mqgen config 5's filters (5%
+    $SHARE, 20% '+', 5% '#') also subscribed, `--retained` topics retained.
+    A step = one mqm_messages_device call over the whole filter batch, inputs
+    resident in HBM (it synchronises per trie level to size the worklists)."""
+    import torch
+
+    import maxmq_amd
+    from tools import mqgen
+
+    cfg = 5
+    nf = args.filters or 1000000
+    t0 = time.time()
+    w = mqgen.generate(cfg, n_filters=nf, n_topics=args.retained)
+    log(f"[rank {rank}] generated {len(w.filters)} filters / {len(w.topics)} retained topics in {time.time() - t0:.1f}s")
+    t0 = time.time()
+    idx = maxmq_amd.TopicsIndex(device=local, autocommit=False)
+    idx.subscribe_workload(w)
+    refs = np.arange(len(w.topics), dtype=np.uint64)
+    idx.retain_many(w.topics, refs)
+    idx.commit()
+    snap = idx.snapshot_stats()
+    log(f"[rank {rank}] index built in {time.time() - t0:.1f}s: {snap} retained={idx.retained_len()}")
+    fb = torch.from_numpy(w.filters.data).to(dev)
+    fo = torch.from_numpy(w.filters.offs.view(np.int64)).to(dev)
+    stream = torch.cuda.current_stream(dev)
+    n = len(w.filters)
+
+    def step():
+        return idx.messages_device(fb.data_ptr(), fo.data_ptr(), n, stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    refs_out = items = ranges = 0
+    for _ in range(args.steps):
+        r = step()
+        refs_out += int(r.n_refs)
+        items += int(r.n_items)
+        ranges += int(r.n_ranges)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    if rank == 0:
+        steps = args.steps
+        tbytes = int(w.filters.offs[-1])
+        # algorithmic bytes per batch: filter bytes + offsets in/out (16 B) + one
+        # 64-B trie read per (filter, node) step + refs read and written (16 B)
+        per_batch = tbytes + 16 * n + 64 * items / steps + 16 * refs_out / steps
+        achieved = per_batch / (dt / steps) / 1e9
+        cpu = None
+        if not args.no_cpu_baseline:
+            cpu = cpu_reverse(w, refs, args)
+        out = {
+            "metric": "retained reverse match: filters matched/sec + retained hits/sec",
+            "value": n * steps * world / dt,
+            "unit": "filters/s",
+            "n_gpus": world,
+            "steps": steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt * 1e3 / steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8/u32 (byte+integer matching)",
+            "data": "synthetic (tools/mqgen config 5, deterministic seed); inputs resident in HBM",
+            "config": {"workload": f"mqgen config 5: {n} filters vs {len(w.topics)} retained topics "
+                                   f"(+ the filters subscribed), depth<=8",
+                       "filters_per_batch": n, "retained": len(w.topics), "parallelism": f"replicas{world}"},
+            "retained_hits_per_s": refs_out * world / dt,
+            "hits_per_filter": refs_out / (n * steps),
+            "items_per_filter": items / (n * steps),
+            "snapshot": snap,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "algorithmic_bytes_per_batch": per_batch,
+                         "kernel": "reverse-match pipeline (wall time incl. per-level host syncs)"},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_reverse(w, refs, args):
+    """oracle/mochi_ref.c scan_messages over a time-bounded sample of the filters."""
+    from oracle.binding import OracleIndex
+
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    t0 = time.time()
+    ora = OracleIndex()
+    ora.subscribe_workload(w)
+    ora.retain_many(w.topics, refs)
+    build_s = time.time() - t0
+    f = w.filters
+    n = len(f)
+    done, busy, hits, chunk = 0, 0.0, 0, 2000
+    while done < n and busy < args.cpu_seconds:
+        hi = min(n, done + chunk)
+        o = (f.offs[done:hi + 1] - f.offs[done]).astype(np.uint64)
+        d = f.data[int(f.offs[done]):int(f.offs[hi])]
+        t1 = time.perf_counter()
+        mo, _ = ora.messages(d, o, nthreads=threads)
+        busy += time.perf_counter() - t1
+        hits += int(mo[-1])
+        done = hi
+        chunk = min(chunk * 2, 100000)
+    ora.close()
+    return {"value": done / busy, "unit": "filters/s", "cores": threads, "kind": "port",
+            "sample": f"first {done} filters ({busy:.1f}s of matching, index build {build_s:.0f}s excluded); "
+                      f"C restatement of mochi v2.2.12 TopicsIndex.Messages (oracle/mochi_ref.c); Go toolchain "
+                      f"unavailable",
+            "retained_hits_per_s": hits / busy}
 
 
 def _dev_to_tensor(ptr, t):

@@ -167,6 +167,7 @@ typedef struct {
   const uint64_t *offsets; /* device, n_filters + 1 */
   const uint64_t *refs;    /* device */
   uint64_t n_ranges;       /* emitted ranges (roofline bookkeeping)      */
+  uint64_t n_items;        /* (filter, trie node) steps over all levels  */
 } mqm_device_messages;
 int mqm_messages_device(mqm_index *h, const uint8_t *d_filter_bytes, const uint64_t *d_filter_offsets,
                         uint32_t n_filters, void *hip_stream, mqm_device_messages *out);

@@ -70,7 +70,7 @@ class DeviceResult(C.Structure):
 
 class DeviceMessages(C.Structure):
     _fields_ = [("n_filters", C.c_uint32), ("n_refs", C.c_uint64), ("offsets", C.c_void_p), ("refs", C.c_void_p),
-                ("n_ranges", C.c_uint64)]
+                ("n_ranges", C.c_uint64), ("n_items", C.c_uint64)]
 
 
 class SnapshotStats(C.Structure):

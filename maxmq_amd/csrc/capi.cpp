@@ -325,6 +325,7 @@ int mqm_messages_device(mqm_index *h, const uint8_t *d_filter_bytes, const uint6
     out->offsets = mo.offsets;
     out->refs = mo.refs;
     out->n_ranges = mo.n_emissions;
+    out->n_items = mo.n_items;
     return MQM_OK;
   });
 }

@@ -19,6 +19,7 @@ struct MessagesOutput {
   uint32_t n_filters = 0;
   uint64_t n_refs = 0;
   uint64_t n_emissions = 0;
+  uint64_t n_items = 0;  // (filter, node) worklist items over all levels
   const uint64_t *offsets = nullptr;  // device, n_filters + 1
   const uint64_t *refs = nullptr;     // device, message refs (order within a filter unspecified)
 };

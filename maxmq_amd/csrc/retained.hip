@@ -318,7 +318,7 @@ int messages_device(const DeviceSnapshot &s, const DeviceRetained *r, Workspace 
     HIP_TRY(hipGetLastError());
   }
   uint64_t n_items = hp[0];
-  uint64_t n_emit = 0;
+  uint64_t n_emit = 0, items_total = 0;
   W::Slot cur_f = W::kRItemF0, cur_n = W::kRItemN0, nxt_f = W::kRItemF1, nxt_n = W::kRItemN1;
   for (uint32_t d = 0; n_items > 0; d++) {
     if (ws.get(W::kRChild, sizeof(uint32_t) * (n_items + 1)) || ws.get(W::kRNCount, sizeof(uint32_t) * (n_items + 1)) ||
@@ -363,6 +363,7 @@ int messages_device(const DeviceSnapshot &s, const DeviceRetained *r, Workspace 
     hipLaunchKernelGGL(k_bfs<true>, dim3(blocks_for(n_items)), dim3(256), 0, st, a);
     HIP_TRY(hipGetLastError());
     n_emit += ne;
+    items_total += n_items;
     n_items = nn;
     std::swap(cur_f, nxt_f);
     std::swap(cur_n, nxt_n);
@@ -402,6 +403,7 @@ int messages_device(const DeviceSnapshot &s, const DeviceRetained *r, Workspace 
   out->n_refs = n_refs;
   out->refs = refs_out;
   out->n_emissions = n_emit;
+  out->n_items = items_total;
   return 0;
 }
 

@@ -55,6 +55,8 @@ def lib():
         L.oref_filter_name.restype = u32
         L.oref_client_name.argtypes = [vp, u32, C.c_char_p, u32]
         L.oref_client_name.restype = u32
+        L.oref_retain_many.argtypes = [vp, u64, vp, vp, vp, u32]
+        L.oref_retain_many.restype = None
         L.oref_retained_len.argtypes = [vp]
         L.oref_retained_len.restype = u64
         L.oref_match_counts.argtypes = [vp, vp, vp, u32, C.c_int, vp, vp, C.POINTER(Stats)]
@@ -117,6 +119,11 @@ class OracleIndex:
     def retain_message(self, topic, msg_ref, payload_len, retain_flag=True) -> int:
         t = _b(topic)
         return int(self._L.oref_retain(self._h, t, len(t), msg_ref, payload_len, int(retain_flag)))
+
+    def retain_many(self, topics, refs: np.ndarray, payload_len: int = 1):
+        """RetainMessage of every topic of a tools.mqgen.Strings, in order."""
+        refs = np.ascontiguousarray(refs, dtype=np.uint64)
+        self._L.oref_retain_many(self._h, len(topics), _ptr(topics.data), _ptr(topics.offs), _ptr(refs), payload_len)
 
     def retained_len(self) -> int:
         return int(self._L.oref_retained_len(self._h))

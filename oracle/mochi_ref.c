@@ -550,6 +550,12 @@ int64_t oref_retain(oref *x, const char *topic, uint32_t tlen, uint64_t msg_ref,
   return out;
 }
 
+void oref_retain_many(oref *x, uint64_t n, const char *bytes, const uint64_t *offs, const uint64_t *msg_refs,
+                      uint32_t payload_len) {
+  for (uint64_t i = 0; i < n; i++)
+    oref_retain(x, bytes + offs[i], (uint32_t)(offs[i + 1] - offs[i]), msg_refs[i], payload_len, 1);
+}
+
 uint32_t oref_num_clients(const oref *x) { return x->clients.n; }
 uint32_t oref_num_filters(const oref *x) { return x->filters.n; }
 uint64_t oref_retained_len(const oref *x) { return x->retained.n; }

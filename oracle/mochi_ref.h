@@ -78,6 +78,10 @@ int oref_unsubscribe(oref *x, const char *filter, uint32_t flen, const char *cli
 int64_t oref_retain(oref *x, const char *topic, uint32_t tlen, uint64_t msg_ref, uint32_t payload_len,
                     uint8_t retain_flag);
 
+/* n RetainMessage calls in order (topic i = bytes[offs[i] .. offs[i+1])) */
+void oref_retain_many(oref *x, uint64_t n, const char *bytes, const uint64_t *offs, const uint64_t *msg_refs,
+                      uint32_t payload_len);
+
 uint32_t oref_num_clients(const oref *x);
 uint32_t oref_num_filters(const oref *x);
 /* copies the interned string (no NUL) into buf; returns its length */
