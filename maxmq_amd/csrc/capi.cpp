@@ -2,6 +2,7 @@
 // store, the snapshot builder and the HIP match pipeline.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -126,6 +127,7 @@ int mqm_create(const mqm_config *cfg, mqm_index **out) {
     if (h->cfg.device < 0 || h->cfg.device >= ndev) return MQM_EINVAL;
     if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) return MQM_EHIP;
+    if (const char *e = getenv("MQM_WALK_LANES")) h->ws.walk_lanes = atoi(e) == 8 ? 8 : 16;
     *out = h.release();
     return MQM_OK;
   });

@@ -10,18 +10,17 @@
 //                   fans out to 3 lanes (literal edge probe / '+' child /
 //                   '#' child), so a level costs one dependent memory round
 //                   trip (the literal child's descriptor is inline in its
-//                   edge entry).  Hits and the next frontier are compacted
-//                   with ballot + popcount into LDS.
-//     3. order    : hits ranked by counting (rank = the reference's emission
-//                   order, snapshot.h); the ordered hit list, the prefix of
-//                   its range sizes and the shared hits go to a per-topic
-//                   record; S (raw entries) and H (shared candidates) counted.
+//                   edge entry).  Hits are compacted with ballot + popcount
+//                   and written straight to the topic's record with their
+//                   raw-entry prefix and their rank (2 * node + slot = the
+//                   reference's emission order, snapshot.h); S (raw
+//                   entries) and H (shared candidates) are counted.
 //   scan      S and H -> each topic's segment start (S is the upper bound of
 //             its deliveries, so every later kernel writes final positions).
 //   k_small   a wavefront per topic with <= kSMax raw entries: per-wave LDS
 //             hash table keyed by client; atomicOr folds QoS (one-hot) and
-//             NoLocal, atomicMin keeps the lowest hit index; an entry is its
-//             client's winner iff its hit is that minimum — exactly
+//             NoLocal, atomicMin keeps the lowest hit rank; an entry is its
+//             client's winner iff its hit has that rank — exactly
 //             Subscription.Merge (packets.go:250-270) with the first-merged
 //             subscription's fields.  Winners are compacted with ballot.
 //             Also writes every topic's shared candidates.
@@ -48,20 +47,21 @@ namespace mqm {
 namespace {
 
 constexpr int kWave = 64;
-constexpr int kG = 16;                   // lanes per topic in k_walk
-constexpr int kGroups = kWave / kG;      // topics per wavefront
 constexpr int kWalkWaves = 4;            // wavefronts per k_walk block
-constexpr int kLMax = 16;                // levels cached per topic (one per lane)
+constexpr int kLMax = 16;                // levels cached per topic
 constexpr int kFCap = 16;                // frontier nodes per level
 constexpr int kHCap = 48;                // non-shared hits per topic (3 per lane)
 constexpr int kShCap = 16;               // shared hits per topic
 constexpr int kStage = 64;               // topic bytes staged in LDS (4 per lane, one round trip)
-// record (compact, so one 64-lane load usually fetches it whole):
+// record, written while walking (hits in discovery order; rank orders them):
 //   [0] nh | nsh << 8, [1] S,
-//   [2 + 2r] off, [3 + 2r] pre of the hit of rank r (r < nh),
-//   [2 + 2nh + 2i] off, [3 + 2nh + 2i] cnt of shared hit i (i < nsh)
-constexpr int kRecStride = 2 + 2 * kHCap + 2 * kShCap;  // 130 words (max)
-constexpr int kRecStrideAlloc = 132;                    // 16-B aligned per topic
+//   [2 + 3h] off, [3 + 3h] pre, [4 + 3h] rank of hit h (h < nh): its entries
+//            are subs[off .. off + cnt) and raw entries pre .. pre + cnt - 1
+//   [kRecSh + 2i] off, [kRecSh + 1 + 2i] cnt of shared hit i (i < nsh)
+// One 64-lane load fetches the header and the first 20 hits.
+constexpr int kRecSh = 2 + 3 * kHCap;                // 146
+constexpr int kRecStride = kRecSh + 2 * kShCap;       // 178 words (max)
+constexpr int kRecStrideAlloc = 180;                  // 16-B aligned per topic
 constexpr int kSMax = 384;               // raw entries per k_small topic
 constexpr int kSmallPer = kSMax / kWave; // entries per lane
 constexpr int kSmallSlots = 256;         // k_small merge table slots (per wave)
@@ -74,8 +74,6 @@ constexpr int kBigMax = 3072;            // raw entries per k_big topic
 constexpr int kBigPer = kBigMax / kBigThreads;
 constexpr uint32_t kNoWhy = 0xFFFFFFFFu;
 
-static_assert(kLMax == kG, "one lane per cached level");
-static_assert(kHCap == 3 * kG, "three ranked hits per lane");
 static_assert(kRecStrideAlloc % 4 == 0 && kRecStrideAlloc >= kRecStride, "16-B aligned records");
 static_assert(kSmallMulti * 4 <= kSmallSlots * 3, "k_small table load factor");
 static_assert(kBigMax * 4 <= kBigSlotsB * 3, "the overflow tier holds every bounded topic");
@@ -105,16 +103,8 @@ struct Outputs {
 };
 
 struct TopicLds {              // k_walk context of one topic (one 16-lane group)
-  uint64_t key0[kLMax];
-  uint64_t key1[kLMax];
   uint32_t sep[kLMax];         // position of the '/' ending level k
   uint32_t front[2][3][kFCap]; // (node, plus, hash) of the frontier
-  uint32_t hit_rank[kHCap];
-  uint32_t hit_off[kHCap];
-  uint32_t hit_cnt[kHCap];
-  uint32_t s_cnt[kHCap];       // counts in rank order
-  uint32_t sh_off[kShCap];
-  uint32_t sh_cnt[kShCap];
   uint8_t stage[kStage];       // the topic's first kStage bytes
 };
 
@@ -141,12 +131,12 @@ __device__ __forceinline__ uint64_t pack_delivery(uint32_t client, uint32_t sid,
 // QoS one-hot (bits 0..2) | NoLocal (bit 3): OR-merged, max QoS = top set bit
 __device__ __forceinline__ uint32_t qos_bits(uint32_t meta) { return (1u << (meta & 3)) | (((meta >> 2) & 1) << 3); }
 
-// hit h with pre(h) <= r < pre(h+1), pre(h) = rec[3 + 2h] (strictly
-// increasing: empty hits are never recorded)
+// hit h with pre(h) <= r < pre(h+1), pre(h) = rec[3 + 3h] (strictly
+// increasing in h: empty hits are never recorded)
 __device__ __forceinline__ uint32_t find_hit(const uint32_t *rec, uint32_t nh, uint32_t r) {
   uint32_t h = 0;
   for (uint32_t step = 32; step > 0; step >>= 1)
-    if (h + step < nh && rec[3 + 2 * (h + step)] <= r) h += step;
+    if (h + step < nh && rec[3 + 3 * (h + step)] <= r) h += step;
   return h;
 }
 
@@ -171,11 +161,32 @@ __device__ __forceinline__ uint32_t table_find(const uint32_t *tkey, uint32_t ma
 }
 
 // ---------------------------------------------------------------------------
-// k_walk: tokenize + walk + order hits, a 16-lane group per topic
+// k_walk: tokenize + walk, a 16-lane group per topic.  Level keys and the
+// running hit count live in registers (lane k holds level k's key); LDS holds
+// only the separators, the frontier and the first bytes of the topic, so many
+// topics stay in flight per CU.  Hits go straight to the topic's record with
+// their rank (= 2 * node + slot, the reference's emission order).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, const uint8_t *__restrict__ tbytes,
+template <int kG>
+__device__ __forceinline__ uint32_t group_scan_ex(uint32_t v, int gl, uint32_t *total, int gbase) {
+  uint32_t inc = v;
+  for (int d = 1; d < kG; d <<= 1) {
+    const uint32_t u = __shfl_up(inc, d, kG);
+    if (gl >= d) inc += u;
+  }
+  *total = __shfl(inc, gbase + kG - 1, 64);
+  return inc - v;
+}
+
+// kG lanes per topic (8 or 16), kWave / kG topics per wavefront
+template <int kG>
+__global__ __launch_bounds__(kWave * kWalkWaves, 5) void k_walk(DeviceSnapshot s, const uint8_t *__restrict__ tbytes,
                                                            const uint64_t *__restrict__ toffs, uint32_t n,
                                                            Outputs o) {
+  constexpr int kGroups = kWave / kG;
+  constexpr int kLPer = kLMax / kG;  // level keys held per lane
+  constexpr uint32_t kGMask = (1u << kG) - 1u;
+  static_assert(kLMax % kG == 0, "levels per lane");
   __shared__ TopicLds lds_all[kWalkWaves * kGroups];
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / kG, gl = lane & (kG - 1), gbase = g * kG;
@@ -184,15 +195,20 @@ __global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, co
   const uint64_t stride = (uint64_t)gridDim.x * kWalkWaves * kGroups;
   const NodeDesc root = load_desc(s.nodes);
 
-  for (uint64_t tb = ((uint64_t)blockIdx.x * kWalkWaves + threadIdx.x / kWave) * kGroups; tb < n; tb += stride) {
+  uint64_t tb = ((uint64_t)blockIdx.x * kWalkWaves + threadIdx.x / kWave) * kGroups;
+  uint64_t nx_off = 0, nx_end = 0;  // the next topic's byte range, one topic ahead
+  if (tb + g < n) {
+    nx_off = toffs[tb + g];
+    nx_end = toffs[tb + g + 1];
+  }
+  for (; tb < n; tb += stride) {
     const uint32_t t = (uint32_t)(tb + g);
     const bool active = t < n;
-    uint32_t len = 0;
-    const uint8_t *tp = tbytes;
-    if (active) {
-      const uint64_t off = toffs[t];
-      len = (uint32_t)(toffs[t + 1] - off);
-      tp = tbytes + off;
+    const uint32_t len = active ? (uint32_t)(nx_end - nx_off) : 0;
+    const uint8_t *tp = tbytes + (active ? nx_off : 0);
+    if (tb + stride + g < n) {
+      nx_off = toffs[tb + stride + g];
+      nx_end = toffs[tb + stride + g + 1];
     }
     uint32_t why = kNoWhy;
 
@@ -217,7 +233,7 @@ __global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, co
       for (int j = 0; j < kStage / kG; j++) {
         const uint32_t p = base + j * kG + gl;
         const bool sep = p < len && b[j] == '/';
-        const uint32_t m = (uint32_t)(__ballot(sep) >> gbase) & 0xFFFFu;
+        const uint32_t m = (uint32_t)(__ballot(sep) >> gbase) & kGMask;
         if (sep) {
           const uint32_t idx = nsep + __popc(m & gmask_lt);
           if (idx < (uint32_t)kLMax) L.sep[idx] = p;
@@ -228,13 +244,19 @@ __global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, co
     // levels known: 0 .. nlev-1, with nlev capped at kLMax + 1
     const uint32_t nlev = len == 0 ? 0 : (nsep >= (uint32_t)kLMax ? kLMax + 1 : nsep + 1);
     wave_lds_sync();
-    if ((uint32_t)gl < nlev) {
-      const uint32_t st = gl == 0 ? 0 : L.sep[gl - 1] + 1;
-      const uint32_t en = ((uint32_t)gl < nsep) ? L.sep[gl] : len;
-      Key k = en <= (uint32_t)kStage ? make_key([&](uint32_t i) { return L.stage[st + i]; }, en - st)
-                                     : make_key([&](uint32_t i) { return tp[st + i]; }, en - st);
-      L.key0[gl] = k.k0;
-      L.key1[gl] = k.k1;
+    uint64_t my_k0[kLPer], my_k1[kLPer];  // lane gl: the keys of levels gl, gl + kG, ...
+#pragma unroll
+    for (int j = 0; j < kLPer; j++) {
+      const uint32_t lv = gl + j * kG;
+      my_k0[j] = my_k1[j] = 0;
+      if (lv < nlev && lv < (uint32_t)kLMax) {
+        const uint32_t st = lv == 0 ? 0 : L.sep[lv - 1] + 1;
+        const uint32_t en = (lv < nsep) ? L.sep[lv] : len;
+        Key k = en <= (uint32_t)kStage ? make_key([&](uint32_t i) { return L.stage[st + i]; }, en - st)
+                                       : make_key([&](uint32_t i) { return tp[st + i]; }, en - st);
+        my_k0[j] = k.k0;
+        my_k1[j] = k.k1;
+      }
     }
     if (gl == 0) {
       L.front[0][0][0] = 0;
@@ -244,14 +266,19 @@ __global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, co
     wave_lds_sync();
 
     // ---- 2. walk ----------------------------------------------------------
-    uint32_t nf = nlev > 0 ? 1 : 0, nh = 0, nsh = 0;
+    uint32_t *rec = o.recs + (uint64_t)(active ? t : 0) * kRecStrideAlloc;
+    uint32_t nf = nlev > 0 ? 1 : 0, nh = 0, nsh = 0, S = 0, H = 0;
     int cur = 0;
     for (uint32_t d = 0; d < nlev && nf > 0; d++) {
       if (d >= (uint32_t)kLMax) {
         why = kWhyLevels;
         break;
       }
-      const uint64_t k0 = L.key0[d], k1 = L.key1[d];
+      uint64_t s0 = my_k0[0], s1 = my_k1[0];
+#pragma unroll
+      for (int j = 1; j < kLPer; j++)
+        if (d / kG == (uint32_t)j) s0 = my_k0[j], s1 = my_k1[j];
+      const uint64_t k0 = shfl64(s0, gbase + (int)(d % kG)), k1 = shfl64(s1, gbase + (int)(d % kG));
       const bool has_next = d + 1 < nlev;
       // key == "+" / "#": the literal probe IS the wildcard probe (the
       // reference visits that child twice; no parent probe: topics.go:507)
@@ -276,35 +303,38 @@ __global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, co
         const bool found = c != kNone;
         const uint32_t fl = found ? dc.sh_cnt_flags >> 24 : 0;
         const bool skip_dollar = dollar && (fl & kFlagDollarWild);  // topics.go:527
-        const bool h_own = found && dc.sub_cnt > 0 && !skip_dollar;
-        const bool h_par = found && type == 0 && dc.hsub_cnt > 0 && !skip_dollar;  // topics.go:507-509
-        const bool h_sh = found && (dc.sh_cnt_flags & kShCntMask) > 0;
+        const uint32_t c_own = found && !skip_dollar ? dc.sub_cnt : 0;
+        const uint32_t c_par = found && type == 0 && !skip_dollar ? dc.hsub_cnt : 0;  // topics.go:507-509
+        const uint32_t c_sh = found ? dc.sh_cnt_flags & kShCntMask : 0;
         const bool push = found && has_next && (fl & kFlagHasChildren);
-        const uint32_t m_own = (uint32_t)(__ballot(h_own) >> gbase) & 0xFFFFu;
-        const uint32_t m_par = (uint32_t)(__ballot(h_par) >> gbase) & 0xFFFFu;
-        const uint32_t m_sh = (uint32_t)(__ballot(h_sh) >> gbase) & 0xFFFFu;
-        const uint32_t m_push = (uint32_t)(__ballot(push) >> gbase) & 0xFFFFu;
+        const uint32_t m_own = (uint32_t)(__ballot(c_own > 0) >> gbase) & kGMask;
+        const uint32_t m_par = (uint32_t)(__ballot(c_par > 0) >> gbase) & kGMask;
+        const uint32_t m_sh = (uint32_t)(__ballot(c_sh > 0) >> gbase) & kGMask;
+        const uint32_t m_push = (uint32_t)(__ballot(push) >> gbase) & kGMask;
         const uint32_t n_own = __popc(m_own), n_par = __popc(m_par);
         if (nh + n_own + n_par > (uint32_t)kHCap) why = kWhyHits;
         if (nsh + __popc(m_sh) > (uint32_t)kShCap) why = kWhyShared;
         if (nnext + __popc(m_push) > (uint32_t)kFCap) why = kWhyFrontier;
         if (why != kNoWhy) break;
-        if (h_own) {
+        uint32_t t_own, t_par;
+        const uint32_t x_own = group_scan_ex<kG>(c_own, gl, &t_own, gbase);
+        const uint32_t x_par = group_scan_ex<kG>(c_par, gl, &t_par, gbase);
+        if (active && c_own) {
           const uint32_t i = nh + __popc(m_own & gmask_lt);
-          L.hit_rank[i] = 2 * c;
-          L.hit_off[i] = dc.sub_off;
-          L.hit_cnt[i] = dc.sub_cnt;
+          rec[2 + 3 * i] = dc.sub_off;
+          rec[3 + 3 * i] = S + x_own;
+          rec[4 + 3 * i] = 2 * c;
         }
-        if (h_par) {
+        if (active && c_par) {
           const uint32_t i = nh + n_own + __popc(m_par & gmask_lt);
-          L.hit_rank[i] = 2 * c + 1;
-          L.hit_off[i] = dc.hsub_off;
-          L.hit_cnt[i] = dc.hsub_cnt;
+          rec[2 + 3 * i] = dc.hsub_off;
+          rec[3 + 3 * i] = S + t_own + x_par;
+          rec[4 + 3 * i] = 2 * c + 1;
         }
-        if (h_sh) {
+        if (active && c_sh) {
           const uint32_t i = nsh + __popc(m_sh & gmask_lt);
-          L.sh_off[i] = dc.sh_off;
-          L.sh_cnt[i] = dc.sh_cnt_flags & kShCntMask;
+          rec[kRecSh + 2 * i] = dc.sh_off;
+          rec[kRecSh + 1 + 2 * i] = c_sh;
         }
         if (push) {
           const uint32_t i = nnext + __popc(m_push & gmask_lt);
@@ -312,62 +342,26 @@ __global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, co
           L.front[cur ^ 1][1][i] = dc.plus;
           L.front[cur ^ 1][2][i] = dc.hash;
         }
+        uint32_t t_sh;
+        (void)group_scan_ex<kG>(c_sh, gl, &t_sh, gbase);
         nh += n_own + n_par;
         nsh += __popc(m_sh);
         nnext += __popc(m_push);
+        S += t_own + t_par;
+        H += t_sh;
       }
       wave_lds_sync();
       if (why != kNoWhy) break;
       cur ^= 1;
       nf = nnext;
     }
-
-    // ---- 3. rank hits, prefix-sum their sizes into the record ---------------
-    uint32_t *rec = o.recs + (uint64_t)(active ? t : 0) * kRecStrideAlloc;
-    const bool ok = active && why == kNoWhy;
-    if (ok) {
-      for (uint32_t i = gl; i < nh; i += kG) {
-        const uint32_t r = L.hit_rank[i];
-        uint32_t pos = 0;
-        for (uint32_t j = 0; j < nh; j++) pos += L.hit_rank[j] < r;  // ranks are distinct
-        rec[2 + 2 * pos] = L.hit_off[i];
-        L.s_cnt[pos] = L.hit_cnt[i];
-      }
-    }
-    wave_lds_sync();
-    uint32_t S = 0, H = 0;
-    if (ok) {
-      uint32_t c3[3], local = 0;
-      for (int k = 0; k < 3; k++) {
-        const uint32_t i = 3 * gl + k;
-        c3[k] = i < nh ? L.s_cnt[i] : 0;
-        local += c3[k];
-      }
-      uint32_t inc = local;  // inclusive scan over the group's 16 lanes
-      for (int d = 1; d < kG; d <<= 1) {
-        const uint32_t v = __shfl_up(inc, d, kG);
-        if (gl >= d) inc += v;
-      }
-      S = __shfl(inc, gbase + kG - 1, 64);
-      uint32_t p = inc - local;
-      for (int k = 0; k < 3; k++) {
-        const uint32_t i = 3 * gl + k;
-        if (i < nh) rec[3 + 2 * i] = p;
-        p += c3[k];
-      }
-      if ((uint32_t)gl < nsh) {
-        rec[2 + 2 * nh + 2 * gl] = L.sh_off[gl];
-        rec[3 + 2 * nh + 2 * gl] = L.sh_cnt[gl];
-      }
-      for (uint32_t i = 0; i < nsh; i++) H += L.sh_cnt[i];
-      if (gl == 0) {
+    if (why == kNoWhy && S > (uint32_t)kBigMax) why = kWhyEntries;
+    if (active && gl == 0) {
+      const bool dfs = why != kNoWhy;
+      if (!dfs) {
         rec[0] = nh | (nsh << 8);
         rec[1] = S;
       }
-      if (S > (uint32_t)kBigMax) why = kWhyEntries;
-    }
-    if (active && gl == 0) {
-      const bool dfs = why != kNoWhy;
       o.cls[t] = dfs ? kClsDfs : S == 0 ? kClsDone : S <= (uint32_t)kSMax ? kClsSmall : kClsBig;
       o.scount[t] = dfs ? 0 : S;
       o.hcount[t] = dfs ? 0 : H;
@@ -420,14 +414,14 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(DeviceSnapshot s, 
     if (cls == kClsDfs || (cls != kClsSmall && H == 0)) continue;
     const uint32_t w0 = __shfl(rw, 0, 64), S = __shfl(rw, 1, 64);
     const uint32_t nh = w0 & 0xFFu, nsh = w0 >> 8;
-    const uint32_t words = 2 + 2 * nh + 2 * nsh;
+    const uint32_t *grec = o.recs + (uint64_t)t * kRecStrideAlloc;
     L.rec[lane] = rw;
-    for (uint32_t i = kWave + lane; i < words; i += kWave) L.rec[i] = o.recs[(uint64_t)t * kRecStrideAlloc + i];
+    for (uint32_t i = kWave + lane; i < 2 + 3 * nh; i += kWave) L.rec[i] = grec[i];
     wave_lds_sync();
     if (H) {  // shared candidates (gatherSharedSubscriptions, topics.go:541-555)
       uint32_t w = 0;
       for (uint32_t i = 0; i < nsh; i++) {
-        const uint32_t so = L.rec[2 + 2 * nh + 2 * i], sc = L.rec[3 + 2 * nh + 2 * i];
+        const uint32_t so = grec[kRecSh + 2 * i], sc = grec[kRecSh + 1 + 2 * i];
         for (uint32_t j = lane; j < sc; j += kWave) o.hout[hb + w + j] = so + j;
         w += sc;
       }
@@ -444,7 +438,7 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(DeviceSnapshot s, 
       meta[k] = 0;
       if (r < S) {
         hh[k] = find_hit(L.rec, nh, r);
-        sid[k] = L.rec[2 + 2 * hh[k]] + (r - L.rec[3 + 2 * hh[k]]);
+        sid[k] = L.rec[2 + 3 * hh[k]] + (r - L.rec[3 + 3 * hh[k]]);
         const SubEnt e = s.subs[sid[k]];
         cl[k] = e.client;
         meta[k] = e.meta;
@@ -477,7 +471,7 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(DeviceSnapshot s, 
       wave_lds_sync();
 #pragma unroll
       for (int k = 0; k < kSmallPer; k++)
-        if (meta[k] & kMetaMulti) table_insert(L.tkey, L.tbits, L.tmin, mask, lg, cl[k], meta[k], hh[k]);
+        if (meta[k] & kMetaMulti) table_insert(L.tkey, L.tbits, L.tmin, mask, lg, cl[k], meta[k], L.rec[4 + 3 * hh[k]]);
       wave_lds_sync();
 #pragma unroll
       for (int k = 0; k < kSmallPer; k++) {
@@ -489,7 +483,7 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(DeviceSnapshot s, 
           win = true;
           if (meta[k] & kMetaMulti) {
             const uint32_t sl = table_find(L.tkey, mask, lg, cl[k]);
-            win = L.tmin[sl] == hh[k];
+            win = L.tmin[sl] == L.rec[4 + 3 * hh[k]];
             v = L.tbits[sl];
           }
           ent = pack_delivery(cl[k], sid[k], 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
@@ -543,8 +537,8 @@ __global__ __launch_bounds__(kBigThreads) void k_big(DeviceSnapshot s, Outputs o
     t_nxt = t_nn;
     __syncthreads();
     const uint32_t nh = rec[0] & 0xFFu, S = rec[1];
-    if (2 + 2 * nh > (uint32_t)kWave) {  // block-uniform
-      for (uint32_t i = kWave + tid; i < 2 + 2 * nh; i += kBigThreads)
+    if (2 + 3 * nh > (uint32_t)kWave) {  // block-uniform
+      for (uint32_t i = kWave + tid; i < 2 + 3 * nh; i += kBigThreads)
         rec[i] = o.recs[(uint64_t)t * kRecStrideAlloc + i];
       __syncthreads();
     }
@@ -556,7 +550,7 @@ __global__ __launch_bounds__(kBigThreads) void k_big(DeviceSnapshot s, Outputs o
       meta[k] = 0;
       if (r < S) {
         hh[k] = find_hit(rec, nh, r);
-        sid[k] = rec[2 + 2 * hh[k]] + (r - rec[3 + 2 * hh[k]]);
+        sid[k] = rec[2 + 3 * hh[k]] + (r - rec[3 + 3 * hh[k]]);
         const SubEnt e = s.subs[sid[k]];
         cl[k] = e.client;
         meta[k] = e.meta;
@@ -595,7 +589,7 @@ __global__ __launch_bounds__(kBigThreads) void k_big(DeviceSnapshot s, Outputs o
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < kBigPer; k++)
-      if (meta[k] & kMetaMulti) table_insert(tkey, tbits, tmin, mask, lg, cl[k], meta[k], hh[k]);
+      if (meta[k] & kMetaMulti) table_insert(tkey, tbits, tmin, mask, lg, cl[k], meta[k], rec[4 + 3 * hh[k]]);
     __syncthreads();
     uint32_t D = 0;
 #pragma unroll
@@ -609,7 +603,7 @@ __global__ __launch_bounds__(kBigThreads) void k_big(DeviceSnapshot s, Outputs o
         win = true;
         if (meta[k] & kMetaMulti) {
           const uint32_t sl = table_find(tkey, mask, lg, cl[k]);
-          win = tmin[sl] == hh[k];
+          win = tmin[sl] == rec[4 + 3 * hh[k]];
           v = tbits[sl];
         }
         ent = pack_delivery(cl[k], sid[k], 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
@@ -987,12 +981,20 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   o.recs = (uint32_t *)ws.ptr(W::kRecs);
   o.ctr = (Counters *)ws.ptr(W::kCounters);
   // the big-topic list reuses the DFS list's tail? no: its own region after the record array
+  const int walk_g = ws.walk_lanes == 8 ? 8 : 16;
+  const uint32_t per_block = kWalkWaves * (kWave / walk_g);
   const uint32_t walk_blocks = std::max<uint32_t>(
-      1, std::min<uint32_t>((n + kWalkWaves * kGroups - 1) / (kWalkWaves * kGroups), ws.max_blocks));
+      1, std::min<uint32_t>((n + per_block - 1) / per_block,
+                            walk_g == 8 ? resident_blocks(ws, 3, k_walk<8>) : resident_blocks(ws, 4, k_walk<16>)));
 
   HIP_TRY(hipMemsetAsync(o.ctr, 0, sizeof(Counters), st));
   mark(ws, 0, st);
-  if (n > 0) hipLaunchKernelGGL(k_walk, dim3(walk_blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o);
+  if (n > 0) {
+    if (walk_g == 8)
+      hipLaunchKernelGGL(k_walk<8>, dim3(walk_blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o);
+    else
+      hipLaunchKernelGGL(k_walk<16>, dim3(walk_blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o);
+  }
   HIP_TRY(hipGetLastError());
   mark(ws, 1, st);
   if (scan_offsets(ws, o.scount, o.dstart, n, st) || scan_offsets(ws, o.hcount, o.hstart, n, st)) return -3;

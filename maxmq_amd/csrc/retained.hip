@@ -41,6 +41,7 @@ namespace mqm {
 namespace {
 
 constexpr uint32_t kEmitChunk = 4096;  // refs copied per wavefront task
+constexpr uint32_t kSmallEmit = 32;    // emissions up to this size: copied by one thread
 
 struct Level {         // one level of one filter
   uint64_t k0, k1;     // key (keys.h)
@@ -204,22 +205,81 @@ __global__ void k_has_levels(uint32_t n, const uint32_t *__restrict__ nlev, uint
   if (f < n) flag[f] = nlev[f] ? 1u : 0u;
 }
 
-__global__ void k_emit_count(uint64_t ne, const Emit *__restrict__ e, unsigned long long *__restrict__ fcount) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < ne) atomicAdd(&fcount[e[i].f], (unsigned long long)(e[i].hi - e[i].lo));
+// Emissions of one filter are adjacent (every level's items and emissions
+// stay in filter order), so a wavefront folds each run of equal filter ids
+// (segmented scan over the lanes) and issues one atomic per run.
+struct Run {
+  uint64_t inc;    // inclusive sum of cnt within the lane's run
+  bool last;       // the lane closes its run
+  int last_lane;   // lane that closes the lane's run
+};
+
+__device__ __forceinline__ Run fold_runs(uint32_t f, uint64_t cnt) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t pf = __shfl_up(f, 1, 64);
+  const bool head = lane == 0 || pf != f;
+  const uint64_t heads = __ballot(head);
+  const uint64_t le = lane == 63 ? ~0ull : ((1ull << (lane + 1)) - 1);
+  const int start = 63 - __builtin_clzll(heads & le);
+  uint64_t inc = cnt;
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t lo = __shfl_up((uint32_t)inc, d, 64), hi = __shfl_up((uint32_t)(inc >> 32), d, 64);
+    if (lane - d >= start) inc += ((uint64_t)hi << 32) | lo;
+  }
+  const uint64_t after = heads & ~le;
+  Run r;
+  r.last_lane = after ? __builtin_ctzll(after) - 1 : 63;
+  r.last = r.last_lane == lane;
+  r.inc = inc;
+  return r;
 }
 
-__global__ void k_emit_pos(uint64_t ne, const Emit *__restrict__ e, const uint64_t *__restrict__ foff,
-                           unsigned long long *__restrict__ fcur, uint64_t *__restrict__ pos,
-                           uint32_t *__restrict__ chunks) {
+__global__ __launch_bounds__(256) void k_emit_count(uint64_t ne, const Emit *__restrict__ e,
+                                                   unsigned long long *__restrict__ fcount) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool ok = i < ne;
+  const uint32_t f = ok ? e[i].f : 0xFFFFFFFFu;
+  const uint64_t cnt = ok ? e[i].hi - e[i].lo : 0;
+  const Run r = fold_runs(f, cnt);
+  if (ok && r.last) atomicAdd(&fcount[f], (unsigned long long)r.inc);
+}
+
+__global__ __launch_bounds__(256) void k_emit_pos(uint64_t ne, const Emit *__restrict__ e,
+                                                 const uint64_t *__restrict__ foff,
+                                                 unsigned long long *__restrict__ fcur, uint64_t *__restrict__ pos,
+                                                 uint32_t *__restrict__ chunks) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool ok = i < ne;
+  const uint32_t f = ok ? e[i].f : 0xFFFFFFFFu;
+  const uint64_t cnt = ok ? e[i].hi - e[i].lo : 0;
+  const Run r = fold_runs(f, cnt);
+  unsigned long long base = 0;
+  if (ok && r.last) base = foff[f] + atomicAdd(&fcur[f], (unsigned long long)r.inc);
+  const uint32_t blo = __shfl((uint32_t)base, r.last_lane, 64), bhi = __shfl((uint32_t)(base >> 32), r.last_lane, 64);
+  const uint32_t tlo = __shfl((uint32_t)r.inc, r.last_lane, 64), thi = __shfl((uint32_t)(r.inc >> 32), r.last_lane, 64);
+  if (!ok) return;
+  const uint64_t run_base = ((uint64_t)bhi << 32) | blo, run_total = ((uint64_t)thi << 32) | tlo;
+  (void)run_total;
+  pos[i] = run_base + (r.inc - cnt);
+  chunks[i] = cnt > kSmallEmit ? (uint32_t)((cnt + kEmitChunk - 1) / kEmitChunk) : 0u;
+}
+
+// emissions of <= kSmallEmit refs: a thread each
+__global__ __launch_bounds__(256) void k_emit_small(uint64_t ne, const Emit *__restrict__ e,
+                                                   const uint64_t *__restrict__ pos,
+                                                   const uint64_t *__restrict__ refs,
+                                                   const uint64_t *__restrict__ rch_refs, uint64_t *__restrict__ out) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= ne) return;
-  const uint32_t cnt = e[i].hi - e[i].lo;
-  pos[i] = foff[e[i].f] + atomicAdd(&fcur[e[i].f], (unsigned long long)cnt);
-  chunks[i] = (cnt + kEmitChunk - 1) / kEmitChunk;
+  const Emit it = e[i];
+  const uint32_t cnt = it.hi - it.lo;
+  if (cnt > kSmallEmit) return;
+  const uint64_t *src = (it.list ? rch_refs : refs) + it.lo;
+  uint64_t *dst = out + pos[i];
+  for (uint32_t j = 0; j < cnt; j++) dst[j] = src[j];
 }
 
-// a wavefront per chunk of kEmitChunk refs
+// larger emissions: a wavefront per chunk of kEmitChunk refs
 __global__ __launch_bounds__(256) void k_emit_fill(uint64_t ne, uint64_t nchunks, const Emit *__restrict__ e,
                                                   const uint64_t *__restrict__ pos, const uint64_t *__restrict__ coff,
                                                   const uint64_t *__restrict__ refs,
@@ -395,6 +455,10 @@ int messages_device(const DeviceSnapshot &s, const DeviceRetained *r, Workspace 
   const uint64_t n_refs = hp[0], nchunks = hp[1];
   if (ws.get(W::kROut, sizeof(uint64_t) * (n_refs + 1))) return -2;
   auto *refs_out = (uint64_t *)ws.ptr(W::kROut);
+  if (n_emit)
+    hipLaunchKernelGGL(k_emit_small, dim3(blocks_for(n_emit)), dim3(256), 0, st, n_emit, emit, pos, r->refs,
+                       r->rch_refs, refs_out);
+  HIP_TRY(hipGetLastError());
   if (nchunks)
     hipLaunchKernelGGL(k_emit_fill, dim3((uint32_t)std::min<uint64_t>((nchunks + 3) / 4, 8192)), dim3(256), 0, st,
                        n_emit, nchunks, emit, pos, coff, r->refs, r->rch_refs, refs_out);
