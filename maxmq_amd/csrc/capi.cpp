@@ -127,7 +127,10 @@ int mqm_create(const mqm_config *cfg, mqm_index **out) {
     if (h->cfg.device < 0 || h->cfg.device >= ndev) return MQM_EINVAL;
     if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) return MQM_EHIP;
-    if (const char *e = getenv("MQM_WALK_LANES")) h->ws.walk_lanes = atoi(e) == 8 ? 8 : 16;
+    if (const char *e = getenv("MQM_WALK_LANES")) {
+      const int g = atoi(e);
+      h->ws.walk_lanes = g == 4 || g == 16 ? g : 8;
+    }
     *out = h.release();
     return MQM_OK;
   });

@@ -25,7 +25,7 @@ struct Workspace {
   Buf bufs[kNumSlots];
   void *host_pinned = nullptr;
   uint32_t max_blocks = 2048;  // walk-kernel grid cap (grid-stride beyond)
-  int walk_lanes = 16;         // lanes per topic in k_walk (8 or 16; env MQM_WALK_LANES)
+  int walk_lanes = 8;          // lanes per topic in k_walk (4, 8 or 16; env MQM_WALK_LANES)
   uint32_t resident[5] = {0, 0, 0, 0, 0};  // k_big tiers, k_small, k_walk<8>, k_walk<16>: resident blocks on the device
   // why the last batch's DFS topics left the bounded path:
   // frontier, hits, cached levels, shared hits, raw entries

@@ -981,16 +981,18 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   o.recs = (uint32_t *)ws.ptr(W::kRecs);
   o.ctr = (Counters *)ws.ptr(W::kCounters);
   // the big-topic list reuses the DFS list's tail? no: its own region after the record array
-  const int walk_g = ws.walk_lanes == 8 ? 8 : 16;
+  const int walk_g = ws.walk_lanes;
   const uint32_t per_block = kWalkWaves * (kWave / walk_g);
   const uint32_t walk_blocks = std::max<uint32_t>(
       1, std::min<uint32_t>((n + per_block - 1) / per_block,
-                            walk_g == 8 ? resident_blocks(ws, 3, k_walk<8>) : resident_blocks(ws, 4, k_walk<16>)));
+                            walk_g == 4 ? resident_blocks(ws, 3, k_walk<4>) : walk_g == 8 ? resident_blocks(ws, 3, k_walk<8>) : resident_blocks(ws, 4, k_walk<16>)));
 
   HIP_TRY(hipMemsetAsync(o.ctr, 0, sizeof(Counters), st));
   mark(ws, 0, st);
   if (n > 0) {
-    if (walk_g == 8)
+    if (walk_g == 4)
+      hipLaunchKernelGGL(k_walk<4>, dim3(walk_blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o);
+    else if (walk_g == 8)
       hipLaunchKernelGGL(k_walk<8>, dim3(walk_blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o);
     else
       hipLaunchKernelGGL(k_walk<16>, dim3(walk_blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o);
