@@ -463,7 +463,7 @@ int mqm_snapshot_stats_get(mqm_index *h, mqm_snapshot_stats *out) {
   const HostSnapshot &hs = *h->snap->host;
   out->nodes = hs.nodes.size();
   out->edges = hs.n_edges;
-  out->edge_buckets = hs.bucket_mask + 1;
+  out->edge_buckets = hs.n_buckets;
   out->subs = hs.sub_info.size();
   out->shared = hs.shared_info.size();
   out->height = hs.height;

@@ -26,9 +26,9 @@ __device__ __forceinline__ NodeDesc load_desc(const NodeDesc *p) {
 // Long keys (>= 16 bytes) are verified byte-for-byte against the token pool.
 __device__ inline uint32_t probe_edge(const DeviceSnapshot &s, uint32_t parent, uint64_t k0, uint64_t k1,
                                const uint8_t *tok, uint32_t tok_len, NodeDesc *desc) {
-  const uint64_t nslots = (s.bucket_mask + 1) * kEdgesPerBucket;
+  const uint64_t nslots = s.n_buckets * kEdgesPerBucket;
   Key key{k0, k1};
-  uint64_t slot = (edge_hash(parent, key) & s.bucket_mask) * kEdgesPerBucket;
+  uint64_t slot = bucket_of(edge_hash(parent, key), s.n_buckets) * kEdgesPerBucket;
   for (;;) {
     // the whole 64-B entry in one round trip: key, header and the child's descriptor
     const uint4 *q = reinterpret_cast<const uint4 *>(s.edges + slot);
@@ -52,7 +52,7 @@ __device__ inline uint32_t probe_edge(const DeviceSnapshot &s, uint32_t parent, 
         return pc.y;
       }
     }
-    slot = (slot + 1) & (nslots - 1);
+    slot = slot + 1 == nslots ? 0 : slot + 1;
   }
 }
 

@@ -9,18 +9,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <unordered_map>
 
 #include "../../include/mqmatch.h"
 
 namespace mqm {
-
-static uint64_t next_pow2(uint64_t x) {
-  uint64_t p = 1;
-  while (p < x) p <<= 1;
-  return p;
-}
 
 // kMetaMulti (snapshot.h).  Levels of a filter are the keys on its node's
 // path; two filters of one client can be gathered for the same topic only if
@@ -188,9 +183,16 @@ int flatten(const Store &st, HostSnapshot *out) {
     }
   }
 
-  // 3. literal edges -> open-addressed table of 128-B buckets (load <= 0.5)
-  const uint64_t buckets = next_pow2(std::max<uint64_t>(n_literal_edges, 1));
-  hs.bucket_mask = buckets - 1;
+  // 3. literal edges -> open-addressed table of 128-B buckets, linear probing
+  //    at load factor edge_load (default 0.5; env MQM_EDGE_LOAD in (0, 0.9])
+  double load = 0.5;
+  if (const char *e = getenv("MQM_EDGE_LOAD")) {
+    const double v = atof(e);
+    if (v > 0.0 && v <= 0.9) load = v;
+  }
+  const uint64_t buckets =
+      std::max<uint64_t>(1, (uint64_t)((double)n_literal_edges / (load * kEdgesPerBucket)) + 1);
+  hs.n_buckets = buckets;
   hs.n_edges = n_literal_edges;
   EdgeEntry empty;
   memset(&empty, 0, sizeof(empty));
@@ -223,8 +225,8 @@ int flatten(const Store &st, HostSnapshot *out) {
         e.tok_off = it->second;
       }
       e.desc = hs.nodes[cn];
-      uint64_t slot = (edge_hash((uint32_t)i, k) & hs.bucket_mask) * kEdgesPerBucket;
-      while (hs.edges[slot].parent != kNone) slot = (slot + 1) & (n_slots - 1);
+      uint64_t slot = bucket_of(edge_hash((uint32_t)i, k), hs.n_buckets) * kEdgesPerBucket;
+      while (hs.edges[slot].parent != kNone) slot = slot + 1 == n_slots ? 0 : slot + 1;
       hs.edges[slot] = e;
     }
   }
@@ -275,7 +277,7 @@ int upload(std::shared_ptr<const HostSnapshot> hs, int device, std::unique_ptr<G
   g->dev.edges = (const EdgeEntry *)g->buffers[1];
   g->dev.subs = (const SubEnt *)g->buffers[2];
   g->dev.tok_pool = (const uint8_t *)g->buffers[3];
-  g->dev.bucket_mask = hs->bucket_mask;
+  g->dev.n_buckets = hs->n_buckets;
   g->dev.n_nodes = (uint32_t)hs->nodes.size();
   g->dev.n_subs = (uint32_t)hs->sub_info.size();
   g->dev.n_shared = (uint32_t)hs->shared_info.size();

@@ -20,12 +20,12 @@ struct SubInfo {
 
 struct HostSnapshot {
   std::vector<NodeDesc> nodes;
-  std::vector<EdgeEntry> edges;  // (bucket_mask + 1) * kEdgesPerBucket
+  std::vector<EdgeEntry> edges;  // n_buckets * kEdgesPerBucket
   std::vector<SubEnt> subs;
   std::vector<SubInfo> sub_info;     // by non-shared sid
   std::vector<SubInfo> shared_info;  // by shared sid
   std::vector<uint8_t> tok_pool;
-  uint64_t bucket_mask = 0;
+  uint64_t n_buckets = 0;
   uint32_t height = 0;
   uint64_t n_edges = 0;
   uint64_t n_solo = 0;  // subscriptions without kMetaMulti

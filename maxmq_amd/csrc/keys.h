@@ -77,6 +77,15 @@ MQM_HD Key make_key(ByteAt at, uint32_t len) {
 
 MQM_HD bool key_is_long(const Key &k) { return (k.k1 >> 56) == 0xFF; }
 
+// bucket of an edge among n buckets (multiply-shift range reduction: any n)
+MQM_HD uint64_t bucket_of(uint64_t h, uint64_t n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umul64hi(h, n);
+#else
+  return (uint64_t)(((unsigned __int128)h * n) >> 64);
+#endif
+}
+
 // bucket hash of an edge (parent node, child key)
 MQM_HD uint64_t edge_hash(uint32_t parent, const Key &k) {
   uint64_t h = fmix64(k.k0 ^ rotl64(k.k1, 29) ^ ((uint64_t)parent * 0x9E3779B97F4A7C15ull));

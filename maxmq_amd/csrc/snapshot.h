@@ -75,7 +75,7 @@ struct DeviceSnapshot {
   const EdgeEntry *edges;
   const SubEnt *subs;
   const uint8_t *tok_pool;
-  uint64_t bucket_mask;   // number of buckets - 1 (power of two)
+  uint64_t n_buckets;     // edge buckets (kEdgesPerBucket entries each; any count)
   uint32_t n_nodes;
   uint32_t n_subs;
   uint32_t n_shared;
