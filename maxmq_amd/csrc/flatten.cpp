@@ -157,6 +157,7 @@ int flatten(const Store &st, HostSnapshot *out) {
       hs.shared_info.push_back(
           SubInfo{s.sub.filter, s.sub.client, s.sub.ident, s.sub.qos, s.sub.no_local, s.sub.rap, s.sub.rh});
     uint8_t f = h.n_children ? (uint8_t)kFlagHasChildren : (uint8_t)0;
+    if (h.n_children > (uint32_t)(pc != kNone) + (uint32_t)(hc != kNone)) f |= kFlagHasLiteral;
     if (i > 0) {
       const uint32_t parent_new = new_id[h.parent];
       if (parent_new == 0) {  // root child: Filter[0] of every sub stored below it
@@ -185,7 +186,7 @@ int flatten(const Store &st, HostSnapshot *out) {
 
   // 3. literal edges -> open-addressed table of 128-B buckets, linear probing
   //    at load factor edge_load (default 0.5; env MQM_EDGE_LOAD in (0, 0.9])
-  double load = 0.5;
+  double load = 0.26;
   if (const char *e = getenv("MQM_EDGE_LOAD")) {
     const double v = atof(e);
     if (v > 0.0 && v <= 0.9) load = v;

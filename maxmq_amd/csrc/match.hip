@@ -73,6 +73,7 @@ constexpr int kBigSlotsB = 4096;         // overflow tier: 48 KiB, holds any bou
 constexpr int kBigMax = 3072;            // raw entries per k_big topic
 constexpr int kBigPer = kBigMax / kBigThreads;
 constexpr uint32_t kNoWhy = 0xFFFFFFFFu;
+constexpr uint32_t kNoLit = 0x80000000u;   // frontier node id flag: no literal child (node ids < 2^31)
 
 static_assert(kRecStrideAlloc % 4 == 0 && kRecStrideAlloc >= kRecStride, "16-B aligned records");
 static_assert(kSmallMulti * 4 <= kSmallSlots * 3, "k_small table load factor");
@@ -258,8 +259,8 @@ __global__ __launch_bounds__(kWave * kWalkWaves, 5) void k_walk(DeviceSnapshot s
         my_k1[j] = k.k1;
       }
     }
-    if (gl == 0) {
-      L.front[0][0][0] = 0;
+    if (gl == 0) {  // frontier node ids carry kNoLit when no child is a literal
+      L.front[0][0][0] = ((root.sh_cnt_flags >> 24) & kFlagHasLiteral) ? 0u : kNoLit;
       L.front[0][1][0] = root.plus;
       L.front[0][2][0] = root.hash;
     }
@@ -294,7 +295,7 @@ __global__ __launch_bounds__(kWave * kWalkWaves, 5) void k_walk(DeviceSnapshot s
         if (item < nf * 3) {
           const uint32_t node = L.front[cur][0][fi];
           if (type == 0) {
-            if (!lit_is_wild) c = probe_edge(s, node, k0, k1, tp + tst, tln, &dc);
+            if (!lit_is_wild && !(node & kNoLit)) c = probe_edge(s, node, k0, k1, tp + tst, tln, &dc);
           } else {
             c = L.front[cur][type][fi];
             if (c != kNone) dc = load_desc(s.nodes + c);
@@ -338,7 +339,7 @@ __global__ __launch_bounds__(kWave * kWalkWaves, 5) void k_walk(DeviceSnapshot s
         }
         if (push) {
           const uint32_t i = nnext + __popc(m_push & gmask_lt);
-          L.front[cur ^ 1][0][i] = c;
+          L.front[cur ^ 1][0][i] = c | ((fl & kFlagHasLiteral) ? 0u : kNoLit);
           L.front[cur ^ 1][1][i] = dc.plus;
           L.front[cur ^ 1][2][i] = dc.hash;
         }

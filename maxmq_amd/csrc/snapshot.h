@@ -17,6 +17,7 @@ namespace mqm {
 enum : uint32_t {
   kFlagHasChildren = 1u,  // any child (literal, '+', '#')
   kFlagDollarWild = 2u,   // node lies under a root child whose key starts with '+'/'#'
+  kFlagHasLiteral = 4u,   // some child is a literal (else the edge probe is skipped)
                           // == the `$` rule's Filter[0] test (topics.go:527)
 };
 
