@@ -15,7 +15,7 @@ __device__ __forceinline__ NodeDesc load_desc(const NodeDesc *p) {
   d.hash = a.y;
   d.sub_off = a.z;
   d.sub_cnt = a.w;
-  d.hsub_off = b.x;
+  d.multi = b.x;
   d.hsub_cnt = b.y;
   d.sh_off = b.z;
   d.sh_cnt_flags = b.w;
@@ -45,7 +45,7 @@ __device__ inline uint32_t probe_edge(const DeviceSnapshot &s, uint32_t parent, 
         desc->hash = d0.y;
         desc->sub_off = d0.z;
         desc->sub_cnt = d0.w;
-        desc->hsub_off = d1.x;
+        desc->multi = d1.x;
         desc->hsub_cnt = d1.y;
         desc->sh_off = d1.z;
         desc->sh_cnt_flags = d1.w;

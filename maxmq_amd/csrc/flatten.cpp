@@ -143,13 +143,23 @@ int flatten(const Store &st, HostSnapshot *out) {
     d.plus = pc == kNone ? kNone : new_id[pc];
     d.hash = hc == kNone ? kNone : new_id[hc];
     n_literal_edges += h.n_children - (pc != kNone) - (hc != kNone);
-    if (hs.subs.size() + h.subs.size() > kMaxSubs) return MQM_ELIMIT;
-    d.sub_off = (uint32_t)hs.subs.size();
-    d.sub_cnt = (uint32_t)h.subs.size();
-    for (const SubRec &s : h.subs) {  // sorted by client (store.cpp)
-      hs.subs.push_back(SubEnt{s.client, (uint32_t)s.qos | ((uint32_t)(s.no_local & 1) << 2) |
-                                             ((uint32_t)(s.rap & 1) << 3) | ((uint32_t)(s.rh & 3) << 4)});
-      hs.sub_info.push_back(SubInfo{s.filter, s.client, s.ident, s.qos, s.no_local, s.rap, s.rh});
+    // subscription ranges: a node's, then its '#' child's, then that one's '#'
+    // child's ... back to back (NodeDesc::hsub_cnt)
+    if (i == 0 || h.key != hash_tok) {
+      for (uint32_t k = (uint32_t)i, sn = order[i];;) {
+        const auto &subs = nodes[sn].subs;
+        if (hs.subs.size() + subs.size() > kMaxSubs) return MQM_ELIMIT;
+        hs.nodes[k].sub_off = (uint32_t)hs.subs.size();
+        hs.nodes[k].sub_cnt = (uint32_t)subs.size();
+        for (const SubRec &s : subs) {
+          hs.subs.push_back(SubEnt{s.client, (uint32_t)s.qos | ((uint32_t)(s.no_local & 1) << 2) |
+                                                 ((uint32_t)(s.rap & 1) << 3) | ((uint32_t)(s.rh & 3) << 4)});
+          hs.sub_info.push_back(SubInfo{s.filter, s.client, s.ident, s.qos, s.no_local, s.rap, s.rh});
+        }
+        sn = st.child(sn, hash_tok);
+        if (sn == kNone) break;
+        k = new_id[sn];
+      }
     }
     if (h.shared.size() > kShCntMask) return MQM_ELIMIT;
     d.sh_off = (uint32_t)hs.shared_info.size();
@@ -173,20 +183,40 @@ int flatten(const Store &st, HostSnapshot *out) {
   }
   mark_multi(st, order, hs);
   if (st.retained_len() > 0) build_retained(st, order, new_id, hs);
+  // every range: solo entries first, then multi (stable); count the multi ones
+  std::vector<uint32_t> own_multi(nn, 0);
+  {
+    std::vector<SubEnt> se;
+    std::vector<SubInfo> si;
+    for (uint64_t i = 0; i < nn; i++) {
+      const uint32_t off = hs.nodes[i].sub_off, cnt = hs.nodes[i].sub_cnt;
+      se.clear();
+      si.clear();
+      for (int pass = 0; pass < 2; pass++)
+        for (uint32_t j = off; j < off + cnt; j++)
+          if (((hs.subs[j].meta & kMetaMulti) != 0) == (pass == 1)) {
+            se.push_back(hs.subs[j]);
+            si.push_back(hs.sub_info[j]);
+            own_multi[i] += pass;
+          }
+      std::copy(se.begin(), se.end(), hs.subs.begin() + off);
+      std::copy(si.begin(), si.end(), hs.sub_info.begin() + off);
+    }
+  }
   for (uint64_t i = 0; i < nn; i++) {
     NodeDesc &d = hs.nodes[i];
-    if (d.hash != kNone) {
-      d.hsub_off = hs.nodes[d.hash].sub_off;
-      d.hsub_cnt = hs.nodes[d.hash].sub_cnt;
-    } else {
-      d.hsub_off = 0;
-      d.hsub_cnt = 0;
-    }
+    const uint32_t hm = d.hash != kNone ? own_multi[d.hash] : 0;
+    d.hsub_cnt = d.hash != kNone ? hs.nodes[d.hash].sub_cnt : 0;
+    d.multi = std::min<uint32_t>(own_multi[i], 0xFFFF) | (std::min<uint32_t>(hm, 0xFFFF) << 16);
+    if (own_multi[i] >= 0xFFFF || hm >= 0xFFFF) d.sh_cnt_flags |= (uint32_t)kFlagMultiSat << 24;
   }
 
   // 3. literal edges -> open-addressed table of 128-B buckets, linear probing
-  //    at load factor edge_load (default 0.5; env MQM_EDGE_LOAD in (0, 0.9])
-  double load = 0.26;
+  //    at load factor `load` (default 0.2; env MQM_EDGE_LOAD in (0, 0.9]): a probe
+  //    chain that leaves its 128-B bucket costs another dependent HBM round
+  //    trip, and a wavefront waits for its longest chain (measured on C3:
+  //    k_walk 9.5 / 10.9 / 16.5 / 71 ms at load 0.15 / 0.26 / 0.5 / 0.8)
+  double load = 0.2;
   if (const char *e = getenv("MQM_EDGE_LOAD")) {
     const double v = atof(e);
     if (v > 0.0 && v <= 0.9) load = v;

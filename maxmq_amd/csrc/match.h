@@ -62,7 +62,7 @@ struct MatchOutput {
   const uint32_t *shared_counts = nullptr;
   const uint32_t *shared = nullptr;
   uint32_t n_fallback = 0;  // topics on the unbounded DFS path
-  uint32_t n_big = 0;       // topics deduplicated by the workgroup tier
+  uint32_t n_big = 0;       // topics whose multi entries the workgroup tier merged
 };
 
 // Runs walk -> scan -> dedupe (small / big / DFS) on `st`; returns 0 or a

@@ -17,16 +17,17 @@
 //                   entries) and H (shared candidates) are counted.
 //   scan      S and H -> each topic's segment start (S is the upper bound of
 //             its deliveries, so every later kernel writes final positions).
-//   k_small   a wavefront per topic with <= kSMax raw entries: per-wave LDS
-//             hash table keyed by client; atomicOr folds QoS (one-hot) and
-//             NoLocal, atomicMin keeps the lowest hit rank; an entry is its
-//             client's winner iff its hit has that rank — exactly
-//             Subscription.Merge (packets.go:250-270) with the first-merged
-//             subscription's fields.  Winners are compacted with ballot.
-//             Also writes every topic's shared candidates.
-//   k_big     a 256-thread workgroup per topic with <= kBigMax raw entries:
-//             the same dedupe in a 48 KiB LDS table shared by 4 waves, the
-//             entries held in registers between the two passes.
+//   k_emit    a wavefront per topic: solo entries (kMetaMulti clear, ~90%)
+//             are copied to their final positions (delivery q = solo entry
+//             q); the multi entries are merged in a per-wave LDS hash table
+//             keyed by client — atomicOr folds QoS (one-hot) and NoLocal,
+//             atomicMin keeps the lowest hit rank, an entry is its client's
+//             winner iff its hit has that rank: exactly Subscription.Merge
+//             (packets.go:250-270) with the first-merged subscription's
+//             fields — and the winners compacted with ballot after the solo
+//             part.  Also writes every topic's shared candidates.
+//   k_multi   a 256-thread workgroup per topic with more multi entries than
+//             a wave's table holds (<= kBigMax): the same merge in LDS.
 //   k_dfs<P>  the unbounded path for topics past a capacity (frontier, hits,
 //             cached levels, shared hits, raw entries): wave-cooperative DFS
 //             with an LDS stack and a global-memory dedupe table, writing to
@@ -54,33 +55,36 @@ constexpr int kHCap = 48;                // non-shared hits per topic (3 per lan
 constexpr int kShCap = 16;               // shared hits per topic
 constexpr int kStage = 64;               // topic bytes staged in LDS (4 per lane, one round trip)
 // record, written while walking (hits in discovery order; rank orders them):
-//   [0] nh | nsh << 8, [1] S,
-//   [2 + 3h] off, [3 + 3h] pre, [4 + 3h] rank of hit h (h < nh): its entries
-//            are subs[off .. off + cnt) and raw entries pre .. pre + cnt - 1
+//   [0] nh | nsh << 8, [1] Ssolo, [2] M, [3] unused
+//   [4 + 4h] off, [5 + 4h] spre, [6 + 4h] mpre, [7 + 4h] rank of hit h (h < nh):
+//            its range subs[off ..) holds solo entries, then multi ones
+//            (snapshot.h); spre / mpre = solo / multi entries of hits < h
 //   [kRecSh + 2i] off, [kRecSh + 1 + 2i] cnt of shared hit i (i < nsh)
-// One 64-lane load fetches the header and the first 20 hits.
-constexpr int kRecSh = 2 + 3 * kHCap;                // 146
-constexpr int kRecStride = kRecSh + 2 * kShCap;       // 178 words (max)
-constexpr int kRecStrideAlloc = 180;                  // 16-B aligned per topic
-constexpr int kSMax = 384;               // raw entries per k_small topic
-constexpr int kSmallPer = kSMax / kWave; // entries per lane
-constexpr int kSmallSlots = 256;         // k_small merge table slots (per wave)
+// One 64-lane load fetches the header and the first 15 hits.
+constexpr int kRecHit = 4;
+constexpr int kRecSh = 4 + kRecHit * kHCap;          // 196
+constexpr int kRecStride = kRecSh + 2 * kShCap;       // 228 words (max)
+constexpr int kRecStrideAlloc = 228;                  // 16-B aligned per topic
+constexpr uint32_t kSMax = 16384;        // raw entries per topic on the bounded path
+constexpr int kEmitU = 4;                // solo entries in flight per lane
+constexpr int kEmitWaves = 4;
+constexpr int kSmallSlots = 256;         // k_emit merge table slots (per wave)
 constexpr int kSmallMulti = 192;         // multi entries it holds (load <= 0.75)
-constexpr int kSmallWaves = 4;
+constexpr int kSmallPer = kSmallMulti / 64;
 constexpr int kBigThreads = 256;
-constexpr int kBigSlotsA = 2048;         // k_big first tier: 24 KiB table
+constexpr int kBigSlotsA = 2048;         // k_multi first tier: 24 KiB table
 constexpr int kBigSlotsB = 4096;         // overflow tier: 48 KiB, holds any bounded topic
-constexpr int kBigMax = 3072;            // raw entries per k_big topic
+constexpr int kBigMax = 3072;            // multi entries per bounded topic
 constexpr int kBigPer = kBigMax / kBigThreads;
 constexpr uint32_t kNoWhy = 0xFFFFFFFFu;
 constexpr uint32_t kNoLit = 0x80000000u;   // frontier node id flag: no literal child (node ids < 2^31)
 
 static_assert(kRecStrideAlloc % 4 == 0 && kRecStrideAlloc >= kRecStride, "16-B aligned records");
-static_assert(kSmallMulti * 4 <= kSmallSlots * 3, "k_small table load factor");
+static_assert(kSmallMulti * 4 <= kSmallSlots * 3, "k_emit table load factor");
 static_assert(kBigMax * 4 <= kBigSlotsB * 3, "the overflow tier holds every bounded topic");
-static_assert(kSMax % kWave == 0 && kBigMax % kBigThreads == 0, "register tiles");
+static_assert(kSmallMulti % kWave == 0 && kBigMax % kBigThreads == 0, "register tiles");
 
-enum : uint8_t { kClsDone = 0, kClsSmall = 1, kClsBig = 2, kClsDfs = 3 };
+enum : uint8_t { kClsDone = 0, kClsBounded = 1, kClsDfs = 3 };
 enum : uint32_t { kWhyFrontier = 0, kWhyHits = 1, kWhyLevels = 2, kWhyShared = 3, kWhyEntries = 4 };
 
 struct Counters {              // zeroed before every batch
@@ -88,7 +92,8 @@ struct Counters {              // zeroed before every batch
   unsigned long long htail;    // DFS shared candidates: likewise
   unsigned int n_dfs;          // topics appended to the DFS list
   unsigned int why[5];         // DFS routing reasons (kWhy*)
-  unsigned int n_ovf;          // topics k_big<kBigSlotsA> passed to the 4096-slot tier
+  unsigned int n_multi;        // topics whose multi entries k_emit passed to k_multi
+  unsigned int n_ovf;          // topics k_multi<kBigSlotsA> passed to the 4096-slot tier
 };
 
 struct Outputs {
@@ -96,7 +101,7 @@ struct Outputs {
   uint64_t *dstart, *hstart;  // n + 1 (exclusive scans; DFS topics overwritten)
   uint8_t *cls;
   uint32_t *dfs_list;
-  uint32_t *big_list, *n_big;
+  uint32_t *multi_list;       // topics for k_multi (Counters::n_multi)
   uint32_t *recs;  // kRecStrideAlloc words per topic
   Counters *ctr;
   uint64_t *dout;
@@ -132,13 +137,20 @@ __device__ __forceinline__ uint64_t pack_delivery(uint32_t client, uint32_t sid,
 // QoS one-hot (bits 0..2) | NoLocal (bit 3): OR-merged, max QoS = top set bit
 __device__ __forceinline__ uint32_t qos_bits(uint32_t meta) { return (1u << (meta & 3)) | (((meta >> 2) & 1) << 3); }
 
-// hit h with pre(h) <= r < pre(h+1), pre(h) = rec[3 + 3h] (strictly
-// increasing in h: empty hits are never recorded)
-__device__ __forceinline__ uint32_t find_hit(const uint32_t *rec, uint32_t nh, uint32_t r) {
+// the hit h holding entry x of a prefix field (kFieldSpre / kFieldMpre): the
+// largest h with field(h) <= x.  Hits with none of those entries tie with
+// their successor, so the largest such h is the one that holds x.
+enum : int { kFieldOff = 0, kFieldSpre = 1, kFieldMpre = 2, kFieldRank = 3 };
+template <int kField>
+__device__ __forceinline__ uint32_t find_hit(const uint32_t *rec, uint32_t nh, uint32_t x) {
   uint32_t h = 0;
   for (uint32_t step = 32; step > 0; step >>= 1)
-    if (h + step < nh && rec[3 + 3 * (h + step)] <= r) h += step;
+    if (h + step < nh && rec[4 + kRecHit * (h + step) + kField] <= x) h += step;
   return h;
+}
+
+__device__ __forceinline__ uint32_t rec_at(const uint32_t *rec, uint32_t h, int field) {
+  return rec[4 + kRecHit * h + field];
 }
 
 // per-topic merge table in LDS (linear probing, key = client + 1):
@@ -268,7 +280,7 @@ __global__ __launch_bounds__(kWave * kWalkWaves, 5) void k_walk(DeviceSnapshot s
 
     // ---- 2. walk ----------------------------------------------------------
     uint32_t *rec = o.recs + (uint64_t)(active ? t : 0) * kRecStrideAlloc;
-    uint32_t nf = nlev > 0 ? 1 : 0, nh = 0, nsh = 0, S = 0, H = 0;
+    uint32_t nf = nlev > 0 ? 1 : 0, nh = 0, nsh = 0, Ss = 0, Ms = 0, H = 0;
     int cur = 0;
     for (uint32_t d = 0; d < nlev && nf > 0; d++) {
       if (d >= (uint32_t)kLMax) {
@@ -316,21 +328,28 @@ __global__ __launch_bounds__(kWave * kWalkWaves, 5) void k_walk(DeviceSnapshot s
         if (nh + n_own + n_par > (uint32_t)kHCap) why = kWhyHits;
         if (nsh + __popc(m_sh) > (uint32_t)kShCap) why = kWhyShared;
         if (nnext + __popc(m_push) > (uint32_t)kFCap) why = kWhyFrontier;
+        if ((uint32_t)(__ballot((c_own | c_par) && (fl & kFlagMultiSat)) >> gbase) & kGMask) why = kWhyEntries;
         if (why != kNoWhy) break;
-        uint32_t t_own, t_par;
-        const uint32_t x_own = group_scan_ex<kG>(c_own, gl, &t_own, gbase);
-        const uint32_t x_par = group_scan_ex<kG>(c_par, gl, &t_par, gbase);
+        // solo / multi split of the two ranges (multi entries sit at the end)
+        const uint32_t mu_own = c_own ? (dc.multi & 0xFFFFu) : 0, mu_par = c_par ? (dc.multi >> 16) : 0;
+        uint32_t ts_own, ts_par, tm_own, tm_par;
+        const uint32_t xs_own = group_scan_ex<kG>(c_own - mu_own, gl, &ts_own, gbase);
+        const uint32_t xs_par = group_scan_ex<kG>(c_par - mu_par, gl, &ts_par, gbase);
+        const uint32_t xm_own = group_scan_ex<kG>(mu_own, gl, &tm_own, gbase);
+        const uint32_t xm_par = group_scan_ex<kG>(mu_par, gl, &tm_par, gbase);
         if (active && c_own) {
-          const uint32_t i = nh + __popc(m_own & gmask_lt);
-          rec[2 + 3 * i] = dc.sub_off;
-          rec[3 + 3 * i] = S + x_own;
-          rec[4 + 3 * i] = 2 * c;
+          uint32_t *hr = rec + 4 + kRecHit * (nh + __popc(m_own & gmask_lt));
+          hr[kFieldOff] = dc.sub_off;
+          hr[kFieldSpre] = Ss + xs_own;
+          hr[kFieldMpre] = Ms + xm_own;
+          hr[kFieldRank] = 2 * c;
         }
         if (active && c_par) {
-          const uint32_t i = nh + n_own + __popc(m_par & gmask_lt);
-          rec[2 + 3 * i] = dc.hsub_off;
-          rec[3 + 3 * i] = S + t_own + x_par;
-          rec[4 + 3 * i] = 2 * c + 1;
+          uint32_t *hr = rec + 4 + kRecHit * (nh + n_own + __popc(m_par & gmask_lt));
+          hr[kFieldOff] = dc.sub_off + dc.sub_cnt;  // the '#' child's range follows (snapshot.h)
+          hr[kFieldSpre] = Ss + ts_own + xs_par;
+          hr[kFieldMpre] = Ms + tm_own + xm_par;
+          hr[kFieldRank] = 2 * c + 1;
         }
         if (active && c_sh) {
           const uint32_t i = nsh + __popc(m_sh & gmask_lt);
@@ -348,7 +367,8 @@ __global__ __launch_bounds__(kWave * kWalkWaves, 5) void k_walk(DeviceSnapshot s
         nh += n_own + n_par;
         nsh += __popc(m_sh);
         nnext += __popc(m_push);
-        S += t_own + t_par;
+        Ss += ts_own + ts_par;
+        Ms += tm_own + tm_par;
         H += t_sh;
       }
       wave_lds_sync();
@@ -356,14 +376,16 @@ __global__ __launch_bounds__(kWave * kWalkWaves, 5) void k_walk(DeviceSnapshot s
       cur ^= 1;
       nf = nnext;
     }
-    if (why == kNoWhy && S > (uint32_t)kBigMax) why = kWhyEntries;
+    const uint32_t S = Ss + Ms;
+    if (why == kNoWhy && (S > kSMax || Ms > (uint32_t)kBigMax)) why = kWhyEntries;
     if (active && gl == 0) {
       const bool dfs = why != kNoWhy;
       if (!dfs) {
         rec[0] = nh | (nsh << 8);
-        rec[1] = S;
+        rec[1] = Ss;
+        rec[2] = Ms;
       }
-      o.cls[t] = dfs ? kClsDfs : S == 0 ? kClsDone : S <= (uint32_t)kSMax ? kClsSmall : kClsBig;
+      o.cls[t] = dfs ? kClsDfs : S == 0 ? kClsDone : kClsBounded;
       o.scount[t] = dfs ? 0 : S;
       o.hcount[t] = dfs ? 0 : H;
       o.dcount[t] = 0;
@@ -377,27 +399,42 @@ __global__ __launch_bounds__(kWave * kWalkWaves, 5) void k_walk(DeviceSnapshot s
 }
 
 // ---------------------------------------------------------------------------
-// k_small: a wavefront per topic with <= kSMax raw entries; also writes every
-// bounded topic's shared candidates.  The next topic's header (class, counts,
-// segment starts, the first 64 record words) is in flight while the current
-// one is processed, so a topic costs about one dependent round trip (its
-// subscription loads).  Topics whose entries are all solo (kMetaMulti clear)
-// are copied; the others merge their multi entries in a per-wave LDS table,
-// and topics with more multi entries than it holds move up to k_big.
+// k_emit: a wavefront per bounded topic.  The next topic's header (class,
+// counts, segment starts, the first 64 record words) is in flight while the
+// current one is processed.
+//   solo entries (kMetaMulti clear) are their clients' merged deliveries:
+//     entry q of the topic's solo sequence goes to out[db + q] — no table, no
+//     compaction, kEmitU entries per lane in flight;
+//   multi entries (at most kSmallMulti) are merged in a per-wave LDS table
+//     keyed by client: atomicOr folds QoS (one-hot) and NoLocal, atomicMin
+//     keeps the lowest hit rank, an entry is its client's winner iff its hit
+//     has that rank — Subscription.Merge (packets.go:250-270) with the
+//     first-merged subscription's fields — and winners are compacted with a
+//     ballot after the solo part.  More multi entries go to k_multi.
+// Also writes every bounded topic's shared candidates.
 // ---------------------------------------------------------------------------
-struct SmallLds {
+struct EmitLds {
   uint32_t rec[kRecStrideAlloc];
   uint32_t tkey[kSmallSlots];
   uint32_t tbits[kSmallSlots];
   uint32_t tmin[kSmallSlots];
 };
 
-__global__ __launch_bounds__(kWave *kSmallWaves) void k_small(DeviceSnapshot s, uint32_t n, Outputs o) {
-  __shared__ SmallLds lds_all[kSmallWaves];
+// multi entry q of a topic: subs index and hit
+__device__ __forceinline__ uint32_t multi_sid(const uint32_t *rec, uint32_t nh, uint32_t Ss, uint32_t q,
+                                              uint32_t *hit) {
+  const uint32_t h = find_hit<kFieldMpre>(rec, nh, q);
+  const uint32_t solo_h = (h + 1 < nh ? rec_at(rec, h + 1, kFieldSpre) : Ss) - rec_at(rec, h, kFieldSpre);
+  *hit = h;
+  return rec_at(rec, h, kFieldOff) + solo_h + (q - rec_at(rec, h, kFieldMpre));
+}
+
+__global__ __launch_bounds__(kWave *kEmitWaves) void k_emit(DeviceSnapshot s, uint32_t n, Outputs o) {
+  __shared__ EmitLds lds_all[kEmitWaves];
   const int lane = threadIdx.x & (kWave - 1);
-  SmallLds &L = lds_all[threadIdx.x / kWave];
-  const uint32_t nwaves = gridDim.x * kSmallWaves;
-  uint32_t t = blockIdx.x * kSmallWaves + threadIdx.x / kWave;
+  EmitLds &L = lds_all[threadIdx.x / kWave];
+  const uint32_t nwaves = gridDim.x * kEmitWaves;
+  uint32_t t = blockIdx.x * kEmitWaves + threadIdx.x / kWave;
   uint32_t n_cls = kClsDone, n_H = 0, n_rw = 0;
   uint64_t n_db = 0, n_hb = 0;
   auto fetch = [&](uint32_t u) {
@@ -412,12 +449,12 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(DeviceSnapshot s, 
     const uint32_t cls = n_cls, H = n_H, rw = n_rw;
     const uint64_t db = n_db, hb = n_hb;
     if (t + nwaves < n) fetch(t + nwaves);
-    if (cls == kClsDfs || (cls != kClsSmall && H == 0)) continue;
-    const uint32_t w0 = __shfl(rw, 0, 64), S = __shfl(rw, 1, 64);
+    if (cls == kClsDfs || (cls == kClsDone && H == 0)) continue;
+    const uint32_t w0 = __shfl(rw, 0, 64), Ss = __shfl(rw, 1, 64), M = __shfl(rw, 2, 64);
     const uint32_t nh = w0 & 0xFFu, nsh = w0 >> 8;
     const uint32_t *grec = o.recs + (uint64_t)t * kRecStrideAlloc;
     L.rec[lane] = rw;
-    for (uint32_t i = kWave + lane; i < 2 + 3 * nh; i += kWave) L.rec[i] = grec[i];
+    for (uint32_t i = kWave + lane; i < 4 + kRecHit * nh; i += kWave) L.rec[i] = grec[i];
     wave_lds_sync();
     if (H) {  // shared candidates (gatherSharedSubscriptions, topics.go:541-555)
       uint32_t w = 0;
@@ -427,40 +464,33 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(DeviceSnapshot s, 
         w += sc;
       }
     }
-    if (cls != kClsSmall) {
+    // solo entries: delivery q of the topic is solo entry q
+    for (uint32_t base = 0; base < Ss; base += kWave * kEmitU) {
+      uint32_t cl[kEmitU], sid[kEmitU], meta[kEmitU];
+#pragma unroll
+      for (int u = 0; u < kEmitU; u++) {
+        const uint32_t q = base + u * kWave + lane;
+        if (q < Ss) {
+          const uint32_t h = find_hit<kFieldSpre>(L.rec, nh, q);
+          sid[u] = rec_at(L.rec, h, kFieldOff) + (q - rec_at(L.rec, h, kFieldSpre));
+          const SubEnt e = s.subs[sid[u]];
+          cl[u] = e.client;
+          meta[u] = e.meta;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kEmitU; u++) {
+        const uint32_t q = base + u * kWave + lane;
+        if (q < Ss) o.dout[db + q] = pack_delivery(cl[u], sid[u], meta[u] & 3u, (meta[u] >> 2) & 1u);
+      }
+    }
+    uint32_t D = Ss;
+    if (M > (uint32_t)kSmallMulti) {  // the workgroup tier merges them (and writes dcount)
+      if (lane == 0) o.multi_list[atomicAdd(&o.ctr->n_multi, 1u)] = t;
       wave_lds_sync();
       continue;
     }
-    uint32_t cl[kSmallPer], sid[kSmallPer], hh[kSmallPer], meta[kSmallPer];
-    // all subscription loads first (independent, in flight together)
-#pragma unroll
-    for (int k = 0; k < kSmallPer; k++) {
-      const uint32_t r = lane + k * kWave;
-      meta[k] = 0;
-      if (r < S) {
-        hh[k] = find_hit(L.rec, nh, r);
-        sid[k] = L.rec[2 + 3 * hh[k]] + (r - L.rec[3 + 3 * hh[k]]);
-        const SubEnt e = s.subs[sid[k]];
-        cl[k] = e.client;
-        meta[k] = e.meta;
-      }
-    }
-    uint32_t M = 0;  // entries that need the merge table (kMetaMulti)
-#pragma unroll
-    for (int k = 0; k < kSmallPer; k++) M += __popcll(__ballot(meta[k] & kMetaMulti));
-    uint32_t D = 0;
-    if (M == 0) {  // every entry is its client's merged delivery: a straight copy
-#pragma unroll
-      for (int k = 0; k < kSmallPer; k++) {
-        const uint32_t r = lane + k * kWave;
-        if (r < S) o.dout[db + r] = pack_delivery(cl[k], sid[k], meta[k] & 3u, (meta[k] >> 2) & 1u);
-      }
-      D = S;
-    } else if (M > (uint32_t)kSmallMulti) {  // the workgroup tier takes it (k_big list is built after this kernel)
-      if (lane == 0) o.cls[t] = kClsBig;
-      wave_lds_sync();
-      continue;
-    } else {
+    if (M > 0) {
       uint32_t lg = 6;
       while ((1u << lg) < 2 * M && (1u << lg) < (uint32_t)kSmallSlots) lg++;
       const uint32_t mask = (1u << lg) - 1;
@@ -469,24 +499,32 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(DeviceSnapshot s, 
         L.tbits[i] = 0;
         L.tmin[i] = 0xFFFFFFFFu;
       }
+      uint32_t cl[kSmallPer], sid[kSmallPer], rk[kSmallPer], meta[kSmallPer];
+#pragma unroll
+      for (int k = 0; k < kSmallPer; k++) {
+        const uint32_t q = lane + k * kWave;
+        if (q < M) {
+          uint32_t h;
+          sid[k] = multi_sid(L.rec, nh, Ss, q, &h);
+          rk[k] = rec_at(L.rec, h, kFieldRank);
+          const SubEnt e = s.subs[sid[k]];
+          cl[k] = e.client;
+          meta[k] = e.meta;
+        }
+      }
       wave_lds_sync();
 #pragma unroll
       for (int k = 0; k < kSmallPer; k++)
-        if (meta[k] & kMetaMulti) table_insert(L.tkey, L.tbits, L.tmin, mask, lg, cl[k], meta[k], L.rec[4 + 3 * hh[k]]);
+        if (lane + k * kWave < M) table_insert(L.tkey, L.tbits, L.tmin, mask, lg, cl[k], meta[k], rk[k]);
       wave_lds_sync();
 #pragma unroll
       for (int k = 0; k < kSmallPer; k++) {
-        const uint32_t r = lane + k * kWave;
         bool win = false;
         uint64_t ent = 0;
-        if (r < S) {
-          uint32_t v = qos_bits(meta[k]);
-          win = true;
-          if (meta[k] & kMetaMulti) {
-            const uint32_t sl = table_find(L.tkey, mask, lg, cl[k]);
-            win = L.tmin[sl] == L.rec[4 + 3 * hh[k]];
-            v = L.tbits[sl];
-          }
+        if (lane + k * kWave < M) {
+          const uint32_t sl = table_find(L.tkey, mask, lg, cl[k]);
+          win = L.tmin[sl] == rk[k];
+          const uint32_t v = L.tbits[sl];
           ent = pack_delivery(cl[k], sid[k], 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
         }
         const uint64_t m = __ballot(win);
@@ -500,16 +538,17 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(DeviceSnapshot s, 
 }
 
 // ---------------------------------------------------------------------------
-// k_big<kSlots>: a 256-thread workgroup per listed topic (<= kBigMax raw
-// entries), LDS merge table of kSlots slots.  Topic ids are prefetched two
-// topics ahead and the record / segment start one topic ahead.  Topics with
+// k_multi<kSlots>: a 256-thread workgroup per listed topic merges its multi
+// entries (<= kBigMax) in an LDS table of kSlots slots and writes the winners
+// after the topic's solo deliveries (k_emit wrote those).  Topic ids are
+// prefetched two topics ahead and the record one topic ahead.  Topics with
 // more multi entries than the table holds go to `ovf` (the 4096-slot tier,
 // which holds any bounded topic).
 // ---------------------------------------------------------------------------
 template <int kSlots>
-__global__ __launch_bounds__(kBigThreads) void k_big(DeviceSnapshot s, Outputs o, const uint32_t *__restrict__ list,
-                                                    const uint32_t *__restrict__ count, uint32_t *__restrict__ ovf,
-                                                    unsigned int *__restrict__ n_ovf) {
+__global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs o, const uint32_t *__restrict__ list,
+                                                      const unsigned int *__restrict__ count,
+                                                      uint32_t *__restrict__ ovf, unsigned int *__restrict__ n_ovf) {
   __shared__ uint32_t tkey[kSlots], tbits[kSlots], tmin[kSlots];
   __shared__ uint32_t rec[kRecStrideAlloc];
   __shared__ uint32_t wsum[kBigThreads / kWave];
@@ -537,42 +576,11 @@ __global__ __launch_bounds__(kBigThreads) void k_big(DeviceSnapshot s, Outputs o
     t_cur = t_nxt;
     t_nxt = t_nn;
     __syncthreads();
-    const uint32_t nh = rec[0] & 0xFFu, S = rec[1];
-    if (2 + 3 * nh > (uint32_t)kWave) {  // block-uniform
-      for (uint32_t i = kWave + tid; i < 2 + 3 * nh; i += kBigThreads)
+    const uint32_t nh = rec[0] & 0xFFu, Ss = rec[1], M = rec[2];
+    if (4 + kRecHit * nh > (uint32_t)kWave) {  // block-uniform
+      for (uint32_t i = kWave + tid; i < 4 + kRecHit * nh; i += kBigThreads)
         rec[i] = o.recs[(uint64_t)t * kRecStrideAlloc + i];
       __syncthreads();
-    }
-    uint32_t cl[kBigPer], sid[kBigPer], hh[kBigPer], meta[kBigPer];
-    // all subscription loads first (independent, in flight together)
-#pragma unroll
-    for (int k = 0; k < kBigPer; k++) {
-      const uint32_t r = tid + k * kBigThreads;
-      meta[k] = 0;
-      if (r < S) {
-        hh[k] = find_hit(rec, nh, r);
-        sid[k] = rec[2 + 3 * hh[k]] + (r - rec[3 + 3 * hh[k]]);
-        const SubEnt e = s.subs[sid[k]];
-        cl[k] = e.client;
-        meta[k] = e.meta;
-      }
-    }
-    uint32_t mw = 0;  // entries that need the merge table (kMetaMulti)
-#pragma unroll
-    for (int k = 0; k < kBigPer; k++) mw += __popcll(__ballot(meta[k] & kMetaMulti));
-    if (lane == 0) wsum[wid] = mw;
-    __syncthreads();
-    uint32_t M = 0;
-    for (int w = 0; w < kBigThreads / kWave; w++) M += wsum[w];
-    if (M == 0) {  // every entry is its client's merged delivery: a straight copy
-#pragma unroll
-      for (int k = 0; k < kBigPer; k++) {
-        const uint32_t r = tid + k * kBigThreads;
-        if (r < S) o.dout[db + r] = pack_delivery(cl[k], sid[k], meta[k] & 3u, (meta[k] >> 2) & 1u);
-      }
-      if (tid == 0) o.dcount[t] = S;
-      __syncthreads();
-      continue;
     }
     if (M > kMCap) {  // block-uniform; unreachable for the tier that holds kBigMax
       if (tid == 0) ovf[atomicAdd(n_ovf, 1u)] = t;
@@ -587,26 +595,35 @@ __global__ __launch_bounds__(kBigThreads) void k_big(DeviceSnapshot s, Outputs o
       tbits[i] = 0;
       tmin[i] = 0xFFFFFFFFu;
     }
+    uint32_t cl[kBigPer], sid[kBigPer], rk[kBigPer], meta[kBigPer];
+#pragma unroll
+    for (int k = 0; k < kBigPer; k++) {
+      const uint32_t q = tid + k * kBigThreads;
+      if (q < M) {
+        uint32_t h;
+        sid[k] = multi_sid(rec, nh, Ss, q, &h);
+        rk[k] = rec_at(rec, h, kFieldRank);
+        const SubEnt e = s.subs[sid[k]];
+        cl[k] = e.client;
+        meta[k] = e.meta;
+      }
+    }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < kBigPer; k++)
-      if (meta[k] & kMetaMulti) table_insert(tkey, tbits, tmin, mask, lg, cl[k], meta[k], rec[4 + 3 * hh[k]]);
+      if (tid + k * kBigThreads < M) table_insert(tkey, tbits, tmin, mask, lg, cl[k], meta[k], rk[k]);
     __syncthreads();
-    uint32_t D = 0;
+    uint32_t D = Ss;
 #pragma unroll
     for (int k = 0; k < kBigPer; k++) {
-      if ((uint32_t)(k * kBigThreads) >= S) break;  // block-uniform
-      const uint32_t r = tid + k * kBigThreads;
+      if ((uint32_t)(k * kBigThreads) >= M) break;  // block-uniform
+      const uint32_t q = tid + k * kBigThreads;
       bool win = false;
       uint64_t ent = 0;
-      if (r < S) {
-        uint32_t v = qos_bits(meta[k]);
-        win = true;
-        if (meta[k] & kMetaMulti) {
-          const uint32_t sl = table_find(tkey, mask, lg, cl[k]);
-          win = tmin[sl] == rec[4 + 3 * hh[k]];
-          v = tbits[sl];
-        }
+      if (q < M) {
+        const uint32_t sl = table_find(tkey, mask, lg, cl[k]);
+        win = tmin[sl] == rk[k];
+        const uint32_t v = tbits[sl];
         ent = pack_delivery(cl[k], sid[k], 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
       }
       const uint64_t m = __ballot(win);
@@ -626,10 +643,6 @@ __global__ __launch_bounds__(kBigThreads) void k_big(DeviceSnapshot s, Outputs o
   }
 }
 
-struct IsBig {
-  const uint8_t *cls;
-  __host__ __device__ bool operator()(uint32_t t) const { return cls[t] == kClsBig; }
-};
 
 // ---------------------------------------------------------------------------
 // k_dfs<P>: the unbounded path.  P0 counts raw entries / shared candidates;
@@ -776,7 +789,7 @@ __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *
         e.hash = __shfl(dc.hash, src, 64);
         e.sub_off = __shfl(dc.sub_off, src, 64);
         e.sub_cnt = __shfl(dc.sub_cnt, src, 64);
-        e.hsub_off = __shfl(dc.hsub_off, src, 64);
+        e.multi = __shfl(dc.multi, src, 64);
         e.hsub_cnt = __shfl(dc.hsub_cnt, src, 64);
         e.sh_off = __shfl(dc.sh_off, src, 64);
         e.sh_cnt_flags = __shfl(dc.sh_cnt_flags, src, 64);
@@ -784,7 +797,7 @@ __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *
         const bool skip_dollar = dollar && (fl & kFlagDollarWild);
         for (int part = 0; part < 2; part++) {
           if (part == 1 && src != 0) break;
-          const uint32_t roff = part ? e.hsub_off : e.sub_off;
+          const uint32_t roff = part ? e.sub_off + e.sub_cnt : e.sub_off;  // '#' child's range follows
           const uint32_t rcnt = skip_dollar ? 0 : (part ? e.hsub_cnt : e.sub_cnt);
           const uint32_t rank = 2 * cc + part;
           S += rcnt;
@@ -1043,32 +1056,26 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   // outputs: scanned segments, then the DFS tails
   if (ws.get(W::kDOut, sizeof(uint64_t) * (s_total + dfs_raw + 1)) ||
       ws.get(W::kHOut, sizeof(uint32_t) * (h_total + dfs_h + 1)) ||
-      ws.get(W::kDense, sizeof(uint32_t) * (n + 1)))  // big list
+      ws.get(W::kDense, sizeof(uint32_t) * (n + 1)))  // multi list
     return -2;
   o.dout = (uint64_t *)ws.ptr(W::kDOut);
   o.hout = (uint32_t *)ws.ptr(W::kHOut);
-  o.big_list = (uint32_t *)ws.ptr(W::kDense);
-  o.n_big = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(o.ctr) + 128);
+  o.multi_list = (uint32_t *)ws.ptr(W::kDense);
 
   mark(ws, 2, st);
-  static_assert(kWave * kSmallWaves == kBigThreads, "resident_blocks assumes 256-thread blocks");
-  const uint32_t small_blocks = std::max<uint32_t>(
-      1, std::min<uint32_t>((n + kSmallWaves - 1) / kSmallWaves, resident_blocks(ws, 2, k_small)));
-  if (n > 0) hipLaunchKernelGGL(k_small, dim3(small_blocks), dim3(kWave * kSmallWaves), 0, st, s, n, o);
-  HIP_TRY(hipGetLastError());
-  if (n > 0) {  // list the big topics (count stays on the device)
-    size_t tmp = 0;
-    hipcub::CountingInputIterator<uint32_t> it(0);
-    HIP_TRY(hipcub::DeviceSelect::If(nullptr, tmp, it, o.big_list, o.n_big, n, IsBig{o.cls}, st));
-    if (ws.get(W::kScanTmp, tmp)) return -2;
-    HIP_TRY(hipcub::DeviceSelect::If(ws.ptr(W::kScanTmp), tmp, it, o.big_list, o.n_big, n, IsBig{o.cls}, st));
+  static_assert(kWave * kEmitWaves == kBigThreads, "resident_blocks assumes 256-thread blocks");
+  const uint32_t emit_blocks = std::max<uint32_t>(
+      1, std::min<uint32_t>((n + kEmitWaves - 1) / kEmitWaves, resident_blocks(ws, 2, k_emit)));
+  if (n > 0) {
+    hipLaunchKernelGGL(k_emit, dim3(emit_blocks), dim3(kWave * kEmitWaves), 0, st, s, n, o);
+    HIP_TRY(hipGetLastError());
     if (ws.get(W::kOvfList, sizeof(uint32_t) * (n + 1))) return -2;
     auto *ovf = (uint32_t *)ws.ptr(W::kOvfList);
-    hipLaunchKernelGGL(k_big<kBigSlotsA>, dim3(resident_blocks(ws, 0, k_big<kBigSlotsA>)), dim3(kBigThreads), 0, st,
-                       s, o, o.big_list, o.n_big, ovf, &o.ctr->n_ovf);
+    hipLaunchKernelGGL(k_multi<kBigSlotsA>, dim3(resident_blocks(ws, 0, k_multi<kBigSlotsA>)), dim3(kBigThreads), 0,
+                       st, s, o, o.multi_list, &o.ctr->n_multi, ovf, &o.ctr->n_ovf);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_big<kBigSlotsB>, dim3(resident_blocks(ws, 1, k_big<kBigSlotsB>)), dim3(kBigThreads), 0, st,
-                       s, o, ovf, &o.ctr->n_ovf, nullptr, nullptr);
+    hipLaunchKernelGGL(k_multi<kBigSlotsB>, dim3(resident_blocks(ws, 1, k_multi<kBigSlotsB>)), dim3(kBigThreads), 0,
+                       st, s, o, ovf, &o.ctr->n_ovf, nullptr, nullptr);
     HIP_TRY(hipGetLastError());
   }
   if (n_dfs) {
@@ -1095,7 +1102,7 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
     HIP_TRY(hipcub::DeviceReduce::Sum(ws.ptr(W::kScanTmp), tmp, o.dcount, sums, n, st));
     HIP_TRY(hipcub::DeviceReduce::Sum(ws.ptr(W::kScanTmp), tmp, o.hcount, sums + 1, n, st));
     HIP_TRY(hipMemcpyAsync(hp, sums, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(hp + 2, o.n_big, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(hp + 2, &o.ctr->n_multi, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
   }
   if (ws.profile) {

@@ -17,8 +17,9 @@ namespace mqm {
 enum : uint32_t {
   kFlagHasChildren = 1u,  // any child (literal, '+', '#')
   kFlagDollarWild = 2u,   // node lies under a root child whose key starts with '+'/'#'
-  kFlagHasLiteral = 4u,   // some child is a literal (else the edge probe is skipped)
                           // == the `$` rule's Filter[0] test (topics.go:527)
+  kFlagHasLiteral = 4u,   // some child is a literal (else the edge probe is skipped)
+  kFlagMultiSat = 8u,     // a multi count in NodeDesc::multi saturated (topics -> DFS path)
 };
 
 struct NodeDesc {         // 32 B
@@ -26,8 +27,10 @@ struct NodeDesc {         // 32 B
   uint32_t hash;          // '#' child or kNone
   uint32_t sub_off;       // non-shared subscriptions [sub_off, sub_off + sub_cnt)
   uint32_t sub_cnt;
-  uint32_t hsub_off;      // copy of the '#' child's non-shared range (parent probe)
-  uint32_t hsub_cnt;
+  uint32_t multi;         // multi entries (kMetaMulti) of the own range (low 16 bits)
+                          //   and of the '#' child's range (high 16), saturating
+  uint32_t hsub_cnt;      // the '#' child's non-shared range (parent probe) is
+                          //   [sub_off + sub_cnt, + hsub_cnt): laid out right after
   uint32_t sh_off;        // shared subscriptions [sh_off, sh_off + sh_cnt)
   uint32_t sh_cnt_flags;  // sh_cnt (low 24 bits) | flags << 24
 };
@@ -47,7 +50,9 @@ static_assert(sizeof(EdgeEntry) == 64, "EdgeEntry layout");
 
 constexpr uint32_t kEdgesPerBucket = 2;
 
-// non-shared subscription entry; sid = index into the array
+// non-shared subscription entry; sid = index into the array.  A node's range
+// holds its solo entries first, then its multi entries (kMetaMulti), and the
+// range of a node's '#' child follows it directly.
 struct SubEnt {
   uint32_t client;
   uint32_t meta;          // qos[1:0] | no_local[2] | rap[3] | rh[5:4] | multi[6]
