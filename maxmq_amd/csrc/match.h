@@ -13,7 +13,7 @@ struct Workspace {
   enum Slot {
     kSCount, kHCount, kDCount, kDStart, kHStart, kCls, kDfsList, kRecs, kCounters, kDOut, kHOut,
     kDense, kDenseShared, kDenseOffs, kDenseHOffs, kScanTmp, kRawCnt, kTabOff, kTabSize, kTable,
-    kInBytes, kInOffs, kOvfList,
+    kInBytes, kInOffs, kOvfList, kOvfList2,
     // reverse match (retained.hip)
     kROffs, kRNLev, kRWild, kRLOff, kRFCount, kRFCur, kRLevels, kRNCount, kRNOff, kRItemF0, kRItemN0, kRItemF1,
     kRItemN1, kRChild, kRECount, kREOff, kREmit, kRPos, kRChunks, kRCOff, kROut, kRInBytes, kRInOffs, kNumSlots
@@ -26,7 +26,7 @@ struct Workspace {
   void *host_pinned = nullptr;
   uint32_t max_blocks = 2048;  // walk-kernel grid cap (grid-stride beyond)
   int walk_lanes = 8;          // lanes per topic in k_walk (4, 8 or 16; env MQM_WALK_LANES)
-  uint32_t resident[5] = {0, 0, 0, 0, 0};  // k_big tiers, k_small, k_walk<8>, k_walk<16>: resident blocks on the device
+  uint32_t resident[6] = {0, 0, 0, 0, 0, 0};  // k_multi tiers 1-2, k_emit, k_walk<8>, k_walk<16>, k_multi tier 3: resident blocks on the device
   // why the last batch's DFS topics left the bounded path:
   // frontier, hits, cached levels, shared hits, raw entries
   uint32_t why[5] = {0, 0, 0, 0, 0};

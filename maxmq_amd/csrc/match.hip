@@ -72,17 +72,14 @@ constexpr int kSmallSlots = 256;         // k_emit merge table slots (per wave)
 constexpr int kSmallMulti = 192;         // multi entries it holds (load <= 0.75)
 constexpr int kSmallPer = kSmallMulti / 64;
 constexpr int kBigThreads = 256;
-constexpr int kBigSlotsA = 2048;         // k_multi first tier: 24 KiB table
-constexpr int kBigSlotsB = 4096;         // overflow tier: 48 KiB, holds any bounded topic
-constexpr int kBigMax = 3072;            // multi entries per bounded topic
-constexpr int kBigPer = kBigMax / kBigThreads;
+constexpr int kBigMax = 3072;            // multi entries per bounded topic (k_multi's last tier)
 constexpr uint32_t kNoWhy = 0xFFFFFFFFu;
 constexpr uint32_t kNoLit = 0x80000000u;   // frontier node id flag: no literal child (node ids < 2^31)
 
 static_assert(kRecStrideAlloc % 4 == 0 && kRecStrideAlloc >= kRecStride, "16-B aligned records");
 static_assert(kSmallMulti * 4 <= kSmallSlots * 3, "k_emit table load factor");
-static_assert(kBigMax * 4 <= kBigSlotsB * 3, "the overflow tier holds every bounded topic");
-static_assert(kSmallMulti % kWave == 0 && kBigMax % kBigThreads == 0, "register tiles");
+static_assert(kBigMax * 4 <= 4096 * 3 && kBigMax <= 12 * kBigThreads, "the last k_multi tier holds every bounded topic");
+static_assert(kSmallMulti % kWave == 0, "register tiles");
 
 enum : uint8_t { kClsDone = 0, kClsBounded = 1, kClsDfs = 3 };
 enum : uint32_t { kWhyFrontier = 0, kWhyHits = 1, kWhyLevels = 2, kWhyShared = 3, kWhyEntries = 4 };
@@ -93,7 +90,8 @@ struct Counters {              // zeroed before every batch
   unsigned int n_dfs;          // topics appended to the DFS list
   unsigned int why[5];         // DFS routing reasons (kWhy*)
   unsigned int n_multi;        // topics whose multi entries k_emit passed to k_multi
-  unsigned int n_ovf;          // topics k_multi<kBigSlotsA> passed to the 4096-slot tier
+  unsigned int n_ovf;          // topics k_multi's first tier passed to the second
+  unsigned int n_ovf2;         // ... the second tier to the third
 };
 
 struct Outputs {
@@ -464,24 +462,52 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_emit(DeviceSnapshot s, ui
         w += sc;
       }
     }
+    // Loads before stores: a wait for a load also waits for every older
+    // store of the wave (one in-order vmcnt), so each chunk's loads are issued
+    // before the previous chunk's stores, and the multi entries' loads before
+    // any store of the topic.
+    const bool merge_here = M > 0 && M <= (uint32_t)kSmallMulti;
+    uint32_t mcl[kSmallPer], msid[kSmallPer], mrk[kSmallPer], mmeta[kSmallPer];
+    if (merge_here) {
+#pragma unroll
+      for (int k = 0; k < kSmallPer; k++) {
+        const uint32_t q = lane + k * kWave;
+        if (q < M) {
+          uint32_t h;
+          msid[k] = multi_sid(L.rec, nh, Ss, q, &h);
+          mrk[k] = rec_at(L.rec, h, kFieldRank);
+          const SubEnt e = s.subs[msid[k]];
+          mcl[k] = e.client;
+          mmeta[k] = e.meta;
+        }
+      }
+    }
     // solo entries: delivery q of the topic is solo entry q
-    for (uint32_t base = 0; base < Ss; base += kWave * kEmitU) {
-      uint32_t cl[kEmitU], sid[kEmitU], meta[kEmitU];
+    uint32_t cl[kEmitU], sid[kEmitU], meta[kEmitU];
+    auto load_solo = [&](uint32_t base, uint32_t *c_, uint32_t *s_, uint32_t *m_) {
 #pragma unroll
       for (int u = 0; u < kEmitU; u++) {
         const uint32_t q = base + u * kWave + lane;
         if (q < Ss) {
           const uint32_t h = find_hit<kFieldSpre>(L.rec, nh, q);
-          sid[u] = rec_at(L.rec, h, kFieldOff) + (q - rec_at(L.rec, h, kFieldSpre));
-          const SubEnt e = s.subs[sid[u]];
-          cl[u] = e.client;
-          meta[u] = e.meta;
+          s_[u] = rec_at(L.rec, h, kFieldOff) + (q - rec_at(L.rec, h, kFieldSpre));
+          const SubEnt e = s.subs[s_[u]];
+          c_[u] = e.client;
+          m_[u] = e.meta;
         }
       }
+    };
+    if (Ss) load_solo(0, cl, sid, meta);
+    for (uint32_t base = 0; base < Ss; base += kWave * kEmitU) {
+      uint32_t ncl[kEmitU], nsid[kEmitU], nmeta[kEmitU];
+      if (base + kWave * kEmitU < Ss) load_solo(base + kWave * kEmitU, ncl, nsid, nmeta);
 #pragma unroll
       for (int u = 0; u < kEmitU; u++) {
         const uint32_t q = base + u * kWave + lane;
         if (q < Ss) o.dout[db + q] = pack_delivery(cl[u], sid[u], meta[u] & 3u, (meta[u] >> 2) & 1u);
+        cl[u] = ncl[u];
+        sid[u] = nsid[u];
+        meta[u] = nmeta[u];
       }
     }
     uint32_t D = Ss;
@@ -490,7 +516,7 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_emit(DeviceSnapshot s, ui
       wave_lds_sync();
       continue;
     }
-    if (M > 0) {
+    if (merge_here) {
       uint32_t lg = 6;
       while ((1u << lg) < 2 * M && (1u << lg) < (uint32_t)kSmallSlots) lg++;
       const uint32_t mask = (1u << lg) - 1;
@@ -499,33 +525,20 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_emit(DeviceSnapshot s, ui
         L.tbits[i] = 0;
         L.tmin[i] = 0xFFFFFFFFu;
       }
-      uint32_t cl[kSmallPer], sid[kSmallPer], rk[kSmallPer], meta[kSmallPer];
-#pragma unroll
-      for (int k = 0; k < kSmallPer; k++) {
-        const uint32_t q = lane + k * kWave;
-        if (q < M) {
-          uint32_t h;
-          sid[k] = multi_sid(L.rec, nh, Ss, q, &h);
-          rk[k] = rec_at(L.rec, h, kFieldRank);
-          const SubEnt e = s.subs[sid[k]];
-          cl[k] = e.client;
-          meta[k] = e.meta;
-        }
-      }
       wave_lds_sync();
 #pragma unroll
       for (int k = 0; k < kSmallPer; k++)
-        if (lane + k * kWave < M) table_insert(L.tkey, L.tbits, L.tmin, mask, lg, cl[k], meta[k], rk[k]);
+        if (lane + k * kWave < M) table_insert(L.tkey, L.tbits, L.tmin, mask, lg, mcl[k], mmeta[k], mrk[k]);
       wave_lds_sync();
 #pragma unroll
       for (int k = 0; k < kSmallPer; k++) {
         bool win = false;
         uint64_t ent = 0;
         if (lane + k * kWave < M) {
-          const uint32_t sl = table_find(L.tkey, mask, lg, cl[k]);
-          win = L.tmin[sl] == rk[k];
+          const uint32_t sl = table_find(L.tkey, mask, lg, mcl[k]);
+          win = L.tmin[sl] == mrk[k];
           const uint32_t v = L.tbits[sl];
-          ent = pack_delivery(cl[k], sid[k], 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
+          ent = pack_delivery(mcl[k], msid[k], 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
         }
         const uint64_t m = __ballot(win);
         if (win) o.dout[db + D + __popcll(m & lanemask_lt(lane))] = ent;
@@ -538,21 +551,22 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_emit(DeviceSnapshot s, ui
 }
 
 // ---------------------------------------------------------------------------
-// k_multi<kSlots>: a 256-thread workgroup per listed topic merges its multi
-// entries (<= kBigMax) in an LDS table of kSlots slots and writes the winners
-// after the topic's solo deliveries (k_emit wrote those).  Topic ids are
-// prefetched two topics ahead and the record one topic ahead.  Topics with
-// more multi entries than the table holds go to `ovf` (the 4096-slot tier,
-// which holds any bounded topic).
+// k_multi<kSlots, kPer>: a 256-thread workgroup per listed topic merges its
+// multi entries (<= kPer per thread) in an LDS table of kSlots slots and writes
+// the winners after the topic's solo deliveries (k_emit wrote those).  Topic
+// ids are prefetched two topics ahead and the record one topic ahead.  Topics
+// with more multi entries than the tier holds go to `ovf`, the next tier
+// (tiers of 768 / 1536 / 3072 entries: small tiers keep more blocks resident;
+// the last holds every bounded topic).
 // ---------------------------------------------------------------------------
-template <int kSlots>
+template <int kSlots, int kPer>
 __global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs o, const uint32_t *__restrict__ list,
                                                       const unsigned int *__restrict__ count,
                                                       uint32_t *__restrict__ ovf, unsigned int *__restrict__ n_ovf) {
   __shared__ uint32_t tkey[kSlots], tbits[kSlots], tmin[kSlots];
   __shared__ uint32_t rec[kRecStrideAlloc];
   __shared__ uint32_t wsum[kBigThreads / kWave];
-  constexpr uint32_t kMCap = kSlots * 3 / 4;
+  constexpr uint32_t kMCap = kSlots * 3 / 4 < kPer * kBigThreads ? kSlots * 3 / 4 : kPer * kBigThreads;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
   const uint32_t nb = *count, G = gridDim.x;
   uint32_t bi = blockIdx.x;
@@ -595,9 +609,9 @@ __global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs
       tbits[i] = 0;
       tmin[i] = 0xFFFFFFFFu;
     }
-    uint32_t cl[kBigPer], sid[kBigPer], rk[kBigPer], meta[kBigPer];
+    uint32_t cl[kPer], sid[kPer], rk[kPer], meta[kPer];
 #pragma unroll
-    for (int k = 0; k < kBigPer; k++) {
+    for (int k = 0; k < kPer; k++) {
       const uint32_t q = tid + k * kBigThreads;
       if (q < M) {
         uint32_t h;
@@ -610,12 +624,12 @@ __global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < kBigPer; k++)
+    for (int k = 0; k < kPer; k++)
       if (tid + k * kBigThreads < M) table_insert(tkey, tbits, tmin, mask, lg, cl[k], meta[k], rk[k]);
     __syncthreads();
     uint32_t D = Ss;
 #pragma unroll
-    for (int k = 0; k < kBigPer; k++) {
+    for (int k = 0; k < kPer; k++) {
       if ((uint32_t)(k * kBigThreads) >= M) break;  // block-uniform
       const uint32_t q = tid + k * kBigThreads;
       bool win = false;
@@ -1071,11 +1085,16 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
     HIP_TRY(hipGetLastError());
     if (ws.get(W::kOvfList, sizeof(uint32_t) * (n + 1))) return -2;
     auto *ovf = (uint32_t *)ws.ptr(W::kOvfList);
-    hipLaunchKernelGGL(k_multi<kBigSlotsA>, dim3(resident_blocks(ws, 0, k_multi<kBigSlotsA>)), dim3(kBigThreads), 0,
-                       st, s, o, o.multi_list, &o.ctr->n_multi, ovf, &o.ctr->n_ovf);
+    if (ws.get(W::kOvfList2, sizeof(uint32_t) * (n + 1))) return -2;
+    auto *ovf2 = (uint32_t *)ws.ptr(W::kOvfList2);
+    hipLaunchKernelGGL((k_multi<1024, 3>), dim3(resident_blocks(ws, 0, k_multi<1024, 3>)), dim3(kBigThreads), 0, st, s,
+                       o, o.multi_list, &o.ctr->n_multi, ovf, &o.ctr->n_ovf);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_multi<kBigSlotsB>, dim3(resident_blocks(ws, 1, k_multi<kBigSlotsB>)), dim3(kBigThreads), 0,
-                       st, s, o, ovf, &o.ctr->n_ovf, nullptr, nullptr);
+    hipLaunchKernelGGL((k_multi<2048, 6>), dim3(resident_blocks(ws, 1, k_multi<2048, 6>)), dim3(kBigThreads), 0, st, s,
+                       o, ovf, &o.ctr->n_ovf, ovf2, &o.ctr->n_ovf2);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL((k_multi<4096, 12>), dim3(resident_blocks(ws, 5, k_multi<4096, 12>)), dim3(kBigThreads), 0,
+                       st, s, o, ovf2, &o.ctr->n_ovf2, nullptr, nullptr);
     HIP_TRY(hipGetLastError());
   }
   if (n_dfs) {
