@@ -56,4 +56,56 @@ __device__ inline uint32_t probe_edge(const DeviceSnapshot &s, uint32_t parent, 
   }
 }
 
+// One step of the level walk for one lane, with a single load group: either
+// the literal probe's home slot (64 B: key, header, the child's descriptor) or
+// a wildcard child's descriptor (the node array is padded so 64-B reads of its
+// last entry stay in bounds).  Both kinds issue the same loads unconditionally,
+// so the lanes of a wavefront have them in flight together; only a probe chain
+// that continues past its home slot (rare at the table's load factor) loops.
+__device__ __forceinline__ uint32_t walk_step(const DeviceSnapshot &s, bool do_probe, bool do_desc,
+                                              uint32_t parent, uint32_t wc, uint64_t k0, uint64_t k1,
+                                              const uint8_t *tok, uint32_t tok_len, NodeDesc *desc) {
+  const Key key{k0, k1};
+  const uint64_t nslots = s.n_buckets * kEdgesPerBucket;
+  uint64_t slot = do_probe ? bucket_of(edge_hash(parent, key), s.n_buckets) * kEdgesPerBucket : 0;
+  const uint4 *q = do_probe ? reinterpret_cast<const uint4 *>(s.edges + slot)
+                            : reinterpret_cast<const uint4 *>(s.nodes + (do_desc ? wc : 0));
+  uint4 x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3];
+  uint32_t c = kNone;
+  bool more = false;
+  if (do_desc) {
+    c = wc;
+    *desc = NodeDesc{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+  }
+  for (;;) {
+    if (do_probe && x1.x != kNone) {
+      const bool hit = x1.x == parent && (((uint64_t)x0.y << 32) | x0.x) == k0 &&
+                       (((uint64_t)x0.w << 32) | x0.z) == k1;
+      bool ok = hit;
+      if (hit && key_is_long(key)) {  // hashed long token: verify the bytes
+        ok = x1.w == tok_len;
+        for (uint32_t i = 0; ok && i < tok_len; i++) ok = s.tok_pool[x1.z + i] == tok[i];
+      }
+      if (ok) {
+        c = x1.y;
+        *desc = NodeDesc{x2.x, x2.y, x2.z, x2.w, x3.x, x3.y, x3.z, x3.w};
+      }
+      more = !ok;
+    } else {
+      more = false;
+    }
+    if (!__any(more)) break;  // wave-uniform
+    if (more) {
+      slot = slot + 1 == nslots ? 0 : slot + 1;
+      const uint4 *e = reinterpret_cast<const uint4 *>(s.edges + slot);
+      x0 = e[0];
+      x1 = e[1];
+      x2 = e[2];
+      x3 = e[3];
+    }
+    do_probe = more;
+  }
+  return c;
+}
+
 }  // namespace mqm

@@ -286,7 +286,8 @@ int upload(std::shared_ptr<const HostSnapshot> hs, int device, std::unique_ptr<G
       hs->rch_off.size() * 4,              hs->rch_refs.size() * 8};
   for (int i = 0; i < GpuSnapshot::kNumBuffers; i++) {
     if (i >= 4 && !ret) break;
-    if (hipMalloc(&g->buffers[i], sz[i] ? sz[i] : 16) != hipSuccess) return MQM_ENOMEM;
+    // +64 B: walk_step reads 64 B at any node descriptor (the last one included)
+    if (hipMalloc(&g->buffers[i], (sz[i] ? sz[i] : 16) + 64) != hipSuccess) return MQM_ENOMEM;
     if (sz[i] && hipMemcpy(g->buffers[i], src[i], sz[i], hipMemcpyHostToDevice) != hipSuccess) return MQM_EHIP;
     g->device_bytes += sz[i];
   }

@@ -139,11 +139,19 @@ __device__ __forceinline__ uint32_t qos_bits(uint32_t meta) { return (1u << (met
 // largest h with field(h) <= x.  Hits with none of those entries tie with
 // their successor, so the largest such h is the one that holds x.
 enum : int { kFieldOff = 0, kFieldSpre = 1, kFieldMpre = 2, kFieldRank = 3 };
+// Branch-free (selects, clamped LDS reads): a divergent branch around a load
+// makes the compiler wait for it before the branch joins, which serialises
+// the loads a lane is meant to have in flight together.
 template <int kField>
 __device__ __forceinline__ uint32_t find_hit(const uint32_t *rec, uint32_t nh, uint32_t x) {
   uint32_t h = 0;
-  for (uint32_t step = 32; step > 0; step >>= 1)
-    if (h + step < nh && rec[4 + kRecHit * (h + step) + kField] <= x) h += step;
+  const uint32_t last = nh ? nh - 1 : 0;
+#pragma unroll
+  for (uint32_t step = 32; step > 0; step >>= 1) {
+    const uint32_t c = h + step;
+    const uint32_t v = rec[4 + kRecHit * (c < last ? c : last) + kField];
+    h = (c < nh && v <= x) ? c : h;
+  }
   return h;
 }
 
@@ -191,7 +199,7 @@ __device__ __forceinline__ uint32_t group_scan_ex(uint32_t v, int gl, uint32_t *
 
 // kG lanes per topic (8 or 16), kWave / kG topics per wavefront
 template <int kG>
-__global__ __launch_bounds__(kWave * kWalkWaves, 5) void k_walk(DeviceSnapshot s, const uint8_t *__restrict__ tbytes,
+__global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, const uint8_t *__restrict__ tbytes,
                                                            const uint64_t *__restrict__ toffs, uint32_t n,
                                                            Outputs o) {
   constexpr int kGroups = kWave / kG;
@@ -231,9 +239,10 @@ __global__ __launch_bounds__(kWave * kWalkWaves, 5) void k_walk(DeviceSnapshot s
     for (uint32_t base = 0; base < len && nsep < (uint32_t)kLMax; base += kStage) {
       uint8_t b[kStage / kG];
 #pragma unroll
-      for (int j = 0; j < kStage / kG; j++) {
+      for (int j = 0; j < kStage / kG; j++) {  // unconditional: clamped into the topic (or a dummy byte)
         const uint32_t p = base + j * kG + gl;
-        b[j] = p < len ? tp[p] : 0;
+        const uint8_t v = *(len ? tp + (p < len ? p : len - 1) : o.cls);
+        b[j] = p < len ? v : 0;
       }
       if (base == 0) {
 #pragma unroll
@@ -299,18 +308,13 @@ __global__ __launch_bounds__(kWave * kWalkWaves, 5) void k_walk(DeviceSnapshot s
       uint32_t nnext = 0;
       for (uint32_t base = 0; base < nf * 3; base += kG) {
         const uint32_t item = base + gl;
-        const uint32_t fi = item / 3, type = item % 3;
-        uint32_t c = kNone;
+        const bool live = item < nf * 3;
+        const uint32_t fi = live ? item / 3 : 0, type = item % 3;
+        const uint32_t node = L.front[cur][0][fi], wc = L.front[cur][type == 2 ? 2 : 1][fi];
         NodeDesc dc;
-        if (item < nf * 3) {
-          const uint32_t node = L.front[cur][0][fi];
-          if (type == 0) {
-            if (!lit_is_wild && !(node & kNoLit)) c = probe_edge(s, node, k0, k1, tp + tst, tln, &dc);
-          } else {
-            c = L.front[cur][type][fi];
-            if (c != kNone) dc = load_desc(s.nodes + c);
-          }
-        }
+        const uint32_t c = walk_step(s, live && type == 0 && !lit_is_wild && !(node & kNoLit),
+                                     live && type != 0 && wc != kNone, node & ~kNoLit, wc, k0, k1, tp + tst, tln,
+                                     &dc);
         const bool found = c != kNone;
         const uint32_t fl = found ? dc.sh_cnt_flags >> 24 : 0;
         const bool skip_dollar = dollar && (fl & kFlagDollarWild);  // topics.go:527
@@ -470,31 +474,27 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_emit(DeviceSnapshot s, ui
     uint32_t mcl[kSmallPer], msid[kSmallPer], mrk[kSmallPer], mmeta[kSmallPer];
     if (merge_here) {
 #pragma unroll
-      for (int k = 0; k < kSmallPer; k++) {
+      for (int k = 0; k < kSmallPer; k++) {  // unconditional loads (entry 0 stands in past M)
         const uint32_t q = lane + k * kWave;
-        if (q < M) {
-          uint32_t h;
-          msid[k] = multi_sid(L.rec, nh, Ss, q, &h);
-          mrk[k] = rec_at(L.rec, h, kFieldRank);
-          const SubEnt e = s.subs[msid[k]];
-          mcl[k] = e.client;
-          mmeta[k] = e.meta;
-        }
+        uint32_t h;
+        msid[k] = multi_sid(L.rec, nh, Ss, q < M ? q : 0, &h);
+        mrk[k] = rec_at(L.rec, h, kFieldRank);
+        const SubEnt e = s.subs[msid[k]];
+        mcl[k] = e.client;
+        mmeta[k] = e.meta;
       }
     }
     // solo entries: delivery q of the topic is solo entry q
     uint32_t cl[kEmitU], sid[kEmitU], meta[kEmitU];
     auto load_solo = [&](uint32_t base, uint32_t *c_, uint32_t *s_, uint32_t *m_) {
 #pragma unroll
-      for (int u = 0; u < kEmitU; u++) {
-        const uint32_t q = base + u * kWave + lane;
-        if (q < Ss) {
-          const uint32_t h = find_hit<kFieldSpre>(L.rec, nh, q);
-          s_[u] = rec_at(L.rec, h, kFieldOff) + (q - rec_at(L.rec, h, kFieldSpre));
-          const SubEnt e = s.subs[s_[u]];
-          c_[u] = e.client;
-          m_[u] = e.meta;
-        }
+      for (int u = 0; u < kEmitU; u++) {  // unconditional loads (entry 0 stands in past Ss)
+        const uint32_t q0 = base + u * kWave + lane, q = q0 < Ss ? q0 : 0;
+        const uint32_t h = find_hit<kFieldSpre>(L.rec, nh, q);
+        s_[u] = rec_at(L.rec, h, kFieldOff) + (q - rec_at(L.rec, h, kFieldSpre));
+        const SubEnt e = s.subs[s_[u]];
+        c_[u] = e.client;
+        m_[u] = e.meta;
       }
     };
     if (Ss) load_solo(0, cl, sid, meta);
@@ -611,16 +611,14 @@ __global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs
     }
     uint32_t cl[kPer], sid[kPer], rk[kPer], meta[kPer];
 #pragma unroll
-    for (int k = 0; k < kPer; k++) {
+    for (int k = 0; k < kPer; k++) {  // unconditional loads (entry 0 stands in past M)
       const uint32_t q = tid + k * kBigThreads;
-      if (q < M) {
-        uint32_t h;
-        sid[k] = multi_sid(rec, nh, Ss, q, &h);
-        rk[k] = rec_at(rec, h, kFieldRank);
-        const SubEnt e = s.subs[sid[k]];
-        cl[k] = e.client;
-        meta[k] = e.meta;
-      }
+      uint32_t h;
+      sid[k] = multi_sid(rec, nh, Ss, q < M ? q : 0, &h);
+      rk[k] = rec_at(rec, h, kFieldRank);
+      const SubEnt e = s.subs[sid[k]];
+      cl[k] = e.client;
+      meta[k] = e.meta;
     }
     __syncthreads();
 #pragma unroll
