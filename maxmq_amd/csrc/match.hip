@@ -68,9 +68,10 @@ constexpr int kRecStrideAlloc = 228;                  // 16-B aligned per topic
 constexpr uint32_t kSMax = 16384;        // raw entries per topic on the bounded path
 constexpr int kEmitU = 4;                // solo entries in flight per lane
 constexpr int kEmitWaves = 4;
+constexpr int kSmallLanes = 16;          // k_emit<16>: lanes per topic of the small class
+constexpr uint32_t kSmallSolo = 256;     // small class: at most this many solo entries
 constexpr int kSmallSlots = 256;         // k_emit merge table slots (per wave)
 constexpr int kSmallMulti = 192;         // multi entries it holds (load <= 0.75)
-constexpr int kSmallPer = kSmallMulti / 64;
 constexpr int kBigThreads = 256;
 constexpr int kBigMax = 3072;            // multi entries per bounded topic (k_multi's last tier)
 constexpr uint32_t kNoWhy = 0xFFFFFFFFu;
@@ -81,7 +82,7 @@ static_assert(kSmallMulti * 4 <= kSmallSlots * 3, "k_emit table load factor");
 static_assert(kBigMax * 4 <= 4096 * 3 && kBigMax <= 12 * kBigThreads, "the last k_multi tier holds every bounded topic");
 static_assert(kSmallMulti % kWave == 0, "register tiles");
 
-enum : uint8_t { kClsDone = 0, kClsBounded = 1, kClsDfs = 3 };
+enum : uint8_t { kClsDone = 0, kClsSmall = 1, kClsBig = 2, kClsDfs = 3 };
 enum : uint32_t { kWhyFrontier = 0, kWhyHits = 1, kWhyLevels = 2, kWhyShared = 3, kWhyEntries = 4 };
 
 struct Counters {              // zeroed before every batch
@@ -387,7 +388,10 @@ __global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, co
         rec[1] = Ss;
         rec[2] = Ms;
       }
-      o.cls[t] = dfs ? kClsDfs : S == 0 ? kClsDone : kClsBounded;
+      o.cls[t] = dfs ? kClsDfs
+                 : S == 0 ? kClsDone
+                 : (Ss <= kSmallSolo && Ms <= 3u * kSmallLanes) ? kClsSmall
+                                                                 : kClsBig;
       o.scount[t] = dfs ? 0 : S;
       o.hcount[t] = dfs ? 0 : H;
       o.dcount[t] = 0;
@@ -415,13 +419,6 @@ __global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, co
 //     ballot after the solo part.  More multi entries go to k_multi.
 // Also writes every bounded topic's shared candidates.
 // ---------------------------------------------------------------------------
-struct EmitLds {
-  uint32_t rec[kRecStrideAlloc];
-  uint32_t tkey[kSmallSlots];
-  uint32_t tbits[kSmallSlots];
-  uint32_t tmin[kSmallSlots];
-};
-
 // multi entry q of a topic: subs index and hit
 __device__ __forceinline__ uint32_t multi_sid(const uint32_t *rec, uint32_t nh, uint32_t Ss, uint32_t q,
                                               uint32_t *hit) {
@@ -431,51 +428,92 @@ __device__ __forceinline__ uint32_t multi_sid(const uint32_t *rec, uint32_t nh, 
   return rec_at(rec, h, kFieldOff) + solo_h + (q - rec_at(rec, h, kFieldMpre));
 }
 
+// kE lanes per topic: 16 for the small class (4 topics per wavefront), 64 for
+// the big one (a wavefront per topic; more than kSmallMulti multi entries go on
+// to k_multi).
+template <int kE>
+struct EmitCfg {
+  static constexpr int kGroups = kWave / kE;
+  static constexpr uint32_t kMulti = kE == kWave ? kSmallMulti : 3 * kE;  // multi entries merged here
+  static constexpr uint32_t kSlots = kE == kWave ? kSmallSlots : 64;
+  static constexpr int kMPer = kMulti / kE;
+  static constexpr int kRecPer = 64 / kE;  // record words each lane prefetches (64 per topic)
+};
+
+template <int kE>
+struct EmitLds {
+  uint32_t rec[kRecStrideAlloc];
+  uint32_t tkey[EmitCfg<kE>::kSlots];
+  uint32_t tbits[EmitCfg<kE>::kSlots];
+  uint32_t tmin[EmitCfg<kE>::kSlots];
+};
+
+template <int kE>
 __global__ __launch_bounds__(kWave *kEmitWaves) void k_emit(DeviceSnapshot s, uint32_t n, Outputs o) {
-  __shared__ EmitLds lds_all[kEmitWaves];
+  using Cfg = EmitCfg<kE>;
+  constexpr int kGroups = Cfg::kGroups, kMPer = Cfg::kMPer, kRecPer = Cfg::kRecPer;
+  constexpr uint64_t kGMask = kE == 64 ? ~0ull : (1ull << kE) - 1ull;
+  constexpr uint8_t kMine = kE == kWave ? kClsBig : kClsSmall;
+  __shared__ EmitLds<kE> lds_all[kEmitWaves * kGroups];
   const int lane = threadIdx.x & (kWave - 1);
-  EmitLds &L = lds_all[threadIdx.x / kWave];
-  const uint32_t nwaves = gridDim.x * kEmitWaves;
-  uint32_t t = blockIdx.x * kEmitWaves + threadIdx.x / kWave;
-  uint32_t n_cls = kClsDone, n_H = 0, n_rw = 0;
+  const int g = lane / kE, gl = lane % kE, gbase = g * kE;
+  EmitLds<kE> &L = lds_all[(threadIdx.x / kWave) * kGroups + g];
+  const uint64_t glt = (1ull << gl) - 1ull;  // group lanes below gl (after >> gbase)
+  const uint32_t ngroups = gridDim.x * kEmitWaves * kGroups;
+  uint32_t t = (blockIdx.x * kEmitWaves + threadIdx.x / kWave) * kGroups + g;
+  // the next topic's header and first 64 record words, one topic ahead
+  uint32_t n_cls = kClsDone, n_H = 0, n_rw[kRecPer];
   uint64_t n_db = 0, n_hb = 0;
   auto fetch = [&](uint32_t u) {
     n_cls = o.cls[u];
     n_H = o.hcount[u];
     n_db = o.dstart[u];
     n_hb = o.hstart[u];
-    n_rw = o.recs[(uint64_t)u * kRecStrideAlloc + lane];
+    const uint32_t *r = o.recs + (uint64_t)u * kRecStrideAlloc + gl * kRecPer;
+    if constexpr (kRecPer == 4) {
+      const uint4 v = *reinterpret_cast<const uint4 *>(r);
+      n_rw[0] = v.x, n_rw[1] = v.y, n_rw[2] = v.z, n_rw[3] = v.w;
+    } else {
+      n_rw[0] = r[0];
+    }
   };
   if (t < n) fetch(t);
-  for (; t < n; t += nwaves) {
-    const uint32_t cls = n_cls, H = n_H, rw = n_rw;
+  for (; t < n; t += ngroups) {
+    const uint32_t cls = n_cls, H = n_H;
+    uint32_t rw[kRecPer];
+#pragma unroll
+    for (int i = 0; i < kRecPer; i++) rw[i] = n_rw[i];
     const uint64_t db = n_db, hb = n_hb;
-    if (t + nwaves < n) fetch(t + nwaves);
-    if (cls == kClsDfs || (cls == kClsDone && H == 0)) continue;
-    const uint32_t w0 = __shfl(rw, 0, 64), Ss = __shfl(rw, 1, 64), M = __shfl(rw, 2, 64);
+    if (t + ngroups < n) fetch(t + ngroups);
+    // the small kernel also takes the S == 0 topics (shared candidates only)
+    if (!(cls == kMine || (kE != kWave && cls == kClsDone && H != 0))) continue;
+#pragma unroll
+    for (int i = 0; i < kRecPer; i++) L.rec[gl * kRecPer + i] = rw[i];
+    wave_lds_sync();
+    const uint32_t w0 = L.rec[0], Ss = L.rec[1], M = L.rec[2];
     const uint32_t nh = w0 & 0xFFu, nsh = w0 >> 8;
     const uint32_t *grec = o.recs + (uint64_t)t * kRecStrideAlloc;
-    L.rec[lane] = rw;
-    for (uint32_t i = kWave + lane; i < 4 + kRecHit * nh; i += kWave) L.rec[i] = grec[i];
+    for (uint32_t i = kWave + gl; i < 4 + kRecHit * nh; i += kE) L.rec[i] = grec[i];
     wave_lds_sync();
     if (H) {  // shared candidates (gatherSharedSubscriptions, topics.go:541-555)
       uint32_t w = 0;
       for (uint32_t i = 0; i < nsh; i++) {
         const uint32_t so = grec[kRecSh + 2 * i], sc = grec[kRecSh + 1 + 2 * i];
-        for (uint32_t j = lane; j < sc; j += kWave) o.hout[hb + w + j] = so + j;
+        for (uint32_t j = gl; j < sc; j += kE) o.hout[hb + w + j] = so + j;
         w += sc;
       }
     }
     // Loads before stores: a wait for a load also waits for every older
     // store of the wave (one in-order vmcnt), so each chunk's loads are issued
     // before the previous chunk's stores, and the multi entries' loads before
-    // any store of the topic.
-    const bool merge_here = M > 0 && M <= (uint32_t)kSmallMulti;
-    uint32_t mcl[kSmallPer], msid[kSmallPer], mrk[kSmallPer], mmeta[kSmallPer];
+    // any store of the topic.  Loads are unconditional (entry 0 stands in
+    // past the end): a branch around a load makes the compiler wait for it.
+    const bool merge_here = M > 0 && M <= Cfg::kMulti;
+    uint32_t mcl[kMPer], msid[kMPer], mrk[kMPer], mmeta[kMPer];
     if (merge_here) {
 #pragma unroll
-      for (int k = 0; k < kSmallPer; k++) {  // unconditional loads (entry 0 stands in past M)
-        const uint32_t q = lane + k * kWave;
+      for (int k = 0; k < kMPer; k++) {
+        const uint32_t q = gl + k * kE;
         uint32_t h;
         msid[k] = multi_sid(L.rec, nh, Ss, q < M ? q : 0, &h);
         mrk[k] = rec_at(L.rec, h, kFieldRank);
@@ -488,8 +526,8 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_emit(DeviceSnapshot s, ui
     uint32_t cl[kEmitU], sid[kEmitU], meta[kEmitU];
     auto load_solo = [&](uint32_t base, uint32_t *c_, uint32_t *s_, uint32_t *m_) {
 #pragma unroll
-      for (int u = 0; u < kEmitU; u++) {  // unconditional loads (entry 0 stands in past Ss)
-        const uint32_t q0 = base + u * kWave + lane, q = q0 < Ss ? q0 : 0;
+      for (int u = 0; u < kEmitU; u++) {
+        const uint32_t q0 = base + u * kE + gl, q = q0 < Ss ? q0 : 0;
         const uint32_t h = find_hit<kFieldSpre>(L.rec, nh, q);
         s_[u] = rec_at(L.rec, h, kFieldOff) + (q - rec_at(L.rec, h, kFieldSpre));
         const SubEnt e = s.subs[s_[u]];
@@ -498,12 +536,12 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_emit(DeviceSnapshot s, ui
       }
     };
     if (Ss) load_solo(0, cl, sid, meta);
-    for (uint32_t base = 0; base < Ss; base += kWave * kEmitU) {
+    for (uint32_t base = 0; base < Ss; base += kE * kEmitU) {
       uint32_t ncl[kEmitU], nsid[kEmitU], nmeta[kEmitU];
-      if (base + kWave * kEmitU < Ss) load_solo(base + kWave * kEmitU, ncl, nsid, nmeta);
+      if (base + kE * kEmitU < Ss) load_solo(base + kE * kEmitU, ncl, nsid, nmeta);
 #pragma unroll
       for (int u = 0; u < kEmitU; u++) {
-        const uint32_t q = base + u * kWave + lane;
+        const uint32_t q = base + u * kE + gl;
         if (q < Ss) o.dout[db + q] = pack_delivery(cl[u], sid[u], meta[u] & 3u, (meta[u] >> 2) & 1u);
         cl[u] = ncl[u];
         sid[u] = nsid[u];
@@ -511,41 +549,41 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_emit(DeviceSnapshot s, ui
       }
     }
     uint32_t D = Ss;
-    if (M > (uint32_t)kSmallMulti) {  // the workgroup tier merges them (and writes dcount)
-      if (lane == 0) o.multi_list[atomicAdd(&o.ctr->n_multi, 1u)] = t;
+    if (M > Cfg::kMulti) {  // the workgroup tier merges them and writes dcount (big class only)
+      if (gl == 0) o.multi_list[atomicAdd(&o.ctr->n_multi, 1u)] = t;
       wave_lds_sync();
       continue;
     }
     if (merge_here) {
       uint32_t lg = 6;
-      while ((1u << lg) < 2 * M && (1u << lg) < (uint32_t)kSmallSlots) lg++;
+      while ((1u << lg) < 2 * M && (1u << lg) < Cfg::kSlots) lg++;
       const uint32_t mask = (1u << lg) - 1;
-      for (uint32_t i = lane; i <= mask; i += kWave) {
+      for (uint32_t i = gl; i <= mask; i += kE) {
         L.tkey[i] = 0;
         L.tbits[i] = 0;
         L.tmin[i] = 0xFFFFFFFFu;
       }
       wave_lds_sync();
 #pragma unroll
-      for (int k = 0; k < kSmallPer; k++)
-        if (lane + k * kWave < M) table_insert(L.tkey, L.tbits, L.tmin, mask, lg, mcl[k], mmeta[k], mrk[k]);
+      for (int k = 0; k < kMPer; k++)
+        if (gl + k * kE < M) table_insert(L.tkey, L.tbits, L.tmin, mask, lg, mcl[k], mmeta[k], mrk[k]);
       wave_lds_sync();
 #pragma unroll
-      for (int k = 0; k < kSmallPer; k++) {
+      for (int k = 0; k < kMPer; k++) {
         bool win = false;
         uint64_t ent = 0;
-        if (lane + k * kWave < M) {
+        if (gl + k * kE < M) {
           const uint32_t sl = table_find(L.tkey, mask, lg, mcl[k]);
           win = L.tmin[sl] == mrk[k];
           const uint32_t v = L.tbits[sl];
           ent = pack_delivery(mcl[k], msid[k], 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
         }
-        const uint64_t m = __ballot(win);
-        if (win) o.dout[db + D + __popcll(m & lanemask_lt(lane))] = ent;
+        const uint64_t m = (__ballot(win) >> gbase) & kGMask;
+        if (win) o.dout[db + D + __popcll(m & glt)] = ent;
         D += __popcll(m);
       }
     }
-    if (lane == 0) o.dcount[t] = D;
+    if (gl == 0) o.dcount[t] = D;
     wave_lds_sync();
   }
 }
@@ -1076,10 +1114,14 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
 
   mark(ws, 2, st);
   static_assert(kWave * kEmitWaves == kBigThreads, "resident_blocks assumes 256-thread blocks");
-  const uint32_t emit_blocks = std::max<uint32_t>(
-      1, std::min<uint32_t>((n + kEmitWaves - 1) / kEmitWaves, resident_blocks(ws, 2, k_emit)));
   if (n > 0) {
-    hipLaunchKernelGGL(k_emit, dim3(emit_blocks), dim3(kWave * kEmitWaves), 0, st, s, n, o);
+    const uint32_t small_blocks = std::max<uint32_t>(
+        1, std::min<uint32_t>((n + kEmitWaves * 4 - 1) / (kEmitWaves * 4), resident_blocks(ws, 2, k_emit<16>)));
+    hipLaunchKernelGGL(k_emit<16>, dim3(small_blocks), dim3(kWave * kEmitWaves), 0, st, s, n, o);
+    HIP_TRY(hipGetLastError());
+    const uint32_t big_blocks = std::max<uint32_t>(
+        1, std::min<uint32_t>((n + kEmitWaves - 1) / kEmitWaves, resident_blocks(ws, 6, k_emit<64>)));
+    hipLaunchKernelGGL(k_emit<64>, dim3(big_blocks), dim3(kWave * kEmitWaves), 0, st, s, n, o);
     HIP_TRY(hipGetLastError());
     if (ws.get(W::kOvfList, sizeof(uint32_t) * (n + 1))) return -2;
     auto *ovf = (uint32_t *)ws.ptr(W::kOvfList);
