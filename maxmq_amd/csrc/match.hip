@@ -91,6 +91,8 @@ struct Counters {              // zeroed before every batch
   unsigned int n_dfs;          // topics appended to the DFS list
   unsigned int why[5];         // DFS routing reasons (kWhy*)
   unsigned int n_multi;        // topics whose multi entries k_emit passed to k_multi
+  unsigned int n_small;        // emit lists (DeviceSelect counts)
+  unsigned int n_bigc;
   unsigned int n_ovf;          // topics k_multi's first tier passed to the second
   unsigned int n_ovf2;         // ... the second tier to the third
 };
@@ -449,23 +451,24 @@ struct EmitLds {
 };
 
 template <int kE>
-__global__ __launch_bounds__(kWave *kEmitWaves) void k_emit(DeviceSnapshot s, uint32_t n, Outputs o) {
+__global__ __launch_bounds__(kWave *kEmitWaves) void k_emit(DeviceSnapshot s, Outputs o, const uint32_t *__restrict__ list,
+                                                            const unsigned int *__restrict__ count) {
   using Cfg = EmitCfg<kE>;
   constexpr int kGroups = Cfg::kGroups, kMPer = Cfg::kMPer, kRecPer = Cfg::kRecPer;
   constexpr uint64_t kGMask = kE == 64 ? ~0ull : (1ull << kE) - 1ull;
-  constexpr uint8_t kMine = kE == kWave ? kClsBig : kClsSmall;
   __shared__ EmitLds<kE> lds_all[kEmitWaves * kGroups];
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / kE, gl = lane % kE, gbase = g * kE;
   EmitLds<kE> &L = lds_all[(threadIdx.x / kWave) * kGroups + g];
   const uint64_t glt = (1ull << gl) - 1ull;  // group lanes below gl (after >> gbase)
   const uint32_t ngroups = gridDim.x * kEmitWaves * kGroups;
-  uint32_t t = (blockIdx.x * kEmitWaves + threadIdx.x / kWave) * kGroups + g;
-  // the next topic's header and first 64 record words, one topic ahead
-  uint32_t n_cls = kClsDone, n_H = 0, n_rw[kRecPer];
+  const uint32_t nl = *count;
+  uint32_t i = (blockIdx.x * kEmitWaves + threadIdx.x / kWave) * kGroups + g;
+  // list entries two topics ahead; the next topic's header and first 64
+  // record words one topic ahead
+  uint32_t n_H = 0, n_rw[kRecPer];
   uint64_t n_db = 0, n_hb = 0;
   auto fetch = [&](uint32_t u) {
-    n_cls = o.cls[u];
     n_H = o.hcount[u];
     n_db = o.dstart[u];
     n_hb = o.hstart[u];
@@ -477,28 +480,30 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_emit(DeviceSnapshot s, ui
       n_rw[0] = r[0];
     }
   };
-  if (t < n) fetch(t);
-  for (; t < n; t += ngroups) {
-    const uint32_t cls = n_cls, H = n_H;
+  uint32_t t_nxt = i < nl ? list[i] : 0;
+  uint32_t t_nn = i + ngroups < nl ? list[i + ngroups] : 0;
+  if (i < nl) fetch(t_nxt);
+  for (; i < nl; i += ngroups) {
+    const uint32_t t = t_nxt, H = n_H;
     uint32_t rw[kRecPer];
 #pragma unroll
-    for (int i = 0; i < kRecPer; i++) rw[i] = n_rw[i];
+    for (int j = 0; j < kRecPer; j++) rw[j] = n_rw[j];
     const uint64_t db = n_db, hb = n_hb;
-    if (t + ngroups < n) fetch(t + ngroups);
-    // the small kernel also takes the S == 0 topics (shared candidates only)
-    if (!(cls == kMine || (kE != kWave && cls == kClsDone && H != 0))) continue;
+    t_nxt = t_nn;
+    if (i + ngroups < nl) fetch(t_nxt);
+    t_nn = i + 2 * ngroups < nl ? list[i + 2 * ngroups] : 0;
 #pragma unroll
-    for (int i = 0; i < kRecPer; i++) L.rec[gl * kRecPer + i] = rw[i];
+    for (int j = 0; j < kRecPer; j++) L.rec[gl * kRecPer + j] = rw[j];
     wave_lds_sync();
     const uint32_t w0 = L.rec[0], Ss = L.rec[1], M = L.rec[2];
     const uint32_t nh = w0 & 0xFFu, nsh = w0 >> 8;
     const uint32_t *grec = o.recs + (uint64_t)t * kRecStrideAlloc;
-    for (uint32_t i = kWave + gl; i < 4 + kRecHit * nh; i += kE) L.rec[i] = grec[i];
+    for (uint32_t j = kWave + gl; j < 4 + kRecHit * nh; j += kE) L.rec[j] = grec[j];
     wave_lds_sync();
     if (H) {  // shared candidates (gatherSharedSubscriptions, topics.go:541-555)
       uint32_t w = 0;
-      for (uint32_t i = 0; i < nsh; i++) {
-        const uint32_t so = grec[kRecSh + 2 * i], sc = grec[kRecSh + 1 + 2 * i];
+      for (uint32_t j = 0; j < nsh; j++) {
+        const uint32_t so = grec[kRecSh + 2 * j], sc = grec[kRecSh + 1 + 2 * j];
         for (uint32_t j = gl; j < sc; j += kE) o.hout[hb + w + j] = so + j;
         w += sc;
       }
@@ -558,10 +563,10 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_emit(DeviceSnapshot s, ui
       uint32_t lg = 6;
       while ((1u << lg) < 2 * M && (1u << lg) < Cfg::kSlots) lg++;
       const uint32_t mask = (1u << lg) - 1;
-      for (uint32_t i = gl; i <= mask; i += kE) {
-        L.tkey[i] = 0;
-        L.tbits[i] = 0;
-        L.tmin[i] = 0xFFFFFFFFu;
+      for (uint32_t j = gl; j <= mask; j += kE) {
+        L.tkey[j] = 0;
+        L.tbits[j] = 0;
+        L.tmin[j] = 0xFFFFFFFFu;
       }
       wave_lds_sync();
 #pragma unroll
@@ -918,6 +923,20 @@ __global__ __launch_bounds__(256) void k_densify(uint32_t n, const uint32_t *__r
   }
 }
 
+// emit lists: the small class (and the topics with shared candidates only),
+// the big class
+struct IsSmallClass {
+  const uint8_t *cls;
+  const uint32_t *hcount;
+  __host__ __device__ bool operator()(uint32_t t) const {
+    return cls[t] == kClsSmall || (cls[t] == kClsDone && hcount[t] != 0);
+  }
+};
+struct IsBigClass {
+  const uint8_t *cls;
+  __host__ __device__ bool operator()(uint32_t t) const { return cls[t] == kClsBig; }
+};
+
 #define HIP_TRY(x)                                                                                        \
   do {                                                                                                    \
     hipError_t e_ = (x);                                                                                  \
@@ -1115,13 +1134,20 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   mark(ws, 2, st);
   static_assert(kWave * kEmitWaves == kBigThreads, "resident_blocks assumes 256-thread blocks");
   if (n > 0) {
-    const uint32_t small_blocks = std::max<uint32_t>(
-        1, std::min<uint32_t>((n + kEmitWaves * 4 - 1) / (kEmitWaves * 4), resident_blocks(ws, 2, k_emit<16>)));
-    hipLaunchKernelGGL(k_emit<16>, dim3(small_blocks), dim3(kWave * kEmitWaves), 0, st, s, n, o);
+    if (ws.get(W::kListS, sizeof(uint32_t) * (n + 1)) || ws.get(W::kListB, sizeof(uint32_t) * (n + 1))) return -2;
+    auto *list_s = (uint32_t *)ws.ptr(W::kListS), *list_b = (uint32_t *)ws.ptr(W::kListB);
+    size_t tmp = 0;
+    hipcub::CountingInputIterator<uint32_t> it(0);
+    HIP_TRY(hipcub::DeviceSelect::If(nullptr, tmp, it, list_s, &o.ctr->n_small, n, IsSmallClass{o.cls, o.hcount}, st));
+    if (ws.get(W::kScanTmp, tmp)) return -2;
+    HIP_TRY(hipcub::DeviceSelect::If(ws.ptr(W::kScanTmp), tmp, it, list_s, &o.ctr->n_small, n,
+                                     IsSmallClass{o.cls, o.hcount}, st));
+    HIP_TRY(hipcub::DeviceSelect::If(ws.ptr(W::kScanTmp), tmp, it, list_b, &o.ctr->n_bigc, n, IsBigClass{o.cls}, st));
+    hipLaunchKernelGGL(k_emit<16>, dim3(resident_blocks(ws, 2, k_emit<16>)), dim3(kWave * kEmitWaves), 0, st, s, o,
+                       list_s, &o.ctr->n_small);
     HIP_TRY(hipGetLastError());
-    const uint32_t big_blocks = std::max<uint32_t>(
-        1, std::min<uint32_t>((n + kEmitWaves - 1) / kEmitWaves, resident_blocks(ws, 6, k_emit<64>)));
-    hipLaunchKernelGGL(k_emit<64>, dim3(big_blocks), dim3(kWave * kEmitWaves), 0, st, s, n, o);
+    hipLaunchKernelGGL(k_emit<64>, dim3(resident_blocks(ws, 6, k_emit<64>)), dim3(kWave * kEmitWaves), 0, st, s, o,
+                       list_b, &o.ctr->n_bigc);
     HIP_TRY(hipGetLastError());
     if (ws.get(W::kOvfList, sizeof(uint32_t) * (n + 1))) return -2;
     auto *ovf = (uint32_t *)ws.ptr(W::kOvfList);
