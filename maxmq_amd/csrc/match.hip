@@ -142,20 +142,28 @@ __device__ __forceinline__ uint32_t qos_bits(uint32_t meta) { return (1u << (met
 // largest h with field(h) <= x.  Hits with none of those entries tie with
 // their successor, so the largest such h is the one that holds x.
 enum : int { kFieldOff = 0, kFieldSpre = 1, kFieldMpre = 2, kFieldRank = 3 };
-// Branch-free (selects, clamped LDS reads): a divergent branch around a load
-// makes the compiler wait for it before the branch joins, which serialises
-// the loads a lane is meant to have in flight together.
+// Counting search: every lane of a group reads the same record word per hit
+// (an LDS broadcast) and the reads are independent, so the loop pipelines —
+// a binary search's dependent reads compiled to a branch and a full LDS wait
+// per step.  Hits are few (<= kHCap).
+template <int kField, int kN>
+__device__ __forceinline__ void find_hits(const uint32_t *rec, uint32_t nh, const uint32_t (&x)[kN],
+                                          uint32_t (&h)[kN]) {
+#pragma unroll
+  for (int u = 0; u < kN; u++) h[u] = 0;
+  for (uint32_t j = 1; j < nh; j++) {
+    const uint32_t v = rec[4 + kRecHit * j + kField];
+#pragma unroll
+    for (int u = 0; u < kN; u++) h[u] += v <= x[u] ? 1u : 0u;
+  }
+}
+
 template <int kField>
 __device__ __forceinline__ uint32_t find_hit(const uint32_t *rec, uint32_t nh, uint32_t x) {
-  uint32_t h = 0;
-  const uint32_t last = nh ? nh - 1 : 0;
-#pragma unroll
-  for (uint32_t step = 32; step > 0; step >>= 1) {
-    const uint32_t c = h + step;
-    const uint32_t v = rec[4 + kRecHit * (c < last ? c : last) + kField];
-    h = (c < nh && v <= x) ? c : h;
-  }
-  return h;
+  const uint32_t xs[1] = {x};
+  uint32_t hs[1];
+  find_hits<kField, 1>(rec, nh, xs, hs);
+  return hs[0];
 }
 
 __device__ __forceinline__ uint32_t rec_at(const uint32_t *rec, uint32_t h, int field) {
@@ -530,11 +538,16 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_emit(DeviceSnapshot s, Ou
     // solo entries: delivery q of the topic is solo entry q
     uint32_t cl[kEmitU], sid[kEmitU], meta[kEmitU];
     auto load_solo = [&](uint32_t base, uint32_t *c_, uint32_t *s_, uint32_t *m_) {
+      uint32_t q[kEmitU], h[kEmitU];
+#pragma unroll
+      for (int u = 0; u < kEmitU; u++) {  // unconditional loads (entry 0 stands in past Ss)
+        const uint32_t q0 = base + u * kE + gl;
+        q[u] = q0 < Ss ? q0 : 0;
+      }
+      find_hits<kFieldSpre, kEmitU>(L.rec, nh, q, h);
 #pragma unroll
       for (int u = 0; u < kEmitU; u++) {
-        const uint32_t q0 = base + u * kE + gl, q = q0 < Ss ? q0 : 0;
-        const uint32_t h = find_hit<kFieldSpre>(L.rec, nh, q);
-        s_[u] = rec_at(L.rec, h, kFieldOff) + (q - rec_at(L.rec, h, kFieldSpre));
+        s_[u] = rec_at(L.rec, h[u], kFieldOff) + (q[u] - rec_at(L.rec, h[u], kFieldSpre));
         const SubEnt e = s.subs[s_[u]];
         c_[u] = e.client;
         m_[u] = e.meta;
