@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--workload", choices=["forward", "reverse"], default="forward",
                     help="forward: Subscribers (headline); reverse: Messages over retained topics (config 5)")
     ap.add_argument("--retained", type=int, default=50000000, help="reverse: retained topics")
+    ap.add_argument("--sweep", default="",
+                    help="tuning sweep before the measurement: ';'-separated variants of "
+                         "'ENV=V,ENV=V' (match.hip knobs, e.g. MQM_WALK_OCC=6); per-variant kernel ms to stderr")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per emit launch (profiles/run_pmc.sh)")
     return ap.parse_args()
@@ -140,6 +143,8 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    if args.sweep:
+        run_sweep(args, idx, step, dev, rank)
     idx.profile(True)
     if dist:
         dist.barrier()
@@ -184,7 +189,7 @@ def main():
         stats = None
         if not args.no_cpu_baseline:
             cpu, stats = cpu_baseline(w, args)
-        roof = roofline(stats, n, kms["total"], args.traffic_json)
+        roof = roofline(stats, n, kms, args.traffic_json)
         out = {
             "metric": "publish topics matched/sec (node) + matched deliveries/sec at 10M filters",
             "value": value,
@@ -221,6 +226,36 @@ def main():
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def run_sweep(args, idx, step, dev, rank):
+    """time every variant of --sweep (env knobs read per batch by match.hip)"""
+    import torch
+
+    results = []
+    for var in [v for v in args.sweep.split(";") if v.strip()]:
+        kv = dict(x.split("=", 1) for x in var.split(",") if x.strip())
+        old = {k: os.environ.get(k) for k in kv}
+        os.environ.update(kv)
+        step()
+        torch.cuda.synchronize(dev)
+        idx.profile(True)
+        for _ in range(max(args.steps, 3)):
+            step()
+        torch.cuda.synchronize(dev)
+        prof = idx.profile_read()
+        idx.profile(False)
+        calls = max(prof["calls"], 1)
+        res = {"variant": var, **{f"{k}_ms": prof[f"{k}_ms"] / calls for k in ("walk", "dedupe", "total")}}
+        results.append(res)
+        if rank == 0:
+            log(f"[sweep] {json.dumps(res)}")
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    return results
 
 
 def run_reverse(args, dist, rank, world, local, dev):
@@ -400,17 +435,23 @@ def cpu_baseline(w, args):
     return cpu, tot
 
 
-def roofline(stats, n, total_ms, traffic_json):
+def roofline(stats, n, kms, traffic_json):
     """B = T + 8N + 8P + 8V + 8S + 8D algorithmic bytes per
-    batch, over the device time of the match pipeline (k_walk + k_big +
-    k_dfs + k_compact, first to last kernel, HIP events on the launch stream)."""
+    batch (per-topic counters of the oracle's walk over the CPU sample, scaled
+    to the batch) over the device time of the whole match pipeline (k_walk,
+    scans, k_emit<16|64>, k_multi, k_dfs: first to last kernel, HIP events on
+    the launch stream).  `stages` splits it: the walk moves T + 8N + 8P + 8V,
+    the emit stage 8S + 8D.  `traffic` = HBM bytes per batch of the same
+    kernels from rocprofv3 FETCH_SIZE / WRITE_SIZE (profiles/traffic.json,
+    profiles/run_pmc.sh)."""
+    total_ms = kms["total"]
     if not stats or not stats["topics"] or total_ms <= 0:
         return {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                 "traffic": None}
     k = stats["topics"]
-    per_topic = (stats["topic_bytes"] + 8 * k + 8 * stats["probes"] + 8 * stats["visits"] + 8 * stats["gathered"] +
-                 8 * stats["deliveries"]) / k
-    bytes_per_launch = per_topic * n
+    walk_b = (stats["topic_bytes"] + 8 * k + 8 * stats["probes"] + 8 * stats["visits"]) / k * n
+    emit_b = (8 * stats["gathered"] + 8 * stats["deliveries"]) / k * n
+    bytes_per_launch = walk_b + emit_b
     achieved = bytes_per_launch / (total_ms * 1e-3) / 1e9
     traffic = None
     if traffic_json and os.path.exists(traffic_json):
@@ -419,10 +460,16 @@ def roofline(stats, n, total_ms, traffic_json):
                 traffic = json.load(fh).get("hbm_bytes_per_batch")
         except Exception:
             traffic = None
+
+    def stage(b, ms):
+        return {"bytes": b, "ms": ms, "achieved": b / (ms * 1e-3) / 1e9 if ms > 0 else None,
+                "frac": b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS if ms > 0 else None}
+
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "algorithmic_bytes_per_topic": per_topic, "algorithmic_bytes_per_batch": bytes_per_launch,
-            "kernel": "match pipeline: k_walk + k_big + k_dfs + k_compact per batch"}
+            "algorithmic_bytes_per_topic": bytes_per_launch / n, "algorithmic_bytes_per_batch": bytes_per_launch,
+            "kernel": "match pipeline per batch: k_walk + scans + k_emit<16|64> + k_multi (+ k_dfs)",
+            "stages": {"walk": stage(walk_b, kms["walk"]), "emit": stage(emit_b, kms["dedupe"])}}
 
 
 if __name__ == "__main__":

@@ -4,6 +4,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <unordered_map>
+
 #include "snapshot.h"
 
 namespace mqm {
@@ -26,7 +28,7 @@ struct Workspace {
   void *host_pinned = nullptr;
   uint32_t max_blocks = 2048;  // walk-kernel grid cap (grid-stride beyond)
   int walk_lanes = 8;          // lanes per topic in k_walk (4, 8 or 16; env MQM_WALK_LANES)
-  uint32_t resident[7] = {0, 0, 0, 0, 0, 0, 0};  // k_multi tiers 1-2, k_emit<16>, k_walk<8>, k_walk<16>, k_multi tier 3, k_emit<64>: resident blocks on the device
+  std::unordered_map<const void *, uint32_t> resident;  // kernel -> resident blocks on the device
   // why the last batch's DFS topics left the bounded path:
   // frontier, hits, cached levels, shared hits, raw entries
   uint32_t why[5] = {0, 0, 0, 0, 0};

@@ -38,6 +38,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "device.h"
@@ -209,8 +210,8 @@ __device__ __forceinline__ uint32_t group_scan_ex(uint32_t v, int gl, uint32_t *
 }
 
 // kG lanes per topic (8 or 16), kWave / kG topics per wavefront
-template <int kG>
-__global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, const uint8_t *__restrict__ tbytes,
+template <int kG, int kOcc>
+__global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_eu(kOcc))) void k_walk(DeviceSnapshot s, const uint8_t *__restrict__ tbytes,
                                                            const uint64_t *__restrict__ toffs, uint32_t n,
                                                            Outputs o) {
   constexpr int kGroups = kWave / kG;
@@ -458,8 +459,8 @@ struct EmitLds {
   uint32_t tmin[EmitCfg<kE>::kSlots];
 };
 
-template <int kE>
-__global__ __launch_bounds__(kWave *kEmitWaves) void k_emit(DeviceSnapshot s, Outputs o, const uint32_t *__restrict__ list,
+template <int kE, int kOcc>
+__global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_eu(kOcc))) void k_emit(DeviceSnapshot s, Outputs o, const uint32_t *__restrict__ list,
                                                             const unsigned int *__restrict__ count) {
   using Cfg = EmitCfg<kE>;
   constexpr int kGroups = Cfg::kGroups, kMPer = Cfg::kMPer, kRecPer = Cfg::kRecPer;
@@ -1026,18 +1027,25 @@ static float elapsed(Workspace &ws, int a, int b) {
   return ms;
 }
 
+// tuning knob from the environment (read per batch; 0 = default variant)
+static int tune_knob(const char *name, int def) {
+  const char *v = getenv(name);
+  return v && *v ? atoi(v) : def;
+}
+
 // grid = the blocks of `kern` that fit on the device at once (cached per slot)
 template <class K>
-static uint32_t resident_blocks(Workspace &ws, int slot, K kern) {
-  if (!ws.resident[slot]) {
+static uint32_t resident_blocks(Workspace &ws, int, K kern) {
+  uint32_t &slot_v = ws.resident[reinterpret_cast<const void *>(kern)];
+  if (!slot_v) {
     int dev = 0, cus = 0, per = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, kBigThreads, 0) != hipSuccess || per < 1)
       per = 2, cus = 256;
-    ws.resident[slot] = (uint32_t)(per * cus);
+    slot_v = (uint32_t)(per * cus);
   }
-  return ws.resident[slot];
+  return slot_v;
 }
 
 // counts (n) -> exclusive offsets (u64, n + 1)
@@ -1078,20 +1086,28 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   o.ctr = (Counters *)ws.ptr(W::kCounters);
   // the big-topic list reuses the DFS list's tail? no: its own region after the record array
   const int walk_g = ws.walk_lanes;
-  const uint32_t per_block = kWalkWaves * (kWave / walk_g);
-  const uint32_t walk_blocks = std::max<uint32_t>(
-      1, std::min<uint32_t>((n + per_block - 1) / per_block,
-                            walk_g == 4 ? resident_blocks(ws, 3, k_walk<4>) : walk_g == 8 ? resident_blocks(ws, 3, k_walk<8>) : resident_blocks(ws, 4, k_walk<16>)));
-
+  const int walk_occ = tune_knob("MQM_WALK_OCC", 0);
   HIP_TRY(hipMemsetAsync(o.ctr, 0, sizeof(Counters), st));
   mark(ws, 0, st);
   if (n > 0) {
+    auto launch_walk = [&](auto kern, int g) {
+      const uint32_t per_block = kWalkWaves * (kWave / g);
+      const uint32_t blocks =
+          std::max<uint32_t>(1, std::min<uint32_t>((n + per_block - 1) / per_block, resident_blocks(ws, 0, kern)));
+      hipLaunchKernelGGL(kern, dim3(blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o);
+    };
     if (walk_g == 4)
-      hipLaunchKernelGGL(k_walk<4>, dim3(walk_blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o);
-    else if (walk_g == 8)
-      hipLaunchKernelGGL(k_walk<8>, dim3(walk_blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o);
+      launch_walk(k_walk<4, 1>, 4);
+    else if (walk_g == 16)
+      launch_walk(k_walk<16, 1>, 16);
+    else if (walk_occ == 5)
+      launch_walk(k_walk<8, 5>, 8);
+    else if (walk_occ == 6)
+      launch_walk(k_walk<8, 6>, 8);
+    else if (walk_occ == 8)
+      launch_walk(k_walk<8, 8>, 8);
     else
-      hipLaunchKernelGGL(k_walk<16>, dim3(walk_blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o);
+      launch_walk(k_walk<8, 1>, 8);
   }
   HIP_TRY(hipGetLastError());
   mark(ws, 1, st);
@@ -1156,11 +1172,23 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
     HIP_TRY(hipcub::DeviceSelect::If(ws.ptr(W::kScanTmp), tmp, it, list_s, &o.ctr->n_small, n,
                                      IsSmallClass{o.cls, o.hcount}, st));
     HIP_TRY(hipcub::DeviceSelect::If(ws.ptr(W::kScanTmp), tmp, it, list_b, &o.ctr->n_bigc, n, IsBigClass{o.cls}, st));
-    hipLaunchKernelGGL(k_emit<16>, dim3(resident_blocks(ws, 2, k_emit<16>)), dim3(kWave * kEmitWaves), 0, st, s, o,
-                       list_s, &o.ctr->n_small);
+    auto launch_emit = [&](auto kern, const uint32_t *list, const unsigned int *cnt) {
+      hipLaunchKernelGGL(kern, dim3(resident_blocks(ws, 0, kern)), dim3(kWave * kEmitWaves), 0, st, s, o, list, cnt);
+    };
+    const int e16 = tune_knob("MQM_EMIT16_OCC", 0), e64 = tune_knob("MQM_EMIT64_OCC", 0);
+    if (e16 == 6)
+      launch_emit(k_emit<16, 6>, list_s, &o.ctr->n_small);
+    else if (e16 == 8)
+      launch_emit(k_emit<16, 8>, list_s, &o.ctr->n_small);
+    else
+      launch_emit(k_emit<16, 1>, list_s, &o.ctr->n_small);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_emit<64>, dim3(resident_blocks(ws, 6, k_emit<64>)), dim3(kWave * kEmitWaves), 0, st, s, o,
-                       list_b, &o.ctr->n_bigc);
+    if (e64 == 6)
+      launch_emit(k_emit<64, 6>, list_b, &o.ctr->n_bigc);
+    else if (e64 == 8)
+      launch_emit(k_emit<64, 8>, list_b, &o.ctr->n_bigc);
+    else
+      launch_emit(k_emit<64, 1>, list_b, &o.ctr->n_bigc);
     HIP_TRY(hipGetLastError());
     if (ws.get(W::kOvfList, sizeof(uint32_t) * (n + 1))) return -2;
     auto *ovf = (uint32_t *)ws.ptr(W::kOvfList);

@@ -14,7 +14,7 @@ import os
 import sys
 
 root, batches = sys.argv[1], int(sys.argv[2])
-KERNELS = ("k_walk", "k_small", "k_big", "k_dfs", "k_table_sizes")
+KERNELS = ("k_walk", "k_emit", "k_multi", "k_dfs", "k_table_sizes")
 
 
 def total(counter):
