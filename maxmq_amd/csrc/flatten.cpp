@@ -130,7 +130,7 @@ int flatten(const Store &st, HostSnapshot *out) {
     for (auto it = lits.rbegin(); it != lits.rend(); ++it) stack.push_back(*it);
   }
   const uint64_t nn = order.size();
-  if (nn >= (1ull << 31)) return MQM_ELIMIT;
+  if (nn >= (1ull << 30)) return MQM_ELIMIT;  // k_walk packs node id << 2 | item kind
 
   // 2. descriptors, subscription ranges, flags
   hs.nodes.resize(nn);
@@ -209,6 +209,11 @@ int flatten(const Store &st, HostSnapshot *out) {
     d.hsub_cnt = d.hash != kNone ? hs.nodes[d.hash].sub_cnt : 0;
     d.multi = std::min<uint32_t>(own_multi[i], 0xFFFF) | (std::min<uint32_t>(hm, 0xFFFF) << 16);
     if (own_multi[i] >= 0xFFFF || hm >= 0xFFFF) d.sh_cnt_flags |= (uint32_t)kFlagMultiSat << 24;
+    if (i > 0 && d.hash != kNone) {  // root: its '#' child is dollar-wild, unlike the root itself
+      const NodeDesc &h = hs.nodes[d.hash];
+      if (!((h.sh_cnt_flags >> 24) & kFlagHasChildren) && (h.sh_cnt_flags & kShCntMask) == 0)
+        d.sh_cnt_flags |= (uint32_t)kFlagHashLeaf << 24;
+    }
   }
 
   // 3. literal edges -> open-addressed table of 128-B buckets, linear probing

@@ -76,12 +76,16 @@ constexpr int kSmallMulti = 192;         // multi entries it holds (load <= 0.75
 constexpr int kBigThreads = 256;
 constexpr int kBigMax = 3072;            // multi entries per bounded topic (k_multi's last tier)
 constexpr uint32_t kNoWhy = 0xFFFFFFFFu;
-constexpr uint32_t kNoLit = 0x80000000u;   // frontier node id flag: no literal child (node ids < 2^31)
+constexpr int kICap = 3 * kFCap;         // load items per level (<= 3 per frontier node)
 
 static_assert(kRecStrideAlloc % 4 == 0 && kRecStrideAlloc >= kRecStride, "16-B aligned records");
 static_assert(kSmallMulti * 4 <= kSmallSlots * 3, "k_emit table load factor");
 static_assert(kBigMax * 4 <= 4096 * 3 && kBigMax <= 12 * kBigThreads, "the last k_multi tier holds every bounded topic");
 static_assert(kSmallMulti % kWave == 0, "register tiles");
+
+// a load item of the walk: the literal-child probe of a frontier node, or the
+// descriptor load of its '+' / '#' child
+enum : uint32_t { kItemLit = 0, kItemPlus = 1, kItemHash = 2 };
 
 enum : uint8_t { kClsDone = 0, kClsSmall = 1, kClsBig = 2, kClsDfs = 3 };
 enum : uint32_t { kWhyFrontier = 0, kWhyHits = 1, kWhyLevels = 2, kWhyShared = 3, kWhyEntries = 4 };
@@ -112,7 +116,7 @@ struct Outputs {
 
 struct TopicLds {              // k_walk context of one topic (one 16-lane group)
   uint32_t sep[kLMax];         // position of the '/' ending level k
-  uint32_t front[2][3][kFCap]; // (node, plus, hash) of the frontier
+  uint32_t item[2][kICap];     // the level's load items: node id << 2 | kind (kItem*)
   uint8_t stage[kStage];       // the topic's first kStage bytes
 };
 
@@ -290,18 +294,27 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
         my_k1[j] = k.k1;
       }
     }
-    if (gl == 0) {  // frontier node ids carry kNoLit when no child is a literal
-      L.front[0][0][0] = ((root.sh_cnt_flags >> 24) & kFlagHasLiteral) ? 0u : kNoLit;
-      L.front[0][1][0] = root.plus;
-      L.front[0][2][0] = root.hash;
+    // level 0's items: the root's literal probe, '+' and '#' children
+    if (gl == 0) {
+      uint32_t k = 0;
+      if ((root.sh_cnt_flags >> 24) & kFlagHasLiteral) L.item[0][k++] = (0u << 2) | kItemLit;
+      if (root.plus != kNone) L.item[0][k++] = (root.plus << 2) | kItemPlus;
+      if (root.hash != kNone) L.item[0][k++] = (root.hash << 2) | kItemHash;
     }
+    const uint32_t root_items = (((root.sh_cnt_flags >> 24) & kFlagHasLiteral) ? 1u : 0u) +
+                                (root.plus != kNone ? 1u : 0u) + (root.hash != kNone ? 1u : 0u);
     wave_lds_sync();
 
     // ---- 2. walk ----------------------------------------------------------
+    // Level-synchronous over compact item lists: a node pushed to the next
+    // level enqueues only the loads it needs (its literal probe if it has a
+    // literal child, its '+' child, its '#' child unless kFlagHashLeaf lets
+    // the '#' child's gather be recorded at push time: partKey '#' of the
+    // next level, topics.go:503-505, rank 2 * '#' child).
     uint32_t *rec = o.recs + (uint64_t)(active ? t : 0) * kRecStrideAlloc;
-    uint32_t nf = nlev > 0 ? 1 : 0, nh = 0, nsh = 0, Ss = 0, Ms = 0, H = 0;
+    uint32_t ni = nlev > 0 ? root_items : 0, nh = 0, nsh = 0, Ss = 0, Ms = 0, H = 0;
     int cur = 0;
-    for (uint32_t d = 0; d < nlev && nf > 0; d++) {
+    for (uint32_t d = 0; d < nlev && ni > 0; d++) {
       if (d >= (uint32_t)kLMax) {
         why = kWhyLevels;
         break;
@@ -318,39 +331,49 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
       const uint32_t tst = d == 0 ? 0 : L.sep[d - 1] + 1;
       const uint32_t tln = ((d < nsep) ? L.sep[d] : len) - tst;
       uint32_t nnext = 0;
-      for (uint32_t base = 0; base < nf * 3; base += kG) {
-        const uint32_t item = base + gl;
-        const bool live = item < nf * 3;
-        const uint32_t fi = live ? item / 3 : 0, type = item % 3;
-        const uint32_t node = L.front[cur][0][fi], wc = L.front[cur][type == 2 ? 2 : 1][fi];
+      for (uint32_t base = 0; base < ni; base += kG) {
+        const uint32_t it = base + gl;
+        const bool live = it < ni;
+        const uint32_t iw = L.item[cur][live ? it : 0];
+        const uint32_t kind = iw & 3u, id = iw >> 2;
         NodeDesc dc;
-        const uint32_t c = walk_step(s, live && type == 0 && !lit_is_wild && !(node & kNoLit),
-                                     live && type != 0 && wc != kNone, node & ~kNoLit, wc, k0, k1, tp + tst, tln,
-                                     &dc);
+        const uint32_t c = walk_step(s, live && kind == kItemLit && !lit_is_wild, live && kind != kItemLit, id, id,
+                                     k0, k1, tp + tst, tln, &dc);
         const bool found = c != kNone;
         const uint32_t fl = found ? dc.sh_cnt_flags >> 24 : 0;
         const bool skip_dollar = dollar && (fl & kFlagDollarWild);  // topics.go:527
         const uint32_t c_own = found && !skip_dollar ? dc.sub_cnt : 0;
-        const uint32_t c_par = found && type == 0 && !skip_dollar ? dc.hsub_cnt : 0;  // topics.go:507-509
+        const uint32_t c_par = found && kind == kItemLit && !skip_dollar ? dc.hsub_cnt : 0;  // topics.go:507-509
         const uint32_t c_sh = found ? dc.sh_cnt_flags & kShCntMask : 0;
         const bool push = found && has_next && (fl & kFlagHasChildren);
+        const bool leaf = push && (fl & kFlagHashLeaf);
+        // the '#' child's gather at the next level ('$' flag = this node's)
+        const uint32_t c_hl = leaf && !skip_dollar ? dc.hsub_cnt : 0;
+        const uint32_t n_items = push ? (((fl & kFlagHasLiteral) ? 1u : 0u) + (dc.plus != kNone ? 1u : 0u) +
+                                         (dc.hash != kNone && !leaf ? 1u : 0u))
+                                      : 0u;
         const uint32_t m_own = (uint32_t)(__ballot(c_own > 0) >> gbase) & kGMask;
         const uint32_t m_par = (uint32_t)(__ballot(c_par > 0) >> gbase) & kGMask;
+        const uint32_t m_hl = (uint32_t)(__ballot(c_hl > 0) >> gbase) & kGMask;
         const uint32_t m_sh = (uint32_t)(__ballot(c_sh > 0) >> gbase) & kGMask;
-        const uint32_t m_push = (uint32_t)(__ballot(push) >> gbase) & kGMask;
-        const uint32_t n_own = __popc(m_own), n_par = __popc(m_par);
-        if (nh + n_own + n_par > (uint32_t)kHCap) why = kWhyHits;
+        const uint32_t n_own = __popc(m_own), n_par = __popc(m_par), n_hl = __popc(m_hl);
+        uint32_t t_items;
+        const uint32_t x_items = group_scan_ex<kG>(n_items, gl, &t_items, gbase);
+        if (nh + n_own + n_par + n_hl > (uint32_t)kHCap) why = kWhyHits;
         if (nsh + __popc(m_sh) > (uint32_t)kShCap) why = kWhyShared;
-        if (nnext + __popc(m_push) > (uint32_t)kFCap) why = kWhyFrontier;
-        if ((uint32_t)(__ballot((c_own | c_par) && (fl & kFlagMultiSat)) >> gbase) & kGMask) why = kWhyEntries;
+        if (nnext + t_items > (uint32_t)kICap) why = kWhyFrontier;
+        if ((uint32_t)(__ballot((c_own | c_par | c_hl) && (fl & kFlagMultiSat)) >> gbase) & kGMask) why = kWhyEntries;
         if (why != kNoWhy) break;
-        // solo / multi split of the two ranges (multi entries sit at the end)
+        // solo / multi split of the ranges (multi entries sit at the end)
         const uint32_t mu_own = c_own ? (dc.multi & 0xFFFFu) : 0, mu_par = c_par ? (dc.multi >> 16) : 0;
-        uint32_t ts_own, ts_par, tm_own, tm_par;
+        const uint32_t mu_hl = c_hl ? (dc.multi >> 16) : 0;
+        uint32_t ts_own, ts_par, ts_hl, tm_own, tm_par, tm_hl;
         const uint32_t xs_own = group_scan_ex<kG>(c_own - mu_own, gl, &ts_own, gbase);
         const uint32_t xs_par = group_scan_ex<kG>(c_par - mu_par, gl, &ts_par, gbase);
+        const uint32_t xs_hl = group_scan_ex<kG>(c_hl - mu_hl, gl, &ts_hl, gbase);
         const uint32_t xm_own = group_scan_ex<kG>(mu_own, gl, &tm_own, gbase);
         const uint32_t xm_par = group_scan_ex<kG>(mu_par, gl, &tm_par, gbase);
+        const uint32_t xm_hl = group_scan_ex<kG>(mu_hl, gl, &tm_hl, gbase);
         if (active && c_own) {
           uint32_t *hr = rec + 4 + kRecHit * (nh + __popc(m_own & gmask_lt));
           hr[kFieldOff] = dc.sub_off;
@@ -365,30 +388,38 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
           hr[kFieldMpre] = Ms + tm_own + xm_par;
           hr[kFieldRank] = 2 * c + 1;
         }
+        if (active && c_hl) {
+          uint32_t *hr = rec + 4 + kRecHit * (nh + n_own + n_par + __popc(m_hl & gmask_lt));
+          hr[kFieldOff] = dc.sub_off + dc.sub_cnt;
+          hr[kFieldSpre] = Ss + ts_own + ts_par + xs_hl;
+          hr[kFieldMpre] = Ms + tm_own + tm_par + xm_hl;
+          hr[kFieldRank] = 2 * dc.hash;
+        }
         if (active && c_sh) {
           const uint32_t i = nsh + __popc(m_sh & gmask_lt);
           rec[kRecSh + 2 * i] = dc.sh_off;
           rec[kRecSh + 1 + 2 * i] = c_sh;
         }
         if (push) {
-          const uint32_t i = nnext + __popc(m_push & gmask_lt);
-          L.front[cur ^ 1][0][i] = c | ((fl & kFlagHasLiteral) ? 0u : kNoLit);
-          L.front[cur ^ 1][1][i] = dc.plus;
-          L.front[cur ^ 1][2][i] = dc.hash;
+          uint32_t *nx = &L.item[cur ^ 1][nnext + x_items];
+          uint32_t k = 0;
+          if (fl & kFlagHasLiteral) nx[k++] = (c << 2) | kItemLit;
+          if (dc.plus != kNone) nx[k++] = (dc.plus << 2) | kItemPlus;
+          if (dc.hash != kNone && !leaf) nx[k++] = (dc.hash << 2) | kItemHash;
         }
         uint32_t t_sh;
         (void)group_scan_ex<kG>(c_sh, gl, &t_sh, gbase);
-        nh += n_own + n_par;
+        nh += n_own + n_par + n_hl;
         nsh += __popc(m_sh);
-        nnext += __popc(m_push);
-        Ss += ts_own + ts_par;
-        Ms += tm_own + tm_par;
+        nnext += t_items;
+        Ss += ts_own + ts_par + ts_hl;
+        Ms += tm_own + tm_par + tm_hl;
         H += t_sh;
       }
       wave_lds_sync();
       if (why != kNoWhy) break;
       cur ^= 1;
-      nf = nnext;
+      ni = nnext;
     }
     const uint32_t S = Ss + Ms;
     if (why == kNoWhy && (S > kSMax || Ms > (uint32_t)kBigMax)) why = kWhyEntries;
@@ -1027,12 +1058,6 @@ static float elapsed(Workspace &ws, int a, int b) {
   return ms;
 }
 
-// tuning knob from the environment (read per batch; 0 = default variant)
-static int tune_knob(const char *name, int def) {
-  const char *v = getenv(name);
-  return v && *v ? atoi(v) : def;
-}
-
 // grid = the blocks of `kern` that fit on the device at once (cached per slot)
 template <class K>
 static uint32_t resident_blocks(Workspace &ws, int, K kern) {
@@ -1086,7 +1111,6 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   o.ctr = (Counters *)ws.ptr(W::kCounters);
   // the big-topic list reuses the DFS list's tail? no: its own region after the record array
   const int walk_g = ws.walk_lanes;
-  const int walk_occ = tune_knob("MQM_WALK_OCC", 0);
   HIP_TRY(hipMemsetAsync(o.ctr, 0, sizeof(Counters), st));
   mark(ws, 0, st);
   if (n > 0) {
@@ -1100,12 +1124,6 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
       launch_walk(k_walk<4, 1>, 4);
     else if (walk_g == 16)
       launch_walk(k_walk<16, 1>, 16);
-    else if (walk_occ == 5)
-      launch_walk(k_walk<8, 5>, 8);
-    else if (walk_occ == 6)
-      launch_walk(k_walk<8, 6>, 8);
-    else if (walk_occ == 8)
-      launch_walk(k_walk<8, 8>, 8);
     else
       launch_walk(k_walk<8, 1>, 8);
   }
@@ -1175,20 +1193,11 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
     auto launch_emit = [&](auto kern, const uint32_t *list, const unsigned int *cnt) {
       hipLaunchKernelGGL(kern, dim3(resident_blocks(ws, 0, kern)), dim3(kWave * kEmitWaves), 0, st, s, o, list, cnt);
     };
-    const int e16 = tune_knob("MQM_EMIT16_OCC", 0), e64 = tune_knob("MQM_EMIT64_OCC", 0);
-    if (e16 == 6)
-      launch_emit(k_emit<16, 6>, list_s, &o.ctr->n_small);
-    else if (e16 == 8)
-      launch_emit(k_emit<16, 8>, list_s, &o.ctr->n_small);
-    else
-      launch_emit(k_emit<16, 1>, list_s, &o.ctr->n_small);
+    // (amdgpu_waves_per_eu 6 / 8 variants of both spill and measured slower:
+    // profiles/r01/c3_v6_occupancy_sweep.log)
+    launch_emit(k_emit<16, 1>, list_s, &o.ctr->n_small);
     HIP_TRY(hipGetLastError());
-    if (e64 == 6)
-      launch_emit(k_emit<64, 6>, list_b, &o.ctr->n_bigc);
-    else if (e64 == 8)
-      launch_emit(k_emit<64, 8>, list_b, &o.ctr->n_bigc);
-    else
-      launch_emit(k_emit<64, 1>, list_b, &o.ctr->n_bigc);
+    launch_emit(k_emit<64, 1>, list_b, &o.ctr->n_bigc);
     HIP_TRY(hipGetLastError());
     if (ws.get(W::kOvfList, sizeof(uint32_t) * (n + 1))) return -2;
     auto *ovf = (uint32_t *)ws.ptr(W::kOvfList);

@@ -20,6 +20,10 @@ enum : uint32_t {
                           // == the `$` rule's Filter[0] test (topics.go:527)
   kFlagHasLiteral = 4u,   // some child is a literal (else the edge probe is skipped)
   kFlagMultiSat = 8u,     // a multi count in NodeDesc::multi saturated (topics -> DFS path)
+  kFlagHashLeaf = 16u,    // the '#' child exists, has no children and no shared subscriptions:
+                          //   everything its gather needs is in this descriptor (its range
+                          //   follows this node's, its multi count is multi >> 16, its `$`
+                          //   flag equals this node's), so the walk records it without a load
 };
 
 struct NodeDesc {         // 32 B
