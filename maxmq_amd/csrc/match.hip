@@ -202,15 +202,40 @@ __device__ __forceinline__ uint32_t table_find(const uint32_t *tkey, uint32_t ma
 // topics stay in flight per CU.  Hits go straight to the topic's record with
 // their rank (= 2 * node + slot, the reference's emission order).
 // ---------------------------------------------------------------------------
-template <int kG>
-__device__ __forceinline__ uint32_t group_scan_ex(uint32_t v, int gl, uint32_t *total, int gbase) {
-  uint32_t inc = v;
-  for (int d = 1; d < kG; d <<= 1) {
-    const uint32_t u = __shfl_up(inc, d, kG);
-    if (gl >= d) inc += u;
+// A record's hits carry per-hit solo / multi entry counts (fields 1, 2, as
+// k_walk wrote them); its readers turn them into exclusive prefixes in LDS
+// (find_hits searches those).  A group of kL aligned lanes (kL <= 64, a power
+// of two) converts hits 0 .. nh - 1.
+template <int kL>
+__device__ __forceinline__ void rec_prefix(uint32_t *rec, uint32_t nh, int gl) {
+  constexpr int kP = (kHCap + kL - 1) / kL;
+  uint32_t sc[kP], mc[kP], ss = 0, ms = 0;
+#pragma unroll
+  for (int p = 0; p < kP; p++) {
+    const uint32_t h = gl * kP + p;
+    sc[p] = h < nh ? rec[4 + kRecHit * h + kFieldSpre] : 0;
+    mc[p] = h < nh ? rec[4 + kRecHit * h + kFieldMpre] : 0;
+    ss += sc[p];
+    ms += mc[p];
   }
-  *total = __shfl(inc, gbase + kG - 1, 64);
-  return inc - v;
+  uint32_t si = ss, mi = ms;
+#pragma unroll
+  for (int d = 1; d < kL; d <<= 1) {
+    const uint32_t us = __shfl_up(si, d, kL), um = __shfl_up(mi, d, kL);
+    if (gl >= d) si += us, mi += um;
+  }
+  si -= ss;
+  mi -= ms;
+#pragma unroll
+  for (int p = 0; p < kP; p++) {
+    const uint32_t h = gl * kP + p;
+    if (h < nh) {
+      rec[4 + kRecHit * h + kFieldSpre] = si;
+      rec[4 + kRecHit * h + kFieldMpre] = mi;
+    }
+    si += sc[p];
+    mi += mc[p];
+  }
 }
 
 // kG lanes per topic (8 or 16), kWave / kG topics per wavefront
@@ -312,7 +337,8 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
     // the '#' child's gather be recorded at push time: partKey '#' of the
     // next level, topics.go:503-505, rank 2 * '#' child).
     uint32_t *rec = o.recs + (uint64_t)(active ? t : 0) * kRecStrideAlloc;
-    uint32_t ni = nlev > 0 ? root_items : 0, nh = 0, nsh = 0, Ss = 0, Ms = 0, H = 0;
+    uint32_t ni = nlev > 0 ? root_items : 0, nh = 0, nsh = 0;
+    uint32_t ls = 0, lm = 0, lh = 0;  // this lane's solo / multi / shared entries
     int cur = 0;
     for (uint32_t d = 0; d < nlev && ni > 0; d++) {
       if (d >= (uint32_t)kLMax) {
@@ -356,71 +382,65 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
         const uint32_t m_par = (uint32_t)(__ballot(c_par > 0) >> gbase) & kGMask;
         const uint32_t m_hl = (uint32_t)(__ballot(c_hl > 0) >> gbase) & kGMask;
         const uint32_t m_sh = (uint32_t)(__ballot(c_sh > 0) >> gbase) & kGMask;
+        const uint32_t m_i0 = (uint32_t)(__ballot(n_items & 1u) >> gbase) & kGMask;
+        const uint32_t m_i1 = (uint32_t)(__ballot(n_items & 2u) >> gbase) & kGMask;
         const uint32_t n_own = __popc(m_own), n_par = __popc(m_par), n_hl = __popc(m_hl);
-        uint32_t t_items;
-        const uint32_t x_items = group_scan_ex<kG>(n_items, gl, &t_items, gbase);
+        const uint32_t t_items = __popc(m_i0) + 2 * __popc(m_i1);
         if (nh + n_own + n_par + n_hl > (uint32_t)kHCap) why = kWhyHits;
         if (nsh + __popc(m_sh) > (uint32_t)kShCap) why = kWhyShared;
         if (nnext + t_items > (uint32_t)kICap) why = kWhyFrontier;
-        if ((uint32_t)(__ballot((c_own | c_par | c_hl) && (fl & kFlagMultiSat)) >> gbase) & kGMask) why = kWhyEntries;
+        // a saturated multi count, or a range past the bounded path's entries
+        // (also keeps the per-lane sums below from overflowing)
+        if ((uint32_t)(__ballot(((c_own | c_par | c_hl) && (fl & kFlagMultiSat)) ||
+                                max(c_own, max(c_par, c_hl)) > kSMax) >> gbase) & kGMask)
+          why = kWhyEntries;
         if (why != kNoWhy) break;
-        // solo / multi split of the ranges (multi entries sit at the end)
+        // solo / multi split of the ranges (multi entries sit at the end); the
+        // record keeps per-hit counts, its readers turn them into prefixes
         const uint32_t mu_own = c_own ? (dc.multi & 0xFFFFu) : 0, mu_par = c_par ? (dc.multi >> 16) : 0;
         const uint32_t mu_hl = c_hl ? (dc.multi >> 16) : 0;
-        uint32_t ts_own, ts_par, ts_hl, tm_own, tm_par, tm_hl;
-        const uint32_t xs_own = group_scan_ex<kG>(c_own - mu_own, gl, &ts_own, gbase);
-        const uint32_t xs_par = group_scan_ex<kG>(c_par - mu_par, gl, &ts_par, gbase);
-        const uint32_t xs_hl = group_scan_ex<kG>(c_hl - mu_hl, gl, &ts_hl, gbase);
-        const uint32_t xm_own = group_scan_ex<kG>(mu_own, gl, &tm_own, gbase);
-        const uint32_t xm_par = group_scan_ex<kG>(mu_par, gl, &tm_par, gbase);
-        const uint32_t xm_hl = group_scan_ex<kG>(mu_hl, gl, &tm_hl, gbase);
         if (active && c_own) {
           uint32_t *hr = rec + 4 + kRecHit * (nh + __popc(m_own & gmask_lt));
-          hr[kFieldOff] = dc.sub_off;
-          hr[kFieldSpre] = Ss + xs_own;
-          hr[kFieldMpre] = Ms + xm_own;
-          hr[kFieldRank] = 2 * c;
+          *reinterpret_cast<uint4 *>(hr) = make_uint4(dc.sub_off, c_own - mu_own, mu_own, 2 * c);
         }
-        if (active && c_par) {
+        if (active && c_par) {  // the '#' child's range follows (snapshot.h)
           uint32_t *hr = rec + 4 + kRecHit * (nh + n_own + __popc(m_par & gmask_lt));
-          hr[kFieldOff] = dc.sub_off + dc.sub_cnt;  // the '#' child's range follows (snapshot.h)
-          hr[kFieldSpre] = Ss + ts_own + xs_par;
-          hr[kFieldMpre] = Ms + tm_own + xm_par;
-          hr[kFieldRank] = 2 * c + 1;
+          *reinterpret_cast<uint4 *>(hr) = make_uint4(dc.sub_off + dc.sub_cnt, c_par - mu_par, mu_par, 2 * c + 1);
         }
         if (active && c_hl) {
           uint32_t *hr = rec + 4 + kRecHit * (nh + n_own + n_par + __popc(m_hl & gmask_lt));
-          hr[kFieldOff] = dc.sub_off + dc.sub_cnt;
-          hr[kFieldSpre] = Ss + ts_own + ts_par + xs_hl;
-          hr[kFieldMpre] = Ms + tm_own + tm_par + xm_hl;
-          hr[kFieldRank] = 2 * dc.hash;
+          *reinterpret_cast<uint4 *>(hr) = make_uint4(dc.sub_off + dc.sub_cnt, c_hl - mu_hl, mu_hl, 2 * dc.hash);
         }
         if (active && c_sh) {
           const uint32_t i = nsh + __popc(m_sh & gmask_lt);
-          rec[kRecSh + 2 * i] = dc.sh_off;
-          rec[kRecSh + 1 + 2 * i] = c_sh;
+          *reinterpret_cast<uint2 *>(rec + kRecSh + 2 * i) = make_uint2(dc.sh_off, c_sh);
         }
         if (push) {
-          uint32_t *nx = &L.item[cur ^ 1][nnext + x_items];
+          uint32_t *nx = &L.item[cur ^ 1][nnext + __popc(m_i0 & gmask_lt) + 2 * __popc(m_i1 & gmask_lt)];
           uint32_t k = 0;
           if (fl & kFlagHasLiteral) nx[k++] = (c << 2) | kItemLit;
           if (dc.plus != kNone) nx[k++] = (dc.plus << 2) | kItemPlus;
           if (dc.hash != kNone && !leaf) nx[k++] = (dc.hash << 2) | kItemHash;
         }
-        uint32_t t_sh;
-        (void)group_scan_ex<kG>(c_sh, gl, &t_sh, gbase);
         nh += n_own + n_par + n_hl;
         nsh += __popc(m_sh);
         nnext += t_items;
-        Ss += ts_own + ts_par + ts_hl;
-        Ms += tm_own + tm_par + tm_hl;
-        H += t_sh;
+        ls += c_own - mu_own + c_par - mu_par + c_hl - mu_hl;
+        lm += mu_own + mu_par + mu_hl;
+        lh += c_sh;
       }
       wave_lds_sync();
       if (why != kNoWhy) break;
       cur ^= 1;
       ni = nnext;
     }
+#pragma unroll
+    for (int m = kG / 2; m > 0; m >>= 1) {  // group totals
+      ls += __shfl_xor(ls, m, 64);
+      lm += __shfl_xor(lm, m, 64);
+      lh += __shfl_xor(lh, m, 64);
+    }
+    const uint32_t Ss = ls, Ms = lm, H = lh;
     const uint32_t S = Ss + Ms;
     if (why == kNoWhy && (S > kSMax || Ms > (uint32_t)kBigMax)) why = kWhyEntries;
     if (active && gl == 0) {
@@ -539,6 +559,8 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
     const uint32_t nh = w0 & 0xFFu, nsh = w0 >> 8;
     const uint32_t *grec = o.recs + (uint64_t)t * kRecStrideAlloc;
     for (uint32_t j = kWave + gl; j < 4 + kRecHit * nh; j += kE) L.rec[j] = grec[j];
+    wave_lds_sync();
+    rec_prefix<kE>(L.rec, nh, gl);
     wave_lds_sync();
     if (H) {  // shared candidates (gatherSharedSubscriptions, topics.go:541-555)
       uint32_t w = 0;
@@ -684,6 +706,8 @@ __global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs
         rec[i] = o.recs[(uint64_t)t * kRecStrideAlloc + i];
       __syncthreads();
     }
+    if (wid == 0) rec_prefix<kWave>(rec, nh, lane);
+    __syncthreads();
     if (M > kMCap) {  // block-uniform; unreachable for the tier that holds kBigMax
       if (tid == 0) ovf[atomicAdd(n_ovf, 1u)] = t;
       __syncthreads();
@@ -1197,7 +1221,7 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
     // profiles/r01/c3_v6_occupancy_sweep.log)
     launch_emit(k_emit<16, 1>, list_s, &o.ctr->n_small);
     HIP_TRY(hipGetLastError());
-    launch_emit(k_emit<64, 1>, list_b, &o.ctr->n_bigc);
+    launch_emit(k_emit<64, 5>, list_b, &o.ctr->n_bigc);
     HIP_TRY(hipGetLastError());
     if (ws.get(W::kOvfList, sizeof(uint32_t) * (n + 1))) return -2;
     auto *ovf = (uint32_t *)ws.ptr(W::kOvfList);

@@ -20,6 +20,7 @@ DELIVERY_DTYPE = np.dtype(
      ("rap", "u1"), ("rh", "u1")]
 )
 SHARED_DTYPE = np.dtype([("filter", "<u4"), ("client", "<u4"), ("qos", "u1"), ("pad", "u1", (3,))])
+IDENT_DTYPE = np.dtype([("client", "<u4"), ("filter", "<u4"), ("ident", "<i4")])
 
 
 class Stats(C.Structure):
@@ -61,6 +62,8 @@ def lib():
         L.oref_retained_len.restype = u64
         L.oref_match_counts.argtypes = [vp, vp, vp, u32, C.c_int, vp, vp, C.POINTER(Stats)]
         L.oref_match_fill.argtypes = [vp, vp, vp, u32, C.c_int, vp, vp, vp, vp]
+        L.oref_match_ident_counts.argtypes = [vp, vp, vp, u32, C.c_int, vp]
+        L.oref_match_ident_fill.argtypes = [vp, vp, vp, u32, C.c_int, vp, vp]
         L.oref_messages_counts.argtypes = [vp, vp, vp, u32, C.c_int, vp]
         L.oref_messages_fill.argtypes = [vp, vp, vp, u32, C.c_int, vp, vp]
         L.oref_isolate_particle.argtypes = [cp, u32, C.c_int, C.POINTER(u32), C.POINTER(u32)]
@@ -171,6 +174,21 @@ class OracleIndex:
         self._L.oref_match_fill(self._h, _ptr(data), _ptr(offs), n, nthreads, _ptr(doffs), _ptr(dout),
                                 _ptr(soffs), _ptr(sout))
         return doffs, dout, soffs, sout, st
+
+    def identifiers(self, data: np.ndarray, offs: np.ndarray, nthreads=1):
+        """Subscription.Identifiers of every delivery (packets.go:250-258) ->
+        (ioffs, entries IDENT_DTYPE): per topic, (client, filter, ident) sorted
+        by (client, filter)."""
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        n = len(offs) - 1
+        cnt = np.zeros(n, np.uint32)
+        self._L.oref_match_ident_counts(self._h, _ptr(data), _ptr(offs), n, nthreads, _ptr(cnt))
+        ioffs = np.zeros(n + 1, np.uint64)
+        ioffs[1:] = np.cumsum(cnt, dtype=np.uint64)
+        out = np.zeros(int(ioffs[-1]), IDENT_DTYPE)
+        self._L.oref_match_ident_fill(self._h, _ptr(data), _ptr(offs), n, nthreads, _ptr(ioffs), _ptr(out))
+        return ioffs, out
 
     def messages(self, data: np.ndarray, offs: np.ndarray, nthreads=1):
         data = np.ascontiguousarray(data, dtype=np.uint8)

@@ -587,6 +587,11 @@ typedef struct {
   /* `Subscribers.Shared`: (filter, client, qos) list, deduped at the end */
   oref_shared *sh;
   uint32_t nsh, cap_sh;
+  /* Identifiers (packets.go:250-258): every gathered (client, filter, id>0),
+   * plus the first-merged pair per client; sorted and deduped at the end */
+  oref_ident *id;
+  uint32_t nid, cap_id;
+  int want_ids;
   oref_stats st;
 } scratch;
 
@@ -601,6 +606,18 @@ static void scratch_free(scratch *s) {
   free(s->merged);
   free(s->touched);
   free(s->sh);
+  free(s->id);
+}
+
+static void push_ident(scratch *s, uint32_t client, uint32_t filter, int32_t ident) {
+  if (s->nid == s->cap_id) {
+    s->cap_id = s->cap_id ? s->cap_id * 2 : 256;
+    s->id = (oref_ident *)realloc(s->id, sizeof(oref_ident) * s->cap_id);
+  }
+  oref_ident *o = &s->id[s->nid++];
+  o->client = client;
+  o->filter = filter;
+  o->ident = ident;
 }
 
 /* gatherSubscriptions (topics.go:521-538) with Subscription.Merge
@@ -615,6 +632,8 @@ static void gather_subscriptions(const oref *x, const char *topic, const particl
     s->st.gathered++;
     if (fl > 0 && topic[0] == '$' && (f[0] == '+' || f[0] == '#')) continue; /* [MQTT-4.7.1-1/2] */
     uint32_t c = cs->client;
+    /* Merge: Identifiers[n.Filter] = n.Identifier when n.Identifier > 0 (:257-259) */
+    if (s->want_ids && sub->ident > 0) push_ident(s, c, sub->filter, sub->ident);
     if (s->stamp[c] != s->gen) {
       s->stamp[c] = s->gen;
       s->merged[c] = *sub;
@@ -686,6 +705,12 @@ static int cmp_u32(const void *a, const void *b) {
   return (x > y) - (x < y);
 }
 
+static int cmp_ident(const void *a, const void *b) {
+  const oref_ident *x = (const oref_ident *)a, *y = (const oref_ident *)b;
+  if (x->client != y->client) return (x->client > y->client) - (x->client < y->client);
+  return (x->filter > y->filter) - (x->filter < y->filter);
+}
+
 static int cmp_shared(const void *a, const void *b) {
   const oref_shared *x = (const oref_shared *)a, *y = (const oref_shared *)b;
   if (x->filter != y->filter) return (x->filter > y->filter) - (x->filter < y->filter);
@@ -701,6 +726,7 @@ static void subscribers_one(const oref *x, const char *topic, uint32_t tlen, scr
   }
   s->ntouched = 0;
   s->nsh = 0;
+  s->nid = 0;
   s->st.topics++;
   s->st.topic_bytes += tlen;
   scan_subscribers(x, topic, tlen, 0, x->root, s);
@@ -714,6 +740,21 @@ static void subscribers_one(const oref *x, const char *topic, uint32_t tlen, scr
   }
   s->st.deliveries += s->ntouched;
   s->st.shared += s->nsh;
+  if (s->want_ids) {
+    /* the first-merged subscription's pair, kept even when its id is 0
+     * (Identifiers = {s.Filter: s.Identifier}, packets.go:251-255) */
+    for (uint32_t k = 0; k < s->ntouched; k++) {
+      const sub_t *m = &s->merged[s->touched[k]];
+      push_ident(s, s->touched[k], m->filter, m->ident);
+    }
+    if (s->nid > 1) {
+      qsort(s->id, s->nid, sizeof(oref_ident), cmp_ident);
+      uint32_t w = 1;
+      for (uint32_t i = 1; i < s->nid; i++)
+        if (s->id[i].client != s->id[w - 1].client || s->id[i].filter != s->id[w - 1].filter) s->id[w++] = s->id[i];
+      s->nid = w;
+    }
+  }
 }
 
 /* ------------------------------------------------------------------------ */
@@ -730,6 +771,10 @@ typedef struct {
   const uint64_t *doffs, *soffs;
   oref_delivery *dout;
   oref_shared *sout;
+  int ids;               /* 1: identifiers counts, 2: identifiers fill */
+  uint32_t *icount;
+  const uint64_t *ioffs;
+  oref_ident *iout;
   oref_stats st;
 } job_t;
 
@@ -737,10 +782,19 @@ static void *match_worker(void *arg) {
   job_t *j = (job_t *)arg;
   scratch s;
   scratch_init(&s, j->x->clients.n);
+  s.want_ids = j->ids != 0;
   for (uint32_t i = j->lo; i < j->hi; i++) {
     const char *t = j->bytes + j->offs[i];
     uint32_t tl = (uint32_t)(j->offs[i + 1] - j->offs[i]);
     subscribers_one(j->x, t, tl, &s);
+    if (j->ids == 1) {
+      j->icount[i] = s.nid;
+      continue;
+    }
+    if (j->ids == 2) {
+      if (s.nid) memcpy(j->iout + j->ioffs[i], s.id, sizeof(oref_ident) * s.nid);
+      continue;
+    }
     if (!j->fill) {
       j->dcount[i] = s.ntouched;
       j->scount[i] = s.nsh;
@@ -822,6 +876,33 @@ int oref_match_fill(oref *x, const char *bytes, const uint64_t *offs, uint32_t n
   p.dout = dout;
   p.soffs = soffs;
   p.sout = sout;
+  run_jobs(&p, n, nthreads, match_worker, NULL);
+  return 0;
+}
+
+int oref_match_ident_counts(oref *x, const char *bytes, const uint64_t *offs, uint32_t n, int nthreads,
+                            uint32_t *icount) {
+  job_t p;
+  memset(&p, 0, sizeof(p));
+  p.x = x;
+  p.bytes = bytes;
+  p.offs = offs;
+  p.ids = 1;
+  p.icount = icount;
+  run_jobs(&p, n, nthreads, match_worker, NULL);
+  return 0;
+}
+
+int oref_match_ident_fill(oref *x, const char *bytes, const uint64_t *offs, uint32_t n, int nthreads,
+                          const uint64_t *ioffs, oref_ident *iout) {
+  job_t p;
+  memset(&p, 0, sizeof(p));
+  p.x = x;
+  p.bytes = bytes;
+  p.offs = offs;
+  p.ids = 2;
+  p.ioffs = ioffs;
+  p.iout = iout;
   run_jobs(&p, n, nthreads, match_worker, NULL);
   return 0;
 }

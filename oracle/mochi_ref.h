@@ -50,6 +50,13 @@ typedef struct {
   uint8_t pad[3];
 } oref_shared;
 
+/* one entry of a delivery's Subscription.Identifiers map (packets.go:250-258) */
+typedef struct {
+  uint32_t client;        /* the delivery's client                                */
+  uint32_t filter;        /* map key: Subscription.Filter (interned)              */
+  int32_t ident;          /* map value: Subscription.Identifier                   */
+} oref_ident;
+
 typedef struct {
   uint64_t topics;        /* N: topics matched                                    */
   uint64_t topic_bytes;   /* T                                                    */
@@ -97,6 +104,16 @@ int oref_match_counts(oref *x, const char *bytes, const uint64_t *offs, uint32_t
  * by client id, shared candidates by (filter, client). */
 int oref_match_fill(oref *x, const char *bytes, const uint64_t *offs, uint32_t n, int nthreads,
                     const uint64_t *doffs, oref_delivery *dout, const uint64_t *soffs, oref_shared *sout);
+
+/* Subscription.Identifiers of every delivery (rule M3): per topic, the
+ * (client, filter, ident) entries of all its deliveries' maps, sorted by
+ * (client, filter).  A map holds {first.Filter: first.Identifier} (even when
+ * 0) and {n.Filter: n.Identifier} for every other gathered subscription n of
+ * the client with n.Identifier > 0.  Phase 1 counts, phase 2 fills. */
+int oref_match_ident_counts(oref *x, const char *bytes, const uint64_t *offs, uint32_t n, int nthreads,
+                            uint32_t *icount);
+int oref_match_ident_fill(oref *x, const char *bytes, const uint64_t *offs, uint32_t n, int nthreads,
+                          const uint64_t *ioffs, oref_ident *iout);
 
 /* Messages() over a batch of filters (topics.go:426-480): msg_refs per filter,
  * sorted ascending (the reference's order is map iteration order). */

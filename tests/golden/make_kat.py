@@ -66,11 +66,15 @@ MERGE = [
         "topic": "a/b",
         # DFS order: 'a' literal -> parent probe a/# first, then a/b, then +/b
         "expect": {"c1": {"qos": 2, "no_local": 1, "first": "a/#", "first_ident": 7, "rap": 0, "rh": 0}},
+        # Identifiers (packets.go:251-259): {first: 7}, a/b has id 0 (not added), +/b adds 9
+        "identifiers": {"c1": {"a/#": 7, "+/b": 9}},
     },
     {
         "subs": [["c1", "+/b", 1, 0, 1, 1, 3], ["c1", "a/b", 0, 0, 0, 2, 0]],
         "topic": "a/b",
         "expect": {"c1": {"qos": 1, "no_local": 0, "first": "a/b", "first_ident": 0, "rap": 0, "rh": 2}},
+        # the first pair is kept even with Identifier 0
+        "identifiers": {"c1": {"a/b": 0, "+/b": 3}},
     },
     {
         # a/+ reached through the '+' child of a; a/b/# parent probe happens
@@ -78,6 +82,17 @@ MERGE = [
         "subs": [["c1", "a/+", 0, 0, 1, 0, 1], ["c1", "a/b/#", 1, 0, 0, 0, 2]],
         "topic": "a/b",
         "expect": {"c1": {"qos": 1, "no_local": 0, "first": "a/b/#", "first_ident": 2, "rap": 0, "rh": 0}},
+        "identifiers": {"c1": {"a/b/#": 2, "a/+": 1}},
+    },
+    {
+        # a/# and a/b/# are each gathered twice (parent probe, then the '#'
+        # child itself); c2's root '#' comes last at level 0, after a/b/#
+        "subs": [["c1", "a/#", 0, 0, 0, 0, 5], ["c1", "a/b/c", 2, 0, 0, 0, 0], ["c2", "#", 1, 0, 0, 0, 0],
+                 ["c2", "a/b/#", 0, 0, 0, 0, 4]],
+        "topic": "a/b/c",
+        "expect": {"c1": {"qos": 2, "no_local": 0, "first": "a/#", "first_ident": 5, "rap": 0, "rh": 0},
+                   "c2": {"qos": 1, "no_local": 0, "first": "a/b/#", "first_ident": 4, "rap": 0, "rh": 0}},
+        "identifiers": {"c1": {"a/#": 5}, "c2": {"a/b/#": 4}},
     },
 ]
 

@@ -61,6 +61,10 @@ def test_merge_kat(kat, impl):
                                                               first=idx.filter_name(int(r["first_filter"])),
                                                               first_ident=int(r["first_ident"]), rap=int(r["rap"]),
                                                               rh=int(r["rh"])) for r in dout}
+            ioffs, iout = idx.identifiers(s.data, s.offs)
+            ids = {}
+            for r in iout:
+                ids.setdefault(idx.client_name(int(r["client"])), {})[idx.filter_name(int(r["filter"]))] = int(r["ident"])
         else:
             idx = pyref.TopicsIndex()
             for c, f, q, nl, rap, rh, ident in case["subs"]:
@@ -68,7 +72,9 @@ def test_merge_kat(kat, impl):
             subs, _ = idx.subscribers(case["topic"])
             got = {c: dict(qos=v.qos, no_local=int(v.no_local), first=v.filter, first_ident=v.identifier,
                            rap=int(v.rap), rh=v.rh) for c, v in subs.items()}
+            ids = {c: dict(v.identifiers) for c, v in subs.items()}
         assert got == case["expect"], case
+        assert ids == case["identifiers"], case
 
 
 @pytest.mark.parametrize("impl", ["c", "py"])
@@ -121,6 +127,7 @@ def test_c_vs_python_restatements(config, nf, nt):
     c.subscribe_workload(w)
     py = _py_from_workload(w)
     doffs, dout, soffs, sout, st = c.match(w.topics.data, w.topics.offs, nthreads=4)
+    ioffs, iout = c.identifiers(w.topics.data, w.topics.offs, nthreads=4)
     assert st["deliveries"] > 0
     for i in range(nt):
         subs, shared = py.subscribers(w.topics[i])
@@ -133,6 +140,10 @@ def test_c_vs_python_restatements(config, nf, nt):
         got_sh = sorted((c.filter_name(int(r["filter"])), c.client_name(int(r["client"])))
                         for r in sout[soffs[i]:soffs[i + 1]])
         assert got_sh == exp_sh, w.topics[i]
+        exp_id = sorted((k, f, v) for k, s in subs.items() for f, v in s.identifiers.items())
+        got_id = sorted((c.client_name(int(r["client"])), c.filter_name(int(r["filter"])), int(r["ident"]))
+                        for r in iout[ioffs[i]:ioffs[i + 1]])
+        assert got_id == exp_id, w.topics[i]
 
 
 def _rand_level(rng):
