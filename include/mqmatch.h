@@ -40,6 +40,8 @@ extern "C" {
 #define MQM_ENODEV -5  /* no HIP device                                         */
 
 #define MQM_CFG_AUTOCOMMIT 1u
+/* mqm_match_batch also returns Identifiers support (mqm_result_identifiers) */
+#define MQM_CFG_IDENTIFIERS 2u
 /* device value for a host-only index: the store and its mutation API work,
  * mqm_commit / mqm_match_* return MQM_ENODEV (there is no CPU match path). */
 #define MQM_DEVICE_NONE (-1)
@@ -144,6 +146,30 @@ int mqm_subscribers(mqm_index *h, const char *topic, size_t topic_len, mqm_resul
 /* Device in / device out on `hip_stream` (hipStream_t, NULL = default stream). */
 int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t *d_topic_offsets,
                      uint32_t n_topics, void *hip_stream, mqm_device_result *out);
+
+/* ---- Subscription.Identifiers (packets.go:250-259, rule M3) -------------- */
+/* Merge gives every delivery an Identifiers map: {first.Filter:
+ * first.Identifier} (kept even when 0) plus {n.Filter: n.Identifier} for
+ * every other subscription n of the client gathered for the topic with
+ * n.Identifier > 0 (server.go:805-810 turns it into the PUBLISH's
+ * subscription identifiers).  This pass returns, per topic, the sids of the
+ * gathered non-shared subscriptions with Identifier > 0 (a subscription
+ * gathered twice — a '#' node reached by the parent probe and by '#' — may
+ * repeat); the map of delivery (topic, client) is {filter(first): ident(first)}
+ * plus {filter(s): ident(s)} for the listed s whose client is that client
+ * (resolve with mqm_result_sub_info).  Device form: for the last
+ * mqm_match_device call on the index, whose topic buffers must still hold the
+ * batch; MQM_EINVAL if there was none or a commit replaced its snapshot. */
+typedef struct {
+  uint32_t n_topics;
+  uint64_t n_idents;
+  const uint64_t *offsets; /* device, n_topics + 1 (exclusive prefix)          */
+  const uint32_t *sids;    /* device: subscription ids                         */
+} mqm_device_identifiers;
+int mqm_identifiers_device(mqm_index *h, void *hip_stream, mqm_device_identifiers *out);
+/* host form, filled by mqm_match_batch on an index created with
+ * MQM_CFG_IDENTIFIERS (MQM_EINVAL otherwise); arrays owned by the result */
+int mqm_result_identifiers(const mqm_result *r, const uint64_t **offsets, const uint32_t **sids);
 
 /* ---- reverse match: TopicsIndex.Messages (topics.go:426-480) ------------ */
 /* The message refs retained under each filter (the message_ref given to

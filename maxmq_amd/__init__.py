@@ -111,6 +111,13 @@ class BatchResult:
         ns = int(self.shared_offsets[-1]) if n else 0
         self.deliveries = arr(L.mqm_result_deliveries(handle), nd, capi.DELIVERY_DTYPE)
         self.shared = arr(L.mqm_result_shared(handle), ns, np.uint32)
+        # Identifiers support (MQM_CFG_IDENTIFIERS): per topic, the sids of the
+        # gathered subscriptions with Identifier > 0
+        self.ident_offsets = self.idents = None
+        io, ids = C.c_void_p(), C.c_void_p()
+        if n and L.mqm_result_identifiers(handle, C.byref(io), C.byref(ids)) == 0:
+            self.ident_offsets = arr(io.value, n + 1, np.uint64)
+            self.idents = arr(ids.value, int(self.ident_offsets[-1]), np.uint32)
 
     def close(self):
         if self._h:
@@ -141,18 +148,39 @@ class BatchResult:
             self._h, int(shared), subs.ctypes.data_as(C.c_void_p), len(subs), out.ctypes.data_as(C.c_void_p)))
         return out
 
+    def identifiers(self, i: int) -> dict:
+        """Topic i's Identifiers maps (packets.go:250-259) by client id:
+        {client: {filter id: identifier}}, the first-merged pair included.
+        Needs an index created with identifiers=True."""
+        if self.idents is None:
+            raise MqmError("mqm_result_identifiers", capi.MQM_EINVAL)
+        first, _, _ = capi.delivery_fields(self.deliveries["packed"][self.offsets[i]:self.offsets[i + 1]])
+        out = {}
+        if len(first):
+            for c, r in zip(self.deliveries["client"][self.offsets[i]:self.offsets[i + 1]], self.sub_infos(first)):
+                out[int(c)] = {int(r["filter"]): int(r["identifier"])}
+        sids = self.idents[self.ident_offsets[i]:self.ident_offsets[i + 1]]
+        if len(sids):
+            for r in self.sub_infos(sids):
+                out[int(r["client"])][int(r["filter"])] = int(r["identifier"])
+        return out
+
     def subscribers(self, i: int) -> Subscribers:
         """Topic i's result in the reference's Subscribers shape (names
-        resolved; Identifiers holds the first-merged filter's identifier)."""
+        resolved).  Identifiers is the full map when the index was created
+        with identifiers=True, else the first-merged filter's pair only."""
         out = Subscribers()
         first, qos, nl = capi.delivery_fields(self.deliveries["packed"][self.offsets[i]:self.offsets[i + 1]])
         clients = self.deliveries["client"][self.offsets[i]:self.offsets[i + 1]]
+        ids = self.identifiers(i) if self.idents is not None else None
         for c, f, q, n in zip(clients, first, qos, nl):
             info = self.sub_info(int(f))
             fname = self._index.filter_name(info.filter)
+            idmap = ({self._index.filter_name(k): v for k, v in ids[int(c)].items()} if ids is not None
+                     else {fname: info.identifier})
             out.subscriptions[self._index.client_name(int(c))] = Subscription(
                 fname, int(q), info.identifier, bool(n), bool(info.retain_as_published), info.retain_handling,
-                {fname: info.identifier})
+                idmap)
         for sid in self.shared[self.shared_offsets[i]:self.shared_offsets[i + 1]]:
             info = self.shared_info(int(sid))
             fname = self._index.filter_name(info.filter)
@@ -165,10 +193,13 @@ class BatchResult:
 class TopicsIndex:
     """TopicsIndex (topics.go:285) backed by the MI355X matcher."""
 
-    def __init__(self, device: int | None = 0, autocommit: bool = True):
+    def __init__(self, device: int | None = 0, autocommit: bool = True, identifiers: bool = False):
+        """identifiers=True: match_batch / subscribers also return the full
+        Subscription.Identifiers maps (an extra GPU pass per batch)."""
         L = lib()
         cfg = capi.Config(capi.MQM_DEVICE_NONE if device is None else device,
-                          capi.MQM_CFG_AUTOCOMMIT if autocommit else 0)
+                          (capi.MQM_CFG_AUTOCOMMIT if autocommit else 0) |
+                          (capi.MQM_CFG_IDENTIFIERS if identifiers else 0))
         h = C.c_void_p()
         check("mqm_create", L.mqm_create(C.byref(cfg), C.byref(h)))
         self._h = h
@@ -327,6 +358,13 @@ class TopicsIndex:
         out = capi.DeviceMessages()
         check("mqm_messages_device", lib().mqm_messages_device(
             self._h, C.c_void_p(d_bytes_ptr), C.c_void_p(d_offs_ptr), n, C.c_void_p(stream_ptr), C.byref(out)))
+        return out
+
+    def identifiers_device(self, stream_ptr: int = 0) -> capi.DeviceIdentifiers:
+        """Identifiers support for the last match_device batch (its topic
+        buffers must still hold it): per-topic sids with Identifier > 0."""
+        out = capi.DeviceIdentifiers()
+        check("mqm_identifiers_device", lib().mqm_identifiers_device(self._h, C.c_void_p(stream_ptr), C.byref(out)))
         return out
 
     def match_device(self, d_bytes_ptr: int, d_offs_ptr: int, n: int, stream_ptr: int = 0) -> capi.DeviceResult:

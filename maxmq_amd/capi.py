@@ -22,6 +22,7 @@ MQM_EHIP = -3
 MQM_ELIMIT = -4
 MQM_ENODEV = -5
 MQM_CFG_AUTOCOMMIT = 1
+MQM_CFG_IDENTIFIERS = 2
 MQM_DEVICE_NONE = -1
 
 ERRORS = {MQM_EINVAL: "EINVAL", MQM_ENOMEM: "ENOMEM", MQM_EHIP: "EHIP", MQM_ELIMIT: "ELIMIT",
@@ -36,7 +37,8 @@ EXPORTED = [
     "mqm_result_sub_infos", "mqm_result_free", "mqm_client_name", "mqm_filter_name", "mqm_num_clients", "mqm_is_valid_filter",
     "mqm_is_shared_filter", "mqm_snapshot_stats_get", "mqm_profile_enable", "mqm_profile_read", "mqm_version",
     "mqm_retain_many", "mqm_messages_batch", "mqm_messages_one", "mqm_messages_num_filters", "mqm_messages_offsets",
-    "mqm_messages_refs", "mqm_messages_free", "mqm_messages_device",
+    "mqm_messages_refs", "mqm_messages_free", "mqm_messages_device", "mqm_identifiers_device",
+    "mqm_result_identifiers",
 ]
 
 
@@ -71,6 +73,10 @@ class DeviceResult(C.Structure):
 class DeviceMessages(C.Structure):
     _fields_ = [("n_filters", C.c_uint32), ("n_refs", C.c_uint64), ("offsets", C.c_void_p), ("refs", C.c_void_p),
                 ("n_ranges", C.c_uint64), ("n_items", C.c_uint64)]
+
+
+class DeviceIdentifiers(C.Structure):
+    _fields_ = [("n_topics", C.c_uint32), ("n_idents", C.c_uint64), ("offsets", C.c_void_p), ("sids", C.c_void_p)]
 
 
 class SnapshotStats(C.Structure):
@@ -143,6 +149,8 @@ def lib():
         "mqm_messages_refs": ([vp], vp),
         "mqm_messages_free": ([vp], None),
         "mqm_messages_device": ([vp, vp, vp, u32, vp, C.POINTER(DeviceMessages)], C.c_int),
+        "mqm_identifiers_device": ([vp, vp, C.POINTER(DeviceIdentifiers)], C.c_int),
+        "mqm_result_identifiers": ([vp, C.POINTER(vp), C.POINTER(vp)], C.c_int),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

@@ -26,6 +26,7 @@ struct mqm_index {
   uint64_t snap_version = ~0ull;
   Workspace ws;
   hipStream_t stream = nullptr;
+  const GpuSnapshot *matched = nullptr;  // snapshot of the last forward match (identifiers pass)
 };
 
 struct mqm_messages {
@@ -38,6 +39,9 @@ struct mqm_result {
   std::vector<uint64_t> offsets, shared_offsets;
   std::vector<mqm_delivery> deliveries;
   std::vector<uint32_t> shared;
+  bool has_idents = false;               // MQM_CFG_IDENTIFIERS
+  std::vector<uint64_t> ident_offsets;   // n + 1
+  std::vector<uint32_t> idents;          // sids with Identifier > 0, per topic
   std::shared_ptr<const HostSnapshot> snap;
 };
 
@@ -242,6 +246,7 @@ int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t 
     MatchOutput mo;
     rc = match_device(h->snap->dev, h->ws, d_topic_bytes, d_topic_offsets, n_topics, (hipStream_t)hip_stream, &mo);
     if (rc != 0) return rc;
+    h->matched = h->snap.get();
     out->n_topics = mo.n_topics;
     out->n_deliveries = mo.n_deliveries;
     out->n_shared = mo.n_shared;
@@ -285,6 +290,10 @@ int mqm_match_batch(mqm_index *h, const char *topic_bytes, const uint64_t *topic
     MatchOutput mo;
     rc = match_device(h->snap->dev, ws, d_bytes, d_offs, n_topics, h->stream, &mo);
     if (rc != 0) return rc;
+    h->matched = h->snap.get();
+    IdentOutput io;
+    const bool want_ids = (h->cfg.flags & MQM_CFG_IDENTIFIERS) != 0;
+    if (want_ids && (rc = identifiers_device(h->snap->dev, ws, h->stream, &io)) != 0) return rc;
     DenseOutput dn;
     rc = densify(ws, mo, h->stream, &dn);
     if (rc != 0) return rc;
@@ -306,10 +315,47 @@ int mqm_match_batch(mqm_index *h, const char *topic_bytes, const uint64_t *topic
     if (mo.n_shared && hipMemcpyAsync(r->shared.data(), dn.shared, sizeof(uint32_t) * mo.n_shared,
                                       hipMemcpyDeviceToHost, h->stream) != hipSuccess)
       return MQM_EHIP;
+    if (want_ids) {
+      r->has_idents = true;
+      r->ident_offsets.resize(n_topics + 1);
+      r->idents.resize(io.n_idents);
+      if (hipMemcpyAsync(r->ident_offsets.data(), io.offsets, sizeof(uint64_t) * (n_topics + 1),
+                         hipMemcpyDeviceToHost, h->stream) != hipSuccess)
+        return MQM_EHIP;
+      if (io.n_idents && hipMemcpyAsync(r->idents.data(), io.sids, sizeof(uint32_t) * io.n_idents,
+                                        hipMemcpyDeviceToHost, h->stream) != hipSuccess)
+        return MQM_EHIP;
+    }
     if (hipStreamSynchronize(h->stream) != hipSuccess) return MQM_EHIP;
     *out = r.release();
     return MQM_OK;
   });
+}
+
+int mqm_identifiers_device(mqm_index *h, void *hip_stream, mqm_device_identifiers *out) {
+  if (!h || !out) return MQM_EINVAL;
+  return guarded([&] {
+    std::lock_guard<std::mutex> g(h->mu);
+    if (h->cfg.device == MQM_DEVICE_NONE) return MQM_ENODEV;
+    // the records of the last forward match, against the snapshot it read
+    if (!h->matched || h->matched != h->snap.get()) return MQM_EINVAL;
+    if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
+    IdentOutput io;
+    const int rc = identifiers_device(h->snap->dev, h->ws, (hipStream_t)hip_stream, &io);
+    if (rc != 0) return rc == -2 ? MQM_ENOMEM : rc == -1 ? MQM_EINVAL : MQM_EHIP;
+    out->n_topics = io.n_topics;
+    out->n_idents = io.n_idents;
+    out->offsets = io.offsets;
+    out->sids = io.sids;
+    return MQM_OK;
+  });
+}
+
+int mqm_result_identifiers(const mqm_result *r, const uint64_t **offsets, const uint32_t **sids) {
+  if (!r || !offsets || !sids || !r->has_idents) return MQM_EINVAL;
+  *offsets = r->ident_offsets.data();
+  *sids = r->idents.data();
+  return MQM_OK;
 }
 
 int mqm_messages_device(mqm_index *h, const uint8_t *d_filter_bytes, const uint64_t *d_filter_offsets,

@@ -153,7 +153,8 @@ int flatten(const Store &st, HostSnapshot *out) {
         hs.nodes[k].sub_cnt = (uint32_t)subs.size();
         for (const SubRec &s : subs) {
           hs.subs.push_back(SubEnt{s.client, (uint32_t)s.qos | ((uint32_t)(s.no_local & 1) << 2) |
-                                                 ((uint32_t)(s.rap & 1) << 3) | ((uint32_t)(s.rh & 3) << 4)});
+                                                 ((uint32_t)(s.rap & 1) << 3) | ((uint32_t)(s.rh & 3) << 4) |
+                                                 (s.ident > 0 ? kMetaIdent : 0u)});
           hs.sub_info.push_back(SubInfo{s.filter, s.client, s.ident, s.qos, s.no_local, s.rap, s.rh});
         }
         sn = st.child(sn, hash_tok);

@@ -15,7 +15,7 @@ struct Workspace {
   enum Slot {
     kSCount, kHCount, kDCount, kDStart, kHStart, kCls, kDfsList, kRecs, kCounters, kDOut, kHOut,
     kDense, kDenseShared, kDenseOffs, kDenseHOffs, kScanTmp, kRawCnt, kTabOff, kTabSize, kTable,
-    kInBytes, kInOffs, kOvfList, kOvfList2, kListS, kListB,
+    kInBytes, kInOffs, kOvfList, kOvfList2, kListS, kListB, kICount, kIStart, kIOut,
     // reverse match (retained.hip)
     kROffs, kRNLev, kRWild, kRLOff, kRFCount, kRFCur, kRLevels, kRNCount, kRNOff, kRItemF0, kRItemN0, kRItemF1,
     kRItemN1, kRChild, kRECount, kREOff, kREmit, kRPos, kRChunks, kRCOff, kROut, kRInBytes, kRInOffs, kNumSlots
@@ -32,6 +32,11 @@ struct Workspace {
   // why the last batch's DFS topics left the bounded path:
   // frontier, hits, cached levels, shared hits, raw entries
   uint32_t why[5] = {0, 0, 0, 0, 0};
+  // the last match_device call (identifiers_device works on its records)
+  bool last_valid = false;
+  uint32_t last_n = 0, last_n_dfs = 0;
+  const uint8_t *last_bytes = nullptr;
+  const uint64_t *last_offs = nullptr;
 
   // optional kernel timing (mqm_profile_*): events on the launch stream
   bool profile = false;
@@ -71,6 +76,17 @@ struct MatchOutput {
 // negative MQM_E* code.
 int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes, const uint64_t *d_offs,
                  uint32_t n, hipStream_t st, MatchOutput *out);
+
+// Identifiers support for the last match_device call on `ws` (its topic
+// buffers must still hold the batch): per topic, the sids of the gathered
+// non-shared subscriptions with Identifier > 0 (mqm_device_identifiers).
+struct IdentOutput {
+  uint32_t n_topics = 0;
+  uint64_t n_idents = 0;
+  const uint64_t *offsets = nullptr;  // device, n + 1
+  const uint32_t *sids = nullptr;     // device
+};
+int identifiers_device(const DeviceSnapshot &s, Workspace &ws, hipStream_t st, IdentOutput *out);
 
 // Dense CSR of a MatchOutput (offsets n+1, entries back to back) on `st`.
 struct DenseOutput {

@@ -112,6 +112,10 @@ struct Outputs {
   Counters *ctr;
   uint64_t *dout;
   uint32_t *hout;
+  // identifiers pass (identifiers_device): per-topic counts, starts, sids
+  uint32_t *icount;
+  uint64_t *istart;
+  uint32_t *iout;
 };
 
 struct TopicLds {              // k_walk context of one topic (one 16-lane group)
@@ -614,7 +618,8 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
 #pragma unroll
       for (int u = 0; u < kEmitU; u++) {
         const uint32_t q = base + u * kE + gl;
-        if (q < Ss) o.dout[db + q] = pack_delivery(cl[u], sid[u], meta[u] & 3u, (meta[u] >> 2) & 1u);
+        if (q < Ss)
+          o.dout[db + q] = pack_delivery(cl[u], sid[u], meta[u] & 3u, (meta[u] >> 2) & 1u);
         cl[u] = ncl[u];
         sid[u] = nsid[u];
         meta[u] = nmeta[u];
@@ -798,8 +803,8 @@ __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *
     const uint64_t off = toffs[t];
     const uint32_t len = (uint32_t)(toffs[t + 1] - off);
     const uint8_t *tp = tbytes + off;
-    const uint64_t tsz = kPhase >= 1 ? tab_off[i + 1] - tab_off[i] : 0;
-    GEnt *T = kPhase >= 1 ? tab + tab_off[i] : nullptr;
+    const uint64_t tsz = (kPhase == 1 || kPhase == 2) ? tab_off[i + 1] - tab_off[i] : 0;
+    GEnt *T = (kPhase == 1 || kPhase == 2) ? tab + tab_off[i] : nullptr;
 
     if (kPhase == 2) {
       uint32_t D = 0;
@@ -858,7 +863,7 @@ __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *
     wave_lds_sync();
 
     uint64_t S = 0;
-    uint32_t H = 0;
+    uint32_t H = 0, nid = 0;
     uint64_t hb = 0;
     if (kPhase == 1) {
       const uint32_t hn = (uint32_t)raw_h[i];  // counted by phase 0
@@ -925,6 +930,15 @@ __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *
           const uint32_t rcnt = skip_dollar ? 0 : (part ? e.hsub_cnt : e.sub_cnt);
           const uint32_t rank = 2 * cc + part;
           S += rcnt;
+          if (kPhase >= 3) {  // identifiers: the range's entries with Identifier > 0
+            for (uint32_t b0 = 0; b0 < rcnt; b0 += kWave) {
+              const uint32_t j = b0 + lane;
+              const bool has = j < rcnt && (s.subs[roff + j].meta & kMetaIdent);
+              const uint64_t m = __ballot(has);
+              if (kPhase == 4 && has) o.iout[o.istart[t] + nid + __popcll(m & lanemask_lt(lane))] = roff + j;
+              nid += (uint32_t)__popcll(m);
+            }
+          }
           if (kPhase == 1) {
             for (uint32_t j = lane; j < rcnt; j += kWave) {
               const uint32_t sid = roff + j;
@@ -962,6 +976,43 @@ __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *
       raw_cnt[i] = S;
       raw_h[i] = H;
     }
+    if (lane == 0 && kPhase == 3) o.icount[t] = nid;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_ident<P>: Subscription.Identifiers support (packets.go:250-259).  For every
+// bounded topic, the sids of the gathered non-shared entries whose Identifier
+// is > 0 (kMetaIdent), hit by hit from the walk's record (P0 counts, P1
+// writes at istart).  A node gathered twice repeats its sids; the map the
+// host builds keeps one key per filter, as the reference's does.  DFS topics
+// are handled by k_dfs<3|4>.
+// ---------------------------------------------------------------------------
+template <int kPhase>
+__global__ __launch_bounds__(256) void k_ident(DeviceSnapshot s, Outputs o, uint32_t n) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint32_t waves = gridDim.x * (blockDim.x / kWave);
+  for (uint32_t t = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave; t < n; t += waves) {
+    const uint8_t cls = o.cls[t];
+    if (cls == kClsDfs) continue;
+    uint32_t nid = 0;
+    if (cls != kClsDone) {
+      const uint32_t *rec = o.recs + (uint64_t)t * kRecStrideAlloc;
+      const uint32_t nh = rec[0] & 0xFFu;
+      const uint64_t ib = kPhase == 1 ? o.istart[t] : 0;
+      for (uint32_t h = 0; h < nh; h++) {
+        const uint4 hr = *reinterpret_cast<const uint4 *>(rec + 4 + kRecHit * h);  // off, solo, multi, rank
+        const uint32_t cnt = hr.y + hr.z;
+        for (uint32_t b0 = 0; b0 < cnt; b0 += kWave) {
+          const uint32_t j = b0 + lane;
+          const bool has = j < cnt && (s.subs[hr.x + j].meta & kMetaIdent);
+          const uint64_t m = __ballot(has);
+          if (kPhase == 1 && has) o.iout[ib + nid + __popcll(m & lanemask_lt(lane))] = hr.x + j;
+          nid += (uint32_t)__popcll(m);
+        }
+      }
+    }
+    if (kPhase == 0 && lane == 0) o.icount[t] = nid;
   }
 }
 
@@ -1160,6 +1211,11 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   HIP_TRY(hipStreamSynchronize(st));
   const uint32_t n_dfs = hc->n_dfs;
   const uint64_t s_total = hp[0], h_total = hp[1];
+  ws.last_valid = true;
+  ws.last_n = n;
+  ws.last_bytes = d_bytes;
+  ws.last_offs = d_offs;
+  ws.last_n_dfs = n_dfs;
   for (int i = 0; i < 5; i++) ws.why[i] = hc->why[i];
 
   // DFS phase 0: exact raw / shared counts size the tail regions
@@ -1282,6 +1338,55 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   out->shared_starts = o.hstart;
   out->shared_counts = o.hcount;
   out->shared = o.hout;
+  return 0;
+}
+
+int identifiers_device(const DeviceSnapshot &s, Workspace &ws, hipStream_t st, IdentOutput *out) {
+  using W = Workspace;
+  const uint32_t n = ws.last_n;
+  if (!ws.last_valid) return -1;
+  if (ws.get(W::kICount, sizeof(uint32_t) * (n + 1)) || ws.get(W::kIStart, sizeof(uint64_t) * (n + 1))) return -2;
+  Outputs o{};
+  o.cls = (uint8_t *)ws.ptr(W::kCls);
+  o.recs = (uint32_t *)ws.ptr(W::kRecs);
+  o.dfs_list = (uint32_t *)ws.ptr(W::kDfsList);
+  o.ctr = (Counters *)ws.ptr(W::kCounters);
+  o.icount = (uint32_t *)ws.ptr(W::kICount);
+  o.istart = (uint64_t *)ws.ptr(W::kIStart);
+  const uint32_t max_levels = s.height + 1;
+  const size_t fb_lds = sizeof(uint32_t) * (((max_levels + 1) & ~1u) + 4 * (2 * max_levels + 8)) +
+                        sizeof(uint64_t) * 2 * max_levels;
+  const uint32_t fb_blocks = std::max<uint32_t>(1, std::min<uint32_t>(ws.last_n_dfs, 4096));
+  const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + 3) / 4, 8192));
+  if (n > 0) {
+    hipLaunchKernelGGL(k_ident<0>, dim3(blocks), dim3(256), 0, st, s, o, n);
+    HIP_TRY(hipGetLastError());
+    if (ws.last_n_dfs) {
+      hipLaunchKernelGGL(k_dfs<3>, dim3(fb_blocks), dim3(kWave), fb_lds, st, s, ws.last_bytes, ws.last_offs, o,
+                         nullptr, nullptr, nullptr, nullptr, max_levels);
+      HIP_TRY(hipGetLastError());
+    }
+  }
+  if (scan_offsets(ws, o.icount, o.istart, n, st)) return -3;
+  uint64_t *hp = reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(ws.host_pinned) + 128);
+  HIP_TRY(hipMemcpyAsync(hp, o.istart + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  const uint64_t total = hp[0];
+  if (ws.get(W::kIOut, sizeof(uint32_t) * (total + 1))) return -2;
+  o.iout = (uint32_t *)ws.ptr(W::kIOut);
+  if (n > 0 && total > 0) {
+    hipLaunchKernelGGL(k_ident<1>, dim3(blocks), dim3(256), 0, st, s, o, n);
+    HIP_TRY(hipGetLastError());
+    if (ws.last_n_dfs) {
+      hipLaunchKernelGGL(k_dfs<4>, dim3(fb_blocks), dim3(kWave), fb_lds, st, s, ws.last_bytes, ws.last_offs, o,
+                         nullptr, nullptr, nullptr, nullptr, max_levels);
+      HIP_TRY(hipGetLastError());
+    }
+  }
+  out->n_topics = n;
+  out->n_idents = total;
+  out->offsets = o.istart;
+  out->sids = o.iout;
   return 0;
 }
 

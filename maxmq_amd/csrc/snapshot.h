@@ -59,7 +59,7 @@ constexpr uint32_t kEdgesPerBucket = 2;
 // range of a node's '#' child follows it directly.
 struct SubEnt {
   uint32_t client;
-  uint32_t meta;          // qos[1:0] | no_local[2] | rap[3] | rh[5:4] | multi[6]
+  uint32_t meta;          // qos[1:0] | no_local[2] | rap[3] | rh[5:4] | multi[6] | ident[7]
 };
 
 // meta bit 6 ("multi"): this entry may meet another entry of the same client
@@ -72,6 +72,9 @@ struct SubEnt {
 // levels are equal or one is a wildcard).  A solo entry is its client's
 // merged delivery as is.
 constexpr uint32_t kMetaMulti = 1u << 6;
+// meta bit 7: Identifier > 0 — Subscription.Merge adds the entry to the
+// client's Identifiers map (packets.go:257-259); read by the identifiers pass
+constexpr uint32_t kMetaIdent = 1u << 7;
 
 // delivery written by the matcher (one per (topic, client)):
 //   bits  0..31 client id

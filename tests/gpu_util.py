@@ -56,3 +56,36 @@ def assert_same(gpu, ref, what=""):
         i = int(bad[0]) if len(bad) else n
         raise AssertionError(f"{what}: {len(g)} vs {len(r)} rows; first difference at row {i}: "
                              f"gpu={g[i] if i < len(g) else None} ref={r[i] if i < len(r) else None}")
+
+
+IDENT = np.dtype([("topic", "<u4"), ("client", "<u4"), ("filter", "<u4"), ("ident", "<i4")])
+
+
+def canon_gpu_idents(res):
+    """Every delivery's Identifiers map as (topic, client, filter, ident) rows:
+    the first-merged pair plus the pairs of the topic's listed sids
+    (mqm_result_identifiers), one row per (topic, client, filter)."""
+    n = res.n
+    cnt = np.diff(res.offsets).astype(np.int64)
+    first, _, _ = capi.delivery_fields(res.deliveries["packed"])
+    a = np.zeros(int(cnt.sum()), IDENT)
+    a["topic"] = np.repeat(np.arange(n, dtype=np.uint32), cnt)
+    a["client"] = res.deliveries["client"]
+    info = res.sub_infos(first)
+    a["filter"], a["ident"] = info["filter"], info["identifier"]
+    icnt = np.diff(res.ident_offsets).astype(np.int64)
+    b = np.zeros(int(icnt.sum()), IDENT)
+    b["topic"] = np.repeat(np.arange(n, dtype=np.uint32), icnt)
+    binfo = res.sub_infos(res.idents)
+    b["client"], b["filter"], b["ident"] = binfo["client"], binfo["filter"], binfo["identifier"]
+    assert (binfo["identifier"] > 0).all()
+    return np.unique(np.concatenate([a, b]))
+
+
+def canon_oracle_idents(ioffs, iout):
+    n = len(ioffs) - 1
+    cnt = np.diff(ioffs).astype(np.int64)
+    a = np.zeros(int(cnt.sum()), IDENT)
+    a["topic"] = np.repeat(np.arange(n, dtype=np.uint32), cnt)
+    a["client"], a["filter"], a["ident"] = iout["client"], iout["filter"], iout["ident"]
+    return np.unique(a)

@@ -15,7 +15,7 @@ import maxmq_amd
 from maxmq_amd import capi
 from oracle import mochi_ref as pyref
 from oracle.binding import OracleIndex
-from tests.gpu_util import assert_same, canon_gpu, canon_oracle
+from tests.gpu_util import assert_same, canon_gpu, canon_gpu_idents, canon_oracle, canon_oracle_idents
 from tools import mqgen
 from tools.mqgen import Strings
 
@@ -248,3 +248,58 @@ def _dev_copy(ptr, nbytes):
                            ctypes.c_int(2))
         assert rc == 0
     return out
+
+
+# ---- Subscription.Identifiers (packets.go:250-259, rule M3) -------------------------------------
+
+def test_kat_identifiers(kat):
+    for case in kat["merge"]:
+        idx = maxmq_amd.TopicsIndex(0, identifiers=True)
+        for c, f, q, nl, rap, rh, ident in case["subs"]:
+            idx.subscribe(c, maxmq_amd.Subscription(f, q, ident, bool(nl), bool(rap), rh))
+        got = idx.subscribers(case["topic"])
+        assert {c: s.identifiers for c, s in got.subscriptions.items()} == case["identifiers"], case
+
+
+@pytest.mark.parametrize("config,overrides", [(1, {}), (5, dict(n_filters=200000, n_topics=100000))])
+def test_identifiers_vs_oracle(config, overrides):
+    w = mqgen.generate(config, **overrides)
+    idx = maxmq_amd.TopicsIndex(0, identifiers=True)
+    idx.subscribe_workload(w)
+    ora = OracleIndex()
+    ora.subscribe_workload(w)
+    res = idx.match_batch(w.topics.data, w.topics.offs)
+    g = canon_gpu_idents(res)
+    r = canon_oracle_idents(*ora.identifiers(w.topics.data, w.topics.offs, nthreads=16))
+    assert (r["ident"] > 0).sum() > 0
+    assert_same(g, r, "identifiers")
+
+
+def test_identifiers_dfs_topics_and_device_form():
+    """Topics on the unbounded (DFS) path: hubs of identified subscriptions."""
+    filters, clients, subs = [], [], []
+    for i in range(3000):  # raw entries past the bounded path: DFS
+        filters += ["hub/#", "hub/x", "+/x"]
+        clients += [f"h{i}"] * 3
+        subs += [(1, 0, 0, 0, i + 1), (0, 0, 0, 0, 0), (2, 0, 0, 0, 7)]
+    filters += ["a/#", "a/b", "#"]
+    clients += ["k", "k", "j"]
+    subs += [(0, 0, 0, 0, 3), (1, 0, 0, 0, 4), (0, 0, 0, 0, 0)]
+    topics = ["hub/x", "hub", "a/b", "a/b/c", "zz/x", "$SYS/x"]
+    idx = maxmq_amd.TopicsIndex(0, identifiers=True)
+    ora = OracleIndex()
+    for f, c, (q, nl, rap, rh, ident) in zip(filters, clients, subs):
+        idx.subscribe(c, maxmq_amd.Subscription(f, q, ident, bool(nl), bool(rap), rh))
+        ora.subscribe(c, f, q, nl, rap, rh, ident)
+    s = Strings.from_list(topics)
+    res = idx.match_batch(s.data, s.offs)
+    assert_same(canon_gpu_idents(res), canon_oracle_idents(*ora.identifiers(s.data, s.offs)), "identifiers")
+    # device form over a device-resident batch: same per-topic counts
+    import torch
+    tb = torch.from_numpy(s.data).cuda()
+    to = torch.from_numpy(s.offs.view(np.int64)).cuda()
+    r = idx.match_device(tb.data_ptr(), to.data_ptr(), len(topics))
+    assert r.n_fallback > 0
+    d = idx.identifiers_device()
+    torch.cuda.synchronize()
+    assert d.n_topics == len(topics) and d.n_idents == int(res.ident_offsets[-1])
