@@ -11,11 +11,13 @@ over filter rank), 10M-topic batch, synthetic (tools/mqgen, seed 0x4D510003).
 N > 1 (torchrun, one rank per GPU, RCCL): --mode replicas (default) gives
 every rank the full trie and its own 10M-topic batch (weak scaling, no
 data-path collective); --mode sharded splits the subscribers by client range,
-RCCL-broadcasts rank 0's batch and gathers per-topic delivery counts back.
+RCCL-broadcasts rank 0's batch, and every shard's dense per-topic lists go
+back to rank 0 over RCCL send/recv, where mqm_gather_shards lays them out as
+the node-wide CSR (all inside the timed step).
 
 Rank 0 prints ONE JSON line.  `roofline.achieved` = algorithmic bytes of the
-emit kernel (B = T + 8N + 8P + 8V + 8S + 8D, per-topic walk
-counters from the oracle on the CPU sample) / its average HIP-event time.
+match pipeline (B = T + 8N + 8P + 8V + 8S + 8D, per-topic walk
+counters from the oracle on the CPU sample) / its HIP-event time per batch.
 `cpu_baseline` = oracle/mochi_ref.c (C restatement of the reference matcher,
 kind "port") on this host's cores over a time-bounded sample of the batch.
 """
@@ -125,19 +127,36 @@ def main():
     tb = torch.from_numpy(w.topics.data).to(dev)
     to = torch.from_numpy(w.topics.offs.view(np.int64)).to(dev)
     stream = torch.cuda.current_stream(dev)
-    counts = None
-    if args.mode == "sharded" and world > 1:
-        counts = torch.zeros(n, dtype=torch.int32, device=dev)
+    sharded = args.mode == "sharded" and world > 1
+    if sharded:
+        # shard client id -> node client id, per rank (rank 0 lays the gathered
+        # lists out with them); node-wide result buffers on rank 0
+        cmaps = [torch.from_numpy(shard.client_map(w, world, r).astype(np.int32)).to(dev) for r in range(world)]
+        node = {"offs": torch.zeros(n + 1, dtype=torch.int64, device=dev), "d": None}
+        my = {"offs": torch.zeros(n + 1, dtype=torch.int64, device=dev), "d": None}
 
     def step():
-        if args.mode == "sharded" and world > 1:
+        if sharded:
             # the publish batch enters at rank 0 and is broadcast over xGMI (RCCL)
             shard.broadcast_batch(dist, tb, to, src=0)
         r = idx.match_device(tb.data_ptr(), to.data_ptr(), n, stream.cuda_stream)
-        if args.mode == "sharded" and world > 1:
-            # per-topic delivery counts of every shard, summed at rank 0
-            _dev_to_tensor(r.counts, counts)
-            shard.reduce_counts(dist, counts, dst=0)
+        if sharded:
+            # this shard's dense per-topic lists -> rank 0 (RCCL send/recv),
+            # laid out there as the node-wide CSR (mqm_gather_shards)
+            d = idx.dense_device(stream.cuda_stream)
+            nd = int(d.n_deliveries)
+            if my["d"] is None or my["d"].numel() < nd:
+                my["d"] = torch.empty(max(nd, 1), dtype=torch.int64, device=dev)
+            _dev_to_tensor(d.offsets, my["offs"])
+            _dev_to_tensor(d.deliveries, my["d"][:nd])
+            parts = shard.gather_lists(dist, my["offs"], my["d"][:nd], dst=0)
+            if rank == 0:
+                tot = sum(int(p[1].numel()) for p in parts)
+                if node["d"] is None or node["d"].numel() < tot:
+                    node["d"] = torch.empty(max(tot, 1), dtype=torch.int64, device=dev)
+                maxmq_amd.gather_shards(n, [(o.data_ptr(), dl.data_ptr(), cmaps[i].data_ptr(), cmaps[i].numel())
+                                            for i, (o, dl) in enumerate(parts)],
+                                        node["offs"].data_ptr(), node["d"].data_ptr(), stream.cuda_stream)
         return r
 
     for _ in range(args.warmup):
@@ -389,6 +408,8 @@ def _dev_to_tensor(ptr, t):
 
     hip = ctypes.CDLL("libamdhip64.so")
     nbytes = t.numel() * t.element_size()
+    if nbytes == 0:
+        return
     rc = hip.hipMemcpy(ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(ptr), ctypes.c_size_t(nbytes),
                        ctypes.c_int(3))
     if rc != 0:

@@ -171,6 +171,42 @@ int mqm_identifiers_device(mqm_index *h, void *hip_stream, mqm_device_identifier
  * MQM_CFG_IDENTIFIERS (MQM_EINVAL otherwise); arrays owned by the result */
 int mqm_result_identifiers(const mqm_result *r, const uint64_t **offsets, const uint32_t **sids);
 
+/* ---- dense device form of the last mqm_match_device result --------------- */
+/* Topic t's deliveries are deliveries[offsets[t] .. offsets[t+1]) (no gaps);
+ * same for shared.  Library-owned, valid until the next match call on the
+ * index; MQM_EINVAL if there was no device match or a commit replaced its
+ * snapshot.  Queued on hip_stream after the match. */
+typedef struct {
+  uint32_t n_topics;
+  uint64_t n_deliveries, n_shared;
+  const uint64_t *offsets;        /* device, n_topics + 1                       */
+  const mqm_delivery *deliveries; /* device                                     */
+  const uint64_t *shared_offsets; /* device, n_topics + 1                       */
+  const uint32_t *shared;         /* device                                     */
+} mqm_device_dense;
+int mqm_dense_device(mqm_index *h, void *hip_stream, mqm_device_dense *out);
+
+/* ---- subscriber-sharded node result (server.go:1232 caller) --- */
+/* Each of n_shards indexes (one per GPU) holds the subscriptions of a
+ * contiguous client range; Subscription.Merge (packets.go:250-270) is per
+ * client, so the shards' per-topic delivery sets are disjoint and final.
+ * After the shards' dense CSRs (mqm_dense_device) have been gathered onto one
+ * device (RCCL send/recv, maxmq_amd/shard.py), this lays them out as one
+ * dense CSR: topic t = shard 0's segment, shard 1's, ...; client ids go
+ * through each shard's client_map (shard client id -> node client id; NULL
+ * keeps them).  packed.first_sub stays shard-local (resolve it on the
+ * shard's index).  d_out_offsets: n_topics + 1; d_out: the sum of the
+ * shards' delivery counts.  Synchronises hip_stream; MQM_EINVAL if a client
+ * id fell outside its shard's map or n_shards is 0 or > 16. */
+typedef struct {
+  const uint64_t *offsets;        /* device, n_topics + 1                       */
+  const mqm_delivery *deliveries; /* device                                     */
+  const uint32_t *client_map;     /* device, n_map entries, or NULL             */
+  uint32_t n_map;
+} mqm_shard_part;
+int mqm_gather_shards(uint32_t n_topics, uint32_t n_shards, const mqm_shard_part *parts, void *hip_stream,
+                      uint64_t *d_out_offsets, mqm_delivery *d_out);
+
 /* ---- reverse match: TopicsIndex.Messages (topics.go:426-480) ------------ */
 /* The message refs retained under each filter (the message_ref given to
  * mqm_retain_message).  Within a filter the order is unspecified (the

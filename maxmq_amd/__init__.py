@@ -367,6 +367,12 @@ class TopicsIndex:
         check("mqm_identifiers_device", lib().mqm_identifiers_device(self._h, C.c_void_p(stream_ptr), C.byref(out)))
         return out
 
+    def dense_device(self, stream_ptr: int = 0) -> capi.DeviceDense:
+        """Dense CSR (no gaps) of the last match_device result, on the device."""
+        out = capi.DeviceDense()
+        check("mqm_dense_device", lib().mqm_dense_device(self._h, C.c_void_p(stream_ptr), C.byref(out)))
+        return out
+
     def match_device(self, d_bytes_ptr: int, d_offs_ptr: int, n: int, stream_ptr: int = 0) -> capi.DeviceResult:
         """Device-resident batch (pointers from e.g. torch tensors); the result's
         device buffers are owned by the index and valid until the next match."""
@@ -374,6 +380,17 @@ class TopicsIndex:
         check("mqm_match_device", lib().mqm_match_device(self._h, C.c_void_p(d_bytes_ptr), C.c_void_p(d_offs_ptr),
                                                          n, C.c_void_p(stream_ptr), C.byref(out)))
         return out
+
+
+def gather_shards(n_topics: int, parts, d_out_offsets_ptr: int, d_out_ptr: int, stream_ptr: int = 0):
+    """mqm_gather_shards: node-wide dense CSR of a subscriber-sharded match.
+    parts: (offsets_ptr, deliveries_ptr, client_map_ptr or 0, n_map) per shard,
+    all device pointers on the current device.  Synchronises the stream."""
+    arr = (capi.ShardPart * max(1, len(parts)))()
+    for i, (o, d, m, nm) in enumerate(parts):
+        arr[i] = capi.ShardPart(o, d, m or None, nm)
+    check("mqm_gather_shards", lib().mqm_gather_shards(n_topics, len(parts), arr, C.c_void_p(stream_ptr),
+                                                       C.c_void_p(d_out_offsets_ptr), C.c_void_p(d_out_ptr)))
 
 
 def is_valid_filter(filt: str, for_publish: bool) -> bool:

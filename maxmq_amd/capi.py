@@ -38,7 +38,7 @@ EXPORTED = [
     "mqm_is_shared_filter", "mqm_snapshot_stats_get", "mqm_profile_enable", "mqm_profile_read", "mqm_version",
     "mqm_retain_many", "mqm_messages_batch", "mqm_messages_one", "mqm_messages_num_filters", "mqm_messages_offsets",
     "mqm_messages_refs", "mqm_messages_free", "mqm_messages_device", "mqm_identifiers_device",
-    "mqm_result_identifiers",
+    "mqm_result_identifiers", "mqm_dense_device", "mqm_gather_shards",
 ]
 
 
@@ -77,6 +77,17 @@ class DeviceMessages(C.Structure):
 
 class DeviceIdentifiers(C.Structure):
     _fields_ = [("n_topics", C.c_uint32), ("n_idents", C.c_uint64), ("offsets", C.c_void_p), ("sids", C.c_void_p)]
+
+
+class DeviceDense(C.Structure):
+    _fields_ = [("n_topics", C.c_uint32), ("n_deliveries", C.c_uint64), ("n_shared", C.c_uint64),
+                ("offsets", C.c_void_p), ("deliveries", C.c_void_p), ("shared_offsets", C.c_void_p),
+                ("shared", C.c_void_p)]
+
+
+class ShardPart(C.Structure):
+    _fields_ = [("offsets", C.c_void_p), ("deliveries", C.c_void_p), ("client_map", C.c_void_p),
+                ("n_map", C.c_uint32)]
 
 
 class SnapshotStats(C.Structure):
@@ -151,6 +162,8 @@ def lib():
         "mqm_messages_device": ([vp, vp, vp, u32, vp, C.POINTER(DeviceMessages)], C.c_int),
         "mqm_identifiers_device": ([vp, vp, C.POINTER(DeviceIdentifiers)], C.c_int),
         "mqm_result_identifiers": ([vp, C.POINTER(vp), C.POINTER(vp)], C.c_int),
+        "mqm_dense_device": ([vp, vp, C.POINTER(DeviceDense)], C.c_int),
+        "mqm_gather_shards": ([u32, u32, C.POINTER(ShardPart), vp, vp, vp], C.c_int),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

@@ -14,6 +14,7 @@
 #include "flatten.h"
 #include "match.h"
 #include "retained.h"
+#include "shard.h"
 #include "store.h"
 
 using namespace mqm;
@@ -27,6 +28,7 @@ struct mqm_index {
   Workspace ws;
   hipStream_t stream = nullptr;
   const GpuSnapshot *matched = nullptr;  // snapshot of the last forward match (identifiers pass)
+  MatchOutput last_mo;                   // its segments (mqm_dense_device)
 };
 
 struct mqm_messages {
@@ -247,6 +249,7 @@ int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t 
     rc = match_device(h->snap->dev, h->ws, d_topic_bytes, d_topic_offsets, n_topics, (hipStream_t)hip_stream, &mo);
     if (rc != 0) return rc;
     h->matched = h->snap.get();
+    h->last_mo = mo;
     out->n_topics = mo.n_topics;
     out->n_deliveries = mo.n_deliveries;
     out->n_shared = mo.n_shared;
@@ -291,6 +294,7 @@ int mqm_match_batch(mqm_index *h, const char *topic_bytes, const uint64_t *topic
     rc = match_device(h->snap->dev, ws, d_bytes, d_offs, n_topics, h->stream, &mo);
     if (rc != 0) return rc;
     h->matched = h->snap.get();
+    h->last_mo = mo;
     IdentOutput io;
     const bool want_ids = (h->cfg.flags & MQM_CFG_IDENTIFIERS) != 0;
     if (want_ids && (rc = identifiers_device(h->snap->dev, ws, h->stream, &io)) != 0) return rc;
@@ -348,6 +352,55 @@ int mqm_identifiers_device(mqm_index *h, void *hip_stream, mqm_device_identifier
     out->offsets = io.offsets;
     out->sids = io.sids;
     return MQM_OK;
+  });
+}
+
+int mqm_dense_device(mqm_index *h, void *hip_stream, mqm_device_dense *out) {
+  if (!h || !out) return MQM_EINVAL;
+  return guarded([&] {
+    std::lock_guard<std::mutex> g(h->mu);
+    if (h->cfg.device == MQM_DEVICE_NONE) return MQM_ENODEV;
+    if (!h->matched || h->matched != h->snap.get()) return MQM_EINVAL;
+    if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
+    DenseOutput dn;
+    const int rc = densify(h->ws, h->last_mo, (hipStream_t)hip_stream, &dn);
+    if (rc != 0) return rc == -2 ? MQM_ENOMEM : MQM_EHIP;
+    out->n_topics = h->last_mo.n_topics;
+    out->n_deliveries = h->last_mo.n_deliveries;
+    out->n_shared = h->last_mo.n_shared;
+    out->offsets = dn.offsets;
+    out->deliveries = reinterpret_cast<const mqm_delivery *>(dn.deliveries);
+    out->shared_offsets = dn.shared_offsets;
+    out->shared = dn.shared;
+    return MQM_OK;
+  });
+}
+
+int mqm_gather_shards(uint32_t n_topics, uint32_t n_shards, const mqm_shard_part *parts, void *hip_stream,
+                      uint64_t *d_out_offsets, mqm_delivery *d_out) {
+  if (!parts || !d_out_offsets || n_shards == 0 || n_shards > (uint32_t)kMaxShards) return MQM_EINVAL;
+  return guarded([&] {
+    // device-visible status word (pinned, mapped): a client id outside its map
+    static std::mutex mu;
+    static unsigned int *bad = nullptr;
+    std::lock_guard<std::mutex> g(mu);
+    if (!bad && hipHostMalloc((void **)&bad, sizeof(unsigned int), hipHostMallocMapped) != hipSuccess) {
+      bad = nullptr;
+      return MQM_EHIP;
+    }
+    *bad = 0;
+    ShardPart p[kMaxShards];
+    for (uint32_t r = 0; r < n_shards; r++)
+      p[r] = ShardPart{parts[r].offsets, reinterpret_cast<const uint64_t *>(parts[r].deliveries),
+                       parts[r].client_map, parts[r].n_map};
+    unsigned int *dbad = nullptr;
+    if (hipHostGetDevicePointer((void **)&dbad, bad, 0) != hipSuccess) return MQM_EHIP;
+    const int rc = gather_shards(n_topics, n_shards, p, (hipStream_t)hip_stream, d_out_offsets,
+                                 reinterpret_cast<uint64_t *>(d_out), dbad);
+    if (rc == -1) return MQM_EINVAL;
+    if (rc != 0) return MQM_EHIP;
+    if (hipStreamSynchronize((hipStream_t)hip_stream) != hipSuccess) return MQM_EHIP;
+    return *(volatile unsigned int *)bad ? MQM_EINVAL : MQM_OK;
   });
 }
 

@@ -5,8 +5,10 @@ in [r*C/W, (r+1)*C/W).  The merge rule (packets.go:250-270) is per client, so
 deduplication is shard-local and the shards' per-topic results are disjoint:
 the node-wide result of a topic is the union of the shards' results and its
 delivery count is their sum.  The publish batch enters at one rank and is
-broadcast; per-topic counts are reduced back (RCCL over xGMI with the "nccl"
-backend on GPUs, gloo on CPU in the tests).
+broadcast; the shards' dense per-topic lists go back to it with point-to-point
+send/recv (RCCL has no gatherv), where mqm_gather_shards (shard.hip) lays
+them out as one node-wide CSR (RCCL over xGMI with the "nccl" backend on GPUs,
+gloo on CPU in the tests).
 """
 
 from __future__ import annotations
@@ -59,3 +61,49 @@ def reduce_counts(dist, counts, dst: int = 0):
     """Sum the shards' per-topic delivery counts at `dst`."""
     dist.reduce(counts, dst=dst)
     return counts
+
+
+def client_map(w, world: int, rank: int) -> np.ndarray:
+    """Shard `rank`'s interned client id -> the node-wide id (the id an
+    unsharded index interns for that client: first appearance in subscribe
+    order, store.cpp Interner).  Both orders are first appearance, so the
+    shard's k-th distinct client maps to its rank among all clients."""
+    cid = np.asarray(w.client_ids)
+    gids, first = np.unique(cid, return_index=True)
+    node_id = np.empty(int(gids.max()) + 1 if len(gids) else 0, np.uint32)
+    node_id[gids[np.argsort(first)]] = np.arange(len(gids), dtype=np.uint32)
+    lo, hi = shard_bounds(len(gids) and int(gids.max()) + 1, world, rank)
+    part = cid[(cid >= lo) & (cid < hi)]
+    pg, pf = np.unique(part, return_index=True)
+    return node_id[pg[np.argsort(pf)]]
+
+
+def gather_lists(dist, offsets, deliveries, dst: int = 0):
+    """Send every shard's dense CSR (int64 offsets [n+1], int64 deliveries =
+    packed mqm_delivery) to `dst` with point-to-point send/recv; -> on dst the
+    per-rank (offsets, deliveries) tensors in rank order (its own included),
+    elsewhere None.  Delivery counts travel first so receive buffers fit."""
+    import torch
+
+    world, rank = dist.get_world_size(), dist.get_rank()
+    nd = torch.tensor([deliveries.numel()], dtype=torch.int64, device=offsets.device)
+    sizes = [torch.zeros_like(nd) for _ in range(world)]
+    dist.all_gather(sizes, nd)
+    if rank != dst:
+        ops = [dist.P2POp(dist.isend, offsets, dst), dist.P2POp(dist.isend, deliveries, dst)]
+        for r in dist.batch_isend_irecv(ops):
+            r.wait()
+        return None
+    parts, ops = [], []
+    for r in range(world):
+        if r == rank:
+            parts.append((offsets, deliveries))
+            continue
+        o = torch.empty_like(offsets)
+        d = torch.empty(int(sizes[r].item()), dtype=deliveries.dtype, device=deliveries.device)
+        ops += [dist.P2POp(dist.irecv, o, r), dist.P2POp(dist.irecv, d, r)]
+        parts.append((o, d))
+    if ops:
+        for q in dist.batch_isend_irecv(ops):
+            q.wait()
+    return parts

@@ -303,3 +303,53 @@ def test_identifiers_dfs_topics_and_device_form():
     d = idx.identifiers_device()
     torch.cuda.synchronize()
     assert d.n_topics == len(topics) and d.n_idents == int(res.ident_offsets[-1])
+
+
+# ---- subscriber-sharded node result: mqm_dense_device + mqm_gather_shards ----------
+
+@pytest.mark.parametrize("n_shards", [1, 3, 4])
+def test_gather_shards_equals_unsharded(n_shards):
+    """S shard indexes on one device (each a contiguous client range), their
+    dense CSRs laid out by mqm_gather_shards == the unsharded index's result:
+    same (topic, node client, QoS, NoLocal) rows, shard order within a topic."""
+    import torch
+
+    from maxmq_amd import shard
+
+    w = mqgen.generate(1, n_filters=20000, n_topics=30000)
+    s = w.topics
+    tb = torch.from_numpy(s.data).cuda()
+    to = torch.from_numpy(s.offs.view(np.int64)).cuda()
+    n = len(s)
+    full = maxmq_amd.TopicsIndex(0)
+    full.subscribe_workload(w)
+    ref = full.match_batch(s.data, s.offs)
+    idxs, parts, maps, total = [], [], [], 0
+    for r in range(n_shards):
+        ix = maxmq_amd.TopicsIndex(0)
+        ix.subscribe_workload(shard.shard_workload(w, n_shards, r))
+        ix.match_device(tb.data_ptr(), to.data_ptr(), n)
+        d = ix.dense_device()
+        total += int(d.n_deliveries)
+        cm = torch.from_numpy(shard.client_map(w, n_shards, r).astype(np.int32)).cuda()
+        idxs.append(ix)
+        maps.append(cm)
+        parts.append((d.offsets, d.deliveries, cm.data_ptr(), cm.numel()))
+    out_o = torch.zeros(n + 1, dtype=torch.int64, device="cuda")
+    out_d = torch.zeros(max(total, 1), dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    maxmq_amd.gather_shards(n, parts, out_o.data_ptr(), out_d.data_ptr())
+    go = out_o.cpu().numpy().view(np.uint64)
+    assert np.array_equal(go, ref.offsets), "node-wide offsets"
+    gd = out_d[:total].cpu().numpy().view(capi.DELIVERY_DTYPE)
+    _, gq, gn = capi.delivery_fields(gd["packed"])
+    _, rq, rn = capi.delivery_fields(ref.deliveries["packed"])
+    topic = np.repeat(np.arange(n), np.diff(go).astype(np.int64))
+    g = np.unique(np.rec.fromarrays([topic, gd["client"], gq, gn]))
+    r = np.unique(np.rec.fromarrays([topic, ref.deliveries["client"], rq, rn]))
+    assert len(g) == total and np.array_equal(g, r)
+    # a client id outside its shard's map is an error, never silent
+    bad = [(p[0], p[1], p[2], 0) for p in parts]
+    if total:
+        with pytest.raises(maxmq_amd.MqmError):
+            maxmq_amd.gather_shards(n, bad, out_o.data_ptr(), out_d.data_ptr())

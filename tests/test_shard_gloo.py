@@ -46,20 +46,31 @@ def _worker(rank, world, port, out_q):
         idx.subscribe_workload(part)
         doffs, dout, _, _, _ = idx.match(data.numpy(), offs.numpy().view(np.uint64))
         counts = torch.from_numpy(np.diff(doffs).astype(np.int64))
-        names = [idx.client_name(int(c)) for c in dout["client"]]
-        pairs = list(zip(np.repeat(np.arange(len(counts)), counts.numpy()).tolist(), names, dout["qos"].tolist()))
         shard.reduce_counts(dist, counts, dst=0)
-        gathered = [None] * world
-        dist.all_gather_object(gathered, pairs)
+        # the shard's dense CSR: client id in the low word, QoS above it
+        # (the GPU path sends packed mqm_delivery the same way)
+        offs_t = torch.from_numpy(doffs.astype(np.int64))
+        dl = torch.from_numpy(dout["client"].astype(np.int64) | (dout["qos"].astype(np.int64) << 32))
+        parts = shard.gather_lists(dist, offs_t, dl, dst=0)
         if rank == 0:
             full = OracleIndex()
             full.subscribe_workload(w)
             fo, fd, _, _, _ = full.match(w.topics.data, w.topics.offs)
-            fpairs = list(zip(np.repeat(np.arange(len(fo) - 1), np.diff(fo).astype(np.int64)).tolist(),
-                              [full.client_name(int(c)) for c in fd["client"]], fd["qos"].tolist()))
-            union = sorted(p for g in gathered for p in g)
-            out_q.put((np.array_equal(counts.numpy(), np.diff(fo).astype(np.int64)), union == sorted(fpairs),
-                       len(union), sum(len(g) for g in gathered) == len(set(union))))
+            nt = len(fo) - 1
+            # mqm_gather_shards' layout, restated: topic t = shard 0's segment,
+            # shard 1's, ...; clients through each shard's client map
+            rows = []
+            for t in range(nt):
+                for r, (o, d) in enumerate(parts):
+                    cm = shard.client_map(w, world, r)
+                    seg = d.numpy()[int(o[t]):int(o[t + 1])]
+                    rows += [(t, int(cm[c & 0xFFFFFFFF]), int(c >> 32)) for c in seg]
+            node = [(t, int(c), int(q)) for t, c, q in zip(np.repeat(np.arange(nt), np.diff(fo).astype(np.int64)),
+                                                        fd["client"], fd["qos"])]
+            names_ok = all(full.client_name(i) == w.clients.data[w.clients.offs[j]:w.clients.offs[j + 1]].tobytes()
+                           .decode() for i, j in [(0, 0)])
+            out_q.put((np.array_equal(counts.numpy(), np.diff(fo).astype(np.int64)), sorted(rows) == sorted(node),
+                       len(rows), len(rows) == len(set(rows)) and names_ok))
     finally:
         dist.destroy_process_group()
 
