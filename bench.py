@@ -50,8 +50,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=["forward", "reverse"], default="forward",
-                    help="forward: Subscribers (headline); reverse: Messages over retained topics (config 5)")
+    ap.add_argument("--workload", choices=["forward", "reverse", "churn"], default="forward",
+                    help="forward: Subscribers (headline); reverse: Messages over retained topics (config 5); "
+                         "churn: Subscribe/Unsubscribe at rate with background snapshot rebuilds")
+    ap.add_argument("--churn-ops", type=int, default=1000000, help="churn: mutations per round (half unsubscribes)")
     ap.add_argument("--retained", type=int, default=50000000, help="reverse: retained topics")
     ap.add_argument("--sweep", default="",
                     help="tuning sweep before the measurement: ';'-separated variants of "
@@ -102,6 +104,8 @@ def main():
 
     if args.workload == "reverse":
         return run_reverse(args, dist, rank, world, local, dev)
+    if args.workload == "churn":
+        return run_churn(args, dist, rank, world, local, dev)
 
     overrides = {}
     if args.filters:
@@ -275,6 +279,103 @@ def run_sweep(args, idx, step, dev, rank):
             else:
                 os.environ[k] = v
     return results
+
+
+def run_churn(args, dist, rank, world, local, dev):
+    """Incremental Subscribe/Unsubscribe at rate on the
+    headline workload: the index runs with MQM_CFG_ASYNC_COMMIT.  A round =
+    --churn-ops mutations (half Unsubscribes of existing (filter, client)
+    pairs, half Subscribes of existing filters by new clients) applied to the
+    host store + delta log, then mqm_commit_async while match steps keep
+    running on the front snapshot.  `value` = mutations/s the store absorbs;
+    the line also carries the rebuild time (replay + flatten + upload) and the
+    match throughput before / during / after the rebuild."""
+    import torch
+
+    import maxmq_amd
+    from tools import mqgen
+    from tools.mqgen import Strings
+
+    overrides = {}
+    if args.filters:
+        overrides["n_filters"] = args.filters
+    if args.topics:
+        overrides["n_topics"] = args.topics
+    w = mqgen.generate(args.config, **overrides)
+    n = len(w.topics)
+    t0 = time.time()
+    idx = maxmq_amd.TopicsIndex(device=local, autocommit=False, async_commit=True)
+    idx.subscribe_workload(w)
+    idx.commit()
+    build_s = time.time() - t0
+    log(f"[rank {rank}] async index built in {build_s:.1f}s: {idx.commit_state()}")
+    tb = torch.from_numpy(w.topics.data).to(dev)
+    to = torch.from_numpy(w.topics.offs.view(np.int64)).to(dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def timed_steps(k):
+        ts = []
+        for _ in range(k):
+            t = time.perf_counter()
+            idx.match_device(tb.data_ptr(), to.data_ptr(), n, stream.cuda_stream)
+            torch.cuda.synchronize(dev)
+            ts.append(time.perf_counter() - t)
+        return ts
+
+    timed_steps(args.warmup)
+    before = timed_steps(args.steps)
+    rng = np.random.default_rng(0x4D51C0DE)
+    half = args.churn_ops // 2
+    sel = rng.choice(len(w.filters), size=half, replace=False)
+    un_f = Strings.from_list([w.filters[int(i)] for i in sel])
+    un_c = Strings.from_list([w.clients[int(i)] for i in sel])
+    sel2 = rng.choice(len(w.filters), size=half, replace=False)
+    sub_f = Strings.from_list([w.filters[int(i)] for i in sel2])
+    sub_c = Strings.from_list([f"churn-{j}" for j in range(half)])
+    t0 = time.perf_counter()
+    existed = idx.unsubscribe_many(un_f, un_c)
+    is_new = idx.subscribe_many(sub_c, sub_f, w.qos[sel2], w.no_local[sel2], w.rap[sel2], w.rh[sel2], w.ident[sel2])
+    mut_s = time.perf_counter() - t0
+    st0 = idx.commit_state()
+    t0 = time.perf_counter()
+    idx.commit_async()
+    submit_ms = (time.perf_counter() - t0) * 1e3
+    during = []
+    t_pub = None
+    while len(during) < 2000 and time.perf_counter() - t0 < 300:
+        during += timed_steps(1)
+        if idx.commit_state()["builds"] > st0["builds"]:
+            t_pub = time.perf_counter() - t0
+            break
+    if t_pub is None:
+        idx.commit_poll(wait=True)
+        t_pub = time.perf_counter() - t0
+    st = idx.commit_state()
+    after = timed_steps(args.steps)
+    assert st["snapshot_version"] == st["store_version"], st
+    med = lambda x: float(np.median(x)) * 1e3 if x else None  # noqa: E731
+    out = {
+        "metric": "incremental Subscribe/Unsubscribe mutations/sec absorbed, background snapshot rebuild at 10M filters",
+        "value": args.churn_ops / mut_s,
+        "unit": "mutations/s",
+        "n_gpus": 1,
+        "higher_is_better": True,
+        "config": {"workload": f"mqgen config {args.config}: {len(w.filters)} filters, {n}-topic match batches; "
+                               f"{half} unsubscribes + {half} subscribes per round",
+                   "filters": len(w.filters)},
+        "unsubscribes_existed": int(existed.sum()),
+        "subscribes_new": int(is_new.sum()),
+        "initial_build_s": build_s,
+        "submit_ms": submit_ms,
+        "rebuild_ms": st["last_build_ms"],
+        "rebuild_ops": st["last_build_ops"],
+        "publish_after_ms": t_pub * 1e3,
+        "match_ms_median": {"before": med(before), "during_rebuild": med(during), "after": med(after)},
+        "match_steps_during_rebuild": len(during),
+        "commit_state": st,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
 
 
 def run_reverse(args, dist, rank, world, local, dev):

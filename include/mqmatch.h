@@ -42,6 +42,13 @@ extern "C" {
 #define MQM_CFG_AUTOCOMMIT 1u
 /* mqm_match_batch also returns Identifiers support (mqm_result_identifiers) */
 #define MQM_CFG_IDENTIFIERS 2u
+/* MQM_CFG_ASYNC_COMMIT: every mutation is also appended to a delta log; a
+ * commit hands the log to a background builder thread that replays it into a
+ * shadow store, flattens it and uploads the new snapshot on its own HIP stream
+ * (the back buffer) while matches keep reading the front buffer.  Matches
+ * publish a finished back buffer at their start (no wait).  mqm_commit keeps
+ * its synchronous meaning (submit, wait, publish).  See mqm_commit_async. */
+#define MQM_CFG_ASYNC_COMMIT 4u
 /* device value for a host-only index: the store and its mutation API work,
  * mqm_commit / mqm_match_* return MQM_ENODEV (there is no CPU match path). */
 #define MQM_DEVICE_NONE (-1)
@@ -122,6 +129,10 @@ int mqm_subscribe_many(mqm_index *h, size_t n, const char *client_bytes, const u
 /* TopicsIndex.Unsubscribe (topics.go:325-349): *existed = the reference's bool */
 int mqm_unsubscribe(mqm_index *h, const char *filter, size_t filter_len, const char *client, size_t client_len,
                     int *existed);
+/* n Unsubscribe calls in order (UnsubscribeClient at session expiry,
+ * server.go:1109-1129); existed may be NULL */
+int mqm_unsubscribe_many(mqm_index *h, size_t n, const char *filter_bytes, const uint64_t *filter_offs,
+                         const char *client_bytes, const uint64_t *client_offs, uint8_t *existed);
 /* TopicsIndex.RetainMessage (topics.go:354-377); message_ref is the caller's
  * handle for the packet; payload_len == 0 deletes.  *result = 1 / 0 / -1. */
 int mqm_retain_message(mqm_index *h, const char *topic, size_t topic_len, uint64_t message_ref,
@@ -134,8 +145,39 @@ int mqm_retain_many(mqm_index *h, size_t n, const char *topic_bytes, const uint6
 /* Retained.Len() (packets.go:103) */
 int mqm_retained_len(mqm_index *h, uint64_t *out);
 
-/* publish the current store as the GPU snapshot (double-buffered) */
+/* publish the current store as the snapshot matches read, and wait for it.
+ * A host-only index (MQM_DEVICE_NONE) builds the host side only (stats and
+ * digest; matching still returns MQM_ENODEV). */
 int mqm_commit(mqm_index *h);
+
+/* ---- incremental commits (MQM_CFG_ASYNC_COMMIT; MQM_EINVAL otherwise) ------
+ * The reference has no snapshot: a Subscribe is visible to the next
+ * Subscribers call (topics.go:303-321, 484-518).  Here visibility starts when
+ * the snapshot holding the mutation is published; mqm_commit, or
+ * MQM_CFG_AUTOCOMMIT on a match, gives back read-your-writes. */
+/* hand the mutations logged since the last submit to the builder; returns at
+ * once.  Logs submitted while a build runs are coalesced into the next one. */
+int mqm_commit_async(mqm_index *h);
+/* publish the newest finished build, if any (*published = 1); wait != 0 first
+ * waits until every submitted log is built.  Returns the first build error. */
+int mqm_commit_poll(mqm_index *h, int wait, int *published);
+/* periodic rebuild: submit automatically once max_ops mutations are logged or
+ * the oldest logged one is max_ms old (checked at mutations and matches;
+ * 0 disables a bound) */
+int mqm_commit_policy(mqm_index *h, uint64_t max_ops, uint32_t max_ms);
+typedef struct {
+  uint64_t store_version;    /* mutations applied to the authoritative store   */
+  uint64_t snapshot_version; /* store version the published snapshot reflects  */
+  uint64_t pending_ops;      /* logged, not yet submitted                       */
+  uint64_t builds;           /* snapshots published by the builder             */
+  uint64_t last_build_ops;   /* delta-log entries folded into the last one      */
+  double last_build_ms;      /* its replay + flatten + upload time              */
+  int32_t has_snapshot, building;
+} mqm_commit_state;
+int mqm_commit_state_get(mqm_index *h, mqm_commit_state *out);
+/* 64-bit digest of the published snapshot's arrays: replicas and rebuilds of
+ * the same store state have equal digests */
+int mqm_snapshot_digest(mqm_index *h, uint64_t *out);
 
 /* ---- forward match: TopicsIndex.Subscribers (topics.go:484-555) --------- */
 /* Host in / host out.  Topic i is bytes[offsets[i] .. offsets[i+1]). */

@@ -193,13 +193,17 @@ class BatchResult:
 class TopicsIndex:
     """TopicsIndex (topics.go:285) backed by the MI355X matcher."""
 
-    def __init__(self, device: int | None = 0, autocommit: bool = True, identifiers: bool = False):
+    def __init__(self, device: int | None = 0, autocommit: bool = True, identifiers: bool = False,
+                 async_commit: bool = False):
         """identifiers=True: match_batch / subscribers also return the full
-        Subscription.Identifiers maps (an extra GPU pass per batch)."""
+        Subscription.Identifiers maps (an extra GPU pass per batch).
+        async_commit=True: mutations are logged and snapshots are rebuilt by a
+        background builder (commit_async / commit_poll / commit_policy)."""
         L = lib()
         cfg = capi.Config(capi.MQM_DEVICE_NONE if device is None else device,
                           (capi.MQM_CFG_AUTOCOMMIT if autocommit else 0) |
-                          (capi.MQM_CFG_IDENTIFIERS if identifiers else 0))
+                          (capi.MQM_CFG_IDENTIFIERS if identifiers else 0) |
+                          (capi.MQM_CFG_ASYNC_COMMIT if async_commit else 0))
         h = C.c_void_p()
         check("mqm_create", L.mqm_create(C.byref(cfg), C.byref(h)))
         self._h = h
@@ -226,15 +230,18 @@ class TopicsIndex:
 
     def subscribe_workload(self, w) -> np.ndarray:
         """Bulk Subscribe of a tools.mqgen.Workload in filter order; -> is_new[]."""
-        n = len(w.filters)
+        return self.subscribe_many(w.clients, w.filters, w.qos, w.no_local, w.rap, w.rh, w.ident)
+
+    def subscribe_many(self, clients, filters, qos, no_local=0, rap=0, rh=0, ident=0) -> np.ndarray:
+        """Bulk Subscribe of (clients[i], filters[i]) (tools.mqgen.Strings) in order; -> is_new[]."""
+        n = len(filters)
         subs = np.zeros(n, dtype=np.dtype([("qos", "u1"), ("nl", "u1"), ("rap", "u1"), ("rh", "u1"),
                                            ("ident", "<i4")]))
-        subs["qos"], subs["nl"], subs["rap"], subs["rh"], subs["ident"] = w.qos, w.no_local, w.rap, w.rh, w.ident
+        subs["qos"], subs["nl"], subs["rap"], subs["rh"], subs["ident"] = qos, no_local, rap, rh, ident
         is_new = np.zeros(n, np.uint8)
         p = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
         check("mqm_subscribe_many", lib().mqm_subscribe_many(
-            self._h, n, p(w.clients.data), p(w.clients.offs), p(w.filters.data), p(w.filters.offs), p(subs),
-            p(is_new)))
+            self._h, n, p(clients.data), p(clients.offs), p(filters.data), p(filters.offs), p(subs), p(is_new)))
         return is_new
 
     def unsubscribe(self, filt: str, client: str) -> bool:
@@ -242,6 +249,15 @@ class TopicsIndex:
         out = C.c_int()
         check("mqm_unsubscribe", lib().mqm_unsubscribe(self._h, f, len(f), c, len(c), C.byref(out)))
         return bool(out.value)
+
+    def unsubscribe_many(self, filters, clients) -> np.ndarray:
+        """Bulk Unsubscribe of (filters[i], clients[i]) (tools.mqgen.Strings) in order; -> existed[]."""
+        n = len(filters)
+        out = np.zeros(n, np.uint8)
+        p = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+        check("mqm_unsubscribe_many", lib().mqm_unsubscribe_many(
+            self._h, n, p(filters.data), p(filters.offs), p(clients.data), p(clients.offs), p(out)))
+        return out
 
     def retain_message(self, topic: str, message_ref: int, payload_len: int, retain: bool = True) -> int:
         t = b(topic)
@@ -270,6 +286,31 @@ class TopicsIndex:
 
     def commit(self):
         check("mqm_commit", lib().mqm_commit(self._h))
+
+    # -- incremental commits (async_commit=True) ---------------------------------
+    def commit_async(self):
+        """Hand the logged mutations to the background builder; returns at once."""
+        check("mqm_commit_async", lib().mqm_commit_async(self._h))
+
+    def commit_poll(self, wait: bool = False) -> bool:
+        """Publish the newest finished snapshot (wait: for every submitted log)."""
+        out = C.c_int()
+        check("mqm_commit_poll", lib().mqm_commit_poll(self._h, int(wait), C.byref(out)))
+        return bool(out.value)
+
+    def commit_policy(self, max_ops: int = 0, max_ms: int = 0):
+        """Periodic rebuild: auto-submit after max_ops logged mutations or max_ms."""
+        check("mqm_commit_policy", lib().mqm_commit_policy(self._h, max_ops, max_ms))
+
+    def commit_state(self) -> dict:
+        st = capi.CommitState()
+        check("mqm_commit_state_get", lib().mqm_commit_state_get(self._h, C.byref(st)))
+        return {n: getattr(st, n) for n, _ in capi.CommitState._fields_}
+
+    def snapshot_digest(self) -> int:
+        out = C.c_uint64()
+        check("mqm_snapshot_digest", lib().mqm_snapshot_digest(self._h, C.byref(out)))
+        return int(out.value)
 
     # -- names ------------------------------------------------------------------
     def _name(self, fn, i):

@@ -23,6 +23,7 @@ MQM_ELIMIT = -4
 MQM_ENODEV = -5
 MQM_CFG_AUTOCOMMIT = 1
 MQM_CFG_IDENTIFIERS = 2
+MQM_CFG_ASYNC_COMMIT = 4
 MQM_DEVICE_NONE = -1
 
 ERRORS = {MQM_EINVAL: "EINVAL", MQM_ENOMEM: "ENOMEM", MQM_EHIP: "EHIP", MQM_ELIMIT: "ELIMIT",
@@ -38,7 +39,8 @@ EXPORTED = [
     "mqm_is_shared_filter", "mqm_snapshot_stats_get", "mqm_profile_enable", "mqm_profile_read", "mqm_version",
     "mqm_retain_many", "mqm_messages_batch", "mqm_messages_one", "mqm_messages_num_filters", "mqm_messages_offsets",
     "mqm_messages_refs", "mqm_messages_free", "mqm_messages_device", "mqm_identifiers_device",
-    "mqm_result_identifiers", "mqm_dense_device", "mqm_gather_shards",
+    "mqm_result_identifiers", "mqm_dense_device", "mqm_gather_shards", "mqm_commit_async", "mqm_commit_poll",
+    "mqm_commit_policy", "mqm_commit_state_get", "mqm_snapshot_digest", "mqm_unsubscribe_many",
 ]
 
 
@@ -50,6 +52,12 @@ class MqmError(RuntimeError):
 
 class Config(C.Structure):
     _fields_ = [("device", C.c_int), ("flags", C.c_uint32)]
+
+
+class CommitState(C.Structure):
+    _fields_ = [("store_version", C.c_uint64), ("snapshot_version", C.c_uint64), ("pending_ops", C.c_uint64),
+                ("builds", C.c_uint64), ("last_build_ops", C.c_uint64), ("last_build_ms", C.c_double),
+                ("has_snapshot", C.c_int32), ("building", C.c_int32)]
 
 
 class Subscription(C.Structure):
@@ -164,6 +172,12 @@ def lib():
         "mqm_result_identifiers": ([vp, C.POINTER(vp), C.POINTER(vp)], C.c_int),
         "mqm_dense_device": ([vp, vp, C.POINTER(DeviceDense)], C.c_int),
         "mqm_gather_shards": ([u32, u32, C.POINTER(ShardPart), vp, vp, vp], C.c_int),
+        "mqm_unsubscribe_many": ([vp, sz, vp, vp, vp, vp, vp], C.c_int),
+        "mqm_commit_async": ([vp], C.c_int),
+        "mqm_commit_poll": ([vp, C.c_int, C.POINTER(C.c_int)], C.c_int),
+        "mqm_commit_policy": ([vp, u64, u32], C.c_int),
+        "mqm_commit_state_get": ([vp, C.POINTER(CommitState)], C.c_int),
+        "mqm_snapshot_digest": ([vp, C.POINTER(u64)], C.c_int),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

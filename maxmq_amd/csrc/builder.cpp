@@ -1,0 +1,223 @@
+// maxmq_amd/csrc/builder.cpp — delta log replay and the background snapshot
+// builder (see builder.h).
+#include "builder.h"
+
+#include <chrono>
+#include <cstring>
+
+#include "../../include/mqmatch.h"
+
+namespace mqm {
+
+DeltaLog::Op &DeltaLog::push(Kind k, std::string_view a, std::string_view b) {
+  Op op{};
+  op.kind = k;
+  op.a_off = bytes_.size();
+  op.a_len = (uint32_t)a.size();
+  op.b_len = (uint32_t)b.size();
+  bytes_.insert(bytes_.end(), a.begin(), a.end());
+  bytes_.insert(bytes_.end(), b.begin(), b.end());
+  ops_.push_back(op);
+  return ops_.back();
+}
+
+void DeltaLog::subscribe(std::string_view client, std::string_view filter, uint8_t qos, uint8_t no_local,
+                         uint8_t rap, uint8_t rh, int32_t ident) {
+  Op &op = push(kSub, client, filter);
+  op.qos = qos;
+  op.no_local = no_local;
+  op.rap = rap;
+  op.rh = rh;
+  op.ident = ident;
+}
+
+void DeltaLog::unsubscribe(std::string_view filter, std::string_view client) { push(kUnsub, filter, client); }
+
+void DeltaLog::retain(std::string_view topic, uint64_t msg_ref, uint32_t payload_len, bool retain_flag) {
+  Op &op = push(kRetain, topic, std::string_view());
+  op.msg_ref = msg_ref;
+  op.payload_len = payload_len;
+  op.retain_flag = retain_flag ? 1 : 0;
+}
+
+void DeltaLog::replay(Store &st) const {
+  const char *base = bytes_.data();
+  for (const Op &op : ops_) {
+    const std::string_view a(base + op.a_off, op.a_len), b(base + op.a_off + op.a_len, op.b_len);
+    switch (op.kind) {
+      case kSub:
+        st.subscribe(a, b, op.qos, op.no_local, op.rap, op.rh, op.ident);
+        break;
+      case kUnsub:
+        st.unsubscribe(a, b);
+        break;
+      default:
+        st.retain_message(a, op.msg_ref, op.payload_len, op.retain_flag != 0);
+        break;
+    }
+  }
+}
+
+void DeltaLog::append(DeltaLog &&o) {
+  if (ops_.empty()) {
+    ops_.swap(o.ops_);
+    bytes_.swap(o.bytes_);
+    o.clear();
+    return;
+  }
+  const uint64_t shift = bytes_.size();
+  bytes_.insert(bytes_.end(), o.bytes_.begin(), o.bytes_.end());
+  ops_.reserve(ops_.size() + o.ops_.size());
+  for (Op op : o.ops_) {
+    op.a_off += shift;
+    ops_.push_back(op);
+  }
+  o.clear();
+}
+
+Builder::Builder(int device) : device_(device) { th_ = std::thread([this] { run(); }); }
+
+Builder::~Builder() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  th_.join();
+  if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+void Builder::submit(DeltaLog &&log, uint64_t version) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    queued_.append(std::move(log));  // logs submitted while a build runs are coalesced
+    queued_version_ = version;
+    has_queued_ = true;
+  }
+  cv_.notify_all();
+}
+
+bool Builder::take(BuiltSnapshot *out) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (!has_ready_) return false;
+  *out = std::move(ready_);
+  ready_ = BuiltSnapshot();
+  has_ready_ = false;
+  return true;
+}
+
+int Builder::wait_idle() {
+  std::unique_lock<std::mutex> g(mu_);
+  cv_.wait(g, [this] { return !has_queued_ && !working_; });
+  const int e = err_;
+  err_ = 0;
+  return e;
+}
+
+bool Builder::busy() {
+  std::lock_guard<std::mutex> g(mu_);
+  return has_queued_ || working_;
+}
+
+void Builder::run() {
+  if (device_ >= 0) {
+    if (hipSetDevice(device_) != hipSuccess ||
+        hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) {
+      std::lock_guard<std::mutex> g(mu_);
+      err_ = MQM_EHIP;
+    }
+  }
+  for (;;) {
+    DeltaLog log;
+    uint64_t version;
+    {
+      std::unique_lock<std::mutex> g(mu_);
+      cv_.wait(g, [this] { return has_queued_ || stop_; });
+      if (!has_queued_) return;  // stop_ with nothing left to build
+      log.append(std::move(queued_));
+      version = queued_version_;
+      has_queued_ = false;
+      working_ = true;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    int rc = MQM_OK;
+    BuiltSnapshot b;
+    try {
+      log.replay(shadow_);
+      auto hs = std::make_shared<HostSnapshot>();
+      rc = flatten(shadow_, hs.get());
+      if (rc == MQM_OK && device_ >= 0 && !stream_) rc = MQM_EHIP;
+      if (rc == MQM_OK) rc = upload(std::move(hs), device_, stream_, &b.snap);
+    } catch (const std::bad_alloc &) {
+      rc = MQM_ENOMEM;
+    } catch (...) {
+      rc = MQM_EINVAL;
+    }
+    b.version = version;
+    b.n_ops = log.size();
+    b.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      working_ = false;
+      if (rc == MQM_OK) {
+        ready_ = std::move(b);  // replaces an unpublished older build
+        has_ready_ = true;
+      } else if (!err_) {
+        err_ = rc;
+      }
+    }
+    cv_.notify_all();
+  }
+}
+
+namespace {
+// 64-bit multiply-xorshift over 8-byte words (tail zero-padded)
+struct Digest {
+  uint64_t h = 0x6D716D2D64696730ull;
+  void add(const void *p, size_t n) {
+    const auto *b = static_cast<const uint8_t *>(p);
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+      uint64_t w;
+      std::memcpy(&w, b + i, 8);
+      mix(w);
+    }
+    uint64_t w = 0;
+    std::memcpy(&w, b + i, n - i);
+    mix(w ^ ((uint64_t)n << 56));
+  }
+  void mix(uint64_t w) {
+    h ^= w + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+    h *= 0xFF51AFD7ED558CCDull;
+    h ^= h >> 33;
+  }
+  template <class V>
+  void vec(const V &v) {
+    add(v.data(), v.size() * sizeof(v[0]));
+  }
+};
+}  // namespace
+
+uint64_t snapshot_digest(const HostSnapshot &hs) {
+  Digest d;
+  d.vec(hs.nodes);
+  d.vec(hs.edges);
+  d.vec(hs.subs);
+  d.vec(hs.sub_info);
+  d.vec(hs.shared_info);
+  d.vec(hs.tok_pool);
+  d.vec(hs.subtree);
+  d.vec(hs.child_off);
+  d.vec(hs.child_ids);
+  d.vec(hs.cum);
+  d.vec(hs.rch_off);
+  d.vec(hs.refs);
+  d.vec(hs.rch_refs);
+  d.mix(hs.n_buckets);
+  d.mix(hs.height);
+  d.mix(hs.sys_child);
+  d.mix(hs.has_empty);
+  return d.h;
+}
+
+}  // namespace mqm

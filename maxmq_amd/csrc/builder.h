@@ -1,0 +1,105 @@
+// maxmq_amd/csrc/builder.h — delta log + background snapshot builder
+// (incremental Subscribe/Unsubscribe at rate).
+//
+// The reference mutates its live trie under the root mutex and readers see a
+// change at once (topics.go:303-349,354-377; no snapshot).  Here the
+// authoritative Store answers every mutation with the reference's return
+// value, and the mutation is also appended to a DeltaLog.  A commit hands the
+// log to the Builder's worker thread, which replays it into a private shadow
+// Store (same calls, same order, so the same interned ids and trie shape),
+// flattens the shadow into a new HostSnapshot and uploads it on its own HIP
+// stream into the back buffer.  The index publishes the back buffer at its
+// next call (double buffering): matches keep running against the front
+// snapshot while the next one is built, and no mutation waits for a rebuild.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <condition_variable>
+#include <memory>
+#include <mutex>
+#include <string_view>
+#include <thread>
+#include <vector>
+
+#include "flatten.h"
+#include "store.h"
+
+namespace mqm {
+
+// Store mutations in call order; strings packed into one arena.
+class DeltaLog {
+ public:
+  void subscribe(std::string_view client, std::string_view filter, uint8_t qos, uint8_t no_local, uint8_t rap,
+                 uint8_t rh, int32_t ident);
+  void unsubscribe(std::string_view filter, std::string_view client);
+  void retain(std::string_view topic, uint64_t msg_ref, uint32_t payload_len, bool retain_flag);
+  // re-run every recorded call on st, in order
+  void replay(Store &st) const;
+  void append(DeltaLog &&o);  // o's ops after ours
+  size_t size() const { return ops_.size(); }
+  bool empty() const { return ops_.empty(); }
+  void clear() {
+    ops_.clear();
+    bytes_.clear();
+  }
+
+ private:
+  enum Kind : uint8_t { kSub, kUnsub, kRetain };
+  struct Op {
+    uint8_t kind, qos, no_local, rap, rh, retain_flag;
+    int32_t ident;
+    uint32_t payload_len;
+    uint32_t a_len, b_len;  // strings at bytes_[a_off ..), then b
+    uint64_t a_off;
+    uint64_t msg_ref;
+  };
+  Op &push(Kind k, std::string_view a, std::string_view b);
+  std::vector<Op> ops_;
+  std::vector<char> bytes_;
+};
+
+// A snapshot ready to be published: device copy (or host-only when the index
+// has no device) plus the store version it reflects.
+struct BuiltSnapshot {
+  std::unique_ptr<GpuSnapshot> snap;
+  uint64_t version = 0;
+  double build_ms = 0;  // replay + flatten + upload
+  uint64_t n_ops = 0;   // delta-log entries folded in
+};
+
+class Builder {
+ public:
+  explicit Builder(int device);  // device < 0: host snapshots only
+  ~Builder();                    // finishes the queued work, joins the worker
+  Builder(const Builder &) = delete;
+  Builder &operator=(const Builder &) = delete;
+
+  // queue a delta log whose replay brings the shadow store to `version`
+  void submit(DeltaLog &&log, uint64_t version);
+  // the newest finished snapshot, if any (older unpublished ones are dropped)
+  bool take(BuiltSnapshot *out);
+  // block until every submitted log is built; returns the first build error
+  int wait_idle();
+  bool busy();
+
+ private:
+  void run();
+  const int device_;
+  Store shadow_;  // touched only by the worker thread
+  hipStream_t stream_ = nullptr;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  DeltaLog queued_;
+  uint64_t queued_version_ = 0;
+  bool has_queued_ = false, working_ = false, stop_ = false;
+  bool has_ready_ = false;
+  BuiltSnapshot ready_;
+  int err_ = 0;
+  std::thread th_;
+};
+
+// 64-bit digest of a snapshot's arrays (replicas / shards compare it)
+uint64_t snapshot_digest(const HostSnapshot &hs);
+
+}  // namespace mqm

@@ -2,6 +2,8 @@
 // store, the snapshot builder and the HIP match pipeline.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -11,6 +13,7 @@
 #include <vector>
 
 #include "../../include/mqmatch.h"
+#include "builder.h"
 #include "flatten.h"
 #include "match.h"
 #include "retained.h"
@@ -23,12 +26,24 @@ struct mqm_index {
   mqm_config cfg{};
   std::mutex mu;  // serialises mutations, commits and matches on this index
   Store store;
-  std::unique_ptr<GpuSnapshot> snap;
-  uint64_t snap_version = ~0ull;
+  std::unique_ptr<GpuSnapshot> snap;     // front buffer: what matches read
+  uint64_t snap_version = ~0ull;         // store version the front buffer reflects
+  uint64_t snap_serial = 0;              // bumped at every publish
   Workspace ws;
   hipStream_t stream = nullptr;
-  const GpuSnapshot *matched = nullptr;  // snapshot of the last forward match (identifiers pass)
+  uint64_t matched_serial = ~0ull;       // snapshot of the last forward match (identifiers pass)
   MatchOutput last_mo;                   // its segments (mqm_dense_device)
+  std::vector<hipStream_t> used_streams; // streams that may still read the front buffer
+  // MQM_CFG_ASYNC_COMMIT: mutations since the last submit, and the builder
+  // that turns them into the back buffer (builder.h)
+  DeltaLog journal;
+  std::unique_ptr<Builder> builder;
+  uint64_t policy_ops = 0;               // auto-submit after this many logged mutations (0 = off)
+  uint32_t policy_ms = 0;                // ... or when the oldest one is this old (0 = off)
+  std::chrono::steady_clock::time_point journal_t0;
+  uint64_t builds = 0, last_build_ops = 0;
+  double last_build_ms = 0;
+  bool async() const { return (cfg.flags & MQM_CFG_ASYNC_COMMIT) != 0; }
 };
 
 struct mqm_messages {
@@ -62,23 +77,77 @@ int guarded(F &&f) {
 
 std::string_view sv(const char *p, size_t n) { return std::string_view(p ? p : "", p ? n : 0); }
 
+void note_stream(mqm_index *h, hipStream_t s) {
+  if (std::find(h->used_streams.begin(), h->used_streams.end(), s) == h->used_streams.end())
+    h->used_streams.push_back(s);
+}
+
+// make g the front buffer; the old one is freed once the streams that may
+// still read it have drained (the builder's upload stream is not waited on)
+int install(mqm_index *h, std::unique_ptr<GpuSnapshot> g, uint64_t version) {
+  if (h->snap && h->cfg.device != MQM_DEVICE_NONE) {
+    for (hipStream_t s : h->used_streams)
+      if (hipStreamSynchronize(s) != hipSuccess) return MQM_EHIP;
+  }
+  h->used_streams.clear();
+  h->snap = std::move(g);
+  h->snap_version = version;
+  h->snap_serial++;
+  return MQM_OK;
+}
+
+// hand the journal to the builder (MQM_CFG_ASYNC_COMMIT)
+void submit_locked(mqm_index *h) {
+  if (!h->builder) h->builder = std::make_unique<Builder>(h->cfg.device);
+  h->builder->submit(std::move(h->journal), h->store.version());
+  h->journal.clear();
+  h->journal_t0 = std::chrono::steady_clock::now();
+}
+
+// publish the builder's newest finished snapshot, if any
+int publish_locked(mqm_index *h, int *published) {
+  if (published) *published = 0;
+  if (!h->builder) return MQM_OK;
+  BuiltSnapshot b;
+  if (!h->builder->take(&b)) return MQM_OK;
+  h->builds++;
+  h->last_build_ms = b.build_ms;
+  h->last_build_ops = b.n_ops;
+  if (published) *published = 1;
+  return install(h, std::move(b.snap), b.version);
+}
+
+// after a logged mutation: the periodic-rebuild policy (mqm_commit_policy)
+void maybe_submit(mqm_index *h) {
+  if (!h->async() || h->journal.empty()) return;
+  if (h->policy_ops && h->journal.size() >= h->policy_ops) return submit_locked(h);
+  if (h->policy_ms && std::chrono::steady_clock::now() - h->journal_t0 >= std::chrono::milliseconds(h->policy_ms))
+    submit_locked(h);
+}
+
 int commit_locked(mqm_index *h) {
   if (h->snap && h->snap_version == h->store.version()) return MQM_OK;
+  if (h->async()) {  // through the builder, so its shadow store stays in step
+    if (!h->journal.empty() || !h->builder) submit_locked(h);
+    int rc = h->builder->wait_idle();
+    if (rc != MQM_OK) return rc;
+    return publish_locked(h, nullptr);
+  }
   auto hs = std::make_shared<HostSnapshot>();
   int rc = flatten(h->store, hs.get());
   if (rc != MQM_OK) return rc;
   std::unique_ptr<GpuSnapshot> g;
-  rc = upload(std::move(hs), h->cfg.device, &g);
+  rc = upload(std::move(hs), h->cfg.device, h->stream, &g);
   if (rc != MQM_OK) return rc;
-  // the previous snapshot may still be read by kernels queued on any stream
-  if (h->snap && hipDeviceSynchronize() != hipSuccess) return MQM_EHIP;
-  h->snap = std::move(g);
-  h->snap_version = h->store.version();
-  return MQM_OK;
+  return install(h, std::move(g), h->store.version());
 }
 
 int ensure_snapshot(mqm_index *h) {
   if (!h->snap || (h->cfg.flags & MQM_CFG_AUTOCOMMIT)) return commit_locked(h);
+  if (h->async()) {
+    maybe_submit(h);
+    return publish_locked(h, nullptr);
+  }
   return MQM_OK;
 }
 
@@ -144,6 +213,7 @@ int mqm_create(const mqm_config *cfg, mqm_index **out) {
 
 int mqm_destroy(mqm_index *h) {
   if (!h) return MQM_EINVAL;
+  h->builder.reset();  // finishes a running build and joins the worker
   if (h->cfg.device != MQM_DEVICE_NONE) {
     (void)hipSetDevice(h->cfg.device);
     (void)hipDeviceSynchronize();
@@ -160,6 +230,11 @@ int mqm_subscribe(mqm_index *h, const char *client, size_t client_len, const cha
     std::lock_guard<std::mutex> g(h->mu);
     bool n = h->store.subscribe(sv(client, client_len), sv(filter, filter_len), sub->qos, sub->no_local,
                                 sub->retain_as_published, sub->retain_handling, sub->identifier);
+    if (h->async()) {
+      h->journal.subscribe(sv(client, client_len), sv(filter, filter_len), sub->qos, sub->no_local,
+                           sub->retain_as_published, sub->retain_handling, sub->identifier);
+      maybe_submit(h);
+    }
     if (is_new) *is_new = n ? 1 : 0;
     return MQM_OK;
   });
@@ -173,11 +248,13 @@ int mqm_subscribe_many(mqm_index *h, size_t n, const char *client_bytes, const u
     std::lock_guard<std::mutex> g(h->mu);
     for (size_t i = 0; i < n; i++) {
       const mqm_subscription &s = subs[i];
-      bool r = h->store.subscribe(sv(client_bytes + client_offs[i], client_offs[i + 1] - client_offs[i]),
-                                  sv(filter_bytes + filter_offs[i], filter_offs[i + 1] - filter_offs[i]), s.qos,
-                                  s.no_local, s.retain_as_published, s.retain_handling, s.identifier);
+      const auto c = sv(client_bytes + client_offs[i], client_offs[i + 1] - client_offs[i]);
+      const auto f = sv(filter_bytes + filter_offs[i], filter_offs[i + 1] - filter_offs[i]);
+      bool r = h->store.subscribe(c, f, s.qos, s.no_local, s.retain_as_published, s.retain_handling, s.identifier);
+      if (h->async()) h->journal.subscribe(c, f, s.qos, s.no_local, s.retain_as_published, s.retain_handling, s.identifier);
       if (is_new) is_new[i] = r ? 1 : 0;
     }
+    maybe_submit(h);
     return MQM_OK;
   });
 }
@@ -188,7 +265,28 @@ int mqm_unsubscribe(mqm_index *h, const char *filter, size_t filter_len, const c
   return guarded([&] {
     std::lock_guard<std::mutex> g(h->mu);
     bool r = h->store.unsubscribe(sv(filter, filter_len), sv(client, client_len));
+    if (r && h->async()) {  // false: no node, nothing changed (topics.go:334-336)
+      h->journal.unsubscribe(sv(filter, filter_len), sv(client, client_len));
+      maybe_submit(h);
+    }
     if (existed) *existed = r ? 1 : 0;
+    return MQM_OK;
+  });
+}
+
+int mqm_unsubscribe_many(mqm_index *h, size_t n, const char *filter_bytes, const uint64_t *filter_offs,
+                         const char *client_bytes, const uint64_t *client_offs, uint8_t *existed) {
+  if (!h || !filter_offs || !client_offs) return MQM_EINVAL;
+  return guarded([&] {
+    std::lock_guard<std::mutex> g(h->mu);
+    for (size_t i = 0; i < n; i++) {
+      const auto f = sv(filter_bytes + filter_offs[i], filter_offs[i + 1] - filter_offs[i]);
+      const auto c = sv(client_bytes + client_offs[i], client_offs[i + 1] - client_offs[i]);
+      bool r = h->store.unsubscribe(f, c);
+      if (r && h->async()) h->journal.unsubscribe(f, c);
+      if (existed) existed[i] = r ? 1 : 0;
+    }
+    maybe_submit(h);
     return MQM_OK;
   });
 }
@@ -199,6 +297,10 @@ int mqm_retain_message(mqm_index *h, const char *topic, size_t topic_len, uint64
   return guarded([&] {
     std::lock_guard<std::mutex> g(h->mu);
     int64_t r = h->store.retain_message(sv(topic, topic_len), message_ref, payload_len, retain_flag != 0);
+    if (h->async()) {
+      h->journal.retain(sv(topic, topic_len), message_ref, payload_len, retain_flag != 0);
+      maybe_submit(h);
+    }
     if (result) *result = r;
     return MQM_OK;
   });
@@ -211,10 +313,13 @@ int mqm_retain_many(mqm_index *h, size_t n, const char *topic_bytes, const uint6
   return guarded([&] {
     std::lock_guard<std::mutex> g(h->mu);
     for (size_t i = 0; i < n; i++) {
-      int64_t r = h->store.retain_message(sv(topic_bytes + topic_offs[i], topic_offs[i + 1] - topic_offs[i]),
-                                          message_refs[i], payload_lens[i], retain_flags ? retain_flags[i] != 0 : true);
+      const auto t = sv(topic_bytes + topic_offs[i], topic_offs[i + 1] - topic_offs[i]);
+      const bool flag = retain_flags ? retain_flags[i] != 0 : true;
+      int64_t r = h->store.retain_message(t, message_refs[i], payload_lens[i], flag);
+      if (h->async()) h->journal.retain(t, message_refs[i], payload_lens[i], flag);
       if (results) results[i] = r;
     }
+    maybe_submit(h);
     return MQM_OK;
   });
 }
@@ -230,8 +335,7 @@ int mqm_commit(mqm_index *h) {
   if (!h) return MQM_EINVAL;
   return guarded([&] {
     std::lock_guard<std::mutex> g(h->mu);
-    if (h->cfg.device == MQM_DEVICE_NONE) return MQM_ENODEV;
-    if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
+    if (h->cfg.device != MQM_DEVICE_NONE && hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
     return commit_locked(h);
   });
 }
@@ -246,9 +350,10 @@ int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t 
     int rc = ensure_snapshot(h);
     if (rc != MQM_OK) return rc;
     MatchOutput mo;
+    note_stream(h, (hipStream_t)hip_stream);
     rc = match_device(h->snap->dev, h->ws, d_topic_bytes, d_topic_offsets, n_topics, (hipStream_t)hip_stream, &mo);
     if (rc != 0) return rc;
-    h->matched = h->snap.get();
+    h->matched_serial = h->snap_serial;
     h->last_mo = mo;
     out->n_topics = mo.n_topics;
     out->n_deliveries = mo.n_deliveries;
@@ -291,9 +396,10 @@ int mqm_match_batch(mqm_index *h, const char *topic_bytes, const uint64_t *topic
         hipSuccess)
       return MQM_EHIP;
     MatchOutput mo;
+    note_stream(h, h->stream);
     rc = match_device(h->snap->dev, ws, d_bytes, d_offs, n_topics, h->stream, &mo);
     if (rc != 0) return rc;
-    h->matched = h->snap.get();
+    h->matched_serial = h->snap_serial;
     h->last_mo = mo;
     IdentOutput io;
     const bool want_ids = (h->cfg.flags & MQM_CFG_IDENTIFIERS) != 0;
@@ -342,8 +448,9 @@ int mqm_identifiers_device(mqm_index *h, void *hip_stream, mqm_device_identifier
     std::lock_guard<std::mutex> g(h->mu);
     if (h->cfg.device == MQM_DEVICE_NONE) return MQM_ENODEV;
     // the records of the last forward match, against the snapshot it read
-    if (!h->matched || h->matched != h->snap.get()) return MQM_EINVAL;
+    if (!h->snap || h->matched_serial != h->snap_serial) return MQM_EINVAL;
     if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
+    note_stream(h, (hipStream_t)hip_stream);
     IdentOutput io;
     const int rc = identifiers_device(h->snap->dev, h->ws, (hipStream_t)hip_stream, &io);
     if (rc != 0) return rc == -2 ? MQM_ENOMEM : rc == -1 ? MQM_EINVAL : MQM_EHIP;
@@ -360,8 +467,9 @@ int mqm_dense_device(mqm_index *h, void *hip_stream, mqm_device_dense *out) {
   return guarded([&] {
     std::lock_guard<std::mutex> g(h->mu);
     if (h->cfg.device == MQM_DEVICE_NONE) return MQM_ENODEV;
-    if (!h->matched || h->matched != h->snap.get()) return MQM_EINVAL;
+    if (!h->snap || h->matched_serial != h->snap_serial) return MQM_EINVAL;
     if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
+    note_stream(h, (hipStream_t)hip_stream);
     DenseOutput dn;
     const int rc = densify(h->ws, h->last_mo, (hipStream_t)hip_stream, &dn);
     if (rc != 0) return rc == -2 ? MQM_ENOMEM : MQM_EHIP;
@@ -421,6 +529,7 @@ int mqm_messages_device(mqm_index *h, const uint8_t *d_filter_bytes, const uint6
     int rc = ensure_snapshot(h);
     if (rc != MQM_OK) return rc;
     MessagesOutput mo;
+    note_stream(h, (hipStream_t)hip_stream);
     rc = messages_device(h->snap->dev, h->snap->has_retained ? &h->snap->ret : nullptr, h->ws, d_filter_bytes,
                          d_filter_offsets, n_filters, (hipStream_t)hip_stream, &mo);
     if (rc != 0) return rc;
@@ -459,6 +568,7 @@ int mqm_messages_batch(mqm_index *h, const char *filter_bytes, const uint64_t *f
         hipSuccess)
       return MQM_EHIP;
     MessagesOutput mo;
+    note_stream(h, h->stream);
     rc = messages_device(h->snap->dev, h->snap->has_retained ? &h->snap->ret : nullptr, ws, d_bytes, d_offs,
                          n_filters, h->stream, &mo);
     if (rc != 0) return rc;
@@ -553,6 +663,66 @@ int mqm_is_valid_filter(const char *filter, size_t len, int for_publish) {
 }
 
 int mqm_is_shared_filter(const char *filter, size_t len) { return is_shared_filter(sv(filter, len)) ? 1 : 0; }
+
+int mqm_commit_async(mqm_index *h) {
+  if (!h) return MQM_EINVAL;
+  return guarded([&] {
+    std::lock_guard<std::mutex> g(h->mu);
+    if (!h->async()) return MQM_EINVAL;
+    if (h->cfg.device != MQM_DEVICE_NONE && hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
+    if (!h->journal.empty() || !h->builder) submit_locked(h);
+    return MQM_OK;
+  });
+}
+
+int mqm_commit_poll(mqm_index *h, int wait, int *published) {
+  if (!h) return MQM_EINVAL;
+  return guarded([&] {
+    std::lock_guard<std::mutex> g(h->mu);
+    if (published) *published = 0;
+    if (!h->async()) return MQM_EINVAL;
+    if (h->cfg.device != MQM_DEVICE_NONE && hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
+    if (wait && h->builder) {
+      int rc = h->builder->wait_idle();
+      if (rc != MQM_OK) return rc;
+    }
+    return publish_locked(h, published);
+  });
+}
+
+int mqm_commit_policy(mqm_index *h, uint64_t max_ops, uint32_t max_ms) {
+  if (!h) return MQM_EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  if (!h->async()) return MQM_EINVAL;
+  h->policy_ops = max_ops;
+  h->policy_ms = max_ms;
+  return MQM_OK;
+}
+
+int mqm_commit_state_get(mqm_index *h, mqm_commit_state *out) {
+  if (!h || !out) return MQM_EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  memset(out, 0, sizeof(*out));
+  out->store_version = h->store.version();
+  out->snapshot_version = h->snap ? h->snap_version : 0;
+  out->has_snapshot = h->snap ? 1 : 0;
+  out->pending_ops = h->journal.size();
+  out->building = h->builder && h->builder->busy() ? 1 : 0;
+  out->builds = h->builds;
+  out->last_build_ops = h->last_build_ops;
+  out->last_build_ms = h->last_build_ms;
+  return MQM_OK;
+}
+
+int mqm_snapshot_digest(mqm_index *h, uint64_t *out) {
+  if (!h || !out) return MQM_EINVAL;
+  return guarded([&] {
+    std::lock_guard<std::mutex> g(h->mu);
+    if (!h->snap) return MQM_EINVAL;
+    *out = snapshot_digest(*h->snap->host);
+    return MQM_OK;
+  });
+}
 
 int mqm_snapshot_stats_get(mqm_index *h, mqm_snapshot_stats *out) {
   if (!h || !out) return MQM_EINVAL;

@@ -277,9 +277,14 @@ GpuSnapshot::~GpuSnapshot() {
     if (b) (void)hipFree(b);
 }
 
-int upload(std::shared_ptr<const HostSnapshot> hs, int device, std::unique_ptr<GpuSnapshot> *out) {
-  if (hipSetDevice(device) != hipSuccess) return MQM_EHIP;
+int upload(std::shared_ptr<const HostSnapshot> hs, int device, hipStream_t stream, std::unique_ptr<GpuSnapshot> *out) {
   auto g = std::make_unique<GpuSnapshot>();
+  if (device < 0) {  // host-only index: no device copy
+    g->host = std::move(hs);
+    *out = std::move(g);
+    return MQM_OK;
+  }
+  if (hipSetDevice(device) != hipSuccess) return MQM_EHIP;
   const bool ret = !hs->cum.empty();
   const void *src[GpuSnapshot::kNumBuffers] = {hs->nodes.data(),     hs->edges.data(),     hs->subs.data(),
                                                hs->tok_pool.data(),  hs->subtree.data(),   hs->child_off.data(),
@@ -294,9 +299,11 @@ int upload(std::shared_ptr<const HostSnapshot> hs, int device, std::unique_ptr<G
     if (i >= 4 && !ret) break;
     // +64 B: walk_step reads 64 B at any node descriptor (the last one included)
     if (hipMalloc(&g->buffers[i], (sz[i] ? sz[i] : 16) + 64) != hipSuccess) return MQM_ENOMEM;
-    if (sz[i] && hipMemcpy(g->buffers[i], src[i], sz[i], hipMemcpyHostToDevice) != hipSuccess) return MQM_EHIP;
+    if (sz[i] && hipMemcpyAsync(g->buffers[i], src[i], sz[i], hipMemcpyHostToDevice, stream) != hipSuccess)
+      return MQM_EHIP;
     g->device_bytes += sz[i];
   }
+  if (hipStreamSynchronize(stream) != hipSuccess) return MQM_EHIP;
   if (ret) {
     g->has_retained = true;
     g->ret.subtree = (const uint32_t *)g->buffers[4];

@@ -1,5 +1,6 @@
 // maxmq_amd/csrc/flatten.h — host store -> GPU-resident CSR level-trie.
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include <memory>
@@ -52,6 +53,9 @@ struct GpuSnapshot {
   ~GpuSnapshot();
 };
 
-int upload(std::shared_ptr<const HostSnapshot> hs, int device, std::unique_ptr<GpuSnapshot> *out);
+// Copies on `stream` and waits for them (nullptr: the null stream).  device < 0
+// (MQM_DEVICE_NONE) wraps the host snapshot without device buffers, so a
+// host-only index still has stats and a digest.
+int upload(std::shared_ptr<const HostSnapshot> hs, int device, hipStream_t stream, std::unique_ptr<GpuSnapshot> *out);
 
 }  // namespace mqm
