@@ -9,13 +9,46 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <unordered_map>
+#include <thread>
 
 #include "../../include/mqmatch.h"
 
 namespace mqm {
+
+namespace {
+// run f(t) for t in [0, n) on up to 16 host threads (the box's CPU share)
+template <class F>
+void parallel_for(uint32_t n, F &&f) {
+  const uint32_t hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const uint32_t nt = std::min(hw, n);
+  if (nt <= 1) {
+    for (uint32_t t = 0; t < n; t++) f(t);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (uint32_t w = 0; w < nt; w++)
+    th.emplace_back([&, w] {
+      for (uint32_t t = w; t < n; t += nt) f(t);
+    });
+  for (auto &x : th) x.join();
+}
+
+// MQM_FLATTEN_TRACE=1: per-phase wall time to stderr
+struct PhaseTimer {
+  bool on = getenv("MQM_FLATTEN_TRACE") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void mark(const char *what) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "[flatten] %-10s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(now - t).count());
+    t = now;
+  }
+};
+}  // namespace
 
 // kMetaMulti (snapshot.h).  Levels of a filter are the keys on its node's
 // path; two filters of one client can be gathered for the same topic only if
@@ -46,18 +79,25 @@ static void mark_multi(const Store &st, const std::vector<uint32_t> &order, Host
     }
     return true;
   };
-  for (uint32_t c = 0; c < nc; c++) {
-    const uint32_t lo = cstart[c], hi = cstart[c + 1];
-    for (uint32_t x = lo; x < hi; x++) {
-      const uint32_t sx = by_client[x], nx = sub_node[sx], px = nodes[nx].parent;
-      // the parent probe emits a '#' node's subscriptions after a literal hit on its parent
-      bool multi = hi - lo > kMaxPairwise ||
-                   (nodes[nx].key == hash_tok && px != st.root() && !wild(nodes[px].key));
-      for (uint32_t y = lo; !multi && y < hi; y++) multi = y != x && compatible(nx, sub_node[by_client[y]]);
-      if (multi) hs.subs[sx].meta |= kMetaMulti;
-      else hs.n_solo++;
+  // clients are independent: chunks of them in parallel (each sub belongs to one client)
+  constexpr uint32_t kChunks = 64;
+  std::vector<uint64_t> solo(kChunks, 0);
+  parallel_for(kChunks, [&](uint32_t ch) {
+    const uint32_t c_lo = (uint32_t)((uint64_t)nc * ch / kChunks), c_hi = (uint32_t)((uint64_t)nc * (ch + 1) / kChunks);
+    for (uint32_t c = c_lo; c < c_hi; c++) {
+      const uint32_t lo = cstart[c], hi = cstart[c + 1];
+      for (uint32_t x = lo; x < hi; x++) {
+        const uint32_t sx = by_client[x], nx = sub_node[sx], px = nodes[nx].parent;
+        // the parent probe emits a '#' node's subscriptions after a literal hit on its parent
+        bool multi = hi - lo > kMaxPairwise ||
+                     (nodes[nx].key == hash_tok && px != st.root() && !wild(nodes[px].key));
+        for (uint32_t y = lo; !multi && y < hi; y++) multi = y != x && compatible(nx, sub_node[by_client[y]]);
+        if (multi) hs.subs[sx].meta |= kMetaMulti;
+        else solo[ch]++;
+      }
     }
-  }
+  });
+  for (uint64_t v : solo) hs.n_solo += v;
 }
 
 // DeviceRetained arrays (snapshot.h) over the preorder ids
@@ -104,7 +144,9 @@ static void build_retained(const Store &st, const std::vector<uint32_t> &order, 
   hs.refs.push_back(hs.has_empty ? it->second.msg_ref : 0);
 }
 
+
 int flatten(const Store &st, HostSnapshot *out) {
+  PhaseTimer pt;
   const auto &nodes = st.nodes();
   const uint32_t plus_tok = st.plus_token(), hash_tok = st.hash_token();
   HostSnapshot &hs = *out;
@@ -114,6 +156,11 @@ int flatten(const Store &st, HostSnapshot *out) {
   std::vector<uint32_t> order;
   std::vector<uint32_t> new_id(nodes.size(), kNone);
   order.reserve(nodes.size());
+  // '+' / '#' children (store ids) by preorder id, found on the child list
+  std::vector<uint32_t> pc_of, hc_of, nlit;
+  pc_of.reserve(nodes.size());
+  hc_of.reserve(nodes.size());
+  nlit.reserve(nodes.size());
   std::vector<uint32_t> stack{st.root()};
   std::vector<uint32_t> lits;
   while (!stack.empty()) {
@@ -121,16 +168,26 @@ int flatten(const Store &st, HostSnapshot *out) {
     stack.pop_back();
     new_id[n] = (uint32_t)order.size();
     order.push_back(n);
-    uint32_t pc = st.child(n, plus_tok), hc = st.child(n, hash_tok);
+    uint32_t pc = kNone, hc = kNone;
+    lits.clear();
+    for (uint32_t c = nodes[n].first_child; c != kNone; c = nodes[c].next_sibling) {
+      if (nodes[c].key == plus_tok)
+        pc = c;
+      else if (nodes[c].key == hash_tok)
+        hc = c;
+      else
+        lits.push_back(c);
+    }
+    pc_of.push_back(pc);
+    hc_of.push_back(hc);
+    nlit.push_back((uint32_t)lits.size());
     if (hc != kNone) stack.push_back(hc);  // LIFO: '#' visited last
     if (pc != kNone) stack.push_back(pc);
-    lits.clear();
-    for (uint32_t c = nodes[n].first_child; c != kNone; c = nodes[c].next_sibling)
-      if (c != pc && c != hc) lits.push_back(c);
     for (auto it = lits.rbegin(); it != lits.rend(); ++it) stack.push_back(*it);
   }
   const uint64_t nn = order.size();
   if (nn >= (1ull << 30)) return MQM_ELIMIT;  // k_walk packs node id << 2 | item kind
+  pt.mark("preorder");
 
   // 2. descriptors, subscription ranges, flags
   hs.nodes.resize(nn);
@@ -139,7 +196,7 @@ int flatten(const Store &st, HostSnapshot *out) {
   for (uint64_t i = 0; i < nn; i++) {
     const HNode &h = nodes[order[i]];
     NodeDesc &d = hs.nodes[i];
-    uint32_t pc = st.child(order[i], plus_tok), hc = st.child(order[i], hash_tok);
+    const uint32_t pc = pc_of[i], hc = hc_of[i];
     d.plus = pc == kNone ? kNone : new_id[pc];
     d.hash = hc == kNone ? kNone : new_id[hc];
     n_literal_edges += h.n_children - (pc != kNone) - (hc != kNone);
@@ -157,7 +214,7 @@ int flatten(const Store &st, HostSnapshot *out) {
                                                  (s.ident > 0 ? kMetaIdent : 0u)});
           hs.sub_info.push_back(SubInfo{s.filter, s.client, s.ident, s.qos, s.no_local, s.rap, s.rh});
         }
-        sn = st.child(sn, hash_tok);
+        sn = hc_of[k];
         if (sn == kNone) break;
         k = new_id[sn];
       }
@@ -182,8 +239,11 @@ int flatten(const Store &st, HostSnapshot *out) {
     d.sh_cnt_flags = (uint32_t)h.shared.size() | ((uint32_t)f << 24);
     hs.height = std::max(hs.height, h.depth);
   }
+  pt.mark("nodes");
   mark_multi(st, order, hs);
+  pt.mark("multi");
   if (st.retained_len() > 0) build_retained(st, order, new_id, hs);
+  pt.mark("retained");
   // every range: solo entries first, then multi (stable); count the multi ones
   std::vector<uint32_t> own_multi(nn, 0);
   {
@@ -217,6 +277,7 @@ int flatten(const Store &st, HostSnapshot *out) {
     }
   }
 
+  pt.mark("ranges");
   // 3. literal edges -> open-addressed table of 128-B buckets, linear probing
   //    at load factor `load` (default 0.2; env MQM_EDGE_LOAD in (0, 0.9]): a probe
   //    chain that leaves its 128-B bucket costs another dependent HBM round
@@ -231,42 +292,107 @@ int flatten(const Store &st, HostSnapshot *out) {
       std::max<uint64_t>(1, (uint64_t)((double)n_literal_edges / (load * kEdgesPerBucket)) + 1);
   hs.n_buckets = buckets;
   hs.n_edges = n_literal_edges;
+  const uint64_t n_slots = buckets * kEdgesPerBucket;
+  if (n_literal_edges >= kNone) return MQM_ELIMIT;
+  // long tokens (> kInlineMax bytes) go to the pool in token-id order
+  const Interner &toks = st.tokens();
+  std::vector<uint32_t> pool_off(toks.size(), kNone);
+  for (uint32_t t = 0; t < toks.size(); t++) {
+    const std::string_view tok = toks.name(t);
+    if (tok.size() <= kInlineMax) continue;
+    if (hs.tok_pool.size() + tok.size() > 0xFFFFFFFFull) return MQM_ELIMIT;
+    pool_off[t] = (uint32_t)hs.tok_pool.size();
+    hs.tok_pool.insert(hs.tok_pool.end(), tok.begin(), tok.end());
+  }
+  // (a) every literal edge in (parent preorder, child list) order, in parallel
+  //     over node ranges; (b) stable partition by home slot into kParts
+  //     contiguous slot ranges; (c) linear-probing insertion per partition in
+  //     edge order, in parallel; (d) edges whose probe runs past their
+  //     partition's end, serially in partition order.  The layout depends on
+  //     kParts only, not on the thread count, so digests are reproducible.
+  constexpr uint32_t kParts = 256, kChunks = 64;
+  std::vector<uint64_t> eoff(nn + 1, 0);
+  for (uint64_t i = 0; i < nn; i++) eoff[i + 1] = eoff[i] + nlit[i];
+  std::vector<EdgeEntry, NoInitAlloc<EdgeEntry>> staged(n_literal_edges);
+  std::vector<uint64_t, NoInitAlloc<uint64_t>> home(n_literal_edges);
+  parallel_for(kChunks, [&](uint32_t c) {
+    const uint64_t lo = nn * c / kChunks, hi = nn * (c + 1) / kChunks;
+    for (uint64_t i = lo; i < hi; i++) {
+      uint64_t e_i = eoff[i];
+      const uint32_t pc = pc_of[i], hc = hc_of[i];
+      for (uint32_t c2 = nodes[order[i]].first_child; c2 != kNone; c2 = nodes[c2].next_sibling) {
+        if (c2 == pc || c2 == hc) continue;
+        const uint32_t cn = new_id[c2];
+        const std::string_view tok = toks.name(nodes[c2].key);
+        Key k = make_key([&](uint32_t j) { return (uint8_t)tok[j]; }, (uint32_t)tok.size());
+        EdgeEntry &e = staged[e_i];
+        e.k0 = k.k0;
+        e.k1 = k.k1;
+        e.parent = (uint32_t)i;
+        e.child = cn;
+        e.tok_off = key_is_long(k) ? pool_off[nodes[c2].key] : 0;
+        e.tok_len = (uint32_t)tok.size();
+        e.desc = hs.nodes[cn];
+        home[e_i] = bucket_of(edge_hash((uint32_t)i, k), hs.n_buckets) * kEdgesPerBucket;
+        e_i++;
+      }
+    }
+  });
+  auto part_of = [&](uint64_t slot) { return (uint32_t)((unsigned __int128)slot * kParts / n_slots); };
+  auto part_lo = [&](uint32_t p) { return (uint64_t)(((unsigned __int128)n_slots * p + kParts - 1) / kParts); };
+  pt.mark("e:stage");
+  std::vector<uint64_t> cnt((uint64_t)kChunks * kParts, 0);  // [chunk][part]
+  parallel_for(kChunks, [&](uint32_t c) {
+    const uint64_t lo = n_literal_edges * c / kChunks, hi = n_literal_edges * (c + 1) / kChunks;
+    for (uint64_t e = lo; e < hi; e++) cnt[(uint64_t)c * kParts + part_of(home[e])]++;
+  });
+  std::vector<uint64_t> pstart(kParts + 1, 0);
+  {
+    uint64_t run = 0;
+    for (uint32_t p = 0; p < kParts; p++) {
+      pstart[p] = run;
+      for (uint32_t c = 0; c < kChunks; c++) {
+        const uint64_t v = cnt[(uint64_t)c * kParts + p];
+        cnt[(uint64_t)c * kParts + p] = run;
+        run += v;
+      }
+    }
+    pstart[kParts] = run;
+  }
+  std::vector<uint32_t, NoInitAlloc<uint32_t>> by_part(n_literal_edges);
+  parallel_for(kChunks, [&](uint32_t c) {
+    const uint64_t lo = n_literal_edges * c / kChunks, hi = n_literal_edges * (c + 1) / kChunks;
+    for (uint64_t e = lo; e < hi; e++) by_part[cnt[(uint64_t)c * kParts + part_of(home[e])]++] = (uint32_t)e;
+  });
+  pt.mark("e:part");
   EdgeEntry empty;
   memset(&empty, 0, sizeof(empty));
   empty.parent = kNone;
   empty.child = kNone;
-  hs.edges.assign(buckets * kEdgesPerBucket, empty);
-  const uint64_t n_slots = buckets * kEdgesPerBucket;
-  std::unordered_map<uint32_t, uint32_t> pool_off;
-  for (uint64_t i = 0; i < nn; i++) {
-    const uint32_t pc = hs.nodes[i].plus, hc = hs.nodes[i].hash;
-    for (uint32_t c = nodes[order[i]].first_child; c != kNone; c = nodes[c].next_sibling) {
-      const uint32_t cn = new_id[c];
-      if (cn == pc || cn == hc) continue;
-      const std::string_view tok = st.tokens().name(nodes[c].key);
-      Key k = make_key([&](uint32_t j) { return (uint8_t)tok[j]; }, (uint32_t)tok.size());
-      EdgeEntry e;
-      e.k0 = k.k0;
-      e.k1 = k.k1;
-      e.parent = (uint32_t)i;
-      e.child = cn;
-      e.tok_off = 0;
-      e.tok_len = (uint32_t)tok.size();
-      if (key_is_long(k)) {
-        auto it = pool_off.find(nodes[c].key);
-        if (it == pool_off.end()) {
-          if (hs.tok_pool.size() + tok.size() > 0xFFFFFFFFull) return MQM_ELIMIT;
-          it = pool_off.emplace(nodes[c].key, (uint32_t)hs.tok_pool.size()).first;
-          hs.tok_pool.insert(hs.tok_pool.end(), tok.begin(), tok.end());
-        }
-        e.tok_off = it->second;
-      }
-      e.desc = hs.nodes[cn];
-      uint64_t slot = bucket_of(edge_hash((uint32_t)i, k), hs.n_buckets) * kEdgesPerBucket;
-      while (hs.edges[slot].parent != kNone) slot = slot + 1 == n_slots ? 0 : slot + 1;
-      hs.edges[slot] = e;
+  hs.edges.resize(n_slots);
+  pt.mark("e:alloc");
+  std::vector<std::vector<uint32_t>> spill(kParts);
+  parallel_for(kParts, [&](uint32_t p) {
+    const uint64_t lo = part_lo(p), hi = part_lo(p + 1);
+    std::fill(hs.edges.begin() + lo, hs.edges.begin() + hi, empty);
+    for (uint64_t j = pstart[p]; j < pstart[p + 1]; j++) {
+      const uint32_t e = by_part[j];
+      uint64_t slot = home[e];
+      while (slot < hi && hs.edges[slot].parent != kNone) slot++;
+      if (slot == hi)
+        spill[p].push_back(e);
+      else
+        hs.edges[slot] = staged[e];
     }
-  }
+  });
+  pt.mark("e:insert");
+  for (uint32_t p = 0; p < kParts; p++)
+    for (uint32_t e : spill[p]) {
+      uint64_t slot = home[e];
+      while (hs.edges[slot].parent != kNone) slot = slot + 1 == n_slots ? 0 : slot + 1;
+      hs.edges[slot] = staged[e];
+    }
+  pt.mark("edges");
   if (hs.tok_pool.empty()) hs.tok_pool.push_back(0);
   if (hs.subs.empty()) hs.subs.push_back(SubEnt{0, 0});
   return MQM_OK;

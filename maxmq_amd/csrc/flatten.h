@@ -4,12 +4,33 @@
 #include <stdint.h>
 
 #include <memory>
+#include <utility>
 #include <vector>
 
 #include "snapshot.h"
 #include "store.h"
 
 namespace mqm {
+
+// std::allocator that default-initialises (no zero fill): the big snapshot
+// arrays are first touched by the threads that fill them
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = NoInitAlloc<U>;
+  };
+  NoInitAlloc() = default;
+  template <class U>
+  NoInitAlloc(const NoInitAlloc<U> &) {}
+  template <class U, class... A>
+  void construct(U *p, A &&...a) {
+    if constexpr (sizeof...(A) == 0)
+      ::new ((void *)p) U;
+    else
+      ::new ((void *)p) U(std::forward<A>(a)...);
+  }
+};
 
 // per-subscription side information, kept on the host to resolve result ids
 struct SubInfo {
@@ -21,7 +42,7 @@ struct SubInfo {
 
 struct HostSnapshot {
   std::vector<NodeDesc> nodes;
-  std::vector<EdgeEntry> edges;  // n_buckets * kEdgesPerBucket
+  std::vector<EdgeEntry, NoInitAlloc<EdgeEntry>> edges;  // n_buckets * kEdgesPerBucket
   std::vector<SubEnt> subs;
   std::vector<SubInfo> sub_info;     // by non-shared sid
   std::vector<SubInfo> shared_info;  // by shared sid

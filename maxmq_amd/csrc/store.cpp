@@ -148,10 +148,64 @@ Store::Store() {
   nodes_[0].key = tokens_.intern("");
 }
 
-uint32_t Store::child(uint32_t parent, uint32_t tok) const {
-  auto it = children_.find(edge_id(parent, tok));
-  return it == children_.end() ? kNone : it->second;
+uint32_t EdgeMap::find(uint64_t key) const {
+  if (!n_) return kNone;
+  for (uint64_t i = mix(key) & mask_;; i = (i + 1) & mask_) {
+    if (keys_[i] == key) return vals_[i];
+    if (keys_[i] == ~0ull) return kNone;
+  }
 }
+
+void EdgeMap::grow() {
+  std::vector<uint64_t> ok;
+  std::vector<uint32_t> ov;
+  ok.swap(keys_);
+  ov.swap(vals_);
+  const uint64_t cap = ok.empty() ? 1024 : ok.size() * 2;
+  keys_.assign(cap, ~0ull);
+  vals_.assign(cap, 0);
+  mask_ = cap - 1;
+  for (uint64_t j = 0; j < ok.size(); j++) {
+    if (ok[j] == ~0ull) continue;
+    uint64_t i = mix(ok[j]) & mask_;
+    while (keys_[i] != ~0ull) i = (i + 1) & mask_;
+    keys_[i] = ok[j];
+    vals_[i] = ov[j];
+  }
+}
+
+void EdgeMap::insert(uint64_t key, uint32_t val) {
+  if ((n_ + 1) * 2 > keys_.size()) grow();  // load <= 0.5
+  uint64_t i = mix(key) & mask_;
+  while (keys_[i] != ~0ull) i = (i + 1) & mask_;
+  keys_[i] = key;
+  vals_[i] = val;
+  n_++;
+}
+
+void EdgeMap::erase(uint64_t key) {
+  if (!n_) return;
+  uint64_t i = mix(key) & mask_;
+  while (keys_[i] != key) {
+    if (keys_[i] == ~0ull) return;
+    i = (i + 1) & mask_;
+  }
+  // backward shift: pull later entries of the cluster into the hole when
+  // their home slot does not lie cyclically in (hole, j]
+  for (uint64_t j = (i + 1) & mask_;; j = (j + 1) & mask_) {
+    if (keys_[j] == ~0ull) break;
+    const uint64_t home = mix(keys_[j]) & mask_;
+    if (((j - home) & mask_) >= ((j - i) & mask_)) {
+      keys_[i] = keys_[j];
+      vals_[i] = vals_[j];
+      i = j;
+    }
+  }
+  keys_[i] = ~0ull;
+  n_--;
+}
+
+uint32_t Store::child(uint32_t parent, uint32_t tok) const { return children_.find(edge_id(parent, tok)); }
 
 uint32_t Store::new_node(uint32_t parent, uint32_t tok) {
   uint32_t id;
@@ -173,7 +227,7 @@ uint32_t Store::new_node(uint32_t parent, uint32_t tok) {
   if (p.first_child != kNone) nodes_[p.first_child].prev_sibling = id;
   p.first_child = id;
   p.n_children++;
-  children_.emplace(edge_id(parent, tok), id);
+  children_.insert(edge_id(parent, tok), id);
   return id;
 }
 

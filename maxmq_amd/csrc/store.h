@@ -61,6 +61,28 @@ class Interner {
   std::vector<uint64_t> table_;  // (hash high 32 bits << 32) | (id + 1); 0 = empty
 };
 
+// (parent << 32 | token) -> child: open addressing, linear probing,
+// backward-shift deletion (no tombstones), so lookups on the mutation path
+// touch one or two cache lines instead of a node-based bucket chain.
+class EdgeMap {
+ public:
+  uint32_t find(uint64_t key) const;  // kNone if absent
+  void insert(uint64_t key, uint32_t val);  // key must be absent
+  void erase(uint64_t key);
+  uint64_t size() const { return n_; }
+
+ private:
+  void grow();
+  static uint64_t mix(uint64_t k) {
+    k ^= k >> 31;
+    k *= 0x9E3779B97F4A7C15ull;
+    return k ^ (k >> 29);
+  }
+  std::vector<uint64_t> keys_;  // ~0 = empty
+  std::vector<uint32_t> vals_;
+  uint64_t n_ = 0, mask_ = 0;
+};
+
 struct RetainedRec {
   uint64_t msg_ref;
   uint32_t payload_len;
@@ -98,7 +120,7 @@ class Store {
 
   std::vector<HNode> nodes_;
   std::vector<uint32_t> free_;
-  std::unordered_map<uint64_t, uint32_t> children_;  // (parent << 32 | token) -> child
+  EdgeMap children_;
   Interner tokens_, clients_, filters_;
   std::unordered_map<std::string, RetainedRec> retained_;  // packets.Packets (Retained)
   uint32_t plus_tok_, hash_tok_;
