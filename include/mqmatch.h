@@ -129,6 +129,16 @@ int mqm_subscribe_many(mqm_index *h, size_t n, const char *client_bytes, const u
 /* TopicsIndex.Unsubscribe (topics.go:325-349): *existed = the reference's bool */
 int mqm_unsubscribe(mqm_index *h, const char *filter, size_t filter_len, const char *client, size_t client_len,
                     int *existed);
+/* Server.loadSubscriptions (server.go:1377-1393) over persisted records: json
+ * holds storage.Subscription JSON records (hooks/storage/storage.go:151-161)
+ * as a JSON array or as concatenated / newline-separated objects; each is
+ * decoded with encoding/json's rules (case-insensitive keys, unknown keys
+ * skipped, null = zero value) and Subscribed in order.  *n_loaded = records
+ * applied, *n_new = how many Subscribe calls returned true.  MQM_EINVAL at
+ * the first record encoding/json rejects, MQM_ELIMIT at one outside what the
+ * snapshot stores (qos > 2, retain_handling > 3, identifier outside int32);
+ * the records before it stay applied. */
+int mqm_load_subscriptions_json(mqm_index *h, const char *json, size_t len, uint64_t *n_loaded, uint64_t *n_new);
 /* n Unsubscribe calls in order (UnsubscribeClient at session expiry,
  * server.go:1109-1129); existed may be NULL */
 int mqm_unsubscribe_many(mqm_index *h, size_t n, const char *filter_bytes, const uint64_t *filter_offs,

@@ -250,6 +250,17 @@ class TopicsIndex:
         check("mqm_unsubscribe", lib().mqm_unsubscribe(self._h, f, len(f), c, len(c), C.byref(out)))
         return bool(out.value)
 
+    def load_subscriptions_json(self, blob: bytes) -> tuple:
+        """Server.loadSubscriptions over persisted storage.Subscription JSON
+        records (array or one object per line); -> (n_loaded, n_new)."""
+        n, fresh = C.c_uint64(), C.c_uint64()
+        rc = lib().mqm_load_subscriptions_json(self._h, blob, len(blob), C.byref(n), C.byref(fresh))
+        if rc != capi.MQM_OK:
+            err = MqmError("mqm_load_subscriptions_json", rc)
+            err.n_loaded = int(n.value)
+            raise err
+        return int(n.value), int(fresh.value)
+
     def unsubscribe_many(self, filters, clients) -> np.ndarray:
         """Bulk Unsubscribe of (filters[i], clients[i]) (tools.mqgen.Strings) in order; -> existed[]."""
         n = len(filters)

@@ -40,7 +40,7 @@ EXPORTED = [
     "mqm_retain_many", "mqm_messages_batch", "mqm_messages_one", "mqm_messages_num_filters", "mqm_messages_offsets",
     "mqm_messages_refs", "mqm_messages_free", "mqm_messages_device", "mqm_identifiers_device",
     "mqm_result_identifiers", "mqm_dense_device", "mqm_gather_shards", "mqm_commit_async", "mqm_commit_poll",
-    "mqm_commit_policy", "mqm_commit_state_get", "mqm_snapshot_digest", "mqm_unsubscribe_many",
+    "mqm_commit_policy", "mqm_commit_state_get", "mqm_snapshot_digest", "mqm_unsubscribe_many", "mqm_load_subscriptions_json",
 ]
 
 
@@ -173,6 +173,7 @@ def lib():
         "mqm_dense_device": ([vp, vp, C.POINTER(DeviceDense)], C.c_int),
         "mqm_gather_shards": ([u32, u32, C.POINTER(ShardPart), vp, vp, vp], C.c_int),
         "mqm_unsubscribe_many": ([vp, sz, vp, vp, vp, vp, vp], C.c_int),
+        "mqm_load_subscriptions_json": ([vp, C.c_char_p, sz, C.POINTER(u64), C.POINTER(u64)], C.c_int),
         "mqm_commit_async": ([vp], C.c_int),
         "mqm_commit_poll": ([vp, C.c_int, C.POINTER(C.c_int)], C.c_int),
         "mqm_commit_policy": ([vp, u64, u32], C.c_int),

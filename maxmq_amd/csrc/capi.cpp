@@ -14,6 +14,7 @@
 
 #include "../../include/mqmatch.h"
 #include "builder.h"
+#include "bulkload.h"
 #include "flatten.h"
 #include "match.h"
 #include "retained.h"
@@ -271,6 +272,28 @@ int mqm_unsubscribe(mqm_index *h, const char *filter, size_t filter_len, const c
     }
     if (existed) *existed = r ? 1 : 0;
     return MQM_OK;
+  });
+}
+
+int mqm_load_subscriptions_json(mqm_index *h, const char *json, size_t len, uint64_t *n_loaded, uint64_t *n_new) {
+  if (!h || (len && !json)) return MQM_EINVAL;
+  if (n_loaded) *n_loaded = 0;
+  if (n_new) *n_new = 0;
+  return guarded([&] {
+    std::lock_guard<std::mutex> g(h->mu);
+    uint64_t fresh = 0;
+    auto sink = [&](const std::string &client, const std::string &filter, const SubscriptionRecord &r) {
+      // the snapshot packs QoS in 2 bits and RH in 2; the identifier is int32
+      if (r.qos > 2 || r.retain_handling > 3 || r.identifier < INT32_MIN || r.identifier > INT32_MAX) return false;
+      const uint8_t nl = r.no_local ? 1 : 0, rap = r.retain_as_published ? 1 : 0;
+      if (h->store.subscribe(client, filter, r.qos, nl, rap, r.retain_handling, (int32_t)r.identifier)) fresh++;
+      if (h->async()) h->journal.subscribe(client, filter, r.qos, nl, rap, r.retain_handling, (int32_t)r.identifier);
+      return true;
+    };
+    const int rc = parse_subscription_records(json, len, sink, n_loaded);
+    if (n_new) *n_new = fresh;
+    maybe_submit(h);
+    return rc == 0 ? MQM_OK : rc == -2 ? MQM_ELIMIT : MQM_EINVAL;
   });
 }
 
