@@ -514,7 +514,7 @@ struct EmitLds {
   uint32_t tmin[EmitCfg<kE>::kSlots];
 };
 
-template <int kE, int kOcc>
+template <int kE, int kOcc, int kU = kEmitU>
 __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_eu(kOcc))) void k_emit(DeviceSnapshot s, Outputs o, const uint32_t *__restrict__ list,
                                                             const unsigned int *__restrict__ count) {
   using Cfg = EmitCfg<kE>;
@@ -594,17 +594,17 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
       }
     }
     // solo entries: delivery q of the topic is solo entry q
-    uint32_t cl[kEmitU], sid[kEmitU], meta[kEmitU];
+    uint32_t cl[kU], sid[kU], meta[kU];
     auto load_solo = [&](uint32_t base, uint32_t *c_, uint32_t *s_, uint32_t *m_) {
-      uint32_t q[kEmitU], h[kEmitU];
+      uint32_t q[kU], h[kU];
 #pragma unroll
-      for (int u = 0; u < kEmitU; u++) {  // unconditional loads (entry 0 stands in past Ss)
+      for (int u = 0; u < kU; u++) {  // unconditional loads (entry 0 stands in past Ss)
         const uint32_t q0 = base + u * kE + gl;
         q[u] = q0 < Ss ? q0 : 0;
       }
-      find_hits<kFieldSpre, kEmitU>(L.rec, nh, q, h);
+      find_hits<kFieldSpre, kU>(L.rec, nh, q, h);
 #pragma unroll
-      for (int u = 0; u < kEmitU; u++) {
+      for (int u = 0; u < kU; u++) {
         s_[u] = rec_at(L.rec, h[u], kFieldOff) + (q[u] - rec_at(L.rec, h[u], kFieldSpre));
         const SubEnt e = s.subs[s_[u]];
         c_[u] = e.client;
@@ -612,11 +612,11 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
       }
     };
     if (Ss) load_solo(0, cl, sid, meta);
-    for (uint32_t base = 0; base < Ss; base += kE * kEmitU) {
-      uint32_t ncl[kEmitU], nsid[kEmitU], nmeta[kEmitU];
-      if (base + kE * kEmitU < Ss) load_solo(base + kE * kEmitU, ncl, nsid, nmeta);
+    for (uint32_t base = 0; base < Ss; base += kE * kU) {
+      uint32_t ncl[kU], nsid[kU], nmeta[kU];
+      if (base + kE * kU < Ss) load_solo(base + kE * kU, ncl, nsid, nmeta);
 #pragma unroll
-      for (int u = 0; u < kEmitU; u++) {
+      for (int u = 0; u < kU; u++) {
         const uint32_t q = base + u * kE + gl;
         if (q < Ss)
           o.dout[db + q] = pack_delivery(cl[u], sid[u], meta[u] & 3u, (meta[u] >> 2) & 1u);
@@ -1275,9 +1275,20 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
     };
     // (amdgpu_waves_per_eu 6 / 8 variants of both spill and measured slower:
     // profiles/r01/c3_v6_occupancy_sweep.log)
-    launch_emit(k_emit<16, 1>, list_s, &o.ctr->n_small);
+    // solo entries in flight per lane (env MQM_EMIT_U16 / MQM_EMIT_U64: 4 or 8; tuning sweeps)
+    const int u16 = getenv("MQM_EMIT_U16") ? atoi(getenv("MQM_EMIT_U16")) : 4;
+    const int u64 = getenv("MQM_EMIT_U64") ? atoi(getenv("MQM_EMIT_U64")) : 4;
+    if (u16 == 8)
+      launch_emit(k_emit<16, 1, 8>, list_s, &o.ctr->n_small);
+    else
+      launch_emit(k_emit<16, 1, 4>, list_s, &o.ctr->n_small);
     HIP_TRY(hipGetLastError());
-    launch_emit(k_emit<64, 5>, list_b, &o.ctr->n_bigc);
+    if (u64 == 8)
+      launch_emit(k_emit<64, 4, 8>, list_b, &o.ctr->n_bigc);
+    else if (u64 == 2)
+      launch_emit(k_emit<64, 5, 2>, list_b, &o.ctr->n_bigc);
+    else
+      launch_emit(k_emit<64, 5, 4>, list_b, &o.ctr->n_bigc);
     HIP_TRY(hipGetLastError());
     if (ws.get(W::kOvfList, sizeof(uint32_t) * (n + 1))) return -2;
     auto *ovf = (uint32_t *)ws.ptr(W::kOvfList);
