@@ -152,93 +152,196 @@ int flatten(const Store &st, HostSnapshot *out) {
   HostSnapshot &hs = *out;
   hs = HostSnapshot();
 
-  // 1. preorder ids
-  std::vector<uint32_t> order;
+  // 1. preorder ids.  Visiting order at a node: literal children in child-list
+  //    order, then '+', then '#'.  Nodes above depth kTop are numbered
+  //    serially; the subtrees rooted at depth kTop are counted, then numbered
+  //    at their preorder base, in parallel.
+  constexpr uint32_t kTop = 2;
   std::vector<uint32_t> new_id(nodes.size(), kNone);
-  order.reserve(nodes.size());
-  // '+' / '#' children (store ids) by preorder id, found on the child list
-  std::vector<uint32_t> pc_of, hc_of, nlit;
-  pc_of.reserve(nodes.size());
-  hc_of.reserve(nodes.size());
-  nlit.reserve(nodes.size());
-  std::vector<uint32_t> stack{st.root()};
-  std::vector<uint32_t> lits;
-  while (!stack.empty()) {
-    uint32_t n = stack.back();
-    stack.pop_back();
-    new_id[n] = (uint32_t)order.size();
-    order.push_back(n);
-    uint32_t pc = kNone, hc = kNone;
+  // '+' / '#' children (store ids) and literal-child counts by preorder id
+  auto scan_children = [&](uint32_t n, uint32_t *pc, uint32_t *hc, std::vector<uint32_t> &lits) {
+    *pc = *hc = kNone;
     lits.clear();
     for (uint32_t c = nodes[n].first_child; c != kNone; c = nodes[c].next_sibling) {
       if (nodes[c].key == plus_tok)
-        pc = c;
+        *pc = c;
       else if (nodes[c].key == hash_tok)
-        hc = c;
+        *hc = c;
       else
         lits.push_back(c);
     }
-    pc_of.push_back(pc);
-    hc_of.push_back(hc);
-    nlit.push_back((uint32_t)lits.size());
+  };
+  auto push_children = [](std::vector<uint32_t> &stack, uint32_t pc, uint32_t hc, const std::vector<uint32_t> &lits) {
     if (hc != kNone) stack.push_back(hc);  // LIFO: '#' visited last
     if (pc != kNone) stack.push_back(pc);
     for (auto it = lits.rbegin(); it != lits.rend(); ++it) stack.push_back(*it);
+  };
+  struct Item {
+    uint32_t node;
+    bool task;  // subtree numbered in parallel
+    uint64_t size;
+  };
+  std::vector<Item> seq;  // the top levels in preorder, subtrees as placeholders
+  {
+    std::vector<uint32_t> stack{st.root()}, lits;
+    while (!stack.empty()) {
+      const uint32_t n = stack.back();
+      stack.pop_back();
+      if (nodes[n].depth >= kTop) {
+        seq.push_back(Item{n, true, 0});
+        continue;
+      }
+      seq.push_back(Item{n, false, 1});
+      uint32_t pc, hc;
+      scan_children(n, &pc, &hc, lits);
+      push_children(stack, pc, hc, lits);
+    }
   }
+  // subtree sizes
+  const uint32_t n_items = (uint32_t)seq.size();
+  parallel_for(64, [&](uint32_t w) {
+    std::vector<uint32_t> stack, lits;
+    for (uint32_t j = w; j < n_items; j += 64) {
+      if (!seq[j].task) continue;
+      uint64_t cnt = 0;
+      stack.assign(1, seq[j].node);
+      while (!stack.empty()) {
+        const uint32_t n = stack.back();
+        stack.pop_back();
+        cnt++;
+        for (uint32_t c = nodes[n].first_child; c != kNone; c = nodes[c].next_sibling) stack.push_back(c);
+      }
+      seq[j].size = cnt;
+    }
+  });
+  std::vector<uint64_t> base(n_items);
+  uint64_t total = 0;
+  for (uint32_t j = 0; j < n_items; j++) {
+    base[j] = total;
+    total += seq[j].size;
+  }
+  if (total >= (1ull << 30)) return MQM_ELIMIT;  // k_walk packs node id << 2 | item kind
+  std::vector<uint32_t> order(total), pc_of(total), hc_of(total), nlit(total);
+  // number every item: a top node itself, a subtree by DFS from its base
+  parallel_for(64, [&](uint32_t w) {
+    std::vector<uint32_t> stack, lits;
+    for (uint32_t j = w; j < n_items; j += 64) {
+      uint64_t id = base[j];
+      stack.assign(1, seq[j].node);
+      while (!stack.empty()) {
+        const uint32_t n = stack.back();
+        stack.pop_back();
+        new_id[n] = (uint32_t)id;
+        order[id] = n;
+        uint32_t pc, hc;
+        scan_children(n, &pc, &hc, lits);
+        pc_of[id] = pc;
+        hc_of[id] = hc;
+        nlit[id] = (uint32_t)lits.size();
+        id++;
+        if (seq[j].task) push_children(stack, pc, hc, lits);
+      }
+    }
+  });
   const uint64_t nn = order.size();
-  if (nn >= (1ull << 30)) return MQM_ELIMIT;  // k_walk packs node id << 2 | item kind
   pt.mark("preorder");
 
-  // 2. descriptors, subscription ranges, flags
+  // 2. descriptors, subscription ranges, flags — in parallel over preorder
+  //    chunks: (A) counts, child ids and own flags per node, (prefix sums over
+  //    chunks), (B) ranges filled at their prefix offsets, (C) the `$` flag
+  //    inherited down the preorder (a parent precedes its children).  The
+  //    layout equals that of one serial pass.
   hs.nodes.resize(nn);
   std::vector<uint8_t> flags(nn, 0);
-  uint64_t n_literal_edges = 0;
-  for (uint64_t i = 0; i < nn; i++) {
-    const HNode &h = nodes[order[i]];
-    NodeDesc &d = hs.nodes[i];
-    const uint32_t pc = pc_of[i], hc = hc_of[i];
-    d.plus = pc == kNone ? kNone : new_id[pc];
-    d.hash = hc == kNone ? kNone : new_id[hc];
-    n_literal_edges += h.n_children - (pc != kNone) - (hc != kNone);
-    // subscription ranges: a node's, then its '#' child's, then that one's '#'
-    // child's ... back to back (NodeDesc::hsub_cnt)
-    if (i == 0 || h.key != hash_tok) {
-      for (uint32_t k = (uint32_t)i, sn = order[i];;) {
-        const auto &subs = nodes[sn].subs;
-        if (hs.subs.size() + subs.size() > kMaxSubs) return MQM_ELIMIT;
-        hs.nodes[k].sub_off = (uint32_t)hs.subs.size();
-        hs.nodes[k].sub_cnt = (uint32_t)subs.size();
-        for (const SubRec &s : subs) {
-          hs.subs.push_back(SubEnt{s.client, (uint32_t)s.qos | ((uint32_t)(s.no_local & 1) << 2) |
-                                                 ((uint32_t)(s.rap & 1) << 3) | ((uint32_t)(s.rh & 3) << 4) |
-                                                 (s.ident > 0 ? kMetaIdent : 0u)});
-          hs.sub_info.push_back(SubInfo{s.filter, s.client, s.ident, s.qos, s.no_local, s.rap, s.rh});
+  std::vector<uint32_t> par_new(nn, kNone);
+  constexpr uint32_t kNChunks = 256;
+  std::vector<uint64_t> sub_base(kNChunks + 1, 0), sh_base(kNChunks + 1, 0), lit_c(kNChunks, 0);
+  std::vector<uint32_t> height_c(kNChunks, 0);
+  std::vector<uint8_t> too_many_shared(kNChunks, 0);
+  auto chunk_lo = [&](uint32_t c) { return nn * c / kNChunks; };
+  auto chain_start = [&](uint64_t i) { return i == 0 || nodes[order[i]].key != hash_tok; };
+  pt.mark("n:init");
+  parallel_for(kNChunks, [&](uint32_t c) {
+    uint64_t subs_n = 0, sh_n = 0, lit = 0;
+    uint32_t height = 0;
+    for (uint64_t i = chunk_lo(c); i < chunk_lo(c + 1); i++) {
+      const HNode &h = nodes[order[i]];
+      NodeDesc &d = hs.nodes[i];
+      const uint32_t pc = pc_of[i], hc = hc_of[i];
+      d.plus = pc == kNone ? kNone : new_id[pc];
+      d.hash = hc == kNone ? kNone : new_id[hc];
+      lit += nlit[i];
+      // subscription ranges: a node's, then its '#' child's, then that one's
+      // '#' child's ... back to back (NodeDesc::hsub_cnt); counted at the chain start
+      if (chain_start(i))
+        for (uint32_t sn = order[i];;) {
+          subs_n += nodes[sn].subs.size();
+          sn = hc_of[new_id[sn]];
+          if (sn == kNone) break;
         }
-        sn = hc_of[k];
-        if (sn == kNone) break;
-        k = new_id[sn];
+      if (h.shared.size() > kShCntMask) too_many_shared[c] = 1;
+      sh_n += h.shared.size();
+      uint8_t f = h.n_children ? (uint8_t)kFlagHasChildren : (uint8_t)0;
+      if (nlit[i]) f |= kFlagHasLiteral;
+      if (i > 0) {
+        par_new[i] = new_id[h.parent];
+        if (par_new[i] == 0) {  // root child: Filter[0] of every sub stored below it
+          const std::string_view k = st.tokens().name(h.key);
+          if (!k.empty() && (k[0] == '+' || k[0] == '#')) f |= kFlagDollarWild;
+        }
       }
+      flags[i] = f;
+      d.sh_cnt_flags = (uint32_t)std::min<uint64_t>(h.shared.size(), kShCntMask);
+      height = std::max(height, h.depth);
     }
-    if (h.shared.size() > kShCntMask) return MQM_ELIMIT;
-    d.sh_off = (uint32_t)hs.shared_info.size();
-    for (const SharedRec &s : h.shared)
-      hs.shared_info.push_back(
-          SubInfo{s.sub.filter, s.sub.client, s.sub.ident, s.sub.qos, s.sub.no_local, s.sub.rap, s.sub.rh});
-    uint8_t f = h.n_children ? (uint8_t)kFlagHasChildren : (uint8_t)0;
-    if (h.n_children > (uint32_t)(pc != kNone) + (uint32_t)(hc != kNone)) f |= kFlagHasLiteral;
-    if (i > 0) {
-      const uint32_t parent_new = new_id[h.parent];
-      if (parent_new == 0) {  // root child: Filter[0] of every sub stored below it
-        const std::string_view k = st.tokens().name(h.key);
-        if (!k.empty() && (k[0] == '+' || k[0] == '#')) f |= kFlagDollarWild;
-      } else {
-        f |= flags[parent_new] & kFlagDollarWild;
-      }
-    }
-    flags[i] = f;
-    d.sh_cnt_flags = (uint32_t)h.shared.size() | ((uint32_t)f << 24);
-    hs.height = std::max(hs.height, h.depth);
+    sub_base[c + 1] = subs_n;
+    sh_base[c + 1] = sh_n;
+    lit_c[c] = lit;
+    height_c[c] = height;
+  });
+  pt.mark("n:count");
+  uint64_t n_literal_edges = 0;
+  for (uint32_t c = 0; c < kNChunks; c++) {
+    if (too_many_shared[c]) return MQM_ELIMIT;
+    sub_base[c + 1] += sub_base[c];
+    sh_base[c + 1] += sh_base[c];
+    n_literal_edges += lit_c[c];
+    hs.height = std::max(hs.height, height_c[c]);
   }
+  if (sub_base[kNChunks] > kMaxSubs) return MQM_ELIMIT;
+  hs.subs.resize(sub_base[kNChunks]);
+  hs.sub_info.resize(sub_base[kNChunks]);
+  hs.shared_info.resize(sh_base[kNChunks]);
+  pt.mark("n:alloc");
+  parallel_for(kNChunks, [&](uint32_t c) {
+    uint64_t so = sub_base[c], ho = sh_base[c];
+    for (uint64_t i = chunk_lo(c); i < chunk_lo(c + 1); i++) {
+      if (chain_start(i))
+        for (uint32_t k = (uint32_t)i, sn = order[i];;) {
+          const auto &subs = nodes[sn].subs;
+          hs.nodes[k].sub_off = (uint32_t)so;
+          hs.nodes[k].sub_cnt = (uint32_t)subs.size();
+          for (const SubRec &x : subs) {
+            hs.subs[so] = SubEnt{x.client, (uint32_t)x.qos | ((uint32_t)(x.no_local & 1) << 2) |
+                                              ((uint32_t)(x.rap & 1) << 3) | ((uint32_t)(x.rh & 3) << 4) |
+                                              (x.ident > 0 ? kMetaIdent : 0u)};
+            hs.sub_info[so++] = SubInfo{x.filter, x.client, x.ident, x.qos, x.no_local, x.rap, x.rh};
+          }
+          sn = hc_of[k];
+          if (sn == kNone) break;
+          k = new_id[sn];
+        }
+      hs.nodes[i].sh_off = (uint32_t)ho;
+      for (const SharedRec &x : nodes[order[i]].shared)
+        hs.shared_info[ho++] =
+            SubInfo{x.sub.filter, x.sub.client, x.sub.ident, x.sub.qos, x.sub.no_local, x.sub.rap, x.sub.rh};
+    }
+  });
+  pt.mark("n:fill");
+  for (uint64_t i = 1; i < nn; i++) {
+    if (par_new[i] != 0) flags[i] |= flags[par_new[i]] & kFlagDollarWild;
+  }
+  for (uint64_t i = 0; i < nn; i++) hs.nodes[i].sh_cnt_flags |= (uint32_t)flags[i] << 24;
   pt.mark("nodes");
   mark_multi(st, order, hs);
   pt.mark("multi");
