@@ -13,7 +13,9 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libmqmatch.so")
+# MQM_LIB: an alternative build of the same library (e.g. `make sanitize`'s
+# host-ASan one for CPU tests); default: the in-tree gfx950 build
+LIB_PATH = os.environ.get("MQM_LIB") or os.path.join(_HERE, "_lib", "libmqmatch.so")
 
 MQM_OK = 0
 MQM_EINVAL = -1
