@@ -543,7 +543,23 @@ def cpu_baseline(w, args):
         tot = st if tot is None else {k: tot[k] + st[k] for k in tot}
         done = hi
         chunk = min(chunk * 2, 400000)
+    # single-thread rate over the front of the same sample (<= ~3 s)
+    st_done, st_busy, st_chunk = 0, 0.0, 5000
+    while st_done < done and st_busy < min(3.0, args.cpu_seconds / 4):
+        hi = min(done, st_done + st_chunk)
+        o = (offs[st_done:hi + 1] - offs[st_done]).astype(np.uint64)
+        d = data[int(offs[st_done]):int(offs[hi])]
+        t1 = time.perf_counter()
+        ora.match_counts(d, o, nthreads=1)
+        st_busy += time.perf_counter() - t1
+        st_done = hi
     ora.close()
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            model = next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")), "")
+    except OSError:
+        pass
     cpu = {
         "value": done / busy,
         "unit": "topics/s",
@@ -553,6 +569,8 @@ def cpu_baseline(w, args):
                   f"excluded); C restatement of mochi v2.2.12 TopicsIndex (oracle/mochi_ref.c); Go toolchain "
                   f"unavailable",
         "deliveries_per_s": tot["deliveries"] / busy,
+        "single_thread_value": st_done / st_busy if st_busy > 0 else None,
+        "host": {"cpus_visible": os.cpu_count(), "model": model},
     }
     return cpu, tot
 
