@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--host-topics", type=int, default=1000000,
+                    help="PCIe-inclusive host path (mqm_match_batch) sample, outside the timed region; 0 = skip")
     ap.add_argument("--workload", choices=["forward", "reverse", "churn"], default="forward",
                     help="forward: Subscribers (headline); reverse: Messages over retained topics (config 5); "
                          "churn: Subscribe/Unsubscribe at rate with background snapshot rebuilds")
@@ -210,6 +212,7 @@ def main():
         kms = {k: prof[f"{k}_ms"] / calls for k in ("walk", "dedupe", "total")}
         cpu = None
         stats = None
+        host = host_path(idx, w, args) if args.host_topics and not sharded else None
         if not args.no_cpu_baseline:
             cpu, stats = cpu_baseline(w, args)
         roof = roofline(stats, n, kms, args.traffic_json)
@@ -244,11 +247,45 @@ def main():
             "snapshot": snap,
             "roofline": roof,
             "cpu_baseline": cpu,
+            "host_path": host,
         }
         print(json.dumps(out), flush=True)
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def host_path(idx, w, args):
+    """The boundary's host form, mqm_match_batch: topics in host memory ->
+    H2D copy -> the same match pipeline -> dense CSR copied back into
+    library-owned (pageable) host arrays.  Timed on the first --host-topics
+    topics of the batch, outside the headline's timed region (the headline is
+    HBM-resident)."""
+    import ctypes as C
+    from maxmq_amd import capi
+
+    L = capi.lib()
+    h = min(args.host_topics, len(w.topics))
+    data = w.topics.data
+    offs = np.ascontiguousarray(w.topics.offs[: h + 1], dtype=np.uint64)
+
+    def call():
+        res = C.c_void_p()
+        capi.check("mqm_match_batch", L.mqm_match_batch(idx._h, data.ctypes.data_as(C.c_void_p),
+                                                        offs.ctypes.data_as(C.c_void_p), h, C.byref(res)))
+        return res
+
+    L.mqm_result_free(call())  # warm (workspace sizing)
+    reps, dt, dl = 3, 0.0, 0
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        res = call()
+        dt += time.perf_counter() - t0
+        dl += int(C.cast(L.mqm_result_offsets(res), C.POINTER(C.c_uint64))[h])
+        L.mqm_result_free(res)
+    return {"value": h * reps / dt, "unit": "topics/s", "topics": h, "ms_per_call": dt * 1e3 / reps,
+            "deliveries_per_s": dl / dt,
+            "note": "PCIe-inclusive: topic bytes+offsets H2D, match, dense CSR D2H into pageable host memory"}
 
 
 def run_sweep(args, idx, step, dev, rank):

@@ -44,6 +44,16 @@
 #include "device.h"
 #include "match.h"
 
+// MQM_REC16_WORDS: record words k_emit<16> prefetches per topic (64 or 128)
+#ifndef MQM_REC16_WORDS
+#define MQM_REC16_WORDS 64
+#endif
+// MQM_NT_OUT=1: non-temporal output stores (tuning knob, `make variant`; C3
+// sweep profiles/r01/c3_v14_nt_tail_sweep.log: no gain, off)
+#ifndef MQM_NT_OUT
+#define MQM_NT_OUT 0
+#endif
+
 namespace mqm {
 
 namespace {
@@ -67,6 +77,7 @@ constexpr int kRecSh = 4 + kRecHit * kHCap;          // 196
 constexpr int kRecStride = kRecSh + 2 * kShCap;       // 228 words (max)
 constexpr int kRecStrideAlloc = 228;                  // 16-B aligned per topic
 constexpr uint32_t kSMax = 16384;        // raw entries per topic on the bounded path
+constexpr uint32_t kDPad = 16;         // segment starts aligned to 16 entries (128 B)
 constexpr int kEmitU = 4;                // solo entries in flight per lane
 constexpr int kEmitWaves = 4;
 constexpr int kSmallLanes = 16;          // k_emit<16>: lanes per topic of the small class
@@ -138,6 +149,17 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
 
 __device__ __forceinline__ uint32_t table_slot(uint32_t client, uint32_t lg) {
   return (uint32_t)(((uint64_t)(client * 2654435769u) << lg) >> 32);
+}
+
+// deliveries and shared candidates are written once and never re-read on the
+// device; MQM_NT_OUT streams them past the caches (measured: no gain on C3)
+template <class T>
+__device__ __forceinline__ void put_out(T *p, T v) {
+#if MQM_NT_OUT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
 }
 
 __device__ __forceinline__ uint64_t pack_delivery(uint32_t client, uint32_t sid, uint32_t qos, uint32_t nl) {
@@ -503,11 +525,16 @@ struct EmitCfg {
   static constexpr uint32_t kMulti = kE == kWave ? kSmallMulti : 3 * kE;  // multi entries merged here
   static constexpr uint32_t kSlots = kE == kWave ? kSmallSlots : 64;
   static constexpr int kMPer = kMulti / kE;
-  static constexpr int kRecPer = 64 / kE;  // record words each lane prefetches (64 per topic)
+  // record words each lane prefetches one topic ahead: the whole record for
+  // the big class (one 16-B load per lane), the first MQM_REC16_WORDS for the
+  // small one (the rest is loaded when the header says how many hits there are)
+  static constexpr int kRecPer = kE == kWave ? 4 : MQM_REC16_WORDS / kE;
+  static constexpr int kPre = kRecPer * kE;
+  static_assert(kRecPer % 4 == 0 && (kE == kWave || kPre <= kRecStrideAlloc), "16-B record prefetch");
 };
 
 template <int kE>
-struct EmitLds {
+struct alignas(16) EmitLds {
   uint32_t rec[kRecStrideAlloc];
   uint32_t tkey[EmitCfg<kE>::kSlots];
   uint32_t tbits[EmitCfg<kE>::kSlots];
@@ -528,20 +555,21 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
   const uint32_t ngroups = gridDim.x * kEmitWaves * kGroups;
   const uint32_t nl = *count;
   uint32_t i = (blockIdx.x * kEmitWaves + threadIdx.x / kWave) * kGroups + g;
-  // list entries two topics ahead; the next topic's header and first 64
-  // record words one topic ahead
+  // list entries two topics ahead; the next topic's header and its record's
+  // first Cfg::kPre words one topic ahead
   uint32_t n_H = 0, n_rw[kRecPer];
   uint64_t n_db = 0, n_hb = 0;
   auto fetch = [&](uint32_t u) {
     n_H = o.hcount[u];
     n_db = o.dstart[u];
     n_hb = o.hstart[u];
-    const uint32_t *r = o.recs + (uint64_t)u * kRecStrideAlloc + gl * kRecPer;
-    if constexpr (kRecPer == 4) {
-      const uint4 v = *reinterpret_cast<const uint4 *>(r);
-      n_rw[0] = v.x, n_rw[1] = v.y, n_rw[2] = v.z, n_rw[3] = v.w;
-    } else {
-      n_rw[0] = r[0];
+    // lanes past the record's end (big class) re-read word 0 and store nothing
+    const uint32_t w0 = gl * kRecPer + kRecPer <= kRecStrideAlloc ? gl * kRecPer : 0;
+    const uint32_t *r = o.recs + (uint64_t)u * kRecStrideAlloc + w0;
+#pragma unroll
+    for (int v = 0; v < kRecPer / 4; v++) {
+      const uint4 x = *reinterpret_cast<const uint4 *>(r + 4 * v);
+      n_rw[4 * v] = x.x, n_rw[4 * v + 1] = x.y, n_rw[4 * v + 2] = x.z, n_rw[4 * v + 3] = x.w;
     }
   };
   uint32_t t_nxt = i < nl ? list[i] : 0;
@@ -557,12 +585,28 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
     if (i + ngroups < nl) fetch(t_nxt);
     t_nn = i + 2 * ngroups < nl ? list[i + 2 * ngroups] : 0;
 #pragma unroll
-    for (int j = 0; j < kRecPer; j++) L.rec[gl * kRecPer + j] = rw[j];
+    for (int j = 0; j < kRecPer; j++)
+      if (gl * kRecPer + kRecPer <= kRecStrideAlloc) L.rec[gl * kRecPer + j] = rw[j];
     wave_lds_sync();
     const uint32_t w0 = L.rec[0], Ss = L.rec[1], M = L.rec[2];
     const uint32_t nh = w0 & 0xFFu, nsh = w0 >> 8;
     const uint32_t *grec = o.recs + (uint64_t)t * kRecStrideAlloc;
-    for (uint32_t j = kWave + gl; j < 4 + kRecHit * nh; j += kE) L.rec[j] = grec[j];
+    if constexpr (Cfg::kPre < kRecStride) {  // the hits past the prefetched words: one
+      // round trip of 16-B loads (lanes past the end re-read word kPre)
+      constexpr int kPre = Cfg::kPre, kT = (kRecStride - kPre + 4 * kE - 1) / (4 * kE);
+      const uint32_t nw = 4 + kRecHit * nh;
+      uint4 tv[kT];
+#pragma unroll
+      for (int k = 0; k < kT; k++) {
+        const uint32_t w = kPre + 4 * (k * kE + gl);
+        tv[k] = *reinterpret_cast<const uint4 *>(grec + (w < nw ? w : kPre));
+      }
+#pragma unroll
+      for (int k = 0; k < kT; k++) {
+        const uint32_t w = kPre + 4 * (k * kE + gl);
+        if (w < nw) *reinterpret_cast<uint4 *>(&L.rec[w]) = tv[k];
+      }
+    }
     wave_lds_sync();
     rec_prefix<kE>(L.rec, nh, gl);
     wave_lds_sync();
@@ -570,7 +614,7 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
       uint32_t w = 0;
       for (uint32_t j = 0; j < nsh; j++) {
         const uint32_t so = grec[kRecSh + 2 * j], sc = grec[kRecSh + 1 + 2 * j];
-        for (uint32_t j = gl; j < sc; j += kE) o.hout[hb + w + j] = so + j;
+        for (uint32_t j = gl; j < sc; j += kE) put_out(&o.hout[hb + w + j], so + j);
         w += sc;
       }
     }
@@ -619,7 +663,7 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
       for (int u = 0; u < kU; u++) {
         const uint32_t q = base + u * kE + gl;
         if (q < Ss)
-          o.dout[db + q] = pack_delivery(cl[u], sid[u], meta[u] & 3u, (meta[u] >> 2) & 1u);
+          put_out(&o.dout[db + q], pack_delivery(cl[u], sid[u], meta[u] & 3u, (meta[u] >> 2) & 1u));
         cl[u] = ncl[u];
         sid[u] = nsid[u];
         meta[u] = nmeta[u];
@@ -656,7 +700,7 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
           ent = pack_delivery(mcl[k], msid[k], 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
         }
         const uint64_t m = (__ballot(win) >> gbase) & kGMask;
-        if (win) o.dout[db + D + __popcll(m & glt)] = ent;
+        if (win) put_out(&o.dout[db + D + __popcll(m & glt)], ent);
         D += __popcll(m);
       }
     }
@@ -763,7 +807,7 @@ __global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs
         if (w < wid) before += wsum[w];
         round += wsum[w];
       }
-      if (win) o.dout[db + before + __popcll(m & lanemask_lt(lane))] = ent;
+      if (win) put_out(&o.dout[db + before + __popcll(m & lanemask_lt(lane))], ent);
       D += round;
       __syncthreads();
     }
@@ -1149,8 +1193,13 @@ static uint32_t resident_blocks(Workspace &ws, int, K kern) {
 }
 
 // counts (n) -> exclusive offsets (u64, n + 1)
+struct PadCount {
+  uint32_t mask;  // pad - 1 (pad a power of two)
+  __host__ __device__ uint64_t operator()(uint32_t c) const { return ((uint64_t)c + mask) & ~(uint64_t)mask; }
+};
+
 template <class T>
-static int scan_offsets(Workspace &ws, const T *counts, uint64_t *offs, uint32_t n, hipStream_t st) {
+static int scan_offsets(Workspace &ws, T counts, uint64_t *offs, uint32_t n, hipStream_t st) {
   HIP_TRY(hipMemsetAsync(offs, 0, sizeof(uint64_t), st));
   if (n == 0) return 0;
   size_t tmp = 0;
@@ -1204,7 +1253,14 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   }
   HIP_TRY(hipGetLastError());
   mark(ws, 1, st);
-  if (scan_offsets(ws, o.scount, o.dstart, n, st) || scan_offsets(ws, o.hcount, o.hstart, n, st)) return -3;
+  // segment starts: each topic's raw-entry count rounded up to kDPad entries,
+  // so no two topics' deliveries share a cache line (env MQM_DPAD: 1 | 16)
+  {
+    static const uint32_t pad = getenv("MQM_DPAD") ? (uint32_t)atoi(getenv("MQM_DPAD")) : kDPad;
+    const uint32_t pm = pad > 1 ? pad - 1 : 0;
+    hipcub::TransformInputIterator<uint64_t, PadCount, const uint32_t *> padded(o.scount, PadCount{pm});
+    if (scan_offsets(ws, padded, o.dstart, n, st) || scan_offsets(ws, o.hcount, o.hstart, n, st)) return -3;
+  }
   HIP_TRY(hipMemcpyAsync(hc, o.ctr, sizeof(Counters), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(hp, o.dstart + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(hp + 1, o.hstart + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
