@@ -44,6 +44,11 @@
 #include "device.h"
 #include "match.h"
 
+// MQM_FIND_STEP: hits per batch of LDS reads in find_hits (4 / 8 spill and
+// lose occupancy: slower on C3, profiles/r01/c3_v17_find_step_sweep.log)
+#ifndef MQM_FIND_STEP
+#define MQM_FIND_STEP 1
+#endif
 // MQM_REC16_WORDS: record words k_emit<16> prefetches per topic (64 or 128)
 #ifndef MQM_REC16_WORDS
 #define MQM_REC16_WORDS 64
@@ -77,7 +82,7 @@ constexpr int kRecSh = 4 + kRecHit * kHCap;          // 196
 constexpr int kRecStride = kRecSh + 2 * kShCap;       // 228 words (max)
 constexpr int kRecStrideAlloc = 228;                  // 16-B aligned per topic
 constexpr uint32_t kSMax = 16384;        // raw entries per topic on the bounded path
-constexpr uint32_t kDPad = 16;         // segment starts aligned to 16 entries (128 B)
+constexpr uint32_t kDPad = 1;           // segment start alignment in entries (16 = 128-B lines: no gain on C3)
 constexpr int kEmitU = 4;                // solo entries in flight per lane
 constexpr int kEmitWaves = 4;
 constexpr int kSmallLanes = 16;          // k_emit<16>: lanes per topic of the small class
@@ -173,6 +178,8 @@ __device__ __forceinline__ uint32_t qos_bits(uint32_t meta) { return (1u << (met
 // largest h with field(h) <= x.  Hits with none of those entries tie with
 // their successor, so the largest such h is the one that holds x.
 enum : int { kFieldOff = 0, kFieldSpre = 1, kFieldMpre = 2, kFieldRank = 3 };
+constexpr int kFindStep = MQM_FIND_STEP;
+static_assert(4 + kRecHit * (kHCap - 1 + kFindStep - 1) + kFieldRank < kRecStrideAlloc, "find_hits reads stay in the record");
 // Counting search: every lane of a group reads the same record word per hit
 // (an LDS broadcast) and the reads are independent, so the loop pipelines —
 // a binary search's dependent reads compiled to a branch and a full LDS wait
@@ -182,10 +189,27 @@ __device__ __forceinline__ void find_hits(const uint32_t *rec, uint32_t nh, cons
                                           uint32_t (&h)[kN]) {
 #pragma unroll
   for (int u = 0; u < kN; u++) h[u] = 0;
-  for (uint32_t j = 1; j < nh; j++) {
-    const uint32_t v = rec[4 + kRecHit * j + kField];
+  // 8 hits per step: the 8 LDS reads are issued together and waited for once
+  // (one read per step serialised the loop on LDS latency); reads past nh
+  // stay inside the record (kFindStep) and count for nothing
+  if constexpr (kFindStep == 1) {
+    for (uint32_t j = 1; j < nh; j++) {
+      const uint32_t v = rec[4 + kRecHit * j + kField];
 #pragma unroll
-    for (int u = 0; u < kN; u++) h[u] += v <= x[u] ? 1u : 0u;
+      for (int u = 0; u < kN; u++) h[u] += v <= x[u] ? 1u : 0u;
+    }
+    return;
+  }
+  for (uint32_t j = 1; j < nh; j += kFindStep) {
+    uint32_t v[kFindStep];
+#pragma unroll
+    for (int k = 0; k < kFindStep; k++) v[k] = rec[4 + kRecHit * (j + k) + kField];
+#pragma unroll
+    for (int k = 0; k < kFindStep; k++) {
+      const bool in = j + k < nh;
+#pragma unroll
+      for (int u = 0; u < kN; u++) h[u] += (in && v[k] <= x[u]) ? 1u : 0u;
+    }
   }
 }
 
@@ -525,12 +549,13 @@ struct EmitCfg {
   static constexpr uint32_t kMulti = kE == kWave ? kSmallMulti : 3 * kE;  // multi entries merged here
   static constexpr uint32_t kSlots = kE == kWave ? kSmallSlots : 64;
   static constexpr int kMPer = kMulti / kE;
-  // record words each lane prefetches one topic ahead: the whole record for
-  // the big class (one 16-B load per lane), the first MQM_REC16_WORDS for the
-  // small one (the rest is loaded when the header says how many hits there are)
-  static constexpr int kRecPer = kE == kWave ? 4 : MQM_REC16_WORDS / kE;
+  // record words each lane prefetches one topic ahead: the first 64 for the
+  // big class, MQM_REC16_WORDS for the small one; the rest is loaded when the
+  // header says how many hits there are.  (The whole record for the big class,
+  // one 16-B load per lane, measured no faster and spills at occupancy 5.)
+  static constexpr int kRecPer = kE == kWave ? 1 : MQM_REC16_WORDS / kE;
   static constexpr int kPre = kRecPer * kE;
-  static_assert(kRecPer % 4 == 0 && (kE == kWave || kPre <= kRecStrideAlloc), "16-B record prefetch");
+  static_assert((kRecPer == 1 || kRecPer % 4 == 0) && kPre <= kRecStrideAlloc, "record prefetch");
 };
 
 template <int kE>
@@ -563,13 +588,16 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
     n_H = o.hcount[u];
     n_db = o.dstart[u];
     n_hb = o.hstart[u];
-    // lanes past the record's end (big class) re-read word 0 and store nothing
     const uint32_t w0 = gl * kRecPer + kRecPer <= kRecStrideAlloc ? gl * kRecPer : 0;
     const uint32_t *r = o.recs + (uint64_t)u * kRecStrideAlloc + w0;
+    if constexpr (kRecPer == 1) {
+      n_rw[0] = r[0];
+    } else {
 #pragma unroll
-    for (int v = 0; v < kRecPer / 4; v++) {
-      const uint4 x = *reinterpret_cast<const uint4 *>(r + 4 * v);
-      n_rw[4 * v] = x.x, n_rw[4 * v + 1] = x.y, n_rw[4 * v + 2] = x.z, n_rw[4 * v + 3] = x.w;
+      for (int v = 0; v < kRecPer / 4; v++) {
+        const uint4 x = *reinterpret_cast<const uint4 *>(r + 4 * v);
+        n_rw[4 * v] = x.x, n_rw[4 * v + 1] = x.y, n_rw[4 * v + 2] = x.z, n_rw[4 * v + 3] = x.w;
+      }
     }
   };
   uint32_t t_nxt = i < nl ? list[i] : 0;
@@ -591,8 +619,11 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
     const uint32_t w0 = L.rec[0], Ss = L.rec[1], M = L.rec[2];
     const uint32_t nh = w0 & 0xFFu, nsh = w0 >> 8;
     const uint32_t *grec = o.recs + (uint64_t)t * kRecStrideAlloc;
-    if constexpr (Cfg::kPre < kRecStride) {  // the hits past the prefetched words: one
-      // round trip of 16-B loads (lanes past the end re-read word kPre)
+    if constexpr (kE == kWave) {  // the hits past the first 64 words (a vector
+      // tail here costs the big class its last registers: spills at occupancy 5)
+      for (uint32_t j = kWave + gl; j < 4 + kRecHit * nh; j += kE) L.rec[j] = grec[j];
+    } else {  // the hits past the prefetched words: one round trip of 16-B
+      // loads (lanes past the end re-read word kPre)
       constexpr int kPre = Cfg::kPre, kT = (kRecStride - kPre + 4 * kE - 1) / (4 * kE);
       const uint32_t nw = 4 + kRecHit * nh;
       uint4 tv[kT];
