@@ -21,6 +21,17 @@
  *     read-your-writes visibility (topics.go takes no snapshot at all).
  *   - The match path runs on the GPU only.  There is no CPU fallback: without
  *     a usable HIP device mqm_create fails with MQM_ENODEV.
+ *   - Threading (the reference calls Subscribers() concurrently from every
+ *     connection goroutine, listeners/tcp.go:83): mutations and commits
+ *     serialise on the index mutex (topics.go:304,326,355 take the root
+ *     mutex).  The host-path matches (mqm_match_batch, mqm_subscribers,
+ *     mqm_messages_batch, mqm_messages_one) may be called from any number of
+ *     threads at once: each borrows its own workspace and HIP stream and reads
+ *     the published snapshot without holding the mutex (a commit that
+ *     publishes a new snapshot does not wait for them).  The device-result
+ *     calls (mqm_match_device, mqm_dense_device, mqm_identifiers_device,
+ *     mqm_messages_device) share one library-owned result area per index and
+ *     serialise on it.
  */
 #ifndef MQMATCH_H
 #define MQMATCH_H
@@ -93,7 +104,7 @@ typedef struct {
 } mqm_sub_info;
 
 /* Device-resident result of mqm_match_device (library-owned; valid until the
- * next match call on the same index).  Topic t's deliveries are
+ * next mqm_match_device / mqm_messages_device call on the same index).  Topic t's deliveries are
  * deliveries[starts[t] .. starts[t] + counts[t]) and its shared candidates
  * shared[shared_starts[t] .. + shared_counts[t]).  Segments are in topic
  * order but may leave gaps (a topic reserves its raw-entry count before
@@ -119,10 +130,13 @@ int mqm_create(const mqm_config *cfg, mqm_index **out);
 int mqm_destroy(mqm_index *h);
 
 /* ---- mutation ----------------------------------------------------------- */
-/* TopicsIndex.Subscribe (topics.go:303-321): *is_new = !existed */
+/* TopicsIndex.Subscribe (topics.go:303-321): *is_new = !existed.  MQM_EINVAL
+ * (nothing stored) for qos > 2 or retain_handling > 3: the snapshot packs them
+ * in 2 bits each (the broker never passes more: packets.go:953). */
 int mqm_subscribe(mqm_index *h, const char *client, size_t client_len, const char *filter, size_t filter_len,
                   const mqm_subscription *sub, int *is_new);
-/* bulk form of the above for store reload (server.go:1377-1393); is_new may be NULL */
+/* bulk form of the above for store reload (server.go:1377-1393); is_new may be
+ * NULL.  Any record out of range: MQM_EINVAL and none is applied. */
 int mqm_subscribe_many(mqm_index *h, size_t n, const char *client_bytes, const uint64_t *client_offs,
                        const char *filter_bytes, const uint64_t *filter_offs, const mqm_subscription *subs,
                        uint8_t *is_new);
@@ -188,6 +202,13 @@ int mqm_commit_state_get(mqm_index *h, mqm_commit_state *out);
 /* 64-bit digest of the published snapshot's arrays: replicas and rebuilds of
  * the same store state have equal digests */
 int mqm_snapshot_digest(mqm_index *h, uint64_t *out);
+/* Fault injection for tests (async indexes only): the next `count` background
+ * builds fail at `stage` — 1: part-way through the delta-log replay (as a
+ * bad_alloc while interning would), 2: flatten, 3: upload.  A failed build is
+ * reported by the next commit; the commit after it rebuilds (after a failed
+ * replay, from a full copy of the authoritative store), so a failure never
+ * leaves a stale snapshot published as current. */
+int mqm_debug_fault(mqm_index *h, int stage, int count);
 
 /* ---- forward match: TopicsIndex.Subscribers (topics.go:484-555) --------- */
 /* Host in / host out.  Topic i is bytes[offsets[i] .. offsets[i+1]). */
@@ -211,7 +232,7 @@ int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t 
  * plus {filter(s): ident(s)} for the listed s whose client is that client
  * (resolve with mqm_result_sub_info).  Device form: for the last
  * mqm_match_device call on the index, whose topic buffers must still hold the
- * batch; MQM_EINVAL if there was none or a commit replaced its snapshot. */
+ * batch, against the snapshot that call read; MQM_EINVAL if there was none. */
 typedef struct {
   uint32_t n_topics;
   uint64_t n_idents;
@@ -225,9 +246,9 @@ int mqm_result_identifiers(const mqm_result *r, const uint64_t **offsets, const 
 
 /* ---- dense device form of the last mqm_match_device result --------------- */
 /* Topic t's deliveries are deliveries[offsets[t] .. offsets[t+1]) (no gaps);
- * same for shared.  Library-owned, valid until the next match call on the
- * index; MQM_EINVAL if there was no device match or a commit replaced its
- * snapshot.  Queued on hip_stream after the match. */
+ * same for shared.  Library-owned, valid until the next device-result call on
+ * the index; MQM_EINVAL if there was no device match.  Queued on hip_stream
+ * after the match. */
 typedef struct {
   uint32_t n_topics;
   uint64_t n_deliveries, n_shared;

@@ -43,6 +43,7 @@ EXPORTED = [
     "mqm_messages_refs", "mqm_messages_free", "mqm_messages_device", "mqm_identifiers_device",
     "mqm_result_identifiers", "mqm_dense_device", "mqm_gather_shards", "mqm_commit_async", "mqm_commit_poll",
     "mqm_commit_policy", "mqm_commit_state_get", "mqm_snapshot_digest", "mqm_unsubscribe_many", "mqm_load_subscriptions_json",
+    "mqm_debug_fault",
 ]
 
 
@@ -181,6 +182,7 @@ def lib():
         "mqm_commit_policy": ([vp, u64, u32], C.c_int),
         "mqm_commit_state_get": ([vp, C.POINTER(CommitState)], C.c_int),
         "mqm_snapshot_digest": ([vp, C.POINTER(u64)], C.c_int),
+        "mqm_debug_fault": ([vp, C.c_int, C.c_int], C.c_int),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

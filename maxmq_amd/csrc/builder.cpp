@@ -4,6 +4,7 @@
 
 #include <chrono>
 #include <cstring>
+#include <new>
 
 #include "../../include/mqmatch.h"
 
@@ -40,9 +41,10 @@ void DeltaLog::retain(std::string_view topic, uint64_t msg_ref, uint32_t payload
   op.retain_flag = retain_flag ? 1 : 0;
 }
 
-void DeltaLog::replay(Store &st) const {
+void DeltaLog::replay(Store &st, size_t limit) const {
   const char *base = bytes_.data();
   for (const Op &op : ops_) {
+    if (limit-- == 0) return;
     const std::string_view a(base + op.a_off, op.a_len), b(base + op.a_off + op.a_len, op.b_len);
     switch (op.kind) {
       case kSub:
@@ -97,6 +99,34 @@ void Builder::submit(DeltaLog &&log, uint64_t version) {
   cv_.notify_all();
 }
 
+void Builder::submit_full(const Store &st, uint64_t version) {
+  auto copy = std::make_unique<Store>(st);  // outside mu_: the worker may be mid-build
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    full_ = std::move(copy);
+    queued_.clear();
+    queued_version_ = version;
+    has_queued_ = true;
+  }
+  cv_.notify_all();
+}
+
+void Builder::inject_fault(int stage, int count) {
+  std::lock_guard<std::mutex> g(mu_);
+  fault_stage_ = stage;
+  fault_count_ = count;
+}
+
+bool Builder::dirty() {
+  std::lock_guard<std::mutex> g(mu_);
+  return dirty_;
+}
+
+bool Builder::shadow_bad() {
+  std::lock_guard<std::mutex> g(mu_);
+  return shadow_bad_;
+}
+
 bool Builder::take(BuiltSnapshot *out) {
   std::lock_guard<std::mutex> g(mu_);
   if (!has_ready_) return false;
@@ -130,28 +160,46 @@ void Builder::run() {
   for (;;) {
     DeltaLog log;
     uint64_t version;
+    std::unique_ptr<Store> full;
+    bool stale;
+    int fault;
     {
       std::unique_lock<std::mutex> g(mu_);
       cv_.wait(g, [this] { return has_queued_ || stop_; });
       if (!has_queued_) return;  // stop_ with nothing left to build
+      full = std::move(full_);
       log.append(std::move(queued_));
       version = queued_version_;
       has_queued_ = false;
       working_ = true;
+      stale = shadow_bad_ && !full;
+      fault = fault_count_ > 0 ? fault_stage_ : 0;
+      if (fault) fault_count_--;
     }
     const auto t0 = std::chrono::steady_clock::now();
     int rc = MQM_OK;
+    bool replayed = false;
     BuiltSnapshot b;
-    try {
-      log.replay(shadow_);
-      auto hs = std::make_shared<HostSnapshot>();
-      rc = flatten(shadow_, hs.get());
-      if (rc == MQM_OK && device_ >= 0 && !stream_) rc = MQM_EHIP;
-      if (rc == MQM_OK) rc = upload(std::move(hs), device_, stream_, &b.snap);
-    } catch (const std::bad_alloc &) {
-      rc = MQM_ENOMEM;
-    } catch (...) {
-      rc = MQM_EINVAL;
+    if (stale) {
+      rc = MQM_EINVAL;  // a log on top of a half-replayed shadow would build a wrong trie
+    } else {
+      try {
+        if (full) shadow_ = std::move(*full);
+        if (fault == 1) {  // stop half-way, as a bad_alloc while interning would
+          log.replay(shadow_, log.size() / 2);
+          throw std::bad_alloc();
+        }
+        log.replay(shadow_);
+        replayed = true;
+        auto hs = std::make_shared<HostSnapshot>();
+        rc = fault == 2 ? MQM_ENOMEM : flatten(shadow_, hs.get());
+        if (rc == MQM_OK && device_ >= 0 && !stream_) rc = MQM_EHIP;
+        if (rc == MQM_OK) rc = fault == 3 ? MQM_ENOMEM : upload(std::move(hs), device_, stream_, &b.snap);
+      } catch (const std::bad_alloc &) {
+        rc = MQM_ENOMEM;
+      } catch (...) {
+        rc = MQM_EINVAL;
+      }
     }
     b.version = version;
     b.n_ops = log.size();
@@ -162,8 +210,12 @@ void Builder::run() {
       if (rc == MQM_OK) {
         ready_ = std::move(b);  // replaces an unpublished older build
         has_ready_ = true;
-      } else if (!err_) {
-        err_ = rc;
+        dirty_ = false;
+        shadow_bad_ = false;
+      } else {
+        if (!err_) err_ = rc;
+        dirty_ = true;
+        if (!stale && !replayed) shadow_bad_ = true;  // the replay stopped part-way
       }
     }
     cv_.notify_all();

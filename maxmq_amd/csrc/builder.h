@@ -16,6 +16,7 @@
 #include <stdint.h>
 
 #include <condition_variable>
+#include <cstdint>
 #include <memory>
 #include <mutex>
 #include <string_view>
@@ -34,8 +35,8 @@ class DeltaLog {
                  uint8_t rh, int32_t ident);
   void unsubscribe(std::string_view filter, std::string_view client);
   void retain(std::string_view topic, uint64_t msg_ref, uint32_t payload_len, bool retain_flag);
-  // re-run every recorded call on st, in order
-  void replay(Store &st) const;
+  // re-run the first `limit` recorded calls on st, in order
+  void replay(Store &st, size_t limit = SIZE_MAX) const;
   void append(DeltaLog &&o);  // o's ops after ours
   size_t size() const { return ops_.size(); }
   bool empty() const { return ops_.empty(); }
@@ -77,6 +78,18 @@ class Builder {
 
   // queue a delta log whose replay brings the shadow store to `version`
   void submit(DeltaLog &&log, uint64_t version);
+  // replace the shadow store with a copy of the authoritative one (taken by the
+  // caller under the index mutex, so it holds every mutation up to `version`);
+  // queued logs are dropped: the copy already contains them
+  void submit_full(const Store &st, uint64_t version);
+  // the last build failed: the next commit must build even with an empty log
+  bool dirty();
+  // a replay failed part-way: the shadow store no longer mirrors the
+  // authoritative one, and only submit_full repairs it (plain logs are refused)
+  bool shadow_bad();
+  // fault injection for tests (mqm_debug_fault): the next `count` builds fail
+  // in `stage` (1 = part-way through the replay, 2 = flatten, 3 = upload)
+  void inject_fault(int stage, int count);
   // the newest finished snapshot, if any (older unpublished ones are dropped)
   bool take(BuiltSnapshot *out);
   // block until every submitted log is built; returns the first build error
@@ -91,11 +104,14 @@ class Builder {
   std::mutex mu_;
   std::condition_variable cv_;
   DeltaLog queued_;
+  std::unique_ptr<Store> full_;  // submit_full's copy, applied before queued_
   uint64_t queued_version_ = 0;
   bool has_queued_ = false, working_ = false, stop_ = false;
+  bool dirty_ = false, shadow_bad_ = false;
   bool has_ready_ = false;
   BuiltSnapshot ready_;
   int err_ = 0;
+  int fault_stage_ = 0, fault_count_ = 0;
   std::thread th_;
 };
 

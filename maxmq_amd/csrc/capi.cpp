@@ -1,11 +1,28 @@
 // maxmq_amd/csrc/capi.cpp — the C ABI (include/mqmatch.h) over the host
 // store, the snapshot builder and the HIP match pipeline.
+//
+// Threading (the reference runs Subscribers() concurrently from
+// one goroutine per connection, listeners/tcp.go:83, clients.go:331-356):
+//   * h->mu guards the store, the delta log, the builder and the front-buffer
+//     pointer.  Mutations and commits hold it; a match holds it only to
+//     publish / read the front buffer (RCU style: it takes a shared_ptr).
+//   * Host-path matches (mqm_match_batch, mqm_subscribers, mqm_messages_*)
+//     borrow a MatchCtx (workspace + HIP stream) from a per-index pool, so
+//     any number of threads match concurrently against one snapshot, each on
+//     its own stream; results land in pinned host blocks from a shared pool.
+//   * The device-result API (mqm_match_device and its follow-ups, whose
+//     results live in library memory "until the next call") uses one default
+//     MatchCtx under its own mutex.
+//   * A snapshot is freed when its last holder drops it: the front-buffer
+//     pointer, a running call, or the default context (which keeps the
+//     snapshot its device results refer to until its next call).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <new>
@@ -23,18 +40,79 @@
 
 using namespace mqm;
 
+namespace {
+
+// Pinned host blocks for results: D2H into pinned memory runs at the link
+// rate; pageable memory costs an extra staging copy.  Blocks are recycled
+// (best fit), so steady-state batches allocate nothing.
+class PinnedPool {
+ public:
+  ~PinnedPool() {
+    for (auto &kv : free_) (void)hipHostFree(kv.second);
+  }
+  void *get(size_t need, size_t *cap) {
+    need = std::max<size_t>(need, 4096);
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto it = free_.lower_bound(need);
+      if (it != free_.end() && it->first <= 2 * need + (64u << 20)) {
+        *cap = it->first;
+        void *p = it->second;
+        cached_ -= it->first;
+        free_.erase(it);
+        return p;
+      }
+    }
+    const size_t n = need + need / 8;
+    void *p = nullptr;
+    if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) return nullptr;
+    *cap = n;
+    return p;
+  }
+  void put(void *p, size_t cap) {
+    if (!p) return;
+    std::lock_guard<std::mutex> g(mu_);
+    free_.emplace(cap, p);
+    cached_ += cap;
+    while (cached_ > kMaxCached && !free_.empty()) {  // drop the largest
+      auto it = std::prev(free_.end());
+      cached_ -= it->first;
+      (void)hipHostFree(it->second);
+      free_.erase(it);
+    }
+  }
+
+ private:
+  static constexpr size_t kMaxCached = size_t(16) << 30;
+  std::mutex mu_;
+  std::multimap<size_t, void *> free_;
+  size_t cached_ = 0;
+};
+
+// one caller's pipeline state
+struct MatchCtx {
+  Workspace ws;
+  hipStream_t stream = nullptr;         // own stream (host-path calls)
+  std::shared_ptr<GpuSnapshot> snap;    // what the device results below were computed on
+  bool has_mo = false;
+  MatchOutput last_mo;
+  void *staging = nullptr;              // pinned input staging (topic offsets)
+  size_t staging_cap = 0;
+  ~MatchCtx() {
+    snap.reset();
+    if (staging) (void)hipHostFree(staging);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+}  // namespace
+
 struct mqm_index {
   mqm_config cfg{};
-  std::mutex mu;  // serialises mutations, commits and matches on this index
+  std::mutex mu;  // store, journal, builder, front buffer
   Store store;
-  std::unique_ptr<GpuSnapshot> snap;     // front buffer: what matches read
+  std::shared_ptr<GpuSnapshot> snap;     // front buffer: what matches read
   uint64_t snap_version = ~0ull;         // store version the front buffer reflects
-  uint64_t snap_serial = 0;              // bumped at every publish
-  Workspace ws;
-  hipStream_t stream = nullptr;
-  uint64_t matched_serial = ~0ull;       // snapshot of the last forward match (identifiers pass)
-  MatchOutput last_mo;                   // its segments (mqm_dense_device)
-  std::vector<hipStream_t> used_streams; // streams that may still read the front buffer
   // MQM_CFG_ASYNC_COMMIT: mutations since the last submit, and the builder
   // that turns them into the back buffer (builder.h)
   DeltaLog journal;
@@ -44,7 +122,18 @@ struct mqm_index {
   std::chrono::steady_clock::time_point journal_t0;
   uint64_t builds = 0, last_build_ops = 0;
   double last_build_ms = 0;
+  int walk_lanes = 8;
   bool async() const { return (cfg.flags & MQM_CFG_ASYNC_COMMIT) != 0; }
+  // the device-result API's context (mqm_match_device & follow-ups)
+  std::mutex dev_mu;
+  MatchCtx dev;
+  // host-path contexts, one per concurrent caller
+  std::mutex pool_mu;
+  std::vector<std::unique_ptr<MatchCtx>> pool;
+  std::shared_ptr<PinnedPool> pinned = std::make_shared<PinnedPool>();
+  ~mqm_index() {
+    pool.clear();
+  }
 };
 
 struct mqm_messages {
@@ -54,13 +143,18 @@ struct mqm_messages {
 
 struct mqm_result {
   uint32_t n = 0;
-  std::vector<uint64_t> offsets, shared_offsets;
-  std::vector<mqm_delivery> deliveries;
-  std::vector<uint32_t> shared;
+  // one pinned block: offsets | shared_offsets | ident_offsets | deliveries | shared | idents
+  std::shared_ptr<PinnedPool> pool;
+  void *blk = nullptr;
+  size_t blk_cap = 0;
+  const uint64_t *offsets = nullptr, *shared_offsets = nullptr, *ident_offsets = nullptr;
+  const mqm_delivery *deliveries = nullptr;
+  const uint32_t *shared = nullptr, *idents = nullptr;
   bool has_idents = false;               // MQM_CFG_IDENTIFIERS
-  std::vector<uint64_t> ident_offsets;   // n + 1
-  std::vector<uint32_t> idents;          // sids with Identifier > 0, per topic
   std::shared_ptr<const HostSnapshot> snap;
+  ~mqm_result() {
+    if (pool) pool->put(blk, blk_cap);
+  }
 };
 
 namespace {
@@ -78,29 +172,25 @@ int guarded(F &&f) {
 
 std::string_view sv(const char *p, size_t n) { return std::string_view(p ? p : "", p ? n : 0); }
 
-void note_stream(mqm_index *h, hipStream_t s) {
-  if (std::find(h->used_streams.begin(), h->used_streams.end(), s) == h->used_streams.end())
-    h->used_streams.push_back(s);
-}
+int hip_rc(int rc) { return rc == -2 ? MQM_ENOMEM : rc == -1 ? MQM_EINVAL : rc < 0 ? MQM_EHIP : rc; }
 
-// make g the front buffer; the old one is freed once the streams that may
-// still read it have drained (the builder's upload stream is not waited on)
-int install(mqm_index *h, std::unique_ptr<GpuSnapshot> g, uint64_t version) {
-  if (h->snap && h->cfg.device != MQM_DEVICE_NONE) {
-    for (hipStream_t s : h->used_streams)
-      if (hipStreamSynchronize(s) != hipSuccess) return MQM_EHIP;
-  }
-  h->used_streams.clear();
+// make g the front buffer; readers that hold the old one keep it alive
+int install(mqm_index *h, std::shared_ptr<GpuSnapshot> g, uint64_t version) {
   h->snap = std::move(g);
   h->snap_version = version;
-  h->snap_serial++;
   return MQM_OK;
 }
 
-// hand the journal to the builder (MQM_CFG_ASYNC_COMMIT)
+// hand the journal to the builder (MQM_CFG_ASYNC_COMMIT); after a replay that
+// failed part-way the builder gets a full copy of the store instead
 void submit_locked(mqm_index *h) {
+  // the builder starts empty: the journal of an async index holds every
+  // mutation since mqm_create
   if (!h->builder) h->builder = std::make_unique<Builder>(h->cfg.device);
-  h->builder->submit(std::move(h->journal), h->store.version());
+  if (h->builder->shadow_bad())
+    h->builder->submit_full(h->store, h->store.version());
+  else
+    h->builder->submit(std::move(h->journal), h->store.version());
   h->journal.clear();
   h->journal_t0 = std::chrono::steady_clock::now();
 }
@@ -115,7 +205,7 @@ int publish_locked(mqm_index *h, int *published) {
   h->last_build_ms = b.build_ms;
   h->last_build_ops = b.n_ops;
   if (published) *published = 1;
-  return install(h, std::move(b.snap), b.version);
+  return install(h, std::shared_ptr<GpuSnapshot>(std::move(b.snap)), b.version);
 }
 
 // after a logged mutation: the periodic-rebuild policy (mqm_commit_policy)
@@ -129,26 +219,106 @@ void maybe_submit(mqm_index *h) {
 int commit_locked(mqm_index *h) {
   if (h->snap && h->snap_version == h->store.version()) return MQM_OK;
   if (h->async()) {  // through the builder, so its shadow store stays in step
-    if (!h->journal.empty() || !h->builder) submit_locked(h);
+    if (!h->journal.empty() || !h->builder || h->builder->dirty() || h->builder->shadow_bad()) submit_locked(h);
     int rc = h->builder->wait_idle();
+    if (rc != MQM_OK && h->builder->shadow_bad()) {  // a replay stopped part-way: rebuild from a copy once
+      submit_locked(h);
+      rc = h->builder->wait_idle();
+    }
     if (rc != MQM_OK) return rc;
-    return publish_locked(h, nullptr);
+    rc = publish_locked(h, nullptr);
+    if (rc != MQM_OK) return rc;
+    // every submitted mutation is built and published, or this is an error
+    return h->snap && h->snap_version == h->store.version() ? MQM_OK : MQM_EINVAL;
   }
   auto hs = std::make_shared<HostSnapshot>();
   int rc = flatten(h->store, hs.get());
   if (rc != MQM_OK) return rc;
   std::unique_ptr<GpuSnapshot> g;
-  rc = upload(std::move(hs), h->cfg.device, h->stream, &g);
+  rc = upload(std::move(hs), h->cfg.device, h->dev.stream, &g);
   if (rc != MQM_OK) return rc;
-  return install(h, std::move(g), h->store.version());
+  return install(h, std::shared_ptr<GpuSnapshot>(std::move(g)), h->store.version());
 }
 
-int ensure_snapshot(mqm_index *h) {
+int ensure_snapshot_locked(mqm_index *h) {
   if (!h->snap || (h->cfg.flags & MQM_CFG_AUTOCOMMIT)) return commit_locked(h);
   if (h->async()) {
     maybe_submit(h);
     return publish_locked(h, nullptr);
   }
+  return MQM_OK;
+}
+
+// the front buffer for a match (committing first per the index's flags)
+int front(mqm_index *h, std::shared_ptr<GpuSnapshot> *out) {
+  std::lock_guard<std::mutex> g(h->mu);
+  const int rc = ensure_snapshot_locked(h);
+  if (rc != MQM_OK) return rc;
+  if (!h->snap) return MQM_EINVAL;
+  *out = h->snap;
+  return MQM_OK;
+}
+
+int ctx_init(mqm_index *h, MatchCtx *c) {
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    c->stream = nullptr;
+    return MQM_EHIP;
+  }
+  c->ws.walk_lanes = h->walk_lanes;
+  return MQM_OK;
+}
+
+// a host-path context from the pool (a new one when all are busy)
+std::unique_ptr<MatchCtx> ctx_acquire(mqm_index *h, int *rc) {
+  {
+    std::lock_guard<std::mutex> g(h->pool_mu);
+    if (!h->pool.empty()) {
+      auto c = std::move(h->pool.back());
+      h->pool.pop_back();
+      *rc = MQM_OK;
+      return c;
+    }
+  }
+  auto c = std::make_unique<MatchCtx>();
+  *rc = ctx_init(h, c.get());
+  return c;
+}
+
+void ctx_release(mqm_index *h, std::unique_ptr<MatchCtx> c) {
+  c->snap.reset();  // the call synchronised its stream: nothing reads the snapshot any more
+  c->has_mo = false;
+  std::lock_guard<std::mutex> g(h->pool_mu);
+  h->pool.push_back(std::move(c));
+}
+
+// pinned staging for n + 1 rebased offsets
+uint64_t *ctx_staging(MatchCtx *c, size_t bytes) {
+  if (c->staging_cap < bytes) {
+    if (c->staging) (void)hipHostFree(c->staging);
+    c->staging = nullptr;
+    c->staging_cap = 0;
+    if (hipHostMalloc(&c->staging, bytes + bytes / 4, hipHostMallocDefault) != hipSuccess) return nullptr;
+    c->staging_cap = bytes + bytes / 4;
+  }
+  return static_cast<uint64_t *>(c->staging);
+}
+
+// topic / filter batch from host memory into the context's input buffers
+int upload_batch(MatchCtx *c, Workspace::Slot sb, Workspace::Slot so, const char *bytes, const uint64_t *offs,
+                 uint32_t n, const uint8_t **d_bytes, const uint64_t **d_offs) {
+  Workspace &ws = c->ws;
+  const uint64_t base = offs[0], nbytes = offs[n] - base;
+  if (ws.get(sb, nbytes + 16) || ws.get(so, sizeof(uint64_t) * (n + 1))) return MQM_ENOMEM;
+  uint64_t *st = ctx_staging(c, sizeof(uint64_t) * (n + 1));
+  if (!st) return MQM_ENOMEM;
+  if (hipStreamSynchronize(c->stream) != hipSuccess) return MQM_EHIP;  // the staging block is reused
+  for (uint32_t i = 0; i <= n; i++) st[i] = offs[i] - base;
+  if (nbytes && hipMemcpyAsync(ws.ptr(sb), bytes + base, nbytes, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+    return MQM_EHIP;
+  if (hipMemcpyAsync(ws.ptr(so), st, sizeof(uint64_t) * (n + 1), hipMemcpyHostToDevice, c->stream) != hipSuccess)
+    return MQM_EHIP;
+  *d_bytes = (const uint8_t *)ws.ptr(sb);
+  *d_offs = (const uint64_t *)ws.ptr(so);
   return MQM_OK;
 }
 
@@ -163,6 +333,8 @@ int fill_info(const SubInfo &s, mqm_sub_info *out) {
   return MQM_OK;
 }
 
+bool bad_sub(const mqm_subscription &s) { return s.qos > 2 || s.retain_handling > 3; }
+
 }  // namespace
 
 extern "C" {
@@ -171,20 +343,20 @@ const char *mqm_version(void) { return "mqmatch 0.1 (gfx950)"; }
 
 int mqm_profile_enable(mqm_index *h, int on) {
   if (!h) return MQM_EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
-  h->ws.profile = on != 0;
-  h->ws.reset_profile();
+  std::lock_guard<std::mutex> g(h->dev_mu);
+  h->dev.ws.profile = on != 0;
+  h->dev.ws.reset_profile();
   return MQM_OK;
 }
 
 int mqm_profile_read(mqm_index *h, mqm_profile *out) {
   if (!h || !out) return MQM_EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
-  out->calls = h->ws.prof_calls;
-  out->fallback_topics = h->ws.prof_fallback_topics;
-  out->walk_ms = h->ws.prof_walk_ms;
-  out->dedupe_ms = h->ws.prof_dedupe_ms;
-  out->total_ms = h->ws.prof_total_ms;
+  std::lock_guard<std::mutex> g(h->dev_mu);
+  out->calls = h->dev.ws.prof_calls;
+  out->fallback_topics = h->dev.ws.prof_fallback_topics;
+  out->walk_ms = h->dev.ws.prof_walk_ms;
+  out->dedupe_ms = h->dev.ws.prof_dedupe_ms;
+  out->total_ms = h->dev.ws.prof_total_ms;
   return MQM_OK;
 }
 
@@ -202,11 +374,11 @@ int mqm_create(const mqm_config *cfg, mqm_index **out) {
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return MQM_ENODEV;
     if (h->cfg.device < 0 || h->cfg.device >= ndev) return MQM_EINVAL;
     if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
-    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) return MQM_EHIP;
-    if (const char *e = getenv("MQM_WALK_LANES")) {
+    if (const char *e = getenv("MQM_WALK_LANES")) {  // tuning knob, read once per index
       const int g = atoi(e);
-      h->ws.walk_lanes = g == 4 || g == 16 ? g : 8;
+      h->walk_lanes = g == 4 || g == 16 ? g : 8;
     }
+    if (ctx_init(h.get(), &h->dev) != MQM_OK) return MQM_EHIP;
     *out = h.release();
     return MQM_OK;
   });
@@ -218,15 +390,23 @@ int mqm_destroy(mqm_index *h) {
   if (h->cfg.device != MQM_DEVICE_NONE) {
     (void)hipSetDevice(h->cfg.device);
     (void)hipDeviceSynchronize();
-    if (h->stream) (void)hipStreamDestroy(h->stream);
   }
   delete h;
   return MQM_OK;
 }
 
+int mqm_debug_fault(mqm_index *h, int stage, int count) {
+  if (!h || stage < 1 || stage > 3 || count < 0) return MQM_EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  if (!h->async()) return MQM_EINVAL;
+  if (!h->builder) h->builder = std::make_unique<Builder>(h->cfg.device);
+  h->builder->inject_fault(stage, count);
+  return MQM_OK;
+}
+
 int mqm_subscribe(mqm_index *h, const char *client, size_t client_len, const char *filter, size_t filter_len,
                   const mqm_subscription *sub, int *is_new) {
-  if (!h || !sub) return MQM_EINVAL;
+  if (!h || !sub || bad_sub(*sub)) return MQM_EINVAL;
   return guarded([&] {
     std::lock_guard<std::mutex> g(h->mu);
     bool n = h->store.subscribe(sv(client, client_len), sv(filter, filter_len), sub->qos, sub->no_local,
@@ -245,6 +425,8 @@ int mqm_subscribe_many(mqm_index *h, size_t n, const char *client_bytes, const u
                        const char *filter_bytes, const uint64_t *filter_offs, const mqm_subscription *subs,
                        uint8_t *is_new) {
   if (!h || !client_offs || !filter_offs || !subs) return MQM_EINVAL;
+  for (size_t i = 0; i < n; i++)  // nothing is applied when any record is out of range
+    if (bad_sub(subs[i])) return MQM_EINVAL;
   return guarded([&] {
     std::lock_guard<std::mutex> g(h->mu);
     for (size_t i = 0; i < n; i++) {
@@ -367,17 +549,26 @@ int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t 
                      void *hip_stream, mqm_device_result *out) {
   if (!h || !out || (n_topics && (!d_topic_bytes || !d_topic_offsets))) return MQM_EINVAL;
   return guarded([&] {
-    std::lock_guard<std::mutex> g(h->mu);
     if (h->cfg.device == MQM_DEVICE_NONE) return MQM_ENODEV;
     if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
-    int rc = ensure_snapshot(h);
+    std::shared_ptr<GpuSnapshot> snap;
+    int rc = front(h, &snap);
     if (rc != MQM_OK) return rc;
+    std::lock_guard<std::mutex> g(h->dev_mu);
+    MatchCtx &c = h->dev;
+    const hipStream_t st = (hipStream_t)hip_stream;
+    // earlier device results (and follow-ups queued on other streams) read the
+    // workspace and their snapshot: wait for them before either is replaced
+    if (c.ws.drain()) return MQM_EHIP;
+    c.has_mo = false;
+    c.snap = snap;
+    c.ws.begin(st);
     MatchOutput mo;
-    note_stream(h, (hipStream_t)hip_stream);
-    rc = match_device(h->snap->dev, h->ws, d_topic_bytes, d_topic_offsets, n_topics, (hipStream_t)hip_stream, &mo);
-    if (rc != 0) return rc;
-    h->matched_serial = h->snap_serial;
-    h->last_mo = mo;
+    rc = match_device(snap->dev, c.ws, d_topic_bytes, d_topic_offsets, n_topics, st, &mo);
+    if (c.ws.end(st)) rc = rc ? rc : -3;
+    if (rc != 0) return hip_rc(rc);
+    c.last_mo = mo;
+    c.has_mo = true;
     out->n_topics = mo.n_topics;
     out->n_deliveries = mo.n_deliveries;
     out->n_shared = mo.n_shared;
@@ -389,7 +580,7 @@ int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t 
     out->shared = mo.shared;
     out->n_fallback = mo.n_fallback;
     out->n_big = mo.n_big;
-    for (int i = 0; i < 5; i++) out->fallback_why[i] = h->ws.why[i];
+    for (int i = 0; i < 5; i++) out->fallback_why[i] = c.ws.why[i];
     return MQM_OK;
   });
 }
@@ -399,67 +590,68 @@ int mqm_match_batch(mqm_index *h, const char *topic_bytes, const uint64_t *topic
   if (!h || !out || !topic_offsets || (n_topics && !topic_bytes)) return MQM_EINVAL;
   *out = nullptr;
   return guarded([&] {
-    std::lock_guard<std::mutex> g(h->mu);
     if (h->cfg.device == MQM_DEVICE_NONE) return MQM_ENODEV;
     if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
-    int rc = ensure_snapshot(h);
+    std::shared_ptr<GpuSnapshot> snap;
+    int rc = front(h, &snap);
     if (rc != MQM_OK) return rc;
-    const uint64_t base = topic_offsets[0];
-    const uint64_t nbytes = topic_offsets[n_topics] - base;
-    Workspace &ws = h->ws;
-    if (ws.get(Workspace::kInBytes, nbytes + 16) || ws.get(Workspace::kInOffs, sizeof(uint64_t) * (n_topics + 1)))
-      return MQM_ENOMEM;
-    auto *d_bytes = (uint8_t *)ws.ptr(Workspace::kInBytes);
-    auto *d_offs = (uint64_t *)ws.ptr(Workspace::kInOffs);
-    std::vector<uint64_t> offs(topic_offsets, topic_offsets + n_topics + 1);
-    for (auto &o : offs) o -= base;
-    if (nbytes && hipMemcpyAsync(d_bytes, topic_bytes + base, nbytes, hipMemcpyHostToDevice, h->stream) != hipSuccess)
-      return MQM_EHIP;
-    if (hipMemcpyAsync(d_offs, offs.data(), sizeof(uint64_t) * (n_topics + 1), hipMemcpyHostToDevice, h->stream) !=
-        hipSuccess)
-      return MQM_EHIP;
-    MatchOutput mo;
-    note_stream(h, h->stream);
-    rc = match_device(h->snap->dev, ws, d_bytes, d_offs, n_topics, h->stream, &mo);
-    if (rc != 0) return rc;
-    h->matched_serial = h->snap_serial;
-    h->last_mo = mo;
-    IdentOutput io;
-    const bool want_ids = (h->cfg.flags & MQM_CFG_IDENTIFIERS) != 0;
-    if (want_ids && (rc = identifiers_device(h->snap->dev, ws, h->stream, &io)) != 0) return rc;
-    DenseOutput dn;
-    rc = densify(ws, mo, h->stream, &dn);
-    if (rc != 0) return rc;
+    auto c = ctx_acquire(h, &rc);
+    if (rc != MQM_OK) return rc;
     auto r = std::make_unique<mqm_result>();
-    r->n = n_topics;
-    r->offsets.resize(n_topics + 1);
-    r->shared_offsets.resize(n_topics + 1);
-    r->deliveries.resize(mo.n_deliveries);
-    r->shared.resize(mo.n_shared);
-    r->snap = h->snap->host;
-    if (hipMemcpyAsync(r->offsets.data(), dn.offsets, sizeof(uint64_t) * (n_topics + 1), hipMemcpyDeviceToHost,
-                       h->stream) != hipSuccess ||
-        hipMemcpyAsync(r->shared_offsets.data(), dn.shared_offsets, sizeof(uint64_t) * (n_topics + 1),
-                       hipMemcpyDeviceToHost, h->stream) != hipSuccess)
-      return MQM_EHIP;
-    if (mo.n_deliveries && hipMemcpyAsync(r->deliveries.data(), dn.deliveries, sizeof(uint64_t) * mo.n_deliveries,
-                                          hipMemcpyDeviceToHost, h->stream) != hipSuccess)
-      return MQM_EHIP;
-    if (mo.n_shared && hipMemcpyAsync(r->shared.data(), dn.shared, sizeof(uint32_t) * mo.n_shared,
-                                      hipMemcpyDeviceToHost, h->stream) != hipSuccess)
-      return MQM_EHIP;
-    if (want_ids) {
-      r->has_idents = true;
-      r->ident_offsets.resize(n_topics + 1);
-      r->idents.resize(io.n_idents);
-      if (hipMemcpyAsync(r->ident_offsets.data(), io.offsets, sizeof(uint64_t) * (n_topics + 1),
-                         hipMemcpyDeviceToHost, h->stream) != hipSuccess)
+    rc = [&]() -> int {
+      Workspace &ws = c->ws;
+      const hipStream_t st = c->stream;
+      ws.begin(st);
+      const uint8_t *d_bytes = nullptr;
+      const uint64_t *d_offs = nullptr;
+      int e = upload_batch(c.get(), Workspace::kInBytes, Workspace::kInOffs, topic_bytes, topic_offsets, n_topics,
+                           &d_bytes, &d_offs);
+      if (e != MQM_OK) return e;
+      MatchOutput mo;
+      if ((e = match_device(snap->dev, ws, d_bytes, d_offs, n_topics, st, &mo)) != 0) return hip_rc(e);
+      IdentOutput io;
+      const bool want_ids = (h->cfg.flags & MQM_CFG_IDENTIFIERS) != 0;
+      if (want_ids && (e = identifiers_device(snap->dev, ws, st, &io)) != 0) return hip_rc(e);
+      DenseOutput dn;
+      if ((e = densify(ws, mo, st, &dn)) != 0) return hip_rc(e);
+      // one pinned block: three offset arrays, then the entries (16-B aligned parts)
+      const uint64_t n1 = (uint64_t)n_topics + 1, ni = want_ids ? io.n_idents : 0;
+      auto up = [](uint64_t b) { return (b + 15) & ~15ull; };
+      const uint64_t o_off = 0, o_sh = up(8 * n1), o_io = o_sh + up(8 * n1), o_d = o_io + (want_ids ? up(8 * n1) : 0);
+      const uint64_t o_s = o_d + up(8 * mo.n_deliveries), o_i = o_s + up(4 * mo.n_shared), total = o_i + up(4 * ni);
+      r->pool = h->pinned;
+      r->blk = h->pinned->get(total, &r->blk_cap);
+      if (!r->blk) {
+        r->pool.reset();
+        return MQM_ENOMEM;
+      }
+      char *B = static_cast<char *>(r->blk);
+      r->n = n_topics;
+      r->offsets = reinterpret_cast<const uint64_t *>(B + o_off);
+      r->shared_offsets = reinterpret_cast<const uint64_t *>(B + o_sh);
+      r->deliveries = reinterpret_cast<const mqm_delivery *>(B + o_d);
+      r->shared = reinterpret_cast<const uint32_t *>(B + o_s);
+      r->snap = snap->host;
+      if (hipMemcpyAsync(B + o_off, dn.offsets, 8 * n1, hipMemcpyDeviceToHost, st) != hipSuccess ||
+          hipMemcpyAsync(B + o_sh, dn.shared_offsets, 8 * n1, hipMemcpyDeviceToHost, st) != hipSuccess)
         return MQM_EHIP;
-      if (io.n_idents && hipMemcpyAsync(r->idents.data(), io.sids, sizeof(uint32_t) * io.n_idents,
-                                        hipMemcpyDeviceToHost, h->stream) != hipSuccess)
+      if (mo.n_deliveries &&
+          hipMemcpyAsync(B + o_d, dn.deliveries, 8 * mo.n_deliveries, hipMemcpyDeviceToHost, st) != hipSuccess)
         return MQM_EHIP;
-    }
-    if (hipStreamSynchronize(h->stream) != hipSuccess) return MQM_EHIP;
+      if (mo.n_shared && hipMemcpyAsync(B + o_s, dn.shared, 4 * mo.n_shared, hipMemcpyDeviceToHost, st) != hipSuccess)
+        return MQM_EHIP;
+      if (want_ids) {
+        r->has_idents = true;
+        r->ident_offsets = reinterpret_cast<const uint64_t *>(B + o_io);
+        r->idents = reinterpret_cast<const uint32_t *>(B + o_i);
+        if (hipMemcpyAsync(B + o_io, io.offsets, 8 * n1, hipMemcpyDeviceToHost, st) != hipSuccess) return MQM_EHIP;
+        if (ni && hipMemcpyAsync(B + o_i, io.sids, 4 * ni, hipMemcpyDeviceToHost, st) != hipSuccess) return MQM_EHIP;
+      }
+      if (ws.end(st) || hipStreamSynchronize(st) != hipSuccess) return MQM_EHIP;
+      return MQM_OK;
+    }();
+    ctx_release(h, std::move(c));
+    if (rc != MQM_OK) return rc;
     *out = r.release();
     return MQM_OK;
   });
@@ -468,15 +660,17 @@ int mqm_match_batch(mqm_index *h, const char *topic_bytes, const uint64_t *topic
 int mqm_identifiers_device(mqm_index *h, void *hip_stream, mqm_device_identifiers *out) {
   if (!h || !out) return MQM_EINVAL;
   return guarded([&] {
-    std::lock_guard<std::mutex> g(h->mu);
     if (h->cfg.device == MQM_DEVICE_NONE) return MQM_ENODEV;
-    // the records of the last forward match, against the snapshot it read
-    if (!h->snap || h->matched_serial != h->snap_serial) return MQM_EINVAL;
+    std::lock_guard<std::mutex> g(h->dev_mu);
+    MatchCtx &c = h->dev;
+    if (!c.has_mo) return MQM_EINVAL;  // the records of the last mqm_match_device call
     if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
-    note_stream(h, (hipStream_t)hip_stream);
+    const hipStream_t st = (hipStream_t)hip_stream;
+    c.ws.begin(st);
     IdentOutput io;
-    const int rc = identifiers_device(h->snap->dev, h->ws, (hipStream_t)hip_stream, &io);
-    if (rc != 0) return rc == -2 ? MQM_ENOMEM : rc == -1 ? MQM_EINVAL : MQM_EHIP;
+    int rc = identifiers_device(c.snap->dev, c.ws, st, &io);
+    if (c.ws.end(st)) rc = rc ? rc : -3;
+    if (rc != 0) return hip_rc(rc);
     out->n_topics = io.n_topics;
     out->n_idents = io.n_idents;
     out->offsets = io.offsets;
@@ -488,17 +682,20 @@ int mqm_identifiers_device(mqm_index *h, void *hip_stream, mqm_device_identifier
 int mqm_dense_device(mqm_index *h, void *hip_stream, mqm_device_dense *out) {
   if (!h || !out) return MQM_EINVAL;
   return guarded([&] {
-    std::lock_guard<std::mutex> g(h->mu);
     if (h->cfg.device == MQM_DEVICE_NONE) return MQM_ENODEV;
-    if (!h->snap || h->matched_serial != h->snap_serial) return MQM_EINVAL;
+    std::lock_guard<std::mutex> g(h->dev_mu);
+    MatchCtx &c = h->dev;
+    if (!c.has_mo) return MQM_EINVAL;
     if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
-    note_stream(h, (hipStream_t)hip_stream);
+    const hipStream_t st = (hipStream_t)hip_stream;
+    c.ws.begin(st);
     DenseOutput dn;
-    const int rc = densify(h->ws, h->last_mo, (hipStream_t)hip_stream, &dn);
-    if (rc != 0) return rc == -2 ? MQM_ENOMEM : MQM_EHIP;
-    out->n_topics = h->last_mo.n_topics;
-    out->n_deliveries = h->last_mo.n_deliveries;
-    out->n_shared = h->last_mo.n_shared;
+    int rc = densify(c.ws, c.last_mo, st, &dn);
+    if (c.ws.end(st)) rc = rc ? rc : -3;
+    if (rc != 0) return hip_rc(rc);
+    out->n_topics = c.last_mo.n_topics;
+    out->n_deliveries = c.last_mo.n_deliveries;
+    out->n_shared = c.last_mo.n_shared;
     out->offsets = dn.offsets;
     out->deliveries = reinterpret_cast<const mqm_delivery *>(dn.deliveries);
     out->shared_offsets = dn.shared_offsets;
@@ -537,8 +734,8 @@ int mqm_gather_shards(uint32_t n_topics, uint32_t n_shards, const mqm_shard_part
 
 int mqm_result_identifiers(const mqm_result *r, const uint64_t **offsets, const uint32_t **sids) {
   if (!r || !offsets || !sids || !r->has_idents) return MQM_EINVAL;
-  *offsets = r->ident_offsets.data();
-  *sids = r->idents.data();
+  *offsets = r->ident_offsets;
+  *sids = r->idents;
   return MQM_OK;
 }
 
@@ -546,16 +743,23 @@ int mqm_messages_device(mqm_index *h, const uint8_t *d_filter_bytes, const uint6
                         uint32_t n_filters, void *hip_stream, mqm_device_messages *out) {
   if (!h || !out || (n_filters && (!d_filter_bytes || !d_filter_offsets))) return MQM_EINVAL;
   return guarded([&] {
-    std::lock_guard<std::mutex> g(h->mu);
     if (h->cfg.device == MQM_DEVICE_NONE) return MQM_ENODEV;
     if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
-    int rc = ensure_snapshot(h);
+    std::shared_ptr<GpuSnapshot> snap;
+    int rc = front(h, &snap);
     if (rc != MQM_OK) return rc;
+    std::lock_guard<std::mutex> g(h->dev_mu);
+    MatchCtx &c = h->dev;
+    if (c.ws.drain()) return MQM_EHIP;
+    c.has_mo = false;  // the forward-match records share nothing, but the snapshot changes
+    c.snap = snap;
+    const hipStream_t st = (hipStream_t)hip_stream;
+    c.ws.begin(st);
     MessagesOutput mo;
-    note_stream(h, (hipStream_t)hip_stream);
-    rc = messages_device(h->snap->dev, h->snap->has_retained ? &h->snap->ret : nullptr, h->ws, d_filter_bytes,
-                         d_filter_offsets, n_filters, (hipStream_t)hip_stream, &mo);
-    if (rc != 0) return rc;
+    rc = messages_device(snap->dev, snap->has_retained ? &snap->ret : nullptr, c.ws, d_filter_bytes,
+                         d_filter_offsets, n_filters, st, &mo);
+    if (c.ws.end(st)) rc = rc ? rc : -3;
+    if (rc != 0) return hip_rc(rc);
     out->n_filters = mo.n_filters;
     out->n_refs = mo.n_refs;
     out->offsets = mo.offsets;
@@ -571,41 +775,41 @@ int mqm_messages_batch(mqm_index *h, const char *filter_bytes, const uint64_t *f
   if (!h || !out || !filter_offsets || (n_filters && !filter_bytes)) return MQM_EINVAL;
   *out = nullptr;
   return guarded([&] {
-    std::lock_guard<std::mutex> g(h->mu);
     if (h->cfg.device == MQM_DEVICE_NONE) return MQM_ENODEV;
     if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
-    int rc = ensure_snapshot(h);
+    std::shared_ptr<GpuSnapshot> snap;
+    int rc = front(h, &snap);
     if (rc != MQM_OK) return rc;
-    const uint64_t base = filter_offsets[0];
-    const uint64_t nbytes = filter_offsets[n_filters] - base;
-    Workspace &ws = h->ws;
-    if (ws.get(Workspace::kRInBytes, nbytes + 16) || ws.get(Workspace::kRInOffs, sizeof(uint64_t) * (n_filters + 1)))
-      return MQM_ENOMEM;
-    auto *d_bytes = (uint8_t *)ws.ptr(Workspace::kRInBytes);
-    auto *d_offs = (uint64_t *)ws.ptr(Workspace::kRInOffs);
-    std::vector<uint64_t> offs(filter_offsets, filter_offsets + n_filters + 1);
-    for (auto &o : offs) o -= base;
-    if (nbytes && hipMemcpyAsync(d_bytes, filter_bytes + base, nbytes, hipMemcpyHostToDevice, h->stream) != hipSuccess)
-      return MQM_EHIP;
-    if (hipMemcpyAsync(d_offs, offs.data(), sizeof(uint64_t) * (n_filters + 1), hipMemcpyHostToDevice, h->stream) !=
-        hipSuccess)
-      return MQM_EHIP;
-    MessagesOutput mo;
-    note_stream(h, h->stream);
-    rc = messages_device(h->snap->dev, h->snap->has_retained ? &h->snap->ret : nullptr, ws, d_bytes, d_offs,
-                         n_filters, h->stream, &mo);
-    if (rc != 0) return rc;
+    auto c = ctx_acquire(h, &rc);
+    if (rc != MQM_OK) return rc;
     auto m = std::make_unique<mqm_messages>();
-    m->n = n_filters;
-    m->offsets.resize(n_filters + 1);
-    m->refs.resize(mo.n_refs);
-    if (hipMemcpyAsync(m->offsets.data(), mo.offsets, sizeof(uint64_t) * (n_filters + 1), hipMemcpyDeviceToHost,
-                       h->stream) != hipSuccess)
-      return MQM_EHIP;
-    if (mo.n_refs && hipMemcpyAsync(m->refs.data(), mo.refs, sizeof(uint64_t) * mo.n_refs, hipMemcpyDeviceToHost,
-                                    h->stream) != hipSuccess)
-      return MQM_EHIP;
-    if (hipStreamSynchronize(h->stream) != hipSuccess) return MQM_EHIP;
+    rc = [&]() -> int {
+      Workspace &ws = c->ws;
+      const hipStream_t st = c->stream;
+      ws.begin(st);
+      const uint8_t *d_bytes = nullptr;
+      const uint64_t *d_offs = nullptr;
+      int e = upload_batch(c.get(), Workspace::kRInBytes, Workspace::kRInOffs, filter_bytes, filter_offsets,
+                           n_filters, &d_bytes, &d_offs);
+      if (e != MQM_OK) return e;
+      MessagesOutput mo;
+      e = messages_device(snap->dev, snap->has_retained ? &snap->ret : nullptr, ws, d_bytes, d_offs, n_filters, st,
+                          &mo);
+      if (e != 0) return hip_rc(e);
+      m->n = n_filters;
+      m->offsets.resize(n_filters + 1);
+      m->refs.resize(mo.n_refs);
+      if (hipMemcpyAsync(m->offsets.data(), mo.offsets, sizeof(uint64_t) * (n_filters + 1), hipMemcpyDeviceToHost,
+                         st) != hipSuccess)
+        return MQM_EHIP;
+      if (mo.n_refs &&
+          hipMemcpyAsync(m->refs.data(), mo.refs, sizeof(uint64_t) * mo.n_refs, hipMemcpyDeviceToHost, st) != hipSuccess)
+        return MQM_EHIP;
+      if (ws.end(st) || hipStreamSynchronize(st) != hipSuccess) return MQM_EHIP;
+      return MQM_OK;
+    }();
+    ctx_release(h, std::move(c));
+    if (rc != MQM_OK) return rc;
     *out = m.release();
     return MQM_OK;
   });
@@ -627,10 +831,10 @@ int mqm_subscribers(mqm_index *h, const char *topic, size_t topic_len, mqm_resul
 }
 
 uint32_t mqm_result_num_topics(const mqm_result *r) { return r ? r->n : 0; }
-const uint64_t *mqm_result_offsets(const mqm_result *r) { return r ? r->offsets.data() : nullptr; }
-const mqm_delivery *mqm_result_deliveries(const mqm_result *r) { return r ? r->deliveries.data() : nullptr; }
-const uint64_t *mqm_result_shared_offsets(const mqm_result *r) { return r ? r->shared_offsets.data() : nullptr; }
-const uint32_t *mqm_result_shared(const mqm_result *r) { return r ? r->shared.data() : nullptr; }
+const uint64_t *mqm_result_offsets(const mqm_result *r) { return r ? r->offsets : nullptr; }
+const mqm_delivery *mqm_result_deliveries(const mqm_result *r) { return r ? r->deliveries : nullptr; }
+const uint64_t *mqm_result_shared_offsets(const mqm_result *r) { return r ? r->shared_offsets : nullptr; }
+const uint32_t *mqm_result_shared(const mqm_result *r) { return r ? r->shared : nullptr; }
 
 int mqm_result_sub_info(const mqm_result *r, uint32_t sub, mqm_sub_info *out) {
   if (!r || !out || !r->snap || sub >= r->snap->sub_info.size()) return MQM_EINVAL;
@@ -693,7 +897,7 @@ int mqm_commit_async(mqm_index *h) {
     std::lock_guard<std::mutex> g(h->mu);
     if (!h->async()) return MQM_EINVAL;
     if (h->cfg.device != MQM_DEVICE_NONE && hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
-    if (!h->journal.empty() || !h->builder) submit_locked(h);
+    if (!h->journal.empty() || !h->builder || h->builder->dirty() || h->builder->shadow_bad()) submit_locked(h);
     return MQM_OK;
   });
 }
@@ -705,9 +909,12 @@ int mqm_commit_poll(mqm_index *h, int wait, int *published) {
     if (published) *published = 0;
     if (!h->async()) return MQM_EINVAL;
     if (h->cfg.device != MQM_DEVICE_NONE && hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
-    if (wait && h->builder) {
-      int rc = h->builder->wait_idle();
-      if (rc != MQM_OK) return rc;
+    if (wait) {
+      if (h->builder && (h->builder->dirty() || h->builder->shadow_bad())) submit_locked(h);
+      if (h->builder) {
+        int rc = h->builder->wait_idle();
+        if (rc != MQM_OK) return rc;
+      }
     }
     return publish_locked(h, published);
   });

@@ -322,7 +322,7 @@ int flatten(const Store &st, HostSnapshot *out) {
           hs.nodes[k].sub_off = (uint32_t)so;
           hs.nodes[k].sub_cnt = (uint32_t)subs.size();
           for (const SubRec &x : subs) {
-            hs.subs[so] = SubEnt{x.client, (uint32_t)x.qos | ((uint32_t)(x.no_local & 1) << 2) |
+            hs.subs[so] = SubEnt{x.client, ((uint32_t)x.qos & 3u) | ((uint32_t)(x.no_local & 1) << 2) |
                                               ((uint32_t)(x.rap & 1) << 3) | ((uint32_t)(x.rh & 3) << 4) |
                                               (x.ident > 0 ? kMetaIdent : 0u)};
             hs.sub_info[so++] = SubInfo{x.filter, x.client, x.ident, x.qos, x.no_local, x.rap, x.rh};

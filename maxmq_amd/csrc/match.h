@@ -48,7 +48,17 @@ struct Workspace {
     prof_walk_ms = prof_dedupe_ms = prof_total_ms = 0;
   }
 
-  static int reserve(void **p, size_t *cap, size_t need);
+  // Buffers are stream-ordered allocations (hipMallocAsync / hipFreeAsync on
+  // `cur`), so growing one never waits for other streams (a background
+  // snapshot upload, another index's matches): only for this workspace's own
+  // queued work (`cur`) and its previous calls (`last_use`).
+  hipStream_t cur = nullptr;     // stream of the call in progress (begin())
+  hipEvent_t last_use = nullptr; // recorded by end() after every call's work
+  bool used = false;
+  void begin(hipStream_t st) { cur = st; }
+  int end(hipStream_t st);       // record last_use on st
+  int drain();                   // wait for every queued use of the buffers
+  int reserve(void **p, size_t *cap, size_t need);
   int get(Slot s, size_t need) { return reserve(&bufs[s].p, &bufs[s].cap, need); }
   // like get(), but a reallocation keeps the first `used` bytes (copied on `st`)
   int grow_keep(Slot s, size_t used, size_t need, hipStream_t st);

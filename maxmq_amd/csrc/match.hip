@@ -1146,16 +1146,36 @@ struct IsBigClass {
 // ---------------------------------------------------------------------------
 // workspace / orchestration
 // ---------------------------------------------------------------------------
+int Workspace::end(hipStream_t st) {
+  if (!last_use && hipEventCreateWithFlags(&last_use, hipEventDisableTiming) != hipSuccess) {
+    last_use = nullptr;
+    return -3;
+  }
+  if (hipEventRecord(last_use, st) != hipSuccess) return -3;
+  used = true;
+  return 0;
+}
+
+int Workspace::drain() {
+  if (cur && hipStreamSynchronize(cur) != hipSuccess) return -3;
+  if (used && last_use && hipEventSynchronize(last_use) != hipSuccess) return -3;
+  return 0;
+}
+
 int Workspace::reserve(void **p, size_t *cap, size_t need) {
   if (*cap >= need && *p) return 0;
   if (*p) {
-    (void)hipDeviceSynchronize();  // queued kernels may still read the old buffer
-    (void)hipFree(*p);
+    // queued kernels of this call (cur) or of earlier calls (last_use) may
+    // still read the old buffer; hipFree would also wait for every other
+    // stream on the device, hipFreeAsync does not
+    if (drain()) return -3;
+    (void)hipFreeAsync(*p, cur);
   }
   *p = nullptr;
   size_t n = std::max<size_t>(need, 256);
   n = n + n / 4;
-  if (hipMalloc(p, n) != hipSuccess) {
+  if (hipMallocAsync(p, n, cur) != hipSuccess || hipStreamSynchronize(cur) != hipSuccess) {
+    *p = nullptr;
     *cap = 0;
     return -2;
   }
@@ -1163,18 +1183,19 @@ int Workspace::reserve(void **p, size_t *cap, size_t need) {
   return 0;
 }
 
-int Workspace::grow_keep(Slot s, size_t used, size_t need, hipStream_t st) {
+int Workspace::grow_keep(Slot s, size_t used_bytes, size_t need, hipStream_t st) {
   Buf &b = bufs[s];
   if (b.cap >= need && b.p) return 0;
   void *p = nullptr;
   size_t cap = 0;
+  if (drain()) return -3;
   if (reserve(&p, &cap, need)) return -2;
-  if (used && (hipMemcpyAsync(p, b.p, used, hipMemcpyDeviceToDevice, st) != hipSuccess ||
-               hipStreamSynchronize(st) != hipSuccess)) {
-    (void)hipFree(p);
+  if (used_bytes && (hipMemcpyAsync(p, b.p, used_bytes, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+                     hipStreamSynchronize(st) != hipSuccess)) {
+    (void)hipFreeAsync(p, cur);
     return -3;
   }
-  if (b.p) (void)hipFree(b.p);
+  if (b.p) (void)hipFreeAsync(b.p, cur);
   b.p = p;
   b.cap = cap;
   return 0;
@@ -1186,8 +1207,11 @@ uint64_t *Workspace::pinned_u64() {
 }
 
 Workspace::~Workspace() {
+  // `cur` may name a caller's stream that no longer exists: wait on our event
+  if (used && last_use) (void)hipEventSynchronize(last_use);
   for (auto &b : bufs)
     if (b.p) (void)hipFree(b.p);
+  if (last_use) (void)hipEventDestroy(last_use);
   if (host_pinned) (void)hipHostFree(host_pinned);
   for (auto &e : ev)
     if (e) (void)hipEventDestroy(e);

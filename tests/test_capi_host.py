@@ -93,3 +93,23 @@ def test_interning_order_is_first_appearance():
         idx.subscribe(c, maxmq_amd.Subscription(f))
     assert [idx.client_name(i) for i in range(idx.num_clients())] == ["zed", "amy"]
     assert [idx.filter_name(i) for i in range(3)] == ["a", "b", "c"]
+
+
+def test_subscribe_rejects_out_of_range_options():
+    """qos > 2 or retain_handling > 3 would spill into the packed
+    meta bits of the snapshot; the C ABI rejects them and stores nothing."""
+    import numpy as np
+
+    import maxmq_amd
+    from maxmq_amd import capi
+    from tools.mqgen import Strings
+
+    idx = maxmq_amd.TopicsIndex(device=None)
+    for kw in (dict(qos=3), dict(qos=7), dict(retain_handling=4)):
+        with pytest.raises(maxmq_amd.MqmError) as e:
+            idx.subscribe("c", maxmq_amd.Subscription("a/b", **kw))
+        assert e.value.rc == capi.MQM_EINVAL
+    assert idx.subscribe("c", maxmq_amd.Subscription("a/b", qos=2, retain_handling=3))
+    with pytest.raises(maxmq_amd.MqmError):
+        idx.subscribe_many(Strings.from_list(["x", "y"]), Strings.from_list(["p", "q"]), np.array([1, 3], np.uint8))
+    assert idx.subscribe("x", maxmq_amd.Subscription("p"))  # the bulk call applied nothing

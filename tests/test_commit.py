@@ -224,3 +224,60 @@ def test_unsubscribe_many_matches_single_calls():
     a.commit()
     b.commit()
     assert a.snapshot_digest() == b.snapshot_digest()
+
+
+@pytest.mark.parametrize("stage", [1, 2, 3])
+def test_failed_build_is_reported_then_rebuilt(stage):
+    """a failed background build (replay part-way, flatten, upload)
+    must not leave a stale snapshot published as current.  The commit that
+    waits for it reports the error or repairs it at once; the following
+    commit publishes a snapshot equal to a synchronous flatten of the store."""
+    rng = random.Random(40 + stage)
+    sync = maxmq_amd.TopicsIndex(device=None, autocommit=False)
+    asy = maxmq_amd.TopicsIndex(device=None, autocommit=False, async_commit=True)
+    for step in range(300):
+        _random_op(rng, [sync, asy], step)
+    asy.commit()
+    sync.commit()
+    assert asy.snapshot_digest() == sync.snapshot_digest()
+    for step in range(300, 600):
+        _random_op(rng, [sync, asy], step)
+    sync.commit()
+    check = capi.check
+    check("mqm_debug_fault", capi.lib().mqm_debug_fault(asy._h, stage, 1))
+    asy.commit_async()
+    try:
+        asy.commit()  # a replay fault is repaired inside this commit (full resync)
+    except maxmq_amd.MqmError as e:
+        assert stage != 1 and e.rc == capi.MQM_ENOMEM
+        st = asy.commit_state()
+        assert st["snapshot_version"] != st["store_version"]  # the stale snapshot is not claimed current
+        asy.commit()
+    st = asy.commit_state()
+    assert st["snapshot_version"] == st["store_version"]
+    assert asy.snapshot_digest() == sync.snapshot_digest()
+    # and the shadow store stays in step afterwards
+    for step in range(600, 700):
+        _random_op(rng, [sync, asy], step)
+    sync.commit()
+    asy.commit()
+    assert asy.snapshot_digest() == sync.snapshot_digest()
+
+
+def test_replay_fault_while_logs_queue():
+    """a replay fault with more logs submitted behind it: the stale shadow
+    refuses them, and the next commit resyncs from a full copy"""
+    rng = random.Random(77)
+    sync = maxmq_amd.TopicsIndex(device=None, autocommit=False)
+    asy = maxmq_amd.TopicsIndex(device=None, autocommit=False, async_commit=True)
+    capi.check("mqm_debug_fault", capi.lib().mqm_debug_fault(asy._h, 1, 2))
+    for step in range(400):
+        _random_op(rng, [sync, asy], step)
+        if step % 50 == 49:
+            asy.commit_async()
+    sync.commit()
+    try:
+        asy.commit()
+    except maxmq_amd.MqmError:
+        asy.commit()
+    assert asy.snapshot_digest() == sync.snapshot_digest()
