@@ -48,10 +48,15 @@ def parse():
     ap.add_argument("--topics", type=int, default=0, help="override n_topics")
     ap.add_argument("--mode", choices=["replicas", "sharded"], default="replicas")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0 = one per CPU this process may run on, BASELINE.md §2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-topics", type=int, default=1000000,
-                    help="PCIe-inclusive host path (mqm_match_batch) sample, outside the timed region; 0 = skip")
+                    help="PCIe-inclusive host path (mqm_match_batch): topics per call, outside the timed region; 0 = skip")
+    ap.add_argument("--host-threads", type=int, default=4,
+                    help="host path: concurrent callers (each its own stream), batches overlapped across them")
+    ap.add_argument("--latency-topics", type=int, default=2000,
+                    help="single-topic mqm_subscribers calls timed for the per-publish latency; 0 = skip")
     ap.add_argument("--workload", choices=["forward", "reverse", "churn"], default="forward",
                     help="forward: Subscribers (headline); reverse: Messages over retained topics (config 5); "
                          "churn: Subscribe/Unsubscribe at rate with background snapshot rebuilds")
@@ -84,8 +89,76 @@ def _heartbeat(period=60.0):
     threading.Thread(target=beat, daemon=True).start()
 
 
+def spawn_ranks(args):
+    """--gpus N > 1 outside torchrun: start N rank processes (one per GPU) with
+    torch.distributed.run and exit with its status.  Runs before anything
+    touches the GPU (the parent never initialises HIP)."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    log(f"[bench] starting {args.gpus} ranks: {' '.join(cmd)}")
+    return subprocess.call(cmd, env=env)
+
+
+def cpu_threads(args):
+    """one thread per CPU this process may actually run on —
+    its affinity mask, capped by its cgroup CPU quota (the GPU box grants a
+    16-CPU share of a 2 x 64-core host: more threads would only time-slice) —
+    unless --cpu-threads says otherwise."""
+    info = host_info()
+    avail = info.get("cpus_affinity") or os.cpu_count() or 1
+    q = info.get("cgroup_cpu_quota")
+    if q:
+        avail = min(avail, max(1, int(q)))
+    return max(1, args.cpu_threads or avail)
+
+
+def host_info():
+    """visible CPUs, affinity, cgroup CPU quota, physical cores, model"""
+    info = {"cpus_visible": os.cpu_count()}
+    try:
+        info["cpus_affinity"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()
+            info["cgroup_cpu_quota"] = None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        cores, model = set(), ""
+        phys = core = None
+        with open("/proc/cpuinfo") as fh:
+            for ln in fh:
+                k, _, v = ln.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "model name":
+                    model = v
+                elif k == "physical id":
+                    phys = v
+                elif k == "core id":
+                    core = v
+                elif not k and phys is not None:
+                    cores.add((phys, core))
+        info["physical_cores"] = len(cores) or None
+        info["model"] = model
+    except OSError:
+        pass
+    return info
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
     _heartbeat()
     import torch
 
@@ -213,6 +286,7 @@ def main():
         cpu = None
         stats = None
         host = host_path(idx, w, args) if args.host_topics and not sharded else None
+        lat = latency(idx, w, args) if args.latency_topics and not sharded else None
         if not args.no_cpu_baseline:
             cpu, stats = cpu_baseline(w, args)
         roof = roofline(stats, n, kms, args.traffic_json)
@@ -248,6 +322,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "host_path": host,
+            "single_topic_latency": lat,
         }
         print(json.dumps(out), flush=True)
     if dist:
@@ -256,36 +331,109 @@ def main():
 
 
 def host_path(idx, w, args):
-    """The boundary's host form, mqm_match_batch: topics in host memory ->
-    H2D copy -> the same match pipeline -> dense CSR copied back into
-    library-owned (pageable) host arrays.  Timed on the first --host-topics
-    topics of the batch, outside the headline's timed region (the headline is
-    HBM-resident)."""
+    """The boundary's host form, mqm_match_batch, as a broker would drive it
+    (SURVEY §8d end-to-end): topics in pinned host memory -> H2D -> the match
+    pipeline -> dense CSR D2H into pinned, library-owned result blocks.
+    --host-threads callers each take --host-topics-topic batches of the C3
+    batch in turn; every caller has its own workspace and HIP stream
+    (include/mqmatch.h, Threading), so one batch's copies overlap another's
+    kernels.  Timed outside the headline's region.  `pcie_bound` = the same
+    bytes at the link rates measured here (H2D and D2H run concurrently)."""
     import ctypes as C
+    import threading
+
+    import torch
+
     from maxmq_amd import capi
 
     L = capi.lib()
-    h = min(args.host_topics, len(w.topics))
-    data = w.topics.data
-    offs = np.ascontiguousarray(w.topics.offs[: h + 1], dtype=np.uint64)
+    per = min(args.host_topics, len(w.topics))
+    nb = max(1, len(w.topics) // per)
+    data = torch.from_numpy(w.topics.data).pin_memory()
+    offs = torch.from_numpy(w.topics.offs[: nb * per + 1].astype(np.int64)).pin_memory()
+    dp, op = data.data_ptr(), offs.data_ptr()
 
-    def call():
+    def call(b):
         res = C.c_void_p()
-        capi.check("mqm_match_batch", L.mqm_match_batch(idx._h, data.ctypes.data_as(C.c_void_p),
-                                                        offs.ctypes.data_as(C.c_void_p), h, C.byref(res)))
-        return res
-
-    L.mqm_result_free(call())  # warm (workspace sizing)
-    reps, dt, dl = 3, 0.0, 0
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        res = call()
-        dt += time.perf_counter() - t0
-        dl += int(C.cast(L.mqm_result_offsets(res), C.POINTER(C.c_uint64))[h])
+        capi.check("mqm_match_batch", L.mqm_match_batch(idx._h, C.c_void_p(dp), C.c_void_p(op + 8 * b * per), per,
+                                                        C.byref(res)))
+        d = int(C.cast(L.mqm_result_offsets(res), C.POINTER(C.c_uint64))[per])
         L.mqm_result_free(res)
-    return {"value": h * reps / dt, "unit": "topics/s", "topics": h, "ms_per_call": dt * 1e3 / reps,
-            "deliveries_per_s": dl / dt,
-            "note": "PCIe-inclusive: topic bytes+offsets H2D, match, dense CSR D2H into pageable host memory"}
+        return d
+
+    for t in range(args.host_threads):  # warm every context (workspace sizing, pinned blocks)
+        call(t % nb)
+    done = [0, 0]
+    lock = threading.Lock()
+    nxt = [0]
+
+    def worker():
+        while True:
+            with lock:
+                b = nxt[0]
+                nxt[0] += 1
+            if b >= nb:
+                return
+            d = call(b)
+            with lock:
+                done[0] += per
+                done[1] += d
+
+    t0 = time.perf_counter()
+    ths = [threading.Thread(target=worker) for _ in range(args.host_threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    dt = time.perf_counter() - t0
+    # link rates: 1 GiB pinned <-> device, each direction alone
+    dev = torch.device("cuda", torch.cuda.current_device())
+    g = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
+    h = torch.empty(1 << 30, dtype=torch.uint8).pin_memory()
+    rates = {}
+    for name, (dst, src) in {"h2d": (g, h), "d2h": (h, g)}.items():
+        dst.copy_(src)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(3):
+            dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize()
+        rates[name] = 3 * (1 << 30) / (time.perf_counter() - t1)
+    del g, h
+    n = done[0]
+    in_b = int(w.topics.offs[nb * per]) + 8 * n
+    out_b = 8 * done[1] + 16 * n
+    bound_s = max(in_b / rates["h2d"], out_b / rates["d2h"])
+    return {"value": n / dt, "unit": "topics/s", "topics_per_call": per, "calls": nb, "threads": args.host_threads,
+            "ms_per_call": dt * 1e3 * args.host_threads / nb, "deliveries_per_s": done[1] / dt,
+            "h2d_GBps": rates["h2d"] / 1e9, "d2h_GBps": rates["d2h"] / 1e9,
+            "pcie_bound_topics_per_s": n / bound_s, "frac_of_pcie_bound": (n / dt) / (n / bound_s),
+            "note": "pinned topics in -> match -> dense CSR into pinned result blocks; "
+                    "pcie_bound = max(H2D bytes / H2D rate, D2H bytes / D2H rate)"}
+
+
+def latency(idx, w, args):
+    """Per-publish latency of the reference's call shape: one Subscribers(topic)
+    per call (server.go:776) through mqm_subscribers, host in / host out."""
+    import ctypes as C
+
+    from maxmq_amd import capi
+
+    L = capi.lib()
+    n = min(args.latency_topics, len(w.topics))
+    topics = [bytes(w.topics.data[w.topics.offs[i]:w.topics.offs[i + 1]]) for i in range(n)]
+    ts = []
+    for i, t in enumerate(topics + topics[:50]):
+        res = C.c_void_p()
+        t0 = time.perf_counter()
+        capi.check("mqm_subscribers", L.mqm_subscribers(idx._h, t, len(t), C.byref(res)))
+        dt = time.perf_counter() - t0
+        L.mqm_result_free(res)
+        if i >= 50:
+            ts.append(dt)
+    ts = np.array(ts) * 1e6
+    return {"unit": "us", "calls": len(ts), "p50": float(np.median(ts)), "p90": float(np.percentile(ts, 90)),
+            "p99": float(np.percentile(ts, 99)), "mean": float(ts.mean())}
 
 
 def run_sweep(args, idx, step, dev, rank):
@@ -513,7 +661,7 @@ def cpu_reverse(w, refs, args):
     """oracle/mochi_ref.c scan_messages over a time-bounded sample of the filters."""
     from oracle.binding import OracleIndex
 
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    threads = cpu_threads(args)
     t0 = time.time()
     ora = OracleIndex()
     ora.subscribe_workload(w)
@@ -533,7 +681,7 @@ def cpu_reverse(w, refs, args):
         done = hi
         chunk = min(chunk * 2, 100000)
     ora.close()
-    return {"value": done / busy, "unit": "filters/s", "cores": threads, "kind": "port",
+    return {"value": done / busy, "unit": "filters/s", "cores": threads, "kind": "port", "host": host_info(),
             "sample": f"first {done} filters ({busy:.1f}s of matching, index build {build_s:.0f}s excluded); "
                       f"C restatement of mochi v2.2.12 TopicsIndex.Messages (oracle/mochi_ref.c); Go toolchain "
                       f"unavailable",
@@ -559,7 +707,7 @@ def cpu_baseline(w, args):
     from the front) on this host's cores; index build excluded."""
     from oracle.binding import OracleIndex
 
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    threads = cpu_threads(args)
     t0 = time.time()
     ora = OracleIndex()
     ora.subscribe_workload(w)
@@ -591,12 +739,6 @@ def cpu_baseline(w, args):
         st_busy += time.perf_counter() - t1
         st_done = hi
     ora.close()
-    model = ""
-    try:
-        with open("/proc/cpuinfo") as fh:
-            model = next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")), "")
-    except OSError:
-        pass
     cpu = {
         "value": done / busy,
         "unit": "topics/s",
@@ -607,7 +749,7 @@ def cpu_baseline(w, args):
                   f"unavailable",
         "deliveries_per_s": tot["deliveries"] / busy,
         "single_thread_value": st_done / st_busy if st_busy > 0 else None,
-        "host": {"cpus_visible": os.cpu_count(), "model": model},
+        "host": host_info(),
     }
     return cpu, tot
 

@@ -123,6 +123,10 @@ typedef struct {
   uint32_t n_big;                 /* topics deduplicated by the workgroup tier  */
   uint32_t fallback_why[5];       /* why topics took the unbounded path: frontier,
                                      hits, cached levels, shared hits, raw entries */
+  uint32_t n_small;               /* topics emitted by the 16-lane small-class kernel */
+  uint32_t n_bigc;                /* big-class topics (emitted as chunk items)   */
+  uint64_t n_items;               /* big-class chunk items                        */
+  uint32_t n_tier2, n_tier3;      /* topics the workgroup merge passed to its 2nd / 3rd tier */
 } mqm_device_result;
 
 /* ---- lifecycle: NewTopicsIndex (topics.go:291-299) ---------------------- */

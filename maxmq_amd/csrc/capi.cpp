@@ -581,6 +581,11 @@ int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t 
     out->n_fallback = mo.n_fallback;
     out->n_big = mo.n_big;
     for (int i = 0; i < 5; i++) out->fallback_why[i] = c.ws.why[i];
+    out->n_small = mo.n_small;
+    out->n_bigc = mo.n_bigc;
+    out->n_items = mo.n_items;
+    out->n_tier2 = mo.n_tier2;
+    out->n_tier3 = mo.n_tier3;
     return MQM_OK;
   });
 }

@@ -92,7 +92,7 @@ static void mark_multi(const Store &st, const std::vector<uint32_t> &order, Host
         bool multi = hi - lo > kMaxPairwise ||
                      (nodes[nx].key == hash_tok && px != st.root() && !wild(nodes[px].key));
         for (uint32_t y = lo; !multi && y < hi; y++) multi = y != x && compatible(nx, sub_node[by_client[y]]);
-        if (multi) hs.subs[sx].meta |= kMetaMulti;
+        if (multi) hs.subs[sx].word |= kMetaMulti;
         else solo[ch]++;
       }
     }
@@ -358,7 +358,7 @@ int flatten(const Store &st, HostSnapshot *out) {
       si.clear();
       for (int pass = 0; pass < 2; pass++)
         for (uint32_t j = off; j < off + cnt; j++)
-          if (((hs.subs[j].meta & kMetaMulti) != 0) == (pass == 1)) {
+          if (((hs.subs[j].word & kMetaMulti) != 0) == (pass == 1)) {
             se.push_back(hs.subs[j]);
             si.push_back(hs.sub_info[j]);
             own_multi[i] += pass;
@@ -380,6 +380,14 @@ int flatten(const Store &st, HostSnapshot *out) {
     }
   }
 
+  // the device word (snapshot.h): the entry's own delivery, ident flag on top
+  parallel_for(64, [&](uint32_t c) {
+    const uint64_t n = hs.subs.size(), lo = n * c / 64, hi = n * (c + 1) / 64;
+    for (uint64_t j = lo; j < hi; j++) {
+      const uint32_t m = hs.subs[j].word;
+      hs.subs[j].word = (uint32_t)j | ((m & 3u) << 28) | (((m >> 2) & 1u) << 30) | ((m & kMetaIdent) ? kWordIdent : 0u);
+    }
+  });
   pt.mark("ranges");
   // 3. literal edges -> open-addressed table of 128-B buckets, linear probing
   //    at load factor `load` (default 0.2; env MQM_EDGE_LOAD in (0, 0.9]): a probe

@@ -15,7 +15,7 @@ struct Workspace {
   enum Slot {
     kSCount, kHCount, kDCount, kDStart, kHStart, kCls, kDfsList, kRecs, kCounters, kDOut, kHOut,
     kDense, kDenseShared, kDenseOffs, kDenseHOffs, kScanTmp, kRawCnt, kTabOff, kTabSize, kTable,
-    kInBytes, kInOffs, kOvfList, kOvfList2, kListS, kListB, kICount, kIStart, kIOut,
+    kInBytes, kInOffs, kOvfList, kOvfList2, kListS, kListB, kICount, kIStart, kIOut, kNChunk, kCStart, kItems,
     // reverse match (retained.hip)
     kROffs, kRNLev, kRWild, kRLOff, kRFCount, kRFCur, kRLevels, kRNCount, kRNOff, kRItemF0, kRItemN0, kRItemF1,
     kRItemN1, kRChild, kRECount, kREOff, kREmit, kRPos, kRChunks, kRCOff, kROut, kRInBytes, kRInOffs, kNumSlots
@@ -34,7 +34,8 @@ struct Workspace {
   uint32_t why[5] = {0, 0, 0, 0, 0};
   // the last match_device call (identifiers_device works on its records)
   bool last_valid = false;
-  uint32_t last_n = 0, last_n_dfs = 0;
+  uint32_t last_n = 0, last_n_dfs = 0, last_small = 0, last_bigc = 0;
+  uint64_t last_items = 0;
   const uint8_t *last_bytes = nullptr;
   const uint64_t *last_offs = nullptr;
 
@@ -80,6 +81,9 @@ struct MatchOutput {
   const uint32_t *shared = nullptr;
   uint32_t n_fallback = 0;  // topics on the unbounded DFS path
   uint32_t n_big = 0;       // topics whose multi entries the workgroup tier merged
+  uint32_t n_tier2 = 0, n_tier3 = 0;  // ... of those, passed on to its second / third tier
+  uint32_t n_small = 0, n_bigc = 0;   // topics emitted by k_emit_small / by k_copy items
+  uint64_t n_items = 0;               // k_copy items (kChunk solo entries each at most)
 };
 
 // Runs walk -> scan -> dedupe (small / big / DFS) on `st`; returns 0 or a

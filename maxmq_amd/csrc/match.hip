@@ -44,11 +44,6 @@
 #include "device.h"
 #include "match.h"
 
-// MQM_FIND_STEP: hits per batch of LDS reads in find_hits (4 / 8 spill and
-// lose occupancy: slower on C3, profiles/r01/c3_v17_find_step_sweep.log)
-#ifndef MQM_FIND_STEP
-#define MQM_FIND_STEP 1
-#endif
 // MQM_REC16_WORDS: record words k_emit<16> prefetches per topic (64 or 128)
 #ifndef MQM_REC16_WORDS
 #define MQM_REC16_WORDS 64
@@ -82,10 +77,9 @@ constexpr int kRecSh = 4 + kRecHit * kHCap;          // 196
 constexpr int kRecStride = kRecSh + 2 * kShCap;       // 228 words (max)
 constexpr int kRecStrideAlloc = 228;                  // 16-B aligned per topic
 constexpr uint32_t kSMax = 16384;        // raw entries per topic on the bounded path
-constexpr uint32_t kDPad = 1;           // segment start alignment in entries (16 = 128-B lines: no gain on C3)
 constexpr int kEmitU = 4;                // solo entries in flight per lane
 constexpr int kEmitWaves = 4;
-constexpr int kSmallLanes = 16;          // k_emit<16>: lanes per topic of the small class
+constexpr int kSmallLanes = 16;          // k_emit_small: lanes per topic of the small class
 constexpr uint32_t kSmallSolo = 256;     // small class: at most this many solo entries
 constexpr int kSmallSlots = 256;         // k_emit merge table slots (per wave)
 constexpr int kSmallMulti = 192;         // multi entries it holds (load <= 0.75)
@@ -171,54 +165,35 @@ __device__ __forceinline__ uint64_t pack_delivery(uint32_t client, uint32_t sid,
   return (uint64_t)client | ((uint64_t)(sid | (qos << 28) | (nl << 30)) << 32);
 }
 
-// QoS one-hot (bits 0..2) | NoLocal (bit 3): OR-merged, max QoS = top set bit
-__device__ __forceinline__ uint32_t qos_bits(uint32_t meta) { return (1u << (meta & 3)) | (((meta >> 2) & 1) << 3); }
-
-// the hit h holding entry x of a prefix field (kFieldSpre / kFieldMpre): the
-// largest h with field(h) <= x.  Hits with none of those entries tie with
-// their successor, so the largest such h is the one that holds x.
-enum : int { kFieldOff = 0, kFieldSpre = 1, kFieldMpre = 2, kFieldRank = 3 };
-constexpr int kFindStep = MQM_FIND_STEP;
-static_assert(4 + kRecHit * (kHCap - 1 + kFindStep - 1) + kFieldRank < kRecStrideAlloc, "find_hits reads stay in the record");
-// Counting search: every lane of a group reads the same record word per hit
-// (an LDS broadcast) and the reads are independent, so the loop pipelines —
-// a binary search's dependent reads compiled to a branch and a full LDS wait
-// per step.  Hits are few (<= kHCap).
-template <int kField, int kN>
-__device__ __forceinline__ void find_hits(const uint32_t *rec, uint32_t nh, const uint32_t (&x)[kN],
-                                          uint32_t (&h)[kN]) {
-#pragma unroll
-  for (int u = 0; u < kN; u++) h[u] = 0;
-  // 8 hits per step: the 8 LDS reads are issued together and waited for once
-  // (one read per step serialised the loop on LDS latency); reads past nh
-  // stay inside the record (kFindStep) and count for nothing
-  if constexpr (kFindStep == 1) {
-    for (uint32_t j = 1; j < nh; j++) {
-      const uint32_t v = rec[4 + kRecHit * j + kField];
-#pragma unroll
-      for (int u = 0; u < kN; u++) h[u] += v <= x[u] ? 1u : 0u;
-    }
-    return;
-  }
-  for (uint32_t j = 1; j < nh; j += kFindStep) {
-    uint32_t v[kFindStep];
-#pragma unroll
-    for (int k = 0; k < kFindStep; k++) v[k] = rec[4 + kRecHit * (j + k) + kField];
-#pragma unroll
-    for (int k = 0; k < kFindStep; k++) {
-      const bool in = j + k < nh;
-#pragma unroll
-      for (int u = 0; u < kN; u++) h[u] += (in && v[k] <= x[u]) ? 1u : 0u;
-    }
-  }
+// QoS one-hot (bits 0..2) | NoLocal (bit 3) of a SubEnt word: OR-merged, max
+// QoS = top set bit
+__device__ __forceinline__ uint32_t qos_bits(uint32_t word) {
+  return (1u << ((word >> 28) & 3)) | (((word >> 30) & 1) << 3);
 }
 
+// a SubEnt as its own delivery (snapshot.h)
+__device__ __forceinline__ uint64_t solo_delivery(SubEnt e) {
+  return ((uint64_t)(e.word & 0x7FFFFFFFu) << 32) | e.client;
+}
+
+// the hit h holding entry x of a prefix field (kFieldSpre / kFieldMpre): the
+// largest h < nh with field(h) <= x (field(0) = 0).  Hits with none of those
+// entries tie with their successor, so the largest such h is the one that
+// holds x.  Branch-free binary search over the prefixes in LDS: 6 dependent
+// reads for nh <= 64 (round 1 counted over every hit per entry: ~nh reads and
+// 2 nh VALU ops per entry, which made emission issue-bound on big topics).
+enum : int { kFieldOff = 0, kFieldSpre = 1, kFieldMpre = 2, kFieldRank = 3 };
+static_assert(kHCap <= 64, "hit_of searches 6 levels");
 template <int kField>
-__device__ __forceinline__ uint32_t find_hit(const uint32_t *rec, uint32_t nh, uint32_t x) {
-  const uint32_t xs[1] = {x};
-  uint32_t hs[1];
-  find_hits<kField, 1>(rec, nh, xs, hs);
-  return hs[0];
+__device__ __forceinline__ uint32_t hit_of(const uint32_t *rec, uint32_t nh, uint32_t x) {
+  uint32_t h = 0;
+#pragma unroll
+  for (uint32_t step = 32; step > 0; step >>= 1) {
+    const uint32_t c = h + step;
+    const uint32_t v = rec[4 + kRecHit * (c < nh ? c : 0) + kField];
+    h = (c < nh && v <= x) ? c : h;
+  }
+  return h;
 }
 
 __device__ __forceinline__ uint32_t rec_at(const uint32_t *rec, uint32_t h, int field) {
@@ -228,14 +203,14 @@ __device__ __forceinline__ uint32_t rec_at(const uint32_t *rec, uint32_t h, int 
 // per-topic merge table in LDS (linear probing, key = client + 1):
 // QoS one-hot | NoLocal OR-folded, lowest hit rank kept (first-merged)
 __device__ __forceinline__ void table_insert(uint32_t *tkey, uint32_t *tbits, uint32_t *tmin, uint32_t mask,
-                                             uint32_t lg, uint32_t client, uint32_t meta, uint32_t hit) {
+                                             uint32_t lg, uint32_t client, uint32_t word, uint32_t hit) {
   uint32_t sl = table_slot(client, lg);
   for (;;) {
     const uint32_t prev = atomicCAS(&tkey[sl], 0u, client + 1);
     if (prev == 0 || prev == client + 1) break;
     sl = (sl + 1) & mask;
   }
-  atomicOr(&tbits[sl], qos_bits(meta));
+  atomicOr(&tbits[sl], qos_bits(word));
   atomicMin(&tmin[sl], hit);
 }
 
@@ -517,87 +492,125 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
 }
 
 // ---------------------------------------------------------------------------
-// k_emit: a wavefront per bounded topic.  The next topic's header (class,
-// counts, segment starts, the first 64 record words) is in flight while the
-// current one is processed.
-//   solo entries (kMetaMulti clear) are their clients' merged deliveries:
-//     entry q of the topic's solo sequence goes to out[db + q] — no table, no
-//     compaction, kEmitU entries per lane in flight;
-//   multi entries (at most kSmallMulti) are merged in a per-wave LDS table
-//     keyed by client: atomicOr folds QoS (one-hot) and NoLocal, atomicMin
-//     keeps the lowest hit rank, an entry is its client's winner iff its hit
-//     has that rank — Subscription.Merge (packets.go:250-270) with the
-//     first-merged subscription's fields — and winners are compacted with a
-//     ballot after the solo part.  More multi entries go to k_multi.
-// Also writes every bounded topic's shared candidates.
+// Emission.  A topic's deliveries are written at dstart[t] (the exclusive scan
+// of its raw-entry count S, an upper bound): first its solo entries, each its
+// client's merged delivery as is (delivery q = solo entry q), then the
+// winners of the merge of its multi entries, compacted.  dcount[t] = Ss +
+// winners.  Three kernels by size:
+//   k_emit_small  16 lanes per topic (4 topics per wavefront) for topics with
+//                 Ss <= kSmallSolo and Ms <= 3 * 16: solo copy + a 64-slot
+//                 LDS merge table; also every topic with shared candidates
+//                 only.
+//   k_copy        the big class, cut into items of kChunk solo entries (a
+//                 wavefront per item, static striding over equal-sized
+//                 items: no Zipf hub topic holds a wave for long).  Item 0 of
+//                 a topic also writes its shared candidates and merges up to
+//                 kSmallMulti multi entries in a 256-slot table; more go to
+//                 k_multi.
+//   k_multi       a 256-thread workgroup per topic with more multi entries.
+// The merge: an LDS hash table keyed by client — atomicOr folds QoS (one-hot)
+// and NoLocal, atomicMin keeps the lowest hit rank; an entry is its client's
+// winner iff its hit has that rank: exactly Subscription.Merge
+// (packets.go:250-270) with the first-merged subscription's fields.
 // ---------------------------------------------------------------------------
+constexpr uint32_t kChunk = 2048;  // solo entries per k_copy item
+
 // multi entry q of a topic: subs index and hit
 __device__ __forceinline__ uint32_t multi_sid(const uint32_t *rec, uint32_t nh, uint32_t Ss, uint32_t q,
                                               uint32_t *hit) {
-  const uint32_t h = find_hit<kFieldMpre>(rec, nh, q);
+  const uint32_t h = hit_of<kFieldMpre>(rec, nh, q);
   const uint32_t solo_h = (h + 1 < nh ? rec_at(rec, h + 1, kFieldSpre) : Ss) - rec_at(rec, h, kFieldSpre);
   *hit = h;
   return rec_at(rec, h, kFieldOff) + solo_h + (q - rec_at(rec, h, kFieldMpre));
 }
 
-// kE lanes per topic: 16 for the small class (4 topics per wavefront), 64 for
-// the big one (a wavefront per topic; more than kSmallMulti multi entries go on
-// to k_multi).
-template <int kE>
-struct EmitCfg {
-  static constexpr int kGroups = kWave / kE;
-  static constexpr uint32_t kMulti = kE == kWave ? kSmallMulti : 3 * kE;  // multi entries merged here
-  static constexpr uint32_t kSlots = kE == kWave ? kSmallSlots : 64;
-  static constexpr int kMPer = kMulti / kE;
-  // record words each lane prefetches one topic ahead: the first 64 for the
-  // big class, MQM_REC16_WORDS for the small one; the rest is loaded when the
-  // header says how many hits there are.  (The whole record for the big class,
-  // one 16-B load per lane, measured no faster and spills at occupancy 5.)
-  static constexpr int kRecPer = kE == kWave ? 1 : MQM_REC16_WORDS / kE;
-  static constexpr int kPre = kRecPer * kE;
-  static_assert((kRecPer == 1 || kRecPer % 4 == 0) && kPre <= kRecStrideAlloc, "record prefetch");
-};
+// solo entry q of a topic (hit located by binary search)
+__device__ __forceinline__ uint32_t solo_sid(const uint32_t *rec, uint32_t nh, uint32_t q) {
+  const uint32_t h = hit_of<kFieldSpre>(rec, nh, q);
+  return rec_at(rec, h, kFieldOff) + (q - rec_at(rec, h, kFieldSpre));
+}
 
-template <int kE>
-struct alignas(16) EmitLds {
-  uint32_t rec[kRecStrideAlloc];
-  uint32_t tkey[EmitCfg<kE>::kSlots];
-  uint32_t tbits[EmitCfg<kE>::kSlots];
-  uint32_t tmin[EmitCfg<kE>::kSlots];
-};
+__device__ __forceinline__ SubEnt load_sub(const DeviceSnapshot &s, uint32_t sid) {
+  const uint2 v = *reinterpret_cast<const uint2 *>(s.subs + sid);
+  return SubEnt{v.x, v.y};
+}
 
-template <int kE, int kOcc, int kU = kEmitU>
-__global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_eu(kOcc))) void k_emit(DeviceSnapshot s, Outputs o, const uint32_t *__restrict__ list,
-                                                            const unsigned int *__restrict__ count) {
-  using Cfg = EmitCfg<kE>;
-  constexpr int kGroups = Cfg::kGroups, kMPer = Cfg::kMPer, kRecPer = Cfg::kRecPer;
+// Merge kMPer multi entries per lane of a kE-lane group in a table of
+// (1 << lg) <= kSlots slots and write the winners at out[db + D ..); returns
+// the new D (group-uniform).  Entries past M are inert.
+template <int kE, int kMPer>
+__device__ __forceinline__ uint32_t merge_multi(uint32_t *tkey, uint32_t *tbits, uint32_t *tmin, uint32_t kSlots,
+                                                const uint32_t (&mcl)[kMPer], const uint32_t (&mw)[kMPer],
+                                                const uint32_t (&mrk)[kMPer], uint32_t M, int gl, int gbase,
+                                                uint64_t *out, uint64_t db, uint32_t D) {
   constexpr uint64_t kGMask = kE == 64 ? ~0ull : (1ull << kE) - 1ull;
-  __shared__ EmitLds<kE> lds_all[kEmitWaves * kGroups];
+  const uint64_t glt = (1ull << gl) - 1ull;
+  uint32_t lg = 6;
+  while ((1u << lg) < 2 * M && (1u << lg) < kSlots) lg++;
+  const uint32_t mask = (1u << lg) - 1;
+  for (uint32_t j = gl; j <= mask; j += kE) {
+    tkey[j] = 0;
+    tbits[j] = 0;
+    tmin[j] = 0xFFFFFFFFu;
+  }
+  wave_lds_sync();
+#pragma unroll
+  for (int k = 0; k < kMPer; k++)
+    if (gl + k * kE < M) table_insert(tkey, tbits, tmin, mask, lg, mcl[k], mw[k], mrk[k]);
+  wave_lds_sync();
+#pragma unroll
+  for (int k = 0; k < kMPer; k++) {
+    bool win = false;
+    uint64_t ent = 0;
+    if (gl + k * kE < M) {
+      const uint32_t sl = table_find(tkey, mask, lg, mcl[k]);
+      win = tmin[sl] == mrk[k];
+      const uint32_t v = tbits[sl];
+      ent = pack_delivery(mcl[k], mw[k] & kWordSidMask, 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
+    }
+    const uint64_t m = (__ballot(win) >> gbase) & kGMask;
+    if (win) put_out(&out[db + D + __popcll(m & glt)], ent);
+    D += __popcll(m);
+  }
+  return D;
+}
+
+// ---- k_emit_small -------------------------------------------------------------
+constexpr int kSE = 16;                          // lanes per topic
+constexpr int kSGroups = kWave / kSE;
+constexpr uint32_t kSMulti = 3 * kSE;            // multi entries merged here
+constexpr int kSRecPer = MQM_REC16_WORDS / kSE;  // record words prefetched per lane
+static_assert(kSRecPer % 4 == 0 && kSRecPer * kSE <= kRecStrideAlloc, "record prefetch");
+
+struct alignas(16) SmallLds {
+  uint32_t rec[kRecStrideAlloc];
+  uint32_t tkey[64], tbits[64], tmin[64];
+};
+
+template <int kOcc, int kU>
+__global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_eu(kOcc))) void k_emit_small(
+    DeviceSnapshot s, Outputs o, const uint32_t *__restrict__ list, const unsigned int *__restrict__ count) {
+  constexpr int kMPer = kSMulti / kSE, kRecPer = kSRecPer;
+  __shared__ SmallLds lds_all[kEmitWaves * kSGroups];
   const int lane = threadIdx.x & (kWave - 1);
-  const int g = lane / kE, gl = lane % kE, gbase = g * kE;
-  EmitLds<kE> &L = lds_all[(threadIdx.x / kWave) * kGroups + g];
-  const uint64_t glt = (1ull << gl) - 1ull;  // group lanes below gl (after >> gbase)
-  const uint32_t ngroups = gridDim.x * kEmitWaves * kGroups;
+  const int g = lane / kSE, gl = lane % kSE, gbase = g * kSE;
+  SmallLds &L = lds_all[(threadIdx.x / kWave) * kSGroups + g];
+  const uint32_t ngroups = gridDim.x * kEmitWaves * kSGroups;
   const uint32_t nl = *count;
-  uint32_t i = (blockIdx.x * kEmitWaves + threadIdx.x / kWave) * kGroups + g;
+  uint32_t i = (blockIdx.x * kEmitWaves + threadIdx.x / kWave) * kSGroups + g;
   // list entries two topics ahead; the next topic's header and its record's
-  // first Cfg::kPre words one topic ahead
+  // first kRecPer * kSE words one topic ahead
   uint32_t n_H = 0, n_rw[kRecPer];
   uint64_t n_db = 0, n_hb = 0;
   auto fetch = [&](uint32_t u) {
     n_H = o.hcount[u];
     n_db = o.dstart[u];
     n_hb = o.hstart[u];
-    const uint32_t w0 = gl * kRecPer + kRecPer <= kRecStrideAlloc ? gl * kRecPer : 0;
-    const uint32_t *r = o.recs + (uint64_t)u * kRecStrideAlloc + w0;
-    if constexpr (kRecPer == 1) {
-      n_rw[0] = r[0];
-    } else {
+    const uint32_t *r = o.recs + (uint64_t)u * kRecStrideAlloc + gl * kRecPer;
 #pragma unroll
-      for (int v = 0; v < kRecPer / 4; v++) {
-        const uint4 x = *reinterpret_cast<const uint4 *>(r + 4 * v);
-        n_rw[4 * v] = x.x, n_rw[4 * v + 1] = x.y, n_rw[4 * v + 2] = x.z, n_rw[4 * v + 3] = x.w;
-      }
+    for (int v = 0; v < kRecPer / 4; v++) {
+      const uint4 x = *reinterpret_cast<const uint4 *>(r + 4 * v);
+      n_rw[4 * v] = x.x, n_rw[4 * v + 1] = x.y, n_rw[4 * v + 2] = x.z, n_rw[4 * v + 3] = x.w;
     }
   };
   uint32_t t_nxt = i < nl ? list[i] : 0;
@@ -605,137 +618,217 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
   if (i < nl) fetch(t_nxt);
   for (; i < nl; i += ngroups) {
     const uint32_t t = t_nxt, H = n_H;
-    uint32_t rw[kRecPer];
-#pragma unroll
-    for (int j = 0; j < kRecPer; j++) rw[j] = n_rw[j];
     const uint64_t db = n_db, hb = n_hb;
+#pragma unroll
+    for (int j = 0; j < kRecPer; j++) L.rec[gl * kRecPer + j] = n_rw[j];
     t_nxt = t_nn;
     if (i + ngroups < nl) fetch(t_nxt);
     t_nn = i + 2 * ngroups < nl ? list[i + 2 * ngroups] : 0;
-#pragma unroll
-    for (int j = 0; j < kRecPer; j++)
-      if (gl * kRecPer + kRecPer <= kRecStrideAlloc) L.rec[gl * kRecPer + j] = rw[j];
     wave_lds_sync();
     const uint32_t w0 = L.rec[0], Ss = L.rec[1], M = L.rec[2];
     const uint32_t nh = w0 & 0xFFu, nsh = w0 >> 8;
     const uint32_t *grec = o.recs + (uint64_t)t * kRecStrideAlloc;
-    if constexpr (kE == kWave) {  // the hits past the first 64 words (a vector
-      // tail here costs the big class its last registers: spills at occupancy 5)
-      for (uint32_t j = kWave + gl; j < 4 + kRecHit * nh; j += kE) L.rec[j] = grec[j];
-    } else {  // the hits past the prefetched words: one round trip of 16-B
-      // loads (lanes past the end re-read word kPre)
-      constexpr int kPre = Cfg::kPre, kT = (kRecStride - kPre + 4 * kE - 1) / (4 * kE);
+    {  // the hits past the prefetched words: one round trip of 16-B loads
+      constexpr int kPre = kRecPer * kSE, kT = (kRecStride - kPre + 4 * kSE - 1) / (4 * kSE);
       const uint32_t nw = 4 + kRecHit * nh;
       uint4 tv[kT];
 #pragma unroll
       for (int k = 0; k < kT; k++) {
-        const uint32_t w = kPre + 4 * (k * kE + gl);
+        const uint32_t w = kPre + 4 * (k * kSE + gl);
         tv[k] = *reinterpret_cast<const uint4 *>(grec + (w < nw ? w : kPre));
       }
 #pragma unroll
       for (int k = 0; k < kT; k++) {
-        const uint32_t w = kPre + 4 * (k * kE + gl);
+        const uint32_t w = kPre + 4 * (k * kSE + gl);
         if (w < nw) *reinterpret_cast<uint4 *>(&L.rec[w]) = tv[k];
       }
     }
     wave_lds_sync();
-    rec_prefix<kE>(L.rec, nh, gl);
+    rec_prefix<kSE>(L.rec, nh, gl);
     wave_lds_sync();
     if (H) {  // shared candidates (gatherSharedSubscriptions, topics.go:541-555)
       uint32_t w = 0;
       for (uint32_t j = 0; j < nsh; j++) {
         const uint32_t so = grec[kRecSh + 2 * j], sc = grec[kRecSh + 1 + 2 * j];
-        for (uint32_t j = gl; j < sc; j += kE) put_out(&o.hout[hb + w + j], so + j);
+        for (uint32_t j2 = gl; j2 < sc; j2 += kSE) put_out(&o.hout[hb + w + j2], so + j2);
         w += sc;
       }
     }
-    // Loads before stores: a wait for a load also waits for every older
-    // store of the wave (one in-order vmcnt), so each chunk's loads are issued
-    // before the previous chunk's stores, and the multi entries' loads before
-    // any store of the topic.  Loads are unconditional (entry 0 stands in
-    // past the end): a branch around a load makes the compiler wait for it.
-    const bool merge_here = M > 0 && M <= Cfg::kMulti;
-    uint32_t mcl[kMPer], msid[kMPer], mrk[kMPer], mmeta[kMPer];
-    if (merge_here) {
+    // loads before stores (one in-order vmcnt per wave): the multi entries and
+    // the first solo chunk are loaded before any store of the topic
+    uint32_t mcl[kMPer], mw[kMPer], mrk[kMPer];
+    if (M) {
 #pragma unroll
       for (int k = 0; k < kMPer; k++) {
-        const uint32_t q = gl + k * kE;
+        const uint32_t q = gl + k * kSE;
         uint32_t h;
-        msid[k] = multi_sid(L.rec, nh, Ss, q < M ? q : 0, &h);
+        const uint32_t sid = multi_sid(L.rec, nh, Ss, q < M ? q : 0, &h);
         mrk[k] = rec_at(L.rec, h, kFieldRank);
-        const SubEnt e = s.subs[msid[k]];
+        const SubEnt e = load_sub(s, sid);
         mcl[k] = e.client;
-        mmeta[k] = e.meta;
+        mw[k] = e.word;
       }
     }
-    // solo entries: delivery q of the topic is solo entry q
-    uint32_t cl[kU], sid[kU], meta[kU];
-    auto load_solo = [&](uint32_t base, uint32_t *c_, uint32_t *s_, uint32_t *m_) {
-      uint32_t q[kU], h[kU];
+    uint64_t v[kU];
+    auto load_solo = [&](uint32_t base, uint64_t (&dst)[kU]) {
 #pragma unroll
       for (int u = 0; u < kU; u++) {  // unconditional loads (entry 0 stands in past Ss)
-        const uint32_t q0 = base + u * kE + gl;
-        q[u] = q0 < Ss ? q0 : 0;
-      }
-      find_hits<kFieldSpre, kU>(L.rec, nh, q, h);
-#pragma unroll
-      for (int u = 0; u < kU; u++) {
-        s_[u] = rec_at(L.rec, h[u], kFieldOff) + (q[u] - rec_at(L.rec, h[u], kFieldSpre));
-        const SubEnt e = s.subs[s_[u]];
-        c_[u] = e.client;
-        m_[u] = e.meta;
+        const uint32_t q0 = base + u * kSE + gl;
+        const SubEnt e = load_sub(s, solo_sid(L.rec, nh, q0 < Ss ? q0 : 0));
+        dst[u] = solo_delivery(e);
       }
     };
-    if (Ss) load_solo(0, cl, sid, meta);
-    for (uint32_t base = 0; base < Ss; base += kE * kU) {
-      uint32_t ncl[kU], nsid[kU], nmeta[kU];
-      if (base + kE * kU < Ss) load_solo(base + kE * kU, ncl, nsid, nmeta);
+    if (Ss) load_solo(0, v);
+    for (uint32_t base = 0; base < Ss; base += kSE * kU) {
+      uint64_t nv[kU];
+      if (base + kSE * kU < Ss) load_solo(base + kSE * kU, nv);
 #pragma unroll
       for (int u = 0; u < kU; u++) {
-        const uint32_t q = base + u * kE + gl;
-        if (q < Ss)
-          put_out(&o.dout[db + q], pack_delivery(cl[u], sid[u], meta[u] & 3u, (meta[u] >> 2) & 1u));
-        cl[u] = ncl[u];
-        sid[u] = nsid[u];
-        meta[u] = nmeta[u];
+        const uint32_t q = base + u * kSE + gl;
+        if (q < Ss) put_out(&o.dout[db + q], v[u]);
+        v[u] = nv[u];
       }
     }
     uint32_t D = Ss;
-    if (M > Cfg::kMulti) {  // the workgroup tier merges them and writes dcount (big class only)
-      if (gl == 0) o.multi_list[atomicAdd(&o.ctr->n_multi, 1u)] = t;
-      wave_lds_sync();
-      continue;
+    if (M) D = merge_multi<kSE, kMPer>(L.tkey, L.tbits, L.tmin, 64, mcl, mw, mrk, M, gl, gbase, o.dout, db, D);
+    if (gl == 0) o.dcount[t] = D;
+    wave_lds_sync();
+  }
+}
+
+// ---- k_copy: big-class items -------------------------------------------------
+struct alignas(16) CopyLds {
+  uint32_t rec[kRecStrideAlloc];
+  uint32_t tkey[kSmallSlots], tbits[kSmallSlots], tmin[kSmallSlots];
+};
+
+// chunk items per big-class topic: ceil(Ss / kChunk), at least 1 (item 0 also
+// writes shared candidates, merges or hands on the multi entries, and dcount);
+// zeros past the list so one scan over n covers it
+__global__ __launch_bounds__(256) void k_chunks(Outputs o, const uint32_t *__restrict__ list,
+                                                const unsigned int *__restrict__ count, uint32_t n,
+                                                uint32_t *__restrict__ nchunk) {
+  const uint32_t nb = *count;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    uint32_t c = 0;
+    if (i < nb) {
+      const uint32_t Ss = o.recs[(uint64_t)list[i] * kRecStrideAlloc + 1];
+      c = Ss > kChunk ? (Ss + kChunk - 1) / kChunk : 1u;
     }
-    if (merge_here) {
-      uint32_t lg = 6;
-      while ((1u << lg) < 2 * M && (1u << lg) < Cfg::kSlots) lg++;
-      const uint32_t mask = (1u << lg) - 1;
-      for (uint32_t j = gl; j <= mask; j += kE) {
-        L.tkey[j] = 0;
-        L.tbits[j] = 0;
-        L.tmin[j] = 0xFFFFFFFFu;
+    nchunk[i] = c;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_items(const uint32_t *__restrict__ list, const unsigned int *__restrict__ count,
+                                               const uint64_t *__restrict__ cstart, uint2 *__restrict__ items) {
+  const uint32_t nb = *count;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += gridDim.x * blockDim.x) {
+    const uint64_t a = cstart[i], b = cstart[i + 1];
+    const uint32_t t = list[i];
+    for (uint64_t k = a; k < b; k++) items[k] = make_uint2(t, (uint32_t)(k - a));
+  }
+}
+
+template <int kOcc, int kU>
+__global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_eu(kOcc))) void k_copy(
+    DeviceSnapshot s, Outputs o, const uint2 *__restrict__ items, uint64_t n_items) {
+  constexpr int kMPer = kSmallMulti / kWave;
+  __shared__ CopyLds lds_all[kEmitWaves];
+  const int lane = threadIdx.x & (kWave - 1);
+  CopyLds &L = lds_all[threadIdx.x / kWave];
+  const uint64_t nw = (uint64_t)gridDim.x * kEmitWaves;
+  uint64_t i = (uint64_t)blockIdx.x * kEmitWaves + threadIdx.x / kWave;
+  // the next item's header and first 64 record words one item ahead
+  uint2 n_it = make_uint2(0, 0);
+  uint32_t n_H = 0, n_rw = 0;
+  uint64_t n_db = 0, n_hb = 0;
+  auto fetch = [&](uint64_t k) {
+    n_it = items[k];
+    n_H = o.hcount[n_it.x];
+    n_db = o.dstart[n_it.x];
+    n_hb = o.hstart[n_it.x];
+    n_rw = o.recs[(uint64_t)n_it.x * kRecStrideAlloc + lane];
+  };
+  if (i < n_items) fetch(i);
+  for (; i < n_items; i += nw) {
+    const uint32_t t = n_it.x, j = n_it.y, H = n_H;
+    const uint64_t db = n_db, hb = n_hb;
+    L.rec[lane] = n_rw;
+    if (i + nw < n_items) fetch(i + nw);
+    wave_lds_sync();
+    const uint32_t w0 = L.rec[0], Ss = L.rec[1], M = L.rec[2];
+    const uint32_t nh = w0 & 0xFFu, nsh = w0 >> 8;
+    const uint32_t *grec = o.recs + (uint64_t)t * kRecStrideAlloc;
+    for (uint32_t w = kWave + lane; w < 4 + kRecHit * nh; w += kWave) L.rec[w] = grec[w];
+    wave_lds_sync();
+    rec_prefix<kWave>(L.rec, nh, lane);
+    wave_lds_sync();
+    const bool first = j == 0;
+    if (first && H) {
+      uint32_t w = 0;
+      for (uint32_t k = 0; k < nsh; k++) {
+        const uint32_t so = grec[kRecSh + 2 * k], sc = grec[kRecSh + 1 + 2 * k];
+        for (uint32_t k2 = lane; k2 < sc; k2 += kWave) put_out(&o.hout[hb + w + k2], so + k2);
+        w += sc;
       }
-      wave_lds_sync();
-#pragma unroll
-      for (int k = 0; k < kMPer; k++)
-        if (gl + k * kE < M) table_insert(L.tkey, L.tbits, L.tmin, mask, lg, mcl[k], mmeta[k], mrk[k]);
-      wave_lds_sync();
+    }
+    const bool merge_here = first && M > 0 && M <= kSmallMulti;
+    uint32_t mcl[kMPer], mw[kMPer], mrk[kMPer];
+    if (merge_here) {
 #pragma unroll
       for (int k = 0; k < kMPer; k++) {
-        bool win = false;
-        uint64_t ent = 0;
-        if (gl + k * kE < M) {
-          const uint32_t sl = table_find(L.tkey, mask, lg, mcl[k]);
-          win = L.tmin[sl] == mrk[k];
-          const uint32_t v = L.tbits[sl];
-          ent = pack_delivery(mcl[k], msid[k], 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
-        }
-        const uint64_t m = (__ballot(win) >> gbase) & kGMask;
-        if (win) put_out(&o.dout[db + D + __popcll(m & glt)], ent);
-        D += __popcll(m);
+        const uint32_t q = lane + k * kWave;
+        uint32_t h;
+        const uint32_t sid = multi_sid(L.rec, nh, Ss, q < M ? q : 0, &h);
+        mrk[k] = rec_at(L.rec, h, kFieldRank);
+        const SubEnt e = load_sub(s, sid);
+        mcl[k] = e.client;
+        mw[k] = e.word;
       }
     }
-    if (gl == 0) o.dcount[t] = D;
+    // solo entries [lo, hi) of the topic: delivery q = solo entry q.  When one
+    // hit holds a whole step of positions (hub ranges), no search at all.
+    const uint32_t lo = j * kChunk, hi = min(Ss, lo + kChunk);
+    uint64_t v[kU];
+    auto load_solo = [&](uint32_t base, uint64_t (&dst)[kU]) {
+      const uint32_t h0 = hit_of<kFieldSpre>(L.rec, nh, base);  // wave-uniform
+      const uint32_t end0 = h0 + 1 < nh ? rec_at(L.rec, h0 + 1, kFieldSpre) : Ss;
+      const uint32_t d0 = rec_at(L.rec, h0, kFieldOff) - rec_at(L.rec, h0, kFieldSpre);
+      if (base + kWave * kU <= end0) {
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+          const uint32_t q = base + u * kWave + lane;
+          dst[u] = solo_delivery(load_sub(s, d0 + (q < hi ? q : base)));
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+          const uint32_t q = base + u * kWave + lane;
+          dst[u] = solo_delivery(load_sub(s, solo_sid(L.rec, nh, q < hi ? q : base)));
+        }
+      }
+    };
+    if (lo < hi) load_solo(lo, v);
+    for (uint32_t base = lo; base < hi; base += kWave * kU) {
+      uint64_t nv[kU];
+      if (base + kWave * kU < hi) load_solo(base + kWave * kU, nv);
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+        const uint32_t q = base + u * kWave + lane;
+        if (q < hi) put_out(&o.dout[db + q], v[u]);
+        v[u] = nv[u];
+      }
+    }
+    if (first) {
+      if (M > kSmallMulti) {  // the workgroup tier merges them and writes dcount
+        if (lane == 0) o.multi_list[atomicAdd(&o.ctr->n_multi, 1u)] = t;
+      } else {
+        uint32_t D = Ss;
+        if (merge_here)
+          D = merge_multi<kWave, kMPer>(L.tkey, L.tbits, L.tmin, kSmallSlots, mcl, mw, mrk, M, lane, 0, o.dout, db, D);
+        if (lane == 0) o.dcount[t] = D;
+      }
+    }
     wave_lds_sync();
   }
 }
@@ -743,7 +836,7 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
 // ---------------------------------------------------------------------------
 // k_multi<kSlots, kPer>: a 256-thread workgroup per listed topic merges its
 // multi entries (<= kPer per thread) in an LDS table of kSlots slots and writes
-// the winners after the topic's solo deliveries (k_emit wrote those).  Topic
+// the winners after the topic's solo deliveries (k_copy wrote those).  Topic
 // ids are prefetched two topics ahead and the record one topic ahead.  Topics
 // with more multi entries than the tier holds go to `ovf`, the next tier
 // (tiers of 768 / 1536 / 3072 entries: small tiers keep more blocks resident;
@@ -801,21 +894,21 @@ __global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs
       tbits[i] = 0;
       tmin[i] = 0xFFFFFFFFu;
     }
-    uint32_t cl[kPer], sid[kPer], rk[kPer], meta[kPer];
+    uint32_t cl[kPer], wd[kPer], rk[kPer];
 #pragma unroll
     for (int k = 0; k < kPer; k++) {  // unconditional loads (entry 0 stands in past M)
       const uint32_t q = tid + k * kBigThreads;
       uint32_t h;
-      sid[k] = multi_sid(rec, nh, Ss, q < M ? q : 0, &h);
+      const uint32_t sid = multi_sid(rec, nh, Ss, q < M ? q : 0, &h);
       rk[k] = rec_at(rec, h, kFieldRank);
-      const SubEnt e = s.subs[sid[k]];
+      const SubEnt e = load_sub(s, sid);
       cl[k] = e.client;
-      meta[k] = e.meta;
+      wd[k] = e.word;
     }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < kPer; k++)
-      if (tid + k * kBigThreads < M) table_insert(tkey, tbits, tmin, mask, lg, cl[k], meta[k], rk[k]);
+      if (tid + k * kBigThreads < M) table_insert(tkey, tbits, tmin, mask, lg, cl[k], wd[k], rk[k]);
     __syncthreads();
     uint32_t D = Ss;
 #pragma unroll
@@ -828,7 +921,7 @@ __global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs
         const uint32_t sl = table_find(tkey, mask, lg, cl[k]);
         win = tmin[sl] == rk[k];
         const uint32_t v = tbits[sl];
-        ent = pack_delivery(cl[k], sid[k], 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
+        ent = pack_delivery(cl[k], wd[k] & kWordSidMask, 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
       }
       const uint64_t m = __ballot(win);
       if (lane == 0) wsum[wid] = __popcll(m);
@@ -1008,7 +1101,7 @@ __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *
           if (kPhase >= 3) {  // identifiers: the range's entries with Identifier > 0
             for (uint32_t b0 = 0; b0 < rcnt; b0 += kWave) {
               const uint32_t j = b0 + lane;
-              const bool has = j < rcnt && (s.subs[roff + j].meta & kMetaIdent);
+              const bool has = j < rcnt && (s.subs[roff + j].word & kWordIdent);
               const uint64_t m = __ballot(has);
               if (kPhase == 4 && has) o.iout[o.istart[t] + nid + __popcll(m & lanemask_lt(lane))] = roff + j;
               nid += (uint32_t)__popcll(m);
@@ -1026,7 +1119,7 @@ __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *
                 if (prev == 0 || (uint32_t)prev == se.client + 1) break;
                 slot = (slot + 1) & (tsz - 1);
               }
-              atomicOr(&T[slot].keybits, (unsigned long long)qos_bits(se.meta) << 32);
+              atomicOr(&T[slot].keybits, (unsigned long long)qos_bits(se.word) << 32);
               atomicMax(&T[slot].first, ~(((unsigned long long)rank << 32) | sid));
             }
           }
@@ -1080,7 +1173,7 @@ __global__ __launch_bounds__(256) void k_ident(DeviceSnapshot s, Outputs o, uint
         const uint32_t cnt = hr.y + hr.z;
         for (uint32_t b0 = 0; b0 < cnt; b0 += kWave) {
           const uint32_t j = b0 + lane;
-          const bool has = j < cnt && (s.subs[hr.x + j].meta & kMetaIdent);
+          const bool has = j < cnt && (s.subs[hr.x + j].word & kWordIdent);
           const uint64_t m = __ballot(has);
           if (kPhase == 1 && has) o.iout[ib + nid + __popcll(m & lanemask_lt(lane))] = hr.x + j;
           nid += (uint32_t)__popcll(m);
@@ -1248,11 +1341,6 @@ static uint32_t resident_blocks(Workspace &ws, int, K kern) {
 }
 
 // counts (n) -> exclusive offsets (u64, n + 1)
-struct PadCount {
-  uint32_t mask;  // pad - 1 (pad a power of two)
-  __host__ __device__ uint64_t operator()(uint32_t c) const { return ((uint64_t)c + mask) & ~(uint64_t)mask; }
-};
-
 template <class T>
 static int scan_offsets(Workspace &ws, T counts, uint64_t *offs, uint32_t n, hipStream_t st) {
   HIP_TRY(hipMemsetAsync(offs, 0, sizeof(uint64_t), st));
@@ -1308,26 +1396,47 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   }
   HIP_TRY(hipGetLastError());
   mark(ws, 1, st);
-  // segment starts: each topic's raw-entry count rounded up to kDPad entries,
-  // so no two topics' deliveries share a cache line (env MQM_DPAD: 1 | 16)
-  {
-    static const uint32_t pad = getenv("MQM_DPAD") ? (uint32_t)atoi(getenv("MQM_DPAD")) : kDPad;
-    const uint32_t pm = pad > 1 ? pad - 1 : 0;
-    hipcub::TransformInputIterator<uint64_t, PadCount, const uint32_t *> padded(o.scount, PadCount{pm});
-    if (scan_offsets(ws, padded, o.dstart, n, st) || scan_offsets(ws, o.hcount, o.hstart, n, st)) return -3;
+  // segment starts: exclusive scans of S (raw entries, an upper bound of a
+  // topic's deliveries) and H (shared candidates)
+  if (scan_offsets(ws, (const uint32_t *)o.scount, o.dstart, n, st) || scan_offsets(ws, (const uint32_t *)o.hcount, o.hstart, n, st))
+    return -3;
+  // emit lists (small class + shared-only topics; big class) and the big
+  // class's chunk items, counted before the one host sync that sizes the outputs
+  if (ws.get(W::kListS, sizeof(uint32_t) * (n + 1)) || ws.get(W::kListB, sizeof(uint32_t) * (n + 1)) ||
+      ws.get(W::kNChunk, sizeof(uint32_t) * (n + 1)) || ws.get(W::kCStart, sizeof(uint64_t) * (n + 1)))
+    return -2;
+  auto *list_s = (uint32_t *)ws.ptr(W::kListS), *list_b = (uint32_t *)ws.ptr(W::kListB);
+  auto *nchunk = (uint32_t *)ws.ptr(W::kNChunk);
+  auto *cstart = (uint64_t *)ws.ptr(W::kCStart);
+  if (n > 0) {
+    size_t tmp = 0;
+    hipcub::CountingInputIterator<uint32_t> it(0);
+    HIP_TRY(hipcub::DeviceSelect::If(nullptr, tmp, it, list_s, &o.ctr->n_small, n, IsSmallClass{o.cls, o.hcount}, st));
+    if (ws.get(W::kScanTmp, tmp)) return -2;
+    HIP_TRY(hipcub::DeviceSelect::If(ws.ptr(W::kScanTmp), tmp, it, list_s, &o.ctr->n_small, n,
+                                     IsSmallClass{o.cls, o.hcount}, st));
+    HIP_TRY(hipcub::DeviceSelect::If(ws.ptr(W::kScanTmp), tmp, it, list_b, &o.ctr->n_bigc, n, IsBigClass{o.cls}, st));
+    hipLaunchKernelGGL(k_chunks, dim3(std::min<uint32_t>((n + 255) / 256, 4096)), dim3(256), 0, st, o, list_b,
+                       &o.ctr->n_bigc, n, nchunk);
+    HIP_TRY(hipGetLastError());
   }
+  if (scan_offsets(ws, (const uint32_t *)nchunk, cstart, n, st)) return -3;
   HIP_TRY(hipMemcpyAsync(hc, o.ctr, sizeof(Counters), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(hp, o.dstart + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(hp + 1, o.hstart + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(hp + 3, cstart + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   const uint32_t n_dfs = hc->n_dfs;
-  const uint64_t s_total = hp[0], h_total = hp[1];
+  const uint64_t s_total = hp[0], h_total = hp[1], n_items = hp[3];
   ws.last_valid = true;
   ws.last_n = n;
   ws.last_bytes = d_bytes;
   ws.last_offs = d_offs;
   ws.last_n_dfs = n_dfs;
   for (int i = 0; i < 5; i++) ws.why[i] = hc->why[i];
+  ws.last_small = hc->n_small;
+  ws.last_bigc = hc->n_bigc;
+  ws.last_items = n_items;
 
   // DFS phase 0: exact raw / shared counts size the tail regions
   uint64_t dfs_raw = 0, dfs_h = 0, tab_total = 0;
@@ -1349,7 +1458,7 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_table_sizes, dim3((n_dfs + 255) / 256), dim3(256), 0, st, raw_cnt, o.ctr, tab_size);
     HIP_TRY(hipGetLastError());
-    if (scan_offsets(ws, tab_size, tab_off, n_dfs, st)) return -3;
+    if (scan_offsets(ws, (const uint64_t *)tab_size, tab_off, n_dfs, st)) return -3;
     std::vector<uint64_t> rc(2 * (n_dfs + 1));
     HIP_TRY(hipMemcpyAsync(rc.data(), raw_cnt, sizeof(uint64_t) * 2 * (n_dfs + 1), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(hp, tab_off + n_dfs, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
@@ -1363,44 +1472,29 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   // outputs: scanned segments, then the DFS tails
   if (ws.get(W::kDOut, sizeof(uint64_t) * (s_total + dfs_raw + 1)) ||
       ws.get(W::kHOut, sizeof(uint32_t) * (h_total + dfs_h + 1)) ||
-      ws.get(W::kDense, sizeof(uint32_t) * (n + 1)))  // multi list
+      ws.get(W::kDense, sizeof(uint32_t) * (n + 1)) ||  // multi list
+      ws.get(W::kItems, sizeof(uint2) * (n_items + 1)))
     return -2;
   o.dout = (uint64_t *)ws.ptr(W::kDOut);
   o.hout = (uint32_t *)ws.ptr(W::kHOut);
   o.multi_list = (uint32_t *)ws.ptr(W::kDense);
+  auto *items = (uint2 *)ws.ptr(W::kItems);
 
   mark(ws, 2, st);
   static_assert(kWave * kEmitWaves == kBigThreads, "resident_blocks assumes 256-thread blocks");
   if (n > 0) {
-    if (ws.get(W::kListS, sizeof(uint32_t) * (n + 1)) || ws.get(W::kListB, sizeof(uint32_t) * (n + 1))) return -2;
-    auto *list_s = (uint32_t *)ws.ptr(W::kListS), *list_b = (uint32_t *)ws.ptr(W::kListB);
-    size_t tmp = 0;
-    hipcub::CountingInputIterator<uint32_t> it(0);
-    HIP_TRY(hipcub::DeviceSelect::If(nullptr, tmp, it, list_s, &o.ctr->n_small, n, IsSmallClass{o.cls, o.hcount}, st));
-    if (ws.get(W::kScanTmp, tmp)) return -2;
-    HIP_TRY(hipcub::DeviceSelect::If(ws.ptr(W::kScanTmp), tmp, it, list_s, &o.ctr->n_small, n,
-                                     IsSmallClass{o.cls, o.hcount}, st));
-    HIP_TRY(hipcub::DeviceSelect::If(ws.ptr(W::kScanTmp), tmp, it, list_b, &o.ctr->n_bigc, n, IsBigClass{o.cls}, st));
-    auto launch_emit = [&](auto kern, const uint32_t *list, const unsigned int *cnt) {
-      hipLaunchKernelGGL(kern, dim3(resident_blocks(ws, 0, kern)), dim3(kWave * kEmitWaves), 0, st, s, o, list, cnt);
-    };
-    // (amdgpu_waves_per_eu 6 / 8 variants of both spill and measured slower:
-    // profiles/r01/c3_v6_occupancy_sweep.log)
-    // solo entries in flight per lane (env MQM_EMIT_U16 / MQM_EMIT_U64: 4 or 8; tuning sweeps)
-    const int u16 = getenv("MQM_EMIT_U16") ? atoi(getenv("MQM_EMIT_U16")) : 4;
-    const int u64 = getenv("MQM_EMIT_U64") ? atoi(getenv("MQM_EMIT_U64")) : 4;
-    if (u16 == 8)
-      launch_emit(k_emit<16, 1, 8>, list_s, &o.ctr->n_small);
-    else
-      launch_emit(k_emit<16, 1, 4>, list_s, &o.ctr->n_small);
+    auto grid = [&](auto kern) { return dim3(resident_blocks(ws, 0, kern)); };
+    hipLaunchKernelGGL((k_emit_small<1, kEmitU>), grid(k_emit_small<1, kEmitU>), dim3(kWave * kEmitWaves), 0, st, s,
+                       o, list_s, &o.ctr->n_small);
     HIP_TRY(hipGetLastError());
-    if (u64 == 8)
-      launch_emit(k_emit<64, 4, 8>, list_b, &o.ctr->n_bigc);
-    else if (u64 == 2)
-      launch_emit(k_emit<64, 5, 2>, list_b, &o.ctr->n_bigc);
-    else
-      launch_emit(k_emit<64, 5, 4>, list_b, &o.ctr->n_bigc);
-    HIP_TRY(hipGetLastError());
+    if (n_items) {
+      hipLaunchKernelGGL(k_items, dim3(std::min<uint32_t>((n + 255) / 256, 4096)), dim3(256), 0, st, list_b,
+                         &o.ctr->n_bigc, cstart, items);
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL((k_copy<5, kEmitU>), grid(k_copy<5, kEmitU>), dim3(kWave * kEmitWaves), 0, st, s, o, items,
+                         n_items);
+      HIP_TRY(hipGetLastError());
+    }
     if (ws.get(W::kOvfList, sizeof(uint32_t) * (n + 1))) return -2;
     auto *ovf = (uint32_t *)ws.ptr(W::kOvfList);
     if (ws.get(W::kOvfList2, sizeof(uint32_t) * (n + 1))) return -2;
@@ -1439,7 +1533,7 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
     HIP_TRY(hipcub::DeviceReduce::Sum(ws.ptr(W::kScanTmp), tmp, o.dcount, sums, n, st));
     HIP_TRY(hipcub::DeviceReduce::Sum(ws.ptr(W::kScanTmp), tmp, o.hcount, sums + 1, n, st));
     HIP_TRY(hipMemcpyAsync(hp, sums, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(hp + 2, &o.ctr->n_multi, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(hc, o.ctr, sizeof(Counters), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
   }
   if (ws.profile) {
@@ -1452,7 +1546,12 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   out->n_topics = n;
   out->n_deliveries = hp[0];
   out->n_shared = hp[1];
-  out->n_big = (uint32_t)hp[2];
+  out->n_big = hc->n_multi;
+  out->n_tier2 = hc->n_ovf;
+  out->n_tier3 = hc->n_ovf2;
+  out->n_small = hc->n_small;
+  out->n_bigc = hc->n_bigc;
+  out->n_items = n_items;
   out->n_fallback = n_dfs;
   out->starts = o.dstart;
   out->counts = o.dcount;

@@ -54,15 +54,27 @@ static_assert(sizeof(EdgeEntry) == 64, "EdgeEntry layout");
 
 constexpr uint32_t kEdgesPerBucket = 2;
 
-// non-shared subscription entry; sid = index into the array.  A node's range
-// holds its solo entries first, then its multi entries (kMetaMulti), and the
+// non-shared subscription entry as the device reads it; sid = its index.  A
+// node's range holds its solo entries first, then its multi entries, and the
 // range of a node's '#' child follows it directly.
+//   client
+//   word = sid (bits 0..27) | qos << 28 | no_local << 30 | ident << 31
+// (client, word & 0x7FFFFFFF) is exactly the delivery the matcher writes for
+// the entry when it is its client's only gathered entry (see kMetaMulti), so a
+// solo range is emitted by a masked copy.  Bit 31 (kWordIdent): Identifier > 0
+// (read by the identifiers pass).  RAP / RH / the identifier value stay on the
+// host (SubInfo), resolved through the delivery's sid.
 struct SubEnt {
   uint32_t client;
-  uint32_t meta;          // qos[1:0] | no_local[2] | rap[3] | rh[5:4] | multi[6] | ident[7]
+  uint32_t word;  // while flatten() builds the snapshot: the build-time meta bits below
 };
+constexpr uint32_t kWordSidMask = 0x0FFFFFFFu;
+constexpr uint32_t kWordIdent = 1u << 31;
+constexpr uint64_t kDeliveryMask = 0x7FFFFFFFFFFFFFFFull;  // entry as u64 -> delivery
 
-// meta bit 6 ("multi"): this entry may meet another entry of the same client
+// build-time meta (flatten.cpp): qos[1:0] | no_local[2] | rap[3] | rh[5:4] |
+// multi[6] | ident[7], rewritten into the device word at the end of flatten().
+// Bit 6 ("multi"): this entry may meet another entry of the same client
 // in one topic's gather, so it must go through the per-topic merge
 // (packets.go:250-270).  Clear ("solo") only when the flattener proved that
 // no topic emits it twice (it is not on a '#' node, whose subscriptions the
@@ -73,7 +85,7 @@ struct SubEnt {
 // merged delivery as is.
 constexpr uint32_t kMetaMulti = 1u << 6;
 // meta bit 7: Identifier > 0 — Subscription.Merge adds the entry to the
-// client's Identifiers map (packets.go:257-259); read by the identifiers pass
+// client's Identifiers map (packets.go:257-259); becomes kWordIdent
 constexpr uint32_t kMetaIdent = 1u << 7;
 
 // delivery written by the matcher (one per (topic, client)):

@@ -1,0 +1,34 @@
+#!/bin/bash
+# profiles/run_r02.sh TAG STEP... — round-2 GPU runs, each step under its own
+# time limit, chained so that the first failure ends the call.
+#   tests   : every -m gpu test                         -> gpurun_out/TAG/pytest_gpu.log
+#   quick   : the -m gpu tests except the full-size ones -> gpurun_out/TAG/pytest_quick.log
+#   smoke   : __graft_entry__.smoke()
+#   bench   : the default bench line (C3)               -> gpurun_out/TAG/bench.json
+#   fast    : bench without CPU baseline / host path     -> gpurun_out/TAG/bench_fast.json
+#   prof    : rocprofv3 kernel trace + stats of `fast`   -> gpurun_out/TAG/prof/
+set -euo pipefail
+TAG=$1
+shift
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p $OUT
+cd $ROOT
+FAST="--steps 10 --warmup 3 --no-cpu-baseline --host-topics 0 --latency-topics 0"
+for step in "$@"; do
+  echo "[run_r02] $step $(date +%T)"
+  case $step in
+    tests) timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread \
+             > $OUT/pytest_gpu.log 2>&1 ;;
+    quick) timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+             -k "not full_size and not 20m and not 5m" > $OUT/pytest_quick.log 2>&1 ;;
+    smoke) timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 ;;
+    bench) timeout -k 10 600 python3 -u bench.py > $OUT/bench.json 2> $OUT/bench.log ;;
+    fast) timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast.json 2> $OUT/bench_fast.log ;;
+    prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv \
+             -d $OUT/prof -o prof -- python3 $ROOT/bench.py $FAST \
+             > $OUT/bench_under_rocprof.json 2> $OUT/rocprof.log) ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "[run_r02] done $(date +%T)"

@@ -89,3 +89,51 @@ def canon_oracle_idents(ioffs, iout):
     a["topic"] = np.repeat(np.arange(n, dtype=np.uint32), cnt)
     a["client"], a["filter"], a["ident"] = iout["client"], iout["filter"], iout["ident"]
     return np.unique(a)
+
+
+def dev_tensor(ptr, count, dtype):
+    """A copy (device to device) of `count` elements of a library-owned device
+    buffer, as a torch tensor on cuda:0."""
+    import ctypes
+
+    import torch
+
+    t = torch.empty(max(int(count), 1), dtype=dtype, device="cuda")[: int(count)]
+    nbytes = int(count) * t.element_size()
+    if nbytes:
+        torch.cuda.synchronize()
+        hip = ctypes.CDLL("libamdhip64.so")
+        rc = hip.hipMemcpy(ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(ptr), ctypes.c_size_t(nbytes),
+                           ctypes.c_int(3))
+        assert rc == 0, rc
+    return t
+
+
+def mix64(x):
+    """splitmix64 finaliser on an int64 torch tensor (wrapping arithmetic)."""
+    import torch
+
+    x = x ^ ((x >> 30) & 0x3FFFFFFFF)
+    x = x * torch.tensor(-4658895280553007687, dtype=torch.int64, device=x.device)  # 0xBF58476D1CE4E5B9
+    x = x ^ ((x >> 27) & 0x1FFFFFFFFF)
+    x = x * torch.tensor(-7723592293110705685, dtype=torch.int64, device=x.device)  # 0x94D049BB133111EB
+    return x ^ ((x >> 31) & 0x1FFFFFFFF)
+
+
+def topic_checksums(offs, ents, chunk=1 << 20):
+    """Per-topic order-independent checksum (sum of mix64 of every entry, with
+    the topic id folded in) of a dense device CSR: int64 tensor [n]."""
+    import torch
+
+    n = offs.numel() - 1
+    out = torch.zeros(n, dtype=torch.int64, device=offs.device)
+    for lo in range(0, n, chunk):
+        hi = min(n, lo + chunk)
+        a, b = int(offs[lo]), int(offs[hi])
+        if a == b:
+            continue
+        cnt = (offs[lo + 1:hi + 1] - offs[lo:hi])
+        tid = torch.repeat_interleave(torch.arange(lo, hi, device=offs.device), cnt)
+        h = mix64(ents[a:b] ^ mix64(tid))
+        out.index_add_(0, tid, h)
+    return out

@@ -353,3 +353,86 @@ def test_gather_shards_equals_unsharded(n_shards):
     if total:
         with pytest.raises(maxmq_amd.MqmError):
             maxmq_amd.gather_shards(n, bad, out_o.data_ptr(), out_d.data_ptr())
+
+
+def test_full_size_c3_headline_config():
+    """BASELINE configs[2], the config the headline is quoted on (10M filters,
+    40% '+', 10% '#', Zipf(1.2) topics, 10M-topic batch), through the same
+    mqm_match_device call bench.py times:
+      * bit-exact against the oracle on a 100k-topic sample of the batch (the
+        full-batch rows of those topics are compared with the host-path rows,
+        which are compared with oracle/mochi_ref.c field by field);
+      * over all 10M topics: dense CSR monotone and summing to n_deliveries,
+        QoS <= 2, client ids in range, per-topic client uniqueness (on a 1M
+        sample), run-to-run equality of every topic's checksum of its entries;
+      * the big class and the workgroup merge tier were exercised."""
+    import torch
+
+    from tests.gpu_util import dev_tensor, topic_checksums
+
+    w = mqgen.generate(3)
+    n = len(w.topics)
+    idx = maxmq_amd.TopicsIndex(0, autocommit=False)
+    idx.subscribe_workload(w)
+    idx.commit()
+    dev = torch.device("cuda:0")
+    tb = torch.from_numpy(w.topics.data).to(dev)
+    to = torch.from_numpy(w.topics.offs.view(np.int64)).to(dev)
+
+    def run():
+        r = idx.match_device(tb.data_ptr(), to.data_ptr(), n)
+        d = idx.dense_device()
+        torch.cuda.synchronize()
+        offs = dev_tensor(d.offsets, n + 1, torch.int64)
+        ents = dev_tensor(d.deliveries, int(d.n_deliveries), torch.int64)
+        sh_offs = dev_tensor(d.shared_offsets, n + 1, torch.int64)
+        return r, offs, ents, sh_offs
+
+    r1, offs, ents, sh_offs = run()
+    nd = int(r1.n_deliveries)
+    assert nd > 50 * n, nd  # Zipf fan-out: ~230 deliveries per topic
+    assert r1.n_big > 0, "the workgroup merge tier never ran"
+    assert int(offs[0]) == 0 and int(offs[-1]) == nd
+    assert bool((offs[1:] >= offs[:-1]).all())
+    assert int(sh_offs[-1]) == int(r1.n_shared)
+    clients = ents & 0xFFFFFFFF
+    packed = (ents >> 32) & 0xFFFFFFFF
+    assert int(clients.max()) < idx.num_clients()
+    assert int(((packed >> 28) & 3).max()) <= 2
+    sums1 = topic_checksums(offs, ents)
+    del clients, packed
+    # run-to-run: every topic's entries, as a set, identical
+    _, offs2, ents2, _ = run()
+    assert torch.equal(offs2, offs)
+    assert torch.equal(topic_checksums(offs2, ents2), sums1)
+    del offs2, ents2
+    # per-topic client uniqueness on a 1M-topic sample (host)
+    rng = np.random.default_rng(3)
+    sample = np.sort(rng.choice(n, size=1000000, replace=False))
+    o = offs.cpu().numpy()
+    cnt = (o[sample + 1] - o[sample]).astype(np.int64)
+    pos = torch.from_numpy(np.repeat(o[sample] - np.concatenate([[0], np.cumsum(cnt)[:-1]]), cnt)
+                           + np.arange(cnt.sum())).to(dev)
+    samp = ents[pos].cpu().numpy().view(np.uint64)
+    tid = np.repeat(np.arange(len(sample), dtype=np.uint64), cnt)
+    key = (tid << np.uint64(32)) | (samp & np.uint64(0xFFFFFFFF))
+    assert len(np.unique(key)) == len(key), "a client appears twice in one topic"
+    # bit-exact on a 100k-topic sample: full-batch rows == host-path rows == oracle
+    small = np.sort(rng.choice(n, size=100000, replace=False))
+    sub = Strings.from_list([w.topics[int(i)] for i in small])
+    res = idx.match_batch(sub.data, sub.offs)
+    cnt = (o[small + 1] - o[small]).astype(np.int64)
+    assert np.array_equal(cnt, np.diff(res.offsets).astype(np.int64)), "per-topic counts differ from the host path"
+    pos = torch.from_numpy(np.repeat(o[small] - np.concatenate([[0], np.cumsum(cnt)[:-1]]), cnt)
+                           + np.arange(cnt.sum())).to(dev)
+    full_rows = ents[pos].cpu().numpy().view(np.uint64)
+    tid = np.repeat(np.arange(len(small), dtype=np.uint64), cnt)
+    host_rows = res.deliveries.view(np.uint64)
+    assert np.array_equal(np.unique(np.stack([tid, full_rows], 1), axis=0),
+                          np.unique(np.stack([tid, host_rows], 1), axis=0)), "full-batch rows != host-path rows"
+    ora = OracleIndex()
+    ora.subscribe_workload(w)
+    r, rs = canon_oracle(*ora.match(sub.data, sub.offs, nthreads=16)[:4])
+    g, gs = canon_gpu(res)
+    assert_same(g, r, "C3 deliveries (sample)")
+    assert_same(gs, rs, "C3 shared (sample)")

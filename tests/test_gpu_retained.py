@@ -103,3 +103,92 @@ def test_random_retain_ops():
             s = Strings.from_list(filters)
             assert _per_filter_sets(*idx.messages_batch(s.data, s.offs)) == \
                 _per_filter_sets(*ora.messages(s.data, s.offs)), step
+
+
+def _canon(offs, refs):
+    """(filter, ref) rows sorted: the per-filter sets as one array"""
+    f = np.repeat(np.arange(len(offs) - 1, dtype=np.uint64), np.diff(offs).astype(np.int64))
+    o = np.lexsort((refs, f))
+    return np.stack([f[o], np.asarray(refs, np.uint64)[o]], 1)
+
+
+def test_config5_5m_retained_vs_oracle():
+    """BASELINE configs[4] at 1/10 of the retained store: 100k subscription
+    filters (5% $SHARE) against 5M retained topics, bit-exact per filter."""
+    w = mqgen.generate(5, n_filters=100000, n_topics=5000000)
+    idx = maxmq_amd.TopicsIndex(0)
+    ora = OracleIndex()
+    idx.subscribe_workload(w)
+    ora.subscribe_workload(w)
+    refs = np.arange(len(w.topics), dtype=np.uint64) * 3 + 1
+    idx.retain_many(w.topics, refs)
+    ora.retain_many(w.topics, refs)
+    assert idx.retained_len() == ora.retained_len()
+    f = w.filters
+    go, gr = idx.messages_batch(f.data, f.offs)
+    ro, rr = ora.messages(f.data, f.offs, nthreads=16)
+    assert np.array_equal(go, ro), "per-filter counts differ"
+    assert go[-1] > 1000000
+    assert np.array_equal(_canon(go, gr), _canon(ro, rr))
+
+
+def test_config5_20m_retained_linearity():
+    """BASELINE configs[4] at 1M filters vs 20M retained topics (bench.py
+    --workload reverse checks the same property at the full 50M):
+    the retained set split in two by a content hash of the topic (duplicates
+    land in the same half, so "last retain wins" holds in both) must give, for
+    every filter, count(full) = count(half 0) + count(half 1), and for a
+    sample of filters set(full) = set(half 0) | set(half 1).  Also run-to-run
+    equality of the full counts."""
+    import torch
+
+    w = mqgen.generate(5, n_topics=20000000)
+    t = w.topics
+    lens = np.diff(t.offs).astype(np.int64)
+    byte_sum = np.add.reduceat(t.data.astype(np.int64), t.offs[:-1].astype(np.int64)) if len(t.data) else lens
+    byte_sum = np.where(lens > 0, byte_sum, 0)
+    half = ((byte_sum + 7 * lens) & 1).astype(bool)
+    refs = np.arange(len(t), dtype=np.uint64)
+    f = w.filters
+    fb = torch.from_numpy(f.data).cuda()
+    fo = torch.from_numpy(f.offs.view(np.int64)).cuda()
+    nf = len(f)
+    rng = np.random.default_rng(11)
+    sample = np.sort(rng.choice(nf, size=2000, replace=False))
+    sub = Strings.from_list([f[int(i)] for i in sample])
+
+    def index_of(mask):
+        idx = maxmq_amd.TopicsIndex(0, autocommit=False)
+        idx.subscribe_workload(w)
+        keep = np.nonzero(mask)[0]
+        if mask.all():
+            idx.retain_many(t, refs)
+        else:
+            sub_offs = np.concatenate([[0], np.cumsum(lens[keep])]).astype(np.uint64)
+            idx.retain_many(Strings(t.data[np.repeat(mask, lens)], sub_offs), refs[keep])
+        idx.commit()
+        return idx
+
+    def counts(idx):
+        from tests.gpu_util import dev_tensor
+
+        m = idx.messages_device(fb.data_ptr(), fo.data_ptr(), nf)
+        torch.cuda.synchronize()
+        return dev_tensor(m.offsets, nf + 1, torch.int64).cpu().numpy()
+
+    full = index_of(np.ones(len(t), bool))
+    c_full = counts(full)
+    assert np.array_equal(counts(full), c_full)
+    s_full = _canon(*full.messages_batch(sub.data, sub.offs))
+    assert c_full[-1] > 400000000, c_full[-1]  # ~900 retained hits per filter
+    del full
+    parts_c, parts_s = [], []
+    for h in (False, True):
+        idx = index_of(half == h)
+        parts_c.append(np.diff(counts(idx)))
+        parts_s.append(_canon(*idx.messages_batch(sub.data, sub.offs)))
+        del idx
+    assert np.array_equal(np.diff(c_full), parts_c[0] + parts_c[1]), "count(full) != count(half 0) + count(half 1)"
+    both = np.concatenate(parts_s)
+    both = both[np.lexsort((both[:, 1], both[:, 0]))]
+    assert np.array_equal(s_full, both), "set(full) != set(half 0) | set(half 1)"
