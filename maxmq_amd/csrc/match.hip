@@ -110,10 +110,12 @@ struct Counters {              // zeroed before every batch
   unsigned int n_bigc;
   unsigned int n_ovf;          // topics k_multi's first tier passed to the second
   unsigned int n_ovf2;         // ... the second tier to the third
+  unsigned int n_wmerge;       // big-class topics k_merge dedupes (0 < Ms <= kSmallMulti)
 };
 
 struct Outputs {
   uint32_t *scount, *hcount, *dcount;
+  uint32_t *mcount;           // multi entries per topic (Ms; 0 for DFS topics)
   uint64_t *dstart, *hstart;  // n + 1 (exclusive scans; DFS topics overwritten)
   uint8_t *cls;
   uint32_t *dfs_list;
@@ -171,10 +173,7 @@ __device__ __forceinline__ uint32_t qos_bits(uint32_t word) {
   return (1u << ((word >> 28) & 3)) | (((word >> 30) & 1) << 3);
 }
 
-// a SubEnt as its own delivery (snapshot.h)
-__device__ __forceinline__ uint64_t solo_delivery(SubEnt e) {
-  return ((uint64_t)(e.word & 0x7FFFFFFFu) << 32) | e.client;
-}
+
 
 // the hit h holding entry x of a prefix field (kFieldSpre / kFieldMpre): the
 // largest h < nh with field(h) <= x (field(0) = 0).  Hits with none of those
@@ -191,7 +190,7 @@ __device__ __forceinline__ uint32_t hit_of(const uint32_t *rec, uint32_t nh, uin
   for (uint32_t step = 32; step > 0; step >>= 1) {
     const uint32_t c = h + step;
     const uint32_t v = rec[4 + kRecHit * (c < nh ? c : 0) + kField];
-    h = (c < nh && v <= x) ? c : h;
+    h = ((c < nh) & (v <= x)) ? c : h;  // bitwise: no branch around the read
   }
   return h;
 }
@@ -481,6 +480,7 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
                                                                  : kClsBig;
       o.scount[t] = dfs ? 0 : S;
       o.hcount[t] = dfs ? 0 : H;
+      o.mcount[t] = dfs ? 0 : Ms;
       o.dcount[t] = 0;
       if (dfs) {
         o.dfs_list[atomicAdd(&o.ctr->n_dfs, 1u)] = t;
@@ -533,6 +533,77 @@ __device__ __forceinline__ uint32_t solo_sid(const uint32_t *rec, uint32_t nh, u
 __device__ __forceinline__ SubEnt load_sub(const DeviceSnapshot &s, uint32_t sid) {
   const uint2 v = *reinterpret_cast<const uint2 *>(s.subs + sid);
   return SubEnt{v.x, v.y};
+}
+
+// unaligned-capable 16-B accesses (8-B aligned: gfx950 runs dword-aligned
+// vector memory accesses, ROCm's default alignment mode)
+typedef uint32_t u32x4_a8 __attribute__((ext_vector_type(4), aligned(8)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// solo entries q in [lo, hi) of a topic whose record (prefixes) is in LDS, to
+// out[db + q]: a kE-lane group moves 2 consecutive positions per lane and
+// access — 16-B stores always, 16-B loads when one hit holds the whole step
+// (hub ranges; else each entry's hit is found by hit_of) — kU accesses per
+// lane, and the next step's loads are issued before this step's stores (two
+// register sets, so no register copy waits for a load).
+template <int kE, int kU>
+__device__ __forceinline__ void copy_solo(const DeviceSnapshot &s, const uint32_t *rec, uint32_t nh, uint32_t Ss,
+                                          uint32_t lo, uint32_t hi, int gl, uint64_t *out, uint64_t db) {
+  constexpr uint32_t kStep = 2u * kE * kU;
+  // subs through a buffer descriptor: 32-bit offsets (one VGPR per load
+  // address instead of two) and bounds-checked reads (the snapshot pads the
+  // array by 64 B, so entry n_subs is readable)
+  const __amdgpu_buffer_rsrc_t subs =
+      __builtin_amdgcn_make_buffer_rsrc((void *)s.subs, (short)0, (int)(s.n_subs * 8u + 64u), 0x00020000);
+  auto issue = [&](uint32_t base, u32x4_a8 (&dst)[kU]) {
+    // addresses first (branch-free loads after: a load whose result merged
+    // out of two branches would need a wait before the register copy)
+    const uint32_t h0 = hit_of<kFieldSpre>(rec, nh, base);  // group-uniform
+    const uint32_t end0 = h0 + 1 < nh ? rec_at(rec, h0 + 1, kFieldSpre) : Ss;
+    const uint32_t d0 = rec_at(rec, h0, kFieldOff) - rec_at(rec, h0, kFieldSpre);
+    uint32_t sa[kU], sb[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const uint32_t q = base + 2u * (u * kE + gl);
+      sa[u] = d0 + q;
+      sb[u] = d0 + q + 1;
+    }
+    if (base + kStep > end0) {  // the step crosses a hit boundary: per-entry search
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+        const uint32_t q = base + 2u * (u * kE + gl);
+        sa[u] = solo_sid(rec, nh, q < hi ? q : lo);
+        sb[u] = solo_sid(rec, nh, q + 1 < hi ? q + 1 : lo);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const u32x2 a = __builtin_amdgcn_raw_buffer_load_b64(subs, (int)(sa[u] * 8u), 0, 0);
+      const u32x2 b = __builtin_amdgcn_raw_buffer_load_b64(subs, (int)(sb[u] * 8u), 0, 0);
+      dst[u] = u32x4_a8{a.x, a.y, b.x, b.y};
+    }
+  };
+  auto store = [&](uint32_t base, u32x4_a8 (&v)[kU]) {
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const uint32_t q = base + 2u * (u * kE + gl);
+      u32x4_a8 d = v[u];
+      d.y &= 0x7FFFFFFFu;  // SubEnt word -> delivery (snapshot.h)
+      d.w &= 0x7FFFFFFFu;
+      if (q + 1 < hi)
+        *reinterpret_cast<u32x4_a8 *>(out + db + q) = d;
+      else if (q < hi)
+        out[db + q] = ((uint64_t)d.y << 32) | d.x;
+    }
+  };
+  // latency is hidden by occupancy (many waves, kU 16-B accesses each) rather
+  // than by a software pipeline: a two-register-set pipeline made hipcc reuse
+  // registers with loads in flight and wait for them anyway
+  for (uint32_t base = lo; base < hi; base += kStep) {
+    u32x4_a8 v[kU];
+    issue(base, v);
+    store(base, v);
+  }
 }
 
 // Merge kMPer multi entries per lane of a kE-lane group in a table of
@@ -669,26 +740,7 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
         mw[k] = e.word;
       }
     }
-    uint64_t v[kU];
-    auto load_solo = [&](uint32_t base, uint64_t (&dst)[kU]) {
-#pragma unroll
-      for (int u = 0; u < kU; u++) {  // unconditional loads (entry 0 stands in past Ss)
-        const uint32_t q0 = base + u * kSE + gl;
-        const SubEnt e = load_sub(s, solo_sid(L.rec, nh, q0 < Ss ? q0 : 0));
-        dst[u] = solo_delivery(e);
-      }
-    };
-    if (Ss) load_solo(0, v);
-    for (uint32_t base = 0; base < Ss; base += kSE * kU) {
-      uint64_t nv[kU];
-      if (base + kSE * kU < Ss) load_solo(base + kSE * kU, nv);
-#pragma unroll
-      for (int u = 0; u < kU; u++) {
-        const uint32_t q = base + u * kSE + gl;
-        if (q < Ss) put_out(&o.dout[db + q], v[u]);
-        v[u] = nv[u];
-      }
-    }
+    copy_solo<kSE, kU>(s, L.rec, nh, Ss, 0, Ss, gl, o.dout, db);
     uint32_t D = Ss;
     if (M) D = merge_multi<kSE, kMPer>(L.tkey, L.tbits, L.tmin, 64, mcl, mw, mrk, M, gl, gbase, o.dout, db, D);
     if (gl == 0) o.dcount[t] = D;
@@ -699,8 +751,60 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
 // ---- k_copy: big-class items -------------------------------------------------
 struct alignas(16) CopyLds {
   uint32_t rec[kRecStrideAlloc];
+};
+
+// ---- k_merge: a wavefront per big-class topic with 0 < Ms <= kSmallMulti ------
+struct alignas(16) MergeLds {
+  uint32_t rec[kRecStrideAlloc];
   uint32_t tkey[kSmallSlots], tbits[kSmallSlots], tmin[kSmallSlots];
 };
+
+__global__ __launch_bounds__(kWave *kEmitWaves) void k_merge(DeviceSnapshot s, Outputs o,
+                                                            const uint32_t *__restrict__ list,
+                                                            const unsigned int *__restrict__ count) {
+  constexpr int kMPer = kSmallMulti / kWave;
+  __shared__ MergeLds lds_all[kEmitWaves];
+  const int lane = threadIdx.x & (kWave - 1);
+  MergeLds &L = lds_all[threadIdx.x / kWave];
+  const uint32_t nw = gridDim.x * kEmitWaves, nl = *count;
+  uint32_t i = blockIdx.x * kEmitWaves + threadIdx.x / kWave;
+  uint32_t n_t = 0, n_rw = 0;
+  uint64_t n_db = 0;
+  auto fetch = [&](uint32_t k) {
+    n_t = list[k];
+    n_db = o.dstart[n_t];
+    n_rw = o.recs[(uint64_t)n_t * kRecStrideAlloc + lane];
+  };
+  if (i < nl) fetch(i);
+  for (; i < nl; i += nw) {
+    const uint32_t t = n_t;
+    const uint64_t db = n_db;
+    L.rec[lane] = n_rw;
+    if (i + nw < nl) fetch(i + nw);
+    wave_lds_sync();
+    const uint32_t nh = L.rec[0] & 0xFFu, Ss = L.rec[1], M = L.rec[2];
+    const uint32_t *grec = o.recs + (uint64_t)t * kRecStrideAlloc;
+    for (uint32_t w = kWave + lane; w < 4 + kRecHit * nh; w += kWave) L.rec[w] = grec[w];
+    wave_lds_sync();
+    rec_prefix<kWave>(L.rec, nh, lane);
+    wave_lds_sync();
+    uint32_t mcl[kMPer], mw[kMPer], mrk[kMPer];
+#pragma unroll
+    for (int k = 0; k < kMPer; k++) {
+      const uint32_t q = lane + k * kWave;
+      uint32_t h;
+      const uint32_t sid = multi_sid(L.rec, nh, Ss, q < M ? q : 0, &h);
+      mrk[k] = rec_at(L.rec, h, kFieldRank);
+      const SubEnt e = load_sub(s, sid);
+      mcl[k] = e.client;
+      mw[k] = e.word;
+    }
+    const uint32_t D =
+        merge_multi<kWave, kMPer>(L.tkey, L.tbits, L.tmin, kSmallSlots, mcl, mw, mrk, M, lane, 0, o.dout, db, Ss);
+    if (lane == 0) o.dcount[t] = D;
+    wave_lds_sync();
+  }
+}
 
 // chunk items per big-class topic: ceil(Ss / kChunk), at least 1 (item 0 also
 // writes shared candidates, merges or hands on the multi entries, and dcount);
@@ -732,7 +836,6 @@ __global__ __launch_bounds__(256) void k_items(const uint32_t *__restrict__ list
 template <int kOcc, int kU>
 __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_eu(kOcc))) void k_copy(
     DeviceSnapshot s, Outputs o, const uint2 *__restrict__ items, uint64_t n_items) {
-  constexpr int kMPer = kSmallMulti / kWave;
   __shared__ CopyLds lds_all[kEmitWaves];
   const int lane = threadIdx.x & (kWave - 1);
   CopyLds &L = lds_all[threadIdx.x / kWave];
@@ -772,63 +875,10 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
         w += sc;
       }
     }
-    const bool merge_here = first && M > 0 && M <= kSmallMulti;
-    uint32_t mcl[kMPer], mw[kMPer], mrk[kMPer];
-    if (merge_here) {
-#pragma unroll
-      for (int k = 0; k < kMPer; k++) {
-        const uint32_t q = lane + k * kWave;
-        uint32_t h;
-        const uint32_t sid = multi_sid(L.rec, nh, Ss, q < M ? q : 0, &h);
-        mrk[k] = rec_at(L.rec, h, kFieldRank);
-        const SubEnt e = load_sub(s, sid);
-        mcl[k] = e.client;
-        mw[k] = e.word;
-      }
-    }
-    // solo entries [lo, hi) of the topic: delivery q = solo entry q.  When one
-    // hit holds a whole step of positions (hub ranges), no search at all.
+    // solo entries [lo, hi) of the topic: delivery q = solo entry q
     const uint32_t lo = j * kChunk, hi = min(Ss, lo + kChunk);
-    uint64_t v[kU];
-    auto load_solo = [&](uint32_t base, uint64_t (&dst)[kU]) {
-      const uint32_t h0 = hit_of<kFieldSpre>(L.rec, nh, base);  // wave-uniform
-      const uint32_t end0 = h0 + 1 < nh ? rec_at(L.rec, h0 + 1, kFieldSpre) : Ss;
-      const uint32_t d0 = rec_at(L.rec, h0, kFieldOff) - rec_at(L.rec, h0, kFieldSpre);
-      if (base + kWave * kU <= end0) {
-#pragma unroll
-        for (int u = 0; u < kU; u++) {
-          const uint32_t q = base + u * kWave + lane;
-          dst[u] = solo_delivery(load_sub(s, d0 + (q < hi ? q : base)));
-        }
-      } else {
-#pragma unroll
-        for (int u = 0; u < kU; u++) {
-          const uint32_t q = base + u * kWave + lane;
-          dst[u] = solo_delivery(load_sub(s, solo_sid(L.rec, nh, q < hi ? q : base)));
-        }
-      }
-    };
-    if (lo < hi) load_solo(lo, v);
-    for (uint32_t base = lo; base < hi; base += kWave * kU) {
-      uint64_t nv[kU];
-      if (base + kWave * kU < hi) load_solo(base + kWave * kU, nv);
-#pragma unroll
-      for (int u = 0; u < kU; u++) {
-        const uint32_t q = base + u * kWave + lane;
-        if (q < hi) put_out(&o.dout[db + q], v[u]);
-        v[u] = nv[u];
-      }
-    }
-    if (first) {
-      if (M > kSmallMulti) {  // the workgroup tier merges them and writes dcount
-        if (lane == 0) o.multi_list[atomicAdd(&o.ctr->n_multi, 1u)] = t;
-      } else {
-        uint32_t D = Ss;
-        if (merge_here)
-          D = merge_multi<kWave, kMPer>(L.tkey, L.tbits, L.tmin, kSmallSlots, mcl, mw, mrk, M, lane, 0, o.dout, db, D);
-        if (lane == 0) o.dcount[t] = D;
-      }
-    }
+    copy_solo<kWave, kU>(s, L.rec, nh, Ss, lo, hi, lane, o.dout, db);
+    if (first && M == 0 && lane == 0) o.dcount[t] = Ss;  // else k_merge / k_multi write it
     wave_lds_sync();
   }
 }
@@ -1224,6 +1274,19 @@ struct IsBigClass {
   const uint8_t *cls;
   __host__ __device__ bool operator()(uint32_t t) const { return cls[t] == kClsBig; }
 };
+// big-class topics by the merge that dedupes their multi entries
+struct IsWaveMerge {
+  const uint8_t *cls;
+  const uint32_t *mcount;
+  __host__ __device__ bool operator()(uint32_t t) const {
+    return cls[t] == kClsBig && mcount[t] != 0 && mcount[t] <= kSmallMulti;
+  }
+};
+struct IsGroupMerge {
+  const uint8_t *cls;
+  const uint32_t *mcount;
+  __host__ __device__ bool operator()(uint32_t t) const { return cls[t] == kClsBig && mcount[t] > kSmallMulti; }
+};
 
 #define HIP_TRY(x)                                                                                        \
   do {                                                                                                    \
@@ -1358,7 +1421,7 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   if (ws.get(W::kSCount, sizeof(uint32_t) * (n + 1)) || ws.get(W::kHCount, sizeof(uint32_t) * (n + 1)) ||
       ws.get(W::kDCount, sizeof(uint32_t) * (n + 1)) || ws.get(W::kDStart, sizeof(uint64_t) * (n + 1)) ||
       ws.get(W::kHStart, sizeof(uint64_t) * (n + 1)) || ws.get(W::kCls, n + 1) ||
-      ws.get(W::kDfsList, sizeof(uint32_t) * (n + 2)) ||
+      ws.get(W::kDfsList, sizeof(uint32_t) * (n + 2)) || ws.get(W::kMCount, sizeof(uint32_t) * (n + 1)) ||
       ws.get(W::kRecs, sizeof(uint32_t) * kRecStrideAlloc * ((uint64_t)n + 1)) || ws.get(W::kCounters, 256))
     return -2;
   if (!ws.host_pinned && hipHostMalloc(&ws.host_pinned, 256, hipHostMallocDefault) != hipSuccess) return -2;
@@ -1374,9 +1437,9 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   o.hstart = (uint64_t *)ws.ptr(W::kHStart);
   o.cls = (uint8_t *)ws.ptr(W::kCls);
   o.dfs_list = (uint32_t *)ws.ptr(W::kDfsList);
+  o.mcount = (uint32_t *)ws.ptr(W::kMCount);
   o.recs = (uint32_t *)ws.ptr(W::kRecs);
   o.ctr = (Counters *)ws.ptr(W::kCounters);
-  // the big-topic list reuses the DFS list's tail? no: its own region after the record array
   const int walk_g = ws.walk_lanes;
   HIP_TRY(hipMemsetAsync(o.ctr, 0, sizeof(Counters), st));
   mark(ws, 0, st);
@@ -1403,8 +1466,11 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   // emit lists (small class + shared-only topics; big class) and the big
   // class's chunk items, counted before the one host sync that sizes the outputs
   if (ws.get(W::kListS, sizeof(uint32_t) * (n + 1)) || ws.get(W::kListB, sizeof(uint32_t) * (n + 1)) ||
-      ws.get(W::kNChunk, sizeof(uint32_t) * (n + 1)) || ws.get(W::kCStart, sizeof(uint64_t) * (n + 1)))
+      ws.get(W::kNChunk, sizeof(uint32_t) * (n + 1)) || ws.get(W::kCStart, sizeof(uint64_t) * (n + 1)) ||
+      ws.get(W::kDense, sizeof(uint32_t) * (n + 1)) || ws.get(W::kListW, sizeof(uint32_t) * (n + 1)))
     return -2;
+  o.multi_list = (uint32_t *)ws.ptr(W::kDense);
+  auto *list_w = (uint32_t *)ws.ptr(W::kListW);
   auto *list_s = (uint32_t *)ws.ptr(W::kListS), *list_b = (uint32_t *)ws.ptr(W::kListB);
   auto *nchunk = (uint32_t *)ws.ptr(W::kNChunk);
   auto *cstart = (uint64_t *)ws.ptr(W::kCStart);
@@ -1416,6 +1482,10 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
     HIP_TRY(hipcub::DeviceSelect::If(ws.ptr(W::kScanTmp), tmp, it, list_s, &o.ctr->n_small, n,
                                      IsSmallClass{o.cls, o.hcount}, st));
     HIP_TRY(hipcub::DeviceSelect::If(ws.ptr(W::kScanTmp), tmp, it, list_b, &o.ctr->n_bigc, n, IsBigClass{o.cls}, st));
+    HIP_TRY(hipcub::DeviceSelect::If(ws.ptr(W::kScanTmp), tmp, it, list_w, &o.ctr->n_wmerge, n,
+                                     IsWaveMerge{o.cls, o.mcount}, st));
+    HIP_TRY(hipcub::DeviceSelect::If(ws.ptr(W::kScanTmp), tmp, it, o.multi_list, &o.ctr->n_multi, n,
+                                     IsGroupMerge{o.cls, o.mcount}, st));
     hipLaunchKernelGGL(k_chunks, dim3(std::min<uint32_t>((n + 255) / 256, 4096)), dim3(256), 0, st, o, list_b,
                        &o.ctr->n_bigc, n, nchunk);
     HIP_TRY(hipGetLastError());
@@ -1471,13 +1541,10 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   }
   // outputs: scanned segments, then the DFS tails
   if (ws.get(W::kDOut, sizeof(uint64_t) * (s_total + dfs_raw + 1)) ||
-      ws.get(W::kHOut, sizeof(uint32_t) * (h_total + dfs_h + 1)) ||
-      ws.get(W::kDense, sizeof(uint32_t) * (n + 1)) ||  // multi list
-      ws.get(W::kItems, sizeof(uint2) * (n_items + 1)))
+      ws.get(W::kHOut, sizeof(uint32_t) * (h_total + dfs_h + 1)) || ws.get(W::kItems, sizeof(uint2) * (n_items + 1)))
     return -2;
   o.dout = (uint64_t *)ws.ptr(W::kDOut);
   o.hout = (uint32_t *)ws.ptr(W::kHOut);
-  o.multi_list = (uint32_t *)ws.ptr(W::kDense);
   auto *items = (uint2 *)ws.ptr(W::kItems);
 
   mark(ws, 2, st);
@@ -1491,10 +1558,12 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
       hipLaunchKernelGGL(k_items, dim3(std::min<uint32_t>((n + 255) / 256, 4096)), dim3(256), 0, st, list_b,
                          &o.ctr->n_bigc, cstart, items);
       HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL((k_copy<5, kEmitU>), grid(k_copy<5, kEmitU>), dim3(kWave * kEmitWaves), 0, st, s, o, items,
+      hipLaunchKernelGGL((k_copy<8, kEmitU>), grid(k_copy<8, kEmitU>), dim3(kWave * kEmitWaves), 0, st, s, o, items,
                          n_items);
       HIP_TRY(hipGetLastError());
     }
+    hipLaunchKernelGGL(k_merge, grid(k_merge), dim3(kWave * kEmitWaves), 0, st, s, o, list_w, &o.ctr->n_wmerge);
+    HIP_TRY(hipGetLastError());
     if (ws.get(W::kOvfList, sizeof(uint32_t) * (n + 1))) return -2;
     auto *ovf = (uint32_t *)ws.ptr(W::kOvfList);
     if (ws.get(W::kOvfList2, sizeof(uint32_t) * (n + 1))) return -2;
