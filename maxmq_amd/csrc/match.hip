@@ -79,8 +79,10 @@ constexpr int kRecStrideAlloc = 228;                  // 16-B aligned per topic
 constexpr uint32_t kSMax = 16384;        // raw entries per topic on the bounded path
 constexpr int kEmitU = 4;                // solo entries in flight per lane
 constexpr int kEmitWaves = 4;
-constexpr int kSmallLanes = 16;          // k_emit_small: lanes per topic of the small class
-constexpr uint32_t kSmallSolo = 256;     // small class: at most this many solo entries
+constexpr int kSmallLanes = 8;           // k_emit_small: lanes per topic of the small class
+constexpr uint32_t kSmallSolo = 256;     // small class: at most this many solo entries,
+constexpr uint32_t kSmallHits = 15;      //   hits (its record is one 64-word prefetch)
+constexpr uint32_t kSmallMultiS = 3 * kSmallLanes;  //   and multi entries
 constexpr int kSmallSlots = 256;         // k_emit merge table slots (per wave)
 constexpr int kSmallMulti = 192;         // multi entries it holds (load <= 0.75)
 constexpr int kBigThreads = 256;
@@ -230,9 +232,9 @@ __device__ __forceinline__ uint32_t table_find(const uint32_t *tkey, uint32_t ma
 // k_walk wrote them); its readers turn them into exclusive prefixes in LDS
 // (find_hits searches those).  A group of kL aligned lanes (kL <= 64, a power
 // of two) converts hits 0 .. nh - 1.
-template <int kL>
+template <int kL, int kCap = kHCap>
 __device__ __forceinline__ void rec_prefix(uint32_t *rec, uint32_t nh, int gl) {
-  constexpr int kP = (kHCap + kL - 1) / kL;
+  constexpr int kP = (kCap + kL - 1) / kL;
   uint32_t sc[kP], mc[kP], ss = 0, ms = 0;
 #pragma unroll
   for (int p = 0; p < kP; p++) {
@@ -476,7 +478,7 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
       }
       o.cls[t] = dfs ? kClsDfs
                  : S == 0 ? kClsDone
-                 : (Ss <= kSmallSolo && Ms <= 3u * kSmallLanes) ? kClsSmall
+                 : (Ss <= kSmallSolo && Ms <= kSmallMultiS && nh <= kSmallHits) ? kClsSmall
                                                                  : kClsBig;
       o.scount[t] = dfs ? 0 : S;
       o.hcount[t] = dfs ? 0 : H;
@@ -497,10 +499,10 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
 // client's merged delivery as is (delivery q = solo entry q), then the
 // winners of the merge of its multi entries, compacted.  dcount[t] = Ss +
 // winners.  Three kernels by size:
-//   k_emit_small  16 lanes per topic (4 topics per wavefront) for topics with
-//                 Ss <= kSmallSolo and Ms <= 3 * 16: solo copy + a 64-slot
-//                 LDS merge table; also every topic with shared candidates
-//                 only.
+//   k_emit_small  8 lanes per topic (8 topics per wavefront) for topics with
+//                 Ss <= kSmallSolo, Ms <= 24 and <= 15 hits: solo copy + a
+//                 64-slot LDS merge table; also every topic with shared
+//                 candidates only.
 //   k_copy        the big class, cut into items of kChunk solo entries (a
 //                 wavefront per item, static striding over equal-sized
 //                 items: no Zipf hub topic holds a wave for long).  Item 0 of
@@ -647,21 +649,24 @@ __device__ __forceinline__ uint32_t merge_multi(uint32_t *tkey, uint32_t *tbits,
 }
 
 // ---- k_emit_small -------------------------------------------------------------
-constexpr int kSE = 16;                          // lanes per topic
+// kSmallLanes lanes per topic (8 topics per wavefront): the topic's whole
+// record (header + <= kSmallHits hits = 64 words) is prefetched one topic
+// ahead and its list entry two ahead, so a topic costs one dependent round
+// trip (its subscription entries) after its record arrives.
+constexpr int kSE = kSmallLanes;
 constexpr int kSGroups = kWave / kSE;
-constexpr uint32_t kSMulti = 3 * kSE;            // multi entries merged here
-constexpr int kSRecPer = MQM_REC16_WORDS / kSE;  // record words prefetched per lane
-static_assert(kSRecPer % 4 == 0 && kSRecPer * kSE <= kRecStrideAlloc, "record prefetch");
+constexpr int kSRecPer = 64 / kSE;  // record words prefetched per lane
+static_assert(4 + kRecHit * kSmallHits <= 64 && kSRecPer % 4 == 0, "small-class record prefetch");
 
 struct alignas(16) SmallLds {
-  uint32_t rec[kRecStrideAlloc];
+  uint32_t rec[64];
   uint32_t tkey[64], tbits[64], tmin[64];
 };
 
 template <int kOcc, int kU>
 __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_eu(kOcc))) void k_emit_small(
     DeviceSnapshot s, Outputs o, const uint32_t *__restrict__ list, const unsigned int *__restrict__ count) {
-  constexpr int kMPer = kSMulti / kSE, kRecPer = kSRecPer;
+  constexpr int kMPer = kSmallMultiS / kSE, kRecPer = kSRecPer;
   __shared__ SmallLds lds_all[kEmitWaves * kSGroups];
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / kSE, gl = lane % kSE, gbase = g * kSE;
@@ -669,8 +674,6 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
   const uint32_t ngroups = gridDim.x * kEmitWaves * kSGroups;
   const uint32_t nl = *count;
   uint32_t i = (blockIdx.x * kEmitWaves + threadIdx.x / kWave) * kSGroups + g;
-  // list entries two topics ahead; the next topic's header and its record's
-  // first kRecPer * kSE words one topic ahead
   uint32_t n_H = 0, n_rw[kRecPer];
   uint64_t n_db = 0, n_hb = 0;
   auto fetch = [&](uint32_t u) {
@@ -698,26 +701,10 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
     wave_lds_sync();
     const uint32_t w0 = L.rec[0], Ss = L.rec[1], M = L.rec[2];
     const uint32_t nh = w0 & 0xFFu, nsh = w0 >> 8;
-    const uint32_t *grec = o.recs + (uint64_t)t * kRecStrideAlloc;
-    {  // the hits past the prefetched words: one round trip of 16-B loads
-      constexpr int kPre = kRecPer * kSE, kT = (kRecStride - kPre + 4 * kSE - 1) / (4 * kSE);
-      const uint32_t nw = 4 + kRecHit * nh;
-      uint4 tv[kT];
-#pragma unroll
-      for (int k = 0; k < kT; k++) {
-        const uint32_t w = kPre + 4 * (k * kSE + gl);
-        tv[k] = *reinterpret_cast<const uint4 *>(grec + (w < nw ? w : kPre));
-      }
-#pragma unroll
-      for (int k = 0; k < kT; k++) {
-        const uint32_t w = kPre + 4 * (k * kSE + gl);
-        if (w < nw) *reinterpret_cast<uint4 *>(&L.rec[w]) = tv[k];
-      }
-    }
-    wave_lds_sync();
-    rec_prefix<kSE>(L.rec, nh, gl);
+    rec_prefix<kSE, kSmallHits>(L.rec, nh, gl);
     wave_lds_sync();
     if (H) {  // shared candidates (gatherSharedSubscriptions, topics.go:541-555)
+      const uint32_t *grec = o.recs + (uint64_t)t * kRecStrideAlloc;
       uint32_t w = 0;
       for (uint32_t j = 0; j < nsh; j++) {
         const uint32_t so = grec[kRecSh + 2 * j], sc = grec[kRecSh + 1 + 2 * j];
@@ -725,8 +712,7 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
         w += sc;
       }
     }
-    // loads before stores (one in-order vmcnt per wave): the multi entries and
-    // the first solo chunk are loaded before any store of the topic
+    // the multi entries are loaded before any store of the topic
     uint32_t mcl[kMPer], mw[kMPer], mrk[kMPer];
     if (M) {
 #pragma unroll
@@ -1551,7 +1537,7 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   static_assert(kWave * kEmitWaves == kBigThreads, "resident_blocks assumes 256-thread blocks");
   if (n > 0) {
     auto grid = [&](auto kern) { return dim3(resident_blocks(ws, 0, kern)); };
-    hipLaunchKernelGGL((k_emit_small<1, kEmitU>), grid(k_emit_small<1, kEmitU>), dim3(kWave * kEmitWaves), 0, st, s,
+    hipLaunchKernelGGL((k_emit_small<5, kEmitU>), grid(k_emit_small<5, kEmitU>), dim3(kWave * kEmitWaves), 0, st, s,
                        o, list_s, &o.ctr->n_small);
     HIP_TRY(hipGetLastError());
     if (n_items) {

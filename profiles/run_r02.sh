@@ -25,6 +25,8 @@ for step in "$@"; do
     smoke) timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 ;;
     bench) timeout -k 10 600 python3 -u bench.py > $OUT/bench.json 2> $OUT/bench.log ;;
     fast) timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast.json 2> $OUT/bench_fast.log ;;
+    lanes) for L in 4 16; do MQM_WALK_LANES=$L timeout -k 10 400 python3 -u bench.py $FAST \
+             > $OUT/bench_fast_lanes$L.json 2> $OUT/bench_fast_lanes$L.log; done ;;
     prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv \
              -d $OUT/prof -o prof -- python3 $ROOT/bench.py $FAST \
              > $OUT/bench_under_rocprof.json 2> $OUT/rocprof.log) ;;
