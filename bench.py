@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--filters", type=int, default=0, help="override n_filters")
     ap.add_argument("--topics", type=int, default=0, help="override n_topics")
     ap.add_argument("--mode", choices=["replicas", "sharded"], default="replicas")
+    ap.add_argument("--shard", default="",
+                    help="R/N: this one GPU matches shard R of the N-way subscriber-sharded config "
+                         "(the per-shard cost of a node run, e.g. --config 4 --shard 0/8)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU baseline threads (0 = one per CPU this process may run on, BASELINE.md §2)")
@@ -187,18 +190,22 @@ def main():
         overrides["n_filters"] = args.filters
     if args.topics:
         overrides["n_topics"] = args.topics
+    sharded = args.mode == "sharded" and world > 1
+    shard_of = tuple(int(x) for x in args.shard.split("/")) if args.shard else None
     t0 = time.time()
-    w = mqgen.generate(args.config, **overrides)
+    if sharded:  # this rank's client range only (a 100M-filter config is never whole on one host)
+        w = shard.generated_shard(args.config, world, rank, **overrides)
+    elif shard_of:
+        w = shard.generated_shard(args.config, shard_of[1], shard_of[0], **overrides)
+    else:
+        w = mqgen.generate(args.config, **overrides)
     n = len(w.topics)
     log(f"[rank {rank}] generated {len(w.filters)} filters / {n} topics in {time.time() - t0:.1f}s")
 
     # ---- build the index (host store -> snapshot -> HBM) -------------------------------
     t0 = time.time()
     idx = maxmq_amd.TopicsIndex(device=local, autocommit=False)
-    if args.mode == "sharded" and world > 1:
-        idx.subscribe_workload(shard.shard_workload(w, world, rank))
-    else:
-        idx.subscribe_workload(w)
+    idx.subscribe_workload(w)
     idx.commit()
     snap = idx.snapshot_stats()
     log(f"[rank {rank}] index built in {time.time() - t0:.1f}s: {snap}")
@@ -206,13 +213,21 @@ def main():
     tb = torch.from_numpy(w.topics.data).to(dev)
     to = torch.from_numpy(w.topics.offs.view(np.int64)).to(dev)
     stream = torch.cuda.current_stream(dev)
-    sharded = args.mode == "sharded" and world > 1
     if sharded:
-        # shard client id -> node client id, per rank (rank 0 lays the gathered
-        # lists out with them); node-wide result buffers on rank 0
-        cmaps = [torch.from_numpy(shard.client_map(w, world, r).astype(np.int32)).to(dev) for r in range(world)]
-        node = {"offs": torch.zeros(n + 1, dtype=torch.int64, device=dev), "d": None}
-        my = {"offs": torch.zeros(n + 1, dtype=torch.int64, device=dev), "d": None}
+        # shard client id -> node client id (the generator's global client
+        # index), every rank's map held by rank 0, which lays the gathered
+        # lists out; node-wide result buffers on rank 0
+        mine = torch.from_numpy(shard.local_client_map(w).astype(np.int32)).to(dev)
+        cmaps = shard.gather_maps(dist, mine, dst=0)
+        node = {"offs": torch.zeros(n + 1, dtype=torch.int64, device=dev), "d": None,
+                "soffs": torch.zeros(n + 1, dtype=torch.int64, device=dev), "s": None}
+        my = {"offs": torch.zeros(n + 1, dtype=torch.int64, device=dev), "d": None,
+              "soffs": torch.zeros(n + 1, dtype=torch.int64, device=dev), "s": None}
+
+    def grow(buf, key, count, dtype):
+        if buf[key] is None or buf[key].numel() < count:
+            buf[key] = torch.empty(max(count, 1), dtype=dtype, device=dev)
+        return buf[key][:count]
 
     def step():
         if sharded:
@@ -220,22 +235,27 @@ def main():
             shard.broadcast_batch(dist, tb, to, src=0)
         r = idx.match_device(tb.data_ptr(), to.data_ptr(), n, stream.cuda_stream)
         if sharded:
-            # this shard's dense per-topic lists -> rank 0 (RCCL send/recv),
-            # laid out there as the node-wide CSR (mqm_gather_shards)
+            # this shard's dense per-topic lists (deliveries and shared
+            # candidates) -> rank 0 (RCCL send/recv), laid out there as the
+            # node-wide CSRs (mqm_gather_shards, mqm_gather_shards_shared)
             d = idx.dense_device(stream.cuda_stream)
-            nd = int(d.n_deliveries)
-            if my["d"] is None or my["d"].numel() < nd:
-                my["d"] = torch.empty(max(nd, 1), dtype=torch.int64, device=dev)
+            nd, ns = int(d.n_deliveries), int(d.n_shared)
             _dev_to_tensor(d.offsets, my["offs"])
-            _dev_to_tensor(d.deliveries, my["d"][:nd])
+            _dev_to_tensor(d.deliveries, grow(my, "d", nd, torch.int64))
+            _dev_to_tensor(d.shared_offsets, my["soffs"])
+            _dev_to_tensor(d.shared, grow(my, "s", ns, torch.int32))
             parts = shard.gather_lists(dist, my["offs"], my["d"][:nd], dst=0)
+            sparts = shard.gather_lists(dist, my["soffs"], my["s"][:ns], dst=0)
             if rank == 0:
                 tot = sum(int(p[1].numel()) for p in parts)
-                if node["d"] is None or node["d"].numel() < tot:
-                    node["d"] = torch.empty(max(tot, 1), dtype=torch.int64, device=dev)
+                stot = sum(int(p[1].numel()) for p in sparts)
                 maxmq_amd.gather_shards(n, [(o.data_ptr(), dl.data_ptr(), cmaps[i].data_ptr(), cmaps[i].numel())
                                             for i, (o, dl) in enumerate(parts)],
-                                        node["offs"].data_ptr(), node["d"].data_ptr(), stream.cuda_stream)
+                                        node["offs"].data_ptr(), grow(node, "d", tot, torch.int64).data_ptr(),
+                                        stream.cuda_stream)
+                maxmq_amd.gather_shards_shared(n, [(o.data_ptr(), sl.data_ptr()) for o, sl in sparts],
+                                               node["soffs"].data_ptr(), grow(node, "s", stot, torch.int32).data_ptr(),
+                                               stream.cuda_stream)
         return r
 
     for _ in range(args.warmup):
@@ -274,8 +294,8 @@ def main():
         dist.all_reduce(dsum)
         deliveries, shared = int(dsum[0].item()), int(dsum[1].item())
 
-    if args.mode == "sharded" and world > 1:
-        topics_total = n * args.steps  # every shard walks the same batch
+    if sharded:
+        topics_total = n * args.steps  # every shard walks the same batch: node-wide lists of n topics per step
     else:
         topics_total = n * args.steps * world
     value = topics_total / dt
@@ -299,17 +319,19 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": dt * 1e3 / args.steps,
             "higher_is_better": True,
-            "scaling": "weak" if args.mode == "replicas" else "strong",
+            "scaling": "strong" if sharded else "weak",
             "vs_baseline": None,
             "dtype": "u8/u32 (byte+integer matching)",
             "data": "synthetic (tools/mqgen, deterministic seed); inputs resident in HBM",
             "config": {
-                "workload": f"mqgen config {args.config}: {len(w.filters)} filters "
+                "workload": (f"mqgen config {args.config} shard {shard_of[0]}/{shard_of[1]} (client range), " if shard_of
+                             else f"mqgen config {args.config} {args.mode} over {world} GPU(s), " if sharded else
+                             f"mqgen config {args.config}: ") + f"{len(w.filters)} filters "
                             f"({w.params['p_plus']:.0%} '+', {w.params['p_hash']:.0%} '#', "
                             f"topic Zipf s={w.params['topic_zipf_s']}), {n}-topic batch, depth<={w.params['max_depth']}",
                 "filters": len(w.filters),
                 "topics_per_batch": n,
-                "parallelism": f"{args.mode}{world}",
+                "parallelism": f"{args.mode}{world}" if not shard_of else f"shard{shard_of[0]}of{shard_of[1]}",
             },
             "deliveries_per_s": deliveries / dt,
             "shared_candidates_per_s": shared / dt,

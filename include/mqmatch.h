@@ -283,6 +283,24 @@ typedef struct {
 } mqm_shard_part;
 int mqm_gather_shards(uint32_t n_topics, uint32_t n_shards, const mqm_shard_part *parts, void *hip_stream,
                       uint64_t *d_out_offsets, mqm_delivery *d_out);
+/* The shared-subscription candidates of the same shards (gatherSharedSubscriptions,
+ * topics.go:541-555): a shared subscription belongs to its client's shard, so
+ * the shards' candidate sets are disjoint too.  Each part is a shard's dense
+ * shared CSR (mqm_device_dense.shared_offsets / .shared); topic t's node-wide
+ * candidates are shard 0's, then shard 1's, ..., each entry
+ * MQM_SHARD_SHARED(shard, id) with the shard-local shared id (resolve it on
+ * that shard's index).  d_out_offsets: n_topics + 1; d_out: the sum of the
+ * shards' candidate counts.  Synchronises hip_stream; MQM_EINVAL if an id
+ * does not fit 28 bits or n_shards is 0 or > 16. */
+typedef struct {
+  const uint64_t *offsets; /* device, n_topics + 1                              */
+  const uint32_t *shared;  /* device: shard-local shared-subscription ids       */
+} mqm_shard_shared_part;
+#define MQM_SHARD_SHARED(shard, id) (((uint32_t)(shard) << 28) | (uint32_t)(id))
+#define MQM_SHARED_SHARD(v) ((v) >> 28)
+#define MQM_SHARED_ID(v) ((v) & 0x0FFFFFFFu)
+int mqm_gather_shards_shared(uint32_t n_topics, uint32_t n_shards, const mqm_shard_shared_part *parts,
+                             void *hip_stream, uint64_t *d_out_offsets, uint32_t *d_out);
 
 /* ---- reverse match: TopicsIndex.Messages (topics.go:426-480) ------------ */
 /* The message refs retained under each filter (the message_ref given to

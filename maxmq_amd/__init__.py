@@ -445,6 +445,17 @@ def gather_shards(n_topics: int, parts, d_out_offsets_ptr: int, d_out_ptr: int, 
                                                        C.c_void_p(d_out_offsets_ptr), C.c_void_p(d_out_ptr)))
 
 
+def gather_shards_shared(n_topics: int, parts, d_out_offsets_ptr: int, d_out_ptr: int, stream_ptr: int = 0):
+    """mqm_gather_shards_shared: node-wide shared candidates of a
+    subscriber-sharded match.  parts: (shared_offsets_ptr, shared_ids_ptr) per
+    shard (device pointers); entries come out as shard << 28 | shard-local id."""
+    arr = (capi.ShardSharedPart * max(1, len(parts)))()
+    for i, (o, d) in enumerate(parts):
+        arr[i] = capi.ShardSharedPart(o, d)
+    check("mqm_gather_shards_shared", lib().mqm_gather_shards_shared(
+        n_topics, len(parts), arr, C.c_void_p(stream_ptr), C.c_void_p(d_out_offsets_ptr), C.c_void_p(d_out_ptr)))
+
+
 def is_valid_filter(filt: str, for_publish: bool) -> bool:
     """IsValidFilter (topics.go:586-624)."""
     f = b(filt)

@@ -43,7 +43,7 @@ EXPORTED = [
     "mqm_messages_refs", "mqm_messages_free", "mqm_messages_device", "mqm_identifiers_device",
     "mqm_result_identifiers", "mqm_dense_device", "mqm_gather_shards", "mqm_commit_async", "mqm_commit_poll",
     "mqm_commit_policy", "mqm_commit_state_get", "mqm_snapshot_digest", "mqm_unsubscribe_many", "mqm_load_subscriptions_json",
-    "mqm_debug_fault",
+    "mqm_debug_fault", "mqm_gather_shards_shared",
 ]
 
 
@@ -100,6 +100,10 @@ class DeviceDense(C.Structure):
 class ShardPart(C.Structure):
     _fields_ = [("offsets", C.c_void_p), ("deliveries", C.c_void_p), ("client_map", C.c_void_p),
                 ("n_map", C.c_uint32)]
+
+
+class ShardSharedPart(C.Structure):
+    _fields_ = [("offsets", C.c_void_p), ("shared", C.c_void_p)]
 
 
 class SnapshotStats(C.Structure):
@@ -184,6 +188,7 @@ def lib():
         "mqm_commit_state_get": ([vp, C.POINTER(CommitState)], C.c_int),
         "mqm_snapshot_digest": ([vp, C.POINTER(u64)], C.c_int),
         "mqm_debug_fault": ([vp, C.c_int, C.c_int], C.c_int),
+        "mqm_gather_shards_shared": ([u32, u32, C.POINTER(ShardSharedPart), vp, vp, vp], C.c_int),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

@@ -122,7 +122,7 @@ struct mqm_index {
   std::chrono::steady_clock::time_point journal_t0;
   uint64_t builds = 0, last_build_ops = 0;
   double last_build_ms = 0;
-  int walk_lanes = 8;
+  int walk_lanes = 4;
   bool async() const { return (cfg.flags & MQM_CFG_ASYNC_COMMIT) != 0; }
   // the device-result API's context (mqm_match_device & follow-ups)
   std::mutex dev_mu;
@@ -376,7 +376,7 @@ int mqm_create(const mqm_config *cfg, mqm_index **out) {
     if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
     if (const char *e = getenv("MQM_WALK_LANES")) {  // tuning knob, read once per index
       const int g = atoi(e);
-      h->walk_lanes = g == 4 || g == 16 ? g : 8;
+      h->walk_lanes = g == 8 || g == 16 ? g : 4;
     }
     if (ctx_init(h.get(), &h->dev) != MQM_OK) return MQM_EHIP;
     *out = h.release();
@@ -709,27 +709,56 @@ int mqm_dense_device(mqm_index *h, void *hip_stream, mqm_device_dense *out) {
   });
 }
 
+namespace {
+// device-visible status word for the gather kernels (pinned, mapped)
+int gather_status(unsigned int **host, unsigned int **dev) {
+  static unsigned int *bad = nullptr;
+  if (!bad && hipHostMalloc((void **)&bad, sizeof(unsigned int), hipHostMallocMapped) != hipSuccess) {
+    bad = nullptr;
+    return MQM_EHIP;
+  }
+  *bad = 0;
+  *host = bad;
+  return hipHostGetDevicePointer((void **)dev, bad, 0) == hipSuccess ? MQM_OK : MQM_EHIP;
+}
+std::mutex gather_mu;
+}  // namespace
+
 int mqm_gather_shards(uint32_t n_topics, uint32_t n_shards, const mqm_shard_part *parts, void *hip_stream,
                       uint64_t *d_out_offsets, mqm_delivery *d_out) {
   if (!parts || !d_out_offsets || n_shards == 0 || n_shards > (uint32_t)kMaxShards) return MQM_EINVAL;
   return guarded([&] {
-    // device-visible status word (pinned, mapped): a client id outside its map
-    static std::mutex mu;
-    static unsigned int *bad = nullptr;
-    std::lock_guard<std::mutex> g(mu);
-    if (!bad && hipHostMalloc((void **)&bad, sizeof(unsigned int), hipHostMallocMapped) != hipSuccess) {
-      bad = nullptr;
-      return MQM_EHIP;
-    }
-    *bad = 0;
+    std::lock_guard<std::mutex> g(gather_mu);
+    unsigned int *bad = nullptr, *dbad = nullptr;
+    if (gather_status(&bad, &dbad) != MQM_OK) return MQM_EHIP;
     ShardPart p[kMaxShards];
     for (uint32_t r = 0; r < n_shards; r++)
       p[r] = ShardPart{parts[r].offsets, reinterpret_cast<const uint64_t *>(parts[r].deliveries),
                        parts[r].client_map, parts[r].n_map};
-    unsigned int *dbad = nullptr;
-    if (hipHostGetDevicePointer((void **)&dbad, bad, 0) != hipSuccess) return MQM_EHIP;
     const int rc = gather_shards(n_topics, n_shards, p, (hipStream_t)hip_stream, d_out_offsets,
                                  reinterpret_cast<uint64_t *>(d_out), dbad);
+    if (rc == -1) return MQM_EINVAL;
+    if (rc != 0) return MQM_EHIP;
+    if (hipStreamSynchronize((hipStream_t)hip_stream) != hipSuccess) return MQM_EHIP;
+    return *(volatile unsigned int *)bad ? MQM_EINVAL : MQM_OK;
+  });
+}
+
+int mqm_gather_shards_shared(uint32_t n_topics, uint32_t n_shards, const mqm_shard_shared_part *parts,
+                             void *hip_stream, uint64_t *d_out_offsets, uint32_t *d_out) {
+  if (!parts || !d_out_offsets || n_shards == 0 || n_shards > (uint32_t)kMaxShards) return MQM_EINVAL;
+  return guarded([&] {
+    std::lock_guard<std::mutex> g(gather_mu);
+    unsigned int *bad = nullptr, *dbad = nullptr;
+    if (gather_status(&bad, &dbad) != MQM_OK) return MQM_EHIP;
+    const uint64_t *offs[kMaxShards];
+    const uint32_t *ids[kMaxShards];
+    for (uint32_t r = 0; r < n_shards; r++) {
+      offs[r] = parts[r].offsets;
+      ids[r] = parts[r].shared;
+    }
+    const int rc = gather_shards_shared(n_topics, n_shards, offs, ids, (hipStream_t)hip_stream, d_out_offsets, d_out,
+                                        dbad);
     if (rc == -1) return MQM_EINVAL;
     if (rc != 0) return MQM_EHIP;
     if (hipStreamSynchronize((hipStream_t)hip_stream) != hipSuccess) return MQM_EHIP;

@@ -309,6 +309,7 @@ int flatten(const Store &st, HostSnapshot *out) {
     hs.height = std::max(hs.height, height_c[c]);
   }
   if (sub_base[kNChunks] > kMaxSubs) return MQM_ELIMIT;
+  if (sh_base[kNChunks] > kMaxSubs) return MQM_ELIMIT;  // shared ids fit 28 bits (mqm_gather_shards_shared)
   hs.subs.resize(sub_base[kNChunks]);
   hs.sub_info.resize(sub_base[kNChunks]);
   hs.shared_info.resize(sh_base[kNChunks]);

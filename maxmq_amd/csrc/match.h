@@ -27,7 +27,7 @@ struct Workspace {
   Buf bufs[kNumSlots];
   void *host_pinned = nullptr;
   uint32_t max_blocks = 2048;  // walk-kernel grid cap (grid-stride beyond)
-  int walk_lanes = 8;          // lanes per topic in k_walk (4, 8 or 16; env MQM_WALK_LANES)
+  int walk_lanes = 4;          // lanes per topic in k_walk (4, 8 or 16; env MQM_WALK_LANES; C3: 7.9 / 8.8 / 11.0 ms)
   std::unordered_map<const void *, uint32_t> resident;  // kernel -> resident blocks on the device
   // why the last batch's DFS topics left the bounded path:
   // frontier, hits, cached levels, shared hits, raw entries

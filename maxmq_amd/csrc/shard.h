@@ -8,6 +8,7 @@
 namespace mqm {
 
 constexpr int kMaxShards = 16;
+constexpr uint32_t kShardShift = 28;  // node-wide shared candidate = shard << 28 | shard-local shared id
 
 struct ShardPart {
   const uint64_t *offsets;     // device, n + 1 (dense CSR of one shard)
@@ -21,5 +22,10 @@ struct ShardPart {
 // arguments, -3 on a launch error.
 int gather_shards(uint32_t n, uint32_t S, const ShardPart *parts, hipStream_t st, uint64_t *out_offsets,
                   uint64_t *out, unsigned int *d_bad);
+
+// shared candidates of the shards (dense CSRs: offsets n + 1, u32 shared ids)
+// -> one node-wide CSR of shard << kShardShift | id; an id >= 2^kShardShift sets *d_bad
+int gather_shards_shared(uint32_t n, uint32_t S, const uint64_t *const *offsets, const uint32_t *const *shared,
+                         hipStream_t st, uint64_t *out_offsets, uint32_t *out, unsigned int *d_bad);
 
 }  // namespace mqm

@@ -67,7 +67,48 @@ __global__ __launch_bounds__(256) void k_shard_gather(uint32_t n, uint32_t S, Sh
   }
 }
 
+// shared candidates: shard r's entry sid becomes r << kShardShift | sid (the
+// id stays shard-local: resolve it on shard r's index)
+__global__ __launch_bounds__(256) void k_shard_gather_shared(uint32_t n, uint32_t S, ShardArgs a,
+                                                             const uint64_t *__restrict__ out_offs,
+                                                             uint32_t *__restrict__ out, unsigned int *__restrict__ bad) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint32_t waves = gridDim.x * (blockDim.x / kWave);
+  for (uint32_t t = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave; t < n; t += waves) {
+    uint64_t w = out_offs[t];
+    for (uint32_t r = 0; r < S; r++) {
+      const uint64_t b = a.offsets[r][t], e = a.offsets[r][t + 1];
+      const uint32_t *src = reinterpret_cast<const uint32_t *>(a.deliveries[r]);
+      for (uint64_t j = b + lane; j < e; j += kWave) {
+        const uint32_t v = src[j];
+        if (v >> kShardShift) atomicOr(bad, 1u);
+        out[w + (j - b)] = (r << kShardShift) | (v & ((1u << kShardShift) - 1));
+      }
+      w += e - b;
+    }
+  }
+}
+
 }  // namespace
+
+int gather_shards_shared(uint32_t n, uint32_t S, const uint64_t *const *offsets, const uint32_t *const *shared,
+                         hipStream_t st, uint64_t *out_offsets, uint32_t *out, unsigned int *d_bad) {
+  if (S == 0 || S > (uint32_t)kMaxShards || !out_offsets || !d_bad) return -1;
+  ShardArgs a{};
+  for (uint32_t r = 0; r < S; r++) {
+    if (!offsets[r] || (!shared[r] && n)) return -1;
+    a.offsets[r] = offsets[r];
+    a.deliveries[r] = reinterpret_cast<const uint64_t *>(shared[r]);
+  }
+  hipLaunchKernelGGL(k_shard_offsets, dim3(n / 256 + 1), dim3(256), 0, st, n, S, a, out_offsets);
+  if (hipGetLastError() != hipSuccess) return -3;
+  if (n > 0) {
+    const uint32_t blocks = n / 4 + 1 < 16384u ? n / 4 + 1 : 16384u;
+    hipLaunchKernelGGL(k_shard_gather_shared, dim3(blocks), dim3(256), 0, st, n, S, a, out_offsets, out, d_bad);
+    if (hipGetLastError() != hipSuccess) return -3;
+  }
+  return 0;
+}
 
 int gather_shards(uint32_t n, uint32_t S, const ShardPart *parts, hipStream_t st, uint64_t *out_offsets,
                   uint64_t *out, unsigned int *d_bad) {

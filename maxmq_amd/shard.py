@@ -43,6 +43,28 @@ def shard_workload(w, world: int, rank: int):
     return o
 
 
+def generated_shard(config: int, world: int, rank: int, **overrides):
+    """Shard `rank` of `world` of an mqgen config, generated directly: only
+    the filters of its client range are kept (the full filter sequence is
+    still drawn, so every rank sees the same topics).  This is how a
+    100M-filter config is sharded without any host holding all of it."""
+    from tools import mqgen
+
+    n_filters = overrides.get("n_filters") or mqgen.default_params(config)["n_filters"]
+    n_clients = overrides.get("n_clients") or (n_filters + 3) // 4
+    lo, hi = shard_bounds(n_clients, world, rank)
+    return mqgen.generate(config, client_lo=lo, client_hi=hi, **overrides)
+
+
+def local_client_map(w) -> np.ndarray:
+    """For a generated shard: shard client id (first appearance in subscribe
+    order, as the shard's index interns them) -> the generator's global client
+    index, used as the node-wide client id."""
+    cid = np.asarray(w.client_ids)
+    g, first = np.unique(cid, return_index=True)
+    return g[np.argsort(first)].astype(np.uint32)
+
+
 def broadcast_batch(dist, data, offs, src: int = 0):
     """Broadcast a topic batch (uint8 bytes + int64 offsets tensors) from
     `src`; other ranks pass tensors of the right size (sizes go first)."""
@@ -76,6 +98,33 @@ def client_map(w, world: int, rank: int) -> np.ndarray:
     part = cid[(cid >= lo) & (cid < hi)]
     pg, pf = np.unique(part, return_index=True)
     return node_id[pg[np.argsort(pf)]]
+
+
+def gather_maps(dist, client_map, dst: int = 0):
+    """Every shard's client map (int32 tensor) -> on dst the list of maps in
+    rank order (setup, outside the timed step); elsewhere None."""
+    import torch
+
+    world, rank = dist.get_world_size(), dist.get_rank()
+    nm = torch.tensor([client_map.numel()], dtype=torch.int64, device=client_map.device)
+    sizes = [torch.zeros_like(nm) for _ in range(world)]
+    dist.all_gather(sizes, nm)
+    if rank != dst:
+        for r in dist.batch_isend_irecv([dist.P2POp(dist.isend, client_map, dst)]):
+            r.wait()
+        return None
+    maps, ops = [], []
+    for r in range(world):
+        if r == rank:
+            maps.append(client_map)
+            continue
+        m = torch.empty(int(sizes[r].item()), dtype=client_map.dtype, device=client_map.device)
+        ops.append(dist.P2POp(dist.irecv, m, r))
+        maps.append(m)
+    if ops:
+        for q in dist.batch_isend_irecv(ops):
+            q.wait()
+    return maps
 
 
 def gather_lists(dist, offsets, deliveries, dst: int = 0):

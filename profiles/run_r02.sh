@@ -27,6 +27,10 @@ for step in "$@"; do
     fast) timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast.json 2> $OUT/bench_fast.log ;;
     lanes) for L in 4 16; do MQM_WALK_LANES=$L timeout -k 10 400 python3 -u bench.py $FAST \
              > $OUT/bench_fast_lanes$L.json 2> $OUT/bench_fast_lanes$L.log; done ;;
+    c4shard) timeout -k 10 600 python3 -u bench.py --config 4 --shard 0/8 $FAST \
+             > $OUT/bench_c4_shard0of8.json 2> $OUT/bench_c4_shard0of8.log ;;
+    host) timeout -k 10 600 python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline \
+             > $OUT/bench_host.json 2> $OUT/bench_host.log ;;
     prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv \
              -d $OUT/prof -o prof -- python3 $ROOT/bench.py $FAST \
              > $OUT/bench_under_rocprof.json 2> $OUT/rocprof.log) ;;

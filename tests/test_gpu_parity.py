@@ -316,7 +316,7 @@ def test_gather_shards_equals_unsharded(n_shards):
 
     from maxmq_amd import shard
 
-    w = mqgen.generate(1, n_filters=20000, n_topics=30000)
+    w = mqgen.generate(1, n_filters=20000, n_topics=30000, p_shared=0.1)
     s = w.topics
     tb = torch.from_numpy(s.data).cuda()
     to = torch.from_numpy(s.offs.view(np.int64)).cuda()
@@ -325,16 +325,20 @@ def test_gather_shards_equals_unsharded(n_shards):
     full.subscribe_workload(w)
     ref = full.match_batch(s.data, s.offs)
     idxs, parts, maps, total = [], [], [], 0
+    sparts, stotal, shost = [], 0, []
     for r in range(n_shards):
         ix = maxmq_amd.TopicsIndex(0)
         ix.subscribe_workload(shard.shard_workload(w, n_shards, r))
         ix.match_device(tb.data_ptr(), to.data_ptr(), n)
         d = ix.dense_device()
         total += int(d.n_deliveries)
+        stotal += int(d.n_shared)
         cm = torch.from_numpy(shard.client_map(w, n_shards, r).astype(np.int32)).cuda()
         idxs.append(ix)
         maps.append(cm)
         parts.append((d.offsets, d.deliveries, cm.data_ptr(), cm.numel()))
+        sparts.append((d.shared_offsets, d.shared))
+        shost.append(ix.match_batch(s.data, s.offs))  # resolves the shard's shared ids
     out_o = torch.zeros(n + 1, dtype=torch.int64, device="cuda")
     out_d = torch.zeros(max(total, 1), dtype=torch.int64, device="cuda")
     torch.cuda.synchronize()
@@ -348,6 +352,27 @@ def test_gather_shards_equals_unsharded(n_shards):
     g = np.unique(np.rec.fromarrays([topic, gd["client"], gq, gn]))
     r = np.unique(np.rec.fromarrays([topic, ref.deliveries["client"], rq, rn]))
     assert len(g) == total and np.array_equal(g, r)
+    # shared candidates: shard-tagged, resolved on their shard == the unsharded set
+    so = torch.zeros(n + 1, dtype=torch.int64, device="cuda")
+    sd = torch.zeros(max(stotal, 1), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    maxmq_amd.gather_shards_shared(n, sparts, so.data_ptr(), sd.data_ptr())
+    sov = so.cpu().numpy().view(np.uint64)
+    assert np.array_equal(sov, ref.shared_offsets), "node-wide shared offsets"
+    sdv = sd[:stotal].cpu().numpy().view(np.uint32)
+    assert stotal > 0
+    got = set()
+    for t in range(n):
+        for v in sdv[sov[t]:sov[t + 1]]:
+            r, sid = int(v) >> 28, int(v) & 0x0FFFFFFF
+            info = shost[r].shared_info(sid)
+            got.add((t, idxs[r].filter_name(info.filter), idxs[r].client_name(info.client)))
+    want = set()
+    for t in range(n):
+        for sid in ref.shared[ref.shared_offsets[t]:ref.shared_offsets[t + 1]]:
+            info = ref.shared_info(int(sid))
+            want.add((t, full.filter_name(info.filter), full.client_name(info.client)))
+    assert got == want and len(got) == stotal
     # a client id outside its shard's map is an error, never silent
     bad = [(p[0], p[1], p[2], 0) for p in parts]
     if total:

@@ -184,78 +184,104 @@ extern "C" int mqgen_generate(const mqgen_params *p, mqgen_workload *out) {
   const uint64_t nclients = p->n_clients ? p->n_clients : (p->n_filters + 3) / 4;
 
   Builder fb, cb, tb;
-  std::vector<std::vector<std::string>> flevels;  // kept only to instantiate topics
-  flevels.reserve(p->n_filters);
-  std::vector<uint32_t> cid(p->n_filters);
-  std::vector<uint8_t> qos(p->n_filters), nl(p->n_filters), rap(p->n_filters), rh(p->n_filters);
-  std::vector<int32_t> ident(p->n_filters);
-  std::vector<std::string> lv;
-  for (uint64_t i = 0; i < p->n_filters; i++) {
-    lv.clear();
+  // every filter's RNG state at its start: a topic instantiating filter fi
+  // regenerates its levels (the first draws of the filter) instead of every
+  // filter's levels being kept (100M filters would hold ~20 GB of strings)
+  std::vector<uint64_t> fstate(p->n_filters);
+  const bool all = p->client_lo == 0 && p->client_hi == 0;
+  std::vector<uint32_t> cid;
+  std::vector<uint8_t> qos, nl, rap, rh;
+  std::vector<int32_t> ident;
+  if (all) {
+    cid.reserve(p->n_filters);
+    qos.reserve(p->n_filters);
+    nl.reserve(p->n_filters);
+    rap.reserve(p->n_filters);
+    rh.reserve(p->n_filters);
+    ident.reserve(p->n_filters);
+  }
+  static const std::string kPlus = "+", kHash = "#";
+  std::vector<const std::string *> lv;  // levels as pointers into the vocabulary
+  auto filter_levels = [&](Rng &r, uint64_t i, std::vector<const std::string *> &out) {
+    out.clear();
     if (i < p->n_root_hash) {
-      lv.push_back("#");
-    } else {
-      uint32_t m = draw_depth(rng);
-      for (uint32_t d = 0; d < m; d++) lv.push_back(voc.tok[d][voc.z[d].draw(rng)]);
-      if (m >= 2 && rng.uniform() < p->p_plus) {  // a depth-1 "+" would match every topic
-        int nplus = (m >= 4 && rng.uniform() < p->p_plus) ? 2 : 1;  // "a/+/+"-style filters only when deep
-        for (int k = 0; k < nplus; k++) {
-          // level 0 becomes '+' rarely (a root '+' matches every topic)
-          uint32_t d = (m > 1 && rng.uniform() > 0.02) ? 1 + (uint32_t)rng.below(m - 1) : 0;
-          lv[d] = "+";
-        }
-      }
-      if (m >= 2 && rng.uniform() < p->p_hash) lv[m - 1] = "#";
+      out.push_back(&kHash);
+      return;
     }
+    uint32_t m = draw_depth(r);
+    for (uint32_t d = 0; d < m; d++) out.push_back(&voc.tok[d][voc.z[d].draw(r)]);
+    if (m >= 2 && r.uniform() < p->p_plus) {  // a depth-1 "+" would match every topic
+      int nplus = (m >= 4 && r.uniform() < p->p_plus) ? 2 : 1;  // "a/+/+"-style filters only when deep
+      for (int k = 0; k < nplus; k++) {
+        // level 0 becomes '+' rarely (a root '+' matches every topic)
+        uint32_t d = (m > 1 && r.uniform() > 0.02) ? 1 + (uint32_t)r.below(m - 1) : 0;
+        out[d] = &kPlus;
+      }
+    }
+    if (m >= 2 && r.uniform() < p->p_hash) out[m - 1] = &kHash;
+  };
+  std::string f;
+  for (uint64_t i = 0; i < p->n_filters; i++) {
+    fstate[i] = rng.s;
+    filter_levels(rng, i, lv);
     bool shared = rng.uniform() < p->p_shared;
-    std::string f;
-    if (shared) f = "$SHARE/g" + std::to_string(rng.below(16)) + "/";
+    const uint64_t group = shared ? rng.below(16) : 0;
+    uint32_t c = (uint32_t)rng.below(nclients);
+    const uint8_t q = (uint8_t)rng.below(3);
+    const int32_t id = rng.uniform() < 0.5 ? 0 : (int32_t)(1 + rng.below((1u << 28) - 2));
+    const uint8_t n_l = (!shared && rng.uniform() < 0.1) ? 1 : 0;
+    const uint8_t ra = rng.uniform() < 0.5 ? 1 : 0;
+    const uint8_t r_h = (uint8_t)rng.below(3);
+    if (!all && (c < p->client_lo || c >= p->client_hi)) continue;
+    f.clear();
+    if (shared) f = "$SHARE/g" + std::to_string(group) + "/";
     for (size_t d = 0; d < lv.size(); d++) {
       if (d) f.push_back('/');
-      f += lv[d];
+      f += *lv[d];
     }
     fb.push(f);
-    uint32_t c = (uint32_t)rng.below(nclients);
-    cid[i] = c;
+    cid.push_back(c);
     cb.push("client-" + std::to_string(c));
-    qos[i] = (uint8_t)rng.below(3);
-    ident[i] = rng.uniform() < 0.5 ? 0 : (int32_t)(1 + rng.below((1u << 28) - 2));
-    nl[i] = (!shared && rng.uniform() < 0.1) ? 1 : 0;
-    rap[i] = rng.uniform() < 0.5 ? 1 : 0;
-    rh[i] = (uint8_t)rng.below(3);
-    flevels.push_back(lv);
+    qos.push_back(q);
+    ident.push_back(id);
+    nl.push_back(n_l);
+    rap.push_back(ra);
+    rh.push_back(r_h);
   }
   Zipf fz;
   if (p->topic_zipf_s > 0 && p->n_filters) fz = Zipf(p->n_filters, p->topic_zipf_s);
   std::string t;
+  std::vector<std::string> tl;  // a topic's levels
+  std::vector<const std::string *> fl;
   for (uint64_t i = 0; i < p->n_topics; i++) {
-    lv.clear();
+    tl.clear();
     if (p->n_filters && rng.uniform() < p->p_instantiate) {
       uint64_t fi = p->topic_zipf_s > 0 ? fz.draw(rng) : rng.below(p->n_filters);
-      const auto &fl = flevels[fi];
-      for (size_t d = 0; d < fl.size() && lv.size() < md; d++) {
-        if (fl[d] == "+") {
-          lv.push_back(voc.tok[d][voc.z[d].draw(rng)]);
-        } else if (fl[d] == "#") {
+      Rng fr(fstate[fi]);
+      filter_levels(fr, fi, fl);
+      for (size_t d = 0; d < fl.size() && tl.size() < md; d++) {
+        if (fl[d] == &kPlus) {
+          tl.push_back(voc.tok[d][voc.z[d].draw(rng)]);
+        } else if (fl[d] == &kHash) {
           uint32_t extra = (uint32_t)rng.below(3);
-          for (uint32_t k = 0; k < extra && lv.size() < md; k++) {
-            uint32_t dd = (uint32_t)lv.size();
-            lv.push_back(voc.tok[dd][voc.z[dd].draw(rng)]);
+          for (uint32_t k = 0; k < extra && tl.size() < md; k++) {
+            uint32_t dd = (uint32_t)tl.size();
+            tl.push_back(voc.tok[dd][voc.z[dd].draw(rng)]);
           }
         } else {
-          lv.push_back(fl[d]);
+          tl.push_back(*fl[d]);
         }
       }
-      if (lv.empty()) lv.push_back(voc.tok[0][voc.z[0].draw(rng)]);
+      if (tl.empty()) tl.push_back(voc.tok[0][voc.z[0].draw(rng)]);
     } else {
       uint32_t m = draw_depth(rng);
-      for (uint32_t d = 0; d < m; d++) lv.push_back(voc.tok[d][voc.z[d].draw(rng)]);
+      for (uint32_t d = 0; d < m; d++) tl.push_back(voc.tok[d][voc.z[d].draw(rng)]);
     }
-    if (rng.uniform() < p->p_dollar_topic) lv[0] = rng.uniform() < 0.5 ? "$SYS" : "$dev" + lv[0];
+    if (rng.uniform() < p->p_dollar_topic) tl[0] = rng.uniform() < 0.5 ? "$SYS" : "$dev" + tl[0];
     t.clear();
-    for (size_t d = 0; d < lv.size(); d++) {
+    for (size_t d = 0; d < tl.size(); d++) {
       if (d) t.push_back('/');
-      t += lv[d];
+      t += tl[d];
     }
     tb.push(t);
   }

@@ -34,6 +34,10 @@ typedef struct {
   uint32_t vocab[8];        /* tokens per depth 0..7 (deeper levels use vocab[7])  */
   double depth_w[32];       /* unnormalised weight of filter depth m = i+1         */
   uint32_t n_root_hash;     /* explicit count of root '#' filters                  */
+  uint32_t pad_;
+  uint64_t client_lo;       /* keep only filters whose client index is in           */
+  uint64_t client_hi;       /*   [client_lo, client_hi) (a subscriber shard);       */
+                            /*   0, 0 => all.  Topics are drawn from every filter.  */
 } mqgen_params;
 
 typedef struct {

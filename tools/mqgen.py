@@ -34,6 +34,9 @@ class _Params(C.Structure):
         ("vocab", C.c_uint32 * 8),
         ("depth_w", C.c_double * 32),
         ("n_root_hash", C.c_uint32),
+        ("pad_", C.c_uint32),
+        ("client_lo", C.c_uint64),
+        ("client_hi", C.c_uint64),
     ]
 
 
@@ -120,6 +123,13 @@ def default_params(config: int) -> dict:
         v = getattr(p, name)
         out[name] = list(v) if name in ("vocab", "depth_w") else v
     return out
+
+
+def default_params(config: int) -> dict:
+    p = _Params()
+    _lib().mqgen_default_params(config, C.byref(p))
+    return {name: (list(getattr(p, name)) if name in ("vocab", "depth_w") else getattr(p, name))
+            for name, _ in _Params._fields_}
 
 
 def generate(config: int, **overrides) -> Workload:
