@@ -113,6 +113,7 @@ struct Counters {              // zeroed before every batch
   unsigned int n_ovf;          // topics k_multi's first tier passed to the second
   unsigned int n_ovf2;         // ... the second tier to the third
   unsigned int n_wmerge;       // big-class topics k_merge dedupes (0 < Ms <= kSmallMulti)
+  unsigned int oob;            // a store fell outside its output buffer (never expected)
 };
 
 struct Outputs {
@@ -130,6 +131,9 @@ struct Outputs {
   uint32_t *icount;
   uint64_t *istart;
   uint32_t *iout;
+  // capacities of dout / hout in entries: every store is checked against them
+  // (a wrong offset becomes a reported error, never an out-of-bounds write)
+  uint64_t dcap, hcap;
 };
 
 struct TopicLds {              // k_walk context of one topic (one 16-lane group)
@@ -163,6 +167,15 @@ __device__ __forceinline__ void put_out(T *p, T v) {
 #else
   *p = v;
 #endif
+}
+
+// a checked store: out[i] = v if i < cap, else flag the batch as failed
+template <class T>
+__device__ __forceinline__ void put_checked(T *out, uint64_t i, uint64_t cap, T v, unsigned int *oob) {
+  if (i < cap)
+    put_out(&out[i], v);
+  else
+    atomicOr(oob, 1u);
 }
 
 __device__ __forceinline__ uint64_t pack_delivery(uint32_t client, uint32_t sid, uint32_t qos, uint32_t nl) {
@@ -550,7 +563,8 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 // register sets, so no register copy waits for a load).
 template <int kE, int kU>
 __device__ __forceinline__ void copy_solo(const DeviceSnapshot &s, const uint32_t *rec, uint32_t nh, uint32_t Ss,
-                                          uint32_t lo, uint32_t hi, int gl, uint64_t *out, uint64_t db) {
+                                          uint32_t lo, uint32_t hi, int gl, uint64_t *out, uint64_t db, uint64_t cap,
+                                          unsigned int *oob) {
   constexpr uint32_t kStep = 2u * kE * kU;
   // subs through a buffer descriptor: 32-bit offsets (one VGPR per load
   // address instead of two) and bounds-checked reads (the snapshot pads the
@@ -592,10 +606,13 @@ __device__ __forceinline__ void copy_solo(const DeviceSnapshot &s, const uint32_
       u32x4_a8 d = v[u];
       d.y &= 0x7FFFFFFFu;  // SubEnt word -> delivery (snapshot.h)
       d.w &= 0x7FFFFFFFu;
-      if (q + 1 < hi)
+      if (q < hi && db + q + (q + 1 < hi ? 1 : 0) >= cap) {
+        atomicOr(oob, 1u);
+      } else if (q + 1 < hi) {
         *reinterpret_cast<u32x4_a8 *>(out + db + q) = d;
-      else if (q < hi)
+      } else if (q < hi) {
         out[db + q] = ((uint64_t)d.y << 32) | d.x;
+      }
     }
   };
   // latency is hidden by occupancy (many waves, kU 16-B accesses each) rather
@@ -615,7 +632,8 @@ template <int kE, int kMPer>
 __device__ __forceinline__ uint32_t merge_multi(uint32_t *tkey, uint32_t *tbits, uint32_t *tmin, uint32_t kSlots,
                                                 const uint32_t (&mcl)[kMPer], const uint32_t (&mw)[kMPer],
                                                 const uint32_t (&mrk)[kMPer], uint32_t M, int gl, int gbase,
-                                                uint64_t *out, uint64_t db, uint32_t D) {
+                                                uint64_t *out, uint64_t db, uint32_t D, uint64_t cap,
+                                                unsigned int *oob) {
   constexpr uint64_t kGMask = kE == 64 ? ~0ull : (1ull << kE) - 1ull;
   const uint64_t glt = (1ull << gl) - 1ull;
   uint32_t lg = 6;
@@ -642,7 +660,7 @@ __device__ __forceinline__ uint32_t merge_multi(uint32_t *tkey, uint32_t *tbits,
       ent = pack_delivery(mcl[k], mw[k] & kWordSidMask, 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
     }
     const uint64_t m = (__ballot(win) >> gbase) & kGMask;
-    if (win) put_out(&out[db + D + __popcll(m & glt)], ent);
+    if (win) put_checked(out, db + D + __popcll(m & glt), cap, ent, oob);
     D += __popcll(m);
   }
   return D;
@@ -708,7 +726,7 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
       uint32_t w = 0;
       for (uint32_t j = 0; j < nsh; j++) {
         const uint32_t so = grec[kRecSh + 2 * j], sc = grec[kRecSh + 1 + 2 * j];
-        for (uint32_t j2 = gl; j2 < sc; j2 += kSE) put_out(&o.hout[hb + w + j2], so + j2);
+        for (uint32_t j2 = gl; j2 < sc; j2 += kSE) put_checked(o.hout, hb + w + j2, o.hcap, so + j2, &o.ctr->oob);
         w += sc;
       }
     }
@@ -726,9 +744,11 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
         mw[k] = e.word;
       }
     }
-    copy_solo<kSE, kU>(s, L.rec, nh, Ss, 0, Ss, gl, o.dout, db);
+    copy_solo<kSE, kU>(s, L.rec, nh, Ss, 0, Ss, gl, o.dout, db, o.dcap, &o.ctr->oob);
     uint32_t D = Ss;
-    if (M) D = merge_multi<kSE, kMPer>(L.tkey, L.tbits, L.tmin, 64, mcl, mw, mrk, M, gl, gbase, o.dout, db, D);
+    if (M)
+      D = merge_multi<kSE, kMPer>(L.tkey, L.tbits, L.tmin, 64, mcl, mw, mrk, M, gl, gbase, o.dout, db, D, o.dcap,
+                                  &o.ctr->oob);
     if (gl == 0) o.dcount[t] = D;
     wave_lds_sync();
   }
@@ -786,7 +806,8 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_merge(DeviceSnapshot s, O
       mw[k] = e.word;
     }
     const uint32_t D =
-        merge_multi<kWave, kMPer>(L.tkey, L.tbits, L.tmin, kSmallSlots, mcl, mw, mrk, M, lane, 0, o.dout, db, Ss);
+        merge_multi<kWave, kMPer>(L.tkey, L.tbits, L.tmin, kSmallSlots, mcl, mw, mrk, M, lane, 0, o.dout, db, Ss,
+                                  o.dcap, &o.ctr->oob);
     if (lane == 0) o.dcount[t] = D;
     wave_lds_sync();
   }
@@ -857,13 +878,13 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
       uint32_t w = 0;
       for (uint32_t k = 0; k < nsh; k++) {
         const uint32_t so = grec[kRecSh + 2 * k], sc = grec[kRecSh + 1 + 2 * k];
-        for (uint32_t k2 = lane; k2 < sc; k2 += kWave) put_out(&o.hout[hb + w + k2], so + k2);
+        for (uint32_t k2 = lane; k2 < sc; k2 += kWave) put_checked(o.hout, hb + w + k2, o.hcap, so + k2, &o.ctr->oob);
         w += sc;
       }
     }
     // solo entries [lo, hi) of the topic: delivery q = solo entry q
     const uint32_t lo = j * kChunk, hi = min(Ss, lo + kChunk);
-    copy_solo<kWave, kU>(s, L.rec, nh, Ss, lo, hi, lane, o.dout, db);
+    copy_solo<kWave, kU>(s, L.rec, nh, Ss, lo, hi, lane, o.dout, db, o.dcap, &o.ctr->oob);
     if (first && M == 0 && lane == 0) o.dcount[t] = Ss;  // else k_merge / k_multi write it
     wave_lds_sync();
   }
@@ -967,7 +988,7 @@ __global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs
         if (w < wid) before += wsum[w];
         round += wsum[w];
       }
-      if (win) put_out(&o.dout[db + before + __popcll(m & lanemask_lt(lane))], ent);
+      if (win) put_checked(o.dout, db + before + __popcll(m & lanemask_lt(lane)), o.dcap, ent, &o.ctr->oob);
       D += round;
       __syncthreads();
     }
@@ -1028,8 +1049,10 @@ __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *
         const uint64_t m = __ballot(occ);
         if (occ) {
           const uint32_t bits = (uint32_t)(gg.keybits >> 32);
-          o.dout[db + w + __popcll(m & lanemask_lt(lane))] = pack_delivery(
-              (uint32_t)gg.keybits - 1, (uint32_t)~gg.first, 31u - __builtin_clz(bits & 7u), (bits >> 3) & 1u);
+          put_checked(o.dout, db + w + __popcll(m & lanemask_lt(lane)), o.dcap,
+                      pack_delivery((uint32_t)gg.keybits - 1, (uint32_t)~gg.first, 31u - __builtin_clz(bits & 7u),
+                                    (bits >> 3) & 1u),
+                      &o.ctr->oob);
         }
         w += __popcll(m);
       }
@@ -1162,7 +1185,7 @@ __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *
         }
         const uint32_t shc = e.sh_cnt_flags & kShCntMask;
         if (kPhase == 1)
-          for (uint32_t j = lane; j < shc; j += kWave) o.hout[hb + H + j] = e.sh_off + j;
+          for (uint32_t j = lane; j < shc; j += kWave) put_checked(o.hout, hb + H + j, o.hcap, e.sh_off + j, &o.ctr->oob);
         H += shc;
         if (has_next && (fl & kFlagHasChildren)) {
           if (lane == 0) {
@@ -1389,9 +1412,24 @@ static uint32_t resident_blocks(Workspace &ws, int, K kern) {
   return slot_v;
 }
 
-// counts (n) -> exclusive offsets (u64, n + 1)
+// counts (n) -> exclusive offsets (u64, n + 1).  u32 counts are widened on
+// the fly: hipCUB accumulates in the input type, and a batch's raw entries can
+// pass 2^32 (config 4 shards gather ~6.8G per 10M topics)
+struct Widen {
+  __host__ __device__ uint64_t operator()(uint32_t c) const { return c; }
+};
 template <class T>
-static int scan_offsets(Workspace &ws, T counts, uint64_t *offs, uint32_t n, hipStream_t st) {
+static int scan_offsets_it(Workspace &ws, T counts, uint64_t *offs, uint32_t n, hipStream_t st);
+static int scan_offsets(Workspace &ws, const uint32_t *counts, uint64_t *offs, uint32_t n, hipStream_t st) {
+  return scan_offsets_it(ws, hipcub::TransformInputIterator<uint64_t, Widen, const uint32_t *>(counts, Widen{}), offs,
+                         n, st);
+}
+static int scan_offsets_u64(Workspace &ws, const uint64_t *counts, uint64_t *offs, uint32_t n, hipStream_t st) {
+  return scan_offsets_it(ws, counts, offs, n, st);
+}
+template <class T>
+static int scan_offsets_it(Workspace &ws, T counts, uint64_t *offs, uint32_t n, hipStream_t st) {
+  static_assert(sizeof(typename std::iterator_traits<T>::value_type) == 8, "64-bit accumulation");
   HIP_TRY(hipMemsetAsync(offs, 0, sizeof(uint64_t), st));
   if (n == 0) return 0;
   size_t tmp = 0;
@@ -1514,7 +1552,7 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_table_sizes, dim3((n_dfs + 255) / 256), dim3(256), 0, st, raw_cnt, o.ctr, tab_size);
     HIP_TRY(hipGetLastError());
-    if (scan_offsets(ws, (const uint64_t *)tab_size, tab_off, n_dfs, st)) return -3;
+    if (scan_offsets_u64(ws, tab_size, tab_off, n_dfs, st)) return -3;
     std::vector<uint64_t> rc(2 * (n_dfs + 1));
     HIP_TRY(hipMemcpyAsync(rc.data(), raw_cnt, sizeof(uint64_t) * 2 * (n_dfs + 1), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(hp, tab_off + n_dfs, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
@@ -1531,6 +1569,8 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
     return -2;
   o.dout = (uint64_t *)ws.ptr(W::kDOut);
   o.hout = (uint32_t *)ws.ptr(W::kHOut);
+  o.dcap = s_total + dfs_raw;
+  o.hcap = h_total + dfs_h;
   auto *items = (uint2 *)ws.ptr(W::kItems);
 
   mark(ws, 2, st);
@@ -1583,13 +1623,18 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   {
     size_t tmp = 0;
     uint64_t *sums = reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(o.ctr) + 192);
-    HIP_TRY(hipcub::DeviceReduce::Sum(nullptr, tmp, o.dcount, sums, n, st));
+    hipcub::TransformInputIterator<uint64_t, Widen, const uint32_t *> dc(o.dcount, Widen{}), hc_it(o.hcount, Widen{});
+    HIP_TRY(hipcub::DeviceReduce::Sum(nullptr, tmp, dc, sums, n, st));
     if (ws.get(W::kScanTmp, tmp)) return -2;
-    HIP_TRY(hipcub::DeviceReduce::Sum(ws.ptr(W::kScanTmp), tmp, o.dcount, sums, n, st));
-    HIP_TRY(hipcub::DeviceReduce::Sum(ws.ptr(W::kScanTmp), tmp, o.hcount, sums + 1, n, st));
+    HIP_TRY(hipcub::DeviceReduce::Sum(ws.ptr(W::kScanTmp), tmp, dc, sums, n, st));
+    HIP_TRY(hipcub::DeviceReduce::Sum(ws.ptr(W::kScanTmp), tmp, hc_it, sums + 1, n, st));
     HIP_TRY(hipMemcpyAsync(hp, sums, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(hc, o.ctr, sizeof(Counters), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+  }
+  if (hc->oob) {
+    fprintf(stderr, "mqmatch: an output store fell outside its buffer (batch rejected)\n");
+    return -3;
   }
   if (ws.profile) {
     ws.prof_calls++;

@@ -311,14 +311,22 @@ __global__ __launch_bounds__(256) void k_emit_fill(uint64_t ne, uint64_t nchunks
     }                                                                                                     \
   } while (0)
 
+// hipCUB accumulates in the input type: narrower counts are widened on the fly
+// so the offsets never wrap at 2^32
+template <class T>
+struct WidenU64 {
+  __host__ __device__ uint64_t operator()(T c) const { return (uint64_t)c; }
+};
+
 template <class T>
 int scan_u64(Workspace &ws, const T *counts, uint64_t *offs, uint64_t n, hipStream_t st) {
   HIP_TRY(hipMemsetAsync(offs, 0, sizeof(uint64_t), st));
   if (n == 0) return 0;
+  hipcub::TransformInputIterator<uint64_t, WidenU64<T>, const T *> in(counts, WidenU64<T>{});
   size_t tmp = 0;
-  HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, tmp, counts, offs + 1, n, st));
+  HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, tmp, in, offs + 1, n, st));
   if (ws.get(Workspace::kScanTmp, tmp)) return -2;
-  HIP_TRY(hipcub::DeviceScan::InclusiveSum(ws.ptr(Workspace::kScanTmp), tmp, counts, offs + 1, n, st));
+  HIP_TRY(hipcub::DeviceScan::InclusiveSum(ws.ptr(Workspace::kScanTmp), tmp, in, offs + 1, n, st));
   return 0;
 }
 
