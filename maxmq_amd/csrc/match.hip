@@ -62,7 +62,7 @@ constexpr int kWave = 64;
 constexpr int kWalkWaves = 4;            // wavefronts per k_walk block
 constexpr int kLMax = 16;                // levels cached per topic
 constexpr int kFCap = 16;                // frontier nodes per level
-constexpr int kHCap = 48;                // non-shared hits per topic (3 per lane)
+constexpr int kHCap = 64;                // non-shared hits per topic (hit_of: 6 search steps)
 constexpr int kShCap = 16;               // shared hits per topic
 constexpr int kStage = 64;               // topic bytes staged in LDS (4 per lane, one round trip)
 // record, written while walking (hits in discovery order; rank orders them):
@@ -73,10 +73,13 @@ constexpr int kStage = 64;               // topic bytes staged in LDS (4 per lan
 //   [kRecSh + 2i] off, [kRecSh + 1 + 2i] cnt of shared hit i (i < nsh)
 // One 64-lane load fetches the header and the first 15 hits.
 constexpr int kRecHit = 4;
-constexpr int kRecSh = 4 + kRecHit * kHCap;          // 196
-constexpr int kRecStride = kRecSh + 2 * kShCap;       // 228 words (max)
-constexpr int kRecStrideAlloc = 228;                  // 16-B aligned per topic
-constexpr uint32_t kSMax = 16384;        // raw entries per topic on the bounded path
+constexpr int kRecSh = 4 + kRecHit * kHCap;          // 260
+constexpr int kRecStride = kRecSh + 2 * kShCap;       // 292 words (max)
+constexpr int kRecStrideAlloc = 292;                  // 16-B aligned per topic
+// raw entries per hit range on the bounded path (keeps the per-lane sums of a
+// topic's 64 hits inside 32 bits); emission itself has no per-topic size
+// limit (k_copy items; partitioned merge of any number of multi entries)
+constexpr uint32_t kSMax = 1u << 24;
 constexpr int kEmitU = 4;                // solo entries in flight per lane
 constexpr int kEmitWaves = 4;
 constexpr int kSmallLanes = 8;           // k_emit_small: lanes per topic of the small class
@@ -86,13 +89,12 @@ constexpr uint32_t kSmallMultiS = 3 * kSmallLanes;  //   and multi entries
 constexpr int kSmallSlots = 256;         // k_emit merge table slots (per wave)
 constexpr int kSmallMulti = 192;         // multi entries it holds (load <= 0.75)
 constexpr int kBigThreads = 256;
-constexpr int kBigMax = 3072;            // multi entries per bounded topic (k_multi's last tier)
+constexpr int kPartCap = 2048;           // k_multi_part: multi entries per client partition (expected)
 constexpr uint32_t kNoWhy = 0xFFFFFFFFu;
 constexpr int kICap = 3 * kFCap;         // load items per level (<= 3 per frontier node)
 
 static_assert(kRecStrideAlloc % 4 == 0 && kRecStrideAlloc >= kRecStride, "16-B aligned records");
 static_assert(kSmallMulti * 4 <= kSmallSlots * 3, "k_emit table load factor");
-static_assert(kBigMax * 4 <= 4096 * 3 && kBigMax <= 12 * kBigThreads, "the last k_multi tier holds every bounded topic");
 static_assert(kSmallMulti % kWave == 0, "register tiles");
 
 // a load item of the walk: the literal-child probe of a frontier node, or the
@@ -481,7 +483,7 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
     }
     const uint32_t Ss = ls, Ms = lm, H = lh;
     const uint32_t S = Ss + Ms;
-    if (why == kNoWhy && (S > kSMax || Ms > (uint32_t)kBigMax)) why = kWhyEntries;
+    if (why == kNoWhy && S > kSMax) why = kWhyEntries;
     if (active && gl == 0) {
       const bool dfs = why != kNoWhy;
       if (!dfs) {
@@ -997,6 +999,92 @@ __global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// k_multi_part: topics with more multi entries than k_multi's tiers hold.  A
+// 256-thread workgroup per topic splits the topic's clients into P =
+// ceil(M / kPartCap) hash partitions and merges them one after another in a
+// 4096-slot LDS table: every pass reads all M entries and keeps its
+// partition's (a client's entries all fall in one partition, so each pass is
+// a complete Subscription.Merge of its clients).  Winners are placed with an
+// LDS counter (order within a topic unspecified, as the reference's Go map).
+// A partition that would overfill the table (never for a hash of this
+// spread; checked) fails the batch instead of spinning.
+// ---------------------------------------------------------------------------
+// client -> partition: a hash independent of table_slot's (which takes the
+// top bits of client * 2654435769: a partition must spread over the table)
+__device__ __forceinline__ uint32_t partition_of(uint32_t client, uint32_t P) {
+  uint32_t h = client * 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return (uint32_t)(((uint64_t)h * P) >> 32);
+}
+
+__global__ __launch_bounds__(kBigThreads) void k_multi_part(DeviceSnapshot s, Outputs o,
+                                                           const uint32_t *__restrict__ list,
+                                                           const unsigned int *__restrict__ count) {
+  constexpr uint32_t kSlots = 4096, kFill = kSlots * 7 / 8;
+  __shared__ uint32_t tkey[kSlots], tbits[kSlots], tmin[kSlots];
+  __shared__ uint32_t rec[kRecStrideAlloc];
+  __shared__ uint32_t fill, nwin;
+  const int tid = threadIdx.x;
+  const uint32_t nb = *count;
+  for (uint32_t bi = blockIdx.x; bi < nb; bi += gridDim.x) {
+    const uint32_t t = list[bi];
+    const uint64_t db = o.dstart[t];
+    for (uint32_t i = tid; i < (uint32_t)kRecStrideAlloc; i += kBigThreads)
+      rec[i] = o.recs[(uint64_t)t * kRecStrideAlloc + i];
+    __syncthreads();
+    const uint32_t nh = rec[0] & 0xFFu, Ss = rec[1], M = rec[2];
+    __syncthreads();
+    if (tid < kWave) rec_prefix<kWave>(rec, nh, tid);
+    __syncthreads();
+    const uint32_t P = (M + kPartCap - 1) / kPartCap;
+    uint32_t D = Ss;
+    for (uint32_t p = 0; p < P; p++) {
+      for (uint32_t i = tid; i < kSlots; i += kBigThreads) {
+        tkey[i] = 0;
+        tbits[i] = 0;
+        tmin[i] = 0xFFFFFFFFu;
+      }
+      if (tid == 0) fill = nwin = 0;
+      __syncthreads();
+      for (uint32_t q = tid; q < M; q += kBigThreads) {
+        uint32_t h;
+        const uint32_t sid = multi_sid(rec, nh, Ss, q, &h);
+        const SubEnt e = load_sub(s, sid);
+        if (partition_of(e.client, P) != p) continue;
+        if (atomicAdd(&fill, 1u) >= kFill) {
+          atomicOr(&o.ctr->oob, 1u);
+          continue;
+        }
+        table_insert(tkey, tbits, tmin, kSlots - 1, 12, e.client, e.word, rec_at(rec, h, kFieldRank));
+      }
+      __syncthreads();
+      for (uint32_t q = tid; q < M; q += kBigThreads) {
+        uint32_t h;
+        const uint32_t sid = multi_sid(rec, nh, Ss, q, &h);
+        const SubEnt e = load_sub(s, sid);
+        if (partition_of(e.client, P) != p) continue;
+        uint32_t sl = table_slot(e.client, 12);
+        uint32_t probes = 0;
+        while (tkey[sl] != e.client + 1 && probes++ < kSlots) sl = (sl + 1) & (kSlots - 1);
+        if (tkey[sl] != e.client + 1 || tmin[sl] != rec_at(rec, h, kFieldRank)) continue;  // not its client's winner
+        const uint32_t v = tbits[sl];
+        const uint32_t pos = atomicAdd(&nwin, 1u);
+        put_checked(o.dout, db + D + pos, o.dcap,
+                    pack_delivery(e.client, e.word & kWordSidMask, 31u - __builtin_clz(v & 7u), (v >> 3) & 1u),
+                    &o.ctr->oob);
+      }
+      __syncthreads();
+      D += nwin;
+      __syncthreads();
+    }
+    if (tid == 0) o.dcount[t] = D;
+    __syncthreads();
+  }
+}
 
 // ---------------------------------------------------------------------------
 // k_dfs<P>: the unbounded path.  P0 counts raw entries / shared candidates;
@@ -1600,8 +1688,8 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
     hipLaunchKernelGGL((k_multi<2048, 6>), dim3(resident_blocks(ws, 1, k_multi<2048, 6>)), dim3(kBigThreads), 0, st, s,
                        o, ovf, &o.ctr->n_ovf, ovf2, &o.ctr->n_ovf2);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL((k_multi<4096, 12>), dim3(resident_blocks(ws, 5, k_multi<4096, 12>)), dim3(kBigThreads), 0,
-                       st, s, o, ovf2, &o.ctr->n_ovf2, nullptr, nullptr);
+    hipLaunchKernelGGL(k_multi_part, dim3(resident_blocks(ws, 5, k_multi_part)), dim3(kBigThreads), 0, st, s, o, ovf2,
+                       &o.ctr->n_ovf2);
     HIP_TRY(hipGetLastError());
   }
   if (n_dfs) {

@@ -276,16 +276,23 @@ def test_identifiers_vs_oracle(config, overrides):
 
 
 def test_identifiers_dfs_topics_and_device_form():
-    """Topics on the unbounded (DFS) path: hubs of identified subscriptions."""
+    """Hubs of identified subscriptions (9000 multi entries per topic: the
+    partitioned workgroup merge) and topics deeper than the walk's 16 cached
+    levels (the unbounded DFS path), with identifiers."""
     filters, clients, subs = [], [], []
-    for i in range(3000):  # raw entries past the bounded path: DFS
+    for i in range(3000):  # 3 compatible filters per client: 9000 multi entries on hub/x
         filters += ["hub/#", "hub/x", "+/x"]
         clients += [f"h{i}"] * 3
         subs += [(1, 0, 0, 0, i + 1), (0, 0, 0, 0, 0), (2, 0, 0, 0, 7)]
     filters += ["a/#", "a/b", "#"]
     clients += ["k", "k", "j"]
     subs += [(0, 0, 0, 0, 3), (1, 0, 0, 0, 4), (0, 0, 0, 0, 0)]
-    topics = ["hub/x", "hub", "a/b", "a/b/c", "zz/x", "$SYS/x"]
+    deep = "/".join(f"d{i}" for i in range(20))
+    for i in range(50):  # a 20-level topic: DFS
+        filters += ["d0/#", "d0/d1/+/d3/#", deep]
+        clients += [f"p{i}"] * 3
+        subs += [(i % 3, 0, 0, 0, i + 1), (1, 1, 0, 0, 0), (2, 0, 1, 2, 5)]
+    topics = ["hub/x", "hub", "a/b", "a/b/c", "zz/x", "$SYS/x", deep, deep + "/e"]
     idx = maxmq_amd.TopicsIndex(0, identifiers=True)
     ora = OracleIndex()
     for f, c, (q, nl, rap, rh, ident) in zip(filters, clients, subs):
