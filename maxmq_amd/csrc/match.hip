@@ -109,12 +109,13 @@ struct Counters {              // zeroed before every batch
   unsigned long long htail;    // DFS shared candidates: likewise
   unsigned int n_dfs;          // topics appended to the DFS list
   unsigned int why[5];         // DFS routing reasons (kWhy*)
-  unsigned int n_multi;        // topics whose multi entries k_emit passed to k_multi
-  unsigned int n_small;        // emit lists (DeviceSelect counts)
-  unsigned int n_bigc;
-  unsigned int n_ovf;          // topics k_multi's first tier passed to the second
-  unsigned int n_ovf2;         // ... the second tier to the third
-  unsigned int n_wmerge;       // big-class topics k_merge dedupes (0 < Ms <= kSmallMulti)
+  // emission lists (k_route), in kList* order
+  unsigned int n_small;        // k_emit_small: small class + topics with shared candidates only
+  unsigned int n_bigc;         // k_copy: the big class
+  unsigned int n_wmerge;       // k_merge: big class, 0 < Ms <= kSmallMulti
+  unsigned int n_t1;           // k_multi<1024>: kSmallMulti < Ms <= 768
+  unsigned int n_t2;           // k_multi<2048>: 768 < Ms <= 1536
+  unsigned int n_part;         // k_multi_part: Ms > 1536
   unsigned int oob;            // a store fell outside its output buffer (never expected)
 };
 
@@ -124,7 +125,6 @@ struct Outputs {
   uint64_t *dstart, *hstart;  // n + 1 (exclusive scans; DFS topics overwritten)
   uint8_t *cls;
   uint32_t *dfs_list;
-  uint32_t *multi_list;       // topics for k_multi (Counters::n_multi)
   uint32_t *recs;  // kRecStrideAlloc words per topic
   Counters *ctr;
   uint64_t *dout;
@@ -216,25 +216,40 @@ __device__ __forceinline__ uint32_t rec_at(const uint32_t *rec, uint32_t h, int 
   return rec[4 + kRecHit * h + field];
 }
 
-// per-topic merge table in LDS (linear probing, key = client + 1):
-// QoS one-hot | NoLocal OR-folded, lowest hit rank kept (first-merged)
-__device__ __forceinline__ void table_insert(uint32_t *tkey, uint32_t *tbits, uint32_t *tmin, uint32_t mask,
-                                             uint32_t lg, uint32_t client, uint32_t word, uint32_t hit) {
+// per-topic merge table in LDS (linear probing, key = client + 1): the QoS
+// one-hot | NoLocal of the client's entries OR-folded, and rank << 32 | sid of
+// its first-merged subscription by a 64-bit atomicMin — exactly
+// Subscription.Merge (packets.go:250-270): max QoS, NoLocal OR, every other
+// field from the first subscription in the reference's emission order.  The
+// winners are read off the table afterwards (one delivery per occupied slot).
+struct MergeTable {
+  uint32_t *key, *bits;
+  unsigned long long *first;
+};
+
+__device__ __forceinline__ void mt_clear(MergeTable t, uint32_t j) {
+  t.key[j] = 0;
+  t.bits[j] = 0;
+  t.first[j] = ~0ull;
+}
+
+__device__ __forceinline__ void mt_insert(MergeTable t, uint32_t mask, uint32_t lg, uint32_t client, uint32_t word,
+                                          uint32_t rank) {
   uint32_t sl = table_slot(client, lg);
   for (;;) {
-    const uint32_t prev = atomicCAS(&tkey[sl], 0u, client + 1);
+    const uint32_t prev = atomicCAS(&t.key[sl], 0u, client + 1);
     if (prev == 0 || prev == client + 1) break;
     sl = (sl + 1) & mask;
   }
-  atomicOr(&tbits[sl], qos_bits(word));
-  atomicMin(&tmin[sl], hit);
+  atomicOr(&t.bits[sl], qos_bits(word));
+  atomicMin(&t.first[sl], ((unsigned long long)rank << 32) | (word & kWordSidMask));
 }
 
-__device__ __forceinline__ uint32_t table_find(const uint32_t *tkey, uint32_t mask, uint32_t lg, uint32_t client) {
-  uint32_t sl = table_slot(client, lg);
-  while (tkey[sl] != client + 1) sl = (sl + 1) & mask;
-  return sl;
+__device__ __forceinline__ uint64_t mt_delivery(MergeTable t, uint32_t j) {
+  const uint32_t v = t.bits[j];
+  return pack_delivery(t.key[j] - 1, (uint32_t)t.first[j], 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
 }
+
 
 // ---------------------------------------------------------------------------
 // k_walk: tokenize + walk, a 16-lane group per topic.  Level keys and the
@@ -631,38 +646,26 @@ __device__ __forceinline__ void copy_solo(const DeviceSnapshot &s, const uint32_
 // (1 << lg) <= kSlots slots and write the winners at out[db + D ..); returns
 // the new D (group-uniform).  Entries past M are inert.
 template <int kE, int kMPer>
-__device__ __forceinline__ uint32_t merge_multi(uint32_t *tkey, uint32_t *tbits, uint32_t *tmin, uint32_t kSlots,
-                                                const uint32_t (&mcl)[kMPer], const uint32_t (&mw)[kMPer],
-                                                const uint32_t (&mrk)[kMPer], uint32_t M, int gl, int gbase,
-                                                uint64_t *out, uint64_t db, uint32_t D, uint64_t cap,
-                                                unsigned int *oob) {
+__device__ __forceinline__ uint32_t merge_multi(MergeTable tb, uint32_t kSlots, const uint32_t (&mcl)[kMPer],
+                                                const uint32_t (&mw)[kMPer], const uint32_t (&mrk)[kMPer],
+                                                uint32_t M, int gl, int gbase, uint64_t *out, uint64_t db,
+                                                uint32_t D, uint64_t cap, unsigned int *oob) {
   constexpr uint64_t kGMask = kE == 64 ? ~0ull : (1ull << kE) - 1ull;
   const uint64_t glt = (1ull << gl) - 1ull;
   uint32_t lg = 6;
   while ((1u << lg) < 2 * M && (1u << lg) < kSlots) lg++;
   const uint32_t mask = (1u << lg) - 1;
-  for (uint32_t j = gl; j <= mask; j += kE) {
-    tkey[j] = 0;
-    tbits[j] = 0;
-    tmin[j] = 0xFFFFFFFFu;
-  }
+  for (uint32_t j = gl; j <= mask; j += kE) mt_clear(tb, j);
   wave_lds_sync();
 #pragma unroll
   for (int k = 0; k < kMPer; k++)
-    if (gl + k * kE < M) table_insert(tkey, tbits, tmin, mask, lg, mcl[k], mw[k], mrk[k]);
+    if (gl + k * kE < M) mt_insert(tb, mask, lg, mcl[k], mw[k], mrk[k]);
   wave_lds_sync();
-#pragma unroll
-  for (int k = 0; k < kMPer; k++) {
-    bool win = false;
-    uint64_t ent = 0;
-    if (gl + k * kE < M) {
-      const uint32_t sl = table_find(tkey, mask, lg, mcl[k]);
-      win = tmin[sl] == mrk[k];
-      const uint32_t v = tbits[sl];
-      ent = pack_delivery(mcl[k], mw[k] & kWordSidMask, 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
-    }
-    const uint64_t m = (__ballot(win) >> gbase) & kGMask;
-    if (win) put_checked(out, db + D + __popcll(m & glt), cap, ent, oob);
+  for (uint32_t j0 = 0; j0 <= mask; j0 += kE) {  // one delivery per occupied slot, slot order
+    const uint32_t j = j0 + gl;
+    const bool occ = j <= mask && tb.key[j] != 0;
+    const uint64_t m = (__ballot(occ) >> gbase) & kGMask;
+    if (occ) put_checked(out, db + D + __popcll(m & glt), cap, mt_delivery(tb, j), oob);
     D += __popcll(m);
   }
   return D;
@@ -679,8 +682,9 @@ constexpr int kSRecPer = 64 / kSE;  // record words prefetched per lane
 static_assert(4 + kRecHit * kSmallHits <= 64 && kSRecPer % 4 == 0, "small-class record prefetch");
 
 struct alignas(16) SmallLds {
+  unsigned long long tfirst[64];
   uint32_t rec[64];
-  uint32_t tkey[64], tbits[64], tmin[64];
+  uint32_t tkey[64], tbits[64];
 };
 
 template <int kOcc, int kU>
@@ -749,8 +753,8 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
     copy_solo<kSE, kU>(s, L.rec, nh, Ss, 0, Ss, gl, o.dout, db, o.dcap, &o.ctr->oob);
     uint32_t D = Ss;
     if (M)
-      D = merge_multi<kSE, kMPer>(L.tkey, L.tbits, L.tmin, 64, mcl, mw, mrk, M, gl, gbase, o.dout, db, D, o.dcap,
-                                  &o.ctr->oob);
+      D = merge_multi<kSE, kMPer>(MergeTable{L.tkey, L.tbits, L.tfirst}, 64, mcl, mw, mrk, M, gl, gbase, o.dout, db,
+                                  D, o.dcap, &o.ctr->oob);
     if (gl == 0) o.dcount[t] = D;
     wave_lds_sync();
   }
@@ -763,8 +767,9 @@ struct alignas(16) CopyLds {
 
 // ---- k_merge: a wavefront per big-class topic with 0 < Ms <= kSmallMulti ------
 struct alignas(16) MergeLds {
+  unsigned long long tfirst[kSmallSlots];
   uint32_t rec[kRecStrideAlloc];
-  uint32_t tkey[kSmallSlots], tbits[kSmallSlots], tmin[kSmallSlots];
+  uint32_t tkey[kSmallSlots], tbits[kSmallSlots];
 };
 
 __global__ __launch_bounds__(kWave *kEmitWaves) void k_merge(DeviceSnapshot s, Outputs o,
@@ -808,8 +813,8 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_merge(DeviceSnapshot s, O
       mw[k] = e.word;
     }
     const uint32_t D =
-        merge_multi<kWave, kMPer>(L.tkey, L.tbits, L.tmin, kSmallSlots, mcl, mw, mrk, M, lane, 0, o.dout, db, Ss,
-                                  o.dcap, &o.ctr->oob);
+        merge_multi<kWave, kMPer>(MergeTable{L.tkey, L.tbits, L.tfirst}, kSmallSlots, mcl, mw, mrk, M, lane, 0,
+                                  o.dout, db, Ss, o.dcap, &o.ctr->oob);
     if (lane == 0) o.dcount[t] = D;
     wave_lds_sync();
   }
@@ -893,124 +898,94 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
 }
 
 // ---------------------------------------------------------------------------
-// k_multi<kSlots, kPer>: a 256-thread workgroup per listed topic merges its
-// multi entries (<= kPer per thread) in an LDS table of kSlots slots and writes
-// the winners after the topic's solo deliveries (k_copy wrote those).  Topic
-// ids are prefetched two topics ahead and the record one topic ahead.  Topics
-// with more multi entries than the tier holds go to `ovf`, the next tier
-// (tiers of 768 / 1536 / 3072 entries: small tiers keep more blocks resident;
-// the last holds every bounded topic).
+// Workgroup merges (256 threads per topic) for big-class topics with more
+// multi entries than k_merge's wave table holds, routed by size (k_route):
+//   k_multi<kSlots>  M <= kSlots * 3 / 4 in one LDS table;
+//   k_multi_part     any M: the topic's clients split into P = ceil(M /
+//                    kPartCap) hash partitions merged one after another in a
+//                    4096-slot table (each pass reads all M entries and keeps
+//                    its partition's; a client's entries share a partition).
+// Winners are written after the topic's solo deliveries (k_copy wrote those)
+// in table-slot order: each wave scans a quarter of the table twice (count,
+// then write at its prefix), so the layout is deterministic.
 // ---------------------------------------------------------------------------
-template <int kSlots, int kPer>
-__global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs o, const uint32_t *__restrict__ list,
-                                                      const unsigned int *__restrict__ count,
-                                                      uint32_t *__restrict__ ovf, unsigned int *__restrict__ n_ovf) {
-  __shared__ uint32_t tkey[kSlots], tbits[kSlots], tmin[kSlots];
-  __shared__ uint32_t rec[kRecStrideAlloc];
-  __shared__ uint32_t wsum[kBigThreads / kWave];
-  constexpr uint32_t kMCap = kSlots * 3 / 4 < kPer * kBigThreads ? kSlots * 3 / 4 : kPer * kBigThreads;
+struct alignas(16) MultiLds {
+  uint32_t rec[kRecStrideAlloc];
+  uint32_t wsum[kBigThreads / kWave];
+};
+
+// the block's record of topic t, with prefixes (all threads; ends synced)
+__device__ __forceinline__ void block_record(Outputs o, uint32_t t, uint32_t *rec) {
+  const int tid = threadIdx.x;
+  for (uint32_t i = tid; i < (uint32_t)kRecStrideAlloc; i += kBigThreads)
+    rec[i] = o.recs[(uint64_t)t * kRecStrideAlloc + i];
+  __syncthreads();
+  const uint32_t nh = rec[0] & 0xFFu;
+  __syncthreads();
+  if (tid < kWave) rec_prefix<kWave>(rec, nh, tid);
+  __syncthreads();
+}
+
+// winners of the table [0, nslots) at out[db + D ..); returns the new D
+__device__ __forceinline__ uint32_t block_winners(MergeTable tb, uint32_t nslots, uint32_t *wsum, Outputs o, uint64_t db,
+                                                  uint32_t D) {
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
-  const uint32_t nb = *count, G = gridDim.x;
-  uint32_t bi = blockIdx.x;
-  uint32_t t_cur = bi < nb ? list[bi] : 0;
-  uint32_t t_nxt = bi + G < nb ? list[bi + G] : 0;
-  uint32_t rw = 0;
-  uint64_t db_nxt = 0;
-  if (bi < nb) {
-    if (tid < kWave) rw = o.recs[(uint64_t)t_cur * kRecStrideAlloc + tid];
-    db_nxt = o.dstart[t_cur];
+  constexpr int kW = kBigThreads / kWave;
+  const uint32_t per = (nslots + kW - 1) / kW, lo = wid * per, hi = min(nslots, lo + per);
+  uint32_t c = 0;
+  for (uint32_t j0 = lo; j0 < hi; j0 += kWave) {
+    const uint32_t j = j0 + lane;
+    c += __popcll(__ballot(j < hi && tb.key[j] != 0));
   }
-  for (; bi < nb; bi += G) {
-    const uint32_t t = t_cur;
-    const uint64_t db = db_nxt;
-    if (tid < kWave) rec[tid] = rw;
-    const uint32_t t_nn = bi + 2 * G < nb ? list[bi + 2 * G] : 0;
-    if (bi + G < nb) {
-      if (tid < kWave) rw = o.recs[(uint64_t)t_nxt * kRecStrideAlloc + tid];
-      db_nxt = o.dstart[t_nxt];
-    }
-    t_cur = t_nxt;
-    t_nxt = t_nn;
-    __syncthreads();
-    const uint32_t nh = rec[0] & 0xFFu, Ss = rec[1], M = rec[2];
-    if (4 + kRecHit * nh > (uint32_t)kWave) {  // block-uniform
-      for (uint32_t i = kWave + tid; i < 4 + kRecHit * nh; i += kBigThreads)
-        rec[i] = o.recs[(uint64_t)t * kRecStrideAlloc + i];
-      __syncthreads();
-    }
-    if (wid == 0) rec_prefix<kWave>(rec, nh, lane);
-    __syncthreads();
-    if (M > kMCap) {  // block-uniform; unreachable for the tier that holds kBigMax
-      if (tid == 0) ovf[atomicAdd(n_ovf, 1u)] = t;
-      __syncthreads();
-      continue;
-    }
+  if (lane == 0) wsum[wid] = c;
+  __syncthreads();
+  uint32_t w = D, total = D;
+  for (int k = 0; k < kW; k++) {
+    if (k < wid) w += wsum[k];
+    total += wsum[k];
+  }
+  for (uint32_t j0 = lo; j0 < hi; j0 += kWave) {
+    const uint32_t j = j0 + lane;
+    const bool occ = j < hi && tb.key[j] != 0;
+    const uint64_t m = __ballot(occ);
+    if (occ) put_checked(o.dout, db + w + __popcll(m & lanemask_lt(lane)), o.dcap, mt_delivery(tb, j), &o.ctr->oob);
+    w += __popcll(m);
+  }
+  __syncthreads();
+  return total;
+}
+
+template <int kSlots>
+__global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs o, const uint32_t *__restrict__ list,
+                                                      const unsigned int *__restrict__ count) {
+  __shared__ unsigned long long tfirst[kSlots];
+  __shared__ uint32_t tkey[kSlots], tbits[kSlots];
+  __shared__ MultiLds L;
+  const MergeTable tb{tkey, tbits, tfirst};
+  const int tid = threadIdx.x;
+  const uint32_t nb = *count;
+  for (uint32_t bi = blockIdx.x; bi < nb; bi += gridDim.x) {
+    const uint32_t t = list[bi];
+    const uint64_t db = o.dstart[t];
+    block_record(o, t, L.rec);
+    const uint32_t nh = L.rec[0] & 0xFFu, Ss = L.rec[1], M = L.rec[2];
     uint32_t lg = 6;
     while ((1u << lg) < 2 * M && (1u << lg) < (uint32_t)kSlots) lg++;
     const uint32_t mask = (1u << lg) - 1;
-    for (uint32_t i = tid; i <= mask; i += kBigThreads) {
-      tkey[i] = 0;
-      tbits[i] = 0;
-      tmin[i] = 0xFFFFFFFFu;
-    }
-    uint32_t cl[kPer], wd[kPer], rk[kPer];
-#pragma unroll
-    for (int k = 0; k < kPer; k++) {  // unconditional loads (entry 0 stands in past M)
-      const uint32_t q = tid + k * kBigThreads;
+    for (uint32_t i = tid; i <= mask; i += kBigThreads) mt_clear(tb, i);
+    __syncthreads();
+    for (uint32_t q = tid; q < M; q += kBigThreads) {
       uint32_t h;
-      const uint32_t sid = multi_sid(rec, nh, Ss, q < M ? q : 0, &h);
-      rk[k] = rec_at(rec, h, kFieldRank);
+      const uint32_t sid = multi_sid(L.rec, nh, Ss, q, &h);
       const SubEnt e = load_sub(s, sid);
-      cl[k] = e.client;
-      wd[k] = e.word;
+      mt_insert(tb, mask, lg, e.client, e.word, rec_at(L.rec, h, kFieldRank));
     }
     __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kPer; k++)
-      if (tid + k * kBigThreads < M) table_insert(tkey, tbits, tmin, mask, lg, cl[k], wd[k], rk[k]);
-    __syncthreads();
-    uint32_t D = Ss;
-#pragma unroll
-    for (int k = 0; k < kPer; k++) {
-      if ((uint32_t)(k * kBigThreads) >= M) break;  // block-uniform
-      const uint32_t q = tid + k * kBigThreads;
-      bool win = false;
-      uint64_t ent = 0;
-      if (q < M) {
-        const uint32_t sl = table_find(tkey, mask, lg, cl[k]);
-        win = tmin[sl] == rk[k];
-        const uint32_t v = tbits[sl];
-        ent = pack_delivery(cl[k], wd[k] & kWordSidMask, 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
-      }
-      const uint64_t m = __ballot(win);
-      if (lane == 0) wsum[wid] = __popcll(m);
-      __syncthreads();
-      uint32_t before = D, round = 0;
-      for (int w = 0; w < kBigThreads / kWave; w++) {
-        if (w < wid) before += wsum[w];
-        round += wsum[w];
-      }
-      if (win) put_checked(o.dout, db + before + __popcll(m & lanemask_lt(lane)), o.dcap, ent, &o.ctr->oob);
-      D += round;
-      __syncthreads();
-    }
+    const uint32_t D = block_winners(tb, mask + 1, L.wsum, o, db, Ss);
     if (tid == 0) o.dcount[t] = D;
-    __syncthreads();
   }
 }
 
-
-// ---------------------------------------------------------------------------
-// k_multi_part: topics with more multi entries than k_multi's tiers hold.  A
-// 256-thread workgroup per topic splits the topic's clients into P =
-// ceil(M / kPartCap) hash partitions and merges them one after another in a
-// 4096-slot LDS table: every pass reads all M entries and keeps its
-// partition's (a client's entries all fall in one partition, so each pass is
-// a complete Subscription.Merge of its clients).  Winners are placed with an
-// LDS counter (order within a topic unspecified, as the reference's Go map).
-// A partition that would overfill the table (never for a hash of this
-// spread; checked) fails the batch instead of spinning.
-// ---------------------------------------------------------------------------
 // client -> partition: a hash independent of table_slot's (which takes the
 // top bits of client * 2654435769: a partition must spread over the table)
 __device__ __forceinline__ uint32_t partition_of(uint32_t client, uint32_t P) {
@@ -1025,66 +1000,42 @@ __global__ __launch_bounds__(kBigThreads) void k_multi_part(DeviceSnapshot s, Ou
                                                            const uint32_t *__restrict__ list,
                                                            const unsigned int *__restrict__ count) {
   constexpr uint32_t kSlots = 4096, kFill = kSlots * 7 / 8;
-  __shared__ uint32_t tkey[kSlots], tbits[kSlots], tmin[kSlots];
-  __shared__ uint32_t rec[kRecStrideAlloc];
-  __shared__ uint32_t fill, nwin;
+  __shared__ unsigned long long tfirst[kSlots];
+  __shared__ uint32_t tkey[kSlots], tbits[kSlots];
+  __shared__ MultiLds L;
+  __shared__ uint32_t fill;
+  const MergeTable tb{tkey, tbits, tfirst};
   const int tid = threadIdx.x;
   const uint32_t nb = *count;
   for (uint32_t bi = blockIdx.x; bi < nb; bi += gridDim.x) {
     const uint32_t t = list[bi];
     const uint64_t db = o.dstart[t];
-    for (uint32_t i = tid; i < (uint32_t)kRecStrideAlloc; i += kBigThreads)
-      rec[i] = o.recs[(uint64_t)t * kRecStrideAlloc + i];
-    __syncthreads();
-    const uint32_t nh = rec[0] & 0xFFu, Ss = rec[1], M = rec[2];
-    __syncthreads();
-    if (tid < kWave) rec_prefix<kWave>(rec, nh, tid);
-    __syncthreads();
+    block_record(o, t, L.rec);
+    const uint32_t nh = L.rec[0] & 0xFFu, Ss = L.rec[1], M = L.rec[2];
     const uint32_t P = (M + kPartCap - 1) / kPartCap;
     uint32_t D = Ss;
     for (uint32_t p = 0; p < P; p++) {
-      for (uint32_t i = tid; i < kSlots; i += kBigThreads) {
-        tkey[i] = 0;
-        tbits[i] = 0;
-        tmin[i] = 0xFFFFFFFFu;
-      }
-      if (tid == 0) fill = nwin = 0;
+      for (uint32_t i = tid; i < kSlots; i += kBigThreads) mt_clear(tb, i);
+      if (tid == 0) fill = 0;
       __syncthreads();
       for (uint32_t q = tid; q < M; q += kBigThreads) {
         uint32_t h;
-        const uint32_t sid = multi_sid(rec, nh, Ss, q, &h);
+        const uint32_t sid = multi_sid(L.rec, nh, Ss, q, &h);
         const SubEnt e = load_sub(s, sid);
         if (partition_of(e.client, P) != p) continue;
-        if (atomicAdd(&fill, 1u) >= kFill) {
+        if (atomicAdd(&fill, 1u) >= kFill) {  // never for a hash of this spread: fail, do not spin
           atomicOr(&o.ctr->oob, 1u);
           continue;
         }
-        table_insert(tkey, tbits, tmin, kSlots - 1, 12, e.client, e.word, rec_at(rec, h, kFieldRank));
+        mt_insert(tb, kSlots - 1, 12, e.client, e.word, rec_at(L.rec, h, kFieldRank));
       }
       __syncthreads();
-      for (uint32_t q = tid; q < M; q += kBigThreads) {
-        uint32_t h;
-        const uint32_t sid = multi_sid(rec, nh, Ss, q, &h);
-        const SubEnt e = load_sub(s, sid);
-        if (partition_of(e.client, P) != p) continue;
-        uint32_t sl = table_slot(e.client, 12);
-        uint32_t probes = 0;
-        while (tkey[sl] != e.client + 1 && probes++ < kSlots) sl = (sl + 1) & (kSlots - 1);
-        if (tkey[sl] != e.client + 1 || tmin[sl] != rec_at(rec, h, kFieldRank)) continue;  // not its client's winner
-        const uint32_t v = tbits[sl];
-        const uint32_t pos = atomicAdd(&nwin, 1u);
-        put_checked(o.dout, db + D + pos, o.dcap,
-                    pack_delivery(e.client, e.word & kWordSidMask, 31u - __builtin_clz(v & 7u), (v >> 3) & 1u),
-                    &o.ctr->oob);
-      }
-      __syncthreads();
-      D += nwin;
-      __syncthreads();
+      D = block_winners(tb, kSlots, L.wsum, o, db, D);
     }
     if (tid == 0) o.dcount[t] = D;
-    __syncthreads();
   }
 }
+
 
 // ---------------------------------------------------------------------------
 // k_dfs<P>: the unbounded path.  P0 counts raw entries / shared candidates;
@@ -1358,32 +1309,63 @@ __global__ __launch_bounds__(256) void k_densify(uint32_t n, const uint32_t *__r
   }
 }
 
-// emit lists: the small class (and the topics with shared candidates only),
-// the big class
-struct IsSmallClass {
-  const uint8_t *cls;
-  const uint32_t *hcount;
-  __host__ __device__ bool operator()(uint32_t t) const {
-    return cls[t] == kClsSmall || (cls[t] == kClsDone && hcount[t] != 0);
+// emission lists in one pass over the topics (replaces one DeviceSelect per
+// list): each block counts its chunk's members per list (wave ballots, LDS
+// counters), reserves its ranges with one global atomic per list, then
+// writes them.  Order within a list is unspecified (lists only schedule
+// work; every topic's output position is its own dstart).
+enum : int { kLSmall = 0, kLBig, kLWave, kLT1, kLT2, kLPart, kNLists };
+constexpr uint32_t kT1Max = 768, kT2Max = 1536;  // k_multi<1024> / <2048> capacities (load 0.75)
+struct Lists {
+  uint32_t *l[kNLists];
+};
+
+__device__ __forceinline__ uint32_t route_mask(uint8_t c, uint32_t h, uint32_t m) {
+  if (c == kClsSmall || (c == kClsDone && h != 0)) return 1u << kLSmall;
+  if (c != kClsBig) return 0;
+  const uint32_t mt = m == 0 ? 0 : m <= kSmallMulti ? (1u << kLWave) : m <= kT1Max ? (1u << kLT1)
+                                   : m <= kT2Max ? (1u << kLT2) : (1u << kLPart);
+  return (1u << kLBig) | mt;
+}
+
+__global__ __launch_bounds__(256) void k_route(const uint8_t *__restrict__ cls, const uint32_t *__restrict__ hcount,
+                                               const uint32_t *__restrict__ mcount, uint32_t n, Lists L,
+                                               unsigned int *__restrict__ counts) {
+  __shared__ unsigned int lc[kNLists], base[kNLists];
+  const int tid = threadIdx.x, lane = tid & (kWave - 1);
+  const uint32_t per = (n + gridDim.x - 1) / gridDim.x;
+  const uint32_t lo = blockIdx.x * per, hi = min(n, lo + per);
+  if (tid < kNLists) lc[tid] = 0;
+  __syncthreads();
+  for (uint32_t t0 = lo; t0 < hi; t0 += blockDim.x) {
+    const uint32_t t = t0 + tid;
+    const uint32_t r = t < hi ? route_mask(cls[t], hcount[t], mcount[t]) : 0;
+#pragma unroll
+    for (int l = 0; l < kNLists; l++) {
+      const uint64_t m = __ballot((r >> l) & 1u);
+      if (lane == 0 && m) atomicAdd(&lc[l], (unsigned int)__popcll(m));
+    }
   }
-};
-struct IsBigClass {
-  const uint8_t *cls;
-  __host__ __device__ bool operator()(uint32_t t) const { return cls[t] == kClsBig; }
-};
-// big-class topics by the merge that dedupes their multi entries
-struct IsWaveMerge {
-  const uint8_t *cls;
-  const uint32_t *mcount;
-  __host__ __device__ bool operator()(uint32_t t) const {
-    return cls[t] == kClsBig && mcount[t] != 0 && mcount[t] <= kSmallMulti;
+  __syncthreads();
+  if (tid < kNLists) {
+    base[tid] = lc[tid] ? atomicAdd(&counts[tid], lc[tid]) : 0;
+    lc[tid] = 0;
   }
-};
-struct IsGroupMerge {
-  const uint8_t *cls;
-  const uint32_t *mcount;
-  __host__ __device__ bool operator()(uint32_t t) const { return cls[t] == kClsBig && mcount[t] > kSmallMulti; }
-};
+  __syncthreads();
+  for (uint32_t t0 = lo; t0 < hi; t0 += blockDim.x) {
+    const uint32_t t = t0 + tid;
+    const uint32_t r = t < hi ? route_mask(cls[t], hcount[t], mcount[t]) : 0;
+#pragma unroll
+    for (int l = 0; l < kNLists; l++) {
+      const bool in = (r >> l) & 1u;
+      const uint64_t m = __ballot(in);
+      uint32_t wpos = 0;
+      if (lane == 0 && m) wpos = atomicAdd(&lc[l], (unsigned int)__popcll(m));
+      wpos = __shfl(wpos, 0, 64);
+      if (in) L.l[l][base[l] + wpos + __popcll(m & lanemask_lt(lane))] = t;
+    }
+  }
+}
 
 #define HIP_TRY(x)                                                                                        \
   do {                                                                                                    \
@@ -1577,29 +1559,22 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
     return -3;
   // emit lists (small class + shared-only topics; big class) and the big
   // class's chunk items, counted before the one host sync that sizes the outputs
-  if (ws.get(W::kListS, sizeof(uint32_t) * (n + 1)) || ws.get(W::kListB, sizeof(uint32_t) * (n + 1)) ||
-      ws.get(W::kNChunk, sizeof(uint32_t) * (n + 1)) || ws.get(W::kCStart, sizeof(uint64_t) * (n + 1)) ||
-      ws.get(W::kDense, sizeof(uint32_t) * (n + 1)) || ws.get(W::kListW, sizeof(uint32_t) * (n + 1)))
-    return -2;
-  o.multi_list = (uint32_t *)ws.ptr(W::kDense);
-  auto *list_w = (uint32_t *)ws.ptr(W::kListW);
-  auto *list_s = (uint32_t *)ws.ptr(W::kListS), *list_b = (uint32_t *)ws.ptr(W::kListB);
+  const W::Slot list_slots[kNLists] = {W::kListS, W::kListB, W::kListW, W::kListT1, W::kListT2, W::kListP};
+  Lists lists;
+  for (int l = 0; l < kNLists; l++) {
+    if (ws.get(list_slots[l], sizeof(uint32_t) * (n + 1))) return -2;
+    lists.l[l] = (uint32_t *)ws.ptr(list_slots[l]);
+  }
+  if (ws.get(W::kNChunk, sizeof(uint32_t) * (n + 1)) || ws.get(W::kCStart, sizeof(uint64_t) * (n + 1))) return -2;
   auto *nchunk = (uint32_t *)ws.ptr(W::kNChunk);
   auto *cstart = (uint64_t *)ws.ptr(W::kCStart);
+  unsigned int *lcount = &o.ctr->n_small;  // kNLists consecutive counters
   if (n > 0) {
-    size_t tmp = 0;
-    hipcub::CountingInputIterator<uint32_t> it(0);
-    HIP_TRY(hipcub::DeviceSelect::If(nullptr, tmp, it, list_s, &o.ctr->n_small, n, IsSmallClass{o.cls, o.hcount}, st));
-    if (ws.get(W::kScanTmp, tmp)) return -2;
-    HIP_TRY(hipcub::DeviceSelect::If(ws.ptr(W::kScanTmp), tmp, it, list_s, &o.ctr->n_small, n,
-                                     IsSmallClass{o.cls, o.hcount}, st));
-    HIP_TRY(hipcub::DeviceSelect::If(ws.ptr(W::kScanTmp), tmp, it, list_b, &o.ctr->n_bigc, n, IsBigClass{o.cls}, st));
-    HIP_TRY(hipcub::DeviceSelect::If(ws.ptr(W::kScanTmp), tmp, it, list_w, &o.ctr->n_wmerge, n,
-                                     IsWaveMerge{o.cls, o.mcount}, st));
-    HIP_TRY(hipcub::DeviceSelect::If(ws.ptr(W::kScanTmp), tmp, it, o.multi_list, &o.ctr->n_multi, n,
-                                     IsGroupMerge{o.cls, o.mcount}, st));
-    hipLaunchKernelGGL(k_chunks, dim3(std::min<uint32_t>((n + 255) / 256, 4096)), dim3(256), 0, st, o, list_b,
-                       &o.ctr->n_bigc, n, nchunk);
+    hipLaunchKernelGGL(k_route, dim3(std::min<uint32_t>((n + 4095) / 4096, 2048)), dim3(256), 0, st, o.cls, o.hcount,
+                       o.mcount, n, lists, lcount);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_chunks, dim3(std::min<uint32_t>((n + 255) / 256, 4096)), dim3(256), 0, st, o,
+                       lists.l[kLBig], lcount + kLBig, n, nchunk);
     HIP_TRY(hipGetLastError());
   }
   if (scan_offsets(ws, (const uint32_t *)nchunk, cstart, n, st)) return -3;
@@ -1666,31 +1641,36 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   if (n > 0) {
     auto grid = [&](auto kern) { return dim3(resident_blocks(ws, 0, kern)); };
     hipLaunchKernelGGL((k_emit_small<5, kEmitU>), grid(k_emit_small<5, kEmitU>), dim3(kWave * kEmitWaves), 0, st, s,
-                       o, list_s, &o.ctr->n_small);
+                       o, lists.l[kLSmall], lcount + kLSmall);
     HIP_TRY(hipGetLastError());
     if (n_items) {
-      hipLaunchKernelGGL(k_items, dim3(std::min<uint32_t>((n + 255) / 256, 4096)), dim3(256), 0, st, list_b,
-                         &o.ctr->n_bigc, cstart, items);
+      hipLaunchKernelGGL(k_items, dim3(std::min<uint32_t>((n + 255) / 256, 4096)), dim3(256), 0, st,
+                         lists.l[kLBig], lcount + kLBig, cstart, items);
       HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL((k_copy<8, kEmitU>), grid(k_copy<8, kEmitU>), dim3(kWave * kEmitWaves), 0, st, s, o, items,
                          n_items);
       HIP_TRY(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_merge, grid(k_merge), dim3(kWave * kEmitWaves), 0, st, s, o, list_w, &o.ctr->n_wmerge);
-    HIP_TRY(hipGetLastError());
-    if (ws.get(W::kOvfList, sizeof(uint32_t) * (n + 1))) return -2;
-    auto *ovf = (uint32_t *)ws.ptr(W::kOvfList);
-    if (ws.get(W::kOvfList2, sizeof(uint32_t) * (n + 1))) return -2;
-    auto *ovf2 = (uint32_t *)ws.ptr(W::kOvfList2);
-    hipLaunchKernelGGL((k_multi<1024, 3>), dim3(resident_blocks(ws, 0, k_multi<1024, 3>)), dim3(kBigThreads), 0, st, s,
-                       o, o.multi_list, &o.ctr->n_multi, ovf, &o.ctr->n_ovf);
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL((k_multi<2048, 6>), dim3(resident_blocks(ws, 1, k_multi<2048, 6>)), dim3(kBigThreads), 0, st, s,
-                       o, ovf, &o.ctr->n_ovf, ovf2, &o.ctr->n_ovf2);
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_multi_part, dim3(resident_blocks(ws, 5, k_multi_part)), dim3(kBigThreads), 0, st, s, o, ovf2,
-                       &o.ctr->n_ovf2);
-    HIP_TRY(hipGetLastError());
+    if (hc->n_wmerge) {
+      hipLaunchKernelGGL(k_merge, grid(k_merge), dim3(kWave * kEmitWaves), 0, st, s, o, lists.l[kLWave],
+                         lcount + kLWave);
+      HIP_TRY(hipGetLastError());
+    }
+    if (hc->n_t1) {
+      hipLaunchKernelGGL(k_multi<1024>, grid(k_multi<1024>), dim3(kBigThreads), 0, st, s, o, lists.l[kLT1],
+                         lcount + kLT1);
+      HIP_TRY(hipGetLastError());
+    }
+    if (hc->n_t2) {
+      hipLaunchKernelGGL(k_multi<2048>, grid(k_multi<2048>), dim3(kBigThreads), 0, st, s, o, lists.l[kLT2],
+                         lcount + kLT2);
+      HIP_TRY(hipGetLastError());
+    }
+    if (hc->n_part) {
+      hipLaunchKernelGGL(k_multi_part, grid(k_multi_part), dim3(kBigThreads), 0, st, s, o, lists.l[kLPart],
+                         lcount + kLPart);
+      HIP_TRY(hipGetLastError());
+    }
   }
   if (n_dfs) {
     hp[4] = s_total;  // Counters::dtail, Counters::htail (pinned staging)
@@ -1734,9 +1714,9 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   out->n_topics = n;
   out->n_deliveries = hp[0];
   out->n_shared = hp[1];
-  out->n_big = hc->n_multi;
-  out->n_tier2 = hc->n_ovf;
-  out->n_tier3 = hc->n_ovf2;
+  out->n_big = hc->n_t1 + hc->n_t2 + hc->n_part;
+  out->n_tier2 = hc->n_t2;
+  out->n_tier3 = hc->n_part;
   out->n_small = hc->n_small;
   out->n_bigc = hc->n_bigc;
   out->n_items = n_items;

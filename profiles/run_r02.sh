@@ -31,6 +31,9 @@ for step in "$@"; do
              > $OUT/bench_c4_shard0of8.json 2> $OUT/bench_c4_shard0of8.log ;;
     host) timeout -k 10 600 python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline \
              > $OUT/bench_host.json 2> $OUT/bench_host.log ;;
+    c4prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv \
+             -d $OUT/prof_c4 -o prof -- python3 $ROOT/bench.py --config 4 --shard 0/8 --steps 3 --warmup 1 \
+             --no-cpu-baseline --host-topics 0 --latency-topics 0 > $OUT/c4_under_rocprof.json 2> $OUT/rocprof_c4.log) ;;
     prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv \
              -d $OUT/prof -o prof -- python3 $ROOT/bench.py $FAST \
              > $OUT/bench_under_rocprof.json 2> $OUT/rocprof.log) ;;
