@@ -273,6 +273,7 @@ def main():
     fallback = 0
     big = 0
     why = {}
+    lists = {}
     for _ in range(args.steps):
         r = step()
         deliveries += int(r.n_deliveries)
@@ -280,6 +281,9 @@ def main():
         fallback = int(r.n_fallback)
         big = int(r.n_big)
         why = dict(zip(["frontier", "hits", "levels", "shared_hits", "raw_entries"], list(r.fallback_why)))
+        lists = {"small": int(r.n_small), "big": int(r.n_bigc), "items": int(r.n_items),
+                 "group_merge": int(r.n_big), "tier2": int(r.n_tier2), "tier3": int(r.n_tier3),
+                 "multi_entries_by_tier": [int(x) for x in r.multi_entries]}
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
@@ -339,6 +343,7 @@ def main():
             "fallback_topics_per_batch": fallback,
             "big_topics_per_batch": big,
             "fallback_reasons": why,
+            "emit_lists": lists,
             "kernel_ms": kms,
             "snapshot": snap,
             "roofline": roof,

@@ -127,6 +127,7 @@ typedef struct {
   uint32_t n_bigc;                /* big-class topics (emitted as chunk items)   */
   uint64_t n_items;               /* big-class chunk items                        */
   uint32_t n_tier2, n_tier3;      /* topics the workgroup merge passed to its 2nd / 3rd tier */
+  uint64_t multi_entries[3];      /* multi entries merged by the workgroup tiers 1 / 2 / 3 */
 } mqm_device_result;
 
 /* ---- lifecycle: NewTopicsIndex (topics.go:291-299) ---------------------- */

@@ -586,6 +586,7 @@ int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t 
     out->n_items = mo.n_items;
     out->n_tier2 = mo.n_tier2;
     out->n_tier3 = mo.n_tier3;
+    for (int i = 0; i < 3; i++) out->multi_entries[i] = mo.multi_entries[i];
     return MQM_OK;
   });
 }

@@ -84,6 +84,7 @@ struct MatchOutput {
   uint32_t n_tier2 = 0, n_tier3 = 0;  // ... of those, passed on to its second / third tier
   uint32_t n_small = 0, n_bigc = 0;   // topics emitted by k_emit_small / by k_copy items
   uint64_t n_items = 0;               // k_copy items (kChunk solo entries each at most)
+  uint64_t multi_entries[3] = {0, 0, 0};  // multi entries merged by the three workgroup tiers
 };
 
 // Runs walk -> scan -> dedupe (small / big / DFS) on `st`; returns 0 or a

@@ -116,6 +116,7 @@ struct Counters {              // zeroed before every batch
   unsigned int n_t1;           // k_multi<1024>: kSmallMulti < Ms <= 768
   unsigned int n_t2;           // k_multi<2048>: 768 < Ms <= 1536
   unsigned int n_part;         // k_multi_part: Ms > 1536
+  unsigned long long m_sum[3]; // multi entries of the k_multi<1024> / <2048> / k_multi_part lists
   unsigned int oob;            // a store fell outside its output buffer (never expected)
 };
 
@@ -926,6 +927,20 @@ __device__ __forceinline__ void block_record(Outputs o, uint32_t t, uint32_t *re
   __syncthreads();
 }
 
+// f(sid, rank) for every multi entry of the topic, hit by hit (the entries of
+// a hit are consecutive sids: coalesced loads, no per-entry search); all
+// threads of the block, block-uniform loop
+template <class F>
+__device__ __forceinline__ void for_multi(const uint32_t *rec, uint32_t nh, uint32_t Ss, uint32_t M, F &&f) {
+  for (uint32_t h = 0; h < nh; h++) {
+    const uint32_t m0 = rec_at(rec, h, kFieldMpre), m1 = h + 1 < nh ? rec_at(rec, h + 1, kFieldMpre) : M;
+    if (m0 == m1) continue;
+    const uint32_t s0 = rec_at(rec, h, kFieldSpre), s1 = h + 1 < nh ? rec_at(rec, h + 1, kFieldSpre) : Ss;
+    const uint32_t base = rec_at(rec, h, kFieldOff) + (s1 - s0), rank = rec_at(rec, h, kFieldRank);
+    for (uint32_t j = threadIdx.x; j < m1 - m0; j += blockDim.x) f(base + j, rank);
+  }
+}
+
 // winners of the table [0, nslots) at out[db + D ..); returns the new D
 __device__ __forceinline__ uint32_t block_winners(MergeTable tb, uint32_t nslots, uint32_t *wsum, Outputs o, uint64_t db,
                                                   uint32_t D) {
@@ -974,12 +989,10 @@ __global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs
     const uint32_t mask = (1u << lg) - 1;
     for (uint32_t i = tid; i <= mask; i += kBigThreads) mt_clear(tb, i);
     __syncthreads();
-    for (uint32_t q = tid; q < M; q += kBigThreads) {
-      uint32_t h;
-      const uint32_t sid = multi_sid(L.rec, nh, Ss, q, &h);
+    for_multi(L.rec, nh, Ss, M, [&](uint32_t sid, uint32_t rank) {
       const SubEnt e = load_sub(s, sid);
-      mt_insert(tb, mask, lg, e.client, e.word, rec_at(L.rec, h, kFieldRank));
-    }
+      mt_insert(tb, mask, lg, e.client, e.word, rank);
+    });
     __syncthreads();
     const uint32_t D = block_winners(tb, mask + 1, L.wsum, o, db, Ss);
     if (tid == 0) o.dcount[t] = D;
@@ -1018,17 +1031,15 @@ __global__ __launch_bounds__(kBigThreads) void k_multi_part(DeviceSnapshot s, Ou
       for (uint32_t i = tid; i < kSlots; i += kBigThreads) mt_clear(tb, i);
       if (tid == 0) fill = 0;
       __syncthreads();
-      for (uint32_t q = tid; q < M; q += kBigThreads) {
-        uint32_t h;
-        const uint32_t sid = multi_sid(L.rec, nh, Ss, q, &h);
+      for_multi(L.rec, nh, Ss, M, [&](uint32_t sid, uint32_t rank) {
         const SubEnt e = load_sub(s, sid);
-        if (partition_of(e.client, P) != p) continue;
+        if (partition_of(e.client, P) != p) return;
         if (atomicAdd(&fill, 1u) >= kFill) {  // never for a hash of this spread: fail, do not spin
           atomicOr(&o.ctr->oob, 1u);
-          continue;
+          return;
         }
-        mt_insert(tb, kSlots - 1, 12, e.client, e.word, rec_at(L.rec, h, kFieldRank));
-      }
+        mt_insert(tb, kSlots - 1, 12, e.client, e.word, rank);
+      });
       __syncthreads();
       D = block_winners(tb, kSlots, L.wsum, o, db, D);
     }
@@ -1330,9 +1341,12 @@ __device__ __forceinline__ uint32_t route_mask(uint8_t c, uint32_t h, uint32_t m
 
 __global__ __launch_bounds__(256) void k_route(const uint8_t *__restrict__ cls, const uint32_t *__restrict__ hcount,
                                                const uint32_t *__restrict__ mcount, uint32_t n, Lists L,
-                                               unsigned int *__restrict__ counts) {
+                                               unsigned int *__restrict__ counts,
+                                               unsigned long long *__restrict__ msum) {
   __shared__ unsigned int lc[kNLists], base[kNLists];
+  __shared__ unsigned long long ms[3];
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
+  if (tid < 3) ms[tid] = 0;
   const uint32_t per = (n + gridDim.x - 1) / gridDim.x;
   const uint32_t lo = blockIdx.x * per, hi = min(n, lo + per);
   if (tid < kNLists) lc[tid] = 0;
@@ -1345,8 +1359,10 @@ __global__ __launch_bounds__(256) void k_route(const uint8_t *__restrict__ cls, 
       const uint64_t m = __ballot((r >> l) & 1u);
       if (lane == 0 && m) atomicAdd(&lc[l], (unsigned int)__popcll(m));
     }
+    if (r >> kLT1) atomicAdd(&ms[(r >> kLPart) & 1u ? 2 : (r >> kLT2) & 1u ? 1 : 0], (unsigned long long)mcount[t]);
   }
   __syncthreads();
+  if (tid < 3 && ms[tid]) atomicAdd(&msum[tid], ms[tid]);
   if (tid < kNLists) {
     base[tid] = lc[tid] ? atomicAdd(&counts[tid], lc[tid]) : 0;
     lc[tid] = 0;
@@ -1571,7 +1587,7 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   unsigned int *lcount = &o.ctr->n_small;  // kNLists consecutive counters
   if (n > 0) {
     hipLaunchKernelGGL(k_route, dim3(std::min<uint32_t>((n + 4095) / 4096, 2048)), dim3(256), 0, st, o.cls, o.hcount,
-                       o.mcount, n, lists, lcount);
+                       o.mcount, n, lists, lcount, o.ctr->m_sum);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_chunks, dim3(std::min<uint32_t>((n + 255) / 256, 4096)), dim3(256), 0, st, o,
                        lists.l[kLBig], lcount + kLBig, n, nchunk);
@@ -1717,6 +1733,7 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   out->n_big = hc->n_t1 + hc->n_t2 + hc->n_part;
   out->n_tier2 = hc->n_t2;
   out->n_tier3 = hc->n_part;
+  for (int i = 0; i < 3; i++) out->multi_entries[i] = hc->m_sum[i];
   out->n_small = hc->n_small;
   out->n_bigc = hc->n_bigc;
   out->n_items = n_items;
