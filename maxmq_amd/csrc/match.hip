@@ -927,20 +927,6 @@ __device__ __forceinline__ void block_record(Outputs o, uint32_t t, uint32_t *re
   __syncthreads();
 }
 
-// f(sid, rank) for every multi entry of the topic, hit by hit (the entries of
-// a hit are consecutive sids: coalesced loads, no per-entry search); all
-// threads of the block, block-uniform loop
-template <class F>
-__device__ __forceinline__ void for_multi(const uint32_t *rec, uint32_t nh, uint32_t Ss, uint32_t M, F &&f) {
-  for (uint32_t h = 0; h < nh; h++) {
-    const uint32_t m0 = rec_at(rec, h, kFieldMpre), m1 = h + 1 < nh ? rec_at(rec, h + 1, kFieldMpre) : M;
-    if (m0 == m1) continue;
-    const uint32_t s0 = rec_at(rec, h, kFieldSpre), s1 = h + 1 < nh ? rec_at(rec, h + 1, kFieldSpre) : Ss;
-    const uint32_t base = rec_at(rec, h, kFieldOff) + (s1 - s0), rank = rec_at(rec, h, kFieldRank);
-    for (uint32_t j = threadIdx.x; j < m1 - m0; j += blockDim.x) f(base + j, rank);
-  }
-}
-
 // winners of the table [0, nslots) at out[db + D ..); returns the new D
 __device__ __forceinline__ uint32_t block_winners(MergeTable tb, uint32_t nslots, uint32_t *wsum, Outputs o, uint64_t db,
                                                   uint32_t D) {
@@ -989,10 +975,12 @@ __global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs
     const uint32_t mask = (1u << lg) - 1;
     for (uint32_t i = tid; i <= mask; i += kBigThreads) mt_clear(tb, i);
     __syncthreads();
-    for_multi(L.rec, nh, Ss, M, [&](uint32_t sid, uint32_t rank) {
+    for (uint32_t q = tid; q < M; q += kBigThreads) {  // (a hit-by-hit loop measured slower: idle lanes on small hits)
+      uint32_t h;
+      const uint32_t sid = multi_sid(L.rec, nh, Ss, q, &h);
       const SubEnt e = load_sub(s, sid);
-      mt_insert(tb, mask, lg, e.client, e.word, rank);
-    });
+      mt_insert(tb, mask, lg, e.client, e.word, rec_at(L.rec, h, kFieldRank));
+    }
     __syncthreads();
     const uint32_t D = block_winners(tb, mask + 1, L.wsum, o, db, Ss);
     if (tid == 0) o.dcount[t] = D;
@@ -1031,15 +1019,17 @@ __global__ __launch_bounds__(kBigThreads) void k_multi_part(DeviceSnapshot s, Ou
       for (uint32_t i = tid; i < kSlots; i += kBigThreads) mt_clear(tb, i);
       if (tid == 0) fill = 0;
       __syncthreads();
-      for_multi(L.rec, nh, Ss, M, [&](uint32_t sid, uint32_t rank) {
+      for (uint32_t q = tid; q < M; q += kBigThreads) {
+        uint32_t h;
+        const uint32_t sid = multi_sid(L.rec, nh, Ss, q, &h);
         const SubEnt e = load_sub(s, sid);
-        if (partition_of(e.client, P) != p) return;
+        if (partition_of(e.client, P) != p) continue;
         if (atomicAdd(&fill, 1u) >= kFill) {  // never for a hash of this spread: fail, do not spin
           atomicOr(&o.ctr->oob, 1u);
-          return;
+          continue;
         }
-        mt_insert(tb, kSlots - 1, 12, e.client, e.word, rank);
-      });
+        mt_insert(tb, kSlots - 1, 12, e.client, e.word, rec_at(L.rec, h, kFieldRank));
+      }
       __syncthreads();
       D = block_winners(tb, kSlots, L.wsum, o, db, D);
     }
