@@ -25,6 +25,7 @@ def _make(subdir, target):
 _make("oracle", "oracle/_build/libmochi_ref.so")
 _make("tools", "tools/_build/libmqgen.so")
 _make("maxmq_amd/csrc", "maxmq_amd/_lib/libmqmatch.so")
+_make("tests/harness", "tests/harness/_build/shim_harness")
 
 
 @pytest.fixture(scope="session")
