@@ -281,8 +281,8 @@ def main():
         fallback = int(r.n_fallback)
         big = int(r.n_big)
         why = dict(zip(["frontier", "hits", "levels", "shared_hits", "raw_entries"], list(r.fallback_why)))
-        lists = {"small": int(r.n_small), "big": int(r.n_bigc), "items": int(r.n_items),
-                 "group_merge": int(r.n_big), "tier2": int(r.n_tier2), "tier3": int(r.n_tier3),
+        lists = {"merge_small": int(r.n_merge_small), "merge_wave": int(r.n_merge_wave),
+                 "solo_ranges": int(r.n_solo_ranges), "group_merge": int(r.n_big), "tier2": int(r.n_tier2), "tier3": int(r.n_tier3),
                  "multi_entries_by_tier": [int(x) for x in r.multi_entries]}
     torch.cuda.synchronize(dev)
     if dist:

@@ -108,14 +108,18 @@ typedef struct {
  * deliveries[starts[t] .. starts[t] + counts[t]) and its shared candidates
  * shared[shared_starts[t] .. + shared_counts[t]).  Segments are in topic
  * order but may leave gaps (a topic reserves its raw-entry count before
- * deduplication); mqm_match_batch returns the dense form. */
+ * deduplication); mqm_match_batch / mqm_dense_device return the dense form.
+ * A device delivery is 4 bytes, the `packed` word of mqm_delivery
+ * (first_sub | qos << 28 | no_local << 30): the delivery's client is the
+ * client of its first-merged subscription (mqm_result_sub_info(...).client,
+ * or the dense form, which carries it). */
 typedef struct {
   uint32_t n_topics;
   uint64_t n_deliveries;          /* sum of counts                              */
   uint64_t n_shared;              /* sum of shared_counts                       */
   const uint64_t *starts;         /* device, n_topics                           */
   const uint32_t *counts;         /* device, n_topics                           */
-  const mqm_delivery *deliveries; /* device                                     */
+  const uint32_t *deliveries;     /* device: packed (MQM_DELIVERY_SUB/QOS/NOLOCAL) */
   const uint64_t *shared_starts;  /* device, n_topics                           */
   const uint32_t *shared_counts;  /* device, n_topics                           */
   const uint32_t *shared;         /* device: shared-subscription ids            */
@@ -123,9 +127,9 @@ typedef struct {
   uint32_t n_big;                 /* topics deduplicated by the workgroup tier  */
   uint32_t fallback_why[5];       /* why topics took the unbounded path: frontier,
                                      hits, cached levels, shared hits, raw entries */
-  uint32_t n_small;               /* topics emitted by the 16-lane small-class kernel */
-  uint32_t n_bigc;                /* big-class topics (emitted as chunk items)   */
-  uint64_t n_items;               /* big-class chunk items                        */
+  uint32_t n_merge_small;         /* topics whose <= 24 multi entries an 8-lane group merged */
+  uint32_t n_merge_wave;          /* topics whose <= 192 multi entries a wavefront merged */
+  uint64_t n_solo_ranges;         /* solo copy ranges (hits with solo entries)    */
   uint32_t n_tier2, n_tier3;      /* topics the workgroup merge passed to its 2nd / 3rd tier */
   uint64_t multi_entries[3];      /* multi entries merged by the workgroup tiers 1 / 2 / 3 */
 } mqm_device_result;

@@ -123,6 +123,7 @@ struct mqm_index {
   uint64_t builds = 0, last_build_ops = 0;
   double last_build_ms = 0;
   int walk_lanes = 4;
+  bool overlap = true;  // MQM_NO_OVERLAP=1: merges serialised behind the solo copy (profiling)
   bool async() const { return (cfg.flags & MQM_CFG_ASYNC_COMMIT) != 0; }
   // the device-result API's context (mqm_match_device & follow-ups)
   std::mutex dev_mu;
@@ -265,6 +266,7 @@ int ctx_init(mqm_index *h, MatchCtx *c) {
     return MQM_EHIP;
   }
   c->ws.walk_lanes = h->walk_lanes;
+  c->ws.overlap = h->overlap;
   return MQM_OK;
 }
 
@@ -378,6 +380,7 @@ int mqm_create(const mqm_config *cfg, mqm_index **out) {
       const int g = atoi(e);
       h->walk_lanes = g == 8 || g == 16 ? g : 4;
     }
+    if (const char *e = getenv("MQM_NO_OVERLAP")) h->overlap = atoi(e) == 0;
     if (ctx_init(h.get(), &h->dev) != MQM_OK) return MQM_EHIP;
     *out = h.release();
     return MQM_OK;
@@ -574,16 +577,16 @@ int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t 
     out->n_shared = mo.n_shared;
     out->starts = mo.starts;
     out->counts = mo.counts;
-    out->deliveries = reinterpret_cast<const mqm_delivery *>(mo.deliveries);
+    out->deliveries = mo.deliveries;
     out->shared_starts = mo.shared_starts;
     out->shared_counts = mo.shared_counts;
     out->shared = mo.shared;
     out->n_fallback = mo.n_fallback;
     out->n_big = mo.n_big;
     for (int i = 0; i < 5; i++) out->fallback_why[i] = c.ws.why[i];
-    out->n_small = mo.n_small;
-    out->n_bigc = mo.n_bigc;
-    out->n_items = mo.n_items;
+    out->n_merge_small = mo.n_merge_small;
+    out->n_merge_wave = mo.n_merge_wave;
+    out->n_solo_ranges = mo.n_solo_ranges;
     out->n_tier2 = mo.n_tier2;
     out->n_tier3 = mo.n_tier3;
     for (int i = 0; i < 3; i++) out->multi_entries[i] = mo.multi_entries[i];
@@ -619,7 +622,7 @@ int mqm_match_batch(mqm_index *h, const char *topic_bytes, const uint64_t *topic
       const bool want_ids = (h->cfg.flags & MQM_CFG_IDENTIFIERS) != 0;
       if (want_ids && (e = identifiers_device(snap->dev, ws, st, &io)) != 0) return hip_rc(e);
       DenseOutput dn;
-      if ((e = densify(ws, mo, st, &dn)) != 0) return hip_rc(e);
+      if ((e = densify(snap->dev, ws, mo, st, &dn)) != 0) return hip_rc(e);
       // one pinned block: three offset arrays, then the entries (16-B aligned parts)
       const uint64_t n1 = (uint64_t)n_topics + 1, ni = want_ids ? io.n_idents : 0;
       auto up = [](uint64_t b) { return (b + 15) & ~15ull; };
@@ -696,7 +699,7 @@ int mqm_dense_device(mqm_index *h, void *hip_stream, mqm_device_dense *out) {
     const hipStream_t st = (hipStream_t)hip_stream;
     c.ws.begin(st);
     DenseOutput dn;
-    int rc = densify(c.ws, c.last_mo, st, &dn);
+    int rc = densify(c.snap->dev, c.ws, c.last_mo, st, &dn);
     if (c.ws.end(st)) rc = rc ? rc : -3;
     if (rc != 0) return hip_rc(rc);
     out->n_topics = c.last_mo.n_topics;

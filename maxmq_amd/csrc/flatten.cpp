@@ -5,6 +5,7 @@
 // (vendor/.../mqtt/v2/topics.go:503) — so rank = 2*node+slot orders hits
 // exactly as the reference walk emits them (snapshot.h).
 #include "flatten.h"
+#include "match.h"
 
 #include <hip/hip_runtime.h>
 
@@ -513,6 +514,7 @@ int flatten(const Store &st, HostSnapshot *out) {
 GpuSnapshot::~GpuSnapshot() {
   for (void *b : buffers)
     if (b) (void)hipFree(b);
+  if (words) (void)hipFree(words);
 }
 
 int upload(std::shared_ptr<const HostSnapshot> hs, int device, hipStream_t stream, std::unique_ptr<GpuSnapshot> *out) {
@@ -541,6 +543,11 @@ int upload(std::shared_ptr<const HostSnapshot> hs, int device, hipStream_t strea
       return MQM_EHIP;
     g->device_bytes += sz[i];
   }
+  // the packed delivery of every subscription entry (snapshot.h: words)
+  const uint64_t n_sub_ents = hs->subs.size();
+  if (hipMalloc(&g->words, n_sub_ents * 4 + 64) != hipSuccess) return MQM_ENOMEM;
+  if (derive_words((const SubEnt *)g->buffers[2], (uint32_t *)g->words, n_sub_ents, stream)) return MQM_EHIP;
+  g->device_bytes += n_sub_ents * 4;
   if (hipStreamSynchronize(stream) != hipSuccess) return MQM_EHIP;
   if (ret) {
     g->has_retained = true;
@@ -559,6 +566,7 @@ int upload(std::shared_ptr<const HostSnapshot> hs, int device, hipStream_t strea
   g->dev.nodes = (const NodeDesc *)g->buffers[0];
   g->dev.edges = (const EdgeEntry *)g->buffers[1];
   g->dev.subs = (const SubEnt *)g->buffers[2];
+  g->dev.words = (const uint32_t *)g->words;
   g->dev.tok_pool = (const uint8_t *)g->buffers[3];
   g->dev.n_buckets = hs->n_buckets;
   g->dev.n_nodes = (uint32_t)hs->nodes.size();

@@ -68,6 +68,7 @@ struct GpuSnapshot {
   std::shared_ptr<const HostSnapshot> host;
   static constexpr int kNumBuffers = 11;
   void *buffers[kNumBuffers] = {};
+  void *words = nullptr;  // DeviceSnapshot::words (derived on the device at upload)
   DeviceRetained ret{};
   bool has_retained = false;
   uint64_t device_bytes = 0;

@@ -15,7 +15,7 @@ struct Workspace {
   enum Slot {
     kSCount, kHCount, kDCount, kDStart, kHStart, kCls, kDfsList, kRecs, kCounters, kDOut, kHOut,
     kDense, kDenseShared, kDenseOffs, kDenseHOffs, kScanTmp, kRawCnt, kTabOff, kTabSize, kTable,
-    kInBytes, kInOffs, kOvfList, kOvfList2, kListS, kListB, kICount, kIStart, kIOut, kNChunk, kCStart, kItems, kMCount, kListW, kListT1, kListT2, kListP,
+    kInBytes, kInOffs, kListS, kICount, kIStart, kIOut, kNSolo, kDescStart, kDesc, kWin, kMCount, kListW, kListT1, kListT2, kListP, kListH,
     // reverse match (retained.hip)
     kROffs, kRNLev, kRWild, kRLOff, kRFCount, kRFCur, kRLevels, kRNCount, kRNOff, kRItemF0, kRItemN0, kRItemF1,
     kRItemN1, kRChild, kRECount, kREOff, kREmit, kRPos, kRChunks, kRCOff, kROut, kRInBytes, kRInOffs, kNumSlots
@@ -34,8 +34,7 @@ struct Workspace {
   uint32_t why[5] = {0, 0, 0, 0, 0};
   // the last match_device call (identifiers_device works on its records)
   bool last_valid = false;
-  uint32_t last_n = 0, last_n_dfs = 0, last_small = 0, last_bigc = 0;
-  uint64_t last_items = 0;
+  uint32_t last_n = 0, last_n_dfs = 0;
   const uint8_t *last_bytes = nullptr;
   const uint64_t *last_offs = nullptr;
 
@@ -58,6 +57,13 @@ struct Workspace {
   bool used = false;
   void begin(hipStream_t st) { cur = st; }
   int end(hipStream_t st);       // record last_use on st
+  // a second stream for work that may overlap the call's main stream: fork()
+  // orders it after st's queued work, join() orders st after it (both by events)
+  bool overlap = true;  // merges on the side stream (capi: MQM_NO_OVERLAP=1 serialises them, for profiling)
+  hipStream_t side = nullptr;
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+  int fork(hipStream_t st, hipStream_t *out);
+  int join(hipStream_t st, hipStream_t side_st);
   int drain();                   // wait for every queued use of the buffers
   int reserve(void **p, size_t *cap, size_t need);
   int get(Slot s, size_t need) { return reserve(&bufs[s].p, &bufs[s].cap, need); }
@@ -75,17 +81,20 @@ struct MatchOutput {
   uint64_t n_deliveries = 0, n_shared = 0;
   const uint64_t *starts = nullptr;      // device, n
   const uint32_t *counts = nullptr;      // device, n
-  const uint64_t *deliveries = nullptr;  // device, packed (snapshot.h)
+  const uint32_t *deliveries = nullptr;  // device, packed (snapshot.h: sid | qos << 28 | no_local << 30)
   const uint64_t *shared_starts = nullptr;
   const uint32_t *shared_counts = nullptr;
   const uint32_t *shared = nullptr;
   uint32_t n_fallback = 0;  // topics on the unbounded DFS path
   uint32_t n_big = 0;       // topics whose multi entries the workgroup tier merged
   uint32_t n_tier2 = 0, n_tier3 = 0;  // ... of those, passed on to its second / third tier
-  uint32_t n_small = 0, n_bigc = 0;   // topics emitted by k_emit_small / by k_copy items
-  uint64_t n_items = 0;               // k_copy items (kChunk solo entries each at most)
+  uint32_t n_merge_small = 0, n_merge_wave = 0;  // topics merged by k_merge_small / k_merge
+  uint64_t n_solo_ranges = 0;                     // solo copy descriptors (hits with solo entries)
   uint64_t multi_entries[3] = {0, 0, 0};  // multi entries merged by the three workgroup tiers
 };
+
+// words[i] = subs[i].word & kPackedMask for i < n (snapshot upload, on `st`)
+int derive_words(const SubEnt *subs, uint32_t *words, uint64_t n, hipStream_t st);
 
 // Runs walk -> scan -> dedupe (small / big / DFS) on `st`; returns 0 or a
 // negative MQM_E* code.
@@ -108,6 +117,7 @@ struct DenseOutput {
   const uint64_t *offsets = nullptr, *deliveries = nullptr, *shared_offsets = nullptr;
   const uint32_t *shared = nullptr;
 };
-int densify(Workspace &ws, const MatchOutput &m, hipStream_t st, DenseOutput *out);
+// (clients resolved through the snapshot the match read)
+int densify(const DeviceSnapshot &s, Workspace &ws, const MatchOutput &m, hipStream_t st, DenseOutput *out);
 
 }  // namespace mqm

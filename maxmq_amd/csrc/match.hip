@@ -44,14 +44,20 @@
 #include "device.h"
 #include "match.h"
 
-// MQM_REC16_WORDS: record words k_emit<16> prefetches per topic (64 or 128)
-#ifndef MQM_REC16_WORDS
-#define MQM_REC16_WORDS 64
+// MQM_WALK_OCC: k_walk's waves-per-SIMD target (1 = let the compiler use
+// the registers it wants; `make variant VFLAGS=-DMQM_WALK_OCC=6` sweeps it)
+#ifndef MQM_WALK_OCC
+#define MQM_WALK_OCC 1
 #endif
 // MQM_NT_OUT=1: non-temporal output stores (tuning knob, `make variant`; C3
 // sweep profiles/r01/c3_v14_nt_tail_sweep.log: no gain, off)
 #ifndef MQM_NT_OUT
 #define MQM_NT_OUT 0
+#endif
+// MQM_COPY16=1: solo copies move 2 entries per lane and access (16-B stores,
+// round 1's form) instead of lane-consecutive 8-B entries (tuning knob)
+#ifndef MQM_COPY16
+#define MQM_COPY16 0
 #endif
 
 namespace mqm {
@@ -71,22 +77,24 @@ constexpr int kStage = 64;               // topic bytes staged in LDS (4 per lan
 //            its range subs[off ..) holds solo entries, then multi ones
 //            (snapshot.h); spre / mpre = solo / multi entries of hits < h
 //   [kRecSh + 2i] off, [kRecSh + 1 + 2i] cnt of shared hit i (i < nsh)
+//   [kRecSolo + 2i] off, [kRecSolo + 1 + 2i] solo count of the i-th hit with
+//            solo entries (i < nsolo[t]): k_desc's input, read without the hits
 // One 64-lane load fetches the header and the first 15 hits.
 constexpr int kRecHit = 4;
-constexpr int kRecSh = 4 + kRecHit * kHCap;          // 260
-constexpr int kRecStride = kRecSh + 2 * kShCap;       // 292 words (max)
-constexpr int kRecStrideAlloc = 292;                  // 16-B aligned per topic
+constexpr int kRecSh = 4 + kRecHit * kHCap;          // 260: header + hits (what the merges read)
+constexpr int kRecSolo = kRecSh + 2 * kShCap;         // 292
+constexpr int kRecStride = kRecSolo + 2 * kHCap;      // 420 words (max)
+constexpr int kRecStrideAlloc = 420;                  // 16-B aligned per topic
 // raw entries per hit range on the bounded path (keeps the per-lane sums of a
 // topic's 64 hits inside 32 bits); emission itself has no per-topic size
-// limit (k_copy items; partitioned merge of any number of multi entries)
+// limit (window copy of the solo part; partitioned merge of any number of
+// multi entries)
 constexpr uint32_t kSMax = 1u << 24;
-constexpr int kEmitU = 4;                // solo entries in flight per lane
 constexpr int kEmitWaves = 4;
-constexpr int kSmallLanes = 8;           // k_emit_small: lanes per topic of the small class
-constexpr uint32_t kSmallSolo = 256;     // small class: at most this many solo entries,
-constexpr uint32_t kSmallHits = 15;      //   hits (its record is one 64-word prefetch)
+constexpr int kSmallLanes = 8;           // k_merge_small: lanes per topic
+constexpr uint32_t kSmallHits = 15;      // k_merge_small: at most this many hits (one 64-word record prefetch)
 constexpr uint32_t kSmallMultiS = 3 * kSmallLanes;  //   and multi entries
-constexpr int kSmallSlots = 256;         // k_emit merge table slots (per wave)
+constexpr int kSmallSlots = 256;         // k_merge table slots (per wave)
 constexpr int kSmallMulti = 192;         // multi entries it holds (load <= 0.75)
 constexpr int kBigThreads = 256;
 constexpr int kPartCap = 2048;           // k_multi_part: multi entries per client partition (expected)
@@ -94,6 +102,7 @@ constexpr uint32_t kNoWhy = 0xFFFFFFFFu;
 constexpr int kICap = 3 * kFCap;         // load items per level (<= 3 per frontier node)
 
 static_assert(kRecStrideAlloc % 4 == 0 && kRecStrideAlloc >= kRecStride, "16-B aligned records");
+static_assert(kRecSh % 4 == 0, "16-B aligned record prefix");
 static_assert(kSmallMulti * 4 <= kSmallSlots * 3, "k_emit table load factor");
 static_assert(kSmallMulti % kWave == 0, "register tiles");
 
@@ -101,7 +110,9 @@ static_assert(kSmallMulti % kWave == 0, "register tiles");
 // descriptor load of its '+' / '#' child
 enum : uint32_t { kItemLit = 0, kItemPlus = 1, kItemHash = 2 };
 
-enum : uint8_t { kClsDone = 0, kClsSmall = 1, kClsBig = 2, kClsDfs = 3 };
+// topic class (cls): Done = no entries and no shared candidates; Bounded (+
+// FewHits when nh <= kSmallHits, for k_route) = emitted from its record; Dfs
+enum : uint8_t { kClsDone = 0, kClsBounded = 1, kClsDfs = 2, kClsFewHits = 4 };
 enum : uint32_t { kWhyFrontier = 0, kWhyHits = 1, kWhyLevels = 2, kWhyShared = 3, kWhyEntries = 4 };
 
 struct Counters {              // zeroed before every batch
@@ -109,13 +120,13 @@ struct Counters {              // zeroed before every batch
   unsigned long long htail;    // DFS shared candidates: likewise
   unsigned int n_dfs;          // topics appended to the DFS list
   unsigned int why[5];         // DFS routing reasons (kWhy*)
-  // emission lists (k_route), in kList* order
-  unsigned int n_small;        // k_emit_small: small class + topics with shared candidates only
-  unsigned int n_bigc;         // k_copy: the big class
-  unsigned int n_wmerge;       // k_merge: big class, 0 < Ms <= kSmallMulti
+  // merge lists (k_route), in kList* order
+  unsigned int n_small;        // k_merge_small: 0 < Ms <= kSmallMultiS, nh <= kSmallHits
+  unsigned int n_wmerge;       // k_merge: other topics with Ms <= kSmallMulti
   unsigned int n_t1;           // k_multi<1024>: kSmallMulti < Ms <= 768
   unsigned int n_t2;           // k_multi<2048>: 768 < Ms <= 1536
   unsigned int n_part;         // k_multi_part: Ms > 1536
+  unsigned int n_shlist;       // k_shared: topics with shared candidates
   unsigned long long m_sum[3]; // multi entries of the k_multi<1024> / <2048> / k_multi_part lists
   unsigned int oob;            // a store fell outside its output buffer (never expected)
 };
@@ -123,12 +134,13 @@ struct Counters {              // zeroed before every batch
 struct Outputs {
   uint32_t *scount, *hcount, *dcount;
   uint32_t *mcount;           // multi entries per topic (Ms; 0 for DFS topics)
+  uint32_t *nsolo;            // hits with solo entries per topic (k_desc's descriptors)
   uint64_t *dstart, *hstart;  // n + 1 (exclusive scans; DFS topics overwritten)
   uint8_t *cls;
   uint32_t *dfs_list;
   uint32_t *recs;  // kRecStrideAlloc words per topic
   Counters *ctr;
-  uint64_t *dout;
+  uint32_t *dout;  // packed deliveries (snapshot.h)
   uint32_t *hout;
   // identifiers pass (identifiers_device): per-topic counts, starts, sids
   uint32_t *icount;
@@ -139,11 +151,15 @@ struct Outputs {
   uint64_t dcap, hcap;
 };
 
-struct TopicLds {              // k_walk context of one topic (one 16-lane group)
+struct TopicLds {              // k_walk context of one topic (one lane group)
   uint32_t sep[kLMax];         // position of the '/' ending level k
   uint32_t item[2][kICap];     // the level's load items: node id << 2 | kind (kItem*)
   uint8_t stage[kStage];       // the topic's first kStage bytes
+  uint32_t pad[4];             // 132-dword stride: the groups of a wave reading the same
+                               //   field hit 4 banks apart (a 128-dword stride put all 16
+                               //   groups on one bank: SQ_LDS_BANK_CONFLICT 3x the LDS cycles)
 };
+static_assert(sizeof(TopicLds) % 256 == 16, "bank-skewed topic contexts");
 
 __device__ __forceinline__ void wave_lds_sync() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -181,8 +197,8 @@ __device__ __forceinline__ void put_checked(T *out, uint64_t i, uint64_t cap, T 
     atomicOr(oob, 1u);
 }
 
-__device__ __forceinline__ uint64_t pack_delivery(uint32_t client, uint32_t sid, uint32_t qos, uint32_t nl) {
-  return (uint64_t)client | ((uint64_t)(sid | (qos << 28) | (nl << 30)) << 32);
+__device__ __forceinline__ uint32_t pack_delivery(uint32_t sid, uint32_t qos, uint32_t nl) {
+  return sid | (qos << 28) | (nl << 30);
 }
 
 // QoS one-hot (bits 0..2) | NoLocal (bit 3) of a SubEnt word: OR-merged, max
@@ -246,9 +262,9 @@ __device__ __forceinline__ void mt_insert(MergeTable t, uint32_t mask, uint32_t 
   atomicMin(&t.first[sl], ((unsigned long long)rank << 32) | (word & kWordSidMask));
 }
 
-__device__ __forceinline__ uint64_t mt_delivery(MergeTable t, uint32_t j) {
+__device__ __forceinline__ uint32_t mt_delivery(MergeTable t, uint32_t j) {
   const uint32_t v = t.bits[j];
-  return pack_delivery(t.key[j] - 1, (uint32_t)t.first[j], 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
+  return pack_delivery((uint32_t)t.first[j] & kWordSidMask, 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
 }
 
 
@@ -394,7 +410,7 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
     // the '#' child's gather be recorded at push time: partKey '#' of the
     // next level, topics.go:503-505, rank 2 * '#' child).
     uint32_t *rec = o.recs + (uint64_t)(active ? t : 0) * kRecStrideAlloc;
-    uint32_t ni = nlev > 0 ? root_items : 0, nh = 0, nsh = 0;
+    uint32_t ni = nlev > 0 ? root_items : 0, nh = 0, nsh = 0, nq = 0;
     uint32_t ls = 0, lm = 0, lh = 0;  // this lane's solo / multi / shared entries
     int cur = 0;
     for (uint32_t d = 0; d < nlev && ni > 0; d++) {
@@ -472,6 +488,21 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
           const uint32_t i = nsh + __popc(m_sh & gmask_lt);
           *reinterpret_cast<uint2 *>(rec + kRecSh + 2 * i) = make_uint2(dc.sh_off, c_sh);
         }
+        // the hits with solo entries again, as (off, solo count) pairs in the
+        // same order: k_desc reads these instead of every hit
+        const uint32_t q_own = (uint32_t)(__ballot(c_own > mu_own) >> gbase) & kGMask;
+        const uint32_t q_par = (uint32_t)(__ballot(c_par > mu_par) >> gbase) & kGMask;
+        const uint32_t q_hl = (uint32_t)(__ballot(c_hl > mu_hl) >> gbase) & kGMask;
+        if (active && c_own > mu_own)
+          *reinterpret_cast<uint2 *>(rec + kRecSolo + 2 * (nq + __popc(q_own & gmask_lt))) =
+              make_uint2(dc.sub_off, c_own - mu_own);
+        if (active && c_par > mu_par)
+          *reinterpret_cast<uint2 *>(rec + kRecSolo + 2 * (nq + __popc(q_own) + __popc(q_par & gmask_lt))) =
+              make_uint2(dc.sub_off + dc.sub_cnt, c_par - mu_par);
+        if (active && c_hl > mu_hl)
+          *reinterpret_cast<uint2 *>(rec + kRecSolo + 2 * (nq + __popc(q_own) + __popc(q_par) + __popc(q_hl & gmask_lt))) =
+              make_uint2(dc.sub_off + dc.sub_cnt, c_hl - mu_hl);
+        nq += __popc(q_own) + __popc(q_par) + __popc(q_hl);
         if (push) {
           uint32_t *nx = &L.item[cur ^ 1][nnext + __popc(m_i0 & gmask_lt) + 2 * __popc(m_i1 & gmask_lt)];
           uint32_t k = 0;
@@ -507,10 +538,8 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
         rec[1] = Ss;
         rec[2] = Ms;
       }
-      o.cls[t] = dfs ? kClsDfs
-                 : S == 0 ? kClsDone
-                 : (Ss <= kSmallSolo && Ms <= kSmallMultiS && nh <= kSmallHits) ? kClsSmall
-                                                                 : kClsBig;
+      o.cls[t] = dfs ? kClsDfs : (S == 0 && H == 0) ? kClsDone : (kClsBounded | (nh <= kSmallHits ? kClsFewHits : 0));
+      o.nsolo[t] = dfs ? 0 : nq;
       o.scount[t] = dfs ? 0 : S;
       o.hcount[t] = dfs ? 0 : H;
       o.mcount[t] = dfs ? 0 : Ms;
@@ -529,24 +558,27 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
 // of its raw-entry count S, an upper bound): first its solo entries, each its
 // client's merged delivery as is (delivery q = solo entry q), then the
 // winners of the merge of its multi entries, compacted.  dcount[t] = Ss +
-// winners.  Three kernels by size:
-//   k_emit_small  8 lanes per topic (8 topics per wavefront) for topics with
-//                 Ss <= kSmallSolo, Ms <= 24 and <= 15 hits: solo copy + a
-//                 64-slot LDS merge table; also every topic with shared
-//                 candidates only.
-//   k_copy        the big class, cut into items of kChunk solo entries (a
-//                 wavefront per item, static striding over equal-sized
-//                 items: no Zipf hub topic holds a wave for long).  Item 0 of
-//                 a topic also writes its shared candidates and merges up to
-//                 kSmallMulti multi entries in a 256-slot table; more go to
-//                 k_multi.
-//   k_multi       a 256-thread workgroup per topic with more multi entries.
+// winners.  The two parts are produced independently:
+//   solo   : k_desc turns every topic's solo hits into copy descriptors
+//            (src subs offset, length, absolute output position) in topic
+//            order, so the solo output is a set of disjoint, increasing
+//            ranges of dout; k_winmap / k_wincopy then copy it in fixed
+//            windows of the OUTPUT space (kWin entries, a wavefront each):
+//            perfectly balanced whatever the topic sizes (Zipf hubs and
+//            one-hit topics alike), one dependent setup load per window and
+//            lane-consecutive 8-B loads and stores.  k_desc also writes the
+//            shared candidates (id ranges) and dcount of topics without
+//            multi entries.
+//   merge  : topics with multi entries, by their count Ms (k_route lists):
+//            k_merge_small (8 lanes per topic, Ms <= 24, <= 15 hits),
+//            k_merge (a wavefront, Ms <= 192), k_multi<1024|2048>,
+//            k_multi_part.  They run on a second stream, concurrently with
+//            the solo copy (disjoint outputs).
 // The merge: an LDS hash table keyed by client — atomicOr folds QoS (one-hot)
-// and NoLocal, atomicMin keeps the lowest hit rank; an entry is its client's
-// winner iff its hit has that rank: exactly Subscription.Merge
-// (packets.go:250-270) with the first-merged subscription's fields.
+// and NoLocal, a 64-bit atomicMin keeps the lowest (hit rank, sid): exactly
+// Subscription.Merge (packets.go:250-270) with the first-merged
+// subscription's fields.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kChunk = 2048;  // solo entries per k_copy item
 
 // multi entry q of a topic: subs index and hit
 __device__ __forceinline__ uint32_t multi_sid(const uint32_t *rec, uint32_t nh, uint32_t Ss, uint32_t q,
@@ -557,90 +589,159 @@ __device__ __forceinline__ uint32_t multi_sid(const uint32_t *rec, uint32_t nh, 
   return rec_at(rec, h, kFieldOff) + solo_h + (q - rec_at(rec, h, kFieldMpre));
 }
 
-// solo entry q of a topic (hit located by binary search)
-__device__ __forceinline__ uint32_t solo_sid(const uint32_t *rec, uint32_t nh, uint32_t q) {
-  const uint32_t h = hit_of<kFieldSpre>(rec, nh, q);
-  return rec_at(rec, h, kFieldOff) + (q - rec_at(rec, h, kFieldSpre));
-}
-
 __device__ __forceinline__ SubEnt load_sub(const DeviceSnapshot &s, uint32_t sid) {
   const uint2 v = *reinterpret_cast<const uint2 *>(s.subs + sid);
   return SubEnt{v.x, v.y};
 }
 
-// unaligned-capable 16-B accesses (8-B aligned: gfx950 runs dword-aligned
-// vector memory accesses, ROCm's default alignment mode)
-typedef uint32_t u32x4_a8 __attribute__((ext_vector_type(4), aligned(8)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
-// solo entries q in [lo, hi) of a topic whose record (prefixes) is in LDS, to
-// out[db + q]: a kE-lane group moves 2 consecutive positions per lane and
-// access — 16-B stores always, 16-B loads when one hit holds the whole step
-// (hub ranges; else each entry's hit is found by hit_of) — kU accesses per
-// lane, and the next step's loads are issued before this step's stores (two
-// register sets, so no register copy waits for a load).
-template <int kE, int kU>
-__device__ __forceinline__ void copy_solo(const DeviceSnapshot &s, const uint32_t *rec, uint32_t nh, uint32_t Ss,
-                                          uint32_t lo, uint32_t hi, int gl, uint64_t *out, uint64_t db, uint64_t cap,
-                                          unsigned int *oob) {
-  constexpr uint32_t kStep = 2u * kE * kU;
-  // subs through a buffer descriptor: 32-bit offsets (one VGPR per load
-  // address instead of two) and bounds-checked reads (the snapshot pads the
-  // array by 64 B, so entry n_subs is readable)
-  const __amdgpu_buffer_rsrc_t subs =
-      __builtin_amdgcn_make_buffer_rsrc((void *)s.subs, (short)0, (int)(s.n_subs * 8u + 64u), 0x00020000);
-  auto issue = [&](uint32_t base, u32x4_a8 (&dst)[kU]) {
-    // addresses first (branch-free loads after: a load whose result merged
-    // out of two branches would need a wait before the register copy)
-    const uint32_t h0 = hit_of<kFieldSpre>(rec, nh, base);  // group-uniform
-    const uint32_t end0 = h0 + 1 < nh ? rec_at(rec, h0 + 1, kFieldSpre) : Ss;
-    const uint32_t d0 = rec_at(rec, h0, kFieldOff) - rec_at(rec, h0, kFieldSpre);
-    uint32_t sa[kU], sb[kU];
-#pragma unroll
-    for (int u = 0; u < kU; u++) {
-      const uint32_t q = base + 2u * (u * kE + gl);
-      sa[u] = d0 + q;
-      sb[u] = d0 + q + 1;
+// ---- k_desc: solo hits -> copy descriptors ----------------------------------
+// A thread per topic: its solo pairs (off, solo count; the walk listed them
+// apart from the hits) become descriptors at desc_start[t] .., with the
+// running solo prefix as the output position.  Per-topic arrays are read
+// coalesced; a topic with no solo hit reads nothing else.  Also dcount of
+// topics without multi entries (the merges write the others').
+__global__ __launch_bounds__(256) void k_desc(Outputs o, uint32_t n, const uint64_t *__restrict__ desc_start,
+                                              uint4 *__restrict__ desc, uint64_t desc_cap) {
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+    const uint8_t cls = o.cls[t];
+    if (!(cls & kClsBounded)) continue;
+    const uint32_t q = o.nsolo[t];
+    if (o.mcount[t] == 0) o.dcount[t] = o.scount[t];
+    if (q == 0) continue;
+    const uint64_t db = o.dstart[t], pb = desc_start[t];
+    const uint2 *pr = reinterpret_cast<const uint2 *>(o.recs + (uint64_t)t * kRecStrideAlloc + kRecSolo);
+    uint64_t at = db;
+    for (uint32_t i = 0; i < q; i++) {
+      const uint2 v = pr[i];
+      put_checked(desc, pb + i, desc_cap, make_uint4(v.x, v.y, (uint32_t)at, (uint32_t)(at >> 32)), &o.ctr->oob);
+      at += v.y;
     }
-    if (base + kStep > end0) {  // the step crosses a hit boundary: per-entry search
-#pragma unroll
-      for (int u = 0; u < kU; u++) {
-        const uint32_t q = base + 2u * (u * kE + gl);
-        sa[u] = solo_sid(rec, nh, q < hi ? q : lo);
-        sb[u] = solo_sid(rec, nh, q + 1 < hi ? q + 1 : lo);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < kU; u++) {
-      const u32x2 a = __builtin_amdgcn_raw_buffer_load_b64(subs, (int)(sa[u] * 8u), 0, 0);
-      const u32x2 b = __builtin_amdgcn_raw_buffer_load_b64(subs, (int)(sb[u] * 8u), 0, 0);
-      dst[u] = u32x4_a8{a.x, a.y, b.x, b.y};
-    }
-  };
-  auto store = [&](uint32_t base, u32x4_a8 (&v)[kU]) {
-#pragma unroll
-    for (int u = 0; u < kU; u++) {
-      const uint32_t q = base + 2u * (u * kE + gl);
-      u32x4_a8 d = v[u];
-      d.y &= 0x7FFFFFFFu;  // SubEnt word -> delivery (snapshot.h)
-      d.w &= 0x7FFFFFFFu;
-      if (q < hi && db + q + (q + 1 < hi ? 1 : 0) >= cap) {
-        atomicOr(oob, 1u);
-      } else if (q + 1 < hi) {
-        *reinterpret_cast<u32x4_a8 *>(out + db + q) = d;
-      } else if (q < hi) {
-        out[db + q] = ((uint64_t)d.y << 32) | d.x;
-      }
-    }
-  };
-  // latency is hidden by occupancy (many waves, kU 16-B accesses each) rather
-  // than by a software pipeline: a two-register-set pipeline made hipcc reuse
-  // registers with loads in flight and wait for them anyway
-  for (uint32_t base = lo; base < hi; base += kStep) {
-    u32x4_a8 v[kU];
-    issue(base, v);
-    store(base, v);
   }
+}
+
+// ---- k_shared: shared candidates (gatherSharedSubscriptions, topics.go:541-555)
+// a 16-lane group per topic with H > 0: its shared hits are id ranges
+constexpr int kHL = 16;
+__global__ __launch_bounds__(256) void k_shared(Outputs o, const uint32_t *__restrict__ list,
+                                                const unsigned int *__restrict__ count) {
+  const int lane = threadIdx.x & (kWave - 1), g = lane / kHL, gl = lane % kHL;
+  const uint32_t nl = *count, stride = gridDim.x * (blockDim.x / kHL);
+  for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) / kHL; i < nl; i += stride) {
+    (void)g;
+    const uint32_t t = list[i];
+    const uint32_t *grec = o.recs + (uint64_t)t * kRecStrideAlloc;
+    const uint32_t nsh = grec[0] >> 8;
+    const uint64_t hb = o.hstart[t];
+    uint32_t w = 0;
+    for (uint32_t j = 0; j < nsh; j++) {
+      const uint32_t so = grec[kRecSh + 2 * j], c = grec[kRecSh + 1 + 2 * j];
+      for (uint32_t j2 = gl; j2 < c; j2 += kHL) put_checked(o.hout, hb + w + j2, o.hcap, so + j2, &o.ctr->oob);
+      w += c;
+    }
+  }
+}
+
+// window w of the output space [w * kWin, (w + 1) * kWin) -> the descriptor
+// holding (or, in a gap, preceding) its first position; windows before the
+// first descriptor map to it
+constexpr uint32_t kWin = 4096;
+__global__ __launch_bounds__(256) void k_winmap(const uint4 *__restrict__ desc, uint64_t nd, uint64_t total,
+                                                uint32_t *__restrict__ win) {
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nd; j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint4 a = desc[j];
+    const uint64_t d = a.z | ((uint64_t)a.w << 32);
+    uint64_t e = total;
+    if (j + 1 < nd) {
+      const uint4 b = desc[j + 1];
+      e = b.z | ((uint64_t)b.w << 32);
+    }
+    const uint64_t lo = j == 0 ? 0 : (d + kWin - 1) / kWin, hi = (e + kWin - 1) / kWin;
+    for (uint64_t w = lo; w < hi; w++) win[w] = (uint32_t)j;
+  }
+}
+
+// ---- k_wincopy: the solo deliveries, a wavefront per output window ----------
+// Loads 64 descriptors from the window's first one (one coalesced 16-B load
+// per lane), clips them to the window in LDS, then moves kCU entries per lane
+// and step: position q -> its descriptor by a 6-step search over the clipped
+// starts -> words[src + q - start] -> dout[q] (the word IS the packed
+// delivery: a 4-B copy, lane-consecutive loads and stores).  More than 64
+// descriptors in a window (many tiny topics): the next 64, from where the
+// previous batch ended.
+constexpr int kCU = 16;
+struct alignas(16) WinLds {
+  uint32_t st[kWave], en[kWave], src[kWave];
+};
+
+__global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_eu(8))) void k_wincopy(
+    DeviceSnapshot s, const uint4 *__restrict__ desc, uint64_t nd, const uint32_t *__restrict__ win, uint64_t nwin,
+    uint64_t total, uint32_t *__restrict__ out, uint64_t cap, unsigned int *oob) {
+  __shared__ WinLds lds_all[kEmitWaves];
+  const int lane = threadIdx.x & (kWave - 1);
+  WinLds &L = lds_all[threadIdx.x / kWave];
+  // words through a buffer descriptor: 32-bit offsets, bounds-checked reads
+  const __amdgpu_buffer_rsrc_t words =
+      __builtin_amdgcn_make_buffer_rsrc((void *)s.words, (short)0, (int)(s.n_subs * 4u + 64u), 0x00020000);
+  const uint64_t nw = (uint64_t)gridDim.x * kEmitWaves;
+  for (uint64_t w = (uint64_t)blockIdx.x * kEmitWaves + threadIdx.x / kWave; w < nwin; w += nw) {
+    const uint64_t g0 = w * kWin, g1 = min(g0 + kWin, total);
+    uint64_t j = win[w];
+    uint64_t pos = g0;
+    while (pos < g1 && j < nd) {
+      const uint64_t jj = j + lane;
+      uint4 d = make_uint4(0, 0, 0xFFFFFFFFu, 0xFFFFFFFFu);
+      if (jj < nd) d = desc[jj];
+      const uint64_t dst = d.z | ((uint64_t)d.w << 32);
+      const uint64_t dend = jj < nd ? dst + d.y : ~0ull;
+      uint64_t a = dst > pos ? dst : pos, b = dend < g1 ? dend : g1;
+      if (b < a) b = a;
+      if (a > g1) a = b = g1;
+      // positions handled by this batch: up to the end of its last descriptor
+      const uint64_t last_end = shfl64(dend, kWave - 1);
+      const uint64_t bend = j + kWave < nd ? (last_end < g1 ? (last_end > pos ? last_end : pos) : g1) : g1;
+      L.st[lane] = (uint32_t)(a - g0);
+      L.en[lane] = (uint32_t)(b - g0);
+      L.src[lane] = d.x + (uint32_t)(a - dst);
+      wave_lds_sync();
+      const uint32_t q0 = (uint32_t)(pos - g0), q1 = (uint32_t)(bend - g0);
+      for (uint32_t base = q0; base < q1; base += kWave * kCU) {
+        uint32_t sa[kCU];
+        bool in[kCU];
+#pragma unroll
+        for (int u = 0; u < kCU; u++) {
+          const uint32_t q = base + u * kWave + lane;
+          uint32_t k = 0;  // the last descriptor starting at or before q
+#pragma unroll
+          for (uint32_t step = 32; step > 0; step >>= 1) k = L.st[k + step] <= q ? k + step : k;  // k + step <= 63
+          in[u] = q < q1 && q >= L.st[k] && q < L.en[k];
+          sa[u] = in[u] ? L.src[k] + (q - L.st[k]) : 0u;
+        }
+        uint32_t v[kCU];
+#pragma unroll
+        for (int u = 0; u < kCU; u++) v[u] = __builtin_amdgcn_raw_buffer_load_b32(words, (int)(sa[u] * 4u), 0, 0);
+#pragma unroll
+        for (int u = 0; u < kCU; u++) {
+          if (!in[u]) continue;
+          const uint64_t p = g0 + base + u * kWave + lane;
+          if (p < cap)
+            put_out(out + p, v[u]);
+          else
+            atomicOr(oob, 1u);
+        }
+      }
+      wave_lds_sync();
+      pos = bend;
+      j += kWave;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_words(const SubEnt *__restrict__ subs, uint32_t *__restrict__ words,
+                                               uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    words[i] = subs[i].word & kPackedMask;
 }
 
 // Merge kMPer multi entries per lane of a kE-lane group in a table of
@@ -649,11 +750,11 @@ __device__ __forceinline__ void copy_solo(const DeviceSnapshot &s, const uint32_
 template <int kE, int kMPer>
 __device__ __forceinline__ uint32_t merge_multi(MergeTable tb, uint32_t kSlots, const uint32_t (&mcl)[kMPer],
                                                 const uint32_t (&mw)[kMPer], const uint32_t (&mrk)[kMPer],
-                                                uint32_t M, int gl, int gbase, uint64_t *out, uint64_t db,
+                                                uint32_t M, int gl, int gbase, uint32_t *out, uint64_t db,
                                                 uint32_t D, uint64_t cap, unsigned int *oob) {
   constexpr uint64_t kGMask = kE == 64 ? ~0ull : (1ull << kE) - 1ull;
   const uint64_t glt = (1ull << gl) - 1ull;
-  uint32_t lg = 6;
+  uint32_t lg = 5;
   while ((1u << lg) < 2 * M && (1u << lg) < kSlots) lg++;
   const uint32_t mask = (1u << lg) - 1;
   for (uint32_t j = gl; j <= mask; j += kE) mt_clear(tb, j);
@@ -672,24 +773,29 @@ __device__ __forceinline__ uint32_t merge_multi(MergeTable tb, uint32_t kSlots, 
   return D;
 }
 
-// ---- k_emit_small -------------------------------------------------------------
-// kSmallLanes lanes per topic (8 topics per wavefront): the topic's whole
-// record (header + <= kSmallHits hits = 64 words) is prefetched one topic
-// ahead and its list entry two ahead, so a topic costs one dependent round
-// trip (its subscription entries) after its record arrives.
+// ---- k_merge_small ------------------------------------------------------------
+// kSmallLanes lanes per topic (8 topics per wavefront) for topics with 0 < Ms
+// <= kSmallMultiS and <= kSmallHits hits: the whole record (header + hits =
+// 64 words) is prefetched one topic ahead and its list entry two ahead, so a
+// topic costs one dependent round trip (its multi entries) after its record
+// arrives.
 constexpr int kSE = kSmallLanes;
 constexpr int kSGroups = kWave / kSE;
 constexpr int kSRecPer = 64 / kSE;  // record words prefetched per lane
 static_assert(4 + kRecHit * kSmallHits <= 64 && kSRecPer % 4 == 0, "small-class record prefetch");
 
-struct alignas(16) SmallLds {
-  unsigned long long tfirst[64];
+constexpr int kSmallTab = 32;  // k_merge_small table slots (<= kSmallMultiS entries: load <= 0.75)
+static_assert(kSmallMultiS * 4 <= kSmallTab * 3, "k_merge_small table load factor");
+struct alignas(8) SmallLds {
+  unsigned long long tfirst[kSmallTab];
   uint32_t rec[64];
-  uint32_t tkey[64], tbits[64];
+  uint32_t tkey[kSmallTab], tbits[kSmallTab];
+  uint32_t pad[2];  // 194-dword stride: the 8 groups' contexts start 2 banks apart
 };
+static_assert(sizeof(SmallLds) % 256 == 8, "bank-skewed group contexts");
 
-template <int kOcc, int kU>
-__global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_eu(kOcc))) void k_emit_small(
+template <int kOcc>
+__global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_eu(kOcc))) void k_merge_small(
     DeviceSnapshot s, Outputs o, const uint32_t *__restrict__ list, const unsigned int *__restrict__ count) {
   constexpr int kMPer = kSmallMultiS / kSE, kRecPer = kSRecPer;
   __shared__ SmallLds lds_all[kEmitWaves * kSGroups];
@@ -699,12 +805,10 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
   const uint32_t ngroups = gridDim.x * kEmitWaves * kSGroups;
   const uint32_t nl = *count;
   uint32_t i = (blockIdx.x * kEmitWaves + threadIdx.x / kWave) * kSGroups + g;
-  uint32_t n_H = 0, n_rw[kRecPer];
-  uint64_t n_db = 0, n_hb = 0;
+  uint32_t n_rw[kRecPer];
+  uint64_t n_db = 0;
   auto fetch = [&](uint32_t u) {
-    n_H = o.hcount[u];
     n_db = o.dstart[u];
-    n_hb = o.hstart[u];
     const uint32_t *r = o.recs + (uint64_t)u * kRecStrideAlloc + gl * kRecPer;
 #pragma unroll
     for (int v = 0; v < kRecPer / 4; v++) {
@@ -716,60 +820,40 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
   uint32_t t_nn = i + ngroups < nl ? list[i + ngroups] : 0;
   if (i < nl) fetch(t_nxt);
   for (; i < nl; i += ngroups) {
-    const uint32_t t = t_nxt, H = n_H;
-    const uint64_t db = n_db, hb = n_hb;
+    const uint32_t t = t_nxt;
+    const uint64_t db = n_db;
 #pragma unroll
     for (int j = 0; j < kRecPer; j++) L.rec[gl * kRecPer + j] = n_rw[j];
     t_nxt = t_nn;
     if (i + ngroups < nl) fetch(t_nxt);
     t_nn = i + 2 * ngroups < nl ? list[i + 2 * ngroups] : 0;
     wave_lds_sync();
-    const uint32_t w0 = L.rec[0], Ss = L.rec[1], M = L.rec[2];
-    const uint32_t nh = w0 & 0xFFu, nsh = w0 >> 8;
+    const uint32_t nh = L.rec[0] & 0xFFu, Ss = L.rec[1], M = L.rec[2];
     rec_prefix<kSE, kSmallHits>(L.rec, nh, gl);
     wave_lds_sync();
-    if (H) {  // shared candidates (gatherSharedSubscriptions, topics.go:541-555)
-      const uint32_t *grec = o.recs + (uint64_t)t * kRecStrideAlloc;
-      uint32_t w = 0;
-      for (uint32_t j = 0; j < nsh; j++) {
-        const uint32_t so = grec[kRecSh + 2 * j], sc = grec[kRecSh + 1 + 2 * j];
-        for (uint32_t j2 = gl; j2 < sc; j2 += kSE) put_checked(o.hout, hb + w + j2, o.hcap, so + j2, &o.ctr->oob);
-        w += sc;
-      }
-    }
-    // the multi entries are loaded before any store of the topic
     uint32_t mcl[kMPer], mw[kMPer], mrk[kMPer];
-    if (M) {
 #pragma unroll
-      for (int k = 0; k < kMPer; k++) {
-        const uint32_t q = gl + k * kSE;
-        uint32_t h;
-        const uint32_t sid = multi_sid(L.rec, nh, Ss, q < M ? q : 0, &h);
-        mrk[k] = rec_at(L.rec, h, kFieldRank);
-        const SubEnt e = load_sub(s, sid);
-        mcl[k] = e.client;
-        mw[k] = e.word;
-      }
+    for (int k = 0; k < kMPer; k++) {
+      const uint32_t q = gl + k * kSE;
+      uint32_t h;
+      const uint32_t sid = multi_sid(L.rec, nh, Ss, q < M ? q : 0, &h);
+      mrk[k] = rec_at(L.rec, h, kFieldRank);
+      const SubEnt e = load_sub(s, sid);
+      mcl[k] = e.client;
+      mw[k] = e.word;
     }
-    copy_solo<kSE, kU>(s, L.rec, nh, Ss, 0, Ss, gl, o.dout, db, o.dcap, &o.ctr->oob);
-    uint32_t D = Ss;
-    if (M)
-      D = merge_multi<kSE, kMPer>(MergeTable{L.tkey, L.tbits, L.tfirst}, 64, mcl, mw, mrk, M, gl, gbase, o.dout, db,
-                                  D, o.dcap, &o.ctr->oob);
+    const uint32_t D = merge_multi<kSE, kMPer>(MergeTable{L.tkey, L.tbits, L.tfirst}, kSmallTab, mcl, mw, mrk, M, gl,
+                                               gbase, o.dout, db, Ss, o.dcap, &o.ctr->oob);
     if (gl == 0) o.dcount[t] = D;
     wave_lds_sync();
   }
 }
 
-// ---- k_copy: big-class items -------------------------------------------------
-struct alignas(16) CopyLds {
-  uint32_t rec[kRecStrideAlloc];
-};
-
-// ---- k_merge: a wavefront per big-class topic with 0 < Ms <= kSmallMulti ------
+// ---- k_merge: a wavefront per topic with kSmallMultiS < Ms <= kSmallMulti (or
+// more than kSmallHits hits) ----------------------------------------------------
 struct alignas(16) MergeLds {
   unsigned long long tfirst[kSmallSlots];
-  uint32_t rec[kRecStrideAlloc];
+  uint32_t rec[kRecSh];
   uint32_t tkey[kSmallSlots], tbits[kSmallSlots];
 };
 
@@ -821,83 +905,6 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_merge(DeviceSnapshot s, O
   }
 }
 
-// chunk items per big-class topic: ceil(Ss / kChunk), at least 1 (item 0 also
-// writes shared candidates, merges or hands on the multi entries, and dcount);
-// zeros past the list so one scan over n covers it
-__global__ __launch_bounds__(256) void k_chunks(Outputs o, const uint32_t *__restrict__ list,
-                                                const unsigned int *__restrict__ count, uint32_t n,
-                                                uint32_t *__restrict__ nchunk) {
-  const uint32_t nb = *count;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    uint32_t c = 0;
-    if (i < nb) {
-      const uint32_t Ss = o.recs[(uint64_t)list[i] * kRecStrideAlloc + 1];
-      c = Ss > kChunk ? (Ss + kChunk - 1) / kChunk : 1u;
-    }
-    nchunk[i] = c;
-  }
-}
-
-__global__ __launch_bounds__(256) void k_items(const uint32_t *__restrict__ list, const unsigned int *__restrict__ count,
-                                               const uint64_t *__restrict__ cstart, uint2 *__restrict__ items) {
-  const uint32_t nb = *count;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += gridDim.x * blockDim.x) {
-    const uint64_t a = cstart[i], b = cstart[i + 1];
-    const uint32_t t = list[i];
-    for (uint64_t k = a; k < b; k++) items[k] = make_uint2(t, (uint32_t)(k - a));
-  }
-}
-
-template <int kOcc, int kU>
-__global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_eu(kOcc))) void k_copy(
-    DeviceSnapshot s, Outputs o, const uint2 *__restrict__ items, uint64_t n_items) {
-  __shared__ CopyLds lds_all[kEmitWaves];
-  const int lane = threadIdx.x & (kWave - 1);
-  CopyLds &L = lds_all[threadIdx.x / kWave];
-  const uint64_t nw = (uint64_t)gridDim.x * kEmitWaves;
-  uint64_t i = (uint64_t)blockIdx.x * kEmitWaves + threadIdx.x / kWave;
-  // the next item's header and first 64 record words one item ahead
-  uint2 n_it = make_uint2(0, 0);
-  uint32_t n_H = 0, n_rw = 0;
-  uint64_t n_db = 0, n_hb = 0;
-  auto fetch = [&](uint64_t k) {
-    n_it = items[k];
-    n_H = o.hcount[n_it.x];
-    n_db = o.dstart[n_it.x];
-    n_hb = o.hstart[n_it.x];
-    n_rw = o.recs[(uint64_t)n_it.x * kRecStrideAlloc + lane];
-  };
-  if (i < n_items) fetch(i);
-  for (; i < n_items; i += nw) {
-    const uint32_t t = n_it.x, j = n_it.y, H = n_H;
-    const uint64_t db = n_db, hb = n_hb;
-    L.rec[lane] = n_rw;
-    if (i + nw < n_items) fetch(i + nw);
-    wave_lds_sync();
-    const uint32_t w0 = L.rec[0], Ss = L.rec[1], M = L.rec[2];
-    const uint32_t nh = w0 & 0xFFu, nsh = w0 >> 8;
-    const uint32_t *grec = o.recs + (uint64_t)t * kRecStrideAlloc;
-    for (uint32_t w = kWave + lane; w < 4 + kRecHit * nh; w += kWave) L.rec[w] = grec[w];
-    wave_lds_sync();
-    rec_prefix<kWave>(L.rec, nh, lane);
-    wave_lds_sync();
-    const bool first = j == 0;
-    if (first && H) {
-      uint32_t w = 0;
-      for (uint32_t k = 0; k < nsh; k++) {
-        const uint32_t so = grec[kRecSh + 2 * k], sc = grec[kRecSh + 1 + 2 * k];
-        for (uint32_t k2 = lane; k2 < sc; k2 += kWave) put_checked(o.hout, hb + w + k2, o.hcap, so + k2, &o.ctr->oob);
-        w += sc;
-      }
-    }
-    // solo entries [lo, hi) of the topic: delivery q = solo entry q
-    const uint32_t lo = j * kChunk, hi = min(Ss, lo + kChunk);
-    copy_solo<kWave, kU>(s, L.rec, nh, Ss, lo, hi, lane, o.dout, db, o.dcap, &o.ctr->oob);
-    if (first && M == 0 && lane == 0) o.dcount[t] = Ss;  // else k_merge / k_multi write it
-    wave_lds_sync();
-  }
-}
-
 // ---------------------------------------------------------------------------
 // Workgroup merges (256 threads per topic) for big-class topics with more
 // multi entries than k_merge's wave table holds, routed by size (k_route):
@@ -906,20 +913,19 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
 //                    kPartCap) hash partitions merged one after another in a
 //                    4096-slot table (each pass reads all M entries and keeps
 //                    its partition's; a client's entries share a partition).
-// Winners are written after the topic's solo deliveries (k_copy wrote those)
+// Winners are written after the topic's solo deliveries (k_wincopy writes those)
 // in table-slot order: each wave scans a quarter of the table twice (count,
 // then write at its prefix), so the layout is deterministic.
 // ---------------------------------------------------------------------------
 struct alignas(16) MultiLds {
-  uint32_t rec[kRecStrideAlloc];
+  uint32_t rec[kRecSh];
   uint32_t wsum[kBigThreads / kWave];
 };
 
 // the block's record of topic t, with prefixes (all threads; ends synced)
 __device__ __forceinline__ void block_record(Outputs o, uint32_t t, uint32_t *rec) {
   const int tid = threadIdx.x;
-  for (uint32_t i = tid; i < (uint32_t)kRecStrideAlloc; i += kBigThreads)
-    rec[i] = o.recs[(uint64_t)t * kRecStrideAlloc + i];
+  for (uint32_t i = tid; i < (uint32_t)kRecSh; i += kBigThreads) rec[i] = o.recs[(uint64_t)t * kRecStrideAlloc + i];
   __syncthreads();
   const uint32_t nh = rec[0] & 0xFFu;
   __syncthreads();
@@ -1090,7 +1096,7 @@ __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *
         if (occ) {
           const uint32_t bits = (uint32_t)(gg.keybits >> 32);
           put_checked(o.dout, db + w + __popcll(m & lanemask_lt(lane)), o.dcap,
-                      pack_delivery((uint32_t)gg.keybits - 1, (uint32_t)~gg.first, 31u - __builtin_clz(bits & 7u),
+                      pack_delivery((uint32_t)~gg.first & kWordSidMask, 31u - __builtin_clz(bits & 7u),
                                     (bits >> 3) & 1u),
                       &o.ctr->oob);
         }
@@ -1292,10 +1298,11 @@ __global__ void k_table_sizes(const uint64_t *__restrict__ raw_cnt, const Counte
   sizes[i] = sz;
 }
 
-// segments -> dense CSR (one wavefront per topic)
-__global__ __launch_bounds__(256) void k_densify(uint32_t n, const uint32_t *__restrict__ dcount,
+// segments -> dense CSR (one wavefront per topic); deliveries resolved to
+// {client, packed} (the client of the first-merged subscription)
+__global__ __launch_bounds__(256) void k_densify(DeviceSnapshot s, uint32_t n, const uint32_t *__restrict__ dcount,
                                                 const uint64_t *__restrict__ dstart,
-                                                const uint64_t *__restrict__ doffs, const uint64_t *__restrict__ dsrc,
+                                                const uint64_t *__restrict__ doffs, const uint32_t *__restrict__ dsrc,
                                                 uint64_t *__restrict__ ddst, const uint32_t *__restrict__ hcount,
                                                 const uint64_t *__restrict__ hstart,
                                                 const uint64_t *__restrict__ hoffs, const uint32_t *__restrict__ hsrc,
@@ -1305,32 +1312,37 @@ __global__ __launch_bounds__(256) void k_densify(uint32_t n, const uint32_t *__r
   for (uint32_t t = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave; t < n; t += nwaves) {
     const uint32_t D = dcount[t], H = hcount[t];
     const uint64_t ds = dstart[t], dd = doffs[t], hs = hstart[t], hd = hoffs[t];
-    for (uint32_t j = lane; j < D; j += kWave) ddst[dd + j] = dsrc[ds + j];
+    for (uint32_t j = lane; j < D; j += kWave) {
+      const uint32_t p = dsrc[ds + j];
+      ddst[dd + j] = (uint64_t)s.subs[p & kWordSidMask].client | ((uint64_t)p << 32);
+    }
     for (uint32_t j = lane; j < H; j += kWave) hdst[hd + j] = hsrc[hs + j];
   }
 }
 
-// emission lists in one pass over the topics (replaces one DeviceSelect per
+// merge lists in one pass over the topics (replaces one DeviceSelect per
 // list): each block counts its chunk's members per list (wave ballots, LDS
 // counters), reserves its ranges with one global atomic per list, then
 // writes them.  Order within a list is unspecified (lists only schedule
 // work; every topic's output position is its own dstart).
-enum : int { kLSmall = 0, kLBig, kLWave, kLT1, kLT2, kLPart, kNLists };
+enum : int { kLSmall = 0, kLWave, kLT1, kLT2, kLPart, kLShared, kNLists };
 constexpr uint32_t kT1Max = 768, kT2Max = 1536;  // k_multi<1024> / <2048> capacities (load 0.75)
 struct Lists {
   uint32_t *l[kNLists];
 };
 
-__device__ __forceinline__ uint32_t route_mask(uint8_t c, uint32_t h, uint32_t m) {
-  if (c == kClsSmall || (c == kClsDone && h != 0)) return 1u << kLSmall;
-  if (c != kClsBig) return 0;
-  const uint32_t mt = m == 0 ? 0 : m <= kSmallMulti ? (1u << kLWave) : m <= kT1Max ? (1u << kLT1)
-                                   : m <= kT2Max ? (1u << kLT2) : (1u << kLPart);
-  return (1u << kLBig) | mt;
+// the merge list of a topic with multi entries (by their count m), and the
+// shared-candidate list
+__device__ __forceinline__ uint32_t route_mask(uint8_t c, uint32_t m, uint32_t h) {
+  if (!(c & kClsBounded)) return 0;
+  const uint32_t sh = h ? (1u << kLShared) : 0u;
+  if (m == 0) return sh;
+  if ((c & kClsFewHits) && m <= kSmallMultiS) return sh | (1u << kLSmall);
+  return sh | (m <= kSmallMulti ? (1u << kLWave) : m <= kT1Max ? (1u << kLT1) : m <= kT2Max ? (1u << kLT2) : (1u << kLPart));
 }
 
-__global__ __launch_bounds__(256) void k_route(const uint8_t *__restrict__ cls, const uint32_t *__restrict__ hcount,
-                                               const uint32_t *__restrict__ mcount, uint32_t n, Lists L,
+__global__ __launch_bounds__(256) void k_route(const uint8_t *__restrict__ cls, const uint32_t *__restrict__ mcount,
+                                               const uint32_t *__restrict__ hcount, uint32_t n, Lists L,
                                                unsigned int *__restrict__ counts,
                                                unsigned long long *__restrict__ msum) {
   __shared__ unsigned int lc[kNLists], base[kNLists];
@@ -1343,13 +1355,14 @@ __global__ __launch_bounds__(256) void k_route(const uint8_t *__restrict__ cls, 
   __syncthreads();
   for (uint32_t t0 = lo; t0 < hi; t0 += blockDim.x) {
     const uint32_t t = t0 + tid;
-    const uint32_t r = t < hi ? route_mask(cls[t], hcount[t], mcount[t]) : 0;
+    const uint32_t r = t < hi ? route_mask(cls[t], mcount[t], hcount[t]) : 0;
 #pragma unroll
     for (int l = 0; l < kNLists; l++) {
       const uint64_t m = __ballot((r >> l) & 1u);
       if (lane == 0 && m) atomicAdd(&lc[l], (unsigned int)__popcll(m));
     }
-    if (r >> kLT1) atomicAdd(&ms[(r >> kLPart) & 1u ? 2 : (r >> kLT2) & 1u ? 1 : 0], (unsigned long long)mcount[t]);
+    if (r & ((1u << kLT1) | (1u << kLT2) | (1u << kLPart)))
+      atomicAdd(&ms[(r >> kLPart) & 1u ? 2 : (r >> kLT2) & 1u ? 1 : 0], (unsigned long long)mcount[t]);
   }
   __syncthreads();
   if (tid < 3 && ms[tid]) atomicAdd(&msum[tid], ms[tid]);
@@ -1360,7 +1373,7 @@ __global__ __launch_bounds__(256) void k_route(const uint8_t *__restrict__ cls, 
   __syncthreads();
   for (uint32_t t0 = lo; t0 < hi; t0 += blockDim.x) {
     const uint32_t t = t0 + tid;
-    const uint32_t r = t < hi ? route_mask(cls[t], hcount[t], mcount[t]) : 0;
+    const uint32_t r = t < hi ? route_mask(cls[t], mcount[t], hcount[t]) : 0;
 #pragma unroll
     for (int l = 0; l < kNLists; l++) {
       const bool in = (r >> l) & 1u;
@@ -1394,6 +1407,29 @@ int Workspace::end(hipStream_t st) {
   }
   if (hipEventRecord(last_use, st) != hipSuccess) return -3;
   used = true;
+  return 0;
+}
+
+int Workspace::fork(hipStream_t st, hipStream_t *out) {
+  if (!side && hipStreamCreateWithFlags(&side, hipStreamNonBlocking) != hipSuccess) {
+    side = nullptr;
+    return -3;
+  }
+  if (!fork_ev && hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming) != hipSuccess) {
+    fork_ev = nullptr;
+    return -3;
+  }
+  if (hipEventRecord(fork_ev, st) != hipSuccess || hipStreamWaitEvent(side, fork_ev, 0) != hipSuccess) return -3;
+  *out = side;
+  return 0;
+}
+
+int Workspace::join(hipStream_t st, hipStream_t side_st) {
+  if (!join_ev && hipEventCreateWithFlags(&join_ev, hipEventDisableTiming) != hipSuccess) {
+    join_ev = nullptr;
+    return -3;
+  }
+  if (hipEventRecord(join_ev, side_st) != hipSuccess || hipStreamWaitEvent(st, join_ev, 0) != hipSuccess) return -3;
   return 0;
 }
 
@@ -1453,6 +1489,12 @@ Workspace::~Workspace() {
   for (auto &b : bufs)
     if (b.p) (void)hipFree(b.p);
   if (last_use) (void)hipEventDestroy(last_use);
+  if (side) {
+    (void)hipStreamSynchronize(side);
+    (void)hipStreamDestroy(side);
+  }
+  if (fork_ev) (void)hipEventDestroy(fork_ev);
+  if (join_ev) (void)hipEventDestroy(join_ev);
   if (host_pinned) (void)hipHostFree(host_pinned);
   for (auto &e : ev)
     if (e) (void)hipEventDestroy(e);
@@ -1522,7 +1564,8 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
       ws.get(W::kDCount, sizeof(uint32_t) * (n + 1)) || ws.get(W::kDStart, sizeof(uint64_t) * (n + 1)) ||
       ws.get(W::kHStart, sizeof(uint64_t) * (n + 1)) || ws.get(W::kCls, n + 1) ||
       ws.get(W::kDfsList, sizeof(uint32_t) * (n + 2)) || ws.get(W::kMCount, sizeof(uint32_t) * (n + 1)) ||
-      ws.get(W::kRecs, sizeof(uint32_t) * kRecStrideAlloc * ((uint64_t)n + 1)) || ws.get(W::kCounters, 256))
+      ws.get(W::kRecs, sizeof(uint32_t) * kRecStrideAlloc * ((uint64_t)n + 1)) || ws.get(W::kCounters, 256) ||
+      ws.get(W::kNSolo, sizeof(uint32_t) * (n + 1)) || ws.get(W::kDescStart, sizeof(uint64_t) * (n + 1)))
     return -2;
   if (!ws.host_pinned && hipHostMalloc(&ws.host_pinned, 256, hipHostMallocDefault) != hipSuccess) return -2;
   Counters *hc = reinterpret_cast<Counters *>(ws.host_pinned);
@@ -1540,6 +1583,8 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   o.mcount = (uint32_t *)ws.ptr(W::kMCount);
   o.recs = (uint32_t *)ws.ptr(W::kRecs);
   o.ctr = (Counters *)ws.ptr(W::kCounters);
+  o.nsolo = (uint32_t *)ws.ptr(W::kNSolo);
+  auto *desc_start = (uint64_t *)ws.ptr(W::kDescStart);
   const int walk_g = ws.walk_lanes;
   HIP_TRY(hipMemsetAsync(o.ctr, 0, sizeof(Counters), st));
   mark(ws, 0, st);
@@ -1551,55 +1596,46 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
       hipLaunchKernelGGL(kern, dim3(blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o);
     };
     if (walk_g == 4)
-      launch_walk(k_walk<4, 1>, 4);
+      launch_walk(k_walk<4, MQM_WALK_OCC>, 4);
     else if (walk_g == 16)
-      launch_walk(k_walk<16, 1>, 16);
+      launch_walk(k_walk<16, MQM_WALK_OCC>, 16);
     else
-      launch_walk(k_walk<8, 1>, 8);
+      launch_walk(k_walk<8, MQM_WALK_OCC>, 8);
   }
   HIP_TRY(hipGetLastError());
   mark(ws, 1, st);
   // segment starts: exclusive scans of S (raw entries, an upper bound of a
-  // topic's deliveries) and H (shared candidates)
-  if (scan_offsets(ws, (const uint32_t *)o.scount, o.dstart, n, st) || scan_offsets(ws, (const uint32_t *)o.hcount, o.hstart, n, st))
+  // topic's deliveries) and H (shared candidates); the solo descriptors'
+  // positions: exclusive scan of the solo-hit counts
+  if (scan_offsets(ws, (const uint32_t *)o.scount, o.dstart, n, st) ||
+      scan_offsets(ws, (const uint32_t *)o.hcount, o.hstart, n, st) || scan_offsets(ws, o.nsolo, desc_start, n, st))
     return -3;
-  // emit lists (small class + shared-only topics; big class) and the big
-  // class's chunk items, counted before the one host sync that sizes the outputs
-  const W::Slot list_slots[kNLists] = {W::kListS, W::kListB, W::kListW, W::kListT1, W::kListT2, W::kListP};
+  // merge lists, counted before the one host sync that sizes the outputs
+  const W::Slot list_slots[kNLists] = {W::kListS, W::kListW, W::kListT1, W::kListT2, W::kListP, W::kListH};
   Lists lists;
   for (int l = 0; l < kNLists; l++) {
     if (ws.get(list_slots[l], sizeof(uint32_t) * (n + 1))) return -2;
     lists.l[l] = (uint32_t *)ws.ptr(list_slots[l]);
   }
-  if (ws.get(W::kNChunk, sizeof(uint32_t) * (n + 1)) || ws.get(W::kCStart, sizeof(uint64_t) * (n + 1))) return -2;
-  auto *nchunk = (uint32_t *)ws.ptr(W::kNChunk);
-  auto *cstart = (uint64_t *)ws.ptr(W::kCStart);
   unsigned int *lcount = &o.ctr->n_small;  // kNLists consecutive counters
   if (n > 0) {
-    hipLaunchKernelGGL(k_route, dim3(std::min<uint32_t>((n + 4095) / 4096, 2048)), dim3(256), 0, st, o.cls, o.hcount,
-                       o.mcount, n, lists, lcount, o.ctr->m_sum);
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_chunks, dim3(std::min<uint32_t>((n + 255) / 256, 4096)), dim3(256), 0, st, o,
-                       lists.l[kLBig], lcount + kLBig, n, nchunk);
+    hipLaunchKernelGGL(k_route, dim3(std::min<uint32_t>((n + 4095) / 4096, 2048)), dim3(256), 0, st, o.cls, o.mcount,
+                       o.hcount, n, lists, lcount, o.ctr->m_sum);
     HIP_TRY(hipGetLastError());
   }
-  if (scan_offsets(ws, (const uint32_t *)nchunk, cstart, n, st)) return -3;
   HIP_TRY(hipMemcpyAsync(hc, o.ctr, sizeof(Counters), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(hp, o.dstart + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(hp + 1, o.hstart + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipMemcpyAsync(hp + 3, cstart + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(hp + 3, desc_start + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   const uint32_t n_dfs = hc->n_dfs;
-  const uint64_t s_total = hp[0], h_total = hp[1], n_items = hp[3];
+  const uint64_t s_total = hp[0], h_total = hp[1], n_desc = hp[3];
   ws.last_valid = true;
   ws.last_n = n;
   ws.last_bytes = d_bytes;
   ws.last_offs = d_offs;
   ws.last_n_dfs = n_dfs;
   for (int i = 0; i < 5; i++) ws.why[i] = hc->why[i];
-  ws.last_small = hc->n_small;
-  ws.last_bigc = hc->n_bigc;
-  ws.last_items = n_items;
 
   // DFS phase 0: exact raw / shared counts size the tail regions
   uint64_t dfs_raw = 0, dfs_h = 0, tab_total = 0;
@@ -1633,50 +1669,72 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
     }
   }
   // outputs: scanned segments, then the DFS tails
-  if (ws.get(W::kDOut, sizeof(uint64_t) * (s_total + dfs_raw + 1)) ||
-      ws.get(W::kHOut, sizeof(uint32_t) * (h_total + dfs_h + 1)) || ws.get(W::kItems, sizeof(uint2) * (n_items + 1)))
+  const uint64_t n_win = (s_total + kWin - 1) / kWin;
+  if (ws.get(W::kDOut, sizeof(uint32_t) * (s_total + dfs_raw + 1)) ||
+      ws.get(W::kHOut, sizeof(uint32_t) * (h_total + dfs_h + 1)) || ws.get(W::kDesc, sizeof(uint4) * (n_desc + 1)) ||
+      ws.get(W::kWin, sizeof(uint32_t) * (n_win + 1)))
     return -2;
-  o.dout = (uint64_t *)ws.ptr(W::kDOut);
+  o.dout = (uint32_t *)ws.ptr(W::kDOut);
   o.hout = (uint32_t *)ws.ptr(W::kHOut);
   o.dcap = s_total + dfs_raw;
   o.hcap = h_total + dfs_h;
-  auto *items = (uint2 *)ws.ptr(W::kItems);
+  auto *desc = (uint4 *)ws.ptr(W::kDesc);
+  auto *win = (uint32_t *)ws.ptr(W::kWin);
 
   mark(ws, 2, st);
   static_assert(kWave * kEmitWaves == kBigThreads, "resident_blocks assumes 256-thread blocks");
   if (n > 0) {
     auto grid = [&](auto kern) { return dim3(resident_blocks(ws, 0, kern)); };
-    hipLaunchKernelGGL((k_emit_small<5, kEmitU>), grid(k_emit_small<5, kEmitU>), dim3(kWave * kEmitWaves), 0, st, s,
-                       o, lists.l[kLSmall], lcount + kLSmall);
+    // merges on the side stream, concurrently with the solo copy (they write
+    // disjoint parts of dout and dcount: winners after Ss / topics with Ms > 0)
+    const bool merges = hc->n_small || hc->n_wmerge || hc->n_t1 || hc->n_t2 || hc->n_part;
+    const bool side = merges && ws.overlap;
+    hipStream_t ms = st;
+    if (merges) {
+      if (side && ws.fork(st, &ms)) return -3;
+      if (hc->n_small) {
+        hipLaunchKernelGGL((k_merge_small<6>), grid(k_merge_small<6>), dim3(kWave * kEmitWaves), 0, ms, s, o,
+                           lists.l[kLSmall], lcount + kLSmall);
+        HIP_TRY(hipGetLastError());
+      }
+      if (hc->n_wmerge) {
+        hipLaunchKernelGGL(k_merge, grid(k_merge), dim3(kWave * kEmitWaves), 0, ms, s, o, lists.l[kLWave],
+                           lcount + kLWave);
+        HIP_TRY(hipGetLastError());
+      }
+      if (hc->n_t1) {
+        hipLaunchKernelGGL(k_multi<1024>, grid(k_multi<1024>), dim3(kBigThreads), 0, ms, s, o, lists.l[kLT1],
+                           lcount + kLT1);
+        HIP_TRY(hipGetLastError());
+      }
+      if (hc->n_t2) {
+        hipLaunchKernelGGL(k_multi<2048>, grid(k_multi<2048>), dim3(kBigThreads), 0, ms, s, o, lists.l[kLT2],
+                           lcount + kLT2);
+        HIP_TRY(hipGetLastError());
+      }
+      if (hc->n_part) {
+        hipLaunchKernelGGL(k_multi_part, grid(k_multi_part), dim3(kBigThreads), 0, ms, s, o, lists.l[kLPart],
+                           lcount + kLPart);
+        HIP_TRY(hipGetLastError());
+      }
+    }
+    hipLaunchKernelGGL(k_desc, dim3(std::min<uint32_t>((n + 255) / 256, 8192)), dim3(256), 0, st, o, n, desc_start,
+                       desc, n_desc);
     HIP_TRY(hipGetLastError());
-    if (n_items) {
-      hipLaunchKernelGGL(k_items, dim3(std::min<uint32_t>((n + 255) / 256, 4096)), dim3(256), 0, st,
-                         lists.l[kLBig], lcount + kLBig, cstart, items);
-      HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL((k_copy<8, kEmitU>), grid(k_copy<8, kEmitU>), dim3(kWave * kEmitWaves), 0, st, s, o, items,
-                         n_items);
+    if (hc->n_shlist) {
+      hipLaunchKernelGGL(k_shared, dim3(std::min<uint32_t>((hc->n_shlist + 15) / 16, 8192)), dim3(256), 0, st, o,
+                         lists.l[kLShared], lcount + kLShared);
       HIP_TRY(hipGetLastError());
     }
-    if (hc->n_wmerge) {
-      hipLaunchKernelGGL(k_merge, grid(k_merge), dim3(kWave * kEmitWaves), 0, st, s, o, lists.l[kLWave],
-                         lcount + kLWave);
+    if (n_desc) {
+      hipLaunchKernelGGL(k_winmap, dim3((uint32_t)std::min<uint64_t>((n_desc + 255) / 256, 8192)), dim3(256), 0, st,
+                         desc, n_desc, s_total, win);
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(k_wincopy, grid(k_wincopy), dim3(kWave * kEmitWaves), 0, st, s, desc, n_desc, win, n_win,
+                         s_total, o.dout, o.dcap, &o.ctr->oob);
       HIP_TRY(hipGetLastError());
     }
-    if (hc->n_t1) {
-      hipLaunchKernelGGL(k_multi<1024>, grid(k_multi<1024>), dim3(kBigThreads), 0, st, s, o, lists.l[kLT1],
-                         lcount + kLT1);
-      HIP_TRY(hipGetLastError());
-    }
-    if (hc->n_t2) {
-      hipLaunchKernelGGL(k_multi<2048>, grid(k_multi<2048>), dim3(kBigThreads), 0, st, s, o, lists.l[kLT2],
-                         lcount + kLT2);
-      HIP_TRY(hipGetLastError());
-    }
-    if (hc->n_part) {
-      hipLaunchKernelGGL(k_multi_part, grid(k_multi_part), dim3(kBigThreads), 0, st, s, o, lists.l[kLPart],
-                         lcount + kLPart);
-      HIP_TRY(hipGetLastError());
-    }
+    if (side && ws.join(st, ms)) return -3;
   }
   if (n_dfs) {
     hp[4] = s_total;  // Counters::dtail, Counters::htail (pinned staging)
@@ -1724,9 +1782,9 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   out->n_tier2 = hc->n_t2;
   out->n_tier3 = hc->n_part;
   for (int i = 0; i < 3; i++) out->multi_entries[i] = hc->m_sum[i];
-  out->n_small = hc->n_small;
-  out->n_bigc = hc->n_bigc;
-  out->n_items = n_items;
+  out->n_merge_small = hc->n_small;
+  out->n_merge_wave = hc->n_wmerge;
+  out->n_solo_ranges = n_desc;
   out->n_fallback = n_dfs;
   out->starts = o.dstart;
   out->counts = o.dcount;
@@ -1786,7 +1844,14 @@ int identifiers_device(const DeviceSnapshot &s, Workspace &ws, hipStream_t st, I
   return 0;
 }
 
-int densify(Workspace &ws, const MatchOutput &m, hipStream_t st, DenseOutput *out) {
+int derive_words(const SubEnt *subs, uint32_t *words, uint64_t n, hipStream_t st) {
+  if (n)
+    hipLaunchKernelGGL(k_words, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 16384)), dim3(256), 0, st, subs,
+                       words, n);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+int densify(const DeviceSnapshot &s, Workspace &ws, const MatchOutput &m, hipStream_t st, DenseOutput *out) {
   using W = Workspace;
   const uint32_t n = m.n_topics;
   if (ws.get(W::kDenseOffs, sizeof(uint64_t) * (n + 1)) || ws.get(W::kDenseHOffs, sizeof(uint64_t) * (n + 1)) ||
@@ -1800,7 +1865,7 @@ int densify(Workspace &ws, const MatchOutput &m, hipStream_t st, DenseOutput *ou
   auto *dd = (uint64_t *)ws.ptr(W::kTable);
   auto *hd = (uint32_t *)ws.ptr(W::kDenseShared);
   if (n > 0)
-    hipLaunchKernelGGL(k_densify, dim3(std::min<uint32_t>((n + 3) / 4, 8192)), dim3(256), 0, st, n, m.counts,
+    hipLaunchKernelGGL(k_densify, dim3(std::min<uint32_t>((n + 3) / 4, 8192)), dim3(256), 0, st, s, n, m.counts,
                        m.starts, doffs, m.deliveries, dd, m.shared_counts, m.shared_starts, hoffs, m.shared, hd);
   HIP_TRY(hipGetLastError());
   out->offsets = doffs;

@@ -70,7 +70,7 @@ struct SubEnt {
 };
 constexpr uint32_t kWordSidMask = 0x0FFFFFFFu;
 constexpr uint32_t kWordIdent = 1u << 31;
-constexpr uint64_t kDeliveryMask = 0x7FFFFFFFFFFFFFFFull;  // entry as u64 -> delivery
+constexpr uint32_t kPackedMask = 0x7FFFFFFFu;  // word -> packed delivery (sid | qos << 28 | no_local << 30)
 
 // build-time meta (flatten.cpp): qos[1:0] | no_local[2] | rap[3] | rh[5:4] |
 // multi[6] | ident[7], rewritten into the device word at the end of flatten().
@@ -88,10 +88,13 @@ constexpr uint32_t kMetaMulti = 1u << 6;
 // client's Identifiers map (packets.go:257-259); becomes kWordIdent
 constexpr uint32_t kMetaIdent = 1u << 7;
 
-// delivery written by the matcher (one per (topic, client)):
-//   bits  0..31 client id
-//   bits 32..59 sid of the first-merged subscription
-//   bits 60..61 max QoS, bit 62 NoLocal (OR)
+// delivery written by the matcher (one per (topic, client)), 4 bytes:
+//   bits  0..27 sid of the first-merged subscription (its client is the
+//               delivery's client: subs[sid].client)
+//   bits 28..29 max QoS, bit 30 NoLocal (OR)
+// A solo entry's delivery is its word & kPackedMask, precomputed in `words`,
+// so the solo part of a topic is a plain copy of word ranges.  The dense form
+// (densify) resolves the client: {client, packed}, 8 bytes.
 constexpr uint32_t kSidBits = 28;
 constexpr uint32_t kMaxSubs = 1u << kSidBits;
 
@@ -99,6 +102,7 @@ struct DeviceSnapshot {
   const NodeDesc *nodes;
   const EdgeEntry *edges;
   const SubEnt *subs;
+  const uint32_t *words;  // n_subs: subs[i].word & kPackedMask (the entry's own delivery)
   const uint8_t *tok_pool;
   uint64_t n_buckets;     // edge buckets (kEdgesPerBucket entries each; any count)
   uint32_t n_nodes;

@@ -14,7 +14,8 @@ import os
 import sys
 
 root, batches = sys.argv[1], int(sys.argv[2])
-KERNELS = ("k_walk", "k_emit", "k_multi", "k_dfs", "k_table_sizes")
+KERNELS = ("k_walk", "k_emit_small", "k_copy", "k_merge", "k_multi_part", "k_multi", "k_route", "k_chunks", "k_items",
+           "k_dfs", "k_table_sizes")
 
 
 def total(counter):

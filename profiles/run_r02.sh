@@ -7,6 +7,10 @@
 #   bench   : the default bench line (C3)               -> gpurun_out/TAG/bench.json
 #   fast    : bench without CPU baseline / host path     -> gpurun_out/TAG/bench_fast.json
 #   prof    : rocprofv3 kernel trace + stats of `fast`   -> gpurun_out/TAG/prof/
+#   profser : `prof` with the merges serialised behind the solo copy (MQM_NO_OVERLAP=1): per-kernel times
+#   shim    : the Go shim's call sequence from 4 threads  -> gpurun_out/TAG/pytest_shim.log
+#   variants: `fast` once per tuning build maxmq_amd/_lib/<name>/ (make variant) -> bench_fast_<name>.json
+#   calib   : FETCH_SIZE / WRITE_SIZE on known byte counts (tools/calib_fetch) -> gpurun_out/TAG/calib_*
 set -euo pipefail
 TAG=$1
 shift
@@ -37,6 +41,16 @@ for step in "$@"; do
     prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv \
              -d $OUT/prof -o prof -- python3 $ROOT/bench.py $FAST \
              > $OUT/bench_under_rocprof.json 2> $OUT/rocprof.log) ;;
+    shim) timeout -k 10 300 python3 -u -m pytest tests/test_gpu_shim.py -m gpu -x -v --timeout 240 \
+             --timeout-method thread > $OUT/pytest_shim.log 2>&1 ;;
+    calib) (cd /tmp && export TMPDIR=/tmp && for C in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do
+             tag=$(echo $C | cut -d' ' -f1); timeout -s KILL 120 rocprofv3 --pmc $C --kernel-trace --output-format csv \
+             -d $OUT/calib_$tag -o calib -- $ROOT/tools/_build/calib_fetch > $OUT/calib_$tag.txt 2>&1 || exit 1; done) ;;
+    variants) for L in maxmq_amd/_lib/*/libmqmatch.so; do V=$(basename $(dirname $L)); [ "$V" = asan ] && continue;
+             MQM_LIB=$ROOT/$L timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_$V.json 2> $OUT/bench_fast_$V.log || exit 1; done ;;
+    profser) (cd /tmp && export TMPDIR=/tmp MQM_NO_OVERLAP=1 && timeout -k 10 500 rocprofv3 --kernel-trace --stats \
+             --output-format csv -d $OUT/profser -o prof -- python3 $ROOT/bench.py $FAST \
+             > $OUT/bench_under_rocprof_serial.json 2> $OUT/rocprof_serial.log) ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -192,11 +192,12 @@ def test_full_size_c2_properties():
     sample = np.sort(rng.choice(n, size=100000, replace=False))
 
     def segments(r):
-        """per-topic counts (all topics) and the sample's entries, sorted within topic"""
+        """per-topic counts (all topics) and the sample's packed deliveries
+        (4 B: first sub | qos << 28 | no_local << 30), sorted within topic"""
         starts = _dev_copy(r.starts, n * 8).view(np.uint64).astype(np.int64)
         counts = _dev_copy(r.counts, n * 4).view(np.uint32).astype(np.int64)
         end = int((starts + counts).max()) if n else 0
-        buf = _dev_copy(r.deliveries, end * 8).view(np.uint64)
+        buf = _dev_copy(r.deliveries, end * 4).view(np.uint32)
         st, ct = starts[sample], counts[sample]
         tid = np.repeat(sample, ct)
         pos = np.repeat(st - np.concatenate([[0], np.cumsum(ct)[:-1]]), ct) + np.arange(ct.sum())
@@ -219,17 +220,23 @@ def test_full_size_c2_properties():
     # segments never overlap
     o = np.argsort(starts, kind="stable")
     assert np.all(starts[o][1:] >= (starts + counts)[o][:-1])
-    clients = (ents & 0xFFFFFFFF).astype(np.uint32)
+    sub = Strings.from_list([w.topics[int(i)] for i in sample])
+    res = idx.match_batch(sub.data, sub.offs)  # same snapshot: resolves sids to clients
+    first, qos, _ = capi.delivery_fields(ents)
+    assert np.all(qos <= 2)
+    clients = res.sub_infos(first)["client"].astype(np.uint32)
     assert clients.max() < idx.num_clients()
-    assert np.all(((ents >> 60) & 3) <= 2)
     key = (tid.astype(np.uint64) << np.uint64(32)) | clients.astype(np.uint64)
     assert len(np.unique(key)) == len(key), "a client appears twice in one topic"
+    # the full-batch segments of the sample == the host path's rows for it
+    htid = np.repeat(sample, np.diff(res.offsets).astype(np.int64))
+    hp = res.deliveries["packed"]
+    o2 = np.lexsort((hp, htid))
+    assert np.array_equal(htid[o2], tid) and np.array_equal(hp[o2], ents), "full-batch segments != host-path rows"
     # exact agreement with the oracle on the same sample of topics
-    sub = Strings.from_list([w.topics[int(i)] for i in sample])
     ora = OracleIndex()
     ora.subscribe_workload(w)
     r, rs = canon_oracle(*ora.match(sub.data, sub.offs, nthreads=16)[:4])
-    res = idx.match_batch(sub.data, sub.offs)
     g, gs = canon_gpu(res)
     assert_same(g, r, "deliveries (sample)")
     assert_same(gs, rs, "shared (sample)")
