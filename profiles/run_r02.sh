@@ -41,6 +41,11 @@ for step in "$@"; do
     prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv \
              -d $OUT/prof -o prof -- python3 $ROOT/bench.py $FAST \
              > $OUT/bench_under_rocprof.json 2> $OUT/rocprof.log) ;;
+    rev) timeout -k 10 600 python3 -u bench.py --workload reverse --steps 5 --warmup 1 --no-cpu-baseline \
+             > $OUT/bench_reverse.json 2> $OUT/bench_reverse.log ;;
+    revprof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
+             -d $OUT/prof_rev -o prof -- python3 $ROOT/bench.py --workload reverse --steps 3 --warmup 1 \
+             --no-cpu-baseline > $OUT/rev_under_rocprof.json 2> $OUT/rocprof_rev.log) ;;
     shim) timeout -k 10 300 python3 -u -m pytest tests/test_gpu_shim.py -m gpu -x -v --timeout 240 \
              --timeout-method thread > $OUT/pytest_shim.log 2>&1 ;;
     calib) (cd /tmp && export TMPDIR=/tmp && for C in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do
