@@ -788,8 +788,9 @@ def roofline(stats, n, kms, traffic_json):
     scans, k_emit<16|64>, k_multi, k_dfs: first to last kernel, HIP events on
     the launch stream).  `stages` splits it: the walk moves T + 8N + 8P + 8V,
     the emit stage 8S + 8D.  `traffic` = HBM bytes per batch of the same
-    kernels from rocprofv3 FETCH_SIZE / WRITE_SIZE (profiles/traffic.json,
-    profiles/run_pmc.sh)."""
+    kernels from rocprofv3 FETCH_SIZE / WRITE_SIZE (profiles/traffic.json from
+    profiles/pmc_to_traffic.py over a profiles/run_pmc_r02.sh run, reads
+    converted per access shape as tools/calib_fetch calibrated them)."""
     total_ms = kms["total"]
     if not stats or not stats["topics"] or total_ms <= 0:
         return {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
@@ -799,11 +800,12 @@ def roofline(stats, n, kms, traffic_json):
     emit_b = (8 * stats["gathered"] + 8 * stats["deliveries"]) / k * n
     bytes_per_launch = walk_b + emit_b
     achieved = bytes_per_launch / (total_ms * 1e-3) / 1e9
-    traffic = None
+    traffic = walk_traffic = None
     if traffic_json and os.path.exists(traffic_json):
         try:
             with open(traffic_json) as fh:
-                traffic = json.load(fh).get("hbm_bytes_per_batch")
+                tj = json.load(fh)
+            traffic, walk_traffic = tj.get("hbm_bytes_per_batch"), tj.get("walk_bytes_per_batch")
         except Exception:
             traffic = None
 
@@ -814,8 +816,10 @@ def roofline(stats, n, kms, traffic_json):
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
             "algorithmic_bytes_per_topic": bytes_per_launch / n, "algorithmic_bytes_per_batch": bytes_per_launch,
-            "kernel": "match pipeline per batch: k_walk + scans + k_emit<16|64> + k_multi (+ k_dfs)",
-            "stages": {"walk": stage(walk_b, kms["walk"]), "emit": stage(emit_b, kms["dedupe"])}}
+            "kernel": "match pipeline per batch: k_walk + scans + solo copy (k_desc, k_winmap, k_wincopy) "
+                      "+ merges (k_merge_small, k_merge, k_multi) (+ k_dfs)",
+            "stages": {"walk": dict(stage(walk_b, kms["walk"]), traffic=walk_traffic),
+                       "emit": stage(emit_b, kms["dedupe"])}}
 
 
 if __name__ == "__main__":

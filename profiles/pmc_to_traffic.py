@@ -1,46 +1,55 @@
-"""Sum rocprofv3 FETCH_SIZE / WRITE_SIZE over the match kernels of one batch.
+"""HBM traffic per batch of the match kernels from rocprofv3 FETCH_SIZE /
+WRITE_SIZE passes (profiles/run_pmc_r02.sh output) -> profiles/traffic.json.
 
-Correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE and WRITE_SIZE are in KiB;
-on gfx950 FETCH_SIZE counts exactly half the bytes of wide coalesced reads, so
-read bytes = 2 * FETCH_SIZE * 1024 (our gathers are narrower than 16 B/lane and
-uncalibrated: the doubled figure is an upper estimate of reads), write bytes =
-WRITE_SIZE * 1024.  Infinity-Cache hits are counted too (same section).
-usage: pmc_to_traffic.py <gpurun_out dir> <batches profiled>
+Measurement infrastructure.  Calibration (tools/calib_fetch on the GPU box,
+profiles/r02/r02i/calib_*): FETCH_SIZE = (L2 -> memory read requests) x 64 B,
+where a 16-B/lane coalesced stream issues one request per 128-B line (so its
+bytes are 2 x FETCH_SIZE, as MI355X_MICROARCH.md §HBM says) and a random
+gather of 8, 32 or 64 B per lane issues one request per 64-B sector (its bytes
+are 1 x FETCH_SIZE).  Reads are therefore converted per kernel by its access
+shape: x1 for the gather kernels (trie walk, merges), x2 for the streaming
+copies.  WRITE_SIZE is exact for 4..16-B/lane stores (same calibration).
+usage: pmc_to_traffic.py <pmc dir> [> profiles/traffic.json]
 """
+import collections
 import csv
 import glob
 import json
 import os
+import re
 import sys
 
-root, batches = sys.argv[1], int(sys.argv[2])
-KERNELS = ("k_walk", "k_emit_small", "k_copy", "k_merge", "k_multi_part", "k_multi", "k_route", "k_chunks", "k_items",
-           "k_dfs", "k_table_sizes")
+GATHER = ("k_walk", "k_merge_small", "k_merge", "k_multi", "k_multi_part", "k_dfs", "k_shared")
+STREAM = ("k_desc", "k_winmap", "k_wincopy", "k_route", "k_table_sizes")
 
 
-def total(counter):
-    per_kernel = {}
-    for path in glob.glob(os.path.join(root, f"pmc_{counter}", "**", "*counter_collection.csv"), recursive=True):
-        with open(path) as fh:
-            for row in csv.DictReader(fh):
-                name = row.get("Kernel_Name", "")
-                if row.get("Counter_Name") != counter or not any(k in name for k in KERNELS):
-                    continue
-                k = next(k for k in KERNELS if k in name)
-                per_kernel[k] = per_kernel.get(k, 0.0) + float(row["Counter_Value"])
-    return per_kernel
+def kname(s):
+    m = re.match(r"(?:void )?(?:mqm::\(anonymous namespace\)::)?(k_\w+)", s)
+    return m.group(1) if m else None
 
 
-fetch, write = total("FETCH_SIZE"), total("WRITE_SIZE")
+root = sys.argv[1]
+sums = {c: collections.defaultdict(float) for c in ("FETCH_SIZE", "WRITE_SIZE")}
+disp = {c: collections.defaultdict(set) for c in ("FETCH_SIZE", "WRITE_SIZE")}
+for path in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+    with open(path) as fh:
+        for row in csv.DictReader(fh):
+            c = row.get("Counter_Name")
+            k = kname(row.get("Kernel_Name", ""))
+            if c not in sums or k not in GATHER + STREAM:
+                continue
+            sums[c][k] += float(row["Counter_Value"])
+            disp[c][k].add((path, row["Dispatch_Id"]))
 kib = 1024.0
+reads = {k: v * kib * (1 if k in GATHER else 2) / len(disp["FETCH_SIZE"][k]) for k, v in sums["FETCH_SIZE"].items()}
+writes = {k: v * kib / len(disp["WRITE_SIZE"][k]) for k, v in sums["WRITE_SIZE"].items()}
 out = {
-    "batches": batches,
-    "read_bytes_per_batch_by_kernel": {k: 2 * v * kib / batches for k, v in fetch.items()},
-    "write_bytes_per_batch_by_kernel": {k: v * kib / batches for k, v in write.items()},
+    "read_bytes_per_batch_by_kernel": reads,
+    "write_bytes_per_batch_by_kernel": writes,
+    "walk_bytes_per_batch": reads.get("k_walk", 0) + writes.get("k_walk", 0),
+    "hbm_bytes_per_batch": sum(reads.values()) + sum(writes.values()),
+    "note": ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, per launch of each match kernel; "
+             "reads = FETCH_SIZE KiB x 1 (gather kernels: one request per 64-B sector) or x 2 (streaming "
+             "copies: one request per 128-B line), calibrated by tools/calib_fetch; writes = WRITE_SIZE KiB"),
 }
-out["hbm_bytes_per_batch"] = sum(out["read_bytes_per_batch_by_kernel"].values()) + sum(
-    out["write_bytes_per_batch_by_kernel"].values())
-out["note"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes; reads = 2 x FETCH_SIZE KiB "
-               "(gfx950 correction, upper estimate for our narrow gathers), writes = WRITE_SIZE KiB; "
-               "match kernels only (scans and copies excluded)")
 print(json.dumps(out, indent=1))
