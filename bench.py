@@ -708,11 +708,14 @@ def cpu_reverse(w, refs, args):
         done = hi
         chunk = min(chunk * 2, 100000)
     ora.close()
-    return {"value": done / busy, "unit": "filters/s", "cores": threads, "kind": "port", "host": host_info(),
-            "sample": f"first {done} filters ({busy:.1f}s of matching, index build {build_s:.0f}s excluded); "
-                      f"C restatement of mochi v2.2.12 TopicsIndex.Messages (oracle/mochi_ref.c); Go toolchain "
-                      f"unavailable",
-            "retained_hits_per_s": hits / busy}
+    host = host_info()
+    out = {"value": done / busy, "unit": "filters/s", "cores": threads, "kind": "port", "host": host,
+           "sample": f"first {done} filters ({busy:.1f}s of matching, index build {build_s:.0f}s excluded); "
+                     f"C restatement of mochi v2.2.12 TopicsIndex.Messages (oracle/mochi_ref.c); Go toolchain "
+                     f"unavailable",
+           "retained_hits_per_s": hits / busy}
+    out.update(cores_note(done / busy / threads, threads, host))  # (per-thread share of the parallel rate)
+    return out
 
 
 def _dev_to_tensor(ptr, t):
@@ -778,7 +781,22 @@ def cpu_baseline(w, args):
         "single_thread_value": st_done / st_busy if st_busy > 0 else None,
         "host": host_info(),
     }
+    cpu.update(cores_note(cpu["single_thread_value"], threads, cpu["host"]))
     return cpu, tot
+
+
+def cores_note(single, threads, host):
+    """BASELINE.md §2 asks for one thread per core.  The GPU box grants this
+    process a cgroup CPU quota (16 CPUs of a 2 x 64-core host): more threads
+    than the quota only time-slice, so `cores` is the quota.  For scale, the
+    single-thread rate times the host's physical cores (an upper bound: linear
+    scaling, no memory-bandwidth or SMT limit) is reported beside it."""
+    phys = host.get("physical_cores")
+    out = {"cores_note": f"{threads} threads = the CPUs this process may use (cgroup quota "
+                         f"{host.get('cgroup_cpu_quota')}); host has {phys} physical cores"}
+    if single and phys:
+        out["projected_all_physical_cores"] = single * phys
+    return out
 
 
 def roofline(stats, n, kms, traffic_json):

@@ -265,6 +265,8 @@ uint64_t snapshot_digest(const HostSnapshot &hs) {
   d.vec(hs.rch_off);
   d.vec(hs.refs);
   d.vec(hs.rch_refs);
+  d.vec(hs.rinv);
+  d.vec(hs.rgroups);
   d.mix(hs.n_buckets);
   d.mix(hs.height);
   d.mix(hs.sys_child);

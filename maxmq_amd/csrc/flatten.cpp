@@ -146,6 +146,92 @@ static void build_retained(const Store &st, const std::vector<uint32_t> &order, 
 }
 
 
+// The reverse walk's literal-edge index (DeviceRetained::inv / groups) from
+// the staged literal edges (parent preorder order): stable partition of the
+// edges into 256 buckets by their (token, child depth) group, a stable sort
+// by group within each bucket (edges of one group stay in parent order: at a
+// fixed depth, preorder orders children like their parents), then one table
+// slot per group.  Depends on nothing but the store: digests are reproducible.
+template <class Staged>
+static void build_reverse_index(const Store &st, const std::vector<uint32_t> &order, const Staged &staged,
+                                HostSnapshot &hs) {
+  const auto &nodes = st.nodes();
+  const uint64_t ne = staged.size();
+  hs.rinv.clear();
+  hs.rgroups.clear();
+  if (ne == 0 || ne >= kNone || hs.height >= (1u << 16)) return;  // no index: the walk probes children
+  constexpr uint32_t kB = 256, kC = 64;
+  auto gkey = [&](uint64_t e) {  // token id << 16 | child depth
+    const uint32_t c = order[staged[e].child];
+    return ((uint64_t)nodes[c].key << 16) | nodes[c].depth;
+  };
+  auto bucket = [](uint64_t g) { return (uint32_t)((g * 0x9E3779B97F4A7C15ull) >> 56); };
+  std::vector<uint64_t> cnt((uint64_t)kC * kB, 0);
+  parallel_for(kC, [&](uint32_t c) {
+    const uint64_t lo = ne * c / kC, hi = ne * (c + 1) / kC;
+    for (uint64_t e = lo; e < hi; e++) cnt[(uint64_t)c * kB + bucket(gkey(e))]++;
+  });
+  std::vector<uint64_t> bstart(kB + 1, 0);
+  {
+    uint64_t run = 0;
+    for (uint32_t b = 0; b < kB; b++) {
+      bstart[b] = run;
+      for (uint32_t c = 0; c < kC; c++) {
+        const uint64_t v = cnt[(uint64_t)c * kB + b];
+        cnt[(uint64_t)c * kB + b] = run;
+        run += v;
+      }
+    }
+    bstart[kB] = run;
+  }
+  struct GE {
+    uint64_t g;
+    uint32_t e;
+  };
+  std::vector<GE, NoInitAlloc<GE>> tmp(ne);
+  parallel_for(kC, [&](uint32_t c) {
+    const uint64_t lo = ne * c / kC, hi = ne * (c + 1) / kC;
+    for (uint64_t e = lo; e < hi; e++) {
+      const uint64_t g = gkey(e);
+      tmp[cnt[(uint64_t)c * kB + bucket(g)]++] = GE{g, (uint32_t)e};
+    }
+  });
+  hs.rinv.resize(ne);
+  std::vector<std::vector<RevGroup>> bg(kB);
+  parallel_for(kB, [&](uint32_t b) {
+    std::stable_sort(tmp.begin() + bstart[b], tmp.begin() + bstart[b + 1],
+                     [](const GE &x, const GE &y) { return x.g < y.g; });
+    for (uint64_t j = bstart[b]; j < bstart[b + 1]; j++) {
+      const auto &ed = staged[tmp[j].e];
+      hs.rinv[j] = uint2{ed.parent, ed.child};
+      if (j == bstart[b] || tmp[j].g != tmp[j - 1].g) {
+        RevGroup r;
+        r.k0 = ed.k0;
+        r.k1 = ed.k1;
+        r.depth_len = (uint32_t)(tmp[j].g & 0xFFFFu) | (ed.tok_len << 16);
+        r.tok_off = ed.tok_off;
+        r.start = (uint32_t)j;
+        r.count = 0;
+        bg[b].push_back(r);
+      }
+      bg[b].back().count++;
+    }
+  });
+  uint64_t ng = 0;
+  for (auto &v : bg) ng += v.size();
+  const uint64_t nslots = 2 * ng + 1;
+  RevGroup empty;
+  memset(&empty, 0, sizeof(empty));
+  hs.rgroups.assign(nslots, empty);
+  for (auto &v : bg)
+    for (const RevGroup &r : v) {
+      const Key k{r.k0, r.k1};
+      uint64_t slot = bucket_of(edge_hash(r.depth_len & 0xFFFFu, k), nslots);
+      while (hs.rgroups[slot].count != 0) slot = slot + 1 == nslots ? 0 : slot + 1;
+      hs.rgroups[slot] = r;
+    }
+}
+
 int flatten(const Store &st, HostSnapshot *out) {
   PhaseTimer pt;
   const auto &nodes = st.nodes();
@@ -506,6 +592,10 @@ int flatten(const Store &st, HostSnapshot *out) {
       hs.edges[slot] = staged[e];
     }
   pt.mark("edges");
+  if (st.retained_len() > 0) {
+    build_reverse_index(st, order, staged, hs);
+    pt.mark("rev-index");
+  }
   if (hs.tok_pool.empty()) hs.tok_pool.push_back(0);
   if (hs.subs.empty()) hs.subs.push_back(SubEnt{0, 0});
   return MQM_OK;
@@ -515,6 +605,7 @@ GpuSnapshot::~GpuSnapshot() {
   for (void *b : buffers)
     if (b) (void)hipFree(b);
   if (words) (void)hipFree(words);
+  if (nflags) (void)hipFree(nflags);
 }
 
 int upload(std::shared_ptr<const HostSnapshot> hs, int device, hipStream_t stream, std::unique_ptr<GpuSnapshot> *out) {
@@ -529,12 +620,14 @@ int upload(std::shared_ptr<const HostSnapshot> hs, int device, hipStream_t strea
   const void *src[GpuSnapshot::kNumBuffers] = {hs->nodes.data(),     hs->edges.data(),     hs->subs.data(),
                                                hs->tok_pool.data(),  hs->subtree.data(),   hs->child_off.data(),
                                                hs->child_ids.data(), hs->cum.data(),       hs->refs.data(),
-                                               hs->rch_off.data(),   hs->rch_refs.data()};
+                                               hs->rch_off.data(),   hs->rch_refs.data(),  hs->rinv.data(),
+                                               hs->rgroups.data()};
   const size_t sz[GpuSnapshot::kNumBuffers] = {
       hs->nodes.size() * sizeof(NodeDesc), hs->edges.size() * sizeof(EdgeEntry), hs->subs.size() * sizeof(SubEnt),
       hs->tok_pool.size(),                 hs->subtree.size() * 4,                hs->child_off.size() * 4,
       hs->child_ids.size() * 4,            hs->cum.size() * 4,                    hs->refs.size() * 8,
-      hs->rch_off.size() * 4,              hs->rch_refs.size() * 8};
+      hs->rch_off.size() * 4,              hs->rch_refs.size() * 8,               hs->rinv.size() * 8,
+      hs->rgroups.size() * sizeof(RevGroup)};
   for (int i = 0; i < GpuSnapshot::kNumBuffers; i++) {
     if (i >= 4 && !ret) break;
     // +64 B: walk_step reads 64 B at any node descriptor (the last one included)
@@ -548,9 +641,16 @@ int upload(std::shared_ptr<const HostSnapshot> hs, int device, hipStream_t strea
   if (hipMalloc(&g->words, n_sub_ents * 4 + 64) != hipSuccess) return MQM_ENOMEM;
   if (derive_words((const SubEnt *)g->buffers[2], (uint32_t *)g->words, n_sub_ents, stream)) return MQM_EHIP;
   g->device_bytes += n_sub_ents * 4;
+  if (ret) {  // node flags, one byte per node, for the reverse walk
+    const uint64_t nn = hs->nodes.size();
+    if (hipMalloc(&g->nflags, nn + 64) != hipSuccess) return MQM_ENOMEM;
+    if (derive_node_flags((const NodeDesc *)g->buffers[0], (uint8_t *)g->nflags, nn, stream)) return MQM_EHIP;
+    g->device_bytes += nn;
+  }
   if (hipStreamSynchronize(stream) != hipSuccess) return MQM_EHIP;
   if (ret) {
     g->has_retained = true;
+    g->ret.nflags = (const uint8_t *)g->nflags;
     g->ret.subtree = (const uint32_t *)g->buffers[4];
     g->ret.child_off = (const uint32_t *)g->buffers[5];
     g->ret.child_ids = (const uint32_t *)g->buffers[6];
@@ -558,6 +658,9 @@ int upload(std::shared_ptr<const HostSnapshot> hs, int device, hipStream_t strea
     g->ret.refs = (const uint64_t *)g->buffers[8];
     g->ret.rch_off = (const uint32_t *)g->buffers[9];
     g->ret.rch_refs = (const uint64_t *)g->buffers[10];
+    g->ret.inv = (const uint2 *)g->buffers[11];
+    g->ret.groups = (const RevGroup *)g->buffers[12];
+    g->ret.n_gslots = hs->rgroups.size();
     g->ret.n_ret = hs->refs.size() - 1;
     g->ret.n_nodes = (uint32_t)hs->nodes.size();
     g->ret.sys_child = hs->sys_child;

@@ -54,6 +54,8 @@ struct HostSnapshot {
   // retained side (DeviceRetained), empty when nothing is retained
   std::vector<uint32_t> subtree, child_off, child_ids, cum, rch_off;
   std::vector<uint64_t> refs, rch_refs;
+  std::vector<uint2> rinv;           // DeviceRetained::inv
+  std::vector<RevGroup> rgroups;     // DeviceRetained::groups (empty: no index)
   uint32_t sys_child = kNone;
   bool has_empty = false;
 };
@@ -66,9 +68,10 @@ int flatten(const Store &st, HostSnapshot *out);
 struct GpuSnapshot {
   DeviceSnapshot dev{};
   std::shared_ptr<const HostSnapshot> host;
-  static constexpr int kNumBuffers = 11;
+  static constexpr int kNumBuffers = 13;
   void *buffers[kNumBuffers] = {};
   void *words = nullptr;  // DeviceSnapshot::words (derived on the device at upload)
+  void *nflags = nullptr; // DeviceRetained::nflags (derived on the device at upload)
   DeviceRetained ret{};
   bool has_retained = false;
   uint64_t device_bytes = 0;

@@ -28,6 +28,9 @@ struct Workspace {
   void *host_pinned = nullptr;
   uint32_t max_blocks = 2048;  // walk-kernel grid cap (grid-stride beyond)
   int walk_lanes = 4;          // lanes per topic in k_walk (4, 8 or 16; env MQM_WALK_LANES; C3: 7.9 / 8.8 / 11.0 ms)
+  // reverse match (retained.hip): list capacities carried from call to call
+  // (grown when a call's device counters report an overflow)
+  uint64_t rev_item_cap = 0, rev_emit_cap = 0, rev_task_cap = 0, rev_out_cap = 0;
   std::unordered_map<const void *, uint32_t> resident;  // kernel -> resident blocks on the device
   // why the last batch's DFS topics left the bounded path:
   // frontier, hits, cached levels, shared hits, raw entries
@@ -95,6 +98,8 @@ struct MatchOutput {
 
 // words[i] = subs[i].word & kPackedMask for i < n (snapshot upload, on `st`)
 int derive_words(const SubEnt *subs, uint32_t *words, uint64_t n, hipStream_t st);
+// nflags[i] = nodes[i].sh_cnt_flags >> 24 for i < n (snapshot upload, on `st`)
+int derive_node_flags(const NodeDesc *nodes, uint8_t *nflags, uint64_t n, hipStream_t st);
 
 // Runs walk -> scan -> dedupe (small / big / DFS) on `st`; returns 0 or a
 // negative MQM_E* code.

@@ -56,6 +56,28 @@
 #endif
 // MQM_COPY16=1: solo copies move 2 entries per lane and access (16-B stores,
 // round 1's form) instead of lane-consecutive 8-B entries (tuning knob)
+// MQM_WALK_STATS=1: count the walk's literal probes, the ones that found no
+// child, and the wildcard-child descriptor loads (printed per batch; tuning)
+#ifndef MQM_WALK_STATS
+#define MQM_WALK_STATS 0
+#endif
+// MQM_SIDE_PCT: share of the resident grid the merge kernels (side stream)
+// take while the solo copy runs on the main stream with the rest, so the two
+// actually run side by side (persistent grids sized to the whole device ran
+// one after the other); 100 = both take the whole device (round-1 behaviour)
+#ifndef MQM_SIDE_PCT
+#define MQM_SIDE_PCT 100
+#endif
+// MQM_WALK_ICAP / MQM_WALK_STAGE: k_walk's per-topic LDS context — load items
+// per level (a topic whose frontier needs more takes the DFS path) and topic
+// bytes staged for the key build.  Together with MQM_WALK_OCC they set how
+// many topics the walk keeps in flight per CU (LDS: 64 topics per block).
+#ifndef MQM_WALK_ICAP
+#define MQM_WALK_ICAP 48
+#endif
+#ifndef MQM_WALK_STAGE
+#define MQM_WALK_STAGE 64
+#endif
 #ifndef MQM_COPY16
 #define MQM_COPY16 0
 #endif
@@ -67,24 +89,29 @@ namespace {
 constexpr int kWave = 64;
 constexpr int kWalkWaves = 4;            // wavefronts per k_walk block
 constexpr int kLMax = 16;                // levels cached per topic
-constexpr int kFCap = 16;                // frontier nodes per level
 constexpr int kHCap = 64;                // non-shared hits per topic (hit_of: 6 search steps)
 constexpr int kShCap = 16;               // shared hits per topic
-constexpr int kStage = 64;               // topic bytes staged in LDS (4 per lane, one round trip)
-// record, written while walking (hits in discovery order; rank orders them):
-//   [0] nh | nsh << 8, [1] Ssolo, [2] M, [3] unused
-//   [4 + 4h] off, [5 + 4h] spre, [6 + 4h] mpre, [7 + 4h] rank of hit h (h < nh):
-//            its range subs[off ..) holds solo entries, then multi ones
-//            (snapshot.h); spre / mpre = solo / multi entries of hits < h
+constexpr int kStage = MQM_WALK_STAGE;    // topic bytes staged in LDS (one round trip)
+// record of a topic, written while walking (kRecStrideAlloc words, 64-B
+// aligned).  A hit range subs[off, off + c) holds solo entries, then multi
+// ones (snapshot.h); the two parts are listed apart, each where its reader
+// wants it, so a topic writes (and its readers read) only the parts it has:
+//   from the start: [2i] off, [2i + 1] count of the i-th solo part (i <
+//            nsolo[t]): k_desc's copy descriptors
 //   [kRecSh + 2i] off, [kRecSh + 1 + 2i] cnt of shared hit i (i < nsh)
-//   [kRecSolo + 2i] off, [kRecSolo + 1 + 2i] solo count of the i-th hit with
-//            solo entries (i < nsolo[t]): k_desc's input, read without the hits
-// One 64-lane load fetches the header and the first 15 hits.
+//   the tail, in 16-B units counted back from the record's end (rec_tail):
+//     unit 0      header: nm | nsh << 8, Ssolo, M, nsolo
+//     unit 1 + h  multi part h (h < nm): moff, mcount, rank of its hit, 0 —
+//                 multi entries subs[moff, moff + mcount); the merges copy
+//                 the tail into LDS as header at word 0, part h at 4 + 4h,
+//                 and turn mcount into the prefix mpre (rec_prefix)
+// Round 1 kept every hit (off, solo, multi, rank) plus the solo pairs: on C3
+// the pure-solo hits made up most of the walk's 3.4 GB of record writes.
 constexpr int kRecHit = 4;
-constexpr int kRecSh = 4 + kRecHit * kHCap;          // 260: header + hits (what the merges read)
-constexpr int kRecSolo = kRecSh + 2 * kShCap;         // 292
-constexpr int kRecStride = kRecSolo + 2 * kHCap;      // 420 words (max)
-constexpr int kRecStrideAlloc = 420;                  // 16-B aligned per topic
+constexpr int kRecLds = 4 + kRecHit * kHCap;          // 260: header + multi parts (the merges' LDS copy)
+constexpr int kRecSh = 2 * kHCap;                     // 128: shared pairs
+constexpr int kRecTail = kRecSh + 2 * kShCap;         // 160: the tail area starts at or after this
+constexpr int kRecStrideAlloc = 432;                  // words per topic: 1728 B = 27 x 64 B
 // raw entries per hit range on the bounded path (keeps the per-lane sums of a
 // topic's 64 hits inside 32 bits); emission itself has no per-topic size
 // limit (window copy of the solo part; partitioned merge of any number of
@@ -99,10 +126,9 @@ constexpr int kSmallMulti = 192;         // multi entries it holds (load <= 0.75
 constexpr int kBigThreads = 256;
 constexpr int kPartCap = 2048;           // k_multi_part: multi entries per client partition (expected)
 constexpr uint32_t kNoWhy = 0xFFFFFFFFu;
-constexpr int kICap = 3 * kFCap;         // load items per level (<= 3 per frontier node)
+constexpr int kICap = MQM_WALK_ICAP;     // load items per level (<= 3 per frontier node; more -> DFS path)
 
-static_assert(kRecStrideAlloc % 4 == 0 && kRecStrideAlloc >= kRecStride, "16-B aligned records");
-static_assert(kRecSh % 4 == 0, "16-B aligned record prefix");
+static_assert(kRecStrideAlloc % 16 == 0 && kRecStrideAlloc >= kRecTail + kRecLds, "64-B aligned records");
 static_assert(kSmallMulti * 4 <= kSmallSlots * 3, "k_emit table load factor");
 static_assert(kSmallMulti % kWave == 0, "register tiles");
 
@@ -129,6 +155,9 @@ struct Counters {              // zeroed before every batch
   unsigned int n_shlist;       // k_shared: topics with shared candidates
   unsigned long long m_sum[3]; // multi entries of the k_multi<1024> / <2048> / k_multi_part lists
   unsigned int oob;            // a store fell outside its output buffer (never expected)
+#if MQM_WALK_STATS
+  unsigned long long st_probe, st_miss, st_desc;
+#endif
 };
 
 struct Outputs {
@@ -151,15 +180,17 @@ struct Outputs {
   uint64_t dcap, hcap;
 };
 
+constexpr int kTopicWords = (2 * kLMax + 8 * kICap + kStage) / 4;
 struct TopicLds {              // k_walk context of one topic (one lane group)
-  uint32_t sep[kLMax];         // position of the '/' ending level k
+  uint16_t sep[kLMax];         // position of the '/' ending level k (topics > 64 KiB: DFS path)
   uint32_t item[2][kICap];     // the level's load items: node id << 2 | kind (kItem*)
   uint8_t stage[kStage];       // the topic's first kStage bytes
-  uint32_t pad[4];             // 132-dword stride: the groups of a wave reading the same
-                               //   field hit 4 banks apart (a 128-dword stride put all 16
-                               //   groups on one bank: SQ_LDS_BANK_CONFLICT 3x the LDS cycles)
+  uint32_t pad[kTopicWords % 2 ? 2 : 1];  // odd dword stride: the groups of a wave reading the
+                               //   same field hit different banks (a 128-dword stride put all
+                               //   16 groups on one bank: SQ_LDS_BANK_CONFLICT 3x the LDS cycles)
 };
-static_assert(sizeof(TopicLds) % 256 == 16, "bank-skewed topic contexts");
+static_assert(kStage % 16 == 0 && kICap >= 3, "walk context");
+static_assert((sizeof(TopicLds) / 4) % 2 == 1, "bank-skewed topic contexts");
 
 __device__ __forceinline__ void wave_lds_sync() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -209,13 +240,13 @@ __device__ __forceinline__ uint32_t qos_bits(uint32_t word) {
 
 
 
-// the hit h holding entry x of a prefix field (kFieldSpre / kFieldMpre): the
+// the multi part h holding multi entry x (prefix field kFieldMpre): the
 // largest h < nh with field(h) <= x (field(0) = 0).  Hits with none of those
 // entries tie with their successor, so the largest such h is the one that
 // holds x.  Branch-free binary search over the prefixes in LDS: 6 dependent
 // reads for nh <= 64 (round 1 counted over every hit per entry: ~nh reads and
 // 2 nh VALU ops per entry, which made emission issue-bound on big topics).
-enum : int { kFieldOff = 0, kFieldSpre = 1, kFieldMpre = 2, kFieldRank = 3 };
+enum : int { kFieldOff = 0, kFieldMpre = 1, kFieldRank = 2 };
 static_assert(kHCap <= 64, "hit_of searches 6 levels");
 template <int kField>
 __device__ __forceinline__ uint32_t hit_of(const uint32_t *rec, uint32_t nh, uint32_t x) {
@@ -275,40 +306,39 @@ __device__ __forceinline__ uint32_t mt_delivery(MergeTable t, uint32_t j) {
 // topics stay in flight per CU.  Hits go straight to the topic's record with
 // their rank (= 2 * node + slot, the reference's emission order).
 // ---------------------------------------------------------------------------
-// A record's hits carry per-hit solo / multi entry counts (fields 1, 2, as
-// k_walk wrote them); its readers turn them into exclusive prefixes in LDS
-// (find_hits searches those).  A group of kL aligned lanes (kL <= 64, a power
-// of two) converts hits 0 .. nh - 1.
+// A record's multi parts carry their entry counts (field kFieldMpre, as k_walk
+// wrote them); the merges turn them into exclusive prefixes in their LDS copy
+// (hit_of searches those).  A group of kL aligned lanes (kL <= 64, a power of
+// two) converts parts 0 .. nh - 1.
 template <int kL, int kCap = kHCap>
 __device__ __forceinline__ void rec_prefix(uint32_t *rec, uint32_t nh, int gl) {
   constexpr int kP = (kCap + kL - 1) / kL;
-  uint32_t sc[kP], mc[kP], ss = 0, ms = 0;
+  uint32_t mc[kP], ms = 0;
 #pragma unroll
   for (int p = 0; p < kP; p++) {
     const uint32_t h = gl * kP + p;
-    sc[p] = h < nh ? rec[4 + kRecHit * h + kFieldSpre] : 0;
     mc[p] = h < nh ? rec[4 + kRecHit * h + kFieldMpre] : 0;
-    ss += sc[p];
     ms += mc[p];
   }
-  uint32_t si = ss, mi = ms;
+  uint32_t mi = ms;
 #pragma unroll
   for (int d = 1; d < kL; d <<= 1) {
-    const uint32_t us = __shfl_up(si, d, kL), um = __shfl_up(mi, d, kL);
-    if (gl >= d) si += us, mi += um;
+    const uint32_t um = __shfl_up(mi, d, kL);
+    if (gl >= d) mi += um;
   }
-  si -= ss;
   mi -= ms;
 #pragma unroll
   for (int p = 0; p < kP; p++) {
     const uint32_t h = gl * kP + p;
-    if (h < nh) {
-      rec[4 + kRecHit * h + kFieldSpre] = si;
-      rec[4 + kRecHit * h + kFieldMpre] = mi;
-    }
-    si += sc[p];
+    if (h < nh) rec[4 + kRecHit * h + kFieldMpre] = mi;
     mi += mc[p];
   }
+}
+
+// 16-B unit u of topic t's record tail is rec_tail(recs, t)[-u] (0 = header,
+// 1 + h = multi part h)
+__device__ __forceinline__ const uint4 *rec_tail(const uint32_t *recs, uint32_t t) {
+  return reinterpret_cast<const uint4 *>(recs + ((uint64_t)t + 1) * kRecStrideAlloc) - 1;
 }
 
 // kG lanes per topic (8 or 16), kWave / kG topics per wavefront
@@ -370,7 +400,7 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
         const uint32_t m = (uint32_t)(__ballot(sep) >> gbase) & kGMask;
         if (sep) {
           const uint32_t idx = nsep + __popc(m & gmask_lt);
-          if (idx < (uint32_t)kLMax) L.sep[idx] = p;
+          if (idx < (uint32_t)kLMax) L.sep[idx] = (uint16_t)p;
         }
         nsep += __popc(m);
       }
@@ -410,7 +440,9 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
     // the '#' child's gather be recorded at push time: partKey '#' of the
     // next level, topics.go:503-505, rank 2 * '#' child).
     uint32_t *rec = o.recs + (uint64_t)(active ? t : 0) * kRecStrideAlloc;
-    uint32_t ni = nlev > 0 ? root_items : 0, nh = 0, nsh = 0, nq = 0;
+    uint4 *tail = reinterpret_cast<uint4 *>(rec + kRecStrideAlloc) - 1;  // unit u at tail[-u]
+    if (len > 0xFFFFu) why = kWhyLevels;  // separators are kept as 16-bit positions
+    uint32_t ni = nlev > 0 && why == kNoWhy ? root_items : 0, nh = 0, nsh = 0, nq = 0, nm = 0;
     uint32_t ls = 0, lm = 0, lh = 0;  // this lane's solo / multi / shared entries
     int cur = 0;
     for (uint32_t d = 0; d < nlev && ni > 0; d++) {
@@ -439,6 +471,19 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
         const uint32_t c = walk_step(s, live && kind == kItemLit && !lit_is_wild, live && kind != kItemLit, id, id,
                                      k0, k1, tp + tst, tln, &dc);
         const bool found = c != kNone;
+#if MQM_WALK_STATS
+        {
+          const bool pr = live && kind == kItemLit && !lit_is_wild;
+          const uint32_t mp = (uint32_t)(__ballot(pr) >> gbase) & kGMask;
+          const uint32_t mm = (uint32_t)(__ballot(pr && !found) >> gbase) & kGMask;
+          const uint32_t md = (uint32_t)(__ballot(live && kind != kItemLit) >> gbase) & kGMask;
+          if (gl == 0) {
+            atomicAdd(&o.ctr->st_probe, (unsigned long long)__popc(mp));
+            atomicAdd(&o.ctr->st_miss, (unsigned long long)__popc(mm));
+            atomicAdd(&o.ctr->st_desc, (unsigned long long)__popc(md));
+          }
+        }
+#endif
         const uint32_t fl = found ? dc.sh_cnt_flags >> 24 : 0;
         const bool skip_dollar = dollar && (fl & kFlagDollarWild);  // topics.go:527
         const uint32_t c_own = found && !skip_dollar ? dc.sub_cnt : 0;
@@ -468,40 +513,41 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
                                 max(c_own, max(c_par, c_hl)) > kSMax) >> gbase) & kGMask)
           why = kWhyEntries;
         if (why != kNoWhy) break;
-        // solo / multi split of the ranges (multi entries sit at the end); the
-        // record keeps per-hit counts, its readers turn them into prefixes
+        // solo / multi split of the ranges (multi entries sit at the end of a
+        // range; the '#' child's range follows its parent's, snapshot.h): the
+        // multi parts go to the record's tail with their hit's rank
         const uint32_t mu_own = c_own ? (dc.multi & 0xFFFFu) : 0, mu_par = c_par ? (dc.multi >> 16) : 0;
         const uint32_t mu_hl = c_hl ? (dc.multi >> 16) : 0;
-        if (active && c_own) {
-          uint32_t *hr = rec + 4 + kRecHit * (nh + __popc(m_own & gmask_lt));
-          *reinterpret_cast<uint4 *>(hr) = make_uint4(dc.sub_off, c_own - mu_own, mu_own, 2 * c);
-        }
-        if (active && c_par) {  // the '#' child's range follows (snapshot.h)
-          uint32_t *hr = rec + 4 + kRecHit * (nh + n_own + __popc(m_par & gmask_lt));
-          *reinterpret_cast<uint4 *>(hr) = make_uint4(dc.sub_off + dc.sub_cnt, c_par - mu_par, mu_par, 2 * c + 1);
-        }
-        if (active && c_hl) {
-          uint32_t *hr = rec + 4 + kRecHit * (nh + n_own + n_par + __popc(m_hl & gmask_lt));
-          *reinterpret_cast<uint4 *>(hr) = make_uint4(dc.sub_off + dc.sub_cnt, c_hl - mu_hl, mu_hl, 2 * dc.hash);
-        }
+        const uint32_t hoff = dc.sub_off + dc.sub_cnt;
+        const uint32_t x_own = (uint32_t)(__ballot(mu_own > 0) >> gbase) & kGMask;
+        const uint32_t x_par = (uint32_t)(__ballot(mu_par > 0) >> gbase) & kGMask;
+        const uint32_t x_hl = (uint32_t)(__ballot(mu_hl > 0) >> gbase) & kGMask;
+        if (active && mu_own)
+          tail[-(int)(1 + nm + __popc(x_own & gmask_lt))] = make_uint4(dc.sub_off + c_own - mu_own, mu_own, 2 * c, 0);
+        if (active && mu_par)
+          tail[-(int)(1 + nm + __popc(x_own) + __popc(x_par & gmask_lt))] =
+              make_uint4(hoff + c_par - mu_par, mu_par, 2 * c + 1, 0);
+        if (active && mu_hl)
+          tail[-(int)(1 + nm + __popc(x_own) + __popc(x_par) + __popc(x_hl & gmask_lt))] =
+              make_uint4(hoff + c_hl - mu_hl, mu_hl, 2 * dc.hash, 0);
+        nm += __popc(x_own) + __popc(x_par) + __popc(x_hl);
         if (active && c_sh) {
           const uint32_t i = nsh + __popc(m_sh & gmask_lt);
           *reinterpret_cast<uint2 *>(rec + kRecSh + 2 * i) = make_uint2(dc.sh_off, c_sh);
         }
-        // the hits with solo entries again, as (off, solo count) pairs in the
-        // same order: k_desc reads these instead of every hit
+        // the solo parts, as (off, solo count) pairs from the record's start
         const uint32_t q_own = (uint32_t)(__ballot(c_own > mu_own) >> gbase) & kGMask;
         const uint32_t q_par = (uint32_t)(__ballot(c_par > mu_par) >> gbase) & kGMask;
         const uint32_t q_hl = (uint32_t)(__ballot(c_hl > mu_hl) >> gbase) & kGMask;
         if (active && c_own > mu_own)
-          *reinterpret_cast<uint2 *>(rec + kRecSolo + 2 * (nq + __popc(q_own & gmask_lt))) =
+          *reinterpret_cast<uint2 *>(rec + 2 * (nq + __popc(q_own & gmask_lt))) =
               make_uint2(dc.sub_off, c_own - mu_own);
         if (active && c_par > mu_par)
-          *reinterpret_cast<uint2 *>(rec + kRecSolo + 2 * (nq + __popc(q_own) + __popc(q_par & gmask_lt))) =
-              make_uint2(dc.sub_off + dc.sub_cnt, c_par - mu_par);
+          *reinterpret_cast<uint2 *>(rec + 2 * (nq + __popc(q_own) + __popc(q_par & gmask_lt))) =
+              make_uint2(hoff, c_par - mu_par);
         if (active && c_hl > mu_hl)
-          *reinterpret_cast<uint2 *>(rec + kRecSolo + 2 * (nq + __popc(q_own) + __popc(q_par) + __popc(q_hl & gmask_lt))) =
-              make_uint2(dc.sub_off + dc.sub_cnt, c_hl - mu_hl);
+          *reinterpret_cast<uint2 *>(rec + 2 * (nq + __popc(q_own) + __popc(q_par) + __popc(q_hl & gmask_lt))) =
+              make_uint2(hoff, c_hl - mu_hl);
         nq += __popc(q_own) + __popc(q_par) + __popc(q_hl);
         if (push) {
           uint32_t *nx = &L.item[cur ^ 1][nnext + __popc(m_i0 & gmask_lt) + 2 * __popc(m_i1 & gmask_lt)];
@@ -533,12 +579,8 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
     if (why == kNoWhy && S > kSMax) why = kWhyEntries;
     if (active && gl == 0) {
       const bool dfs = why != kNoWhy;
-      if (!dfs) {
-        rec[0] = nh | (nsh << 8);
-        rec[1] = Ss;
-        rec[2] = Ms;
-      }
-      o.cls[t] = dfs ? kClsDfs : (S == 0 && H == 0) ? kClsDone : (kClsBounded | (nh <= kSmallHits ? kClsFewHits : 0));
+      if (!dfs) tail[0] = make_uint4(nm | (nsh << 8), Ss, Ms, nq);
+      o.cls[t] = dfs ? kClsDfs : (S == 0 && H == 0) ? kClsDone : (kClsBounded | (nm <= kSmallHits ? kClsFewHits : 0));
       o.nsolo[t] = dfs ? 0 : nq;
       o.scount[t] = dfs ? 0 : S;
       o.hcount[t] = dfs ? 0 : H;
@@ -580,13 +622,11 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
 // subscription's fields.
 // ---------------------------------------------------------------------------
 
-// multi entry q of a topic: subs index and hit
-__device__ __forceinline__ uint32_t multi_sid(const uint32_t *rec, uint32_t nh, uint32_t Ss, uint32_t q,
-                                              uint32_t *hit) {
+// multi entry q of a topic: subs index and multi part
+__device__ __forceinline__ uint32_t multi_sid(const uint32_t *rec, uint32_t nh, uint32_t q, uint32_t *hit) {
   const uint32_t h = hit_of<kFieldMpre>(rec, nh, q);
-  const uint32_t solo_h = (h + 1 < nh ? rec_at(rec, h + 1, kFieldSpre) : Ss) - rec_at(rec, h, kFieldSpre);
   *hit = h;
-  return rec_at(rec, h, kFieldOff) + solo_h + (q - rec_at(rec, h, kFieldMpre));
+  return rec_at(rec, h, kFieldOff) + (q - rec_at(rec, h, kFieldMpre));
 }
 
 __device__ __forceinline__ SubEnt load_sub(const DeviceSnapshot &s, uint32_t sid) {
@@ -611,7 +651,7 @@ __global__ __launch_bounds__(256) void k_desc(Outputs o, uint32_t n, const uint6
     if (o.mcount[t] == 0) o.dcount[t] = o.scount[t];
     if (q == 0) continue;
     const uint64_t db = o.dstart[t], pb = desc_start[t];
-    const uint2 *pr = reinterpret_cast<const uint2 *>(o.recs + (uint64_t)t * kRecStrideAlloc + kRecSolo);
+    const uint2 *pr = reinterpret_cast<const uint2 *>(o.recs + (uint64_t)t * kRecStrideAlloc);
     uint64_t at = db;
     for (uint32_t i = 0; i < q; i++) {
       const uint2 v = pr[i];
@@ -632,7 +672,7 @@ __global__ __launch_bounds__(256) void k_shared(Outputs o, const uint32_t *__res
     (void)g;
     const uint32_t t = list[i];
     const uint32_t *grec = o.recs + (uint64_t)t * kRecStrideAlloc;
-    const uint32_t nsh = grec[0] >> 8;
+    const uint32_t nsh = (rec_tail(o.recs, t)[0].x >> 8) & 0xFFu;
     const uint64_t hb = o.hstart[t];
     uint32_t w = 0;
     for (uint32_t j = 0; j < nsh; j++) {
@@ -738,6 +778,12 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
   }
 }
 
+__global__ __launch_bounds__(256) void k_nflags(const NodeDesc *__restrict__ nodes, uint8_t *__restrict__ f,
+                                                uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    f[i] = (uint8_t)(nodes[i].sh_cnt_flags >> 24);
+}
+
 __global__ __launch_bounds__(256) void k_words(const SubEnt *__restrict__ subs, uint32_t *__restrict__ words,
                                                uint64_t n) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
@@ -809,10 +855,10 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
   uint64_t n_db = 0;
   auto fetch = [&](uint32_t u) {
     n_db = o.dstart[u];
-    const uint32_t *r = o.recs + (uint64_t)u * kRecStrideAlloc + gl * kRecPer;
+    const uint4 *r = rec_tail(o.recs, u);  // units gl * kRecPer / 4 ..: header, multi parts
 #pragma unroll
     for (int v = 0; v < kRecPer / 4; v++) {
-      const uint4 x = *reinterpret_cast<const uint4 *>(r + 4 * v);
+      const uint4 x = r[-(gl * (kRecPer / 4) + v)];
       n_rw[4 * v] = x.x, n_rw[4 * v + 1] = x.y, n_rw[4 * v + 2] = x.z, n_rw[4 * v + 3] = x.w;
     }
   };
@@ -836,7 +882,7 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
     for (int k = 0; k < kMPer; k++) {
       const uint32_t q = gl + k * kSE;
       uint32_t h;
-      const uint32_t sid = multi_sid(L.rec, nh, Ss, q < M ? q : 0, &h);
+      const uint32_t sid = multi_sid(L.rec, nh, q < M ? q : 0, &h);
       mrk[k] = rec_at(L.rec, h, kFieldRank);
       const SubEnt e = load_sub(s, sid);
       mcl[k] = e.client;
@@ -853,7 +899,7 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
 // more than kSmallHits hits) ----------------------------------------------------
 struct alignas(16) MergeLds {
   unsigned long long tfirst[kSmallSlots];
-  uint32_t rec[kRecSh];
+  uint32_t rec[kRecLds];
   uint32_t tkey[kSmallSlots], tbits[kSmallSlots];
 };
 
@@ -866,23 +912,25 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_merge(DeviceSnapshot s, O
   MergeLds &L = lds_all[threadIdx.x / kWave];
   const uint32_t nw = gridDim.x * kEmitWaves, nl = *count;
   uint32_t i = blockIdx.x * kEmitWaves + threadIdx.x / kWave;
-  uint32_t n_t = 0, n_rw = 0;
+  uint32_t n_t = 0;
+  uint4 n_rw = make_uint4(0, 0, 0, 0);
   uint64_t n_db = 0;
   auto fetch = [&](uint32_t k) {
     n_t = list[k];
     n_db = o.dstart[n_t];
-    n_rw = o.recs[(uint64_t)n_t * kRecStrideAlloc + lane];
+    if (lane < 16) n_rw = rec_tail(o.recs, n_t)[-lane];  // header + the first 15 multi parts
   };
   if (i < nl) fetch(i);
   for (; i < nl; i += nw) {
     const uint32_t t = n_t;
     const uint64_t db = n_db;
-    L.rec[lane] = n_rw;
+    uint4 *rec4 = reinterpret_cast<uint4 *>(L.rec);
+    if (lane < 16) rec4[lane] = n_rw;
     if (i + nw < nl) fetch(i + nw);
     wave_lds_sync();
     const uint32_t nh = L.rec[0] & 0xFFu, Ss = L.rec[1], M = L.rec[2];
-    const uint32_t *grec = o.recs + (uint64_t)t * kRecStrideAlloc;
-    for (uint32_t w = kWave + lane; w < 4 + kRecHit * nh; w += kWave) L.rec[w] = grec[w];
+    const uint4 *gt = rec_tail(o.recs, t);
+    for (uint32_t u = 16 + lane; u < 1 + nh; u += kWave) rec4[u] = gt[-(int)u];
     wave_lds_sync();
     rec_prefix<kWave>(L.rec, nh, lane);
     wave_lds_sync();
@@ -891,7 +939,7 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_merge(DeviceSnapshot s, O
     for (int k = 0; k < kMPer; k++) {
       const uint32_t q = lane + k * kWave;
       uint32_t h;
-      const uint32_t sid = multi_sid(L.rec, nh, Ss, q < M ? q : 0, &h);
+      const uint32_t sid = multi_sid(L.rec, nh, q < M ? q : 0, &h);
       mrk[k] = rec_at(L.rec, h, kFieldRank);
       const SubEnt e = load_sub(s, sid);
       mcl[k] = e.client;
@@ -918,14 +966,16 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_merge(DeviceSnapshot s, O
 // then write at its prefix), so the layout is deterministic.
 // ---------------------------------------------------------------------------
 struct alignas(16) MultiLds {
-  uint32_t rec[kRecSh];
+  uint32_t rec[kRecLds];
   uint32_t wsum[kBigThreads / kWave];
 };
 
 // the block's record of topic t, with prefixes (all threads; ends synced)
 __device__ __forceinline__ void block_record(Outputs o, uint32_t t, uint32_t *rec) {
   const int tid = threadIdx.x;
-  for (uint32_t i = tid; i < (uint32_t)kRecSh; i += kBigThreads) rec[i] = o.recs[(uint64_t)t * kRecStrideAlloc + i];
+  const uint4 *gt = rec_tail(o.recs, t);
+  for (uint32_t u = tid; u < (uint32_t)kRecLds / 4; u += kBigThreads)
+    reinterpret_cast<uint4 *>(rec)[u] = gt[-(int)u];
   __syncthreads();
   const uint32_t nh = rec[0] & 0xFFu;
   __syncthreads();
@@ -983,7 +1033,7 @@ __global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs
     __syncthreads();
     for (uint32_t q = tid; q < M; q += kBigThreads) {  // (a hit-by-hit loop measured slower: idle lanes on small hits)
       uint32_t h;
-      const uint32_t sid = multi_sid(L.rec, nh, Ss, q, &h);
+      const uint32_t sid = multi_sid(L.rec, nh, q, &h);
       const SubEnt e = load_sub(s, sid);
       mt_insert(tb, mask, lg, e.client, e.word, rec_at(L.rec, h, kFieldRank));
     }
@@ -1027,7 +1077,7 @@ __global__ __launch_bounds__(kBigThreads) void k_multi_part(DeviceSnapshot s, Ou
       __syncthreads();
       for (uint32_t q = tid; q < M; q += kBigThreads) {
         uint32_t h;
-        const uint32_t sid = multi_sid(L.rec, nh, Ss, q, &h);
+        const uint32_t sid = multi_sid(L.rec, nh, q, &h);
         const SubEnt e = load_sub(s, sid);
         if (partition_of(e.client, P) != p) continue;
         if (atomicAdd(&fill, 1u) >= kFill) {  // never for a hash of this spread: fail, do not spin
@@ -1270,17 +1320,27 @@ __global__ __launch_bounds__(256) void k_ident(DeviceSnapshot s, Outputs o, uint
     if (cls == kClsDfs) continue;
     uint32_t nid = 0;
     if (cls != kClsDone) {
+      // every gathered range: the solo parts, then the multi parts
       const uint32_t *rec = o.recs + (uint64_t)t * kRecStrideAlloc;
-      const uint32_t nh = rec[0] & 0xFFu;
+      const uint4 *gt = rec_tail(o.recs, t);
+      const uint4 hd = gt[0];
+      const uint32_t nm = hd.x & 0xFFu, nq = hd.w;
       const uint64_t ib = kPhase == 1 ? o.istart[t] : 0;
-      for (uint32_t h = 0; h < nh; h++) {
-        const uint4 hr = *reinterpret_cast<const uint4 *>(rec + 4 + kRecHit * h);  // off, solo, multi, rank
-        const uint32_t cnt = hr.y + hr.z;
+      for (uint32_t h = 0; h < nq + nm; h++) {
+        uint32_t off, cnt;
+        if (h < nq) {
+          off = rec[2 * h];
+          cnt = rec[2 * h + 1];
+        } else {
+          const uint4 u = gt[-(int)(1 + h - nq)];
+          off = u.x;
+          cnt = u.y;
+        }
         for (uint32_t b0 = 0; b0 < cnt; b0 += kWave) {
           const uint32_t j = b0 + lane;
-          const bool has = j < cnt && (s.subs[hr.x + j].word & kWordIdent);
+          const bool has = j < cnt && (s.subs[off + j].word & kWordIdent);
           const uint64_t m = __ballot(has);
-          if (kPhase == 1 && has) o.iout[ib + nid + __popcll(m & lanemask_lt(lane))] = hr.x + j;
+          if (kPhase == 1 && has) o.iout[ib + nid + __popcll(m & lanemask_lt(lane))] = off + j;
           nid += (uint32_t)__popcll(m);
         }
       }
@@ -1684,11 +1744,18 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   mark(ws, 2, st);
   static_assert(kWave * kEmitWaves == kBigThreads, "resident_blocks assumes 256-thread blocks");
   if (n > 0) {
-    auto grid = [&](auto kern) { return dim3(resident_blocks(ws, 0, kern)); };
     // merges on the side stream, concurrently with the solo copy (they write
     // disjoint parts of dout and dcount: winners after Ss / topics with Ms > 0)
     const bool merges = hc->n_small || hc->n_wmerge || hc->n_t1 || hc->n_t2 || hc->n_part;
     const bool side = merges && ws.overlap;
+    // persistent grids: with both streams busy, each takes its share of the device
+    const uint32_t side_pct = side ? MQM_SIDE_PCT : 100, main_pct = side && MQM_SIDE_PCT < 100 ? 100 - MQM_SIDE_PCT : 100;
+    auto grid = [&](auto kern) {
+      return dim3(std::max<uint32_t>(1, resident_blocks(ws, 0, kern) * side_pct / 100));
+    };
+    auto main_grid = [&](auto kern) {
+      return dim3(std::max<uint32_t>(1, resident_blocks(ws, 0, kern) * main_pct / 100));
+    };
     hipStream_t ms = st;
     if (merges) {
       if (side && ws.fork(st, &ms)) return -3;
@@ -1730,7 +1797,7 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
       hipLaunchKernelGGL(k_winmap, dim3((uint32_t)std::min<uint64_t>((n_desc + 255) / 256, 8192)), dim3(256), 0, st,
                          desc, n_desc, s_total, win);
       HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(k_wincopy, grid(k_wincopy), dim3(kWave * kEmitWaves), 0, st, s, desc, n_desc, win, n_win,
+      hipLaunchKernelGGL(k_wincopy, main_grid(k_wincopy), dim3(kWave * kEmitWaves), 0, st, s, desc, n_desc, win, n_win,
                          s_total, o.dout, o.dcap, &o.ctr->oob);
       HIP_TRY(hipGetLastError());
     }
@@ -1768,6 +1835,10 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
     fprintf(stderr, "mqmatch: an output store fell outside its buffer (batch rejected)\n");
     return -3;
   }
+#if MQM_WALK_STATS
+  fprintf(stderr, "[walk-stats] topics %u literal probes %llu missed %llu wildcard-child loads %llu\n", n,
+          hc->st_probe, hc->st_miss, hc->st_desc);
+#endif
   if (ws.profile) {
     ws.prof_calls++;
     ws.prof_fallback_topics += n_dfs;
@@ -1842,6 +1913,13 @@ int identifiers_device(const DeviceSnapshot &s, Workspace &ws, hipStream_t st, I
   out->offsets = o.istart;
   out->sids = o.iout;
   return 0;
+}
+
+int derive_node_flags(const NodeDesc *nodes, uint8_t *nflags, uint64_t n, hipStream_t st) {
+  if (n)
+    hipLaunchKernelGGL(k_nflags, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 16384)), dim3(256), 0, st, nodes,
+                       nflags, n);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
 int derive_words(const SubEnt *subs, uint32_t *words, uint64_t n, hipStream_t st) {

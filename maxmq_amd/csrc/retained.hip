@@ -5,14 +5,22 @@
 // The reference recurses per filter (scanMessages).  Here the recursion is
 // unrolled level-synchronously over the whole batch, as worklists of
 // (filter, node) items in HBM, so wildcard fan-out never overflows a
-// per-filter buffer and every level is a balanced launch:
+// per-filter buffer and every level is a balanced launch.  The whole call is
+// queued without waiting for the device: every list is appended through
+// wave-aggregated atomic counters that live on the device, every kernel is a
+// grid-stride loop over a count it reads from device memory, and the host
+// reads the counters back once at the end (plus once at the start for the
+// filters' level count).  Lists are sized from the previous call; a list that
+// would overflow is flagged, and the call is re-queued with the sizes the
+// counters report (first call of a workload only).
 //   k_flt_levels   a thread per filter: split into levels (isolateParticle,
 //                  topics.go:558-577), 128-bit level keys, wildcard flag
-//   k_bfs<count|fill>  a thread per item of level d: the reference's three
+//   k_level<d>     a thread per item of level d: the reference's three
 //                  cases (topics.go:447-477) —
 //                    literal : one edge probe (the forward matcher's table)
 //                    '+'/'#' with more levels: every child (minus "$SYS" at
-//                             the root, :450) becomes an item of level d+1
+//                             the root, :450) becomes an item of level d+1;
+//                             a wavefront writes a big child list together
 //                    '+' last : the node's retained children      (:454-460)
 //                    '#' last : every retained node below it      (:462, the
 //                             recursion keeps isolating the last level)
@@ -21,9 +29,11 @@
 //                             topic "" (Retained.Get(""), :474)
 //                  emissions are (filter, list, lo, hi) ranges of message refs:
 //                  subtrees are contiguous in preorder (snapshot.h)
-//   k_emit_*       ranges -> per-filter CSR of message refs, copied in
-//                  fixed-size chunks so one huge '#' range is spread over
-//                  many wavefronts
+//   k_emit_count / k_emit_place / k_task_copy
+//                  ranges -> per-filter CSR of message refs: small ranges
+//                  copied by their thread, large ones cut into fixed-size
+//                  copy tasks so one huge '#' range is spread over many
+//                  wavefronts
 // Exact filters (no '+'/'#', :440-445) are the literal walk of the same items
 // with Retained.Get(filter) semantics (no "" fallback).
 #include <hip/hip_runtime.h>
@@ -31,7 +41,6 @@
 
 #include <algorithm>
 #include <cstdio>
-#include <vector>
 
 #include "device.h"
 #include "retained.h"
@@ -40,8 +49,11 @@ namespace mqm {
 
 namespace {
 
-constexpr uint32_t kEmitChunk = 4096;  // refs copied per wavefront task
-constexpr uint32_t kSmallEmit = 32;    // emissions up to this size: copied by one thread
+constexpr uint32_t kTaskRefs = 8192;   // refs copied per wavefront task
+constexpr uint32_t kSmallEmit = 32;    // emissions up to this size: copied by their own thread
+constexpr uint32_t kCoopItems = 64;    // a lane with more next-level items than this: the wave writes them
+constexpr uint32_t kLevelBatch = 16;   // levels queued between two looks at the counters
+constexpr int kThreads = 256;
 
 struct Level {         // one level of one filter
   uint64_t k0, k1;     // key (keys.h)
@@ -49,6 +61,20 @@ struct Level {         // one level of one filter
 };
 
 enum : uint32_t { kTypeLiteral = 0, kTypePlus = 1, kTypeHash = 2 };
+
+enum : uint32_t { kOvfItems = 1, kOvfEmit = 2, kOvfTasks = 4, kOvfOut = 8 };
+
+// device-side counters of one call (zeroed at its start); items[d] = items
+// appended to level d (d >= 1), the append cursor of that level's list
+struct RevCtr {
+  unsigned long long n_emit, n_tasks;
+  unsigned long long need_items;  // largest level seen (also past the capacity)
+  unsigned long long items_total; // items over all levels (statistics)
+  unsigned long long skipped;     // items the reference visits that the edge index jumps over
+  unsigned int ovf;               // kOvf* bits
+  unsigned int pad;
+  unsigned long long items[1];    // [levels + 1]
+};
 
 __device__ __forceinline__ uint32_t level_type(const Level &l) {
   if (l.k1 != (1ull << 56)) return kTypeLiteral;
@@ -96,7 +122,84 @@ __global__ void k_flt_fill(const uint8_t *__restrict__ bytes, const uint64_t *__
   }
 }
 
-struct BfsArgs {
+// exclusive wave scan of a 64-bit count; *total = the wave's sum
+__device__ __forceinline__ uint64_t wave_excl(uint64_t v, uint64_t *total) {
+  const int lane = threadIdx.x & 63;
+  uint64_t inc = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t lo = __shfl_up((uint32_t)inc, d, 64), hi = __shfl_up((uint32_t)(inc >> 32), d, 64);
+    if (lane >= d) inc += ((uint64_t)hi << 32) | lo;
+  }
+  const uint32_t tlo = __shfl((uint32_t)inc, 63, 64), thi = __shfl((uint32_t)(inc >> 32), 63, 64);
+  *total = ((uint64_t)thi << 32) | tlo;
+  return inc - v;
+}
+
+// one atomic per wavefront: reserve `v` slots of a list for every lane;
+// returns the lane's first slot
+__device__ __forceinline__ uint64_t wave_reserve(unsigned long long *ctr, uint64_t v) {
+  uint64_t total;
+  const uint64_t ex = wave_excl(v, &total);
+  unsigned long long base = 0;
+  if ((threadIdx.x & 63) == 0 && total) base = atomicAdd(ctr, (unsigned long long)total);
+  const uint32_t lo = __shfl((uint32_t)base, 0, 64), hi = __shfl((uint32_t)(base >> 32), 0, 64);
+  return (((uint64_t)hi << 32) | lo) + ex;
+}
+
+__device__ __forceinline__ uint64_t bcast64(uint64_t v, int src) {
+  const uint32_t lo = __shfl((uint32_t)v, src, 64), hi = __shfl((uint32_t)(v >> 32), src, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ bool retained_node(const DeviceRetained &r, uint32_t c) {
+  return r.cum[c + 1] > r.cum[c];
+}
+
+// what a node must have for an item of a level of this type to produce
+// anything: a literal child (its probe) or any child ('+' / '#')
+__device__ __forceinline__ uint32_t need_of(const Level &l, bool wild) {
+  return wild && level_type(l) != kTypeLiteral ? kFlagHasChildren : kFlagHasLiteral;
+}
+
+// the edge index's group (level key of l, child depth): its edges
+// inv[*start, *start + *count); false when no such edge exists
+__device__ bool rev_group(const DeviceRetained &r, const uint8_t *tok_pool, const Level &l, const uint8_t *ftok,
+                          uint32_t depth, uint32_t *start, uint32_t *count) {
+  const Key k{l.k0, l.k1};
+  uint64_t slot = bucket_of(edge_hash(depth, k), r.n_gslots);
+  for (;;) {
+    const RevGroup g = r.groups[slot];
+    if (g.count == 0) return false;
+    if (g.k0 == k.k0 && g.k1 == k.k1 && (g.depth_len & 0xFFFFu) == depth) {
+      bool ok = true;
+      if (key_is_long(k)) {  // hashed long token: verify the bytes
+        ok = (g.depth_len >> 16) == l.len;
+        for (uint32_t i = 0; ok && i < l.len; i++) ok = tok_pool[g.tok_off + i] == ftok[i];
+      }
+      if (ok) {
+        *start = g.start;
+        *count = g.count;
+        return true;
+      }
+    }
+    slot = slot + 1 == r.n_gslots ? 0 : slot + 1;
+  }
+}
+
+// first j in [lo, hi) with inv[j].x >= key (parents are sorted within a group)
+__device__ __forceinline__ uint32_t inv_lower(const uint2 *inv, uint32_t lo, uint32_t hi, uint32_t key) {
+  while (lo < hi) {
+    const uint32_t mid = lo + (hi - lo) / 2;
+    if (inv[mid].x < key)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+struct LevelArgs {
   DeviceSnapshot s;
   DeviceRetained r;
   const uint8_t *bytes;
@@ -105,109 +208,211 @@ struct BfsArgs {
   const uint32_t *nlev;
   const uint8_t *wild;
   const Level *lv;
+  uint32_t n;                       // filters (the implicit level-0 list: item f = (f, root))
   uint32_t d;
-  uint64_t n_items;
-  const uint32_t *item_f, *item_n;  // items of level d
-  uint32_t *child;                  // literal probe result (count pass -> fill pass)
-  uint32_t *ncount, *ecount;        // count pass outputs
-  const uint64_t *noff, *eoff;      // fill pass: exclusive scans of the above
-  uint32_t *next_f, *next_n;        // fill pass: items of level d + 1
-  Emit *emit;                       // fill pass: emissions (already offset by the running base)
+  const uint32_t *item_f, *item_n;  // level d's list (d >= 1)
+  uint32_t *next_f, *next_n;        // level d + 1's list
+  uint32_t *skip_f, *skip_n;        // level d + 2's list (wildcard + literal through the edge index)
+  uint64_t item_cap;                // capacity of each list
+  Emit *emit;
+  uint64_t emit_cap;
+  RevCtr *ctr;
 };
 
-__device__ __forceinline__ bool retained_node(const DeviceRetained &r, uint32_t c) {
-  return r.cum[c + 1] > r.cum[c];
-}
-
-// kFill == false: count next items / emissions; true: write them
-template <bool kFill>
-__global__ void k_bfs(BfsArgs a) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.n_items) return;
-  const uint32_t f = a.item_f[i], p = a.item_n[i];
-  const uint32_t L = a.nlev[f];
-  const Level l = a.lv[a.loff[f] + a.d];
-  const bool has_next = a.d + 1 < L;
-  const uint32_t type = a.wild[f] ? level_type(l) : kTypeLiteral;
+// a thread per item of level d; the loop is grid-stride over the level's
+// count as the previous launch left it in ctr->items[d]
+__global__ __launch_bounds__(kThreads) void k_level(LevelArgs a) {
   const DeviceRetained &r = a.r;
-  uint32_t nn = 0, ne = 0;
-  uint64_t nb = 0, eb = 0;
-  if (kFill) {
-    nb = a.noff[i];
-    eb = a.eoff[i];
-  }
-  auto emit = [&](uint32_t list, uint32_t lo, uint32_t hi) {
-    if (hi <= lo) return;
-    if (kFill) a.emit[eb + ne] = Emit{f, list, lo, hi};
-    ne++;
-  };
-  if (type == kTypeLiteral) {  // topics.go:469-477 (and :440-445 for exact filters)
-    uint32_t c;
-    if (kFill) {
-      c = a.child[i];
-    } else {
-      NodeDesc dc;
-      c = probe_edge(a.s, p, l.k0, l.k1, a.bytes + a.offs[f] + l.start, l.len, &dc);
-      a.child[i] = c;
+  const int lane = threadIdx.x & 63;
+  const uint64_t cnt = a.d == 0 ? a.n : min((uint64_t)a.ctr->items[a.d], a.item_cap);
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  // whole wavefronts iterate together (the appends below are wave-collective)
+  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < cnt; base += stride) {
+    const uint64_t i = base + lane;
+    uint32_t f = 0, p = kNone;
+    if (i < cnt) {
+      if (a.d == 0) {
+        f = (uint32_t)i;
+        p = a.nlev[f] ? 0u : kNone;
+      } else {
+        f = a.item_f[i];
+        p = a.item_n[i];
+      }
     }
-    if (c != kNone) {
+    // outputs of this lane: one next item (literal), a child range (wildcard
+    // with more levels), or up to two emissions
+    uint32_t nx_one = kNone, ch_lo = 0, ch_hi = 0, ne = 0;
+    // what a node of the next level must have to continue (need_of)
+    uint32_t need = 0;
+    // wildcard + literal through the edge index: edges inv[rg_lo, rg_hi) give
+    // the level d + 2 nodes (or, the literal being last, the emissions)
+    uint32_t rg_lo = 0, rg_hi = 0, need2 = 0, skipped = 0;
+    bool rg_emit = false;
+    Emit e0{f, 0, 0, 0}, e1{f, 0, 0, 0};
+    if (p != kNone) {
+      const uint32_t L = a.nlev[f];
+      const Level l = a.lv[a.loff[f] + a.d];
+      const bool has_next = a.d + 1 < L;
+      const bool wild = a.wild[f] != 0;
+      const uint32_t type = wild ? level_type(l) : kTypeLiteral;
+      Level l1{};
       if (has_next) {
-        if (kFill) {
-          a.next_f[nb] = f;
-          a.next_n[nb] = c;
+        l1 = a.lv[a.loff[f] + a.d + 1];
+        need = need_of(l1, wild);
+      }
+      if (type == kTypeLiteral) {  // topics.go:469-477 (and :440-445 for exact filters)
+        NodeDesc dc;
+        const uint32_t c = probe_edge(a.s, p, l.k0, l.k1, a.bytes + a.offs[f] + l.start, l.len, &dc);
+        if (c != kNone) {
+          if (has_next) {
+            if ((dc.sh_cnt_flags >> 24) & need) nx_one = c;  // else no item of the next level can match
+          } else if (retained_node(r, c)) {
+            e0 = Emit{f, 0, r.cum[c], r.cum[c] + 1};
+            ne = 1;
+          } else if (wild && r.has_empty) {  // Retained.Get("") through an empty retainPath
+            e0 = Emit{f, 0, (uint32_t)r.n_ret, (uint32_t)r.n_ret + 1};
+            ne = 1;
+          }
         }
-        nn = 1;
-      } else if (retained_node(r, c)) {
-        emit(0, r.cum[c], r.cum[c] + 1);
-      } else if (a.wild[f] && r.has_empty) {  // Retained.Get("") through an empty retainPath
-        emit(0, (uint32_t)r.n_ret, (uint32_t)r.n_ret + 1);
+      } else if (has_next && r.n_gslots && level_type(l1) == kTypeLiteral) {
+        // '+' / '#', then a literal K: the reference probes K under every
+        // child x of p (:449-477); the index lists exactly the x that have a
+        // child K — edges of group (K, depth d + 2) whose parent lies in p's
+        // subtree (a node of depth d + 1 there is a child of p)
+        uint32_t gs, gc;
+        if (rev_group(r, a.s.tok_pool, l1, a.bytes + a.offs[f] + l1.start, a.d + 2, &gs, &gc)) {
+          rg_lo = inv_lower(r.inv, gs, gs + gc, p + 1);
+          rg_hi = inv_lower(r.inv, rg_lo, gs + gc, p + r.subtree[p]);
+        }
+        rg_emit = a.d + 2 >= L;
+        if (!rg_emit) need2 = need_of(a.lv[a.loff[f] + a.d + 2], wild);
+        skipped = r.child_off[p + 1] - r.child_off[p] - (a.d == 0 && r.sys_child != kNone ? 1u : 0u);
+      } else if (has_next) {  // '+' or '#' followed by more levels: every child (:449-465)
+        ch_lo = r.child_off[p];
+        ch_hi = r.child_off[p + 1];
+      } else if (type == kTypePlus) {  // the retained children (root's list excludes "$SYS")
+        e0 = Emit{f, 1, r.rch_off[p], r.rch_off[p + 1]};
+        ne = e0.hi > e0.lo;
+      } else {  // '#' last: the subtree below p, "$SYS" skipped at the root (:450)
+        const uint32_t end = p + r.subtree[p];
+        if (a.d == 0 && r.sys_child != kNone) {
+          const uint32_t sys = r.sys_child;
+          e0 = Emit{f, 0, r.cum[p + 1], r.cum[sys]};
+          e1 = Emit{f, 0, r.cum[sys + r.subtree[sys]], r.cum[end]};
+          if (e0.hi <= e0.lo) e0 = e1, e1.hi = e1.lo;
+          ne = (e0.hi > e0.lo) + (e1.hi > e1.lo);
+        } else {
+          e0 = Emit{f, 0, r.cum[p + 1], r.cum[end]};
+          ne = e0.hi > e0.lo;
+        }
       }
     }
-  } else if (has_next) {  // '+' or '#' followed by more levels: recurse into every child (:449-465)
-    const uint32_t skip = a.d == 0 ? r.sys_child : kNone;
-    for (uint32_t j = r.child_off[p]; j < r.child_off[p + 1]; j++) {
-      const uint32_t c = r.child_ids[j];
-      if (c == skip) continue;
-      if (kFill) {
-        a.next_f[nb + nn] = f;
-        a.next_n[nb + nn] = c;
+    // next-level items: one per literal hit, the child list of a wildcard
+    const uint32_t nn = nx_one != kNone ? 1u : ch_hi - ch_lo;
+    if (__any(nn != 0)) {
+      const uint64_t at = wave_reserve(&a.ctr->items[a.d + 1], nn);
+      if (lane == 63) atomicMax(&a.ctr->need_items, (unsigned long long)(at + nn));
+      if (at + nn > a.item_cap) atomicOr(&a.ctr->ovf, (unsigned)kOvfItems);
+      // "$SYS" at the root, and every child that cannot continue (node flags),
+      // become dead items (kNone): the next level skips them without a read
+      const uint32_t skip = a.d == 0 ? r.sys_child : kNone;
+      const uint32_t sneed = need;
+      if (nx_one != kNone) {
+        if (at < a.item_cap) {
+          a.next_f[at] = f;
+          a.next_n[at] = nx_one;
+        }
+      } else if (nn <= kCoopItems) {
+        for (uint32_t k = 0; k < nn; k++) {
+          if (at + k >= a.item_cap) break;
+          const uint32_t c = r.child_ids[ch_lo + k];
+          a.next_f[at + k] = f;
+          a.next_n[at + k] = c == skip || !(r.nflags[c] & sneed) ? kNone : c;
+        }
       }
-      nn++;
+      uint64_t big = __ballot(nx_one == kNone && nn > kCoopItems);
+      while (big) {  // long child lists: the whole wavefront writes each
+        const int src = __builtin_ctzll(big);
+        big &= big - 1;
+        const uint32_t sf = __shfl(f, src, 64), slo = __shfl(ch_lo, src, 64), snn = __shfl(nn, src, 64);
+        const uint32_t bneed = __shfl(need, src, 64);
+        const uint64_t sat = bcast64(at, src);
+        for (uint32_t k = lane; k < snn; k += 64) {
+          if (sat + k >= a.item_cap) break;
+          const uint32_t c = r.child_ids[slo + k];
+          a.next_f[sat + k] = sf;
+          a.next_n[sat + k] = c == skip || !(r.nflags[c] & bneed) ? kNone : c;
+        }
+      }
     }
-  } else if (type == kTypePlus) {  // the retained children (root's list excludes "$SYS")
-    emit(1, r.rch_off[p], r.rch_off[p + 1]);
-  } else {  // '#' last: the subtree below p, "$SYS" skipped at the root (:450)
-    const uint32_t end = p + r.subtree[p];
-    if (a.d == 0 && r.sys_child != kNone) {
-      const uint32_t sys = r.sys_child;
-      emit(0, r.cum[p + 1], r.cum[sys]);
-      emit(0, r.cum[sys + r.subtree[sys]], r.cum[end]);
-    } else {
-      emit(0, r.cum[p + 1], r.cum[end]);
+    if (__any(ne != 0)) {
+      const uint64_t at = wave_reserve(&a.ctr->n_emit, ne);
+      if (at + ne > a.emit_cap) atomicOr(&a.ctr->ovf, (unsigned)kOvfEmit);
+      if (ne > 0 && at < a.emit_cap) a.emit[at] = e0;
+      if (ne > 1 && at + 1 < a.emit_cap) a.emit[at + 1] = e1;
+    }
+    if (__any(skipped != 0)) {  // statistics: the reference's level d + 1 items
+      uint64_t tot;
+      (void)wave_excl(skipped, &tot);
+      if (lane == 0) atomicAdd(&a.ctr->skipped, (unsigned long long)tot);
+    }
+    // index ranges, a wavefront each, 64 edges per step, outputs compacted
+    uint64_t rt = __ballot(rg_hi > rg_lo);
+    while (rt) {
+      const int src = __builtin_ctzll(rt);
+      rt &= rt - 1;
+      const uint32_t sf = __shfl(f, src, 64), slo = __shfl(rg_lo, src, 64), shi = __shfl(rg_hi, src, 64);
+      const uint32_t sneed = __shfl(need2, src, 64);
+      const bool semit = __shfl((uint32_t)rg_emit, src, 64) != 0;
+      const bool sroot = a.d == 0;
+      for (uint32_t j0 = slo; j0 < shi; j0 += 64) {
+        const uint32_t j = j0 + lane;
+        bool valid = j < shi;
+        uint32_t c = 0;
+        Emit em{sf, 0, 0, 0};
+        if (valid) {
+          const uint2 ed = r.inv[j];
+          c = ed.y;
+          valid = !(sroot && ed.x == r.sys_child);
+          if (valid && !semit) {
+            valid = (r.nflags[c] & sneed) != 0;
+          } else if (valid) {  // the literal is last: c's message, else Retained.Get("") (:474)
+            if (retained_node(r, c))
+              em = Emit{sf, 0, r.cum[c], r.cum[c] + 1};
+            else if (r.has_empty)
+              em = Emit{sf, 0, (uint32_t)r.n_ret, (uint32_t)r.n_ret + 1};
+            else
+              valid = false;
+          }
+        }
+        const uint64_t m = __ballot(valid);
+        if (!m) continue;
+        const uint32_t k = (uint32_t)__popcll(m);
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(semit ? &a.ctr->n_emit : &a.ctr->items[a.d + 2], (unsigned long long)k);
+        base = bcast64(base, 0);
+        const uint64_t pos = base + __popcll(m & ((1ull << lane) - 1ull));
+        if (semit) {
+          if (lane == 0 && base + k > a.emit_cap) atomicOr(&a.ctr->ovf, (unsigned)kOvfEmit);
+          if (valid && pos < a.emit_cap) a.emit[pos] = em;
+        } else {
+          if (lane == 0) {
+            atomicMax(&a.ctr->need_items, base + k);
+            if (base + k > a.item_cap) atomicOr(&a.ctr->ovf, (unsigned)kOvfItems);
+          }
+          if (valid && pos < a.item_cap) {
+            a.skip_f[pos] = sf;
+            a.skip_n[pos] = c;
+          }
+        }
+      }
     }
   }
-  if (!kFill) {
-    a.ncount[i] = nn;
-    a.ecount[i] = ne;
-  }
 }
 
-__global__ void k_init_items(uint32_t n, const uint32_t *__restrict__ nlev, uint32_t *__restrict__ item_f,
-                             uint32_t *__restrict__ item_n, const uint64_t *__restrict__ pos) {
-  const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= n || nlev[f] == 0) return;
-  item_f[pos[f]] = f;
-  item_n[pos[f]] = 0;
-}
-
-__global__ void k_has_levels(uint32_t n, const uint32_t *__restrict__ nlev, uint32_t *__restrict__ flag) {
-  const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f < n) flag[f] = nlev[f] ? 1u : 0u;
-}
-
-// Emissions of one filter are adjacent (every level's items and emissions
-// stay in filter order), so a wavefront folds each run of equal filter ids
-// (segmented scan over the lanes) and issues one atomic per run.
+// Emissions of one filter are mostly adjacent (a wave appends its lanes' in
+// order), so a wavefront folds each run of equal filter ids (segmented scan
+// over the lanes) and issues one atomic per run.
 struct Run {
   uint64_t inc;    // inclusive sum of cnt within the lane's run
   bool last;       // the lane closes its run
@@ -234,71 +439,88 @@ __device__ __forceinline__ Run fold_runs(uint32_t f, uint64_t cnt) {
   return r;
 }
 
-__global__ __launch_bounds__(256) void k_emit_count(uint64_t ne, const Emit *__restrict__ e,
-                                                   unsigned long long *__restrict__ fcount) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool ok = i < ne;
-  const uint32_t f = ok ? e[i].f : 0xFFFFFFFFu;
-  const uint64_t cnt = ok ? e[i].hi - e[i].lo : 0;
-  const Run r = fold_runs(f, cnt);
-  if (ok && r.last) atomicAdd(&fcount[f], (unsigned long long)r.inc);
+// grid-stride over the emissions the level kernels appended
+__global__ __launch_bounds__(kThreads) void k_emit_count(const Emit *__restrict__ e, uint64_t cap, RevCtr *ctr,
+                                                        unsigned long long *__restrict__ fcount, uint32_t levels) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // the level kernels are done: total their lists
+    unsigned long long t = 0;
+    for (uint32_t d = 1; d <= levels; d++) t += ctr->items[d];
+    ctr->items_total = t + ctr->skipped;
+  }
+  const uint64_t ne = min((uint64_t)ctr->n_emit, cap);
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < ne; base += stride) {
+    const uint64_t i = base + (threadIdx.x & 63);
+    const bool ok = i < ne;
+    const uint32_t f = ok ? e[i].f : 0xFFFFFFFFu;
+    const uint64_t cnt = ok ? e[i].hi - e[i].lo : 0;
+    const Run r = fold_runs(f, cnt);
+    if (ok && r.last) atomicAdd(&fcount[f], (unsigned long long)r.inc);
+  }
 }
 
-__global__ __launch_bounds__(256) void k_emit_pos(uint64_t ne, const Emit *__restrict__ e,
-                                                 const uint64_t *__restrict__ foff,
-                                                 unsigned long long *__restrict__ fcur, uint64_t *__restrict__ pos,
-                                                 uint32_t *__restrict__ chunks) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool ok = i < ne;
-  const uint32_t f = ok ? e[i].f : 0xFFFFFFFFu;
-  const uint64_t cnt = ok ? e[i].hi - e[i].lo : 0;
-  const Run r = fold_runs(f, cnt);
-  unsigned long long base = 0;
-  if (ok && r.last) base = foff[f] + atomicAdd(&fcur[f], (unsigned long long)r.inc);
-  const uint32_t blo = __shfl((uint32_t)base, r.last_lane, 64), bhi = __shfl((uint32_t)(base >> 32), r.last_lane, 64);
-  const uint32_t tlo = __shfl((uint32_t)r.inc, r.last_lane, 64), thi = __shfl((uint32_t)(r.inc >> 32), r.last_lane, 64);
-  if (!ok) return;
-  const uint64_t run_base = ((uint64_t)bhi << 32) | blo, run_total = ((uint64_t)thi << 32) | tlo;
-  (void)run_total;
-  pos[i] = run_base + (r.inc - cnt);
-  chunks[i] = cnt > kSmallEmit ? (uint32_t)((cnt + kEmitChunk - 1) / kEmitChunk) : 0u;
-}
+struct Task {            // copy list[lo, lo + len) to out[dst ..)
+  uint64_t dst;
+  uint32_t lo, len_list; // len | list << 31
+};
 
-// emissions of <= kSmallEmit refs: a thread each
-__global__ __launch_bounds__(256) void k_emit_small(uint64_t ne, const Emit *__restrict__ e,
-                                                   const uint64_t *__restrict__ pos,
-                                                   const uint64_t *__restrict__ refs,
-                                                   const uint64_t *__restrict__ rch_refs, uint64_t *__restrict__ out) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= ne) return;
-  const Emit it = e[i];
-  const uint32_t cnt = it.hi - it.lo;
-  if (cnt > kSmallEmit) return;
-  const uint64_t *src = (it.list ? rch_refs : refs) + it.lo;
-  uint64_t *dst = out + pos[i];
-  for (uint32_t j = 0; j < cnt; j++) dst[j] = src[j];
-}
-
-// larger emissions: a wavefront per chunk of kEmitChunk refs
-__global__ __launch_bounds__(256) void k_emit_fill(uint64_t ne, uint64_t nchunks, const Emit *__restrict__ e,
-                                                  const uint64_t *__restrict__ pos, const uint64_t *__restrict__ coff,
-                                                  const uint64_t *__restrict__ refs,
-                                                  const uint64_t *__restrict__ rch_refs, uint64_t *__restrict__ out) {
+// each emission's place in its filter's segment: small ones copied here,
+// large ones cut into kTaskRefs copy tasks
+__global__ __launch_bounds__(kThreads) void k_emit_place(const Emit *__restrict__ e, uint64_t cap, RevCtr *ctr,
+                                                        const uint64_t *__restrict__ foff,
+                                                        unsigned long long *__restrict__ fcur,
+                                                        const uint64_t *__restrict__ refs,
+                                                        const uint64_t *__restrict__ rch_refs,
+                                                        uint64_t *__restrict__ out, uint64_t out_cap,
+                                                        Task *__restrict__ tasks, uint64_t task_cap) {
+  const uint64_t ne = min((uint64_t)ctr->n_emit, cap);
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   const int lane = threadIdx.x & 63;
-  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / 64);
-  for (uint64_t c = (uint64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; c < nchunks; c += nw) {
-    uint64_t lo = 0, hi = ne;  // item i with coff[i] <= c < coff[i + 1]
-    while (hi - lo > 1) {
-      const uint64_t mid = (lo + hi) / 2;
-      if (coff[mid] <= c) lo = mid;
-      else hi = mid;
+  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < ne; base += stride) {
+    const uint64_t i = base + lane;
+    const bool ok = i < ne;
+    const Emit it = ok ? e[i] : Emit{0xFFFFFFFFu, 0, 0, 0};
+    const uint64_t cnt = it.hi - it.lo;
+    const Run r = fold_runs(it.f, cnt);
+    unsigned long long rb = 0;
+    if (ok && r.last) rb = foff[it.f] + atomicAdd(&fcur[it.f], (unsigned long long)r.inc);
+    const uint64_t pos = bcast64(rb, r.last_lane) + (r.inc - cnt);  // run base + the run's entries before this lane
+    if (!ok || cnt == 0) continue;
+    if (pos + cnt > out_cap) {
+      atomicOr(&ctr->ovf, (unsigned)kOvfOut);
+      continue;
     }
-    const Emit it = e[lo];
-    const uint64_t k0 = (c - coff[lo]) * kEmitChunk;
-    const uint64_t cnt = std::min<uint64_t>(kEmitChunk, (uint64_t)(it.hi - it.lo) - k0);
-    const uint64_t *src = (it.list ? rch_refs : refs) + it.lo + k0;
-    uint64_t *dst = out + pos[lo] + k0;
-    for (uint64_t j = lane; j < cnt; j += 64) dst[j] = src[j];
+    const uint64_t *src = (it.list ? rch_refs : refs) + it.lo;
+    if (cnt <= kSmallEmit) {
+      for (uint32_t j = 0; j < (uint32_t)cnt; j++) out[pos + j] = src[j];
+      continue;
+    }
+    const uint32_t nt = (uint32_t)((cnt + kTaskRefs - 1) / kTaskRefs);
+    const unsigned long long t0 = atomicAdd(&ctr->n_tasks, (unsigned long long)nt);
+    if (t0 + nt > task_cap) atomicOr(&ctr->ovf, (unsigned)kOvfTasks);
+    // every slot below the capacity is written (k_task_copy reads them all)
+    for (uint32_t k = 0; k < nt && t0 + k < task_cap; k++) {
+      const uint32_t len = (uint32_t)min<uint64_t>(kTaskRefs, cnt - (uint64_t)k * kTaskRefs);
+      tasks[t0 + k] = Task{pos + (uint64_t)k * kTaskRefs, it.lo + k * kTaskRefs, len | (it.list << 31)};
+    }
+  }
+}
+
+// a wavefront per copy task, grid-stride over the tasks k_emit_place queued
+__global__ __launch_bounds__(kThreads) void k_task_copy(const Task *__restrict__ tasks, uint64_t cap,
+                                                       const RevCtr *ctr, const uint64_t *__restrict__ refs,
+                                                       const uint64_t *__restrict__ rch_refs,
+                                                       uint64_t *__restrict__ out) {
+  if (ctr->ovf) return;  // this attempt is discarded (re-queued with larger lists)
+  const uint64_t nt = min((uint64_t)ctr->n_tasks, cap);
+  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / 64);
+  const int lane = threadIdx.x & 63;
+  for (uint64_t t = (uint64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; t < nt; t += nw) {
+    const Task k = tasks[t];
+    const uint32_t len = k.len_list & 0x7FFFFFFFu;
+    const uint64_t *src = ((k.len_list >> 31) ? rch_refs : refs) + k.lo;
+    uint64_t *dst = out + k.dst;
+    for (uint32_t j = lane; j < len; j += 64) dst[j] = src[j];
   }
 }
 
@@ -330,7 +552,24 @@ int scan_u64(Workspace &ws, const T *counts, uint64_t *offs, uint64_t n, hipStre
   return 0;
 }
 
-uint32_t blocks_for(uint64_t n, uint32_t threads = 256) { return (uint32_t)std::max<uint64_t>(1, (n + threads - 1) / threads); }
+uint32_t blocks_for(uint64_t n, uint32_t threads = kThreads) {
+  return (uint32_t)std::max<uint64_t>(1, (n + threads - 1) / threads);
+}
+
+// blocks of a grid-stride kernel: what stays resident on the device
+uint32_t resident_grid() {
+  static uint32_t g = 0;
+  if (!g) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+      cus = 256;
+    g = (uint32_t)cus * 8;  // 8 blocks of 256 threads = 32 waves per CU
+  }
+  return g;
+}
+
+size_t ctr_bytes(uint32_t levels) { return sizeof(RevCtr) + sizeof(unsigned long long) * (levels + 1); }
 
 }  // namespace
 
@@ -354,12 +593,11 @@ int messages_device(const DeviceSnapshot &s, const DeviceRetained *r, Workspace 
   auto *nlev = (uint32_t *)ws.ptr(W::kRNLev);
   auto *wild = (uint8_t *)ws.ptr(W::kRWild);
   auto *loff = (uint64_t *)ws.ptr(W::kRLOff);
-  auto *fcount = (uint64_t *)ws.ptr(W::kRFCount);
-  auto *fcur = (uint64_t *)ws.ptr(W::kRFCur);
   uint64_t *hp = ws.pinned_u64();
   if (!hp) return -2;
 
-  hipLaunchKernelGGL(k_flt_count, dim3(blocks_for(n)), dim3(256), 0, st, d_bytes, d_offs, n, nlev, wild);
+  // the filters' levels: the one read-back before the walk sizes their array
+  hipLaunchKernelGGL(k_flt_count, dim3(blocks_for(n)), dim3(kThreads), 0, st, d_bytes, d_offs, n, nlev, wild);
   HIP_TRY(hipGetLastError());
   if (scan_u64(ws, nlev, loff, n, st)) return -3;
   HIP_TRY(hipMemcpyAsync(hp, loff + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
@@ -367,33 +605,32 @@ int messages_device(const DeviceSnapshot &s, const DeviceRetained *r, Workspace 
   const uint64_t total_levels = hp[0];
   if (ws.get(W::kRLevels, sizeof(Level) * (total_levels + 1))) return -2;
   auto *lv = (Level *)ws.ptr(W::kRLevels);
-  hipLaunchKernelGGL(k_flt_fill, dim3(blocks_for(n)), dim3(256), 0, st, d_bytes, d_offs, n, loff, lv);
+  hipLaunchKernelGGL(k_flt_fill, dim3(blocks_for(n)), dim3(kThreads), 0, st, d_bytes, d_offs, n, loff, lv);
   HIP_TRY(hipGetLastError());
 
-  // level-0 items: (f, root) for every non-empty filter, in filter order
-  if (ws.get(W::kRNCount, sizeof(uint32_t) * (n + 1)) || ws.get(W::kRNOff, sizeof(uint64_t) * (n + 2))) return -2;
-  {
-    auto *flag = (uint32_t *)ws.ptr(W::kRNCount);
-    auto *pos = (uint64_t *)ws.ptr(W::kRNOff);
-    hipLaunchKernelGGL(k_has_levels, dim3(blocks_for(n)), dim3(256), 0, st, n, nlev, flag);
-    if (scan_u64(ws, flag, pos, n, st)) return -3;
-    HIP_TRY(hipMemcpyAsync(hp, pos + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    if (ws.get(W::kRItemF0, sizeof(uint32_t) * (hp[0] + 1)) || ws.get(W::kRItemN0, sizeof(uint32_t) * (hp[0] + 1)))
+  // every list starts at its size from the previous call (grown on overflow)
+  uint64_t &item_cap = ws.rev_item_cap, &emit_cap = ws.rev_emit_cap, &task_cap = ws.rev_task_cap,
+           &out_cap = ws.rev_out_cap;
+  item_cap = std::max<uint64_t>(item_cap, std::max<uint64_t>(4ull * n, 1u << 16));
+  emit_cap = std::max<uint64_t>(emit_cap, std::max<uint64_t>(2ull * n, 1u << 16));
+  task_cap = std::max<uint64_t>(task_cap, 1u << 12);
+  out_cap = std::max<uint64_t>(out_cap, std::max<uint64_t>(4ull * n, 1u << 16));
+  const uint32_t grid = resident_grid();
+  for (int attempt = 0;; attempt++) {
+    if (ws.get(W::kRItemF0, sizeof(uint32_t) * item_cap) || ws.get(W::kRItemN0, sizeof(uint32_t) * item_cap) ||
+        ws.get(W::kRItemF1, sizeof(uint32_t) * item_cap) || ws.get(W::kRItemN1, sizeof(uint32_t) * item_cap) ||
+        ws.get(W::kRChild, sizeof(uint32_t) * item_cap) || ws.get(W::kRECount, sizeof(uint32_t) * item_cap) ||
+        ws.get(W::kREmit, sizeof(Emit) * emit_cap) || ws.get(W::kRChunks, sizeof(Task) * task_cap) ||
+        ws.get(W::kROut, sizeof(uint64_t) * out_cap))
       return -2;
-    hipLaunchKernelGGL(k_init_items, dim3(blocks_for(n)), dim3(256), 0, st, n, nlev, (uint32_t *)ws.ptr(W::kRItemF0),
-                       (uint32_t *)ws.ptr(W::kRItemN0), pos);
-    HIP_TRY(hipGetLastError());
-  }
-  uint64_t n_items = hp[0];
-  uint64_t n_emit = 0, items_total = 0;
-  W::Slot cur_f = W::kRItemF0, cur_n = W::kRItemN0, nxt_f = W::kRItemF1, nxt_n = W::kRItemN1;
-  for (uint32_t d = 0; n_items > 0; d++) {
-    if (ws.get(W::kRChild, sizeof(uint32_t) * (n_items + 1)) || ws.get(W::kRNCount, sizeof(uint32_t) * (n_items + 1)) ||
-        ws.get(W::kRECount, sizeof(uint32_t) * (n_items + 1)) || ws.get(W::kRNOff, sizeof(uint64_t) * (n_items + 1)) ||
-        ws.get(W::kREOff, sizeof(uint64_t) * (n_items + 1)))
-      return -2;
-    BfsArgs a{};
+    // levels 0 .. height: an item of level d sits on a node of depth d
+    const uint32_t max_levels = s.height + 1;
+    if (ws.get(W::kRNCount, ctr_bytes(max_levels + 1))) return -2;
+    auto *ctr = (RevCtr *)ws.ptr(W::kRNCount);
+    HIP_TRY(hipMemsetAsync(ctr, 0, ctr_bytes(max_levels + 1), st));
+    HIP_TRY(hipMemsetAsync(ws.ptr(W::kRFCount), 0, sizeof(uint64_t) * (n + 1), st));
+    HIP_TRY(hipMemsetAsync(ws.ptr(W::kRFCur), 0, sizeof(uint64_t) * (n + 1), st));
+    LevelArgs a{};
     a.s = s;
     a.r = *r;
     a.bytes = d_bytes;
@@ -402,81 +639,71 @@ int messages_device(const DeviceSnapshot &s, const DeviceRetained *r, Workspace 
     a.nlev = nlev;
     a.wild = wild;
     a.lv = lv;
-    a.d = d;
-    a.n_items = n_items;
-    a.item_f = (const uint32_t *)ws.ptr(cur_f);
-    a.item_n = (const uint32_t *)ws.ptr(cur_n);
-    a.child = (uint32_t *)ws.ptr(W::kRChild);
-    a.ncount = (uint32_t *)ws.ptr(W::kRNCount);
-    a.ecount = (uint32_t *)ws.ptr(W::kRECount);
-    hipLaunchKernelGGL(k_bfs<false>, dim3(blocks_for(n_items)), dim3(256), 0, st, a);
+    a.n = n;
+    a.item_cap = item_cap;
+    a.emit = (Emit *)ws.ptr(W::kREmit);
+    a.emit_cap = emit_cap;
+    a.ctr = ctr;
+    // level L's list lives in buffer pair L % 3 (a level appends to the next
+    // two: wildcard + literal through the edge index jumps one level)
+    const W::Slot lf[3] = {W::kRItemF0, W::kRItemF1, W::kRChild}, ln[3] = {W::kRItemN0, W::kRItemN1, W::kRECount};
+    for (uint32_t d = 0; d < max_levels; d++) {
+      a.d = d;
+      a.item_f = (const uint32_t *)ws.ptr(lf[d % 3]);
+      a.item_n = (const uint32_t *)ws.ptr(ln[d % 3]);
+      a.next_f = (uint32_t *)ws.ptr(lf[(d + 1) % 3]);
+      a.next_n = (uint32_t *)ws.ptr(ln[(d + 1) % 3]);
+      a.skip_f = (uint32_t *)ws.ptr(lf[(d + 2) % 3]);
+      a.skip_n = (uint32_t *)ws.ptr(ln[(d + 2) % 3]);
+      const uint32_t g = d == 0 ? std::min<uint32_t>(grid, blocks_for(n)) : grid;
+      hipLaunchKernelGGL(k_level, dim3(g), dim3(kThreads), 0, st, a);
+      HIP_TRY(hipGetLastError());
+      // every kLevelBatch levels, stop early once the next two levels are empty
+      if ((d + 1) % kLevelBatch == 0 && d + 1 < max_levels) {
+        HIP_TRY(hipMemcpyAsync(hp, &ctr->items[d + 1], 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (hp[0] == 0 && hp[1] == 0) break;
+      }
+    }
+    // emissions -> per-filter CSR
+    auto *fcount = (unsigned long long *)ws.ptr(W::kRFCount);
+    hipLaunchKernelGGL(k_emit_count, dim3(grid), dim3(kThreads), 0, st, a.emit, emit_cap, ctr, fcount,
+                       max_levels);
     HIP_TRY(hipGetLastError());
-    auto *noff = (uint64_t *)ws.ptr(W::kRNOff);
-    auto *eoff = (uint64_t *)ws.ptr(W::kREOff);
-    if (scan_u64(ws, a.ncount, noff, n_items, st) || scan_u64(ws, a.ecount, eoff, n_items, st)) return -3;
-    HIP_TRY(hipMemcpyAsync(hp, noff + n_items, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(hp + 1, eoff + n_items, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    if (scan_u64(ws, (const uint64_t *)fcount, foff, n, st)) return -3;
+    auto *refs_out = (uint64_t *)ws.ptr(W::kROut);
+    auto *tasks = (Task *)ws.ptr(W::kRChunks);
+    hipLaunchKernelGGL(k_emit_place, dim3(grid), dim3(kThreads), 0, st, a.emit, emit_cap, ctr, foff,
+                       (unsigned long long *)ws.ptr(W::kRFCur), r->refs, r->rch_refs, refs_out, out_cap, tasks,
+                       task_cap);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_task_copy, dim3(grid), dim3(kThreads), 0, st, tasks, task_cap, ctr, r->refs, r->rch_refs,
+                       refs_out);
+    HIP_TRY(hipGetLastError());
+    // the one read-back: sizes and overflow flags
+    RevCtr *hc = reinterpret_cast<RevCtr *>(hp);
+    static_assert(sizeof(RevCtr) + 8 <= 128, "pinned read-back area");
+    HIP_TRY(hipMemcpyAsync(hc, ctr, sizeof(RevCtr), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(hp + 15, foff + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    const uint64_t nn = hp[0], ne = hp[1];
-    if (ws.get(nxt_f, sizeof(uint32_t) * (nn + 1)) || ws.get(nxt_n, sizeof(uint32_t) * (nn + 1)) ||
-        ws.grow_keep(W::kREmit, sizeof(Emit) * n_emit, sizeof(Emit) * (n_emit + ne + 1), st))
-      return -2;
-    a.item_f = (const uint32_t *)ws.ptr(cur_f);  // (unchanged slots; pointers re-read after growth)
-    a.item_n = (const uint32_t *)ws.ptr(cur_n);
-    a.noff = noff;
-    a.eoff = eoff;
-    a.next_f = (uint32_t *)ws.ptr(nxt_f);
-    a.next_n = (uint32_t *)ws.ptr(nxt_n);
-    a.emit = (Emit *)ws.ptr(W::kREmit) + n_emit;
-    hipLaunchKernelGGL(k_bfs<true>, dim3(blocks_for(n_items)), dim3(256), 0, st, a);
-    HIP_TRY(hipGetLastError());
-    n_emit += ne;
-    items_total += n_items;
-    n_items = nn;
-    std::swap(cur_f, nxt_f);
-    std::swap(cur_n, nxt_n);
+    const uint64_t n_refs = hp[15];
+    const unsigned ovf = hc->ovf;
+    const uint64_t n_emit = hc->n_emit, n_tasks = hc->n_tasks, need_items = hc->need_items;
+    if (ovf == 0) {
+      out->n_refs = n_refs;
+      out->refs = refs_out;
+      out->n_emissions = n_emit;
+      out->n_items = hc->items_total + n;  // level 0 = one item per filter
+      return 0;
+    }
+    if (attempt >= 64) return -3;  // (the counters only ever grow: never reached)
+    // re-queue with the sizes this attempt needed (its later levels may have
+    // been cut short, so another round can still grow them)
+    if (ovf & kOvfItems) item_cap = std::max(item_cap, need_items + need_items / 4);
+    if (ovf & kOvfEmit) emit_cap = std::max(emit_cap, n_emit + n_emit / 4);
+    if (ovf & kOvfTasks) task_cap = std::max(task_cap, n_tasks + n_tasks / 4);
+    if (ovf & kOvfOut) out_cap = std::max(out_cap, n_refs + n_refs / 4);
   }
-
-  // emissions -> per-filter CSR
-  auto *emit = (Emit *)ws.ptr(W::kREmit);
-  HIP_TRY(hipMemsetAsync(fcount, 0, sizeof(uint64_t) * (n + 1), st));
-  HIP_TRY(hipMemsetAsync(fcur, 0, sizeof(uint64_t) * (n + 1), st));
-  if (n_emit)
-    hipLaunchKernelGGL(k_emit_count, dim3(blocks_for(n_emit)), dim3(256), 0, st, n_emit, emit,
-                       (unsigned long long *)fcount);
-  HIP_TRY(hipGetLastError());
-  if (scan_u64(ws, fcount, foff, n, st)) return -3;
-  if (ws.get(W::kRPos, sizeof(uint64_t) * (n_emit + 1)) || ws.get(W::kRChunks, sizeof(uint32_t) * (n_emit + 1)) ||
-      ws.get(W::kRCOff, sizeof(uint64_t) * (n_emit + 1)))
-    return -2;
-  auto *pos = (uint64_t *)ws.ptr(W::kRPos);
-  auto *chunks = (uint32_t *)ws.ptr(W::kRChunks);
-  auto *coff = (uint64_t *)ws.ptr(W::kRCOff);
-  if (n_emit)
-    hipLaunchKernelGGL(k_emit_pos, dim3(blocks_for(n_emit)), dim3(256), 0, st, n_emit, emit, foff,
-                       (unsigned long long *)fcur, pos, chunks);
-  HIP_TRY(hipGetLastError());
-  if (scan_u64(ws, chunks, coff, n_emit, st)) return -3;
-  HIP_TRY(hipMemcpyAsync(hp, foff + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipMemcpyAsync(hp + 1, coff + n_emit, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
-  const uint64_t n_refs = hp[0], nchunks = hp[1];
-  if (ws.get(W::kROut, sizeof(uint64_t) * (n_refs + 1))) return -2;
-  auto *refs_out = (uint64_t *)ws.ptr(W::kROut);
-  if (n_emit)
-    hipLaunchKernelGGL(k_emit_small, dim3(blocks_for(n_emit)), dim3(256), 0, st, n_emit, emit, pos, r->refs,
-                       r->rch_refs, refs_out);
-  HIP_TRY(hipGetLastError());
-  if (nchunks)
-    hipLaunchKernelGGL(k_emit_fill, dim3((uint32_t)std::min<uint64_t>((nchunks + 3) / 4, 8192)), dim3(256), 0, st,
-                       n_emit, nchunks, emit, pos, coff, r->refs, r->rch_refs, refs_out);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipStreamSynchronize(st));
-  out->n_refs = n_refs;
-  out->refs = refs_out;
-  out->n_emissions = n_emit;
-  out->n_items = items_total;
-  return 0;
 }
 
 }  // namespace mqm

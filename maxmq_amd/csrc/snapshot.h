@@ -111,6 +111,15 @@ struct DeviceSnapshot {
   uint32_t height;        // max node depth (root = 0)
 };
 
+// one (token, depth) group of the reverse walk's literal-edge index
+struct RevGroup {
+  uint64_t k0, k1;    // the token's level key (keys.h); count == 0: empty slot
+  uint32_t depth_len; // child depth | token length << 16 (long tokens: bytes verified)
+  uint32_t tok_off;   // long tokens: bytes at tok_pool[tok_off ..)
+  uint32_t start, count;  // its edges: inv[start, start + count)
+};
+static_assert(sizeof(RevGroup) == 32, "RevGroup layout");
+
 // Retained-message side of the snapshot (TopicsIndex.Messages, topics.go:426-480),
 // built only when the store holds retained messages.  Preorder ids make every
 // subtree the contiguous id range [i, i + subtree[i]), so "all retained
@@ -124,7 +133,19 @@ struct DeviceRetained {
                               //   message retained at topic "" (has_empty), see below
   const uint32_t *rch_off;    // n_nodes + 1: retained children of i = rch_refs[rch_off[i] ..)
   const uint64_t *rch_refs;   // (the root's list leaves out the root child "$SYS")
+  const uint8_t *nflags;      // n_nodes: NodeDesc flags (kFlagHasChildren, kFlagHasLiteral) of every
+                              //   node, one byte each (79 MB at config 5: stays in the Infinity Cache),
+                              //   so a wildcard's expansion drops children that cannot continue
+                              //   without reading their descriptors
   uint64_t n_ret;
+  // literal-edge index for a wildcard followed by a literal level: the edges
+  // (parent, child) grouped by (child token, child depth), each group sorted
+  // by parent.  Children of node p are the ids in (p, p + subtree[p]) at
+  // depth(p) + 1, so "every child x of p, then the literal K under x" is one
+  // binary-searched range of group (K, depth(p) + 2): no per-child probe.
+  const uint2 *inv;           // {parent, child} per literal edge, by (group, parent)
+  const struct RevGroup *groups;  // open-addressed (linear probing), n_gslots slots
+  uint64_t n_gslots;          // 0: no index (the walk probes every child)
   uint32_t n_nodes;
   uint32_t sys_child;         // the root child named exactly "$SYS", or kNone
   uint32_t has_empty;         // a message is retained at topic "": its retainPath is ""
