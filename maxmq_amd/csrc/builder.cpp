@@ -258,6 +258,7 @@ uint64_t snapshot_digest(const HostSnapshot &hs) {
   d.vec(hs.sub_info);
   d.vec(hs.shared_info);
   d.vec(hs.tok_pool);
+  d.vec(hs.bloom);
   d.vec(hs.subtree);
   d.vec(hs.child_off);
   d.vec(hs.child_ids);

@@ -67,7 +67,13 @@ __device__ __forceinline__ uint32_t walk_step(const DeviceSnapshot &s, bool do_p
                                               const uint8_t *tok, uint32_t tok_len, NodeDesc *desc) {
   const Key key{k0, k1};
   const uint64_t nslots = s.n_buckets * kEdgesPerBucket;
-  uint64_t slot = do_probe ? bucket_of(edge_hash(parent, key), s.n_buckets) * kEdgesPerBucket : 0;
+  const uint64_t h = do_probe ? edge_hash(parent, key) : 0;
+  if (s.bloom) {  // a literal no edge has: no probe (its bucket would be a DRAM request)
+    const uint64_t w = do_probe ? s.bloom[bloom_word(h, s.bloom_mask)] : 0;
+    const uint64_t b = bloom_bits(h);
+    do_probe = do_probe && (w & b) == b;
+  }
+  uint64_t slot = do_probe ? bucket_of(h, s.n_buckets) * kEdgesPerBucket : 0;
   const uint4 *q = do_probe ? reinterpret_cast<const uint4 *>(s.edges + slot)
                             : reinterpret_cast<const uint4 *>(s.nodes + (do_desc ? wc : 0));
   uint4 x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3];

@@ -537,6 +537,24 @@ int flatten(const Store &st, HostSnapshot *out) {
       }
     }
   });
+  // the edge-existence filter: >= 16 bits per edge, a power of two of words
+  // (env MQM_NO_BLOOM=1: none, for A/B runs); OR is order-free, so the
+  // parallel fill is deterministic
+  hs.bloom.clear();
+  if (n_literal_edges && !getenv("MQM_NO_BLOOM")) {
+    uint64_t bits = 4096;
+    while (bits < 16 * n_literal_edges) bits <<= 1;
+    hs.bloom.assign(bits / 64, 0);
+    const uint64_t mask = bits / 64 - 1;
+    parallel_for(kChunks, [&](uint32_t c) {
+      const uint64_t lo = n_literal_edges * c / kChunks, hi = n_literal_edges * (c + 1) / kChunks;
+      for (uint64_t e = lo; e < hi; e++) {
+        const EdgeEntry &x = staged[e];
+        const uint64_t h = edge_hash(x.parent, Key{x.k0, x.k1});
+        __atomic_fetch_or(&hs.bloom[bloom_word(h, mask)], bloom_bits(h), __ATOMIC_RELAXED);
+      }
+    });
+  }
   auto part_of = [&](uint64_t slot) { return (uint32_t)((unsigned __int128)slot * kParts / n_slots); };
   auto part_lo = [&](uint32_t p) { return (uint64_t)(((unsigned __int128)n_slots * p + kParts - 1) / kParts); };
   pt.mark("e:stage");
@@ -606,6 +624,7 @@ GpuSnapshot::~GpuSnapshot() {
     if (b) (void)hipFree(b);
   if (words) (void)hipFree(words);
   if (nflags) (void)hipFree(nflags);
+  if (bloom) (void)hipFree(bloom);
 }
 
 int upload(std::shared_ptr<const HostSnapshot> hs, int device, hipStream_t stream, std::unique_ptr<GpuSnapshot> *out) {
@@ -640,6 +659,12 @@ int upload(std::shared_ptr<const HostSnapshot> hs, int device, hipStream_t strea
   const uint64_t n_sub_ents = hs->subs.size();
   if (hipMalloc(&g->words, n_sub_ents * 4 + 64) != hipSuccess) return MQM_ENOMEM;
   if (derive_words((const SubEnt *)g->buffers[2], (uint32_t *)g->words, n_sub_ents, stream)) return MQM_EHIP;
+  if (!hs->bloom.empty()) {
+    const size_t bb = hs->bloom.size() * 8;
+    if (hipMalloc(&g->bloom, bb) != hipSuccess) return MQM_ENOMEM;
+    if (hipMemcpyAsync(g->bloom, hs->bloom.data(), bb, hipMemcpyHostToDevice, stream) != hipSuccess) return MQM_EHIP;
+    g->device_bytes += bb;
+  }
   g->device_bytes += n_sub_ents * 4;
   if (ret) {  // node flags, one byte per node, for the reverse walk
     const uint64_t nn = hs->nodes.size();
@@ -670,6 +695,8 @@ int upload(std::shared_ptr<const HostSnapshot> hs, int device, hipStream_t strea
   g->dev.edges = (const EdgeEntry *)g->buffers[1];
   g->dev.subs = (const SubEnt *)g->buffers[2];
   g->dev.words = (const uint32_t *)g->words;
+  g->dev.bloom = (const uint64_t *)g->bloom;
+  g->dev.bloom_mask = g->bloom ? hs->bloom.size() - 1 : 0;
   g->dev.tok_pool = (const uint8_t *)g->buffers[3];
   g->dev.n_buckets = hs->n_buckets;
   g->dev.n_nodes = (uint32_t)hs->nodes.size();

@@ -47,6 +47,7 @@ struct HostSnapshot {
   std::vector<SubInfo> sub_info;     // by non-shared sid
   std::vector<SubInfo> shared_info;  // by shared sid
   std::vector<uint8_t> tok_pool;
+  std::vector<uint64_t> bloom;       // DeviceSnapshot::bloom (empty: none)
   uint64_t n_buckets = 0;
   uint32_t height = 0;
   uint64_t n_edges = 0;
@@ -72,6 +73,7 @@ struct GpuSnapshot {
   void *buffers[kNumBuffers] = {};
   void *words = nullptr;  // DeviceSnapshot::words (derived on the device at upload)
   void *nflags = nullptr; // DeviceRetained::nflags (derived on the device at upload)
+  void *bloom = nullptr;  // DeviceSnapshot::bloom
   DeviceRetained ret{};
   bool has_retained = false;
   uint64_t device_bytes = 0;

@@ -92,4 +92,11 @@ MQM_HD uint64_t edge_hash(uint32_t parent, const Key &k) {
   return h ^ (h >> 29);
 }
 
+// edge-existence filter (DeviceSnapshot::bloom): a blocked Bloom filter, the 3
+// bits of an edge hash in one 64-bit word (bits independent of bucket_of's)
+MQM_HD uint64_t bloom_word(uint64_t h, uint64_t mask) { return (h ^ (h >> 31)) & mask; }
+MQM_HD uint64_t bloom_bits(uint64_t h) {
+  return (1ull << ((h >> 34) & 63)) | (1ull << ((h >> 40) & 63)) | (1ull << ((h >> 46) & 63));
+}
+
 }  // namespace mqm

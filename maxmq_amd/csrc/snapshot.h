@@ -105,6 +105,12 @@ struct DeviceSnapshot {
   const uint32_t *words;  // n_subs: subs[i].word & kPackedMask (the entry's own delivery)
   const uint8_t *tok_pool;
   uint64_t n_buckets;     // edge buckets (kEdgesPerBucket entries each; any count)
+  // literal-edge existence filter, >= 16 bits per edge (64 MB at 10M filters:
+  // it stays in the Infinity Cache), checked before a literal probe: half the
+  // walk's probes are for tokens no edge has (random topic levels under a
+  // node that also has a '+' child), and each would cost a DRAM request
+  const uint64_t *bloom;  // nullptr: no filter
+  uint64_t bloom_mask;    // words - 1 (a power of two)
   uint32_t n_nodes;
   uint32_t n_subs;
   uint32_t n_shared;

@@ -41,6 +41,8 @@ for step in "$@"; do
     prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv \
              -d $OUT/prof -o prof -- python3 $ROOT/bench.py $FAST \
              > $OUT/bench_under_rocprof.json 2> $OUT/rocprof.log) ;;
+    nobloom) MQM_NO_BLOOM=1 timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_nobloom.json \
+             2> $OUT/bench_fast_nobloom.log ;;
     ret) timeout -k 10 600 python3 -u -m pytest tests/test_gpu_retained.py -m gpu -x -v --timeout 300 \
              --timeout-method thread > $OUT/pytest_ret.log 2>&1 ;;
     rev) timeout -k 10 600 python3 -u bench.py --workload reverse --steps 5 --warmup 1 --no-cpu-baseline \
