@@ -309,10 +309,17 @@ def main():
         kms = {k: prof[f"{k}_ms"] / calls for k in ("walk", "dedupe", "total")}
         cpu = None
         stats = None
-        host = host_path(idx, w, args) if args.host_topics and not sharded else None
-        lat = latency(idx, w, args) if args.latency_topics and not sharded else None
+        # per-GPU side measurements at N = 1 only (the contract's cpu_baseline
+        # leg; host path and latency are per-GPU properties too); at N > 1 the
+        # oracle runs only a short sample for the roofline's algorithmic bytes
+        host = host_path(idx, w, args) if args.host_topics and world == 1 else None
+        lat = latency(idx, w, args) if args.latency_topics and world == 1 else None
         if not args.no_cpu_baseline:
-            cpu, stats = cpu_baseline(w, args)
+            if world == 1:
+                cpu, stats = cpu_baseline(w, args)
+            else:
+                short = argparse.Namespace(**dict(vars(args), cpu_seconds=min(args.cpu_seconds, 2.0)))
+                _, stats = cpu_baseline(w, short)
         roof = roofline(stats, n, kms, args.traffic_json)
         out = {
             "metric": "publish topics matched/sec (node) + matched deliveries/sec at 10M filters",

@@ -62,14 +62,15 @@ __device__ inline uint32_t probe_edge(const DeviceSnapshot &s, uint32_t parent, 
 // last entry stay in bounds).  Both kinds issue the same loads unconditionally,
 // so the lanes of a wavefront have them in flight together; only a probe chain
 // that continues past its home slot (rare at the table's load factor) loops.
-__device__ __forceinline__ uint32_t walk_step(const DeviceSnapshot &s, bool do_probe, bool do_desc,
+__device__ __forceinline__ uint32_t walk_step(const DeviceSnapshot &s, bool do_probe, bool do_desc, bool use_bloom,
                                               uint32_t parent, uint32_t wc, uint64_t k0, uint64_t k1,
                                               const uint8_t *tok, uint32_t tok_len, NodeDesc *desc) {
   const Key key{k0, k1};
   const uint64_t nslots = s.n_buckets * kEdgesPerBucket;
   const uint64_t h = do_probe ? edge_hash(parent, key) : 0;
   if (s.bloom) {  // a literal no edge has: no probe (its bucket would be a DRAM request)
-    const uint64_t w = do_probe ? s.bloom[bloom_word(h, s.bloom_mask)] : 0;
+    const bool chk = do_probe && use_bloom;
+    const uint64_t w = chk ? s.bloom[bloom_word(h, s.bloom_mask)] : ~0ull;
     const uint64_t b = bloom_bits(h);
     do_probe = do_probe && (w & b) == b;
   }

@@ -134,7 +134,17 @@ static_assert(kSmallMulti % kWave == 0, "register tiles");
 
 // a load item of the walk: the literal-child probe of a frontier node, or the
 // descriptor load of its '+' / '#' child
-enum : uint32_t { kItemLit = 0, kItemPlus = 1, kItemHash = 2 };
+// kItemLitB: a literal probe checked against the edge-existence filter first.
+// MQM_BLOOM_PLUS_ONLY=1 gives that kind only to nodes with a '+' child (where
+// topic levels drawn for a wildcard make probes miss); other literal probes
+// then skip the filter's round trip
+enum : uint32_t { kItemLit = 0, kItemPlus = 1, kItemHash = 2, kItemLitB = 3 };
+#ifndef MQM_BLOOM_PLUS_ONLY
+#define MQM_BLOOM_PLUS_ONLY 0
+#endif
+__device__ __forceinline__ uint32_t lit_kind(uint32_t plus) {
+  return MQM_BLOOM_PLUS_ONLY && plus == kNone ? kItemLit : kItemLitB;
+}
 
 // topic class (cls): Done = no entries and no shared candidates; Bounded (+
 // FewHits when nh <= kSmallHits, for k_route) = emitted from its record; Dfs
@@ -425,7 +435,7 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
     // level 0's items: the root's literal probe, '+' and '#' children
     if (gl == 0) {
       uint32_t k = 0;
-      if ((root.sh_cnt_flags >> 24) & kFlagHasLiteral) L.item[0][k++] = (0u << 2) | kItemLit;
+      if ((root.sh_cnt_flags >> 24) & kFlagHasLiteral) L.item[0][k++] = (0u << 2) | lit_kind(root.plus);
       if (root.plus != kNone) L.item[0][k++] = (root.plus << 2) | kItemPlus;
       if (root.hash != kNone) L.item[0][k++] = (root.hash << 2) | kItemHash;
     }
@@ -467,16 +477,17 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
         const bool live = it < ni;
         const uint32_t iw = L.item[cur][live ? it : 0];
         const uint32_t kind = iw & 3u, id = iw >> 2;
+        const bool lit = kind == kItemLit || kind == kItemLitB;
         NodeDesc dc;
-        const uint32_t c = walk_step(s, live && kind == kItemLit && !lit_is_wild, live && kind != kItemLit, id, id,
+        const uint32_t c = walk_step(s, live && lit && !lit_is_wild, live && !lit, kind == kItemLitB, id, id,
                                      k0, k1, tp + tst, tln, &dc);
         const bool found = c != kNone;
 #if MQM_WALK_STATS
         {
-          const bool pr = live && kind == kItemLit && !lit_is_wild;
+          const bool pr = live && lit && !lit_is_wild;
           const uint32_t mp = (uint32_t)(__ballot(pr) >> gbase) & kGMask;
           const uint32_t mm = (uint32_t)(__ballot(pr && !found) >> gbase) & kGMask;
-          const uint32_t md = (uint32_t)(__ballot(live && kind != kItemLit) >> gbase) & kGMask;
+          const uint32_t md = (uint32_t)(__ballot(live && !lit) >> gbase) & kGMask;
           if (gl == 0) {
             atomicAdd(&o.ctr->st_probe, (unsigned long long)__popc(mp));
             atomicAdd(&o.ctr->st_miss, (unsigned long long)__popc(mm));
@@ -487,7 +498,7 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
         const uint32_t fl = found ? dc.sh_cnt_flags >> 24 : 0;
         const bool skip_dollar = dollar && (fl & kFlagDollarWild);  // topics.go:527
         const uint32_t c_own = found && !skip_dollar ? dc.sub_cnt : 0;
-        const uint32_t c_par = found && kind == kItemLit && !skip_dollar ? dc.hsub_cnt : 0;  // topics.go:507-509
+        const uint32_t c_par = found && lit && !skip_dollar ? dc.hsub_cnt : 0;  // topics.go:507-509
         const uint32_t c_sh = found ? dc.sh_cnt_flags & kShCntMask : 0;
         const bool push = found && has_next && (fl & kFlagHasChildren);
         const bool leaf = push && (fl & kFlagHashLeaf);
@@ -552,7 +563,7 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
         if (push) {
           uint32_t *nx = &L.item[cur ^ 1][nnext + __popc(m_i0 & gmask_lt) + 2 * __popc(m_i1 & gmask_lt)];
           uint32_t k = 0;
-          if (fl & kFlagHasLiteral) nx[k++] = (c << 2) | kItemLit;
+          if (fl & kFlagHasLiteral) nx[k++] = (c << 2) | lit_kind(dc.plus);
           if (dc.plus != kNone) nx[k++] = (dc.plus << 2) | kItemPlus;
           if (dc.hash != kNone && !leaf) nx[k++] = (dc.hash << 2) | kItemHash;
         }
@@ -636,27 +647,75 @@ __device__ __forceinline__ SubEnt load_sub(const DeviceSnapshot &s, uint32_t sid
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
-// ---- k_desc: solo hits -> copy descriptors ----------------------------------
-// A thread per topic: its solo pairs (off, solo count; the walk listed them
-// apart from the hits) become descriptors at desc_start[t] .., with the
-// running solo prefix as the output position.  Per-topic arrays are read
-// coalesced; a topic with no solo hit reads nothing else.  Also dcount of
-// topics without multi entries (the merges write the others').
+// ---- k_desc: solo parts -> copy descriptors ----------------------------------
+// A wavefront per 64 consecutive topics.  Their descriptors are one contiguous
+// range of desc (desc_start is the exclusive scan of nsolo), so lane k writes
+// descriptor k of the range (coalesced 16-B stores): its topic by a 6-step
+// search over the wave's prefix of solo-part counts in LDS, its output
+// position by a segmented scan of the part sizes (running per-topic position
+// carried in LDS across 64-part steps).  Also dcount of topics without multi
+// entries (the merges write the others').  Round 1 ran a thread per topic:
+// scattered 16-B stores wrote 2.8x the descriptor bytes.
+struct alignas(8) DescLds {
+  unsigned long long run[kWave];  // next output position of each topic's solo part
+  uint32_t pre[kWave + 1];        // exclusive prefix of the topics' solo-part counts
+};
+
 __global__ __launch_bounds__(256) void k_desc(Outputs o, uint32_t n, const uint64_t *__restrict__ desc_start,
                                               uint4 *__restrict__ desc, uint64_t desc_cap) {
-  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
-    const uint8_t cls = o.cls[t];
-    if (!(cls & kClsBounded)) continue;
-    const uint32_t q = o.nsolo[t];
-    if (o.mcount[t] == 0) o.dcount[t] = o.scount[t];
-    if (q == 0) continue;
-    const uint64_t db = o.dstart[t], pb = desc_start[t];
-    const uint2 *pr = reinterpret_cast<const uint2 *>(o.recs + (uint64_t)t * kRecStrideAlloc);
-    uint64_t at = db;
-    for (uint32_t i = 0; i < q; i++) {
-      const uint2 v = pr[i];
-      put_checked(desc, pb + i, desc_cap, make_uint4(v.x, v.y, (uint32_t)at, (uint32_t)(at >> 32)), &o.ctr->oob);
-      at += v.y;
+  __shared__ DescLds lds_all[4];
+  const int lane = threadIdx.x & (kWave - 1);
+  DescLds &L = lds_all[threadIdx.x / kWave];
+  const uint32_t nw = gridDim.x * (blockDim.x / kWave);
+  for (uint32_t w = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave; (uint64_t)w * kWave < n; w += nw) {
+    const uint32_t t0 = w * kWave, t = t0 + lane;
+    uint32_t q = 0;
+    uint64_t db = 0;
+    if (t < n) {
+      const uint8_t cls = o.cls[t];
+      if (cls & kClsBounded) {
+        q = o.nsolo[t];
+        db = o.dstart[t];
+        if (o.mcount[t] == 0) o.dcount[t] = o.scount[t];
+      }
+    }
+    uint32_t inc = q;  // inclusive scan of q over the wave
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const uint32_t v = __shfl_up(inc, d, kWave);
+      if (lane >= d) inc += v;
+    }
+    const uint32_t Q = __shfl(inc, kWave - 1, kWave);
+    if (Q == 0) continue;  // wave-uniform
+    L.pre[lane] = inc - q;
+    if (lane == 0) L.pre[kWave] = Q;
+    L.run[lane] = db;
+    const uint64_t pb = desc_start[t0];
+    wave_lds_sync();
+    for (uint32_t k0 = 0; k0 < Q; k0 += kWave) {
+      const uint32_t k = k0 + lane;
+      const bool valid = k < Q;
+      uint32_t j = 0;  // the topic holding part k: the largest j with pre[j] <= k
+#pragma unroll
+      for (uint32_t step = 32; step > 0; step >>= 1) j = L.pre[j + step] <= k ? j + step : j;  // j + step <= 63
+      uint2 part = make_uint2(0, 0);
+      if (valid) part = *reinterpret_cast<const uint2 *>(o.recs + (uint64_t)(t0 + j) * kRecStrideAlloc + 2 * (k - L.pre[j]));
+      const uint32_t seg = valid ? j : kWave;  // invalid lanes: a segment of their own, size 0
+      uint32_t si = part.y;
+#pragma unroll
+      for (int d = 1; d < kWave; d <<= 1) {
+        const uint32_t v = __shfl_up(si, d, kWave);
+        const uint32_t sj = __shfl_up(seg, d, kWave);
+        if (lane >= d && sj == seg) si += v;
+      }
+      const uint64_t at = valid ? L.run[j] + (si - part.y) : 0;
+      const bool seg_end = __shfl_down(seg, 1, kWave) != seg || lane == kWave - 1;
+      wave_lds_sync();
+      if (valid) {
+        put_checked(desc, pb + k, desc_cap, make_uint4(part.x, part.y, (uint32_t)at, (uint32_t)(at >> 32)), &o.ctr->oob);
+        if (seg_end) L.run[j] += si;
+      }
+      wave_lds_sync();
     }
   }
 }
@@ -971,11 +1030,26 @@ struct alignas(16) MultiLds {
 };
 
 // the block's record of topic t, with prefixes (all threads; ends synced)
-__device__ __forceinline__ void block_record(Outputs o, uint32_t t, uint32_t *rec) {
+// The next topic of a workgroup's list is fetched while the current one is
+// merged (its list entry, segment start and record tail in registers: one
+// 16-B unit per thread), so a topic's record never costs a round trip of
+// its own.
+static_assert(kRecLds / 4 <= kBigThreads, "one record unit per thread");
+struct NextTopic {
+  uint32_t t = 0;
+  uint64_t db = 0;
+  uint4 unit = make_uint4(0, 0, 0, 0);
+  __device__ __forceinline__ void fetch(Outputs o, const uint32_t *list, uint32_t bi, uint32_t nb) {
+    if (bi >= nb) return;
+    t = list[bi];
+    db = o.dstart[t];
+    if (threadIdx.x < (uint32_t)kRecLds / 4) unit = rec_tail(o.recs, t)[-(int)threadIdx.x];
+  }
+};
+
+__device__ __forceinline__ void block_record(const NextTopic &nx, uint32_t *rec) {
   const int tid = threadIdx.x;
-  const uint4 *gt = rec_tail(o.recs, t);
-  for (uint32_t u = tid; u < (uint32_t)kRecLds / 4; u += kBigThreads)
-    reinterpret_cast<uint4 *>(rec)[u] = gt[-(int)u];
+  if (tid < kRecLds / 4) reinterpret_cast<uint4 *>(rec)[tid] = nx.unit;
   __syncthreads();
   const uint32_t nh = rec[0] & 0xFFu;
   __syncthreads();
@@ -1021,10 +1095,13 @@ __global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs
   const MergeTable tb{tkey, tbits, tfirst};
   const int tid = threadIdx.x;
   const uint32_t nb = *count;
+  NextTopic nx;
+  nx.fetch(o, list, blockIdx.x, nb);
   for (uint32_t bi = blockIdx.x; bi < nb; bi += gridDim.x) {
-    const uint32_t t = list[bi];
-    const uint64_t db = o.dstart[t];
-    block_record(o, t, L.rec);
+    const uint32_t t = nx.t;
+    const uint64_t db = nx.db;
+    block_record(nx, L.rec);
+    nx.fetch(o, list, bi + gridDim.x, nb);
     const uint32_t nh = L.rec[0] & 0xFFu, Ss = L.rec[1], M = L.rec[2];
     uint32_t lg = 6;
     while ((1u << lg) < 2 * M && (1u << lg) < (uint32_t)kSlots) lg++;
@@ -1064,10 +1141,13 @@ __global__ __launch_bounds__(kBigThreads) void k_multi_part(DeviceSnapshot s, Ou
   const MergeTable tb{tkey, tbits, tfirst};
   const int tid = threadIdx.x;
   const uint32_t nb = *count;
+  NextTopic nx;
+  nx.fetch(o, list, blockIdx.x, nb);
   for (uint32_t bi = blockIdx.x; bi < nb; bi += gridDim.x) {
-    const uint32_t t = list[bi];
-    const uint64_t db = o.dstart[t];
-    block_record(o, t, L.rec);
+    const uint32_t t = nx.t;
+    const uint64_t db = nx.db;
+    block_record(nx, L.rec);
+    nx.fetch(o, list, bi + gridDim.x, nb);
     const uint32_t nh = L.rec[0] & 0xFFu, Ss = L.rec[1], M = L.rec[2];
     const uint32_t P = (M + kPartCap - 1) / kPartCap;
     uint32_t D = Ss;
@@ -1786,7 +1866,7 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
       }
     }
     hipLaunchKernelGGL(k_desc, dim3(std::min<uint32_t>((n + 255) / 256, 8192)), dim3(256), 0, st, o, n, desc_start,
-                       desc, n_desc);
+                       desc, n_desc);  // a wavefront per 64 topics
     HIP_TRY(hipGetLastError());
     if (hc->n_shlist) {
       hipLaunchKernelGGL(k_shared, dim3(std::min<uint32_t>((hc->n_shlist + 15) / 16, 8192)), dim3(256), 0, st, o,
