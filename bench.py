@@ -602,7 +602,7 @@ def run_reverse(args, dist, rank, world, local, dev):
     the retained topics (BASELINE configs[4]): mqgen config 5's filters (5%
     $SHARE, 20% '+', 5% '#') also subscribed, `--retained` topics retained.
     A step = one mqm_messages_device call over the whole filter batch, inputs
-    resident in HBM (it synchronises per trie level to size the worklists)."""
+    resident in HBM (device-side worklist counters: one read-back per call)."""
     import torch
 
     import maxmq_amd
@@ -656,6 +656,14 @@ def run_reverse(args, dist, rank, world, local, dev):
         # 64-B trie read per (filter, node) step + refs read and written (16 B)
         per_batch = tbytes + 16 * n + 64 * items / steps + 16 * refs_out / steps
         achieved = per_batch / (dt / steps) / 1e9
+        traffic = None  # PMC bytes per call (profiles/traffic_reverse.json, pmc_to_traffic.py --per-call)
+        tj = os.path.join(ROOT, "profiles", "traffic_reverse.json")
+        if os.path.exists(tj):
+            try:
+                with open(tj) as fh:
+                    traffic = json.load(fh).get("hbm_bytes_per_batch")
+            except Exception:
+                traffic = None
         cpu = None
         if not args.no_cpu_baseline:
             cpu = cpu_reverse(w, refs, args)
@@ -680,9 +688,10 @@ def run_reverse(args, dist, rank, world, local, dev):
             "items_per_filter": items / (n * steps),
             "snapshot": snap,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "algorithmic_bytes_per_batch": per_batch,
-                         "kernel": "reverse-match pipeline (wall time incl. per-level host syncs)"},
+                         "kernel": "reverse-match pipeline per batch (k_flt_*, k_level per depth, k_emit_*, "
+                                   "k_task_copy; wall time, one read-back per call)"},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -61,6 +61,9 @@
 #ifndef MQM_WALK_STATS
 #define MQM_WALK_STATS 0
 #endif
+#ifndef MQM_MERGE_BIG_FIRST
+#define MQM_MERGE_BIG_FIRST 0
+#endif
 // MQM_SIDE_PCT: share of the resident grid the merge kernels (side stream)
 // take while the solo copy runs on the main stream with the rest, so the two
 // actually run side by side (persistent grids sized to the whole device ran
@@ -88,7 +91,10 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr int kWalkWaves = 4;            // wavefronts per k_walk block
-constexpr int kLMax = 16;                // levels cached per topic
+#ifndef MQM_WALK_LMAX
+#define MQM_WALK_LMAX 16
+#endif
+constexpr int kLMax = MQM_WALK_LMAX;     // levels cached per topic (deeper topics: DFS path)
 constexpr int kHCap = 64;                // non-shared hits per topic (hit_of: 6 search steps)
 constexpr int kShCap = 16;               // shared hits per topic
 constexpr int kStage = MQM_WALK_STAGE;    // topic bytes staged in LDS (one round trip)
@@ -357,9 +363,9 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
                                                            const uint64_t *__restrict__ toffs, uint32_t n,
                                                            Outputs o) {
   constexpr int kGroups = kWave / kG;
-  constexpr int kLPer = kLMax / kG;  // level keys held per lane
+  constexpr int kLPer = (kLMax + kG - 1) / kG;  // level keys held per lane
   constexpr uint32_t kGMask = (1u << kG) - 1u;
-  static_assert(kLMax % kG == 0, "levels per lane");
+  static_assert(kLMax % kG == 0 || kG > kLMax, "levels per lane");
   __shared__ TopicLds lds_all[kWalkWaves * kGroups];
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / kG, gl = lane & (kG - 1), gbase = g * kG;
@@ -1839,6 +1845,35 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
     hipStream_t ms = st;
     if (merges) {
       if (side && ws.fork(st, &ms)) return -3;
+      // MQM_MERGE_BIG_FIRST=1: the workgroup merges first, the small-topic
+      // merges last (they fill the device better at the end of the stream)
+#if MQM_MERGE_BIG_FIRST
+      if (hc->n_t1) {
+        hipLaunchKernelGGL(k_multi<1024>, grid(k_multi<1024>), dim3(kBigThreads), 0, ms, s, o, lists.l[kLT1],
+                           lcount + kLT1);
+        HIP_TRY(hipGetLastError());
+      }
+      if (hc->n_t2) {
+        hipLaunchKernelGGL(k_multi<2048>, grid(k_multi<2048>), dim3(kBigThreads), 0, ms, s, o, lists.l[kLT2],
+                           lcount + kLT2);
+        HIP_TRY(hipGetLastError());
+      }
+      if (hc->n_part) {
+        hipLaunchKernelGGL(k_multi_part, grid(k_multi_part), dim3(kBigThreads), 0, ms, s, o, lists.l[kLPart],
+                           lcount + kLPart);
+        HIP_TRY(hipGetLastError());
+      }
+      if (hc->n_small) {
+        hipLaunchKernelGGL((k_merge_small<6>), grid(k_merge_small<6>), dim3(kWave * kEmitWaves), 0, ms, s, o,
+                           lists.l[kLSmall], lcount + kLSmall);
+        HIP_TRY(hipGetLastError());
+      }
+      if (hc->n_wmerge) {
+        hipLaunchKernelGGL(k_merge, grid(k_merge), dim3(kWave * kEmitWaves), 0, ms, s, o, lists.l[kLWave],
+                           lcount + kLWave);
+        HIP_TRY(hipGetLastError());
+      }
+#else
       if (hc->n_small) {
         hipLaunchKernelGGL((k_merge_small<6>), grid(k_merge_small<6>), dim3(kWave * kEmitWaves), 0, ms, s, o,
                            lists.l[kLSmall], lcount + kLSmall);
@@ -1864,6 +1899,7 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
                            lcount + kLPart);
         HIP_TRY(hipGetLastError());
       }
+#endif
     }
     hipLaunchKernelGGL(k_desc, dim3(std::min<uint32_t>((n + 255) / 256, 8192)), dim3(256), 0, st, o, n, desc_start,
                        desc, n_desc);  // a wavefront per 64 topics

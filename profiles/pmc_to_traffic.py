@@ -19,8 +19,10 @@ import os
 import re
 import sys
 
-GATHER = ("k_walk", "k_merge_small", "k_merge", "k_multi", "k_multi_part", "k_dfs", "k_shared")
-STREAM = ("k_desc", "k_winmap", "k_wincopy", "k_route", "k_table_sizes")
+GATHER = ("k_walk", "k_merge_small", "k_merge", "k_multi", "k_multi_part", "k_dfs", "k_shared",
+          "k_level")  # (reverse match: k_level walks the trie and the edge index)
+STREAM = ("k_desc", "k_winmap", "k_wincopy", "k_route", "k_table_sizes",
+          "k_flt_count", "k_flt_fill", "k_emit_count", "k_emit_place", "k_task_copy")
 
 
 def kname(s):
@@ -29,20 +31,29 @@ def kname(s):
 
 
 root = sys.argv[1]
+# --last-call: sum every launch of the last call in each pass (the reverse
+# match launches k_level once per trie depth; a call starts with k_flt_count)
+last_call = "--last-call" in sys.argv
 sums = {c: collections.defaultdict(float) for c in ("FETCH_SIZE", "WRITE_SIZE")}
 disp = {c: collections.defaultdict(set) for c in ("FETCH_SIZE", "WRITE_SIZE")}
 for path in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
     with open(path) as fh:
-        for row in csv.DictReader(fh):
-            c = row.get("Counter_Name")
-            k = kname(row.get("Kernel_Name", ""))
-            if c not in sums or k not in GATHER + STREAM:
-                continue
-            sums[c][k] += float(row["Counter_Value"])
-            disp[c][k].add((path, row["Dispatch_Id"]))
+        rows = list(csv.DictReader(fh))
+    cut = 0
+    if last_call:
+        starts = [int(r["Dispatch_Id"]) for r in rows if kname(r.get("Kernel_Name", "")) == "k_flt_count"]
+        cut = max(starts) if starts else 0
+    for row in rows:
+        c = row.get("Counter_Name")
+        k = kname(row.get("Kernel_Name", ""))
+        if c not in sums or k not in GATHER + STREAM or int(row["Dispatch_Id"]) < cut:
+            continue
+        sums[c][k] += float(row["Counter_Value"])
+        disp[c][k].add((path, row["Dispatch_Id"]))
 kib = 1024.0
-reads = {k: v * kib * (1 if k in GATHER else 2) / len(disp["FETCH_SIZE"][k]) for k, v in sums["FETCH_SIZE"].items()}
-writes = {k: v * kib / len(disp["WRITE_SIZE"][k]) for k, v in sums["WRITE_SIZE"].items()}
+div = (lambda c, k: 1) if last_call else (lambda c, k: len(disp[c][k]))
+reads = {k: v * kib * (1 if k in GATHER else 2) / div("FETCH_SIZE", k) for k, v in sums["FETCH_SIZE"].items()}
+writes = {k: v * kib / div("WRITE_SIZE", k) for k, v in sums["WRITE_SIZE"].items()}
 out = {
     "read_bytes_per_batch_by_kernel": reads,
     "write_bytes_per_batch_by_kernel": writes,

@@ -50,6 +50,10 @@ for step in "$@"; do
     revprof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
              -d $OUT/prof_rev -o prof -- python3 $ROOT/bench.py --workload reverse --steps 3 --warmup 1 \
              --no-cpu-baseline > $OUT/rev_under_rocprof.json 2> $OUT/rocprof_rev.log) ;;
+    revpmc) (cd /tmp && export TMPDIR=/tmp && for C in FETCH_SIZE WRITE_SIZE; do
+             timeout -s KILL 600 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/revpmc_$C -o pmc \
+             -- python3 $ROOT/bench.py --workload reverse --steps 2 --warmup 1 --no-cpu-baseline \
+             > $OUT/revpmc_$C.json 2> $OUT/revpmc_$C.log || exit 1; done) ;;
     shim) timeout -k 10 300 python3 -u -m pytest tests/test_gpu_shim.py -m gpu -x -v --timeout 240 \
              --timeout-method thread > $OUT/pytest_shim.log 2>&1 ;;
     calib) (cd /tmp && export TMPDIR=/tmp && for C in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do
