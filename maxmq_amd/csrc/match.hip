@@ -62,7 +62,7 @@
 #define MQM_WALK_STATS 0
 #endif
 #ifndef MQM_MERGE_BIG_FIRST
-#define MQM_MERGE_BIG_FIRST 0
+#define MQM_MERGE_BIG_FIRST 1
 #endif
 // MQM_SIDE_PCT: share of the resident grid the merge kernels (side stream)
 // take while the solo copy runs on the main stream with the rest, so the two

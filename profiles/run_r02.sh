@@ -43,6 +43,10 @@ for step in "$@"; do
              > $OUT/bench_under_rocprof.json 2> $OUT/rocprof.log) ;;
     nobloom) MQM_NO_BLOOM=1 timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_nobloom.json \
              2> $OUT/bench_fast_nobloom.log ;;
+    edgeload) for L in 0.12 0.35; do MQM_EDGE_LOAD=$L timeout -k 10 400 python3 -u bench.py $FAST \
+             > $OUT/bench_fast_load$L.json 2> $OUT/bench_fast_load$L.log || exit 1; done ;;
+    nooverlap) MQM_NO_OVERLAP=1 timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_nooverlap.json \
+             2> $OUT/bench_fast_nooverlap.log ;;
     ret) timeout -k 10 600 python3 -u -m pytest tests/test_gpu_retained.py -m gpu -x -v --timeout 300 \
              --timeout-method thread > $OUT/pytest_ret.log 2>&1 ;;
     rev) timeout -k 10 600 python3 -u bench.py --workload reverse --steps 5 --warmup 1 --no-cpu-baseline \
