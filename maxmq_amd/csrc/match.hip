@@ -280,37 +280,43 @@ __device__ __forceinline__ uint32_t rec_at(const uint32_t *rec, uint32_t h, int 
   return rec[4 + kRecHit * h + field];
 }
 
-// per-topic merge table in LDS (linear probing, key = client + 1): the QoS
-// one-hot | NoLocal of the client's entries OR-folded, and rank << 32 | sid of
-// its first-merged subscription by a 64-bit atomicMin — exactly
-// Subscription.Merge (packets.go:250-270): max QoS, NoLocal OR, every other
-// field from the first subscription in the reference's emission order.  The
-// winners are read off the table afterwards (one delivery per occupied slot).
+// per-topic merge table in LDS (linear probing): kb = (client + 1) << 32 |
+// the QoS one-hot | NoLocal of the client's entries OR-folded, first = rank
+// << 32 | sid of its first-merged subscription by a 64-bit atomicMin —
+// exactly Subscription.Merge (packets.go:250-270): max QoS, NoLocal OR,
+// every other field from the first subscription in the reference's emission
+// order.  A client's first entry claims its slot with key and bits in one
+// 64-bit CAS; only a repeated client pays an OR.  The winners are read off
+// the table afterwards (one delivery per occupied slot).
 struct MergeTable {
-  uint32_t *key, *bits;
-  unsigned long long *first;
+  unsigned long long *kb, *first;
 };
 
 __device__ __forceinline__ void mt_clear(MergeTable t, uint32_t j) {
-  t.key[j] = 0;
-  t.bits[j] = 0;
+  t.kb[j] = 0;
   t.first[j] = ~0ull;
 }
+
+__device__ __forceinline__ bool mt_occupied(MergeTable t, uint32_t j) { return t.kb[j] != 0; }
 
 __device__ __forceinline__ void mt_insert(MergeTable t, uint32_t mask, uint32_t lg, uint32_t client, uint32_t word,
                                           uint32_t rank) {
   uint32_t sl = table_slot(client, lg);
+  const unsigned long long key = (unsigned long long)(client + 1u) << 32, kb = key | qos_bits(word);
   for (;;) {
-    const uint32_t prev = atomicCAS(&t.key[sl], 0u, client + 1);
-    if (prev == 0 || prev == client + 1) break;
+    const unsigned long long prev = atomicCAS(&t.kb[sl], 0ull, kb);
+    if (prev == 0) break;
+    if ((prev >> 32) == (key >> 32)) {
+      if ((prev | kb) != prev) atomicOr(&t.kb[sl], kb);
+      break;
+    }
     sl = (sl + 1) & mask;
   }
-  atomicOr(&t.bits[sl], qos_bits(word));
   atomicMin(&t.first[sl], ((unsigned long long)rank << 32) | (word & kWordSidMask));
 }
 
 __device__ __forceinline__ uint32_t mt_delivery(MergeTable t, uint32_t j) {
-  const uint32_t v = t.bits[j];
+  const uint32_t v = (uint32_t)t.kb[j];
   return pack_delivery((uint32_t)t.first[j] & kWordSidMask, 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
 }
 
@@ -876,7 +882,7 @@ __device__ __forceinline__ uint32_t merge_multi(MergeTable tb, uint32_t kSlots, 
   wave_lds_sync();
   for (uint32_t j0 = 0; j0 <= mask; j0 += kE) {  // one delivery per occupied slot, slot order
     const uint32_t j = j0 + gl;
-    const bool occ = j <= mask && tb.key[j] != 0;
+    const bool occ = j <= mask && mt_occupied(tb, j);
     const uint64_t m = (__ballot(occ) >> gbase) & kGMask;
     if (occ) put_checked(out, db + D + __popcll(m & glt), cap, mt_delivery(tb, j), oob);
     D += __popcll(m);
@@ -898,9 +904,8 @@ static_assert(4 + kRecHit * kSmallHits <= 64 && kSRecPer % 4 == 0, "small-class 
 constexpr int kSmallTab = 32;  // k_merge_small table slots (<= kSmallMultiS entries: load <= 0.75)
 static_assert(kSmallMultiS * 4 <= kSmallTab * 3, "k_merge_small table load factor");
 struct alignas(8) SmallLds {
-  unsigned long long tfirst[kSmallTab];
+  unsigned long long tfirst[kSmallTab], tkb[kSmallTab];
   uint32_t rec[64];
-  uint32_t tkey[kSmallTab], tbits[kSmallTab];
   uint32_t pad[2];  // 194-dword stride: the 8 groups' contexts start 2 banks apart
 };
 static_assert(sizeof(SmallLds) % 256 == 8, "bank-skewed group contexts");
@@ -953,7 +958,7 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
       mcl[k] = e.client;
       mw[k] = e.word;
     }
-    const uint32_t D = merge_multi<kSE, kMPer>(MergeTable{L.tkey, L.tbits, L.tfirst}, kSmallTab, mcl, mw, mrk, M, gl,
+    const uint32_t D = merge_multi<kSE, kMPer>(MergeTable{L.tkb, L.tfirst}, kSmallTab, mcl, mw, mrk, M, gl,
                                                gbase, o.dout, db, Ss, o.dcap, &o.ctr->oob);
     if (gl == 0) o.dcount[t] = D;
     wave_lds_sync();
@@ -963,9 +968,8 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
 // ---- k_merge: a wavefront per topic with kSmallMultiS < Ms <= kSmallMulti (or
 // more than kSmallHits hits) ----------------------------------------------------
 struct alignas(16) MergeLds {
-  unsigned long long tfirst[kSmallSlots];
+  unsigned long long tfirst[kSmallSlots], tkb[kSmallSlots];
   uint32_t rec[kRecLds];
-  uint32_t tkey[kSmallSlots], tbits[kSmallSlots];
 };
 
 __global__ __launch_bounds__(kWave *kEmitWaves) void k_merge(DeviceSnapshot s, Outputs o,
@@ -1011,7 +1015,7 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_merge(DeviceSnapshot s, O
       mw[k] = e.word;
     }
     const uint32_t D =
-        merge_multi<kWave, kMPer>(MergeTable{L.tkey, L.tbits, L.tfirst}, kSmallSlots, mcl, mw, mrk, M, lane, 0,
+        merge_multi<kWave, kMPer>(MergeTable{L.tkb, L.tfirst}, kSmallSlots, mcl, mw, mrk, M, lane, 0,
                                   o.dout, db, Ss, o.dcap, &o.ctr->oob);
     if (lane == 0) o.dcount[t] = D;
     wave_lds_sync();
@@ -1072,7 +1076,7 @@ __device__ __forceinline__ uint32_t block_winners(MergeTable tb, uint32_t nslots
   uint32_t c = 0;
   for (uint32_t j0 = lo; j0 < hi; j0 += kWave) {
     const uint32_t j = j0 + lane;
-    c += __popcll(__ballot(j < hi && tb.key[j] != 0));
+    c += __popcll(__ballot(j < hi && mt_occupied(tb, j)));
   }
   if (lane == 0) wsum[wid] = c;
   __syncthreads();
@@ -1083,7 +1087,7 @@ __device__ __forceinline__ uint32_t block_winners(MergeTable tb, uint32_t nslots
   }
   for (uint32_t j0 = lo; j0 < hi; j0 += kWave) {
     const uint32_t j = j0 + lane;
-    const bool occ = j < hi && tb.key[j] != 0;
+    const bool occ = j < hi && mt_occupied(tb, j);
     const uint64_t m = __ballot(occ);
     if (occ) put_checked(o.dout, db + w + __popcll(m & lanemask_lt(lane)), o.dcap, mt_delivery(tb, j), &o.ctr->oob);
     w += __popcll(m);
@@ -1095,10 +1099,9 @@ __device__ __forceinline__ uint32_t block_winners(MergeTable tb, uint32_t nslots
 template <int kSlots>
 __global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs o, const uint32_t *__restrict__ list,
                                                       const unsigned int *__restrict__ count) {
-  __shared__ unsigned long long tfirst[kSlots];
-  __shared__ uint32_t tkey[kSlots], tbits[kSlots];
+  __shared__ unsigned long long tfirst[kSlots], tkb[kSlots];
   __shared__ MultiLds L;
-  const MergeTable tb{tkey, tbits, tfirst};
+  const MergeTable tb{tkb, tfirst};
   const int tid = threadIdx.x;
   const uint32_t nb = *count;
   NextTopic nx;
@@ -1140,11 +1143,10 @@ __global__ __launch_bounds__(kBigThreads) void k_multi_part(DeviceSnapshot s, Ou
                                                            const uint32_t *__restrict__ list,
                                                            const unsigned int *__restrict__ count) {
   constexpr uint32_t kSlots = 4096, kFill = kSlots * 7 / 8;
-  __shared__ unsigned long long tfirst[kSlots];
-  __shared__ uint32_t tkey[kSlots], tbits[kSlots];
+  __shared__ unsigned long long tfirst[kSlots], tkb[kSlots];
   __shared__ MultiLds L;
   __shared__ uint32_t fill;
-  const MergeTable tb{tkey, tbits, tfirst};
+  const MergeTable tb{tkb, tfirst};
   const int tid = threadIdx.x;
   const uint32_t nb = *count;
   NextTopic nx;
