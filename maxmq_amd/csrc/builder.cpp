@@ -2,9 +2,11 @@
 // builder (see builder.h).
 #include "builder.h"
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <new>
+#include <thread>
 
 #include "../../include/mqmatch.h"
 
@@ -250,10 +252,32 @@ struct Digest {
 };
 }  // namespace
 
+uint64_t edges_digest_of(const HostSnapshot &hs) {
+  constexpr uint64_t kChunks = 64;
+  const uint64_t n = hs.edges.size();
+  std::vector<uint64_t> part(kChunks, 0);
+  std::vector<std::thread> th;
+  const uint32_t nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  for (uint32_t w = 0; w < nt; w++)
+    th.emplace_back([&, w] {
+      for (uint64_t c = w; c < kChunks; c += nt) {
+        const uint64_t lo = n * c / kChunks, hi = n * (c + 1) / kChunks;
+        Digest d;
+        d.add(hs.edges.data() + lo, (hi - lo) * sizeof(EdgeEntry));
+        part[c] = d.h;
+      }
+    });
+  for (auto &x : th) x.join();
+  Digest d;
+  for (uint64_t v : part) d.mix(v);
+  d.mix(n);
+  return d.h;
+}
+
 uint64_t snapshot_digest(const HostSnapshot &hs) {
   Digest d;
   d.vec(hs.nodes);
-  d.vec(hs.edges);
+  d.mix(hs.edges.empty() ? hs.edges_digest : edges_digest_of(hs));
   d.vec(hs.subs);
   d.vec(hs.sub_info);
   d.vec(hs.shared_info);

@@ -117,5 +117,8 @@ class Builder {
 
 // 64-bit digest of a snapshot's arrays (replicas / shards compare it)
 uint64_t snapshot_digest(const HostSnapshot &hs);
+// digest of the edge table (64 fixed chunks hashed in parallel, combined in
+// order); snapshot_digest uses the kept value once the host copy is released
+uint64_t edges_digest_of(const HostSnapshot &hs);
 
 }  // namespace mqm

@@ -5,6 +5,7 @@
 // (vendor/.../mqtt/v2/topics.go:503) — so rank = 2*node+slot orders hits
 // exactly as the reference walk emits them (snapshot.h).
 #include "flatten.h"
+#include "builder.h"
 #include "match.h"
 
 #include <hip/hip_runtime.h>
@@ -630,7 +631,7 @@ GpuSnapshot::~GpuSnapshot() {
   if (bloom) (void)hipFree(bloom);
 }
 
-int upload(std::shared_ptr<const HostSnapshot> hs, int device, hipStream_t stream, std::unique_ptr<GpuSnapshot> *out) {
+int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std::unique_ptr<GpuSnapshot> *out) {
   auto g = std::make_unique<GpuSnapshot>();
   if (device < 0) {  // host-only index: no device copy
     g->host = std::move(hs);
@@ -676,6 +677,9 @@ int upload(std::shared_ptr<const HostSnapshot> hs, int device, hipStream_t strea
     g->device_bytes += nn;
   }
   if (hipStreamSynchronize(stream) != hipSuccess) return MQM_EHIP;
+  // the device holds the edge table now: keep its digest, release the host copy
+  hs->edges_digest = edges_digest_of(*hs);
+  decltype(hs->edges)().swap(hs->edges);
   if (ret) {
     g->has_retained = true;
     g->ret.nflags = (const uint8_t *)g->nflags;

@@ -42,7 +42,8 @@ struct SubInfo {
 
 struct HostSnapshot {
   std::vector<NodeDesc> nodes;
-  std::vector<EdgeEntry, NoInitAlloc<EdgeEntry>> edges;  // n_buckets * kEdgesPerBucket
+  std::vector<EdgeEntry, NoInitAlloc<EdgeEntry>> edges;  // n_buckets * kEdgesPerBucket (empty after upload)
+  uint64_t edges_digest = 0;  // edges_digest_of(edges), kept when the host copy is released
   std::vector<SubEnt> subs;
   std::vector<SubInfo> sub_info;     // by non-shared sid
   std::vector<SubInfo> shared_info;  // by shared sid
@@ -83,6 +84,8 @@ struct GpuSnapshot {
 // Copies on `stream` and waits for them (nullptr: the null stream).  device < 0
 // (MQM_DEVICE_NONE) wraps the host snapshot without device buffers, so a
 // host-only index still has stats and a digest.
-int upload(std::shared_ptr<const HostSnapshot> hs, int device, hipStream_t stream, std::unique_ptr<GpuSnapshot> *out);
+// The host copy of the edge table (the snapshot's largest array: 18.5 GB at
+// config 3) is released once it is on the device; its digest is kept.
+int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std::unique_ptr<GpuSnapshot> *out);
 
 }  // namespace mqm
