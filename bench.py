@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU baseline threads (0 = one per CPU this process may run on, BASELINE.md §2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--host-topics", type=int, default=1000000,
+    ap.add_argument("--host-topics", type=int, default=500000,
                     help="PCIe-inclusive host path (mqm_match_batch): topics per call, outside the timed region; 0 = skip")
     ap.add_argument("--host-threads", type=int, default=4,
                     help="host path: concurrent callers (each its own stream), batches overlapped across them")
@@ -395,8 +395,14 @@ def host_path(idx, w, args):
         L.mqm_result_free(res)
         return d
 
-    for t in range(args.host_threads):  # warm every context (workspace sizing, pinned blocks)
-        call(t % nb)
+    # warm every caller's context (workspace sizing, pinned result blocks):
+    # contexts come from a pool, so only concurrent calls create one each
+    for _ in range(2):
+        warm = [threading.Thread(target=call, args=(t % nb,)) for t in range(args.host_threads)]
+        for th in warm:
+            th.start()
+        for th in warm:
+            th.join()
     done = [0, 0]
     lock = threading.Lock()
     nxt = [0]

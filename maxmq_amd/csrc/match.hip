@@ -64,6 +64,12 @@
 #ifndef MQM_MERGE_BIG_FIRST
 #define MQM_MERGE_BIG_FIRST 1
 #endif
+// MQM_WALK_SORT=1: the walk visits topics grouped by length (a proxy for
+// depth, longest first) through a permutation, so the 16 topics of a
+// wavefront walk similar numbers of levels (lockstep waste: VALU lane use 0.47)
+#ifndef MQM_WALK_SORT
+#define MQM_WALK_SORT 0
+#endif
 // MQM_SIDE_PCT: share of the resident grid the merge kernels (side stream)
 // take while the solo copy runs on the main stream with the rest, so the two
 // actually run side by side (persistent grids sized to the whole device ran
@@ -184,6 +190,7 @@ struct Outputs {
   uint8_t *cls;
   uint32_t *dfs_list;
   uint32_t *recs;  // kRecStrideAlloc words per topic
+  const uint32_t *perm;  // k_walk's visiting order (nullptr: topic order)
   Counters *ctr;
   uint32_t *dout;  // packed deliveries (snapshot.h)
   uint32_t *hout;
@@ -382,18 +389,21 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
 
   uint64_t tb = ((uint64_t)blockIdx.x * kWalkWaves + threadIdx.x / kWave) * kGroups;
   uint64_t nx_off = 0, nx_end = 0;  // the next topic's byte range, one topic ahead
+  uint32_t nx_t = 0;
   if (tb + g < n) {
-    nx_off = toffs[tb + g];
-    nx_end = toffs[tb + g + 1];
+    nx_t = o.perm ? o.perm[tb + g] : (uint32_t)(tb + g);
+    nx_off = toffs[nx_t];
+    nx_end = toffs[nx_t + 1];
   }
   for (; tb < n; tb += stride) {
-    const uint32_t t = (uint32_t)(tb + g);
-    const bool active = t < n;
+    const bool active = tb + g < n;
+    const uint32_t t = active ? nx_t : (uint32_t)n;  // (inactive lanes never use t)
     const uint32_t len = active ? (uint32_t)(nx_end - nx_off) : 0;
     const uint8_t *tp = tbytes + (active ? nx_off : 0);
     if (tb + stride + g < n) {
-      nx_off = toffs[tb + stride + g];
-      nx_end = toffs[tb + stride + g + 1];
+      nx_t = o.perm ? o.perm[tb + stride + g] : (uint32_t)(tb + stride + g);
+      nx_off = toffs[nx_t];
+      nx_end = toffs[nx_t + 1];
     }
     uint32_t why = kNoWhy;
 
@@ -617,6 +627,54 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
     wave_lds_sync();
   }
 }
+
+// ---- walk visiting order (MQM_WALK_SORT): topics by length bucket --------------
+#if MQM_WALK_SORT
+constexpr int kLenBins = 32;
+__device__ __forceinline__ uint32_t len_bin(const uint64_t *toffs, uint32_t t) {
+  const uint64_t len = toffs[t + 1] - toffs[t];
+  return kLenBins - 1 - (uint32_t)min<uint64_t>(len >> 3, kLenBins - 1);  // longest first
+}
+
+__global__ __launch_bounds__(256) void k_len_hist(const uint64_t *__restrict__ toffs, uint32_t n,
+                                                  unsigned int *__restrict__ bins) {
+  __shared__ unsigned int c[kLenBins];
+  if (threadIdx.x < kLenBins) c[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x)
+    atomicAdd(&c[len_bin(toffs, t)], 1u);
+  __syncthreads();
+  if (threadIdx.x < kLenBins && c[threadIdx.x]) atomicAdd(&bins[threadIdx.x], c[threadIdx.x]);
+}
+
+__global__ void k_len_prefix(unsigned int *bins) {  // one wavefront: counts -> exclusive starts
+  const int lane = threadIdx.x;
+  const unsigned int v = lane < kLenBins ? bins[lane] : 0;
+  unsigned int inc = v;
+  for (int d = 1; d < kLenBins; d <<= 1) {
+    const unsigned int u = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += u;
+  }
+  if (lane < kLenBins) bins[lane] = inc - v;
+}
+
+__global__ __launch_bounds__(256) void k_len_scatter(const uint64_t *__restrict__ toffs, uint32_t n,
+                                                     unsigned int *__restrict__ cursor, uint32_t *__restrict__ perm) {
+  __shared__ unsigned int c[kLenBins], base[kLenBins];
+  for (uint32_t t0 = blockIdx.x * blockDim.x; t0 < n; t0 += gridDim.x * blockDim.x) {
+    if (threadIdx.x < kLenBins) c[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t t = t0 + threadIdx.x;
+    const uint32_t b = t < n ? len_bin(toffs, t) : 0;
+    const unsigned int r = t < n ? atomicAdd(&c[b], 1u) : 0;
+    __syncthreads();
+    if (threadIdx.x < kLenBins && c[threadIdx.x]) base[threadIdx.x] = atomicAdd(&cursor[threadIdx.x], c[threadIdx.x]);
+    __syncthreads();
+    if (t < n) perm[base[b] + r] = t;
+    __syncthreads();
+  }
+}
+#endif
 
 // ---------------------------------------------------------------------------
 // Emission.  A topic's deliveries are written at dstart[t] (the exclusive scan
@@ -1736,6 +1794,21 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   const int walk_g = ws.walk_lanes;
   HIP_TRY(hipMemsetAsync(o.ctr, 0, sizeof(Counters), st));
   mark(ws, 0, st);
+  o.perm = nullptr;
+#if MQM_WALK_SORT
+  if (n > 0) {
+    if (ws.get(W::kPerm, sizeof(uint32_t) * (n + 1)) || ws.get(W::kPermBins, sizeof(unsigned int) * kLenBins))
+      return -2;
+    auto *bins = (unsigned int *)ws.ptr(W::kPermBins);
+    HIP_TRY(hipMemsetAsync(bins, 0, sizeof(unsigned int) * kLenBins, st));
+    const uint32_t gb = std::min<uint32_t>((n + 255) / 256, 2048);
+    hipLaunchKernelGGL(k_len_hist, dim3(gb), dim3(256), 0, st, d_offs, n, bins);
+    hipLaunchKernelGGL(k_len_prefix, dim3(1), dim3(64), 0, st, bins);
+    hipLaunchKernelGGL(k_len_scatter, dim3(gb), dim3(256), 0, st, d_offs, n, bins, (uint32_t *)ws.ptr(W::kPerm));
+    HIP_TRY(hipGetLastError());
+    o.perm = (const uint32_t *)ws.ptr(W::kPerm);
+  }
+#endif
   if (n > 0) {
     auto launch_walk = [&](auto kern, int g) {
       const uint32_t per_block = kWalkWaves * (kWave / g);
