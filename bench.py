@@ -60,6 +60,9 @@ def parse():
                     help="host path: concurrent callers (each its own stream), batches overlapped across them")
     ap.add_argument("--latency-topics", type=int, default=2000,
                     help="single-topic mqm_subscribers calls timed for the per-publish latency; 0 = skip")
+    ap.add_argument("--conc-threads", type=int, default=16,
+                    help="latency leg: concurrent single-topic callers (direct, then batched)")
+    ap.add_argument("--conc-calls", type=int, default=300, help="latency leg: calls per concurrent caller")
     ap.add_argument("--workload", choices=["forward", "reverse", "churn"], default="forward",
                     help="forward: Subscribers (headline); reverse: Messages over retained topics (config 5); "
                          "churn: Subscribe/Unsubscribe at rate with background snapshot rebuilds")
@@ -472,8 +475,55 @@ def latency(idx, w, args):
         if i >= 50:
             ts.append(dt)
     ts = np.array(ts) * 1e6
-    return {"unit": "us", "calls": len(ts), "p50": float(np.median(ts)), "p90": float(np.percentile(ts, 90)),
-            "p99": float(np.percentile(ts, 99)), "mean": float(ts.mean())}
+    out = {"unit": "us", "calls": len(ts), "p50": float(np.median(ts)), "p90": float(np.percentile(ts, 90)),
+           "p99": float(np.percentile(ts, 99)), "mean": float(ts.mean())}
+    out["concurrent"] = concurrent_single_topic(idx, topics, args)
+    return out
+
+
+def concurrent_single_topic(idx, topics, args):
+    """--conc-threads callers each issuing single-topic mqm_subscribers calls
+    (one goroutine per connection, listeners/tcp.go:83): every call its own
+    pipeline, then with the MQM_CFG_BATCHING collector gathering concurrent
+    calls into GPU batches.  Topics/s over all callers and per-call latency."""
+    import ctypes as C
+    import threading
+
+    from maxmq_amd import capi
+
+    L = capi.lib()
+    T, per = args.conc_threads, args.conc_calls
+
+    def run():
+        lat = [[] for _ in range(T)]
+
+        def worker(k):
+            for j in range(per):
+                t = topics[(k * per + j) % len(topics)]
+                res = C.c_void_p()
+                t0 = time.perf_counter()
+                capi.check("mqm_subscribers", L.mqm_subscribers(idx._h, t, len(t), C.byref(res)))
+                lat[k].append(time.perf_counter() - t0)
+                L.mqm_result_free(res)
+
+        ths = [threading.Thread(target=worker, args=(k,)) for k in range(T)]
+        t0 = time.perf_counter()
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        dt = time.perf_counter() - t0
+        a = np.concatenate([np.array(x) for x in lat]) * 1e6
+        return {"topics_per_s": T * per / dt, "p50_us": float(np.median(a)), "p99_us": float(np.percentile(a, 99))}
+
+    out = {"threads": T, "calls_per_thread": per, "direct": run()}
+    idx.batching_policy(0, 0)  # MQM_CFG_BATCHING on from here
+    run()  # warm the collector's contexts
+    b0, t0_ = idx.batching_stats()
+    out["batched"] = run()
+    b1, t1 = idx.batching_stats()
+    out["batched"]["mean_batch"] = (t1 - t0_) / max(1, b1 - b0)
+    return out
 
 
 def run_sweep(args, idx, step, dev, rank):

@@ -60,6 +60,13 @@ extern "C" {
  * publish a finished back buffer at their start (no wait).  mqm_commit keeps
  * its synchronous meaning (submit, wait, publish).  See mqm_commit_async. */
 #define MQM_CFG_ASYNC_COMMIT 4u
+/* MQM_CFG_BATCHING: mqm_subscribers calls from concurrent threads (the
+ * reference's one-goroutine-per-connection Subscribers(topic) calls,
+ * listeners/tcp.go:83, server.go:776) are gathered by a collector thread into
+ * one mqm_match_batch; each caller gets its own single-topic result.  Calls
+ * arriving while a batch runs form the next batch (no added latency when
+ * idle; mqm_batching_policy can add a linger).  Results are identical. */
+#define MQM_CFG_BATCHING 8u
 /* device value for a host-only index: the store and its mutation API work,
  * mqm_commit / mqm_match_* return MQM_ENODEV (there is no CPU match path). */
 #define MQM_DEVICE_NONE (-1)
@@ -223,8 +230,18 @@ int mqm_debug_fault(mqm_index *h, int stage, int count);
 /* Host in / host out.  Topic i is bytes[offsets[i] .. offsets[i+1]). */
 int mqm_match_batch(mqm_index *h, const char *topic_bytes, const uint64_t *topic_offsets, uint32_t n_topics,
                     mqm_result **out);
-/* single-topic convenience == Subscribers(topic) */
+/* single-topic convenience == Subscribers(topic) (batched across concurrent
+ * callers with MQM_CFG_BATCHING) */
 int mqm_subscribers(mqm_index *h, const char *topic, size_t topic_len, mqm_result **out);
+/* MQM_CFG_BATCHING: at most max_batch topics per gathered batch (0 = 8192),
+ * and how long the collector waits for more after the first (microseconds,
+ * default 0); on an index created without the flag it turns batching on.
+ * Statistics: batches run and topics they carried (MQM_EINVAL while batching
+ * is off).  Both MQM_EINVAL on a host-only index.  Call the policy before the
+ * index is shared between threads (mqm_subscribers reads the collector
+ * pointer without a lock). */
+int mqm_batching_policy(mqm_index *h, uint32_t max_batch, uint32_t linger_us);
+int mqm_batching_stats(mqm_index *h, uint64_t *batches, uint64_t *topics);
 /* Device in / device out on `hip_stream` (hipStream_t, NULL = default stream). */
 int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t *d_topic_offsets,
                      uint32_t n_topics, void *hip_stream, mqm_device_result *out);

@@ -194,20 +194,32 @@ class TopicsIndex:
     """TopicsIndex (topics.go:285) backed by the MI355X matcher."""
 
     def __init__(self, device: int | None = 0, autocommit: bool = True, identifiers: bool = False,
-                 async_commit: bool = False):
+                 async_commit: bool = False, batching: bool = False):
         """identifiers=True: match_batch / subscribers also return the full
         Subscription.Identifiers maps (an extra GPU pass per batch).
         async_commit=True: mutations are logged and snapshots are rebuilt by a
-        background builder (commit_async / commit_poll / commit_policy)."""
+        background builder (commit_async / commit_poll / commit_policy).
+        batching=True: concurrent subscribers() calls are gathered into GPU
+        batches by a collector thread (MQM_CFG_BATCHING)."""
         L = lib()
         cfg = capi.Config(capi.MQM_DEVICE_NONE if device is None else device,
                           (capi.MQM_CFG_AUTOCOMMIT if autocommit else 0) |
                           (capi.MQM_CFG_IDENTIFIERS if identifiers else 0) |
-                          (capi.MQM_CFG_ASYNC_COMMIT if async_commit else 0))
+                          (capi.MQM_CFG_ASYNC_COMMIT if async_commit else 0) |
+                          (capi.MQM_CFG_BATCHING if batching else 0))
         h = C.c_void_p()
         check("mqm_create", L.mqm_create(C.byref(cfg), C.byref(h)))
         self._h = h
         self.device = device
+
+    def batching_policy(self, max_batch: int = 0, linger_us: int = 0):
+        check("mqm_batching_policy", lib().mqm_batching_policy(self._h, max_batch, linger_us))
+
+    def batching_stats(self):
+        """(batches run, topics they carried) of the MQM_CFG_BATCHING collector"""
+        b, t = C.c_uint64(), C.c_uint64()
+        check("mqm_batching_stats", lib().mqm_batching_stats(self._h, C.byref(b), C.byref(t)))
+        return b.value, t.value
 
     def close(self):
         if getattr(self, "_h", None):

@@ -26,6 +26,7 @@ MQM_ENODEV = -5
 MQM_CFG_AUTOCOMMIT = 1
 MQM_CFG_IDENTIFIERS = 2
 MQM_CFG_ASYNC_COMMIT = 4
+MQM_CFG_BATCHING = 8
 MQM_DEVICE_NONE = -1
 
 ERRORS = {MQM_EINVAL: "EINVAL", MQM_ENOMEM: "ENOMEM", MQM_EHIP: "EHIP", MQM_ELIMIT: "ELIMIT",
@@ -35,6 +36,7 @@ ERRORS = {MQM_EINVAL: "EINVAL", MQM_ENOMEM: "ENOMEM", MQM_EHIP: "EHIP", MQM_ELIM
 EXPORTED = [
     "mqm_create", "mqm_destroy", "mqm_subscribe", "mqm_subscribe_many", "mqm_unsubscribe",
     "mqm_retain_message", "mqm_retained_len", "mqm_commit", "mqm_match_batch", "mqm_subscribers",
+    "mqm_batching_policy", "mqm_batching_stats",
     "mqm_match_device", "mqm_result_num_topics", "mqm_result_offsets", "mqm_result_deliveries",
     "mqm_result_shared_offsets", "mqm_result_shared", "mqm_result_sub_info", "mqm_result_shared_info",
     "mqm_result_sub_infos", "mqm_result_free", "mqm_client_name", "mqm_filter_name", "mqm_num_clients", "mqm_is_valid_filter",
@@ -150,6 +152,8 @@ def lib():
         "mqm_commit": ([vp], C.c_int),
         "mqm_match_batch": ([vp, vp, vp, u32, C.POINTER(vp)], C.c_int),
         "mqm_subscribers": ([vp, cp, sz, C.POINTER(vp)], C.c_int),
+        "mqm_batching_policy": ([vp, u32, u32], C.c_int),
+        "mqm_batching_stats": ([vp, C.POINTER(u64), C.POINTER(u64)], C.c_int),
         "mqm_match_device": ([vp, vp, vp, u32, vp, C.POINTER(DeviceResult)], C.c_int),
         "mqm_result_num_topics": ([vp], u32),
         "mqm_result_offsets": ([vp], vp),

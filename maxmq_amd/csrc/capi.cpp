@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -27,6 +28,7 @@
 #include <mutex>
 #include <new>
 #include <string_view>
+#include <thread>
 #include <vector>
 
 #include "../../include/mqmatch.h"
@@ -107,6 +109,10 @@ struct MatchCtx {
 
 }  // namespace
 
+namespace {
+struct Collector;
+}
+
 struct mqm_index {
   mqm_config cfg{};
   std::mutex mu;  // store, journal, builder, front buffer
@@ -132,9 +138,10 @@ struct mqm_index {
   std::mutex pool_mu;
   std::vector<std::unique_ptr<MatchCtx>> pool;
   std::shared_ptr<PinnedPool> pinned = std::make_shared<PinnedPool>();
-  ~mqm_index() {
-    pool.clear();
-  }
+  // MQM_CFG_BATCHING: declared last, so it stops (joins its thread) before
+  // anything it uses is destroyed
+  std::unique_ptr<Collector> collector;
+  ~mqm_index();
 };
 
 struct mqm_messages {
@@ -382,6 +389,7 @@ int mqm_create(const mqm_config *cfg, mqm_index **out) {
     }
     if (const char *e = getenv("MQM_NO_OVERLAP")) h->overlap = atoi(e) == 0;
     if (ctx_init(h.get(), &h->dev) != MQM_OK) return MQM_EHIP;
+    if (h->cfg.flags & MQM_CFG_BATCHING) h->collector = std::make_unique<Collector>(h.get());
     *out = h.release();
     return MQM_OK;
   });
@@ -863,9 +871,181 @@ const uint64_t *mqm_messages_offsets(const mqm_messages *m) { return m ? m->offs
 const uint64_t *mqm_messages_refs(const mqm_messages *m) { return m ? m->refs.data() : nullptr; }
 void mqm_messages_free(mqm_messages *m) { delete m; }
 
+namespace {
+
+// MQM_CFG_BATCHING: single-topic calls queue a request and wait; one thread
+// drains the queue into mqm_match_batch and hands every caller its own
+// single-topic result (a pinned block from the index's pool, split off the
+// batch result).  Calls that arrive while a batch runs form the next one, so
+// batches grow with the offered load and an idle index adds no latency.
+struct Collector {
+  struct Req {
+    const char *topic;
+    size_t len;
+    mqm_result *res = nullptr;
+    int rc = MQM_OK;
+    bool done = false;
+  };
+  mqm_index *h;
+  std::mutex mu;
+  std::condition_variable cv, cv_done;
+  std::vector<Req *> q;
+  bool stop = false;
+  uint32_t max_batch = 8192, linger_us = 0;
+  uint64_t batches = 0, topics = 0;
+  std::thread th;
+
+  explicit Collector(mqm_index *idx) : h(idx), th([this] { run(); }) {}
+  ~Collector() {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      stop = true;
+    }
+    cv.notify_all();
+    th.join();
+  }
+
+  int submit(const char *topic, size_t len, mqm_result **out) {
+    Req r{topic ? topic : "", len};
+    {
+      std::lock_guard<std::mutex> g(mu);
+      q.push_back(&r);
+    }
+    cv.notify_one();
+    std::unique_lock<std::mutex> lk(mu);
+    cv_done.wait(lk, [&] { return r.done; });
+    *out = r.res;
+    return r.rc;
+  }
+
+  // topic i of batch result b as a result of its own
+  static int split(mqm_index *h, const mqm_result *b, uint32_t i, mqm_result **out) {
+    auto r = std::make_unique<mqm_result>();
+    const uint64_t d0 = b->offsets[i], d = b->offsets[i + 1] - d0;
+    const uint64_t s0 = b->shared_offsets[i], sn = b->shared_offsets[i + 1] - s0;
+    const uint64_t i0 = b->has_idents ? b->ident_offsets[i] : 0, in = b->has_idents ? b->ident_offsets[i + 1] - i0 : 0;
+    auto up = [](uint64_t x) { return (x + 15) & ~15ull; };
+    const uint64_t o_sh = 16, o_io = 32, o_d = 48, o_s = o_d + up(8 * d), o_i = o_s + up(4 * sn), total = o_i + up(4 * in);
+    r->pool = h->pinned;
+    r->blk = h->pinned->get(total, &r->blk_cap);
+    if (!r->blk) {
+      r->pool.reset();
+      return MQM_ENOMEM;
+    }
+    char *B = static_cast<char *>(r->blk);
+    uint64_t *off = reinterpret_cast<uint64_t *>(B), *soff = reinterpret_cast<uint64_t *>(B + o_sh),
+             *ioff = reinterpret_cast<uint64_t *>(B + o_io);
+    off[0] = soff[0] = ioff[0] = 0;
+    off[1] = d;
+    soff[1] = sn;
+    ioff[1] = in;
+    if (d) memcpy(B + o_d, b->deliveries + d0, 8 * d);
+    if (sn) memcpy(B + o_s, b->shared + s0, 4 * sn);
+    if (in) memcpy(B + o_i, b->idents + i0, 4 * in);
+    r->n = 1;
+    r->offsets = off;
+    r->shared_offsets = soff;
+    r->deliveries = reinterpret_cast<const mqm_delivery *>(B + o_d);
+    r->shared = reinterpret_cast<const uint32_t *>(B + o_s);
+    if (b->has_idents) {
+      r->has_idents = true;
+      r->ident_offsets = ioff;
+      r->idents = reinterpret_cast<const uint32_t *>(B + o_i);
+    }
+    r->snap = b->snap;
+    *out = r.release();
+    return MQM_OK;
+  }
+
+  void run() {
+    std::vector<Req *> batch;
+    std::string bytes;
+    std::vector<uint64_t> offs;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return stop || !q.empty(); });
+        if (q.empty()) return;  // stop requested and nothing pending
+        if (linger_us && q.size() < max_batch)
+          cv.wait_for(lk, std::chrono::microseconds(linger_us), [&] { return stop || q.size() >= max_batch; });
+        const size_t n = std::min<size_t>(q.size(), max_batch);
+        batch.assign(q.begin(), q.begin() + n);
+        q.erase(q.begin(), q.begin() + n);
+      }
+      bytes.clear();
+      offs.assign(1, 0);
+      for (Req *r : batch) {
+        bytes.append(r->topic, r->len);
+        offs.push_back(bytes.size());
+      }
+      mqm_result *b = nullptr;
+      const int rc = mqm_match_batch(h, bytes.data(), offs.data(), (uint32_t)batch.size(), &b);
+      for (uint32_t i = 0; i < batch.size(); i++) {
+        batch[i]->rc = rc;
+        if (rc == MQM_OK) {
+          try {
+            batch[i]->rc = split(h, b, i, &batch[i]->res);
+          } catch (const std::bad_alloc &) {
+            batch[i]->rc = MQM_ENOMEM;
+          }
+        }
+      }
+      if (b) mqm_result_free(b);
+      {
+        std::lock_guard<std::mutex> g(mu);
+        for (Req *r : batch) r->done = true;
+        batches++;
+        topics += batch.size();
+      }
+      cv_done.notify_all();
+    }
+  }
+};
+
+}  // namespace
+
+mqm_index::~mqm_index() {
+  collector.reset();  // first: its thread matches through this index
+  pool.clear();
+}
+
 int mqm_subscribers(mqm_index *h, const char *topic, size_t topic_len, mqm_result **out) {
+  if (!h || !out) return MQM_EINVAL;
+  if (h->collector) {
+    *out = nullptr;
+    return guarded([&] { return h->collector->submit(topic, topic_len, out); });
+  }
   uint64_t offs[2] = {0, topic_len};
   return mqm_match_batch(h, topic ? topic : "", offs, 1, out);
+}
+
+int mqm_batching_policy(mqm_index *h, uint32_t max_batch, uint32_t linger_us) {
+  if (!h || h->cfg.device == MQM_DEVICE_NONE) return MQM_EINVAL;
+  {
+    // (turns batching on for an index created without MQM_CFG_BATCHING; calls
+    // already inside mqm_subscribers finish on the direct path)
+    std::lock_guard<std::mutex> g(h->mu);
+    if (!h->collector) {
+      int rc = guarded([&] {
+        h->collector = std::make_unique<Collector>(h);
+        return MQM_OK;
+      });
+      if (rc != MQM_OK) return rc;
+      h->cfg.flags |= MQM_CFG_BATCHING;
+    }
+  }
+  std::lock_guard<std::mutex> g(h->collector->mu);
+  h->collector->max_batch = max_batch ? max_batch : 8192;
+  h->collector->linger_us = linger_us;
+  return MQM_OK;
+}
+
+int mqm_batching_stats(mqm_index *h, uint64_t *batches, uint64_t *topics) {
+  if (!h || !h->collector || !batches || !topics) return MQM_EINVAL;
+  std::lock_guard<std::mutex> g(h->collector->mu);
+  *batches = h->collector->batches;
+  *topics = h->collector->topics;
+  return MQM_OK;
 }
 
 uint32_t mqm_result_num_topics(const mqm_result *r) { return r ? r->n : 0; }

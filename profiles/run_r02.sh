@@ -58,6 +58,8 @@ for step in "$@"; do
              timeout -s KILL 600 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/revpmc_$C -o pmc \
              -- python3 $ROOT/bench.py --workload reverse --steps 2 --warmup 1 --no-cpu-baseline \
              > $OUT/revpmc_$C.json 2> $OUT/revpmc_$C.log || exit 1; done) ;;
+    batching) timeout -k 10 300 python3 -u -m pytest tests/test_gpu_batching.py -m gpu -x -v --timeout 240 \
+             --timeout-method thread > $OUT/pytest_batching.log 2>&1 ;;
     shim) timeout -k 10 300 python3 -u -m pytest tests/test_gpu_shim.py -m gpu -x -v --timeout 240 \
              --timeout-method thread > $OUT/pytest_shim.log 2>&1 ;;
     calib) (cd /tmp && export TMPDIR=/tmp && for C in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do

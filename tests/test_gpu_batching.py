@@ -1,0 +1,100 @@
+"""MQM_CFG_BATCHING: concurrent single-topic Subscribers(topic) calls — the
+reference's call shape, one goroutine per connection (listeners/tcp.go:83,
+server.go:776) — gathered by the collector thread into GPU batches.  Every
+caller's single-topic result must equal the same topic's row of a plain
+batched match (deliveries, shared candidates, Identifiers support), and the
+collector must actually have batched (fewer batches than calls)."""
+
+import ctypes as C
+import threading
+
+import numpy as np
+import pytest
+
+import maxmq_amd
+from maxmq_amd import capi
+from tools import mqgen
+
+
+def _rows(res):
+    """per topic: sorted deliveries, sorted shared candidates, sorted idents"""
+    out = []
+    for i in range(res.n):
+        d = res.deliveries[int(res.offsets[i]):int(res.offsets[i + 1])]
+        s = res.shared[int(res.shared_offsets[i]):int(res.shared_offsets[i + 1])]
+        ids = () if res.idents is None else tuple(sorted(
+            int(x) for x in res.idents[int(res.ident_offsets[i]):int(res.ident_offsets[i + 1])]))
+        out.append((tuple(sorted((int(c), int(p)) for c, p in zip(d["client"], d["packed"]))),
+                    tuple(sorted(int(x) for x in s)), ids))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("threads", [16])
+def test_batched_subscribers_concurrent_equal_plain(threads):
+    w = mqgen.generate(1, n_filters=20000, n_topics=3200, p_shared=0.05)
+    plain = maxmq_amd.TopicsIndex(device=0, identifiers=True)
+    plain.subscribe_workload(w)
+    plain.commit()
+    want = _rows(plain.match_batch(w.topics.data, w.topics.offs))
+    plain.close()
+
+    idx = maxmq_amd.TopicsIndex(device=0, identifiers=True, batching=True)
+    idx.subscribe_workload(w)
+    idx.commit()
+    L = capi.lib()
+    n = len(w.topics)
+    got = [None] * n
+    errors = []
+
+    def worker(k):
+        try:
+            for i in range(k, n, threads):
+                t = bytes(w.topics.data[int(w.topics.offs[i]):int(w.topics.offs[i + 1])])
+                h = C.c_void_p()
+                capi.check("mqm_subscribers", L.mqm_subscribers(idx._h, t, len(t), C.byref(h)))
+                r = maxmq_amd.BatchResult(idx, h)
+                try:
+                    assert r.n == 1
+                    got[i] = _rows(r)[0]
+                finally:
+                    r.close()
+        except Exception as e:  # surfaced below
+            errors.append(e)
+
+    ths = [threading.Thread(target=worker, args=(k,)) for k in range(threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errors, errors[0]
+    batches, topics = idx.batching_stats()
+    idx.close()
+    assert topics == n
+    assert batches < n, "the collector never gathered more than one call"
+    bad = [i for i in range(n) if got[i] != want[i]]
+    assert not bad, f"{len(bad)} topics differ, first {bad[0]}: {got[bad[0]]} vs {want[bad[0]]}"
+
+
+@pytest.mark.gpu
+def test_batching_policy_and_single_caller():
+    w = mqgen.generate(1, n_filters=2000, n_topics=50)
+    idx = maxmq_amd.TopicsIndex(device=0, batching=True)
+    idx.subscribe_workload(w)
+    idx.commit()
+    idx.batching_policy(max_batch=4, linger_us=200)
+    for i in range(10):
+        t = bytes(w.topics.data[int(w.topics.offs[i]):int(w.topics.offs[i + 1])]).decode()
+        idx.subscribers(t)
+    b, t = idx.batching_stats()
+    assert (b, t) == (10, 10)  # one caller: one topic per batch, whatever the linger
+    idx.close()
+
+
+def test_batching_api_refused_without_flag():
+    idx = maxmq_amd.TopicsIndex(device=None)
+    with pytest.raises(capi.MqmError):
+        idx.batching_stats()
+    with pytest.raises(capi.MqmError):
+        idx.batching_policy(8, 0)
+    idx.close()
