@@ -60,9 +60,9 @@ def parse():
                     help="host path: concurrent callers (each its own stream), batches overlapped across them")
     ap.add_argument("--latency-topics", type=int, default=2000,
                     help="single-topic mqm_subscribers calls timed for the per-publish latency; 0 = skip")
-    ap.add_argument("--conc-threads", type=int, default=16,
+    ap.add_argument("--conc-threads", type=int, default=64,
                     help="latency leg: concurrent single-topic callers (direct, then batched)")
-    ap.add_argument("--conc-calls", type=int, default=300, help="latency leg: calls per concurrent caller")
+    ap.add_argument("--conc-calls", type=int, default=200, help="latency leg: calls per concurrent caller")
     ap.add_argument("--workload", choices=["forward", "reverse", "churn"], default="forward",
                     help="forward: Subscribers (headline); reverse: Messages over retained topics (config 5); "
                          "churn: Subscribe/Unsubscribe at rate with background snapshot rebuilds")

@@ -173,9 +173,10 @@ struct Counters {              // zeroed before every batch
   unsigned int n_wmerge;       // k_merge: other topics with Ms <= kSmallMulti
   unsigned int n_t1;           // k_multi<1024>: kSmallMulti < Ms <= 768
   unsigned int n_t2;           // k_multi<2048>: 768 < Ms <= 1536
-  unsigned int n_part;         // k_multi_part: Ms > 1536
+  unsigned int n_t3;           // k_multi<4096>: 1536 < Ms <= 3072
+  unsigned int n_part;         // k_multi_part: Ms > 3072
   unsigned int n_shlist;       // k_shared: topics with shared candidates
-  unsigned long long m_sum[3]; // multi entries of the k_multi<1024> / <2048> / k_multi_part lists
+  unsigned long long m_sum[3]; // multi entries of the k_multi<1024> / <2048> / <4096> + k_multi_part lists
   unsigned int oob;            // a store fell outside its output buffer (never expected)
 #if MQM_WALK_STATS
   unsigned long long st_probe, st_miss, st_desc;
@@ -1531,8 +1532,11 @@ __global__ __launch_bounds__(256) void k_densify(DeviceSnapshot s, uint32_t n, c
 // counters), reserves its ranges with one global atomic per list, then
 // writes them.  Order within a list is unspecified (lists only schedule
 // work; every topic's output position is its own dstart).
-enum : int { kLSmall = 0, kLWave, kLT1, kLT2, kLPart, kLShared, kNLists };
-constexpr uint32_t kT1Max = 768, kT2Max = 1536;  // k_multi<1024> / <2048> capacities (load 0.75)
+enum : int { kLSmall = 0, kLWave, kLT1, kLT2, kLT3, kLPart, kLShared, kNLists };
+// k_multi<1024> / <2048> / <4096> capacities (load 0.75); k_multi_part beyond
+// (partition passes re-read every entry: a single-pass 4096-slot table is
+// cheaper up to its capacity)
+constexpr uint32_t kT1Max = 768, kT2Max = 1536, kT3Max = 3072;
 struct Lists {
   uint32_t *l[kNLists];
 };
@@ -1544,7 +1548,11 @@ __device__ __forceinline__ uint32_t route_mask(uint8_t c, uint32_t m, uint32_t h
   const uint32_t sh = h ? (1u << kLShared) : 0u;
   if (m == 0) return sh;
   if ((c & kClsFewHits) && m <= kSmallMultiS) return sh | (1u << kLSmall);
-  return sh | (m <= kSmallMulti ? (1u << kLWave) : m <= kT1Max ? (1u << kLT1) : m <= kT2Max ? (1u << kLT2) : (1u << kLPart));
+  return sh | (m <= kSmallMulti ? (1u << kLWave)
+               : m <= kT1Max  ? (1u << kLT1)
+               : m <= kT2Max  ? (1u << kLT2)
+               : m <= kT3Max  ? (1u << kLT3)
+                              : (1u << kLPart));
 }
 
 __global__ __launch_bounds__(256) void k_route(const uint8_t *__restrict__ cls, const uint32_t *__restrict__ mcount,
@@ -1567,8 +1575,8 @@ __global__ __launch_bounds__(256) void k_route(const uint8_t *__restrict__ cls, 
       const uint64_t m = __ballot((r >> l) & 1u);
       if (lane == 0 && m) atomicAdd(&lc[l], (unsigned int)__popcll(m));
     }
-    if (r & ((1u << kLT1) | (1u << kLT2) | (1u << kLPart)))
-      atomicAdd(&ms[(r >> kLPart) & 1u ? 2 : (r >> kLT2) & 1u ? 1 : 0], (unsigned long long)mcount[t]);
+    if (r & ((1u << kLT1) | (1u << kLT2) | (1u << kLT3) | (1u << kLPart)))
+      atomicAdd(&ms[(r >> kLPart) & 1u || (r >> kLT3) & 1u ? 2 : (r >> kLT2) & 1u ? 1 : 0], (unsigned long long)mcount[t]);
   }
   __syncthreads();
   if (tid < 3 && ms[tid]) atomicAdd(&msum[tid], ms[tid]);
@@ -1832,7 +1840,7 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
       scan_offsets(ws, (const uint32_t *)o.hcount, o.hstart, n, st) || scan_offsets(ws, o.nsolo, desc_start, n, st))
     return -3;
   // merge lists, counted before the one host sync that sizes the outputs
-  const W::Slot list_slots[kNLists] = {W::kListS, W::kListW, W::kListT1, W::kListT2, W::kListP, W::kListH};
+  const W::Slot list_slots[kNLists] = {W::kListS, W::kListW, W::kListT1, W::kListT2, W::kListT3, W::kListP, W::kListH};
   Lists lists;
   for (int l = 0; l < kNLists; l++) {
     if (ws.get(list_slots[l], sizeof(uint32_t) * (n + 1))) return -2;
@@ -1907,7 +1915,7 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   if (n > 0) {
     // merges on the side stream, concurrently with the solo copy (they write
     // disjoint parts of dout and dcount: winners after Ss / topics with Ms > 0)
-    const bool merges = hc->n_small || hc->n_wmerge || hc->n_t1 || hc->n_t2 || hc->n_part;
+    const bool merges = hc->n_small || hc->n_wmerge || hc->n_t1 || hc->n_t2 || hc->n_t3 || hc->n_part;
     const bool side = merges && ws.overlap;
     // persistent grids: with both streams busy, each takes its share of the device
     const uint32_t side_pct = side ? MQM_SIDE_PCT : 100, main_pct = side && MQM_SIDE_PCT < 100 ? 100 - MQM_SIDE_PCT : 100;
@@ -1931,6 +1939,11 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
       if (hc->n_t2) {
         hipLaunchKernelGGL(k_multi<2048>, grid(k_multi<2048>), dim3(kBigThreads), 0, ms, s, o, lists.l[kLT2],
                            lcount + kLT2);
+        HIP_TRY(hipGetLastError());
+      }
+      if (hc->n_t3) {
+        hipLaunchKernelGGL(k_multi<4096>, grid(k_multi<4096>), dim3(kBigThreads), 0, ms, s, o, lists.l[kLT3],
+                           lcount + kLT3);
         HIP_TRY(hipGetLastError());
       }
       if (hc->n_part) {
@@ -1967,6 +1980,11 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
       if (hc->n_t2) {
         hipLaunchKernelGGL(k_multi<2048>, grid(k_multi<2048>), dim3(kBigThreads), 0, ms, s, o, lists.l[kLT2],
                            lcount + kLT2);
+        HIP_TRY(hipGetLastError());
+      }
+      if (hc->n_t3) {
+        hipLaunchKernelGGL(k_multi<4096>, grid(k_multi<4096>), dim3(kBigThreads), 0, ms, s, o, lists.l[kLT3],
+                           lcount + kLT3);
         HIP_TRY(hipGetLastError());
       }
       if (hc->n_part) {
@@ -2040,9 +2058,9 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   out->n_topics = n;
   out->n_deliveries = hp[0];
   out->n_shared = hp[1];
-  out->n_big = hc->n_t1 + hc->n_t2 + hc->n_part;
+  out->n_big = hc->n_t1 + hc->n_t2 + hc->n_t3 + hc->n_part;
   out->n_tier2 = hc->n_t2;
-  out->n_tier3 = hc->n_part;
+  out->n_tier3 = hc->n_t3 + hc->n_part;
   for (int i = 0; i < 3; i++) out->multi_entries[i] = hc->m_sum[i];
   out->n_merge_small = hc->n_small;
   out->n_merge_wave = hc->n_wmerge;

@@ -107,6 +107,12 @@ def test_edge_cases_and_fallback_paths():
         filters += ["hub/#", "hub/x"]
         clients += [f"h{i}", f"h{i}"]
     topics += ["hub/x", "hub", "hub/x/y"]
+    # 4000 multi entries for one topic: past the 4096-slot single-pass tier
+    # (k_multi<4096> takes up to 3072) -> the partitioned workgroup merge
+    for i in range(2000):
+        filters += ["hub2/#", "hub2/x"]
+        clients += [f"k{i}", f"k{i}"]
+    topics += ["hub2/x", "hub2/x/y"]
     # 300 raw entries, all multi: the wave tier's table is too small -> workgroup tier
     for i in range(100):
         filters += ["m/#", "m/y"]
