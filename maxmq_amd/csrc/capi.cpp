@@ -397,7 +397,8 @@ int mqm_create(const mqm_config *cfg, mqm_index **out) {
 
 int mqm_destroy(mqm_index *h) {
   if (!h) return MQM_EINVAL;
-  h->builder.reset();  // finishes a running build and joins the worker
+  h->collector.reset();  // first: its thread matches (and may commit) through this index
+  h->builder.reset();    // finishes a running build and joins the worker
   if (h->cfg.device != MQM_DEVICE_NONE) {
     (void)hipSetDevice(h->cfg.device);
     (void)hipDeviceSynchronize();

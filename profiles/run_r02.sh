@@ -51,6 +51,8 @@ for step in "$@"; do
              --timeout-method thread > $OUT/pytest_ret.log 2>&1 ;;
     rev) timeout -k 10 600 python3 -u bench.py --workload reverse --steps 5 --warmup 1 --no-cpu-baseline \
              > $OUT/bench_reverse.json 2> $OUT/bench_reverse.log ;;
+    revfull) timeout -k 10 900 python3 -u bench.py --workload reverse --steps 5 --warmup 1 \
+             > $OUT/bench_reverse_full.json 2> $OUT/bench_reverse_full.log ;;
     revprof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
              -d $OUT/prof_rev -o prof -- python3 $ROOT/bench.py --workload reverse --steps 3 --warmup 1 \
              --no-cpu-baseline > $OUT/rev_under_rocprof.json 2> $OUT/rocprof_rev.log) ;;
