@@ -840,7 +840,10 @@ __global__ __launch_bounds__(256) void k_winmap(const uint4 *__restrict__ desc, 
 // delivery: a 4-B copy, lane-consecutive loads and stores).  More than 64
 // descriptors in a window (many tiny topics): the next 64, from where the
 // previous batch ended.
-constexpr int kCU = 16;
+#ifndef MQM_WINCOPY_CU
+#define MQM_WINCOPY_CU 16
+#endif
+constexpr int kCU = MQM_WINCOPY_CU;  // entries per lane per step (tuning knob)
 struct alignas(16) WinLds {
   uint32_t st[kWave], en[kWave], src[kWave];
 };
@@ -1093,6 +1096,12 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_merge(DeviceSnapshot s, O
 // in table-slot order: each wave scans a quarter of the table twice (count,
 // then write at its prefix), so the layout is deterministic.
 // ---------------------------------------------------------------------------
+// k_multi's table: >= 2 slots per entry (MQM_MERGE_DENSE=1: >= 4/3, fewer
+// slots to clear and scan, longer probe runs; tuning knob)
+#ifndef MQM_MERGE_DENSE
+#define MQM_MERGE_DENSE 0
+#endif
+
 struct alignas(16) MultiLds {
   uint32_t rec[kRecLds];
   uint32_t wsum[kBigThreads / kWave];
@@ -1172,7 +1181,8 @@ __global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs
     nx.fetch(o, list, bi + gridDim.x, nb);
     const uint32_t nh = L.rec[0] & 0xFFu, Ss = L.rec[1], M = L.rec[2];
     uint32_t lg = 6;
-    while ((1u << lg) < 2 * M && (1u << lg) < (uint32_t)kSlots) lg++;
+    const uint32_t need = MQM_MERGE_DENSE ? (4 * M + 2) / 3 : 2 * M;
+    while ((1u << lg) < need && (1u << lg) < (uint32_t)kSlots) lg++;
     const uint32_t mask = (1u << lg) - 1;
     for (uint32_t i = tid; i <= mask; i += kBigThreads) mt_clear(tb, i);
     __syncthreads();
