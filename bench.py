@@ -516,6 +516,7 @@ def concurrent_single_topic(idx, topics, args):
         a = np.concatenate([np.array(x) for x in lat]) * 1e6
         return {"topics_per_s": T * per / dt, "p50_us": float(np.median(a)), "p99_us": float(np.percentile(a, 99))}
 
+    run()  # warm: every caller's context (stream, workspace) exists before timing
     out = {"threads": T, "calls_per_thread": per, "direct": run()}
     idx.batching_policy(0, 0)  # MQM_CFG_BATCHING on from here
     run()  # warm the collector's contexts
