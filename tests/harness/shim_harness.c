@@ -211,8 +211,8 @@ static char *next_field(char **s) {
 }
 
 int main(int argc, char **argv) {
-  if (argc != 4) {
-    fprintf(stderr, "usage: %s IN OUT THREADS\n", argv[0]);
+  if (argc != 4 && argc != 5) {
+    fprintf(stderr, "usage: %s IN OUT THREADS [batching]\n", argv[0]);
     return 2;
   }
   n_threads = atoi(argv[3]);
@@ -223,6 +223,10 @@ int main(int argc, char **argv) {
   unsigned long ns = 0, nt = 0;
   if (fscanf(in, "%lu %lu\n", &ns, &nt) != 2) return 2;
   mqm_config cfg = {0, MQM_CFG_AUTOCOMMIT | MQM_CFG_IDENTIFIERS};
+  /* "batching": the shim's per-connection Subscribers calls go through the
+   * library's collector (MQM_CFG_BATCHING), as a broker with many
+   * connections would run it */
+  if (argc == 5 && strcmp(argv[4], "batching") == 0) cfg.flags |= MQM_CFG_BATCHING;
   if (mqm_create(&cfg, &H) != MQM_OK) {
     fprintf(stderr, "mqm_create failed\n");
     return 3;

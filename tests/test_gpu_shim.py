@@ -72,12 +72,15 @@ def _expected(w):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("threads", [4])
-def test_shim_call_sequence_concurrent_readers(tmp_path, threads):
+@pytest.mark.parametrize("threads,mode", [(4, "direct"), (16, "batching")])
+def test_shim_call_sequence_concurrent_readers(tmp_path, threads, mode):
+    """mode "batching": the same call sequence with MQM_CFG_BATCHING, so the
+    16 threads' single-topic calls are gathered by the collector"""
     w = mqgen.generate(1, n_filters=4000, n_topics=6000, n_clients=400, p_shared=0.05, seed=0x5A17)
     inp, out = tmp_path / "in.txt", tmp_path / "out.txt"
     _write_input(inp, w)
-    r = subprocess.run([_harness(), str(inp), str(out), str(threads)], capture_output=True, text=True, timeout=300)
+    args = [_harness(), str(inp), str(out), str(threads)] + (["batching"] if mode == "batching" else [])
+    r = subprocess.run(args, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     got = sorted(out.read_text(encoding="utf-8").splitlines())
     want = _expected(w)
