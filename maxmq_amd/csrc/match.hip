@@ -151,6 +151,12 @@ static_assert(kSmallMulti % kWave == 0, "register tiles");
 // topic levels drawn for a wildcard make probes miss); other literal probes
 // then skip the filter's round trip
 enum : uint32_t { kItemLit = 0, kItemPlus = 1, kItemHash = 2, kItemLitB = 3 };
+// MQM_WALK_PRECHECK=1: a frontier node's literal item is checked against the
+// filter when it is pushed (its load overlapping the pushing level's record
+// writes) and only a positive is pushed, as kItemLit
+#ifndef MQM_WALK_PRECHECK
+#define MQM_WALK_PRECHECK 1
+#endif
 #ifndef MQM_BLOOM_PLUS_ONLY
 #define MQM_BLOOM_PLUS_ONLY 0
 #endif
@@ -492,6 +498,16 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
       // key == "+" / "#": the literal probe IS the wildcard probe (the
       // reference visits that child twice; no parent probe: topics.go:507)
       const bool lit_is_wild = (k1 == (1ull << 56)) && (k0 == '+' || k0 == '#');
+#if MQM_WALK_PRECHECK
+      // the next level's key, for the filter check of the literal items this
+      // level pushes (d + 1 < kLMax; the walk leaves at kLMax otherwise)
+      uint64_t n0 = my_k0[0], n1 = my_k1[0];
+#pragma unroll
+      for (int j = 1; j < kLPer; j++)
+        if ((d + 1) / kG == (uint32_t)j) n0 = my_k0[j], n1 = my_k1[j];
+      const uint64_t nk0 = shfl64(n0, gbase + (int)((d + 1) % kG)), nk1 = shfl64(n1, gbase + (int)((d + 1) % kG));
+      const bool next_wild = (nk1 == (1ull << 56)) && (nk0 == '+' || nk0 == '#');
+#endif
       const uint32_t tst = d == 0 ? 0 : L.sep[d - 1] + 1;
       const uint32_t tln = ((d < nsep) ? L.sep[d] : len) - tst;
       uint32_t nnext = 0;
@@ -527,20 +543,22 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
         const bool leaf = push && (fl & kFlagHashLeaf);
         // the '#' child's gather at the next level ('$' flag = this node's)
         const uint32_t c_hl = leaf && !skip_dollar ? dc.hsub_cnt : 0;
-        const uint32_t n_items = push ? (((fl & kFlagHasLiteral) ? 1u : 0u) + (dc.plus != kNone ? 1u : 0u) +
-                                         (dc.hash != kNone && !leaf ? 1u : 0u))
-                                      : 0u;
+#if MQM_WALK_PRECHECK
+        // the pushed literal probe's filter word, loaded now: its round trip
+        // overlaps this level's record writes, and a negative (or a '+' / '#'
+        // next level, whose literal probe is the wildcard's) drops the item
+        const bool chk = push && (fl & kFlagHasLiteral) && s.bloom && d + 1 < (uint32_t)kLMax && !next_wild;
+        const uint64_t nh2 = chk ? edge_hash(c, Key{nk0, nk1}) : 0;
+        const uint64_t bw = chk ? s.bloom[bloom_word(nh2, s.bloom_mask)] : 0;
+        const uint64_t bb = bloom_bits(nh2);
+#endif
         const uint32_t m_own = (uint32_t)(__ballot(c_own > 0) >> gbase) & kGMask;
         const uint32_t m_par = (uint32_t)(__ballot(c_par > 0) >> gbase) & kGMask;
         const uint32_t m_hl = (uint32_t)(__ballot(c_hl > 0) >> gbase) & kGMask;
         const uint32_t m_sh = (uint32_t)(__ballot(c_sh > 0) >> gbase) & kGMask;
-        const uint32_t m_i0 = (uint32_t)(__ballot(n_items & 1u) >> gbase) & kGMask;
-        const uint32_t m_i1 = (uint32_t)(__ballot(n_items & 2u) >> gbase) & kGMask;
         const uint32_t n_own = __popc(m_own), n_par = __popc(m_par), n_hl = __popc(m_hl);
-        const uint32_t t_items = __popc(m_i0) + 2 * __popc(m_i1);
         if (nh + n_own + n_par + n_hl > (uint32_t)kHCap) why = kWhyHits;
         if (nsh + __popc(m_sh) > (uint32_t)kShCap) why = kWhyShared;
-        if (nnext + t_items > (uint32_t)kICap) why = kWhyFrontier;
         // a saturated multi count, or a range past the bounded path's entries
         // (also keeps the per-lane sums below from overflowing)
         if ((uint32_t)(__ballot(((c_own | c_par | c_hl) && (fl & kFlagMultiSat)) ||
@@ -583,10 +601,31 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
           *reinterpret_cast<uint2 *>(rec + 2 * (nq + __popc(q_own) + __popc(q_par) + __popc(q_hl & gmask_lt))) =
               make_uint2(hoff, c_hl - mu_hl);
         nq += __popc(q_own) + __popc(q_par) + __popc(q_hl);
+        // the next level's items (after the record writes: the frontier cap
+        // needs the filter's answer; a topic leaving here goes to the DFS path)
+#if MQM_WALK_PRECHECK
+        // (at d + 1 == kLMax the item is kept: the next level routes the topic to the DFS path)
+        const bool lit_next = (fl & kFlagHasLiteral) &&
+                              (d + 1 >= (uint32_t)kLMax || (s.bloom ? (chk && (bw & bb) == bb) : !next_wild));
+        const uint32_t lit_item = kItemLit;
+#else
+        const bool lit_next = fl & kFlagHasLiteral;
+        const uint32_t lit_item = lit_kind(dc.plus);
+#endif
+        const uint32_t n_items = push ? ((lit_next ? 1u : 0u) + (dc.plus != kNone ? 1u : 0u) +
+                                         (dc.hash != kNone && !leaf ? 1u : 0u))
+                                      : 0u;
+        const uint32_t m_i0 = (uint32_t)(__ballot(n_items & 1u) >> gbase) & kGMask;
+        const uint32_t m_i1 = (uint32_t)(__ballot(n_items & 2u) >> gbase) & kGMask;
+        const uint32_t t_items = __popc(m_i0) + 2 * __popc(m_i1);
+        if (nnext + t_items > (uint32_t)kICap) {
+          why = kWhyFrontier;
+          break;
+        }
         if (push) {
           uint32_t *nx = &L.item[cur ^ 1][nnext + __popc(m_i0 & gmask_lt) + 2 * __popc(m_i1 & gmask_lt)];
           uint32_t k = 0;
-          if (fl & kFlagHasLiteral) nx[k++] = (c << 2) | lit_kind(dc.plus);
+          if (lit_next) nx[k++] = (c << 2) | lit_item;
           if (dc.plus != kNone) nx[k++] = (dc.plus << 2) | kItemPlus;
           if (dc.hash != kNone && !leaf) nx[k++] = (dc.hash << 2) | kItemHash;
         }
