@@ -51,7 +51,9 @@ for path in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recur
         sums[c][k] += float(row["Counter_Value"])
         disp[c][k].add((path, row["Dispatch_Id"]))
 kib = 1024.0
-div = (lambda c, k: 1) if last_call else (lambda c, k: len(disp[c][k]))
+# per batch: a kernel may launch more than once per batch (the k_multi tiers
+# share one name here), so divide by the batches (k_walk launches once each)
+div = (lambda c, k: 1) if last_call else (lambda c, k: len(disp[c]["k_walk"]) or len(disp[c][k]))
 reads = {k: v * kib * (1 if k in GATHER else 2) / div("FETCH_SIZE", k) for k, v in sums["FETCH_SIZE"].items()}
 writes = {k: v * kib / div("WRITE_SIZE", k) for k, v in sums["WRITE_SIZE"].items()}
 out = {

@@ -10,9 +10,9 @@ STEPS=${STEPS:-2}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 cd /tmp && export TMPDIR=/tmp
 for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 600 rocprofv3 --pmc $C --kernel-trace --output-format csv \
+  timeout -s KILL 240 rocprofv3 --pmc $C --kernel-trace --output-format csv \
     -d $ROOT/gpurun_out/pmc_$C -o pmc -- \
-    python3 $ROOT/bench.py --config $CFG --steps $STEPS --warmup 1 --no-cpu-baseline \
+    python3 $ROOT/bench.py --config $CFG --steps $STEPS --warmup 1 --no-cpu-baseline --host-topics 0 --latency-topics 0 \
     > $ROOT/gpurun_out/pmc_$C.json 2> $ROOT/gpurun_out/pmc_$C.log
 done
 python3 $ROOT/profiles/pmc_to_traffic.py $ROOT/gpurun_out $((STEPS + 1)) > $ROOT/gpurun_out/traffic.json
