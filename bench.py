@@ -13,7 +13,11 @@ every rank the full trie and its own 10M-topic batch (weak scaling, no
 data-path collective); --mode sharded splits the subscribers by client range,
 RCCL-broadcasts rank 0's batch, and every shard's dense per-topic lists go
 back to rank 0 over RCCL send/recv, where mqm_gather_shards lays them out as
-the node-wide CSR (all inside the timed step).
+the node-wide CSR (all inside the timed step), in chunks of topics sized so
+one gathered chunk fits --gather-budget-gb on rank 0 (maxmq_amd/shard.py
+node_step / plan_chunk); --mode hybrid runs GPUs / --shards independent
+replica groups of --shards subscriber shards each (own process group, own
+batch, own leader).
 
 Rank 0 prints ONE JSON line.  `roofline.achieved` = algorithmic bytes of the
 match pipeline (B = T + 8N + 8P + 8V + 8S + 8D, per-topic walk
@@ -46,7 +50,13 @@ def parse():
     ap.add_argument("--config", type=int, default=3, help="BASELINE configs index + 1 (mqgen config)")
     ap.add_argument("--filters", type=int, default=0, help="override n_filters")
     ap.add_argument("--topics", type=int, default=0, help="override n_topics")
-    ap.add_argument("--mode", choices=["replicas", "sharded"], default="replicas")
+    ap.add_argument("--mode", choices=["replicas", "sharded", "hybrid"], default="replicas",
+                    help="replicas: full trie per GPU, own batch each; sharded: subscriber shards over all GPUs, "
+                         "one batch; hybrid: --shards subscriber shards x (GPUs / --shards) topic replicas")
+    ap.add_argument("--shards", type=int, default=2, help="hybrid: subscriber shards per replica group")
+    ap.add_argument("--gather-budget-gb", type=float, default=48.0,
+                    help="sharded/hybrid: HBM the group leader may hold for one gathered chunk (received lists "
+                         "+ laid-out node CSR); topics per gather are sized from it (shard.plan_chunk)")
     ap.add_argument("--shard", default="",
                     help="R/N: this one GPU matches shard R of the N-way subscriber-sharded config "
                          "(the per-shard cost of a node run, e.g. --config 4 --shard 0/8)")
@@ -193,11 +203,18 @@ def main():
         overrides["n_filters"] = args.filters
     if args.topics:
         overrides["n_topics"] = args.topics
-    sharded = args.mode == "sharded" and world > 1
+    sharded = args.mode in ("sharded", "hybrid") and world > 1
     shard_of = tuple(int(x) for x in args.shard.split("/")) if args.shard else None
+    if sharded:
+        # replica groups of k subscriber shards (sharded: one group of all ranks)
+        k = world if args.mode == "sharded" else args.shards
+        groups, lay = shard.hybrid_layout(world, k)
+        pgs = [dist.new_group(g_) for g_ in groups]  # every rank creates every group, in order
+        grp, my_shard = lay[rank]
+        pg, leader = pgs[grp], groups[grp][0]
     t0 = time.time()
     if sharded:  # this rank's client range only (a 100M-filter config is never whole on one host)
-        w = shard.generated_shard(args.config, world, rank, **overrides)
+        w = shard.generated_shard(args.config, k, my_shard, **overrides)
     elif shard_of:
         w = shard.generated_shard(args.config, shard_of[1], shard_of[0], **overrides)
     else:
@@ -216,50 +233,69 @@ def main():
     tb = torch.from_numpy(w.topics.data).to(dev)
     to = torch.from_numpy(w.topics.offs.view(np.int64)).to(dev)
     stream = torch.cuda.current_stream(dev)
+    chunk = n
     if sharded:
-        # shard client id -> node client id (the generator's global client
-        # index), every rank's map held by rank 0, which lays the gathered
-        # lists out; node-wide result buffers on rank 0
-        mine = torch.from_numpy(shard.local_client_map(w).astype(np.int32)).to(dev)
-        cmaps = shard.gather_maps(dist, mine, dst=0)
-        node = {"offs": torch.zeros(n + 1, dtype=torch.int64, device=dev), "d": None,
-                "soffs": torch.zeros(n + 1, dtype=torch.int64, device=dev), "s": None}
-        my = {"offs": torch.zeros(n + 1, dtype=torch.int64, device=dev), "d": None,
-              "soffs": torch.zeros(n + 1, dtype=torch.int64, device=dev), "s": None}
+        from maxmq_amd.devbuf import copy_from_ptr
 
-    def grow(buf, key, count, dtype):
-        if buf[key] is None or buf[key].numel() < count:
-            buf[key] = torch.empty(max(count, 1), dtype=dtype, device=dev)
-        return buf[key][:count]
+        # shard client id -> node client id (the generator's global client
+        # index), every shard's map held by its group leader, which lays the
+        # gathered lists out
+        mine = torch.from_numpy(shard.local_client_map(w).astype(np.int32)).to(dev)
+        cmaps = shard.gather_maps(dist, mine, dst=leader, group=pg)
+        bufs, node, cache = {}, {}, {}
+
+        def grow(buf, key, count, dtype):
+            if key not in buf or buf[key].numel() < count:
+                buf.pop(key, None)
+                buf[key] = torch.empty(max(int(count * 1.25), 1), dtype=dtype, device=dev)
+            return buf[key][:count]
+
+        def match_chunk(c0, c1):
+            """this shard's dense CSR of topics [c0, c1) (the offsets array is
+            absolute into the batch bytes, so a chunk is a pointer offset)"""
+            m = c1 - c0
+            idx.match_device(tb.data_ptr(), to.data_ptr() + 8 * c0, m, stream.cuda_stream)
+            d = idx.dense_device(stream.cuda_stream)
+            nd, ns = int(d.n_deliveries), int(d.n_shared)
+            o = copy_from_ptr(grow(bufs, "offs", m + 1, torch.int64), d.offsets)
+            dl = copy_from_ptr(grow(bufs, "d", nd, torch.int64), d.deliveries)
+            so = copy_from_ptr(grow(bufs, "soffs", m + 1, torch.int64), d.shared_offsets)
+            sl = copy_from_ptr(grow(bufs, "s", ns, torch.int32), d.shared)
+            return o, dl, so, sl
+
+        def layout(c0, c1, parts, sparts):
+            """group leader: the chunk's node-wide CSRs (mqm_gather_shards*)"""
+            m = c1 - c0
+            tot = sum(int(p[1].numel()) for p in parts)
+            stot = sum(int(p[1].numel()) for p in sparts)
+            maxmq_amd.gather_shards(m, [(o.data_ptr(), dl.data_ptr(), cmaps[i].data_ptr(), cmaps[i].numel())
+                                        for i, (o, dl) in enumerate(parts)],
+                                    grow(node, "offs", m + 1, torch.int64).data_ptr(),
+                                    grow(node, "d", tot, torch.int64).data_ptr(), stream.cuda_stream)
+            maxmq_amd.gather_shards_shared(m, [(o.data_ptr(), sl.data_ptr()) for o, sl in sparts],
+                                           grow(node, "soffs", m + 1, torch.int64).data_ptr(),
+                                           grow(node, "s", stot, torch.int32).data_ptr(), stream.cuda_stream)
+
+        # topics per gather: the group's deliveries per topic over the batch's
+        # first topics, summed over its shards, against the leader's budget
+        probe = min(n, 200000)
+        _, pdl, _, psl = match_chunk(0, probe)
+        tot = torch.tensor([pdl.numel(), psl.numel()], dtype=torch.float64, device=dev)
+        dist.all_reduce(tot, group=pg)
+        dpt, spt = float(tot[0]) / probe, float(tot[1]) / probe
+        chunk = shard.plan_chunk(n, dpt * 1.1, spt * 1.1, args.gather_budget_gb * 1e9)
+        log(f"[rank {rank}] group {grp} shard {my_shard}/{k}: {dpt:.0f} node deliveries per topic -> "
+            f"{chunk} topics per gather ({(n + chunk - 1) // chunk} gathers per step)")
 
     def step():
         if sharded:
-            # the publish batch enters at rank 0 and is broadcast over xGMI (RCCL)
-            shard.broadcast_batch(dist, tb, to, src=0)
-        r = idx.match_device(tb.data_ptr(), to.data_ptr(), n, stream.cuda_stream)
-        if sharded:
-            # this shard's dense per-topic lists (deliveries and shared
-            # candidates) -> rank 0 (RCCL send/recv), laid out there as the
-            # node-wide CSRs (mqm_gather_shards, mqm_gather_shards_shared)
-            d = idx.dense_device(stream.cuda_stream)
-            nd, ns = int(d.n_deliveries), int(d.n_shared)
-            _dev_to_tensor(d.offsets, my["offs"])
-            _dev_to_tensor(d.deliveries, grow(my, "d", nd, torch.int64))
-            _dev_to_tensor(d.shared_offsets, my["soffs"])
-            _dev_to_tensor(d.shared, grow(my, "s", ns, torch.int32))
-            parts = shard.gather_lists(dist, my["offs"], my["d"][:nd], dst=0)
-            sparts = shard.gather_lists(dist, my["soffs"], my["s"][:ns], dst=0)
-            if rank == 0:
-                tot = sum(int(p[1].numel()) for p in parts)
-                stot = sum(int(p[1].numel()) for p in sparts)
-                maxmq_amd.gather_shards(n, [(o.data_ptr(), dl.data_ptr(), cmaps[i].data_ptr(), cmaps[i].numel())
-                                            for i, (o, dl) in enumerate(parts)],
-                                        node["offs"].data_ptr(), grow(node, "d", tot, torch.int64).data_ptr(),
-                                        stream.cuda_stream)
-                maxmq_amd.gather_shards_shared(n, [(o.data_ptr(), sl.data_ptr()) for o, sl in sparts],
-                                               node["soffs"].data_ptr(), grow(node, "s", stot, torch.int32).data_ptr(),
-                                               stream.cuda_stream)
-        return r
+            # the publish batch enters at the group leader and is broadcast over
+            # xGMI (RCCL); every shard matches it chunk by chunk and its dense
+            # lists go back to the leader (RCCL send/recv), laid out there
+            nd_, ns_ = shard.node_step(dist, tb, to, match_chunk, layout, chunk, src=leader, group=pg, cache=cache)
+            return None, nd_, ns_
+        r_ = idx.match_device(tb.data_ptr(), to.data_ptr(), n, stream.cuda_stream)
+        return r_, int(r_.n_deliveries), int(r_.n_shared)
 
     for _ in range(args.warmup):
         step()
@@ -278,9 +314,11 @@ def main():
     why = {}
     lists = {}
     for _ in range(args.steps):
-        r = step()
-        deliveries += int(r.n_deliveries)
-        shared += int(r.n_shared)
+        r, nd_, ns_ = step()
+        deliveries += nd_
+        shared += ns_
+        if r is None:  # sharded node step: per-shard kernel statistics are not summed over chunks
+            continue
         fallback = int(r.n_fallback)
         big = int(r.n_big)
         why = dict(zip(["frontier", "hits", "levels", "shared_hits", "raw_entries"], list(r.fallback_why)))
@@ -302,7 +340,9 @@ def main():
         deliveries, shared = int(dsum[0].item()), int(dsum[1].item())
 
     if sharded:
-        topics_total = n * args.steps  # every shard walks the same batch: node-wide lists of n topics per step
+        # every shard of a group walks the group's batch: node-wide lists of n
+        # topics per step and group
+        topics_total = n * args.steps * len(groups)
     else:
         topics_total = n * args.steps * world
     value = topics_total / dt
@@ -333,19 +373,21 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": dt * 1e3 / args.steps,
             "higher_is_better": True,
-            "scaling": "strong" if sharded else "weak",
+            "scaling": "strong" if sharded and len(groups) == 1 else "weak",
             "vs_baseline": None,
             "dtype": "u8/u32 (byte+integer matching)",
             "data": "synthetic (tools/mqgen, deterministic seed); inputs resident in HBM",
             "config": {
                 "workload": (f"mqgen config {args.config} shard {shard_of[0]}/{shard_of[1]} (client range), " if shard_of
-                             else f"mqgen config {args.config} {args.mode} over {world} GPU(s), " if sharded else
-                             f"mqgen config {args.config}: ") + f"{len(w.filters)} filters "
+                             else f"mqgen config {args.config} {args.mode} over {world} GPU(s) ({len(groups)} "
+                                  f"group(s) of {k} subscriber shards, {chunk} topics per gather), rank 0 holds "
+                             if sharded else f"mqgen config {args.config}: ") + f"{len(w.filters)} filters "
                             f"({w.params['p_plus']:.0%} '+', {w.params['p_hash']:.0%} '#', "
                             f"topic Zipf s={w.params['topic_zipf_s']}), {n}-topic batch, depth<={w.params['max_depth']}",
                 "filters": len(w.filters),
                 "topics_per_batch": n,
-                "parallelism": f"{args.mode}{world}" if not shard_of else f"shard{shard_of[0]}of{shard_of[1]}",
+                "parallelism": (f"shard{shard_of[0]}of{shard_of[1]}" if shard_of else
+                                f"hybrid{k}x{len(groups)}" if sharded and args.mode == "hybrid" else f"{args.mode}{world}"),
             },
             "deliveries_per_s": deliveries / dt,
             "shared_candidates_per_s": shared / dt,
@@ -692,11 +734,12 @@ def run_reverse(args, dist, rank, world, local, dev):
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
-    refs_out = items = ranges = 0
+    refs_out = items = ranges = skipped = 0
     for _ in range(args.steps):
         r = step()
         refs_out += int(r.n_refs)
         items += int(r.n_items)
+        skipped += int(r.n_skipped)
         ranges += int(r.n_ranges)
     torch.cuda.synchronize(dev)
     if dist:
@@ -706,12 +749,22 @@ def run_reverse(args, dist, rank, world, local, dev):
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    # full-size property check, outside the timed region: the same call twice
+    # gives the same per-filter counts and the same checksum of every filter's
+    # refs (order-independent: sum of mixed refs per filter)
+    check = reverse_selfcheck(idx, fb, fo, n, dev, stream)
     if rank == 0:
         steps = args.steps
         tbytes = int(w.filters.offs[-1])
-        # algorithmic bytes per batch: filter bytes + offsets in/out (16 B) + one
-        # 64-B trie read per (filter, node) step + refs read and written (16 B)
-        per_batch = tbytes + 16 * n + 64 * items / steps + 16 * refs_out / steps
+        # algorithmic bytes per batch, for the work this pipeline performs
+        # (SURVEY §8d's forward model applied to the reverse walk): filter bytes
+        # + offsets in/out (16 B) + per (filter, node) item actually loaded an
+        # 8-B key probe and an 8-B descriptor read (16 B; the reference's items
+        # that the literal-edge index jumps over are not charged, they are
+        # reported as reference_items) + per retained hit one ref read and one
+        # written (16 B)
+        loaded = (items - skipped) / steps
+        per_batch = tbytes + 16 * n + 16 * loaded + 16 * refs_out / steps
         achieved = per_batch / (dt / steps) / 1e9
         traffic = None  # PMC bytes per call (profiles/traffic_reverse.json, pmc_to_traffic.py --per-call)
         tj = os.path.join(ROOT, "profiles", "traffic_reverse.json")
@@ -742,11 +795,14 @@ def run_reverse(args, dist, rank, world, local, dev):
                        "filters_per_batch": n, "retained": len(w.topics), "parallelism": f"replicas{world}"},
             "retained_hits_per_s": refs_out * world / dt,
             "hits_per_filter": refs_out / (n * steps),
-            "items_per_filter": items / (n * steps),
+            "items_per_filter": (items - skipped) / (n * steps),
+            "reference_items_per_filter": items / (n * steps),
+            "selfcheck": check,
             "snapshot": snap,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "algorithmic_bytes_per_batch": per_batch,
+                         "model": "T + 16 N + 16 x items loaded + 16 x retained hits",
                          "kernel": "reverse-match pipeline per batch (k_flt_*, k_level per depth, k_emit_*, "
                                    "k_task_copy; wall time, one read-back per call)"},
             "cpu_baseline": cpu,
@@ -755,6 +811,29 @@ def run_reverse(args, dist, rank, world, local, dev):
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def reverse_selfcheck(idx, fb, fo, n, dev, stream):
+    """Two mqm_messages_device calls on the full batch: identical per-filter
+    counts and identical per-filter checksums of the refs (sum of splitmix64
+    of every ref, order-independent), plus every ref below the retained count."""
+    import torch
+
+    from maxmq_amd.devbuf import dev_view_copy, segment_checksums
+
+    def once():
+        m = idx.messages_device(fb.data_ptr(), fo.data_ptr(), n, stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        offs = dev_view_copy(m.offsets, n + 1, torch.int64, dev)
+        sums = segment_checksums(offs, m.refs, torch.int64)
+        return offs, sums
+
+    o1, s1 = once()
+    o2, s2 = once()
+    cnt = o1[1:] - o1[:-1]
+    return {"run_to_run_counts_equal": bool(torch.equal(o1, o2)),
+            "run_to_run_ref_checksums_equal": bool(torch.equal(s1, s2)),
+            "offsets_monotone": bool((cnt >= 0).all()), "refs": int(o1[-1])}
 
 
 def cpu_reverse(w, refs, args):
@@ -789,20 +868,6 @@ def cpu_reverse(w, refs, args):
            "retained_hits_per_s": hits / busy}
     out.update(cores_note(done / busy / threads, threads, host))  # (per-thread share of the parallel rate)
     return out
-
-
-def _dev_to_tensor(ptr, t):
-    """copy a device buffer owned by the library into tensor t (device to device)."""
-    import ctypes
-
-    hip = ctypes.CDLL("libamdhip64.so")
-    nbytes = t.numel() * t.element_size()
-    if nbytes == 0:
-        return
-    rc = hip.hipMemcpy(ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(ptr), ctypes.c_size_t(nbytes),
-                       ctypes.c_int(3))
-    if rc != 0:
-        raise RuntimeError(f"hipMemcpy D2D failed: {rc}")
 
 
 def cpu_baseline(w, args):

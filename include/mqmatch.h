@@ -139,6 +139,7 @@ typedef struct {
   uint64_t n_solo_ranges;         /* solo copy ranges (hits with solo entries)    */
   uint32_t n_tier2, n_tier3;      /* topics the workgroup merge passed to its 2nd / 3rd tier */
   uint64_t multi_entries[3];      /* multi entries merged by the workgroup tiers 1 / 2 / 3 */
+  uint32_t n_part;                /* tier-3 topics merged in client-hash partitions (> 3072 multi entries) */
 } mqm_device_result;
 
 /* ---- lifecycle: NewTopicsIndex (topics.go:291-299) ---------------------- */
@@ -237,9 +238,9 @@ int mqm_subscribers(mqm_index *h, const char *topic, size_t topic_len, mqm_resul
  * and how long the collector waits for more after the first (microseconds,
  * default 0); on an index created without the flag it turns batching on.
  * Statistics: batches run and topics they carried (MQM_EINVAL while batching
- * is off).  Both MQM_EINVAL on a host-only index.  Call the policy before the
- * index is shared between threads (mqm_subscribers reads the collector
- * pointer without a lock). */
+ * is off).  Both MQM_EINVAL on a host-only index.  Safe to call while other
+ * threads are inside mqm_subscribers: the collector is published atomically,
+ * and calls already past that point finish on the direct path. */
 int mqm_batching_policy(mqm_index *h, uint32_t max_batch, uint32_t linger_us);
 int mqm_batching_stats(mqm_index *h, uint64_t *batches, uint64_t *topics);
 /* Device in / device out on `hip_stream` (hipStream_t, NULL = default stream). */
@@ -346,7 +347,8 @@ typedef struct {
   const uint64_t *offsets; /* device, n_filters + 1 */
   const uint64_t *refs;    /* device */
   uint64_t n_ranges;       /* emitted ranges (roofline bookkeeping)      */
-  uint64_t n_items;        /* (filter, trie node) steps over all levels  */
+  uint64_t n_items;        /* (filter, trie node) steps of the reference's recursion, all levels */
+  uint64_t n_skipped;      /* ... of those, children the literal-edge index jumped over (not loaded) */
 } mqm_device_messages;
 int mqm_messages_device(mqm_index *h, const uint8_t *d_filter_bytes, const uint64_t *d_filter_offsets,
                         uint32_t n_filters, void *hip_stream, mqm_device_messages *out);

@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdlib>
@@ -57,7 +58,9 @@ class PinnedPool {
     {
       std::lock_guard<std::mutex> g(mu_);
       auto it = free_.lower_bound(need);
-      if (it != free_.end() && it->first <= 2 * need + (64u << 20)) {
+      // slack proportional to the request (a small single-topic result never
+      // holds on to a large batch block)
+      if (it != free_.end() && it->first <= 2 * need + std::min<size_t>(need, 64u << 20)) {
         *cap = it->first;
         void *p = it->second;
         cached_ -= it->first;
@@ -139,8 +142,12 @@ struct mqm_index {
   std::vector<std::unique_ptr<MatchCtx>> pool;
   std::shared_ptr<PinnedPool> pinned = std::make_shared<PinnedPool>();
   // MQM_CFG_BATCHING: declared last, so it stops (joins its thread) before
-  // anything it uses is destroyed
-  std::unique_ptr<Collector> collector;
+  // anything it uses is destroyed.  `collector` is what callers read (no
+  // lock: an acquire load), published once with a release store under mu;
+  // collector_owner keeps it alive until the index is destroyed
+  std::unique_ptr<Collector> collector_owner;
+  std::atomic<Collector *> collector{nullptr};
+  void stop_collector();
   ~mqm_index();
 };
 
@@ -389,7 +396,10 @@ int mqm_create(const mqm_config *cfg, mqm_index **out) {
     }
     if (const char *e = getenv("MQM_NO_OVERLAP")) h->overlap = atoi(e) == 0;
     if (ctx_init(h.get(), &h->dev) != MQM_OK) return MQM_EHIP;
-    if (h->cfg.flags & MQM_CFG_BATCHING) h->collector = std::make_unique<Collector>(h.get());
+    if (h->cfg.flags & MQM_CFG_BATCHING) {
+      h->collector_owner = std::make_unique<Collector>(h.get());
+      h->collector.store(h->collector_owner.get(), std::memory_order_release);
+    }
     *out = h.release();
     return MQM_OK;
   });
@@ -397,7 +407,7 @@ int mqm_create(const mqm_config *cfg, mqm_index **out) {
 
 int mqm_destroy(mqm_index *h) {
   if (!h) return MQM_EINVAL;
-  h->collector.reset();  // first: its thread matches (and may commit) through this index
+  h->stop_collector();  // first: its thread matches (and may commit) through this index
   h->builder.reset();    // finishes a running build and joins the worker
   if (h->cfg.device != MQM_DEVICE_NONE) {
     (void)hipSetDevice(h->cfg.device);
@@ -599,6 +609,7 @@ int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t 
     out->n_tier2 = mo.n_tier2;
     out->n_tier3 = mo.n_tier3;
     for (int i = 0; i < 3; i++) out->multi_entries[i] = mo.multi_entries[i];
+    out->n_part = mo.n_part;
     return MQM_OK;
   });
 }
@@ -813,6 +824,7 @@ int mqm_messages_device(mqm_index *h, const uint8_t *d_filter_bytes, const uint6
     out->refs = mo.refs;
     out->n_ranges = mo.n_emissions;
     out->n_items = mo.n_items;
+    out->n_skipped = mo.n_skipped;
     return MQM_OK;
   });
 }
@@ -1005,16 +1017,21 @@ struct Collector {
 
 }  // namespace
 
+void mqm_index::stop_collector() {
+  collector.store(nullptr, std::memory_order_release);
+  collector_owner.reset();
+}
+
 mqm_index::~mqm_index() {
-  collector.reset();  // first: its thread matches through this index
+  stop_collector();  // first: its thread matches through this index
   pool.clear();
 }
 
 int mqm_subscribers(mqm_index *h, const char *topic, size_t topic_len, mqm_result **out) {
   if (!h || !out) return MQM_EINVAL;
-  if (h->collector) {
+  if (Collector *c = h->collector.load(std::memory_order_acquire)) {
     *out = nullptr;
-    return guarded([&] { return h->collector->submit(topic, topic_len, out); });
+    return guarded([&] { return c->submit(topic, topic_len, out); });
   }
   uint64_t offs[2] = {0, topic_len};
   return mqm_match_batch(h, topic ? topic : "", offs, 1, out);
@@ -1026,26 +1043,30 @@ int mqm_batching_policy(mqm_index *h, uint32_t max_batch, uint32_t linger_us) {
     // (turns batching on for an index created without MQM_CFG_BATCHING; calls
     // already inside mqm_subscribers finish on the direct path)
     std::lock_guard<std::mutex> g(h->mu);
-    if (!h->collector) {
+    if (!h->collector_owner) {
       int rc = guarded([&] {
-        h->collector = std::make_unique<Collector>(h);
+        h->collector_owner = std::make_unique<Collector>(h);
         return MQM_OK;
       });
       if (rc != MQM_OK) return rc;
-      h->cfg.flags |= MQM_CFG_BATCHING;
+      // published fully constructed: a concurrent mqm_subscribers either sees
+      // nullptr (direct path) or this collector (release / acquire)
+      h->collector.store(h->collector_owner.get(), std::memory_order_release);
     }
   }
-  std::lock_guard<std::mutex> g(h->collector->mu);
-  h->collector->max_batch = max_batch ? max_batch : 8192;
-  h->collector->linger_us = linger_us;
+  Collector *c = h->collector.load(std::memory_order_acquire);
+  std::lock_guard<std::mutex> g(c->mu);
+  c->max_batch = max_batch ? max_batch : 8192;
+  c->linger_us = linger_us;
   return MQM_OK;
 }
 
 int mqm_batching_stats(mqm_index *h, uint64_t *batches, uint64_t *topics) {
-  if (!h || !h->collector || !batches || !topics) return MQM_EINVAL;
-  std::lock_guard<std::mutex> g(h->collector->mu);
-  *batches = h->collector->batches;
-  *topics = h->collector->topics;
+  Collector *c = h ? h->collector.load(std::memory_order_acquire) : nullptr;
+  if (!c || !batches || !topics) return MQM_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  *batches = c->batches;
+  *topics = c->topics;
   return MQM_OK;
 }
 

@@ -94,6 +94,7 @@ struct MatchOutput {
   uint32_t n_merge_small = 0, n_merge_wave = 0;  // topics merged by k_merge_small / k_merge
   uint64_t n_solo_ranges = 0;                     // solo copy descriptors (hits with solo entries)
   uint64_t multi_entries[3] = {0, 0, 0};  // multi entries merged by the three workgroup tiers
+  uint32_t n_part = 0;                    // ... of the third tier's topics, merged in client-hash partitions
 };
 
 // words[i] = subs[i].word & kPackedMask for i < n (snapshot upload, on `st`)

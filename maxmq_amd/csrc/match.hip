@@ -2111,6 +2111,7 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   out->n_tier2 = hc->n_t2;
   out->n_tier3 = hc->n_t3 + hc->n_part;
   for (int i = 0; i < 3; i++) out->multi_entries[i] = hc->m_sum[i];
+  out->n_part = hc->n_part;
   out->n_merge_small = hc->n_small;
   out->n_merge_wave = hc->n_wmerge;
   out->n_solo_ranges = n_desc;

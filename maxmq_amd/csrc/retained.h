@@ -20,6 +20,7 @@ struct MessagesOutput {
   uint64_t n_refs = 0;
   uint64_t n_emissions = 0;
   uint64_t n_items = 0;  // (filter, node) worklist items over all levels
+  uint64_t n_skipped = 0;  // ... of those, the reference's items the edge index jumped over (never loaded)
   const uint64_t *offsets = nullptr;  // device, n_filters + 1
   const uint64_t *refs = nullptr;     // device, message refs (order within a filter unspecified)
 };

@@ -41,6 +41,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 
 #include "device.h"
 #include "retained.h"
@@ -611,10 +612,18 @@ int messages_device(const DeviceSnapshot &s, const DeviceRetained *r, Workspace 
   // every list starts at its size from the previous call (grown on overflow)
   uint64_t &item_cap = ws.rev_item_cap, &emit_cap = ws.rev_emit_cap, &task_cap = ws.rev_task_cap,
            &out_cap = ws.rev_out_cap;
-  item_cap = std::max<uint64_t>(item_cap, std::max<uint64_t>(4ull * n, 1u << 16));
-  emit_cap = std::max<uint64_t>(emit_cap, std::max<uint64_t>(2ull * n, 1u << 16));
-  task_cap = std::max<uint64_t>(task_cap, 1u << 12);
-  out_cap = std::max<uint64_t>(out_cap, std::max<uint64_t>(4ull * n, 1u << 16));
+  // MQM_REV_CAP0=k (tests): a fresh workspace starts every list at k entries,
+  // so the first calls overflow and re-queue at every level
+  const char *cap0_env = getenv("MQM_REV_CAP0");
+  const uint64_t cap0 = cap0_env ? strtoull(cap0_env, nullptr, 10) : 0;
+  if (cap0) {
+    if (!item_cap) item_cap = emit_cap = task_cap = out_cap = cap0;
+  } else {
+    item_cap = std::max<uint64_t>(item_cap, std::max<uint64_t>(4ull * n, 1u << 16));
+    emit_cap = std::max<uint64_t>(emit_cap, std::max<uint64_t>(2ull * n, 1u << 16));
+    task_cap = std::max<uint64_t>(task_cap, 1u << 12);
+    out_cap = std::max<uint64_t>(out_cap, std::max<uint64_t>(4ull * n, 1u << 16));
+  }
   const uint32_t grid = resident_grid();
   for (int attempt = 0;; attempt++) {
     if (ws.get(W::kRItemF0, sizeof(uint32_t) * item_cap) || ws.get(W::kRItemN0, sizeof(uint32_t) * item_cap) ||
@@ -694,6 +703,7 @@ int messages_device(const DeviceSnapshot &s, const DeviceRetained *r, Workspace 
       out->refs = refs_out;
       out->n_emissions = n_emit;
       out->n_items = hc->items_total + n;  // level 0 = one item per filter
+      out->n_skipped = hc->skipped;
       return 0;
     }
     if (attempt >= 64) return -3;  // (the counters only ever grow: never reached)

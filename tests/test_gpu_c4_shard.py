@@ -1,0 +1,116 @@
+"""BASELINE configs[3] (100M filters, subscriber-sharded over 8 GPUs) as the
+per-GPU unit of a node step: shard 0 of the 8-way client-range split
+(maxmq_amd/shard.py: 12.5M filters, generated directly) against the full
+10M-topic batch, through the same mqm_match_device call `bench.py --shard 0/8
+--config 4` and the sharded node step time.
+
+C4 is the config that drives the widest merges (tens of thousands of multi
+entries per hub topic: the k_multi<4096> tier and the client-partitioned
+merge) and the unbounded DFS path under load (topics with more than 64 hits),
+so the test asserts those ran, then checks:
+  * over all 10M topics (~6G deliveries, walked in chunks of whole topics):
+    dense CSR monotone and summing to n_deliveries, client ids below the
+    shard's client count, QoS <= 2, no client twice in a topic, run-to-run
+    equality of every topic's checksum (mix64 sum of its entries);
+  * bit-exact against oracle/mochi_ref.c built from the same shard on a
+    sample of 50k random topics plus the 300 topics with the most deliveries
+    (where the partitioned merge and the DFS path run): the full-batch rows of
+    those topics equal the host-path rows, which equal the oracle's field by
+    field (client, max QoS, NoLocal, first filter, its identifier, RAP, RH;
+    shared candidates by (filter, client)).
+Reference: vendor/github.com/mochi-co/mqtt/v2/topics.go:484-555 (Subscribers,
+gatherSubscriptions, gatherSharedSubscriptions), packets/packets.go:250-270
+(Subscription.Merge); north_star C4."""
+
+import numpy as np
+import pytest
+
+import maxmq_amd
+from maxmq_amd import shard
+from oracle.binding import OracleIndex
+from tests.gpu_util import assert_same, canon_gpu, canon_oracle
+from tools.mqgen import Strings
+
+pytestmark = pytest.mark.gpu
+
+
+def test_config4_shard0of8_full_batch():
+    import torch
+
+    from maxmq_amd.devbuf import dev_view_copy, iter_csr_chunks, mix64
+
+    w = shard.generated_shard(4, 8, 0)
+    n = len(w.topics)
+    assert n == 10_000_000 and len(w.filters) > 12_000_000, (n, len(w.filters))
+    idx = maxmq_amd.TopicsIndex(0, autocommit=False)
+    idx.subscribe_workload(w)
+    idx.commit()
+    dev = torch.device("cuda:0")
+    tb = torch.from_numpy(w.topics.data).to(dev)
+    to = torch.from_numpy(w.topics.offs.view(np.int64)).to(dev)
+    ncl = idx.num_clients()
+
+    def run():
+        r = idx.match_device(tb.data_ptr(), to.data_ptr(), n)
+        d = idx.dense_device()
+        offs = dev_view_copy(d.offsets, n + 1, torch.int64, dev)
+        torch.cuda.synchronize()
+        return r, d, offs
+
+    r1, d1, offs = run()
+    nd = int(r1.n_deliveries)
+    assert nd > 300 * n, nd  # ~620 deliveries per topic on this shard
+    assert r1.n_tier3 > 0, "the k_multi<4096> / partitioned tier never ran"
+    assert r1.n_part > 0, "the client-partitioned merge never ran"
+    assert r1.n_fallback > 0, "no topic took the unbounded DFS path"
+    assert int(offs[0]) == 0 and int(offs[-1]) == nd
+    assert bool((offs[1:] >= offs[:-1]).all())
+    # every entry of every topic, in chunks of whole topics: client in range,
+    # QoS <= 2, no client twice in a topic, per-topic checksum
+    sums1 = torch.zeros(n, dtype=torch.int64, device=dev)
+    for lo, hi, a, e, sid in iter_csr_chunks(offs, d1.deliveries, torch.int64):
+        client = e & 0xFFFFFFFF
+        assert int(client.max()) < ncl
+        assert int(((e >> 60) & 3).max()) <= 2  # packed word (high half): qos at its bits 28..29
+        key = torch.sort((sid << 32) | client).values
+        assert not bool((key[1:] == key[:-1]).any()), f"a client appears twice in one topic of [{lo}, {hi})"
+        sums1.index_add_(0, sid, mix64(e ^ mix64(sid)))
+        del client, key
+    # the bit-exact sample: 50k random topics + the 300 with the most deliveries
+    rng = np.random.default_rng(4)
+    o = offs.cpu().numpy()
+    top = np.argsort(np.diff(o))[-300:]
+    small = np.unique(np.concatenate([rng.choice(n, size=50000, replace=False), top]))
+    cnt = (o[small + 1] - o[small]).astype(np.int64)
+    pos = torch.from_numpy(np.repeat(o[small] - np.concatenate([[0], np.cumsum(cnt)[:-1]]), cnt)
+                           + np.arange(cnt.sum())).to(dev)
+    # run-to-run: the same call again gives the same per-topic checksums; the
+    # sample's rows are taken from this second result
+    r2, d2, offs2 = run()
+    assert torch.equal(offs2, offs)
+    sums2 = torch.zeros(n, dtype=torch.int64, device=dev)
+    full_rows = torch.empty(len(pos), dtype=torch.int64, device=dev)
+    for lo, hi, a, e, sid in iter_csr_chunks(offs2, d2.deliveries, torch.int64):
+        sums2.index_add_(0, sid, mix64(e ^ mix64(sid)))
+        inside = torch.nonzero((pos >= a) & (pos < a + e.numel())).flatten()
+        full_rows[inside] = e[pos[inside] - a]
+    assert torch.equal(sums2, sums1), "run-to-run per-topic checksums differ"
+    full_rows = full_rows.cpu().numpy().view(np.uint64)
+    del offs2, sums1, sums2, pos
+    sub = Strings.from_list([w.topics[int(i)] for i in small])
+    res = idx.match_batch(sub.data, sub.offs)
+    assert np.array_equal(cnt, np.diff(res.offsets).astype(np.int64)), "per-topic counts differ from the host path"
+    tid = np.repeat(np.arange(len(small), dtype=np.uint64), cnt)
+    host_rows = res.deliveries.view(np.uint64)
+    assert np.array_equal(np.unique(np.stack([tid, full_rows], 1), axis=0),
+                          np.unique(np.stack([tid, host_rows], 1), axis=0)), "full-batch rows != host-path rows"
+    del full_rows, host_rows, tid
+    g, gs = canon_gpu(res)
+    del res
+    ora = OracleIndex()
+    ora.subscribe_workload(w)
+    ref, rs = canon_oracle(*ora.match(sub.data, sub.offs, nthreads=16)[:4])
+    ora.close()
+    assert len(g) > 1_000_000
+    assert_same(g, ref, "C4 shard 0/8 deliveries (sample)")
+    assert_same(gs, rs, "C4 shard 0/8 shared (sample)")

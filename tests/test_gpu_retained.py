@@ -133,8 +133,9 @@ def test_config5_5m_retained_vs_oracle():
 
 
 def test_config5_20m_retained_linearity():
-    """BASELINE configs[4] at 1M filters vs 20M retained topics (bench.py
-    --workload reverse checks the same property at the full 50M):
+    """BASELINE configs[4] at 1M filters vs 20M retained topics (at the full
+    50M, bench.py --workload reverse checks run-to-run equality of the
+    per-filter counts and of a checksum of every filter's refs, not this split):
     the retained set split in two by a content hash of the topic (duplicates
     land in the same half, so "last retain wins" holds in both) must give, for
     every filter, count(full) = count(half 0) + count(half 1), and for a
@@ -192,3 +193,54 @@ def test_config5_20m_retained_linearity():
     both = np.concatenate(parts_s)
     both = both[np.lexsort((both[:, 1], both[:, 0]))]
     assert np.array_equal(s_full, both), "set(full) != set(half 0) | set(half 1)"
+
+
+def test_reverse_workspace_reuse_and_overflow_requeue(monkeypatch):
+    """The shape of the r02j fault (an illegal access at the first
+    messages_device call on a freshly built index, round-2 work in progress):
+    every list starts at 64 entries (MQM_REV_CAP0), so the first calls overflow
+    and are re-queued at every level; then one index (one device workspace,
+    its capacities carried from call to call) goes through three snapshots of
+    different sizes (small, 50x larger, then mostly deleted), each compared with
+    the oracle bit for bit, device form and host form."""
+    import torch
+
+    from tests.gpu_util import dev_tensor
+
+    monkeypatch.setenv("MQM_REV_CAP0", "64")
+    w = mqgen.generate(5, n_filters=20000, n_topics=300000)
+    f = w.filters
+    fb = torch.from_numpy(f.data).cuda()
+    fo = torch.from_numpy(f.offs.view(np.int64)).cuda()
+    nf = len(f)
+    idx = maxmq_amd.TopicsIndex(0, autocommit=False)
+    ora = OracleIndex()
+    idx.subscribe_workload(w)
+    ora.subscribe_workload(w)
+    t = w.topics
+    refs = np.arange(len(t), dtype=np.uint64) * 5 + 2
+
+    def retain(lo, hi, payload=1):
+        for i in range(lo, hi):
+            assert idx.retain_message(t[i], int(refs[i]), payload) == ora.retain_message(t[i], int(refs[i]), payload)
+
+    def check(what):
+        idx.commit()
+        m = idx.messages_device(fb.data_ptr(), fo.data_ptr(), nf)
+        torch.cuda.synchronize()
+        go = dev_tensor(m.offsets, nf + 1, torch.int64).cpu().numpy().view(np.uint64)
+        gr = dev_tensor(m.refs, int(m.n_refs), torch.int64).cpu().numpy().view(np.uint64)
+        ro, rr = ora.messages(f.data, f.offs, nthreads=16)
+        assert np.array_equal(go, ro), f"{what}: per-filter counts differ"
+        assert np.array_equal(_canon(go, gr), _canon(ro, rr)), f"{what}: refs differ"
+        ho, hr = idx.messages_batch(f.data, f.offs)  # a pool context: its own workspace, also at 64 entries
+        assert np.array_equal(_canon(ho, hr), _canon(ro, rr)), f"{what}: host form differs"
+        return int(ro[-1])
+
+    retain(0, 6000)
+    small = check("small snapshot")
+    retain(6000, len(t))
+    big = check("50x larger snapshot on the same workspace")
+    assert big > 20 * max(small, 1)
+    retain(0, len(t) - 3000, payload=0)  # delete all but the last 3000
+    check("mostly deleted snapshot on the grown workspace")

@@ -118,16 +118,6 @@ def _copy_strings(s: _Strings) -> Strings:
 def default_params(config: int) -> dict:
     p = _Params()
     _lib().mqgen_default_params(config, C.byref(p))
-    out = {}
-    for name, _ in _Params._fields_:
-        v = getattr(p, name)
-        out[name] = list(v) if name in ("vocab", "depth_w") else v
-    return out
-
-
-def default_params(config: int) -> dict:
-    p = _Params()
-    _lib().mqgen_default_params(config, C.byref(p))
     return {name: (list(getattr(p, name)) if name in ("vocab", "depth_w") else getattr(p, name))
             for name, _ in _Params._fields_}
 
