@@ -497,75 +497,68 @@ def host_path(idx, w, args):
                     "pcie_bound = max(H2D bytes / H2D rate, D2H bytes / D2H rate)"}
 
 
+def _driver():
+    """tools/_build/libmqdrive.so: native threads issuing mqm_subscribers
+    calls (the reference's one-goroutine-per-connection call shape)"""
+    import ctypes as C
+
+    from maxmq_amd import capi
+
+    L = capi.lib()
+    D = C.CDLL(os.path.join(ROOT, "tools", "_build", "libmqdrive.so"))
+
+    class Api(C.Structure):
+        _fields_ = [("subscribers", C.c_void_p), ("offsets", C.c_void_p), ("result_free", C.c_void_p)]
+
+    api = Api(C.cast(L.mqm_subscribers, C.c_void_p), C.cast(L.mqm_result_offsets, C.c_void_p),
+              C.cast(L.mqm_result_free, C.c_void_p))
+    D.mqd_concurrent.argtypes = [C.POINTER(Api), C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_int, C.c_int,
+                                 C.c_void_p, C.POINTER(C.c_uint64)]
+    D.mqd_concurrent.restype = C.c_int64
+    return D, api
+
+
 def latency(idx, w, args):
-    """Per-publish latency of the reference's call shape: one Subscribers(topic)
-    per call (server.go:776) through mqm_subscribers, host in / host out."""
+    """Per-publish latency and throughput of the reference's call shape: one
+    Subscribers(topic) per call (server.go:776) through mqm_subscribers, host
+    in / host out, issued by native threads (tools/conc_driver.cpp): one
+    caller, then --conc-threads concurrent callers (one goroutine per
+    connection, listeners/tcp.go:83) each calling directly, then through the
+    MQM_CFG_BATCHING collector."""
     import ctypes as C
 
-    from maxmq_amd import capi
+    D, api = _driver()
+    n = min(max(args.latency_topics, args.conc_threads * args.conc_calls), len(w.topics))
+    data = np.ascontiguousarray(w.topics.data[: int(w.topics.offs[n])])
+    offs = np.ascontiguousarray(w.topics.offs[: n + 1].astype(np.uint64))
 
-    L = capi.lib()
-    n = min(args.latency_topics, len(w.topics))
-    topics = [bytes(w.topics.data[w.topics.offs[i]:w.topics.offs[i + 1]]) for i in range(n)]
-    ts = []
-    for i, t in enumerate(topics + topics[:50]):
-        res = C.c_void_p()
-        t0 = time.perf_counter()
-        capi.check("mqm_subscribers", L.mqm_subscribers(idx._h, t, len(t), C.byref(res)))
-        dt = time.perf_counter() - t0
-        L.mqm_result_free(res)
-        if i >= 50:
-            ts.append(dt)
-    ts = np.array(ts) * 1e6
-    out = {"unit": "us", "calls": len(ts), "p50": float(np.median(ts)), "p90": float(np.percentile(ts, 90)),
-           "p99": float(np.percentile(ts, 99)), "mean": float(ts.mean())}
-    out["concurrent"] = concurrent_single_topic(idx, topics, args)
-    return out
+    def run(threads, calls):
+        lat = np.zeros(threads * calls, np.uint64)
+        dsum = C.c_uint64()
+        ns = D.mqd_concurrent(C.byref(api), idx._h, data.ctypes.data_as(C.c_void_p), offs.ctypes.data_as(C.c_void_p),
+                              n, threads, calls, lat.ctypes.data_as(C.c_void_p), C.byref(dsum))
+        if ns < 0:
+            raise RuntimeError("mqm_subscribers failed in the driver")
+        us = lat.astype(np.float64) / 1e3
+        return {"topics_per_s": threads * calls / (ns * 1e-9), "p50_us": float(np.median(us)),
+                "p90_us": float(np.percentile(us, 90)), "p99_us": float(np.percentile(us, 99)),
+                "deliveries_per_topic": dsum.value / (threads * calls)}
 
-
-def concurrent_single_topic(idx, topics, args):
-    """--conc-threads callers each issuing single-topic mqm_subscribers calls
-    (one goroutine per connection, listeners/tcp.go:83): every call its own
-    pipeline, then with the MQM_CFG_BATCHING collector gathering concurrent
-    calls into GPU batches.  Topics/s over all callers and per-call latency."""
-    import ctypes as C
-    import threading
-
-    from maxmq_amd import capi
-
-    L = capi.lib()
+    single = min(args.latency_topics, n)
+    run(1, 50)  # warm
+    one = run(1, single)
+    out = {"unit": "us", "calls": single, "p50": one["p50_us"], "p90": one["p90_us"], "p99": one["p99_us"],
+           "topics_per_s": one["topics_per_s"], "driver": "native threads (tools/conc_driver.cpp)"}
     T, per = args.conc_threads, args.conc_calls
-
-    def run():
-        lat = [[] for _ in range(T)]
-
-        def worker(k):
-            for j in range(per):
-                t = topics[(k * per + j) % len(topics)]
-                res = C.c_void_p()
-                t0 = time.perf_counter()
-                capi.check("mqm_subscribers", L.mqm_subscribers(idx._h, t, len(t), C.byref(res)))
-                lat[k].append(time.perf_counter() - t0)
-                L.mqm_result_free(res)
-
-        ths = [threading.Thread(target=worker, args=(k,)) for k in range(T)]
-        t0 = time.perf_counter()
-        for th in ths:
-            th.start()
-        for th in ths:
-            th.join()
-        dt = time.perf_counter() - t0
-        a = np.concatenate([np.array(x) for x in lat]) * 1e6
-        return {"topics_per_s": T * per / dt, "p50_us": float(np.median(a)), "p99_us": float(np.percentile(a, 99))}
-
-    run()  # warm: every caller's context (stream, workspace) exists before timing
-    out = {"threads": T, "calls_per_thread": per, "direct": run()}
+    run(T, 20)  # warm: every caller's context (stream, workspace, pinned blocks) exists before timing
+    conc = {"threads": T, "calls_per_thread": per, "direct": run(T, per)}
     idx.batching_policy(0, 0)  # MQM_CFG_BATCHING on from here
-    run()  # warm the collector's contexts
+    run(T, 20)
     b0, t0_ = idx.batching_stats()
-    out["batched"] = run()
+    conc["batched"] = run(T, per)
     b1, t1 = idx.batching_stats()
-    out["batched"]["mean_batch"] = (t1 - t0_) / max(1, b1 - b0)
+    conc["batched"]["mean_batch"] = (t1 - t0_) / max(1, b1 - b0)
+    out["concurrent"] = conc
     return out
 
 

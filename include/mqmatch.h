@@ -247,6 +247,28 @@ int mqm_batching_stats(mqm_index *h, uint64_t *batches, uint64_t *topics);
 int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t *d_topic_offsets,
                      uint32_t n_topics, void *hip_stream, mqm_device_result *out);
 
+/* ---- queued device matching (steady state) ------------------------------
+ * mqm_match_device waits for its batch.  A broker streaming batches through
+ * the GPU keeps several in flight instead: each caller-owned context holds one
+ * batch's pipeline state and results; mqm_match_device_async queues the whole
+ * pipeline on hip_stream and returns without waiting (no host read-back
+ * before the end: the outputs are sized from the context's earlier batches),
+ * mqm_match_ctx_wait waits for it and returns its result (device buffers owned
+ * by the context, valid until its next call).  A batch that outgrows the
+ * buffers the earlier ones sized is run again inside mqm_match_ctx_wait, sized
+ * exactly (mqm_match_ctx_stats counts those), so the topic buffers must stay
+ * valid until the wait returns.  One batch in flight per context (a second
+ * async call before the wait: MQM_EINVAL); contexts are independent, so
+ * batches on different contexts and streams overlap.  The snapshot a batch
+ * reads is the published one when it was queued. */
+typedef struct mqm_match_ctx mqm_match_ctx;
+int mqm_match_ctx_create(mqm_index *h, mqm_match_ctx **out);
+int mqm_match_ctx_destroy(mqm_match_ctx *ctx);
+int mqm_match_device_async(mqm_match_ctx *ctx, const uint8_t *d_topic_bytes, const uint64_t *d_topic_offsets,
+                           uint32_t n_topics, void *hip_stream);
+int mqm_match_ctx_wait(mqm_match_ctx *ctx, mqm_device_result *out);
+int mqm_match_ctx_stats(mqm_match_ctx *ctx, uint64_t *requeued);
+
 /* ---- Subscription.Identifiers (packets.go:250-259, rule M3) -------------- */
 /* Merge gives every delivery an Identifiers map: {first.Filter:
  * first.Identifier} (kept even when 0) plus {n.Filter: n.Identifier} for

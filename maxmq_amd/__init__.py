@@ -437,6 +437,10 @@ class TopicsIndex:
         check("mqm_dense_device", lib().mqm_dense_device(self._h, C.c_void_p(stream_ptr), C.byref(out)))
         return out
 
+    def match_context(self) -> "MatchContext":
+        """A context of the queued device API (several batches in flight)."""
+        return MatchContext(self)
+
     def match_device(self, d_bytes_ptr: int, d_offs_ptr: int, n: int, stream_ptr: int = 0) -> capi.DeviceResult:
         """Device-resident batch (pointers from e.g. torch tensors); the result's
         device buffers are owned by the index and valid until the next match."""
@@ -444,6 +448,43 @@ class TopicsIndex:
         check("mqm_match_device", lib().mqm_match_device(self._h, C.c_void_p(d_bytes_ptr), C.c_void_p(d_offs_ptr),
                                                          n, C.c_void_p(stream_ptr), C.byref(out)))
         return out
+
+
+class MatchContext:
+    """A caller-owned context of the queued device API (mqm_match_device_async
+    / mqm_match_ctx_wait): one batch in flight at a time; contexts on
+    different streams overlap.  The result's device buffers belong to the
+    context and stay valid until its next submit."""
+
+    def __init__(self, index: "TopicsIndex"):
+        self._index = index  # keeps the index alive
+        self._c = C.c_void_p()
+        check("mqm_match_ctx_create", lib().mqm_match_ctx_create(index._h, C.byref(self._c)))
+
+    def submit(self, d_bytes_ptr: int, d_offs_ptr: int, n: int, stream_ptr: int = 0):
+        check("mqm_match_device_async", lib().mqm_match_device_async(
+            self._c, C.c_void_p(d_bytes_ptr), C.c_void_p(d_offs_ptr), n, C.c_void_p(stream_ptr)))
+
+    def wait(self) -> capi.DeviceResult:
+        out = capi.DeviceResult()
+        check("mqm_match_ctx_wait", lib().mqm_match_ctx_wait(self._c, C.byref(out)))
+        return out
+
+    def requeued(self) -> int:
+        v = C.c_uint64()
+        check("mqm_match_ctx_stats", lib().mqm_match_ctx_stats(self._c, C.byref(v)))
+        return int(v.value)
+
+    def close(self):
+        if self._c:
+            lib().mqm_match_ctx_destroy(self._c)
+            self._c = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def gather_shards(n_topics: int, parts, d_out_offsets_ptr: int, d_out_ptr: int, stream_ptr: int = 0):

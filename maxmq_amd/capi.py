@@ -45,7 +45,8 @@ EXPORTED = [
     "mqm_messages_refs", "mqm_messages_free", "mqm_messages_device", "mqm_identifiers_device",
     "mqm_result_identifiers", "mqm_dense_device", "mqm_gather_shards", "mqm_commit_async", "mqm_commit_poll",
     "mqm_commit_policy", "mqm_commit_state_get", "mqm_snapshot_digest", "mqm_unsubscribe_many", "mqm_load_subscriptions_json",
-    "mqm_debug_fault", "mqm_gather_shards_shared",
+    "mqm_debug_fault", "mqm_gather_shards_shared", "mqm_match_ctx_create", "mqm_match_ctx_destroy",
+    "mqm_match_device_async", "mqm_match_ctx_wait", "mqm_match_ctx_stats",
 ]
 
 
@@ -195,6 +196,11 @@ def lib():
         "mqm_snapshot_digest": ([vp, C.POINTER(u64)], C.c_int),
         "mqm_debug_fault": ([vp, C.c_int, C.c_int], C.c_int),
         "mqm_gather_shards_shared": ([u32, u32, C.POINTER(ShardSharedPart), vp, vp, vp], C.c_int),
+        "mqm_match_ctx_create": ([vp, C.POINTER(vp)], C.c_int),
+        "mqm_match_ctx_destroy": ([vp], C.c_int),
+        "mqm_match_device_async": ([vp, vp, vp, u32, vp], C.c_int),
+        "mqm_match_ctx_wait": ([vp, C.POINTER(DeviceResult)], C.c_int),
+        "mqm_match_ctx_stats": ([vp, C.POINTER(u64)], C.c_int),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

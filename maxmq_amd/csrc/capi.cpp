@@ -132,6 +132,7 @@ struct mqm_index {
   uint64_t builds = 0, last_build_ops = 0;
   double last_build_ms = 0;
   int walk_lanes = 4;
+  bool fast_path = true;  // MQM_NO_FAST=1: small batches also take the batch pipeline (A/B, tests)
   bool overlap = true;  // MQM_NO_OVERLAP=1: merges serialised behind the solo copy (profiling)
   bool async() const { return (cfg.flags & MQM_CFG_ASYNC_COMMIT) != 0; }
   // the device-result API's context (mqm_match_device & follow-ups)
@@ -351,6 +352,82 @@ int fill_info(const SubInfo &s, mqm_sub_info *out) {
 
 bool bad_sub(const mqm_subscription &s) { return s.qos > 2 || s.retain_handling > 3; }
 
+void fill_device_result(const MatchOutput &mo, const Workspace &ws, mqm_device_result *out) {
+  out->n_topics = mo.n_topics;
+  out->n_deliveries = mo.n_deliveries;
+  out->n_shared = mo.n_shared;
+  out->starts = mo.starts;
+  out->counts = mo.counts;
+  out->deliveries = mo.deliveries;
+  out->shared_starts = mo.shared_starts;
+  out->shared_counts = mo.shared_counts;
+  out->shared = mo.shared;
+  out->n_fallback = mo.n_fallback;
+  out->n_big = mo.n_big;
+  for (int i = 0; i < 5; i++) out->fallback_why[i] = ws.why[i];
+  out->n_merge_small = mo.n_merge_small;
+  out->n_merge_wave = mo.n_merge_wave;
+  out->n_solo_ranges = mo.n_solo_ranges;
+  out->n_tier2 = mo.n_tier2;
+  out->n_tier3 = mo.n_tier3;
+  for (int i = 0; i < 3; i++) out->multi_entries[i] = mo.multi_entries[i];
+  out->n_part = mo.n_part;
+}
+
+// a result block laid out like mqm_match_batch's: offsets | shared_offsets |
+// deliveries | shared (16-B aligned parts), from per-topic counts
+struct ResultLayout {
+  uint64_t o_sh = 0, o_d = 0, o_s = 0, total = 0;
+  ResultLayout(uint64_t n1, uint64_t nd, uint64_t ns) {
+    auto up = [](uint64_t b) { return (b + 15) & ~15ull; };
+    o_sh = up(8 * n1);
+    o_d = o_sh + up(8 * n1);
+    o_s = o_d + up(8 * nd);
+    total = o_s + up(4 * ns);
+  }
+};
+
+// the small-batch path's per-topic segments (FastRec: anywhere in the pinned
+// output blocks, in completion order) -> one result block in topic order
+int fast_result(mqm_index *h, const std::shared_ptr<GpuSnapshot> &snap, const FastOutput &fo, mqm_result *r) {
+  const uint32_t n = fo.n_topics;
+  uint64_t nd = 0, ns = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    nd += fo.recs[i].dcount;
+    ns += fo.recs[i].hcount;
+  }
+  const ResultLayout lay(n + 1ull, nd, ns);
+  r->pool = h->pinned;
+  r->blk = h->pinned->get(lay.total, &r->blk_cap);
+  if (!r->blk) {
+    r->pool.reset();
+    return MQM_ENOMEM;
+  }
+  char *B = static_cast<char *>(r->blk);
+  auto *off = reinterpret_cast<uint64_t *>(B), *soff = reinterpret_cast<uint64_t *>(B + lay.o_sh);
+  auto *dl = reinterpret_cast<uint64_t *>(B + lay.o_d);
+  auto *sh = reinterpret_cast<uint32_t *>(B + lay.o_s);
+  uint64_t d = 0, q = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    const FastRec &x = fo.recs[i];
+    off[i] = d;
+    soff[i] = q;
+    if (x.dcount) memcpy(dl + d, fo.dout + x.dbase, 8ull * x.dcount);
+    if (x.hcount) memcpy(sh + q, fo.hout + x.hbase, 4ull * x.hcount);
+    d += x.dcount;
+    q += x.hcount;
+  }
+  off[n] = d;
+  soff[n] = q;
+  r->n = n;
+  r->offsets = off;
+  r->shared_offsets = soff;
+  r->deliveries = reinterpret_cast<const mqm_delivery *>(dl);
+  r->shared = sh;
+  r->snap = snap->host;
+  return MQM_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -395,6 +472,7 @@ int mqm_create(const mqm_config *cfg, mqm_index **out) {
       h->walk_lanes = g == 8 || g == 16 ? g : 4;
     }
     if (const char *e = getenv("MQM_NO_OVERLAP")) h->overlap = atoi(e) == 0;
+    if (const char *e = getenv("MQM_NO_FAST")) h->fast_path = atoi(e) == 0;
     if (ctx_init(h.get(), &h->dev) != MQM_OK) return MQM_EHIP;
     if (h->cfg.flags & MQM_CFG_BATCHING) {
       h->collector_owner = std::make_unique<Collector>(h.get());
@@ -591,25 +669,7 @@ int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t 
     if (rc != 0) return hip_rc(rc);
     c.last_mo = mo;
     c.has_mo = true;
-    out->n_topics = mo.n_topics;
-    out->n_deliveries = mo.n_deliveries;
-    out->n_shared = mo.n_shared;
-    out->starts = mo.starts;
-    out->counts = mo.counts;
-    out->deliveries = mo.deliveries;
-    out->shared_starts = mo.shared_starts;
-    out->shared_counts = mo.shared_counts;
-    out->shared = mo.shared;
-    out->n_fallback = mo.n_fallback;
-    out->n_big = mo.n_big;
-    for (int i = 0; i < 5; i++) out->fallback_why[i] = c.ws.why[i];
-    out->n_merge_small = mo.n_merge_small;
-    out->n_merge_wave = mo.n_merge_wave;
-    out->n_solo_ranges = mo.n_solo_ranges;
-    out->n_tier2 = mo.n_tier2;
-    out->n_tier3 = mo.n_tier3;
-    for (int i = 0; i < 3; i++) out->multi_entries[i] = mo.multi_entries[i];
-    out->n_part = mo.n_part;
+    fill_device_result(mo, c.ws, out);
     return MQM_OK;
   });
 }
@@ -627,6 +687,26 @@ int mqm_match_batch(mqm_index *h, const char *topic_bytes, const uint64_t *topic
     auto c = ctx_acquire(h, &rc);
     if (rc != MQM_OK) return rc;
     auto r = std::make_unique<mqm_result>();
+    const bool want_ids = (h->cfg.flags & MQM_CFG_IDENTIFIERS) != 0;
+    // small batches (the per-publish call shape): the one-launch path, unless
+    // a topic is past one of its capacities (then the pipeline below)
+    if (n_topics <= kFastMaxTopics && !want_ids && h->fast_path) {
+      c->ws.begin(c->stream);
+      FastOutput fo;
+      const int e = match_small(snap->dev, c->ws, topic_bytes, topic_offsets, n_topics, c->stream, &fo);
+      const int e2 = c->ws.end(c->stream);
+      if (e < 0 || e2) {
+        ctx_release(h, std::move(c));
+        return e < 0 ? hip_rc(e) : MQM_EHIP;
+      }
+      if (e == 0) {
+        rc = fast_result(h, snap, fo, r.get());
+        ctx_release(h, std::move(c));
+        if (rc != MQM_OK) return rc;
+        *out = r.release();
+        return MQM_OK;
+      }
+    }
     rc = [&]() -> int {
       Workspace &ws = c->ws;
       const hipStream_t st = c->stream;
@@ -639,7 +719,6 @@ int mqm_match_batch(mqm_index *h, const char *topic_bytes, const uint64_t *topic
       MatchOutput mo;
       if ((e = match_device(snap->dev, ws, d_bytes, d_offs, n_topics, st, &mo)) != 0) return hip_rc(e);
       IdentOutput io;
-      const bool want_ids = (h->cfg.flags & MQM_CFG_IDENTIFIERS) != 0;
       if (want_ids && (e = identifiers_device(snap->dev, ws, st, &io)) != 0) return hip_rc(e);
       DenseOutput dn;
       if ((e = densify(snap->dev, ws, mo, st, &dn)) != 0) return hip_rc(e);
@@ -684,6 +763,97 @@ int mqm_match_batch(mqm_index *h, const char *topic_bytes, const uint64_t *topic
     *out = r.release();
     return MQM_OK;
   });
+}
+
+}  // extern "C"
+
+// a caller-owned context of the queued device API (mqm_match_device_async)
+struct mqm_match_ctx {
+  mqm_index *h = nullptr;
+  MatchCtx c;
+  hipStream_t st = nullptr;
+  const uint8_t *bytes = nullptr;
+  const uint64_t *offs = nullptr;
+  uint32_t n = 0;
+  bool queued = false;
+};
+
+extern "C" {
+
+int mqm_match_ctx_create(mqm_index *h, mqm_match_ctx **out) {
+  if (!h || !out) return MQM_EINVAL;
+  *out = nullptr;
+  return guarded([&] {
+    if (h->cfg.device == MQM_DEVICE_NONE) return MQM_ENODEV;
+    if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
+    auto x = std::make_unique<mqm_match_ctx>();
+    x->h = h;
+    x->c.ws.walk_lanes = h->walk_lanes;
+    x->c.ws.overlap = h->overlap;
+    *out = x.release();
+    return MQM_OK;
+  });
+}
+
+int mqm_match_ctx_destroy(mqm_match_ctx *x) {
+  if (!x) return MQM_EINVAL;
+  if (x->queued) (void)hipStreamSynchronize(x->st);
+  (void)x->c.ws.drain();
+  delete x;
+  return MQM_OK;
+}
+
+int mqm_match_device_async(mqm_match_ctx *x, const uint8_t *d_topic_bytes, const uint64_t *d_topic_offsets,
+                           uint32_t n_topics, void *hip_stream) {
+  if (!x || x->queued || (n_topics && (!d_topic_bytes || !d_topic_offsets))) return MQM_EINVAL;
+  return guarded([&] {
+    mqm_index *h = x->h;
+    if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
+    std::shared_ptr<GpuSnapshot> snap;
+    int rc = front(h, &snap);
+    if (rc != MQM_OK) return rc;
+    const hipStream_t st = (hipStream_t)hip_stream;
+    x->c.snap = snap;  // held until the next call on this context
+    x->c.has_mo = false;
+    x->c.ws.begin(st);
+    rc = match_enqueue(snap->dev, x->c.ws, d_topic_bytes, d_topic_offsets, n_topics, st, false);
+    if (x->c.ws.end(st)) rc = rc ? rc : -3;
+    if (rc != 0) return hip_rc(rc);
+    x->st = st;
+    x->bytes = d_topic_bytes;
+    x->offs = d_topic_offsets;
+    x->n = n_topics;
+    x->queued = true;
+    return MQM_OK;
+  });
+}
+
+int mqm_match_ctx_wait(mqm_match_ctx *x, mqm_device_result *out) {
+  if (!x || !out || !x->queued) return MQM_EINVAL;
+  return guarded([&] {
+    x->queued = false;
+    if (hipSetDevice(x->h->cfg.device) != hipSuccess) return MQM_EHIP;
+    MatchOutput mo;
+    int rc = match_collect(x->c.ws, x->st, &mo);
+    if (rc == 1) {  // outgrew the buffers earlier calls sized: again, sized exactly
+      x->c.ws.begin(x->st);
+      rc = match_enqueue(x->c.snap->dev, x->c.ws, x->bytes, x->offs, x->n, x->st, true);
+      if (x->c.ws.end(x->st)) rc = rc ? rc : -3;
+      if (rc == 0) rc = match_collect(x->c.ws, x->st, &mo);
+      if (rc == 0) x->c.ws.requeued++;
+    }
+    if (rc != 0) return hip_rc(rc);
+    x->c.last_mo = mo;
+    x->c.has_mo = true;
+    fill_device_result(mo, x->c.ws, out);
+    return MQM_OK;
+  });
+}
+
+int mqm_match_ctx_stats(mqm_match_ctx *x, uint64_t *requeued) {
+  if (!x || !requeued) return MQM_EINVAL;
+  *requeued = x->c.ws.requeued;
+  return MQM_OK;
 }
 
 int mqm_identifiers_device(mqm_index *h, void *hip_stream, mqm_device_identifiers *out) {
@@ -886,11 +1056,16 @@ void mqm_messages_free(mqm_messages *m) { delete m; }
 
 namespace {
 
-// MQM_CFG_BATCHING: single-topic calls queue a request and wait; one thread
-// drains the queue into mqm_match_batch and hands every caller its own
-// single-topic result (a pinned block from the index's pool, split off the
-// batch result).  Calls that arrive while a batch runs form the next one, so
-// batches grow with the offered load and an idle index adds no latency.
+// MQM_CFG_BATCHING: single-topic calls queue a request and wait; worker
+// threads drain the queue into GPU batches and hand every caller its own
+// single-topic result (a pinned block from the index's pool).  Calls that
+// arrive while a batch runs form the next one, so batches grow with the
+// offered load and an idle index adds no latency.  Two workers by default:
+// while one waits for its batch on the GPU, the other gathers and launches
+// the next (each borrows its own context: workspace and stream).  A batch
+// takes the small-batch path (fast.hip: one launch, results read straight
+// from its pinned blocks), or mqm_match_batch when Identifiers are on or a
+// topic is past that path's capacities.
 struct Collector {
   struct Req {
     const char *topic;
@@ -906,16 +1081,18 @@ struct Collector {
   bool stop = false;
   uint32_t max_batch = 8192, linger_us = 0;
   uint64_t batches = 0, topics = 0;
-  std::thread th;
+  std::vector<std::thread> ths;
 
-  explicit Collector(mqm_index *idx) : h(idx), th([this] { run(); }) {}
+  explicit Collector(mqm_index *idx, int workers = 2) : h(idx) {
+    for (int i = 0; i < workers; i++) ths.emplace_back([this] { run(); });
+  }
   ~Collector() {
     {
       std::lock_guard<std::mutex> g(mu);
       stop = true;
     }
     cv.notify_all();
-    th.join();
+    for (auto &t : ths) t.join();
   }
 
   int submit(const char *topic, size_t len, mqm_result **out) {
@@ -931,12 +1108,11 @@ struct Collector {
     return r.rc;
   }
 
-  // topic i of batch result b as a result of its own
-  static int split(mqm_index *h, const mqm_result *b, uint32_t i, mqm_result **out) {
+  // one topic's deliveries / shared candidates as a result of its own
+  static int single(mqm_index *h, std::shared_ptr<const HostSnapshot> hs, const uint64_t *dl, uint64_t d,
+                    const uint32_t *sh, uint64_t sn, const uint32_t *ids, uint64_t in, bool has_ids,
+                    mqm_result **out) {
     auto r = std::make_unique<mqm_result>();
-    const uint64_t d0 = b->offsets[i], d = b->offsets[i + 1] - d0;
-    const uint64_t s0 = b->shared_offsets[i], sn = b->shared_offsets[i + 1] - s0;
-    const uint64_t i0 = b->has_idents ? b->ident_offsets[i] : 0, in = b->has_idents ? b->ident_offsets[i + 1] - i0 : 0;
     auto up = [](uint64_t x) { return (x + 15) & ~15ull; };
     const uint64_t o_sh = 16, o_io = 32, o_d = 48, o_s = o_d + up(8 * d), o_i = o_s + up(4 * sn), total = o_i + up(4 * in);
     r->pool = h->pinned;
@@ -952,22 +1128,62 @@ struct Collector {
     off[1] = d;
     soff[1] = sn;
     ioff[1] = in;
-    if (d) memcpy(B + o_d, b->deliveries + d0, 8 * d);
-    if (sn) memcpy(B + o_s, b->shared + s0, 4 * sn);
-    if (in) memcpy(B + o_i, b->idents + i0, 4 * in);
+    if (d) memcpy(B + o_d, dl, 8 * d);
+    if (sn) memcpy(B + o_s, sh, 4 * sn);
+    if (in) memcpy(B + o_i, ids, 4 * in);
     r->n = 1;
     r->offsets = off;
     r->shared_offsets = soff;
     r->deliveries = reinterpret_cast<const mqm_delivery *>(B + o_d);
     r->shared = reinterpret_cast<const uint32_t *>(B + o_s);
-    if (b->has_idents) {
+    if (has_ids) {
       r->has_idents = true;
       r->ident_offsets = ioff;
       r->idents = reinterpret_cast<const uint32_t *>(B + o_i);
     }
-    r->snap = b->snap;
+    r->snap = std::move(hs);
     *out = r.release();
     return MQM_OK;
+  }
+
+  // topic i of batch result b as a result of its own
+  static int split(mqm_index *h, const mqm_result *b, uint32_t i, mqm_result **out) {
+    const uint64_t d0 = b->offsets[i], d = b->offsets[i + 1] - d0;
+    const uint64_t s0 = b->shared_offsets[i], sn = b->shared_offsets[i + 1] - s0;
+    const uint64_t i0 = b->has_idents ? b->ident_offsets[i] : 0, in = b->has_idents ? b->ident_offsets[i + 1] - i0 : 0;
+    return single(h, b->snap, reinterpret_cast<const uint64_t *>(b->deliveries) + d0, d, b->shared + s0, sn,
+                  b->has_idents ? b->idents + i0 : nullptr, in, b->has_idents, out);
+  }
+
+  // the batch on the small-batch path, every caller's result split off the
+  // pinned blocks; false: not taken (the caller falls back to mqm_match_batch)
+  bool run_fast(const std::vector<Req *> &batch, const std::string &bytes, const std::vector<uint64_t> &offs) {
+    if ((h->cfg.flags & MQM_CFG_IDENTIFIERS) || !h->fast_path || batch.size() > kFastMaxTopics) return false;
+    if (hipSetDevice(h->cfg.device) != hipSuccess) return false;
+    std::shared_ptr<GpuSnapshot> snap;
+    if (front(h, &snap) != MQM_OK) return false;
+    int rc = MQM_OK;
+    auto c = ctx_acquire(h, &rc);
+    if (rc != MQM_OK) return false;
+    c->ws.begin(c->stream);
+    FastOutput fo;
+    const int e = match_small(snap->dev, c->ws, bytes.data(), offs.data(), (uint32_t)batch.size(), c->stream, &fo);
+    const int e2 = c->ws.end(c->stream);
+    if (e != 0 || e2) {
+      ctx_release(h, std::move(c));
+      return false;
+    }
+    for (uint32_t i = 0; i < batch.size(); i++) {
+      const FastRec &x = fo.recs[i];
+      try {
+        batch[i]->rc = single(h, snap->host, fo.dout + x.dbase, x.dcount, fo.hout + x.hbase, x.hcount, nullptr, 0,
+                              false, &batch[i]->res);
+      } catch (const std::bad_alloc &) {
+        batch[i]->rc = MQM_ENOMEM;
+      }
+    }
+    ctx_release(h, std::move(c));
+    return true;
   }
 
   void run() {
@@ -984,6 +1200,7 @@ struct Collector {
         const size_t n = std::min<size_t>(q.size(), max_batch);
         batch.assign(q.begin(), q.begin() + n);
         q.erase(q.begin(), q.begin() + n);
+        if (!q.empty()) cv.notify_one();  // more queued than one batch: wake another worker
       }
       bytes.clear();
       offs.assign(1, 0);
@@ -991,19 +1208,27 @@ struct Collector {
         bytes.append(r->topic, r->len);
         offs.push_back(bytes.size());
       }
-      mqm_result *b = nullptr;
-      const int rc = mqm_match_batch(h, bytes.data(), offs.data(), (uint32_t)batch.size(), &b);
-      for (uint32_t i = 0; i < batch.size(); i++) {
-        batch[i]->rc = rc;
-        if (rc == MQM_OK) {
-          try {
-            batch[i]->rc = split(h, b, i, &batch[i]->res);
-          } catch (const std::bad_alloc &) {
-            batch[i]->rc = MQM_ENOMEM;
+      bool fast = false;
+      try {
+        fast = run_fast(batch, bytes, offs);
+      } catch (...) {
+        fast = false;
+      }
+      if (!fast) {
+        mqm_result *b = nullptr;
+        const int rc = mqm_match_batch(h, bytes.data(), offs.data(), (uint32_t)batch.size(), &b);
+        for (uint32_t i = 0; i < batch.size(); i++) {
+          batch[i]->rc = rc;
+          if (rc == MQM_OK) {
+            try {
+              batch[i]->rc = split(h, b, i, &batch[i]->res);
+            } catch (const std::bad_alloc &) {
+              batch[i]->rc = MQM_ENOMEM;
+            }
           }
         }
+        if (b) mqm_result_free(b);
       }
-      if (b) mqm_result_free(b);
       {
         std::lock_guard<std::mutex> g(mu);
         for (Req *r : batch) r->done = true;

@@ -10,6 +10,42 @@
 
 namespace mqm {
 
+// ---- small-batch path (fast.hip) --------------------------------------------
+// device counters of one k_fast launch; the last workgroup resets them
+struct FastCtl {
+  unsigned long long dcur, hcur;  // delivery / shared-candidate slots reserved
+  unsigned int flags, done;
+};
+enum : uint32_t { kFastFallback = 1u, kFastOverflow = 2u };
+// topic t's result: deliveries dout[dbase .. + dcount), shared hout[hbase .. + hcount)
+struct FastRec {
+  uint32_t dbase, dcount, hbase, hcount;
+};
+struct FastStatus {  // written by the last workgroup (pinned)
+  unsigned long long d_total, h_total;
+  unsigned int flags, done;
+};
+// pinned, device-mapped host blocks of one context (grown, never shrunk)
+struct FastArena {
+  char *in_bytes = nullptr;
+  uint64_t *in_offs = nullptr;
+  FastRec *recs = nullptr;
+  uint64_t *dout = nullptr;  // {client, packed} deliveries (mqm_delivery)
+  uint32_t *hout = nullptr;  // shared-subscription ids
+  FastStatus *status = nullptr;
+  size_t in_cap = 0, offs_cap = 0, rec_cap = 0, dout_cap = 0, hout_cap = 0, status_cap = 0;
+  FastCtl *ctl = nullptr;  // device
+  uint32_t grid = 0;       // resident k_fast workgroups
+  ~FastArena();
+};
+struct FastOutput {
+  uint32_t n_topics = 0;
+  uint64_t n_slots = 0, n_shared_slots = 0;  // reserved (raw-entry upper bounds)
+  const FastRec *recs = nullptr;             // pinned host, n_topics
+  const uint64_t *dout = nullptr;            // pinned host
+  const uint32_t *hout = nullptr;            // pinned host
+};
+
 // Grow-only device buffers reused across batches (no allocation in steady state).
 struct Workspace {
   enum Slot {
@@ -35,11 +71,21 @@ struct Workspace {
   // why the last batch's DFS topics left the bounded path:
   // frontier, hits, cached levels, shared hits, raw entries
   uint32_t why[5] = {0, 0, 0, 0, 0};
+  // the batch pipeline's queued calls (match_enqueue / match_collect): every
+  // output buffer sized by an earlier call (caps_known), the DFS list capacity
+  // a queued call assumes, the call in flight, and how many queued calls had
+  // to be run again exact
+  bool caps_known = false, pending = false, pend_exact = false;
+  uint32_t dfs_cap = 0;
+  uint64_t requeued = 0;
   // the last match_device call (identifiers_device works on its records)
   bool last_valid = false;
   uint32_t last_n = 0, last_n_dfs = 0;
   const uint8_t *last_bytes = nullptr;
   const uint64_t *last_offs = nullptr;
+
+  // the small-batch path's pinned blocks (fast.hip)
+  FastArena fast;
 
   // optional kernel timing (mqm_profile_*): events on the launch stream
   bool profile = false;
@@ -95,6 +141,7 @@ struct MatchOutput {
   uint64_t n_solo_ranges = 0;                     // solo copy descriptors (hits with solo entries)
   uint64_t multi_entries[3] = {0, 0, 0};  // multi entries merged by the three workgroup tiers
   uint32_t n_part = 0;                    // ... of the third tier's topics, merged in client-hash partitions
+  bool exact = false;                     // sized by its own read-back (the first call of a workspace, or a re-run)
 };
 
 // words[i] = subs[i].word & kPackedMask for i < n (snapshot upload, on `st`)
@@ -102,10 +149,27 @@ int derive_words(const SubEnt *subs, uint32_t *words, uint64_t n, hipStream_t st
 // nflags[i] = nodes[i].sh_cnt_flags >> 24 for i < n (snapshot upload, on `st`)
 int derive_node_flags(const NodeDesc *nodes, uint8_t *nflags, uint64_t n, hipStream_t st);
 
-// Runs walk -> scan -> dedupe (small / big / DFS) on `st`; returns 0 or a
-// negative MQM_E* code.
+// Runs walk -> scan -> dedupe (small / big / DFS) on `st` and waits for it;
+// returns 0 or a negative MQM_E* code.
 int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes, const uint64_t *d_offs,
                  uint32_t n, hipStream_t st, MatchOutput *out);
+// The same in two halves: queue the whole pipeline on `st` (exact: size the
+// outputs by a read-back after the walk; otherwise from earlier calls, no
+// host sync), then wait and read its counters.  match_collect returns 1 when
+// the queued call outgrew the buffers earlier calls sized (run it again with
+// exact = true; the inputs must still hold the batch).
+int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes, const uint64_t *d_offs, uint32_t n,
+                  hipStream_t st, bool exact);
+int match_collect(Workspace &ws, hipStream_t st, MatchOutput *out);
+
+// Small batches (the per-publish call shape): one kernel over host topics
+// (bytes[offs[0] .. offs[n])), results in the workspace's pinned blocks, valid
+// until the next call on `ws`.  Synchronises `st`.  Returns 0, 1 when a topic
+// is past a capacity of this path (the caller runs the batch pipeline), or a
+// negative MQM_E* code.
+constexpr uint32_t kFastMaxTopics = 4096;
+int match_small(const DeviceSnapshot &s, Workspace &ws, const char *bytes, const uint64_t *offs, uint32_t n,
+                hipStream_t st, FastOutput *out);
 
 // Identifiers support for the last match_device call on `ws` (its topic
 // buffers must still hold the batch): per topic, the sids of the gathered

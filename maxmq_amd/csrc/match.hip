@@ -183,7 +183,13 @@ struct Counters {              // zeroed before every batch
   unsigned int n_part;         // k_multi_part: Ms > 3072
   unsigned int n_shlist;       // k_shared: topics with shared candidates
   unsigned long long m_sum[3]; // multi entries of the k_multi<1024> / <2048> / <4096> + k_multi_part lists
-  unsigned int oob;            // a store fell outside its output buffer (never expected)
+  unsigned int oob;            // a store fell outside its output buffer (queued calls: buffers sized
+                               //   from an earlier call were too small; the call is re-run)
+  unsigned int cap_ovf;        // queued calls: the DFS lists / table / tails did not fit (re-run)
+  // what the call needed (k_totals / k_dfs_prep): the next call's capacities
+  unsigned long long s_total, h_total, n_desc;  // raw-entry slots, shared slots, solo descriptors
+  unsigned long long tab_total, dfs_raw, dfs_h; // DFS: dedupe table, raw entries, shared candidates
+  unsigned long long d_sum, h_sum;              // deliveries, shared candidates (after dedupe)
 #if MQM_WALK_STATS
   unsigned long long st_probe, st_miss, st_desc;
 #endif
@@ -208,6 +214,7 @@ struct Outputs {
   // capacities of dout / hout in entries: every store is checked against them
   // (a wrong offset becomes a reported error, never an out-of-bounds write)
   uint64_t dcap, hcap;
+  uint32_t dfs_cap;  // DFS topics raw_cnt / raw_h / tab_off hold
 };
 
 constexpr int kTopicWords = (2 * kLMax + 8 * kICap + kStage) / 4;
@@ -856,8 +863,12 @@ __global__ __launch_bounds__(256) void k_shared(Outputs o, const uint32_t *__res
 // holding (or, in a gap, preceding) its first position; windows before the
 // first descriptor map to it
 constexpr uint32_t kWin = 4096;
-__global__ __launch_bounds__(256) void k_winmap(const uint4 *__restrict__ desc, uint64_t nd, uint64_t total,
-                                                uint32_t *__restrict__ win) {
+// (counts read on the device: nd = solo descriptors, clamped to their buffer;
+// total = solo output positions; windows past win_cap flag the call)
+__global__ __launch_bounds__(256) void k_winmap(const uint4 *__restrict__ desc, const uint64_t *__restrict__ nd_ptr,
+                                                uint64_t desc_cap, const uint64_t *__restrict__ total_ptr,
+                                                uint32_t *__restrict__ win, uint64_t win_cap, unsigned int *oob) {
+  const uint64_t nd = min(*nd_ptr, desc_cap), total = *total_ptr;
   for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nd; j += (uint64_t)gridDim.x * blockDim.x) {
     const uint4 a = desc[j];
     const uint64_t d = a.z | ((uint64_t)a.w << 32);
@@ -867,7 +878,8 @@ __global__ __launch_bounds__(256) void k_winmap(const uint4 *__restrict__ desc, 
       e = b.z | ((uint64_t)b.w << 32);
     }
     const uint64_t lo = j == 0 ? 0 : (d + kWin - 1) / kWin, hi = (e + kWin - 1) / kWin;
-    for (uint64_t w = lo; w < hi; w++) win[w] = (uint32_t)j;
+    if (hi > win_cap) atomicOr(oob, 1u);
+    for (uint64_t w = lo; w < hi && w < win_cap; w++) win[w] = (uint32_t)j;
   }
 }
 
@@ -888,9 +900,12 @@ struct alignas(16) WinLds {
 };
 
 __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_eu(8))) void k_wincopy(
-    DeviceSnapshot s, const uint4 *__restrict__ desc, uint64_t nd, const uint32_t *__restrict__ win, uint64_t nwin,
-    uint64_t total, uint32_t *__restrict__ out, uint64_t cap, unsigned int *oob) {
+    DeviceSnapshot s, const uint4 *__restrict__ desc, const uint64_t *__restrict__ nd_ptr, uint64_t desc_cap,
+    const uint32_t *__restrict__ win, uint64_t win_cap, const uint64_t *__restrict__ total_ptr,
+    uint32_t *__restrict__ out, uint64_t cap, unsigned int *oob) {
   __shared__ WinLds lds_all[kEmitWaves];
+  const uint64_t nd = min(*nd_ptr, desc_cap), total = *total_ptr;
+  const uint64_t nwin = min((total + kWin - 1) / kWin, win_cap);
   const int lane = threadIdx.x & (kWave - 1);
   WinLds &L = lds_all[threadIdx.x / kWave];
   // words through a buffer descriptor: 32-bit offsets, bounds-checked reads
@@ -1314,7 +1329,10 @@ __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *
   uint64_t *key1 = key0 + max_levels;
   uint32_t *stk = reinterpret_cast<uint32_t *>(key1 + max_levels);
   const int lane = threadIdx.x;
-  const uint32_t cnt = o.ctr->n_dfs;
+  // raw_cnt / raw_h / tab_off hold dfs_cap topics (o.dfs_cap); a longer list
+  // (or DFS tails that do not fit) makes k_dfs_prep flag the call for a re-run
+  const uint32_t cnt = min(o.ctr->n_dfs, o.dfs_cap);
+  if ((kPhase == 1 || kPhase == 2) && o.ctr->cap_ovf) return;
   for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
     const uint32_t t = o.dfs_list[i];
     const uint64_t off = toffs[t];
@@ -1545,13 +1563,78 @@ __global__ __launch_bounds__(256) void k_ident(DeviceSnapshot s, Outputs o, uint
   }
 }
 
-__global__ void k_table_sizes(const uint64_t *__restrict__ raw_cnt, const Counters *__restrict__ ctr,
-                              uint64_t *__restrict__ sizes) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= ctr->n_dfs) return;
-  uint64_t sz = 64;
-  while (sz < 2 * raw_cnt[i]) sz <<= 1;
-  sizes[i] = sz;
+// DFS sizing on the device (one workgroup): per DFS topic a dedupe table of
+// the next power of two >= 2 x its raw entries (>= 64), their offsets, the
+// DFS tails' start after the scanned segments, the totals — and the capacity
+// check of a queued call (its buffers were sized from an earlier call)
+__global__ __launch_bounds__(256) void k_dfs_prep(Counters *ctr, const uint64_t *__restrict__ raw_cnt,
+                                                  const uint64_t *__restrict__ raw_h, uint64_t *__restrict__ tab_off,
+                                                  uint32_t dfs_cap, uint64_t tab_cap,
+                                                  const uint64_t *__restrict__ s_tot_ptr,
+                                                  const uint64_t *__restrict__ h_tot_ptr, uint64_t dcap, uint64_t hcap) {
+  __shared__ unsigned long long wsum[4], wraw[4], wh[4];
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+  const uint32_t nd = ctr->n_dfs, n = min(nd, dfs_cap);
+  unsigned long long run = 0, raw = 0, hh = 0;
+  for (uint32_t b = 0; b < n; b += 256) {
+    const uint32_t i = b + tid;
+    unsigned long long sz = 0;
+    if (i < n) {
+      sz = 64;
+      while (sz < 2 * raw_cnt[i]) sz <<= 1;
+      raw += raw_cnt[i];
+      hh += raw_h[i];
+    }
+    unsigned long long inc = sz;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const unsigned long long u = shfl64(inc, max(lane - d, 0));
+      if (lane >= d) inc += u;
+    }
+    if (lane == kWave - 1) wsum[wid] = inc;
+    __syncthreads();
+    unsigned long long before = run;
+    for (int k = 0; k < wid; k++) before += wsum[k];
+    if (i < n) tab_off[i] = before + inc - sz;
+    for (int k = 0; k < 4; k++) run += wsum[k];
+    __syncthreads();
+  }
+#pragma unroll
+  for (int d = kWave / 2; d > 0; d >>= 1) {
+    raw += shfl64(raw, lane ^ d);
+    hh += shfl64(hh, lane ^ d);
+  }
+  if (lane == 0) wraw[wid] = raw, wh[wid] = hh;
+  __syncthreads();
+  if (tid == 0) {
+    raw = wraw[0] + wraw[1] + wraw[2] + wraw[3];
+    hh = wh[0] + wh[1] + wh[2] + wh[3];
+    tab_off[n] = run;
+    const unsigned long long st = *s_tot_ptr, ht = *h_tot_ptr;
+    ctr->dtail = st;
+    ctr->htail = ht;
+    ctr->tab_total = run;
+    ctr->dfs_raw = raw;
+    ctr->dfs_h = hh;
+    if (nd > dfs_cap || run > tab_cap || st + raw > dcap || ht + hh > hcap) ctr->cap_ovf = 1;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_zero_tab(unsigned long long *__restrict__ tab, const Counters *ctr,
+                                                  uint64_t tab_cap) {
+  const uint64_t n = 2 * min((uint64_t)ctr->tab_total, tab_cap);  // GEnt = two 64-bit words
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    tab[i] = 0;
+}
+
+// what the call needed, for the host (read back once, at the end)
+__global__ void k_totals(Counters *ctr, const uint64_t *__restrict__ dstart, const uint64_t *__restrict__ hstart,
+                         const uint64_t *__restrict__ desc_start, uint32_t n) {
+  if (threadIdx.x == 0) {
+    ctr->s_total = dstart[n];
+    ctr->h_total = hstart[n];
+    ctr->n_desc = desc_start[n];
+  }
 }
 
 // segments -> dense CSR (one wavefront per topic); deliveries resolved to
@@ -1741,9 +1824,11 @@ int Workspace::grow_keep(Slot s, size_t used_bytes, size_t need, hipStream_t st)
   return 0;
 }
 
+// pinned scratch: the batch pipeline's Counters at 0, small read-backs at 256
+constexpr size_t kPinnedBytes = 512, kPinnedU64 = 256;
 uint64_t *Workspace::pinned_u64() {
-  if (!host_pinned && hipHostMalloc(&host_pinned, 256, hipHostMallocDefault) != hipSuccess) return nullptr;
-  return reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(host_pinned) + 128);
+  if (!host_pinned && hipHostMalloc(&host_pinned, kPinnedBytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+  return reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(host_pinned) + kPinnedU64);
 }
 
 Workspace::~Workspace() {
@@ -1805,9 +1890,6 @@ static int scan_offsets(Workspace &ws, const uint32_t *counts, uint64_t *offs, u
   return scan_offsets_it(ws, hipcub::TransformInputIterator<uint64_t, Widen, const uint32_t *>(counts, Widen{}), offs,
                          n, st);
 }
-static int scan_offsets_u64(Workspace &ws, const uint64_t *counts, uint64_t *offs, uint32_t n, hipStream_t st) {
-  return scan_offsets_it(ws, counts, offs, n, st);
-}
 template <class T>
 static int scan_offsets_it(Workspace &ws, T counts, uint64_t *offs, uint32_t n, hipStream_t st) {
   static_assert(sizeof(typename std::iterator_traits<T>::value_type) == 8, "64-bit accumulation");
@@ -1820,9 +1902,34 @@ static int scan_offsets_it(Workspace &ws, T counts, uint64_t *offs, uint32_t n, 
   return 0;
 }
 
-int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes, const uint64_t *d_offs,
-                 uint32_t n, hipStream_t st, MatchOutput *out) {
+// ---------------------------------------------------------------------------
+// One batch = match_enqueue (every launch of the pipeline, queued on st) +
+// match_collect (wait, read the counters back once).
+//   exact  : the first call of a workspace (or after an overflow): one
+//            read-back after the walk and the scans sizes every output buffer
+//            and picks the merge kernels that have work (and one more for the
+//            DFS tails when a topic took that path);
+//   queued : every later call: no read-back before the end — the output
+//            buffers are the ones earlier calls sized, every kernel reads its
+//            count from the device (an empty list costs an empty launch), and
+//            every store is checked against its buffer; a call that needed
+//            more reports it (Counters::oob / cap_ovf and the sizes it needed)
+//            and match_device runs it again, exact.  So consecutive batches
+//            queue back to back on a stream, on several streams at once
+//            (one workspace each), with no host round trip in between.
+// ---------------------------------------------------------------------------
+static Counters *pinned_counters(Workspace &ws) {
+  if (!ws.pinned_u64()) return nullptr;
+  static_assert(sizeof(Counters) <= kPinnedU64, "pinned layout");
+  return reinterpret_cast<Counters *>(ws.host_pinned);
+}
+
+int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes, const uint64_t *d_offs, uint32_t n,
+                  hipStream_t st, bool exact) {
   using W = Workspace;
+  if (ws.pending) return -1;  // one call in flight per workspace (collect it first)
+  // queued calls need every output buffer sized by an earlier call
+  exact = exact || !ws.caps_known;
   if (ws.get(W::kSCount, sizeof(uint32_t) * (n + 1)) || ws.get(W::kHCount, sizeof(uint32_t) * (n + 1)) ||
       ws.get(W::kDCount, sizeof(uint32_t) * (n + 1)) || ws.get(W::kDStart, sizeof(uint64_t) * (n + 1)) ||
       ws.get(W::kHStart, sizeof(uint64_t) * (n + 1)) || ws.get(W::kCls, n + 1) ||
@@ -1830,10 +1937,9 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
       ws.get(W::kRecs, sizeof(uint32_t) * kRecStrideAlloc * ((uint64_t)n + 1)) || ws.get(W::kCounters, 256) ||
       ws.get(W::kNSolo, sizeof(uint32_t) * (n + 1)) || ws.get(W::kDescStart, sizeof(uint64_t) * (n + 1)))
     return -2;
-  if (!ws.host_pinned && hipHostMalloc(&ws.host_pinned, 256, hipHostMallocDefault) != hipSuccess) return -2;
-  Counters *hc = reinterpret_cast<Counters *>(ws.host_pinned);
-  uint64_t *hp = reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(ws.host_pinned) + 128);
-  static_assert(sizeof(Counters) <= 128, "pinned layout");
+  Counters *hc = pinned_counters(ws);
+  if (!hc) return -2;
+  uint64_t *hp = ws.pinned_u64();
 
   Outputs o;
   o.scount = (uint32_t *)ws.ptr(W::kSCount);
@@ -1847,11 +1953,11 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   o.recs = (uint32_t *)ws.ptr(W::kRecs);
   o.ctr = (Counters *)ws.ptr(W::kCounters);
   o.nsolo = (uint32_t *)ws.ptr(W::kNSolo);
+  o.perm = nullptr;
   auto *desc_start = (uint64_t *)ws.ptr(W::kDescStart);
   const int walk_g = ws.walk_lanes;
   HIP_TRY(hipMemsetAsync(o.ctr, 0, sizeof(Counters), st));
   mark(ws, 0, st);
-  o.perm = nullptr;
 #if MQM_WALK_SORT
   if (n > 0) {
     if (ws.get(W::kPerm, sizeof(uint32_t) * (n + 1)) || ws.get(W::kPermBins, sizeof(unsigned int) * kLenBins))
@@ -1888,7 +1994,7 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   if (scan_offsets(ws, (const uint32_t *)o.scount, o.dstart, n, st) ||
       scan_offsets(ws, (const uint32_t *)o.hcount, o.hstart, n, st) || scan_offsets(ws, o.nsolo, desc_start, n, st))
     return -3;
-  // merge lists, counted before the one host sync that sizes the outputs
+  // merge lists
   const W::Slot list_slots[kNLists] = {W::kListS, W::kListW, W::kListT1, W::kListT2, W::kListT3, W::kListP, W::kListH};
   Lists lists;
   for (int l = 0; l < kNLists; l++) {
@@ -1901,70 +2007,94 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
                        o.hcount, n, lists, lcount, o.ctr->m_sum);
     HIP_TRY(hipGetLastError());
   }
-  HIP_TRY(hipMemcpyAsync(hc, o.ctr, sizeof(Counters), hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipMemcpyAsync(hp, o.dstart + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipMemcpyAsync(hp + 1, o.hstart + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipMemcpyAsync(hp + 3, desc_start + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
-  const uint32_t n_dfs = hc->n_dfs;
-  const uint64_t s_total = hp[0], h_total = hp[1], n_desc = hp[3];
-  ws.last_valid = true;
-  ws.last_n = n;
-  ws.last_bytes = d_bytes;
-  ws.last_offs = d_offs;
-  ws.last_n_dfs = n_dfs;
-  for (int i = 0; i < 5; i++) ws.why[i] = hc->why[i];
-
-  // DFS phase 0: exact raw / shared counts size the tail regions
-  uint64_t dfs_raw = 0, dfs_h = 0, tab_total = 0;
+  hipLaunchKernelGGL(k_totals, dim3(1), dim3(64), 0, st, o.ctr, o.dstart, o.hstart, desc_start, n);
+  HIP_TRY(hipGetLastError());
+  if (exact) {  // the one read-back that sizes the outputs
+    HIP_TRY(hipMemcpyAsync(hc, o.ctr, sizeof(Counters), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+  }
+  // DFS topics (a capacity of the walk exceeded): phase 0 counts each one's
+  // raw entries, k_dfs_prep sizes their tables and tails on the device
+  const bool dfs = !exact || hc->n_dfs > 0;
   const uint32_t max_levels = s.height + 1;
   const size_t fb_lds = sizeof(uint32_t) * (((max_levels + 1) & ~1u) + 4 * (2 * max_levels + 8)) +
                         sizeof(uint64_t) * 2 * max_levels;
-  const uint32_t fb_blocks = std::max<uint32_t>(1, std::min<uint32_t>(n_dfs, 4096));
   uint64_t *raw_cnt = nullptr, *raw_h = nullptr, *tab_off = nullptr;
-  if (n_dfs) {
-    if (ws.get(W::kRawCnt, sizeof(uint64_t) * 2 * (n_dfs + 1)) || ws.get(W::kTabOff, sizeof(uint64_t) * (n_dfs + 2)) ||
-        ws.get(W::kTabSize, sizeof(uint64_t) * (n_dfs + 1)))
+  uint32_t dfs_cap = 0;
+  if (dfs) {
+    dfs_cap = exact ? hc->n_dfs : ws.dfs_cap;
+    if (ws.get(W::kRawCnt, sizeof(uint64_t) * 2 * (dfs_cap + 1)) || ws.get(W::kTabOff, sizeof(uint64_t) * (dfs_cap + 2)))
       return -2;
     raw_cnt = (uint64_t *)ws.ptr(W::kRawCnt);
-    raw_h = raw_cnt + n_dfs + 1;
+    raw_h = raw_cnt + dfs_cap + 1;
     tab_off = (uint64_t *)ws.ptr(W::kTabOff);
-    auto *tab_size = (uint64_t *)ws.ptr(W::kTabSize);
-    hipLaunchKernelGGL(k_dfs<0>, dim3(fb_blocks), dim3(kWave), fb_lds, st, s, d_bytes, d_offs, o, raw_cnt, raw_h,
-                       nullptr, nullptr, max_levels);
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_table_sizes, dim3((n_dfs + 255) / 256), dim3(256), 0, st, raw_cnt, o.ctr, tab_size);
-    HIP_TRY(hipGetLastError());
-    if (scan_offsets_u64(ws, tab_size, tab_off, n_dfs, st)) return -3;
-    std::vector<uint64_t> rc(2 * (n_dfs + 1));
-    HIP_TRY(hipMemcpyAsync(rc.data(), raw_cnt, sizeof(uint64_t) * 2 * (n_dfs + 1), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(hp, tab_off + n_dfs, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    tab_total = hp[0];
-    for (uint32_t i = 0; i < n_dfs; i++) {
-      dfs_raw += rc[i];
-      dfs_h += rc[n_dfs + 1 + i];
-    }
   }
-  // outputs: scanned segments, then the DFS tails
-  const uint64_t n_win = (s_total + kWin - 1) / kWin;
-  if (ws.get(W::kDOut, sizeof(uint32_t) * (s_total + dfs_raw + 1)) ||
-      ws.get(W::kHOut, sizeof(uint32_t) * (h_total + dfs_h + 1)) || ws.get(W::kDesc, sizeof(uint4) * (n_desc + 1)) ||
-      ws.get(W::kWin, sizeof(uint32_t) * (n_win + 1)))
+  o.dfs_cap = dfs_cap;
+  const uint32_t fb_blocks = exact ? std::max<uint32_t>(1, std::min<uint32_t>(hc->n_dfs, 4096)) : 1024;
+  uint64_t dcap, hcap, desc_cap, win_cap, tab_cap = 0;
+  if (exact) {
+    if (dfs) {
+      hipLaunchKernelGGL(k_dfs<0>, dim3(fb_blocks), dim3(kWave), fb_lds, st, s, d_bytes, d_offs, o, raw_cnt, raw_h,
+                         nullptr, nullptr, max_levels);
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(k_dfs_prep, dim3(1), dim3(256), 0, st, o.ctr, raw_cnt, raw_h, tab_off, dfs_cap, ~0ull,
+                         o.dstart + n, o.hstart + n, ~0ull, ~0ull);
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipMemcpyAsync(hc, o.ctr, sizeof(Counters), hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+    }
+    dcap = hc->s_total + hc->dfs_raw;
+    hcap = hc->h_total + hc->dfs_h;
+    desc_cap = hc->n_desc;
+    win_cap = (hc->s_total + kWin - 1) / kWin;
+    tab_cap = hc->tab_total;
+  } else {  // what the buffers hold (one element kept spare, as the exact sizing does)
+    auto cap_of = [&](W::Slot sl, size_t elem) -> uint64_t {
+      const size_t c = ws.bufs[sl].cap / elem;
+      return c ? c - 1 : 0;
+    };
+    dcap = cap_of(W::kDOut, sizeof(uint32_t));
+    hcap = cap_of(W::kHOut, sizeof(uint32_t));
+    desc_cap = cap_of(W::kDesc, sizeof(uint4));
+    win_cap = cap_of(W::kWin, sizeof(uint32_t));
+    tab_cap = std::max<uint64_t>(cap_of(W::kTable, sizeof(GEnt)), 1u << 16);
+  }
+  if (ws.get(W::kDOut, sizeof(uint32_t) * (dcap + 1)) || ws.get(W::kHOut, sizeof(uint32_t) * (hcap + 1)) ||
+      ws.get(W::kDesc, sizeof(uint4) * (desc_cap + 1)) || ws.get(W::kWin, sizeof(uint32_t) * (win_cap + 1)))
     return -2;
   o.dout = (uint32_t *)ws.ptr(W::kDOut);
   o.hout = (uint32_t *)ws.ptr(W::kHOut);
-  o.dcap = s_total + dfs_raw;
-  o.hcap = h_total + dfs_h;
+  o.dcap = dcap;
+  o.hcap = hcap;
   auto *desc = (uint4 *)ws.ptr(W::kDesc);
   auto *win = (uint32_t *)ws.ptr(W::kWin);
+  GEnt *tab = nullptr;
+  if (dfs) {
+    if (ws.get(W::kTable, sizeof(GEnt) * (tab_cap + 1))) return -2;
+    tab = (GEnt *)ws.ptr(W::kTable);
+    if (!exact) {  // sized on the device, checked against the buffers above
+      hipLaunchKernelGGL(k_dfs<0>, dim3(fb_blocks), dim3(kWave), fb_lds, st, s, d_bytes, d_offs, o, raw_cnt, raw_h,
+                         nullptr, nullptr, max_levels);
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(k_dfs_prep, dim3(1), dim3(256), 0, st, o.ctr, raw_cnt, raw_h, tab_off, dfs_cap, tab_cap,
+                         o.dstart + n, o.hstart + n, dcap, hcap);
+      HIP_TRY(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_zero_tab, dim3(exact ? (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((tab_cap + 127) / 128, 4096))
+                                              : 1024),
+                       dim3(256), 0, st, reinterpret_cast<unsigned long long *>(tab), o.ctr, tab_cap);
+    HIP_TRY(hipGetLastError());
+  }
 
   mark(ws, 2, st);
   static_assert(kWave * kEmitWaves == kBigThreads, "resident_blocks assumes 256-thread blocks");
   if (n > 0) {
     // merges on the side stream, concurrently with the solo copy (they write
-    // disjoint parts of dout and dcount: winners after Ss / topics with Ms > 0)
-    const bool merges = hc->n_small || hc->n_wmerge || hc->n_t1 || hc->n_t2 || hc->n_t3 || hc->n_part;
+    // disjoint parts of dout and dcount: winners after Ss / topics with Ms > 0);
+    // a queued call launches every list's kernel (each reads its count)
+    auto has = [&](uint32_t c) { return !exact || c > 0; };
+    const bool merges = has(hc->n_small) || has(hc->n_wmerge) || has(hc->n_t1) || has(hc->n_t2) || has(hc->n_t3) ||
+                        has(hc->n_part);
     const bool side = merges && ws.overlap;
     // persistent grids: with both streams busy, each takes its share of the device
     const uint32_t side_pct = side ? MQM_SIDE_PCT : 100, main_pct = side && MQM_SIDE_PCT < 100 ? 100 - MQM_SIDE_PCT : 100;
@@ -1979,95 +2109,65 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
       if (side && ws.fork(st, &ms)) return -3;
       // MQM_MERGE_BIG_FIRST=1: the workgroup merges first, the small-topic
       // merges last (they fill the device better at the end of the stream)
-#if MQM_MERGE_BIG_FIRST
-      if (hc->n_t1) {
-        hipLaunchKernelGGL(k_multi<1024>, grid(k_multi<1024>), dim3(kBigThreads), 0, ms, s, o, lists.l[kLT1],
-                           lcount + kLT1);
-        HIP_TRY(hipGetLastError());
-      }
-      if (hc->n_t2) {
-        hipLaunchKernelGGL(k_multi<2048>, grid(k_multi<2048>), dim3(kBigThreads), 0, ms, s, o, lists.l[kLT2],
-                           lcount + kLT2);
-        HIP_TRY(hipGetLastError());
-      }
-      if (hc->n_t3) {
-        hipLaunchKernelGGL(k_multi<4096>, grid(k_multi<4096>), dim3(kBigThreads), 0, ms, s, o, lists.l[kLT3],
-                           lcount + kLT3);
-        HIP_TRY(hipGetLastError());
-      }
-      if (hc->n_part) {
-        hipLaunchKernelGGL(k_multi_part, grid(k_multi_part), dim3(kBigThreads), 0, ms, s, o, lists.l[kLPart],
-                           lcount + kLPart);
-        HIP_TRY(hipGetLastError());
-      }
-      if (hc->n_small) {
-        hipLaunchKernelGGL((k_merge_small<6>), grid(k_merge_small<6>), dim3(kWave * kEmitWaves), 0, ms, s, o,
-                           lists.l[kLSmall], lcount + kLSmall);
-        HIP_TRY(hipGetLastError());
-      }
-      if (hc->n_wmerge) {
-        hipLaunchKernelGGL(k_merge, grid(k_merge), dim3(kWave * kEmitWaves), 0, ms, s, o, lists.l[kLWave],
-                           lcount + kLWave);
-        HIP_TRY(hipGetLastError());
-      }
-#else
-      if (hc->n_small) {
-        hipLaunchKernelGGL((k_merge_small<6>), grid(k_merge_small<6>), dim3(kWave * kEmitWaves), 0, ms, s, o,
-                           lists.l[kLSmall], lcount + kLSmall);
-        HIP_TRY(hipGetLastError());
-      }
-      if (hc->n_wmerge) {
-        hipLaunchKernelGGL(k_merge, grid(k_merge), dim3(kWave * kEmitWaves), 0, ms, s, o, lists.l[kLWave],
-                           lcount + kLWave);
-        HIP_TRY(hipGetLastError());
-      }
-      if (hc->n_t1) {
-        hipLaunchKernelGGL(k_multi<1024>, grid(k_multi<1024>), dim3(kBigThreads), 0, ms, s, o, lists.l[kLT1],
-                           lcount + kLT1);
-        HIP_TRY(hipGetLastError());
-      }
-      if (hc->n_t2) {
-        hipLaunchKernelGGL(k_multi<2048>, grid(k_multi<2048>), dim3(kBigThreads), 0, ms, s, o, lists.l[kLT2],
-                           lcount + kLT2);
-        HIP_TRY(hipGetLastError());
-      }
-      if (hc->n_t3) {
-        hipLaunchKernelGGL(k_multi<4096>, grid(k_multi<4096>), dim3(kBigThreads), 0, ms, s, o, lists.l[kLT3],
-                           lcount + kLT3);
-        HIP_TRY(hipGetLastError());
-      }
-      if (hc->n_part) {
-        hipLaunchKernelGGL(k_multi_part, grid(k_multi_part), dim3(kBigThreads), 0, ms, s, o, lists.l[kLPart],
-                           lcount + kLPart);
-        HIP_TRY(hipGetLastError());
-      }
-#endif
+      auto big = [&]() -> int {
+        if (has(hc->n_t1)) {
+          hipLaunchKernelGGL(k_multi<1024>, grid(k_multi<1024>), dim3(kBigThreads), 0, ms, s, o, lists.l[kLT1],
+                             lcount + kLT1);
+          HIP_TRY(hipGetLastError());
+        }
+        if (has(hc->n_t2)) {
+          hipLaunchKernelGGL(k_multi<2048>, grid(k_multi<2048>), dim3(kBigThreads), 0, ms, s, o, lists.l[kLT2],
+                             lcount + kLT2);
+          HIP_TRY(hipGetLastError());
+        }
+        if (has(hc->n_t3)) {
+          hipLaunchKernelGGL(k_multi<4096>, grid(k_multi<4096>), dim3(kBigThreads), 0, ms, s, o, lists.l[kLT3],
+                             lcount + kLT3);
+          HIP_TRY(hipGetLastError());
+        }
+        if (has(hc->n_part)) {
+          hipLaunchKernelGGL(k_multi_part, grid(k_multi_part), dim3(kBigThreads), 0, ms, s, o, lists.l[kLPart],
+                             lcount + kLPart);
+          HIP_TRY(hipGetLastError());
+        }
+        return 0;
+      };
+      auto small = [&]() -> int {
+        if (has(hc->n_small)) {
+          hipLaunchKernelGGL((k_merge_small<6>), grid(k_merge_small<6>), dim3(kWave * kEmitWaves), 0, ms, s, o,
+                             lists.l[kLSmall], lcount + kLSmall);
+          HIP_TRY(hipGetLastError());
+        }
+        if (has(hc->n_wmerge)) {
+          hipLaunchKernelGGL(k_merge, grid(k_merge), dim3(kWave * kEmitWaves), 0, ms, s, o, lists.l[kLWave],
+                             lcount + kLWave);
+          HIP_TRY(hipGetLastError());
+        }
+        return 0;
+      };
+      if (MQM_MERGE_BIG_FIRST ? (big() || small()) : (small() || big())) return -3;
     }
     hipLaunchKernelGGL(k_desc, dim3(std::min<uint32_t>((n + 255) / 256, 8192)), dim3(256), 0, st, o, n, desc_start,
-                       desc, n_desc);  // a wavefront per 64 topics
+                       desc, desc_cap);  // a wavefront per 64 topics
     HIP_TRY(hipGetLastError());
-    if (hc->n_shlist) {
-      hipLaunchKernelGGL(k_shared, dim3(std::min<uint32_t>((hc->n_shlist + 15) / 16, 8192)), dim3(256), 0, st, o,
+    if (has(hc->n_shlist)) {
+      const uint32_t nsh = exact ? hc->n_shlist : n;
+      hipLaunchKernelGGL(k_shared, dim3(std::min<uint32_t>((nsh + 15) / 16, 8192)), dim3(256), 0, st, o,
                          lists.l[kLShared], lcount + kLShared);
       HIP_TRY(hipGetLastError());
     }
-    if (n_desc) {
-      hipLaunchKernelGGL(k_winmap, dim3((uint32_t)std::min<uint64_t>((n_desc + 255) / 256, 8192)), dim3(256), 0, st,
-                         desc, n_desc, s_total, win);
+    if (has((uint32_t)std::min<uint64_t>(hc->n_desc, 1))) {
+      const uint64_t nd_grid = exact ? hc->n_desc : desc_cap;
+      hipLaunchKernelGGL(k_winmap, dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nd_grid + 255) / 256, 8192))),
+                         dim3(256), 0, st, desc, desc_start + n, desc_cap, o.dstart + n, win, win_cap, &o.ctr->oob);
       HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(k_wincopy, main_grid(k_wincopy), dim3(kWave * kEmitWaves), 0, st, s, desc, n_desc, win, n_win,
-                         s_total, o.dout, o.dcap, &o.ctr->oob);
+      hipLaunchKernelGGL(k_wincopy, main_grid(k_wincopy), dim3(kWave * kEmitWaves), 0, st, s, desc, desc_start + n,
+                         desc_cap, win, win_cap, o.dstart + n, o.dout, o.dcap, &o.ctr->oob);
       HIP_TRY(hipGetLastError());
     }
     if (side && ws.join(st, ms)) return -3;
   }
-  if (n_dfs) {
-    hp[4] = s_total;  // Counters::dtail, Counters::htail (pinned staging)
-    hp[5] = h_total;
-    HIP_TRY(hipMemcpyAsync(o.ctr, hp + 4, 2 * sizeof(unsigned long long), hipMemcpyHostToDevice, st));
-    if (ws.get(W::kTable, sizeof(GEnt) * (tab_total + 1))) return -2;
-    GEnt *tab = (GEnt *)ws.ptr(W::kTable);
-    HIP_TRY(hipMemsetAsync(tab, 0, sizeof(GEnt) * tab_total, st));
+  if (dfs) {
     hipLaunchKernelGGL(k_dfs<1>, dim3(fb_blocks), dim3(kWave), fb_lds, st, s, d_bytes, d_offs, o, raw_cnt, raw_h,
                        tab_off, tab, max_levels);
     HIP_TRY(hipGetLastError());
@@ -2076,37 +2176,60 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
     HIP_TRY(hipGetLastError());
   }
   mark(ws, 3, st);
-  // totals for the caller: sum of counts
+  // totals for the caller: sums of the counts, then the one read-back
   {
     size_t tmp = 0;
-    uint64_t *sums = reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(o.ctr) + 192);
     hipcub::TransformInputIterator<uint64_t, Widen, const uint32_t *> dc(o.dcount, Widen{}), hc_it(o.hcount, Widen{});
-    HIP_TRY(hipcub::DeviceReduce::Sum(nullptr, tmp, dc, sums, n, st));
+    HIP_TRY(hipcub::DeviceReduce::Sum(nullptr, tmp, dc, &o.ctr->d_sum, n, st));
     if (ws.get(W::kScanTmp, tmp)) return -2;
-    HIP_TRY(hipcub::DeviceReduce::Sum(ws.ptr(W::kScanTmp), tmp, dc, sums, n, st));
-    HIP_TRY(hipcub::DeviceReduce::Sum(ws.ptr(W::kScanTmp), tmp, hc_it, sums + 1, n, st));
-    HIP_TRY(hipMemcpyAsync(hp, sums, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipcub::DeviceReduce::Sum(ws.ptr(W::kScanTmp), tmp, dc, &o.ctr->d_sum, n, st));
+    HIP_TRY(hipcub::DeviceReduce::Sum(ws.ptr(W::kScanTmp), tmp, hc_it, &o.ctr->h_sum, n, st));
     HIP_TRY(hipMemcpyAsync(hc, o.ctr, sizeof(Counters), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
   }
-  if (hc->oob) {
-    fprintf(stderr, "mqmatch: an output store fell outside its buffer (batch rejected)\n");
-    return -3;
+  (void)hp;
+  ws.last_valid = false;  // until collected
+  ws.last_n = n;
+  ws.last_bytes = d_bytes;
+  ws.last_offs = d_offs;
+  ws.pend_exact = exact;
+  ws.pending = true;
+  return 0;
+}
+
+int match_collect(Workspace &ws, hipStream_t st, MatchOutput *out) {
+  using W = Workspace;
+  if (!ws.pending) return -1;
+  ws.pending = false;
+  HIP_TRY(hipStreamSynchronize(st));
+  Counters *hc = pinned_counters(ws);
+  const uint32_t n = ws.last_n;
+  // the next queued call's DFS capacity: what this one needed, with room
+  ws.dfs_cap = std::max<uint32_t>(ws.dfs_cap, std::max<uint32_t>(1024, hc->n_dfs + hc->n_dfs / 4));
+  if (hc->oob || hc->cap_ovf) {
+    if (ws.pend_exact) {  // sized exactly from this call's own counts: never expected
+      fprintf(stderr, "mqmatch: an output store fell outside its buffer (batch rejected)\n");
+      return -3;
+    }
+    return 1;  // outgrew buffers sized by an earlier call: match_device re-runs it, exact
   }
+  ws.caps_known = true;
+  ws.last_valid = true;
+  ws.last_n_dfs = hc->n_dfs;
+  for (int i = 0; i < 5; i++) ws.why[i] = hc->why[i];
 #if MQM_WALK_STATS
   fprintf(stderr, "[walk-stats] topics %u literal probes %llu missed %llu wildcard-child loads %llu\n", n,
           hc->st_probe, hc->st_miss, hc->st_desc);
 #endif
   if (ws.profile) {
     ws.prof_calls++;
-    ws.prof_fallback_topics += n_dfs;
+    ws.prof_fallback_topics += hc->n_dfs;
     ws.prof_walk_ms += elapsed(ws, 0, 1);
     ws.prof_dedupe_ms += elapsed(ws, 2, 3);
     ws.prof_total_ms += elapsed(ws, 0, 3);
   }
   out->n_topics = n;
-  out->n_deliveries = hp[0];
-  out->n_shared = hp[1];
+  out->n_deliveries = hc->d_sum;
+  out->n_shared = hc->h_sum;
   out->n_big = hc->n_t1 + hc->n_t2 + hc->n_t3 + hc->n_part;
   out->n_tier2 = hc->n_t2;
   out->n_tier3 = hc->n_t3 + hc->n_part;
@@ -2114,15 +2237,28 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
   out->n_part = hc->n_part;
   out->n_merge_small = hc->n_small;
   out->n_merge_wave = hc->n_wmerge;
-  out->n_solo_ranges = n_desc;
-  out->n_fallback = n_dfs;
-  out->starts = o.dstart;
-  out->counts = o.dcount;
-  out->deliveries = o.dout;
-  out->shared_starts = o.hstart;
-  out->shared_counts = o.hcount;
-  out->shared = o.hout;
+  out->n_solo_ranges = hc->n_desc;
+  out->n_fallback = hc->n_dfs;
+  out->starts = (const uint64_t *)ws.ptr(W::kDStart);
+  out->counts = (const uint32_t *)ws.ptr(W::kDCount);
+  out->deliveries = (const uint32_t *)ws.ptr(W::kDOut);
+  out->shared_starts = (const uint64_t *)ws.ptr(W::kHStart);
+  out->shared_counts = (const uint32_t *)ws.ptr(W::kHCount);
+  out->shared = (const uint32_t *)ws.ptr(W::kHOut);
+  out->exact = ws.pend_exact;
   return 0;
+}
+
+int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes, const uint64_t *d_offs,
+                 uint32_t n, hipStream_t st, MatchOutput *out) {
+  int rc = match_enqueue(s, ws, d_bytes, d_offs, n, st, false);
+  if (rc == 0) rc = match_collect(ws, st, out);
+  if (rc == 1) {  // a queued call outgrew its buffers: again, sized exactly
+    rc = match_enqueue(s, ws, d_bytes, d_offs, n, st, true);
+    if (rc == 0) rc = match_collect(ws, st, out);
+    if (rc == 0) ws.requeued++;
+  }
+  return rc;
 }
 
 int identifiers_device(const DeviceSnapshot &s, Workspace &ws, hipStream_t st, IdentOutput *out) {
@@ -2134,6 +2270,7 @@ int identifiers_device(const DeviceSnapshot &s, Workspace &ws, hipStream_t st, I
   o.cls = (uint8_t *)ws.ptr(W::kCls);
   o.recs = (uint32_t *)ws.ptr(W::kRecs);
   o.dfs_list = (uint32_t *)ws.ptr(W::kDfsList);
+  o.dfs_cap = ws.last_n_dfs;  // the whole list (phases 3 / 4 keep no per-topic arrays)
   o.ctr = (Counters *)ws.ptr(W::kCounters);
   o.icount = (uint32_t *)ws.ptr(W::kICount);
   o.istart = (uint64_t *)ws.ptr(W::kIStart);
@@ -2152,7 +2289,8 @@ int identifiers_device(const DeviceSnapshot &s, Workspace &ws, hipStream_t st, I
     }
   }
   if (scan_offsets(ws, o.icount, o.istart, n, st)) return -3;
-  uint64_t *hp = reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(ws.host_pinned) + 128);
+  uint64_t *hp = ws.pinned_u64();
+  if (!hp) return -2;
   HIP_TRY(hipMemcpyAsync(hp, o.istart + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   const uint64_t total = hp[0];

@@ -1,0 +1,57 @@
+#!/bin/bash
+# profiles/run_r03.sh TAG STEP... — round-3 GPU runs, each step under its own
+# time limit, chained so that the first failure ends the call.
+#   tests   : every -m gpu test                          -> gpurun_out/TAG/pytest_gpu.log
+#   c4test  : the C4 shard 0/8 full-batch test            -> gpurun_out/TAG/pytest_c4.log
+#   ret     : the retained (reverse-match) tests           -> gpurun_out/TAG/pytest_ret.log
+#   nobloom : the edge-case / random-op parity tests with the edge filter off (MQM_NO_BLOOM=1)
+#   fastt   : small-batch path + batching collector + shim tests -> gpurun_out/TAG/pytest_fast.log
+#   quick   : every -m gpu test except the full-size ones
+#   lat     : C3 bench with the per-publish legs (single topic, 64 native callers direct / batched)
+#   smoke   : __graft_entry__.smoke()
+#   bench   : the default bench line (C3)                -> gpurun_out/TAG/bench.json
+#   fast    : bench without CPU baseline / host path      -> gpurun_out/TAG/bench_fast.json
+#   prof    : rocprofv3 kernel trace + stats of `fast`    -> gpurun_out/TAG/prof/
+#   c4shard : C4 shard 0/8 bench line with roofline and CPU baseline
+#   c4prof  : rocprofv3 kernel stats of the C4 shard bench
+#   rev     : C5 reverse bench line (full 50M retained, CPU baseline, full-size selfcheck)
+set -euo pipefail
+TAG=$1
+shift
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p $OUT
+cd $ROOT
+FAST="--steps 10 --warmup 3 --no-cpu-baseline --host-topics 0 --latency-topics 0"
+PYT="python3 -u -m pytest -x -v --timeout-method thread"
+for step in "$@"; do
+  echo "[run_r03] $step $(date +%T)"
+  case $step in
+    tests) timeout -k 10 1000 $PYT tests -m gpu --timeout 600 > $OUT/pytest_gpu.log 2>&1 ;;
+    c4test) timeout -k 10 600 $PYT tests/test_gpu_c4_shard.py -m gpu --timeout 500 > $OUT/pytest_c4.log 2>&1 ;;
+    ret) timeout -k 10 600 $PYT tests/test_gpu_retained.py -m gpu --timeout 300 > $OUT/pytest_ret.log 2>&1 ;;
+    nobloom) MQM_NO_BLOOM=1 timeout -k 10 400 $PYT tests/test_gpu_parity.py -m gpu --timeout 200 \
+             -k "edge_cases or random_ops or config_vs_oracle" > $OUT/pytest_nobloom.log 2>&1 ;;
+    fastt) timeout -k 10 500 $PYT tests/test_gpu_fast.py tests/test_gpu_batching.py tests/test_gpu_shim.py -m gpu \
+             --timeout 200 > $OUT/pytest_fast.log 2>&1 ;;
+    quick) timeout -k 10 600 $PYT tests -m gpu --timeout 300 -k "not full_size and not 20m and not 5m and not config4" \
+             > $OUT/pytest_quick.log 2>&1 ;;
+    lat) timeout -k 10 600 python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --host-topics 0 \
+             > $OUT/bench_lat.json 2> $OUT/bench_lat.log ;;
+    smoke) timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 ;;
+    bench) timeout -k 10 600 python3 -u bench.py > $OUT/bench.json 2> $OUT/bench.log ;;
+    fast) timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast.json 2> $OUT/bench_fast.log ;;
+    prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv \
+             -d $OUT/prof -o prof -- python3 $ROOT/bench.py $FAST \
+             > $OUT/bench_under_rocprof.json 2> $OUT/rocprof.log) ;;
+    c4shard) timeout -k 10 700 python3 -u bench.py --config 4 --shard 0/8 --steps 5 --warmup 2 --host-topics 0 \
+             --latency-topics 0 --cpu-seconds 10 > $OUT/bench_c4_shard0of8.json 2> $OUT/bench_c4_shard0of8.log ;;
+    c4prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv \
+             -d $OUT/prof_c4 -o prof -- python3 $ROOT/bench.py --config 4 --shard 0/8 --steps 3 --warmup 1 \
+             --no-cpu-baseline --host-topics 0 --latency-topics 0 > $OUT/c4_under_rocprof.json 2> $OUT/rocprof_c4.log) ;;
+    rev) timeout -k 10 900 python3 -u bench.py --workload reverse --steps 5 --warmup 1 --cpu-seconds 10 \
+             > $OUT/bench_reverse.json 2> $OUT/bench_reverse.log ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "[run_r03] done $(date +%T)"

@@ -30,16 +30,21 @@ def _rows(res):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("threads", [16])
-def test_batched_subscribers_concurrent_equal_plain(threads):
+@pytest.mark.parametrize("threads,identifiers", [(16, True), (16, False)])
+def test_batched_subscribers_concurrent_equal_plain(threads, identifiers, monkeypatch):
+    """identifiers=False: batches take the small-batch path (fast.hip);
+    identifiers=True: mqm_match_batch.  `plain` is the batch pipeline
+    (MQM_NO_FAST=1) in both cases."""
     w = mqgen.generate(1, n_filters=20000, n_topics=3200, p_shared=0.05)
-    plain = maxmq_amd.TopicsIndex(device=0, identifiers=True)
+    monkeypatch.setenv("MQM_NO_FAST", "1")
+    plain = maxmq_amd.TopicsIndex(device=0, identifiers=identifiers)
+    monkeypatch.delenv("MQM_NO_FAST")
     plain.subscribe_workload(w)
     plain.commit()
     want = _rows(plain.match_batch(w.topics.data, w.topics.offs))
     plain.close()
 
-    idx = maxmq_amd.TopicsIndex(device=0, identifiers=True, batching=True)
+    idx = maxmq_amd.TopicsIndex(device=0, identifiers=identifiers, batching=True)
     idx.subscribe_workload(w)
     idx.commit()
     L = capi.lib()
