@@ -68,6 +68,8 @@ def parse():
                     help="PCIe-inclusive host path (mqm_match_batch): topics per call, outside the timed region; 0 = skip")
     ap.add_argument("--host-threads", type=int, default=4,
                     help="host path: concurrent callers (each its own stream), batches overlapped across them")
+    ap.add_argument("--steady-steps", type=int, default=20,
+                    help="steady-state leg: batches queued back to back on two contexts (0 = skip)")
     ap.add_argument("--latency-topics", type=int, default=2000,
                     help="single-topic mqm_subscribers calls timed for the per-publish latency; 0 = skip")
     ap.add_argument("--conc-threads", type=int, default=64,
@@ -356,6 +358,9 @@ def main():
         # leg; host path and latency are per-GPU properties too); at N > 1 the
         # oracle runs only a short sample for the roofline's algorithmic bytes
         host = host_path(idx, w, args) if args.host_topics and world == 1 else None
+        if host:
+            host["packed"] = host_path(idx, w, args, packed=True)
+        steady = steady_state(idx, tb, to, n, dev, args) if world == 1 and not shard_of and args.steady_steps else None
         lat = latency(idx, w, args) if args.latency_topics and world == 1 else None
         if not args.no_cpu_baseline:
             if world == 1:
@@ -401,6 +406,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "host_path": host,
+            "steady_state": steady,
             "single_topic_latency": lat,
         }
         print(json.dumps(out), flush=True)
@@ -409,7 +415,44 @@ def main():
         dist.destroy_process_group()
 
 
-def host_path(idx, w, args):
+def steady_state(idx, tb, to, n, dev, args):
+    """SURVEY §8(d) steady state: --steady-steps batches queued back to back
+    through the queued device API (mqm_match_device_async), two contexts on
+    two streams, the host waiting only for the batch queued two steps earlier
+    (so the device always has the next batch queued).  Inputs resident in
+    HBM; the same batch each time."""
+    import torch
+
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    ctxs = [idx.match_context(), idx.match_context()]
+    for c, st in zip(ctxs, streams):  # size each context (its first batch is exact)
+        c.submit(tb.data_ptr(), to.data_ptr(), n, st.cuda_stream)
+        c.wait()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    pend = [False, False]
+    dsum = 0
+    for k in range(args.steady_steps):
+        c = k % 2
+        if pend[c]:
+            dsum += int(ctxs[c].wait().n_deliveries)
+        ctxs[c].submit(tb.data_ptr(), to.data_ptr(), n, streams[c].cuda_stream)
+        pend[c] = True
+    for c in (0, 1):
+        if pend[c]:
+            dsum += int(ctxs[c].wait().n_deliveries)
+    dt = time.perf_counter() - t0
+    requeued = sum(c.requeued() for c in ctxs)
+    for c in ctxs:
+        c.close()
+    return {"value": args.steady_steps * n / dt, "unit": "topics/s", "batches": args.steady_steps,
+            "ms_per_batch": dt * 1e3 / args.steady_steps, "deliveries_per_s": dsum / dt, "contexts": 2,
+            "requeued_batches": requeued,
+            "note": "mqm_match_device_async on 2 contexts / 2 streams, host waits only for the batch queued two "
+                    "steps earlier; no read-back inside a batch (outputs sized by the contexts' first batch)"}
+
+
+def host_path(idx, w, args, packed=False):
     """The boundary's host form, mqm_match_batch, as a broker would drive it
     (SURVEY §8d end-to-end): topics in pinned host memory -> H2D -> the match
     pipeline -> dense CSR D2H into pinned, library-owned result blocks.
@@ -426,6 +469,7 @@ def host_path(idx, w, args):
     from maxmq_amd import capi
 
     L = capi.lib()
+    fn = L.mqm_match_batch_packed if packed else L.mqm_match_batch
     per = min(args.host_topics, len(w.topics))
     nb = max(1, len(w.topics) // per)
     data = torch.from_numpy(w.topics.data).pin_memory()
@@ -434,8 +478,7 @@ def host_path(idx, w, args):
 
     def call(b):
         res = C.c_void_p()
-        capi.check("mqm_match_batch", L.mqm_match_batch(idx._h, C.c_void_p(dp), C.c_void_p(op + 8 * b * per), per,
-                                                        C.byref(res)))
+        capi.check("mqm_match_batch", fn(idx._h, C.c_void_p(dp), C.c_void_p(op + 8 * b * per), per, C.byref(res)))
         d = int(C.cast(L.mqm_result_offsets(res), C.POINTER(C.c_uint64))[per])
         L.mqm_result_free(res)
         return d
@@ -487,14 +530,16 @@ def host_path(idx, w, args):
     del g, h
     n = done[0]
     in_b = int(w.topics.offs[nb * per]) + 8 * n
-    out_b = 8 * done[1] + 16 * n
+    out_b = (4 if packed else 8) * done[1] + 16 * n
     bound_s = max(in_b / rates["h2d"], out_b / rates["d2h"])
     return {"value": n / dt, "unit": "topics/s", "topics_per_call": per, "calls": nb, "threads": args.host_threads,
             "ms_per_call": dt * 1e3 * args.host_threads / nb, "deliveries_per_s": done[1] / dt,
             "h2d_GBps": rates["h2d"] / 1e9, "d2h_GBps": rates["d2h"] / 1e9,
             "pcie_bound_topics_per_s": n / bound_s, "frac_of_pcie_bound": (n / dt) / (n / bound_s),
-            "note": "pinned topics in -> match -> dense CSR into pinned result blocks; "
-                    "pcie_bound = max(H2D bytes / H2D rate, D2H bytes / D2H rate)"}
+            "delivery_bytes": 4 if packed else 8,
+            "note": "pinned topics in -> match -> dense CSR into pinned result blocks (" +
+                    ("mqm_match_batch_packed: 4-B packed words" if packed else "mqm_match_batch: 8-B {client, packed}") +
+                    "); pcie_bound = max(H2D bytes / H2D rate, D2H bytes / D2H rate)"}
 
 
 def _driver():

@@ -231,6 +231,13 @@ int mqm_debug_fault(mqm_index *h, int stage, int count);
 /* Host in / host out.  Topic i is bytes[offsets[i] .. offsets[i+1]). */
 int mqm_match_batch(mqm_index *h, const char *topic_bytes, const uint64_t *topic_offsets, uint32_t n_topics,
                     mqm_result **out);
+/* The same with 4-byte deliveries: the result carries the packed words
+ * (mqm_result_packed; mqm_result_deliveries is NULL).  A delivery's client is
+ * its first-merged subscription's (mqm_result_sub_info(...).client, which a
+ * caller resolving the Subscription fields reads anyway), so nothing is lost
+ * and the device-to-host copy halves (the host path is PCIe-bound). */
+int mqm_match_batch_packed(mqm_index *h, const char *topic_bytes, const uint64_t *topic_offsets, uint32_t n_topics,
+                           mqm_result **out);
 /* single-topic convenience == Subscribers(topic) (batched across concurrent
  * callers with MQM_CFG_BATCHING) */
 int mqm_subscribers(mqm_index *h, const char *topic, size_t topic_len, mqm_result **out);
@@ -378,7 +385,8 @@ int mqm_messages_device(mqm_index *h, const uint8_t *d_filter_bytes, const uint6
 /* ---- result accessors --------------------------------------------------- */
 uint32_t mqm_result_num_topics(const mqm_result *r);
 const uint64_t *mqm_result_offsets(const mqm_result *r);          /* n + 1          */
-const mqm_delivery *mqm_result_deliveries(const mqm_result *r);
+const mqm_delivery *mqm_result_deliveries(const mqm_result *r); /* NULL for a packed result */
+const uint32_t *mqm_result_packed(const mqm_result *r);         /* packed words (mqm_match_batch_packed) */
 const uint64_t *mqm_result_shared_offsets(const mqm_result *r);   /* n + 1          */
 const uint32_t *mqm_result_shared(const mqm_result *r);           /* shared sub ids */
 /* resolve a delivery's first_sub / a shared sub id (snapshot-relative) */

@@ -109,8 +109,15 @@ class BatchResult:
         self.shared_offsets = arr(L.mqm_result_shared_offsets(handle), n + 1, np.uint64)
         nd = int(self.offsets[-1]) if n else 0
         ns = int(self.shared_offsets[-1]) if n else 0
-        self.deliveries = arr(L.mqm_result_deliveries(handle), nd, capi.DELIVERY_DTYPE)
         self.shared = arr(L.mqm_result_shared(handle), ns, np.uint32)
+        self.packed_only = bool(nd) and not L.mqm_result_deliveries(handle) and bool(L.mqm_result_packed(handle))
+        if self.packed_only:  # mqm_match_batch_packed: the client is the first-merged subscription's
+            packed = arr(L.mqm_result_packed(handle), nd, np.uint32)
+            self.deliveries = np.zeros(nd, capi.DELIVERY_DTYPE)
+            self.deliveries["packed"] = packed
+            self.deliveries["client"] = self.sub_infos(packed & 0x0FFFFFFF)["client"]
+        else:
+            self.deliveries = arr(L.mqm_result_deliveries(handle), nd, capi.DELIVERY_DTYPE)
         # Identifiers support (MQM_CFG_IDENTIFIERS): per topic, the sids of the
         # gathered subscriptions with Identifier > 0
         self.ident_offsets = self.idents = None
@@ -373,6 +380,17 @@ class TopicsIndex:
         offs = np.ascontiguousarray(offs, dtype=np.uint64)
         h = C.c_void_p()
         check("mqm_match_batch", lib().mqm_match_batch(
+            self._h, data.ctypes.data_as(C.c_void_p), offs.ctypes.data_as(C.c_void_p), len(offs) - 1,
+            C.byref(h)))
+        return BatchResult(self, h)
+
+    def match_batch_packed(self, data: np.ndarray, offs: np.ndarray) -> BatchResult:
+        """mqm_match_batch_packed (4-B deliveries); the BatchResult resolves
+        each delivery's client through its first-merged subscription."""
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        h = C.c_void_p()
+        check("mqm_match_batch_packed", lib().mqm_match_batch_packed(
             self._h, data.ctypes.data_as(C.c_void_p), offs.ctypes.data_as(C.c_void_p), len(offs) - 1,
             C.byref(h)))
         return BatchResult(self, h)

@@ -46,7 +46,8 @@ EXPORTED = [
     "mqm_result_identifiers", "mqm_dense_device", "mqm_gather_shards", "mqm_commit_async", "mqm_commit_poll",
     "mqm_commit_policy", "mqm_commit_state_get", "mqm_snapshot_digest", "mqm_unsubscribe_many", "mqm_load_subscriptions_json",
     "mqm_debug_fault", "mqm_gather_shards_shared", "mqm_match_ctx_create", "mqm_match_ctx_destroy",
-    "mqm_match_device_async", "mqm_match_ctx_wait", "mqm_match_ctx_stats",
+    "mqm_match_device_async", "mqm_match_ctx_wait", "mqm_match_ctx_stats", "mqm_match_batch_packed",
+    "mqm_result_packed",
 ]
 
 
@@ -201,6 +202,8 @@ def lib():
         "mqm_match_device_async": ([vp, vp, vp, u32, vp], C.c_int),
         "mqm_match_ctx_wait": ([vp, C.POINTER(DeviceResult)], C.c_int),
         "mqm_match_ctx_stats": ([vp, C.POINTER(u64)], C.c_int),
+        "mqm_match_batch_packed": ([vp, vp, vp, u32, C.POINTER(vp)], C.c_int),
+        "mqm_result_packed": ([vp], vp),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

@@ -164,7 +164,8 @@ struct mqm_result {
   void *blk = nullptr;
   size_t blk_cap = 0;
   const uint64_t *offsets = nullptr, *shared_offsets = nullptr, *ident_offsets = nullptr;
-  const mqm_delivery *deliveries = nullptr;
+  const mqm_delivery *deliveries = nullptr;  // nullptr for a packed result
+  const uint32_t *packed = nullptr;           // mqm_match_batch_packed: 4-B packed words
   const uint32_t *shared = nullptr, *idents = nullptr;
   bool has_idents = false;               // MQM_CFG_IDENTIFIERS
   std::shared_ptr<const HostSnapshot> snap;
@@ -378,25 +379,26 @@ void fill_device_result(const MatchOutput &mo, const Workspace &ws, mqm_device_r
 // deliveries | shared (16-B aligned parts), from per-topic counts
 struct ResultLayout {
   uint64_t o_sh = 0, o_d = 0, o_s = 0, total = 0;
-  ResultLayout(uint64_t n1, uint64_t nd, uint64_t ns) {
+  ResultLayout(uint64_t n1, uint64_t nd, uint64_t ns, uint64_t dsize) {
     auto up = [](uint64_t b) { return (b + 15) & ~15ull; };
     o_sh = up(8 * n1);
     o_d = o_sh + up(8 * n1);
-    o_s = o_d + up(8 * nd);
+    o_s = o_d + up(dsize * nd);
     total = o_s + up(4 * ns);
   }
 };
 
 // the small-batch path's per-topic segments (FastRec: anywhere in the pinned
 // output blocks, in completion order) -> one result block in topic order
-int fast_result(mqm_index *h, const std::shared_ptr<GpuSnapshot> &snap, const FastOutput &fo, mqm_result *r) {
+int fast_result(mqm_index *h, const std::shared_ptr<GpuSnapshot> &snap, const FastOutput &fo, bool packed,
+                mqm_result *r) {
   const uint32_t n = fo.n_topics;
   uint64_t nd = 0, ns = 0;
   for (uint32_t i = 0; i < n; i++) {
     nd += fo.recs[i].dcount;
     ns += fo.recs[i].hcount;
   }
-  const ResultLayout lay(n + 1ull, nd, ns);
+  const ResultLayout lay(n + 1ull, nd, ns, packed ? 4 : 8);
   r->pool = h->pinned;
   r->blk = h->pinned->get(lay.total, &r->blk_cap);
   if (!r->blk) {
@@ -412,7 +414,12 @@ int fast_result(mqm_index *h, const std::shared_ptr<GpuSnapshot> &snap, const Fa
     const FastRec &x = fo.recs[i];
     off[i] = d;
     soff[i] = q;
-    if (x.dcount) memcpy(dl + d, fo.dout + x.dbase, 8ull * x.dcount);
+    if (packed) {
+      uint32_t *p4 = reinterpret_cast<uint32_t *>(dl) + d;
+      for (uint32_t j = 0; j < x.dcount; j++) p4[j] = (uint32_t)(fo.dout[x.dbase + j] >> 32);
+    } else if (x.dcount) {
+      memcpy(dl + d, fo.dout + x.dbase, 8ull * x.dcount);
+    }
     if (x.hcount) memcpy(sh + q, fo.hout + x.hbase, 4ull * x.hcount);
     d += x.dcount;
     q += x.hcount;
@@ -422,7 +429,10 @@ int fast_result(mqm_index *h, const std::shared_ptr<GpuSnapshot> &snap, const Fa
   r->n = n;
   r->offsets = off;
   r->shared_offsets = soff;
-  r->deliveries = reinterpret_cast<const mqm_delivery *>(dl);
+  if (packed)
+    r->packed = reinterpret_cast<const uint32_t *>(dl);
+  else
+    r->deliveries = reinterpret_cast<const mqm_delivery *>(dl);
   r->shared = sh;
   r->snap = snap->host;
   return MQM_OK;
@@ -674,8 +684,10 @@ int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t 
   });
 }
 
-int mqm_match_batch(mqm_index *h, const char *topic_bytes, const uint64_t *topic_offsets, uint32_t n_topics,
-                    mqm_result **out) {
+}  // extern "C"
+
+static int match_batch_impl(mqm_index *h, const char *topic_bytes, const uint64_t *topic_offsets, uint32_t n_topics,
+                            bool packed, mqm_result **out) {
   if (!h || !out || !topic_offsets || (n_topics && !topic_bytes)) return MQM_EINVAL;
   *out = nullptr;
   return guarded([&] {
@@ -700,7 +712,7 @@ int mqm_match_batch(mqm_index *h, const char *topic_bytes, const uint64_t *topic
         return e < 0 ? hip_rc(e) : MQM_EHIP;
       }
       if (e == 0) {
-        rc = fast_result(h, snap, fo, r.get());
+        rc = fast_result(h, snap, fo, packed, r.get());
         ctx_release(h, std::move(c));
         if (rc != MQM_OK) return rc;
         *out = r.release();
@@ -721,12 +733,13 @@ int mqm_match_batch(mqm_index *h, const char *topic_bytes, const uint64_t *topic
       IdentOutput io;
       if (want_ids && (e = identifiers_device(snap->dev, ws, st, &io)) != 0) return hip_rc(e);
       DenseOutput dn;
-      if ((e = densify(snap->dev, ws, mo, st, &dn)) != 0) return hip_rc(e);
+      if ((e = densify(snap->dev, ws, mo, st, &dn, packed)) != 0) return hip_rc(e);
       // one pinned block: three offset arrays, then the entries (16-B aligned parts)
       const uint64_t n1 = (uint64_t)n_topics + 1, ni = want_ids ? io.n_idents : 0;
       auto up = [](uint64_t b) { return (b + 15) & ~15ull; };
       const uint64_t o_off = 0, o_sh = up(8 * n1), o_io = o_sh + up(8 * n1), o_d = o_io + (want_ids ? up(8 * n1) : 0);
-      const uint64_t o_s = o_d + up(8 * mo.n_deliveries), o_i = o_s + up(4 * mo.n_shared), total = o_i + up(4 * ni);
+      const uint64_t dsz = packed ? 4 : 8;
+      const uint64_t o_s = o_d + up(dsz * mo.n_deliveries), o_i = o_s + up(4 * mo.n_shared), total = o_i + up(4 * ni);
       r->pool = h->pinned;
       r->blk = h->pinned->get(total, &r->blk_cap);
       if (!r->blk) {
@@ -737,14 +750,17 @@ int mqm_match_batch(mqm_index *h, const char *topic_bytes, const uint64_t *topic
       r->n = n_topics;
       r->offsets = reinterpret_cast<const uint64_t *>(B + o_off);
       r->shared_offsets = reinterpret_cast<const uint64_t *>(B + o_sh);
-      r->deliveries = reinterpret_cast<const mqm_delivery *>(B + o_d);
+      if (packed)
+        r->packed = reinterpret_cast<const uint32_t *>(B + o_d);
+      else
+        r->deliveries = reinterpret_cast<const mqm_delivery *>(B + o_d);
       r->shared = reinterpret_cast<const uint32_t *>(B + o_s);
       r->snap = snap->host;
       if (hipMemcpyAsync(B + o_off, dn.offsets, 8 * n1, hipMemcpyDeviceToHost, st) != hipSuccess ||
           hipMemcpyAsync(B + o_sh, dn.shared_offsets, 8 * n1, hipMemcpyDeviceToHost, st) != hipSuccess)
         return MQM_EHIP;
       if (mo.n_deliveries &&
-          hipMemcpyAsync(B + o_d, dn.deliveries, 8 * mo.n_deliveries, hipMemcpyDeviceToHost, st) != hipSuccess)
+          hipMemcpyAsync(B + o_d, dn.deliveries, dsz * mo.n_deliveries, hipMemcpyDeviceToHost, st) != hipSuccess)
         return MQM_EHIP;
       if (mo.n_shared && hipMemcpyAsync(B + o_s, dn.shared, 4 * mo.n_shared, hipMemcpyDeviceToHost, st) != hipSuccess)
         return MQM_EHIP;
@@ -763,6 +779,18 @@ int mqm_match_batch(mqm_index *h, const char *topic_bytes, const uint64_t *topic
     *out = r.release();
     return MQM_OK;
   });
+}
+
+extern "C" {
+
+int mqm_match_batch(mqm_index *h, const char *topic_bytes, const uint64_t *topic_offsets, uint32_t n_topics,
+                    mqm_result **out) {
+  return match_batch_impl(h, topic_bytes, topic_offsets, n_topics, false, out);
+}
+
+int mqm_match_batch_packed(mqm_index *h, const char *topic_bytes, const uint64_t *topic_offsets, uint32_t n_topics,
+                           mqm_result **out) {
+  return match_batch_impl(h, topic_bytes, topic_offsets, n_topics, true, out);
 }
 
 }  // extern "C"
@@ -1298,6 +1326,7 @@ int mqm_batching_stats(mqm_index *h, uint64_t *batches, uint64_t *topics) {
 uint32_t mqm_result_num_topics(const mqm_result *r) { return r ? r->n : 0; }
 const uint64_t *mqm_result_offsets(const mqm_result *r) { return r ? r->offsets : nullptr; }
 const mqm_delivery *mqm_result_deliveries(const mqm_result *r) { return r ? r->deliveries : nullptr; }
+const uint32_t *mqm_result_packed(const mqm_result *r) { return r ? r->packed : nullptr; }
 const uint64_t *mqm_result_shared_offsets(const mqm_result *r) { return r ? r->shared_offsets : nullptr; }
 const uint32_t *mqm_result_shared(const mqm_result *r) { return r ? r->shared : nullptr; }
 

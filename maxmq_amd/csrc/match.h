@@ -187,7 +187,9 @@ struct DenseOutput {
   const uint64_t *offsets = nullptr, *deliveries = nullptr, *shared_offsets = nullptr;
   const uint32_t *shared = nullptr;
 };
-// (clients resolved through the snapshot the match read)
-int densify(const DeviceSnapshot &s, Workspace &ws, const MatchOutput &m, hipStream_t st, DenseOutput *out);
+// (clients resolved through the snapshot the match read; packed: the 4-B
+// packed words only, `deliveries` then points at uint32_t)
+int densify(const DeviceSnapshot &s, Workspace &ws, const MatchOutput &m, hipStream_t st, DenseOutput *out,
+            bool packed = false);
 
 }  // namespace mqm

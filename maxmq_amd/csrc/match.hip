@@ -1638,11 +1638,14 @@ __global__ void k_totals(Counters *ctr, const uint64_t *__restrict__ dstart, con
 }
 
 // segments -> dense CSR (one wavefront per topic); deliveries resolved to
-// {client, packed} (the client of the first-merged subscription)
+// {client, packed} (the client of the first-merged subscription), or the
+// packed words alone (kPacked: 4 B per delivery, the client being the first
+// subscription's)
+template <bool kPacked>
 __global__ __launch_bounds__(256) void k_densify(DeviceSnapshot s, uint32_t n, const uint32_t *__restrict__ dcount,
                                                 const uint64_t *__restrict__ dstart,
                                                 const uint64_t *__restrict__ doffs, const uint32_t *__restrict__ dsrc,
-                                                uint64_t *__restrict__ ddst, const uint32_t *__restrict__ hcount,
+                                                void *__restrict__ ddst_v, const uint32_t *__restrict__ hcount,
                                                 const uint64_t *__restrict__ hstart,
                                                 const uint64_t *__restrict__ hoffs, const uint32_t *__restrict__ hsrc,
                                                 uint32_t *__restrict__ hdst) {
@@ -1651,9 +1654,15 @@ __global__ __launch_bounds__(256) void k_densify(DeviceSnapshot s, uint32_t n, c
   for (uint32_t t = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave; t < n; t += nwaves) {
     const uint32_t D = dcount[t], H = hcount[t];
     const uint64_t ds = dstart[t], dd = doffs[t], hs = hstart[t], hd = hoffs[t];
-    for (uint32_t j = lane; j < D; j += kWave) {
-      const uint32_t p = dsrc[ds + j];
-      ddst[dd + j] = (uint64_t)s.subs[p & kWordSidMask].client | ((uint64_t)p << 32);
+    if (kPacked) {
+      uint32_t *ddst = static_cast<uint32_t *>(ddst_v);
+      for (uint32_t j = lane; j < D; j += kWave) ddst[dd + j] = dsrc[ds + j];
+    } else {
+      uint64_t *ddst = static_cast<uint64_t *>(ddst_v);
+      for (uint32_t j = lane; j < D; j += kWave) {
+        const uint32_t p = dsrc[ds + j];
+        ddst[dd + j] = (uint64_t)s.subs[p & kWordSidMask].client | ((uint64_t)p << 32);
+      }
     }
     for (uint32_t j = lane; j < H; j += kWave) hdst[hd + j] = hsrc[hs + j];
   }
@@ -2326,7 +2335,8 @@ int derive_words(const SubEnt *subs, uint32_t *words, uint64_t n, hipStream_t st
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
-int densify(const DeviceSnapshot &s, Workspace &ws, const MatchOutput &m, hipStream_t st, DenseOutput *out) {
+int densify(const DeviceSnapshot &s, Workspace &ws, const MatchOutput &m, hipStream_t st, DenseOutput *out,
+            bool packed) {
   using W = Workspace;
   const uint32_t n = m.n_topics;
   if (ws.get(W::kDenseOffs, sizeof(uint64_t) * (n + 1)) || ws.get(W::kDenseHOffs, sizeof(uint64_t) * (n + 1)) ||
@@ -2339,9 +2349,16 @@ int densify(const DeviceSnapshot &s, Workspace &ws, const MatchOutput &m, hipStr
   if (ws.get(W::kDenseShared, sizeof(uint32_t) * (m.n_shared + 1))) return -2;
   auto *dd = (uint64_t *)ws.ptr(W::kTable);
   auto *hd = (uint32_t *)ws.ptr(W::kDenseShared);
-  if (n > 0)
-    hipLaunchKernelGGL(k_densify, dim3(std::min<uint32_t>((n + 3) / 4, 8192)), dim3(256), 0, st, s, n, m.counts,
-                       m.starts, doffs, m.deliveries, dd, m.shared_counts, m.shared_starts, hoffs, m.shared, hd);
+  if (n > 0) {
+    if (packed)
+      hipLaunchKernelGGL(k_densify<true>, dim3(std::min<uint32_t>((n + 3) / 4, 8192)), dim3(256), 0, st, s, n,
+                         m.counts, m.starts, doffs, m.deliveries, (void *)dd, m.shared_counts, m.shared_starts, hoffs,
+                         m.shared, hd);
+    else
+      hipLaunchKernelGGL(k_densify<false>, dim3(std::min<uint32_t>((n + 3) / 4, 8192)), dim3(256), 0, st, s, n,
+                         m.counts, m.starts, doffs, m.deliveries, (void *)dd, m.shared_counts, m.shared_starts, hoffs,
+                         m.shared, hd);
+  }
   HIP_TRY(hipGetLastError());
   out->offsets = doffs;
   out->deliveries = dd;

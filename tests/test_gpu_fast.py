@@ -62,6 +62,14 @@ def test_fast_batches_vs_oracle_and_pipeline(monkeypatch, config, overrides):
         pick = rng.choice(n, size=min(size, n), replace=False)
         total += _check(fast, pipe, ora, Strings.from_list([w.topics[int(i)] for i in pick]), f"batch of {size}")
     assert total > 1000
+    # the 4-B packed form: the same rows once each client is resolved
+    for size in (5, 4096, min(n, 20000)):
+        pick = rng.choice(n, size=size, replace=False)
+        sub = Strings.from_list([w.topics[int(i)] for i in pick])
+        g, gs = canon_gpu(fast.match_batch_packed(sub.data, sub.offs))
+        r, rs = canon_oracle(*ora.match(sub.data, sub.offs, nthreads=8)[:4])
+        assert_same(g, r, f"packed batch of {size}")
+        assert_same(gs, rs, f"packed batch of {size} (shared)")
     # single-topic calls (mqm_subscribers, the reference's per-publish shape)
     for i in rng.choice(n, size=50, replace=False):
         t = bytes(w.topics[int(i)]).decode("utf-8", "surrogateescape")
