@@ -1218,6 +1218,84 @@ __device__ __forceinline__ uint32_t block_winners(MergeTable tb, uint32_t nslots
   return total;
 }
 
+// MQM_MULTI_PIPE=1: software-pipelined k_multi — while topic i is merged,
+// topic i+1's multi entries (client, word, rank) are already loading into
+// registers (its record double-buffered in LDS, topic i+2's record in
+// flight), so a topic no longer waits a dependent HBM round trip for its
+// entries after its record (the tier is latency-bound: ~400 entries a topic
+// at C3, 256 threads)
+#ifndef MQM_MULTI_PIPE
+#define MQM_MULTI_PIPE 1
+#endif
+#if MQM_MULTI_PIPE
+template <int kSlots>
+__global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs o, const uint32_t *__restrict__ list,
+                                                      const unsigned int *__restrict__ count) {
+  constexpr int kMPer = (kSlots * 3 / 4 + kBigThreads - 1) / kBigThreads;  // entries per thread at the tier's cap
+  __shared__ unsigned long long tfirst[kSlots], tkb[kSlots];
+  __shared__ MultiLds L[2];
+  const MergeTable tb{tkb, tfirst};
+  const int tid = threadIdx.x;
+  const uint32_t nb = *count;
+  const uint32_t g = gridDim.x;
+  uint32_t cl[kMPer], wd[kMPer], rk[kMPer];  // the current topic's entries (registers)
+  auto load_entries = [&](const uint32_t *rec, uint32_t (&c)[kMPer], uint32_t (&w)[kMPer], uint32_t (&r)[kMPer]) {
+    const uint32_t nh = rec[0] & 0xFFu, M = rec[2];
+#pragma unroll
+    for (int k = 0; k < kMPer; k++) {
+      const uint32_t q = tid + k * kBigThreads;
+      uint32_t h;
+      const uint32_t sid = multi_sid(rec, nh, q < M ? q : 0, &h);
+      const SubEnt e = q < M ? load_sub(s, sid) : SubEnt{0, 0};
+      c[k] = e.client;
+      w[k] = e.word;
+      r[k] = rec_at(rec, h, kFieldRank);
+    }
+  };
+  NextTopic nx;
+  uint32_t t_cur = 0, t_nxt = 0;
+  uint64_t db_cur = 0, db_nxt = 0;
+  // prologue: records of the first two topics in LDS, the first one's entries in registers
+  nx.fetch(o, list, blockIdx.x, nb);
+  t_cur = nx.t, db_cur = nx.db;
+  block_record(nx, L[0].rec);
+  nx.fetch(o, list, blockIdx.x + g, nb);
+  t_nxt = nx.t, db_nxt = nx.db;
+  block_record(nx, L[1].rec);
+  nx.fetch(o, list, blockIdx.x + 2 * g, nb);
+  if (blockIdx.x < nb) load_entries(L[0].rec, cl, wd, rk);
+  int b = 0;
+  for (uint32_t bi = blockIdx.x; bi < nb; bi += g, b ^= 1) {
+    const uint32_t *rec = L[b].rec;
+    const uint32_t Ss = rec[1], M = rec[2];
+    // the next topic's entries: loads in flight while this topic merges
+    uint32_t ncl[kMPer], nwd[kMPer], nrk[kMPer];
+    if (bi + g < nb) load_entries(L[b ^ 1].rec, ncl, nwd, nrk);
+    uint32_t lg = 6;
+    const uint32_t need = MQM_MERGE_DENSE ? (4 * M + 2) / 3 : 2 * M;
+    while ((1u << lg) < need && (1u << lg) < (uint32_t)kSlots) lg++;
+    const uint32_t mask = (1u << lg) - 1;
+    for (uint32_t i = tid; i <= mask; i += kBigThreads) mt_clear(tb, i);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kMPer; k++)
+      if (tid + k * kBigThreads < M) mt_insert(tb, mask, lg, cl[k], wd[k], rk[k]);
+    __syncthreads();
+    const uint32_t D = block_winners(tb, mask + 1, L[b].wsum, o, db_cur, Ss);
+    if (tid == 0) o.dcount[t_cur] = D;
+    // topic bi + 2g's record (fetched a topic ago) replaces this one's, whose
+    // reads are all done; topic bi + 3g's record starts loading
+    block_record(nx, L[b].rec);
+    const uint32_t t_nn = nx.t;
+    const uint64_t db_nn = nx.db;
+    nx.fetch(o, list, bi + 3 * g, nb);
+#pragma unroll
+    for (int k = 0; k < kMPer; k++) cl[k] = ncl[k], wd[k] = nwd[k], rk[k] = nrk[k];
+    t_cur = t_nxt, db_cur = db_nxt;
+    t_nxt = t_nn, db_nxt = db_nn;
+  }
+}
+#else
 template <int kSlots>
 __global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs o, const uint32_t *__restrict__ list,
                                                       const unsigned int *__restrict__ count) {
@@ -1251,6 +1329,7 @@ __global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs
     if (tid == 0) o.dcount[t] = D;
   }
 }
+#endif
 
 // client -> partition: a hash independent of table_slot's (which takes the
 // top bits of client * 2654435769: a partition must spread over the table)

@@ -8,6 +8,8 @@
 #   fastt   : small-batch path + batching collector + shim tests -> gpurun_out/TAG/pytest_fast.log
 #   quick   : every -m gpu test except the full-size ones
 #   lat     : C3 bench with the per-publish legs (single topic, 64 native callers direct / batched)
+#   variants: `fast` once per tuning build maxmq_amd/_lib/<name>/ (make variant) -> bench_fast_<name>.json
+#   c4fast / c4var: the C4 shard bench without CPU baseline (default build / every variant)
 #   smoke   : __graft_entry__.smoke()
 #   bench   : the default bench line (C3)                -> gpurun_out/TAG/bench.json
 #   fast    : bench without CPU baseline / host path      -> gpurun_out/TAG/bench_fast.json
@@ -22,7 +24,7 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p $OUT
 cd $ROOT
-FAST="--steps 10 --warmup 3 --no-cpu-baseline --host-topics 0 --latency-topics 0"
+FAST="--steps 10 --warmup 3 --no-cpu-baseline --host-topics 0 --latency-topics 0 --steady-steps 0"
 PYT="python3 -u -m pytest -x -v --timeout-method thread"
 for step in "$@"; do
   echo "[run_r03] $step $(date +%T)"
@@ -38,6 +40,12 @@ for step in "$@"; do
              > $OUT/pytest_quick.log 2>&1 ;;
     lat) timeout -k 10 600 python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --host-topics 0 \
              > $OUT/bench_lat.json 2> $OUT/bench_lat.log ;;
+    variants) for L in maxmq_amd/_lib/*/libmqmatch.so; do V=$(basename $(dirname $L)); [ "$V" = asan ] && continue;
+             MQM_LIB=$ROOT/$L timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_$V.json 2> $OUT/bench_fast_$V.log || exit 1; done ;;
+    c4fast) timeout -k 10 600 python3 -u bench.py --config 4 --shard 0/8 $FAST > $OUT/bench_c4_fast.json 2> $OUT/bench_c4_fast.log ;;
+    c4var) for L in maxmq_amd/_lib/*/libmqmatch.so; do V=$(basename $(dirname $L)); [ "$V" = asan ] && continue;
+             MQM_LIB=$ROOT/$L timeout -k 10 600 python3 -u bench.py --config 4 --shard 0/8 $FAST > $OUT/bench_c4_fast_$V.json \
+             2> $OUT/bench_c4_fast_$V.log || exit 1; done ;;
     smoke) timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 ;;
     bench) timeout -k 10 600 python3 -u bench.py > $OUT/bench.json 2> $OUT/bench.log ;;
     fast) timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast.json 2> $OUT/bench_fast.log ;;

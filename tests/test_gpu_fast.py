@@ -72,8 +72,9 @@ def test_fast_batches_vs_oracle_and_pipeline(monkeypatch, config, overrides):
         assert_same(gs, rs, f"packed batch of {size} (shared)")
     # single-topic calls (mqm_subscribers, the reference's per-publish shape)
     for i in rng.choice(n, size=50, replace=False):
-        t = bytes(w.topics[int(i)]).decode("utf-8", "surrogateescape")
-        assert fast.subscribers(t).subscriptions == pipe.subscribers(t).subscriptions, t
+        t = w.topics[int(i)]
+        a, b = fast.subscribers(t), pipe.subscribers(t)
+        assert a.subscriptions == b.subscriptions and a.shared == b.shared, t
 
 
 def test_fast_partitioned_merge_and_overflow_regrowth(monkeypatch):
