@@ -18,6 +18,10 @@
 //     snapshot its device results refer to until its next call).
 #include <hip/hip_runtime.h>
 
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -169,8 +173,26 @@ struct mqm_result {
   const uint32_t *shared = nullptr, *idents = nullptr;
   bool has_idents = false;               // MQM_CFG_IDENTIFIERS
   std::shared_ptr<const HostSnapshot> snap;
+  bool heap = false;  // blk from malloc (results filled by host copies, no DMA into them)
   ~mqm_result() {
-    if (pool) pool->put(blk, blk_cap);
+    if (heap)
+      free(blk);
+    else if (pool)
+      pool->put(blk, blk_cap);
+  }
+  // the result's block: pinned (from the index's pool) when a DMA fills it,
+  // plain host memory when host copies do
+  bool alloc(const std::shared_ptr<PinnedPool> &p, size_t bytes, bool pinned) {
+    if (pinned) {
+      pool = p;
+      blk = p->get(bytes, &blk_cap);
+      if (!blk) pool.reset();
+    } else {
+      heap = true;
+      blk = malloc(std::max<size_t>(bytes, 64));
+      blk_cap = bytes;
+    }
+    return blk != nullptr;
   }
 };
 
@@ -399,12 +421,7 @@ int fast_result(mqm_index *h, const std::shared_ptr<GpuSnapshot> &snap, const Fa
     ns += fo.recs[i].hcount;
   }
   const ResultLayout lay(n + 1ull, nd, ns, packed ? 4 : 8);
-  r->pool = h->pinned;
-  r->blk = h->pinned->get(lay.total, &r->blk_cap);
-  if (!r->blk) {
-    r->pool.reset();
-    return MQM_ENOMEM;
-  }
+  if (!r->alloc(h->pinned, lay.total, false)) return MQM_ENOMEM;
   char *B = static_cast<char *>(r->blk);
   auto *off = reinterpret_cast<uint64_t *>(B), *soff = reinterpret_cast<uint64_t *>(B + lay.o_sh);
   auto *dl = reinterpret_cast<uint64_t *>(B + lay.o_d);
@@ -1085,33 +1102,59 @@ void mqm_messages_free(mqm_messages *m) { delete m; }
 namespace {
 
 // MQM_CFG_BATCHING: single-topic calls queue a request and wait; worker
-// threads drain the queue into GPU batches and hand every caller its own
-// single-topic result (a pinned block from the index's pool).  Calls that
-// arrive while a batch runs form the next one, so batches grow with the
-// offered load and an idle index adds no latency.  Two workers by default:
-// while one waits for its batch on the GPU, the other gathers and launches
-// the next (each borrows its own context: workspace and stream).  A batch
-// takes the small-batch path (fast.hip: one launch, results read straight
-// from its pinned blocks), or mqm_match_batch when Identifiers are on or a
-// topic is past that path's capacities.
+// threads drain the queue into GPU batches.  Calls that arrive while a batch
+// runs form the next one, so batches grow with the offered load and an idle
+// index adds no latency.  MQM_BATCH_WORKERS workers (default 3): while one
+// waits for its batch on the GPU, the others gather and launch the next ones
+// (each borrows its own context: workspace, stream, pinned blocks).  A batch
+// takes the small-batch path (fast.hip: one launch); each caller is woken on
+// its own futex and copies its own topic's result out of the batch's pinned
+// blocks (in parallel, on the callers' threads); the last one returns the
+// context to the pool.  With Identifiers on, or a topic past the small-batch
+// path's capacities, the worker runs mqm_match_batch and splits the result.
 struct Collector {
+  struct Batch {  // one small-batch call, shared by its callers until they have copied their results
+    mqm_index *h = nullptr;
+    std::unique_ptr<MatchCtx> ctx;
+    std::shared_ptr<GpuSnapshot> snap;
+    FastOutput fo;
+    std::atomic<uint32_t> refs{0};
+    void release() {
+      if (refs.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+        ctx_release(h, std::move(ctx));
+        delete this;
+      }
+    }
+  };
   struct Req {
     const char *topic;
     size_t len;
     mqm_result *res = nullptr;
     int rc = MQM_OK;
-    bool done = false;
+    Batch *batch = nullptr;  // set: copy topic `index` of the batch's result
+    uint32_t index = 0;
+    std::atomic<uint32_t> state{0};  // futex word: 0 waiting, 1 done
+    void wake() {
+      state.store(1, std::memory_order_release);
+      syscall(SYS_futex, reinterpret_cast<uint32_t *>(&state), FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+    }
+    void wait() {
+      while (state.load(std::memory_order_acquire) == 0)
+        syscall(SYS_futex, reinterpret_cast<uint32_t *>(&state), FUTEX_WAIT_PRIVATE, 0, nullptr, nullptr, 0);
+    }
   };
   mqm_index *h;
   std::mutex mu;
-  std::condition_variable cv, cv_done;
+  std::condition_variable cv;
   std::vector<Req *> q;
   bool stop = false;
   uint32_t max_batch = 8192, linger_us = 0;
   uint64_t batches = 0, topics = 0;
   std::vector<std::thread> ths;
 
-  explicit Collector(mqm_index *idx, int workers = 2) : h(idx) {
+  explicit Collector(mqm_index *idx) : h(idx) {
+    int workers = 3;
+    if (const char *e = getenv("MQM_BATCH_WORKERS")) workers = std::max(1, std::min(16, atoi(e)));
     for (int i = 0; i < workers; i++) ths.emplace_back([this] { run(); });
   }
   ~Collector() {
@@ -1130,25 +1173,28 @@ struct Collector {
       q.push_back(&r);
     }
     cv.notify_one();
-    std::unique_lock<std::mutex> lk(mu);
-    cv_done.wait(lk, [&] { return r.done; });
+    r.wait();
+    if (r.batch) {  // the small-batch path: this caller's topic, copied off the batch's blocks
+      const FastRec &x = r.batch->fo.recs[r.index];
+      try {
+        r.rc = single(r.batch->snap->host, r.batch->fo.dout + x.dbase, x.dcount, r.batch->fo.hout + x.hbase,
+                      x.hcount, nullptr, 0, false, &r.res);
+      } catch (const std::bad_alloc &) {
+        r.rc = MQM_ENOMEM;
+      }
+      r.batch->release();
+    }
     *out = r.res;
     return r.rc;
   }
 
-  // one topic's deliveries / shared candidates as a result of its own
-  static int single(mqm_index *h, std::shared_ptr<const HostSnapshot> hs, const uint64_t *dl, uint64_t d,
-                    const uint32_t *sh, uint64_t sn, const uint32_t *ids, uint64_t in, bool has_ids,
-                    mqm_result **out) {
+  // one topic's deliveries / shared candidates as a result of its own (host memory)
+  static int single(std::shared_ptr<const HostSnapshot> hs, const uint64_t *dl, uint64_t d, const uint32_t *sh,
+                    uint64_t sn, const uint32_t *ids, uint64_t in, bool has_ids, mqm_result **out) {
     auto r = std::make_unique<mqm_result>();
     auto up = [](uint64_t x) { return (x + 15) & ~15ull; };
     const uint64_t o_sh = 16, o_io = 32, o_d = 48, o_s = o_d + up(8 * d), o_i = o_s + up(4 * sn), total = o_i + up(4 * in);
-    r->pool = h->pinned;
-    r->blk = h->pinned->get(total, &r->blk_cap);
-    if (!r->blk) {
-      r->pool.reset();
-      return MQM_ENOMEM;
-    }
+    if (!r->alloc(nullptr, total, false)) return MQM_ENOMEM;
     char *B = static_cast<char *>(r->blk);
     uint64_t *off = reinterpret_cast<uint64_t *>(B), *soff = reinterpret_cast<uint64_t *>(B + o_sh),
              *ioff = reinterpret_cast<uint64_t *>(B + o_io);
@@ -1175,43 +1221,35 @@ struct Collector {
   }
 
   // topic i of batch result b as a result of its own
-  static int split(mqm_index *h, const mqm_result *b, uint32_t i, mqm_result **out) {
+  static int split(const mqm_result *b, uint32_t i, mqm_result **out) {
     const uint64_t d0 = b->offsets[i], d = b->offsets[i + 1] - d0;
     const uint64_t s0 = b->shared_offsets[i], sn = b->shared_offsets[i + 1] - s0;
     const uint64_t i0 = b->has_idents ? b->ident_offsets[i] : 0, in = b->has_idents ? b->ident_offsets[i + 1] - i0 : 0;
-    return single(h, b->snap, reinterpret_cast<const uint64_t *>(b->deliveries) + d0, d, b->shared + s0, sn,
+    return single(b->snap, reinterpret_cast<const uint64_t *>(b->deliveries) + d0, d, b->shared + s0, sn,
                   b->has_idents ? b->idents + i0 : nullptr, in, b->has_idents, out);
   }
 
-  // the batch on the small-batch path, every caller's result split off the
-  // pinned blocks; false: not taken (the caller falls back to mqm_match_batch)
-  bool run_fast(const std::vector<Req *> &batch, const std::string &bytes, const std::vector<uint64_t> &offs) {
-    if ((h->cfg.flags & MQM_CFG_IDENTIFIERS) || !h->fast_path || batch.size() > kFastMaxTopics) return false;
-    if (hipSetDevice(h->cfg.device) != hipSuccess) return false;
-    std::shared_ptr<GpuSnapshot> snap;
-    if (front(h, &snap) != MQM_OK) return false;
+  // the batch on the small-batch path: a Batch the callers copy their results
+  // from; nullptr when not taken (the worker falls back to mqm_match_batch)
+  Batch *run_fast(const std::vector<Req *> &batch, const std::string &bytes, const std::vector<uint64_t> &offs) {
+    if ((h->cfg.flags & MQM_CFG_IDENTIFIERS) || !h->fast_path || batch.size() > kFastMaxTopics) return nullptr;
+    if (hipSetDevice(h->cfg.device) != hipSuccess) return nullptr;
+    auto b = std::make_unique<Batch>();
+    b->h = h;
+    if (front(h, &b->snap) != MQM_OK) return nullptr;
     int rc = MQM_OK;
-    auto c = ctx_acquire(h, &rc);
-    if (rc != MQM_OK) return false;
-    c->ws.begin(c->stream);
-    FastOutput fo;
-    const int e = match_small(snap->dev, c->ws, bytes.data(), offs.data(), (uint32_t)batch.size(), c->stream, &fo);
-    const int e2 = c->ws.end(c->stream);
+    b->ctx = ctx_acquire(h, &rc);
+    if (rc != MQM_OK) return nullptr;
+    b->ctx->ws.begin(b->ctx->stream);
+    const int e = match_small(b->snap->dev, b->ctx->ws, bytes.data(), offs.data(), (uint32_t)batch.size(),
+                              b->ctx->stream, &b->fo);
+    const int e2 = b->ctx->ws.end(b->ctx->stream);
     if (e != 0 || e2) {
-      ctx_release(h, std::move(c));
-      return false;
+      ctx_release(h, std::move(b->ctx));
+      return nullptr;
     }
-    for (uint32_t i = 0; i < batch.size(); i++) {
-      const FastRec &x = fo.recs[i];
-      try {
-        batch[i]->rc = single(h, snap->host, fo.dout + x.dbase, x.dcount, fo.hout + x.hbase, x.hcount, nullptr, 0,
-                              false, &batch[i]->res);
-      } catch (const std::bad_alloc &) {
-        batch[i]->rc = MQM_ENOMEM;
-      }
-    }
-    ctx_release(h, std::move(c));
-    return true;
+    b->refs.store((uint32_t)batch.size(), std::memory_order_relaxed);
+    return b.release();
   }
 
   void run() {
@@ -1228,6 +1266,8 @@ struct Collector {
         const size_t n = std::min<size_t>(q.size(), max_batch);
         batch.assign(q.begin(), q.begin() + n);
         q.erase(q.begin(), q.begin() + n);
+        batches++;
+        topics += n;
         if (!q.empty()) cv.notify_one();  // more queued than one batch: wake another worker
       }
       bytes.clear();
@@ -1236,34 +1276,34 @@ struct Collector {
         bytes.append(r->topic, r->len);
         offs.push_back(bytes.size());
       }
-      bool fast = false;
+      Batch *fb = nullptr;
       try {
-        fast = run_fast(batch, bytes, offs);
+        fb = run_fast(batch, bytes, offs);
       } catch (...) {
-        fast = false;
+        fb = nullptr;
       }
-      if (!fast) {
-        mqm_result *b = nullptr;
-        const int rc = mqm_match_batch(h, bytes.data(), offs.data(), (uint32_t)batch.size(), &b);
+      if (fb) {
         for (uint32_t i = 0; i < batch.size(); i++) {
-          batch[i]->rc = rc;
-          if (rc == MQM_OK) {
-            try {
-              batch[i]->rc = split(h, b, i, &batch[i]->res);
-            } catch (const std::bad_alloc &) {
-              batch[i]->rc = MQM_ENOMEM;
-            }
+          batch[i]->batch = fb;
+          batch[i]->index = i;
+          batch[i]->wake();
+        }
+        continue;
+      }
+      mqm_result *b = nullptr;
+      const int rc = mqm_match_batch(h, bytes.data(), offs.data(), (uint32_t)batch.size(), &b);
+      for (uint32_t i = 0; i < batch.size(); i++) {
+        batch[i]->rc = rc;
+        if (rc == MQM_OK) {
+          try {
+            batch[i]->rc = split(b, i, &batch[i]->res);
+          } catch (const std::bad_alloc &) {
+            batch[i]->rc = MQM_ENOMEM;
           }
         }
-        if (b) mqm_result_free(b);
       }
-      {
-        std::lock_guard<std::mutex> g(mu);
-        for (Req *r : batch) r->done = true;
-        batches++;
-        topics += batch.size();
-      }
-      cv_done.notify_all();
+      if (b) mqm_result_free(b);
+      for (Req *r : batch) r->wake();
     }
   }
 };

@@ -1244,12 +1244,15 @@ __global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs
 #pragma unroll
     for (int k = 0; k < kMPer; k++) {
       const uint32_t q = tid + k * kBigThreads;
-      uint32_t h;
-      const uint32_t sid = multi_sid(rec, nh, q < M ? q : 0, &h);
-      const SubEnt e = q < M ? load_sub(s, sid) : SubEnt{0, 0};
-      c[k] = e.client;
-      w[k] = e.word;
-      r[k] = rec_at(rec, h, kFieldRank);
+      c[k] = w[k] = r[k] = 0;
+      if (q < M) {  // (slots past the topic's entries: no LDS search, no load)
+        uint32_t h;
+        const uint32_t sid = multi_sid(rec, nh, q, &h);
+        const SubEnt e = load_sub(s, sid);
+        c[k] = e.client;
+        w[k] = e.word;
+        r[k] = rec_at(rec, h, kFieldRank);
+      }
     }
   };
   NextTopic nx;
@@ -2017,7 +2020,9 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
   using W = Workspace;
   if (ws.pending) return -1;  // one call in flight per workspace (collect it first)
   // queued calls need every output buffer sized by an earlier call
-  exact = exact || !ws.caps_known;
+  // (MQM_QUEUED=0: every call exact, for A/B runs)
+  static const bool queued_ok = !getenv("MQM_QUEUED") || atoi(getenv("MQM_QUEUED")) != 0;
+  exact = exact || !ws.caps_known || !queued_ok;
   if (ws.get(W::kSCount, sizeof(uint32_t) * (n + 1)) || ws.get(W::kHCount, sizeof(uint32_t) * (n + 1)) ||
       ws.get(W::kDCount, sizeof(uint32_t) * (n + 1)) || ws.get(W::kDStart, sizeof(uint64_t) * (n + 1)) ||
       ws.get(W::kHStart, sizeof(uint64_t) * (n + 1)) || ws.get(W::kCls, n + 1) ||

@@ -26,8 +26,16 @@ STREAM = ("k_desc", "k_winmap", "k_wincopy", "k_route", "k_table_sizes",
 
 
 def kname(s):
-    m = re.match(r"(?:void )?(?:mqm::\(anonymous namespace\)::)?(k_\w+)", s)
-    return m.group(1) if m else None
+    """kernel name with its template argument when it has one (k_multi<2048>
+    -> k_multi2048: the workgroup merge tiers are reported apart)"""
+    m = re.match(r"(?:void )?(?:mqm::\(anonymous namespace\)::)?(k_\w+)(?:<(\d+)[,>])?", s)
+    if not m:
+        return None
+    return m.group(1) + (m.group(2) if m.group(1) == "k_multi" and m.group(2) else "")
+
+
+def base(k):
+    return re.sub(r"\d+$", "", k) if k else k
 
 
 root = sys.argv[1]
@@ -46,7 +54,7 @@ for path in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recur
     for row in rows:
         c = row.get("Counter_Name")
         k = kname(row.get("Kernel_Name", ""))
-        if c not in sums or k not in GATHER + STREAM or int(row["Dispatch_Id"]) < cut:
+        if c not in sums or base(k) not in GATHER + STREAM or int(row["Dispatch_Id"]) < cut:
             continue
         sums[c][k] += float(row["Counter_Value"])
         disp[c][k].add((path, row["Dispatch_Id"]))
@@ -54,7 +62,7 @@ kib = 1024.0
 # per batch: a kernel may launch more than once per batch (the k_multi tiers
 # share one name here), so divide by the batches (k_walk launches once each)
 div = (lambda c, k: 1) if last_call else (lambda c, k: len(disp[c]["k_walk"]) or len(disp[c][k]))
-reads = {k: v * kib * (1 if k in GATHER else 2) / div("FETCH_SIZE", k) for k, v in sums["FETCH_SIZE"].items()}
+reads = {k: v * kib * (1 if base(k) in GATHER else 2) / div("FETCH_SIZE", k) for k, v in sums["FETCH_SIZE"].items()}
 writes = {k: v * kib / div("WRITE_SIZE", k) for k, v in sums["WRITE_SIZE"].items()}
 out = {
     "read_bytes_per_batch_by_kernel": reads,

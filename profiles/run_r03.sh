@@ -10,6 +10,7 @@
 #   lat     : C3 bench with the per-publish legs (single topic, 64 native callers direct / batched)
 #   variants: `fast` once per tuning build maxmq_amd/_lib/<name>/ (make variant) -> bench_fast_<name>.json
 #   c4fast / c4var: the C4 shard bench without CPU baseline (default build / every variant)
+#   c4pmc / pmc: FETCH_SIZE / WRITE_SIZE passes (C4 shard / C3) -> traffic_c4.json / traffic.json
 #   smoke   : __graft_entry__.smoke()
 #   bench   : the default bench line (C3)                -> gpurun_out/TAG/bench.json
 #   fast    : bench without CPU baseline / host path      -> gpurun_out/TAG/bench_fast.json
@@ -46,6 +47,18 @@ for step in "$@"; do
     c4var) for L in maxmq_amd/_lib/*/libmqmatch.so; do V=$(basename $(dirname $L)); [ "$V" = asan ] && continue;
              MQM_LIB=$ROOT/$L timeout -k 10 600 python3 -u bench.py --config 4 --shard 0/8 $FAST > $OUT/bench_c4_fast_$V.json \
              2> $OUT/bench_c4_fast_$V.log || exit 1; done ;;
+    c4pmc) (cd /tmp && export TMPDIR=/tmp && for C in FETCH_SIZE WRITE_SIZE; do
+             timeout -s KILL 400 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/c4pmc/pmc_$C -o pmc \
+             -- python3 $ROOT/bench.py --config 4 --shard 0/8 --steps 1 --warmup 1 --no-cpu-baseline --host-topics 0 \
+             --latency-topics 0 --steady-steps 0 > $OUT/c4pmc_$C.json 2> $OUT/c4pmc_$C.log || exit 1; done) &&
+             python3 profiles/pmc_to_traffic.py $OUT/c4pmc > $OUT/traffic_c4.json ;;
+    pmc) (cd /tmp && export TMPDIR=/tmp && for C in FETCH_SIZE WRITE_SIZE; do
+             timeout -s KILL 300 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/pmc/pmc_$C -o pmc \
+             -- python3 $ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline --host-topics 0 \
+             --latency-topics 0 --steady-steps 0 > $OUT/pmc_$C.json 2> $OUT/pmc_$C.log || exit 1; done) &&
+             python3 profiles/pmc_to_traffic.py $OUT/pmc > $OUT/traffic.json ;;
+    abq) for V in 1 0; do MQM_QUEUED=$V timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_q$V.json \
+             2> $OUT/bench_fast_q$V.log || exit 1; done ;;
     smoke) timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 ;;
     bench) timeout -k 10 600 python3 -u bench.py > $OUT/bench.json 2> $OUT/bench.log ;;
     fast) timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast.json 2> $OUT/bench_fast.log ;;
