@@ -35,6 +35,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 
@@ -389,9 +390,12 @@ __global__ __launch_bounds__(kFT) void k_fast(DeviceSnapshot s, const uint8_t *_
     }
     __syncthreads();
   }
-  // the last workgroup to finish publishes the totals and resets the counters
+  // the last workgroup to finish publishes the totals and resets the counters;
+  // every workgroup's host writes are made visible (system scope) before its
+  // ticket, so a host that sees `done` sees every result
+  __syncthreads();
   if (tid == 0) {
-    __threadfence();
+    __threadfence_system();
     const unsigned int ticket = atomicAdd(&ctl->done, 1u);
     if (ticket == gridDim.x - 1) {
       __threadfence();
@@ -400,7 +404,8 @@ __global__ __launch_bounds__(kFT) void k_fast(DeviceSnapshot s, const uint8_t *_
       status->d_total = dt;
       status->h_total = ht;
       status->flags = fl;
-      status->done = 1;
+      __threadfence_system();
+      __hip_atomic_store(&status->done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       atomicExch(&ctl->dcur, 0ull);
       atomicExch(&ctl->hcur, 0ull);
       atomicExch(&ctl->flags, 0u);
@@ -426,7 +431,9 @@ int pinned_grow(void **p, size_t *cap, size_t need) {
   *p = nullptr;
   *cap = 0;
   const size_t n = std::max<size_t>(need + need / 4, 4096);
-  if (hipHostMalloc(p, n, hipHostMallocMapped) != hipSuccess) {
+  // coherent (fine-grained): the kernel's writes reach host memory as they
+  // are made, so the host can poll the status word instead of synchronising
+  if (hipHostMalloc(p, n, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
     *p = nullptr;
     return -2;
   }
@@ -479,6 +486,14 @@ int match_small(const DeviceSnapshot &s, Workspace &ws, const char *bytes, const
                        a.recs, a.dout, a.dout_cap / sizeof(uint64_t), a.hout, a.hout_cap / sizeof(uint32_t),
                        a.status);
     HIP_TRY(hipGetLastError());
+    // wait: poll the status word the last workgroup writes (a few us sooner
+    // than a stream synchronisation's wake-up), then synchronise anyway once
+    // it is set or after ~2 ms (errors are reported there)
+    {
+      volatile unsigned int *done = &a.status->done;
+      const auto t0 = std::chrono::steady_clock::now();
+      while (!*done && std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(2)) __builtin_ia32_pause();
+    }
     HIP_TRY(hipStreamSynchronize(st));
     FastStatus stt;
     memcpy(&stt, (const void *)a.status, sizeof(stt));  // after the stream synchronisation

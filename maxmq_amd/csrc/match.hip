@@ -1218,14 +1218,14 @@ __device__ __forceinline__ uint32_t block_winners(MergeTable tb, uint32_t nslots
   return total;
 }
 
-// MQM_MULTI_PIPE=1: software-pipelined k_multi — while topic i is merged,
+// MQM_MULTI_PIPE=1: software-pipelined k_multi (tuning knob) — while topic i is merged,
 // topic i+1's multi entries (client, word, rank) are already loading into
 // registers (its record double-buffered in LDS, topic i+2's record in
 // flight), so a topic no longer waits a dependent HBM round trip for its
 // entries after its record (the tier is latency-bound: ~400 entries a topic
 // at C3, 256 threads)
 #ifndef MQM_MULTI_PIPE
-#define MQM_MULTI_PIPE 1
+#define MQM_MULTI_PIPE 0  // measured slower on C3 (r03e: 16.99 vs 16.01 ms per batch, same box): off
 #endif
 #if MQM_MULTI_PIPE
 template <int kSlots>
@@ -2080,6 +2080,10 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
       launch_walk(k_walk<8, MQM_WALK_OCC>, 8);
   }
   HIP_TRY(hipGetLastError());
+  // MQM_FLUSH=1 (A/B): hand the queued walk to the device now (hipStreamQuery
+  // flushes the runtime's pending dispatches) instead of with later commands
+  static const bool flush = getenv("MQM_FLUSH") && atoi(getenv("MQM_FLUSH")) != 0;
+  if (flush) (void)hipStreamQuery(st);
   mark(ws, 1, st);
   // segment starts: exclusive scans of S (raw entries, an upper bound of a
   // topic's deliveries) and H (shared candidates); the solo descriptors'

@@ -59,6 +59,8 @@ for step in "$@"; do
              python3 profiles/pmc_to_traffic.py $OUT/pmc > $OUT/traffic.json ;;
     abq) for V in 1 0; do MQM_QUEUED=$V timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_q$V.json \
              2> $OUT/bench_fast_q$V.log || exit 1; done ;;
+    abf) for V in 0 1; do MQM_FLUSH=$V timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_flush$V.json \
+             2> $OUT/bench_fast_flush$V.log || exit 1; done ;;
     smoke) timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 ;;
     bench) timeout -k 10 600 python3 -u bench.py > $OUT/bench.json 2> $OUT/bench.log ;;
     fast) timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast.json 2> $OUT/bench_fast.log ;;
