@@ -400,13 +400,15 @@ void fill_device_result(const MatchOutput &mo, const Workspace &ws, mqm_device_r
 // a result block laid out like mqm_match_batch's: offsets | shared_offsets |
 // deliveries | shared (16-B aligned parts), from per-topic counts
 struct ResultLayout {
-  uint64_t o_sh = 0, o_d = 0, o_s = 0, total = 0;
-  ResultLayout(uint64_t n1, uint64_t nd, uint64_t ns, uint64_t dsize) {
+  uint64_t o_sh = 0, o_io = 0, o_d = 0, o_s = 0, o_i = 0, total = 0;
+  ResultLayout(uint64_t n1, uint64_t nd, uint64_t ns, uint64_t dsize, uint64_t ni = 0, bool ids = false) {
     auto up = [](uint64_t b) { return (b + 15) & ~15ull; };
     o_sh = up(8 * n1);
-    o_d = o_sh + up(8 * n1);
+    o_io = o_sh + up(8 * n1);
+    o_d = o_io + (ids ? up(8 * n1) : 0);
     o_s = o_d + up(dsize * nd);
-    total = o_s + up(4 * ns);
+    o_i = o_s + up(4 * ns);
+    total = o_i + up(4 * ni);
   }
 };
 
@@ -415,22 +417,31 @@ struct ResultLayout {
 int fast_result(mqm_index *h, const std::shared_ptr<GpuSnapshot> &snap, const FastOutput &fo, bool packed,
                 mqm_result *r) {
   const uint32_t n = fo.n_topics;
-  uint64_t nd = 0, ns = 0;
+  const bool ids = fo.iout != nullptr;
+  uint64_t nd = 0, ns = 0, ni = 0;
   for (uint32_t i = 0; i < n; i++) {
     nd += fo.recs[i].dcount;
     ns += fo.recs[i].hcount;
+    ni += ids ? fo.recs[i].icount : 0;
   }
-  const ResultLayout lay(n + 1ull, nd, ns, packed ? 4 : 8);
+  const ResultLayout lay(n + 1ull, nd, ns, packed ? 4 : 8, ni, ids);
   if (!r->alloc(h->pinned, lay.total, false)) return MQM_ENOMEM;
   char *B = static_cast<char *>(r->blk);
   auto *off = reinterpret_cast<uint64_t *>(B), *soff = reinterpret_cast<uint64_t *>(B + lay.o_sh);
+  auto *ioff = reinterpret_cast<uint64_t *>(B + lay.o_io);
   auto *dl = reinterpret_cast<uint64_t *>(B + lay.o_d);
   auto *sh = reinterpret_cast<uint32_t *>(B + lay.o_s);
-  uint64_t d = 0, q = 0;
+  auto *idv = reinterpret_cast<uint32_t *>(B + lay.o_i);
+  uint64_t d = 0, q = 0, k = 0;
   for (uint32_t i = 0; i < n; i++) {
     const FastRec &x = fo.recs[i];
     off[i] = d;
     soff[i] = q;
+    if (ids) {
+      ioff[i] = k;
+      if (x.icount) memcpy(idv + k, fo.iout + x.ibase, 4ull * x.icount);
+      k += x.icount;
+    }
     if (packed) {
       uint32_t *p4 = reinterpret_cast<uint32_t *>(dl) + d;
       for (uint32_t j = 0; j < x.dcount; j++) p4[j] = (uint32_t)(fo.dout[x.dbase + j] >> 32);
@@ -443,6 +454,12 @@ int fast_result(mqm_index *h, const std::shared_ptr<GpuSnapshot> &snap, const Fa
   }
   off[n] = d;
   soff[n] = q;
+  if (ids) {
+    ioff[n] = k;
+    r->has_idents = true;
+    r->ident_offsets = ioff;
+    r->idents = idv;
+  }
   r->n = n;
   r->offsets = off;
   r->shared_offsets = soff;
@@ -719,10 +736,10 @@ static int match_batch_impl(mqm_index *h, const char *topic_bytes, const uint64_
     const bool want_ids = (h->cfg.flags & MQM_CFG_IDENTIFIERS) != 0;
     // small batches (the per-publish call shape): the one-launch path, unless
     // a topic is past one of its capacities (then the pipeline below)
-    if (n_topics <= kFastMaxTopics && !want_ids && h->fast_path) {
+    if (n_topics <= kFastMaxTopics && h->fast_path) {
       c->ws.begin(c->stream);
       FastOutput fo;
-      const int e = match_small(snap->dev, c->ws, topic_bytes, topic_offsets, n_topics, c->stream, &fo);
+      const int e = match_small(snap->dev, c->ws, topic_bytes, topic_offsets, n_topics, c->stream, &fo, want_ids);
       const int e2 = c->ws.end(c->stream);
       if (e < 0 || e2) {
         ctx_release(h, std::move(c));
@@ -1110,8 +1127,8 @@ namespace {
 // takes the small-batch path (fast.hip: one launch); each caller is woken on
 // its own futex and copies its own topic's result out of the batch's pinned
 // blocks (in parallel, on the callers' threads); the last one returns the
-// context to the pool.  With Identifiers on, or a topic past the small-batch
-// path's capacities, the worker runs mqm_match_batch and splits the result.
+// context to the pool.  With a topic past the small-batch path's capacities
+// the worker runs mqm_match_batch and splits the result.
 struct Collector {
   struct Batch {  // one small-batch call, shared by its callers until they have copied their results
     mqm_index *h = nullptr;
@@ -1175,10 +1192,11 @@ struct Collector {
     cv.notify_one();
     r.wait();
     if (r.batch) {  // the small-batch path: this caller's topic, copied off the batch's blocks
-      const FastRec &x = r.batch->fo.recs[r.index];
+      const FastOutput &fo = r.batch->fo;
+      const FastRec &x = fo.recs[r.index];
       try {
-        r.rc = single(r.batch->snap->host, r.batch->fo.dout + x.dbase, x.dcount, r.batch->fo.hout + x.hbase,
-                      x.hcount, nullptr, 0, false, &r.res);
+        r.rc = single(r.batch->snap->host, fo.dout + x.dbase, x.dcount, fo.hout + x.hbase, x.hcount,
+                      fo.iout ? fo.iout + x.ibase : nullptr, fo.iout ? x.icount : 0, fo.iout != nullptr, &r.res);
       } catch (const std::bad_alloc &) {
         r.rc = MQM_ENOMEM;
       }
@@ -1232,7 +1250,7 @@ struct Collector {
   // the batch on the small-batch path: a Batch the callers copy their results
   // from; nullptr when not taken (the worker falls back to mqm_match_batch)
   Batch *run_fast(const std::vector<Req *> &batch, const std::string &bytes, const std::vector<uint64_t> &offs) {
-    if ((h->cfg.flags & MQM_CFG_IDENTIFIERS) || !h->fast_path || batch.size() > kFastMaxTopics) return nullptr;
+    if (!h->fast_path || batch.size() > kFastMaxTopics) return nullptr;
     if (hipSetDevice(h->cfg.device) != hipSuccess) return nullptr;
     auto b = std::make_unique<Batch>();
     b->h = h;
@@ -1242,7 +1260,7 @@ struct Collector {
     if (rc != MQM_OK) return nullptr;
     b->ctx->ws.begin(b->ctx->stream);
     const int e = match_small(b->snap->dev, b->ctx->ws, bytes.data(), offs.data(), (uint32_t)batch.size(),
-                              b->ctx->stream, &b->fo);
+                              b->ctx->stream, &b->fo, (h->cfg.flags & MQM_CFG_IDENTIFIERS) != 0);
     const int e2 = b->ctx->ws.end(b->ctx->stream);
     if (e != 0 || e2) {
       ctx_release(h, std::move(b->ctx));

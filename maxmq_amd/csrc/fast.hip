@@ -69,8 +69,8 @@ struct alignas(16) FastLds {
   uint64_t key0[kFLevels], key1[kFLevels];
   uint16_t sep[kFLevels];
   uint8_t stage[kFStage];
-  uint32_t nitems[2], nh, nsh, fail, nsep, fill, wsum[kFWaves];
-  unsigned long long dbase, hbase;
+  uint32_t nitems[2], nh, nsh, fail, nsep, fill, nid, wsum[kFWaves];
+  unsigned long long dbase, hbase, ibase;
 };
 
 __device__ __forceinline__ uint64_t f_lanemask_lt(int lane) { return (1ull << lane) - 1ull; }
@@ -146,7 +146,8 @@ __device__ __forceinline__ void f_prefix(const uint32_t *v, uint32_t *pre, uint3
 __global__ __launch_bounds__(kFT) void k_fast(DeviceSnapshot s, const uint8_t *__restrict__ tb,
                                               const uint64_t *__restrict__ to, uint32_t n, FastCtl *ctl,
                                               FastRec *__restrict__ recs, uint64_t *__restrict__ dout, uint64_t dcap,
-                                              uint32_t *__restrict__ hout, uint64_t hcap, FastStatus *status) {
+                                              uint32_t *__restrict__ hout, uint64_t hcap, uint32_t *__restrict__ iout,
+                                              uint64_t icap, FastStatus *status) {
   __shared__ FastLds L;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (uint32_t t = blockIdx.x; t < n; t += gridDim.x) {
@@ -275,7 +276,7 @@ __global__ __launch_bounds__(kFT) void k_fast(DeviceSnapshot s, const uint8_t *_
     if (L.fail) {  // block-uniform: the batch takes the pipeline without limits
       if (tid == 0) {
         atomicOr(&ctl->flags, kFastFallback);
-        recs[t] = FastRec{0, 0, 0, 0};
+        recs[t] = FastRec{0, 0, 0, 0, 0, 0};
       }
       __syncthreads();
       continue;
@@ -301,25 +302,30 @@ __global__ __launch_bounds__(kFT) void k_fast(DeviceSnapshot s, const uint8_t *_
       const unsigned long long need = (unsigned long long)Ss + Ms;
       const unsigned long long db = need ? atomicAdd(&ctl->dcur, need) : 0ull;
       const unsigned long long hb = H ? atomicAdd(&ctl->hcur, (unsigned long long)H) : 0ull;
-      const bool ovf = db + need > dcap || hb + H > hcap;
+      // identifiers: at most one per gathered entry
+      const unsigned long long ib = (iout && need) ? atomicAdd(&ctl->icur, need) : 0ull;
+      const bool ovf = db + need > dcap || hb + H > hcap || (iout && ib + need > icap);
       if (ovf) atomicOr(&ctl->flags, kFastOverflow);
       L.dbase = db;
       L.hbase = hb;
+      L.ibase = ib;
+      L.nid = 0;
       L.fail = ovf ? 1u : 0u;
     }
     __syncthreads();
     if (L.fail) {  // the host grows the blocks to the reported totals and runs the batch again
-      if (tid == 0) recs[t] = FastRec{0, 0, 0, 0};
+      if (tid == 0) recs[t] = FastRec{0, 0, 0, 0, 0, 0};
       __syncthreads();
       continue;
     }
-    const uint64_t db = L.dbase, hb = L.hbase;
+    const uint64_t db = L.dbase, hb = L.hbase, ib = L.ibase;
     // solo entries: each its client's merged delivery as is
     for (uint32_t q = tid; q < Ss; q += kFT) {
       const uint32_t h = f_search(L.spre, nh, q);
       const uint32_t sid = L.hoff[h] + (q - L.spre[h]);
       const uint2 e = *reinterpret_cast<const uint2 *>(s.subs + sid);
       dout[db + q] = (uint64_t)e.x | ((uint64_t)(e.y & kPackedMask) << 32);
+      if (iout && (e.y & kWordIdent)) iout[ib + atomicAdd(&L.nid, 1u)] = sid;  // packets.go:257-259
     }
     // shared candidates
     for (uint32_t j = tid; j < H; j += kFT) {
@@ -346,6 +352,7 @@ __global__ __launch_bounds__(kFT) void k_fast(DeviceSnapshot s, const uint8_t *_
         const uint32_t sid = L.hoff[h] + (L.hcnt[h] - L.hmu[h]) + (q - L.mpre[h]);
         const uint2 e = *reinterpret_cast<const uint2 *>(s.subs + sid);
         if (P > 1 && f_partition(e.x, P) != p) continue;
+        if (iout && (e.y & kWordIdent)) iout[ib + atomicAdd(&L.nid, 1u)] = sid;
         if (atomicAdd(&L.fill, 1u) >= (P > 1 ? kFFill : mask)) {  // an unlucky partition: never spin
           atomicOr(&L.fail, 1u);
           continue;
@@ -386,7 +393,7 @@ __global__ __launch_bounds__(kFT) void k_fast(DeviceSnapshot s, const uint8_t *_
     __syncthreads();
     if (tid == 0) {
       if (L.fail) atomicOr(&ctl->flags, kFastFallback);
-      recs[t] = FastRec{(uint32_t)db, Ss + W, (uint32_t)hb, H};
+      recs[t] = FastRec{(uint32_t)db, Ss + W, (uint32_t)hb, H, (uint32_t)ib, L.nid};
     }
     __syncthreads();
   }
@@ -399,15 +406,18 @@ __global__ __launch_bounds__(kFT) void k_fast(DeviceSnapshot s, const uint8_t *_
     const unsigned int ticket = atomicAdd(&ctl->done, 1u);
     if (ticket == gridDim.x - 1) {
       __threadfence();
-      const unsigned long long dt = atomicAdd(&ctl->dcur, 0ull), ht = atomicAdd(&ctl->hcur, 0ull);
+      const unsigned long long dt = atomicAdd(&ctl->dcur, 0ull), ht = atomicAdd(&ctl->hcur, 0ull),
+                               it = atomicAdd(&ctl->icur, 0ull);
       const unsigned int fl = atomicOr(&ctl->flags, 0u);
       status->d_total = dt;
       status->h_total = ht;
+      status->i_total = it;
       status->flags = fl;
       __threadfence_system();
       __hip_atomic_store(&status->done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       atomicExch(&ctl->dcur, 0ull);
       atomicExch(&ctl->hcur, 0ull);
+      atomicExch(&ctl->icur, 0ull);
       atomicExch(&ctl->flags, 0u);
       atomicExch(&ctl->done, 0u);
       __threadfence_system();
@@ -444,13 +454,14 @@ int pinned_grow(void **p, size_t *cap, size_t need) {
 }  // namespace
 
 FastArena::~FastArena() {
-  for (void *p : {(void *)in_bytes, (void *)in_offs, (void *)recs, (void *)dout, (void *)hout, (void *)status})
+  for (void *p : {(void *)in_bytes, (void *)in_offs, (void *)recs, (void *)dout, (void *)hout, (void *)iout,
+                  (void *)status})
     if (p) (void)hipHostFree(p);
   if (ctl) (void)hipFree(ctl);
 }
 
 int match_small(const DeviceSnapshot &s, Workspace &ws, const char *bytes, const uint64_t *offs, uint32_t n,
-                hipStream_t st, FastOutput *out) {
+                hipStream_t st, FastOutput *out, bool want_ids) {
   FastArena &a = ws.fast;
   const uint64_t base = offs[0], nbytes = offs[n] - base;
   if (!a.ctl) {
@@ -476,6 +487,7 @@ int match_small(const DeviceSnapshot &s, Workspace &ws, const char *bytes, const
   if (!a.dout && (pinned_grow((void **)&a.dout, &a.dout_cap, sizeof(uint64_t) * (1u << 16)) ||
                   pinned_grow((void **)&a.hout, &a.hout_cap, sizeof(uint32_t) * (1u << 12))))
     return -2;
+  if (want_ids && !a.iout && pinned_grow((void **)&a.iout, &a.iout_cap, sizeof(uint32_t) * (1u << 16))) return -2;
   // the previous call on this workspace has been waited for (its results read)
   if (nbytes) memcpy(a.in_bytes, bytes + base, nbytes);
   for (uint32_t i = 0; i <= n; i++) a.in_offs[i] = offs[i] - base;
@@ -484,7 +496,7 @@ int match_small(const DeviceSnapshot &s, Workspace &ws, const char *bytes, const
     const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(n, a.grid));
     hipLaunchKernelGGL(k_fast, dim3(grid), dim3(kFT), 0, st, s, (const uint8_t *)a.in_bytes, a.in_offs, n, a.ctl,
                        a.recs, a.dout, a.dout_cap / sizeof(uint64_t), a.hout, a.hout_cap / sizeof(uint32_t),
-                       a.status);
+                       want_ids ? a.iout : nullptr, a.iout_cap / sizeof(uint32_t), a.status);
     HIP_TRY(hipGetLastError());
     // wait: poll the status word the last workgroup writes (a few us sooner
     // than a stream synchronisation's wake-up), then synchronise anyway once
@@ -506,11 +518,13 @@ int match_small(const DeviceSnapshot &s, Workspace &ws, const char *bytes, const
       out->recs = a.recs;
       out->dout = a.dout;
       out->hout = a.hout;
+      out->iout = want_ids ? a.iout : nullptr;
       return 0;
     }
-    // a result block was too small: grow both to the totals this attempt reported
+    // a result block was too small: grow them to the totals this attempt reported
     if (pinned_grow((void **)&a.dout, &a.dout_cap, sizeof(uint64_t) * (stt.d_total + 1)) ||
-        pinned_grow((void **)&a.hout, &a.hout_cap, sizeof(uint32_t) * (stt.h_total + 1)))
+        pinned_grow((void **)&a.hout, &a.hout_cap, sizeof(uint32_t) * (stt.h_total + 1)) ||
+        (want_ids && pinned_grow((void **)&a.iout, &a.iout_cap, sizeof(uint32_t) * (stt.i_total + 1))))
       return -2;
   }
   return 1;

@@ -13,16 +13,18 @@ namespace mqm {
 // ---- small-batch path (fast.hip) --------------------------------------------
 // device counters of one k_fast launch; the last workgroup resets them
 struct FastCtl {
-  unsigned long long dcur, hcur;  // delivery / shared-candidate slots reserved
+  unsigned long long dcur, hcur, icur;  // delivery / shared-candidate / identifier slots reserved
   unsigned int flags, done;
 };
 enum : uint32_t { kFastFallback = 1u, kFastOverflow = 2u };
-// topic t's result: deliveries dout[dbase .. + dcount), shared hout[hbase .. + hcount)
+// topic t's result: deliveries dout[dbase .. + dcount), shared hout[hbase ..
+// + hcount), Identifiers support iout[ibase .. + icount) (the sids of its
+// gathered non-shared subscriptions with Identifier > 0, kWordIdent)
 struct FastRec {
-  uint32_t dbase, dcount, hbase, hcount;
+  uint32_t dbase, dcount, hbase, hcount, ibase, icount;
 };
 struct FastStatus {  // written by the last workgroup (pinned)
-  unsigned long long d_total, h_total;
+  unsigned long long d_total, h_total, i_total;
   unsigned int flags, done;
 };
 // pinned, device-mapped host blocks of one context (grown, never shrunk)
@@ -32,8 +34,9 @@ struct FastArena {
   FastRec *recs = nullptr;
   uint64_t *dout = nullptr;  // {client, packed} deliveries (mqm_delivery)
   uint32_t *hout = nullptr;  // shared-subscription ids
+  uint32_t *iout = nullptr;  // identifier sids (MQM_CFG_IDENTIFIERS)
   FastStatus *status = nullptr;
-  size_t in_cap = 0, offs_cap = 0, rec_cap = 0, dout_cap = 0, hout_cap = 0, status_cap = 0;
+  size_t in_cap = 0, offs_cap = 0, rec_cap = 0, dout_cap = 0, hout_cap = 0, iout_cap = 0, status_cap = 0;
   FastCtl *ctl = nullptr;  // device
   uint32_t grid = 0;       // resident k_fast workgroups
   ~FastArena();
@@ -44,6 +47,7 @@ struct FastOutput {
   const FastRec *recs = nullptr;             // pinned host, n_topics
   const uint64_t *dout = nullptr;            // pinned host
   const uint32_t *hout = nullptr;            // pinned host
+  const uint32_t *iout = nullptr;            // pinned host (want_ids)
 };
 
 // Grow-only device buffers reused across batches (no allocation in steady state).
@@ -169,7 +173,7 @@ int match_collect(Workspace &ws, hipStream_t st, MatchOutput *out);
 // negative MQM_E* code.
 constexpr uint32_t kFastMaxTopics = 4096;
 int match_small(const DeviceSnapshot &s, Workspace &ws, const char *bytes, const uint64_t *offs, uint32_t n,
-                hipStream_t st, FastOutput *out);
+                hipStream_t st, FastOutput *out, bool want_ids = false);
 
 // Identifiers support for the last match_device call on `ws` (its topic
 // buffers must still hold the batch): per topic, the sids of the gathered

@@ -13,7 +13,7 @@ import pytest
 
 import maxmq_amd
 from oracle.binding import OracleIndex
-from tests.gpu_util import assert_same, canon_gpu, canon_oracle
+from tests.gpu_util import assert_same, canon_gpu, canon_gpu_idents, canon_oracle, canon_oracle_idents
 from tools import mqgen
 from tools.mqgen import Strings
 
@@ -132,3 +132,26 @@ def test_fast_capacity_fallback(monkeypatch):
     _check(fast, pipe, ora, topics, "capacity fallback")
     # a topic level that is '+' or '#' (a topic the broker would refuse) and "" and "$SYS/x"
     _check(fast, pipe, ora, ["", "+/a/b/z", "#", "$SYS/x", "/", "//"], "odd topics")
+
+
+def test_fast_identifiers_vs_oracle(monkeypatch):
+    """MQM_CFG_IDENTIFIERS (the Go shim's configuration) on the small-batch
+    path: every delivery's full Identifiers map (packets.go:250-259) equals the
+    oracle's, and the batch pipeline's on the same index built with
+    MQM_NO_FAST=1."""
+    w = mqgen.generate(1, n_filters=20000, n_topics=5000, p_shared=0.05)
+    monkeypatch.setenv("MQM_NO_FAST", "1")
+    pipe = maxmq_amd.TopicsIndex(0, identifiers=True)
+    monkeypatch.delenv("MQM_NO_FAST")
+    fast = maxmq_amd.TopicsIndex(0, identifiers=True)
+    ora = OracleIndex()
+    for idx in (pipe, fast):
+        idx.subscribe_workload(w)
+    ora.subscribe_workload(w)
+    for lo, hi in ((0, 1), (1, 65), (65, 4096)):
+        s = Strings.from_list([w.topics[i] for i in range(lo, hi)])
+        g = canon_gpu_idents(fast.match_batch(s.data, s.offs))
+        p = canon_gpu_idents(pipe.match_batch(s.data, s.offs))
+        r = canon_oracle_idents(*ora.identifiers(s.data, s.offs, nthreads=8))
+        assert np.array_equal(g, r), f"topics [{lo}, {hi}): fast vs oracle identifiers"
+        assert np.array_equal(p, r), f"topics [{lo}, {hi}): pipeline vs oracle identifiers"
