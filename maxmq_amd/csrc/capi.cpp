@@ -1121,7 +1121,7 @@ namespace {
 // MQM_CFG_BATCHING: single-topic calls queue a request and wait; worker
 // threads drain the queue into GPU batches.  Calls that arrive while a batch
 // runs form the next one, so batches grow with the offered load and an idle
-// index adds no latency.  MQM_BATCH_WORKERS workers (default 4): while one
+// index adds no latency.  MQM_BATCH_WORKERS workers (default 3): while one
 // waits for its batch on the GPU, the others gather and launch the next ones
 // (each borrows its own context: workspace, stream, pinned blocks).  A batch
 // takes the small-batch path (fast.hip: one launch); each caller is woken on
@@ -1170,7 +1170,7 @@ struct Collector {
   std::vector<std::thread> ths;
 
   explicit Collector(mqm_index *idx) : h(idx) {
-    int workers = 4;
+    int workers = 3;
     if (const char *e = getenv("MQM_BATCH_WORKERS")) workers = std::max(1, std::min(16, atoi(e)));
     for (int i = 0; i < workers; i++) ths.emplace_back([this] { run(); });
   }

@@ -37,6 +37,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "device.h"
@@ -434,16 +435,17 @@ __global__ __launch_bounds__(kFT) void k_fast(DeviceSnapshot s, const uint8_t *_
     }                                                                                                     \
   } while (0)
 
-// a pinned, device-mapped host block of at least `need` bytes (grown, never shrunk)
-int pinned_grow(void **p, size_t *cap, size_t need) {
+// a pinned, device-mapped host block of at least `need` bytes (grown, never
+// shrunk); coherent (fine-grained: the kernel's writes reach host memory as
+// they are made) only for the status word the host polls — inputs and
+// results stay cached (coarse-grained), read after the stream synchronisation
+int pinned_grow(void **p, size_t *cap, size_t need, bool coherent = false) {
   if (*p && *cap >= need) return 0;
   if (*p) (void)hipHostFree(*p);
   *p = nullptr;
   *cap = 0;
   const size_t n = std::max<size_t>(need + need / 4, 4096);
-  // coherent (fine-grained): the kernel's writes reach host memory as they
-  // are made, so the host can poll the status word instead of synchronising
-  if (hipHostMalloc(p, n, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+  if (hipHostMalloc(p, n, hipHostMallocMapped | (coherent ? hipHostMallocCoherent : 0)) != hipSuccess) {
     *p = nullptr;
     return -2;
   }
@@ -482,7 +484,7 @@ int match_small(const DeviceSnapshot &s, Workspace &ws, const char *bytes, const
   if (pinned_grow((void **)&a.in_bytes, &a.in_cap, nbytes + 16) ||
       pinned_grow((void **)&a.in_offs, &a.offs_cap, sizeof(uint64_t) * (n + 1)) ||
       pinned_grow((void **)&a.recs, &a.rec_cap, sizeof(FastRec) * (n + 1)) ||
-      pinned_grow((void **)&a.status, &a.status_cap, sizeof(FastStatus)))
+      pinned_grow((void **)&a.status, &a.status_cap, sizeof(FastStatus), true))
     return -2;
   if (!a.dout && (pinned_grow((void **)&a.dout, &a.dout_cap, sizeof(uint64_t) * (1u << 16)) ||
                   pinned_grow((void **)&a.hout, &a.hout_cap, sizeof(uint32_t) * (1u << 12))))
@@ -498,13 +500,15 @@ int match_small(const DeviceSnapshot &s, Workspace &ws, const char *bytes, const
                        a.recs, a.dout, a.dout_cap / sizeof(uint64_t), a.hout, a.hout_cap / sizeof(uint32_t),
                        want_ids ? a.iout : nullptr, a.iout_cap / sizeof(uint32_t), a.status);
     HIP_TRY(hipGetLastError());
-    // wait: poll the status word the last workgroup writes (a few us sooner
-    // than a stream synchronisation's wake-up), then synchronise anyway once
-    // it is set or after ~2 ms (errors are reported there)
-    {
+    // MQM_FAST_POLL=us: poll the status word the last workgroup writes for up
+    // to that long before the stream synchronisation (which reports errors);
+    // off by default: measured slower under many concurrent callers
+    static const long poll_us = getenv("MQM_FAST_POLL") ? atol(getenv("MQM_FAST_POLL")) : 0;
+    if (poll_us > 0) {
       volatile unsigned int *done = &a.status->done;
       const auto t0 = std::chrono::steady_clock::now();
-      while (!*done && std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(2)) __builtin_ia32_pause();
+      while (!*done && std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(poll_us))
+        __builtin_ia32_pause();
     }
     HIP_TRY(hipStreamSynchronize(st));
     FastStatus stt;

@@ -61,6 +61,16 @@ for step in "$@"; do
              2> $OUT/bench_fast_q$V.log || exit 1; done ;;
     abf) for V in 0 1; do MQM_FLUSH=$V timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_flush$V.json \
              2> $OUT/bench_fast_flush$V.log || exit 1; done ;;
+    profser) (cd /tmp && export TMPDIR=/tmp MQM_NO_OVERLAP=1 && timeout -k 10 500 rocprofv3 --kernel-trace --stats \
+             --output-format csv -d $OUT/profser -o prof -- python3 $ROOT/bench.py $FAST \
+             > $OUT/bench_under_rocprof_serial.json 2> $OUT/rocprof_serial.log) ;;
+    c4profser) (cd /tmp && export TMPDIR=/tmp MQM_NO_OVERLAP=1 && timeout -k 10 500 rocprofv3 --kernel-trace --stats \
+             --output-format csv -d $OUT/prof_c4ser -o prof -- python3 $ROOT/bench.py --config 4 --shard 0/8 --steps 3 \
+             --warmup 1 --no-cpu-baseline --host-topics 0 --latency-topics 0 --steady-steps 0 \
+             > $OUT/c4_under_rocprof_serial.json 2> $OUT/rocprof_c4ser.log) ;;
+    latab) LAT="--steps 1 --warmup 0 --no-cpu-baseline --host-topics 0 --steady-steps 0"
+             for V in "A" "MQM_FAST_POLL=60" "MQM_BATCH_WORKERS=2" "MQM_BATCH_WORKERS=6"; do
+             env $V timeout -k 10 400 python3 -u bench.py $LAT > $OUT/bench_lat_${V//=/_}.json 2> $OUT/bench_lat_${V//=/_}.log || exit 1; done ;;
     smoke) timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 ;;
     bench) timeout -k 10 600 python3 -u bench.py > $OUT/bench.json 2> $OUT/bench.log ;;
     fast) timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast.json 2> $OUT/bench_fast.log ;;
