@@ -5,6 +5,10 @@
 
 #include "snapshot.h"
 
+#ifndef MQM_DESC32
+#define MQM_DESC32 1
+#endif
+
 namespace mqm {
 
 __device__ __forceinline__ NodeDesc load_desc(const NodeDesc *p) {
@@ -77,7 +81,22 @@ __device__ __forceinline__ uint32_t walk_step(const DeviceSnapshot &s, bool do_p
   uint64_t slot = do_probe ? bucket_of(h, s.n_buckets) * kEdgesPerBucket : 0;
   const uint4 *q = do_probe ? reinterpret_cast<const uint4 *>(s.edges + slot)
                             : reinterpret_cast<const uint4 *>(s.nodes + (do_desc ? wc : 0));
-  uint4 x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3];
+  uint4 x0 = q[0], x1 = q[1], x2, x3;
+#if MQM_DESC32
+  // a descriptor is 32 B: a wildcard step's lanes skip the entry's second half
+  // (the next descriptor, for an odd id in the next 64-B sector) — every load
+  // instruction costs the memory pipeline one access per distinct line it
+  // touches, so a masked lane saves an access, not only bytes
+  if (do_probe) {
+    x2 = q[2];
+    x3 = q[3];
+  } else {
+    x2 = x3 = make_uint4(0, 0, 0, 0);
+  }
+#else
+  x2 = q[2];
+  x3 = q[3];
+#endif
   uint32_t c = kNone;
   bool more = false;
   if (do_desc) {
@@ -102,6 +121,117 @@ __device__ __forceinline__ uint32_t walk_step(const DeviceSnapshot &s, bool do_p
       more = false;
     }
     if (!__any(more)) break;  // wave-uniform
+    if (more) {
+      slot = slot + 1 == nslots ? 0 : slot + 1;
+      const uint4 *e = reinterpret_cast<const uint4 *>(s.edges + slot);
+      x0 = e[0];
+      x1 = e[1];
+      x2 = e[2];
+      x3 = e[3];
+    }
+    do_probe = more;
+  }
+  return c;
+}
+
+// ---- cooperative form for a 4-lane group (k_walk<4>) ------------------------
+// A lane that loads a 64-B entry by itself issues four 16-B loads, each a line
+// access of its own, so a wave-instruction touches 64 lines and the memory
+// pipeline's per-line address work — not DRAM — bounds random gathers
+// (tools/calib_fetch: k_gather64 vs k_coop4x16).  Here the four lanes of a
+// group load each of their four items' blocks together, 16 B per lane (one
+// line per group per instruction), and a quad transpose (DPP, no LDS) hands
+// every lane its own item's block.
+template <int kCtrl>
+__device__ __forceinline__ uint32_t quad_dpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kCtrl, 0xF, 0xF, true);
+}
+template <int kCtrl>
+__device__ __forceinline__ uint4 quad_dpp4(uint4 v) {
+  return make_uint4(quad_dpp<kCtrl>(v.x), quad_dpp<kCtrl>(v.y), quad_dpp<kCtrl>(v.z), quad_dpp<kCtrl>(v.w));
+}
+// r[j] = chunk q of item j (q = this lane's index in its quad)  ->  r[j] = chunk j of item q
+__device__ __forceinline__ void quad_transpose(uint4 (&r)[4], int q) {
+  const bool h2 = q & 2, h1 = q & 1;
+#pragma unroll
+  for (int j = 0; j < 2; j++) {  // 2x2 blocks: lanes q, q ^ 2 swap the off-diagonal pair
+    const uint4 snd = h2 ? r[j] : r[j + 2];
+    const uint4 rcv = quad_dpp4<0x4E>(snd);  // quad_perm [2, 3, 0, 1]
+    if (h2)
+      r[j] = rcv;
+    else
+      r[j + 2] = rcv;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; j += 2) {  // inside each block: lanes q, q ^ 1
+    const uint4 snd = h1 ? r[j] : r[j + 1];
+    const uint4 rcv = quad_dpp4<0xB1>(snd);  // quad_perm [1, 0, 3, 2]
+    if (h1)
+      r[j] = rcv;
+    else
+      r[j + 1] = rcv;
+  }
+}
+
+// walk_step for lane q of a 4-lane group whose four lanes all call it together
+// (same arguments as walk_step)
+__device__ __forceinline__ uint32_t walk_step_quad(const DeviceSnapshot &s, bool do_probe, bool do_desc, bool use_bloom,
+                                                   uint32_t parent, uint32_t wc, uint64_t k0, uint64_t k1,
+                                                   const uint8_t *tok, uint32_t tok_len, NodeDesc *desc, int q) {
+  const Key key{k0, k1};
+  const uint64_t nslots = s.n_buckets * kEdgesPerBucket;
+  const uint64_t h = do_probe ? edge_hash(parent, key) : 0;
+  if (s.bloom) {
+    const bool chk = do_probe && use_bloom;
+    const uint64_t w = chk ? s.bloom[bloom_word(h, s.bloom_mask)] : ~0ull;
+    const uint64_t b = bloom_bits(h);
+    do_probe = do_probe && (w & b) == b;
+  }
+  uint64_t slot = do_probe ? bucket_of(h, s.n_buckets) * kEdgesPerBucket : 0;
+  // this lane's block | 1 (64-B edge entry) or | 2 (32-B descriptor); blocks are 32-B aligned
+  const uint64_t a = do_probe ? (reinterpret_cast<uint64_t>(s.edges + slot) | 1u)
+                              : do_desc ? (reinterpret_cast<uint64_t>(s.nodes + wc) | 2u) : 0;
+  const uint32_t alo = (uint32_t)a, ahi = (uint32_t)(a >> 32);
+  uint4 r[4];
+#define MQM_QUAD_LOAD(j)                                                                          \
+  {                                                                                               \
+    const uint32_t lo = quad_dpp<(j) * 0x55>(alo), hi = quad_dpp<(j) * 0x55>(ahi);                \
+    const uint32_t kd = lo & 3u;                                                                  \
+    const uint4 *p = reinterpret_cast<const uint4 *>((((uint64_t)hi << 32) | lo) & ~3ull) + q;    \
+    r[j] = make_uint4(0, 0, 0, 0);                                                                \
+    if (kd == 1u || (kd == 2u && q < 2)) r[j] = *p;                                               \
+  }
+  MQM_QUAD_LOAD(0)
+  MQM_QUAD_LOAD(1)
+  MQM_QUAD_LOAD(2)
+  MQM_QUAD_LOAD(3)
+#undef MQM_QUAD_LOAD
+  quad_transpose(r, q);
+  uint4 x0 = r[0], x1 = r[1], x2 = r[2], x3 = r[3];
+  uint32_t c = kNone;
+  bool more = false;
+  if (do_desc) {
+    c = wc;
+    *desc = NodeDesc{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+  }
+  for (;;) {  // a probe chain past its home slot (rare): per lane, as walk_step
+    if (do_probe && x1.x != kNone) {
+      const bool hit = x1.x == parent && (((uint64_t)x0.y << 32) | x0.x) == k0 &&
+                       (((uint64_t)x0.w << 32) | x0.z) == k1;
+      bool ok = hit;
+      if (hit && key_is_long(key)) {
+        ok = x1.w == tok_len;
+        for (uint32_t i = 0; ok && i < tok_len; i++) ok = s.tok_pool[x1.z + i] == tok[i];
+      }
+      if (ok) {
+        c = x1.y;
+        *desc = NodeDesc{x2.x, x2.y, x2.z, x2.w, x3.x, x3.y, x3.z, x3.w};
+      }
+      more = !ok;
+    } else {
+      more = false;
+    }
+    if (!__any(more)) break;
     if (more) {
       slot = slot + 1 == nslots ? 0 : slot + 1;
       const uint4 *e = reinterpret_cast<const uint4 *>(s.edges + slot);

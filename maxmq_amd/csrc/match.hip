@@ -90,6 +90,11 @@
 #ifndef MQM_COPY16
 #define MQM_COPY16 0
 #endif
+// MQM_WALK_COOP=1: k_walk<4> loads each group's edge entries / descriptors
+// cooperatively, 16 B per lane (device.h walk_step_quad)
+#ifndef MQM_WALK_COOP
+#define MQM_WALK_COOP 0
+#endif
 
 namespace mqm {
 
@@ -525,8 +530,13 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
         const uint32_t kind = iw & 3u, id = iw >> 2;
         const bool lit = kind == kItemLit || kind == kItemLitB;
         NodeDesc dc;
-        const uint32_t c = walk_step(s, live && lit && !lit_is_wild, live && !lit, kind == kItemLitB, id, id,
-                                     k0, k1, tp + tst, tln, &dc);
+        uint32_t c;
+        if constexpr (kG == 4 && MQM_WALK_COOP)  // the group's four items loaded together (device.h)
+          c = walk_step_quad(s, live && lit && !lit_is_wild, live && !lit, kind == kItemLitB, id, id, k0, k1,
+                             tp + tst, tln, &dc, gl);
+        else
+          c = walk_step(s, live && lit && !lit_is_wild, live && !lit, kind == kItemLitB, id, id, k0, k1, tp + tst,
+                        tln, &dc);
         const bool found = c != kNone;
 #if MQM_WALK_STATS
         {

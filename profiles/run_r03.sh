@@ -11,6 +11,7 @@
 #   variants: `fast` once per tuning build maxmq_amd/_lib/<name>/ (make variant) -> bench_fast_<name>.json
 #   c4fast / c4var: the C4 shard bench without CPU baseline (default build / every variant)
 #   c4pmc / pmc: FETCH_SIZE / WRITE_SIZE passes (C4 shard / C3) -> traffic_c4.json / traffic.json
+#   calib   : tools/_build/calib_fetch (random-gather / cooperative-gather rates) -> calib_kernels.txt
 #   smoke   : __graft_entry__.smoke()
 #   bench   : the default bench line (C3)                -> gpurun_out/TAG/bench.json
 #   fast    : bench without CPU baseline / host path      -> gpurun_out/TAG/bench_fast.json
@@ -71,6 +72,7 @@ for step in "$@"; do
     latab) LAT="--steps 1 --warmup 0 --no-cpu-baseline --host-topics 0 --steady-steps 0"
              for V in "MQM_BASE=1" "MQM_FAST_POLL=60" "MQM_BATCH_WORKERS=2" "MQM_BATCH_WORKERS=6"; do
              env $V timeout -k 10 400 python3 -u bench.py $LAT > $OUT/bench_lat_${V//=/_}.json 2> $OUT/bench_lat_${V//=/_}.log || exit 1; done ;;
+    calib) timeout -k 10 120 tools/_build/calib_fetch > $OUT/calib_kernels.txt 2>&1 ;;
     smoke) timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 ;;
     bench) timeout -k 10 600 python3 -u bench.py > $OUT/bench.json 2> $OUT/bench.log ;;
     fast) timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast.json 2> $OUT/bench_fast.log ;;

@@ -62,6 +62,20 @@ __global__ void k_gather(const uint4 *__restrict__ t, uint64_t n, uint4 *__restr
   if ((acc.x & acc.y & acc.z & acc.w) == 0x12345678u) sink[0] = acc;
 }
 
+// kL lanes read one random (kL x 16)-B entry together, 16 B each: one load
+// instruction touches 64 / kL lines instead of 64 (the walk's cooperative probe)
+template <int kL>
+__global__ void k_coop(const uint4 *__restrict__ t, uint64_t n, uint4 *__restrict__ sink) {
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  const uint64_t g0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kL, gs = (uint64_t)gridDim.x * blockDim.x / kL;
+  const int c = threadIdx.x % kL;
+  for (uint64_t i = g0; i < n; i += gs) {
+    const uint4 v = t[line_of(i) * 8 + c];
+    acc.x ^= v.x, acc.y ^= v.y, acc.z ^= v.z, acc.w ^= v.w;
+  }
+  if ((acc.x & acc.y & acc.z & acc.w) == 0x12345678u) sink[0] = acc;
+}
+
 __global__ void k_gather8(const uint2 *__restrict__ t, uint64_t n, uint4 *__restrict__ sink) {
   uint2 acc = make_uint2(0, 0);
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
@@ -104,7 +118,7 @@ int main() {
   struct Row {
     const char *name;
     double bytes;
-  } rows[8];
+  } rows[16];
   int nr = 0;
   hipEvent_t a, b;
   CHECK(hipEventCreate(&a));
@@ -128,6 +142,14 @@ int main() {
         [&] { hipLaunchKernelGGL(k_gather<4>, grid, block, 0, 0, t4, gathers, (uint4 *)sink); });
   timed("k_gather32", 32.0 * gathers,
         [&] { hipLaunchKernelGGL(k_gather<2>, grid, block, 0, 0, t4, gathers, (uint4 *)sink); });
+  timed("k_coop4x16", 64.0 * gathers,
+        [&] { hipLaunchKernelGGL(k_coop<4>, grid, block, 0, 0, t4, gathers, (uint4 *)sink); });
+  timed("k_coop2x16", 32.0 * gathers,
+        [&] { hipLaunchKernelGGL(k_coop<2>, grid, block, 0, 0, t4, gathers, (uint4 *)sink); });
+  timed("k_coop8x16", 128.0 * gathers,
+        [&] { hipLaunchKernelGGL(k_coop<8>, grid, block, 0, 0, t4, gathers, (uint4 *)sink); });
+  timed("k_coop1x16", 16.0 * gathers,
+        [&] { hipLaunchKernelGGL(k_coop<1>, grid, block, 0, 0, t4, gathers, (uint4 *)sink); });
   timed("k_gather8", 8.0 * gathers,
         [&] { hipLaunchKernelGGL(k_gather8, grid, block, 0, 0, (const uint2 *)tab, gathers, (uint4 *)sink); });
   const uint64_t runs = 4ull << 20;
