@@ -226,7 +226,8 @@ __global__ __launch_bounds__(kFT) void k_fast(DeviceSnapshot s, const uint8_t *_
         if (c == kNone) continue;
         const uint32_t fl = dc.sh_cnt_flags >> 24;
         const bool skip_dollar = dollar && (fl & kFlagDollarWild);      // topics.go:527
-        const uint32_t c_own = skip_dollar ? 0 : dc.sub_cnt;
+        // a '#' node after a literal parent: gathered by the parent probe (kFlagParentLit)
+        const uint32_t c_own = skip_dollar || (fl & kFlagParentLit) ? 0 : dc.sub_cnt;
         const uint32_t c_par = lit && !skip_dollar ? dc.hsub_cnt : 0;  // topics.go:507-509
         const uint32_t c_sh = dc.sh_cnt_flags & kShCntMask;
         if (((c_own | c_par) && (fl & kFlagMultiSat)) || c_own > kFRangeMax || c_par > kFRangeMax)

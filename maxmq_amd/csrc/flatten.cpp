@@ -72,6 +72,7 @@ static void mark_multi(const Store &st, const std::vector<uint32_t> &order, Host
   for (uint32_t c = 0; c < nc; c++) cstart[c + 2] += cstart[c + 1];
   for (uint64_t s = 0; s < nsub; s++) by_client[cstart[hs.subs[s].client + 1]++] = (uint32_t)s;
   auto wild = [&](uint32_t tok) { return tok == plus_tok || tok == hash_tok; };
+  static const bool hash_multi = getenv("MQM_HASH_MULTI") && atoi(getenv("MQM_HASH_MULTI")) != 0;
   auto compatible = [&](uint32_t a, uint32_t b) {
     while (nodes[a].depth > nodes[b].depth) a = nodes[a].parent;
     while (nodes[b].depth > nodes[a].depth) b = nodes[b].parent;
@@ -90,9 +91,11 @@ static void mark_multi(const Store &st, const std::vector<uint32_t> &order, Host
       const uint32_t lo = cstart[c], hi = cstart[c + 1];
       for (uint32_t x = lo; x < hi; x++) {
         const uint32_t sx = by_client[x], nx = sub_node[sx], px = nodes[nx].parent;
-        // the parent probe emits a '#' node's subscriptions after a literal hit on its parent
+        // the parent probe emits a '#' node's subscriptions after a literal hit on its
+        // parent; the walks skip the own visit of such a node (kFlagParentLit), so
+        // it is emitted once per topic.  MQM_HASH_MULTI=1 (A/B): treat them as multi.
         bool multi = hi - lo > kMaxPairwise ||
-                     (nodes[nx].key == hash_tok && px != st.root() && !wild(nodes[px].key));
+                     (hash_multi && nodes[nx].key == hash_tok && px != st.root() && !wild(nodes[px].key));
         for (uint32_t y = lo; !multi && y < hi; y++) multi = y != x && compatible(nx, sub_node[by_client[y]]);
         if (multi) hs.subs[sx].word |= kMetaMulti;
         else solo[ch]++;
@@ -373,6 +376,9 @@ int flatten(const Store &st, HostSnapshot *out) {
       if (nlit[i]) f |= kFlagHasLiteral;
       if (i > 0) {
         par_new[i] = new_id[h.parent];
+        if (h.key == hash_tok && par_new[i] != 0 && nodes[h.parent].key != hash_tok &&
+            nodes[h.parent].key != plus_tok)
+          f |= kFlagParentLit;
         if (par_new[i] == 0) {  // root child: Filter[0] of every sub stored below it
           const std::string_view k = st.tokens().name(h.key);
           if (!k.empty() && (k[0] == '+' || k[0] == '#')) f |= kFlagDollarWild;

@@ -553,13 +553,15 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
 #endif
         const uint32_t fl = found ? dc.sh_cnt_flags >> 24 : 0;
         const bool skip_dollar = dollar && (fl & kFlagDollarWild);  // topics.go:527
-        const uint32_t c_own = found && !skip_dollar ? dc.sub_cnt : 0;
+        // (a '#' node after a literal parent: its parent probe gathered it, kFlagParentLit)
+        const uint32_t c_own = found && !skip_dollar && !(fl & kFlagParentLit) ? dc.sub_cnt : 0;
         const uint32_t c_par = found && lit && !skip_dollar ? dc.hsub_cnt : 0;  // topics.go:507-509
         const uint32_t c_sh = found ? dc.sh_cnt_flags & kShCntMask : 0;
         const bool push = found && has_next && (fl & kFlagHasChildren);
         const bool leaf = push && (fl & kFlagHashLeaf);
-        // the '#' child's gather at the next level ('$' flag = this node's)
-        const uint32_t c_hl = leaf && !skip_dollar ? dc.hsub_cnt : 0;
+        // the '#' child's gather at the next level ('$' flag = this node's); after
+        // a literal hit c_par gathered the same range (kFlagParentLit)
+        const uint32_t c_hl = leaf && !skip_dollar && !lit ? dc.hsub_cnt : 0;
 #if MQM_WALK_PRECHECK
         // the pushed literal probe's filter word, loaded now: its round trip
         // overlaps this level's record writes, and a negative (or a '+' / '#'

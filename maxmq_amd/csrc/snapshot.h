@@ -24,6 +24,12 @@ enum : uint32_t {
                           //   everything its gather needs is in this descriptor (its range
                           //   follows this node's, its multi count is multi >> 16, its `$`
                           //   flag equals this node's), so the walk records it without a load
+  kFlagParentLit = 32u,   // a '#' node whose parent is a non-root node with a literal key: the
+                          //   parent is only ever reached by a literal probe, whose parent-'#'
+                          //   probe (topics.go:507-509) gathers this node's subscriptions, and
+                          //   this node's own visit (the next level's '#' probe, :503) happens
+                          //   only when that probe did, so the walks skip the own visit's
+                          //   (non-shared) gather: a set gathered twice is the same set once
 };
 
 struct NodeDesc {         // 32 B
