@@ -72,7 +72,8 @@ static void mark_multi(const Store &st, const std::vector<uint32_t> &order, Host
   for (uint32_t c = 0; c < nc; c++) cstart[c + 2] += cstart[c + 1];
   for (uint64_t s = 0; s < nsub; s++) by_client[cstart[hs.subs[s].client + 1]++] = (uint32_t)s;
   auto wild = [&](uint32_t tok) { return tok == plus_tok || tok == hash_tok; };
-  static const bool hash_multi = getenv("MQM_HASH_MULTI") && atoi(getenv("MQM_HASH_MULTI")) != 0;
+  // (read at every flatten: a test compares both markings in one process)
+  const bool hash_multi = getenv("MQM_HASH_MULTI") && atoi(getenv("MQM_HASH_MULTI")) != 0;
   auto compatible = [&](uint32_t a, uint32_t b) {
     while (nodes[a].depth > nodes[b].depth) a = nodes[a].parent;
     while (nodes[b].depth > nodes[a].depth) b = nodes[b].parent;

@@ -281,3 +281,18 @@ def test_replay_fault_while_logs_queue():
     except maxmq_amd.MqmError:
         asy.commit()
     assert asy.snapshot_digest() == sync.snapshot_digest()
+
+
+def test_solo_marking_of_hash_nodes():
+    """kFlagParentLit (snapshot.h): a '#' node whose parent has a literal key is
+    gathered once per topic by the walks (the parent-'#' probe, topics.go:507-509;
+    its own visit is skipped), so its subscription is solo unless the client has
+    a level-compatible partner.  "a/#" alone: solo; "+/#" alone: solo (no parent
+    probe after '+'); "x/y" with "x/#" (one client, compatible): both multi."""
+    idx = maxmq_amd.TopicsIndex(device=None)
+    idx.subscribe("c1", maxmq_amd.Subscription("a/#"))
+    idx.subscribe("c2", maxmq_amd.Subscription("+/#"))
+    idx.subscribe("c3", maxmq_amd.Subscription("x/y"))
+    idx.subscribe("c3", maxmq_amd.Subscription("x/#"))
+    idx.commit()
+    assert idx.snapshot_stats()["solo_subs"] == 2

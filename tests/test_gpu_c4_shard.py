@@ -4,10 +4,14 @@ per-GPU unit of a node step: shard 0 of the 8-way client-range split
 10M-topic batch, through the same mqm_match_device call `bench.py --shard 0/8
 --config 4` and the sharded node step time.
 
-C4 is the config that drives the widest merges (tens of thousands of multi
-entries per hub topic: the k_multi<4096> tier and the client-partitioned
-merge) and the unbounded DFS path under load (topics with more than 64 hits),
-so the test asserts those ran, then checks:
+C4 is the config that drove the widest merges before '#' subscriptions after a
+literal parent became solo (kFlagParentLit, snapshot.h): with the old marking
+(MQM_HASH_MULTI=1, a second index of the same shard) hub topics carry
+thousands of multi entries (the k_multi<4096> tier and the client-partitioned
+merge) and the unbounded DFS path runs under load (topics with more than 64
+hits); the test asserts those ran there and that both markings give the same
+result for every topic (per-topic counts and checksums).  On the default index
+it checks:
   * over all 10M topics (~6G deliveries, walked in chunks of whole topics):
     dense CSR monotone and summing to n_deliveries, client ids below the
     shard's client count, QoS <= 2, no client twice in a topic, run-to-run
@@ -60,9 +64,8 @@ def test_config4_shard0of8_full_batch():
     r1, d1, offs = run()
     nd = int(r1.n_deliveries)
     assert nd > 300 * n, nd  # ~620 deliveries per topic on this shard
-    assert r1.n_tier3 > 0, "the k_multi<4096> / partitioned tier never ran"
-    assert r1.n_part > 0, "the client-partitioned merge never ran"
-    assert r1.n_fallback > 0, "no topic took the unbounded DFS path"
+    print(f"C4 shard 0/8 default marking: tiers t2={r1.n_tier2} t3={r1.n_tier3} part={r1.n_part} "
+          f"dfs={r1.n_fallback}")
     assert int(offs[0]) == 0 and int(offs[-1]) == nd
     assert bool((offs[1:] >= offs[:-1]).all())
     # every entry of every topic, in chunks of whole topics: client in range,
@@ -95,8 +98,9 @@ def test_config4_shard0of8_full_batch():
         inside = torch.nonzero((pos >= a) & (pos < a + e.numel())).flatten()
         full_rows[inside] = e[pos[inside] - a]
     assert torch.equal(sums2, sums1), "run-to-run per-topic checksums differ"
+
     full_rows = full_rows.cpu().numpy().view(np.uint64)
-    del offs2, sums1, sums2, pos
+    del offs2, sums2, pos, d1, d2
     sub = Strings.from_list([w.topics[int(i)] for i in small])
     res = idx.match_batch(sub.data, sub.offs)
     assert np.array_equal(cnt, np.diff(res.offsets).astype(np.int64)), "per-topic counts differ from the host path"
@@ -114,3 +118,30 @@ def test_config4_shard0of8_full_batch():
     assert len(g) > 1_000_000
     assert_same(g, ref, "C4 shard 0/8 deliveries (sample)")
     assert_same(gs, rs, "C4 shard 0/8 shared (sample)")
+    idx.close()
+    del idx
+    # the old marking ('#' subscriptions after a literal parent multi): the wide
+    # merge tiers and the DFS path under load, and the same result per topic
+    import os
+
+    os.environ["MQM_HASH_MULTI"] = "1"
+    try:
+        idx_h = maxmq_amd.TopicsIndex(0, autocommit=False)
+        idx_h.subscribe_workload(w)
+        idx_h.commit()
+    finally:
+        del os.environ["MQM_HASH_MULTI"]
+    rh = idx_h.match_device(tb.data_ptr(), to.data_ptr(), n)
+    dh = idx_h.dense_device()
+    offs_h = dev_view_copy(dh.offsets, n + 1, torch.int64, dev)
+    torch.cuda.synchronize()
+    assert rh.n_tier3 > 0, "the k_multi<4096> / partitioned tier never ran"
+    assert rh.n_part > 0, "the client-partitioned merge never ran"
+    assert rh.n_fallback > 0, "no topic took the unbounded DFS path"
+    assert torch.equal(offs_h, offs), "per-topic counts differ between the two markings"
+    sums_h = torch.zeros(n, dtype=torch.int64, device=dev)
+    for lo, hi, a, e, sid in iter_csr_chunks(offs_h, dh.deliveries, torch.int64):
+        sums_h.index_add_(0, sid, mix64(e ^ mix64(sid)))
+    assert torch.equal(sums_h, sums1), "per-topic checksums differ between the two markings"
+    del dh, offs_h, sums_h
+    idx_h.close()
