@@ -146,30 +146,40 @@ template <int kCtrl>
 __device__ __forceinline__ uint32_t quad_dpp(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kCtrl, 0xF, 0xF, true);
 }
+typedef unsigned int U32x4 __attribute__((ext_vector_type(4)));  // native vector: no struct copies
+typedef const U32x4 __attribute__((address_space(1))) *GPtr4;     // global_load, not flat_load
 template <int kCtrl>
-__device__ __forceinline__ uint4 quad_dpp4(uint4 v) {
-  return make_uint4(quad_dpp<kCtrl>(v.x), quad_dpp<kCtrl>(v.y), quad_dpp<kCtrl>(v.z), quad_dpp<kCtrl>(v.w));
+__device__ __forceinline__ U32x4 quad_dpp4(U32x4 v) {
+  U32x4 r;
+  r.x = quad_dpp<kCtrl>(v.x);
+  r.y = quad_dpp<kCtrl>(v.y);
+  r.z = quad_dpp<kCtrl>(v.z);
+  r.w = quad_dpp<kCtrl>(v.w);
+  return r;
 }
-// r[j] = chunk q of item j (q = this lane's index in its quad)  ->  r[j] = chunk j of item q
-__device__ __forceinline__ void quad_transpose(uint4 (&r)[4], int q) {
+// lane q of a quad holds r0..r3 = chunk q of items 0..3; afterwards r0..r3 =
+// chunks 0..3 of item q (two butterfly stages over the quad, no LDS)
+__device__ __forceinline__ void quad_transpose(U32x4 &r0, U32x4 &r1, U32x4 &r2, U32x4 &r3, int q) {
   const bool h2 = q & 2, h1 = q & 1;
-#pragma unroll
-  for (int j = 0; j < 2; j++) {  // 2x2 blocks: lanes q, q ^ 2 swap the off-diagonal pair
-    const uint4 snd = h2 ? r[j] : r[j + 2];
-    const uint4 rcv = quad_dpp4<0x4E>(snd);  // quad_perm [2, 3, 0, 1]
-    if (h2)
-      r[j] = rcv;
-    else
-      r[j + 2] = rcv;
+  {  // 2x2 blocks: lanes q, q ^ 2 swap the off-diagonal pair (quad_perm [2, 3, 0, 1])
+    const U32x4 v0 = quad_dpp4<0x4E>(h2 ? r0 : r2), v1 = quad_dpp4<0x4E>(h2 ? r1 : r3);
+    if (h2) {
+      r0 = v0;
+      r1 = v1;
+    } else {
+      r2 = v0;
+      r3 = v1;
+    }
   }
-#pragma unroll
-  for (int j = 0; j < 4; j += 2) {  // inside each block: lanes q, q ^ 1
-    const uint4 snd = h1 ? r[j] : r[j + 1];
-    const uint4 rcv = quad_dpp4<0xB1>(snd);  // quad_perm [1, 0, 3, 2]
-    if (h1)
-      r[j] = rcv;
-    else
-      r[j + 1] = rcv;
+  {  // inside each block: lanes q, q ^ 1 (quad_perm [1, 0, 3, 2])
+    const U32x4 v0 = quad_dpp4<0xB1>(h1 ? r0 : r1), v1 = quad_dpp4<0xB1>(h1 ? r2 : r3);
+    if (h1) {
+      r0 = v0;
+      r2 = v1;
+    } else {
+      r1 = v0;
+      r3 = v1;
+    }
   }
 }
 
@@ -192,22 +202,23 @@ __device__ __forceinline__ uint32_t walk_step_quad(const DeviceSnapshot &s, bool
   const uint64_t a = do_probe ? (reinterpret_cast<uint64_t>(s.edges + slot) | 1u)
                               : do_desc ? (reinterpret_cast<uint64_t>(s.nodes + wc) | 2u) : 0;
   const uint32_t alo = (uint32_t)a, ahi = (uint32_t)(a >> 32);
-  uint4 r[4];
-#define MQM_QUAD_LOAD(j)                                                                          \
-  {                                                                                               \
+  // every lane loads unconditionally (one basic block: the four loads are in
+  // flight together): a descriptor's lanes 2, 3 re-read its 32 B (same line),
+  // an empty item's lanes the root descriptor (a line every CU holds)
+  const uint64_t dummy = reinterpret_cast<uint64_t>(s.nodes);
+#define MQM_QUAD_ADDR(j)                                                                          \
+  [&] {                                                                                           \
     const uint32_t lo = quad_dpp<(j) * 0x55>(alo), hi = quad_dpp<(j) * 0x55>(ahi);                \
     const uint32_t kd = lo & 3u;                                                                  \
-    const uint4 *p = reinterpret_cast<const uint4 *>((((uint64_t)hi << 32) | lo) & ~3ull) + q;    \
-    r[j] = make_uint4(0, 0, 0, 0);                                                                \
-    if (kd == 1u || (kd == 2u && q < 2)) r[j] = *p;                                               \
-  }
-  MQM_QUAD_LOAD(0)
-  MQM_QUAD_LOAD(1)
-  MQM_QUAD_LOAD(2)
-  MQM_QUAD_LOAD(3)
-#undef MQM_QUAD_LOAD
-  quad_transpose(r, q);
-  uint4 x0 = r[0], x1 = r[1], x2 = r[2], x3 = r[3];
+    const uint64_t base = kd ? ((((uint64_t)hi << 32) | lo) & ~3ull) : dummy;                     \
+    return (GPtr4)(base + 16u * (uint32_t)(kd == 1u ? q : (q & 1)));                              \
+  }()
+  const GPtr4 p0 = MQM_QUAD_ADDR(0), p1 = MQM_QUAD_ADDR(1), p2 = MQM_QUAD_ADDR(2), p3 = MQM_QUAD_ADDR(3);
+#undef MQM_QUAD_ADDR
+  U32x4 r0 = *p0, r1 = *p1, r2 = *p2, r3 = *p3;
+  quad_transpose(r0, r1, r2, r3, q);
+  uint4 x0 = make_uint4(r0.x, r0.y, r0.z, r0.w), x1 = make_uint4(r1.x, r1.y, r1.z, r1.w);
+  uint4 x2 = make_uint4(r2.x, r2.y, r2.z, r2.w), x3 = make_uint4(r3.x, r3.y, r3.z, r3.w);
   uint32_t c = kNone;
   bool more = false;
   if (do_desc) {
