@@ -81,6 +81,11 @@ struct Workspace {
   // to be run again exact
   bool caps_known = false, pending = false, pend_exact = false;
   uint32_t dfs_cap = 0;
+  // merge / shared lists (bit per list, match.hip kList*) that had topics in the
+  // last collected call: a queued call launches only their kernels (an empty
+  // list's persistent grid still queues behind the solo copy), and a call
+  // whose topics land in a list it did not launch is run again, exact
+  uint32_t lists_seen = ~0u, pend_launched = ~0u;
   uint64_t requeued = 0;
   // the last match_device call (identifiers_device works on its records)
   bool last_valid = false;

@@ -2201,9 +2201,19 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
     // merges on the side stream, concurrently with the solo copy (they write
     // disjoint parts of dout and dcount: winners after Ss / topics with Ms > 0);
     // a queued call launches every list's kernel (each reads its count)
+    // (a queued call: the lists the last collected call had topics in)
+    uint32_t launched = 0;
+    auto has_list = [&](uint32_t c, int list) {
+      const bool l = exact ? c > 0 : ((ws.lists_seen >> list) & 1u) != 0;
+      if (l) launched |= 1u << list;
+      return l;
+    };
+    const bool l_small = has_list(hc->n_small, kLSmall), l_wave = has_list(hc->n_wmerge, kLWave),
+               l_t1 = has_list(hc->n_t1, kLT1), l_t2 = has_list(hc->n_t2, kLT2), l_t3 = has_list(hc->n_t3, kLT3),
+               l_part = has_list(hc->n_part, kLPart), l_sh = has_list(hc->n_shlist, kLShared);
+    ws.pend_launched = launched;
     auto has = [&](uint32_t c) { return !exact || c > 0; };
-    const bool merges = has(hc->n_small) || has(hc->n_wmerge) || has(hc->n_t1) || has(hc->n_t2) || has(hc->n_t3) ||
-                        has(hc->n_part);
+    const bool merges = l_small || l_wave || l_t1 || l_t2 || l_t3 || l_part;
     const bool side = merges && ws.overlap;
     // persistent grids: with both streams busy, each takes its share of the device
     const uint32_t side_pct = side ? MQM_SIDE_PCT : 100, main_pct = side && MQM_SIDE_PCT < 100 ? 100 - MQM_SIDE_PCT : 100;
@@ -2219,22 +2229,22 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
       // MQM_MERGE_BIG_FIRST=1: the workgroup merges first, the small-topic
       // merges last (they fill the device better at the end of the stream)
       auto big = [&]() -> int {
-        if (has(hc->n_t1)) {
+        if (l_t1) {
           hipLaunchKernelGGL(k_multi<1024>, grid(k_multi<1024>), dim3(kBigThreads), 0, ms, s, o, lists.l[kLT1],
                              lcount + kLT1);
           HIP_TRY(hipGetLastError());
         }
-        if (has(hc->n_t2)) {
+        if (l_t2) {
           hipLaunchKernelGGL(k_multi<2048>, grid(k_multi<2048>), dim3(kBigThreads), 0, ms, s, o, lists.l[kLT2],
                              lcount + kLT2);
           HIP_TRY(hipGetLastError());
         }
-        if (has(hc->n_t3)) {
+        if (l_t3) {
           hipLaunchKernelGGL(k_multi<4096>, grid(k_multi<4096>), dim3(kBigThreads), 0, ms, s, o, lists.l[kLT3],
                              lcount + kLT3);
           HIP_TRY(hipGetLastError());
         }
-        if (has(hc->n_part)) {
+        if (l_part) {
           hipLaunchKernelGGL(k_multi_part, grid(k_multi_part), dim3(kBigThreads), 0, ms, s, o, lists.l[kLPart],
                              lcount + kLPart);
           HIP_TRY(hipGetLastError());
@@ -2242,12 +2252,12 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
         return 0;
       };
       auto small = [&]() -> int {
-        if (has(hc->n_small)) {
+        if (l_small) {
           hipLaunchKernelGGL((k_merge_small<6>), grid(k_merge_small<6>), dim3(kWave * kEmitWaves), 0, ms, s, o,
                              lists.l[kLSmall], lcount + kLSmall);
           HIP_TRY(hipGetLastError());
         }
-        if (has(hc->n_wmerge)) {
+        if (l_wave) {
           hipLaunchKernelGGL(k_merge, grid(k_merge), dim3(kWave * kEmitWaves), 0, ms, s, o, lists.l[kLWave],
                              lcount + kLWave);
           HIP_TRY(hipGetLastError());
@@ -2259,7 +2269,7 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
     hipLaunchKernelGGL(k_desc, dim3(std::min<uint32_t>((n + 255) / 256, 8192)), dim3(256), 0, st, o, n, desc_start,
                        desc, desc_cap);  // a wavefront per 64 topics
     HIP_TRY(hipGetLastError());
-    if (has(hc->n_shlist)) {
+    if (l_sh) {
       const uint32_t nsh = exact ? hc->n_shlist : n;
       hipLaunchKernelGGL(k_shared, dim3(std::min<uint32_t>((nsh + 15) / 16, 8192)), dim3(256), 0, st, o,
                          lists.l[kLShared], lcount + kLShared);
@@ -2320,6 +2330,19 @@ int match_collect(Workspace &ws, hipStream_t st, MatchOutput *out) {
       return -3;
     }
     return 1;  // outgrew buffers sized by an earlier call: match_device re-runs it, exact
+  }
+  {
+    uint32_t seen = 0;
+    const unsigned int c[][2] = {{hc->n_small, kLSmall}, {hc->n_wmerge, kLWave}, {hc->n_t1, kLT1}, {hc->n_t2, kLT2},
+                                 {hc->n_t3, kLT3},       {hc->n_part, kLPart},   {hc->n_shlist, kLShared}};
+    for (const auto &x : c)
+      if (x[0]) seen |= 1u << x[1];
+    const bool missed = (seen & ~ws.pend_launched) != 0;
+    ws.lists_seen = seen;
+    if (missed) {  // a queued call had topics in a list whose kernel it did not launch
+      if (ws.pend_exact) return -3;
+      return 1;
+    }
   }
   ws.caps_known = true;
   ws.last_valid = true;

@@ -121,3 +121,37 @@ def test_queued_outgrown_buffers_and_dfs_topics():
             assert r.n_fallback >= 3
     assert ctx.requeued() >= 1, "the 50x larger batch should have outgrown the context's buffers"
     ctx.close()
+
+
+def test_queued_merge_lists_that_were_empty():
+    """a queued call launches only the merge / shared lists the previous call
+    had topics in (match.hip lists_seen); batches whose topics need a merge
+    tier (or shared candidates) after batches that needed none are re-run
+    exact and equal the synchronous result"""
+    import torch
+
+    w = mqgen.generate(1, n_filters=20000, n_topics=60000)
+    idx = maxmq_amd.TopicsIndex(0, autocommit=False)
+    idx.subscribe_workload(w)
+    # clients whose filters co-match "zz/q/r": multi entries -> a merge list;
+    # 900 clients with 3 co-matching filters each: a workgroup-merge tier
+    for c in range(900):
+        for f in ("zz/q/r", "zz/+/r", "zz/#"):
+            idx.subscribe(f"m{c}", maxmq_amd.Subscription(f, c % 3))
+    idx.subscribe("s0", maxmq_amd.Subscription("$SHARE/g/zz/q/r", 1))
+    idx.commit()
+    solo = Strings.from_list(["nomatch/" + str(i) for i in range(2000)])
+    solo_b = (torch.from_numpy(solo.data).cuda(), torch.from_numpy(solo.offs.view(np.int64)).cuda(), len(solo))
+    hot = Strings.from_list(["zz/q/r"] * 5 + [w.topics[i] for i in range(2000)])
+    hot_b = (torch.from_numpy(hot.data).cuda(), torch.from_numpy(hot.offs.view(np.int64)).cuda(), len(hot))
+    order = [solo_b, solo_b, hot_b, solo_b, hot_b, hot_b]
+    want = _want(idx, order)
+    ctx = idx.match_context()
+    for j, (tb, to, n) in enumerate(order):
+        ctx.submit(tb.data_ptr(), to.data_ptr(), n)
+        r = ctx.wait()
+        assert _dense_rows(idx, r, n) == want[j], f"batch {j}"
+        if j == 2:
+            assert r.n_big >= 5 and r.n_shared > 0
+    assert ctx.requeued() >= 2, "merge / shared lists unseen by the previous call must re-run the batch"
+    ctx.close()
