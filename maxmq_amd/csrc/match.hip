@@ -91,7 +91,11 @@
 #define MQM_COPY16 0
 #endif
 // MQM_WALK_COOP=1: k_walk<4> loads each group's edge entries / descriptors
-// cooperatively, 16 B per lane (device.h walk_step_quad)
+// cooperatively, 16 B per lane (device.h walk_step_quad).  Measured slower on
+// C3 (walk 6.65 vs 6.11 ms, profiles/r03/r03c): the walk is not bound by the
+// per-line address work that bounds a pure random gather (where the
+// cooperative form is 2.2x faster, tools/calib_fetch), so the transpose's
+// instructions cost more than the loads save.  Off.
 #ifndef MQM_WALK_COOP
 #define MQM_WALK_COOP 0
 #endif

@@ -34,3 +34,46 @@ def kat():
 
     with open(os.path.join(ROOT, "tests", "golden", "kat.json")) as fh:
         return json.load(fh)
+
+
+# A heartbeat for long GPU tests (the C4 shard test runs for minutes): every
+# 30 s one line on the terminal (through pytest's terminal reporter, which
+# writes past output capture) and into gpurun_out/pytest_heartbeat.log, so a
+# runner that takes minutes of silence for a hang sees progress.
+_current = {"test": None, "t0": 0.0}
+
+
+def pytest_runtest_logstart(nodeid, location):
+    import time
+
+    _current["test"], _current["t0"] = nodeid, time.time()
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _heartbeat(request):
+    import threading
+    import time
+
+    tr = request.config.pluginmanager.get_plugin("terminalreporter")
+    stop = threading.Event()
+    path = os.path.join(ROOT, "gpurun_out", "pytest_heartbeat.log")
+
+    def beat():
+        while not stop.wait(30.0):
+            t = _current["test"]
+            if t is None:
+                continue
+            line = f"[heartbeat {time.strftime('%H:%M:%S')}] {t} running {time.time() - _current['t0']:.0f} s"
+            try:
+                if tr is not None:
+                    tr.write_line(line)
+                os.makedirs(os.path.dirname(path), exist_ok=True)
+                with open(path, "a") as fh:
+                    fh.write(line + "\n")
+            except Exception:
+                pass
+
+    th = threading.Thread(target=beat, daemon=True)
+    th.start()
+    yield
+    stop.set()
