@@ -9,7 +9,8 @@ literal parent became solo (kFlagParentLit, snapshot.h): with the old marking
 (MQM_HASH_MULTI=1, a second index of the same shard) hub topics carry
 thousands of multi entries (the k_multi<4096> tier) and the unbounded DFS path
 runs under load (topics with more than 64
-hits); the test asserts those ran there and that both markings give the same
+hits; none since the walk records a '#' child after a literal once); the test
+asserts the k_multi<4096> tier ran there and that both markings give the same
 result for every topic (per-topic counts and checksums).  On the default index
 it checks:
   * over all 10M topics (~6G deliveries, walked in chunks of whole topics):
@@ -138,7 +139,10 @@ def test_config4_shard0of8_full_batch():
     # (no C4 topic has more than 3072 multi entries, so the client-partitioned
     # merge does not run here: tests/test_gpu_parity.py's 4000-entry topic covers it)
     assert rh.n_tier3 > 0, "the k_multi<4096> tier never ran"
-    assert rh.n_fallback > 0, "no topic took the unbounded DFS path"
+    # (no C4 topic has more than 64 hits since the walk records a '#' child
+    # after a literal once; the DFS path is covered by test_gpu_queued.py and
+    # test_gpu_parity.py's edge cases)
+    print(f"C4 shard 0/8 old marking: tiers t2={rh.n_tier2} t3={rh.n_tier3} part={rh.n_part} dfs={rh.n_fallback}")
     assert torch.equal(offs_h, offs), "per-topic counts differ between the two markings"
     sums_h = torch.zeros(n, dtype=torch.int64, device=dev)
     for lo, hi, a, e, sid in iter_csr_chunks(offs_h, dh.deliveries, torch.int64):
