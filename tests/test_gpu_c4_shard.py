@@ -7,11 +7,10 @@ per-GPU unit of a node step: shard 0 of the 8-way client-range split
 C4 is the config that drove the widest merges before '#' subscriptions after a
 literal parent became solo (kFlagParentLit, snapshot.h): with the old marking
 (MQM_HASH_MULTI=1, a second index of the same shard) hub topics carry
-thousands of multi entries (the k_multi<4096> tier) and the unbounded DFS path
-runs under load (topics with more than 64
-hits; none since the walk records a '#' child after a literal once); the test
+thousands of multi entries (the k_multi<4096> tier); the test
 asserts the k_multi<4096> tier ran there and that both markings give the same
-result for every topic (per-topic counts and checksums).  On the default index
+result for every topic (per-topic counts, and checksums over (client, first
+filter, QoS, NoLocal): sids are snapshot positions, which the marking moves).  On the default index
 it checks:
   * over all 10M topics (~6G deliveries, walked in chunks of whole topics):
     dense CSR monotone and summing to n_deliveries, client ids below the
@@ -37,6 +36,30 @@ from tests.gpu_util import assert_same, canon_gpu, canon_oracle
 from tools.mqgen import Strings
 
 pytestmark = pytest.mark.gpu
+
+
+def _filter_map(idx, w, dev):
+    """sid -> interned filter id of the index's current snapshot (device int64)"""
+    import torch
+
+    nsub = int(idx.snapshot_stats()["subs"])
+    res = idx.match_batch(*_one_topic(w))
+    f = res.sub_infos(np.arange(nsub, dtype=np.uint32))["filter"].astype(np.int64)
+    return torch.from_numpy(f).to(dev)
+
+
+def _one_topic(w):
+    s = Strings.from_list([w.topics[0]])
+    return s.data, s.offs
+
+
+def _stable_mix(e, fmap, tid):
+    """a delivery (client | packed << 32) as (client, first filter, QoS | NoLocal), mixed with its topic"""
+    from maxmq_amd.devbuf import mix64
+
+    packed = e >> 32
+    key = (e & 0xFFFFFFFF) | (fmap[packed & 0x0FFFFFFF] << 32)
+    return mix64(key ^ mix64(((packed >> 28) & 7) ^ mix64(tid)))
 
 
 def test_config4_shard0of8_full_batch():
@@ -72,7 +95,13 @@ def test_config4_shard0of8_full_batch():
     # every entry of every topic, in chunks of whole topics: client in range,
     # QoS <= 2, no client twice in a topic, per-topic checksum
     sums1 = torch.zeros(n, dtype=torch.int64, device=dev)
+    # per-topic checksums over (client, first filter, QoS, NoLocal): sids are
+    # snapshot positions and differ between snapshots built with different
+    # markings (a range lists its solo entries first), filter ids do not
+    fmap = _filter_map(idx, w, dev)
+    stable1 = torch.zeros(n, dtype=torch.int64, device=dev)
     for lo, hi, a, e, sid in iter_csr_chunks(offs, d1.deliveries, torch.int64):
+        stable1.index_add_(0, sid, _stable_mix(e, fmap, sid))
         client = e & 0xFFFFFFFF
         assert int(client.max()) < ncl
         assert int(((e >> 60) & 3).max()) <= 2  # packed word (high half): qos at its bits 28..29
@@ -144,9 +173,10 @@ def test_config4_shard0of8_full_batch():
     # test_gpu_parity.py's edge cases)
     print(f"C4 shard 0/8 old marking: tiers t2={rh.n_tier2} t3={rh.n_tier3} part={rh.n_part} dfs={rh.n_fallback}")
     assert torch.equal(offs_h, offs), "per-topic counts differ between the two markings"
-    sums_h = torch.zeros(n, dtype=torch.int64, device=dev)
+    fmap_h = _filter_map(idx_h, w, dev)
+    stable_h = torch.zeros(n, dtype=torch.int64, device=dev)
     for lo, hi, a, e, sid in iter_csr_chunks(offs_h, dh.deliveries, torch.int64):
-        sums_h.index_add_(0, sid, mix64(e ^ mix64(sid)))
-    assert torch.equal(sums_h, sums1), "per-topic checksums differ between the two markings"
-    del dh, offs_h, sums_h
+        stable_h.index_add_(0, sid, _stable_mix(e, fmap_h, sid))
+    assert torch.equal(stable_h, stable1), "per-topic (client, first filter, QoS, NoLocal) differ between the markings"
+    del dh, offs_h, stable_h
     idx_h.close()
