@@ -68,6 +68,11 @@ def parse():
                     help="PCIe-inclusive host path (mqm_match_batch): topics per call, outside the timed region; 0 = skip")
     ap.add_argument("--host-threads", type=int, default=4,
                     help="host path: concurrent callers (each its own stream), batches overlapped across them")
+    ap.add_argument("--pipeline", type=int, default=0,
+                    help="timed steps through the queued device API on this many contexts / streams (a step "
+                         "submits its batch and waits for the one submitted that many steps earlier; every "
+                         "batch's result is complete before the timed region ends); 0 = one blocking "
+                         "mqm_match_device call per step")
     ap.add_argument("--steady-steps", type=int, default=20,
                     help="steady-state leg: batches queued back to back on two contexts (0 = skip)")
     ap.add_argument("--latency-topics", type=int, default=2000,
@@ -289,7 +294,34 @@ def main():
         log(f"[rank {rank}] group {grp} shard {my_shard}/{k}: {dpt:.0f} node deliveries per topic -> "
             f"{chunk} topics per gather ({(n + chunk - 1) // chunk} gathers per step)")
 
+    pipe = {}
+    if args.pipeline > 0 and not sharded:
+        pipe["streams"] = [torch.cuda.Stream(dev) for _ in range(args.pipeline)]
+        pipe["ctxs"] = [idx.match_context() for _ in range(args.pipeline)]
+        pipe["pend"] = [False] * args.pipeline
+        pipe["k"] = 0
+
+    def drain():
+        """pipelined steps: wait for every batch still in flight (their results)"""
+        out = []
+        for c in range(args.pipeline):
+            if pipe["pend"][c]:
+                out.append(pipe["ctxs"][c].wait())
+                pipe["pend"][c] = False
+        return out
+
     def step():
+        if pipe:
+            # the queued device API: submit this step's batch on the next
+            # context, collect the batch that context held (submitted
+            # `--pipeline` steps ago); the device always has the next batches
+            # queued, so one batch's walk overlaps another's emission
+            c = pipe["k"] % args.pipeline
+            pipe["k"] += 1
+            r_ = pipe["ctxs"][c].wait() if pipe["pend"][c] else None
+            pipe["ctxs"][c].submit(tb.data_ptr(), to.data_ptr(), n, pipe["streams"][c].cuda_stream)
+            pipe["pend"][c] = True
+            return r_, (int(r_.n_deliveries) if r_ else 0), (int(r_.n_shared) if r_ else 0)
         if sharded:
             # the publish batch enters at the group leader and is broadcast over
             # xGMI (RCCL); every shard matches it chunk by chunk and its dense
@@ -301,6 +333,8 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    if pipe:
+        drain()
     torch.cuda.synchronize(dev)
     if args.sweep:
         run_sweep(args, idx, step, dev, rank)
@@ -315,8 +349,12 @@ def main():
     big = 0
     why = {}
     lists = {}
+    results = []
     for _ in range(args.steps):
-        r, nd_, ns_ = step()
+        results.append(step())
+    if pipe:  # the batches still in flight belong to the timed steps
+        results += [(r_, int(r_.n_deliveries), int(r_.n_shared)) for r_ in drain()]
+    for r, nd_, ns_ in results:
         deliveries += nd_
         shared += ns_
         if r is None:  # sharded node step: per-shard kernel statistics are not summed over chunks
@@ -331,6 +369,17 @@ def main():
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
+    if pipe:
+        # kernel times of the stages: isolated (blocking) batches on the index's
+        # own workspace after the timed region (the pipelined contexts overlap
+        # batches, so a batch has no device time of its own there)
+        for c in pipe["ctxs"]:
+            c.close()
+        idx.profile(False)
+        idx.profile(True)
+        for _ in range(3):
+            idx.match_device(tb.data_ptr(), to.data_ptr(), n, stream.cuda_stream)
+        torch.cuda.synchronize(dev)
     prof = idx.profile_read()
     idx.profile(False)
     if dist:
@@ -368,7 +417,7 @@ def main():
             else:
                 short = argparse.Namespace(**dict(vars(args), cpu_seconds=min(args.cpu_seconds, 2.0)))
                 _, stats = cpu_baseline(w, short)
-        roof = roofline(stats, n, kms, args.traffic_json)
+        roof = roofline(stats, n, kms, args.traffic_json, dt * 1e3 / args.steps if pipe else None)
         out = {
             "metric": "publish topics matched/sec (node) + matched deliveries/sec at 10M filters",
             "value": value,
@@ -391,6 +440,8 @@ def main():
                             f"topic Zipf s={w.params['topic_zipf_s']}), {n}-topic batch, depth<={w.params['max_depth']}",
                 "filters": len(w.filters),
                 "topics_per_batch": n,
+                "pipeline": (f"{args.pipeline} contexts / streams (queued device API)" if pipe else
+                             "one blocking mqm_match_device per step"),
                 "parallelism": (f"shard{shard_of[0]}of{shard_of[1]}" if shard_of else
                                 f"hybrid{k}x{len(groups)}" if sharded and args.mode == "hybrid" else f"{args.mode}{world}"),
             },
@@ -768,6 +819,8 @@ def run_reverse(args, dist, rank, world, local, dev):
 
     for _ in range(args.warmup):
         step()
+    if pipe:
+        drain()
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
@@ -975,7 +1028,7 @@ def cores_note(single, threads, host):
     return out
 
 
-def roofline(stats, n, kms, traffic_json):
+def roofline(stats, n, kms, traffic_json, step_ms=None):
     """B = T + 8N + 8P + 8V + 8S + 8D algorithmic bytes per
     batch (per-topic counters of the oracle's walk over the CPU sample, scaled
     to the batch) over the device time of the whole match pipeline (k_walk,
@@ -984,8 +1037,11 @@ def roofline(stats, n, kms, traffic_json):
     the emit stage 8S + 8D.  `traffic` = HBM bytes per batch of the same
     kernels from rocprofv3 FETCH_SIZE / WRITE_SIZE (profiles/traffic.json from
     profiles/pmc_to_traffic.py over a profiles/run_pmc_r02.sh run, reads
-    converted per access shape as tools/calib_fetch calibrated them)."""
-    total_ms = kms["total"]
+    converted per access shape as tools/calib_fetch calibrated them).
+    With pipelined steps (--pipeline) batches overlap, so `achieved` divides by
+    the time per step (throughput); the stages keep the isolated batch's kernel
+    times."""
+    total_ms = step_ms if step_ms else kms["total"]
     if not stats or not stats["topics"] or total_ms <= 0:
         return {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                 "traffic": None}
@@ -1012,6 +1068,9 @@ def roofline(stats, n, kms, traffic_json):
             "algorithmic_bytes_per_topic": bytes_per_launch / n, "algorithmic_bytes_per_batch": bytes_per_launch,
             "kernel": "match pipeline per batch: k_walk + scans + solo copy (k_desc, k_winmap, k_wincopy) "
                       "+ merges (k_merge_small, k_merge, k_multi) (+ k_dfs)",
+            "time_basis": ("ms per pipelined step (batches overlap)" if step_ms else
+                           "device time of one batch (HIP events, first to last kernel)"),
+            "ms": total_ms, "isolated_batch_ms": kms["total"],
             "stages": {"walk": dict(stage(walk_b, kms["walk"]), traffic=walk_traffic),
                        "emit": stage(emit_b, kms["dedupe"])}}
 

@@ -12,6 +12,7 @@
 #   c4fast / c4var: the C4 shard bench without CPU baseline (default build / every variant)
 #   c4pmc / pmc: FETCH_SIZE / WRITE_SIZE passes (C4 shard / C3) -> traffic_c4.json / traffic.json
 #   calib   : tools/_build/calib_fetch (random-gather / cooperative-gather rates) -> calib_kernels.txt
+#   pipe    : `fast` with pipelined steps on 2 and 3 contexts -> bench_fast_pipe{2,3}.json
 #   smoke   : __graft_entry__.smoke()
 #   bench   : the default bench line (C3)                -> gpurun_out/TAG/bench.json
 #   fast    : bench without CPU baseline / host path      -> gpurun_out/TAG/bench_fast.json
@@ -58,6 +59,8 @@ for step in "$@"; do
              -- python3 $ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline --host-topics 0 \
              --latency-topics 0 --steady-steps 0 > $OUT/pmc_$C.json 2> $OUT/pmc_$C.log || exit 1; done) &&
              python3 profiles/pmc_to_traffic.py $OUT/pmc > $OUT/traffic.json ;;
+    pipe) for P in 2 3; do timeout -k 10 400 python3 -u bench.py $FAST --pipeline $P > $OUT/bench_fast_pipe$P.json \
+             2> $OUT/bench_fast_pipe$P.log || exit 1; done ;;
     abq) for V in 1 0; do MQM_QUEUED=$V timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_q$V.json \
              2> $OUT/bench_fast_q$V.log || exit 1; done ;;
     abf) for V in 0 1; do MQM_FLUSH=$V timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_flush$V.json \
