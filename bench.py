@@ -362,7 +362,7 @@ def main():
         fallback = int(r.n_fallback)
         big = int(r.n_big)
         why = dict(zip(["frontier", "hits", "levels", "shared_hits", "raw_entries"], list(r.fallback_why)))
-        lists = {"merge_small": int(r.n_merge_small), "merge_wave": int(r.n_merge_wave),
+        lists = {"resolve": int(r.n_resolve), "merge_small": int(r.n_merge_small), "merge_wave": int(r.n_merge_wave),
                  "solo_ranges": int(r.n_solo_ranges), "group_merge": int(r.n_big), "tier2": int(r.n_tier2), "tier3": int(r.n_tier3),
                  "multi_entries_by_tier": [int(x) for x in r.multi_entries]}
     torch.cuda.synchronize(dev)
@@ -1067,7 +1067,7 @@ def roofline(stats, n, kms, traffic_json, step_ms=None):
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
             "algorithmic_bytes_per_topic": bytes_per_launch / n, "algorithmic_bytes_per_batch": bytes_per_launch,
             "kernel": "match pipeline per batch: k_walk + scans + solo copy (k_desc, k_winmap, k_wincopy) "
-                      "+ merges (k_merge_small, k_merge, k_multi) (+ k_dfs)",
+                      "+ merges (k_resolve; heavy topics k_merge_small, k_merge, k_multi) (+ k_dfs)",
             "time_basis": ("ms per pipelined step (batches overlap)" if step_ms else
                            "device time of one batch (HIP events, first to last kernel)"),
             "ms": total_ms, "isolated_batch_ms": kms["total"],

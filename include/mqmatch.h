@@ -140,6 +140,7 @@ typedef struct {
   uint32_t n_tier2, n_tier3;      /* topics the workgroup merge passed to its 2nd / 3rd tier */
   uint64_t multi_entries[3];      /* multi entries merged by the workgroup tiers 1 / 2 / 3 */
   uint32_t n_part;                /* tier-3 topics merged in client-hash partitions (> 3072 multi entries) */
+  uint32_t n_resolve;             /* topics merged by resolution (partner lists, no table) */
 } mqm_device_result;
 
 /* ---- lifecycle: NewTopicsIndex (topics.go:291-299) ---------------------- */

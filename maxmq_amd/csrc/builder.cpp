@@ -283,6 +283,8 @@ uint64_t snapshot_digest(const HostSnapshot &hs) {
   d.vec(hs.shared_info);
   d.vec(hs.tok_pool);
   d.vec(hs.bloom);
+  d.vec(hs.pinfo);
+  d.vec(hs.partners);
   d.vec(hs.subtree);
   d.vec(hs.child_off);
   d.vec(hs.child_ids);

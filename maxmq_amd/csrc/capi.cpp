@@ -395,6 +395,7 @@ void fill_device_result(const MatchOutput &mo, const Workspace &ws, mqm_device_r
   out->n_tier3 = mo.n_tier3;
   for (int i = 0; i < 3; i++) out->multi_entries[i] = mo.multi_entries[i];
   out->n_part = mo.n_part;
+  out->n_resolve = mo.n_resolve;
 }
 
 // a result block laid out like mqm_match_batch's: offsets | shared_offsets |

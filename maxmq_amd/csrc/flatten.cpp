@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -57,9 +58,21 @@ struct PhaseTimer {
 // the levels both have are pairwise equal or wildcards (a topic level cannot
 // equal two different literals), so a subscription whose client has no such
 // partner — and which the parent-'#' probe cannot emit twice — is solo.
+// A multi subscription's partners (its client's level-compatible
+// subscriptions) go to `part` (old sids, by `poff`), for the merge by
+// resolution (snapshot.h: pinfo); a subscription whose merge needs the hash
+// table instead gets kPHeavy (client with more than kMaxPairwise
+// subscriptions, more than kMaxPartners partners, or the old '#' marking).
 static constexpr uint32_t kMaxPairwise = 64;  // clients with more subscriptions: all multi
+static constexpr uint32_t kPHeavy = 0xFFFFu;
 
-static void mark_multi(const Store &st, const std::vector<uint32_t> &order, HostSnapshot &hs) {
+struct Partners {
+  std::vector<uint16_t> cnt;   // by old sid: 0 solo, 1..kMaxPartners partners, kPHeavy
+  std::vector<uint64_t> off;   // by old sid: start in `part`
+  std::vector<uint32_t> part;  // partner old sids
+};
+
+static void mark_multi(const Store &st, const std::vector<uint32_t> &order, HostSnapshot &hs, Partners &pt) {
   const auto &nodes = st.nodes();
   const uint32_t plus_tok = st.plus_token(), hash_tok = st.hash_token();
   const uint64_t nsub = hs.sub_info.size();
@@ -83,11 +96,17 @@ static void mark_multi(const Store &st, const std::vector<uint32_t> &order, Host
     }
     return true;
   };
+  pt.cnt.assign(nsub, 0);
   // clients are independent: chunks of them in parallel (each sub belongs to one client)
   constexpr uint32_t kChunks = 64;
   std::vector<uint64_t> solo(kChunks, 0);
+  auto client_range = [&](uint32_t ch, uint32_t *c_lo, uint32_t *c_hi) {
+    *c_lo = (uint32_t)((uint64_t)nc * ch / kChunks);
+    *c_hi = (uint32_t)((uint64_t)nc * (ch + 1) / kChunks);
+  };
   parallel_for(kChunks, [&](uint32_t ch) {
-    const uint32_t c_lo = (uint32_t)((uint64_t)nc * ch / kChunks), c_hi = (uint32_t)((uint64_t)nc * (ch + 1) / kChunks);
+    uint32_t c_lo, c_hi;
+    client_range(ch, &c_lo, &c_hi);
     for (uint32_t c = c_lo; c < c_hi; c++) {
       const uint32_t lo = cstart[c], hi = cstart[c + 1];
       for (uint32_t x = lo; x < hi; x++) {
@@ -95,15 +114,36 @@ static void mark_multi(const Store &st, const std::vector<uint32_t> &order, Host
         // the parent probe emits a '#' node's subscriptions after a literal hit on its
         // parent; the walks skip the own visit of such a node (kFlagParentLit), so
         // it is emitted once per topic.  MQM_HASH_MULTI=1 (A/B): treat them as multi.
-        bool multi = hi - lo > kMaxPairwise ||
-                     (hash_multi && nodes[nx].key == hash_tok && px != st.root() && !wild(nodes[px].key));
-        for (uint32_t y = lo; !multi && y < hi; y++) multi = y != x && compatible(nx, sub_node[by_client[y]]);
+        const bool heavy = hi - lo > kMaxPairwise ||
+                           (hash_multi && nodes[nx].key == hash_tok && px != st.root() && !wild(nodes[px].key));
+        uint32_t pc = 0;
+        if (!heavy)
+          for (uint32_t y = lo; y < hi; y++) pc += y != x && compatible(nx, sub_node[by_client[y]]);
+        const bool multi = heavy || pc > 0;
+        pt.cnt[sx] = heavy || pc > kMaxPartners ? (uint16_t)kPHeavy : (uint16_t)pc;
         if (multi) hs.subs[sx].word |= kMetaMulti;
         else solo[ch]++;
       }
     }
   });
   for (uint64_t v : solo) hs.n_solo += v;
+  pt.off.assign(nsub + 1, 0);
+  for (uint64_t sx = 0; sx < nsub; sx++) pt.off[sx + 1] = pt.off[sx] + (pt.cnt[sx] == kPHeavy ? 0 : pt.cnt[sx]);
+  pt.part.resize(pt.off[nsub]);
+  parallel_for(kChunks, [&](uint32_t ch) {
+    uint32_t c_lo, c_hi;
+    client_range(ch, &c_lo, &c_hi);
+    for (uint32_t c = c_lo; c < c_hi; c++) {
+      const uint32_t lo = cstart[c], hi = cstart[c + 1];
+      for (uint32_t x = lo; x < hi; x++) {
+        const uint32_t sx = by_client[x];
+        if (pt.cnt[sx] == 0 || pt.cnt[sx] == kPHeavy) continue;
+        uint64_t w = pt.off[sx];
+        for (uint32_t y = lo; y < hi; y++)
+          if (y != x && compatible(sub_node[sx], sub_node[by_client[y]])) pt.part[w++] = by_client[y];
+      }
+    }
+  });
 }
 
 // DeviceRetained arrays (snapshot.h) over the preorder ids
@@ -439,12 +479,14 @@ int flatten(const Store &st, HostSnapshot *out) {
   }
   for (uint64_t i = 0; i < nn; i++) hs.nodes[i].sh_cnt_flags |= (uint32_t)flags[i] << 24;
   pt.mark("nodes");
-  mark_multi(st, order, hs);
+  Partners partners;
+  mark_multi(st, order, hs, partners);
   pt.mark("multi");
   if (st.retained_len() > 0) build_retained(st, order, new_id, hs);
   pt.mark("retained");
   // every range: solo entries first, then multi (stable); count the multi ones
   std::vector<uint32_t> own_multi(nn, 0);
+  std::vector<uint32_t> new_sid(hs.subs.size());
   {
     std::vector<SubEnt> se;
     std::vector<SubInfo> si;
@@ -455,6 +497,7 @@ int flatten(const Store &st, HostSnapshot *out) {
       for (int pass = 0; pass < 2; pass++)
         for (uint32_t j = off; j < off + cnt; j++)
           if (((hs.subs[j].word & kMetaMulti) != 0) == (pass == 1)) {
+            new_sid[j] = off + (uint32_t)se.size();
             se.push_back(hs.subs[j]);
             si.push_back(hs.sub_info[j]);
             own_multi[i] += pass;
@@ -463,12 +506,45 @@ int flatten(const Store &st, HostSnapshot *out) {
       std::copy(si.begin(), si.end(), hs.sub_info.begin() + off);
     }
   }
+  // the multi subscriptions' partner lists in final sids (snapshot.h: pinfo)
+  {
+    const uint64_t nsub = hs.subs.size();
+    hs.pinfo.assign(nsub, make_uint2(0, 0));
+    hs.partners.clear();
+    std::vector<uint8_t> heavy_at(nsub, 0);
+    for (uint64_t x = 0; x < nsub; x++) {
+      const uint16_t c = partners.cnt[x];
+      if (c == 0) continue;
+      const uint32_t nx = new_sid[x];
+      if (c == kPHeavy) {
+        hs.pinfo[nx] = make_uint2(kNone, kPInfoHeavy);
+        heavy_at[nx] = 1;
+      } else if (c <= 2) {
+        const uint64_t o = partners.off[x];
+        hs.pinfo[nx] = make_uint2(new_sid[partners.part[o]], c == 2 ? new_sid[partners.part[o + 1]] : kNone);
+      } else {
+        hs.pinfo[nx] = make_uint2((uint32_t)hs.partners.size(), kPInfoList | c);
+        for (uint64_t o = partners.off[x]; o < partners.off[x + 1]; o++) hs.partners.push_back(new_sid[partners.part[o]]);
+      }
+    }
+    // a node whose range (multi tail) holds a heavy entry: its topics merge by hash table
+    for (uint64_t i = 0; i < nn; i++) {
+      const uint32_t off = hs.nodes[i].sub_off, cnt = hs.nodes[i].sub_cnt;
+      for (uint32_t j = off + cnt - own_multi[i]; j < off + cnt; j++)
+        if (heavy_at[j]) {
+          flags[i] |= kFlagHeavyOwn;
+          break;
+        }
+    }
+  }
   for (uint64_t i = 0; i < nn; i++) {
     NodeDesc &d = hs.nodes[i];
     const uint32_t hm = d.hash != kNone ? own_multi[d.hash] : 0;
     d.hsub_cnt = d.hash != kNone ? hs.nodes[d.hash].sub_cnt : 0;
     d.multi = std::min<uint32_t>(own_multi[i], 0xFFFF) | (std::min<uint32_t>(hm, 0xFFFF) << 16);
     if (own_multi[i] >= 0xFFFF || hm >= 0xFFFF) d.sh_cnt_flags |= (uint32_t)kFlagMultiSat << 24;
+    d.sh_cnt_flags |= (uint32_t)(flags[i] & kFlagHeavyOwn) << 24;
+    if (d.hash != kNone && (flags[d.hash] & kFlagHeavyOwn)) d.sh_cnt_flags |= (uint32_t)kFlagHeavyHash << 24;
     if (i > 0 && d.hash != kNone) {  // root: its '#' child is dollar-wild, unlike the root itself
       const NodeDesc &h = hs.nodes[d.hash];
       if (!((h.sh_cnt_flags >> 24) & kFlagHasChildren) && (h.sh_cnt_flags & kShCntMask) == 0)
@@ -636,6 +712,8 @@ GpuSnapshot::~GpuSnapshot() {
   if (words) (void)hipFree(words);
   if (nflags) (void)hipFree(nflags);
   if (bloom) (void)hipFree(bloom);
+  if (pinfo) (void)hipFree(pinfo);
+  if (partners) (void)hipFree(partners);
 }
 
 int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std::unique_ptr<GpuSnapshot> *out) {
@@ -677,6 +755,16 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
     g->device_bytes += bb;
   }
   g->device_bytes += n_sub_ents * 4;
+  {  // partners of the multi entries (merge by resolution)
+    const size_t pb = hs->pinfo.size() * sizeof(uint2), qb = hs->partners.size() * 4;
+    if (hipMalloc(&g->pinfo, pb + 64) != hipSuccess || hipMalloc(&g->partners, qb + 64) != hipSuccess)
+      return MQM_ENOMEM;
+    if (pb && hipMemcpyAsync(g->pinfo, hs->pinfo.data(), pb, hipMemcpyHostToDevice, stream) != hipSuccess)
+      return MQM_EHIP;
+    if (qb && hipMemcpyAsync(g->partners, hs->partners.data(), qb, hipMemcpyHostToDevice, stream) != hipSuccess)
+      return MQM_EHIP;
+    g->device_bytes += pb + qb;
+  }
   if (ret) {  // node flags, one byte per node, for the reverse walk
     const uint64_t nn = hs->nodes.size();
     if (hipMalloc(&g->nflags, nn + 64) != hipSuccess) return MQM_ENOMEM;
@@ -709,6 +797,8 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
   g->dev.edges = (const EdgeEntry *)g->buffers[1];
   g->dev.subs = (const SubEnt *)g->buffers[2];
   g->dev.words = (const uint32_t *)g->words;
+  g->dev.pinfo = (const uint2 *)g->pinfo;
+  g->dev.partners = (const uint32_t *)g->partners;
   g->dev.bloom = (const uint64_t *)g->bloom;
   g->dev.bloom_mask = g->bloom ? hs->bloom.size() - 1 : 0;
   g->dev.tok_pool = (const uint8_t *)g->buffers[3];

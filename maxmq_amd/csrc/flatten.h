@@ -49,6 +49,8 @@ struct HostSnapshot {
   std::vector<SubInfo> shared_info;  // by shared sid
   std::vector<uint8_t> tok_pool;
   std::vector<uint64_t> bloom;       // DeviceSnapshot::bloom (empty: none)
+  std::vector<uint2> pinfo;          // DeviceSnapshot::pinfo (by final sid)
+  std::vector<uint32_t> partners;    // DeviceSnapshot::partners
   uint64_t n_buckets = 0;
   uint32_t height = 0;
   uint64_t n_edges = 0;
@@ -75,6 +77,7 @@ struct GpuSnapshot {
   void *words = nullptr;  // DeviceSnapshot::words (derived on the device at upload)
   void *nflags = nullptr; // DeviceRetained::nflags (derived on the device at upload)
   void *bloom = nullptr;  // DeviceSnapshot::bloom
+  void *pinfo = nullptr, *partners = nullptr;  // DeviceSnapshot::pinfo / partners
   DeviceRetained ret{};
   bool has_retained = false;
   uint64_t device_bytes = 0;

@@ -55,7 +55,7 @@ struct Workspace {
   enum Slot {
     kSCount, kHCount, kDCount, kDStart, kHStart, kCls, kDfsList, kRecs, kCounters, kDOut, kHOut,
     kDense, kDenseShared, kDenseOffs, kDenseHOffs, kScanTmp, kRawCnt, kTabOff, kTabSize, kTable,
-    kInBytes, kInOffs, kListS, kICount, kIStart, kIOut, kNSolo, kDescStart, kDesc, kWin, kMCount, kListW, kListT1, kListT2, kListT3, kListP, kListH, kPerm, kPermBins,
+    kInBytes, kInOffs, kListS, kICount, kIStart, kIOut, kNSolo, kDescStart, kDesc, kWin, kMCount, kListW, kListT1, kListT2, kListT3, kListP, kListH, kListRS, kListR, kPerm, kPermBins,
     // reverse match (retained.hip)
     kROffs, kRNLev, kRWild, kRLOff, kRFCount, kRFCur, kRLevels, kRNCount, kRNOff, kRItemF0, kRItemN0, kRItemF1,
     kRItemN1, kRChild, kRECount, kREOff, kREmit, kRPos, kRChunks, kRCOff, kROut, kRInBytes, kRInOffs, kNumSlots
@@ -150,6 +150,7 @@ struct MatchOutput {
   uint64_t n_solo_ranges = 0;                     // solo copy descriptors (hits with solo entries)
   uint64_t multi_entries[3] = {0, 0, 0};  // multi entries merged by the three workgroup tiers
   uint32_t n_part = 0;                    // ... of the third tier's topics, merged in client-hash partitions
+  uint32_t n_resolve = 0;                 // topics merged by resolution (k_resolve: no table)
   bool exact = false;                     // sized by its own read-back (the first call of a workspace, or a re-run)
 };
 

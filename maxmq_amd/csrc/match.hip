@@ -175,7 +175,9 @@ __device__ __forceinline__ uint32_t lit_kind(uint32_t plus) {
 
 // topic class (cls): Done = no entries and no shared candidates; Bounded (+
 // FewHits when nh <= kSmallHits, for k_route) = emitted from its record; Dfs
-enum : uint8_t { kClsDone = 0, kClsBounded = 1, kClsDfs = 2, kClsFewHits = 4 };
+// kClsHeavy: a gathered multi range holds an entry the merge by resolution
+// cannot take (kFlagHeavyOwn / kFlagHeavyHash): the topic merges by hash table
+enum : uint8_t { kClsDone = 0, kClsBounded = 1, kClsDfs = 2, kClsFewHits = 4, kClsHeavy = 8 };
 enum : uint32_t { kWhyFrontier = 0, kWhyHits = 1, kWhyLevels = 2, kWhyShared = 3, kWhyEntries = 4 };
 
 struct Counters {              // zeroed before every batch
@@ -191,6 +193,8 @@ struct Counters {              // zeroed before every batch
   unsigned int n_t3;           // k_multi<4096>: 1536 < Ms <= 3072
   unsigned int n_part;         // k_multi_part: Ms > 3072
   unsigned int n_shlist;       // k_shared: topics with shared candidates
+  unsigned int n_res_small;    // k_resolve<8>: no heavy entry, Ms <= kSmallMultiS, nh <= kSmallHits
+  unsigned int n_res;          // k_resolve<64>: other topics with multi entries and no heavy entry
   unsigned long long m_sum[3]; // multi entries of the k_multi<1024> / <2048> / <4096> + k_multi_part lists
   unsigned int oob;            // a store fell outside its output buffer (queued calls: buffers sized
                                //   from an earlier call were too small; the call is re-run)
@@ -499,6 +503,7 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
     if (len > 0xFFFFu) why = kWhyLevels;  // separators are kept as 16-bit positions
     uint32_t ni = nlev > 0 && why == kNoWhy ? root_items : 0, nh = 0, nsh = 0, nq = 0, nm = 0;
     uint32_t ls = 0, lm = 0, lh = 0;  // this lane's solo / multi / shared entries
+    bool heavy = false;                // a gathered multi range with a heavy entry (kClsHeavy)
     int cur = 0;
     for (uint32_t d = 0; d < nlev && ni > 0; d++) {
       if (d >= (uint32_t)kLMax) {
@@ -593,6 +598,7 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
         // multi parts go to the record's tail with their hit's rank
         const uint32_t mu_own = c_own ? (dc.multi & 0xFFFFu) : 0, mu_par = c_par ? (dc.multi >> 16) : 0;
         const uint32_t mu_hl = c_hl ? (dc.multi >> 16) : 0;
+        heavy |= (mu_own && (fl & kFlagHeavyOwn)) || ((mu_par | mu_hl) && (fl & kFlagHeavyHash));
         const uint32_t hoff = dc.sub_off + dc.sub_cnt;
         const uint32_t x_own = (uint32_t)(__ballot(mu_own > 0) >> gbase) & kGMask;
         const uint32_t x_par = (uint32_t)(__ballot(mu_par > 0) >> gbase) & kGMask;
@@ -672,11 +678,14 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
     }
     const uint32_t Ss = ls, Ms = lm, H = lh;
     const uint32_t S = Ss + Ms;
+    const bool any_heavy = ((__ballot(heavy) >> gbase) & kGMask) != 0;
     if (why == kNoWhy && S > kSMax) why = kWhyEntries;
     if (active && gl == 0) {
       const bool dfs = why != kNoWhy;
       if (!dfs) tail[0] = make_uint4(nm | (nsh << 8), Ss, Ms, nq);
-      o.cls[t] = dfs ? kClsDfs : (S == 0 && H == 0) ? kClsDone : (kClsBounded | (nm <= kSmallHits ? kClsFewHits : 0));
+      o.cls[t] = dfs ? kClsDfs
+                     : (S == 0 && H == 0) ? kClsDone
+                                          : (kClsBounded | (nm <= kSmallHits ? kClsFewHits : 0) | (any_heavy ? kClsHeavy : 0));
       o.nsolo[t] = dfs ? 0 : nq;
       o.scount[t] = dfs ? 0 : S;
       o.hcount[t] = dfs ? 0 : H;
@@ -1403,6 +1412,130 @@ __global__ __launch_bounds__(kBigThreads) void k_multi_part(DeviceSnapshot s, Ou
 }
 
 
+
+// ---------------------------------------------------------------------------
+// k_resolve<kE, kH>: the merge by resolution (snapshot.h: pinfo) for topics
+// whose multi entries are all light (no kClsHeavy): kE lanes per topic (8 for
+// topics with <= kSmallMultiS entries and <= kSmallHits multi parts, 64
+// otherwise), no table, no atomics.  The topic's multi parts (the walk's
+// record: range start, count, hit rank) are sorted by range start in LDS;
+// every multi entry reads its packed word and its partners, looks each
+// partner up among the gathered ranges (binary search: a partner is gathered
+// iff its sid lies in one of them, since it is a multi entry itself and sits in
+// its range's multi tail), and is its client's delivery iff no gathered
+// partner comes first in the reference's order (rank, sid) — the winner folds
+// the gathered partners' QoS / NoLocal in: Subscription.Merge
+// (packets.go:250-270) without a table.  Winners are written after the
+// topic's solo deliveries in entry order (deterministic).
+// ---------------------------------------------------------------------------
+// MQM_NO_RESOLVE=1 (A/B, read at every batch so a test can compare both in
+// one process): every topic with multi entries merges by hash table
+static bool resolve_on() {
+  const char *v = getenv("MQM_NO_RESOLVE");
+  return !v || atoi(v) == 0;
+}
+
+template <int kH>
+struct alignas(16) ResolveLds {
+  uint32_t rec[4 + kRecHit * kH];  // header + multi parts (the record's tail, in the walk's order)
+  uint32_t sk[kH], se[kH], sr[kH]; // the parts by range start: start, end, rank
+};
+
+template <int kE, int kH, int kPer>
+__global__ __launch_bounds__(kWave *kEmitWaves) void k_resolve(DeviceSnapshot s, Outputs o,
+                                                               const uint32_t *__restrict__ list,
+                                                               const unsigned int *__restrict__ count) {
+  constexpr int kGroups = kWave / kE;
+  constexpr uint64_t kGMask = kE == 64 ? ~0ull : (1ull << kE) - 1ull;
+  constexpr int kUnits = 1 + kH;  // record units (16 B) read per topic
+  static_assert(kH <= kHCap && kUnits <= kRecStrideAlloc / 4, "record tail");
+  __shared__ ResolveLds<kH> lds_all[kEmitWaves * kGroups];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane / kE, gl = lane % kE, gbase = g * kE;
+  const uint64_t glt = (1ull << gl) - 1ull;
+  ResolveLds<kH> &L = lds_all[(threadIdx.x / kWave) * kGroups + g];
+  const uint32_t ngroups = gridDim.x * kEmitWaves * kGroups, nl = *count;
+  for (uint32_t i = (blockIdx.x * kEmitWaves + threadIdx.x / kWave) * kGroups + g; i < nl; i += ngroups) {
+    const uint32_t t = list[i];
+    const uint64_t db = o.dstart[t];
+    // the record's tail: header + kH parts, unconditionally (inside the slot)
+    const uint4 *gt = rec_tail(o.recs, t);
+    uint4 *rec4 = reinterpret_cast<uint4 *>(L.rec);
+#pragma unroll
+    for (int u0 = 0; u0 < kUnits; u0 += kE)
+      if (u0 + gl < kUnits) rec4[u0 + gl] = gt[-(u0 + gl)];
+    wave_lds_sync();
+    const uint32_t nh = L.rec[0] & 0xFFu, Ss = L.rec[1], M = L.rec[2];
+    for (uint32_t h = gl; h < nh; h += kE) {  // rank sort by range start (ranges are disjoint)
+      const uint32_t mo = rec_at(L.rec, h, kFieldOff), mc = rec_at(L.rec, h, kFieldMpre);
+      uint32_t r = 0;
+      for (uint32_t j = 0; j < nh; j++) r += rec_at(L.rec, j, kFieldOff) < mo ? 1u : 0u;
+      L.sk[r] = mo;
+      L.se[r] = mo + mc;
+      L.sr[r] = rec_at(L.rec, h, kFieldRank);
+    }
+    wave_lds_sync();
+    rec_prefix<kE, kH>(L.rec, nh, gl);  // part counts -> exclusive prefixes (multi_sid)
+    wave_lds_sync();
+    // the gathered rank of sid p (false: p's range is not gathered)
+    auto gathered = [&](uint32_t p, uint32_t *rank) {
+      uint32_t j = 0;
+#pragma unroll
+      for (uint32_t step = kH / 2; step > 0; step >>= 1) {
+        const uint32_t c = j + step;
+        j = (c < nh && L.sk[c < nh ? c : 0] <= p) ? c : j;
+      }
+      const bool in = nh > 0 && L.sk[j] <= p && p < L.se[j];
+      *rank = in ? L.sr[j] : 0;
+      return in;
+    };
+    uint32_t D = 0;
+    for (uint32_t q0 = 0; q0 < M; q0 += kE * kPer) {
+      uint32_t sid[kPer], rk[kPer], wd[kPer];
+      uint2 pi[kPer];
+#pragma unroll
+      for (int k = 0; k < kPer; k++) {  // every entry's loads in flight together
+        const uint32_t q = q0 + k * kE + gl;
+        uint32_t h;
+        sid[k] = multi_sid(L.rec, nh, q < M ? q : 0, &h);
+        rk[k] = rec_at(L.rec, h, kFieldRank);
+        wd[k] = s.words[sid[k]];
+        pi[k] = s.pinfo[sid[k]];
+      }
+#pragma unroll
+      for (int k = 0; k < kPer; k++) {
+        const uint32_t q = q0 + k * kE + gl;
+        bool win = q < M;
+        uint32_t qb = qos_bits(wd[k]);
+        auto meet = [&](uint32_t p) {
+          uint32_t rp;
+          if (!gathered(p, &rp)) return;
+          qb |= qos_bits(s.words[p]);
+          if (rp < rk[k] || (rp == rk[k] && p < sid[k])) win = false;
+        };
+        if (win) {
+          if (pi[k].y == kPInfoHeavy) {  // routed here by mistake: never expected (kClsHeavy)
+            atomicOr(&o.ctr->oob, 1u);
+          } else if (pi[k].y & kPInfoList) {
+            const uint32_t c = pi[k].y & 0xFFu;
+            for (uint32_t j = 0; j < c; j++) meet(s.partners[pi[k].x + j]);
+          } else {
+            if (pi[k].x != kNone) meet(pi[k].x);
+            if (pi[k].y != kNone) meet(pi[k].y);
+          }
+        }
+        const uint64_t m = (__ballot(win) >> gbase) & kGMask;
+        if (win)
+          put_checked(o.dout, db + Ss + D + __popcll(m & glt), o.dcap,
+                      pack_delivery(sid[k], 31u - __builtin_clz(qb & 7u), (qb >> 3) & 1u), &o.ctr->oob);
+        D += __popcll(m);
+      }
+    }
+    if (gl == 0) o.dcount[t] = Ss + D;
+    wave_lds_sync();
+  }
+}
+
 // ---------------------------------------------------------------------------
 // k_dfs<P>: the unbounded path.  P0 counts raw entries / shared candidates;
 // P1 inserts into a per-topic global table and writes the shared candidates;
@@ -1562,7 +1695,8 @@ __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *
         for (int part = 0; part < 2; part++) {
           if (part == 1 && src != 0) break;
           const uint32_t roff = part ? e.sub_off + e.sub_cnt : e.sub_off;  // '#' child's range follows
-          const uint32_t rcnt = skip_dollar ? 0 : (part ? e.hsub_cnt : e.sub_cnt);
+          // (a '#' node after a literal parent: its parent probe gathered it, kFlagParentLit)
+          const uint32_t rcnt = skip_dollar || (part == 0 && (fl & kFlagParentLit)) ? 0 : (part ? e.hsub_cnt : e.sub_cnt);
           const uint32_t rank = 2 * cc + part;
           S += rcnt;
           if (kPhase >= 3) {  // identifiers: the range's entries with Identifier > 0
@@ -1771,7 +1905,7 @@ __global__ __launch_bounds__(256) void k_densify(DeviceSnapshot s, uint32_t n, c
 // counters), reserves its ranges with one global atomic per list, then
 // writes them.  Order within a list is unspecified (lists only schedule
 // work; every topic's output position is its own dstart).
-enum : int { kLSmall = 0, kLWave, kLT1, kLT2, kLT3, kLPart, kLShared, kNLists };
+enum : int { kLSmall = 0, kLWave, kLT1, kLT2, kLT3, kLPart, kLShared, kLResSmall, kLRes, kNLists };
 // k_multi<1024> / <2048> / <4096> capacities (load 0.75); k_multi_part beyond
 // (partition passes re-read every entry: a single-pass 4096-slot table is
 // cheaper up to its capacity)
@@ -1782,10 +1916,12 @@ struct Lists {
 
 // the merge list of a topic with multi entries (by their count m), and the
 // shared-candidate list
-__device__ __forceinline__ uint32_t route_mask(uint8_t c, uint32_t m, uint32_t h) {
+__device__ __forceinline__ uint32_t route_mask(uint8_t c, uint32_t m, uint32_t h, bool resolve) {
   if (!(c & kClsBounded)) return 0;
   const uint32_t sh = h ? (1u << kLShared) : 0u;
   if (m == 0) return sh;
+  if (resolve && !(c & kClsHeavy))  // merge by resolution (k_resolve)
+    return sh | (((c & kClsFewHits) && m <= kSmallMultiS) ? (1u << kLResSmall) : (1u << kLRes));
   if ((c & kClsFewHits) && m <= kSmallMultiS) return sh | (1u << kLSmall);
   return sh | (m <= kSmallMulti ? (1u << kLWave)
                : m <= kT1Max  ? (1u << kLT1)
@@ -1797,7 +1933,7 @@ __device__ __forceinline__ uint32_t route_mask(uint8_t c, uint32_t m, uint32_t h
 __global__ __launch_bounds__(256) void k_route(const uint8_t *__restrict__ cls, const uint32_t *__restrict__ mcount,
                                                const uint32_t *__restrict__ hcount, uint32_t n, Lists L,
                                                unsigned int *__restrict__ counts,
-                                               unsigned long long *__restrict__ msum) {
+                                               unsigned long long *__restrict__ msum, int resolve) {
   __shared__ unsigned int lc[kNLists], base[kNLists];
   __shared__ unsigned long long ms[3];
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
@@ -1808,7 +1944,7 @@ __global__ __launch_bounds__(256) void k_route(const uint8_t *__restrict__ cls, 
   __syncthreads();
   for (uint32_t t0 = lo; t0 < hi; t0 += blockDim.x) {
     const uint32_t t = t0 + tid;
-    const uint32_t r = t < hi ? route_mask(cls[t], mcount[t], hcount[t]) : 0;
+    const uint32_t r = t < hi ? route_mask(cls[t], mcount[t], hcount[t], resolve != 0) : 0;
 #pragma unroll
     for (int l = 0; l < kNLists; l++) {
       const uint64_t m = __ballot((r >> l) & 1u);
@@ -1826,7 +1962,7 @@ __global__ __launch_bounds__(256) void k_route(const uint8_t *__restrict__ cls, 
   __syncthreads();
   for (uint32_t t0 = lo; t0 < hi; t0 += blockDim.x) {
     const uint32_t t = t0 + tid;
-    const uint32_t r = t < hi ? route_mask(cls[t], mcount[t], hcount[t]) : 0;
+    const uint32_t r = t < hi ? route_mask(cls[t], mcount[t], hcount[t], resolve != 0) : 0;
 #pragma unroll
     for (int l = 0; l < kNLists; l++) {
       const bool in = (r >> l) & 1u;
@@ -2108,7 +2244,8 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
       scan_offsets(ws, (const uint32_t *)o.hcount, o.hstart, n, st) || scan_offsets(ws, o.nsolo, desc_start, n, st))
     return -3;
   // merge lists
-  const W::Slot list_slots[kNLists] = {W::kListS, W::kListW, W::kListT1, W::kListT2, W::kListT3, W::kListP, W::kListH};
+  const W::Slot list_slots[kNLists] = {W::kListS, W::kListW, W::kListT1, W::kListT2, W::kListT3,
+                                       W::kListP, W::kListH, W::kListRS, W::kListR};
   Lists lists;
   for (int l = 0; l < kNLists; l++) {
     if (ws.get(list_slots[l], sizeof(uint32_t) * (n + 1))) return -2;
@@ -2117,7 +2254,7 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
   unsigned int *lcount = &o.ctr->n_small;  // kNLists consecutive counters
   if (n > 0) {
     hipLaunchKernelGGL(k_route, dim3(std::min<uint32_t>((n + 4095) / 4096, 2048)), dim3(256), 0, st, o.cls, o.mcount,
-                       o.hcount, n, lists, lcount, o.ctr->m_sum);
+                       o.hcount, n, lists, lcount, o.ctr->m_sum, resolve_on() ? 1 : 0);
     HIP_TRY(hipGetLastError());
   }
   hipLaunchKernelGGL(k_totals, dim3(1), dim3(64), 0, st, o.ctr, o.dstart, o.hstart, desc_start, n);
@@ -2214,10 +2351,11 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
     };
     const bool l_small = has_list(hc->n_small, kLSmall), l_wave = has_list(hc->n_wmerge, kLWave),
                l_t1 = has_list(hc->n_t1, kLT1), l_t2 = has_list(hc->n_t2, kLT2), l_t3 = has_list(hc->n_t3, kLT3),
-               l_part = has_list(hc->n_part, kLPart), l_sh = has_list(hc->n_shlist, kLShared);
+               l_part = has_list(hc->n_part, kLPart), l_sh = has_list(hc->n_shlist, kLShared),
+               l_rs = has_list(hc->n_res_small, kLResSmall), l_r = has_list(hc->n_res, kLRes);
     ws.pend_launched = launched;
     auto has = [&](uint32_t c) { return !exact || c > 0; };
-    const bool merges = l_small || l_wave || l_t1 || l_t2 || l_t3 || l_part;
+    const bool merges = l_small || l_wave || l_t1 || l_t2 || l_t3 || l_part || l_rs || l_r;
     const bool side = merges && ws.overlap;
     // persistent grids: with both streams busy, each takes its share of the device
     const uint32_t side_pct = side ? MQM_SIDE_PCT : 100, main_pct = side && MQM_SIDE_PCT < 100 ? 100 - MQM_SIDE_PCT : 100;
@@ -2233,6 +2371,11 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
       // MQM_MERGE_BIG_FIRST=1: the workgroup merges first, the small-topic
       // merges last (they fill the device better at the end of the stream)
       auto big = [&]() -> int {
+        if (l_r) {
+          hipLaunchKernelGGL((k_resolve<kWave, kHCap, 4>), grid((k_resolve<kWave, kHCap, 4>)),
+                             dim3(kWave * kEmitWaves), 0, ms, s, o, lists.l[kLRes], lcount + kLRes);
+          HIP_TRY(hipGetLastError());
+        }
         if (l_t1) {
           hipLaunchKernelGGL(k_multi<1024>, grid(k_multi<1024>), dim3(kBigThreads), 0, ms, s, o, lists.l[kLT1],
                              lcount + kLT1);
@@ -2256,6 +2399,11 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
         return 0;
       };
       auto small = [&]() -> int {
+        if (l_rs) {
+          hipLaunchKernelGGL((k_resolve<kSmallLanes, 16, 3>), grid((k_resolve<kSmallLanes, 16, 3>)),
+                             dim3(kWave * kEmitWaves), 0, ms, s, o, lists.l[kLResSmall], lcount + kLResSmall);
+          HIP_TRY(hipGetLastError());
+        }
         if (l_small) {
           hipLaunchKernelGGL((k_merge_small<6>), grid(k_merge_small<6>), dim3(kWave * kEmitWaves), 0, ms, s, o,
                              lists.l[kLSmall], lcount + kLSmall);
@@ -2337,8 +2485,9 @@ int match_collect(Workspace &ws, hipStream_t st, MatchOutput *out) {
   }
   {
     uint32_t seen = 0;
-    const unsigned int c[][2] = {{hc->n_small, kLSmall}, {hc->n_wmerge, kLWave}, {hc->n_t1, kLT1}, {hc->n_t2, kLT2},
-                                 {hc->n_t3, kLT3},       {hc->n_part, kLPart},   {hc->n_shlist, kLShared}};
+    const unsigned int c[][2] = {{hc->n_small, kLSmall}, {hc->n_wmerge, kLWave},     {hc->n_t1, kLT1},
+                                 {hc->n_t2, kLT2},       {hc->n_t3, kLT3},         {hc->n_part, kLPart},
+                                 {hc->n_shlist, kLShared}, {hc->n_res_small, kLResSmall}, {hc->n_res, kLRes}};
     for (const auto &x : c)
       if (x[0]) seen |= 1u << x[1];
     const bool missed = (seen & ~ws.pend_launched) != 0;
@@ -2371,6 +2520,7 @@ int match_collect(Workspace &ws, hipStream_t st, MatchOutput *out) {
   out->n_tier3 = hc->n_t3 + hc->n_part;
   for (int i = 0; i < 3; i++) out->multi_entries[i] = hc->m_sum[i];
   out->n_part = hc->n_part;
+  out->n_resolve = hc->n_res_small + hc->n_res;
   out->n_merge_small = hc->n_small;
   out->n_merge_wave = hc->n_wmerge;
   out->n_solo_ranges = hc->n_desc;

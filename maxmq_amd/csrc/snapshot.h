@@ -30,6 +30,9 @@ enum : uint32_t {
                           //   this node's own visit (the next level's '#' probe, :503) happens
                           //   only when that probe did, so the walks skip the own visit's
                           //   (non-shared) gather: a set gathered twice is the same set once
+  kFlagHeavyOwn = 64u,    // the node's own range has a multi entry the merge by resolution cannot take
+                          //   (pinfo kPInfoHeavy): a topic gathering it merges by hash table
+  kFlagHeavyHash = 128u,  // likewise the '#' child's range (gathered by the parent probe / at push)
 };
 
 struct NodeDesc {         // 32 B
@@ -104,6 +107,20 @@ constexpr uint32_t kMetaIdent = 1u << 7;
 constexpr uint32_t kSidBits = 28;
 constexpr uint32_t kMaxSubs = 1u << kSidBits;
 
+// Merge by resolution (match.hip k_resolve).  pinfo[sid] of a multi entry
+// lists its partners — the other subscriptions of its client whose filters are
+// level-compatible with its own (flatten.cpp mark_multi), i.e. every entry it
+// can meet in one topic's gather (the parent-'#' double gather is gone:
+// kFlagParentLit).  {p0, p1} inline for one or two partners (kNone when
+// absent); {offset into partners, kPInfoList | count} for up to kMaxPartners;
+// {kNone, kPInfoHeavy}: merged by hash table only.  A gathered entry whose
+// gathered partners all come later in the reference's order (rank, sid) is its
+// client's first-merged entry and writes the delivery with every gathered
+// partner's QoS / NoLocal folded in (packets.go:250-270); the others write
+// nothing.  Solo entries: {0, 0} (unused).
+constexpr uint32_t kPInfoList = 0x80000000u, kPInfoHeavy = 0xFFFFFFFEu;
+constexpr uint32_t kMaxPartners = 15;
+
 struct DeviceSnapshot {
   const NodeDesc *nodes;
   const EdgeEntry *edges;
@@ -115,6 +132,8 @@ struct DeviceSnapshot {
   // it stays in the Infinity Cache), checked before a literal probe: half the
   // walk's probes are for tokens no edge has (random topic levels under a
   // node that also has a '+' child), and each would cost a DRAM request
+  const uint2 *pinfo;     // n_subs: partners of a multi entry (above)
+  const uint32_t *partners;
   const uint64_t *bloom;  // nullptr: no filter
   uint64_t bloom_mask;    // words - 1 (a power of two)
   uint32_t n_nodes;

@@ -100,8 +100,38 @@ def test_config_vs_oracle(config, overrides):
     assert_same(gs, rs, "shared")
 
 
-def test_edge_cases_and_fallback_paths():
+@pytest.mark.parametrize("merge", ["fast", "resolve", "table"])
+def test_edge_cases_and_fallback_paths(merge, monkeypatch):
+    """every edge case through the one-launch path for small batches (fast.hip,
+    the default for this batch size) and through the batch pipeline
+    (MQM_NO_FAST=1) with multi entries merged by resolution (partner lists, its
+    default) or by hash table (MQM_NO_RESOLVE=1: the k_merge_small / k_merge /
+    k_multi<1024|2048|4096> / k_multi_part tiers)"""
+    if merge != "fast":
+        monkeypatch.setenv("MQM_NO_FAST", "1")
+    if merge == "table":
+        monkeypatch.setenv("MQM_NO_RESOLVE", "1")
     filters, clients, topics = [], [], []
+    # heavy clients (merged by hash table even with resolution on): 70 filters
+    # each (> 64 per client: no pairwise marking), all matching "hv/a/b/c/d/e/f"
+    # (every prefix, each level literal or '+'), 50 clients -> 3500 heavy multi
+    # entries in one topic (the partitioned workgroup merge); and a client with
+    # 20 compatible filters (> 15 partners each: heavy)
+    hv = ["hv", "a", "b", "c", "d", "e", "f"]
+    hvf = []
+    for k in range(1, 8):
+        for m in range(1 << k):
+            hvf.append("/".join("+" if (m >> b) & 1 else hv[b] for b in range(k)))
+    for i in range(50):
+        filters += hvf[:70]
+        clients += [f"hv{i}"] * 70
+    filters += hvf[100:120]
+    clients += ["p20"] * 20
+    # 4 compatible filters per client (3 partners: the partner list, not inline)
+    for i in range(30):
+        filters += ["q4/a/b", "q4/+/b", "q4/a/+", "q4/#"]
+        clients += [f"q{i}"] * 4
+    topics += ["hv/a/b/c/d/e/f", "hv/a/b", "hv/x/b/c/d/e/f/g", "q4/a/b", "q4/z/b", "q4"]
     # hub: 1000 clients on a/# and a/b -> S > 384 per topic (global dedupe path)
     for i in range(1000):
         filters += ["hub/#", "hub/x"]
@@ -150,9 +180,20 @@ def test_edge_cases_and_fallback_paths():
     (g, gs), (r, rs), res = _gpu_and_oracle(filters, topics, clients)
     assert_same(g, r, "deliveries")
     assert_same(gs, rs, "shared")
+    # the same batch through the device pipeline: the merge kernels that ran
+    import torch
 
-
-def test_random_ops_with_autocommit():
+    s = Strings.from_list(topics)
+    idx = res._index
+    tb = torch.from_numpy(s.data).cuda()
+    to = torch.from_numpy(s.offs.view(np.int64)).cuda()
+    r = idx.match_device(tb.data_ptr(), to.data_ptr(), len(topics))
+    torch.cuda.synchronize()
+    assert int(r.n_deliveries) == len(g), (int(r.n_deliveries), len(g))
+    if merge != "table":
+        assert r.n_resolve > 0 and r.n_big > 0, (r.n_resolve, r.n_big)
+    else:
+        assert r.n_resolve == 0 and r.n_part > 0, (r.n_resolve, r.n_part)
     rng = random.Random(99)
     levels = ["a", "b", "", "+", "#", "$SYS", "$x", "c" * 18]
     for trial in range(8):
