@@ -13,6 +13,8 @@
 #   c4pmc / pmc: FETCH_SIZE / WRITE_SIZE passes (C4 shard / C3) -> traffic_c4.json / traffic.json
 #   calib   : tools/_build/calib_fetch (random-gather / cooperative-gather rates) -> calib_kernels.txt
 #   pipe    : `fast` with pipelined steps on 2 and 3 contexts -> bench_fast_pipe{2,3}.json
+#   abr     : `fast` with merge by resolution on / off (MQM_NO_RESOLVE=0/1)
+#   par     : the parity and queued-call GPU tests only
 #   smoke   : __graft_entry__.smoke()
 #   bench   : the default bench line (C3)                -> gpurun_out/TAG/bench.json
 #   fast    : bench without CPU baseline / host path      -> gpurun_out/TAG/bench_fast.json
@@ -61,6 +63,10 @@ for step in "$@"; do
              python3 profiles/pmc_to_traffic.py $OUT/pmc > $OUT/traffic.json ;;
     pipe) for P in 2 3; do timeout -k 10 400 python3 -u bench.py $FAST --pipeline $P > $OUT/bench_fast_pipe$P.json \
              2> $OUT/bench_fast_pipe$P.log || exit 1; done ;;
+    abr) for V in 0 1; do MQM_NO_RESOLVE=$V timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_nores$V.json \
+             2> $OUT/bench_fast_nores$V.log || exit 1; done ;;
+    par) timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_gpu_queued.py -m gpu --timeout 300 \
+             > $OUT/pytest_par.log 2>&1 ;;
     abq) for V in 1 0; do MQM_QUEUED=$V timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_q$V.json \
              2> $OUT/bench_fast_q$V.log || exit 1; done ;;
     abf) for V in 0 1; do MQM_FLUSH=$V timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_flush$V.json \
