@@ -920,8 +920,16 @@ __global__ __launch_bounds__(256) void k_winmap(const uint4 *__restrict__ desc, 
 #define MQM_WINCOPY_CU 16
 #endif
 constexpr int kCU = MQM_WINCOPY_CU;  // entries per lane per step (tuning knob)
+// MQM_WINCOPY_BLK=1: position -> descriptor through a per-64-position block
+// index (the last descriptor starting at or before each block, one search per
+// block and descriptor batch), then a search inside the block's few
+// descriptors — usually none or one step instead of six per entry
+#ifndef MQM_WINCOPY_BLK
+#define MQM_WINCOPY_BLK 1
+#endif
 struct alignas(16) WinLds {
   uint32_t st[kWave], en[kWave], src[kWave];
+  uint32_t blk[kWin / kWave];
 };
 
 __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_eu(8))) void k_wincopy(
@@ -957,6 +965,17 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
       L.en[lane] = (uint32_t)(b - g0);
       L.src[lane] = d.x + (uint32_t)(a - dst);
       wave_lds_sync();
+#if MQM_WINCOPY_BLK
+      {  // block lane (positions lane * 64 ..): the last descriptor starting at or before its start
+        static_assert(kWin / kWave == kWave, "one block per lane");
+        const uint32_t q = (uint32_t)lane * kWave;
+        uint32_t k = 0;
+#pragma unroll
+        for (uint32_t step = 32; step > 0; step >>= 1) k = L.st[k + step] <= q ? k + step : k;
+        L.blk[lane] = k;
+      }
+      wave_lds_sync();
+#endif
       const uint32_t q0 = (uint32_t)(pos - g0), q1 = (uint32_t)(bend - g0);
       for (uint32_t base = q0; base < q1; base += kWave * kCU) {
         uint32_t sa[kCU];
@@ -964,9 +983,24 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
 #pragma unroll
         for (int u = 0; u < kCU; u++) {
           const uint32_t q = base + u * kWave + lane;
+#if MQM_WINCOPY_BLK
+          // the last descriptor starting at or before q: within [blk[b], blk[b + 1]]
+          const uint32_t bq = min(q, (uint32_t)kWin - 1) / kWave;
+          uint32_t k = L.blk[bq], left = (bq + 1 < kWin / kWave ? L.blk[bq + 1] : kWave - 1) - k;
+          while (left > 0) {
+            const uint32_t half = (left + 1) / 2;
+            if (L.st[k + half] <= q) {
+              k += half;
+              left -= half;
+            } else {
+              left = half - 1;
+            }
+          }
+#else
           uint32_t k = 0;  // the last descriptor starting at or before q
 #pragma unroll
           for (uint32_t step = 32; step > 0; step >>= 1) k = L.st[k + step] <= q ? k + step : k;  // k + step <= 63
+#endif
           in[u] = q < q1 && q >= L.st[k] && q < L.en[k];
           sa[u] = in[u] ? L.src[k] + (q - L.st[k]) : 0u;
         }
