@@ -1550,7 +1550,7 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_resolve(DeviceSnapshot s,
         if (win) {
           if (pi[k].y == kPInfoHeavy) {  // routed here by mistake: never expected (kClsHeavy)
             atomicOr(&o.ctr->oob, 1u);
-          } else if (pi[k].y & kPInfoList) {
+          } else if (pi[k].y != kNone && (pi[k].y & kPInfoList)) {  // (kNone: one inline partner)
             const uint32_t c = pi[k].y & 0xFFu;
             for (uint32_t j = 0; j < c; j++) meet(s.partners[pi[k].x + j]);
           } else {

@@ -113,7 +113,8 @@ constexpr uint32_t kMaxSubs = 1u << kSidBits;
 // can meet in one topic's gather (the parent-'#' double gather is gone:
 // kFlagParentLit).  {p0, p1} inline for one or two partners (kNone when
 // absent); {offset into partners, kPInfoList | count} for up to kMaxPartners;
-// {kNone, kPInfoHeavy}: merged by hash table only.  A gathered entry whose
+// {kNone, kPInfoHeavy}: merged by hash table only (an inline second partner is
+// a sid < 2^28, so kPInfoList | count, kNone and kPInfoHeavy stay distinct).  A gathered entry whose
 // gathered partners all come later in the reference's order (rank, sid) is its
 // client's first-merged entry and writes the delivery with every gathered
 // partner's QoS / NoLocal folded in (packets.go:250-270); the others write
