@@ -113,15 +113,15 @@ def test_edge_cases_and_fallback_paths(merge, monkeypatch):
         monkeypatch.setenv("MQM_NO_RESOLVE", "1")
     filters, clients, topics = [], [], []
     # heavy clients (merged by hash table even with resolution on): 70 filters
-    # each (> 64 per client: no pairwise marking), all matching "hv/a/b/c/d/e/f"
-    # (every prefix, each level literal or '+'), 50 clients -> 3500 heavy multi
-    # entries in one topic (the partitioned workgroup merge); and a client with
-    # 20 compatible filters (> 15 partners each: heavy)
+    # each (> 64 per client: no pairwise marking), all under "hv" and matching
+    # "hv/a/b/c/d/e/f" (every prefix, each level after the first literal or
+    # '+'), 50 clients -> 350 heavy multi entries for "hv/a/b" (a workgroup
+    # tier); and a client with 20 compatible filters (> 15 partners each: heavy)
     hv = ["hv", "a", "b", "c", "d", "e", "f"]
     hvf = []
     for k in range(1, 8):
-        for m in range(1 << k):
-            hvf.append("/".join("+" if (m >> b) & 1 else hv[b] for b in range(k)))
+        for m in range(1 << (k - 1)):
+            hvf.append("/".join(["hv"] + ["+" if (m >> (b - 1)) & 1 else hv[b] for b in range(1, k)]))
     for i in range(50):
         filters += hvf[:70]
         clients += [f"hv{i}"] * 70
