@@ -451,7 +451,8 @@ def test_full_size_c3_headline_config():
       * over all 10M topics: dense CSR monotone and summing to n_deliveries,
         QoS <= 2, client ids in range, per-topic client uniqueness (on a 1M
         sample), run-to-run equality of every topic's checksum of its entries;
-      * the big class and the workgroup merge tier were exercised."""
+      * the merge by resolution was exercised (every C3 multi entry is light:
+        no client has more than 64 subscriptions or 15 partners)."""
     import torch
 
     from tests.gpu_util import dev_tensor, topic_checksums
@@ -477,7 +478,7 @@ def test_full_size_c3_headline_config():
     r1, offs, ents, sh_offs = run()
     nd = int(r1.n_deliveries)
     assert nd > 50 * n, nd  # Zipf fan-out: ~230 deliveries per topic
-    assert r1.n_big > 0, "the workgroup merge tier never ran"
+    assert r1.n_resolve > 0, "the merge by resolution never ran"
     assert int(offs[0]) == 0 and int(offs[-1]) == nd
     assert bool((offs[1:] >= offs[:-1]).all())
     assert int(sh_offs[-1]) == int(r1.n_shared)
