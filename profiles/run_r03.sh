@@ -15,6 +15,8 @@
 #   pipe    : `fast` with pipelined steps on 2 and 3 contexts -> bench_fast_pipe{2,3}.json
 #   abr     : `fast` with merge by resolution on / off (MQM_NO_RESOLVE=0/1)
 #   par     : the parity and queued-call GPU tests only
+#   c4ab    : the C4 shard bench with merge by resolution on / off
+#   profres : serial rocprof kernel stats of `fast` (merge by resolution on)
 #   smoke   : __graft_entry__.smoke()
 #   bench   : the default bench line (C3)                -> gpurun_out/TAG/bench.json
 #   fast    : bench without CPU baseline / host path      -> gpurun_out/TAG/bench_fast.json
@@ -65,6 +67,11 @@ for step in "$@"; do
              2> $OUT/bench_fast_pipe$P.log || exit 1; done ;;
     abr) for V in 0 1; do MQM_NO_RESOLVE=$V timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_nores$V.json \
              2> $OUT/bench_fast_nores$V.log || exit 1; done ;;
+    c4ab) for V in 0 1; do MQM_NO_RESOLVE=$V timeout -k 10 600 python3 -u bench.py --config 4 --shard 0/8 $FAST \
+             > $OUT/bench_c4_fast_nores$V.json 2> $OUT/bench_c4_fast_nores$V.log || exit 1; done ;;
+    profres) (cd /tmp && export TMPDIR=/tmp MQM_NO_OVERLAP=1 && timeout -k 10 500 rocprofv3 --kernel-trace --stats \
+             --output-format csv -d $OUT/profres -o prof -- python3 $ROOT/bench.py $FAST \
+             > $OUT/bench_under_rocprof_res.json 2> $OUT/rocprof_res.log) ;;
     par) timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_gpu_queued.py -m gpu --timeout 300 \
              > $OUT/pytest_par.log 2>&1 ;;
     abq) for V in 1 0; do MQM_QUEUED=$V timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_q$V.json \
