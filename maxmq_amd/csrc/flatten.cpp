@@ -519,9 +519,13 @@ int flatten(const Store &st, HostSnapshot *out) {
       if (c == kPHeavy) {
         hs.pinfo[nx] = make_uint2(kNone, kPInfoHeavy);
         heavy_at[nx] = 1;
-      } else if (c <= 2) {
+      } else if (c <= 2) {  // inline: sid | the partner's QoS << 28 | NoLocal << 30 (its packed word)
         const uint64_t o = partners.off[x];
-        hs.pinfo[nx] = make_uint2(new_sid[partners.part[o]], c == 2 ? new_sid[partners.part[o + 1]] : kNone);
+        auto inl = [&](uint32_t old) {
+          const uint32_t m = hs.subs[new_sid[old]].word;  // build-time meta (snapshot.h): qos[1:0], nl[2]
+          return new_sid[old] | (m & 3u) << 28 | ((m >> 2) & 1u) << 30;
+        };
+        hs.pinfo[nx] = make_uint2(inl(partners.part[o]), c == 2 ? inl(partners.part[o + 1]) : kNone);
       } else {
         hs.pinfo[nx] = make_uint2((uint32_t)hs.partners.size(), kPInfoList | c);
         for (uint64_t o = partners.off[x]; o < partners.off[x + 1]; o++) hs.partners.push_back(new_sid[partners.part[o]]);

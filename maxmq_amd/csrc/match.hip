@@ -1489,15 +1489,30 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_resolve(DeviceSnapshot s,
   const uint64_t glt = (1ull << gl) - 1ull;
   ResolveLds<kH> &L = lds_all[(threadIdx.x / kWave) * kGroups + g];
   const uint32_t ngroups = gridDim.x * kEmitWaves * kGroups, nl = *count;
-  for (uint32_t i = (blockIdx.x * kEmitWaves + threadIdx.x / kWave) * kGroups + g; i < nl; i += ngroups) {
-    const uint32_t t = list[i];
-    const uint64_t db = o.dstart[t];
-    // the record's tail: header + kH parts, unconditionally (inside the slot)
-    const uint4 *gt = rec_tail(o.recs, t);
+  // the next topic's list entry, segment start and record tail (header + kH
+  // parts, unconditionally: inside the record slot) load while this one resolves
+  constexpr int kUPer = (kUnits + kE - 1) / kE;
+  uint32_t t_n = 0;
+  uint64_t db_n = 0;
+  uint4 u_n[kUPer];
+  auto fetch = [&](uint32_t k) {
+    t_n = list[k];
+    db_n = o.dstart[t_n];
+    const uint4 *gt = rec_tail(o.recs, t_n);
+#pragma unroll
+    for (int v = 0; v < kUPer; v++)
+      if (v * kE + gl < kUnits) u_n[v] = gt[-(v * kE + gl)];
+  };
+  uint32_t i = (blockIdx.x * kEmitWaves + threadIdx.x / kWave) * kGroups + g;
+  if (i < nl) fetch(i);
+  for (; i < nl; i += ngroups) {
+    const uint32_t t = t_n;
+    const uint64_t db = db_n;
     uint4 *rec4 = reinterpret_cast<uint4 *>(L.rec);
 #pragma unroll
-    for (int u0 = 0; u0 < kUnits; u0 += kE)
-      if (u0 + gl < kUnits) rec4[u0 + gl] = gt[-(u0 + gl)];
+    for (int v = 0; v < kUPer; v++)
+      if (v * kE + gl < kUnits) rec4[v * kE + gl] = u_n[v];
+    if (i + ngroups < nl) fetch(i + ngroups);
     wave_lds_sync();
     const uint32_t nh = L.rec[0] & 0xFFu, Ss = L.rec[1], M = L.rec[2];
     for (uint32_t h = gl; h < nh; h += kE) {  // rank sort by range start (ranges are disjoint)
@@ -1541,10 +1556,12 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_resolve(DeviceSnapshot s,
         const uint32_t q = q0 + k * kE + gl;
         bool win = q < M;
         uint32_t qb = qos_bits(wd[k]);
-        auto meet = [&](uint32_t p) {
+        // a partner: its sid | QoS << 28 | NoLocal << 30 (its packed word)
+        auto meet = [&](uint32_t pw) {
+          const uint32_t p = pw & kWordSidMask;
           uint32_t rp;
           if (!gathered(p, &rp)) return;
-          qb |= qos_bits(s.words[p]);
+          qb |= qos_bits(pw);
           if (rp < rk[k] || (rp == rk[k] && p < sid[k])) win = false;
         };
         if (win) {
@@ -1552,7 +1569,7 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_resolve(DeviceSnapshot s,
             atomicOr(&o.ctr->oob, 1u);
           } else if (pi[k].y != kNone && (pi[k].y & kPInfoList)) {  // (kNone: one inline partner)
             const uint32_t c = pi[k].y & 0xFFu;
-            for (uint32_t j = 0; j < c; j++) meet(s.partners[pi[k].x + j]);
+            for (uint32_t j = 0; j < c; j++) meet(s.words[s.partners[pi[k].x + j]]);
           } else {
             if (pi[k].x != kNone) meet(pi[k].x);
             if (pi[k].y != kNone) meet(pi[k].y);

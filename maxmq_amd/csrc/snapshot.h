@@ -111,8 +111,9 @@ constexpr uint32_t kMaxSubs = 1u << kSidBits;
 // lists its partners — the other subscriptions of its client whose filters are
 // level-compatible with its own (flatten.cpp mark_multi), i.e. every entry it
 // can meet in one topic's gather (the parent-'#' double gather is gone:
-// kFlagParentLit).  {p0, p1} inline for one or two partners (kNone when
-// absent); {offset into partners, kPInfoList | count} for up to kMaxPartners;
+// kFlagParentLit).  {p0, p1} inline for one or two partners, each the
+// partner's packed word (sid | QoS << 28 | NoLocal << 30: no load for its
+// bits), kNone when absent; {offset into partners, kPInfoList | count} for up to kMaxPartners;
 // {kNone, kPInfoHeavy}: merged by hash table only (an inline second partner is
 // a sid < 2^28, so kPInfoList | count, kNone and kPInfoHeavy stay distinct).  A gathered entry whose
 // gathered partners all come later in the reference's order (rank, sid) is its
