@@ -1462,11 +1462,17 @@ __global__ __launch_bounds__(kBigThreads) void k_multi_part(DeviceSnapshot s, Ou
 // (packets.go:250-270) without a table.  Winners are written after the
 // topic's solo deliveries in entry order (deterministic).
 // ---------------------------------------------------------------------------
-// MQM_NO_RESOLVE=1 (A/B, read at every batch so a test can compare both in
-// one process): every topic with multi entries merges by hash table
+// MQM_RESOLVE=1 / 0 (read at every batch so a test can compare both in one
+// process; MQM_NO_RESOLVE=1 = MQM_RESOLVE=0): light topics merge by
+// resolution / every topic with multi entries merges by hash table.  Default:
+// kResolveDefault (on C3 the hash-table tiers measured faster, profiles/r03)
+#ifndef MQM_RESOLVE_DEFAULT
+#define MQM_RESOLVE_DEFAULT 0
+#endif
 static bool resolve_on() {
-  const char *v = getenv("MQM_NO_RESOLVE");
-  return !v || atoi(v) == 0;
+  if (const char *v = getenv("MQM_RESOLVE")) return atoi(v) != 0;
+  if (const char *v = getenv("MQM_NO_RESOLVE")) return atoi(v) == 0;
+  return MQM_RESOLVE_DEFAULT != 0;
 }
 
 template <int kH>

@@ -65,11 +65,11 @@ for step in "$@"; do
              python3 profiles/pmc_to_traffic.py $OUT/pmc > $OUT/traffic.json ;;
     pipe) for P in 2 3; do timeout -k 10 400 python3 -u bench.py $FAST --pipeline $P > $OUT/bench_fast_pipe$P.json \
              2> $OUT/bench_fast_pipe$P.log || exit 1; done ;;
-    abr) for V in 0 1; do MQM_NO_RESOLVE=$V timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_nores$V.json \
-             2> $OUT/bench_fast_nores$V.log || exit 1; done ;;
-    c4ab) for V in 0 1; do MQM_NO_RESOLVE=$V timeout -k 10 600 python3 -u bench.py --config 4 --shard 0/8 $FAST \
-             > $OUT/bench_c4_fast_nores$V.json 2> $OUT/bench_c4_fast_nores$V.log || exit 1; done ;;
-    profres) (cd /tmp && export TMPDIR=/tmp MQM_NO_OVERLAP=1 && timeout -k 10 500 rocprofv3 --kernel-trace --stats \
+    abr) for V in 1 0; do MQM_RESOLVE=$V timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_res$V.json \
+             2> $OUT/bench_fast_res$V.log || exit 1; done ;;
+    c4ab) for V in 1 0; do MQM_RESOLVE=$V timeout -k 10 600 python3 -u bench.py --config 4 --shard 0/8 $FAST \
+             > $OUT/bench_c4_fast_res$V.json 2> $OUT/bench_c4_fast_res$V.log || exit 1; done ;;
+    profres) (cd /tmp && export TMPDIR=/tmp MQM_NO_OVERLAP=1 MQM_RESOLVE=1 && timeout -k 10 500 rocprofv3 --kernel-trace --stats \
              --output-format csv -d $OUT/profres -o prof -- python3 $ROOT/bench.py $FAST \
              > $OUT/bench_under_rocprof_res.json 2> $OUT/rocprof_res.log) ;;
     par) timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_gpu_queued.py -m gpu --timeout 300 \
