@@ -512,6 +512,17 @@ int flatten(const Store &st, HostSnapshot *out) {
     hs.pinfo.assign(nsub, make_uint2(0, 0));
     hs.partners.clear();
     std::vector<uint8_t> heavy_at(nsub, 0);
+    // a partner is known by the multi-tail start of its node's range (where
+    // the walk's multi part of that range starts, whichever probe gathered it)
+    std::vector<uint32_t> tail_of(nsub, 0);
+    for (uint64_t i = 0; i < nn; i++) {
+      const uint32_t off = hs.nodes[i].sub_off, cnt = hs.nodes[i].sub_cnt;
+      for (uint32_t j = off + cnt - own_multi[i]; j < off + cnt; j++) tail_of[j] = off + cnt - own_multi[i];
+    }
+    auto pkey = [&](uint32_t old) {
+      const uint32_t p = new_sid[old], m = hs.subs[p].word;  // build-time meta (snapshot.h): qos[1:0], nl[2]
+      return tail_of[p] | (m & 3u) << 28 | ((m >> 2) & 1u) << 30;
+    };
     for (uint64_t x = 0; x < nsub; x++) {
       const uint16_t c = partners.cnt[x];
       if (c == 0) continue;
@@ -519,16 +530,12 @@ int flatten(const Store &st, HostSnapshot *out) {
       if (c == kPHeavy) {
         hs.pinfo[nx] = make_uint2(kNone, kPInfoHeavy);
         heavy_at[nx] = 1;
-      } else if (c <= 2) {  // inline: sid | the partner's QoS << 28 | NoLocal << 30 (its packed word)
+      } else if (c <= 2) {  // inline: the partner's key | QoS << 28 | NoLocal << 30
         const uint64_t o = partners.off[x];
-        auto inl = [&](uint32_t old) {
-          const uint32_t m = hs.subs[new_sid[old]].word;  // build-time meta (snapshot.h): qos[1:0], nl[2]
-          return new_sid[old] | (m & 3u) << 28 | ((m >> 2) & 1u) << 30;
-        };
-        hs.pinfo[nx] = make_uint2(inl(partners.part[o]), c == 2 ? inl(partners.part[o + 1]) : kNone);
+        hs.pinfo[nx] = make_uint2(pkey(partners.part[o]), c == 2 ? pkey(partners.part[o + 1]) : kNone);
       } else {
         hs.pinfo[nx] = make_uint2((uint32_t)hs.partners.size(), kPInfoList | c);
-        for (uint64_t o = partners.off[x]; o < partners.off[x + 1]; o++) hs.partners.push_back(new_sid[partners.part[o]]);
+        for (uint64_t o = partners.off[x]; o < partners.off[x + 1]; o++) hs.partners.push_back(pkey(partners.part[o]));
       }
     }
     // a node whose range (multi tail) holds a heavy entry: its topics merge by hash table

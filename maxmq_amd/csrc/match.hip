@@ -1452,12 +1452,12 @@ __global__ __launch_bounds__(kBigThreads) void k_multi_part(DeviceSnapshot s, Ou
 // whose multi entries are all light (no kClsHeavy): kE lanes per topic (8 for
 // topics with <= kSmallMultiS entries and <= kSmallHits multi parts, 64
 // otherwise), no table, no atomics.  The topic's multi parts (the walk's
-// record: range start, count, hit rank) are sorted by range start in LDS;
-// every multi entry reads its packed word and its partners, looks each
-// partner up among the gathered ranges (binary search: a partner is gathered
-// iff its sid lies in one of them, since it is a multi entry itself and sits in
-// its range's multi tail), and is its client's delivery iff no gathered
-// partner comes first in the reference's order (rank, sid) — the winner folds
+// record: multi-tail start, count, hit rank) go into a small LDS hash by
+// multi-tail start; every multi entry reads its packed word and its partners
+// (each encoded as the multi-tail start of its node's range, which is where a
+// gathered partner's part starts, with its QoS / NoLocal bits) and is its
+// client's delivery iff no gathered partner has a lower hit rank (the
+// reference's emission order; partners sit on other nodes) — the winner folds
 // the gathered partners' QoS / NoLocal in: Subscription.Merge
 // (packets.go:250-270) without a table.  Winners are written after the
 // topic's solo deliveries in entry order (deterministic).
@@ -1478,7 +1478,7 @@ static bool resolve_on() {
 template <int kH>
 struct alignas(16) ResolveLds {
   uint32_t rec[4 + kRecHit * kH];  // header + multi parts (the record's tail, in the walk's order)
-  uint32_t sk[kH], se[kH], sr[kH]; // the parts by range start: start, end, rank
+  uint32_t key[2 * kH], rank[2 * kH];  // gathered multi parts by multi-tail start + 1 (0: empty) -> hit rank
 };
 
 template <int kE, int kH, int kPer>
@@ -1488,13 +1488,15 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_resolve(DeviceSnapshot s,
   constexpr int kGroups = kWave / kE;
   constexpr uint64_t kGMask = kE == 64 ? ~0ull : (1ull << kE) - 1ull;
   constexpr int kUnits = 1 + kH;  // record units (16 B) read per topic
-  static_assert(kH <= kHCap && kUnits <= kRecStrideAlloc / 4, "record tail");
+  constexpr uint32_t kT = 2 * kH, kTBits = kH == 64 ? 7 : kH == 32 ? 6 : kH == 16 ? 5 : 4;
+  static_assert(kH <= kHCap && kUnits <= kRecStrideAlloc / 4 && (1u << kTBits) == kT, "record tail / table");
   __shared__ ResolveLds<kH> lds_all[kEmitWaves * kGroups];
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / kE, gl = lane % kE, gbase = g * kE;
   const uint64_t glt = (1ull << gl) - 1ull;
   ResolveLds<kH> &L = lds_all[(threadIdx.x / kWave) * kGroups + g];
   const uint32_t ngroups = gridDim.x * kEmitWaves * kGroups, nl = *count;
+  auto tslot = [](uint32_t k) { return (k * 2654435769u) >> (32 - kTBits); };
   // the next topic's list entry, segment start and record tail (header + kH
   // parts, unconditionally: inside the record slot) load while this one resolves
   constexpr int kUPer = (kUnits + kE - 1) / kE;
@@ -1518,32 +1520,21 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_resolve(DeviceSnapshot s,
 #pragma unroll
     for (int v = 0; v < kUPer; v++)
       if (v * kE + gl < kUnits) rec4[v * kE + gl] = u_n[v];
+    for (uint32_t j = gl; j < kT; j += kE) L.key[j] = 0;
     if (i + ngroups < nl) fetch(i + ngroups);
     wave_lds_sync();
     const uint32_t nh = L.rec[0] & 0xFFu, Ss = L.rec[1], M = L.rec[2];
-    for (uint32_t h = gl; h < nh; h += kE) {  // rank sort by range start (ranges are disjoint)
-      const uint32_t mo = rec_at(L.rec, h, kFieldOff), mc = rec_at(L.rec, h, kFieldMpre);
-      uint32_t r = 0;
-      for (uint32_t j = 0; j < nh; j++) r += rec_at(L.rec, j, kFieldOff) < mo ? 1u : 0u;
-      L.sk[r] = mo;
-      L.se[r] = mo + mc;
-      L.sr[r] = rec_at(L.rec, h, kFieldRank);
+    // the gathered multi parts by their range's multi-tail start (a node's
+    // range is gathered at most once per topic: distinct keys)
+    for (uint32_t h = gl; h < nh; h += kE) {
+      const uint32_t k = rec_at(L.rec, h, kFieldOff) + 1u;
+      uint32_t sl = tslot(k);
+      while (atomicCAS(&L.key[sl], 0u, k) != 0u) sl = (sl + 1) & (kT - 1);
+      L.rank[sl] = rec_at(L.rec, h, kFieldRank);
     }
     wave_lds_sync();
     rec_prefix<kE, kH>(L.rec, nh, gl);  // part counts -> exclusive prefixes (multi_sid)
     wave_lds_sync();
-    // the gathered rank of sid p (false: p's range is not gathered)
-    auto gathered = [&](uint32_t p, uint32_t *rank) {
-      uint32_t j = 0;
-#pragma unroll
-      for (uint32_t step = kH / 2; step > 0; step >>= 1) {
-        const uint32_t c = j + step;
-        j = (c < nh && L.sk[c < nh ? c : 0] <= p) ? c : j;
-      }
-      const bool in = nh > 0 && L.sk[j] <= p && p < L.se[j];
-      *rank = in ? L.sr[j] : 0;
-      return in;
-    };
     uint32_t D = 0;
     for (uint32_t q0 = 0; q0 < M; q0 += kE * kPer) {
       uint32_t sid[kPer], rk[kPer], wd[kPer];
@@ -1562,20 +1553,23 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_resolve(DeviceSnapshot s,
         const uint32_t q = q0 + k * kE + gl;
         bool win = q < M;
         uint32_t qb = qos_bits(wd[k]);
-        // a partner: its sid | QoS << 28 | NoLocal << 30 (its packed word)
+        // a partner: its range's multi-tail start | QoS << 28 | NoLocal << 30;
+        // gathered iff that range is one of the topic's multi parts (its own
+        // node differs from this entry's, so its hit rank does too)
         auto meet = [&](uint32_t pw) {
-          const uint32_t p = pw & kWordSidMask;
-          uint32_t rp;
-          if (!gathered(p, &rp)) return;
+          const uint32_t key = (pw & kWordSidMask) + 1u;
+          uint32_t sl = tslot(key), kk;
+          while ((kk = L.key[sl]) != 0u && kk != key) sl = (sl + 1) & (kT - 1);
+          if (kk != key) return;
           qb |= qos_bits(pw);
-          if (rp < rk[k] || (rp == rk[k] && p < sid[k])) win = false;
+          if (L.rank[sl] < rk[k]) win = false;
         };
         if (win) {
           if (pi[k].y == kPInfoHeavy) {  // routed here by mistake: never expected (kClsHeavy)
             atomicOr(&o.ctr->oob, 1u);
           } else if (pi[k].y != kNone && (pi[k].y & kPInfoList)) {  // (kNone: one inline partner)
             const uint32_t c = pi[k].y & 0xFFu;
-            for (uint32_t j = 0; j < c; j++) meet(s.words[s.partners[pi[k].x + j]]);
+            for (uint32_t j = 0; j < c; j++) meet(s.partners[pi[k].x + j]);
           } else {
             if (pi[k].x != kNone) meet(pi[k].x);
             if (pi[k].y != kNone) meet(pi[k].y);

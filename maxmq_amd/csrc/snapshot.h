@@ -111,15 +111,17 @@ constexpr uint32_t kMaxSubs = 1u << kSidBits;
 // lists its partners — the other subscriptions of its client whose filters are
 // level-compatible with its own (flatten.cpp mark_multi), i.e. every entry it
 // can meet in one topic's gather (the parent-'#' double gather is gone:
-// kFlagParentLit).  {p0, p1} inline for one or two partners, each the
-// partner's packed word (sid | QoS << 28 | NoLocal << 30: no load for its
-// bits), kNone when absent; {offset into partners, kPInfoList | count} for up to kMaxPartners;
-// {kNone, kPInfoHeavy}: merged by hash table only (an inline second partner is
-// a sid < 2^28, so kPInfoList | count, kNone and kPInfoHeavy stay distinct).  A gathered entry whose
-// gathered partners all come later in the reference's order (rank, sid) is its
-// client's first-merged entry and writes the delivery with every gathered
+// kFlagParentLit).  A partner is encoded as the multi-tail start of its
+// node's range (the range start of the walk's multi part when that range is
+// gathered) | QoS << 28 | NoLocal << 30: {p0, p1} inline for one or two
+// partners, kNone when absent; {offset into partners, kPInfoList | count} for up to kMaxPartners;
+// {kNone, kPInfoHeavy}: merged by hash table only (an inline partner has bit 31
+// clear, so kPInfoList | count, kNone and kPInfoHeavy stay distinct).  A
+// gathered entry whose gathered partners all come later in the reference's
+// order (hit rank) is its client's first-merged entry and writes the delivery with every gathered
 // partner's QoS / NoLocal folded in (packets.go:250-270); the others write
-// nothing.  Solo entries: {0, 0} (unused).
+// nothing (partners sit on other nodes than the entry, so their hit ranks
+// differ from its own).  Solo entries: {0, 0} (unused).
 constexpr uint32_t kPInfoList = 0x80000000u, kPInfoHeavy = 0xFFFFFFFEu;
 constexpr uint32_t kMaxPartners = 15;
 

@@ -17,6 +17,7 @@
 #   par     : the parity and queued-call GPU tests only
 #   c4ab    : the C4 shard bench with merge by resolution on / off
 #   profres : serial rocprof kernel stats of `fast` (merge by resolution on)
+#   parres  : `par` with the merge by resolution on (MQM_RESOLVE=1)
 #   smoke   : __graft_entry__.smoke()
 #   bench   : the default bench line (C3)                -> gpurun_out/TAG/bench.json
 #   fast    : bench without CPU baseline / host path      -> gpurun_out/TAG/bench_fast.json
@@ -72,6 +73,8 @@ for step in "$@"; do
     profres) (cd /tmp && export TMPDIR=/tmp MQM_NO_OVERLAP=1 MQM_RESOLVE=1 && timeout -k 10 500 rocprofv3 --kernel-trace --stats \
              --output-format csv -d $OUT/profres -o prof -- python3 $ROOT/bench.py $FAST \
              > $OUT/bench_under_rocprof_res.json 2> $OUT/rocprof_res.log) ;;
+    parres) MQM_RESOLVE=1 timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_gpu_queued.py -m gpu --timeout 300 \
+             > $OUT/pytest_parres.log 2>&1 ;;
     par) timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_gpu_queued.py -m gpu --timeout 300 \
              > $OUT/pytest_par.log 2>&1 ;;
     abq) for V in 1 0; do MQM_QUEUED=$V timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_q$V.json \
