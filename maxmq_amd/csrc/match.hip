@@ -1462,17 +1462,22 @@ __global__ __launch_bounds__(kBigThreads) void k_multi_part(DeviceSnapshot s, Ou
 // (packets.go:250-270) without a table.  Winners are written after the
 // topic's solo deliveries in entry order (deterministic).
 // ---------------------------------------------------------------------------
-// MQM_RESOLVE=1 / 0 (read at every batch so a test can compare both in one
-// process; MQM_NO_RESOLVE=1 = MQM_RESOLVE=0): light topics merge by
-// resolution / every topic with multi entries merges by hash table.  Default:
-// kResolveDefault (on C3 the hash-table tiers measured faster, profiles/r03)
-#ifndef MQM_RESOLVE_DEFAULT
-#define MQM_RESOLVE_DEFAULT 0
+// Which light topics merge by resolution: those with at least this many multi
+// entries (the rest, and every heavy topic, by hash table).  Measured
+// (profiles/r03/r03m): resolution wins on wide topics (C4 shard, ~1000 multi
+// entries per topic: emission 33.1 -> 23.5 ms) and loses on many small ones
+// (C3: 8.1 -> 10.8 ms), so by default it takes the topics past the 1024-slot
+// table tier.  Read at every batch (a test compares modes in one process):
+// MQM_RESOLVE=1 every light topic, MQM_RESOLVE=0 none (= MQM_NO_RESOLVE=1),
+// MQM_RESOLVE_MIN=m the threshold.
+#ifndef MQM_RESOLVE_MIN_DEFAULT
+#define MQM_RESOLVE_MIN_DEFAULT 769u
 #endif
-static bool resolve_on() {
-  if (const char *v = getenv("MQM_RESOLVE")) return atoi(v) != 0;
-  if (const char *v = getenv("MQM_NO_RESOLVE")) return atoi(v) == 0;
-  return MQM_RESOLVE_DEFAULT != 0;
+static uint32_t resolve_min() {
+  if (const char *v = getenv("MQM_RESOLVE")) return atoi(v) != 0 ? 1u : 0xFFFFFFFFu;
+  if (const char *v = getenv("MQM_NO_RESOLVE")) return atoi(v) == 0 ? 1u : 0xFFFFFFFFu;
+  if (const char *v = getenv("MQM_RESOLVE_MIN")) return (uint32_t)std::max(1L, atol(v));
+  return MQM_RESOLVE_MIN_DEFAULT;
 }
 
 template <int kH>
@@ -1967,11 +1972,11 @@ struct Lists {
 
 // the merge list of a topic with multi entries (by their count m), and the
 // shared-candidate list
-__device__ __forceinline__ uint32_t route_mask(uint8_t c, uint32_t m, uint32_t h, bool resolve) {
+__device__ __forceinline__ uint32_t route_mask(uint8_t c, uint32_t m, uint32_t h, uint32_t res_min) {
   if (!(c & kClsBounded)) return 0;
   const uint32_t sh = h ? (1u << kLShared) : 0u;
   if (m == 0) return sh;
-  if (resolve && !(c & kClsHeavy))  // merge by resolution (k_resolve)
+  if (m >= res_min && !(c & kClsHeavy))  // merge by resolution (k_resolve)
     return sh | (((c & kClsFewHits) && m <= kSmallMultiS) ? (1u << kLResSmall) : (1u << kLRes));
   if ((c & kClsFewHits) && m <= kSmallMultiS) return sh | (1u << kLSmall);
   return sh | (m <= kSmallMulti ? (1u << kLWave)
@@ -1984,7 +1989,7 @@ __device__ __forceinline__ uint32_t route_mask(uint8_t c, uint32_t m, uint32_t h
 __global__ __launch_bounds__(256) void k_route(const uint8_t *__restrict__ cls, const uint32_t *__restrict__ mcount,
                                                const uint32_t *__restrict__ hcount, uint32_t n, Lists L,
                                                unsigned int *__restrict__ counts,
-                                               unsigned long long *__restrict__ msum, int resolve) {
+                                               unsigned long long *__restrict__ msum, uint32_t res_min) {
   __shared__ unsigned int lc[kNLists], base[kNLists];
   __shared__ unsigned long long ms[3];
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
@@ -1995,7 +2000,7 @@ __global__ __launch_bounds__(256) void k_route(const uint8_t *__restrict__ cls, 
   __syncthreads();
   for (uint32_t t0 = lo; t0 < hi; t0 += blockDim.x) {
     const uint32_t t = t0 + tid;
-    const uint32_t r = t < hi ? route_mask(cls[t], mcount[t], hcount[t], resolve != 0) : 0;
+    const uint32_t r = t < hi ? route_mask(cls[t], mcount[t], hcount[t], res_min) : 0;
 #pragma unroll
     for (int l = 0; l < kNLists; l++) {
       const uint64_t m = __ballot((r >> l) & 1u);
@@ -2013,7 +2018,7 @@ __global__ __launch_bounds__(256) void k_route(const uint8_t *__restrict__ cls, 
   __syncthreads();
   for (uint32_t t0 = lo; t0 < hi; t0 += blockDim.x) {
     const uint32_t t = t0 + tid;
-    const uint32_t r = t < hi ? route_mask(cls[t], mcount[t], hcount[t], resolve != 0) : 0;
+    const uint32_t r = t < hi ? route_mask(cls[t], mcount[t], hcount[t], res_min) : 0;
 #pragma unroll
     for (int l = 0; l < kNLists; l++) {
       const bool in = (r >> l) & 1u;
@@ -2305,7 +2310,7 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
   unsigned int *lcount = &o.ctr->n_small;  // kNLists consecutive counters
   if (n > 0) {
     hipLaunchKernelGGL(k_route, dim3(std::min<uint32_t>((n + 4095) / 4096, 2048)), dim3(256), 0, st, o.cls, o.mcount,
-                       o.hcount, n, lists, lcount, o.ctr->m_sum, resolve_on() ? 1 : 0);
+                       o.hcount, n, lists, lcount, o.ctr->m_sum, resolve_min());
     HIP_TRY(hipGetLastError());
   }
   hipLaunchKernelGGL(k_totals, dim3(1), dim3(64), 0, st, o.ctr, o.dstart, o.hstart, desc_start, n);

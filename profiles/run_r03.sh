@@ -18,6 +18,7 @@
 #   c4ab    : the C4 shard bench with merge by resolution on / off
 #   profres : serial rocprof kernel stats of `fast` (merge by resolution on)
 #   parres  : `par` with the merge by resolution on (MQM_RESOLVE=1)
+#   abmin   : C3 and C4-shard `fast` with resolution from 193 multi entries (default 769)
 #   smoke   : __graft_entry__.smoke()
 #   bench   : the default bench line (C3)                -> gpurun_out/TAG/bench.json
 #   fast    : bench without CPU baseline / host path      -> gpurun_out/TAG/bench_fast.json
@@ -75,6 +76,9 @@ for step in "$@"; do
              > $OUT/bench_under_rocprof_res.json 2> $OUT/rocprof_res.log) ;;
     parres) MQM_RESOLVE=1 timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_gpu_queued.py -m gpu --timeout 300 \
              > $OUT/pytest_parres.log 2>&1 ;;
+    abmin) MQM_RESOLVE_MIN=193 timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_min193.json \
+             2> $OUT/bench_fast_min193.log && MQM_RESOLVE_MIN=193 timeout -k 10 600 python3 -u bench.py --config 4 \
+             --shard 0/8 $FAST > $OUT/bench_c4_fast_min193.json 2> $OUT/bench_c4_fast_min193.log ;;
     par) timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_gpu_queued.py -m gpu --timeout 300 \
              > $OUT/pytest_par.log 2>&1 ;;
     abq) for V in 1 0; do MQM_QUEUED=$V timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_q$V.json \
