@@ -1466,12 +1466,13 @@ __global__ __launch_bounds__(kBigThreads) void k_multi_part(DeviceSnapshot s, Ou
 // entries (the rest, and every heavy topic, by hash table).  Measured
 // (profiles/r03/r03m): resolution wins on wide topics (C4 shard, ~1000 multi
 // entries per topic: emission 33.1 -> 23.5 ms) and loses on many small ones
-// (C3: 8.1 -> 10.8 ms), so by default it takes the topics past the 1024-slot
-// table tier.  Read at every batch (a test compares modes in one process):
+// (C3: 8.1 -> 10.8 ms), so by default it takes the topics past the wave-table
+// tier (> 192 entries: r03n, C3 14.35 vs 14.48 ms and C4 shard 28.24 vs 28.80
+// ms against a threshold of 769).  Read at every batch (a test compares modes in one process):
 // MQM_RESOLVE=1 every light topic, MQM_RESOLVE=0 none (= MQM_NO_RESOLVE=1),
 // MQM_RESOLVE_MIN=m the threshold.
 #ifndef MQM_RESOLVE_MIN_DEFAULT
-#define MQM_RESOLVE_MIN_DEFAULT 769u
+#define MQM_RESOLVE_MIN_DEFAULT 193u
 #endif
 static uint32_t resolve_min() {
   if (const char *v = getenv("MQM_RESOLVE")) return atoi(v) != 0 ? 1u : 0xFFFFFFFFu;
