@@ -19,7 +19,7 @@ import os
 import re
 import sys
 
-GATHER = ("k_walk", "k_merge_small", "k_merge", "k_multi", "k_multi_part", "k_dfs", "k_shared",
+GATHER = ("k_walk", "k_merge_small", "k_merge", "k_multi", "k_multi_part", "k_resolve", "k_dfs", "k_shared",
           "k_level")  # (reverse match: k_level walks the trie and the edge index)
 STREAM = ("k_desc", "k_winmap", "k_wincopy", "k_route", "k_table_sizes",
           "k_flt_count", "k_flt_fill", "k_emit_count", "k_emit_place", "k_task_copy")
@@ -31,7 +31,7 @@ def kname(s):
     m = re.match(r"(?:void )?(?:mqm::\(anonymous namespace\)::)?(k_\w+)(?:<(\d+)[,>])?", s)
     if not m:
         return None
-    return m.group(1) + (m.group(2) if m.group(1) == "k_multi" and m.group(2) else "")
+    return m.group(1) + (m.group(2) if m.group(1) in ("k_multi", "k_resolve") and m.group(2) else "")
 
 
 def base(k):
