@@ -1131,11 +1131,13 @@ namespace {
 // context to the pool.  With a topic past the small-batch path's capacities
 // the worker runs mqm_match_batch and splits the result.
 struct Collector {
+  struct Req;
   struct Batch {  // one small-batch call, shared by its callers until they have copied their results
     mqm_index *h = nullptr;
     std::unique_ptr<MatchCtx> ctx;
     std::shared_ptr<GpuSnapshot> snap;
     FastOutput fo;
+    std::vector<Req *> reqs;  // the callers, for the wake tree (submit)
     std::atomic<uint32_t> refs{0};
     void release() {
       if (refs.fetch_sub(1, std::memory_order_acq_rel) == 1) {
@@ -1193,6 +1195,11 @@ struct Collector {
     cv.notify_one();
     r.wait();
     if (r.batch) {  // the small-batch path: this caller's topic, copied off the batch's blocks
+      // a wake tree: the worker wakes the first caller, caller i wakes 2i+1 and
+      // 2i+2, so a batch's wake syscalls run on many threads instead of one
+      // after another on the worker (each FUTEX_WAKE of a sleeper costs us)
+      const auto &rq = r.batch->reqs;
+      for (size_t c = 2 * (size_t)r.index + 1; c <= 2 * (size_t)r.index + 2 && c < rq.size(); c++) rq[c]->wake();
       const FastOutput &fo = r.batch->fo;
       const FastRec &x = fo.recs[r.index];
       try {
@@ -1305,8 +1312,9 @@ struct Collector {
         for (uint32_t i = 0; i < batch.size(); i++) {
           batch[i]->batch = fb;
           batch[i]->index = i;
-          batch[i]->wake();
         }
+        fb->reqs = batch;
+        batch[0]->wake();  // the rest through the wake tree (submit)
         continue;
       }
       mqm_result *b = nullptr;
