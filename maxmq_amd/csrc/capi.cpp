@@ -1169,6 +1169,7 @@ struct Collector {
   std::vector<Req *> q;
   bool stop = false;
   uint32_t max_batch = 8192, linger_us = 0;
+  const bool wake_tree = getenv("MQM_WAKE_TREE") && atoi(getenv("MQM_WAKE_TREE")) != 0;
   uint64_t batches = 0, topics = 0;
   std::vector<std::thread> ths;
 
@@ -1198,8 +1199,10 @@ struct Collector {
       // a wake tree: the worker wakes the first caller, caller i wakes 2i+1 and
       // 2i+2, so a batch's wake syscalls run on many threads instead of one
       // after another on the worker (each FUTEX_WAKE of a sleeper costs us)
+      // (MQM_WAKE_TREE=1; off by default until measured on the GPU box)
       const auto &rq = r.batch->reqs;
-      for (size_t c = 2 * (size_t)r.index + 1; c <= 2 * (size_t)r.index + 2 && c < rq.size(); c++) rq[c]->wake();
+      if (wake_tree)
+        for (size_t c = 2 * (size_t)r.index + 1; c <= 2 * (size_t)r.index + 2 && c < rq.size(); c++) rq[c]->wake();
       const FastOutput &fo = r.batch->fo;
       const FastRec &x = fo.recs[r.index];
       try {
@@ -1313,8 +1316,12 @@ struct Collector {
           batch[i]->batch = fb;
           batch[i]->index = i;
         }
-        fb->reqs = batch;
-        batch[0]->wake();  // the rest through the wake tree (submit)
+        if (wake_tree) {
+          fb->reqs = batch;
+          batch[0]->wake();  // the rest through the wake tree (submit)
+        } else {
+          for (Req *r : batch) r->wake();
+        }
         continue;
       }
       mqm_result *b = nullptr;

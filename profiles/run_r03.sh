@@ -93,7 +93,7 @@ for step in "$@"; do
              --warmup 1 --no-cpu-baseline --host-topics 0 --latency-topics 0 --steady-steps 0 \
              > $OUT/c4_under_rocprof_serial.json 2> $OUT/rocprof_c4ser.log) ;;
     latab) LAT="--steps 1 --warmup 0 --no-cpu-baseline --host-topics 0 --steady-steps 0"
-             for V in "MQM_BASE=1" "MQM_FAST_POLL=60" "MQM_BATCH_WORKERS=2" "MQM_BATCH_WORKERS=6"; do
+             for V in "MQM_BASE=1" "MQM_WAKE_TREE=1" "MQM_BATCH_WORKERS=6"; do
              env $V timeout -k 10 400 python3 -u bench.py $LAT > $OUT/bench_lat_${V//=/_}.json 2> $OUT/bench_lat_${V//=/_}.log || exit 1; done ;;
     calib) timeout -k 10 120 tools/_build/calib_fetch > $OUT/calib_kernels.txt 2>&1 ;;
     smoke) timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 ;;
