@@ -79,6 +79,8 @@ for step in "$@"; do
     abmin) MQM_RESOLVE_MIN=193 timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_min193.json \
              2> $OUT/bench_fast_min193.log && MQM_RESOLVE_MIN=193 timeout -k 10 600 python3 -u bench.py --config 4 \
              --shard 0/8 $FAST > $OUT/bench_c4_fast_min193.json 2> $OUT/bench_c4_fast_min193.log ;;
+    fasttw) MQM_WAKE_TREE=1 timeout -k 10 500 $PYT tests/test_gpu_batching.py tests/test_gpu_shim.py -m gpu \
+             --timeout 200 > $OUT/pytest_fast_wake.log 2>&1 ;;
     par) timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_gpu_queued.py -m gpu --timeout 300 \
              > $OUT/pytest_par.log 2>&1 ;;
     abq) for V in 1 0; do MQM_QUEUED=$V timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_q$V.json \
