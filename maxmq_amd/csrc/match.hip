@@ -158,7 +158,10 @@ static_assert(kSmallMulti % kWave == 0, "register tiles");
 // kItemLitB: a literal probe checked against the edge-existence filter first.
 // MQM_BLOOM_PLUS_ONLY=1 gives that kind only to nodes with a '+' child (where
 // topic levels drawn for a wildcard make probes miss); other literal probes
-// then skip the filter's round trip
+// then skip the filter's round trip.  Both apply only with
+// MQM_WALK_PRECHECK=0: the default checks the filter when an item is pushed
+// and pushes positives as kItemLit (with MQM_NO_BLOOM=1, a snapshot without
+// the filter, every literal item is pushed unless the next level is '+' / '#')
 enum : uint32_t { kItemLit = 0, kItemPlus = 1, kItemHash = 2, kItemLitB = 3 };
 // MQM_WALK_PRECHECK=1: a frontier node's literal item is checked against the
 // filter when it is pushed (its load overlapping the pushing level's record
