@@ -3,8 +3,8 @@
 
 One "step" = one TopicsIndex.Subscribers pass (topics.go:484-555) of the HIP
 path over a batch of publish topics already resident in HBM, through the C ABI
-(mqm_match_device): tokenize -> walk -> dedupe -> CSR deliveries + shared
-candidates.  Workload (BASELINE.json `metric` is quoted "at 10M filters"):
+(mqm_match_device): tokenize -> walk (+ output reservation and solo copy) ->
+merges -> per-topic segments of deliveries + shared candidates.  Workload (BASELINE.json `metric` is quoted "at 10M filters"):
 configs[2], 10M wildcard-heavy filters (40% '+', 10% '#', topics Zipf(1.2)
 over filter rank), 10M-topic batch, synthetic (tools/mqgen, seed 0x4D510003).
 
@@ -87,7 +87,7 @@ def parse():
     ap.add_argument("--retained", type=int, default=50000000, help="reverse: retained topics")
     ap.add_argument("--sweep", default="",
                     help="tuning sweep before the measurement: ';'-separated variants of "
-                         "'ENV=V,ENV=V' (match.hip knobs, e.g. MQM_WALK_OCC=6); per-variant kernel ms to stderr")
+                         "'ENV=V,ENV=V' (runtime knobs, e.g. MQM_RESOLVE_MIN=769); per-variant kernel ms to stderr")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per emit launch (profiles/run_pmc.sh)")
     return ap.parse_args()
@@ -363,7 +363,7 @@ def main():
         big = int(r.n_big)
         why = dict(zip(["frontier", "hits", "levels", "shared_hits", "raw_entries"], list(r.fallback_why)))
         lists = {"resolve": int(r.n_resolve), "merge_small": int(r.n_merge_small), "merge_wave": int(r.n_merge_wave),
-                 "solo_ranges": int(r.n_solo_ranges), "group_merge": int(r.n_big), "tier2": int(r.n_tier2), "tier3": int(r.n_tier3),
+                 "solo_ranges": int(r.n_solo_ranges), "solo_deliveries": int(r.n_solo), "group_merge": int(r.n_big), "tier2": int(r.n_tier2), "tier3": int(r.n_tier3),
                  "multi_entries_by_tier": [int(x) for x in r.multi_entries]}
     torch.cuda.synchronize(dev)
     if dist:
@@ -417,7 +417,8 @@ def main():
             else:
                 short = argparse.Namespace(**dict(vars(args), cpu_seconds=min(args.cpu_seconds, 2.0)))
                 _, stats = cpu_baseline(w, short)
-        roof = roofline(stats, n, kms, args.traffic_json, dt * 1e3 / args.steps if pipe else None)
+        roof = roofline(stats, n, kms, args.traffic_json, dt * 1e3 / args.steps if pipe else None,
+                        n_solo=lists.get("solo_deliveries"))
         out = {
             "metric": "publish topics matched/sec (node) + matched deliveries/sec at 10M filters",
             "value": value,
@@ -1028,13 +1029,15 @@ def cores_note(single, threads, host):
     return out
 
 
-def roofline(stats, n, kms, traffic_json, step_ms=None):
+def roofline(stats, n, kms, traffic_json, step_ms=None, n_solo=None):
     """B = T + 8N + 8P + 8V + 8S + 8D algorithmic bytes per
     batch (per-topic counters of the oracle's walk over the CPU sample, scaled
     to the batch) over the device time of the whole match pipeline (k_walk,
     scans, k_emit<16|64>, k_multi, k_dfs: first to last kernel, HIP events on
-    the launch stream).  `stages` splits it: the walk moves T + 8N + 8P + 8V,
-    the emit stage 8S + 8D.  `traffic` = HBM bytes per batch of the same
+    the launch stream).  `stages` splits it by kernel: k_walk (HIP events
+    around it) moves T + 8N + 8P + 8V and the solo entries it copies as they
+    stand (8 B gathered + 8 B delivered each in the model: 16 x n_solo, the
+    count the GPU reports), the merges the rest of 8S + 8D.  `traffic` = HBM bytes per batch of the same
     kernels from rocprofv3 FETCH_SIZE / WRITE_SIZE (profiles/traffic.json from
     profiles/pmc_to_traffic.py over a profiles/run_pmc_r02.sh run, reads
     converted per access shape as tools/calib_fetch calibrated them).
@@ -1049,6 +1052,9 @@ def roofline(stats, n, kms, traffic_json, step_ms=None):
     walk_b = (stats["topic_bytes"] + 8 * k + 8 * stats["probes"] + 8 * stats["visits"]) / k * n
     emit_b = (8 * stats["gathered"] + 8 * stats["deliveries"]) / k * n
     bytes_per_launch = walk_b + emit_b
+    if n_solo:  # the walk's solo copy, out of the emission's share
+        walk_b += 16 * n_solo
+        emit_b -= 16 * n_solo
     achieved = bytes_per_launch / (total_ms * 1e-3) / 1e9
     traffic = walk_traffic = None
     if traffic_json and os.path.exists(traffic_json):
@@ -1066,13 +1072,13 @@ def roofline(stats, n, kms, traffic_json, step_ms=None):
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
             "algorithmic_bytes_per_topic": bytes_per_launch / n, "algorithmic_bytes_per_batch": bytes_per_launch,
-            "kernel": "match pipeline per batch: k_walk + scans + solo copy (k_desc, k_winmap, k_wincopy) "
+            "kernel": "match pipeline per batch: k_walk (walk + output reservation + solo copy) + scan + k_route "
                       "+ merges (k_resolve; heavy topics k_merge_small, k_merge, k_multi) (+ k_dfs)",
             "time_basis": ("ms per pipelined step (batches overlap)" if step_ms else
                            "device time of one batch (HIP events, first to last kernel)"),
             "ms": total_ms, "isolated_batch_ms": kms["total"],
             "stages": {"walk": dict(stage(walk_b, kms["walk"]), traffic=walk_traffic),
-                       "emit": stage(emit_b, kms["dedupe"])}}
+                       "merge": stage(emit_b, kms["dedupe"])}}
 
 
 if __name__ == "__main__":

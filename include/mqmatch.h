@@ -136,11 +136,12 @@ typedef struct {
                                      hits, cached levels, shared hits, raw entries */
   uint32_t n_merge_small;         /* topics whose <= 24 multi entries an 8-lane group merged */
   uint32_t n_merge_wave;          /* topics whose <= 192 multi entries a wavefront merged */
-  uint64_t n_solo_ranges;         /* solo copy ranges (hits with solo entries)    */
+  uint64_t n_solo_ranges;         /* solo parts the walk copied (hits with solo entries) */
   uint32_t n_tier2, n_tier3;      /* topics the workgroup merge passed to its 2nd / 3rd tier */
   uint64_t multi_entries[3];      /* multi entries merged by the workgroup tiers 1 / 2 / 3 */
   uint32_t n_part;                /* tier-3 topics merged in client-hash partitions (> 3072 multi entries) */
   uint32_t n_resolve;             /* topics merged by resolution (partner lists, no table) */
+  uint64_t n_solo;                /* deliveries the walk copied as they stand (solo entries) */
 } mqm_device_result;
 
 /* ---- lifecycle: NewTopicsIndex (topics.go:291-299) ---------------------- */
@@ -268,7 +269,9 @@ int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t 
  * valid until the wait returns.  One batch in flight per context (a second
  * async call before the wait: MQM_EINVAL); contexts are independent, so
  * batches on different contexts and streams overlap.  The snapshot a batch
- * reads is the published one when it was queued. */
+ * reads is the published one when it was queued.  A context reads its index:
+ * destroy every context before the index (mqm_destroy returns MQM_EINVAL
+ * while any is alive and leaves the index intact). */
 typedef struct mqm_match_ctx mqm_match_ctx;
 int mqm_match_ctx_create(mqm_index *h, mqm_match_ctx **out);
 int mqm_match_ctx_destroy(mqm_match_ctx *ctx);

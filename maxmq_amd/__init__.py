@@ -22,6 +22,7 @@ host store (mutation semantics) and raises on matching.
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -218,6 +219,7 @@ class TopicsIndex:
         check("mqm_create", L.mqm_create(C.byref(cfg), C.byref(h)))
         self._h = h
         self.device = device
+        self._ctxs = weakref.WeakSet()  # live MatchContexts (destroyed before the index)
 
     def batching_policy(self, max_batch: int = 0, linger_us: int = 0):
         check("mqm_batching_policy", lib().mqm_batching_policy(self._h, max_batch, linger_us))
@@ -230,7 +232,9 @@ class TopicsIndex:
 
     def close(self):
         if getattr(self, "_h", None):
-            lib().mqm_destroy(self._h)
+            for c in list(getattr(self, "_ctxs", ())):  # mqm_destroy refuses while a context lives
+                c.close()
+            check("mqm_destroy", lib().mqm_destroy(self._h))
             self._h = None
 
     def __del__(self):
@@ -457,7 +461,9 @@ class TopicsIndex:
 
     def match_context(self) -> "MatchContext":
         """A context of the queued device API (several batches in flight)."""
-        return MatchContext(self)
+        c = MatchContext(self)
+        self._ctxs.add(c)
+        return c
 
     def match_device(self, d_bytes_ptr: int, d_offs_ptr: int, n: int, stream_ptr: int = 0) -> capi.DeviceResult:
         """Device-resident batch (pointers from e.g. torch tensors); the result's

@@ -84,7 +84,8 @@ class DeviceResult(C.Structure):
                 ("shared", C.c_void_p), ("n_fallback", C.c_uint32), ("n_big", C.c_uint32),
                 ("fallback_why", C.c_uint32 * 5), ("n_merge_small", C.c_uint32), ("n_merge_wave", C.c_uint32),
                 ("n_solo_ranges", C.c_uint64), ("n_tier2", C.c_uint32), ("n_tier3", C.c_uint32),
-                ("multi_entries", C.c_uint64 * 3), ("n_part", C.c_uint32), ("n_resolve", C.c_uint32)]
+                ("multi_entries", C.c_uint64 * 3), ("n_part", C.c_uint32), ("n_resolve", C.c_uint32),
+                ("n_solo", C.c_uint64)]
 
 
 class DeviceMessages(C.Structure):

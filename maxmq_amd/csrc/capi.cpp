@@ -135,9 +135,7 @@ struct mqm_index {
   std::chrono::steady_clock::time_point journal_t0;
   uint64_t builds = 0, last_build_ops = 0;
   double last_build_ms = 0;
-  int walk_lanes = 4;
   bool fast_path = true;  // MQM_NO_FAST=1: small batches also take the batch pipeline (A/B, tests)
-  bool overlap = true;  // MQM_NO_OVERLAP=1: merges serialised behind the solo copy (profiling)
   bool async() const { return (cfg.flags & MQM_CFG_ASYNC_COMMIT) != 0; }
   // the device-result API's context (mqm_match_device & follow-ups)
   std::mutex dev_mu;
@@ -152,6 +150,7 @@ struct mqm_index {
   // collector_owner keeps it alive until the index is destroyed
   std::unique_ptr<Collector> collector_owner;
   std::atomic<Collector *> collector{nullptr};
+  std::atomic<uint32_t> live_ctxs{0};  // mqm_match_ctx objects of this index (mqm_destroy refuses while any live)
   void stop_collector();
   ~mqm_index();
 };
@@ -299,12 +298,11 @@ int front(mqm_index *h, std::shared_ptr<GpuSnapshot> *out) {
 }
 
 int ctx_init(mqm_index *h, MatchCtx *c) {
+  c->ws.keep_solo = (h->cfg.flags & MQM_CFG_IDENTIFIERS) != 0;  // the identifiers pass reads them
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     c->stream = nullptr;
     return MQM_EHIP;
   }
-  c->ws.walk_lanes = h->walk_lanes;
-  c->ws.overlap = h->overlap;
   return MQM_OK;
 }
 
@@ -396,6 +394,7 @@ void fill_device_result(const MatchOutput &mo, const Workspace &ws, mqm_device_r
   for (int i = 0; i < 3; i++) out->multi_entries[i] = mo.multi_entries[i];
   out->n_part = mo.n_part;
   out->n_resolve = mo.n_resolve;
+  out->n_solo = mo.n_solo;
 }
 
 // a result block laid out like mqm_match_batch's: offsets | shared_offsets |
@@ -512,11 +511,6 @@ int mqm_create(const mqm_config *cfg, mqm_index **out) {
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return MQM_ENODEV;
     if (h->cfg.device < 0 || h->cfg.device >= ndev) return MQM_EINVAL;
     if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
-    if (const char *e = getenv("MQM_WALK_LANES")) {  // tuning knob, read once per index
-      const int g = atoi(e);
-      h->walk_lanes = g == 8 || g == 16 ? g : 4;
-    }
-    if (const char *e = getenv("MQM_NO_OVERLAP")) h->overlap = atoi(e) == 0;
     if (const char *e = getenv("MQM_NO_FAST")) h->fast_path = atoi(e) == 0;
     if (ctx_init(h.get(), &h->dev) != MQM_OK) return MQM_EHIP;
     if (h->cfg.flags & MQM_CFG_BATCHING) {
@@ -530,6 +524,8 @@ int mqm_create(const mqm_config *cfg, mqm_index **out) {
 
 int mqm_destroy(mqm_index *h) {
   if (!h) return MQM_EINVAL;
+  // a match context reads the index: it must be destroyed first
+  if (h->live_ctxs.load(std::memory_order_acquire) != 0) return MQM_EINVAL;
   h->stop_collector();  // first: its thread matches (and may commit) through this index
   h->builder.reset();    // finishes a running build and joins the worker
   if (h->cfg.device != MQM_DEVICE_NONE) {
@@ -721,8 +717,10 @@ int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t 
 
 }  // extern "C"
 
+// skip_small: the caller already ran this batch on the small-batch path and
+// it fell back (a topic past one of its capacities): go straight to the pipeline
 static int match_batch_impl(mqm_index *h, const char *topic_bytes, const uint64_t *topic_offsets, uint32_t n_topics,
-                            bool packed, mqm_result **out) {
+                            bool packed, mqm_result **out, bool skip_small = false) {
   if (!h || !out || !topic_offsets || (n_topics && !topic_bytes)) return MQM_EINVAL;
   *out = nullptr;
   return guarded([&] {
@@ -737,7 +735,7 @@ static int match_batch_impl(mqm_index *h, const char *topic_bytes, const uint64_
     const bool want_ids = (h->cfg.flags & MQM_CFG_IDENTIFIERS) != 0;
     // small batches (the per-publish call shape): the one-launch path, unless
     // a topic is past one of its capacities (then the pipeline below)
-    if (n_topics <= kFastMaxTopics && h->fast_path) {
+    if (n_topics <= kFastMaxTopics && h->fast_path && !skip_small) {
       c->ws.begin(c->stream);
       FastOutput fo;
       const int e = match_small(snap->dev, c->ws, topic_bytes, topic_offsets, n_topics, c->stream, &fo, want_ids);
@@ -851,8 +849,8 @@ int mqm_match_ctx_create(mqm_index *h, mqm_match_ctx **out) {
     if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
     auto x = std::make_unique<mqm_match_ctx>();
     x->h = h;
-    x->c.ws.walk_lanes = h->walk_lanes;
-    x->c.ws.overlap = h->overlap;
+    x->c.ws.keep_solo = (h->cfg.flags & MQM_CFG_IDENTIFIERS) != 0;
+    h->live_ctxs.fetch_add(1, std::memory_order_acq_rel);
     *out = x.release();
     return MQM_OK;
   });
@@ -862,7 +860,9 @@ int mqm_match_ctx_destroy(mqm_match_ctx *x) {
   if (!x) return MQM_EINVAL;
   if (x->queued) (void)hipStreamSynchronize(x->st);
   (void)x->c.ws.drain();
+  mqm_index *h = x->h;
   delete x;
+  h->live_ctxs.fetch_sub(1, std::memory_order_acq_rel);
   return MQM_OK;
 }
 
@@ -1137,7 +1137,6 @@ struct Collector {
     std::unique_ptr<MatchCtx> ctx;
     std::shared_ptr<GpuSnapshot> snap;
     FastOutput fo;
-    std::vector<Req *> reqs;  // the callers, for the wake tree (submit)
     std::atomic<uint32_t> refs{0};
     void release() {
       if (refs.fetch_sub(1, std::memory_order_acq_rel) == 1) {
@@ -1169,7 +1168,6 @@ struct Collector {
   std::vector<Req *> q;
   bool stop = false;
   uint32_t max_batch = 8192, linger_us = 0;
-  const bool wake_tree = getenv("MQM_WAKE_TREE") && atoi(getenv("MQM_WAKE_TREE")) != 0;
   uint64_t batches = 0, topics = 0;
   std::vector<std::thread> ths;
 
@@ -1196,13 +1194,6 @@ struct Collector {
     cv.notify_one();
     r.wait();
     if (r.batch) {  // the small-batch path: this caller's topic, copied off the batch's blocks
-      // a wake tree: the worker wakes the first caller, caller i wakes 2i+1 and
-      // 2i+2, so a batch's wake syscalls run on many threads instead of one
-      // after another on the worker (each FUTEX_WAKE of a sleeper costs us)
-      // (MQM_WAKE_TREE=1; off by default until measured on the GPU box)
-      const auto &rq = r.batch->reqs;
-      if (wake_tree)
-        for (size_t c = 2 * (size_t)r.index + 1; c <= 2 * (size_t)r.index + 2 && c < rq.size(); c++) rq[c]->wake();
       const FastOutput &fo = r.batch->fo;
       const FastRec &x = fo.recs[r.index];
       try {
@@ -1259,8 +1250,11 @@ struct Collector {
   }
 
   // the batch on the small-batch path: a Batch the callers copy their results
-  // from; nullptr when not taken (the worker falls back to mqm_match_batch)
-  Batch *run_fast(const std::vector<Req *> &batch, const std::string &bytes, const std::vector<uint64_t> &offs) {
+  // from; nullptr when not taken (the worker falls back to the batch pipeline;
+  // *ran: the small-batch kernel ran and reported a topic past its capacities)
+  Batch *run_fast(const std::vector<Req *> &batch, const std::string &bytes, const std::vector<uint64_t> &offs,
+                  bool *ran) {
+    *ran = false;
     if (!h->fast_path || batch.size() > kFastMaxTopics) return nullptr;
     if (hipSetDevice(h->cfg.device) != hipSuccess) return nullptr;
     auto b = std::make_unique<Batch>();
@@ -1274,6 +1268,7 @@ struct Collector {
                               b->ctx->stream, &b->fo, (h->cfg.flags & MQM_CFG_IDENTIFIERS) != 0);
     const int e2 = b->ctx->ws.end(b->ctx->stream);
     if (e != 0 || e2) {
+      *ran = e == 1 && !e2;
       ctx_release(h, std::move(b->ctx));
       return nullptr;
     }
@@ -1290,8 +1285,15 @@ struct Collector {
         std::unique_lock<std::mutex> lk(mu);
         cv.wait(lk, [&] { return stop || !q.empty(); });
         if (q.empty()) return;  // stop requested and nothing pending
-        if (linger_us && q.size() < max_batch)
+        if (linger_us && q.size() < max_batch) {
           cv.wait_for(lk, std::chrono::microseconds(linger_us), [&] { return stop || q.size() >= max_batch; });
+          // another worker lingering on the same queue may have taken it all:
+          // never run (or count) an empty batch
+          if (q.empty()) {
+            if (stop) return;
+            continue;
+          }
+        }
         const size_t n = std::min<size_t>(q.size(), max_batch);
         batch.assign(q.begin(), q.begin() + n);
         q.erase(q.begin(), q.begin() + n);
@@ -1306,8 +1308,9 @@ struct Collector {
         offs.push_back(bytes.size());
       }
       Batch *fb = nullptr;
+      bool ran_small = false;
       try {
-        fb = run_fast(batch, bytes, offs);
+        fb = run_fast(batch, bytes, offs, &ran_small);
       } catch (...) {
         fb = nullptr;
       }
@@ -1316,16 +1319,12 @@ struct Collector {
           batch[i]->batch = fb;
           batch[i]->index = i;
         }
-        if (wake_tree) {
-          fb->reqs = batch;
-          batch[0]->wake();  // the rest through the wake tree (submit)
-        } else {
-          for (Req *r : batch) r->wake();
-        }
+        for (Req *r : batch) r->wake();
         continue;
       }
       mqm_result *b = nullptr;
-      const int rc = mqm_match_batch(h, bytes.data(), offs.data(), (uint32_t)batch.size(), &b);
+      // (a batch the small-batch kernel already rejected skips it: one launch, not two)
+      const int rc = match_batch_impl(h, bytes.data(), offs.data(), (uint32_t)batch.size(), false, &b, ran_small);
       for (uint32_t i = 0; i < batch.size(); i++) {
         batch[i]->rc = rc;
         if (rc == MQM_OK) {

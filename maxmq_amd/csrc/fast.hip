@@ -221,7 +221,7 @@ __global__ __launch_bounds__(kFT) void k_fast(DeviceSnapshot s, const uint8_t *_
         const uint32_t kind = iw & 3u, id = iw >> 2;
         const bool lit = kind == kFItemLit;
         NodeDesc dc;
-        const uint32_t c = walk_step(s, live && lit && !lit_is_wild, live && !lit, false, id, id, k0, k1,
+        const uint32_t c = walk_step(s, live && lit && !lit_is_wild, live && !lit, id, id, k0, k1,
                                      L.stage + tst, tln, &dc);
         if (c == kNone) continue;
         const uint32_t fl = dc.sh_cnt_flags >> 24;
@@ -307,12 +307,16 @@ __global__ __launch_bounds__(kFT) void k_fast(DeviceSnapshot s, const uint8_t *_
       // identifiers: at most one per gathered entry
       const unsigned long long ib = (iout && need) ? atomicAdd(&ctl->icur, need) : 0ull;
       const bool ovf = db + need > dcap || hb + H > hcap || (iout && ib + need > icap);
-      if (ovf) atomicOr(&ctl->flags, kFastOverflow);
+      // FastRec keeps 32-bit offsets: a batch whose results pass 2^32 entries
+      // takes the batch pipeline (64-bit segments) instead of growing the blocks
+      const bool wide = db + need > 0xFFFFFFFFull || hb + H > 0xFFFFFFFFull || ib + need > 0xFFFFFFFFull;
+      if (wide) atomicOr(&ctl->flags, kFastFallback);
+      else if (ovf) atomicOr(&ctl->flags, kFastOverflow);
       L.dbase = db;
       L.hbase = hb;
       L.ibase = ib;
       L.nid = 0;
-      L.fail = ovf ? 1u : 0u;
+      L.fail = ovf || wide ? 1u : 0u;
     }
     __syncthreads();
     if (L.fail) {  // the host grows the blocks to the reported totals and runs the batch again
@@ -514,7 +518,13 @@ int match_small(const DeviceSnapshot &s, Workspace &ws, const char *bytes, const
     HIP_TRY(hipStreamSynchronize(st));
     FastStatus stt;
     memcpy(&stt, (const void *)a.status, sizeof(stt));  // after the stream synchronisation
-    if (!stt.done) return -3;
+    if (!stt.done) {
+      // the last workgroup never reset the counters: clear them, so the next
+      // call on this context starts from zero instead of failing the same way
+      (void)hipMemsetAsync(a.ctl, 0, sizeof(FastCtl), st);
+      (void)hipStreamSynchronize(st);
+      return -3;
+    }
     if (stt.flags & kFastFallback) return 1;  // the caller runs the batch pipeline
     if (!(stt.flags & kFastOverflow)) {
       out->n_topics = n;

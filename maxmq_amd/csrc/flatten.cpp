@@ -573,18 +573,14 @@ int flatten(const Store &st, HostSnapshot *out) {
   });
   pt.mark("ranges");
   // 3. literal edges -> open-addressed table of 128-B buckets, linear probing
-  //    at load factor `load` (env MQM_EDGE_LOAD in (0, 0.9]): a probe chain
+  //    at load factor `load`: a probe chain
   //    that leaves its home entry costs another dependent HBM round trip, and
   //    a wavefront waits for its longest chain (measured on C3: k_walk 9.5 /
   //    10.9 / 16.5 / 71 ms at load 0.15 / 0.26 / 0.5 / 0.8 in round 1; with the
   //    edge filter 6.44 / 6.79 / 7.49 ms at 0.12 / 0.2 / 0.35).  Default 0.12
   //    up to 64M edges (18.5 GB at C3), 0.2 beyond (the table's host copy and
   //    upload grow with it: config 5 has 79M edges)
-  double load = n_literal_edges <= (64ull << 20) ? 0.12 : 0.2;
-  if (const char *e = getenv("MQM_EDGE_LOAD")) {
-    const double v = atof(e);
-    if (v > 0.0 && v <= 0.9) load = v;
-  }
+  const double load = n_literal_edges <= (64ull << 20) ? 0.12 : 0.2;
   const uint64_t buckets =
       std::max<uint64_t>(1, (uint64_t)((double)n_literal_edges / (load * kEdgesPerBucket)) + 1);
   hs.n_buckets = buckets;

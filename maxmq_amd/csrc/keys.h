@@ -77,20 +77,14 @@ MQM_HD Key make_key(ByteAt at, uint32_t len) {
 
 MQM_HD bool key_is_long(const Key &k) { return (k.k1 >> 56) == 0xFF; }
 
-// MQM_OLD_HASH=1 (A/B; host and device must agree, so a whole build): the
-// round-2 edge hash (fmix64, two 64-bit multiplies) and a 64x64 range
-// reduction.  Default: one 64-bit multiply and a 32x32 range reduction — the
-// walk hashes every literal probe twice (the push-time filter check, the
-// probe), and 32-bit integer multiplies are multi-cycle VALU instructions.
-#ifndef MQM_OLD_HASH
-#define MQM_OLD_HASH 0
-#endif
+// Edge hash: one 64-bit multiply and a 32x32 range reduction — the walk
+// hashes every literal probe twice (the push-time filter check, the probe),
+// and 64-bit integer multiplies are multi-cycle VALU instructions (round 2's
+// fmix64 with a 64x64 reduction measured slower, profiles/r03/r03k).
 
 // bucket of an edge among n buckets (multiply-shift range reduction: any n)
 MQM_HD uint64_t bucket_of(uint64_t h, uint64_t n) {
-#if !MQM_OLD_HASH
   if (n <= 0xFFFFFFFFull) return ((h >> 32) * n) >> 32;  // the hash's top 32 bits
-#endif
 #if defined(__HIP_DEVICE_COMPILE__)
   return __umul64hi(h, n);
 #else
@@ -100,16 +94,11 @@ MQM_HD uint64_t bucket_of(uint64_t h, uint64_t n) {
 
 // bucket hash of an edge (parent node, child key)
 MQM_HD uint64_t edge_hash(uint32_t parent, const Key &k) {
-#if MQM_OLD_HASH
-  uint64_t h = fmix64(k.k0 ^ rotl64(k.k1, 29) ^ ((uint64_t)parent * 0x9E3779B97F4A7C15ull));
-  return h ^ (h >> 29);
-#else
   // one multiply: every product bit above bit i depends on every input bit up
   // to i, and the fold brings the well-mixed top half down for the low bits
   const uint64_t x = k.k0 ^ rotl64(k.k1, 29) ^ ((uint64_t)parent * 0x9E3779B97F4A7C15ull);
   uint64_t h = (x ^ (x >> 31)) * 0xff51afd7ed558ccdull;
   return h ^ (h >> 32);
-#endif
 }
 
 // edge-existence filter (DeviceSnapshot::bloom): a blocked Bloom filter, the 3

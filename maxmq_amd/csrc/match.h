@@ -53,9 +53,9 @@ struct FastOutput {
 // Grow-only device buffers reused across batches (no allocation in steady state).
 struct Workspace {
   enum Slot {
-    kSCount, kHCount, kDCount, kDStart, kHStart, kCls, kDfsList, kRecs, kCounters, kDOut, kHOut,
+    kHCount, kDCount, kDStart, kHStart, kCls, kDfsList, kRecs, kCounters, kDOut, kHOut,
     kDense, kDenseShared, kDenseOffs, kDenseHOffs, kScanTmp, kRawCnt, kTabOff, kTabSize, kTable,
-    kInBytes, kInOffs, kListS, kICount, kIStart, kIOut, kNSolo, kDescStart, kDesc, kWin, kMCount, kListW, kListT1, kListT2, kListT3, kListP, kListH, kListRS, kListR, kPerm, kPermBins,
+    kInBytes, kInOffs, kListS, kICount, kIStart, kIOut, kMCount, kListW, kListT1, kListT2, kListT3, kListP, kListH, kListRS, kListR,
     // reverse match (retained.hip)
     kROffs, kRNLev, kRWild, kRLOff, kRFCount, kRFCur, kRLevels, kRNCount, kRNOff, kRItemF0, kRItemN0, kRItemF1,
     kRItemN1, kRChild, kRECount, kREOff, kREmit, kRPos, kRChunks, kRCOff, kROut, kRInBytes, kRInOffs, kNumSlots
@@ -67,7 +67,6 @@ struct Workspace {
   Buf bufs[kNumSlots];
   void *host_pinned = nullptr;
   uint32_t max_blocks = 2048;  // walk-kernel grid cap (grid-stride beyond)
-  int walk_lanes = 4;          // lanes per topic in k_walk (4, 8 or 16; env MQM_WALK_LANES; C3: 7.9 / 8.8 / 11.0 ms)
   // reverse match (retained.hip): list capacities carried from call to call
   // (grown when a call's device counters report an overflow)
   uint64_t rev_item_cap = 0, rev_emit_cap = 0, rev_task_cap = 0, rev_out_cap = 0;
@@ -90,6 +89,9 @@ struct Workspace {
   // the last match_device call (identifiers_device works on its records)
   bool last_valid = false;
   uint32_t last_n = 0, last_n_dfs = 0;
+  // the walk also writes every solo part to the topic records (the
+  // identifiers pass reads them; capi: MQM_CFG_IDENTIFIERS)
+  bool keep_solo = false, last_keep_solo = false;
   const uint8_t *last_bytes = nullptr;
   const uint64_t *last_offs = nullptr;
 
@@ -115,13 +117,6 @@ struct Workspace {
   bool used = false;
   void begin(hipStream_t st) { cur = st; }
   int end(hipStream_t st);       // record last_use on st
-  // a second stream for work that may overlap the call's main stream: fork()
-  // orders it after st's queued work, join() orders st after it (both by events)
-  bool overlap = true;  // merges on the side stream (capi: MQM_NO_OVERLAP=1 serialises them, for profiling)
-  hipStream_t side = nullptr;
-  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
-  int fork(hipStream_t st, hipStream_t *out);
-  int join(hipStream_t st, hipStream_t side_st);
   int drain();                   // wait for every queued use of the buffers
   int reserve(void **p, size_t *cap, size_t need);
   int get(Slot s, size_t need) { return reserve(&bufs[s].p, &bufs[s].cap, need); }
@@ -147,10 +142,11 @@ struct MatchOutput {
   uint32_t n_big = 0;       // topics whose multi entries the workgroup tier merged
   uint32_t n_tier2 = 0, n_tier3 = 0;  // ... of those, passed on to its second / third tier
   uint32_t n_merge_small = 0, n_merge_wave = 0;  // topics merged by k_merge_small / k_merge
-  uint64_t n_solo_ranges = 0;                     // solo copy descriptors (hits with solo entries)
+  uint64_t n_solo_ranges = 0;                     // solo parts the walk copied (hits with solo entries)
   uint64_t multi_entries[3] = {0, 0, 0};  // multi entries merged by the three workgroup tiers
   uint32_t n_part = 0;                    // ... of the third tier's topics, merged in client-hash partitions
   uint32_t n_resolve = 0;                 // topics merged by resolution (k_resolve: no table)
+  uint64_t n_solo = 0;                    // deliveries the walk copied as they stand (solo entries)
   bool exact = false;                     // sized by its own read-back (the first call of a workspace, or a re-run)
 };
 

@@ -3,35 +3,44 @@
 // publish topics, against the GPU-resident CSR level-trie (snapshot.h).
 //
 // One pass over the trie per topic, then deduplication sized to the topic:
-//   k_walk    a 16-lane group per topic, 4 topics per wavefront.
-//     1. tokenize : the group scans the topic 16 bytes at a time and ballots
-//                   the '/' positions; lane k builds level k's 128-bit key.
+//   k_walk    a 4-lane group per topic, 16 topics per wavefront.
+//     1. tokenize : the group scans the topic kStage bytes at a time and
+//                   ballots the '/' positions; lane k builds the 128-bit keys
+//                   of levels k, k + 4, ...
 //     2. walk     : level-synchronous over the frontier; each frontier node
-//                   fans out to 3 lanes (literal edge probe / '+' child /
+//                   enqueues only the loads it needs (literal edge probe,
+//                   checked against the edge filter when pushed / '+' child /
 //                   '#' child), so a level costs one dependent memory round
 //                   trip (the literal child's descriptor is inline in its
-//                   edge entry).  Hits are compacted with ballot + popcount
-//                   and written straight to the topic's record with their
-//                   raw-entry prefix and their rank (2 * node + slot = the
-//                   reference's emission order, snapshot.h); S (raw
-//                   entries) and H (shared candidates) are counted.
-//   scan      S and H -> each topic's segment start (S is the upper bound of
-//             its deliveries, so every later kernel writes final positions).
-//   k_emit    a wavefront per topic: solo entries (kMetaMulti clear, ~90%)
-//             are copied to their final positions (delivery q = solo entry
-//             q); the multi entries are merged in a per-wave LDS hash table
-//             keyed by client — atomicOr folds QoS (one-hot) and NoLocal,
-//             atomicMin keeps the lowest hit rank, an entry is its client's
-//             winner iff its hit has that rank: exactly Subscription.Merge
-//             (packets.go:250-270) with the first-merged subscription's
-//             fields — and the winners compacted with ballot after the solo
-//             part.  Also writes every topic's shared candidates.
-//   k_multi   a 256-thread workgroup per topic with more multi entries than
-//             a wave's table holds (<= kBigMax): the same merge in LDS.
+//                   edge entry).  Hits are compacted with ballot + popcount:
+//                   solo parts (off, count) into the topic's LDS context,
+//                   multi parts (off, count, rank = 2 * node + slot, the
+//                   reference's emission order, snapshot.h) and shared ranges
+//                   into the topic's record in HBM.
+//     3. segments : one reservation per wavefront for its 16 topics' raw
+//                   entries (S, an upper bound of the deliveries), from a
+//                   chunk of the output the wavefront holds (one global
+//                   atomic per kChunk entries): dstart[t] is final when the
+//                   topic's walk ends, so no scan and no second pass.
+//     4. solo copy: the wavefront copies its topics' solo entries (~90 % of
+//                   the deliveries: an entry whose client meets no other of
+//                   its subscriptions in the topic is its client's merged
+//                   delivery as is) straight from the LDS parts: lane-
+//                   consecutive 4-B loads of `words` and stores to dout.  The
+//                   copy streams while other wavefronts of the CU chase
+//                   pointers, and the walk's records hold only what the merges
+//                   read (round 3 wrote every solo part to HBM for k_desc /
+//                   k_winmap / k_wincopy to read back: 4.3 ms of a 14.4 ms
+//                   batch at C3).
+//   k_route   topics with multi entries -> merge lists by their count Ms.
+//   merges    k_resolve (partner lists, no table), k_merge_small / k_merge /
+//             k_multi<N> / k_multi_part (LDS hash tables keyed by client):
+//             Subscription.Merge (packets.go:250-270), winners after the
+//             topic's solo deliveries.  k_shared writes shared candidates.
 //   k_dfs<P>  the unbounded path for topics past a capacity (frontier, hits,
 //             cached levels, shared hits, raw entries): wave-cooperative DFS
 //             with an LDS stack and a global-memory dedupe table, writing to
-//             a tail region after the scanned segments.
+//             a tail region after the reserved segments.
 // Nothing runs on the CPU.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -44,60 +53,11 @@
 #include "device.h"
 #include "match.h"
 
-// MQM_WALK_OCC: k_walk's waves-per-SIMD target (1 = let the compiler use
-// the registers it wants; `make variant VFLAGS=-DMQM_WALK_OCC=6` sweeps it)
-#ifndef MQM_WALK_OCC
-#define MQM_WALK_OCC 1
-#endif
-// MQM_NT_OUT=1: non-temporal output stores (tuning knob, `make variant`; C3
-// sweep profiles/r01/c3_v14_nt_tail_sweep.log: no gain, off)
-#ifndef MQM_NT_OUT
-#define MQM_NT_OUT 0
-#endif
-// MQM_COPY16=1: solo copies move 2 entries per lane and access (16-B stores,
-// round 1's form) instead of lane-consecutive 8-B entries (tuning knob)
 // MQM_WALK_STATS=1: count the walk's literal probes, the ones that found no
-// child, and the wildcard-child descriptor loads (printed per batch; tuning)
+// child, and the wildcard-child descriptor loads (printed per batch;
+// instrumentation build, `make variant VFLAGS=-DMQM_WALK_STATS=1`)
 #ifndef MQM_WALK_STATS
 #define MQM_WALK_STATS 0
-#endif
-#ifndef MQM_MERGE_BIG_FIRST
-#define MQM_MERGE_BIG_FIRST 1
-#endif
-// MQM_WALK_SORT=1: the walk visits topics grouped by length (a proxy for
-// depth, longest first) through a permutation, so the 16 topics of a
-// wavefront walk similar numbers of levels (lockstep waste: VALU lane use 0.47)
-#ifndef MQM_WALK_SORT
-#define MQM_WALK_SORT 0
-#endif
-// MQM_SIDE_PCT: share of the resident grid the merge kernels (side stream)
-// take while the solo copy runs on the main stream with the rest, so the two
-// actually run side by side (persistent grids sized to the whole device ran
-// one after the other); 100 = both take the whole device (round-1 behaviour)
-#ifndef MQM_SIDE_PCT
-#define MQM_SIDE_PCT 100
-#endif
-// MQM_WALK_ICAP / MQM_WALK_STAGE: k_walk's per-topic LDS context — load items
-// per level (a topic whose frontier needs more takes the DFS path) and topic
-// bytes staged for the key build.  Together with MQM_WALK_OCC they set how
-// many topics the walk keeps in flight per CU (LDS: 64 topics per block).
-#ifndef MQM_WALK_ICAP
-#define MQM_WALK_ICAP 48
-#endif
-#ifndef MQM_WALK_STAGE
-#define MQM_WALK_STAGE 64
-#endif
-#ifndef MQM_COPY16
-#define MQM_COPY16 0
-#endif
-// MQM_WALK_COOP=1: k_walk<4> loads each group's edge entries / descriptors
-// cooperatively, 16 B per lane (device.h walk_step_quad).  Measured slower on
-// C3 (walk 6.65 vs 6.11 ms, profiles/r03/r03c): the walk is not bound by the
-// per-line address work that bounds a pure random gather (where the
-// cooperative form is 2.2x faster, tools/calib_fetch), so the transpose's
-// instructions cost more than the loads save.  Off.
-#ifndef MQM_WALK_COOP
-#define MQM_WALK_COOP 0
 #endif
 
 namespace mqm {
@@ -106,28 +66,28 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr int kWalkWaves = 4;            // wavefronts per k_walk block
-#ifndef MQM_WALK_LMAX
-#define MQM_WALK_LMAX 16
-#endif
-constexpr int kLMax = MQM_WALK_LMAX;     // levels cached per topic (deeper topics: DFS path)
+constexpr int kWalkG = 4;                // k_walk lanes per topic (C3, round 2: 4 / 8 / 16 lanes 7.9 / 8.8 / 11.0 ms)
+constexpr int kLMax = 16;                // levels cached per topic (deeper topics: DFS path)
 constexpr int kHCap = 64;                // non-shared hits per topic (hit_of: 6 search steps)
 constexpr int kShCap = 16;               // shared hits per topic
-constexpr int kStage = MQM_WALK_STAGE;    // topic bytes staged in LDS (one round trip)
+constexpr int kStage = 64;               // topic bytes staged in LDS (one round trip)
+constexpr int kICap = 48;                // load items per level (<= 3 per frontier node; more -> DFS path)
+constexpr int kSoloLds = 16;             // solo parts per topic held in LDS (more: the record's front)
+constexpr uint32_t kChunk = 1u << 15;    // output entries a walk wavefront reserves at a time
+constexpr int kCopyU = 4;                // solo entries per lane per copy step (loads in flight)
 // record of a topic, written while walking (kRecStrideAlloc words, 64-B
-// aligned).  A hit range subs[off, off + c) holds solo entries, then multi
-// ones (snapshot.h); the two parts are listed apart, each where its reader
-// wants it, so a topic writes (and its readers read) only the parts it has:
-//   from the start: [2i] off, [2i + 1] count of the i-th solo part (i <
-//            nsolo[t]): k_desc's copy descriptors
+// aligned), read by the merges, k_shared and the identifiers pass:
+//   from the start: [2i] off, [2i + 1] count of the i-th solo part — only
+//            parts i >= kSoloLds, or every part when the identifiers pass
+//            will read them (Outputs::keep_solo)
 //   [kRecSh + 2i] off, [kRecSh + 1 + 2i] cnt of shared hit i (i < nsh)
 //   the tail, in 16-B units counted back from the record's end (rec_tail):
-//     unit 0      header: nm | nsh << 8, Ssolo, M, nsolo
+//     unit 0      header: nm | nsh << 8, Ssolo, M, nsolo (written when a
+//                 reader exists: M > 0, nsh > 0 or keep_solo)
 //     unit 1 + h  multi part h (h < nm): moff, mcount, rank of its hit, 0 —
 //                 multi entries subs[moff, moff + mcount); the merges copy
 //                 the tail into LDS as header at word 0, part h at 4 + 4h,
 //                 and turn mcount into the prefix mpre (rec_prefix)
-// Round 1 kept every hit (off, solo, multi, rank) plus the solo pairs: on C3
-// the pure-solo hits made up most of the walk's 3.4 GB of record writes.
 constexpr int kRecHit = 4;
 constexpr int kRecLds = 4 + kRecHit * kHCap;          // 260: header + multi parts (the merges' LDS copy)
 constexpr int kRecSh = 2 * kHCap;                     // 128: shared pairs
@@ -135,8 +95,7 @@ constexpr int kRecTail = kRecSh + 2 * kShCap;         // 160: the tail area star
 constexpr int kRecStrideAlloc = 432;                  // words per topic: 1728 B = 27 x 64 B
 // raw entries per hit range on the bounded path (keeps the per-lane sums of a
 // topic's 64 hits inside 32 bits); emission itself has no per-topic size
-// limit (window copy of the solo part; partitioned merge of any number of
-// multi entries)
+// limit (the solo copy loops; partitioned merge of any number of multi entries)
 constexpr uint32_t kSMax = 1u << 24;
 constexpr int kEmitWaves = 4;
 constexpr int kSmallLanes = 8;           // k_merge_small: lanes per topic
@@ -147,34 +106,17 @@ constexpr int kSmallMulti = 192;         // multi entries it holds (load <= 0.75
 constexpr int kBigThreads = 256;
 constexpr int kPartCap = 2048;           // k_multi_part: multi entries per client partition (expected)
 constexpr uint32_t kNoWhy = 0xFFFFFFFFu;
-constexpr int kICap = MQM_WALK_ICAP;     // load items per level (<= 3 per frontier node; more -> DFS path)
 
 static_assert(kRecStrideAlloc % 16 == 0 && kRecStrideAlloc >= kRecTail + kRecLds, "64-B aligned records");
 static_assert(kSmallMulti * 4 <= kSmallSlots * 3, "k_emit table load factor");
 static_assert(kSmallMulti % kWave == 0, "register tiles");
+static_assert(kSoloLds == 4 * kWalkG && kSoloLds <= kHCap, "solo parts: 4 per lane of a group");
+static_assert(kLMax % kWalkG == 0, "levels per lane");
 
-// a load item of the walk: the literal-child probe of a frontier node, or the
-// descriptor load of its '+' / '#' child
-// kItemLitB: a literal probe checked against the edge-existence filter first.
-// MQM_BLOOM_PLUS_ONLY=1 gives that kind only to nodes with a '+' child (where
-// topic levels drawn for a wildcard make probes miss); other literal probes
-// then skip the filter's round trip.  Both apply only with
-// MQM_WALK_PRECHECK=0: the default checks the filter when an item is pushed
-// and pushes positives as kItemLit (with MQM_NO_BLOOM=1, a snapshot without
-// the filter, every literal item is pushed unless the next level is '+' / '#')
-enum : uint32_t { kItemLit = 0, kItemPlus = 1, kItemHash = 2, kItemLitB = 3 };
-// MQM_WALK_PRECHECK=1: a frontier node's literal item is checked against the
-// filter when it is pushed (its load overlapping the pushing level's record
-// writes) and only a positive is pushed, as kItemLit
-#ifndef MQM_WALK_PRECHECK
-#define MQM_WALK_PRECHECK 1
-#endif
-#ifndef MQM_BLOOM_PLUS_ONLY
-#define MQM_BLOOM_PLUS_ONLY 0
-#endif
-__device__ __forceinline__ uint32_t lit_kind(uint32_t plus) {
-  return MQM_BLOOM_PLUS_ONLY && plus == kNone ? kItemLit : kItemLitB;
-}
+// a load item of the walk: the literal-child probe of a frontier node (pushed
+// only when the edge filter says the next level's key may be a child of it),
+// or the descriptor load of its '+' / '#' child
+enum : uint32_t { kItemLit = 0, kItemPlus = 1, kItemHash = 2 };
 
 // topic class (cls): Done = no entries and no shared candidates; Bounded (+
 // FewHits when nh <= kSmallHits, for k_route) = emitted from its record; Dfs
@@ -184,8 +126,9 @@ enum : uint8_t { kClsDone = 0, kClsBounded = 1, kClsDfs = 2, kClsFewHits = 4, kC
 enum : uint32_t { kWhyFrontier = 0, kWhyHits = 1, kWhyLevels = 2, kWhyShared = 3, kWhyEntries = 4 };
 
 struct Counters {              // zeroed before every batch
-  unsigned long long dtail;    // DFS deliveries: next free entry after the scanned segments
+  unsigned long long dtail;    // DFS deliveries: next free entry after the reserved segments
   unsigned long long htail;    // DFS shared candidates: likewise
+  unsigned long long dcur;     // the walk's output reservations (chunks and large segments)
   unsigned int n_dfs;          // topics appended to the DFS list
   unsigned int why[5];         // DFS routing reasons (kWhy*)
   // merge lists (k_route), in kList* order
@@ -199,11 +142,12 @@ struct Counters {              // zeroed before every batch
   unsigned int n_res_small;    // k_resolve<8>: no heavy entry, Ms <= kSmallMultiS, nh <= kSmallHits
   unsigned int n_res;          // k_resolve<64>: other topics with multi entries and no heavy entry
   unsigned long long m_sum[3]; // multi entries of the k_multi<1024> / <2048> / <4096> + k_multi_part lists
-  unsigned int oob;            // a store fell outside its output buffer (queued calls: buffers sized
-                               //   from an earlier call were too small; the call is re-run)
+  unsigned int oob;            // a store fell outside its output buffer (the call is re-run with
+                               //   buffers sized by what it reported)
   unsigned int cap_ovf;        // queued calls: the DFS lists / table / tails did not fit (re-run)
   // what the call needed (k_totals / k_dfs_prep): the next call's capacities
-  unsigned long long s_total, h_total, n_desc;  // raw-entry slots, shared slots, solo descriptors
+  unsigned long long s_total, h_total, n_desc;  // reserved output entries, shared slots, solo parts
+  unsigned long long n_solo;                    // solo entries the walk copied
   unsigned long long tab_total, dfs_raw, dfs_h; // DFS: dedupe table, raw entries, shared candidates
   unsigned long long d_sum, h_sum;              // deliveries, shared candidates (after dedupe)
 #if MQM_WALK_STATS
@@ -212,14 +156,12 @@ struct Counters {              // zeroed before every batch
 };
 
 struct Outputs {
-  uint32_t *scount, *hcount, *dcount;
+  uint32_t *hcount, *dcount;
   uint32_t *mcount;           // multi entries per topic (Ms; 0 for DFS topics)
-  uint32_t *nsolo;            // hits with solo entries per topic (k_desc's descriptors)
-  uint64_t *dstart, *hstart;  // n + 1 (exclusive scans; DFS topics overwritten)
+  uint64_t *dstart, *hstart;  // n + 1 (dstart: the walk's reservations; hstart: exclusive scan)
   uint8_t *cls;
   uint32_t *dfs_list;
   uint32_t *recs;  // kRecStrideAlloc words per topic
-  const uint32_t *perm;  // k_walk's visiting order (nullptr: topic order)
   Counters *ctr;
   uint32_t *dout;  // packed deliveries (snapshot.h)
   uint32_t *hout;
@@ -231,19 +173,33 @@ struct Outputs {
   // (a wrong offset becomes a reported error, never an out-of-bounds write)
   uint64_t dcap, hcap;
   uint32_t dfs_cap;  // DFS topics raw_cnt / raw_h / tab_off hold
+  uint32_t keep_solo;  // the walk also writes every solo part to the record (identifiers pass)
 };
 
-constexpr int kTopicWords = (2 * kLMax + 8 * kICap + kStage) / 4;
-struct TopicLds {              // k_walk context of one topic (one lane group)
+// k_walk context of one topic (one lane group).  The solo parts are kept as
+// words, not uint2: the context's dword stride must stay odd (below)
+struct TopicLds {
   uint16_t sep[kLMax];         // position of the '/' ending level k (topics > 64 KiB: DFS path)
   uint32_t item[2][kICap];     // the level's load items: node id << 2 | kind (kItem*)
+  uint32_t sp[2 * kSoloLds];   // solo part j: off - rel, rel (rel = the topic's solo entries before it;
+                               //   ~0 past the topic's parts)
   uint8_t stage[kStage];       // the topic's first kStage bytes
-  uint32_t pad[kTopicWords % 2 ? 2 : 1];  // odd dword stride: the groups of a wave reading the
-                               //   same field hit different banks (a 128-dword stride put all
-                               //   16 groups on one bank: SQ_LDS_BANK_CONFLICT 3x the LDS cycles)
+  uint32_t q16;                // rel of solo part kSoloLds (the first one in the record)
 };
 static_assert(kStage % 16 == 0 && kICap >= 3, "walk context");
-static_assert((sizeof(TopicLds) / 4) % 2 == 1, "bank-skewed topic contexts");
+// odd dword stride: the groups of a wave reading the same field hit different
+// banks (a 128-dword stride put all 16 groups on one bank: SQ_LDS_BANK_CONFLICT
+// 3x the LDS cycles)
+static_assert(sizeof(TopicLds) % 4 == 0 && (sizeof(TopicLds) / 4) % 2 == 1, "bank-skewed topic contexts");
+// the solo copy's per-wavefront tables: the groups' starts in the wavefront's
+// solo space and their output segments
+struct CopyLds {
+  uint32_t F[kWave / kWalkG + 2];  // exclusive prefix of the groups' LDS-part entries; [16] = total
+  uint32_t E[kWave / kWalkG];      // each group's segment, relative to the wavefront's reservation
+};
+// 4 blocks per CU (16 waves: the walk's VGPR limit) must fit in 160 KiB
+static_assert(4 * (kWalkWaves * (kWave / kWalkG) * sizeof(TopicLds) + kWalkWaves * sizeof(CopyLds)) <= 163840,
+              "k_walk LDS for 4 blocks per CU");
 
 __device__ __forceinline__ void wave_lds_sync() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -261,25 +217,19 @@ __device__ __forceinline__ uint32_t table_slot(uint32_t client, uint32_t lg) {
   return (uint32_t)(((uint64_t)(client * 2654435769u) << lg) >> 32);
 }
 
-// deliveries and shared candidates are written once and never re-read on the
-// device; MQM_NT_OUT streams them past the caches (measured: no gain on C3)
-template <class T>
-__device__ __forceinline__ void put_out(T *p, T v) {
-#if MQM_NT_OUT
-  __builtin_nontemporal_store(v, p);
-#else
-  *p = v;
-#endif
-}
+// Counters::oob bits: which check failed (reported when an exact call fails)
+enum : unsigned int { kOobWalk = 1u, kOobStore = 2u, kOobShared = 4u, kOobHeavy = 8u, kOobPart = 16u, kOobDfs = 32u };
 
 // a checked store: out[i] = v if i < cap, else flag the batch as failed
 template <class T>
-__device__ __forceinline__ void put_checked(T *out, uint64_t i, uint64_t cap, T v, unsigned int *oob) {
+__device__ __forceinline__ void put_checked(T *out, uint64_t i, uint64_t cap, T v, unsigned int *oob,
+                                            unsigned int bit = kOobStore) {
   if (i < cap)
-    put_out(&out[i], v);
+    out[i] = v;
   else
-    atomicOr(oob, 1u);
+    atomicOr(oob, bit);
 }
+
 
 __device__ __forceinline__ uint32_t pack_delivery(uint32_t sid, uint32_t qos, uint32_t nl) {
   return sid | (qos << 28) | (nl << 30);
@@ -357,13 +307,12 @@ __device__ __forceinline__ uint32_t mt_delivery(MergeTable t, uint32_t j) {
   return pack_delivery((uint32_t)t.first[j] & kWordSidMask, 31u - __builtin_clz(v & 7u), (v >> 3) & 1u);
 }
 
-
 // ---------------------------------------------------------------------------
-// k_walk: tokenize + walk, a 16-lane group per topic.  Level keys and the
-// running hit count live in registers (lane k holds level k's key); LDS holds
-// only the separators, the frontier and the first bytes of the topic, so many
-// topics stay in flight per CU.  Hits go straight to the topic's record with
-// their rank (= 2 * node + slot, the reference's emission order).
+// k_walk: tokenize + walk + output segments + solo copy, a kG-lane group per
+// topic.  Level keys and the running hit counts live in registers (lane k
+// holds the keys of levels k, k + kG, ...); LDS holds the separators, the
+// frontier, the first bytes of the topic and its first kSoloLds solo parts,
+// so many topics stay in flight per CU.
 // ---------------------------------------------------------------------------
 // A record's multi parts carry their entry counts (field kFieldMpre, as k_walk
 // wrote them); the merges turn them into exclusive prefixes in their LDS copy
@@ -400,40 +349,48 @@ __device__ __forceinline__ const uint4 *rec_tail(const uint32_t *recs, uint32_t 
   return reinterpret_cast<const uint4 *>(recs + ((uint64_t)t + 1) * kRecStrideAlloc) - 1;
 }
 
-// kG lanes per topic (8 or 16), kWave / kG topics per wavefront
-template <int kG, int kOcc>
-__global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_eu(kOcc))) void k_walk(DeviceSnapshot s, const uint8_t *__restrict__ tbytes,
+// `words` through a buffer descriptor: 32-bit offsets, bounds-checked reads
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t words_rsrc(const DeviceSnapshot &s) {
+  return __builtin_amdgcn_make_buffer_rsrc((void *)s.words, (short)0, (int)(s.n_subs * 4u + 64u), 0x00020000);
+}
+
+template <int kG>
+__global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, const uint8_t *__restrict__ tbytes,
                                                            const uint64_t *__restrict__ toffs, uint32_t n,
                                                            Outputs o) {
   constexpr int kGroups = kWave / kG;
   constexpr int kLPer = (kLMax + kG - 1) / kG;  // level keys held per lane
   constexpr uint32_t kGMask = (1u << kG) - 1u;
   static_assert(kLMax % kG == 0 || kG > kLMax, "levels per lane");
+  static_assert(kG == kWalkG, "TopicLds / CopyLds are sized for kWalkG lanes per topic");
   __shared__ TopicLds lds_all[kWalkWaves * kGroups];
+  __shared__ CopyLds copy_all[kWalkWaves];
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / kG, gl = lane & (kG - 1), gbase = g * kG;
   TopicLds &L = lds_all[(threadIdx.x / kWave) * kGroups + g];
+  TopicLds *WL = &lds_all[(threadIdx.x / kWave) * kGroups];  // the wavefront's topic contexts
+  CopyLds &C = copy_all[threadIdx.x / kWave];
   const uint32_t gmask_lt = (1u << gl) - 1u;
   const uint64_t stride = (uint64_t)gridDim.x * kWalkWaves * kGroups;
   const NodeDesc root = load_desc(s.nodes);
+  uint64_t c_cur = 0, c_end = 0;  // the wavefront's output chunk (wave-uniform)
+  uint32_t n_parts = 0;           // solo parts of this wavefront's topics (Counters::n_desc)
+  uint32_t n_solo = 0;            // their entries (Counters::n_solo; group leaders, flushed before 2^32)
 
   uint64_t tb = ((uint64_t)blockIdx.x * kWalkWaves + threadIdx.x / kWave) * kGroups;
   uint64_t nx_off = 0, nx_end = 0;  // the next topic's byte range, one topic ahead
-  uint32_t nx_t = 0;
   if (tb + g < n) {
-    nx_t = o.perm ? o.perm[tb + g] : (uint32_t)(tb + g);
-    nx_off = toffs[nx_t];
-    nx_end = toffs[nx_t + 1];
+    nx_off = toffs[tb + g];
+    nx_end = toffs[tb + g + 1];
   }
   for (; tb < n; tb += stride) {
     const bool active = tb + g < n;
-    const uint32_t t = active ? nx_t : (uint32_t)n;  // (inactive lanes never use t)
+    const uint32_t t = active ? (uint32_t)(tb + g) : n;  // (inactive lanes never use t)
     const uint32_t len = active ? (uint32_t)(nx_end - nx_off) : 0;
     const uint8_t *tp = tbytes + (active ? nx_off : 0);
     if (tb + stride + g < n) {
-      nx_t = o.perm ? o.perm[tb + stride + g] : (uint32_t)(tb + stride + g);
-      nx_off = toffs[nx_t];
-      nx_end = toffs[nx_t + 1];
+      nx_off = toffs[tb + stride + g];
+      nx_end = toffs[tb + stride + g + 1];
     }
     uint32_t why = kNoWhy;
 
@@ -487,7 +444,7 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
     // level 0's items: the root's literal probe, '+' and '#' children
     if (gl == 0) {
       uint32_t k = 0;
-      if ((root.sh_cnt_flags >> 24) & kFlagHasLiteral) L.item[0][k++] = (0u << 2) | lit_kind(root.plus);
+      if ((root.sh_cnt_flags >> 24) & kFlagHasLiteral) L.item[0][k++] = (0u << 2) | kItemLit;
       if (root.plus != kNone) L.item[0][k++] = (root.plus << 2) | kItemPlus;
       if (root.hash != kNone) L.item[0][k++] = (root.hash << 2) | kItemHash;
     }
@@ -497,14 +454,29 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
 
     // ---- 2. walk ----------------------------------------------------------
     // Level-synchronous over compact item lists: a node pushed to the next
-    // level enqueues only the loads it needs (its literal probe if it has a
-    // literal child, its '+' child, its '#' child unless kFlagHashLeaf lets
-    // the '#' child's gather be recorded at push time: partKey '#' of the
-    // next level, topics.go:503-505, rank 2 * '#' child).
+    // level enqueues only the loads it needs (its literal probe if the edge
+    // filter admits the next level's key under it, its '+' child, its '#'
+    // child unless kFlagHashLeaf lets the '#' child's gather be recorded at
+    // push time: partKey '#' of the next level, topics.go:503-505, rank 2 *
+    // '#' child).
     uint32_t *rec = o.recs + (uint64_t)(active ? t : 0) * kRecStrideAlloc;
     uint4 *tail = reinterpret_cast<uint4 *>(rec + kRecStrideAlloc) - 1;  // unit u at tail[-u]
+    // solo part i (its first entry is the topic's solo entry rel): LDS for i <
+    // kSoloLds, else (and with keep_solo always) the record's front
+    auto put_solo = [&](uint32_t i, uint32_t off, uint32_t cnt, uint32_t rel) {
+      if (i < (uint32_t)kSoloLds) {
+        L.sp[2 * i] = off - rel;
+        L.sp[2 * i + 1] = rel;
+      } else if (i == (uint32_t)kSoloLds) {
+        L.q16 = rel;
+      }
+      if (i >= (uint32_t)kSoloLds || o.keep_solo) *reinterpret_cast<uint2 *>(rec + 2 * i) = make_uint2(off, cnt);
+    };
+#pragma unroll
+    for (int k = 0; k < kSoloLds / kG; k++) L.sp[2 * (gl + k * kG) + 1] = 0xFFFFFFFFu;
     if (len > 0xFFFFu) why = kWhyLevels;  // separators are kept as 16-bit positions
     uint32_t ni = nlev > 0 && why == kNoWhy ? root_items : 0, nh = 0, nsh = 0, nq = 0, nm = 0;
+    uint32_t qrun = 0;                 // the group's solo entries so far (group-uniform)
     uint32_t ls = 0, lm = 0, lh = 0;  // this lane's solo / multi / shared entries
     bool heavy = false;                // a gathered multi range with a heavy entry (kClsHeavy)
     int cur = 0;
@@ -522,7 +494,6 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
       // key == "+" / "#": the literal probe IS the wildcard probe (the
       // reference visits that child twice; no parent probe: topics.go:507)
       const bool lit_is_wild = (k1 == (1ull << 56)) && (k0 == '+' || k0 == '#');
-#if MQM_WALK_PRECHECK
       // the next level's key, for the filter check of the literal items this
       // level pushes (d + 1 < kLMax; the walk leaves at kLMax otherwise)
       uint64_t n0 = my_k0[0], n1 = my_k1[0];
@@ -531,7 +502,6 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
         if ((d + 1) / kG == (uint32_t)j) n0 = my_k0[j], n1 = my_k1[j];
       const uint64_t nk0 = shfl64(n0, gbase + (int)((d + 1) % kG)), nk1 = shfl64(n1, gbase + (int)((d + 1) % kG));
       const bool next_wild = (nk1 == (1ull << 56)) && (nk0 == '+' || nk0 == '#');
-#endif
       const uint32_t tst = d == 0 ? 0 : L.sep[d - 1] + 1;
       const uint32_t tln = ((d < nsep) ? L.sep[d] : len) - tst;
       uint32_t nnext = 0;
@@ -540,15 +510,9 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
         const bool live = it < ni;
         const uint32_t iw = L.item[cur][live ? it : 0];
         const uint32_t kind = iw & 3u, id = iw >> 2;
-        const bool lit = kind == kItemLit || kind == kItemLitB;
+        const bool lit = kind == kItemLit;
         NodeDesc dc;
-        uint32_t c;
-        if constexpr (kG == 4 && MQM_WALK_COOP)  // the group's four items loaded together (device.h)
-          c = walk_step_quad(s, live && lit && !lit_is_wild, live && !lit, kind == kItemLitB, id, id, k0, k1,
-                             tp + tst, tln, &dc, gl);
-        else
-          c = walk_step(s, live && lit && !lit_is_wild, live && !lit, kind == kItemLitB, id, id, k0, k1, tp + tst,
-                        tln, &dc);
+        const uint32_t c = walk_step(s, live && lit && !lit_is_wild, live && !lit, id, id, k0, k1, tp + tst, tln, &dc);
         const bool found = c != kNone;
 #if MQM_WALK_STATS
         {
@@ -574,7 +538,6 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
         // the '#' child's gather at the next level ('$' flag = this node's); after
         // a literal hit c_par gathered the same range (kFlagParentLit)
         const uint32_t c_hl = leaf && !skip_dollar && !lit ? dc.hsub_cnt : 0;
-#if MQM_WALK_PRECHECK
         // the pushed literal probe's filter word, loaded now: its round trip
         // overlaps this level's record writes, and a negative (or a '+' / '#'
         // next level, whose literal probe is the wildcard's) drops the item
@@ -582,7 +545,6 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
         const uint64_t nh2 = chk ? edge_hash(c, Key{nk0, nk1}) : 0;
         const uint64_t bw = chk ? s.bloom[bloom_word(nh2, s.bloom_mask)] : 0;
         const uint64_t bb = bloom_bits(nh2);
-#endif
         const uint32_t m_own = (uint32_t)(__ballot(c_own > 0) >> gbase) & kGMask;
         const uint32_t m_par = (uint32_t)(__ballot(c_par > 0) >> gbase) & kGMask;
         const uint32_t m_hl = (uint32_t)(__ballot(c_hl > 0) >> gbase) & kGMask;
@@ -619,31 +581,34 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
           const uint32_t i = nsh + __popc(m_sh & gmask_lt);
           *reinterpret_cast<uint2 *>(rec + kRecSh + 2 * i) = make_uint2(dc.sh_off, c_sh);
         }
-        // the solo parts, as (off, solo count) pairs from the record's start
-        const uint32_t q_own = (uint32_t)(__ballot(c_own > mu_own) >> gbase) & kGMask;
-        const uint32_t q_par = (uint32_t)(__ballot(c_par > mu_par) >> gbase) & kGMask;
-        const uint32_t q_hl = (uint32_t)(__ballot(c_hl > mu_hl) >> gbase) & kGMask;
-        if (active && c_own > mu_own)
-          *reinterpret_cast<uint2 *>(rec + 2 * (nq + __popc(q_own & gmask_lt))) =
-              make_uint2(dc.sub_off, c_own - mu_own);
-        if (active && c_par > mu_par)
-          *reinterpret_cast<uint2 *>(rec + 2 * (nq + __popc(q_own) + __popc(q_par & gmask_lt))) =
-              make_uint2(hoff, c_par - mu_par);
-        if (active && c_hl > mu_hl)
-          *reinterpret_cast<uint2 *>(rec + 2 * (nq + __popc(q_own) + __popc(q_par) + __popc(q_hl & gmask_lt))) =
-              make_uint2(hoff, c_hl - mu_hl);
-        nq += __popc(q_own) + __popc(q_par) + __popc(q_hl);
+        // the solo parts (off, solo count, rel), lane by lane (own, parent-'#',
+        // '#' leaf): one group scan of (parts << 28 | entries) gives every
+        // part its index and its first solo entry
+        const uint32_t so_own = c_own - mu_own, so_par = c_par - mu_par, so_hl = c_hl - mu_hl;
+        const uint32_t kp = (so_own > 0) + (so_par > 0) + (so_hl > 0);
+        const uint32_t pk = (kp << 28) | (so_own + so_par + so_hl);  // entries < 2^26, sums < 2^28
+        uint32_t pinc = pk;
+#pragma unroll
+        for (int dd = 1; dd < kG; dd <<= 1) {
+          const uint32_t u = __shfl_up(pinc, dd, kG);
+          if (gl >= dd) pinc += u;
+        }
+        const uint32_t ptot = __shfl(pinc, gbase + kG - 1, kWave);
+        if (active && kp) {
+          uint32_t pi = nq + ((pinc - pk) >> 28), pe = qrun + ((pinc - pk) & 0x0FFFFFFFu);
+          if (so_own) put_solo(pi++, dc.sub_off, so_own, pe), pe += so_own;
+          if (so_par) put_solo(pi++, hoff, so_par, pe), pe += so_par;
+          if (so_hl) put_solo(pi, hoff, so_hl, pe);
+        }
+        nq += ptot >> 28;
+        qrun += ptot & 0x0FFFFFFFu;
         // the next level's items (after the record writes: the frontier cap
         // needs the filter's answer; a topic leaving here goes to the DFS path)
-#if MQM_WALK_PRECHECK
-        // (at d + 1 == kLMax the item is kept: the next level routes the topic to the DFS path)
+        // (at d + 1 == kLMax the item is kept: the next level routes the topic to
+        // the DFS path; without a filter, every literal item unless the next
+        // level is '+' / '#')
         const bool lit_next = (fl & kFlagHasLiteral) &&
                               (d + 1 >= (uint32_t)kLMax || (s.bloom ? (chk && (bw & bb) == bb) : !next_wild));
-        const uint32_t lit_item = kItemLit;
-#else
-        const bool lit_next = fl & kFlagHasLiteral;
-        const uint32_t lit_item = lit_kind(dc.plus);
-#endif
         const uint32_t n_items = push ? ((lit_next ? 1u : 0u) + (dc.plus != kNone ? 1u : 0u) +
                                          (dc.hash != kNone && !leaf ? 1u : 0u))
                                       : 0u;
@@ -657,7 +622,7 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
         if (push) {
           uint32_t *nx = &L.item[cur ^ 1][nnext + __popc(m_i0 & gmask_lt) + 2 * __popc(m_i1 & gmask_lt)];
           uint32_t k = 0;
-          if (lit_next) nx[k++] = (c << 2) | lit_item;
+          if (lit_next) nx[k++] = (c << 2) | kItemLit;
           if (dc.plus != kNone) nx[k++] = (dc.plus << 2) | kItemPlus;
           if (dc.hash != kNone && !leaf) nx[k++] = (dc.hash << 2) | kItemHash;
         }
@@ -683,99 +648,146 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
     const uint32_t S = Ss + Ms;
     const bool any_heavy = ((__ballot(heavy) >> gbase) & kGMask) != 0;
     if (why == kNoWhy && S > kSMax) why = kWhyEntries;
+    const bool bounded = active && why == kNoWhy;
+
+    // ---- 3. output segments: one reservation for the wavefront's topics ----
+    // (raw entries S: solo entries at dstart, the merge's winners after them;
+    // DFS topics reserve nothing here: k_dfs writes them after dcur)
+    const uint32_t need = bounded && gl == 0 ? S : 0;
+    uint32_t inc = need;
+#pragma unroll
+    for (int dd = 1; dd < kWave; dd <<= 1) {
+      const uint32_t u = __shfl_up(inc, dd, kWave);
+      if (lane >= dd) inc += u;
+    }
+    const uint32_t tot = __shfl(inc, kWave - 1, kWave);   // < 2^28 (16 topics of <= kSMax)
+    const uint32_t ex = __shfl(inc - need, gbase, kWave);  // this group's offset
+    uint64_t base = 0;
+    auto reserve = [&](uint32_t k) {  // k entries of the output, one atomic (wave-uniform result)
+      uint64_t b = 0;
+      if (lane == 0) b = atomicAdd(&o.ctr->dcur, (unsigned long long)k);
+      // (readfirstlane returns int: widen through uint32_t, never sign-extend)
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(b >> 32));
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+      return ((uint64_t)hi << 32) | lo;
+    };
+    if (tot > kChunk / 2) {  // a large reservation: its own atomic, the chunk is kept
+      base = reserve(tot);
+    } else if (tot > 0) {
+      if (c_cur + tot > c_end) {
+        c_cur = reserve(kChunk);
+        c_end = c_cur + kChunk;
+      }
+      base = c_cur;
+      c_cur += tot;
+    }
+    const bool fits = base + tot <= o.dcap;  // wave-uniform
+    if (!fits && lane == 0) atomicOr(&o.ctr->oob, kOobWalk);  // the call is re-run with dout sized by dcur
+    const uint64_t ds = base + ex;
     if (active && gl == 0) {
-      const bool dfs = why != kNoWhy;
-      if (!dfs) tail[0] = make_uint4(nm | (nsh << 8), Ss, Ms, nq);
-      o.cls[t] = dfs ? kClsDfs
-                     : (S == 0 && H == 0) ? kClsDone
-                                          : (kClsBounded | (nm <= kSmallHits ? kClsFewHits : 0) | (any_heavy ? kClsHeavy : 0));
-      o.nsolo[t] = dfs ? 0 : nq;
-      o.scount[t] = dfs ? 0 : S;
-      o.hcount[t] = dfs ? 0 : H;
-      o.mcount[t] = dfs ? 0 : Ms;
-      o.dcount[t] = 0;
-      if (dfs) {
+      if (bounded && (Ms > 0 || nsh > 0 || o.keep_solo)) tail[0] = make_uint4(nm | (nsh << 8), Ss, Ms, nq);
+      o.cls[t] = !bounded ? kClsDfs
+                 : (S == 0 && H == 0) ? kClsDone
+                                      : (kClsBounded | (nm <= kSmallHits ? kClsFewHits : 0) | (any_heavy ? kClsHeavy : 0));
+      o.hcount[t] = bounded ? H : 0;
+      o.mcount[t] = bounded ? Ms : 0;
+      o.dstart[t] = ds;
+      o.dcount[t] = bounded && Ms == 0 ? Ss : 0;  // the merges write the others (k_dfs the DFS topics')
+      if (!bounded) {
         o.dfs_list[atomicAdd(&o.ctr->n_dfs, 1u)] = t;
         atomicAdd(&o.ctr->why[why], 1u);
       }
     }
+
+    // ---- 4. solo copy -----------------------------------------------------
+    // the entries of the group's LDS parts: all its solo entries, or those
+    // before its first record part
+    const uint32_t Qf = !bounded ? 0 : nq <= (uint32_t)kSoloLds ? Ss : L.q16;
+    // the groups' starts in the wavefront's solo space
+    const uint32_t qn = gl == 0 && fits ? Qf : 0;
+    uint32_t qinc = qn;
+#pragma unroll
+    for (int dd = 1; dd < kWave; dd <<= 1) {
+      const uint32_t u = __shfl_up(qinc, dd, kWave);
+      if (lane >= dd) qinc += u;
+    }
+    const uint32_t Qw = __shfl(qinc, kWave - 1, kWave);
+    if (gl == 0) {
+      C.F[g] = qinc - qn;
+      C.E[g] = ex;
+    }
+    if (lane == 0) C.F[kGroups] = Qw;
+    wave_lds_sync();
+    const __amdgpu_buffer_rsrc_t words = words_rsrc(s);
+    for (uint32_t b0 = 0; b0 < Qw; b0 += kWave * kCopyU) {
+      uint32_t sa[kCopyU], da[kCopyU], v[kCopyU];
+#pragma unroll
+      for (int u = 0; u < kCopyU; u++) {
+        const uint32_t q = b0 + u * kWave + lane;
+        uint32_t gg = 0;  // the group holding q: the largest gg with F[gg] <= q
+#pragma unroll
+        for (uint32_t st = kGroups / 2; st > 0; st >>= 1) gg = C.F[gg + st] <= q ? gg + st : gg;
+        const uint32_t p = q - C.F[gg];
+        const uint32_t *sp = WL[gg].sp;
+        uint32_t j = 0;  // its part: the largest j with rel[j] <= p
+#pragma unroll
+        for (uint32_t st = kSoloLds / 2; st > 0; st >>= 1) j = sp[2 * (j + st) + 1] <= p ? j + st : j;  // (~0 past the parts)
+        sa[u] = q < Qw ? sp[2 * j] + p : 0u;
+        da[u] = q < Qw ? C.E[gg] + p : ~0u;
+      }
+#pragma unroll
+      for (int u = 0; u < kCopyU; u++) v[u] = __builtin_amdgcn_raw_buffer_load_b32(words, (int)(sa[u] * 4u), 0, 0);
+#pragma unroll
+      for (int u = 0; u < kCopyU; u++)
+        if (da[u] != ~0u) o.dout[base + da[u]] = v[u];
+    }
+    // topics with more than kSoloLds solo parts: the rest from the record,
+    // part by part (a wavefront per part; rare: Zipf hub topics)
+    uint64_t ovm = __ballot(gl == 0 && bounded && fits && nq > (uint32_t)kSoloLds);
+    if (ovm) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wavefront's record stores have landed
+      __builtin_amdgcn_wave_barrier();
+    }
+    while (ovm) {
+      const int src = __ffsll((unsigned long long)ovm) - 1;
+      ovm &= ovm - 1;
+      const uint32_t tq = __shfl(t, src, kWave), nqq = __shfl(nq, src, kWave);
+      uint64_t at = shfl64(ds, src) + __shfl(Qf, src, kWave);
+      const uint32_t *rg = o.recs + (uint64_t)tq * kRecStrideAlloc;
+      for (uint32_t j = kSoloLds; j < nqq; j++) {
+        const uint32_t off = __hip_atomic_load(rg + 2 * j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t cnt = __hip_atomic_load(rg + 2 * j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (uint32_t i = lane; i < cnt; i += kWave)
+          o.dout[at + i] = __builtin_amdgcn_raw_buffer_load_b32(words, (int)((off + i) * 4u), 0, 0);
+        at += cnt;
+      }
+    }
+    if (gl == 0 && bounded) {
+      n_parts += nq;
+      if (n_solo + Ss < n_solo) atomicAdd(&o.ctr->n_solo, (unsigned long long)n_solo), n_solo = 0;
+      n_solo += Ss;
+    }
     wave_lds_sync();
   }
+  // the wavefront's solo parts (one atomic per wavefront, not per topic)
+#pragma unroll
+  for (int m = kWave / 2; m > 0; m >>= 1) n_parts += __shfl_xor(n_parts, m, kWave);
+  if (lane == 0 && n_parts) atomicAdd(&o.ctr->n_desc, (unsigned long long)n_parts);
+  if (n_solo) atomicAdd(&o.ctr->n_solo, (unsigned long long)n_solo);  // (group leaders)
 }
-
-// ---- walk visiting order (MQM_WALK_SORT): topics by length bucket --------------
-#if MQM_WALK_SORT
-constexpr int kLenBins = 32;
-__device__ __forceinline__ uint32_t len_bin(const uint64_t *toffs, uint32_t t) {
-  const uint64_t len = toffs[t + 1] - toffs[t];
-  return kLenBins - 1 - (uint32_t)min<uint64_t>(len >> 3, kLenBins - 1);  // longest first
-}
-
-__global__ __launch_bounds__(256) void k_len_hist(const uint64_t *__restrict__ toffs, uint32_t n,
-                                                  unsigned int *__restrict__ bins) {
-  __shared__ unsigned int c[kLenBins];
-  if (threadIdx.x < kLenBins) c[threadIdx.x] = 0;
-  __syncthreads();
-  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x)
-    atomicAdd(&c[len_bin(toffs, t)], 1u);
-  __syncthreads();
-  if (threadIdx.x < kLenBins && c[threadIdx.x]) atomicAdd(&bins[threadIdx.x], c[threadIdx.x]);
-}
-
-__global__ void k_len_prefix(unsigned int *bins) {  // one wavefront: counts -> exclusive starts
-  const int lane = threadIdx.x;
-  const unsigned int v = lane < kLenBins ? bins[lane] : 0;
-  unsigned int inc = v;
-  for (int d = 1; d < kLenBins; d <<= 1) {
-    const unsigned int u = __shfl_up(inc, d, 64);
-    if (lane >= d) inc += u;
-  }
-  if (lane < kLenBins) bins[lane] = inc - v;
-}
-
-__global__ __launch_bounds__(256) void k_len_scatter(const uint64_t *__restrict__ toffs, uint32_t n,
-                                                     unsigned int *__restrict__ cursor, uint32_t *__restrict__ perm) {
-  __shared__ unsigned int c[kLenBins], base[kLenBins];
-  for (uint32_t t0 = blockIdx.x * blockDim.x; t0 < n; t0 += gridDim.x * blockDim.x) {
-    if (threadIdx.x < kLenBins) c[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t t = t0 + threadIdx.x;
-    const uint32_t b = t < n ? len_bin(toffs, t) : 0;
-    const unsigned int r = t < n ? atomicAdd(&c[b], 1u) : 0;
-    __syncthreads();
-    if (threadIdx.x < kLenBins && c[threadIdx.x]) base[threadIdx.x] = atomicAdd(&cursor[threadIdx.x], c[threadIdx.x]);
-    __syncthreads();
-    if (t < n) perm[base[b] + r] = t;
-    __syncthreads();
-  }
-}
-#endif
 
 // ---------------------------------------------------------------------------
-// Emission.  A topic's deliveries are written at dstart[t] (the exclusive scan
-// of its raw-entry count S, an upper bound): first its solo entries, each its
-// client's merged delivery as is (delivery q = solo entry q), then the
+// Emission of the topics with multi entries.  A topic's deliveries are
+// written at dstart[t] (the walk's reservation of its raw-entry count S, an
+// upper bound): first its solo entries (the walk copied them), then the
 // winners of the merge of its multi entries, compacted.  dcount[t] = Ss +
-// winners.  The two parts are produced independently:
-//   solo   : k_desc turns every topic's solo hits into copy descriptors
-//            (src subs offset, length, absolute output position) in topic
-//            order, so the solo output is a set of disjoint, increasing
-//            ranges of dout; k_winmap / k_wincopy then copy it in fixed
-//            windows of the OUTPUT space (kWin entries, a wavefront each):
-//            perfectly balanced whatever the topic sizes (Zipf hubs and
-//            one-hit topics alike), one dependent setup load per window and
-//            lane-consecutive 8-B loads and stores.  k_desc also writes the
-//            shared candidates (id ranges) and dcount of topics without
-//            multi entries.
-//   merge  : topics with multi entries, by their count Ms (k_route lists):
-//            k_merge_small (8 lanes per topic, Ms <= 24, <= 15 hits),
-//            k_merge (a wavefront, Ms <= 192), k_multi<1024|2048>,
-//            k_multi_part.  They run on a second stream, concurrently with
-//            the solo copy (disjoint outputs).
-// The merge: an LDS hash table keyed by client — atomicOr folds QoS (one-hot)
-// and NoLocal, a 64-bit atomicMin keeps the lowest (hit rank, sid): exactly
-// Subscription.Merge (packets.go:250-270) with the first-merged
-// subscription's fields.
+// winners.  Merges by the topic's multi count Ms (k_route lists):
+// k_resolve<8|64> (by resolution, no table), k_merge_small (8 lanes per
+// topic, Ms <= 24, <= 15 hits), k_merge (a wavefront, Ms <= 192),
+// k_multi<1024|2048|4096>, k_multi_part.  The table merge: an LDS hash table
+// keyed by client — atomicOr folds QoS (one-hot) and NoLocal, a 64-bit
+// atomicMin keeps the lowest (hit rank, sid): exactly Subscription.Merge
+// (packets.go:250-270) with the first-merged subscription's fields.
 // ---------------------------------------------------------------------------
 
 // multi entry q of a topic: subs index and multi part
@@ -791,79 +803,6 @@ __device__ __forceinline__ SubEnt load_sub(const DeviceSnapshot &s, uint32_t sid
 }
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-
-// ---- k_desc: solo parts -> copy descriptors ----------------------------------
-// A wavefront per 64 consecutive topics.  Their descriptors are one contiguous
-// range of desc (desc_start is the exclusive scan of nsolo), so lane k writes
-// descriptor k of the range (coalesced 16-B stores): its topic by a 6-step
-// search over the wave's prefix of solo-part counts in LDS, its output
-// position by a segmented scan of the part sizes (running per-topic position
-// carried in LDS across 64-part steps).  Also dcount of topics without multi
-// entries (the merges write the others').  Round 1 ran a thread per topic:
-// scattered 16-B stores wrote 2.8x the descriptor bytes.
-struct alignas(8) DescLds {
-  unsigned long long run[kWave];  // next output position of each topic's solo part
-  uint32_t pre[kWave + 1];        // exclusive prefix of the topics' solo-part counts
-};
-
-__global__ __launch_bounds__(256) void k_desc(Outputs o, uint32_t n, const uint64_t *__restrict__ desc_start,
-                                              uint4 *__restrict__ desc, uint64_t desc_cap) {
-  __shared__ DescLds lds_all[4];
-  const int lane = threadIdx.x & (kWave - 1);
-  DescLds &L = lds_all[threadIdx.x / kWave];
-  const uint32_t nw = gridDim.x * (blockDim.x / kWave);
-  for (uint32_t w = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave; (uint64_t)w * kWave < n; w += nw) {
-    const uint32_t t0 = w * kWave, t = t0 + lane;
-    uint32_t q = 0;
-    uint64_t db = 0;
-    if (t < n) {
-      const uint8_t cls = o.cls[t];
-      if (cls & kClsBounded) {
-        q = o.nsolo[t];
-        db = o.dstart[t];
-        if (o.mcount[t] == 0) o.dcount[t] = o.scount[t];
-      }
-    }
-    uint32_t inc = q;  // inclusive scan of q over the wave
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-      const uint32_t v = __shfl_up(inc, d, kWave);
-      if (lane >= d) inc += v;
-    }
-    const uint32_t Q = __shfl(inc, kWave - 1, kWave);
-    if (Q == 0) continue;  // wave-uniform
-    L.pre[lane] = inc - q;
-    if (lane == 0) L.pre[kWave] = Q;
-    L.run[lane] = db;
-    const uint64_t pb = desc_start[t0];
-    wave_lds_sync();
-    for (uint32_t k0 = 0; k0 < Q; k0 += kWave) {
-      const uint32_t k = k0 + lane;
-      const bool valid = k < Q;
-      uint32_t j = 0;  // the topic holding part k: the largest j with pre[j] <= k
-#pragma unroll
-      for (uint32_t step = 32; step > 0; step >>= 1) j = L.pre[j + step] <= k ? j + step : j;  // j + step <= 63
-      uint2 part = make_uint2(0, 0);
-      if (valid) part = *reinterpret_cast<const uint2 *>(o.recs + (uint64_t)(t0 + j) * kRecStrideAlloc + 2 * (k - L.pre[j]));
-      const uint32_t seg = valid ? j : kWave;  // invalid lanes: a segment of their own, size 0
-      uint32_t si = part.y;
-#pragma unroll
-      for (int d = 1; d < kWave; d <<= 1) {
-        const uint32_t v = __shfl_up(si, d, kWave);
-        const uint32_t sj = __shfl_up(seg, d, kWave);
-        if (lane >= d && sj == seg) si += v;
-      }
-      const uint64_t at = valid ? L.run[j] + (si - part.y) : 0;
-      const bool seg_end = __shfl_down(seg, 1, kWave) != seg || lane == kWave - 1;
-      wave_lds_sync();
-      if (valid) {
-        put_checked(desc, pb + k, desc_cap, make_uint4(part.x, part.y, (uint32_t)at, (uint32_t)(at >> 32)), &o.ctr->oob);
-        if (seg_end) L.run[j] += si;
-      }
-      wave_lds_sync();
-    }
-  }
-}
 
 // ---- k_shared: shared candidates (gatherSharedSubscriptions, topics.go:541-555)
 // a 16-lane group per topic with H > 0: its shared hits are id ranges
@@ -881,148 +820,8 @@ __global__ __launch_bounds__(256) void k_shared(Outputs o, const uint32_t *__res
     uint32_t w = 0;
     for (uint32_t j = 0; j < nsh; j++) {
       const uint32_t so = grec[kRecSh + 2 * j], c = grec[kRecSh + 1 + 2 * j];
-      for (uint32_t j2 = gl; j2 < c; j2 += kHL) put_checked(o.hout, hb + w + j2, o.hcap, so + j2, &o.ctr->oob);
+      for (uint32_t j2 = gl; j2 < c; j2 += kHL) put_checked(o.hout, hb + w + j2, o.hcap, so + j2, &o.ctr->oob, kOobShared);
       w += c;
-    }
-  }
-}
-
-// window w of the output space [w * kWin, (w + 1) * kWin) -> the descriptor
-// holding (or, in a gap, preceding) its first position; windows before the
-// first descriptor map to it
-constexpr uint32_t kWin = 4096;
-// (counts read on the device: nd = solo descriptors, clamped to their buffer;
-// total = solo output positions; windows past win_cap flag the call)
-__global__ __launch_bounds__(256) void k_winmap(const uint4 *__restrict__ desc, const uint64_t *__restrict__ nd_ptr,
-                                                uint64_t desc_cap, const uint64_t *__restrict__ total_ptr,
-                                                uint32_t *__restrict__ win, uint64_t win_cap, unsigned int *oob) {
-  const uint64_t nd = min(*nd_ptr, desc_cap), total = *total_ptr;
-  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nd; j += (uint64_t)gridDim.x * blockDim.x) {
-    const uint4 a = desc[j];
-    const uint64_t d = a.z | ((uint64_t)a.w << 32);
-    uint64_t e = total;
-    if (j + 1 < nd) {
-      const uint4 b = desc[j + 1];
-      e = b.z | ((uint64_t)b.w << 32);
-    }
-    const uint64_t lo = j == 0 ? 0 : (d + kWin - 1) / kWin, hi = (e + kWin - 1) / kWin;
-    if (hi > win_cap) atomicOr(oob, 1u);
-    for (uint64_t w = lo; w < hi && w < win_cap; w++) win[w] = (uint32_t)j;
-  }
-}
-
-// ---- k_wincopy: the solo deliveries, a wavefront per output window ----------
-// Loads 64 descriptors from the window's first one (one coalesced 16-B load
-// per lane), clips them to the window in LDS, then moves kCU entries per lane
-// and step: position q -> its descriptor by a 6-step search over the clipped
-// starts -> words[src + q - start] -> dout[q] (the word IS the packed
-// delivery: a 4-B copy, lane-consecutive loads and stores).  More than 64
-// descriptors in a window (many tiny topics): the next 64, from where the
-// previous batch ended.
-#ifndef MQM_WINCOPY_CU
-#define MQM_WINCOPY_CU 16
-#endif
-constexpr int kCU = MQM_WINCOPY_CU;  // entries per lane per step (tuning knob)
-// MQM_WINCOPY_BLK=1: position -> descriptor through a per-64-position block
-// index (the last descriptor starting at or before each block, one search per
-// block and descriptor batch), then a search inside the block's few
-// descriptors — usually none or one step instead of six per entry
-#ifndef MQM_WINCOPY_BLK
-#define MQM_WINCOPY_BLK 1
-#endif
-struct alignas(16) WinLds {
-  uint32_t st[kWave], en[kWave], src[kWave];
-  uint32_t blk[kWin / kWave];
-};
-
-__global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_eu(8))) void k_wincopy(
-    DeviceSnapshot s, const uint4 *__restrict__ desc, const uint64_t *__restrict__ nd_ptr, uint64_t desc_cap,
-    const uint32_t *__restrict__ win, uint64_t win_cap, const uint64_t *__restrict__ total_ptr,
-    uint32_t *__restrict__ out, uint64_t cap, unsigned int *oob) {
-  __shared__ WinLds lds_all[kEmitWaves];
-  const uint64_t nd = min(*nd_ptr, desc_cap), total = *total_ptr;
-  const uint64_t nwin = min((total + kWin - 1) / kWin, win_cap);
-  const int lane = threadIdx.x & (kWave - 1);
-  WinLds &L = lds_all[threadIdx.x / kWave];
-  // words through a buffer descriptor: 32-bit offsets, bounds-checked reads
-  const __amdgpu_buffer_rsrc_t words =
-      __builtin_amdgcn_make_buffer_rsrc((void *)s.words, (short)0, (int)(s.n_subs * 4u + 64u), 0x00020000);
-  const uint64_t nw = (uint64_t)gridDim.x * kEmitWaves;
-  for (uint64_t w = (uint64_t)blockIdx.x * kEmitWaves + threadIdx.x / kWave; w < nwin; w += nw) {
-    const uint64_t g0 = w * kWin, g1 = min(g0 + kWin, total);
-    uint64_t j = win[w];
-    uint64_t pos = g0;
-    while (pos < g1 && j < nd) {
-      const uint64_t jj = j + lane;
-      uint4 d = make_uint4(0, 0, 0xFFFFFFFFu, 0xFFFFFFFFu);
-      if (jj < nd) d = desc[jj];
-      const uint64_t dst = d.z | ((uint64_t)d.w << 32);
-      const uint64_t dend = jj < nd ? dst + d.y : ~0ull;
-      uint64_t a = dst > pos ? dst : pos, b = dend < g1 ? dend : g1;
-      if (b < a) b = a;
-      if (a > g1) a = b = g1;
-      // positions handled by this batch: up to the end of its last descriptor
-      const uint64_t last_end = shfl64(dend, kWave - 1);
-      const uint64_t bend = j + kWave < nd ? (last_end < g1 ? (last_end > pos ? last_end : pos) : g1) : g1;
-      L.st[lane] = (uint32_t)(a - g0);
-      L.en[lane] = (uint32_t)(b - g0);
-      L.src[lane] = d.x + (uint32_t)(a - dst);
-      wave_lds_sync();
-#if MQM_WINCOPY_BLK
-      {  // block lane (positions lane * 64 ..): the last descriptor starting at or before its start
-        static_assert(kWin / kWave == kWave, "one block per lane");
-        const uint32_t q = (uint32_t)lane * kWave;
-        uint32_t k = 0;
-#pragma unroll
-        for (uint32_t step = 32; step > 0; step >>= 1) k = L.st[k + step] <= q ? k + step : k;
-        L.blk[lane] = k;
-      }
-      wave_lds_sync();
-#endif
-      const uint32_t q0 = (uint32_t)(pos - g0), q1 = (uint32_t)(bend - g0);
-      for (uint32_t base = q0; base < q1; base += kWave * kCU) {
-        uint32_t sa[kCU];
-        bool in[kCU];
-#pragma unroll
-        for (int u = 0; u < kCU; u++) {
-          const uint32_t q = base + u * kWave + lane;
-#if MQM_WINCOPY_BLK
-          // the last descriptor starting at or before q: within [blk[b], blk[b + 1]]
-          const uint32_t bq = min(q, (uint32_t)kWin - 1) / kWave;
-          uint32_t k = L.blk[bq], left = (bq + 1 < kWin / kWave ? L.blk[bq + 1] : kWave - 1) - k;
-          while (left > 0) {
-            const uint32_t half = (left + 1) / 2;
-            if (L.st[k + half] <= q) {
-              k += half;
-              left -= half;
-            } else {
-              left = half - 1;
-            }
-          }
-#else
-          uint32_t k = 0;  // the last descriptor starting at or before q
-#pragma unroll
-          for (uint32_t step = 32; step > 0; step >>= 1) k = L.st[k + step] <= q ? k + step : k;  // k + step <= 63
-#endif
-          in[u] = q < q1 && q >= L.st[k] && q < L.en[k];
-          sa[u] = in[u] ? L.src[k] + (q - L.st[k]) : 0u;
-        }
-        uint32_t v[kCU];
-#pragma unroll
-        for (int u = 0; u < kCU; u++) v[u] = __builtin_amdgcn_raw_buffer_load_b32(words, (int)(sa[u] * 4u), 0, 0);
-#pragma unroll
-        for (int u = 0; u < kCU; u++) {
-          if (!in[u]) continue;
-          const uint64_t p = g0 + base + u * kWave + lane;
-          if (p < cap)
-            put_out(out + p, v[u]);
-          else
-            atomicOr(oob, 1u);
-        }
-      }
-      wave_lds_sync();
-      pos = bend;
-      j += kWave;
     }
   }
 }
@@ -1212,11 +1011,7 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_merge(DeviceSnapshot s, O
 // in table-slot order: each wave scans a quarter of the table twice (count,
 // then write at its prefix), so the layout is deterministic.
 // ---------------------------------------------------------------------------
-// k_multi's table: >= 2 slots per entry (MQM_MERGE_DENSE=1: >= 4/3, fewer
-// slots to clear and scan, longer probe runs; tuning knob)
-#ifndef MQM_MERGE_DENSE
-#define MQM_MERGE_DENSE 0
-#endif
+// k_multi's table: >= 2 slots per entry
 
 struct alignas(16) MultiLds {
   uint32_t rec[kRecLds];
@@ -1280,87 +1075,6 @@ __device__ __forceinline__ uint32_t block_winners(MergeTable tb, uint32_t nslots
   return total;
 }
 
-// MQM_MULTI_PIPE=1: software-pipelined k_multi (tuning knob) — while topic i is merged,
-// topic i+1's multi entries (client, word, rank) are already loading into
-// registers (its record double-buffered in LDS, topic i+2's record in
-// flight), so a topic no longer waits a dependent HBM round trip for its
-// entries after its record (the tier is latency-bound: ~400 entries a topic
-// at C3, 256 threads)
-#ifndef MQM_MULTI_PIPE
-#define MQM_MULTI_PIPE 0  // measured slower on C3 (r03e: 16.99 vs 16.01 ms per batch, same box): off
-#endif
-#if MQM_MULTI_PIPE
-template <int kSlots>
-__global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs o, const uint32_t *__restrict__ list,
-                                                      const unsigned int *__restrict__ count) {
-  constexpr int kMPer = (kSlots * 3 / 4 + kBigThreads - 1) / kBigThreads;  // entries per thread at the tier's cap
-  __shared__ unsigned long long tfirst[kSlots], tkb[kSlots];
-  __shared__ MultiLds L[2];
-  const MergeTable tb{tkb, tfirst};
-  const int tid = threadIdx.x;
-  const uint32_t nb = *count;
-  const uint32_t g = gridDim.x;
-  uint32_t cl[kMPer], wd[kMPer], rk[kMPer];  // the current topic's entries (registers)
-  auto load_entries = [&](const uint32_t *rec, uint32_t (&c)[kMPer], uint32_t (&w)[kMPer], uint32_t (&r)[kMPer]) {
-    const uint32_t nh = rec[0] & 0xFFu, M = rec[2];
-#pragma unroll
-    for (int k = 0; k < kMPer; k++) {
-      const uint32_t q = tid + k * kBigThreads;
-      c[k] = w[k] = r[k] = 0;
-      if (q < M) {  // (slots past the topic's entries: no LDS search, no load)
-        uint32_t h;
-        const uint32_t sid = multi_sid(rec, nh, q, &h);
-        const SubEnt e = load_sub(s, sid);
-        c[k] = e.client;
-        w[k] = e.word;
-        r[k] = rec_at(rec, h, kFieldRank);
-      }
-    }
-  };
-  NextTopic nx;
-  uint32_t t_cur = 0, t_nxt = 0;
-  uint64_t db_cur = 0, db_nxt = 0;
-  // prologue: records of the first two topics in LDS, the first one's entries in registers
-  nx.fetch(o, list, blockIdx.x, nb);
-  t_cur = nx.t, db_cur = nx.db;
-  block_record(nx, L[0].rec);
-  nx.fetch(o, list, blockIdx.x + g, nb);
-  t_nxt = nx.t, db_nxt = nx.db;
-  block_record(nx, L[1].rec);
-  nx.fetch(o, list, blockIdx.x + 2 * g, nb);
-  if (blockIdx.x < nb) load_entries(L[0].rec, cl, wd, rk);
-  int b = 0;
-  for (uint32_t bi = blockIdx.x; bi < nb; bi += g, b ^= 1) {
-    const uint32_t *rec = L[b].rec;
-    const uint32_t Ss = rec[1], M = rec[2];
-    // the next topic's entries: loads in flight while this topic merges
-    uint32_t ncl[kMPer], nwd[kMPer], nrk[kMPer];
-    if (bi + g < nb) load_entries(L[b ^ 1].rec, ncl, nwd, nrk);
-    uint32_t lg = 6;
-    const uint32_t need = MQM_MERGE_DENSE ? (4 * M + 2) / 3 : 2 * M;
-    while ((1u << lg) < need && (1u << lg) < (uint32_t)kSlots) lg++;
-    const uint32_t mask = (1u << lg) - 1;
-    for (uint32_t i = tid; i <= mask; i += kBigThreads) mt_clear(tb, i);
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kMPer; k++)
-      if (tid + k * kBigThreads < M) mt_insert(tb, mask, lg, cl[k], wd[k], rk[k]);
-    __syncthreads();
-    const uint32_t D = block_winners(tb, mask + 1, L[b].wsum, o, db_cur, Ss);
-    if (tid == 0) o.dcount[t_cur] = D;
-    // topic bi + 2g's record (fetched a topic ago) replaces this one's, whose
-    // reads are all done; topic bi + 3g's record starts loading
-    block_record(nx, L[b].rec);
-    const uint32_t t_nn = nx.t;
-    const uint64_t db_nn = nx.db;
-    nx.fetch(o, list, bi + 3 * g, nb);
-#pragma unroll
-    for (int k = 0; k < kMPer; k++) cl[k] = ncl[k], wd[k] = nwd[k], rk[k] = nrk[k];
-    t_cur = t_nxt, db_cur = db_nxt;
-    t_nxt = t_nn, db_nxt = db_nn;
-  }
-}
-#else
 template <int kSlots>
 __global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs o, const uint32_t *__restrict__ list,
                                                       const unsigned int *__restrict__ count) {
@@ -1378,7 +1092,7 @@ __global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs
     nx.fetch(o, list, bi + gridDim.x, nb);
     const uint32_t nh = L.rec[0] & 0xFFu, Ss = L.rec[1], M = L.rec[2];
     uint32_t lg = 6;
-    const uint32_t need = MQM_MERGE_DENSE ? (4 * M + 2) / 3 : 2 * M;
+    const uint32_t need = 2 * M;
     while ((1u << lg) < need && (1u << lg) < (uint32_t)kSlots) lg++;
     const uint32_t mask = (1u << lg) - 1;
     for (uint32_t i = tid; i <= mask; i += kBigThreads) mt_clear(tb, i);
@@ -1394,7 +1108,6 @@ __global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs
     if (tid == 0) o.dcount[t] = D;
   }
 }
-#endif
 
 // client -> partition: a hash independent of table_slot's (which takes the
 // top bits of client * 2654435769: a partition must spread over the table)
@@ -1436,7 +1149,7 @@ __global__ __launch_bounds__(kBigThreads) void k_multi_part(DeviceSnapshot s, Ou
         const SubEnt e = load_sub(s, sid);
         if (partition_of(e.client, P) != p) continue;
         if (atomicAdd(&fill, 1u) >= kFill) {  // never for a hash of this spread: fail, do not spin
-          atomicOr(&o.ctr->oob, 1u);
+          atomicOr(&o.ctr->oob, kOobPart);
           continue;
         }
         mt_insert(tb, kSlots - 1, 12, e.client, e.word, rec_at(L.rec, h, kFieldRank));
@@ -1474,14 +1187,12 @@ __global__ __launch_bounds__(kBigThreads) void k_multi_part(DeviceSnapshot s, Ou
 // ms against a threshold of 769).  Read at every batch (a test compares modes in one process):
 // MQM_RESOLVE=1 every light topic, MQM_RESOLVE=0 none (= MQM_NO_RESOLVE=1),
 // MQM_RESOLVE_MIN=m the threshold.
-#ifndef MQM_RESOLVE_MIN_DEFAULT
-#define MQM_RESOLVE_MIN_DEFAULT 193u
-#endif
+constexpr uint32_t kResolveMinDefault = 193;
 static uint32_t resolve_min() {
   if (const char *v = getenv("MQM_RESOLVE")) return atoi(v) != 0 ? 1u : 0xFFFFFFFFu;
   if (const char *v = getenv("MQM_NO_RESOLVE")) return atoi(v) == 0 ? 1u : 0xFFFFFFFFu;
   if (const char *v = getenv("MQM_RESOLVE_MIN")) return (uint32_t)std::max(1L, atol(v));
-  return MQM_RESOLVE_MIN_DEFAULT;
+  return kResolveMinDefault;
 }
 
 template <int kH>
@@ -1575,7 +1286,7 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_resolve(DeviceSnapshot s,
         };
         if (win) {
           if (pi[k].y == kPInfoHeavy) {  // routed here by mistake: never expected (kClsHeavy)
-            atomicOr(&o.ctr->oob, 1u);
+            atomicOr(&o.ctr->oob, kOobHeavy);
           } else if (pi[k].y != kNone && (pi[k].y & kPInfoList)) {  // (kNone: one inline partner)
             const uint32_t c = pi[k].y & 0xFFu;
             for (uint32_t j = 0; j < c; j++) meet(s.partners[pi[k].x + j]);
@@ -1653,7 +1364,7 @@ __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *
           put_checked(o.dout, db + w + __popcll(m & lanemask_lt(lane)), o.dcap,
                       pack_delivery((uint32_t)~gg.first & kWordSidMask, 31u - __builtin_clz(bits & 7u),
                                     (bits >> 3) & 1u),
-                      &o.ctr->oob);
+                      &o.ctr->oob, kOobDfs);
         }
         w += __popcll(m);
       }
@@ -1787,7 +1498,7 @@ __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *
         }
         const uint32_t shc = e.sh_cnt_flags & kShCntMask;
         if (kPhase == 1)
-          for (uint32_t j = lane; j < shc; j += kWave) put_checked(o.hout, hb + H + j, o.hcap, e.sh_off + j, &o.ctr->oob);
+          for (uint32_t j = lane; j < shc; j += kWave) put_checked(o.hout, hb + H + j, o.hcap, e.sh_off + j, &o.ctr->oob, kOobDfs);
         H += shc;
         if (has_next && (fl & kFlagHasChildren)) {
           if (lane == 0) {
@@ -1919,13 +1630,13 @@ __global__ __launch_bounds__(256) void k_zero_tab(unsigned long long *__restrict
     tab[i] = 0;
 }
 
-// what the call needed, for the host (read back once, at the end)
-__global__ void k_totals(Counters *ctr, const uint64_t *__restrict__ dstart, const uint64_t *__restrict__ hstart,
-                         const uint64_t *__restrict__ desc_start, uint32_t n) {
+// what the call needed, for the host: the walk's reservations (dstart[n]: the
+// DFS tails start there) and the shared candidates' total
+__global__ void k_totals(Counters *ctr, uint64_t *__restrict__ dstart, const uint64_t *__restrict__ hstart, uint32_t n) {
   if (threadIdx.x == 0) {
-    ctr->s_total = dstart[n];
+    ctr->s_total = ctr->dcur;
+    dstart[n] = ctr->dcur;
     ctr->h_total = hstart[n];
-    ctr->n_desc = desc_start[n];
   }
 }
 
@@ -2059,29 +1770,6 @@ int Workspace::end(hipStream_t st) {
   return 0;
 }
 
-int Workspace::fork(hipStream_t st, hipStream_t *out) {
-  if (!side && hipStreamCreateWithFlags(&side, hipStreamNonBlocking) != hipSuccess) {
-    side = nullptr;
-    return -3;
-  }
-  if (!fork_ev && hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming) != hipSuccess) {
-    fork_ev = nullptr;
-    return -3;
-  }
-  if (hipEventRecord(fork_ev, st) != hipSuccess || hipStreamWaitEvent(side, fork_ev, 0) != hipSuccess) return -3;
-  *out = side;
-  return 0;
-}
-
-int Workspace::join(hipStream_t st, hipStream_t side_st) {
-  if (!join_ev && hipEventCreateWithFlags(&join_ev, hipEventDisableTiming) != hipSuccess) {
-    join_ev = nullptr;
-    return -3;
-  }
-  if (hipEventRecord(join_ev, side_st) != hipSuccess || hipStreamWaitEvent(st, join_ev, 0) != hipSuccess) return -3;
-  return 0;
-}
-
 int Workspace::drain() {
   if (cur && hipStreamSynchronize(cur) != hipSuccess) return -3;
   if (used && last_use && hipEventSynchronize(last_use) != hipSuccess) return -3;
@@ -2140,12 +1828,6 @@ Workspace::~Workspace() {
   for (auto &b : bufs)
     if (b.p) (void)hipFree(b.p);
   if (last_use) (void)hipEventDestroy(last_use);
-  if (side) {
-    (void)hipStreamSynchronize(side);
-    (void)hipStreamDestroy(side);
-  }
-  if (fork_ev) (void)hipEventDestroy(fork_ev);
-  if (join_ev) (void)hipEventDestroy(join_ev);
   if (host_pinned) (void)hipHostFree(host_pinned);
   for (auto &e : ev)
     if (e) (void)hipEventDestroy(e);
@@ -2232,22 +1914,17 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
   using W = Workspace;
   if (ws.pending) return -1;  // one call in flight per workspace (collect it first)
   // queued calls need every output buffer sized by an earlier call
-  // (MQM_QUEUED=0: every call exact, for A/B runs)
-  static const bool queued_ok = !getenv("MQM_QUEUED") || atoi(getenv("MQM_QUEUED")) != 0;
-  exact = exact || !ws.caps_known || !queued_ok;
-  if (ws.get(W::kSCount, sizeof(uint32_t) * (n + 1)) || ws.get(W::kHCount, sizeof(uint32_t) * (n + 1)) ||
-      ws.get(W::kDCount, sizeof(uint32_t) * (n + 1)) || ws.get(W::kDStart, sizeof(uint64_t) * (n + 1)) ||
-      ws.get(W::kHStart, sizeof(uint64_t) * (n + 1)) || ws.get(W::kCls, n + 1) ||
-      ws.get(W::kDfsList, sizeof(uint32_t) * (n + 2)) || ws.get(W::kMCount, sizeof(uint32_t) * (n + 1)) ||
-      ws.get(W::kRecs, sizeof(uint32_t) * kRecStrideAlloc * ((uint64_t)n + 1)) || ws.get(W::kCounters, 256) ||
-      ws.get(W::kNSolo, sizeof(uint32_t) * (n + 1)) || ws.get(W::kDescStart, sizeof(uint64_t) * (n + 1)))
+  exact = exact || !ws.caps_known;
+  if (ws.get(W::kHCount, sizeof(uint32_t) * (n + 1)) || ws.get(W::kDCount, sizeof(uint32_t) * (n + 1)) ||
+      ws.get(W::kDStart, sizeof(uint64_t) * (n + 1)) || ws.get(W::kHStart, sizeof(uint64_t) * (n + 1)) ||
+      ws.get(W::kCls, n + 1) || ws.get(W::kDfsList, sizeof(uint32_t) * (n + 2)) ||
+      ws.get(W::kMCount, sizeof(uint32_t) * (n + 1)) ||
+      ws.get(W::kRecs, sizeof(uint32_t) * kRecStrideAlloc * ((uint64_t)n + 1)) || ws.get(W::kCounters, 256))
     return -2;
   Counters *hc = pinned_counters(ws);
   if (!hc) return -2;
-  uint64_t *hp = ws.pinned_u64();
 
-  Outputs o;
-  o.scount = (uint32_t *)ws.ptr(W::kSCount);
+  Outputs o{};
   o.hcount = (uint32_t *)ws.ptr(W::kHCount);
   o.dcount = (uint32_t *)ws.ptr(W::kDCount);
   o.dstart = (uint64_t *)ws.ptr(W::kDStart);
@@ -2257,52 +1934,7 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
   o.mcount = (uint32_t *)ws.ptr(W::kMCount);
   o.recs = (uint32_t *)ws.ptr(W::kRecs);
   o.ctr = (Counters *)ws.ptr(W::kCounters);
-  o.nsolo = (uint32_t *)ws.ptr(W::kNSolo);
-  o.perm = nullptr;
-  auto *desc_start = (uint64_t *)ws.ptr(W::kDescStart);
-  const int walk_g = ws.walk_lanes;
-  HIP_TRY(hipMemsetAsync(o.ctr, 0, sizeof(Counters), st));
-  mark(ws, 0, st);
-#if MQM_WALK_SORT
-  if (n > 0) {
-    if (ws.get(W::kPerm, sizeof(uint32_t) * (n + 1)) || ws.get(W::kPermBins, sizeof(unsigned int) * kLenBins))
-      return -2;
-    auto *bins = (unsigned int *)ws.ptr(W::kPermBins);
-    HIP_TRY(hipMemsetAsync(bins, 0, sizeof(unsigned int) * kLenBins, st));
-    const uint32_t gb = std::min<uint32_t>((n + 255) / 256, 2048);
-    hipLaunchKernelGGL(k_len_hist, dim3(gb), dim3(256), 0, st, d_offs, n, bins);
-    hipLaunchKernelGGL(k_len_prefix, dim3(1), dim3(64), 0, st, bins);
-    hipLaunchKernelGGL(k_len_scatter, dim3(gb), dim3(256), 0, st, d_offs, n, bins, (uint32_t *)ws.ptr(W::kPerm));
-    HIP_TRY(hipGetLastError());
-    o.perm = (const uint32_t *)ws.ptr(W::kPerm);
-  }
-#endif
-  if (n > 0) {
-    auto launch_walk = [&](auto kern, int g) {
-      const uint32_t per_block = kWalkWaves * (kWave / g);
-      const uint32_t blocks =
-          std::max<uint32_t>(1, std::min<uint32_t>((n + per_block - 1) / per_block, resident_blocks(ws, 0, kern)));
-      hipLaunchKernelGGL(kern, dim3(blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o);
-    };
-    if (walk_g == 4)
-      launch_walk(k_walk<4, MQM_WALK_OCC>, 4);
-    else if (walk_g == 16)
-      launch_walk(k_walk<16, MQM_WALK_OCC>, 16);
-    else
-      launch_walk(k_walk<8, MQM_WALK_OCC>, 8);
-  }
-  HIP_TRY(hipGetLastError());
-  // MQM_FLUSH=1 (A/B): hand the queued walk to the device now (hipStreamQuery
-  // flushes the runtime's pending dispatches) instead of with later commands
-  static const bool flush = getenv("MQM_FLUSH") && atoi(getenv("MQM_FLUSH")) != 0;
-  if (flush) (void)hipStreamQuery(st);
-  mark(ws, 1, st);
-  // segment starts: exclusive scans of S (raw entries, an upper bound of a
-  // topic's deliveries) and H (shared candidates); the solo descriptors'
-  // positions: exclusive scan of the solo-hit counts
-  if (scan_offsets(ws, (const uint32_t *)o.scount, o.dstart, n, st) ||
-      scan_offsets(ws, (const uint32_t *)o.hcount, o.hstart, n, st) || scan_offsets(ws, o.nsolo, desc_start, n, st))
-    return -3;
+  o.keep_solo = ws.keep_solo ? 1u : 0u;
   // merge lists
   const W::Slot list_slots[kNLists] = {W::kListS, W::kListW, W::kListT1, W::kListT2, W::kListT3,
                                        W::kListP, W::kListH, W::kListRS, W::kListR};
@@ -2312,17 +1944,58 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
     lists.l[l] = (uint32_t *)ws.ptr(list_slots[l]);
   }
   unsigned int *lcount = &o.ctr->n_small;  // kNLists consecutive counters
-  if (n > 0) {
-    hipLaunchKernelGGL(k_route, dim3(std::min<uint32_t>((n + 4095) / 4096, 2048)), dim3(256), 0, st, o.cls, o.mcount,
-                       o.hcount, n, lists, lcount, o.ctr->m_sum, resolve_min());
+  // capacity of a buffer in elements (one element kept spare, as the exact sizing does)
+  auto cap_of = [&](W::Slot sl, size_t elem) -> uint64_t {
+    const size_t c = ws.bufs[sl].cap / elem;
+    return c ? c - 1 : 0;
+  };
+
+  // walk (tokenize, walk, reserve the output segments, copy the solo
+  // entries into dout), the shared candidates' offsets, the merge lists, the
+  // totals.  A walk whose reservations outgrow dout flags oob and copies
+  // nothing past it.
+  auto walk_phase = [&](uint64_t dcap) -> int {
+    o.dout = (uint32_t *)ws.ptr(W::kDOut);
+    o.dcap = o.dout ? dcap : 0;
+    HIP_TRY(hipMemsetAsync(o.ctr, 0, sizeof(Counters), st));
+    mark(ws, 0, st);
+    if (n > 0) {
+      constexpr uint32_t per_block = kWalkWaves * (kWave / kWalkG);
+      const uint32_t blocks = std::max<uint32_t>(
+          1, std::min<uint32_t>((n + per_block - 1) / per_block, resident_blocks(ws, 0, k_walk<kWalkG>)));
+      hipLaunchKernelGGL(k_walk<kWalkG>, dim3(blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o);
+    }
     HIP_TRY(hipGetLastError());
-  }
-  hipLaunchKernelGGL(k_totals, dim3(1), dim3(64), 0, st, o.ctr, o.dstart, o.hstart, desc_start, n);
-  HIP_TRY(hipGetLastError());
-  if (exact) {  // the one read-back that sizes the outputs
+    mark(ws, 1, st);
+    if (scan_offsets(ws, (const uint32_t *)o.hcount, o.hstart, n, st)) return -3;
+    if (n > 0) {
+      hipLaunchKernelGGL(k_route, dim3(std::min<uint32_t>((n + 4095) / 4096, 2048)), dim3(256), 0, st, o.cls,
+                         o.mcount, o.hcount, n, lists, lcount, o.ctr->m_sum, resolve_min());
+      HIP_TRY(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_totals, dim3(1), dim3(64), 0, st, o.ctr, o.dstart, o.hstart, n);
+    HIP_TRY(hipGetLastError());
+    return 0;
+  };
+  // exact: read the reservations back (the one read-back that sizes the
+  // outputs) and walk again into a dout that holds them if it did not; the
+  // chunked reservations vary a little from run to run, so a rerun gets the
+  // 25 % headroom every buffer gets
+  uint64_t dcap = cap_of(W::kDOut, sizeof(uint32_t));
+  for (int attempt = 0;; attempt++) {
+    if (int rc = walk_phase(dcap)) return rc;
+    if (!exact) break;
     HIP_TRY(hipMemcpyAsync(hc, o.ctr, sizeof(Counters), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    if (hc->s_total <= o.dcap && !(hc->oob & kOobWalk)) break;
+    if (attempt == 3) {
+      fprintf(stderr, "mqmatch: the walk's output reservations kept outgrowing their buffer\n");
+      return -3;
+    }
+    if (ws.get(W::kDOut, sizeof(uint32_t) * (hc->s_total + hc->s_total / 8 + 1))) return -2;
+    dcap = cap_of(W::kDOut, sizeof(uint32_t));
   }
+
   // DFS topics (a capacity of the walk exceeded): phase 0 counts each one's
   // raw entries, k_dfs_prep sizes their tables and tails on the device
   const bool dfs = !exact || hc->n_dfs > 0;
@@ -2341,7 +2014,7 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
   }
   o.dfs_cap = dfs_cap;
   const uint32_t fb_blocks = exact ? std::max<uint32_t>(1, std::min<uint32_t>(hc->n_dfs, 4096)) : 1024;
-  uint64_t dcap, hcap, desc_cap, win_cap, tab_cap = 0;
+  uint64_t hcap, tab_cap = 0;
   if (exact) {
     if (dfs) {
       hipLaunchKernelGGL(k_dfs<0>, dim3(fb_blocks), dim3(kWave), fb_lds, st, s, d_bytes, d_offs, o, raw_cnt, raw_h,
@@ -2355,29 +2028,18 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
     }
     dcap = hc->s_total + hc->dfs_raw;
     hcap = hc->h_total + hc->dfs_h;
-    desc_cap = hc->n_desc;
-    win_cap = (hc->s_total + kWin - 1) / kWin;
     tab_cap = hc->tab_total;
-  } else {  // what the buffers hold (one element kept spare, as the exact sizing does)
-    auto cap_of = [&](W::Slot sl, size_t elem) -> uint64_t {
-      const size_t c = ws.bufs[sl].cap / elem;
-      return c ? c - 1 : 0;
-    };
-    dcap = cap_of(W::kDOut, sizeof(uint32_t));
+    // (dout keeps the walk's solo deliveries when it grows for the DFS tails)
+    if (ws.grow_keep(W::kDOut, sizeof(uint32_t) * hc->s_total, sizeof(uint32_t) * (dcap + 1), st)) return -2;
+  } else {  // what the buffers hold
     hcap = cap_of(W::kHOut, sizeof(uint32_t));
-    desc_cap = cap_of(W::kDesc, sizeof(uint4));
-    win_cap = cap_of(W::kWin, sizeof(uint32_t));
     tab_cap = std::max<uint64_t>(cap_of(W::kTable, sizeof(GEnt)), 1u << 16);
   }
-  if (ws.get(W::kDOut, sizeof(uint32_t) * (dcap + 1)) || ws.get(W::kHOut, sizeof(uint32_t) * (hcap + 1)) ||
-      ws.get(W::kDesc, sizeof(uint4) * (desc_cap + 1)) || ws.get(W::kWin, sizeof(uint32_t) * (win_cap + 1)))
-    return -2;
+  if (ws.get(W::kHOut, sizeof(uint32_t) * (hcap + 1))) return -2;
   o.dout = (uint32_t *)ws.ptr(W::kDOut);
   o.hout = (uint32_t *)ws.ptr(W::kHOut);
   o.dcap = dcap;
   o.hcap = hcap;
-  auto *desc = (uint4 *)ws.ptr(W::kDesc);
-  auto *win = (uint32_t *)ws.ptr(W::kWin);
   GEnt *tab = nullptr;
   if (dfs) {
     if (ws.get(W::kTable, sizeof(GEnt) * (tab_cap + 1))) return -2;
@@ -2399,10 +2061,8 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
   mark(ws, 2, st);
   static_assert(kWave * kEmitWaves == kBigThreads, "resident_blocks assumes 256-thread blocks");
   if (n > 0) {
-    // merges on the side stream, concurrently with the solo copy (they write
-    // disjoint parts of dout and dcount: winners after Ss / topics with Ms > 0);
-    // a queued call launches every list's kernel (each reads its count)
-    // (a queued call: the lists the last collected call had topics in)
+    // a queued call launches the merge / shared kernels of the lists the last
+    // collected call had topics in (each reads its count from the device)
     uint32_t launched = 0;
     auto has_list = [&](uint32_t c, int list) {
       const bool l = exact ? c > 0 : ((ws.lists_seen >> list) & 1u) != 0;
@@ -2414,89 +2074,56 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
                l_part = has_list(hc->n_part, kLPart), l_sh = has_list(hc->n_shlist, kLShared),
                l_rs = has_list(hc->n_res_small, kLResSmall), l_r = has_list(hc->n_res, kLRes);
     ws.pend_launched = launched;
-    auto has = [&](uint32_t c) { return !exact || c > 0; };
-    const bool merges = l_small || l_wave || l_t1 || l_t2 || l_t3 || l_part || l_rs || l_r;
-    const bool side = merges && ws.overlap;
-    // persistent grids: with both streams busy, each takes its share of the device
-    const uint32_t side_pct = side ? MQM_SIDE_PCT : 100, main_pct = side && MQM_SIDE_PCT < 100 ? 100 - MQM_SIDE_PCT : 100;
-    auto grid = [&](auto kern) {
-      return dim3(std::max<uint32_t>(1, resident_blocks(ws, 0, kern) * side_pct / 100));
-    };
-    auto main_grid = [&](auto kern) {
-      return dim3(std::max<uint32_t>(1, resident_blocks(ws, 0, kern) * main_pct / 100));
-    };
-    hipStream_t ms = st;
-    if (merges) {
-      if (side && ws.fork(st, &ms)) return -3;
-      // MQM_MERGE_BIG_FIRST=1: the workgroup merges first, the small-topic
-      // merges last (they fill the device better at the end of the stream)
-      auto big = [&]() -> int {
-        if (l_r) {
-          hipLaunchKernelGGL((k_resolve<kWave, kHCap, 4>), grid((k_resolve<kWave, kHCap, 4>)),
-                             dim3(kWave * kEmitWaves), 0, ms, s, o, lists.l[kLRes], lcount + kLRes);
-          HIP_TRY(hipGetLastError());
-        }
-        if (l_t1) {
-          hipLaunchKernelGGL(k_multi<1024>, grid(k_multi<1024>), dim3(kBigThreads), 0, ms, s, o, lists.l[kLT1],
-                             lcount + kLT1);
-          HIP_TRY(hipGetLastError());
-        }
-        if (l_t2) {
-          hipLaunchKernelGGL(k_multi<2048>, grid(k_multi<2048>), dim3(kBigThreads), 0, ms, s, o, lists.l[kLT2],
-                             lcount + kLT2);
-          HIP_TRY(hipGetLastError());
-        }
-        if (l_t3) {
-          hipLaunchKernelGGL(k_multi<4096>, grid(k_multi<4096>), dim3(kBigThreads), 0, ms, s, o, lists.l[kLT3],
-                             lcount + kLT3);
-          HIP_TRY(hipGetLastError());
-        }
-        if (l_part) {
-          hipLaunchKernelGGL(k_multi_part, grid(k_multi_part), dim3(kBigThreads), 0, ms, s, o, lists.l[kLPart],
-                             lcount + kLPart);
-          HIP_TRY(hipGetLastError());
-        }
-        return 0;
-      };
-      auto small = [&]() -> int {
-        if (l_rs) {
-          hipLaunchKernelGGL((k_resolve<kSmallLanes, 16, 3>), grid((k_resolve<kSmallLanes, 16, 3>)),
-                             dim3(kWave * kEmitWaves), 0, ms, s, o, lists.l[kLResSmall], lcount + kLResSmall);
-          HIP_TRY(hipGetLastError());
-        }
-        if (l_small) {
-          hipLaunchKernelGGL((k_merge_small<6>), grid(k_merge_small<6>), dim3(kWave * kEmitWaves), 0, ms, s, o,
-                             lists.l[kLSmall], lcount + kLSmall);
-          HIP_TRY(hipGetLastError());
-        }
-        if (l_wave) {
-          hipLaunchKernelGGL(k_merge, grid(k_merge), dim3(kWave * kEmitWaves), 0, ms, s, o, lists.l[kLWave],
-                             lcount + kLWave);
-          HIP_TRY(hipGetLastError());
-        }
-        return 0;
-      };
-      if (MQM_MERGE_BIG_FIRST ? (big() || small()) : (small() || big())) return -3;
+    // persistent grids: the blocks that fit on the device at once
+    auto grid = [&](auto kern) { return dim3(std::max<uint32_t>(1, resident_blocks(ws, 0, kern))); };
+    // the workgroup merges first, the small-topic merges last (they fill the
+    // device better at the end of the stream)
+    if (l_r) {
+      hipLaunchKernelGGL((k_resolve<kWave, kHCap, 4>), grid((k_resolve<kWave, kHCap, 4>)), dim3(kWave * kEmitWaves),
+                         0, st, s, o, lists.l[kLRes], lcount + kLRes);
+      HIP_TRY(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_desc, dim3(std::min<uint32_t>((n + 255) / 256, 8192)), dim3(256), 0, st, o, n, desc_start,
-                       desc, desc_cap);  // a wavefront per 64 topics
-    HIP_TRY(hipGetLastError());
+    if (l_t1) {
+      hipLaunchKernelGGL(k_multi<1024>, grid(k_multi<1024>), dim3(kBigThreads), 0, st, s, o, lists.l[kLT1],
+                         lcount + kLT1);
+      HIP_TRY(hipGetLastError());
+    }
+    if (l_t2) {
+      hipLaunchKernelGGL(k_multi<2048>, grid(k_multi<2048>), dim3(kBigThreads), 0, st, s, o, lists.l[kLT2],
+                         lcount + kLT2);
+      HIP_TRY(hipGetLastError());
+    }
+    if (l_t3) {
+      hipLaunchKernelGGL(k_multi<4096>, grid(k_multi<4096>), dim3(kBigThreads), 0, st, s, o, lists.l[kLT3],
+                         lcount + kLT3);
+      HIP_TRY(hipGetLastError());
+    }
+    if (l_part) {
+      hipLaunchKernelGGL(k_multi_part, grid(k_multi_part), dim3(kBigThreads), 0, st, s, o, lists.l[kLPart],
+                         lcount + kLPart);
+      HIP_TRY(hipGetLastError());
+    }
+    if (l_rs) {
+      hipLaunchKernelGGL((k_resolve<kSmallLanes, 16, 3>), grid((k_resolve<kSmallLanes, 16, 3>)),
+                         dim3(kWave * kEmitWaves), 0, st, s, o, lists.l[kLResSmall], lcount + kLResSmall);
+      HIP_TRY(hipGetLastError());
+    }
+    if (l_small) {
+      hipLaunchKernelGGL((k_merge_small<6>), grid(k_merge_small<6>), dim3(kWave * kEmitWaves), 0, st, s, o,
+                         lists.l[kLSmall], lcount + kLSmall);
+      HIP_TRY(hipGetLastError());
+    }
+    if (l_wave) {
+      hipLaunchKernelGGL(k_merge, grid(k_merge), dim3(kWave * kEmitWaves), 0, st, s, o, lists.l[kLWave],
+                         lcount + kLWave);
+      HIP_TRY(hipGetLastError());
+    }
     if (l_sh) {
       const uint32_t nsh = exact ? hc->n_shlist : n;
       hipLaunchKernelGGL(k_shared, dim3(std::min<uint32_t>((nsh + 15) / 16, 8192)), dim3(256), 0, st, o,
                          lists.l[kLShared], lcount + kLShared);
       HIP_TRY(hipGetLastError());
     }
-    if (has((uint32_t)std::min<uint64_t>(hc->n_desc, 1))) {
-      const uint64_t nd_grid = exact ? hc->n_desc : desc_cap;
-      hipLaunchKernelGGL(k_winmap, dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nd_grid + 255) / 256, 8192))),
-                         dim3(256), 0, st, desc, desc_start + n, desc_cap, o.dstart + n, win, win_cap, &o.ctr->oob);
-      HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(k_wincopy, main_grid(k_wincopy), dim3(kWave * kEmitWaves), 0, st, s, desc, desc_start + n,
-                         desc_cap, win, win_cap, o.dstart + n, o.dout, o.dcap, &o.ctr->oob);
-      HIP_TRY(hipGetLastError());
-    }
-    if (side && ws.join(st, ms)) return -3;
   }
   if (dfs) {
     hipLaunchKernelGGL(k_dfs<1>, dim3(fb_blocks), dim3(kWave), fb_lds, st, s, d_bytes, d_offs, o, raw_cnt, raw_h,
@@ -2517,11 +2144,11 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
     HIP_TRY(hipcub::DeviceReduce::Sum(ws.ptr(W::kScanTmp), tmp, hc_it, &o.ctr->h_sum, n, st));
     HIP_TRY(hipMemcpyAsync(hc, o.ctr, sizeof(Counters), hipMemcpyDeviceToHost, st));
   }
-  (void)hp;
   ws.last_valid = false;  // until collected
   ws.last_n = n;
   ws.last_bytes = d_bytes;
   ws.last_offs = d_offs;
+  ws.last_keep_solo = ws.keep_solo;
   ws.pend_exact = exact;
   ws.pending = true;
   return 0;
@@ -2538,7 +2165,8 @@ int match_collect(Workspace &ws, hipStream_t st, MatchOutput *out) {
   ws.dfs_cap = std::max<uint32_t>(ws.dfs_cap, std::max<uint32_t>(1024, hc->n_dfs + hc->n_dfs / 4));
   if (hc->oob || hc->cap_ovf) {
     if (ws.pend_exact) {  // sized exactly from this call's own counts: never expected
-      fprintf(stderr, "mqmatch: an output store fell outside its buffer (batch rejected)\n");
+      fprintf(stderr, "mqmatch: an output store fell outside its buffer (batch rejected; oob %#x, cap_ovf %u)\n",
+              hc->oob, hc->cap_ovf);
       return -3;
     }
     return 1;  // outgrew buffers sized by an earlier call: match_device re-runs it, exact
@@ -2581,6 +2209,7 @@ int match_collect(Workspace &ws, hipStream_t st, MatchOutput *out) {
   for (int i = 0; i < 3; i++) out->multi_entries[i] = hc->m_sum[i];
   out->n_part = hc->n_part;
   out->n_resolve = hc->n_res_small + hc->n_res;
+  out->n_solo = hc->n_solo;
   out->n_merge_small = hc->n_small;
   out->n_merge_wave = hc->n_wmerge;
   out->n_solo_ranges = hc->n_desc;
@@ -2610,7 +2239,7 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
 int identifiers_device(const DeviceSnapshot &s, Workspace &ws, hipStream_t st, IdentOutput *out) {
   using W = Workspace;
   const uint32_t n = ws.last_n;
-  if (!ws.last_valid) return -1;
+  if (!ws.last_valid || !ws.last_keep_solo) return -1;  // (the walk kept the solo parts in LDS only)
   if (ws.get(W::kICount, sizeof(uint32_t) * (n + 1)) || ws.get(W::kIStart, sizeof(uint64_t) * (n + 1))) return -2;
   Outputs o{};
   o.cls = (uint8_t *)ws.ptr(W::kCls);

@@ -30,11 +30,13 @@ def _rows(res):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("threads,identifiers", [(16, True), (16, False)])
-def test_batched_subscribers_concurrent_equal_plain(threads, identifiers, monkeypatch):
+@pytest.mark.parametrize("threads,identifiers,linger_us", [(16, True, 0), (16, False, 0), (32, False, 300)])
+def test_batched_subscribers_concurrent_equal_plain(threads, identifiers, linger_us, monkeypatch):
     """identifiers=False: batches take the small-batch path (fast.hip);
     identifiers=True: mqm_match_batch.  `plain` is the batch pipeline
-    (MQM_NO_FAST=1) in both cases."""
+    (MQM_NO_FAST=1) in both cases.  linger_us > 0 with the collector's
+    several workers: two workers can wait out the linger on one queue and the
+    first takes it all (the other must not run an empty batch)."""
     w = mqgen.generate(1, n_filters=20000, n_topics=3200, p_shared=0.05)
     monkeypatch.setenv("MQM_NO_FAST", "1")
     plain = maxmq_amd.TopicsIndex(device=0, identifiers=identifiers)
@@ -45,6 +47,8 @@ def test_batched_subscribers_concurrent_equal_plain(threads, identifiers, monkey
     plain.close()
 
     idx = maxmq_amd.TopicsIndex(device=0, identifiers=identifiers, batching=True)
+    if linger_us:
+        idx.batching_policy(0, linger_us)
     idx.subscribe_workload(w)
     idx.commit()
     L = capi.lib()

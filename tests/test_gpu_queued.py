@@ -156,3 +156,20 @@ def test_queued_merge_lists_that_were_empty():
             assert r.n_resolve + r.n_big >= 5 and r.n_shared > 0
     assert ctx.requeued() >= 2, "merge / shared lists unseen by the previous call must re-run the batch"
     ctx.close()
+
+
+def test_index_destroy_refused_while_a_context_lives():
+    """mqm_destroy returns MQM_EINVAL while a match context of the index is
+    alive (a context reads its index) and leaves the index usable; the Python
+    wrapper closes its contexts first"""
+    from maxmq_amd import capi
+
+    w = mqgen.generate(1, n_filters=2000, n_topics=100)
+    idx = maxmq_amd.TopicsIndex(0)
+    idx.subscribe_workload(w)
+    ctx = idx.match_context()
+    assert capi.lib().mqm_destroy(idx._h) == capi.MQM_EINVAL
+    res = idx.match_batch(w.topics.data, w.topics.offs)  # still usable
+    assert res.n == len(w.topics)
+    idx.close()  # closes ctx, then the index
+    assert not ctx._c
