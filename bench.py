@@ -54,6 +54,12 @@ def parse():
                     help="replicas: full trie per GPU, own batch each; sharded: subscriber shards over all GPUs, "
                          "one batch; hybrid: --shards subscriber shards x (GPUs / --shards) topic replicas")
     ap.add_argument("--shards", type=int, default=2, help="hybrid: subscriber shards per replica group")
+    ap.add_argument("--gather", choices=["host", "device"], default="host",
+                    help="sharded/hybrid: host = every shard runs the host path (runs form) over the whole batch "
+                         "and its clients' deliveries land in its own pinned host memory over its own PCIe link "
+                         "(no data-path collective); device = the shards' dense lists go to the group leader "
+                         "over RCCL and mqm_gather_shards lays out one node-wide CSR there (bound by the "
+                         "leader's xGMI ingress, DESIGN §6)")
     ap.add_argument("--gather-budget-gb", type=float, default=48.0,
                     help="sharded/hybrid: HBM the group leader may hold for one gathered chunk (received lists "
                          "+ laid-out node CSR); topics per gather are sized from it (shard.plan_chunk)")
@@ -66,7 +72,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-topics", type=int, default=500000,
                     help="PCIe-inclusive host path (mqm_match_batch): topics per call, outside the timed region; 0 = skip")
-    ap.add_argument("--host-threads", type=int, default=4,
+    ap.add_argument("--host-threads", type=int, default=8,
                     help="host path: concurrent callers (each its own stream), batches overlapped across them")
     ap.add_argument("--pipeline", type=int, default=0,
                     help="timed steps through the queued device API on this many contexts / streams (a step "
@@ -241,7 +247,17 @@ def main():
     to = torch.from_numpy(w.topics.offs.view(np.int64)).to(dev)
     stream = torch.cuda.current_stream(dev)
     chunk = n
-    if sharded:
+    if sharded and args.gather == "host":
+        # every shard runs the host path over the group's whole batch: the
+        # batch is node input in host memory (every rank process holds the
+        # same generated topics, as a shared pinned buffer would); each shard
+        # matches it against its client range and its deliveries land in its
+        # own pinned host memory, consumed on its caller threads (iterate)
+        hrun, _, hper, hnb, _, _ = host_runner(idx, w, args, "runs")
+        for _ in range(2):
+            hrun(args.host_threads, 0)
+        log(f"[rank {rank}] group {grp} shard {my_shard}/{k}: host gather, {hnb} calls of {hper} topics per step")
+    if sharded and args.gather == "device":
         from maxmq_amd.devbuf import copy_from_ptr
 
         # shard client id -> node client id (the generator's global client
@@ -322,6 +338,9 @@ def main():
             pipe["ctxs"][c].submit(tb.data_ptr(), to.data_ptr(), n, pipe["streams"][c].cuda_stream)
             pipe["pend"][c] = True
             return r_, (int(r_.n_deliveries) if r_ else 0), (int(r_.n_shared) if r_ else 0)
+        if sharded and args.gather == "host":
+            _, nd_ = hrun(hnb, 1)
+            return None, nd_, 0
         if sharded:
             # the publish batch enters at the group leader and is broadcast over
             # xGMI (RCCL); every shard matches it chunk by chunk and its dense
@@ -406,9 +425,9 @@ def main():
         # per-GPU side measurements at N = 1 only (the contract's cpu_baseline
         # leg; host path and latency are per-GPU properties too); at N > 1 the
         # oracle runs only a short sample for the roofline's algorithmic bytes
-        host = host_path(idx, w, args) if args.host_topics and world == 1 else None
+        host = host_path(idx, w, args, "runs") if args.host_topics and world == 1 else None
         if host:
-            host["packed"] = host_path(idx, w, args, packed=True)
+            host["packed"] = host_path(idx, w, args, "packed")
         steady = steady_state(idx, tb, to, n, dev, args) if world == 1 and not shard_of and args.steady_steps else None
         lat = latency(idx, w, args) if args.latency_topics and world == 1 else None
         if not args.no_cpu_baseline:
@@ -435,7 +454,9 @@ def main():
             "config": {
                 "workload": (f"mqgen config {args.config} shard {shard_of[0]}/{shard_of[1]} (client range), " if shard_of
                              else f"mqgen config {args.config} {args.mode} over {world} GPU(s) ({len(groups)} "
-                                  f"group(s) of {k} subscriber shards, {chunk} topics per gather), rank 0 holds "
+                                  f"group(s) of {k} subscriber shards, " + (
+                                      f"{chunk} topics per gather to the group leader" if args.gather == "device" else
+                                      "each shard's results to its own pinned host memory, runs form") + "), rank 0 holds "
                              if sharded else f"mqgen config {args.config}: ") + f"{len(w.filters)} filters "
                             f"({w.params['p_plus']:.0%} '+', {w.params['p_hash']:.0%} '#', "
                             f"topic Zipf s={w.params['topic_zipf_s']}), {n}-topic batch, depth<={w.params['max_depth']}",
@@ -458,6 +479,10 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "host_path": host,
+            # SURVEY §8(d)'s end-to-end definition (pinned topics in -> usable
+            # per-topic rows in host memory), beside the HBM-resident `value`
+            "end_to_end": ({"value": host["value"], "unit": "topics/s", "form": host["form"],
+                            "consume": host["consume"]} if host else None),
             "steady_state": steady,
             "single_topic_latency": lat,
         }
@@ -504,68 +529,48 @@ def steady_state(idx, tb, to, n, dev, args):
                     "steps earlier; no read-back inside a batch (outputs sized by the contexts' first batch)"}
 
 
-def host_path(idx, w, args, packed=False):
-    """The boundary's host form, mqm_match_batch, as a broker would drive it
-    (SURVEY §8d end-to-end): topics in pinned host memory -> H2D -> the match
-    pipeline -> dense CSR D2H into pinned, library-owned result blocks.
-    --host-threads callers each take --host-topics-topic batches of the C3
-    batch in turn; every caller has its own workspace and HIP stream
-    (include/mqmatch.h, Threading), so one batch's copies overlap another's
-    kernels.  Timed outside the headline's region.  `pcie_bound` = the same
-    bytes at the link rates measured here (H2D and D2H run concurrently)."""
+def host_path(idx, w, args, form="runs"):
+    """The boundary's host form as a broker drives it (SURVEY §8d end to end):
+    topics in pinned host memory -> H2D -> the match pipeline -> result D2H
+    into pinned, library-owned blocks -> consumed on the calling thread.
+    --host-threads native callers (tools/conc_driver.cpp mqd_host_path; no
+    interpreter lock) each take --host-topics-topic batches of the C3 batch in
+    turn, each with its own workspace and HIP stream (include/mqmatch.h,
+    Threading), so one batch's copies and consumption overlap another's
+    kernels.  form "packed": mqm_match_batch_packed (4 B per delivery over
+    PCIe); "runs": mqm_match_batch_runs (8 B per solo run, 4 B per merged
+    winner).  Consumption: "to_host" (the result in host memory), "iterate"
+    (every delivery read once, as the cgo shim's loop over a topic's
+    subscribers), "expand" (plain packed rows, mqm_result_expand).  Timed
+    outside the headline's region.  `pcie_bound` = the same bytes at the link
+    rates measured here (H2D and D2H run concurrently)."""
     import ctypes as C
-    import threading
 
     import torch
 
     from maxmq_amd import capi
 
     L = capi.lib()
-    fn = L.mqm_match_batch_packed if packed else L.mqm_match_batch
-    per = min(args.host_topics, len(w.topics))
-    nb = max(1, len(w.topics) // per)
-    data = torch.from_numpy(w.topics.data).pin_memory()
-    offs = torch.from_numpy(w.topics.offs[: nb * per + 1].astype(np.int64)).pin_memory()
-    dp, op = data.data_ptr(), offs.data_ptr()
-
-    def call(b):
-        res = C.c_void_p()
-        capi.check("mqm_match_batch", fn(idx._h, C.c_void_p(dp), C.c_void_p(op + 8 * b * per), per, C.byref(res)))
-        d = int(C.cast(L.mqm_result_offsets(res), C.POINTER(C.c_uint64))[per])
-        L.mqm_result_free(res)
-        return d
-
+    run, fn, per, nb, dp, op = host_runner(idx, w, args, form)
     # warm every caller's context (workspace sizing, pinned result blocks):
     # contexts come from a pool, so only concurrent calls create one each
     for _ in range(2):
-        warm = [threading.Thread(target=call, args=(t % nb,)) for t in range(args.host_threads)]
-        for th in warm:
-            th.start()
-        for th in warm:
-            th.join()
-    done = [0, 0]
-    lock = threading.Lock()
-    nxt = [0]
-
-    def worker():
-        while True:
-            with lock:
-                b = nxt[0]
-                nxt[0] += 1
-            if b >= nb:
-                return
-            d = call(b)
-            with lock:
-                done[0] += per
-                done[1] += d
-
-    t0 = time.perf_counter()
-    ths = [threading.Thread(target=worker) for _ in range(args.host_threads)]
-    for th in ths:
-        th.start()
-    for th in ths:
-        th.join()
-    dt = time.perf_counter() - t0
+        run(args.host_threads, 0)
+    # the bytes one batch moves (batch 0), for the PCIe model
+    res = C.c_void_p()
+    capi.check("host path", fn(idx._h, C.c_void_p(dp), C.c_void_p(op), per, C.byref(res)))
+    win = int(C.cast(L.mqm_result_offsets(res), C.POINTER(C.c_uint64))[per])
+    sh = int(C.cast(L.mqm_result_shared_offsets(res), C.POINTER(C.c_uint64))[per])
+    ro, rr, rw, nw = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_uint64()
+    n_runs = 0
+    if L.mqm_result_runs(res, C.byref(ro), C.byref(rr), C.byref(rw), C.byref(nw)) == 0:
+        n_runs = int(C.cast(ro, C.POINTER(C.c_uint64))[per])
+    L.mqm_result_free(res)
+    out_per_batch = 8 * n_runs + 4 * win + 4 * sh + (24 if form == "runs" else 16) * per
+    legs = {}
+    for consume, name in ((0, "to_host"), (1, "iterate"), (2, "expand")):
+        dt, nd = run(nb, consume)
+        legs[name] = {"value": nb * per / dt, "deliveries_per_s": nd / dt, "ms_per_call": dt * 1e3 * args.host_threads / nb}
     # link rates: 1 GiB pinned <-> device, each direction alone
     dev = torch.device("cuda", torch.cuda.current_device())
     g = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
@@ -580,18 +585,63 @@ def host_path(idx, w, args, packed=False):
         torch.cuda.synchronize()
         rates[name] = 3 * (1 << 30) / (time.perf_counter() - t1)
     del g, h
-    n = done[0]
-    in_b = int(w.topics.offs[nb * per]) + 8 * n
-    out_b = (4 if packed else 8) * done[1] + 16 * n
+    n = nb * per
+    in_b = int(w.topics.offs[n]) + 8 * n
+    out_b = out_per_batch * nb
     bound_s = max(in_b / rates["h2d"], out_b / rates["d2h"])
-    return {"value": n / dt, "unit": "topics/s", "topics_per_call": per, "calls": nb, "threads": args.host_threads,
-            "ms_per_call": dt * 1e3 * args.host_threads / nb, "deliveries_per_s": done[1] / dt,
+    best = legs["iterate"]
+    return {"value": best["value"], "unit": "topics/s", "consume": "iterate", "form": form, "legs": legs,
+            "topics_per_call": per, "calls": nb, "threads": args.host_threads,
+            "d2h_bytes_per_topic": out_b / n, "runs_per_topic": n_runs / per, "winners_per_topic": win / per,
             "h2d_GBps": rates["h2d"] / 1e9, "d2h_GBps": rates["d2h"] / 1e9,
-            "pcie_bound_topics_per_s": n / bound_s, "frac_of_pcie_bound": (n / dt) / (n / bound_s),
-            "delivery_bytes": 4 if packed else 8,
-            "note": "pinned topics in -> match -> dense CSR into pinned result blocks (" +
-                    ("mqm_match_batch_packed: 4-B packed words" if packed else "mqm_match_batch: 8-B {client, packed}") +
-                    "); pcie_bound = max(H2D bytes / H2D rate, D2H bytes / D2H rate)"}
+            "pcie_bound_topics_per_s": n / bound_s, "frac_of_pcie_bound": best["value"] / (n / bound_s),
+            "note": "pinned topics in -> match -> result into pinned blocks -> consumed on the calling thread (" +
+                    ("mqm_match_batch_runs: 8-B solo runs of the host word table + 4-B merged winners"
+                     if form == "runs" else "mqm_match_batch_packed: 4-B packed words") +
+                    "); native caller threads (tools/conc_driver.cpp); pcie_bound = max(H2D bytes / H2D rate, "
+                    "D2H bytes / D2H rate)"}
+
+
+def host_runner(idx, w, args, form="runs"):
+    """The native host-path driver (tools/conc_driver.cpp mqd_host_path) over
+    --host-topics-topic batches of w's topics in pinned memory -> (run,
+    batch entry point, topics per call, calls per pass, data / offsets
+    pointers); run(n_batches, consume) -> (seconds, deliveries)."""
+    import ctypes as C
+
+    import torch
+
+    from maxmq_amd import capi
+
+    L = capi.lib()
+    D, _ = _driver()
+    vp = C.c_void_p
+
+    class HApi(C.Structure):
+        _fields_ = [("batch", vp), ("offsets", vp), ("packed", vp), ("runs", vp), ("expand", vp), ("result_free", vp)]
+
+    fn = L.mqm_match_batch_runs if form == "runs" else L.mqm_match_batch_packed
+    api = HApi(C.cast(fn, vp), C.cast(L.mqm_result_offsets, vp), C.cast(L.mqm_result_packed, vp),
+               C.cast(L.mqm_result_runs, vp), C.cast(L.mqm_result_expand, vp), C.cast(L.mqm_result_free, vp))
+    D.mqd_host_path.argtypes = [C.POINTER(HApi), vp, vp, vp, C.c_uint32, C.c_uint32, C.c_int, C.c_int,
+                                C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    D.mqd_host_path.restype = C.c_int64
+    per = min(args.host_topics, len(w.topics))
+    nb = max(1, len(w.topics) // per)
+    data = torch.from_numpy(w.topics.data).pin_memory()
+    offs = torch.from_numpy(w.topics.offs[: nb * per + 1].astype(np.int64)).pin_memory()
+    dp, op = data.data_ptr(), offs.data_ptr()
+    d, c = C.c_uint64(), C.c_uint64()
+    keep = (data, offs, api)  # alive as long as run is
+
+    def run(n_batches, consume):
+        ns = D.mqd_host_path(C.byref(keep[2]), idx._h, C.c_void_p(dp), C.c_void_p(op), per, n_batches,
+                             args.host_threads, consume, C.byref(d), C.byref(c))
+        if ns < 0:
+            raise RuntimeError(f"host path ({form}) call failed")
+        return ns * 1e-9, d.value
+
+    return run, fn, per, nb, dp, op
 
 
 def _driver():

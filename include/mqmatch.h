@@ -240,6 +240,24 @@ int mqm_match_batch(mqm_index *h, const char *topic_bytes, const uint64_t *topic
  * and the device-to-host copy halves (the host path is PCIe-bound). */
 int mqm_match_batch_packed(mqm_index *h, const char *topic_bytes, const uint64_t *topic_offsets, uint32_t n_topics,
                            mqm_result **out);
+/* The runs form: the PCIe-bound host path without a 4-byte transfer per
+ * delivery.  ~90 % of deliveries are solo entries (a subscription whose
+ * client meets no other of its subscriptions in the topic is its client's
+ * merged delivery as it stands, packets.go:250-270), and a gathered node's
+ * solo entries are one contiguous run of the snapshot's packed-word table —
+ * which the host built and keeps.  So a topic's deliveries are its runs,
+ * words[run.off .. run.off + run.count) for runs[run_offsets[t] ..
+ * run_offsets[t+1]) (mqm_result_runs), then its merged winners,
+ * packed[offsets[t] .. offsets[t+1]) (mqm_result_offsets / _packed).
+ * mqm_result_expand writes the plain packed rows of a topic range (e.g. one
+ * range per consumer thread).  Only 8 B per run and 4 B per winner cross
+ * PCIe.  Replaces Subscribers (topics.go:484-555) like mqm_match_batch; the
+ * same sets, same Identifiers support. */
+typedef struct {
+  uint32_t off, count;
+} mqm_run;
+int mqm_match_batch_runs(mqm_index *h, const char *topic_bytes, const uint64_t *topic_offsets, uint32_t n_topics,
+                         mqm_result **out);
 /* single-topic convenience == Subscribers(topic) (batched across concurrent
  * callers with MQM_CFG_BATCHING) */
 int mqm_subscribers(mqm_index *h, const char *topic, size_t topic_len, mqm_result **out);
@@ -390,7 +408,16 @@ int mqm_messages_device(mqm_index *h, const uint8_t *d_filter_bytes, const uint6
 uint32_t mqm_result_num_topics(const mqm_result *r);
 const uint64_t *mqm_result_offsets(const mqm_result *r);          /* n + 1          */
 const mqm_delivery *mqm_result_deliveries(const mqm_result *r); /* NULL for a packed result */
-const uint32_t *mqm_result_packed(const mqm_result *r);         /* packed words (mqm_match_batch_packed) */
+const uint32_t *mqm_result_packed(const mqm_result *r);         /* packed words (mqm_match_batch_packed;
+                                                                   the runs form: merged winners only) */
+/* the runs form's solo runs and the snapshot's packed-word table they index
+ * (owned by the result's snapshot); MQM_EINVAL for any other result */
+int mqm_result_runs(const mqm_result *r, const uint64_t **run_offsets, const mqm_run **runs, const uint32_t **words,
+                    uint64_t *n_words);
+/* topics [t0, t1) of a packed or runs-form result as plain packed rows:
+ * offsets[0 .. t1 - t0] (relative to dst), dst the rows back to back (NULL:
+ * offsets only, to size dst).  Thread-safe on disjoint ranges. */
+int mqm_result_expand(const mqm_result *r, uint32_t t0, uint32_t t1, uint64_t *offsets, uint32_t *dst);
 const uint64_t *mqm_result_shared_offsets(const mqm_result *r);   /* n + 1          */
 const uint32_t *mqm_result_shared(const mqm_result *r);           /* shared sub ids */
 /* resolve a delivery's first_sub / a shared sub id (snapshot-relative) */

@@ -108,12 +108,28 @@ class BatchResult:
 
         self.offsets = arr(L.mqm_result_offsets(handle), n + 1, np.uint64)
         self.shared_offsets = arr(L.mqm_result_shared_offsets(handle), n + 1, np.uint64)
+        # the runs form (mqm_match_batch_runs): solo runs of the snapshot's words
+        # + merged winners, expanded here (mqm_result_expand) into plain rows
+        self.runs_form = False
+        ro, rr, rw, nw = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_uint64()
+        expanded = None
+        if n and L.mqm_result_runs(handle, C.byref(ro), C.byref(rr), C.byref(rw), C.byref(nw)) == 0:
+            self.runs_form = True
+            self.run_offsets = arr(ro.value, n + 1, np.uint64)
+            self.runs = arr(rr.value, int(self.run_offsets[-1]), np.uint32).reshape(-1, 2)
+            self.winner_offsets = self.offsets
+            eo = np.zeros(n + 1, np.uint64)
+            check("mqm_result_expand", L.mqm_result_expand(handle, 0, n, eo.ctypes.data_as(C.c_void_p), None))
+            expanded = np.zeros(int(eo[-1]), np.uint32)
+            check("mqm_result_expand", L.mqm_result_expand(handle, 0, n, eo.ctypes.data_as(C.c_void_p),
+                                                           expanded.ctypes.data_as(C.c_void_p)))
+            self.offsets = eo
         nd = int(self.offsets[-1]) if n else 0
         ns = int(self.shared_offsets[-1]) if n else 0
         self.shared = arr(L.mqm_result_shared(handle), ns, np.uint32)
         self.packed_only = bool(nd) and not L.mqm_result_deliveries(handle) and bool(L.mqm_result_packed(handle))
         if self.packed_only:  # mqm_match_batch_packed: the client is the first-merged subscription's
-            packed = arr(L.mqm_result_packed(handle), nd, np.uint32)
+            packed = expanded if expanded is not None else arr(L.mqm_result_packed(handle), nd, np.uint32)
             self.deliveries = np.zeros(nd, capi.DELIVERY_DTYPE)
             self.deliveries["packed"] = packed
             self.deliveries["client"] = self.sub_infos(packed & 0x0FFFFFFF)["client"]
@@ -395,6 +411,19 @@ class TopicsIndex:
         offs = np.ascontiguousarray(offs, dtype=np.uint64)
         h = C.c_void_p()
         check("mqm_match_batch_packed", lib().mqm_match_batch_packed(
+            self._h, data.ctypes.data_as(C.c_void_p), offs.ctypes.data_as(C.c_void_p), len(offs) - 1,
+            C.byref(h)))
+        return BatchResult(self, h)
+
+    def match_batch_runs(self, data: np.ndarray, offs: np.ndarray) -> BatchResult:
+        """mqm_match_batch_runs (solo deliveries as runs of the snapshot's
+        packed words, merged winners explicit); the BatchResult expands them
+        into plain rows and keeps the raw form (run_offsets, runs,
+        winner_offsets)."""
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        h = C.c_void_p()
+        check("mqm_match_batch_runs", lib().mqm_match_batch_runs(
             self._h, data.ctypes.data_as(C.c_void_p), offs.ctypes.data_as(C.c_void_p), len(offs) - 1,
             C.byref(h)))
         return BatchResult(self, h)

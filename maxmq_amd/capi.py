@@ -47,7 +47,7 @@ EXPORTED = [
     "mqm_commit_policy", "mqm_commit_state_get", "mqm_snapshot_digest", "mqm_unsubscribe_many", "mqm_load_subscriptions_json",
     "mqm_debug_fault", "mqm_gather_shards_shared", "mqm_match_ctx_create", "mqm_match_ctx_destroy",
     "mqm_match_device_async", "mqm_match_ctx_wait", "mqm_match_ctx_stats", "mqm_match_batch_packed",
-    "mqm_result_packed",
+    "mqm_result_packed", "mqm_match_batch_runs", "mqm_result_runs", "mqm_result_expand",
 ]
 
 
@@ -205,6 +205,9 @@ def lib():
         "mqm_match_ctx_stats": ([vp, C.POINTER(u64)], C.c_int),
         "mqm_match_batch_packed": ([vp, vp, vp, u32, C.POINTER(vp)], C.c_int),
         "mqm_result_packed": ([vp], vp),
+        "mqm_match_batch_runs": ([vp, vp, vp, u32, C.POINTER(vp)], C.c_int),
+        "mqm_result_runs": ([vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), C.POINTER(u64)], C.c_int),
+        "mqm_result_expand": ([vp, u32, u32, vp, vp], C.c_int),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

@@ -171,6 +171,11 @@ struct mqm_result {
   const uint32_t *packed = nullptr;           // mqm_match_batch_packed: 4-B packed words
   const uint32_t *shared = nullptr, *idents = nullptr;
   bool has_idents = false;               // MQM_CFG_IDENTIFIERS
+  // the runs form (mqm_match_batch_runs): offsets / packed are the merged
+  // winners; topic t's solo deliveries are snap->words over its runs
+  const uint64_t *run_offsets = nullptr;
+  const mqm_run *runs = nullptr;
+  uint64_t n_solo = 0;
   std::shared_ptr<const HostSnapshot> snap;
   bool heap = false;  // blk from malloc (results filled by host copies, no DMA into them)
   ~mqm_result() {
@@ -719,8 +724,12 @@ int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t 
 
 // skip_small: the caller already ran this batch on the small-batch path and
 // it fell back (a topic past one of its capacities): go straight to the pipeline
+// runs: the runs form (mqm_match_batch_runs): solo parts as runs of the
+// snapshot's words, the merged winners packed (implies packed)
 static int match_batch_impl(mqm_index *h, const char *topic_bytes, const uint64_t *topic_offsets, uint32_t n_topics,
-                            bool packed, mqm_result **out, bool skip_small = false) {
+                            bool packed, mqm_result **out, bool skip_small = false, bool runs = false) {
+  packed = packed || runs;
+  skip_small = skip_small || runs;  // (the small-batch path writes deliveries, not runs)
   if (!h || !out || !topic_offsets || (n_topics && !topic_bytes)) return MQM_EINVAL;
   *out = nullptr;
   return guarded([&] {
@@ -762,7 +771,12 @@ static int match_batch_impl(mqm_index *h, const char *topic_bytes, const uint64_
                            &d_bytes, &d_offs);
       if (e != MQM_OK) return e;
       MatchOutput mo;
-      if ((e = match_device(snap->dev, ws, d_bytes, d_offs, n_topics, st, &mo)) != 0) return hip_rc(e);
+      ws.runs = runs;
+      e = match_device(snap->dev, ws, d_bytes, d_offs, n_topics, st, &mo);
+      ws.runs = false;
+      if (e != 0) return hip_rc(e);
+      RunsOutput ro;
+      if (runs && (e = runs_device(ws, st, mo, &ro)) != 0) return hip_rc(e);
       IdentOutput io;
       if (want_ids && (e = identifiers_device(snap->dev, ws, st, &io)) != 0) return hip_rc(e);
       DenseOutput dn;
@@ -772,7 +786,8 @@ static int match_batch_impl(mqm_index *h, const char *topic_bytes, const uint64_
       auto up = [](uint64_t b) { return (b + 15) & ~15ull; };
       const uint64_t o_off = 0, o_sh = up(8 * n1), o_io = o_sh + up(8 * n1), o_d = o_io + (want_ids ? up(8 * n1) : 0);
       const uint64_t dsz = packed ? 4 : 8;
-      const uint64_t o_s = o_d + up(dsz * mo.n_deliveries), o_i = o_s + up(4 * mo.n_shared), total = o_i + up(4 * ni);
+      const uint64_t o_s = o_d + up(dsz * mo.n_deliveries), o_i = o_s + up(4 * mo.n_shared), o_ro = o_i + up(4 * ni);
+      const uint64_t o_r = o_ro + (runs ? up(8 * n1) : 0), total = o_r + (runs ? up(8 * ro.n_runs) : 0);
       r->pool = h->pinned;
       r->blk = h->pinned->get(total, &r->blk_cap);
       if (!r->blk) {
@@ -797,6 +812,14 @@ static int match_batch_impl(mqm_index *h, const char *topic_bytes, const uint64_
         return MQM_EHIP;
       if (mo.n_shared && hipMemcpyAsync(B + o_s, dn.shared, 4 * mo.n_shared, hipMemcpyDeviceToHost, st) != hipSuccess)
         return MQM_EHIP;
+      if (runs) {
+        r->run_offsets = reinterpret_cast<const uint64_t *>(B + o_ro);
+        r->runs = reinterpret_cast<const mqm_run *>(B + o_r);
+        r->n_solo = mo.n_solo;
+        if (hipMemcpyAsync(B + o_ro, ro.offsets, 8 * n1, hipMemcpyDeviceToHost, st) != hipSuccess) return MQM_EHIP;
+        if (ro.n_runs && hipMemcpyAsync(B + o_r, ro.runs, 8 * ro.n_runs, hipMemcpyDeviceToHost, st) != hipSuccess)
+          return MQM_EHIP;
+      }
       if (want_ids) {
         r->has_idents = true;
         r->ident_offsets = reinterpret_cast<const uint64_t *>(B + o_io);
@@ -824,6 +847,11 @@ int mqm_match_batch(mqm_index *h, const char *topic_bytes, const uint64_t *topic
 int mqm_match_batch_packed(mqm_index *h, const char *topic_bytes, const uint64_t *topic_offsets, uint32_t n_topics,
                            mqm_result **out) {
   return match_batch_impl(h, topic_bytes, topic_offsets, n_topics, true, out);
+}
+
+int mqm_match_batch_runs(mqm_index *h, const char *topic_bytes, const uint64_t *topic_offsets, uint32_t n_topics,
+                         mqm_result **out) {
+  return match_batch_impl(h, topic_bytes, topic_offsets, n_topics, true, out, false, true);
 }
 
 }  // extern "C"
@@ -1400,6 +1428,39 @@ uint32_t mqm_result_num_topics(const mqm_result *r) { return r ? r->n : 0; }
 const uint64_t *mqm_result_offsets(const mqm_result *r) { return r ? r->offsets : nullptr; }
 const mqm_delivery *mqm_result_deliveries(const mqm_result *r) { return r ? r->deliveries : nullptr; }
 const uint32_t *mqm_result_packed(const mqm_result *r) { return r ? r->packed : nullptr; }
+
+int mqm_result_runs(const mqm_result *r, const uint64_t **run_offsets, const mqm_run **runs, const uint32_t **words,
+                    uint64_t *n_words) {
+  if (!r || !r->run_offsets || !r->snap || !run_offsets || !runs || !words) return MQM_EINVAL;
+  *run_offsets = r->run_offsets;
+  *runs = r->runs;
+  *words = r->snap->words.data();
+  if (n_words) *n_words = r->snap->words.size();
+  return MQM_OK;
+}
+
+int mqm_result_expand(const mqm_result *r, uint32_t t0, uint32_t t1, uint64_t *offsets, uint32_t *dst) {
+  if (!r || !r->packed || t0 > t1 || t1 > r->n || !offsets) return MQM_EINVAL;
+  const uint32_t *W = r->run_offsets && r->snap ? r->snap->words.data() : nullptr;
+  const uint64_t nw = W ? r->snap->words.size() : 0;
+  uint64_t at = 0;
+  for (uint32_t t = t0; t < t1; t++) {
+    offsets[t - t0] = at;
+    if (W) {
+      for (uint64_t k = r->run_offsets[t]; k < r->run_offsets[t + 1]; k++) {
+        const mqm_run run = r->runs[k];
+        if ((uint64_t)run.off + run.count > nw) return MQM_EINVAL;
+        if (dst) memcpy(dst + at, W + run.off, 4ull * run.count);
+        at += run.count;
+      }
+    }
+    const uint64_t w0 = r->offsets[t], w1 = r->offsets[t + 1];
+    if (dst && w1 > w0) memcpy(dst + at, r->packed + w0, 4 * (w1 - w0));
+    at += w1 - w0;
+  }
+  offsets[t1 - t0] = at;
+  return MQM_OK;
+}
 const uint64_t *mqm_result_shared_offsets(const mqm_result *r) { return r ? r->shared_offsets : nullptr; }
 const uint32_t *mqm_result_shared(const mqm_result *r) { return r ? r->shared : nullptr; }
 

@@ -564,11 +564,14 @@ int flatten(const Store &st, HostSnapshot *out) {
   }
 
   // the device word (snapshot.h): the entry's own delivery, ident flag on top
+  // (and the host copy of DeviceSnapshot::words: the runs form's deliveries)
+  hs.words.resize(hs.subs.size());
   parallel_for(64, [&](uint32_t c) {
     const uint64_t n = hs.subs.size(), lo = n * c / 64, hi = n * (c + 1) / 64;
     for (uint64_t j = lo; j < hi; j++) {
       const uint32_t m = hs.subs[j].word;
       hs.subs[j].word = (uint32_t)j | ((m & 3u) << 28) | (((m >> 2) & 1u) << 30) | ((m & kMetaIdent) ? kWordIdent : 0u);
+      hs.words[j] = hs.subs[j].word & kPackedMask;
     }
   });
   pt.mark("ranges");

@@ -45,6 +45,7 @@ struct HostSnapshot {
   std::vector<EdgeEntry, NoInitAlloc<EdgeEntry>> edges;  // n_buckets * kEdgesPerBucket (empty after upload)
   uint64_t edges_digest = 0;  // edges_digest_of(edges), kept when the host copy is released
   std::vector<SubEnt> subs;
+  std::vector<uint32_t> words;       // subs[i].word & kPackedMask (mqm_result_runs: a run's deliveries)
   std::vector<SubInfo> sub_info;     // by non-shared sid
   std::vector<SubInfo> shared_info;  // by shared sid
   std::vector<uint8_t> tok_pool;

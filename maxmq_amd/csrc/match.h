@@ -53,9 +53,9 @@ struct FastOutput {
 // Grow-only device buffers reused across batches (no allocation in steady state).
 struct Workspace {
   enum Slot {
-    kHCount, kDCount, kDStart, kHStart, kCls, kDfsList, kRecs, kCounters, kDOut, kHOut,
+    kSCount, kHCount, kDCount, kDStart, kHStart, kCls, kDfsList, kRecs, kCounters, kDOut, kHOut,
     kDense, kDenseShared, kDenseOffs, kDenseHOffs, kScanTmp, kRawCnt, kTabOff, kTabSize, kTable,
-    kInBytes, kInOffs, kListS, kICount, kIStart, kIOut, kMCount, kListW, kListT1, kListT2, kListT3, kListP, kListH, kListRS, kListR,
+    kInBytes, kInOffs, kListS, kICount, kIStart, kIOut, kMCount, kRunCount, kRunOffs, kRuns, kListW, kListT1, kListT2, kListT3, kListP, kListH, kListRS, kListR,
     // reverse match (retained.hip)
     kROffs, kRNLev, kRWild, kRLOff, kRFCount, kRFCur, kRLevels, kRNCount, kRNOff, kRItemF0, kRItemN0, kRItemF1,
     kRItemN1, kRChild, kRECount, kREOff, kREmit, kRPos, kRChunks, kRCOff, kROut, kRInBytes, kRInOffs, kNumSlots
@@ -92,6 +92,9 @@ struct Workspace {
   // the walk also writes every solo part to the topic records (the
   // identifiers pass reads them; capi: MQM_CFG_IDENTIFIERS)
   bool keep_solo = false, last_keep_solo = false;
+  // the runs form (mqm_match_batch_runs): solo parts stay runs of `words`
+  // (runs_device lists them), dout holds the merged winners only
+  bool runs = false, last_runs = false;
   const uint8_t *last_bytes = nullptr;
   const uint64_t *last_offs = nullptr;
 
@@ -187,6 +190,19 @@ struct IdentOutput {
   const uint32_t *sids = nullptr;     // device
 };
 int identifiers_device(const DeviceSnapshot &s, Workspace &ws, hipStream_t st, IdentOutput *out);
+
+// The runs form of the last match_device call on `ws` (made with ws.runs):
+// topic t's solo deliveries are words[run.x .. run.x + run.y) for its runs
+// runs[offsets[t] .. offsets[t+1]); its merged winners are the MatchOutput's
+// segments (dcount = winners only).  Device pointers, valid until the next call.
+struct RunsOutput {
+  uint32_t n_topics = 0;
+  uint64_t n_runs = 0;
+  const uint64_t *offsets = nullptr;   // n + 1
+  const uint2 *runs = nullptr;         // (words offset, count)
+  const uint32_t *solo_counts = nullptr;  // per topic: its runs' total
+};
+int runs_device(Workspace &ws, hipStream_t st, const MatchOutput &m, RunsOutput *out);
 
 // Dense CSR of a MatchOutput (offsets n+1, entries back to back) on `st`.
 struct DenseOutput {

@@ -174,6 +174,11 @@ struct Outputs {
   uint64_t dcap, hcap;
   uint32_t dfs_cap;  // DFS topics raw_cnt / raw_h / tab_off hold
   uint32_t keep_solo;  // the walk also writes every solo part to the record (identifiers pass)
+  // runs form (runs_device, mqm_match_batch_runs): the walk copies nothing;
+  // every solo part stays in the record as a run of `words`, the reservation
+  // and the header's solo count cover only the merge's winners, scount[t] = Ss
+  uint32_t runs;
+  uint32_t *scount;
 };
 
 // k_walk context of one topic (one lane group).  The solo parts are kept as
@@ -354,8 +359,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t words_rsrc(const DeviceSnapsho
   return __builtin_amdgcn_make_buffer_rsrc((void *)s.words, (short)0, (int)(s.n_subs * 4u + 64u), 0x00020000);
 }
 
+// MQM_WALK_W4=1 (A/B, `make variant`): hold k_walk to 4 waves per SIMD (128
+// VGPRs, a few spilled) instead of the 3 its registers allow
+#ifndef MQM_WALK_W4
+#define MQM_WALK_W4 0
+#endif
 template <int kG>
-__global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, const uint8_t *__restrict__ tbytes,
+__global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_eu(MQM_WALK_W4 ? 4 : 1))) void k_walk(DeviceSnapshot s, const uint8_t *__restrict__ tbytes,
                                                            const uint64_t *__restrict__ toffs, uint32_t n,
                                                            Outputs o) {
   constexpr int kGroups = kWave / kG;
@@ -470,7 +480,7 @@ __global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, co
       } else if (i == (uint32_t)kSoloLds) {
         L.q16 = rel;
       }
-      if (i >= (uint32_t)kSoloLds || o.keep_solo) *reinterpret_cast<uint2 *>(rec + 2 * i) = make_uint2(off, cnt);
+      if (i >= (uint32_t)kSoloLds || o.keep_solo || o.runs) *reinterpret_cast<uint2 *>(rec + 2 * i) = make_uint2(off, cnt);
     };
 #pragma unroll
     for (int k = 0; k < kSoloLds / kG; k++) L.sp[2 * (gl + k * kG) + 1] = 0xFFFFFFFFu;
@@ -652,8 +662,9 @@ __global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, co
 
     // ---- 3. output segments: one reservation for the wavefront's topics ----
     // (raw entries S: solo entries at dstart, the merge's winners after them;
-    // DFS topics reserve nothing here: k_dfs writes them after dcur)
-    const uint32_t need = bounded && gl == 0 ? S : 0;
+    // runs form: the winners only; DFS topics reserve nothing here: k_dfs
+    // writes them after dcur)
+    const uint32_t need = bounded && gl == 0 ? (o.runs ? Ms : S) : 0;
     uint32_t inc = need;
 #pragma unroll
     for (int dd = 1; dd < kWave; dd <<= 1) {
@@ -685,14 +696,16 @@ __global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, co
     if (!fits && lane == 0) atomicOr(&o.ctr->oob, kOobWalk);  // the call is re-run with dout sized by dcur
     const uint64_t ds = base + ex;
     if (active && gl == 0) {
-      if (bounded && (Ms > 0 || nsh > 0 || o.keep_solo)) tail[0] = make_uint4(nm | (nsh << 8), Ss, Ms, nq);
+      if (bounded && (Ms > 0 || nsh > 0 || o.keep_solo || o.runs))
+        tail[0] = make_uint4(nm | (nsh << 8), o.runs ? 0u : Ss, Ms, nq);  // (runs: winners at dstart)
+      if (o.runs) o.scount[t] = bounded ? Ss : 0;
       o.cls[t] = !bounded ? kClsDfs
                  : (S == 0 && H == 0) ? kClsDone
                                       : (kClsBounded | (nm <= kSmallHits ? kClsFewHits : 0) | (any_heavy ? kClsHeavy : 0));
       o.hcount[t] = bounded ? H : 0;
       o.mcount[t] = bounded ? Ms : 0;
       o.dstart[t] = ds;
-      o.dcount[t] = bounded && Ms == 0 ? Ss : 0;  // the merges write the others (k_dfs the DFS topics')
+      o.dcount[t] = bounded && Ms == 0 && !o.runs ? Ss : 0;  // the merges write the others (k_dfs the DFS topics')
       if (!bounded) {
         o.dfs_list[atomicAdd(&o.ctr->n_dfs, 1u)] = t;
         atomicAdd(&o.ctr->why[why], 1u);
@@ -702,7 +715,7 @@ __global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, co
     // ---- 4. solo copy -----------------------------------------------------
     // the entries of the group's LDS parts: all its solo entries, or those
     // before its first record part
-    const uint32_t Qf = !bounded ? 0 : nq <= (uint32_t)kSoloLds ? Ss : L.q16;
+    const uint32_t Qf = !bounded || o.runs ? 0 : nq <= (uint32_t)kSoloLds ? Ss : L.q16;
     // the groups' starts in the wavefront's solo space
     const uint32_t qn = gl == 0 && fits ? Qf : 0;
     uint32_t qinc = qn;
@@ -743,7 +756,7 @@ __global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, co
     }
     // topics with more than kSoloLds solo parts: the rest from the record,
     // part by part (a wavefront per part; rare: Zipf hub topics)
-    uint64_t ovm = __ballot(gl == 0 && bounded && fits && nq > (uint32_t)kSoloLds);
+    uint64_t ovm = __ballot(gl == 0 && bounded && fits && !o.runs && nq > (uint32_t)kSoloLds);
     if (ovm) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wavefront's record stores have landed
       __builtin_amdgcn_wave_barrier();
@@ -1566,6 +1579,25 @@ __global__ __launch_bounds__(256) void k_ident(DeviceSnapshot s, Outputs o, uint
   }
 }
 
+// ---- the runs form (runs_device): every bounded topic's solo parts, listed
+// from its record (the walk wrote them there and copied nothing) ------------
+__global__ __launch_bounds__(256) void k_run_count(Outputs o, uint32_t n, uint32_t *__restrict__ nrun) {
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x)
+    nrun[t] = (o.cls[t] & kClsBounded) ? rec_tail(o.recs, t)[0].w : 0u;
+}
+
+// 8 lanes per topic: its runs (8 B each) to runs[roff[t] ..)
+__global__ __launch_bounds__(256) void k_run_copy(Outputs o, uint32_t n, const uint64_t *__restrict__ roff,
+                                                  uint2 *__restrict__ runs, uint64_t cap) {
+  constexpr int kL = 8;
+  const uint32_t gl = threadIdx.x % kL, ng = gridDim.x * (blockDim.x / kL);
+  for (uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) / kL; t < n; t += ng) {
+    const uint64_t a = roff[t], c = roff[t + 1] - a;
+    const uint2 *rec = reinterpret_cast<const uint2 *>(o.recs + (uint64_t)t * kRecStrideAlloc);
+    for (uint32_t j = gl; j < c; j += kL) put_checked(runs, a + j, cap, rec[j], &o.ctr->oob);
+  }
+}
+
 // DFS sizing on the device (one workgroup): per DFS topic a dedupe table of
 // the next power of two >= 2 x its raw entries (>= 64), their offsets, the
 // DFS tails' start after the scanned segments, the totals — and the capacity
@@ -1935,6 +1967,11 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
   o.recs = (uint32_t *)ws.ptr(W::kRecs);
   o.ctr = (Counters *)ws.ptr(W::kCounters);
   o.keep_solo = ws.keep_solo ? 1u : 0u;
+  o.runs = ws.runs ? 1u : 0u;
+  if (ws.runs) {
+    if (ws.get(W::kSCount, sizeof(uint32_t) * (n + 1))) return -2;
+    o.scount = (uint32_t *)ws.ptr(W::kSCount);
+  }
   // merge lists
   const W::Slot list_slots[kNLists] = {W::kListS, W::kListW, W::kListT1, W::kListT2, W::kListT3,
                                        W::kListP, W::kListH, W::kListRS, W::kListR};
@@ -2148,7 +2185,8 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
   ws.last_n = n;
   ws.last_bytes = d_bytes;
   ws.last_offs = d_offs;
-  ws.last_keep_solo = ws.keep_solo;
+  ws.last_keep_solo = ws.keep_solo || ws.runs;
+  ws.last_runs = ws.runs;
   ws.pend_exact = exact;
   ws.pending = true;
   return 0;
@@ -2234,6 +2272,39 @@ int match_device(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes,
     if (rc == 0) ws.requeued++;
   }
   return rc;
+}
+
+int runs_device(Workspace &ws, hipStream_t st, const MatchOutput &m, RunsOutput *out) {
+  using W = Workspace;
+  const uint32_t n = ws.last_n;
+  if (!ws.last_valid || !ws.last_runs) return -1;
+  if (ws.get(W::kRunCount, sizeof(uint32_t) * (n + 1)) || ws.get(W::kRunOffs, sizeof(uint64_t) * (n + 1)) ||
+      ws.get(W::kRuns, sizeof(uint2) * (m.n_solo_ranges + 1)))
+    return -2;
+  Outputs o{};
+  o.cls = (uint8_t *)ws.ptr(W::kCls);
+  o.recs = (uint32_t *)ws.ptr(W::kRecs);
+  o.ctr = (Counters *)ws.ptr(W::kCounters);
+  auto *nrun = (uint32_t *)ws.ptr(W::kRunCount);
+  auto *roff = (uint64_t *)ws.ptr(W::kRunOffs);
+  auto *runs = (uint2 *)ws.ptr(W::kRuns);
+  if (n > 0) {
+    hipLaunchKernelGGL(k_run_count, dim3(std::min<uint32_t>((n + 255) / 256, 8192)), dim3(256), 0, st, o, n, nrun);
+    HIP_TRY(hipGetLastError());
+  }
+  if (scan_offsets(ws, nrun, roff, n, st)) return -3;
+  if (n > 0) {
+    // (the walk counted these parts: Counters::n_desc; a mismatch is a checked store)
+    hipLaunchKernelGGL(k_run_copy, dim3(std::min<uint32_t>((n + 31) / 32, 8192)), dim3(256), 0, st, o, n, roff, runs,
+                       (uint64_t)m.n_solo_ranges);
+    HIP_TRY(hipGetLastError());
+  }
+  out->n_topics = n;
+  out->n_runs = m.n_solo_ranges;
+  out->offsets = roff;
+  out->runs = runs;
+  out->solo_counts = (const uint32_t *)ws.ptr(W::kSCount);
+  return 0;
 }
 
 int identifiers_device(const DeviceSnapshot &s, Workspace &ws, hipStream_t st, IdentOutput *out) {
