@@ -429,6 +429,7 @@ def main():
         if host:
             host["packed"] = host_path(idx, w, args, "packed")
         steady = steady_state(idx, tb, to, n, dev, args) if world == 1 and not shard_of and args.steady_steps else None
+        gproxy = gather_proxy(idx, tb, to, n, dev, args, shard_of[1]) if world == 1 and shard_of else None
         lat = latency(idx, w, args) if args.latency_topics and world == 1 else None
         if not args.no_cpu_baseline:
             if world == 1:
@@ -479,6 +480,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "host_path": host,
+            "gather_proxy": gproxy,
             # SURVEY §8(d)'s end-to-end definition (pinned topics in -> usable
             # per-topic rows in host memory), beside the HBM-resident `value`
             "end_to_end": ({"value": host["value"], "unit": "topics/s", "form": host["form"],
@@ -600,6 +602,64 @@ def host_path(idx, w, args, form="runs"):
                      if form == "runs" else "mqm_match_batch_packed: 4-B packed words") +
                     "); native caller threads (tools/conc_driver.cpp); pcie_bound = max(H2D bytes / H2D rate, "
                     "D2H bytes / D2H rate)"}
+
+
+def gather_proxy(idx, tb, to, n, dev, args, shards=8):
+    """Single-GPU proxy of the device-gather node step (`--gather device`,
+    DESIGN §6): this shard's dense result of one planned chunk stands in for
+    each of `shards` shards; timed on this GPU: the densify + copy-out a shard
+    does per chunk, the D2D copies of the other shards' lists (a lower bound of
+    their xGMI transfer: local HBM, not links) and mqm_gather_shards' layout of
+    the node-wide CSR.  The xGMI time of the same bytes is projected at 7 links
+    x 153 GB/s into the leader (MI355X_MICROARCH / the prompt's figure), the
+    ideal; RCCL point-to-point reaches a fraction of it."""
+    import torch
+
+    import maxmq_amd
+    from maxmq_amd import shard
+    from maxmq_amd.devbuf import copy_from_ptr
+
+    st = torch.cuda.current_stream(dev)
+    probe = min(n, 200000)
+    idx.match_device(tb.data_ptr(), to.data_ptr(), probe, st.cuda_stream)
+    d = idx.dense_device(st.cuda_stream)
+    dpt = int(d.n_deliveries) / probe
+    chunk = shard.plan_chunk(n, shards * dpt * 1.1, 0.0, args.gather_budget_gb * 1e9)
+    chunk = min(chunk, n)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    ev[0].record(st)
+    idx.match_device(tb.data_ptr(), to.data_ptr(), chunk, st.cuda_stream)
+    ev[1].record(st)
+    d = idx.dense_device(st.cuda_stream)
+    nd = int(d.n_deliveries)
+    offs = copy_from_ptr(torch.empty(chunk + 1, dtype=torch.int64, device=dev), d.offsets)
+    dl = copy_from_ptr(torch.empty(nd, dtype=torch.int64, device=dev), d.deliveries)
+    ev[2].record(st)
+    recv = [torch.empty_like(dl) for _ in range(shards - 1)]
+    for r in recv:
+        r.copy_(dl)
+    ev[3].record(st)
+    torch.cuda.synchronize(dev)
+    out_o = torch.empty(chunk + 1, dtype=torch.int64, device=dev)
+    out_d = torch.empty(shards * nd, dtype=torch.int64, device=dev)
+    parts = [(offs.data_ptr(), dl.data_ptr(), 0, 0)] + [(offs.data_ptr(), r.data_ptr(), 0, 0) for r in recv]
+    t0 = time.perf_counter()
+    maxmq_amd.gather_shards(chunk, parts, out_o.data_ptr(), out_d.data_ptr(), st.cuda_stream)
+    torch.cuda.synchronize(dev)
+    layout_ms = (time.perf_counter() - t0) * 1e3
+    ingress = (shards - 1) * nd * 8
+    xgmi_ms = ingress / (7 * 153e9) * 1e3
+    step_chunks = (n + chunk - 1) // chunk
+    per_chunk_ms = ev[0].elapsed_time(ev[1]) + ev[1].elapsed_time(ev[2]) + max(xgmi_ms, ev[2].elapsed_time(ev[3])) + layout_ms
+    del recv, out_d
+    return {"shards": shards, "chunk_topics": chunk, "chunks_per_step": step_chunks,
+            "deliveries_per_topic_per_shard": dpt, "leader_ingress_bytes_per_chunk": ingress,
+            "match_ms": ev[0].elapsed_time(ev[1]), "densify_copy_ms": ev[1].elapsed_time(ev[2]),
+            "d2d_copies_ms": ev[2].elapsed_time(ev[3]), "layout_ms": layout_ms,
+            "xgmi_ideal_ms": xgmi_ms, "projected_step_ms": per_chunk_ms * step_chunks,
+            "projected_node_topics_per_s": n / (per_chunk_ms * step_chunks * 1e-3),
+            "note": "one GPU standing in for every shard (its own chunk result copied shards - 1 times); "
+                    "serial stages, no overlap; xGMI at the 7 x 153 GB/s ideal into the leader"}
 
 
 def host_runner(idx, w, args, form="runs"):

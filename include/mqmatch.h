@@ -136,12 +136,12 @@ typedef struct {
                                      hits, cached levels, shared hits, raw entries */
   uint32_t n_merge_small;         /* topics whose <= 24 multi entries an 8-lane group merged */
   uint32_t n_merge_wave;          /* topics whose <= 192 multi entries a wavefront merged */
-  uint64_t n_solo_ranges;         /* solo parts the walk copied (hits with solo entries) */
+  uint64_t n_solo_ranges;         /* solo copy ranges (hits with solo entries)    */
   uint32_t n_tier2, n_tier3;      /* topics the workgroup merge passed to its 2nd / 3rd tier */
   uint64_t multi_entries[3];      /* multi entries merged by the workgroup tiers 1 / 2 / 3 */
   uint32_t n_part;                /* tier-3 topics merged in client-hash partitions (> 3072 multi entries) */
   uint32_t n_resolve;             /* topics merged by resolution (partner lists, no table) */
-  uint64_t n_solo;                /* deliveries the walk copied as they stand (solo entries) */
+  uint64_t n_solo;                /* solo entries: deliveries copied as they stand */
 } mqm_device_result;
 
 /* ---- lifecycle: NewTopicsIndex (topics.go:291-299) ---------------------- */

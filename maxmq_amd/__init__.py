@@ -116,7 +116,7 @@ class BatchResult:
         if n and L.mqm_result_runs(handle, C.byref(ro), C.byref(rr), C.byref(rw), C.byref(nw)) == 0:
             self.runs_form = True
             self.run_offsets = arr(ro.value, n + 1, np.uint64)
-            self.runs = arr(rr.value, int(self.run_offsets[-1]), np.uint32).reshape(-1, 2)
+            self.runs = arr(rr.value, 2 * int(self.run_offsets[-1]), np.uint32).reshape(-1, 2)  # (off, count)
             self.winner_offsets = self.offsets
             eo = np.zeros(n + 1, np.uint64)
             check("mqm_result_expand", L.mqm_result_expand(handle, 0, n, eo.ctypes.data_as(C.c_void_p), None))

@@ -302,8 +302,7 @@ int front(mqm_index *h, std::shared_ptr<GpuSnapshot> *out) {
   return MQM_OK;
 }
 
-int ctx_init(mqm_index *h, MatchCtx *c) {
-  c->ws.keep_solo = (h->cfg.flags & MQM_CFG_IDENTIFIERS) != 0;  // the identifiers pass reads them
+int ctx_init(mqm_index *, MatchCtx *c) {
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     c->stream = nullptr;
     return MQM_EHIP;
@@ -828,6 +827,11 @@ static int match_batch_impl(mqm_index *h, const char *topic_bytes, const uint64_
         if (ni && hipMemcpyAsync(B + o_i, io.sids, 4 * ni, hipMemcpyDeviceToHost, st) != hipSuccess) return MQM_EHIP;
       }
       if (ws.end(st) || hipStreamSynchronize(st) != hipSuccess) return MQM_EHIP;
+      if (runs && r->run_offsets[n_topics] != ro.n_runs) {  // the records' part counts vs the walk's tally
+        fprintf(stderr, "mqmatch: runs form: %llu runs listed, %llu counted by the walk\n",
+                (unsigned long long)r->run_offsets[n_topics], (unsigned long long)ro.n_runs);
+        return MQM_EHIP;
+      }
       return MQM_OK;
     }();
     ctx_release(h, std::move(c));
@@ -877,7 +881,6 @@ int mqm_match_ctx_create(mqm_index *h, mqm_match_ctx **out) {
     if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
     auto x = std::make_unique<mqm_match_ctx>();
     x->h = h;
-    x->c.ws.keep_solo = (h->cfg.flags & MQM_CFG_IDENTIFIERS) != 0;
     h->live_ctxs.fetch_add(1, std::memory_order_acq_rel);
     *out = x.release();
     return MQM_OK;

@@ -55,7 +55,7 @@ struct Workspace {
   enum Slot {
     kSCount, kHCount, kDCount, kDStart, kHStart, kCls, kDfsList, kRecs, kCounters, kDOut, kHOut,
     kDense, kDenseShared, kDenseOffs, kDenseHOffs, kScanTmp, kRawCnt, kTabOff, kTabSize, kTable,
-    kInBytes, kInOffs, kListS, kICount, kIStart, kIOut, kMCount, kRunCount, kRunOffs, kRuns, kListW, kListT1, kListT2, kListT3, kListP, kListH, kListRS, kListR,
+    kInBytes, kInOffs, kListS, kICount, kIStart, kIOut, kNSolo, kDescStart, kDesc, kWin, kMCount, kRunCount, kRunOffs, kRuns, kListW, kListT1, kListT2, kListT3, kListP, kListH, kListRS, kListR,
     // reverse match (retained.hip)
     kROffs, kRNLev, kRWild, kRLOff, kRFCount, kRFCur, kRLevels, kRNCount, kRNOff, kRItemF0, kRItemN0, kRItemF1,
     kRItemN1, kRChild, kRECount, kREOff, kREmit, kRPos, kRChunks, kRCOff, kROut, kRInBytes, kRInOffs, kNumSlots
@@ -89,9 +89,6 @@ struct Workspace {
   // the last match_device call (identifiers_device works on its records)
   bool last_valid = false;
   uint32_t last_n = 0, last_n_dfs = 0;
-  // the walk also writes every solo part to the topic records (the
-  // identifiers pass reads them; capi: MQM_CFG_IDENTIFIERS)
-  bool keep_solo = false, last_keep_solo = false;
   // the runs form (mqm_match_batch_runs): solo parts stay runs of `words`
   // (runs_device lists them), dout holds the merged winners only
   bool runs = false, last_runs = false;
@@ -145,11 +142,11 @@ struct MatchOutput {
   uint32_t n_big = 0;       // topics whose multi entries the workgroup tier merged
   uint32_t n_tier2 = 0, n_tier3 = 0;  // ... of those, passed on to its second / third tier
   uint32_t n_merge_small = 0, n_merge_wave = 0;  // topics merged by k_merge_small / k_merge
-  uint64_t n_solo_ranges = 0;                     // solo parts the walk copied (hits with solo entries)
+  uint64_t n_solo_ranges = 0;                     // solo parts (copy descriptors / runs: hits with solo entries)
   uint64_t multi_entries[3] = {0, 0, 0};  // multi entries merged by the three workgroup tiers
   uint32_t n_part = 0;                    // ... of the third tier's topics, merged in client-hash partitions
   uint32_t n_resolve = 0;                 // topics merged by resolution (k_resolve: no table)
-  uint64_t n_solo = 0;                    // deliveries the walk copied as they stand (solo entries)
+  uint64_t n_solo = 0;                    // solo entries: deliveries copied as they stand
   bool exact = false;                     // sized by its own read-back (the first call of a workspace, or a re-run)
 };
 

@@ -12,26 +12,22 @@
 //                   checked against the edge filter when pushed / '+' child /
 //                   '#' child), so a level costs one dependent memory round
 //                   trip (the literal child's descriptor is inline in its
-//                   edge entry).  Hits are compacted with ballot + popcount:
-//                   solo parts (off, count) into the topic's LDS context,
-//                   multi parts (off, count, rank = 2 * node + slot, the
-//                   reference's emission order, snapshot.h) and shared ranges
-//                   into the topic's record in HBM.
-//     3. segments : one reservation per wavefront for its 16 topics' raw
-//                   entries (S, an upper bound of the deliveries), from a
-//                   chunk of the output the wavefront holds (one global
-//                   atomic per kChunk entries): dstart[t] is final when the
-//                   topic's walk ends, so no scan and no second pass.
-//     4. solo copy: the wavefront copies its topics' solo entries (~90 % of
-//                   the deliveries: an entry whose client meets no other of
-//                   its subscriptions in the topic is its client's merged
-//                   delivery as is) straight from the LDS parts: lane-
-//                   consecutive 4-B loads of `words` and stores to dout.  The
-//                   copy streams while other wavefronts of the CU chase
-//                   pointers, and the walk's records hold only what the merges
-//                   read (round 3 wrote every solo part to HBM for k_desc /
-//                   k_winmap / k_wincopy to read back: 4.3 ms of a 14.4 ms
-//                   batch at C3).
+//                   edge entry).  Hits are compacted with ballot + popcount
+//                   and written to the topic's record: solo parts (off,
+//                   count), multi parts (off, count, rank = 2 * node + slot,
+//                   the reference's emission order, snapshot.h), shared
+//                   ranges; S (raw entries) and H (shared candidates) counted.
+//   scans     S and H -> each topic's segment start (S bounds its
+//             deliveries, so every later kernel writes final positions).
+//   solo copy k_desc turns the records' solo parts into copy descriptors in
+//             topic order; k_winmap / k_wincopy copy the solo entries (~90 %
+//             of the deliveries: an entry whose client meets no other of its
+//             subscriptions in the topic is its client's merged delivery as
+//             it stands) in fixed windows of the output space.  (Round 4
+//             measured the copy fused into k_walk from LDS-held parts: 15.2
+//             / 17.5 ms per C3 batch at 4 / 3 waves per SIMD against 14.4 ms
+//             this way — the walk's register budget leaves too few loads in
+//             flight for a streaming copy; profiles/r04/r04f.)
 //   k_route   topics with multi entries -> merge lists by their count Ms.
 //   merges    k_resolve (partner lists, no table), k_merge_small / k_merge /
 //             k_multi<N> / k_multi_part (LDS hash tables keyed by client):
@@ -72,18 +68,15 @@ constexpr int kHCap = 64;                // non-shared hits per topic (hit_of: 6
 constexpr int kShCap = 16;               // shared hits per topic
 constexpr int kStage = 64;               // topic bytes staged in LDS (one round trip)
 constexpr int kICap = 48;                // load items per level (<= 3 per frontier node; more -> DFS path)
-constexpr int kSoloLds = 16;             // solo parts per topic held in LDS (more: the record's front)
-constexpr uint32_t kChunk = 1u << 15;    // output entries a walk wavefront reserves at a time
-constexpr int kCopyU = 4;                // solo entries per lane per copy step (loads in flight)
 // record of a topic, written while walking (kRecStrideAlloc words, 64-B
-// aligned), read by the merges, k_shared and the identifiers pass:
-//   from the start: [2i] off, [2i + 1] count of the i-th solo part — only
-//            parts i >= kSoloLds, or every part when the identifiers pass
-//            will read them (Outputs::keep_solo)
+// aligned).  A hit range subs[off, off + c) holds solo entries, then multi
+// ones (snapshot.h); the two parts are listed apart, each where its reader
+// wants it, so a topic writes (and its readers read) only the parts it has:
+//   from the start: [2i] off, [2i + 1] count of the i-th solo part (i <
+//            nsolo[t]): k_desc's copy descriptors (and the runs form's runs)
 //   [kRecSh + 2i] off, [kRecSh + 1 + 2i] cnt of shared hit i (i < nsh)
 //   the tail, in 16-B units counted back from the record's end (rec_tail):
-//     unit 0      header: nm | nsh << 8, Ssolo, M, nsolo (written when a
-//                 reader exists: M > 0, nsh > 0 or keep_solo)
+//     unit 0      header: nm | nsh << 8, Ssolo, M, nsolo
 //     unit 1 + h  multi part h (h < nm): moff, mcount, rank of its hit, 0 —
 //                 multi entries subs[moff, moff + mcount); the merges copy
 //                 the tail into LDS as header at word 0, part h at 4 + 4h,
@@ -110,7 +103,6 @@ constexpr uint32_t kNoWhy = 0xFFFFFFFFu;
 static_assert(kRecStrideAlloc % 16 == 0 && kRecStrideAlloc >= kRecTail + kRecLds, "64-B aligned records");
 static_assert(kSmallMulti * 4 <= kSmallSlots * 3, "k_emit table load factor");
 static_assert(kSmallMulti % kWave == 0, "register tiles");
-static_assert(kSoloLds == 4 * kWalkG && kSoloLds <= kHCap, "solo parts: 4 per lane of a group");
 static_assert(kLMax % kWalkG == 0, "levels per lane");
 
 // a load item of the walk: the literal-child probe of a frontier node (pushed
@@ -126,9 +118,8 @@ enum : uint8_t { kClsDone = 0, kClsBounded = 1, kClsDfs = 2, kClsFewHits = 4, kC
 enum : uint32_t { kWhyFrontier = 0, kWhyHits = 1, kWhyLevels = 2, kWhyShared = 3, kWhyEntries = 4 };
 
 struct Counters {              // zeroed before every batch
-  unsigned long long dtail;    // DFS deliveries: next free entry after the reserved segments
+  unsigned long long dtail;    // DFS deliveries: next free entry after the scanned segments
   unsigned long long htail;    // DFS shared candidates: likewise
-  unsigned long long dcur;     // the walk's output reservations (chunks and large segments)
   unsigned int n_dfs;          // topics appended to the DFS list
   unsigned int why[5];         // DFS routing reasons (kWhy*)
   // merge lists (k_route), in kList* order
@@ -142,11 +133,11 @@ struct Counters {              // zeroed before every batch
   unsigned int n_res_small;    // k_resolve<8>: no heavy entry, Ms <= kSmallMultiS, nh <= kSmallHits
   unsigned int n_res;          // k_resolve<64>: other topics with multi entries and no heavy entry
   unsigned long long m_sum[3]; // multi entries of the k_multi<1024> / <2048> / <4096> + k_multi_part lists
-  unsigned int oob;            // a store fell outside its output buffer (the call is re-run with
-                               //   buffers sized by what it reported)
+  unsigned int oob;            // a store fell outside its output buffer (queued calls: buffers sized
+                               //   from an earlier call were too small; the call is re-run)
   unsigned int cap_ovf;        // queued calls: the DFS lists / table / tails did not fit (re-run)
   // what the call needed (k_totals / k_dfs_prep): the next call's capacities
-  unsigned long long s_total, h_total, n_desc;  // reserved output entries, shared slots, solo parts
+  unsigned long long s_total, h_total, n_desc;  // raw-entry slots, shared slots, solo parts (descriptors)
   unsigned long long n_solo;                    // solo entries the walk copied
   unsigned long long tab_total, dfs_raw, dfs_h; // DFS: dedupe table, raw entries, shared candidates
   unsigned long long d_sum, h_sum;              // deliveries, shared candidates (after dedupe)
@@ -158,7 +149,9 @@ struct Counters {              // zeroed before every batch
 struct Outputs {
   uint32_t *hcount, *dcount;
   uint32_t *mcount;           // multi entries per topic (Ms; 0 for DFS topics)
-  uint64_t *dstart, *hstart;  // n + 1 (dstart: the walk's reservations; hstart: exclusive scan)
+  uint32_t *scount;           // raw entries per topic (the segment; runs form: the multi entries only)
+  uint32_t *nsolo;            // solo parts per topic (k_desc's descriptors; 0 in the runs form)
+  uint64_t *dstart, *hstart;  // n + 1 (exclusive scans; DFS topics overwritten)
   uint8_t *cls;
   uint32_t *dfs_list;
   uint32_t *recs;  // kRecStrideAlloc words per topic
@@ -173,38 +166,23 @@ struct Outputs {
   // (a wrong offset becomes a reported error, never an out-of-bounds write)
   uint64_t dcap, hcap;
   uint32_t dfs_cap;  // DFS topics raw_cnt / raw_h / tab_off hold
-  uint32_t keep_solo;  // the walk also writes every solo part to the record (identifiers pass)
-  // runs form (runs_device, mqm_match_batch_runs): the walk copies nothing;
-  // every solo part stays in the record as a run of `words`, the reservation
-  // and the header's solo count cover only the merge's winners, scount[t] = Ss
+  // runs form (runs_device, mqm_match_batch_runs): no solo copy; every solo
+  // part stays in the record as a run of `words`, the segment and the
+  // header's solo count cover only the merge's winners
   uint32_t runs;
-  uint32_t *scount;
 };
 
-// k_walk context of one topic (one lane group).  The solo parts are kept as
-// words, not uint2: the context's dword stride must stay odd (below)
-struct TopicLds {
+constexpr int kTopicWords = (2 * kLMax + 8 * kICap + kStage) / 4;
+struct TopicLds {              // k_walk context of one topic (one lane group)
   uint16_t sep[kLMax];         // position of the '/' ending level k (topics > 64 KiB: DFS path)
   uint32_t item[2][kICap];     // the level's load items: node id << 2 | kind (kItem*)
-  uint32_t sp[2 * kSoloLds];   // solo part j: off - rel, rel (rel = the topic's solo entries before it;
-                               //   ~0 past the topic's parts)
   uint8_t stage[kStage];       // the topic's first kStage bytes
-  uint32_t q16;                // rel of solo part kSoloLds (the first one in the record)
+  uint32_t pad[kTopicWords % 2 ? 2 : 1];  // odd dword stride: the groups of a wave reading the
+                               //   same field hit different banks (a 128-dword stride put all
+                               //   16 groups on one bank: SQ_LDS_BANK_CONFLICT 3x the LDS cycles)
 };
 static_assert(kStage % 16 == 0 && kICap >= 3, "walk context");
-// odd dword stride: the groups of a wave reading the same field hit different
-// banks (a 128-dword stride put all 16 groups on one bank: SQ_LDS_BANK_CONFLICT
-// 3x the LDS cycles)
-static_assert(sizeof(TopicLds) % 4 == 0 && (sizeof(TopicLds) / 4) % 2 == 1, "bank-skewed topic contexts");
-// the solo copy's per-wavefront tables: the groups' starts in the wavefront's
-// solo space and their output segments
-struct CopyLds {
-  uint32_t F[kWave / kWalkG + 2];  // exclusive prefix of the groups' LDS-part entries; [16] = total
-  uint32_t E[kWave / kWalkG];      // each group's segment, relative to the wavefront's reservation
-};
-// 4 blocks per CU (16 waves: the walk's VGPR limit) must fit in 160 KiB
-static_assert(4 * (kWalkWaves * (kWave / kWalkG) * sizeof(TopicLds) + kWalkWaves * sizeof(CopyLds)) <= 163840,
-              "k_walk LDS for 4 blocks per CU");
+static_assert((sizeof(TopicLds) / 4) % 2 == 1, "bank-skewed topic contexts");
 
 __device__ __forceinline__ void wave_lds_sync() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -223,7 +201,7 @@ __device__ __forceinline__ uint32_t table_slot(uint32_t client, uint32_t lg) {
 }
 
 // Counters::oob bits: which check failed (reported when an exact call fails)
-enum : unsigned int { kOobWalk = 1u, kOobStore = 2u, kOobShared = 4u, kOobHeavy = 8u, kOobPart = 16u, kOobDfs = 32u };
+enum : unsigned int { kOobDesc = 1u, kOobStore = 2u, kOobShared = 4u, kOobHeavy = 8u, kOobPart = 16u, kOobDfs = 32u };
 
 // a checked store: out[i] = v if i < cap, else flag the batch as failed
 template <class T>
@@ -313,11 +291,11 @@ __device__ __forceinline__ uint32_t mt_delivery(MergeTable t, uint32_t j) {
 }
 
 // ---------------------------------------------------------------------------
-// k_walk: tokenize + walk + output segments + solo copy, a kG-lane group per
-// topic.  Level keys and the running hit counts live in registers (lane k
-// holds the keys of levels k, k + kG, ...); LDS holds the separators, the
-// frontier, the first bytes of the topic and its first kSoloLds solo parts,
-// so many topics stay in flight per CU.
+// k_walk: tokenize + walk, a kG-lane group per topic.  Level keys and the
+// running hit counts live in registers (lane k holds the keys of levels k,
+// k + kG, ...); LDS holds only the separators, the frontier and the first
+// bytes of the topic, so many topics stay in flight per CU.  Hits go straight
+// to the topic's record with their rank.
 // ---------------------------------------------------------------------------
 // A record's multi parts carry their entry counts (field kFieldMpre, as k_walk
 // wrote them); the merges turn them into exclusive prefixes in their LDS copy
@@ -354,38 +332,24 @@ __device__ __forceinline__ const uint4 *rec_tail(const uint32_t *recs, uint32_t 
   return reinterpret_cast<const uint4 *>(recs + ((uint64_t)t + 1) * kRecStrideAlloc) - 1;
 }
 
-// `words` through a buffer descriptor: 32-bit offsets, bounds-checked reads
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t words_rsrc(const DeviceSnapshot &s) {
-  return __builtin_amdgcn_make_buffer_rsrc((void *)s.words, (short)0, (int)(s.n_subs * 4u + 64u), 0x00020000);
-}
 
-// MQM_WALK_W4=1 (A/B, `make variant`): hold k_walk to 4 waves per SIMD (128
-// VGPRs, a few spilled) instead of the 3 its registers allow
-#ifndef MQM_WALK_W4
-#define MQM_WALK_W4 0
-#endif
 template <int kG>
-__global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_eu(MQM_WALK_W4 ? 4 : 1))) void k_walk(DeviceSnapshot s, const uint8_t *__restrict__ tbytes,
+__global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, const uint8_t *__restrict__ tbytes,
                                                            const uint64_t *__restrict__ toffs, uint32_t n,
                                                            Outputs o) {
   constexpr int kGroups = kWave / kG;
   constexpr int kLPer = (kLMax + kG - 1) / kG;  // level keys held per lane
   constexpr uint32_t kGMask = (1u << kG) - 1u;
   static_assert(kLMax % kG == 0 || kG > kLMax, "levels per lane");
-  static_assert(kG == kWalkG, "TopicLds / CopyLds are sized for kWalkG lanes per topic");
   __shared__ TopicLds lds_all[kWalkWaves * kGroups];
-  __shared__ CopyLds copy_all[kWalkWaves];
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / kG, gl = lane & (kG - 1), gbase = g * kG;
   TopicLds &L = lds_all[(threadIdx.x / kWave) * kGroups + g];
-  TopicLds *WL = &lds_all[(threadIdx.x / kWave) * kGroups];  // the wavefront's topic contexts
-  CopyLds &C = copy_all[threadIdx.x / kWave];
   const uint32_t gmask_lt = (1u << gl) - 1u;
   const uint64_t stride = (uint64_t)gridDim.x * kWalkWaves * kGroups;
   const NodeDesc root = load_desc(s.nodes);
-  uint64_t c_cur = 0, c_end = 0;  // the wavefront's output chunk (wave-uniform)
-  uint32_t n_parts = 0;           // solo parts of this wavefront's topics (Counters::n_desc)
-  uint32_t n_solo = 0;            // their entries (Counters::n_solo; group leaders, flushed before 2^32)
+  uint32_t n_parts = 0; // solo parts of this lane's topics (Counters::n_desc; group leaders)
+  uint32_t n_solo = 0;  // solo entries of this lane's topics (Counters::n_solo; group leaders, flushed before 2^32)
 
   uint64_t tb = ((uint64_t)blockIdx.x * kWalkWaves + threadIdx.x / kWave) * kGroups;
   uint64_t nx_off = 0, nx_end = 0;  // the next topic's byte range, one topic ahead
@@ -464,29 +428,14 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
 
     // ---- 2. walk ----------------------------------------------------------
     // Level-synchronous over compact item lists: a node pushed to the next
-    // level enqueues only the loads it needs (its literal probe if the edge
-    // filter admits the next level's key under it, its '+' child, its '#'
-    // child unless kFlagHashLeaf lets the '#' child's gather be recorded at
-    // push time: partKey '#' of the next level, topics.go:503-505, rank 2 *
-    // '#' child).
+    // level enqueues only the loads it needs (its literal probe if it has a
+    // literal child, its '+' child, its '#' child unless kFlagHashLeaf lets
+    // the '#' child's gather be recorded at push time: partKey '#' of the
+    // next level, topics.go:503-505, rank 2 * '#' child).
     uint32_t *rec = o.recs + (uint64_t)(active ? t : 0) * kRecStrideAlloc;
     uint4 *tail = reinterpret_cast<uint4 *>(rec + kRecStrideAlloc) - 1;  // unit u at tail[-u]
-    // solo part i (its first entry is the topic's solo entry rel): LDS for i <
-    // kSoloLds, else (and with keep_solo always) the record's front
-    auto put_solo = [&](uint32_t i, uint32_t off, uint32_t cnt, uint32_t rel) {
-      if (i < (uint32_t)kSoloLds) {
-        L.sp[2 * i] = off - rel;
-        L.sp[2 * i + 1] = rel;
-      } else if (i == (uint32_t)kSoloLds) {
-        L.q16 = rel;
-      }
-      if (i >= (uint32_t)kSoloLds || o.keep_solo || o.runs) *reinterpret_cast<uint2 *>(rec + 2 * i) = make_uint2(off, cnt);
-    };
-#pragma unroll
-    for (int k = 0; k < kSoloLds / kG; k++) L.sp[2 * (gl + k * kG) + 1] = 0xFFFFFFFFu;
     if (len > 0xFFFFu) why = kWhyLevels;  // separators are kept as 16-bit positions
     uint32_t ni = nlev > 0 && why == kNoWhy ? root_items : 0, nh = 0, nsh = 0, nq = 0, nm = 0;
-    uint32_t qrun = 0;                 // the group's solo entries so far (group-uniform)
     uint32_t ls = 0, lm = 0, lh = 0;  // this lane's solo / multi / shared entries
     bool heavy = false;                // a gathered multi range with a heavy entry (kClsHeavy)
     int cur = 0;
@@ -591,27 +540,20 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
           const uint32_t i = nsh + __popc(m_sh & gmask_lt);
           *reinterpret_cast<uint2 *>(rec + kRecSh + 2 * i) = make_uint2(dc.sh_off, c_sh);
         }
-        // the solo parts (off, solo count, rel), lane by lane (own, parent-'#',
-        // '#' leaf): one group scan of (parts << 28 | entries) gives every
-        // part its index and its first solo entry
-        const uint32_t so_own = c_own - mu_own, so_par = c_par - mu_par, so_hl = c_hl - mu_hl;
-        const uint32_t kp = (so_own > 0) + (so_par > 0) + (so_hl > 0);
-        const uint32_t pk = (kp << 28) | (so_own + so_par + so_hl);  // entries < 2^26, sums < 2^28
-        uint32_t pinc = pk;
-#pragma unroll
-        for (int dd = 1; dd < kG; dd <<= 1) {
-          const uint32_t u = __shfl_up(pinc, dd, kG);
-          if (gl >= dd) pinc += u;
-        }
-        const uint32_t ptot = __shfl(pinc, gbase + kG - 1, kWave);
-        if (active && kp) {
-          uint32_t pi = nq + ((pinc - pk) >> 28), pe = qrun + ((pinc - pk) & 0x0FFFFFFFu);
-          if (so_own) put_solo(pi++, dc.sub_off, so_own, pe), pe += so_own;
-          if (so_par) put_solo(pi++, hoff, so_par, pe), pe += so_par;
-          if (so_hl) put_solo(pi, hoff, so_hl, pe);
-        }
-        nq += ptot >> 28;
-        qrun += ptot & 0x0FFFFFFFu;
+        // the solo parts, as (off, solo count) pairs from the record's start
+        const uint32_t q_own = (uint32_t)(__ballot(c_own > mu_own) >> gbase) & kGMask;
+        const uint32_t q_par = (uint32_t)(__ballot(c_par > mu_par) >> gbase) & kGMask;
+        const uint32_t q_hl = (uint32_t)(__ballot(c_hl > mu_hl) >> gbase) & kGMask;
+        if (active && c_own > mu_own)
+          *reinterpret_cast<uint2 *>(rec + 2 * (nq + __popc(q_own & gmask_lt))) =
+              make_uint2(dc.sub_off, c_own - mu_own);
+        if (active && c_par > mu_par)
+          *reinterpret_cast<uint2 *>(rec + 2 * (nq + __popc(q_own) + __popc(q_par & gmask_lt))) =
+              make_uint2(hoff, c_par - mu_par);
+        if (active && c_hl > mu_hl)
+          *reinterpret_cast<uint2 *>(rec + 2 * (nq + __popc(q_own) + __popc(q_par) + __popc(q_hl & gmask_lt))) =
+              make_uint2(hoff, c_hl - mu_hl);
+        nq += __popc(q_own) + __popc(q_par) + __popc(q_hl);
         // the next level's items (after the record writes: the frontier cap
         // needs the filter's answer; a topic leaving here goes to the DFS path)
         // (at d + 1 == kLMax the item is kept: the next level routes the topic to
@@ -658,136 +600,33 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
     const uint32_t S = Ss + Ms;
     const bool any_heavy = ((__ballot(heavy) >> gbase) & kGMask) != 0;
     if (why == kNoWhy && S > kSMax) why = kWhyEntries;
-    const bool bounded = active && why == kNoWhy;
-
-    // ---- 3. output segments: one reservation for the wavefront's topics ----
-    // (raw entries S: solo entries at dstart, the merge's winners after them;
-    // runs form: the winners only; DFS topics reserve nothing here: k_dfs
-    // writes them after dcur)
-    const uint32_t need = bounded && gl == 0 ? (o.runs ? Ms : S) : 0;
-    uint32_t inc = need;
-#pragma unroll
-    for (int dd = 1; dd < kWave; dd <<= 1) {
-      const uint32_t u = __shfl_up(inc, dd, kWave);
-      if (lane >= dd) inc += u;
-    }
-    const uint32_t tot = __shfl(inc, kWave - 1, kWave);   // < 2^28 (16 topics of <= kSMax)
-    const uint32_t ex = __shfl(inc - need, gbase, kWave);  // this group's offset
-    uint64_t base = 0;
-    auto reserve = [&](uint32_t k) {  // k entries of the output, one atomic (wave-uniform result)
-      uint64_t b = 0;
-      if (lane == 0) b = atomicAdd(&o.ctr->dcur, (unsigned long long)k);
-      // (readfirstlane returns int: widen through uint32_t, never sign-extend)
-      const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(b >> 32));
-      const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
-      return ((uint64_t)hi << 32) | lo;
-    };
-    if (tot > kChunk / 2) {  // a large reservation: its own atomic, the chunk is kept
-      base = reserve(tot);
-    } else if (tot > 0) {
-      if (c_cur + tot > c_end) {
-        c_cur = reserve(kChunk);
-        c_end = c_cur + kChunk;
-      }
-      base = c_cur;
-      c_cur += tot;
-    }
-    const bool fits = base + tot <= o.dcap;  // wave-uniform
-    if (!fits && lane == 0) atomicOr(&o.ctr->oob, kOobWalk);  // the call is re-run with dout sized by dcur
-    const uint64_t ds = base + ex;
     if (active && gl == 0) {
-      if (bounded && (Ms > 0 || nsh > 0 || o.keep_solo || o.runs))
-        tail[0] = make_uint4(nm | (nsh << 8), o.runs ? 0u : Ss, Ms, nq);  // (runs: winners at dstart)
-      if (o.runs) o.scount[t] = bounded ? Ss : 0;
-      o.cls[t] = !bounded ? kClsDfs
-                 : (S == 0 && H == 0) ? kClsDone
-                                      : (kClsBounded | (nm <= kSmallHits ? kClsFewHits : 0) | (any_heavy ? kClsHeavy : 0));
-      o.hcount[t] = bounded ? H : 0;
-      o.mcount[t] = bounded ? Ms : 0;
-      o.dstart[t] = ds;
-      o.dcount[t] = bounded && Ms == 0 && !o.runs ? Ss : 0;  // the merges write the others (k_dfs the DFS topics')
-      if (!bounded) {
+      const bool dfs = why != kNoWhy;
+      if (!dfs) tail[0] = make_uint4(nm | (nsh << 8), o.runs ? 0u : Ss, Ms, nq);  // (runs: winners at dstart)
+      o.cls[t] = dfs ? kClsDfs
+                     : (S == 0 && H == 0) ? kClsDone
+                                          : (kClsBounded | (nm <= kSmallHits ? kClsFewHits : 0) | (any_heavy ? kClsHeavy : 0));
+      o.nsolo[t] = dfs || o.runs ? 0 : nq;  // (runs form: no solo copy; the parts stay in the record)
+      o.scount[t] = dfs ? 0 : o.runs ? Ms : S;  // the segment: raw entries (runs form: the winners' only)
+      if (!dfs) {
+        if (n_solo + Ss < n_solo) atomicAdd(&o.ctr->n_solo, (unsigned long long)n_solo), n_solo = 0;
+        n_solo += Ss;
+        n_parts += nq;
+      }
+      o.hcount[t] = dfs ? 0 : H;
+      o.mcount[t] = dfs ? 0 : Ms;
+      o.dcount[t] = 0;
+      if (dfs) {
         o.dfs_list[atomicAdd(&o.ctr->n_dfs, 1u)] = t;
         atomicAdd(&o.ctr->why[why], 1u);
       }
     }
-
-    // ---- 4. solo copy -----------------------------------------------------
-    // the entries of the group's LDS parts: all its solo entries, or those
-    // before its first record part
-    const uint32_t Qf = !bounded || o.runs ? 0 : nq <= (uint32_t)kSoloLds ? Ss : L.q16;
-    // the groups' starts in the wavefront's solo space
-    const uint32_t qn = gl == 0 && fits ? Qf : 0;
-    uint32_t qinc = qn;
-#pragma unroll
-    for (int dd = 1; dd < kWave; dd <<= 1) {
-      const uint32_t u = __shfl_up(qinc, dd, kWave);
-      if (lane >= dd) qinc += u;
-    }
-    const uint32_t Qw = __shfl(qinc, kWave - 1, kWave);
-    if (gl == 0) {
-      C.F[g] = qinc - qn;
-      C.E[g] = ex;
-    }
-    if (lane == 0) C.F[kGroups] = Qw;
-    wave_lds_sync();
-    const __amdgpu_buffer_rsrc_t words = words_rsrc(s);
-    for (uint32_t b0 = 0; b0 < Qw; b0 += kWave * kCopyU) {
-      uint32_t sa[kCopyU], da[kCopyU], v[kCopyU];
-#pragma unroll
-      for (int u = 0; u < kCopyU; u++) {
-        const uint32_t q = b0 + u * kWave + lane;
-        uint32_t gg = 0;  // the group holding q: the largest gg with F[gg] <= q
-#pragma unroll
-        for (uint32_t st = kGroups / 2; st > 0; st >>= 1) gg = C.F[gg + st] <= q ? gg + st : gg;
-        const uint32_t p = q - C.F[gg];
-        const uint32_t *sp = WL[gg].sp;
-        uint32_t j = 0;  // its part: the largest j with rel[j] <= p
-#pragma unroll
-        for (uint32_t st = kSoloLds / 2; st > 0; st >>= 1) j = sp[2 * (j + st) + 1] <= p ? j + st : j;  // (~0 past the parts)
-        sa[u] = q < Qw ? sp[2 * j] + p : 0u;
-        da[u] = q < Qw ? C.E[gg] + p : ~0u;
-      }
-#pragma unroll
-      for (int u = 0; u < kCopyU; u++) v[u] = __builtin_amdgcn_raw_buffer_load_b32(words, (int)(sa[u] * 4u), 0, 0);
-#pragma unroll
-      for (int u = 0; u < kCopyU; u++)
-        if (da[u] != ~0u) o.dout[base + da[u]] = v[u];
-    }
-    // topics with more than kSoloLds solo parts: the rest from the record,
-    // part by part (a wavefront per part; rare: Zipf hub topics)
-    uint64_t ovm = __ballot(gl == 0 && bounded && fits && !o.runs && nq > (uint32_t)kSoloLds);
-    if (ovm) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wavefront's record stores have landed
-      __builtin_amdgcn_wave_barrier();
-    }
-    while (ovm) {
-      const int src = __ffsll((unsigned long long)ovm) - 1;
-      ovm &= ovm - 1;
-      const uint32_t tq = __shfl(t, src, kWave), nqq = __shfl(nq, src, kWave);
-      uint64_t at = shfl64(ds, src) + __shfl(Qf, src, kWave);
-      const uint32_t *rg = o.recs + (uint64_t)tq * kRecStrideAlloc;
-      for (uint32_t j = kSoloLds; j < nqq; j++) {
-        const uint32_t off = __hip_atomic_load(rg + 2 * j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t cnt = __hip_atomic_load(rg + 2 * j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (uint32_t i = lane; i < cnt; i += kWave)
-          o.dout[at + i] = __builtin_amdgcn_raw_buffer_load_b32(words, (int)((off + i) * 4u), 0, 0);
-        at += cnt;
-      }
-    }
-    if (gl == 0 && bounded) {
-      n_parts += nq;
-      if (n_solo + Ss < n_solo) atomicAdd(&o.ctr->n_solo, (unsigned long long)n_solo), n_solo = 0;
-      n_solo += Ss;
-    }
     wave_lds_sync();
   }
-  // the wavefront's solo parts (one atomic per wavefront, not per topic)
-#pragma unroll
-  for (int m = kWave / 2; m > 0; m >>= 1) n_parts += __shfl_xor(n_parts, m, kWave);
-  if (lane == 0 && n_parts) atomicAdd(&o.ctr->n_desc, (unsigned long long)n_parts);
   if (n_solo) atomicAdd(&o.ctr->n_solo, (unsigned long long)n_solo);  // (group leaders)
+  if (n_parts) atomicAdd(&o.ctr->n_desc, (unsigned long long)n_parts);
 }
+
 
 // ---------------------------------------------------------------------------
 // Emission of the topics with multi entries.  A topic's deliveries are
@@ -816,6 +655,205 @@ __device__ __forceinline__ SubEnt load_sub(const DeviceSnapshot &s, uint32_t sid
 }
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// ---- k_desc: solo parts -> copy descriptors ----------------------------------
+// A wavefront per 64 consecutive topics.  Their descriptors are one contiguous
+// range of desc (desc_start is the exclusive scan of nsolo), so lane k writes
+// descriptor k of the range (coalesced 16-B stores): its topic by a 6-step
+// search over the wave's prefix of solo-part counts in LDS, its output
+// position by a segmented scan of the part sizes (running per-topic position
+// carried in LDS across 64-part steps).  Also dcount of topics without multi
+// entries (the merges write the others').  Round 1 ran a thread per topic:
+// scattered 16-B stores wrote 2.8x the descriptor bytes.
+struct alignas(8) DescLds {
+  unsigned long long run[kWave];  // next output position of each topic's solo part
+  uint32_t pre[kWave + 1];        // exclusive prefix of the topics' solo-part counts
+};
+
+__global__ __launch_bounds__(256) void k_desc(Outputs o, uint32_t n, const uint64_t *__restrict__ desc_start,
+                                              uint4 *__restrict__ desc, uint64_t desc_cap) {
+  __shared__ DescLds lds_all[4];
+  const int lane = threadIdx.x & (kWave - 1);
+  DescLds &L = lds_all[threadIdx.x / kWave];
+  const uint32_t nw = gridDim.x * (blockDim.x / kWave);
+  for (uint32_t w = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave; (uint64_t)w * kWave < n; w += nw) {
+    const uint32_t t0 = w * kWave, t = t0 + lane;
+    uint32_t q = 0;
+    uint64_t db = 0;
+    if (t < n) {
+      const uint8_t cls = o.cls[t];
+      if (cls & kClsBounded) {
+        q = o.nsolo[t];
+        db = o.dstart[t];
+        if (o.mcount[t] == 0) o.dcount[t] = o.scount[t];
+      }
+    }
+    uint32_t inc = q;  // inclusive scan of q over the wave
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const uint32_t v = __shfl_up(inc, d, kWave);
+      if (lane >= d) inc += v;
+    }
+    const uint32_t Q = __shfl(inc, kWave - 1, kWave);
+    if (Q == 0) continue;  // wave-uniform
+    L.pre[lane] = inc - q;
+    if (lane == 0) L.pre[kWave] = Q;
+    L.run[lane] = db;
+    const uint64_t pb = desc_start[t0];
+    wave_lds_sync();
+    for (uint32_t k0 = 0; k0 < Q; k0 += kWave) {
+      const uint32_t k = k0 + lane;
+      const bool valid = k < Q;
+      uint32_t j = 0;  // the topic holding part k: the largest j with pre[j] <= k
+#pragma unroll
+      for (uint32_t step = 32; step > 0; step >>= 1) j = L.pre[j + step] <= k ? j + step : j;  // j + step <= 63
+      uint2 part = make_uint2(0, 0);
+      if (valid) part = *reinterpret_cast<const uint2 *>(o.recs + (uint64_t)(t0 + j) * kRecStrideAlloc + 2 * (k - L.pre[j]));
+      const uint32_t seg = valid ? j : kWave;  // invalid lanes: a segment of their own, size 0
+      uint32_t si = part.y;
+#pragma unroll
+      for (int d = 1; d < kWave; d <<= 1) {
+        const uint32_t v = __shfl_up(si, d, kWave);
+        const uint32_t sj = __shfl_up(seg, d, kWave);
+        if (lane >= d && sj == seg) si += v;
+      }
+      const uint64_t at = valid ? L.run[j] + (si - part.y) : 0;
+      const bool seg_end = __shfl_down(seg, 1, kWave) != seg || lane == kWave - 1;
+      wave_lds_sync();
+      if (valid) {
+        put_checked(desc, pb + k, desc_cap, make_uint4(part.x, part.y, (uint32_t)at, (uint32_t)(at >> 32)), &o.ctr->oob);
+        if (seg_end) L.run[j] += si;
+      }
+      wave_lds_sync();
+    }
+  }
+}
+
+// window w of the output space [w * kWin, (w + 1) * kWin) -> the descriptor
+// holding (or, in a gap, preceding) its first position; windows before the
+// first descriptor map to it
+constexpr uint32_t kWin = 4096;
+// (counts read on the device: nd = solo descriptors, clamped to their buffer;
+// total = solo output positions; windows past win_cap flag the call)
+__global__ __launch_bounds__(256) void k_winmap(const uint4 *__restrict__ desc, const uint64_t *__restrict__ nd_ptr,
+                                                uint64_t desc_cap, const uint64_t *__restrict__ total_ptr,
+                                                uint32_t *__restrict__ win, uint64_t win_cap, unsigned int *oob) {
+  const uint64_t nd = min(*nd_ptr, desc_cap), total = *total_ptr;
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nd; j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint4 a = desc[j];
+    const uint64_t d = a.z | ((uint64_t)a.w << 32);
+    uint64_t e = total;
+    if (j + 1 < nd) {
+      const uint4 b = desc[j + 1];
+      e = b.z | ((uint64_t)b.w << 32);
+    }
+    const uint64_t lo = j == 0 ? 0 : (d + kWin - 1) / kWin, hi = (e + kWin - 1) / kWin;
+    if (hi > win_cap) atomicOr(oob, 1u);
+    for (uint64_t w = lo; w < hi && w < win_cap; w++) win[w] = (uint32_t)j;
+  }
+}
+
+// ---- k_wincopy: the solo deliveries, a wavefront per output window ----------
+// Loads 64 descriptors from the window's first one (one coalesced 16-B load
+// per lane), clips them to the window in LDS, then moves kCU entries per lane
+// and step: position q -> its descriptor by a 6-step search over the clipped
+// starts -> words[src + q - start] -> dout[q] (the word IS the packed
+// delivery: a 4-B copy, lane-consecutive loads and stores).  More than 64
+// descriptors in a window (many tiny topics): the next 64, from where the
+// previous batch ended.
+constexpr int kCU = 16;  // entries per lane per step
+// position -> descriptor through a per-64-position block index (the last
+// descriptor starting at or before each block, one search per block and
+// descriptor batch), then a search inside the block's few descriptors —
+// usually none or one step instead of six per entry
+struct alignas(16) WinLds {
+  uint32_t st[kWave], en[kWave], src[kWave];
+  uint32_t blk[kWin / kWave];
+};
+
+__global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_eu(8))) void k_wincopy(
+    DeviceSnapshot s, const uint4 *__restrict__ desc, const uint64_t *__restrict__ nd_ptr, uint64_t desc_cap,
+    const uint32_t *__restrict__ win, uint64_t win_cap, const uint64_t *__restrict__ total_ptr,
+    uint32_t *__restrict__ out, uint64_t cap, unsigned int *oob) {
+  __shared__ WinLds lds_all[kEmitWaves];
+  const uint64_t nd = min(*nd_ptr, desc_cap), total = *total_ptr;
+  const uint64_t nwin = min((total + kWin - 1) / kWin, win_cap);
+  const int lane = threadIdx.x & (kWave - 1);
+  WinLds &L = lds_all[threadIdx.x / kWave];
+  // words through a buffer descriptor: 32-bit offsets, bounds-checked reads
+  const __amdgpu_buffer_rsrc_t words =
+      __builtin_amdgcn_make_buffer_rsrc((void *)s.words, (short)0, (int)(s.n_subs * 4u + 64u), 0x00020000);
+  const uint64_t nw = (uint64_t)gridDim.x * kEmitWaves;
+  for (uint64_t w = (uint64_t)blockIdx.x * kEmitWaves + threadIdx.x / kWave; w < nwin; w += nw) {
+    const uint64_t g0 = w * kWin, g1 = min(g0 + kWin, total);
+    uint64_t j = win[w];
+    uint64_t pos = g0;
+    while (pos < g1 && j < nd) {
+      const uint64_t jj = j + lane;
+      uint4 d = make_uint4(0, 0, 0xFFFFFFFFu, 0xFFFFFFFFu);
+      if (jj < nd) d = desc[jj];
+      const uint64_t dst = d.z | ((uint64_t)d.w << 32);
+      const uint64_t dend = jj < nd ? dst + d.y : ~0ull;
+      uint64_t a = dst > pos ? dst : pos, b = dend < g1 ? dend : g1;
+      if (b < a) b = a;
+      if (a > g1) a = b = g1;
+      // positions handled by this batch: up to the end of its last descriptor
+      const uint64_t last_end = shfl64(dend, kWave - 1);
+      const uint64_t bend = j + kWave < nd ? (last_end < g1 ? (last_end > pos ? last_end : pos) : g1) : g1;
+      L.st[lane] = (uint32_t)(a - g0);
+      L.en[lane] = (uint32_t)(b - g0);
+      L.src[lane] = d.x + (uint32_t)(a - dst);
+      wave_lds_sync();
+      {  // block lane (positions lane * 64 ..): the last descriptor starting at or before its start
+        static_assert(kWin / kWave == kWave, "one block per lane");
+        const uint32_t q = (uint32_t)lane * kWave;
+        uint32_t k = 0;
+#pragma unroll
+        for (uint32_t step = 32; step > 0; step >>= 1) k = L.st[k + step] <= q ? k + step : k;
+        L.blk[lane] = k;
+      }
+      wave_lds_sync();
+      const uint32_t q0 = (uint32_t)(pos - g0), q1 = (uint32_t)(bend - g0);
+      for (uint32_t base = q0; base < q1; base += kWave * kCU) {
+        uint32_t sa[kCU];
+        bool in[kCU];
+#pragma unroll
+        for (int u = 0; u < kCU; u++) {
+          const uint32_t q = base + u * kWave + lane;
+          // the last descriptor starting at or before q: within [blk[b], blk[b + 1]]
+          const uint32_t bq = min(q, (uint32_t)kWin - 1) / kWave;
+          uint32_t k = L.blk[bq], left = (bq + 1 < kWin / kWave ? L.blk[bq + 1] : kWave - 1) - k;
+          while (left > 0) {
+            const uint32_t half = (left + 1) / 2;
+            if (L.st[k + half] <= q) {
+              k += half;
+              left -= half;
+            } else {
+              left = half - 1;
+            }
+          }
+          in[u] = q < q1 && q >= L.st[k] && q < L.en[k];
+          sa[u] = in[u] ? L.src[k] + (q - L.st[k]) : 0u;
+        }
+        uint32_t v[kCU];
+#pragma unroll
+        for (int u = 0; u < kCU; u++) v[u] = __builtin_amdgcn_raw_buffer_load_b32(words, (int)(sa[u] * 4u), 0, 0);
+#pragma unroll
+        for (int u = 0; u < kCU; u++) {
+          if (!in[u]) continue;
+          const uint64_t p = g0 + base + u * kWave + lane;
+          if (p < cap)
+            out[p] = v[u];
+          else
+            atomicOr(oob, kOobStore);
+        }
+      }
+      wave_lds_sync();
+      pos = bend;
+      j += kWave;
+    }
+  }
+}
 
 // ---- k_shared: shared candidates (gatherSharedSubscriptions, topics.go:541-555)
 // a 16-lane group per topic with H > 0: its shared hits are id ranges
@@ -1662,13 +1700,13 @@ __global__ __launch_bounds__(256) void k_zero_tab(unsigned long long *__restrict
     tab[i] = 0;
 }
 
-// what the call needed, for the host: the walk's reservations (dstart[n]: the
-// DFS tails start there) and the shared candidates' total
-__global__ void k_totals(Counters *ctr, uint64_t *__restrict__ dstart, const uint64_t *__restrict__ hstart, uint32_t n) {
+// what the call needed, for the host (read back once, at the end)
+__global__ void k_totals(Counters *ctr, const uint64_t *__restrict__ dstart, const uint64_t *__restrict__ hstart,
+                         const uint64_t *__restrict__ desc_start, uint32_t n) {
   if (threadIdx.x == 0) {
-    ctr->s_total = ctr->dcur;
-    dstart[n] = ctr->dcur;
+    ctr->s_total = dstart[n];
     ctr->h_total = hstart[n];
+    (void)desc_start;  // (n_desc: the walk counts the solo parts, runs form included)
   }
 }
 
@@ -1947,16 +1985,18 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
   if (ws.pending) return -1;  // one call in flight per workspace (collect it first)
   // queued calls need every output buffer sized by an earlier call
   exact = exact || !ws.caps_known;
-  if (ws.get(W::kHCount, sizeof(uint32_t) * (n + 1)) || ws.get(W::kDCount, sizeof(uint32_t) * (n + 1)) ||
-      ws.get(W::kDStart, sizeof(uint64_t) * (n + 1)) || ws.get(W::kHStart, sizeof(uint64_t) * (n + 1)) ||
-      ws.get(W::kCls, n + 1) || ws.get(W::kDfsList, sizeof(uint32_t) * (n + 2)) ||
-      ws.get(W::kMCount, sizeof(uint32_t) * (n + 1)) ||
-      ws.get(W::kRecs, sizeof(uint32_t) * kRecStrideAlloc * ((uint64_t)n + 1)) || ws.get(W::kCounters, 256))
+  if (ws.get(W::kSCount, sizeof(uint32_t) * (n + 1)) || ws.get(W::kHCount, sizeof(uint32_t) * (n + 1)) ||
+      ws.get(W::kDCount, sizeof(uint32_t) * (n + 1)) || ws.get(W::kDStart, sizeof(uint64_t) * (n + 1)) ||
+      ws.get(W::kHStart, sizeof(uint64_t) * (n + 1)) || ws.get(W::kCls, n + 1) ||
+      ws.get(W::kDfsList, sizeof(uint32_t) * (n + 2)) || ws.get(W::kMCount, sizeof(uint32_t) * (n + 1)) ||
+      ws.get(W::kRecs, sizeof(uint32_t) * kRecStrideAlloc * ((uint64_t)n + 1)) || ws.get(W::kCounters, 256) ||
+      ws.get(W::kNSolo, sizeof(uint32_t) * (n + 1)) || ws.get(W::kDescStart, sizeof(uint64_t) * (n + 1)))
     return -2;
   Counters *hc = pinned_counters(ws);
   if (!hc) return -2;
 
   Outputs o{};
+  o.scount = (uint32_t *)ws.ptr(W::kSCount);
   o.hcount = (uint32_t *)ws.ptr(W::kHCount);
   o.dcount = (uint32_t *)ws.ptr(W::kDCount);
   o.dstart = (uint64_t *)ws.ptr(W::kDStart);
@@ -1966,12 +2006,25 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
   o.mcount = (uint32_t *)ws.ptr(W::kMCount);
   o.recs = (uint32_t *)ws.ptr(W::kRecs);
   o.ctr = (Counters *)ws.ptr(W::kCounters);
-  o.keep_solo = ws.keep_solo ? 1u : 0u;
+  o.nsolo = (uint32_t *)ws.ptr(W::kNSolo);
   o.runs = ws.runs ? 1u : 0u;
-  if (ws.runs) {
-    if (ws.get(W::kSCount, sizeof(uint32_t) * (n + 1))) return -2;
-    o.scount = (uint32_t *)ws.ptr(W::kSCount);
+  auto *desc_start = (uint64_t *)ws.ptr(W::kDescStart);
+  HIP_TRY(hipMemsetAsync(o.ctr, 0, sizeof(Counters), st));
+  mark(ws, 0, st);
+  if (n > 0) {
+    constexpr uint32_t per_block = kWalkWaves * (kWave / kWalkG);
+    const uint32_t blocks = std::max<uint32_t>(
+        1, std::min<uint32_t>((n + per_block - 1) / per_block, resident_blocks(ws, 0, k_walk<kWalkG>)));
+    hipLaunchKernelGGL(k_walk<kWalkG>, dim3(blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o);
   }
+  HIP_TRY(hipGetLastError());
+  mark(ws, 1, st);
+  // segment starts: exclusive scans of S (raw entries, an upper bound of a
+  // topic's deliveries) and H (shared candidates); the solo descriptors'
+  // positions: exclusive scan of the solo-part counts
+  if (scan_offsets(ws, (const uint32_t *)o.scount, o.dstart, n, st) ||
+      scan_offsets(ws, (const uint32_t *)o.hcount, o.hstart, n, st) || scan_offsets(ws, o.nsolo, desc_start, n, st))
+    return -3;
   // merge lists
   const W::Slot list_slots[kNLists] = {W::kListS, W::kListW, W::kListT1, W::kListT2, W::kListT3,
                                        W::kListP, W::kListH, W::kListRS, W::kListR};
@@ -1981,57 +2034,22 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
     lists.l[l] = (uint32_t *)ws.ptr(list_slots[l]);
   }
   unsigned int *lcount = &o.ctr->n_small;  // kNLists consecutive counters
+  if (n > 0) {
+    hipLaunchKernelGGL(k_route, dim3(std::min<uint32_t>((n + 4095) / 4096, 2048)), dim3(256), 0, st, o.cls, o.mcount,
+                       o.hcount, n, lists, lcount, o.ctr->m_sum, resolve_min());
+    HIP_TRY(hipGetLastError());
+  }
+  hipLaunchKernelGGL(k_totals, dim3(1), dim3(64), 0, st, o.ctr, o.dstart, o.hstart, desc_start, n);
+  HIP_TRY(hipGetLastError());
+  if (exact) {  // the one read-back that sizes the outputs
+    HIP_TRY(hipMemcpyAsync(hc, o.ctr, sizeof(Counters), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+  }
   // capacity of a buffer in elements (one element kept spare, as the exact sizing does)
   auto cap_of = [&](W::Slot sl, size_t elem) -> uint64_t {
     const size_t c = ws.bufs[sl].cap / elem;
     return c ? c - 1 : 0;
   };
-
-  // walk (tokenize, walk, reserve the output segments, copy the solo
-  // entries into dout), the shared candidates' offsets, the merge lists, the
-  // totals.  A walk whose reservations outgrow dout flags oob and copies
-  // nothing past it.
-  auto walk_phase = [&](uint64_t dcap) -> int {
-    o.dout = (uint32_t *)ws.ptr(W::kDOut);
-    o.dcap = o.dout ? dcap : 0;
-    HIP_TRY(hipMemsetAsync(o.ctr, 0, sizeof(Counters), st));
-    mark(ws, 0, st);
-    if (n > 0) {
-      constexpr uint32_t per_block = kWalkWaves * (kWave / kWalkG);
-      const uint32_t blocks = std::max<uint32_t>(
-          1, std::min<uint32_t>((n + per_block - 1) / per_block, resident_blocks(ws, 0, k_walk<kWalkG>)));
-      hipLaunchKernelGGL(k_walk<kWalkG>, dim3(blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o);
-    }
-    HIP_TRY(hipGetLastError());
-    mark(ws, 1, st);
-    if (scan_offsets(ws, (const uint32_t *)o.hcount, o.hstart, n, st)) return -3;
-    if (n > 0) {
-      hipLaunchKernelGGL(k_route, dim3(std::min<uint32_t>((n + 4095) / 4096, 2048)), dim3(256), 0, st, o.cls,
-                         o.mcount, o.hcount, n, lists, lcount, o.ctr->m_sum, resolve_min());
-      HIP_TRY(hipGetLastError());
-    }
-    hipLaunchKernelGGL(k_totals, dim3(1), dim3(64), 0, st, o.ctr, o.dstart, o.hstart, n);
-    HIP_TRY(hipGetLastError());
-    return 0;
-  };
-  // exact: read the reservations back (the one read-back that sizes the
-  // outputs) and walk again into a dout that holds them if it did not; the
-  // chunked reservations vary a little from run to run, so a rerun gets the
-  // 25 % headroom every buffer gets
-  uint64_t dcap = cap_of(W::kDOut, sizeof(uint32_t));
-  for (int attempt = 0;; attempt++) {
-    if (int rc = walk_phase(dcap)) return rc;
-    if (!exact) break;
-    HIP_TRY(hipMemcpyAsync(hc, o.ctr, sizeof(Counters), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    if (hc->s_total <= o.dcap && !(hc->oob & kOobWalk)) break;
-    if (attempt == 3) {
-      fprintf(stderr, "mqmatch: the walk's output reservations kept outgrowing their buffer\n");
-      return -3;
-    }
-    if (ws.get(W::kDOut, sizeof(uint32_t) * (hc->s_total + hc->s_total / 8 + 1))) return -2;
-    dcap = cap_of(W::kDOut, sizeof(uint32_t));
-  }
 
   // DFS topics (a capacity of the walk exceeded): phase 0 counts each one's
   // raw entries, k_dfs_prep sizes their tables and tails on the device
@@ -2051,7 +2069,7 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
   }
   o.dfs_cap = dfs_cap;
   const uint32_t fb_blocks = exact ? std::max<uint32_t>(1, std::min<uint32_t>(hc->n_dfs, 4096)) : 1024;
-  uint64_t hcap, tab_cap = 0;
+  uint64_t dcap, hcap, desc_cap, win_cap, tab_cap = 0;
   if (exact) {
     if (dfs) {
       hipLaunchKernelGGL(k_dfs<0>, dim3(fb_blocks), dim3(kWave), fb_lds, st, s, d_bytes, d_offs, o, raw_cnt, raw_h,
@@ -2065,18 +2083,25 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
     }
     dcap = hc->s_total + hc->dfs_raw;
     hcap = hc->h_total + hc->dfs_h;
+    desc_cap = hc->n_desc;
+    win_cap = (hc->s_total + kWin - 1) / kWin;
     tab_cap = hc->tab_total;
-    // (dout keeps the walk's solo deliveries when it grows for the DFS tails)
-    if (ws.grow_keep(W::kDOut, sizeof(uint32_t) * hc->s_total, sizeof(uint32_t) * (dcap + 1), st)) return -2;
   } else {  // what the buffers hold
+    dcap = cap_of(W::kDOut, sizeof(uint32_t));
     hcap = cap_of(W::kHOut, sizeof(uint32_t));
+    desc_cap = cap_of(W::kDesc, sizeof(uint4));
+    win_cap = cap_of(W::kWin, sizeof(uint32_t));
     tab_cap = std::max<uint64_t>(cap_of(W::kTable, sizeof(GEnt)), 1u << 16);
   }
-  if (ws.get(W::kHOut, sizeof(uint32_t) * (hcap + 1))) return -2;
+  if (ws.get(W::kDOut, sizeof(uint32_t) * (dcap + 1)) || ws.get(W::kHOut, sizeof(uint32_t) * (hcap + 1)) ||
+      ws.get(W::kDesc, sizeof(uint4) * (desc_cap + 1)) || ws.get(W::kWin, sizeof(uint32_t) * (win_cap + 1)))
+    return -2;
   o.dout = (uint32_t *)ws.ptr(W::kDOut);
   o.hout = (uint32_t *)ws.ptr(W::kHOut);
   o.dcap = dcap;
   o.hcap = hcap;
+  auto *desc = (uint4 *)ws.ptr(W::kDesc);
+  auto *win = (uint32_t *)ws.ptr(W::kWin);
   GEnt *tab = nullptr;
   if (dfs) {
     if (ws.get(W::kTable, sizeof(GEnt) * (tab_cap + 1))) return -2;
@@ -2155,6 +2180,22 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
                          lcount + kLWave);
       HIP_TRY(hipGetLastError());
     }
+    // the solo copy (none in the runs form: the solo parts stay runs)
+    if (!ws.runs) {
+      hipLaunchKernelGGL(k_desc, dim3(std::min<uint32_t>((n + 255) / 256, 8192)), dim3(256), 0, st, o, n, desc_start,
+                         desc, desc_cap);  // a wavefront per 64 topics
+      HIP_TRY(hipGetLastError());
+      if (!exact || hc->n_desc > 0) {
+        const uint64_t nd_grid = exact ? hc->n_desc : desc_cap;
+        hipLaunchKernelGGL(k_winmap,
+                           dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nd_grid + 255) / 256, 8192))),
+                           dim3(256), 0, st, desc, desc_start + n, desc_cap, o.dstart + n, win, win_cap, &o.ctr->oob);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_wincopy, grid(k_wincopy), dim3(kWave * kEmitWaves), 0, st, s, desc, desc_start + n,
+                           desc_cap, win, win_cap, o.dstart + n, o.dout, o.dcap, &o.ctr->oob);
+        HIP_TRY(hipGetLastError());
+      }
+    }
     if (l_sh) {
       const uint32_t nsh = exact ? hc->n_shlist : n;
       hipLaunchKernelGGL(k_shared, dim3(std::min<uint32_t>((nsh + 15) / 16, 8192)), dim3(256), 0, st, o,
@@ -2185,7 +2226,6 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
   ws.last_n = n;
   ws.last_bytes = d_bytes;
   ws.last_offs = d_offs;
-  ws.last_keep_solo = ws.keep_solo || ws.runs;
   ws.last_runs = ws.runs;
   ws.pend_exact = exact;
   ws.pending = true;
@@ -2310,7 +2350,7 @@ int runs_device(Workspace &ws, hipStream_t st, const MatchOutput &m, RunsOutput 
 int identifiers_device(const DeviceSnapshot &s, Workspace &ws, hipStream_t st, IdentOutput *out) {
   using W = Workspace;
   const uint32_t n = ws.last_n;
-  if (!ws.last_valid || !ws.last_keep_solo) return -1;  // (the walk kept the solo parts in LDS only)
+  if (!ws.last_valid) return -1;
   if (ws.get(W::kICount, sizeof(uint32_t) * (n + 1)) || ws.get(W::kIStart, sizeof(uint64_t) * (n + 1))) return -2;
   Outputs o{};
   o.cls = (uint8_t *)ws.ptr(W::kCls);
