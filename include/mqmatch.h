@@ -67,6 +67,17 @@ extern "C" {
  * arriving while a batch runs form the next batch (no added latency when
  * idle; mqm_batching_policy can add a linger).  Results are identical. */
 #define MQM_CFG_BATCHING 8u
+/* MQM_CFG_SERVE: mqm_subscribers calls go to a persistent GPU server instead
+ * (the per-publish call shape with no kernel launch and no stream
+ * synchronisation per call): the caller writes its topic into a ring slot in
+ * pinned host memory, one of the server's resident workgroups claims it, runs
+ * the small-batch path's per-topic match straight into the slot and flags it
+ * done; the caller spins on that flag.  The server occupies `grid` CUs while
+ * it runs and exits after `idle_us` without a call (relaunched on the next);
+ * mqm_serve_policy sets both (default 32 workgroups, 20000 us).  Topics or
+ * results past a slot's capacities take the batch path.  Results are
+ * identical.  Takes precedence over MQM_CFG_BATCHING. */
+#define MQM_CFG_SERVE 16u
 /* device value for a host-only index: the store and its mutation API work,
  * mqm_commit / mqm_match_* return MQM_ENODEV (there is no CPU match path). */
 #define MQM_DEVICE_NONE (-1)
@@ -269,6 +280,12 @@ int mqm_subscribers(mqm_index *h, const char *topic, size_t topic_len, mqm_resul
  * threads are inside mqm_subscribers: the collector is published atomically,
  * and calls already past that point finish on the direct path. */
 int mqm_batching_policy(mqm_index *h, uint32_t max_batch, uint32_t linger_us);
+/* MQM_CFG_SERVE: the server's workgroups and idle timeout (applied at its
+ * next launch; on an index created without the flag it turns serving on);
+ * statistics: calls served in the ring, calls that took the batch path, server
+ * launches.  MQM_EINVAL on a host-only index (or for stats while off). */
+int mqm_serve_policy(mqm_index *h, uint32_t grid, uint32_t idle_us);
+int mqm_serve_stats(mqm_index *h, uint64_t *served, uint64_t *fallbacks, uint64_t *launches);
 int mqm_batching_stats(mqm_index *h, uint64_t *batches, uint64_t *topics);
 /* Device in / device out on `hip_stream` (hipStream_t, NULL = default stream). */
 int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t *d_topic_offsets,

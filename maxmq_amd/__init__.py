@@ -218,19 +218,22 @@ class TopicsIndex:
     """TopicsIndex (topics.go:285) backed by the MI355X matcher."""
 
     def __init__(self, device: int | None = 0, autocommit: bool = True, identifiers: bool = False,
-                 async_commit: bool = False, batching: bool = False):
+                 async_commit: bool = False, batching: bool = False, serve: bool = False):
         """identifiers=True: match_batch / subscribers also return the full
         Subscription.Identifiers maps (an extra GPU pass per batch).
         async_commit=True: mutations are logged and snapshots are rebuilt by a
         background builder (commit_async / commit_poll / commit_policy).
         batching=True: concurrent subscribers() calls are gathered into GPU
-        batches by a collector thread (MQM_CFG_BATCHING)."""
+        batches by a collector thread (MQM_CFG_BATCHING).
+        serve=True: subscribers() calls go to a persistent GPU server through
+        a ring of pinned slots (MQM_CFG_SERVE; no launch per call)."""
         L = lib()
         cfg = capi.Config(capi.MQM_DEVICE_NONE if device is None else device,
                           (capi.MQM_CFG_AUTOCOMMIT if autocommit else 0) |
                           (capi.MQM_CFG_IDENTIFIERS if identifiers else 0) |
                           (capi.MQM_CFG_ASYNC_COMMIT if async_commit else 0) |
-                          (capi.MQM_CFG_BATCHING if batching else 0))
+                          (capi.MQM_CFG_BATCHING if batching else 0) |
+                          (capi.MQM_CFG_SERVE if serve else 0))
         h = C.c_void_p()
         check("mqm_create", L.mqm_create(C.byref(cfg), C.byref(h)))
         self._h = h
@@ -239,6 +242,15 @@ class TopicsIndex:
 
     def batching_policy(self, max_batch: int = 0, linger_us: int = 0):
         check("mqm_batching_policy", lib().mqm_batching_policy(self._h, max_batch, linger_us))
+
+    def serve_policy(self, grid: int = 0, idle_us: int = 0):
+        check("mqm_serve_policy", lib().mqm_serve_policy(self._h, grid, idle_us))
+
+    def serve_stats(self):
+        """(calls served in the ring, calls that took the batch path, server launches)"""
+        a, b_, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        check("mqm_serve_stats", lib().mqm_serve_stats(self._h, C.byref(a), C.byref(b_), C.byref(c)))
+        return a.value, b_.value, c.value
 
     def batching_stats(self):
         """(batches run, topics they carried) of the MQM_CFG_BATCHING collector"""

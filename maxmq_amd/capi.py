@@ -27,6 +27,7 @@ MQM_CFG_AUTOCOMMIT = 1
 MQM_CFG_IDENTIFIERS = 2
 MQM_CFG_ASYNC_COMMIT = 4
 MQM_CFG_BATCHING = 8
+MQM_CFG_SERVE = 16
 MQM_DEVICE_NONE = -1
 
 ERRORS = {MQM_EINVAL: "EINVAL", MQM_ENOMEM: "ENOMEM", MQM_EHIP: "EHIP", MQM_ELIMIT: "ELIMIT",
@@ -48,6 +49,7 @@ EXPORTED = [
     "mqm_debug_fault", "mqm_gather_shards_shared", "mqm_match_ctx_create", "mqm_match_ctx_destroy",
     "mqm_match_device_async", "mqm_match_ctx_wait", "mqm_match_ctx_stats", "mqm_match_batch_packed",
     "mqm_result_packed", "mqm_match_batch_runs", "mqm_result_runs", "mqm_result_expand",
+    "mqm_serve_policy", "mqm_serve_stats",
 ]
 
 
@@ -208,6 +210,8 @@ def lib():
         "mqm_match_batch_runs": ([vp, vp, vp, u32, C.POINTER(vp)], C.c_int),
         "mqm_result_runs": ([vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), C.POINTER(u64)], C.c_int),
         "mqm_result_expand": ([vp, u32, u32, vp, vp], C.c_int),
+        "mqm_serve_policy": ([vp, u32, u32], C.c_int),
+        "mqm_serve_stats": ([vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)], C.c_int),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

@@ -118,6 +118,7 @@ struct MatchCtx {
 
 namespace {
 struct Collector;
+struct Server;
 }
 
 struct mqm_index {
@@ -149,6 +150,10 @@ struct mqm_index {
   // lock: an acquire load), published once with a release store under mu;
   // collector_owner keeps it alive until the index is destroyed
   std::unique_ptr<Collector> collector_owner;
+  // MQM_CFG_SERVE: the persistent per-publish server (published like the collector)
+  std::atomic<Server *> server{nullptr};
+  std::unique_ptr<Server> server_owner;
+  void stop_server();
   std::atomic<Collector *> collector{nullptr};
   std::atomic<uint32_t> live_ctxs{0};  // mqm_match_ctx objects of this index (mqm_destroy refuses while any live)
   void stop_collector();
@@ -517,6 +522,7 @@ int mqm_create(const mqm_config *cfg, mqm_index **out) {
     if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
     if (const char *e = getenv("MQM_NO_FAST")) h->fast_path = atoi(e) == 0;
     if (ctx_init(h.get(), &h->dev) != MQM_OK) return MQM_EHIP;
+    if ((h->cfg.flags & MQM_CFG_SERVE) && mqm_serve_policy(h.get(), 0, 0) != MQM_OK) return MQM_EHIP;
     if (h->cfg.flags & MQM_CFG_BATCHING) {
       h->collector_owner = std::make_unique<Collector>(h.get());
       h->collector.store(h->collector_owner.get(), std::memory_order_release);
@@ -530,7 +536,8 @@ int mqm_destroy(mqm_index *h) {
   if (!h) return MQM_EINVAL;
   // a match context reads the index: it must be destroyed first
   if (h->live_ctxs.load(std::memory_order_acquire) != 0) return MQM_EINVAL;
-  h->stop_collector();  // first: its thread matches (and may commit) through this index
+  h->stop_server();     // first: its kernel reads the snapshot
+  h->stop_collector();  // its thread matches (and may commit) through this index
   h->builder.reset();    // finishes a running build and joins the worker
   if (h->cfg.device != MQM_DEVICE_NONE) {
     (void)hipSetDevice(h->cfg.device);
@@ -1372,7 +1379,143 @@ struct Collector {
   }
 };
 
+// MQM_CFG_SERVE: the persistent per-publish server (fast.hip k_serve).
+struct Server {
+  mqm_index *h;
+  ServeQueue *q = nullptr;                // pinned, coherent, device-mapped
+  unsigned long long *claimed = nullptr;  // device: requests claimed so far
+  hipStream_t st = nullptr;
+  std::mutex mu;                          // launches / snapshot switches
+  std::shared_ptr<GpuSnapshot> snap;      // what the running kernel reads
+  bool launched = false;                  // (mu) a launch may still run
+  uint32_t grid = 32, idle_us = 20000;
+  const bool want_ids;
+  std::atomic<uint64_t> ticket{0};
+  std::unique_ptr<std::atomic<uint64_t>[]> free_seq;  // slot i takes request k once free_seq[i] == k
+  std::atomic<uint64_t> served{0}, fallbacks{0}, launches{0};
+  std::atomic<bool> live{false};                   // launched (may have exited idle since)
+  std::atomic<const GpuSnapshot *> running_on{nullptr};
+
+  explicit Server(mqm_index *idx) : h(idx), want_ids((idx->cfg.flags & MQM_CFG_IDENTIFIERS) != 0) {
+    free_seq.reset(new std::atomic<uint64_t>[kServeSlots]);
+    for (uint32_t i = 0; i < kServeSlots; i++) free_seq[i].store(i);
+  }
+  int init() {
+    if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
+    void *p = nullptr;
+    if (hipHostMalloc(&p, sizeof(ServeQueue), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+      return MQM_ENOMEM;
+    q = static_cast<ServeQueue *>(p);
+    memset((void *)q, 0, sizeof(ServeQueue));
+    if (hipMalloc(&claimed, sizeof(unsigned long long)) != hipSuccess) return MQM_ENOMEM;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return MQM_EHIP;
+    if (hipMemsetAsync(claimed, 0, sizeof(unsigned long long), st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return MQM_EHIP;
+    return MQM_OK;
+  }
+  // (mu held) stop a running kernel and wait for it
+  void halt() {
+    if (!launched) return;
+    __atomic_store_n(&q->stop, 1ull, __ATOMIC_SEQ_CST);
+    (void)hipStreamSynchronize(st);
+    __atomic_store_n(&q->stop, 0ull, __ATOMIC_SEQ_CST);
+    launched = false;
+    live.store(false, std::memory_order_release);
+  }
+  ~Server() {
+    if (q) {
+      std::lock_guard<std::mutex> g(mu);
+      halt();
+    }
+    if (st) (void)hipStreamDestroy(st);
+    if (claimed) (void)hipFree(claimed);
+    if (q) (void)hipHostFree(q);
+  }
+  // the kernel runs on `cur` (mu held): relaunch when it has exited (idle) or
+  // the snapshot it reads is not the current one
+  int ensure(const std::shared_ptr<GpuSnapshot> &cur) {
+    if (launched && snap == cur && hipStreamQuery(st) == hipErrorNotReady) return MQM_OK;
+    halt();
+    snap = cur;
+    if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
+    if (serve_launch(snap->dev, q, claimed, grid, idle_us, want_ids, st) != 0) return MQM_EHIP;
+    launched = true;
+    launches++;
+    running_on.store(snap.get(), std::memory_order_release);
+    live.store(true, std::memory_order_release);
+    return MQM_OK;
+  }
+
+  int submit(const char *topic, size_t len, mqm_result **out) {
+    if (len > kServeTopic) {  // longer than a slot's topic bytes
+      fallbacks++;
+      return direct(topic, len, out);
+    }
+    std::shared_ptr<GpuSnapshot> cur;
+    int rc = front(h, &cur);  // (commits first with MQM_CFG_AUTOCOMMIT)
+    if (rc != MQM_OK) return rc;
+    const uint64_t k = ticket.fetch_add(1, std::memory_order_relaxed);
+    const uint32_t i = (uint32_t)(k % kServeSlots);
+    while (free_seq[i].load(std::memory_order_acquire) != k) __builtin_ia32_pause();  // the slot's previous caller is done
+    ServeSlot &sl = q->slot[i];
+    memcpy(sl.topic, topic, len);
+    sl.len = (uint32_t)len;
+    __atomic_store_n(&sl.seq, k + 1, __ATOMIC_RELEASE);
+    // (no HIP call on the common path: the kernel's liveness is checked only
+    // when a result is late, below)
+    if (!live.load(std::memory_order_acquire) || running_on.load(std::memory_order_acquire) != cur.get()) {
+      std::lock_guard<std::mutex> g(mu);
+      if ((rc = ensure(cur)) != MQM_OK) {
+        free_seq[i].store(k + kServeSlots, std::memory_order_release);
+        return rc;
+      }
+    }
+    // spin on the slot's done word; every ~50 us without it, make sure a
+    // server is still running (it exits after idle_us without a claim; the
+    // request then waits, unclaimed, for the relaunch)
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    auto check = t0 + std::chrono::microseconds(50);
+    while (__atomic_load_n(&sl.done, __ATOMIC_ACQUIRE) != k + 1) {
+      __builtin_ia32_pause();
+      const auto now = clk::now();
+      if (now < check) continue;
+      if (now - t0 > std::chrono::seconds(10)) {
+        fprintf(stderr, "mqmatch: per-publish server: no result for 10 s\n");
+        return MQM_EHIP;  // (the slot stays taken: its late result is never read)
+      }
+      std::lock_guard<std::mutex> g(mu);
+      if ((rc = ensure(snap ? snap : cur)) != MQM_OK) return rc;
+      check = now + std::chrono::microseconds(50);
+    }
+    const uint32_t status = sl.status;
+    if (status == kServeOk) {
+      try {
+        rc = Collector::single(cur->host, sl.dout, sl.dcount, sl.hout, sl.hcount, want_ids ? sl.iout : nullptr,
+                               want_ids ? sl.icount : 0, want_ids, out);
+      } catch (const std::bad_alloc &) {
+        rc = MQM_ENOMEM;
+      }
+      served++;
+    }
+    free_seq[i].store(k + kServeSlots, std::memory_order_release);
+    if (status == kServeOk) return rc;
+    fallbacks++;
+    return direct(topic, len, out);
+  }
+  int direct(const char *topic, size_t len, mqm_result **out) {
+    uint64_t offs[2] = {0, len};
+    return mqm_match_batch(h, topic ? topic : "", offs, 1, out);
+  }
+};
+
 }  // namespace
+
+void mqm_index::stop_server() {
+  server.store(nullptr, std::memory_order_release);
+  server_owner.reset();
+}
 
 void mqm_index::stop_collector() {
   collector.store(nullptr, std::memory_order_release);
@@ -1380,12 +1523,17 @@ void mqm_index::stop_collector() {
 }
 
 mqm_index::~mqm_index() {
-  stop_collector();  // first: its thread matches through this index
+  stop_server();     // first: its kernel reads this index's snapshot
+  stop_collector();  // its thread matches through this index
   pool.clear();
 }
 
 int mqm_subscribers(mqm_index *h, const char *topic, size_t topic_len, mqm_result **out) {
   if (!h || !out) return MQM_EINVAL;
+  if (Server *sv = h->server.load(std::memory_order_acquire)) {
+    *out = nullptr;
+    return guarded([&] { return sv->submit(topic ? topic : "", topic_len, out); });
+  }
   if (Collector *c = h->collector.load(std::memory_order_acquire)) {
     *out = nullptr;
     return guarded([&] { return c->submit(topic, topic_len, out); });
@@ -1415,6 +1563,42 @@ int mqm_batching_policy(mqm_index *h, uint32_t max_batch, uint32_t linger_us) {
   std::lock_guard<std::mutex> g(c->mu);
   c->max_batch = max_batch ? max_batch : 8192;
   c->linger_us = linger_us;
+  return MQM_OK;
+}
+
+// (the server is created once and kept: calls in flight hold no reference
+// beyond the index's lifetime)
+static int serve_enable_impl(mqm_index *h) {
+  std::lock_guard<std::mutex> g(h->mu);
+  if (h->server_owner) return MQM_OK;
+  return guarded([&] {
+    auto sv = std::make_unique<Server>(h);
+    const int rc = sv->init();
+    if (rc != MQM_OK) return rc;
+    h->server_owner = std::move(sv);
+    h->server.store(h->server_owner.get(), std::memory_order_release);
+    return MQM_OK;
+  });
+}
+
+int mqm_serve_policy(mqm_index *h, uint32_t grid, uint32_t idle_us) {
+  if (!h || h->cfg.device == MQM_DEVICE_NONE) return MQM_EINVAL;
+  int rc = serve_enable_impl(h);
+  if (rc != MQM_OK) return rc;
+  Server *sv = h->server.load(std::memory_order_acquire);
+  std::lock_guard<std::mutex> g(sv->mu);
+  sv->grid = grid ? std::min<uint32_t>(grid, 1024) : 32;
+  sv->idle_us = idle_us ? idle_us : 20000;
+  sv->halt();  // the next call launches with these
+  return MQM_OK;
+}
+
+int mqm_serve_stats(mqm_index *h, uint64_t *served, uint64_t *fallbacks, uint64_t *launches) {
+  Server *sv = h ? h->server.load(std::memory_order_acquire) : nullptr;
+  if (!sv || !served || !fallbacks || !launches) return MQM_EINVAL;
+  *served = sv->served.load();
+  *fallbacks = sv->fallbacks.load();
+  *launches = sv->launches.load();
   return MQM_OK;
 }
 

@@ -144,264 +144,305 @@ __device__ __forceinline__ void f_prefix(const uint32_t *v, uint32_t *pre, uint3
   if (lane == 0) pre[n] = run;
 }
 
+// ---------------------------------------------------------------------------
+// One topic's Subscribers by one workgroup: topic bytes (host-mapped) ->
+// the sink's result blocks.  Sink: reserve(L, raw entries, shared) -> false
+// when its blocks cannot take them (it records why; L.dbase / hbase / ibase
+// otherwise), fallback() (a capacity of this path: the batch pipeline has
+// none), done(L, deliveries, shared); dout / hout / iout its blocks (iout
+// nullptr: no Identifiers support).  Called by every thread of the block.
+// ---------------------------------------------------------------------------
+template <class Sink>
+__device__ __forceinline__ void fast_topic(const DeviceSnapshot &s, FastLds &L, const uint8_t *__restrict__ topic,
+                                           uint32_t len, Sink &sink) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (tid == 0) {
+    L.fail = len > kFStage ? 1u : 0u;
+    L.nh = L.nsh = 0;
+    L.nitems[0] = L.nitems[1] = 0;
+  }
+  __syncthreads();
+  const bool staged = len <= kFStage;
+  if (staged)
+    for (uint32_t i = tid; i < len; i += kFT) L.stage[i] = topic[i];
+  __syncthreads();
+  // ---- 1. separators and level keys ---------------------------------------
+  if (wid == 0 && staged) {
+    uint32_t nsep = 0;
+    for (uint32_t base = 0; base < len; base += 64) {
+      const uint32_t p = base + lane;
+      const bool sep = p < len && L.stage[p] == '/';
+      const uint64_t m = __ballot(sep);
+      if (sep) {
+        const uint32_t idx = nsep + __popcll(m & f_lanemask_lt(lane));
+        if (idx < kFLevels) L.sep[idx] = (uint16_t)p;
+      }
+      nsep += __popcll(m);
+    }
+    if (lane == 0) {
+      L.nsep = nsep;
+      if (nsep >= kFLevels) L.fail = 1;
+    }
+  }
+  __syncthreads();
+  const uint32_t nsep = staged ? L.nsep : 0;
+  const uint32_t nlev = (len == 0 || L.fail) ? 0 : nsep + 1;
+  const bool dollar = len > 0 && staged && L.stage[0] == '$';
+  if ((uint32_t)tid < nlev) {
+    const uint32_t st = tid == 0 ? 0 : L.sep[tid - 1] + 1u;
+    const uint32_t en = (uint32_t)tid < nsep ? L.sep[tid] : len;
+    const Key k = make_key([&](uint32_t i) { return L.stage[st + i]; }, en - st);
+    L.key0[tid] = k.k0;
+    L.key1[tid] = k.k1;
+  }
+  if (tid == 0 && nlev > 0) {  // level 0's items: the root's literal probe, '+' and '#' children
+    const NodeDesc root = load_desc(s.nodes);
+    uint32_t k = 0;
+    if ((root.sh_cnt_flags >> 24) & kFlagHasLiteral) L.item[0][k++] = (0u << 2) | kFItemLit;
+    if (root.plus != kNone) L.item[0][k++] = (root.plus << 2) | kFItemPlus;
+    if (root.hash != kNone) L.item[0][k++] = (root.hash << 2) | kFItemHash;
+    L.nitems[0] = k;
+  }
+  __syncthreads();
+  // ---- 2. level-synchronous walk -------------------------------------------
+  int cur = 0;
+  for (uint32_t d = 0; d < nlev; d++) {
+    const uint32_t ni = L.nitems[cur];
+    if (ni == 0 || L.fail) break;  // block-uniform (read after a barrier)
+    const uint64_t k0 = L.key0[d], k1 = L.key1[d];
+    const bool has_next = d + 1 < nlev;
+    // a topic level "+" / "#": its literal probe is the wildcard's (the
+    // reference visits that child twice, with no parent probe)
+    const bool lit_is_wild = (k1 == (1ull << 56)) && (k0 == '+' || k0 == '#');
+    const uint32_t tst = d == 0 ? 0 : L.sep[d - 1] + 1u;
+    const uint32_t tln = (d < nsep ? L.sep[d] : len) - tst;
+    for (uint32_t base = 0; base < ni; base += kFT) {
+      const uint32_t it = base + tid;
+      const bool live = it < ni;
+      const uint32_t iw = live ? L.item[cur][it] : 0;
+      const uint32_t kind = iw & 3u, id = iw >> 2;
+      const bool lit = kind == kFItemLit;
+      NodeDesc dc;
+      const uint32_t c = walk_step(s, live && lit && !lit_is_wild, live && !lit, id, id, k0, k1,
+                                   L.stage + tst, tln, &dc);
+      if (c == kNone) continue;
+      const uint32_t fl = dc.sh_cnt_flags >> 24;
+      const bool skip_dollar = dollar && (fl & kFlagDollarWild);      // topics.go:527
+      // a '#' node after a literal parent: gathered by the parent probe (kFlagParentLit)
+      const uint32_t c_own = skip_dollar || (fl & kFlagParentLit) ? 0 : dc.sub_cnt;
+      const uint32_t c_par = lit && !skip_dollar ? dc.hsub_cnt : 0;  // topics.go:507-509
+      const uint32_t c_sh = dc.sh_cnt_flags & kShCntMask;
+      if (((c_own | c_par) && (fl & kFlagMultiSat)) || c_own > kFRangeMax || c_par > kFRangeMax)
+        atomicOr(&L.fail, 1u);
+      if (c_own) {
+        const uint32_t h = atomicAdd(&L.nh, 1u);
+        if (h < kFHits) {
+          L.hoff[h] = dc.sub_off, L.hcnt[h] = c_own, L.hmu[h] = dc.multi & 0xFFFFu, L.hrank[h] = 2 * c;
+        } else {
+          atomicOr(&L.fail, 1u);
+        }
+      }
+      if (c_par) {  // the '#' child's range follows this node's (snapshot.h)
+        const uint32_t h = atomicAdd(&L.nh, 1u);
+        if (h < kFHits) {
+          L.hoff[h] = dc.sub_off + dc.sub_cnt, L.hcnt[h] = c_par, L.hmu[h] = dc.multi >> 16, L.hrank[h] = 2 * c + 1;
+        } else {
+          atomicOr(&L.fail, 1u);
+        }
+      }
+      if (c_sh) {
+        const uint32_t h = atomicAdd(&L.nsh, 1u);
+        if (h < kFSh) {
+          L.shoff[h] = dc.sh_off, L.shcnt[h] = c_sh;
+        } else {
+          atomicOr(&L.fail, 1u);
+        }
+      }
+      if (has_next && (fl & kFlagHasChildren)) {
+        const bool has_lit = fl & kFlagHasLiteral;
+        const uint32_t k = (has_lit ? 1u : 0u) + (dc.plus != kNone ? 1u : 0u) + (dc.hash != kNone ? 1u : 0u);
+        const uint32_t at = k ? atomicAdd(&L.nitems[cur ^ 1], k) : 0;
+        if (at + k > kFItems) {
+          atomicOr(&L.fail, 1u);
+        } else {
+          uint32_t j = at;
+          if (has_lit) L.item[cur ^ 1][j++] = (c << 2) | kFItemLit;
+          if (dc.plus != kNone) L.item[cur ^ 1][j++] = (dc.plus << 2) | kFItemPlus;
+          if (dc.hash != kNone) L.item[cur ^ 1][j++] = (dc.hash << 2) | kFItemHash;
+        }
+      }
+    }
+    __syncthreads();
+    if (tid == 0) L.nitems[cur] = 0;  // becomes the level after next's list
+    cur ^= 1;
+    __syncthreads();
+  }
+  if (L.fail) {  // block-uniform: the batch takes the pipeline without limits
+    if (tid == 0) sink.fallback();
+    __syncthreads();
+    return;
+  }
+  // ---- 3. emission -----------------------------------------------------------
+  // prefixes of the hits' solo counts, multi counts and the shared counts
+  // (one wave each, in place)
+  const uint32_t nh = L.nh, nsh = L.nsh;
+  if (wid == 0) {
+    for (uint32_t i = lane; i < nh; i += 64) L.spre[i] = L.hcnt[i] - L.hmu[i];
+    f_wave_lds_sync();
+    f_prefix(L.spre, L.spre, nh, lane);
+  } else if (wid == 1) {
+    for (uint32_t i = lane; i < nh; i += 64) L.mpre[i] = L.hmu[i];
+    f_wave_lds_sync();
+    f_prefix(L.mpre, L.mpre, nh, lane);
+  } else if (wid == 2) {
+    f_prefix(L.shcnt, L.shpre, nsh, lane);
+  }
+  __syncthreads();
+  const uint32_t Ss = L.spre[nh], Ms = L.mpre[nh], H = L.shpre[nsh];
+  if (tid == 0) {
+    L.nid = 0;
+    L.fail = sink.reserve(L, (unsigned long long)Ss + Ms, H) ? 0u : 1u;  // sets L.dbase / hbase / ibase
+  }
+  __syncthreads();
+  if (L.fail) {  // (the sink has recorded why: grow and run again, or the pipeline)
+    __syncthreads();
+    return;
+  }
+  uint64_t *const dout = sink.dout;
+  uint32_t *const hout = sink.hout;
+  uint32_t *const iout = sink.iout;
+  const uint64_t db = L.dbase, hb = L.hbase, ib = L.ibase;
+  // solo entries: each its client's merged delivery as is
+  for (uint32_t q = tid; q < Ss; q += kFT) {
+    const uint32_t h = f_search(L.spre, nh, q);
+    const uint32_t sid = L.hoff[h] + (q - L.spre[h]);
+    const uint2 e = *reinterpret_cast<const uint2 *>(s.subs + sid);
+    dout[db + q] = (uint64_t)e.x | ((uint64_t)(e.y & kPackedMask) << 32);
+    if (iout && (e.y & kWordIdent)) iout[ib + atomicAdd(&L.nid, 1u)] = sid;  // packets.go:257-259
+  }
+  // shared candidates
+  for (uint32_t j = tid; j < H; j += kFT) {
+    const uint32_t h = f_search(L.shpre, nsh, j);
+    hout[hb + j] = L.shoff[h] + (j - L.shpre[h]);
+  }
+  // multi entries: the per-client merge, in client-hash partitions
+  uint32_t W = 0;
+  const uint32_t P = Ms ? (Ms + kFPartCap - 1) / kFPartCap : 0;
+  const uint32_t per = P ? (Ms + P - 1) / P : 0;
+  uint32_t lg = 6;
+  while ((1u << lg) < 2 * per && (1u << lg) < kFSlots) lg++;
+  const uint32_t mask = (1u << lg) - 1;
+  for (uint32_t p = 0; p < P; p++) {
+    __syncthreads();  // the previous pass's winners are read
+    for (uint32_t j = tid; j <= mask; j += kFT) {
+      L.tkb[j] = 0;
+      L.tfirst[j] = ~0ull;
+    }
+    if (tid == 0) L.fill = 0;
+    __syncthreads();
+    for (uint32_t q = tid; q < Ms; q += kFT) {
+      const uint32_t h = f_search(L.mpre, nh, q);
+      const uint32_t sid = L.hoff[h] + (L.hcnt[h] - L.hmu[h]) + (q - L.mpre[h]);
+      const uint2 e = *reinterpret_cast<const uint2 *>(s.subs + sid);
+      if (P > 1 && f_partition(e.x, P) != p) continue;
+      if (iout && (e.y & kWordIdent)) iout[ib + atomicAdd(&L.nid, 1u)] = sid;
+      if (atomicAdd(&L.fill, 1u) >= (P > 1 ? kFFill : mask)) {  // an unlucky partition: never spin
+        atomicOr(&L.fail, 1u);
+        continue;
+      }
+      f_insert(L, mask, lg, e.x, e.y, L.hrank[h]);
+    }
+    __syncthreads();
+    // winners in slot order: wave w scans its quarter of the table twice
+    const uint32_t slots = mask + 1, q4 = (slots + kFWaves - 1) / kFWaves;
+    const uint32_t lo = wid * q4, hi = min(slots, lo + q4);
+    uint32_t cnt = 0;
+    for (uint32_t j0 = lo; j0 < hi; j0 += 64) {
+      const uint32_t j = j0 + lane;
+      cnt += __popcll(__ballot(j < hi && L.tkb[j] != 0));
+    }
+    if (lane == 0) L.wsum[wid] = cnt;
+    __syncthreads();
+    uint32_t w = W, tot = W;
+    for (int k = 0; k < kFWaves; k++) {
+      if (k < wid) w += L.wsum[k];
+      tot += L.wsum[k];
+    }
+    for (uint32_t j0 = lo; j0 < hi; j0 += 64) {
+      const uint32_t j = j0 + lane;
+      const bool occ = j < hi && L.tkb[j] != 0;
+      const uint64_t m = __ballot(occ);
+      if (occ) {
+        const unsigned long long kb = L.tkb[j];
+        const uint32_t v = (uint32_t)kb;
+        const uint32_t packed = ((uint32_t)L.tfirst[j] & kWordSidMask) | ((31u - __builtin_clz(v & 7u)) << 28) |
+                                (((v >> 3) & 1u) << 30);
+        dout[db + Ss + w + __popcll(m & f_lanemask_lt(lane))] = (uint64_t)((kb >> 32) - 1) | ((uint64_t)packed << 32);
+      }
+      w += __popcll(m);
+    }
+    W = tot;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    if (L.fail)
+      sink.fallback();
+    else
+      sink.done(L, Ss + W, H);
+  }
+  __syncthreads();
+}
+
+// the batch form's sink: ranges of the pinned result blocks reserved with one
+// atomic per topic, a FastRec per topic, flags for the host
+struct BatchSink {
+  FastCtl *ctl;
+  FastRec *recs;
+  uint32_t t;
+  uint64_t *dout;
+  uint64_t dcap;
+  uint32_t *hout;
+  uint64_t hcap;
+  uint32_t *iout;
+  uint64_t icap;
+  __device__ bool reserve(FastLds &L, unsigned long long need, uint32_t H) {
+    const unsigned long long db = need ? atomicAdd(&ctl->dcur, need) : 0ull;
+    const unsigned long long hb = H ? atomicAdd(&ctl->hcur, (unsigned long long)H) : 0ull;
+    // identifiers: at most one per gathered entry
+    const unsigned long long ib = (iout && need) ? atomicAdd(&ctl->icur, need) : 0ull;
+    const bool ovf = db + need > dcap || hb + H > hcap || (iout && ib + need > icap);
+    // FastRec keeps 32-bit offsets: a batch whose results pass 2^32 entries
+    // takes the batch pipeline (64-bit segments) instead of growing the blocks
+    const bool wide = db + need > 0xFFFFFFFFull || hb + H > 0xFFFFFFFFull || ib + need > 0xFFFFFFFFull;
+    if (wide)
+      atomicOr(&ctl->flags, kFastFallback);
+    else if (ovf)
+      atomicOr(&ctl->flags, kFastOverflow);  // the host grows the blocks to the reported totals, runs again
+    L.dbase = db;
+    L.hbase = hb;
+    L.ibase = ib;
+    if (ovf || wide) recs[t] = FastRec{0, 0, 0, 0, 0, 0};
+    return !(ovf || wide);
+  }
+  __device__ void fallback() {
+    atomicOr(&ctl->flags, kFastFallback);
+    recs[t] = FastRec{0, 0, 0, 0, 0, 0};
+  }
+  __device__ void done(FastLds &L, uint32_t d, uint32_t h) {
+    recs[t] = FastRec{(uint32_t)L.dbase, d, (uint32_t)L.hbase, h, (uint32_t)L.ibase, L.nid};
+  }
+};
+
 __global__ __launch_bounds__(kFT) void k_fast(DeviceSnapshot s, const uint8_t *__restrict__ tb,
                                               const uint64_t *__restrict__ to, uint32_t n, FastCtl *ctl,
                                               FastRec *__restrict__ recs, uint64_t *__restrict__ dout, uint64_t dcap,
                                               uint32_t *__restrict__ hout, uint64_t hcap, uint32_t *__restrict__ iout,
                                               uint64_t icap, FastStatus *status) {
   __shared__ FastLds L;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x;
   for (uint32_t t = blockIdx.x; t < n; t += gridDim.x) {
-    const uint64_t off = to[t];
-    const uint32_t len = (uint32_t)(to[t + 1] - off);
-    if (tid == 0) {
-      L.fail = len > kFStage ? 1u : 0u;
-      L.nh = L.nsh = 0;
-      L.nitems[0] = L.nitems[1] = 0;
-    }
-    __syncthreads();
-    const bool staged = len <= kFStage;
-    if (staged)
-      for (uint32_t i = tid; i < len; i += kFT) L.stage[i] = tb[off + i];
-    __syncthreads();
-    // ---- 1. separators and level keys ---------------------------------------
-    if (wid == 0 && staged) {
-      uint32_t nsep = 0;
-      for (uint32_t base = 0; base < len; base += 64) {
-        const uint32_t p = base + lane;
-        const bool sep = p < len && L.stage[p] == '/';
-        const uint64_t m = __ballot(sep);
-        if (sep) {
-          const uint32_t idx = nsep + __popcll(m & f_lanemask_lt(lane));
-          if (idx < kFLevels) L.sep[idx] = (uint16_t)p;
-        }
-        nsep += __popcll(m);
-      }
-      if (lane == 0) {
-        L.nsep = nsep;
-        if (nsep >= kFLevels) L.fail = 1;
-      }
-    }
-    __syncthreads();
-    const uint32_t nsep = staged ? L.nsep : 0;
-    const uint32_t nlev = (len == 0 || L.fail) ? 0 : nsep + 1;
-    const bool dollar = len > 0 && staged && L.stage[0] == '$';
-    if ((uint32_t)tid < nlev) {
-      const uint32_t st = tid == 0 ? 0 : L.sep[tid - 1] + 1u;
-      const uint32_t en = (uint32_t)tid < nsep ? L.sep[tid] : len;
-      const Key k = make_key([&](uint32_t i) { return L.stage[st + i]; }, en - st);
-      L.key0[tid] = k.k0;
-      L.key1[tid] = k.k1;
-    }
-    if (tid == 0 && nlev > 0) {  // level 0's items: the root's literal probe, '+' and '#' children
-      const NodeDesc root = load_desc(s.nodes);
-      uint32_t k = 0;
-      if ((root.sh_cnt_flags >> 24) & kFlagHasLiteral) L.item[0][k++] = (0u << 2) | kFItemLit;
-      if (root.plus != kNone) L.item[0][k++] = (root.plus << 2) | kFItemPlus;
-      if (root.hash != kNone) L.item[0][k++] = (root.hash << 2) | kFItemHash;
-      L.nitems[0] = k;
-    }
-    __syncthreads();
-    // ---- 2. level-synchronous walk -------------------------------------------
-    int cur = 0;
-    for (uint32_t d = 0; d < nlev; d++) {
-      const uint32_t ni = L.nitems[cur];
-      if (ni == 0 || L.fail) break;  // block-uniform (read after a barrier)
-      const uint64_t k0 = L.key0[d], k1 = L.key1[d];
-      const bool has_next = d + 1 < nlev;
-      // a topic level "+" / "#": its literal probe is the wildcard's (the
-      // reference visits that child twice, with no parent probe)
-      const bool lit_is_wild = (k1 == (1ull << 56)) && (k0 == '+' || k0 == '#');
-      const uint32_t tst = d == 0 ? 0 : L.sep[d - 1] + 1u;
-      const uint32_t tln = (d < nsep ? L.sep[d] : len) - tst;
-      for (uint32_t base = 0; base < ni; base += kFT) {
-        const uint32_t it = base + tid;
-        const bool live = it < ni;
-        const uint32_t iw = live ? L.item[cur][it] : 0;
-        const uint32_t kind = iw & 3u, id = iw >> 2;
-        const bool lit = kind == kFItemLit;
-        NodeDesc dc;
-        const uint32_t c = walk_step(s, live && lit && !lit_is_wild, live && !lit, id, id, k0, k1,
-                                     L.stage + tst, tln, &dc);
-        if (c == kNone) continue;
-        const uint32_t fl = dc.sh_cnt_flags >> 24;
-        const bool skip_dollar = dollar && (fl & kFlagDollarWild);      // topics.go:527
-        // a '#' node after a literal parent: gathered by the parent probe (kFlagParentLit)
-        const uint32_t c_own = skip_dollar || (fl & kFlagParentLit) ? 0 : dc.sub_cnt;
-        const uint32_t c_par = lit && !skip_dollar ? dc.hsub_cnt : 0;  // topics.go:507-509
-        const uint32_t c_sh = dc.sh_cnt_flags & kShCntMask;
-        if (((c_own | c_par) && (fl & kFlagMultiSat)) || c_own > kFRangeMax || c_par > kFRangeMax)
-          atomicOr(&L.fail, 1u);
-        if (c_own) {
-          const uint32_t h = atomicAdd(&L.nh, 1u);
-          if (h < kFHits) {
-            L.hoff[h] = dc.sub_off, L.hcnt[h] = c_own, L.hmu[h] = dc.multi & 0xFFFFu, L.hrank[h] = 2 * c;
-          } else {
-            atomicOr(&L.fail, 1u);
-          }
-        }
-        if (c_par) {  // the '#' child's range follows this node's (snapshot.h)
-          const uint32_t h = atomicAdd(&L.nh, 1u);
-          if (h < kFHits) {
-            L.hoff[h] = dc.sub_off + dc.sub_cnt, L.hcnt[h] = c_par, L.hmu[h] = dc.multi >> 16, L.hrank[h] = 2 * c + 1;
-          } else {
-            atomicOr(&L.fail, 1u);
-          }
-        }
-        if (c_sh) {
-          const uint32_t h = atomicAdd(&L.nsh, 1u);
-          if (h < kFSh) {
-            L.shoff[h] = dc.sh_off, L.shcnt[h] = c_sh;
-          } else {
-            atomicOr(&L.fail, 1u);
-          }
-        }
-        if (has_next && (fl & kFlagHasChildren)) {
-          const bool has_lit = fl & kFlagHasLiteral;
-          const uint32_t k = (has_lit ? 1u : 0u) + (dc.plus != kNone ? 1u : 0u) + (dc.hash != kNone ? 1u : 0u);
-          const uint32_t at = k ? atomicAdd(&L.nitems[cur ^ 1], k) : 0;
-          if (at + k > kFItems) {
-            atomicOr(&L.fail, 1u);
-          } else {
-            uint32_t j = at;
-            if (has_lit) L.item[cur ^ 1][j++] = (c << 2) | kFItemLit;
-            if (dc.plus != kNone) L.item[cur ^ 1][j++] = (dc.plus << 2) | kFItemPlus;
-            if (dc.hash != kNone) L.item[cur ^ 1][j++] = (dc.hash << 2) | kFItemHash;
-          }
-        }
-      }
-      __syncthreads();
-      if (tid == 0) L.nitems[cur] = 0;  // becomes the level after next's list
-      cur ^= 1;
-      __syncthreads();
-    }
-    if (L.fail) {  // block-uniform: the batch takes the pipeline without limits
-      if (tid == 0) {
-        atomicOr(&ctl->flags, kFastFallback);
-        recs[t] = FastRec{0, 0, 0, 0, 0, 0};
-      }
-      __syncthreads();
-      continue;
-    }
-    // ---- 3. emission -----------------------------------------------------------
-    // prefixes of the hits' solo counts, multi counts and the shared counts
-    // (one wave each, in place)
-    const uint32_t nh = L.nh, nsh = L.nsh;
-    if (wid == 0) {
-      for (uint32_t i = lane; i < nh; i += 64) L.spre[i] = L.hcnt[i] - L.hmu[i];
-      f_wave_lds_sync();
-      f_prefix(L.spre, L.spre, nh, lane);
-    } else if (wid == 1) {
-      for (uint32_t i = lane; i < nh; i += 64) L.mpre[i] = L.hmu[i];
-      f_wave_lds_sync();
-      f_prefix(L.mpre, L.mpre, nh, lane);
-    } else if (wid == 2) {
-      f_prefix(L.shcnt, L.shpre, nsh, lane);
-    }
-    __syncthreads();
-    const uint32_t Ss = L.spre[nh], Ms = L.mpre[nh], H = L.shpre[nsh];
-    if (tid == 0) {
-      const unsigned long long need = (unsigned long long)Ss + Ms;
-      const unsigned long long db = need ? atomicAdd(&ctl->dcur, need) : 0ull;
-      const unsigned long long hb = H ? atomicAdd(&ctl->hcur, (unsigned long long)H) : 0ull;
-      // identifiers: at most one per gathered entry
-      const unsigned long long ib = (iout && need) ? atomicAdd(&ctl->icur, need) : 0ull;
-      const bool ovf = db + need > dcap || hb + H > hcap || (iout && ib + need > icap);
-      // FastRec keeps 32-bit offsets: a batch whose results pass 2^32 entries
-      // takes the batch pipeline (64-bit segments) instead of growing the blocks
-      const bool wide = db + need > 0xFFFFFFFFull || hb + H > 0xFFFFFFFFull || ib + need > 0xFFFFFFFFull;
-      if (wide) atomicOr(&ctl->flags, kFastFallback);
-      else if (ovf) atomicOr(&ctl->flags, kFastOverflow);
-      L.dbase = db;
-      L.hbase = hb;
-      L.ibase = ib;
-      L.nid = 0;
-      L.fail = ovf || wide ? 1u : 0u;
-    }
-    __syncthreads();
-    if (L.fail) {  // the host grows the blocks to the reported totals and runs the batch again
-      if (tid == 0) recs[t] = FastRec{0, 0, 0, 0, 0, 0};
-      __syncthreads();
-      continue;
-    }
-    const uint64_t db = L.dbase, hb = L.hbase, ib = L.ibase;
-    // solo entries: each its client's merged delivery as is
-    for (uint32_t q = tid; q < Ss; q += kFT) {
-      const uint32_t h = f_search(L.spre, nh, q);
-      const uint32_t sid = L.hoff[h] + (q - L.spre[h]);
-      const uint2 e = *reinterpret_cast<const uint2 *>(s.subs + sid);
-      dout[db + q] = (uint64_t)e.x | ((uint64_t)(e.y & kPackedMask) << 32);
-      if (iout && (e.y & kWordIdent)) iout[ib + atomicAdd(&L.nid, 1u)] = sid;  // packets.go:257-259
-    }
-    // shared candidates
-    for (uint32_t j = tid; j < H; j += kFT) {
-      const uint32_t h = f_search(L.shpre, nsh, j);
-      hout[hb + j] = L.shoff[h] + (j - L.shpre[h]);
-    }
-    // multi entries: the per-client merge, in client-hash partitions
-    uint32_t W = 0;
-    const uint32_t P = Ms ? (Ms + kFPartCap - 1) / kFPartCap : 0;
-    const uint32_t per = P ? (Ms + P - 1) / P : 0;
-    uint32_t lg = 6;
-    while ((1u << lg) < 2 * per && (1u << lg) < kFSlots) lg++;
-    const uint32_t mask = (1u << lg) - 1;
-    for (uint32_t p = 0; p < P; p++) {
-      __syncthreads();  // the previous pass's winners are read
-      for (uint32_t j = tid; j <= mask; j += kFT) {
-        L.tkb[j] = 0;
-        L.tfirst[j] = ~0ull;
-      }
-      if (tid == 0) L.fill = 0;
-      __syncthreads();
-      for (uint32_t q = tid; q < Ms; q += kFT) {
-        const uint32_t h = f_search(L.mpre, nh, q);
-        const uint32_t sid = L.hoff[h] + (L.hcnt[h] - L.hmu[h]) + (q - L.mpre[h]);
-        const uint2 e = *reinterpret_cast<const uint2 *>(s.subs + sid);
-        if (P > 1 && f_partition(e.x, P) != p) continue;
-        if (iout && (e.y & kWordIdent)) iout[ib + atomicAdd(&L.nid, 1u)] = sid;
-        if (atomicAdd(&L.fill, 1u) >= (P > 1 ? kFFill : mask)) {  // an unlucky partition: never spin
-          atomicOr(&L.fail, 1u);
-          continue;
-        }
-        f_insert(L, mask, lg, e.x, e.y, L.hrank[h]);
-      }
-      __syncthreads();
-      // winners in slot order: wave w scans its quarter of the table twice
-      const uint32_t slots = mask + 1, q4 = (slots + kFWaves - 1) / kFWaves;
-      const uint32_t lo = wid * q4, hi = min(slots, lo + q4);
-      uint32_t cnt = 0;
-      for (uint32_t j0 = lo; j0 < hi; j0 += 64) {
-        const uint32_t j = j0 + lane;
-        cnt += __popcll(__ballot(j < hi && L.tkb[j] != 0));
-      }
-      if (lane == 0) L.wsum[wid] = cnt;
-      __syncthreads();
-      uint32_t w = W, tot = W;
-      for (int k = 0; k < kFWaves; k++) {
-        if (k < wid) w += L.wsum[k];
-        tot += L.wsum[k];
-      }
-      for (uint32_t j0 = lo; j0 < hi; j0 += 64) {
-        const uint32_t j = j0 + lane;
-        const bool occ = j < hi && L.tkb[j] != 0;
-        const uint64_t m = __ballot(occ);
-        if (occ) {
-          const unsigned long long kb = L.tkb[j];
-          const uint32_t v = (uint32_t)kb;
-          const uint32_t packed = ((uint32_t)L.tfirst[j] & kWordSidMask) | ((31u - __builtin_clz(v & 7u)) << 28) |
-                                  (((v >> 3) & 1u) << 30);
-          dout[db + Ss + w + __popcll(m & f_lanemask_lt(lane))] = (uint64_t)((kb >> 32) - 1) | ((uint64_t)packed << 32);
-        }
-        w += __popcll(m);
-      }
-      W = tot;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      if (L.fail) atomicOr(&ctl->flags, kFastFallback);
-      recs[t] = FastRec{(uint32_t)db, Ss + W, (uint32_t)hb, H, (uint32_t)ib, L.nid};
-    }
-    __syncthreads();
+    BatchSink sink{ctl, recs, t, dout, dcap, hout, hcap, iout, icap};
+    fast_topic(s, L, tb + to[t], (uint32_t)(to[t + 1] - to[t]), sink);
   }
   // the last workgroup to finish publishes the totals and resets the counters;
   // every workgroup's host writes are made visible (system scope) before its
@@ -428,6 +469,79 @@ __global__ __launch_bounds__(kFT) void k_fast(DeviceSnapshot s, const uint8_t *_
       atomicExch(&ctl->done, 0u);
       __threadfence_system();
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_serve: the per-publish server (match.h ServeQueue).  Lane 0 of an idle
+// workgroup polls the next unclaimed slot (system-scope loads of host
+// memory, with a growing s_sleep between polls) and claims it with one CAS on
+// the device counter; the workgroup runs fast_topic into the slot and
+// publishes done after a system fence.  Exit: the host's stop word, or
+// idle_us without a claim (s_memrealtime, 100 MHz).
+// ---------------------------------------------------------------------------
+struct ServeSink {
+  ServeSlot *slot;
+  uint64_t *dout;
+  uint32_t *hout;
+  uint32_t *iout;
+  unsigned long long k;
+  __device__ bool reserve(FastLds &L, unsigned long long need, uint32_t H) {
+    L.dbase = L.hbase = L.ibase = 0;
+    if (need > kServeD || H > kServeH || (iout && need > kServeI)) {  // too big for a slot: the pipeline
+      fallback();
+      return false;
+    }
+    return true;
+  }
+  __device__ void publish(uint32_t status, uint32_t d, uint32_t h, uint32_t i) {
+    slot->status = status;
+    slot->dcount = d;
+    slot->hcount = h;
+    slot->icount = i;
+    __threadfence_system();  // the result reaches host memory before done
+    __hip_atomic_store(&slot->done, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __device__ void fallback() { publish(kServeFallback, 0, 0, 0); }
+  __device__ void done(FastLds &L, uint32_t d, uint32_t h) { publish(kServeOk, d, h, L.nid); }
+};
+
+__global__ __launch_bounds__(kFT) void k_serve(DeviceSnapshot s, ServeQueue *q, unsigned long long *claimed,
+                                               uint64_t idle_ticks, int want_ids) {
+  __shared__ FastLds L;
+  __shared__ unsigned long long job;
+  __shared__ int quit;
+  const int tid = threadIdx.x;
+  for (;;) {
+    if (tid == 0) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      uint32_t nap = 1;
+      quit = 1;
+      for (;;) {
+        const unsigned long long c = __hip_atomic_load(claimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long seq =
+            __hip_atomic_load(&q->slot[c % kServeSlots].seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (seq == c + 1) {  // request c is posted: claim it
+          if (atomicCAS(claimed, c, c + 1) == c) {
+            job = c;
+            quit = 0;
+            break;
+          }
+          continue;
+        }
+        if (__hip_atomic_load(&q->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;
+        // back off: ~0.1 us while requests flow, up to ~1.7 us when idle
+        for (uint32_t z = 0; z < nap; z++) __builtin_amdgcn_s_sleep(4);
+        nap = nap < 16 ? nap + 1 : nap;
+      }
+    }
+    __syncthreads();
+    if (quit) break;
+    ServeSlot *slot = &q->slot[job % kServeSlots];
+    ServeSink sink{slot, slot->dout, slot->hout, want_ids ? slot->iout : nullptr, job};
+    fast_topic(s, L, reinterpret_cast<const uint8_t *>(slot->topic), min(slot->len, kServeTopic + 1), sink);
+    __syncthreads();
   }
 }
 
@@ -465,6 +579,15 @@ FastArena::~FastArena() {
                   (void *)status})
     if (p) (void)hipHostFree(p);
   if (ctl) (void)hipFree(ctl);
+}
+
+int serve_launch(const DeviceSnapshot &s, ServeQueue *q, unsigned long long *claimed, uint32_t grid, uint32_t idle_us,
+                 bool want_ids, hipStream_t st) {
+  const uint64_t idle_ticks = (uint64_t)idle_us * 100;  // s_memrealtime: 100 MHz
+  hipLaunchKernelGGL(k_serve, dim3(std::max<uint32_t>(1, grid)), dim3(kFT), 0, st, s, q, claimed, idle_ticks,
+                     want_ids ? 1 : 0);
+  HIP_TRY(hipGetLastError());
+  return 0;
 }
 
 int match_small(const DeviceSnapshot &s, Workspace &ws, const char *bytes, const uint64_t *offs, uint32_t n,

@@ -177,6 +177,39 @@ constexpr uint32_t kFastMaxTopics = 4096;
 int match_small(const DeviceSnapshot &s, Workspace &ws, const char *bytes, const uint64_t *offs, uint32_t n,
                 hipStream_t st, FastOutput *out, bool want_ids = false);
 
+// ---- the per-publish server (fast.hip k_serve) -------------------------------
+// A persistent kernel of `grid` workgroups serves single-topic Subscribers
+// calls posted to a ring of slots in pinned, coherent host memory: the caller
+// writes the topic into slot k % kServeSlots and then seq = k + 1; an idle
+// workgroup claims request k (a device counter), runs the small-batch path's
+// per-topic body (fast_topic) straight into the slot and publishes done = k +
+// 1.  No launch and no stream synchronisation per call.  Every workgroup exits
+// on `stop`, or after idle_us without a request (the host relaunches on the
+// next call; unclaimed requests wait in the ring).
+constexpr uint32_t kServeSlots = 256;
+constexpr uint32_t kServeTopic = 1024;  // topic bytes a slot holds (the small-batch path's kFStage)
+constexpr uint32_t kServeD = 4096, kServeH = 512, kServeI = 4096;  // result capacities per slot
+enum : uint32_t { kServeOk = 0, kServeFallback = 1 };
+struct alignas(64) ServeSlot {
+  unsigned long long seq;   // host: k + 1 once request k's topic is in place
+  unsigned long long done;  // device: k + 1 once request k's result is complete
+  uint32_t len, status;     // topic length; kServe* (fallback: the caller runs the batch pipeline)
+  uint32_t dcount, hcount, icount, pad[3];
+  char topic[kServeTopic];
+  uint64_t dout[kServeD];   // {client, packed} deliveries
+  uint32_t hout[kServeH];   // shared-subscription ids
+  uint32_t iout[kServeI];   // identifier sids (want_ids)
+};
+struct ServeQueue {
+  unsigned long long stop;  // host: 1 = every workgroup exits
+  unsigned long long pad[7];
+  ServeSlot slot[kServeSlots];
+};
+// launch the server on `st` (q: host-mapped; claimed: device counter, zeroed
+// once before the first launch and kept across relaunches)
+int serve_launch(const DeviceSnapshot &s, ServeQueue *q, unsigned long long *claimed, uint32_t grid, uint32_t idle_us,
+                 bool want_ids, hipStream_t st);
+
 // Identifiers support for the last match_device call on `ws` (its topic
 // buffers must still hold the batch): per topic, the sids of the gathered
 // non-shared subscriptions with Identifier > 0 (mqm_device_identifiers).

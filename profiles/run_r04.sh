@@ -26,6 +26,8 @@
 #   c4shard : C4 shard 0/8 bench line with roofline and CPU baseline
 #   c4prof  : rocprofv3 kernel stats of the C4 shard bench
 #   rev     : C5 reverse bench line (full 50M retained, CPU baseline, full-size selfcheck)
+#   counters / c4counters: the five rocprofv3 --pmc passes (profiles/run_pmc_r02.sh) over C3 / the C4
+#             shard -> c3_counters.txt (profiles/derive_counters.py), traffic.json
 set -euo pipefail
 TAG=$1
 shift
@@ -111,6 +113,12 @@ for step in "$@"; do
              --no-cpu-baseline --host-topics 0 --latency-topics 0 > $OUT/c4_under_rocprof.json 2> $OUT/rocprof_c4.log) ;;
     rev) timeout -k 10 900 python3 -u bench.py --workload reverse --steps 5 --warmup 1 --cpu-seconds 10 \
              > $OUT/bench_reverse.json 2> $OUT/bench_reverse.log ;;
+    counters) bash profiles/run_pmc_r02.sh $TAG/pmc_c3 > $OUT/pmc_c3.log 2>&1 &&
+             python3 profiles/derive_counters.py $OUT/pmc_c3 --json $OUT/c3_counters.json > $OUT/c3_counters.txt &&
+             python3 profiles/pmc_to_traffic.py $OUT/pmc_c3 > $OUT/traffic.json ;;
+    c4counters) bash profiles/run_pmc_r02.sh $TAG/pmc_c4 --config 4 --shard 0/8 > $OUT/pmc_c4.log 2>&1 &&
+             python3 profiles/derive_counters.py $OUT/pmc_c4 --json $OUT/c4_counters.json > $OUT/c4_counters.txt &&
+             python3 profiles/pmc_to_traffic.py $OUT/pmc_c4 > $OUT/traffic_c4.json ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
