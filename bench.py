@@ -777,13 +777,15 @@ def latency(idx, w, args):
     idx.serve_policy(T, 20000)
     run(1, 50)
     one = run(1, single)
-    served = {"p50": one["p50_us"], "p90": one["p90_us"], "p99": one["p99_us"], "topics_per_s": one["topics_per_s"]}
+    single_dev_us = idx.serve_device_us()
+    served = {"device_us_single": single_dev_us, "p50": one["p50_us"], "p90": one["p90_us"], "p99": one["p99_us"], "topics_per_s": one["topics_per_s"]}
     run(T, 20)
     s0 = idx.serve_stats()
     served["concurrent"] = dict(run(T, per), threads=T, calls_per_thread=per)
     s1 = idx.serve_stats()
     served["ring_share"] = (s1[0] - s0[0]) / max(1, (s1[0] - s0[0]) + (s1[1] - s0[1]))
     served["launches"] = s1[2]
+    served["device_us_per_call"] = idx.serve_device_us()
     served["grid"] = T
     out["served"] = served
     return out

@@ -252,6 +252,12 @@ class TopicsIndex:
         check("mqm_serve_stats", lib().mqm_serve_stats(self._h, C.byref(a), C.byref(b_), C.byref(c)))
         return a.value, b_.value, c.value
 
+    def serve_device_us(self) -> float:
+        """mean device time per served call, claim to published result (us)"""
+        v = C.c_double()
+        check("mqm_serve_device_us", lib().mqm_serve_device_us(self._h, C.byref(v)))
+        return v.value
+
     def batching_stats(self):
         """(batches run, topics they carried) of the MQM_CFG_BATCHING collector"""
         b, t = C.c_uint64(), C.c_uint64()

@@ -49,7 +49,7 @@ EXPORTED = [
     "mqm_debug_fault", "mqm_gather_shards_shared", "mqm_match_ctx_create", "mqm_match_ctx_destroy",
     "mqm_match_device_async", "mqm_match_ctx_wait", "mqm_match_ctx_stats", "mqm_match_batch_packed",
     "mqm_result_packed", "mqm_match_batch_runs", "mqm_result_runs", "mqm_result_expand",
-    "mqm_serve_policy", "mqm_serve_stats",
+    "mqm_serve_policy", "mqm_serve_stats", "mqm_serve_device_us",
 ]
 
 
@@ -212,6 +212,7 @@ def lib():
         "mqm_result_expand": ([vp, u32, u32, vp, vp], C.c_int),
         "mqm_serve_policy": ([vp, u32, u32], C.c_int),
         "mqm_serve_stats": ([vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)], C.c_int),
+        "mqm_serve_device_us": ([vp, C.POINTER(C.c_double)], C.c_int),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

@@ -1393,6 +1393,7 @@ struct Server {
   std::atomic<uint64_t> ticket{0};
   std::unique_ptr<std::atomic<uint64_t>[]> free_seq;  // slot i takes request k once free_seq[i] == k
   std::atomic<uint64_t> served{0}, fallbacks{0}, launches{0};
+  std::atomic<uint64_t> device_ticks{0};  // claim -> publish on the device, summed (100 MHz ticks)
   std::atomic<bool> live{false};                   // launched (may have exited idle since)
   std::atomic<const GpuSnapshot *> running_on{nullptr};
 
@@ -1457,7 +1458,7 @@ struct Server {
     if (rc != MQM_OK) return rc;
     const uint64_t k = ticket.fetch_add(1, std::memory_order_relaxed);
     const uint32_t i = (uint32_t)(k % kServeSlots);
-    while (free_seq[i].load(std::memory_order_acquire) != k) __builtin_ia32_pause();  // the slot's previous caller is done
+    while (free_seq[i].load(std::memory_order_acquire) != k) std::this_thread::yield();  // the slot's previous caller is done
     ServeSlot &sl = q->slot[i];
     memcpy(sl.topic, topic, len);
     sl.len = (uint32_t)len;
@@ -1477,8 +1478,14 @@ struct Server {
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
     auto check = t0 + std::chrono::microseconds(50);
+    // (spin ~20 us, then yield between polls: more callers than CPUs must not
+    // starve the ones whose results are ready)
+    uint32_t spins = 0;
     while (__atomic_load_n(&sl.done, __ATOMIC_ACQUIRE) != k + 1) {
-      __builtin_ia32_pause();
+      if (++spins < 4096)
+        __builtin_ia32_pause();
+      else
+        std::this_thread::yield();
       const auto now = clk::now();
       if (now < check) continue;
       if (now - t0 > std::chrono::seconds(10)) {
@@ -1490,6 +1497,7 @@ struct Server {
       check = now + std::chrono::microseconds(50);
     }
     const uint32_t status = sl.status;
+    if (sl.t_done > sl.t_claim) device_ticks += sl.t_done - sl.t_claim;
     if (status == kServeOk) {
       try {
         rc = Collector::single(cur->host, sl.dout, sl.dcount, sl.hout, sl.hcount, want_ids ? sl.iout : nullptr,
@@ -1599,6 +1607,14 @@ int mqm_serve_stats(mqm_index *h, uint64_t *served, uint64_t *fallbacks, uint64_
   *served = sv->served.load();
   *fallbacks = sv->fallbacks.load();
   *launches = sv->launches.load();
+  return MQM_OK;
+}
+
+int mqm_serve_device_us(mqm_index *h, double *us) {
+  Server *sv = h ? h->server.load(std::memory_order_acquire) : nullptr;
+  if (!sv || !us) return MQM_EINVAL;
+  const uint64_t n = sv->served.load() + sv->fallbacks.load();
+  *us = n ? (double)sv->device_ticks.load() / 100.0 / (double)n : 0.0;  // s_memrealtime: 100 MHz
   return MQM_OK;
 }
 

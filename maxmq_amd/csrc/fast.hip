@@ -499,6 +499,7 @@ struct ServeSink {
     slot->dcount = d;
     slot->hcount = h;
     slot->icount = i;
+    slot->t_done = __builtin_amdgcn_s_memrealtime();
     __threadfence_system();  // the result reaches host memory before done
     __hip_atomic_store(&slot->done, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -531,14 +532,16 @@ __global__ __launch_bounds__(kFT) void k_serve(DeviceSnapshot s, ServeQueue *q, 
         }
         if (__hip_atomic_load(&q->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
         if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;
-        // back off: ~0.1 us while requests flow, up to ~1.7 us when idle
+        // back off: ~0.1 us while requests flow, up to ~0.4 us when idle (a
+        // poll is one PCIe read of the slot's word)
         for (uint32_t z = 0; z < nap; z++) __builtin_amdgcn_s_sleep(4);
-        nap = nap < 16 ? nap + 1 : nap;
+        nap = nap < 4 ? nap + 1 : nap;
       }
     }
     __syncthreads();
     if (quit) break;
     ServeSlot *slot = &q->slot[job % kServeSlots];
+    if (tid == 0) slot->t_claim = __builtin_amdgcn_s_memrealtime();
     ServeSink sink{slot, slot->dout, slot->hout, want_ids ? slot->iout : nullptr, job};
     fast_topic(s, L, reinterpret_cast<const uint8_t *>(slot->topic), min(slot->len, kServeTopic + 1), sink);
     __syncthreads();

@@ -194,7 +194,8 @@ struct alignas(64) ServeSlot {
   unsigned long long seq;   // host: k + 1 once request k's topic is in place
   unsigned long long done;  // device: k + 1 once request k's result is complete
   uint32_t len, status;     // topic length; kServe* (fallback: the caller runs the batch pipeline)
-  uint32_t dcount, hcount, icount, pad[3];
+  uint32_t dcount, hcount, icount, pad;
+  unsigned long long t_claim, t_done;  // device clock (s_memrealtime, 100 MHz): claimed, published
   char topic[kServeTopic];
   uint64_t dout[kServeD];   // {client, packed} deliveries
   uint32_t hout[kServeH];   // shared-subscription ids
