@@ -286,7 +286,8 @@ int mqm_batching_policy(mqm_index *h, uint32_t max_batch, uint32_t linger_us);
  * launches.  MQM_EINVAL on a host-only index (or for stats while off). */
 int mqm_serve_policy(mqm_index *h, uint32_t grid, uint32_t idle_us);
 int mqm_serve_stats(mqm_index *h, uint64_t *served, uint64_t *fallbacks, uint64_t *launches);
-/* mean device time per served call, claim to published result (us) */
+/* mean device time per served call (us[4]): claim to published result, then
+ * its phases: topic staged + level keys, trie walk, emission + publish */
 int mqm_serve_device_us(mqm_index *h, double *us);
 int mqm_batching_stats(mqm_index *h, uint64_t *batches, uint64_t *topics);
 /* Device in / device out on `hip_stream` (hipStream_t, NULL = default stream). */

@@ -254,9 +254,9 @@ class TopicsIndex:
 
     def serve_device_us(self) -> float:
         """mean device time per served call, claim to published result (us)"""
-        v = C.c_double()
-        check("mqm_serve_device_us", lib().mqm_serve_device_us(self._h, C.byref(v)))
-        return v.value
+        v = (C.c_double * 4)()
+        check("mqm_serve_device_us", lib().mqm_serve_device_us(self._h, v))
+        return {"total": v[0], "stage_keys": v[1], "walk": v[2], "emit_publish": v[3]}
 
     def batching_stats(self):
         """(batches run, topics they carried) of the MQM_CFG_BATCHING collector"""

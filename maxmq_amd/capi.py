@@ -212,7 +212,7 @@ def lib():
         "mqm_result_expand": ([vp, u32, u32, vp, vp], C.c_int),
         "mqm_serve_policy": ([vp, u32, u32], C.c_int),
         "mqm_serve_stats": ([vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)], C.c_int),
-        "mqm_serve_device_us": ([vp, C.POINTER(C.c_double)], C.c_int),
+        "mqm_serve_device_us": ([vp, vp], C.c_int),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

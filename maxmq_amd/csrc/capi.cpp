@@ -1394,12 +1394,49 @@ struct Server {
   std::unique_ptr<std::atomic<uint64_t>[]> free_seq;  // slot i takes request k once free_seq[i] == k
   std::atomic<uint64_t> served{0}, fallbacks{0}, launches{0};
   std::atomic<uint64_t> device_ticks{0};  // claim -> publish on the device, summed (100 MHz ticks)
+  std::atomic<uint64_t> phase_ticks[3] = {};  // stage + keys, walk, emission + publish
+  std::atomic<uint64_t> timed{0};
   std::atomic<bool> live{false};                   // launched (may have exited idle since)
+  // completion poller: callers that stopped spinning sleep on waitw[slot];
+  // the poller watches their slots' done words and wakes them
+  std::unique_ptr<std::atomic<uint64_t>[]> waiting;  // slot -> the done value its sleeper waits for (0: none)
+  std::unique_ptr<std::atomic<uint32_t>[]> waitw;    // futex words
+  std::atomic<uint32_t> sleepers{0}, poll_word{0}, inflight{0};
+  std::atomic<bool> poller_quit{false};
+  std::thread poller;
+  void poke_poller() {
+    poll_word.fetch_add(1, std::memory_order_acq_rel);
+    syscall(SYS_futex, reinterpret_cast<uint32_t *>(&poll_word), FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+  }
+  void poll_loop() {
+    while (!poller_quit.load(std::memory_order_acquire)) {
+      const uint32_t pw = poll_word.load(std::memory_order_acquire);
+      if (sleepers.load(std::memory_order_acquire) == 0) {
+        const struct timespec ts = {0, 1000000};  // 1 ms (quit is checked at least that often)
+        syscall(SYS_futex, reinterpret_cast<uint32_t *>(&poll_word), FUTEX_WAIT_PRIVATE, pw, &ts, nullptr, 0);
+        continue;
+      }
+      for (uint32_t i = 0; i < kServeSlots; i++) {
+        const uint64_t w = waiting[i].load(std::memory_order_acquire);
+        if (w && __atomic_load_n(&q->slot[i].done, __ATOMIC_ACQUIRE) == w && !waitw[i].load(std::memory_order_relaxed)) {
+          waitw[i].store(1, std::memory_order_release);
+          syscall(SYS_futex, reinterpret_cast<uint32_t *>(&waitw[i]), FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+        }
+      }
+      __builtin_ia32_pause();
+    }
+  }
   std::atomic<const GpuSnapshot *> running_on{nullptr};
 
   explicit Server(mqm_index *idx) : h(idx), want_ids((idx->cfg.flags & MQM_CFG_IDENTIFIERS) != 0) {
     free_seq.reset(new std::atomic<uint64_t>[kServeSlots]);
-    for (uint32_t i = 0; i < kServeSlots; i++) free_seq[i].store(i);
+    waiting.reset(new std::atomic<uint64_t>[kServeSlots]);
+    waitw.reset(new std::atomic<uint32_t>[kServeSlots]);
+    for (uint32_t i = 0; i < kServeSlots; i++) {
+      free_seq[i].store(i);
+      waiting[i].store(0);
+      waitw[i].store(0);
+    }
   }
   int init() {
     if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
@@ -1413,6 +1450,7 @@ struct Server {
     if (hipMemsetAsync(claimed, 0, sizeof(unsigned long long), st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
       return MQM_EHIP;
+    poller = std::thread([this] { poll_loop(); });
     return MQM_OK;
   }
   // (mu held) stop a running kernel and wait for it
@@ -1425,6 +1463,11 @@ struct Server {
     live.store(false, std::memory_order_release);
   }
   ~Server() {
+    if (poller.joinable()) {
+      poller_quit.store(true, std::memory_order_release);
+      poke_poller();
+      poller.join();
+    }
     if (q) {
       std::lock_guard<std::mutex> g(mu);
       halt();
@@ -1472,32 +1515,60 @@ struct Server {
         return rc;
       }
     }
-    // spin on the slot's done word; every ~50 us without it, make sure a
-    // server is still running (it exits after idle_us without a claim; the
-    // request then waits, unclaimed, for the relaunch)
+    // spin on the slot's done word for a while (the single-caller latency
+    // path), then sleep on a futex the completion poller wakes (more callers
+    // than CPUs: a spinning caller would delay the ones whose results are
+    // ready); every ~100 us without a result, make sure a server is still
+    // running (it exits after idle_us without a claim; the request then
+    // waits, unclaimed, for the relaunch)
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
-    auto check = t0 + std::chrono::microseconds(50);
-    // (spin ~20 us, then yield between polls: more callers than CPUs must not
-    // starve the ones whose results are ready)
-    uint32_t spins = 0;
-    while (__atomic_load_n(&sl.done, __ATOMIC_ACQUIRE) != k + 1) {
-      if (++spins < 4096)
-        __builtin_ia32_pause();
-      else
-        std::this_thread::yield();
-      const auto now = clk::now();
-      if (now < check) continue;
-      if (now - t0 > std::chrono::seconds(10)) {
-        fprintf(stderr, "mqmatch: per-publish server: no result for 10 s\n");
-        return MQM_EHIP;  // (the slot stays taken: its late result is never read)
-      }
-      std::lock_guard<std::mutex> g(mu);
-      if ((rc = ensure(snap ? snap : cur)) != MQM_OK) return rc;
-      check = now + std::chrono::microseconds(50);
+    bool ready = false;
+    // (few callers in flight: spin through a whole call; many: sleep early)
+    const uint32_t budget = inflight.fetch_add(1, std::memory_order_acq_rel) < 4 ? 40000u : 1024u;
+    for (uint32_t spin = 0; spin < budget && !ready; spin++) {
+      __builtin_ia32_pause();
+      ready = __atomic_load_n(&sl.done, __ATOMIC_ACQUIRE) == k + 1;
     }
+    if (!ready) {
+      waitw[i].store(0, std::memory_order_relaxed);
+      waiting[i].store(k + 1, std::memory_order_release);
+      if (sleepers.fetch_add(1, std::memory_order_acq_rel) == 0) poke_poller();
+      while (__atomic_load_n(&sl.done, __ATOMIC_ACQUIRE) != k + 1) {
+        const struct timespec ts = {0, 100000};  // 100 us
+        syscall(SYS_futex, reinterpret_cast<uint32_t *>(&waitw[i]), FUTEX_WAIT_PRIVATE, 0, &ts, nullptr, 0);
+        if (__atomic_load_n(&sl.done, __ATOMIC_ACQUIRE) == k + 1) break;
+        const auto now = clk::now();
+        if (now - t0 > std::chrono::seconds(10)) {
+          fprintf(stderr, "mqmatch: per-publish server: no result for 10 s\n");
+          waiting[i].store(0, std::memory_order_release);
+          sleepers.fetch_sub(1, std::memory_order_acq_rel);
+          inflight.fetch_sub(1, std::memory_order_acq_rel);
+          return MQM_EHIP;  // (the slot stays taken: its late result is never read)
+        }
+        if (now - t0 > std::chrono::microseconds(100)) {
+          std::lock_guard<std::mutex> g(mu);
+          if ((rc = ensure(snap ? snap : cur)) != MQM_OK) {
+            waiting[i].store(0, std::memory_order_release);
+            sleepers.fetch_sub(1, std::memory_order_acq_rel);
+            inflight.fetch_sub(1, std::memory_order_acq_rel);
+            return rc;
+          }
+        }
+      }
+      waiting[i].store(0, std::memory_order_release);
+      sleepers.fetch_sub(1, std::memory_order_acq_rel);
+    }
+    inflight.fetch_sub(1, std::memory_order_acq_rel);
     const uint32_t status = sl.status;
-    if (sl.t_done > sl.t_claim) device_ticks += sl.t_done - sl.t_claim;
+    if (sl.t_done > sl.t_claim && sl.t_phase[0] >= sl.t_claim && sl.t_phase[1] >= sl.t_phase[0] &&
+        sl.t_done >= sl.t_phase[1]) {
+      device_ticks += sl.t_done - sl.t_claim;
+      phase_ticks[0] += sl.t_phase[0] - sl.t_claim;
+      phase_ticks[1] += sl.t_phase[1] - sl.t_phase[0];
+      phase_ticks[2] += sl.t_done - sl.t_phase[1];
+      timed++;
+    }
     if (status == kServeOk) {
       try {
         rc = Collector::single(cur->host, sl.dout, sl.dcount, sl.hout, sl.hcount, want_ids ? sl.iout : nullptr,
@@ -1613,8 +1684,10 @@ int mqm_serve_stats(mqm_index *h, uint64_t *served, uint64_t *fallbacks, uint64_
 int mqm_serve_device_us(mqm_index *h, double *us) {
   Server *sv = h ? h->server.load(std::memory_order_acquire) : nullptr;
   if (!sv || !us) return MQM_EINVAL;
-  const uint64_t n = sv->served.load() + sv->fallbacks.load();
-  *us = n ? (double)sv->device_ticks.load() / 100.0 / (double)n : 0.0;  // s_memrealtime: 100 MHz
+  const uint64_t n = sv->timed.load();
+  // s_memrealtime: 100 MHz; us[0] claim -> published, us[1..3] its phases
+  us[0] = n ? (double)sv->device_ticks.load() / 100.0 / (double)n : 0.0;
+  for (int i = 0; i < 3; i++) us[1 + i] = n ? (double)sv->phase_ticks[i].load() / 100.0 / (double)n : 0.0;
   return MQM_OK;
 }
 

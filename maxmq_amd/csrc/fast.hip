@@ -204,6 +204,7 @@ __device__ __forceinline__ void fast_topic(const DeviceSnapshot &s, FastLds &L, 
     L.nitems[0] = k;
   }
   __syncthreads();
+  if (tid == 0) sink.stamp(0);  // staged, keys built
   // ---- 2. level-synchronous walk -------------------------------------------
   int cur = 0;
   for (uint32_t d = 0; d < nlev; d++) {
@@ -282,6 +283,7 @@ __device__ __forceinline__ void fast_topic(const DeviceSnapshot &s, FastLds &L, 
     __syncthreads();
     return;
   }
+  if (tid == 0) sink.stamp(1);  // walked
   // ---- 3. emission -----------------------------------------------------------
   // prefixes of the hits' solo counts, multi counts and the shared counts
   // (one wave each, in place)
@@ -431,6 +433,7 @@ struct BatchSink {
   __device__ void done(FastLds &L, uint32_t d, uint32_t h) {
     recs[t] = FastRec{(uint32_t)L.dbase, d, (uint32_t)L.hbase, h, (uint32_t)L.ibase, L.nid};
   }
+  __device__ void stamp(int) {}
 };
 
 __global__ __launch_bounds__(kFT) void k_fast(DeviceSnapshot s, const uint8_t *__restrict__ tb,
@@ -504,6 +507,7 @@ struct ServeSink {
     __hip_atomic_store(&slot->done, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   __device__ void fallback() { publish(kServeFallback, 0, 0, 0); }
+  __device__ void stamp(int i) { slot->t_phase[i] = __builtin_amdgcn_s_memrealtime(); }
   __device__ void done(FastLds &L, uint32_t d, uint32_t h) { publish(kServeOk, d, h, L.nid); }
 };
 

@@ -196,6 +196,7 @@ struct alignas(64) ServeSlot {
   uint32_t len, status;     // topic length; kServe* (fallback: the caller runs the batch pipeline)
   uint32_t dcount, hcount, icount, pad;
   unsigned long long t_claim, t_done;  // device clock (s_memrealtime, 100 MHz): claimed, published
+  unsigned long long t_phase[2];       // ... topic staged and keys built, trie walked
   char topic[kServeTopic];
   uint64_t dout[kServeD];   // {client, packed} deliveries
   uint32_t hout[kServeH];   // shared-subscription ids
