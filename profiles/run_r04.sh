@@ -119,6 +119,8 @@ for step in "$@"; do
     c4counters) bash profiles/run_pmc_r02.sh $TAG/pmc_c4 --config 4 --shard 0/8 > $OUT/pmc_c4.log 2>&1 &&
              python3 profiles/derive_counters.py $OUT/pmc_c4 --json $OUT/c4_counters.json > $OUT/c4_counters.txt &&
              python3 profiles/pmc_to_traffic.py $OUT/pmc_c4 > $OUT/traffic_c4.json ;;
+    ab16) for V in 1 0; do MQM_COPY16=$V timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_copy16_$V.json \
+             2> $OUT/bench_fast_copy16_$V.log || exit 1; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
