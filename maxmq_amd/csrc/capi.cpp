@@ -1505,7 +1505,8 @@ struct Server {
     ServeSlot &sl = q->slot[i];
     memcpy(sl.topic, topic, len);
     sl.len = (uint32_t)len;
-    __atomic_store_n(&sl.seq, k + 1, __ATOMIC_RELEASE);
+    // the length rides in the word the server polls (no second PCIe read)
+    __atomic_store_n(&sl.seq, (k + 1) | ((unsigned long long)len << kServeSeqBits), __ATOMIC_RELEASE);
     // (no HIP call on the common path: the kernel's liveness is checked only
     // when a result is late, below)
     if (!live.load(std::memory_order_acquire) || running_on.load(std::memory_order_acquire) != cur.get()) {
@@ -1524,11 +1525,14 @@ struct Server {
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
     bool ready = false;
-    // (few callers in flight: spin through a whole call; many: sleep early)
-    const uint32_t budget = inflight.fetch_add(1, std::memory_order_acq_rel) < 4 ? 40000u : 1024u;
-    for (uint32_t spin = 0; spin < budget && !ready; spin++) {
+    // (few callers in flight: spin through a whole call; many: sleep almost
+    // at once — a spinning caller holds a CPU another caller's finished
+    // result is waiting for)
+    const auto spin_for = std::chrono::microseconds(inflight.fetch_add(1, std::memory_order_acq_rel) < 4 ? 300 : 2);
+    for (uint32_t spin = 0; !ready; spin++) {
       __builtin_ia32_pause();
       ready = __atomic_load_n(&sl.done, __ATOMIC_ACQUIRE) == k + 1;
+      if (!ready && (spin & 15) == 15 && clk::now() - t0 > spin_for) break;
     }
     if (!ready) {
       waitw[i].store(0, std::memory_order_relaxed);

@@ -156,6 +156,10 @@ template <class Sink>
 __device__ __forceinline__ void fast_topic(const DeviceSnapshot &s, FastLds &L, const uint8_t *__restrict__ topic,
                                            uint32_t len, Sink &sink) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // the root's descriptor: its load is in flight with the topic's (a PCIe
+  // read when the topic is in host memory)
+  NodeDesc root{};
+  if (tid == 0) root = load_desc(s.nodes);
   if (tid == 0) {
     L.fail = len > kFStage ? 1u : 0u;
     L.nh = L.nsh = 0;
@@ -196,7 +200,6 @@ __device__ __forceinline__ void fast_topic(const DeviceSnapshot &s, FastLds &L, 
     L.key1[tid] = k.k1;
   }
   if (tid == 0 && nlev > 0) {  // level 0's items: the root's literal probe, '+' and '#' children
-    const NodeDesc root = load_desc(s.nodes);
     uint32_t k = 0;
     if ((root.sh_cnt_flags >> 24) & kFlagHasLiteral) L.item[0][k++] = (0u << 2) | kFItemLit;
     if (root.plus != kNone) L.item[0][k++] = (root.plus << 2) | kFItemPlus;
@@ -515,6 +518,7 @@ __global__ __launch_bounds__(kFT) void k_serve(DeviceSnapshot s, ServeQueue *q, 
                                                uint64_t idle_ticks, int want_ids) {
   __shared__ FastLds L;
   __shared__ unsigned long long job;
+  __shared__ uint32_t job_len;
   __shared__ int quit;
   const int tid = threadIdx.x;
   for (;;) {
@@ -526,9 +530,10 @@ __global__ __launch_bounds__(kFT) void k_serve(DeviceSnapshot s, ServeQueue *q, 
         const unsigned long long c = __hip_atomic_load(claimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long seq =
             __hip_atomic_load(&q->slot[c % kServeSlots].seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (seq == c + 1) {  // request c is posted: claim it
+        if ((seq & kServeSeqMask) == c + 1) {  // request c is posted: claim it
           if (atomicCAS(claimed, c, c + 1) == c) {
             job = c;
+            job_len = (uint32_t)(seq >> kServeSeqBits);
             quit = 0;
             break;
           }
@@ -547,7 +552,7 @@ __global__ __launch_bounds__(kFT) void k_serve(DeviceSnapshot s, ServeQueue *q, 
     ServeSlot *slot = &q->slot[job % kServeSlots];
     if (tid == 0) slot->t_claim = __builtin_amdgcn_s_memrealtime();
     ServeSink sink{slot, slot->dout, slot->hout, want_ids ? slot->iout : nullptr, job};
-    fast_topic(s, L, reinterpret_cast<const uint8_t *>(slot->topic), min(slot->len, kServeTopic + 1), sink);
+    fast_topic(s, L, reinterpret_cast<const uint8_t *>(slot->topic), min(job_len, kServeTopic + 1), sink);
     __syncthreads();
   }
 }
@@ -635,16 +640,6 @@ int match_small(const DeviceSnapshot &s, Workspace &ws, const char *bytes, const
                        a.recs, a.dout, a.dout_cap / sizeof(uint64_t), a.hout, a.hout_cap / sizeof(uint32_t),
                        want_ids ? a.iout : nullptr, a.iout_cap / sizeof(uint32_t), a.status);
     HIP_TRY(hipGetLastError());
-    // MQM_FAST_POLL=us: poll the status word the last workgroup writes for up
-    // to that long before the stream synchronisation (which reports errors);
-    // off by default: measured slower under many concurrent callers
-    static const long poll_us = getenv("MQM_FAST_POLL") ? atol(getenv("MQM_FAST_POLL")) : 0;
-    if (poll_us > 0) {
-      volatile unsigned int *done = &a.status->done;
-      const auto t0 = std::chrono::steady_clock::now();
-      while (!*done && std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(poll_us))
-        __builtin_ia32_pause();
-    }
     HIP_TRY(hipStreamSynchronize(st));
     FastStatus stt;
     memcpy(&stt, (const void *)a.status, sizeof(stt));  // after the stream synchronisation

@@ -190,8 +190,10 @@ constexpr uint32_t kServeSlots = 256;
 constexpr uint32_t kServeTopic = 1024;  // topic bytes a slot holds (the small-batch path's kFStage)
 constexpr uint32_t kServeD = 4096, kServeH = 512, kServeI = 4096;  // result capacities per slot
 enum : uint32_t { kServeOk = 0, kServeFallback = 1 };
+constexpr int kServeSeqBits = 48;  // ServeSlot::seq: request number + 1 below, the topic length above
+constexpr unsigned long long kServeSeqMask = (1ull << kServeSeqBits) - 1;
 struct alignas(64) ServeSlot {
-  unsigned long long seq;   // host: k + 1 once request k's topic is in place
+  unsigned long long seq;   // host: (k + 1) | len << kServeSeqBits once request k's topic is in place
   unsigned long long done;  // device: k + 1 once request k's result is complete
   uint32_t len, status;     // topic length; kServe* (fallback: the caller runs the batch pipeline)
   uint32_t dcount, hcount, icount, pad;

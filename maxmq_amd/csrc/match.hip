@@ -855,117 +855,6 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
   }
 }
 
-// k_wincopy's store side in 16-B quads: a step's 64 x kCU positions are
-// loaded as before (lane-consecutive 4-B loads of the descriptors' word runs),
-// staged in LDS, and written back as aligned 16-B stores — a quad every one of
-// whose 4 positions the step covers (the window base is 4096-entry aligned and
-// a step starts on a multiple of 4), else its covered positions one by one:
-// a quad may straddle a gap another kernel fills (a topic's merged winners)
-struct alignas(16) WinLds16 {
-  uint32_t st[kWave], en[kWave], src[kWave];
-  uint32_t blk[kWin / kWave];
-  uint32_t obuf[kWave * kCU];
-};
-
-__global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_eu(8))) void k_wincopy16(
-    DeviceSnapshot s, const uint4 *__restrict__ desc, const uint64_t *__restrict__ nd_ptr, uint64_t desc_cap,
-    const uint32_t *__restrict__ win, uint64_t win_cap, const uint64_t *__restrict__ total_ptr,
-    uint32_t *__restrict__ out, uint64_t cap, unsigned int *oob) {
-  __shared__ WinLds16 lds_all[kEmitWaves];
-  const uint64_t nd = min(*nd_ptr, desc_cap), total = *total_ptr;
-  const uint64_t nwin = min((total + kWin - 1) / kWin, win_cap);
-  const int lane = threadIdx.x & (kWave - 1);
-  WinLds16 &L = lds_all[threadIdx.x / kWave];
-  const __amdgpu_buffer_rsrc_t words =
-      __builtin_amdgcn_make_buffer_rsrc((void *)s.words, (short)0, (int)(s.n_subs * 4u + 64u), 0x00020000);
-  const uint64_t nw = (uint64_t)gridDim.x * kEmitWaves;
-  for (uint64_t w = (uint64_t)blockIdx.x * kEmitWaves + threadIdx.x / kWave; w < nwin; w += nw) {
-    const uint64_t g0 = w * kWin, g1 = min(g0 + kWin, total);
-    uint64_t j = win[w];
-    uint64_t pos = g0;
-    while (pos < g1 && j < nd) {
-      const uint64_t jj = j + lane;
-      uint4 d = make_uint4(0, 0, 0xFFFFFFFFu, 0xFFFFFFFFu);
-      if (jj < nd) d = desc[jj];
-      const uint64_t dst = d.z | ((uint64_t)d.w << 32);
-      const uint64_t dend = jj < nd ? dst + d.y : ~0ull;
-      uint64_t a = dst > pos ? dst : pos, b = dend < g1 ? dend : g1;
-      if (b < a) b = a;
-      if (a > g1) a = b = g1;
-      const uint64_t last_end = shfl64(dend, kWave - 1);
-      const uint64_t bend = j + kWave < nd ? (last_end < g1 ? (last_end > pos ? last_end : pos) : g1) : g1;
-      L.st[lane] = (uint32_t)(a - g0);
-      L.en[lane] = (uint32_t)(b - g0);
-      L.src[lane] = d.x + (uint32_t)(a - dst);
-      wave_lds_sync();
-      {
-        const uint32_t q = (uint32_t)lane * kWave;
-        uint32_t k = 0;
-#pragma unroll
-        for (uint32_t step = 32; step > 0; step >>= 1) k = L.st[k + step] <= q ? k + step : k;
-        L.blk[lane] = k;
-      }
-      wave_lds_sync();
-      const uint32_t q0 = (uint32_t)(pos - g0), q1 = (uint32_t)(bend - g0);
-      for (uint32_t base = q0 & ~3u; base < q1; base += kWave * kCU) {
-        uint32_t sa[kCU];
-        uint64_t m[kCU];  // positions the step covers (wave-uniform)
-#pragma unroll
-        for (int u = 0; u < kCU; u++) {
-          const uint32_t q = base + u * kWave + lane;
-          const uint32_t bq = min(q, (uint32_t)kWin - 1) / kWave;
-          uint32_t k = L.blk[bq], left = (bq + 1 < kWin / kWave ? L.blk[bq + 1] : kWave - 1) - k;
-          while (left > 0) {
-            const uint32_t half = (left + 1) / 2;
-            if (L.st[k + half] <= q) {
-              k += half;
-              left -= half;
-            } else {
-              left = half - 1;
-            }
-          }
-          const bool in = q >= q0 && q < q1 && q >= L.st[k] && q < L.en[k];
-          m[u] = __ballot(in);
-          sa[u] = in ? L.src[k] + (q - L.st[k]) : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < kCU; u++)
-          L.obuf[u * kWave + lane] = __builtin_amdgcn_raw_buffer_load_b32(words, (int)(sa[u] * 4u), 0, 0);
-        wave_lds_sync();
-#pragma unroll
-        for (int u2 = 0; u2 < kCU / 4; u2++) {
-          const uint32_t jq = u2 * kWave + lane;        // quad: step positions 4 jq .. 4 jq + 3
-          const int ub = u2 * 4 + lane / 16;            // (4 jq) / 64
-          uint64_t mu = 0;
-#pragma unroll
-          for (int u = 0; u < kCU; u++) mu = ub == u ? m[u] : mu;
-          const uint32_t bits = (uint32_t)(mu >> (4 * (lane & 15))) & 0xFu;
-          if (!bits) continue;
-          const uint64_t p = g0 + base + 4 * jq;
-          const uint4 v = *reinterpret_cast<const uint4 *>(&L.obuf[4 * jq]);
-          if (bits == 0xFu && p + 4 <= cap) {
-            *reinterpret_cast<uint4 *>(out + p) = v;
-          } else {
-            const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int e = 0; e < 4; e++)
-              if ((bits >> e) & 1u) {
-                if (p + e < cap)
-                  out[p + e] = vv[e];
-                else
-                  atomicOr(oob, kOobStore);
-              }
-          }
-        }
-        wave_lds_sync();
-      }
-      wave_lds_sync();
-      pos = bend;
-      j += kWave;
-    }
-  }
-}
-
 // ---- k_shared: shared candidates (gatherSharedSubscriptions, topics.go:541-555)
 // a 16-lane group per topic with H > 0: its shared hits are id ranges
 constexpr int kHL = 16;
@@ -1347,12 +1236,11 @@ __global__ __launch_bounds__(kBigThreads) void k_multi_part(DeviceSnapshot s, Ou
 // (C3: 8.1 -> 10.8 ms), so by default it takes the topics past the wave-table
 // tier (> 192 entries: r03n, C3 14.35 vs 14.48 ms and C4 shard 28.24 vs 28.80
 // ms against a threshold of 769).  Read at every batch (a test compares modes in one process):
-// MQM_RESOLVE=1 every light topic, MQM_RESOLVE=0 none (= MQM_NO_RESOLVE=1),
+// MQM_RESOLVE=1 every light topic, MQM_RESOLVE=0 none,
 // MQM_RESOLVE_MIN=m the threshold.
 constexpr uint32_t kResolveMinDefault = 193;
 static uint32_t resolve_min() {
   if (const char *v = getenv("MQM_RESOLVE")) return atoi(v) != 0 ? 1u : 0xFFFFFFFFu;
-  if (const char *v = getenv("MQM_NO_RESOLVE")) return atoi(v) == 0 ? 1u : 0xFFFFFFFFu;
   if (const char *v = getenv("MQM_RESOLVE_MIN")) return (uint32_t)std::max(1L, atol(v));
   return kResolveMinDefault;
 }
@@ -2302,13 +2190,8 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
                            dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nd_grid + 255) / 256, 8192))),
                            dim3(256), 0, st, desc, desc_start + n, desc_cap, o.dstart + n, win, win_cap, &o.ctr->oob);
         HIP_TRY(hipGetLastError());
-        static const bool copy16 = !getenv("MQM_COPY16") || atoi(getenv("MQM_COPY16")) != 0;  // A/B (temporary)
-        if (copy16)
-          hipLaunchKernelGGL(k_wincopy16, grid(k_wincopy16), dim3(kWave * kEmitWaves), 0, st, s, desc, desc_start + n,
-                             desc_cap, win, win_cap, o.dstart + n, o.dout, o.dcap, &o.ctr->oob);
-        else
-          hipLaunchKernelGGL(k_wincopy, grid(k_wincopy), dim3(kWave * kEmitWaves), 0, st, s, desc, desc_start + n,
-                             desc_cap, win, win_cap, o.dstart + n, o.dout, o.dcap, &o.ctr->oob);
+        hipLaunchKernelGGL(k_wincopy, grid(k_wincopy), dim3(kWave * kEmitWaves), 0, st, s, desc, desc_start + n,
+                           desc_cap, win, win_cap, o.dstart + n, o.dout, o.dcap, &o.ctr->oob);
         HIP_TRY(hipGetLastError());
       }
     }

@@ -8,17 +8,11 @@
 #   fastt   : small-batch path + batching collector + shim tests -> gpurun_out/TAG/pytest_fast.log
 #   quick   : every -m gpu test except the full-size ones
 #   lat     : C3 bench with the per-publish legs (single topic, 64 native callers direct / batched)
-#   variants: `fast` once per tuning build maxmq_amd/_lib/<name>/ (make variant) -> bench_fast_<name>.json
-#   c4fast / c4var: the C4 shard bench without CPU baseline (default build / every variant)
 #   c4pmc / pmc: FETCH_SIZE / WRITE_SIZE passes (C4 shard / C3) -> traffic_c4.json / traffic.json
 #   calib   : tools/_build/calib_fetch (random-gather / cooperative-gather rates) -> calib_kernels.txt
+#   c4fast  : the C4 shard bench without CPU baseline
 #   pipe    : `fast` with pipelined steps on 2 and 3 contexts -> bench_fast_pipe{2,3}.json
-#   abr     : `fast` with merge by resolution on / off (MQM_NO_RESOLVE=0/1)
 #   par     : the parity and queued-call GPU tests only
-#   c4ab    : the C4 shard bench with merge by resolution on / off
-#   profres : serial rocprof kernel stats of `fast` (merge by resolution on)
-#   parres  : `par` with the merge by resolution on (MQM_RESOLVE=1)
-#   abmin   : C3 and C4-shard `fast` with resolution from 193 multi entries (default 769)
 #   smoke   : __graft_entry__.smoke()
 #   bench   : the default bench line (C3)                -> gpurun_out/TAG/bench.json
 #   fast    : bench without CPU baseline / host path      -> gpurun_out/TAG/bench_fast.json
@@ -51,12 +45,7 @@ for step in "$@"; do
              > $OUT/pytest_quick.log 2>&1 ;;
     lat) timeout -k 10 600 python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --host-topics 0 \
              > $OUT/bench_lat.json 2> $OUT/bench_lat.log ;;
-    variants) for L in maxmq_amd/_lib/*/libmqmatch.so; do V=$(basename $(dirname $L)); [ "$V" = asan ] && continue;
-             MQM_LIB=$ROOT/$L timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_$V.json 2> $OUT/bench_fast_$V.log || exit 1; done ;;
     c4fast) timeout -k 10 600 python3 -u bench.py --config 4 --shard 0/8 $FAST > $OUT/bench_c4_fast.json 2> $OUT/bench_c4_fast.log ;;
-    c4var) for L in maxmq_amd/_lib/*/libmqmatch.so; do V=$(basename $(dirname $L)); [ "$V" = asan ] && continue;
-             MQM_LIB=$ROOT/$L timeout -k 10 600 python3 -u bench.py --config 4 --shard 0/8 $FAST > $OUT/bench_c4_fast_$V.json \
-             2> $OUT/bench_c4_fast_$V.log || exit 1; done ;;
     c4pmc) (cd /tmp && export TMPDIR=/tmp && for C in FETCH_SIZE WRITE_SIZE; do
              timeout -s KILL 400 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/c4pmc/pmc_$C -o pmc \
              -- python3 $ROOT/bench.py --config 4 --shard 0/8 --steps 1 --warmup 1 --no-cpu-baseline --host-topics 0 \
@@ -69,26 +58,8 @@ for step in "$@"; do
              python3 profiles/pmc_to_traffic.py $OUT/pmc > $OUT/traffic.json ;;
     pipe) for P in 2 3; do timeout -k 10 400 python3 -u bench.py $FAST --pipeline $P > $OUT/bench_fast_pipe$P.json \
              2> $OUT/bench_fast_pipe$P.log || exit 1; done ;;
-    abr) for V in 1 0; do MQM_RESOLVE=$V timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_res$V.json \
-             2> $OUT/bench_fast_res$V.log || exit 1; done ;;
-    c4ab) for V in 1 0; do MQM_RESOLVE=$V timeout -k 10 600 python3 -u bench.py --config 4 --shard 0/8 $FAST \
-             > $OUT/bench_c4_fast_res$V.json 2> $OUT/bench_c4_fast_res$V.log || exit 1; done ;;
-    profres) (cd /tmp && export TMPDIR=/tmp MQM_NO_OVERLAP=1 MQM_RESOLVE=1 && timeout -k 10 500 rocprofv3 --kernel-trace --stats \
-             --output-format csv -d $OUT/profres -o prof -- python3 $ROOT/bench.py $FAST \
-             > $OUT/bench_under_rocprof_res.json 2> $OUT/rocprof_res.log) ;;
-    parres) MQM_RESOLVE=1 timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_gpu_queued.py -m gpu --timeout 300 \
-             > $OUT/pytest_parres.log 2>&1 ;;
-    abmin) MQM_RESOLVE_MIN=193 timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_min193.json \
-             2> $OUT/bench_fast_min193.log && MQM_RESOLVE_MIN=193 timeout -k 10 600 python3 -u bench.py --config 4 \
-             --shard 0/8 $FAST > $OUT/bench_c4_fast_min193.json 2> $OUT/bench_c4_fast_min193.log ;;
-    fasttw) MQM_WAKE_TREE=1 timeout -k 10 500 $PYT tests/test_gpu_batching.py tests/test_gpu_shim.py -m gpu \
-             --timeout 200 > $OUT/pytest_fast_wake.log 2>&1 ;;
     par) timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_gpu_queued.py -m gpu --timeout 300 \
              > $OUT/pytest_par.log 2>&1 ;;
-    abq) for V in 1 0; do MQM_QUEUED=$V timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_q$V.json \
-             2> $OUT/bench_fast_q$V.log || exit 1; done ;;
-    abf) for V in 0 1; do MQM_FLUSH=$V timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_flush$V.json \
-             2> $OUT/bench_fast_flush$V.log || exit 1; done ;;
     profser) (cd /tmp && export TMPDIR=/tmp MQM_NO_OVERLAP=1 && timeout -k 10 500 rocprofv3 --kernel-trace --stats \
              --output-format csv -d $OUT/profser -o prof -- python3 $ROOT/bench.py $FAST \
              > $OUT/bench_under_rocprof_serial.json 2> $OUT/rocprof_serial.log) ;;
@@ -96,9 +67,6 @@ for step in "$@"; do
              --output-format csv -d $OUT/prof_c4ser -o prof -- python3 $ROOT/bench.py --config 4 --shard 0/8 --steps 3 \
              --warmup 1 --no-cpu-baseline --host-topics 0 --latency-topics 0 --steady-steps 0 \
              > $OUT/c4_under_rocprof_serial.json 2> $OUT/rocprof_c4ser.log) ;;
-    latab) LAT="--steps 1 --warmup 0 --no-cpu-baseline --host-topics 0 --steady-steps 0"
-             for V in "MQM_BASE=1" "MQM_WAKE_TREE=1" "MQM_BATCH_WORKERS=6"; do
-             env $V timeout -k 10 400 python3 -u bench.py $LAT > $OUT/bench_lat_${V//=/_}.json 2> $OUT/bench_lat_${V//=/_}.log || exit 1; done ;;
     calib) timeout -k 10 120 tools/_build/calib_fetch > $OUT/calib_kernels.txt 2>&1 ;;
     smoke) timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 ;;
     bench) timeout -k 10 600 python3 -u bench.py > $OUT/bench.json 2> $OUT/bench.log ;;
@@ -119,8 +87,6 @@ for step in "$@"; do
     c4counters) bash profiles/run_pmc_r02.sh $TAG/pmc_c4 --config 4 --shard 0/8 > $OUT/pmc_c4.log 2>&1 &&
              python3 profiles/derive_counters.py $OUT/pmc_c4 --json $OUT/c4_counters.json > $OUT/c4_counters.txt &&
              python3 profiles/pmc_to_traffic.py $OUT/pmc_c4 > $OUT/traffic_c4.json ;;
-    ab16) for V in 1 0; do MQM_COPY16=$V timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_copy16_$V.json \
-             2> $OUT/bench_fast_copy16_$V.log || exit 1; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
