@@ -1383,7 +1383,8 @@ struct Collector {
 struct Server {
   mqm_index *h;
   ServeQueue *q = nullptr;                // pinned, coherent, device-mapped
-  unsigned long long *claimed = nullptr;  // device: requests claimed so far
+  unsigned long long *claimed = nullptr;  // device: the next request number a workgroup takes
+  unsigned long long claim_from = 0;      // (mu) its value at the last launch
   hipStream_t st = nullptr;
   std::mutex mu;                          // launches / snapshot switches
   std::shared_ptr<GpuSnapshot> snap;      // what the running kernel reads
@@ -1483,6 +1484,17 @@ struct Server {
     halt();
     snap = cur;
     if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
+    // (no kernel runs now) the device counter restarts at the first request
+    // not yet served: a stopped kernel may have taken numbers past it
+    const uint64_t T = ticket.load(std::memory_order_acquire);
+    claim_from = T;
+    for (uint64_t k = T > kServeSlots ? T - kServeSlots : 0; k < T; k++)
+      if (__atomic_load_n(&q->slot[k % kServeSlots].done, __ATOMIC_ACQUIRE) < k + 1) {
+        claim_from = k;
+        break;
+      }
+    if (hipMemcpyAsync(claimed, &claim_from, sizeof(claim_from), hipMemcpyHostToDevice, st) != hipSuccess)
+      return MQM_EHIP;
     if (serve_launch(snap->dev, q, claimed, grid, idle_us, want_ids, st) != 0) return MQM_EHIP;
     launched = true;
     launches++;

@@ -480,11 +480,11 @@ __global__ __launch_bounds__(kFT) void k_fast(DeviceSnapshot s, const uint8_t *_
 
 // ---------------------------------------------------------------------------
 // k_serve: the per-publish server (match.h ServeQueue).  Lane 0 of an idle
-// workgroup polls the next unclaimed slot (system-scope loads of host
-// memory, with a growing s_sleep between polls) and claims it with one CAS on
-// the device counter; the workgroup runs fast_topic into the slot and
+// workgroup takes the next request number from the device counter and polls
+// that request's slot (system-scope loads of host memory, with a growing
+// s_sleep between polls); the workgroup runs fast_topic into the slot and
 // publishes done after a system fence.  Exit: the host's stop word, or
-// idle_us without a claim (s_memrealtime, 100 MHz).
+// idle_us without a request (s_memrealtime, 100 MHz).
 // ---------------------------------------------------------------------------
 struct ServeSink {
   ServeSlot *slot;
@@ -523,24 +523,29 @@ __global__ __launch_bounds__(kFT) void k_serve(DeviceSnapshot s, ServeQueue *q, 
   const int tid = threadIdx.x;
   for (;;) {
     if (tid == 0) {
+      // take the next request number first (a device atomic: workgroups wait
+      // on distinct requests in parallel, instead of queueing behind one PCIe
+      // poll per claim), then wait for its topic
+      const unsigned long long c = atomicAdd(claimed, 1ull);
+      ServeSlot *sl = &q->slot[c % kServeSlots];
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       uint32_t nap = 1;
       quit = 1;
       for (;;) {
-        const unsigned long long c = __hip_atomic_load(claimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long seq =
-            __hip_atomic_load(&q->slot[c % kServeSlots].seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-        if ((seq & kServeSeqMask) == c + 1) {  // request c is posted: claim it
-          if (atomicCAS(claimed, c, c + 1) == c) {
-            job = c;
-            job_len = (uint32_t)(seq >> kServeSeqBits);
-            quit = 0;
-            break;
-          }
-          continue;
+        const unsigned long long seq = __hip_atomic_load(&sl->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if ((seq & kServeSeqMask) == c + 1) {  // request c is posted
+          job = c;
+          job_len = (uint32_t)(seq >> kServeSeqBits);
+          quit = 0;
+          break;
         }
+        // stop: the host resets the counter to its first unserved request
+        // before the next launch (Server::ensure)
         if (__hip_atomic_load(&q->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;
+        // idle: give the number back — possible only while it is the last one
+        // taken, so idle workgroups leave newest first and no posted request
+        // is left without a waiter while the kernel runs
+        if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks && atomicCAS(claimed, c + 1, c) == c + 1) break;
         // back off: ~0.1 us while requests flow, up to ~0.4 us when idle (a
         // poll is one PCIe read of the slot's word)
         for (uint32_t z = 0; z < nap; z++) __builtin_amdgcn_s_sleep(4);

@@ -180,12 +180,13 @@ int match_small(const DeviceSnapshot &s, Workspace &ws, const char *bytes, const
 // ---- the per-publish server (fast.hip k_serve) -------------------------------
 // A persistent kernel of `grid` workgroups serves single-topic Subscribers
 // calls posted to a ring of slots in pinned, coherent host memory: the caller
-// writes the topic into slot k % kServeSlots and then seq = k + 1; an idle
-// workgroup claims request k (a device counter), runs the small-batch path's
-// per-topic body (fast_topic) straight into the slot and publishes done = k +
-// 1.  No launch and no stream synchronisation per call.  Every workgroup exits
-// on `stop`, or after idle_us without a request (the host relaunches on the
-// next call; unclaimed requests wait in the ring).
+// writes the topic into slot k % kServeSlots and then seq = k + 1 (with the
+// length); an idle workgroup takes the next request number k from a device
+// counter, waits for that slot's seq, runs the small-batch path's per-topic
+// body (fast_topic) straight into the slot and publishes done = k + 1.  No
+// launch and no stream synchronisation per call.  Every workgroup exits on
+// `stop`, or after idle_us without a request, returning its number (the host
+// relaunches on the next call; unserved requests wait in the ring).
 constexpr uint32_t kServeSlots = 256;
 constexpr uint32_t kServeTopic = 1024;  // topic bytes a slot holds (the small-batch path's kFStage)
 constexpr uint32_t kServeD = 4096, kServeH = 512, kServeI = 4096;  // result capacities per slot
@@ -209,8 +210,8 @@ struct ServeQueue {
   unsigned long long pad[7];
   ServeSlot slot[kServeSlots];
 };
-// launch the server on `st` (q: host-mapped; claimed: device counter, zeroed
-// once before the first launch and kept across relaunches)
+// launch the server on `st` (q: host-mapped; claimed: the device counter, set
+// by the host before every launch to the first request not yet served)
 int serve_launch(const DeviceSnapshot &s, ServeQueue *q, unsigned long long *claimed, uint32_t grid, uint32_t idle_us,
                  bool want_ids, hipStream_t st);
 
