@@ -289,6 +289,12 @@ int mqm_serve_stats(mqm_index *h, uint64_t *served, uint64_t *fallbacks, uint64_
 /* mean device time per served call (us[4]): claim to published result, then
  * its phases: topic staged + level keys, trie walk, emission + publish */
 int mqm_serve_device_us(mqm_index *h, double *us);
+/* mean host time per served call since the previous call of this function
+ * (us[4]; reads and resets): entry to request posted (snapshot check + slot
+ * wait + topic copy), posted to result seen (device time + detection +
+ * wake-up), result seen to return (result block built); then the share of
+ * calls that slept on the completion poller instead of spinning */
+int mqm_serve_host_us(mqm_index *h, double *us);
 int mqm_batching_stats(mqm_index *h, uint64_t *batches, uint64_t *topics);
 /* Device in / device out on `hip_stream` (hipStream_t, NULL = default stream). */
 int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t *d_topic_offsets,

@@ -258,6 +258,13 @@ class TopicsIndex:
         check("mqm_serve_device_us", lib().mqm_serve_device_us(self._h, v))
         return {"total": v[0], "stage_keys": v[1], "walk": v[2], "emit_publish": v[3]}
 
+    def serve_host_us(self):
+        """mean host time per served call since the previous read (us): entry
+        -> posted, posted -> result seen, seen -> returned; share that slept"""
+        v = (C.c_double * 4)()
+        check("mqm_serve_host_us", lib().mqm_serve_host_us(self._h, v))
+        return {"post": v[0], "wait": v[1], "collect": v[2], "slept_share": v[3]}
+
     def batching_stats(self):
         """(batches run, topics they carried) of the MQM_CFG_BATCHING collector"""
         b, t = C.c_uint64(), C.c_uint64()

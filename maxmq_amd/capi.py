@@ -49,7 +49,7 @@ EXPORTED = [
     "mqm_debug_fault", "mqm_gather_shards_shared", "mqm_match_ctx_create", "mqm_match_ctx_destroy",
     "mqm_match_device_async", "mqm_match_ctx_wait", "mqm_match_ctx_stats", "mqm_match_batch_packed",
     "mqm_result_packed", "mqm_match_batch_runs", "mqm_result_runs", "mqm_result_expand",
-    "mqm_serve_policy", "mqm_serve_stats", "mqm_serve_device_us",
+    "mqm_serve_policy", "mqm_serve_stats", "mqm_serve_device_us", "mqm_serve_host_us",
 ]
 
 
@@ -213,6 +213,7 @@ def lib():
         "mqm_serve_policy": ([vp, u32, u32], C.c_int),
         "mqm_serve_stats": ([vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)], C.c_int),
         "mqm_serve_device_us": ([vp, vp], C.c_int),
+        "mqm_serve_host_us": ([vp, vp], C.c_int),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

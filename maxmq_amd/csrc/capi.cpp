@@ -31,6 +31,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <new>
 #include <string_view>
 #include <thread>
@@ -127,6 +128,7 @@ struct mqm_index {
   Store store;
   std::shared_ptr<GpuSnapshot> snap;     // front buffer: what matches read
   uint64_t snap_version = ~0ull;         // store version the front buffer reflects
+  std::shared_mutex snap_rw;             // snap / snap_version: written under mu + this, read under either
   // MQM_CFG_ASYNC_COMMIT: mutations since the last submit, and the builder
   // that turns them into the back buffer (builder.h)
   DeltaLog journal;
@@ -224,6 +226,7 @@ int hip_rc(int rc) { return rc == -2 ? MQM_ENOMEM : rc == -1 ? MQM_EINVAL : rc <
 
 // make g the front buffer; readers that hold the old one keep it alive
 int install(mqm_index *h, std::shared_ptr<GpuSnapshot> g, uint64_t version) {
+  std::unique_lock<std::shared_mutex> w(h->snap_rw);
   h->snap = std::move(g);
   h->snap_version = version;
   return MQM_OK;
@@ -305,6 +308,19 @@ int front(mqm_index *h, std::shared_ptr<GpuSnapshot> *out) {
   if (!h->snap) return MQM_EINVAL;
   *out = h->snap;
   return MQM_OK;
+}
+
+// front() without the index lock, when nothing is to commit or publish: an
+// index without MQM_CFG_ASYNC_COMMIT whose front buffer exists and (with
+// MQM_CFG_AUTOCOMMIT) reflects the store's current version.  false: take
+// front().  (The per-publish server's callers: 64 of them on mu queue up.)
+bool front_fast(mqm_index *h, std::shared_ptr<GpuSnapshot> *out) {
+  if (h->async()) return false;
+  std::shared_lock<std::shared_mutex> r(h->snap_rw);
+  if (!h->snap) return false;
+  if ((h->cfg.flags & MQM_CFG_AUTOCOMMIT) && h->snap_version != h->store.version()) return false;
+  *out = h->snap;
+  return true;
 }
 
 int ctx_init(mqm_index *, MatchCtx *c) {
@@ -1397,29 +1413,42 @@ struct Server {
   std::atomic<uint64_t> device_ticks{0};  // claim -> publish on the device, summed (100 MHz ticks)
   std::atomic<uint64_t> phase_ticks[3] = {};  // stage + keys, walk, emission + publish
   std::atomic<uint64_t> timed{0};
+  // host-side time per call (ns, summed; mqm_serve_host_us reads and resets):
+  // entry -> posted, posted -> result seen, result seen -> returned; calls that slept
+  std::atomic<uint64_t> host_ns[3] = {}, host_calls{0}, host_slept{0};
   std::atomic<bool> live{false};                   // launched (may have exited idle since)
-  // completion poller: callers that stopped spinning sleep on waitw[slot];
-  // the poller watches their slots' done words and wakes them
+  // completion pollers: callers that stopped spinning sleep on waitw[slot];
+  // poller p watches the done words of the sleepers on slots i = p mod
+  // n_pollers and wakes them (one thread's FUTEX_WAKE calls cap the wake rate
+  // near 0.6M/s)
   std::unique_ptr<std::atomic<uint64_t>[]> waiting;  // slot -> the done value its sleeper waits for (0: none)
   std::unique_ptr<std::atomic<uint32_t>[]> waitw;    // futex words
-  std::atomic<uint32_t> sleepers{0}, poll_word{0}, inflight{0};
+  struct Poller {
+    std::atomic<uint32_t> sleepers{0}, word{0};
+    std::thread th;
+  };
+  static constexpr uint32_t kMaxPollers = 8;
+  Poller pollers[kMaxPollers];
+  uint32_t n_pollers = 4;
+  std::atomic<uint32_t> inflight{0};
+  std::atomic<int64_t> last_check_ns{0};  // the last liveness check of a late caller (steady clock)
   std::atomic<bool> poller_quit{false};
-  std::thread poller;
-  void poke_poller() {
-    poll_word.fetch_add(1, std::memory_order_acq_rel);
-    syscall(SYS_futex, reinterpret_cast<uint32_t *>(&poll_word), FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+  void poke_poller(Poller &pl) {
+    pl.word.fetch_add(1, std::memory_order_acq_rel);
+    syscall(SYS_futex, reinterpret_cast<uint32_t *>(&pl.word), FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
   }
-  void poll_loop() {
+  void poll_loop(uint32_t p) {
+    Poller &pl = pollers[p];
     while (!poller_quit.load(std::memory_order_acquire)) {
-      const uint32_t pw = poll_word.load(std::memory_order_acquire);
-      if (sleepers.load(std::memory_order_acquire) == 0) {
+      const uint32_t pw = pl.word.load(std::memory_order_acquire);
+      if (pl.sleepers.load(std::memory_order_acquire) == 0) {
         const struct timespec ts = {0, 1000000};  // 1 ms (quit is checked at least that often)
-        syscall(SYS_futex, reinterpret_cast<uint32_t *>(&poll_word), FUTEX_WAIT_PRIVATE, pw, &ts, nullptr, 0);
+        syscall(SYS_futex, reinterpret_cast<uint32_t *>(&pl.word), FUTEX_WAIT_PRIVATE, pw, &ts, nullptr, 0);
         continue;
       }
-      for (uint32_t i = 0; i < kServeSlots; i++) {
+      for (uint32_t i = p; i < kServeSlots; i += n_pollers) {
         const uint64_t w = waiting[i].load(std::memory_order_acquire);
-        if (w && __atomic_load_n(&q->slot[i].done, __ATOMIC_ACQUIRE) == w && !waitw[i].load(std::memory_order_relaxed)) {
+        if (w && __atomic_load_n(&q->done[i], __ATOMIC_ACQUIRE) == w && !waitw[i].load(std::memory_order_relaxed)) {
           waitw[i].store(1, std::memory_order_release);
           syscall(SYS_futex, reinterpret_cast<uint32_t *>(&waitw[i]), FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
         }
@@ -1451,7 +1480,8 @@ struct Server {
     if (hipMemsetAsync(claimed, 0, sizeof(unsigned long long), st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
       return MQM_EHIP;
-    poller = std::thread([this] { poll_loop(); });
+    if (const char *e = getenv("MQM_SERVE_POLLERS")) n_pollers = std::max(1, std::min<int>(kMaxPollers, atoi(e)));  // A/B (temporary)
+    for (uint32_t p = 0; p < n_pollers; p++) pollers[p].th = std::thread([this, p] { poll_loop(p); });
     return MQM_OK;
   }
   // (mu held) stop a running kernel and wait for it
@@ -1464,11 +1494,12 @@ struct Server {
     live.store(false, std::memory_order_release);
   }
   ~Server() {
-    if (poller.joinable()) {
-      poller_quit.store(true, std::memory_order_release);
-      poke_poller();
-      poller.join();
-    }
+    poller_quit.store(true, std::memory_order_release);
+    for (uint32_t p = 0; p < n_pollers; p++)
+      if (pollers[p].th.joinable()) {
+        poke_poller(pollers[p]);
+        pollers[p].th.join();
+      }
     if (q) {
       std::lock_guard<std::mutex> g(mu);
       halt();
@@ -1489,7 +1520,7 @@ struct Server {
     const uint64_t T = ticket.load(std::memory_order_acquire);
     claim_from = T;
     for (uint64_t k = T > kServeSlots ? T - kServeSlots : 0; k < T; k++)
-      if (__atomic_load_n(&q->slot[k % kServeSlots].done, __ATOMIC_ACQUIRE) < k + 1) {
+      if (__atomic_load_n(&q->done[k % kServeSlots], __ATOMIC_ACQUIRE) < k + 1) {
         claim_from = k;
         break;
       }
@@ -1508,8 +1539,10 @@ struct Server {
       fallbacks++;
       return direct(topic, len, out);
     }
+    using clk = std::chrono::steady_clock;
+    const auto t_in = clk::now();
     std::shared_ptr<GpuSnapshot> cur;
-    int rc = front(h, &cur);  // (commits first with MQM_CFG_AUTOCOMMIT)
+    int rc = front_fast(h, &cur) ? MQM_OK : front(h, &cur);  // (commits first with MQM_CFG_AUTOCOMMIT)
     if (rc != MQM_OK) return rc;
     const uint64_t k = ticket.fetch_add(1, std::memory_order_relaxed);
     const uint32_t i = (uint32_t)(k % kServeSlots);
@@ -1531,10 +1564,9 @@ struct Server {
     // spin on the slot's done word for a while (the single-caller latency
     // path), then sleep on a futex the completion poller wakes (more callers
     // than CPUs: a spinning caller would delay the ones whose results are
-    // ready); every ~100 us without a result, make sure a server is still
-    // running (it exits after idle_us without a claim; the request then
-    // waits, unclaimed, for the relaunch)
-    using clk = std::chrono::steady_clock;
+    // ready); a caller still without a result after 200 us makes sure a server
+    // is still running (it exits after idle_us without a request; the request
+    // then waits in the ring for the relaunch)
     const auto t0 = clk::now();
     bool ready = false;
     // (few callers in flight: spin through a whole call; many: sleep almost
@@ -1543,38 +1575,51 @@ struct Server {
     const auto spin_for = std::chrono::microseconds(inflight.fetch_add(1, std::memory_order_acq_rel) < 4 ? 300 : 2);
     for (uint32_t spin = 0; !ready; spin++) {
       __builtin_ia32_pause();
-      ready = __atomic_load_n(&sl.done, __ATOMIC_ACQUIRE) == k + 1;
+      ready = __atomic_load_n(&q->done[i], __ATOMIC_ACQUIRE) == k + 1;
       if (!ready && (spin & 15) == 15 && clk::now() - t0 > spin_for) break;
     }
     if (!ready) {
       waitw[i].store(0, std::memory_order_relaxed);
       waiting[i].store(k + 1, std::memory_order_release);
-      if (sleepers.fetch_add(1, std::memory_order_acq_rel) == 0) poke_poller();
-      while (__atomic_load_n(&sl.done, __ATOMIC_ACQUIRE) != k + 1) {
-        const struct timespec ts = {0, 100000};  // 100 us
+      Poller &pl = pollers[i % n_pollers];
+      if (pl.sleepers.fetch_add(1, std::memory_order_acq_rel) == 0) poke_poller(pl);
+      while (__atomic_load_n(&q->done[i], __ATOMIC_ACQUIRE) != k + 1) {
+        const struct timespec ts = {0, 500000};  // 500 us (a late result: the liveness check below)
         syscall(SYS_futex, reinterpret_cast<uint32_t *>(&waitw[i]), FUTEX_WAIT_PRIVATE, 0, &ts, nullptr, 0);
-        if (__atomic_load_n(&sl.done, __ATOMIC_ACQUIRE) == k + 1) break;
+        if (__atomic_load_n(&q->done[i], __ATOMIC_ACQUIRE) == k + 1) break;
+        // a wake meant for this slot's previous request (a waker that read
+        // `waiting` before this call stored it): re-arm, so the wait sleeps
+        waitw[i].store(0, std::memory_order_release);
+        if (__atomic_load_n(&q->done[i], __ATOMIC_ACQUIRE) == k + 1) break;
         const auto now = clk::now();
         if (now - t0 > std::chrono::seconds(10)) {
           fprintf(stderr, "mqmatch: per-publish server: no result for 10 s\n");
           waiting[i].store(0, std::memory_order_release);
-          sleepers.fetch_sub(1, std::memory_order_acq_rel);
+          pl.sleepers.fetch_sub(1, std::memory_order_acq_rel);
           inflight.fetch_sub(1, std::memory_order_acq_rel);
           return MQM_EHIP;  // (the slot stays taken: its late result is never read)
         }
-        if (now - t0 > std::chrono::microseconds(100)) {
+        // one liveness check per 200 us across all late callers (each is a
+        // HIP call under mu; 64 callers checking at once cost more CPU than
+        // the calls they wait for)
+        const int64_t now_ns = std::chrono::duration_cast<std::chrono::nanoseconds>(now.time_since_epoch()).count();
+        int64_t last = last_check_ns.load(std::memory_order_relaxed);
+        if (now - t0 > std::chrono::microseconds(200) && now_ns - last > 200000 &&
+            last_check_ns.compare_exchange_strong(last, now_ns, std::memory_order_acq_rel)) {
           std::lock_guard<std::mutex> g(mu);
           if ((rc = ensure(snap ? snap : cur)) != MQM_OK) {
             waiting[i].store(0, std::memory_order_release);
-            sleepers.fetch_sub(1, std::memory_order_acq_rel);
+            pl.sleepers.fetch_sub(1, std::memory_order_acq_rel);
             inflight.fetch_sub(1, std::memory_order_acq_rel);
             return rc;
           }
         }
       }
       waiting[i].store(0, std::memory_order_release);
-      sleepers.fetch_sub(1, std::memory_order_acq_rel);
+      pl.sleepers.fetch_sub(1, std::memory_order_acq_rel);
+      host_slept++;
     }
+    const auto t_seen = clk::now();
     inflight.fetch_sub(1, std::memory_order_acq_rel);
     const uint32_t status = sl.status;
     if (sl.t_done > sl.t_claim && sl.t_phase[0] >= sl.t_claim && sl.t_phase[1] >= sl.t_phase[0] &&
@@ -1595,6 +1640,10 @@ struct Server {
       served++;
     }
     free_seq[i].store(k + kServeSlots, std::memory_order_release);
+    host_ns[0] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t0 - t_in).count();
+    host_ns[1] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t_seen - t0).count();
+    host_ns[2] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - t_seen).count();
+    host_calls++;
     if (status == kServeOk) return rc;
     fallbacks++;
     return direct(topic, len, out);
@@ -1704,6 +1753,19 @@ int mqm_serve_device_us(mqm_index *h, double *us) {
   // s_memrealtime: 100 MHz; us[0] claim -> published, us[1..3] its phases
   us[0] = n ? (double)sv->device_ticks.load() / 100.0 / (double)n : 0.0;
   for (int i = 0; i < 3; i++) us[1 + i] = n ? (double)sv->phase_ticks[i].load() / 100.0 / (double)n : 0.0;
+  return MQM_OK;
+}
+
+int mqm_serve_host_us(mqm_index *h, double *us) {
+  Server *sv = h ? h->server.load(std::memory_order_acquire) : nullptr;
+  if (!sv || !us) return MQM_EINVAL;
+  const uint64_t n = sv->host_calls.exchange(0);
+  for (int i = 0; i < 3; i++) {
+    const uint64_t t = sv->host_ns[i].exchange(0);
+    us[i] = n ? (double)t / 1e3 / (double)n : 0.0;
+  }
+  const uint64_t sl = sv->host_slept.exchange(0);
+  us[3] = n ? (double)sl / (double)n : 0.0;
   return MQM_OK;
 }
 

@@ -488,6 +488,7 @@ __global__ __launch_bounds__(kFT) void k_fast(DeviceSnapshot s, const uint8_t *_
 // ---------------------------------------------------------------------------
 struct ServeSink {
   ServeSlot *slot;
+  unsigned long long *done_word;  // the slot's word of ServeQueue::done
   uint64_t *dout;
   uint32_t *hout;
   uint32_t *iout;
@@ -507,7 +508,7 @@ struct ServeSink {
     slot->icount = i;
     slot->t_done = __builtin_amdgcn_s_memrealtime();
     __threadfence_system();  // the result reaches host memory before done
-    __hip_atomic_store(&slot->done, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(done_word, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   __device__ void fallback() { publish(kServeFallback, 0, 0, 0); }
   __device__ void stamp(int i) { slot->t_phase[i] = __builtin_amdgcn_s_memrealtime(); }
@@ -556,7 +557,7 @@ __global__ __launch_bounds__(kFT) void k_serve(DeviceSnapshot s, ServeQueue *q, 
     if (quit) break;
     ServeSlot *slot = &q->slot[job % kServeSlots];
     if (tid == 0) slot->t_claim = __builtin_amdgcn_s_memrealtime();
-    ServeSink sink{slot, slot->dout, slot->hout, want_ids ? slot->iout : nullptr, job};
+    ServeSink sink{slot, &q->done[job % kServeSlots], slot->dout, slot->hout, want_ids ? slot->iout : nullptr, job};
     fast_topic(s, L, reinterpret_cast<const uint8_t *>(slot->topic), min(job_len, kServeTopic + 1), sink);
     __syncthreads();
   }

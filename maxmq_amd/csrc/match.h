@@ -195,7 +195,6 @@ constexpr int kServeSeqBits = 48;  // ServeSlot::seq: request number + 1 below, 
 constexpr unsigned long long kServeSeqMask = (1ull << kServeSeqBits) - 1;
 struct alignas(64) ServeSlot {
   unsigned long long seq;   // host: (k + 1) | len << kServeSeqBits once request k's topic is in place
-  unsigned long long done;  // device: k + 1 once request k's result is complete
   uint32_t len, status;     // topic length; kServe* (fallback: the caller runs the batch pipeline)
   uint32_t dcount, hcount, icount, pad;
   unsigned long long t_claim, t_done;  // device clock (s_memrealtime, 100 MHz): claimed, published
@@ -208,6 +207,10 @@ struct alignas(64) ServeSlot {
 struct ServeQueue {
   unsigned long long stop;  // host: 1 = every workgroup exits
   unsigned long long pad[7];
+  // device: done[i] = k + 1 once request k's result (slot i = k % kServeSlots)
+  // is complete — one contiguous 2-KB array, so the host's completion poller
+  // scans 32 cache lines rather than a line (and a page) per slot
+  unsigned long long done[kServeSlots];
   ServeSlot slot[kServeSlots];
 };
 // launch the server on `st` (q: host-mapped; claimed: the device counter, set

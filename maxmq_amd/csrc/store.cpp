@@ -294,7 +294,7 @@ bool Store::subscribe(std::string_view client, std::string_view filter, uint8_t 
   rec.no_local = no_local;
   rec.rap = rap;
   rec.rh = rh;
-  version_++;
+  version_.v.fetch_add(1, std::memory_order_release);
   std::string_view prefix;
   isolate_particle(filter, 0, &prefix);
   if (equal_fold_share(prefix)) {
@@ -327,7 +327,7 @@ bool Store::unsubscribe(std::string_view filter, std::string_view client) {
   int d = filter.substr(0, 6) == "$SHARE" ? 2 : 0;  // strings.HasPrefix: case-sensitive (topics.go:330)
   uint32_t n = seek_path(filter, d);
   if (n == kNone) return false;
-  version_++;
+  version_.v.fetch_add(1, std::memory_order_release);
   uint32_t cid = clients_.find(client);
   std::string_view prefix;
   isolate_particle(filter, 0, &prefix);
@@ -352,7 +352,7 @@ bool Store::unsubscribe(std::string_view filter, std::string_view client) {
 }
 
 int64_t Store::retain_message(std::string_view topic, uint64_t msg_ref, uint32_t payload_len, bool retain_flag) {
-  version_++;
+  version_.v.fetch_add(1, std::memory_order_release);
   uint32_t n = set_path(topic, 0);
   std::string key(topic);
   if (payload_len > 0) {

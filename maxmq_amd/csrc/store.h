@@ -7,6 +7,7 @@
 // GPU-resident CSR level-trie.  Strings are interned: tokens (level keys),
 // clients and filters each get dense u32 ids in first-appearance order.
 #pragma once
+#include <atomic>
 #include <stdint.h>
 
 #include <string>
@@ -108,7 +109,7 @@ class Store {
   uint32_t plus_token() const { return plus_tok_; }
   uint32_t hash_token() const { return hash_tok_; }
   uint32_t child(uint32_t parent, uint32_t tok) const;
-  uint64_t version() const { return version_; }
+  uint64_t version() const { return version_.v.load(std::memory_order_acquire); }
   const std::unordered_map<std::string, RetainedRec> &retained() const { return retained_; }
 
  private:
@@ -124,7 +125,17 @@ class Store {
   Interner tokens_, clients_, filters_;
   std::unordered_map<std::string, RetainedRec> retained_;  // packets.Packets (Retained)
   uint32_t plus_tok_, hash_tok_;
-  uint64_t version_ = 0;
+  // bumped by every mutation (under the index lock); read without it by the
+  // per-publish server's snapshot check (capi.cpp front_fast)
+  struct Version {
+    std::atomic<uint64_t> v{0};
+    Version() = default;
+    Version(const Version &o) : v(o.v.load(std::memory_order_relaxed)) {}
+    Version &operator=(const Version &o) {
+      v.store(o.v.load(std::memory_order_relaxed), std::memory_order_relaxed);
+      return *this;
+    }
+  } version_;
 };
 
 // isolateParticle (topics.go:558-577) over a byte string: level d and hasNext.
