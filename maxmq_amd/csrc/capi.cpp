@@ -1427,9 +1427,12 @@ struct Server {
     std::atomic<uint32_t> sleepers{0}, word{0};
     std::thread th;
   };
-  static constexpr uint32_t kMaxPollers = 8;
-  Poller pollers[kMaxPollers];
-  uint32_t n_pollers = 4;
+  // 3: measured on the 16-CPU box (r04p-r04r, 1M-filter index): 1 / 2 / 3 / 4
+  // pollers give 0.51 / 0.78 / 1.07 / 1.07M calls/s from 64 callers, and
+  // with 128 callers 3 pollers keep 0.96M where 4 spin the process into its
+  // CPU quota (0.37M)
+  static constexpr uint32_t n_pollers = 3;
+  Poller pollers[n_pollers];
   std::atomic<uint32_t> inflight{0};
   std::atomic<int64_t> last_check_ns{0};  // the last liveness check of a late caller (steady clock)
   std::atomic<bool> poller_quit{false};
@@ -1480,7 +1483,6 @@ struct Server {
     if (hipMemsetAsync(claimed, 0, sizeof(unsigned long long), st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
       return MQM_EHIP;
-    if (const char *e = getenv("MQM_SERVE_POLLERS")) n_pollers = std::max(1, std::min<int>(kMaxPollers, atoi(e)));  // A/B (temporary)
     for (uint32_t p = 0; p < n_pollers; p++) pollers[p].th = std::thread([this, p] { poll_loop(p); });
     return MQM_OK;
   }
