@@ -437,8 +437,7 @@ def main():
             else:
                 short = argparse.Namespace(**dict(vars(args), cpu_seconds=min(args.cpu_seconds, 2.0)))
                 _, stats = cpu_baseline(w, short)
-        roof = roofline(stats, n, kms, args.traffic_json, dt * 1e3 / args.steps if pipe else None,
-                        n_solo=lists.get("solo_deliveries"))
+        roof = roofline(stats, n, kms, args.traffic_json, dt * 1e3 / args.steps if pipe else None)
         out = {
             "metric": "publish topics matched/sec (node) + matched deliveries/sec at 10M filters",
             "value": value,
@@ -1161,15 +1160,14 @@ def cores_note(single, threads, host):
     return out
 
 
-def roofline(stats, n, kms, traffic_json, step_ms=None, n_solo=None):
+def roofline(stats, n, kms, traffic_json, step_ms=None):
     """B = T + 8N + 8P + 8V + 8S + 8D algorithmic bytes per
     batch (per-topic counters of the oracle's walk over the CPU sample, scaled
     to the batch) over the device time of the whole match pipeline (k_walk,
     scans, k_emit<16|64>, k_multi, k_dfs: first to last kernel, HIP events on
     the launch stream).  `stages` splits it by kernel: k_walk (HIP events
-    around it) moves T + 8N + 8P + 8V and the solo entries it copies as they
-    stand (8 B gathered + 8 B delivered each in the model: 16 x n_solo, the
-    count the GPU reports), the merges the rest of 8S + 8D.  `traffic` = HBM bytes per batch of the same
+    around it) moves T + 8N + 8P + 8V, everything after it (scans, route,
+    solo copy, merges) 8S + 8D.  `traffic` = HBM bytes per batch of the same
     kernels from rocprofv3 FETCH_SIZE / WRITE_SIZE (profiles/traffic.json from
     profiles/pmc_to_traffic.py over a profiles/run_pmc_r02.sh run, reads
     converted per access shape as tools/calib_fetch calibrated them).
@@ -1184,9 +1182,6 @@ def roofline(stats, n, kms, traffic_json, step_ms=None, n_solo=None):
     walk_b = (stats["topic_bytes"] + 8 * k + 8 * stats["probes"] + 8 * stats["visits"]) / k * n
     emit_b = (8 * stats["gathered"] + 8 * stats["deliveries"]) / k * n
     bytes_per_launch = walk_b + emit_b
-    if n_solo:  # the walk's solo copy, out of the emission's share
-        walk_b += 16 * n_solo
-        emit_b -= 16 * n_solo
     achieved = bytes_per_launch / (total_ms * 1e-3) / 1e9
     traffic = walk_traffic = None
     if traffic_json and os.path.exists(traffic_json):
@@ -1204,13 +1199,13 @@ def roofline(stats, n, kms, traffic_json, step_ms=None, n_solo=None):
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
             "algorithmic_bytes_per_topic": bytes_per_launch / n, "algorithmic_bytes_per_batch": bytes_per_launch,
-            "kernel": "match pipeline per batch: k_walk (walk + output reservation + solo copy) + scan + k_route "
-                      "+ merges (k_resolve; heavy topics k_merge_small, k_merge, k_multi) (+ k_dfs)",
+            "kernel": "match pipeline per batch: k_walk + scans + k_route + solo copy (k_desc, k_winmap, k_wincopy) "
+                      "+ merges (k_resolve; heavy topics k_merge_small, k_merge, k_multi) + k_shared (+ k_dfs)",
             "time_basis": ("ms per pipelined step (batches overlap)" if step_ms else
                            "device time of one batch (HIP events, first to last kernel)"),
             "ms": total_ms, "isolated_batch_ms": kms["total"],
             "stages": {"walk": dict(stage(walk_b, kms["walk"]), traffic=walk_traffic),
-                       "merge": stage(emit_b, kms["dedupe"])}}
+                       "emission": stage(emit_b, kms["dedupe"])}}
 
 
 if __name__ == "__main__":
