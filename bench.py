@@ -94,8 +94,10 @@ def parse():
     ap.add_argument("--sweep", default="",
                     help="tuning sweep before the measurement: ';'-separated variants of "
                          "'ENV=V,ENV=V' (runtime knobs, e.g. MQM_RESOLVE_MIN=769); per-variant kernel ms to stderr")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
-                    help="PMC-derived HBM bytes per emit launch (profiles/run_pmc.sh)")
+    ap.add_argument("--traffic-json", default="",
+                    help="PMC-derived HBM bytes per batch (profiles/pmc_to_traffic.py); default: the file of this "
+                         "workload, profiles/traffic.json (config 3) or profiles/traffic_c4.json (config 4 shard), "
+                         "none for other workloads")
     return ap.parse_args()
 
 
@@ -437,7 +439,13 @@ def main():
             else:
                 short = argparse.Namespace(**dict(vars(args), cpu_seconds=min(args.cpu_seconds, 2.0)))
                 _, stats = cpu_baseline(w, short)
-        roof = roofline(stats, n, kms, args.traffic_json, dt * 1e3 / args.steps if pipe else None)
+        tj = args.traffic_json
+        if not tj and not args.filters and not args.topics:  # counters are per workload
+            if args.config == 3 and not shard_of:
+                tj = os.path.join(ROOT, "profiles", "traffic.json")
+            elif args.config == 4 and shard_of:
+                tj = os.path.join(ROOT, "profiles", "traffic_c4.json")
+        roof = roofline(stats, n, kms, tj, dt * 1e3 / args.steps if pipe else None)
         out = {
             "metric": "publish topics matched/sec (node) + matched deliveries/sec at 10M filters",
             "value": value,

@@ -19,6 +19,7 @@
 #   prof    : rocprofv3 kernel trace + stats of `fast`    -> gpurun_out/TAG/prof/
 #   c4shard : C4 shard 0/8 bench line with roofline and CPU baseline
 #   c4prof  : rocprofv3 kernel stats of the C4 shard bench
+#   c4host  : the C4 shard bench with the host-path legs (runs / packed forms: the per-shard end-to-end rate)
 #   rev     : C5 reverse bench line (full 50M retained, CPU baseline, full-size selfcheck)
 #   counters / c4counters: the five rocprofv3 --pmc passes (profiles/run_pmc_r02.sh) over C3 / the C4
 #             shard -> c3_counters.txt (profiles/derive_counters.py), traffic.json
@@ -79,6 +80,8 @@ for step in "$@"; do
     c4prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv \
              -d $OUT/prof_c4 -o prof -- python3 $ROOT/bench.py --config 4 --shard 0/8 --steps 3 --warmup 1 \
              --no-cpu-baseline --host-topics 0 --latency-topics 0 > $OUT/c4_under_rocprof.json 2> $OUT/rocprof_c4.log) ;;
+    c4host) timeout -k 10 700 python3 -u bench.py --config 4 --shard 0/8 --steps 3 --warmup 1 --no-cpu-baseline \
+             --latency-topics 0 --steady-steps 0 > $OUT/bench_c4_host.json 2> $OUT/bench_c4_host.log ;;
     rev) timeout -k 10 900 python3 -u bench.py --workload reverse --steps 5 --warmup 1 --cpu-seconds 10 \
              > $OUT/bench_reverse.json 2> $OUT/bench_reverse.log ;;
     counters) bash profiles/run_pmc_r02.sh $TAG/pmc_c3 > $OUT/pmc_c3.log 2>&1 &&
