@@ -959,8 +959,6 @@ def run_reverse(args, dist, rank, world, local, dev):
 
     for _ in range(args.warmup):
         step()
-    if pipe:
-        drain()
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
@@ -999,7 +997,7 @@ def run_reverse(args, dist, rank, world, local, dev):
         achieved = per_batch / (dt / steps) / 1e9
         traffic = None  # PMC bytes per call (profiles/traffic_reverse.json, pmc_to_traffic.py --per-call)
         tj = os.path.join(ROOT, "profiles", "traffic_reverse.json")
-        if os.path.exists(tj):
+        if os.path.exists(tj) and not args.filters and args.retained == 50_000_000:
             try:
                 with open(tj) as fh:
                     traffic = json.load(fh).get("hbm_bytes_per_batch")

@@ -1306,15 +1306,19 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_resolve(DeviceSnapshot s,
     rec_prefix<kE, kH>(L.rec, nh, gl);  // part counts -> exclusive prefixes (multi_sid)
     wave_lds_sync();
     uint32_t D = 0;
+    // a lane's entries q rise (by kE per step): its part index hc only moves
+    // forward — one LDS read per entry and per part crossed, instead of a
+    // dependent 6-step search per entry
+    uint32_t hc = 0;
     for (uint32_t q0 = 0; q0 < M; q0 += kE * kPer) {
       uint32_t sid[kPer], rk[kPer], wd[kPer];
       uint2 pi[kPer];
 #pragma unroll
       for (int k = 0; k < kPer; k++) {  // every entry's loads in flight together
-        const uint32_t q = q0 + k * kE + gl;
-        uint32_t h;
-        sid[k] = multi_sid(L.rec, nh, q < M ? q : 0, &h);
-        rk[k] = rec_at(L.rec, h, kFieldRank);
+        const uint32_t q = min(q0 + k * kE + gl, M - 1);
+        while (hc + 1 < nh && rec_at(L.rec, hc + 1, kFieldMpre) <= q) hc++;
+        sid[k] = rec_at(L.rec, hc, kFieldOff) + (q - rec_at(L.rec, hc, kFieldMpre));
+        rk[k] = rec_at(L.rec, hc, kFieldRank);
         wd[k] = s.words[sid[k]];
         pi[k] = s.pinfo[sid[k]];
       }

@@ -20,6 +20,7 @@
 #   c4shard : C4 shard 0/8 bench line with roofline and CPU baseline
 #   c4prof  : rocprofv3 kernel stats of the C4 shard bench
 #   c4host  : the C4 shard bench with the host-path legs (runs / packed forms: the per-shard end-to-end rate)
+#   revpmc  : FETCH_SIZE / WRITE_SIZE passes of the C5 reverse bench -> traffic_reverse.json
 #   rev     : C5 reverse bench line (full 50M retained, CPU baseline, full-size selfcheck)
 #   counters / c4counters: the five rocprofv3 --pmc passes (profiles/run_pmc_r02.sh) over C3 / the C4
 #             shard -> c3_counters.txt (profiles/derive_counters.py), traffic.json
@@ -84,6 +85,11 @@ for step in "$@"; do
              --latency-topics 0 --steady-steps 0 > $OUT/bench_c4_host.json 2> $OUT/bench_c4_host.log ;;
     rev) timeout -k 10 900 python3 -u bench.py --workload reverse --steps 5 --warmup 1 --cpu-seconds 10 \
              > $OUT/bench_reverse.json 2> $OUT/bench_reverse.log ;;
+    revpmc) (cd /tmp && export TMPDIR=/tmp && for C in FETCH_SIZE WRITE_SIZE; do
+             timeout -s KILL 500 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/revpmc/pmc_$C -o pmc \
+             -- python3 $ROOT/bench.py --workload reverse --steps 1 --warmup 1 --no-cpu-baseline \
+             > $OUT/revpmc_$C.json 2> $OUT/revpmc_$C.log || exit 1; done) &&
+             python3 profiles/pmc_to_traffic.py $OUT/revpmc > $OUT/traffic_reverse.json ;;
     counters) bash profiles/run_pmc_r02.sh $TAG/pmc_c3 > $OUT/pmc_c3.log 2>&1 &&
              python3 profiles/derive_counters.py $OUT/pmc_c3 --json $OUT/c3_counters.json > $OUT/c3_counters.txt &&
              python3 profiles/pmc_to_traffic.py $OUT/pmc_c3 > $OUT/traffic.json ;;
