@@ -3,21 +3,24 @@
 
 One "step" = one TopicsIndex.Subscribers pass (topics.go:484-555) of the HIP
 path over a batch of publish topics already resident in HBM, through the C ABI
-(mqm_match_device): tokenize -> walk (+ output reservation and solo copy) ->
-merges -> per-topic segments of deliveries + shared candidates.  Workload (BASELINE.json `metric` is quoted "at 10M filters"):
+(mqm_match_device): tokenize + walk -> scans -> solo copy + merges ->
+per-topic segments of deliveries + shared candidates.  Workload (BASELINE.json `metric` is quoted "at 10M filters"):
 configs[2], 10M wildcard-heavy filters (40% '+', 10% '#', topics Zipf(1.2)
 over filter rank), 10M-topic batch, synthetic (tools/mqgen, seed 0x4D510003).
 
 N > 1 (torchrun, one rank per GPU, RCCL): --mode replicas (default) gives
 every rank the full trie and its own 10M-topic batch (weak scaling, no
-data-path collective); --mode sharded splits the subscribers by client range,
-RCCL-broadcasts rank 0's batch, and every shard's dense per-topic lists go
-back to rank 0 over RCCL send/recv, where mqm_gather_shards lays them out as
-the node-wide CSR (all inside the timed step), in chunks of topics sized so
-one gathered chunk fits --gather-budget-gb on rank 0 (maxmq_amd/shard.py
-node_step / plan_chunk); --mode hybrid runs GPUs / --shards independent
-replica groups of --shards subscriber shards each (own process group, own
-batch, own leader).
+data-path collective); --mode sharded splits the subscribers by client range
+and every shard matches the whole batch: with --gather host (default) each
+shard's runs-form result lands in pinned host memory over its own PCIe link
+(no data-path collective; DESIGN §6: the node step is PCIe-bound there), with
+--gather device rank 0's batch is RCCL-broadcast and every shard's dense
+per-topic lists go back to rank 0 over RCCL send/recv, where
+mqm_gather_shards lays them out as the node-wide CSR, in chunks of topics
+sized so one gathered chunk fits --gather-budget-gb on rank 0
+(maxmq_amd/shard.py node_step / plan_chunk); --mode hybrid runs GPUs /
+--shards independent replica groups of --shards subscriber shards each (own
+process group, own batch, own leader).
 
 Rank 0 prints ONE JSON line.  `roofline.achieved` = algorithmic bytes of the
 match pipeline (B = T + 8N + 8P + 8V + 8S + 8D, per-topic walk

@@ -76,7 +76,8 @@ constexpr int kICap = 48;                // load items per level (<= 3 per front
 //            nsolo[t]): k_desc's copy descriptors (and the runs form's runs)
 //   [kRecSh + 2i] off, [kRecSh + 1 + 2i] cnt of shared hit i (i < nsh)
 //   the tail, in 16-B units counted back from the record's end (rec_tail):
-//     unit 0      header: nm | nsh << 8, Ssolo, M, nsolo
+//     unit 0      header: nm | nsh << 8, Ssolo, M, nsolo (written only when M > 0,
+//                 H > 0 or in the runs form: its readers)
 //     unit 1 + h  multi part h (h < nm): moff, mcount, rank of its hit, 0 —
 //                 multi entries subs[moff, moff + mcount); the merges copy
 //                 the tail into LDS as header at word 0, part h at 4 + 4h,
@@ -602,7 +603,10 @@ __global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, co
     if (why == kNoWhy && S > kSMax) why = kWhyEntries;
     if (active && gl == 0) {
       const bool dfs = why != kNoWhy;
-      if (!dfs) tail[0] = make_uint4(nm | (nsh << 8), o.runs ? 0u : Ss, Ms, nq);  // (runs: winners at dstart)
+      // the header: read by the merges (Ms > 0), k_shared (H > 0) and the
+      // runs form's run listing; k_ident takes nq from nsolo and nm = 0 from
+      // Ms == 0 otherwise — most topics skip this 16-B write (a sector of its own)
+      if (!dfs && (Ms || H || o.runs)) tail[0] = make_uint4(nm | (nsh << 8), o.runs ? 0u : Ss, Ms, nq);
       o.cls[t] = dfs ? kClsDfs
                      : (S == 0 && H == 0) ? kClsDone
                                           : (kClsBounded | (nm <= kSmallHits ? kClsFewHits : 0) | (any_heavy ? kClsHeavy : 0));
@@ -817,12 +821,15 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
       for (uint32_t base = q0; base < q1; base += kWave * kCU) {
         uint32_t sa[kCU];
         bool in[kCU];
-#pragma unroll
-        for (int u = 0; u < kCU; u++) {
-          const uint32_t q = base + u * kWave + lane;
-          // the last descriptor starting at or before q: within [blk[b], blk[b + 1]]
+        // the lane's positions rise by 64 per entry: its descriptor (the last
+        // one starting at or before q) is found once per step through the
+        // block index, then only moves forward
+        uint32_t k;
+        {
+          const uint32_t q = base + lane;
           const uint32_t bq = min(q, (uint32_t)kWin - 1) / kWave;
-          uint32_t k = L.blk[bq], left = (bq + 1 < kWin / kWave ? L.blk[bq + 1] : kWave - 1) - k;
+          k = L.blk[bq];
+          uint32_t left = (bq + 1 < kWin / kWave ? L.blk[bq + 1] : kWave - 1) - k;
           while (left > 0) {
             const uint32_t half = (left + 1) / 2;
             if (L.st[k + half] <= q) {
@@ -832,6 +839,11 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
               left = half - 1;
             }
           }
+        }
+#pragma unroll
+        for (int u = 0; u < kCU; u++) {
+          const uint32_t q = base + u * kWave + lane;
+          while (k + 1 < kWave && L.st[k + 1] <= q) k++;
           in[u] = q < q1 && q >= L.st[k] && q < L.en[k];
           sa[u] = in[u] ? L.src[k] + (q - L.st[k]) : 0u;
         }
@@ -1594,7 +1606,10 @@ __global__ __launch_bounds__(256) void k_ident(DeviceSnapshot s, Outputs o, uint
       // every gathered range: the solo parts, then the multi parts
       const uint32_t *rec = o.recs + (uint64_t)t * kRecStrideAlloc;
       const uint4 *gt = rec_tail(o.recs, t);
-      const uint4 hd = gt[0];
+      // (the walk writes the header only for topics with multi parts or
+      // shared hits, or in the runs form, where nsolo is 0)
+      const bool hdr = o.runs || o.mcount[t] || o.hcount[t];
+      const uint4 hd = hdr ? gt[0] : make_uint4(0, 0, 0, o.nsolo[t]);
       const uint32_t nm = hd.x & 0xFFu, nq = hd.w;
       const uint64_t ib = kPhase == 1 ? o.istart[t] : 0;
       for (uint32_t h = 0; h < nq + nm; h++) {
