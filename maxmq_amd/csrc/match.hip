@@ -2378,6 +2378,12 @@ int identifiers_device(const DeviceSnapshot &s, Workspace &ws, hipStream_t st, I
   o.ctr = (Counters *)ws.ptr(W::kCounters);
   o.icount = (uint32_t *)ws.ptr(W::kICount);
   o.istart = (uint64_t *)ws.ptr(W::kIStart);
+  // (k_ident: a record header exists only where these say so, k_walk)
+  o.nsolo = (uint32_t *)ws.ptr(W::kNSolo);
+  o.mcount = (uint32_t *)ws.ptr(W::kMCount);
+  o.hcount = (uint32_t *)ws.ptr(W::kHCount);
+  o.runs = ws.last_runs ? 1u : 0u;
+  if (!o.nsolo || !o.mcount || !o.hcount) return -1;
   const uint32_t max_levels = s.height + 1;
   const size_t fb_lds = sizeof(uint32_t) * (((max_levels + 1) & ~1u) + 4 * (2 * max_levels + 8)) +
                         sizeof(uint64_t) * 2 * max_levels;
