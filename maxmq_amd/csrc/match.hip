@@ -821,15 +821,12 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
       for (uint32_t base = q0; base < q1; base += kWave * kCU) {
         uint32_t sa[kCU];
         bool in[kCU];
-        // the lane's positions rise by 64 per entry: its descriptor (the last
-        // one starting at or before q) is found once per step through the
-        // block index, then only moves forward
-        uint32_t k;
-        {
-          const uint32_t q = base + lane;
+#pragma unroll
+        for (int u = 0; u < kCU; u++) {
+          const uint32_t q = base + u * kWave + lane;
+          // the last descriptor starting at or before q: within [blk[b], blk[b + 1]]
           const uint32_t bq = min(q, (uint32_t)kWin - 1) / kWave;
-          k = L.blk[bq];
-          uint32_t left = (bq + 1 < kWin / kWave ? L.blk[bq + 1] : kWave - 1) - k;
+          uint32_t k = L.blk[bq], left = (bq + 1 < kWin / kWave ? L.blk[bq + 1] : kWave - 1) - k;
           while (left > 0) {
             const uint32_t half = (left + 1) / 2;
             if (L.st[k + half] <= q) {
@@ -839,11 +836,6 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
               left = half - 1;
             }
           }
-        }
-#pragma unroll
-        for (int u = 0; u < kCU; u++) {
-          const uint32_t q = base + u * kWave + lane;
-          while (k + 1 < kWave && L.st[k + 1] <= q) k++;
           in[u] = q < q1 && q >= L.st[k] && q < L.en[k];
           sa[u] = in[u] ? L.src[k] + (q - L.st[k]) : 0u;
         }
@@ -1318,19 +1310,15 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_resolve(DeviceSnapshot s,
     rec_prefix<kE, kH>(L.rec, nh, gl);  // part counts -> exclusive prefixes (multi_sid)
     wave_lds_sync();
     uint32_t D = 0;
-    // a lane's entries q rise (by kE per step): its part index hc only moves
-    // forward — one LDS read per entry and per part crossed, instead of a
-    // dependent 6-step search per entry
-    uint32_t hc = 0;
     for (uint32_t q0 = 0; q0 < M; q0 += kE * kPer) {
       uint32_t sid[kPer], rk[kPer], wd[kPer];
       uint2 pi[kPer];
 #pragma unroll
       for (int k = 0; k < kPer; k++) {  // every entry's loads in flight together
-        const uint32_t q = min(q0 + k * kE + gl, M - 1);
-        while (hc + 1 < nh && rec_at(L.rec, hc + 1, kFieldMpre) <= q) hc++;
-        sid[k] = rec_at(L.rec, hc, kFieldOff) + (q - rec_at(L.rec, hc, kFieldMpre));
-        rk[k] = rec_at(L.rec, hc, kFieldRank);
+        const uint32_t q = q0 + k * kE + gl;
+        uint32_t h;
+        sid[k] = multi_sid(L.rec, nh, q < M ? q : 0, &h);
+        rk[k] = rec_at(L.rec, h, kFieldRank);
         wd[k] = s.words[sid[k]];
         pi[k] = s.pinfo[sid[k]];
       }
