@@ -133,6 +133,7 @@ struct Counters {              // zeroed before every batch
   unsigned int n_shlist;       // k_shared: topics with shared candidates
   unsigned int n_res_small;    // k_resolve<8>: no heavy entry, Ms <= kSmallMultiS, nh <= kSmallHits
   unsigned int n_res;          // k_resolve<64>: other topics with multi entries and no heavy entry
+  unsigned int res_next;       // k_resolve<.., kChunk>: the next list entry to hand out
   unsigned long long m_sum[3]; // multi entries of the k_multi<1024> / <2048> / <4096> + k_multi_part lists
   unsigned int oob;            // a store fell outside its output buffer (queued calls: buffers sized
                                //   from an earlier call were too small; the call is re-run)
@@ -1255,7 +1256,7 @@ struct alignas(16) ResolveLds {
   uint32_t key[2 * kH], rank[2 * kH];  // gathered multi parts by multi-tail start + 1 (0: empty) -> hit rank
 };
 
-template <int kE, int kH, int kPer>
+template <int kE, int kH, int kPer, int kChunk = 0>
 __global__ __launch_bounds__(kWave *kEmitWaves) void k_resolve(DeviceSnapshot s, Outputs o,
                                                                const uint32_t *__restrict__ list,
                                                                const unsigned int *__restrict__ count) {
@@ -1285,10 +1286,22 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_resolve(DeviceSnapshot s,
     for (int v = 0; v < kUPer; v++)
       if (v * kE + gl < kUnits) u_n[v] = gt[-(v * kE + gl)];
   };
-  uint32_t i = (blockIdx.x * kEmitWaves + threadIdx.x / kWave) * kGroups + g;
+  // kChunk > 0 (a wave per topic only): list entries taken kChunk at a time
+  // from a device counter, so a wave that drew wide topics takes fewer;
+  // else a fixed stride over the list
+  uint32_t c_end = 0;
+  auto take = [&](uint32_t cur) -> uint32_t {
+    if (cur + 1 < c_end) return cur + 1;
+    uint32_t v = 0;
+    if (gl == 0) v = atomicAdd(&o.ctr->res_next, (unsigned)kChunk);
+    v = __shfl(v, 0, 64);
+    c_end = v + kChunk;
+    return v;
+  };
+  uint32_t i = kChunk ? take(~0u) : (blockIdx.x * kEmitWaves + threadIdx.x / kWave) * kGroups + g;
   if (i < nl) fetch(i);
   for (uint32_t i_next; i < nl; i = i_next) {
-    i_next = i + ngroups;
+    i_next = kChunk ? take(i) : i + ngroups;
     const uint32_t t = t_n;
     const uint64_t db = db_n;
     uint4 *rec4 = reinterpret_cast<uint4 *>(L.rec);
@@ -2149,9 +2162,11 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
     // device better at the end of the stream)
     if (l_r) {
       // 6 entries per lane in flight: C4 shard emission 20.39 ms against 21.64
-      // (4, 64 VGPRs) and 21.07 (8, 86 VGPRs, 5 waves/SIMD) — r04z
-      hipLaunchKernelGGL((k_resolve<kWave, kHCap, 6>), grid((k_resolve<kWave, kHCap, 6>)), dim3(kWave * kEmitWaves),
-                         0, st, s, o, lists.l[kLRes], lcount + kLRes);
+      // (4, 64 VGPRs) and 21.07 (8, 86 VGPRs, 5 waves/SIMD) — r04z;
+      // topics handed out 4 at a time from a device counter: C4 shard emission
+      // 19.03 ms against 20.22 with a fixed stride and 19.15 with 16 (r04ae)
+      hipLaunchKernelGGL((k_resolve<kWave, kHCap, 6, 4>), grid((k_resolve<kWave, kHCap, 6, 4>)),
+                         dim3(kWave * kEmitWaves), 0, st, s, o, lists.l[kLRes], lcount + kLRes);
       HIP_TRY(hipGetLastError());
     }
     if (l_t1) {
