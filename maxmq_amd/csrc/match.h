@@ -92,13 +92,6 @@ struct Workspace {
   // the runs form (mqm_match_batch_runs): solo parts stay runs of `words`
   // (runs_device lists them), dout holds the merged winners only
   bool runs = false, last_runs = false;
-  // the merges' stream: forked from the caller's stream after the routing,
-  // joined back before the totals (the merges and the solo copy write
-  // disjoint parts of the output and run side by side)
-  hipStream_t side = nullptr;
-  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
-  int fork(hipStream_t st, hipStream_t *out);
-  int join(hipStream_t st, hipStream_t side_st);
   const uint8_t *last_bytes = nullptr;
   const uint64_t *last_offs = nullptr;
 

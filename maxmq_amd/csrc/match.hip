@@ -1912,38 +1912,9 @@ uint64_t *Workspace::pinned_u64() {
   return reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(host_pinned) + kPinnedU64);
 }
 
-int Workspace::fork(hipStream_t st, hipStream_t *out) {
-  if (!side && hipStreamCreateWithFlags(&side, hipStreamNonBlocking) != hipSuccess) {
-    side = nullptr;
-    return -3;
-  }
-  if (!fork_ev && hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming) != hipSuccess) {
-    fork_ev = nullptr;
-    return -3;
-  }
-  if (hipEventRecord(fork_ev, st) != hipSuccess || hipStreamWaitEvent(side, fork_ev, 0) != hipSuccess) return -3;
-  *out = side;
-  return 0;
-}
-
-int Workspace::join(hipStream_t st, hipStream_t side_st) {
-  if (!join_ev && hipEventCreateWithFlags(&join_ev, hipEventDisableTiming) != hipSuccess) {
-    join_ev = nullptr;
-    return -3;
-  }
-  if (hipEventRecord(join_ev, side_st) != hipSuccess || hipStreamWaitEvent(st, join_ev, 0) != hipSuccess) return -3;
-  return 0;
-}
-
 Workspace::~Workspace() {
   // `cur` may name a caller's stream that no longer exists: wait on our event
   if (used && last_use) (void)hipEventSynchronize(last_use);
-  if (side) {
-    (void)hipStreamSynchronize(side);
-    (void)hipStreamDestroy(side);
-  }
-  if (fork_ev) (void)hipEventDestroy(fork_ev);
-  if (join_ev) (void)hipEventDestroy(join_ev);
   for (auto &b : bufs)
     if (b.p) (void)hipFree(b.p);
   if (last_use) (void)hipEventDestroy(last_use);
@@ -2187,54 +2158,49 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
     ws.pend_launched = launched;
     // persistent grids: the blocks that fit on the device at once
     auto grid = [&](auto kern) { return dim3(std::max<uint32_t>(1, resident_blocks(ws, 0, kern))); };
-    // the merges on the side stream, side by side with the solo copy (they
-    // write disjoint parts of dout and dcount: winners after Ss / topics with
-    // Ms > 0); the workgroup merges first, the small-topic merges last (they
-    // fill the device better at the end of the stream)
-    const bool merges = l_small || l_wave || l_t1 || l_t2 || l_t3 || l_part || l_rs || l_r;
-    hipStream_t ms = st;
-    if (merges && ws.fork(st, &ms)) return -3;
+    // the workgroup merges first, the small-topic merges last (they fill the
+    // device better at the end of the stream)
     if (l_r) {
       // 6 entries per lane in flight: C4 shard emission 20.39 ms against 21.64
       // (4, 64 VGPRs) and 21.07 (8, 86 VGPRs, 5 waves/SIMD) — r04z;
       // topics handed out 4 at a time from a device counter: C4 shard emission
       // 19.03 ms against 20.22 with a fixed stride and 19.15 with 16 (r04ae)
       hipLaunchKernelGGL((k_resolve<kWave, kHCap, 6, 4>), grid((k_resolve<kWave, kHCap, 6, 4>)),
-                         dim3(kWave * kEmitWaves), 0, ms, s, o, lists.l[kLRes], lcount + kLRes);
+                         dim3(kWave * kEmitWaves), 0, st, s, o, lists.l[kLRes], lcount + kLRes);
       HIP_TRY(hipGetLastError());
     }
     if (l_t1) {
-      hipLaunchKernelGGL(k_multi<1024>, grid(k_multi<1024>), dim3(kBigThreads), 0, ms, s, o, lists.l[kLT1],
+      hipLaunchKernelGGL(k_multi<1024>, grid(k_multi<1024>), dim3(kBigThreads), 0, st, s, o, lists.l[kLT1],
                          lcount + kLT1);
       HIP_TRY(hipGetLastError());
     }
     if (l_t2) {
-      hipLaunchKernelGGL(k_multi<2048>, grid(k_multi<2048>), dim3(kBigThreads), 0, ms, s, o, lists.l[kLT2],
+      hipLaunchKernelGGL(k_multi<2048>, grid(k_multi<2048>), dim3(kBigThreads), 0, st, s, o, lists.l[kLT2],
                          lcount + kLT2);
       HIP_TRY(hipGetLastError());
     }
     if (l_t3) {
-      hipLaunchKernelGGL(k_multi<4096>, grid(k_multi<4096>), dim3(kBigThreads), 0, ms, s, o, lists.l[kLT3],
+      hipLaunchKernelGGL(k_multi<4096>, grid(k_multi<4096>), dim3(kBigThreads), 0, st, s, o, lists.l[kLT3],
                          lcount + kLT3);
       HIP_TRY(hipGetLastError());
     }
     if (l_part) {
-      hipLaunchKernelGGL(k_multi_part, grid(k_multi_part), dim3(kBigThreads), 0, ms, s, o, lists.l[kLPart],
+      hipLaunchKernelGGL(k_multi_part, grid(k_multi_part), dim3(kBigThreads), 0, st, s, o, lists.l[kLPart],
                          lcount + kLPart);
       HIP_TRY(hipGetLastError());
     }
     if (l_rs) {
       hipLaunchKernelGGL((k_resolve<kSmallLanes, 16, 3>), grid((k_resolve<kSmallLanes, 16, 3>)),
-                         dim3(kWave * kEmitWaves), 0, ms, s, o, lists.l[kLResSmall], lcount + kLResSmall);
+                         dim3(kWave * kEmitWaves), 0, st, s, o, lists.l[kLResSmall], lcount + kLResSmall);
       HIP_TRY(hipGetLastError());
     }
     if (l_small) {
-      hipLaunchKernelGGL((k_merge_small<6>), grid(k_merge_small<6>), dim3(kWave * kEmitWaves), 0, ms, s, o,
+      hipLaunchKernelGGL((k_merge_small<6>), grid(k_merge_small<6>), dim3(kWave * kEmitWaves), 0, st, s, o,
                          lists.l[kLSmall], lcount + kLSmall);
       HIP_TRY(hipGetLastError());
     }
     if (l_wave) {
-      hipLaunchKernelGGL(k_merge, grid(k_merge), dim3(kWave * kEmitWaves), 0, ms, s, o, lists.l[kLWave],
+      hipLaunchKernelGGL(k_merge, grid(k_merge), dim3(kWave * kEmitWaves), 0, st, s, o, lists.l[kLWave],
                          lcount + kLWave);
       HIP_TRY(hipGetLastError());
     }
@@ -2260,7 +2226,6 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
                          lists.l[kLShared], lcount + kLShared);
       HIP_TRY(hipGetLastError());
     }
-    if (merges && ws.join(st, ms)) return -3;
   }
   if (dfs) {
     hipLaunchKernelGGL(k_dfs<1>, dim3(fb_blocks), dim3(kWave), fb_lds, st, s, d_bytes, d_offs, o, raw_cnt, raw_h,
