@@ -773,10 +773,10 @@ constexpr int kCU = 16;  // entries per lane per step
 // usually none or one step instead of six per entry
 struct alignas(16) WinLds {
   uint32_t st[kWave], en[kWave], src[kWave];
-  uint32_t map[kWave * kCU];  // a step's positions -> 1 + the descriptor holding (or preceding) each
+  uint32_t blk[kWin / kWave];
 };
 
-__global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_eu(6))) void k_wincopy(
+__global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_eu(8))) void k_wincopy(
     DeviceSnapshot s, const uint4 *__restrict__ desc, const uint64_t *__restrict__ nd_ptr, uint64_t desc_cap,
     const uint32_t *__restrict__ win, uint64_t win_cap, const uint64_t *__restrict__ total_ptr,
     uint32_t *__restrict__ out, uint64_t cap, unsigned int *oob) {
@@ -805,59 +805,39 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
       // positions handled by this batch: up to the end of its last descriptor
       const uint64_t last_end = shfl64(dend, kWave - 1);
       const uint64_t bend = j + kWave < nd ? (last_end < g1 ? (last_end > pos ? last_end : pos) : g1) : g1;
-      const uint32_t my_st = (uint32_t)(a - g0);
-      L.st[lane] = my_st;
+      L.st[lane] = (uint32_t)(a - g0);
       L.en[lane] = (uint32_t)(b - g0);
       L.src[lane] = d.x + (uint32_t)(a - dst);
-      // of descriptors starting at one position (empty ones before a real
-      // one) only the last marks it: every map entry has one writer
-      const uint32_t next_st = __shfl_down(my_st, 1, kWave);
-      const bool last_here = lane == kWave - 1 || next_st != my_st;
+      wave_lds_sync();
+      {  // block lane (positions lane * 64 ..): the last descriptor starting at or before its start
+        static_assert(kWin / kWave == kWave, "one block per lane");
+        const uint32_t q = (uint32_t)lane * kWave;
+        uint32_t k = 0;
+#pragma unroll
+        for (uint32_t step = 32; step > 0; step >>= 1) k = L.st[k + step] <= q ? k + step : k;
+        L.blk[lane] = k;
+      }
+      wave_lds_sync();
       const uint32_t q0 = (uint32_t)(pos - g0), q1 = (uint32_t)(bend - g0);
       for (uint32_t base = q0; base < q1; base += kWave * kCU) {
-        // position -> descriptor for the step's kWave * kCU positions without a
-        // search per entry (a chain of dependent LDS reads): mark each
-        // descriptor's start, then a running max over the positions (lane i
-        // owns positions 16 i .. 16 i + 15, a max-scan across lanes), read
-        // back lane-strided.  Descriptor starts are non-decreasing.
-        uint4 *m4 = reinterpret_cast<uint4 *>(L.map) + lane * (kCU / 4);
-#pragma unroll
-        for (int v = 0; v < kCU / 4; v++) m4[v] = make_uint4(0, 0, 0, 0);
-        // the descriptor holding `base`: the last one starting at or before it
-        const uint64_t before = __ballot(my_st <= base);
-        const uint32_t carry = before ? 64u - (uint32_t)__clzll(before) : 0u;  // 1 + its index, 0: none
-        wave_lds_sync();
-        if (last_here && my_st > base && my_st < base + kWave * kCU) L.map[my_st - base] = (uint32_t)lane + 1u;
-        wave_lds_sync();
-        uint32_t run[kCU], mx = 0;
-#pragma unroll
-        for (int v = 0; v < kCU / 4; v++) {
-          const uint4 x = m4[v];
-          run[4 * v] = x.x, run[4 * v + 1] = x.y, run[4 * v + 2] = x.z, run[4 * v + 3] = x.w;
-        }
-#pragma unroll
-        for (int e = 0; e < kCU; e++) mx = run[e] = max(mx, run[e]);
-        uint32_t inc = mx;  // inclusive max-scan of the lanes' maxima
-#pragma unroll
-        for (int dd = 1; dd < kWave; dd <<= 1) {
-          const uint32_t o_ = __shfl_up(inc, dd, kWave);
-          if (lane >= dd) inc = max(inc, o_);
-        }
-        uint32_t cin = __shfl_up(inc, 1, kWave);
-        cin = lane == 0 ? carry : max(cin, carry);
-#pragma unroll
-        for (int v = 0; v < kCU / 4; v++)
-          m4[v] = make_uint4(max(run[4 * v], cin), max(run[4 * v + 1], cin), max(run[4 * v + 2], cin),
-                             max(run[4 * v + 3], cin));
-        wave_lds_sync();
         uint32_t sa[kCU];
         bool in[kCU];
 #pragma unroll
         for (int u = 0; u < kCU; u++) {
           const uint32_t q = base + u * kWave + lane;
-          const uint32_t k1 = L.map[u * kWave + lane];
-          const uint32_t k = k1 ? k1 - 1 : 0;
-          in[u] = k1 != 0 && q < q1 && q < L.en[k];
+          // the last descriptor starting at or before q: within [blk[b], blk[b + 1]]
+          const uint32_t bq = min(q, (uint32_t)kWin - 1) / kWave;
+          uint32_t k = L.blk[bq], left = (bq + 1 < kWin / kWave ? L.blk[bq + 1] : kWave - 1) - k;
+          while (left > 0) {
+            const uint32_t half = (left + 1) / 2;
+            if (L.st[k + half] <= q) {
+              k += half;
+              left -= half;
+            } else {
+              left = half - 1;
+            }
+          }
+          in[u] = q < q1 && q >= L.st[k] && q < L.en[k];
           sa[u] = in[u] ? L.src[k] + (q - L.st[k]) : 0u;
         }
         uint32_t v[kCU];
@@ -872,7 +852,6 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
           else
             atomicOr(oob, kOobStore);
         }
-        wave_lds_sync();  // (the map is rewritten by the next step)
       }
       wave_lds_sync();
       pos = bend;
