@@ -1552,8 +1552,14 @@ struct Server {
     ServeSlot &sl = q->slot[i];
     memcpy(sl.topic, topic, len);
     sl.len = (uint32_t)len;
-    // the length rides in the word the server polls (no second PCIe read)
-    __atomic_store_n(&sl.seq, (k + 1) | ((unsigned long long)len << kServeSeqBits), __ATOMIC_RELEASE);
+    // the length rides in the word the server polls, the first kServeHead
+    // topic bytes in the same 64-B line (one PCIe read for a short topic),
+    // checked by chk
+    const unsigned long long seqw = (k + 1) | ((unsigned long long)len << kServeSeqBits);
+    unsigned long long head[kServeHead / 8];
+    memcpy(head, sl.topic, kServeHead);
+    sl.chk = serve_check(seqw, head);
+    __atomic_store_n(&sl.seq, seqw, __ATOMIC_RELEASE);
     // (no HIP call on the common path: the kernel's liveness is checked only
     // when a result is late, below)
     if (!live.load(std::memory_order_acquire) || running_on.load(std::memory_order_acquire) != cur.get()) {

@@ -69,7 +69,7 @@ struct alignas(16) FastLds {
   uint32_t item[2][kFItems];
   uint64_t key0[kFLevels], key1[kFLevels];
   uint16_t sep[kFLevels];
-  uint8_t stage[kFStage];
+  alignas(8) uint8_t stage[kFStage];
   uint32_t nitems[2], nh, nsh, fail, nsep, fill, nid, wsum[kFWaves];
   unsigned long long dbase, hbase, ibase;
 };
@@ -154,7 +154,7 @@ __device__ __forceinline__ void f_prefix(const uint32_t *v, uint32_t *pre, uint3
 // ---------------------------------------------------------------------------
 template <class Sink>
 __device__ __forceinline__ void fast_topic(const DeviceSnapshot &s, FastLds &L, const uint8_t *__restrict__ topic,
-                                           uint32_t len, Sink &sink) {
+                                           uint32_t len, Sink &sink, uint32_t pre = 0) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   // the root's descriptor: its load is in flight with the topic's (a PCIe
   // read when the topic is in host memory)
@@ -167,8 +167,8 @@ __device__ __forceinline__ void fast_topic(const DeviceSnapshot &s, FastLds &L, 
   }
   __syncthreads();
   const bool staged = len <= kFStage;
-  if (staged)
-    for (uint32_t i = tid; i < len; i += kFT) L.stage[i] = topic[i];
+  if (staged)  // (the first `pre` bytes: in LDS already, from the request's line)
+    for (uint32_t i = pre + tid; i < len; i += kFT) L.stage[i] = topic[i];
   __syncthreads();
   // ---- 1. separators and level keys ---------------------------------------
   if (wid == 0 && staged) {
@@ -521,24 +521,47 @@ __global__ __launch_bounds__(kFT) void k_serve(DeviceSnapshot s, ServeQueue *q, 
   __shared__ unsigned long long job;
   __shared__ uint32_t job_len;
   __shared__ int quit;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
   for (;;) {
-    if (tid == 0) {
+    if (tid < 64) {  // wave 0
       // take the next request number first (a device atomic: workgroups wait
       // on distinct requests in parallel, instead of queueing behind one PCIe
       // poll per claim), then wait for its topic
-      const unsigned long long c = atomicAdd(claimed, 1ull);
-      ServeSlot *sl = &q->slot[c % kServeSlots];
+      unsigned int clo = 0, chi = 0;
+      if (lane == 0) {
+        const unsigned long long c0 = atomicAdd(claimed, 1ull);
+        clo = (unsigned int)c0, chi = (unsigned int)(c0 >> 32);
+      }
+      const unsigned long long c = ((unsigned long long)__shfl(chi, 0, 64) << 32) | __shfl(clo, 0, 64);
+      const unsigned long long *line = reinterpret_cast<const unsigned long long *>(&q->slot[c % kServeSlots]);
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       uint32_t nap = 1;
-      quit = 1;
+      bool got = false;
       for (;;) {
-        const unsigned long long seq = __hip_atomic_load(&sl->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        // line 0 in one instruction: the request word, the check word and
+        // the topic's first kServeHead bytes (lanes 2 .. 7)
+        unsigned long long w = 0;
+        if (lane < 8) w = __hip_atomic_load(line + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const unsigned long long seq =
+            ((unsigned long long)__shfl((unsigned int)(w >> 32), 0, 64) << 32) | __shfl((unsigned int)w, 0, 64);
         if ((seq & kServeSeqMask) == c + 1) {  // request c is posted
-          job = c;
-          job_len = (uint32_t)(seq >> kServeSeqBits);
-          quit = 0;
-          break;
+          unsigned long long head[kServeHead / 8];
+#pragma unroll
+          for (int i = 0; i < (int)(kServeHead / 8); i++)
+            head[i] = ((unsigned long long)__shfl((unsigned int)(w >> 32), 2 + i, 64) << 32) |
+                      __shfl((unsigned int)w, 2 + i, 64);
+          const uint32_t chk = __shfl((unsigned int)w, 1, 64);
+          if (chk == serve_check(seq, head)) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the topic's later bytes: written before seq
+            if (lane >= 2 && lane < 8) *reinterpret_cast<unsigned long long *>(&L.stage[8 * (lane - 2)]) = w;
+            if (lane == 0) {
+              job = c;
+              job_len = (uint32_t)(seq >> kServeSeqBits);
+            }
+            got = true;
+            break;
+          }
+          continue;  // a read that tore (line 0 caught mid-write): read it again
         }
         // stop: the host resets the counter to its first unserved request
         // before the next launch (Server::ensure)
@@ -546,19 +569,24 @@ __global__ __launch_bounds__(kFT) void k_serve(DeviceSnapshot s, ServeQueue *q, 
         // idle: give the number back — possible only while it is the last one
         // taken, so idle workgroups leave newest first and no posted request
         // is left without a waiter while the kernel runs
-        if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks && atomicCAS(claimed, c + 1, c) == c + 1) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
+          unsigned int back = 0;
+          if (lane == 0) back = atomicCAS(claimed, c + 1, c) == c + 1 ? 1u : 0u;
+          if (__shfl(back, 0, 64)) break;
+        }
         // back off: ~0.1 us while requests flow, up to ~0.4 us when idle (a
-        // poll is one PCIe read of the slot's word)
+        // poll is one PCIe read of the slot's line 0)
         for (uint32_t z = 0; z < nap; z++) __builtin_amdgcn_s_sleep(4);
         nap = nap < 4 ? nap + 1 : nap;
       }
+      if (lane == 0) quit = got ? 0 : 1;
     }
     __syncthreads();
     if (quit) break;
     ServeSlot *slot = &q->slot[job % kServeSlots];
     if (tid == 0) slot->t_claim = __builtin_amdgcn_s_memrealtime();
     ServeSink sink{slot, &q->done[job % kServeSlots], slot->dout, slot->hout, want_ids ? slot->iout : nullptr, job};
-    fast_topic(s, L, reinterpret_cast<const uint8_t *>(slot->topic), min(job_len, kServeTopic + 1), sink);
+    fast_topic(s, L, reinterpret_cast<const uint8_t *>(slot->topic), min(job_len, kServeTopic + 1), sink, kServeHead);
     __syncthreads();
   }
 }

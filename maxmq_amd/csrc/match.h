@@ -193,17 +193,32 @@ constexpr uint32_t kServeD = 4096, kServeH = 512, kServeI = 4096;  // result cap
 enum : uint32_t { kServeOk = 0, kServeFallback = 1 };
 constexpr int kServeSeqBits = 48;  // ServeSlot::seq: request number + 1 below, the topic length above
 constexpr unsigned long long kServeSeqMask = (1ull << kServeSeqBits) - 1;
+constexpr uint32_t kServeHead = 48;  // topic bytes in the slot's first 64-B line, with seq and chk
 struct alignas(64) ServeSlot {
+  // line 0, read by the polling workgroup in one 64-B load: the request word,
+  // a check word and the topic's first kServeHead bytes
   unsigned long long seq;   // host: (k + 1) | len << kServeSeqBits once request k's topic is in place
+  uint32_t chk, pad0;       // host: serve_check(seq, the head bytes): a read of line 0 that tore fails it
+  char topic[kServeTopic];  // topic bytes (0 .. kServeHead - 1 in line 0)
   uint32_t len, status;     // topic length; kServe* (fallback: the caller runs the batch pipeline)
   uint32_t dcount, hcount, icount, pad;
   unsigned long long t_claim, t_done;  // device clock (s_memrealtime, 100 MHz): claimed, published
   unsigned long long t_phase[2];       // ... topic staged and keys built, trie walked
-  char topic[kServeTopic];
   uint64_t dout[kServeD];   // {client, packed} deliveries
   uint32_t hout[kServeH];   // shared-subscription ids
   uint32_t iout[kServeI];   // identifier sids (want_ids)
 };
+static_assert(offsetof(ServeSlot, topic) + kServeHead == 64, "ServeSlot line 0");
+// the check word of line 0 (host and device): a mix of the request word and
+// the kServeHead topic bytes as 6 little-endian words
+MQM_HD uint32_t serve_check(unsigned long long seq, const unsigned long long *head) {
+  unsigned long long x = seq * 0x9E3779B97F4A7C15ull;
+  for (int i = 0; i < (int)(kServeHead / 8); i++) {
+    x = (x ^ head[i]) * 0xD6E8FEB86659FD93ull;
+    x ^= x >> 32;
+  }
+  return (uint32_t)(x >> 29);
+}
 struct ServeQueue {
   unsigned long long stop;  // host: 1 = every workgroup exits
   unsigned long long pad[7];
