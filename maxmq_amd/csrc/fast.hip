@@ -70,7 +70,7 @@ struct alignas(16) FastLds {
   uint64_t key0[kFLevels], key1[kFLevels];
   uint16_t sep[kFLevels];
   alignas(8) uint8_t stage[kFStage];
-  uint32_t nitems[2], nh, nsh, fail, nsep, fill, nid, wsum[kFWaves];
+  uint32_t nitems[3], nh, nsh, fail, nsep, fill, nid, wsum[kFWaves];  // item counts of levels d mod 3
   unsigned long long dbase, hbase, ibase;
 };
 
@@ -163,7 +163,7 @@ __device__ __forceinline__ void fast_topic(const DeviceSnapshot &s, FastLds &L, 
   if (tid == 0) {
     L.fail = len > kFStage ? 1u : 0u;
     L.nh = L.nsh = 0;
-    L.nitems[0] = L.nitems[1] = 0;
+    L.nitems[0] = L.nitems[1] = L.nitems[2] = 0;
   }
   __syncthreads();
   const bool staged = len <= kFStage;
@@ -209,9 +209,12 @@ __device__ __forceinline__ void fast_topic(const DeviceSnapshot &s, FastLds &L, 
   __syncthreads();
   if (tid == 0) sink.stamp(0);  // staged, keys built
   // ---- 2. level-synchronous walk -------------------------------------------
-  int cur = 0;
+  int cur = 0;  // item lists alternate; their counts rotate over three words, so
+                // the count two levels ahead is cleared during this level and one
+                // barrier per level suffices
   for (uint32_t d = 0; d < nlev; d++) {
-    const uint32_t ni = L.nitems[cur];
+    const uint32_t ni = L.nitems[d % 3];
+    if (tid == 0) L.nitems[(d + 2) % 3] = 0;  // (last read at level d - 1)
     if (ni == 0 || L.fail) break;  // block-uniform (read after a barrier)
     const uint64_t k0 = L.key0[d], k1 = L.key1[d];
     const bool has_next = d + 1 < nlev;
@@ -265,7 +268,7 @@ __device__ __forceinline__ void fast_topic(const DeviceSnapshot &s, FastLds &L, 
       if (has_next && (fl & kFlagHasChildren)) {
         const bool has_lit = fl & kFlagHasLiteral;
         const uint32_t k = (has_lit ? 1u : 0u) + (dc.plus != kNone ? 1u : 0u) + (dc.hash != kNone ? 1u : 0u);
-        const uint32_t at = k ? atomicAdd(&L.nitems[cur ^ 1], k) : 0;
+        const uint32_t at = k ? atomicAdd(&L.nitems[(d + 1) % 3], k) : 0;
         if (at + k > kFItems) {
           atomicOr(&L.fail, 1u);
         } else {
@@ -277,9 +280,7 @@ __device__ __forceinline__ void fast_topic(const DeviceSnapshot &s, FastLds &L, 
       }
     }
     __syncthreads();
-    if (tid == 0) L.nitems[cur] = 0;  // becomes the level after next's list
     cur ^= 1;
-    __syncthreads();
   }
   if (L.fail) {  // block-uniform: the batch takes the pipeline without limits
     if (tid == 0) sink.fallback();
