@@ -20,6 +20,7 @@
 #   c4shard : C4 shard 0/8 bench line with roofline and CPU baseline
 #   c4prof  : rocprofv3 kernel stats of the C4 shard bench
 #   c4host  : the C4 shard bench with the host-path legs (runs / packed forms: the per-shard end-to-end rate)
+#   revprof : rocprofv3 kernel trace + stats of the C5 reverse bench
 #   revpmc  : FETCH_SIZE / WRITE_SIZE passes of the C5 reverse bench -> traffic_reverse.json
 #   rev     : C5 reverse bench line (full 50M retained, CPU baseline, full-size selfcheck)
 #   counters / c4counters: the five rocprofv3 --pmc passes (profiles/run_pmc_r02.sh) over C3 / the C4
@@ -90,6 +91,9 @@ for step in "$@"; do
              -- python3 $ROOT/bench.py --workload reverse --steps 1 --warmup 1 --no-cpu-baseline \
              > $OUT/revpmc_$C.json 2> $OUT/revpmc_$C.log || exit 1; done) &&
              python3 profiles/pmc_to_traffic.py $OUT/revpmc > $OUT/traffic_reverse.json ;;
+    revprof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
+             -d $OUT/prof_rev -o prof -- python3 $ROOT/bench.py --workload reverse --steps 2 --warmup 1 --no-cpu-baseline \
+             > $OUT/rev_under_rocprof.json 2> $OUT/rocprof_rev.log) ;;
     counters) bash profiles/run_pmc_r02.sh $TAG/pmc_c3 > $OUT/pmc_c3.log 2>&1 &&
              python3 profiles/derive_counters.py $OUT/pmc_c3 --json $OUT/c3_counters.json > $OUT/c3_counters.txt &&
              python3 profiles/pmc_to_traffic.py $OUT/pmc_c3 > $OUT/traffic.json ;;
