@@ -90,8 +90,12 @@ def test_served_fallbacks_idle_relaunch_and_new_snapshot():
     for x in (idx, ref):
         x.subscribe("a", maxmq_amd.Subscription("a/+", 1))
         x.subscribe("b", maxmq_amd.Subscription("a/b", 2))
+        x.subscribe("h", maxmq_amd.Subscription("#", 1))  # not for '$' topics (topics.go:527)
     long_topic = "a/" + "x" * 2000  # longer than a slot's topic bytes
-    topics = [b"big/q", b"a/b", long_topic.encode(), b"zzz"]
+    # around the 48 topic bytes that ride in the slot's polled line (ServeSlot
+    # line 0): empty, 47 / 48 / 49 bytes, and a '$' topic
+    edge = [b"", b"a/" + b"y" * 45, b"a/" + b"y" * 46, b"a/" + b"y" * 47, b"$SYS/a"]
+    topics = [b"big/q", b"a/b", long_topic.encode(), b"zzz"] + edge
 
     def check_all():
         for t in topics:
@@ -100,7 +104,7 @@ def test_served_fallbacks_idle_relaunch_and_new_snapshot():
 
     check_all()
     served, fallbacks, launches = idx.serve_stats()
-    assert fallbacks == 2 and served == 2, (served, fallbacks)
+    assert fallbacks == 2 and served == 2 + len(edge), (served, fallbacks)
     time.sleep(0.05)  # the server exits idle; the next call relaunches it
     check_all()
     assert idx.serve_stats()[2] >= 2, idx.serve_stats()
