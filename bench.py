@@ -402,8 +402,9 @@ def main():
         # kernel times of the stages: isolated (blocking) batches on the index's
         # own workspace after the timed region (the pipelined contexts overlap
         # batches, so a batch has no device time of its own there)
-        for c in pipe["ctxs"]:
-            c.close()
+        # (the contexts stay open until the end: freeing their ~30 GB of
+        # workspace here slowed the host-path leg that follows, 113M vs 156M
+        # topics/s on one box, r04al / r04am)
         idx.profile(False)
         idx.profile(True)
         for _ in range(3):
@@ -505,6 +506,8 @@ def main():
             "single_topic_latency": lat,
         }
         print(json.dumps(out), flush=True)
+    for c in pipe.get("ctxs", []):
+        c.close()
     if dist:
         dist.barrier()
         dist.destroy_process_group()
