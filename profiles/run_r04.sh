@@ -37,7 +37,7 @@ PYT="python3 -u -m pytest -x -v --timeout-method thread"
 for step in "$@"; do
   echo "[run_r04] $step $(date +%T)"
   case $step in
-    tests) timeout -k 10 1000 $PYT tests -m gpu --timeout 600 > $OUT/pytest_gpu.log 2>&1 ;;
+    tests) timeout -k 10 1000 $PYT tests -m gpu --timeout 600 --durations=15 > $OUT/pytest_gpu.log 2>&1 ;;
     c4test) timeout -k 10 600 $PYT tests/test_gpu_c4_shard.py -m gpu --timeout 500 > $OUT/pytest_c4.log 2>&1 ;;
     ret) timeout -k 10 600 $PYT tests/test_gpu_retained.py -m gpu --timeout 300 > $OUT/pytest_ret.log 2>&1 ;;
     nobloom) MQM_NO_BLOOM=1 timeout -k 10 400 $PYT tests/test_gpu_parity.py -m gpu --timeout 200 \
