@@ -364,6 +364,9 @@ def main():
         step()
     if pipe:
         drain()
+        # the index's own workspace (the isolated batches timed per stage after
+        # the timed region) sized now, so those batches allocate nothing
+        idx.match_device(tb.data_ptr(), to.data_ptr(), n, stream.cuda_stream)
     torch.cuda.synchronize(dev)
     if args.sweep:
         run_sweep(args, idx, step, dev, rank)
