@@ -16,7 +16,8 @@
 #   smoke   : __graft_entry__.smoke()
 #   bench   : the default bench line (C3)                -> gpurun_out/TAG/bench.json
 #   fast    : bench without CPU baseline / host path      -> gpurun_out/TAG/bench_fast.json
-#   prof    : rocprofv3 kernel trace + stats of `fast`    -> gpurun_out/TAG/prof/
+#   prof    : rocprofv3 kernel trace + stats of `fast`, one batch at a time (pipelined batches overlap
+#             their kernels, so per-kernel durations would mix)  -> gpurun_out/TAG/prof/
 #   c4shard : C4 shard 0/8 bench line with roofline and CPU baseline
 #   c4prof  : rocprofv3 kernel stats of the C4 shard bench
 #   c4host  : the C4 shard bench with the host-path legs (runs / packed forms: the per-shard end-to-end rate)
@@ -75,12 +76,12 @@ for step in "$@"; do
     bench) timeout -k 10 600 python3 -u bench.py > $OUT/bench.json 2> $OUT/bench.log ;;
     fast) timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast.json 2> $OUT/bench_fast.log ;;
     prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv \
-             -d $OUT/prof -o prof -- python3 $ROOT/bench.py $FAST \
+             -d $OUT/prof -o prof -- python3 $ROOT/bench.py $FAST --pipeline 0 \
              > $OUT/bench_under_rocprof.json 2> $OUT/rocprof.log) ;;
     c4shard) timeout -k 10 700 python3 -u bench.py --config 4 --shard 0/8 --steps 5 --warmup 2 --host-topics 0 \
              --latency-topics 0 --cpu-seconds 10 > $OUT/bench_c4_shard0of8.json 2> $OUT/bench_c4_shard0of8.log ;;
     c4prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv \
-             -d $OUT/prof_c4 -o prof -- python3 $ROOT/bench.py --config 4 --shard 0/8 --steps 3 --warmup 1 \
+             -d $OUT/prof_c4 -o prof -- python3 $ROOT/bench.py --config 4 --shard 0/8 --steps 3 --warmup 1 --pipeline 0 \
              --no-cpu-baseline --host-topics 0 --latency-topics 0 > $OUT/c4_under_rocprof.json 2> $OUT/rocprof_c4.log) ;;
     c4host) timeout -k 10 700 python3 -u bench.py --config 4 --shard 0/8 --steps 3 --warmup 1 --no-cpu-baseline \
              --latency-topics 0 --steady-steps 0 > $OUT/bench_c4_host.json 2> $OUT/bench_c4_host.log ;;
