@@ -790,7 +790,6 @@ struct alignas(16) WinLds {
   uint32_t blk[kWin / kWave];
 };
 
-template <bool kPair = false>
 __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_eu(8))) void k_wincopy(
     DeviceSnapshot s, const uint4 *__restrict__ desc, const uint64_t *__restrict__ nd_ptr, uint64_t desc_cap,
     const uint32_t *__restrict__ win, uint64_t win_cap, const uint64_t *__restrict__ total_ptr,
@@ -834,83 +833,24 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
       }
       wave_lds_sync();
       const uint32_t q0 = (uint32_t)(pos - g0), q1 = (uint32_t)(bend - g0);
-      // the last descriptor starting at or before q: within [blk[b], blk[b + 1]]
-      auto find = [&](uint32_t q) -> uint32_t {
-        const uint32_t bq = min(q, (uint32_t)kWin - 1) / kWave;
-        uint32_t k = L.blk[bq], left = (bq + 1 < kWin / kWave ? L.blk[bq + 1] : kWave - 1) - k;
-        while (left > 0) {
-          const uint32_t half = (left + 1) / 2;
-          if (L.st[k + half] <= q) {
-            k += half;
-            left -= half;
-          } else {
-            left = half - 1;
-          }
-        }
-        return k;
-      };
-      if constexpr (kPair) {
-        // two consecutive positions per lane and entry step: one search per
-        // pair (a second only where a run ends between them), one 8-B store
-        // where both are copied — half the search work and the stores per
-        // entry (the window base is even, so pairs are 8-B aligned)
-        constexpr int kP = kCU / 2;
-        for (uint32_t base = q0 & ~1u; base < q1; base += kWave * kCU) {
-          uint32_t sa0[kP], sa1[kP];
-          bool in0[kP], in1[kP];
-#pragma unroll
-          for (int u = 0; u < kP; u++) {
-            const uint32_t q = base + u * 2 * kWave + 2 * lane, qq = q + 1;
-            const uint32_t k = find(q);
-            const uint32_t sk = L.st[k], ek = L.en[k];
-            in0[u] = q >= q0 && q < q1 && q >= sk && q < ek;
-            uint32_t k1 = k, sk1 = sk, ek1 = ek;
-            if (qq >= ek) {  // a run ends at q: q + 1 is the next descriptor's, if any
-              k1 = find(qq);
-              sk1 = L.st[k1], ek1 = L.en[k1];
-            }
-            in1[u] = qq >= q0 && qq < q1 && qq >= sk1 && qq < ek1;
-            sa0[u] = in0[u] ? L.src[k] + (q - sk) : 0u;
-            sa1[u] = in1[u] ? L.src[k1] + (qq - sk1) : 0u;
-          }
-          uint32_t v0[kP], v1[kP];
-#pragma unroll
-          for (int u = 0; u < kP; u++) {
-            v0[u] = __builtin_amdgcn_raw_buffer_load_b32(words, (int)(sa0[u] * 4u), 0, 0);
-            v1[u] = __builtin_amdgcn_raw_buffer_load_b32(words, (int)(sa1[u] * 4u), 0, 0);
-          }
-#pragma unroll
-          for (int u = 0; u < kP; u++) {
-            const uint64_t p = g0 + base + u * 2 * kWave + 2 * lane;
-            if (in0[u] && in1[u]) {
-              if (p + 2 <= cap)
-                *reinterpret_cast<uint2 *>(out + p) = make_uint2(v0[u], v1[u]);
-              else
-                atomicOr(oob, kOobStore);
-            } else {
-              if (in0[u]) {
-                if (p < cap)
-                  out[p] = v0[u];
-                else
-                  atomicOr(oob, kOobStore);
-              }
-              if (in1[u]) {
-                if (p + 1 < cap)
-                  out[p + 1] = v1[u];
-                else
-                  atomicOr(oob, kOobStore);
-              }
-            }
-          }
-        }
-      } else {
       for (uint32_t base = q0; base < q1; base += kWave * kCU) {
         uint32_t sa[kCU];
         bool in[kCU];
 #pragma unroll
         for (int u = 0; u < kCU; u++) {
           const uint32_t q = base + u * kWave + lane;
-          const uint32_t k = find(q);
+          // the last descriptor starting at or before q: within [blk[b], blk[b + 1]]
+          const uint32_t bq = min(q, (uint32_t)kWin - 1) / kWave;
+          uint32_t k = L.blk[bq], left = (bq + 1 < kWin / kWave ? L.blk[bq + 1] : kWave - 1) - k;
+          while (left > 0) {
+            const uint32_t half = (left + 1) / 2;
+            if (L.st[k + half] <= q) {
+              k += half;
+              left -= half;
+            } else {
+              left = half - 1;
+            }
+          }
           in[u] = q < q1 && q >= L.st[k] && q < L.en[k];
           sa[u] = in[u] ? L.src[k] + (q - L.st[k]) : 0u;
         }
@@ -926,7 +866,6 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
           else
             atomicOr(oob, kOobStore);
         }
-      }
       }
       wave_lds_sync();
       pos = bend;
@@ -2301,13 +2240,8 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
                            dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nd_grid + 255) / 256, 8192))),
                            dim3(256), 0, st, desc, desc_start + n, desc_cap, o.dstart + n, win, win_cap, &o.ctr->oob);
         HIP_TRY(hipGetLastError());
-        static const bool cpair = getenv("MQM_COPY_PAIR") && atoi(getenv("MQM_COPY_PAIR"));  // A/B (temporary)
-        if (cpair)
-          hipLaunchKernelGGL(k_wincopy<true>, grid(k_wincopy<true>), dim3(kWave * kEmitWaves), 0, st, s, desc,
-                             desc_start + n, desc_cap, win, win_cap, o.dstart + n, o.dout, o.dcap, &o.ctr->oob);
-        else
-          hipLaunchKernelGGL(k_wincopy<false>, grid(k_wincopy<false>), dim3(kWave * kEmitWaves), 0, st, s, desc,
-                             desc_start + n, desc_cap, win, win_cap, o.dstart + n, o.dout, o.dcap, &o.ctr->oob);
+        hipLaunchKernelGGL(k_wincopy, grid(k_wincopy), dim3(kWave * kEmitWaves), 0, st, s, desc, desc_start + n,
+                           desc_cap, win, win_cap, o.dstart + n, o.dout, o.dcap, &o.ctr->oob);
         HIP_TRY(hipGetLastError());
       }
     }

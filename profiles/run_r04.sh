@@ -101,10 +101,6 @@ for step in "$@"; do
     c4counters) bash profiles/run_pmc_r02.sh $TAG/pmc_c4 --config 4 --shard 0/8 > $OUT/pmc_c4.log 2>&1 &&
              python3 profiles/derive_counters.py $OUT/pmc_c4 --json $OUT/c4_counters.json > $OUT/c4_counters.txt &&
              python3 profiles/pmc_to_traffic.py $OUT/pmc_c4 > $OUT/traffic_c4.json ;;
-    abpair) for V in 0 1 0 1; do MQM_COPY_PAIR=$V timeout -k 10 400 python3 -u bench.py $FAST --pipeline 0 \
-             >> $OUT/bench_fast_pair$V.jsonl 2>> $OUT/bench_fast_pair$V.log || exit 1; done
-           for V in 0 1; do MQM_COPY_PAIR=$V timeout -k 10 600 python3 -u bench.py --config 4 --shard 0/8 $FAST \
-             --pipeline 0 > $OUT/bench_c4_fast_pair$V.json 2> $OUT/bench_c4_fast_pair$V.log || exit 1; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
