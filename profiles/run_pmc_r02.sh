@@ -11,7 +11,7 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-ARGS="--steps 2 --warmup 1 --no-cpu-baseline --host-topics 0 --latency-topics 0 $*"
+ARGS="--steps 2 --warmup 1 --no-cpu-baseline --host-topics 0 --latency-topics 0 --steady-steps 0 --pipeline 0 $*"
 timeout -s KILL 120 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
 PASSES=(
   "FETCH_SIZE"
