@@ -64,13 +64,6 @@ for step in "$@"; do
              2> $OUT/bench_fast_pipe$P.log || exit 1; done ;;
     par) timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_gpu_queued.py -m gpu --timeout 300 \
              > $OUT/pytest_par.log 2>&1 ;;
-    profser) (cd /tmp && export TMPDIR=/tmp MQM_NO_OVERLAP=1 && timeout -k 10 500 rocprofv3 --kernel-trace --stats \
-             --output-format csv -d $OUT/profser -o prof -- python3 $ROOT/bench.py $FAST \
-             > $OUT/bench_under_rocprof_serial.json 2> $OUT/rocprof_serial.log) ;;
-    c4profser) (cd /tmp && export TMPDIR=/tmp MQM_NO_OVERLAP=1 && timeout -k 10 500 rocprofv3 --kernel-trace --stats \
-             --output-format csv -d $OUT/prof_c4ser -o prof -- python3 $ROOT/bench.py --config 4 --shard 0/8 --steps 3 \
-             --warmup 1 --no-cpu-baseline --host-topics 0 --latency-topics 0 --steady-steps 0 \
-             > $OUT/c4_under_rocprof_serial.json 2> $OUT/rocprof_c4ser.log) ;;
     calib) timeout -k 10 120 tools/_build/calib_fetch > $OUT/calib_kernels.txt 2>&1 ;;
     smoke) timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 ;;
     bench) timeout -k 10 600 python3 -u bench.py > $OUT/bench.json 2> $OUT/bench.log ;;
