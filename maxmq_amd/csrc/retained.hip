@@ -190,22 +190,6 @@ __device__ bool rev_group(const DeviceRetained &r, const uint8_t *tok_pool, cons
 
 // first j in [lo, hi) with inv[j].x >= key (parents are sorted within a group)
 __device__ __forceinline__ uint32_t inv_lower(const uint2 *inv, uint32_t lo, uint32_t hi, uint32_t key) {
-  // 8-ary steps first: 7 independent probes per step (one round trip) cut the
-  // dependent loads of a search over a large group ~3x; the answer stays in
-  // [lo, hi] throughout (hi: the first entry >= key, or the end)
-  while (hi - lo > 8) {
-    const uint32_t step = (hi - lo) / 8;
-    uint32_t v[7];
-#pragma unroll
-    for (int j = 0; j < 7; j++) v[j] = inv[lo + step * (uint32_t)(j + 1)].x;
-    uint32_t cnt = 0;  // probes below key: a prefix (the group is sorted)
-#pragma unroll
-    for (int j = 0; j < 7; j++) cnt += v[j] < key ? 1u : 0u;
-    const uint32_t nlo = cnt ? lo + step * cnt + 1 : lo;
-    const uint32_t nhi = cnt < 7 ? lo + step * (cnt + 1) : hi;
-    lo = nlo;
-    hi = nhi;
-  }
   while (lo < hi) {
     const uint32_t mid = lo + (hi - lo) / 2;
     if (inv[mid].x < key)
