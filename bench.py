@@ -89,6 +89,9 @@ def parse():
                          "mqm_match_device call per step")
     ap.add_argument("--steady-steps", type=int, default=20,
                     help="steady-state leg: batches queued back to back on two contexts (0 = skip)")
+    ap.add_argument("--ident-steps", type=int, default=3,
+                    help="Identifiers leg (the drop-in's MQM_CFG_IDENTIFIERS configuration): blocking batches "
+                         "with and without the Identifiers pass; 0 = skip")
     ap.add_argument("--latency-topics", type=int, default=2000,
                     help="single-topic mqm_subscribers calls timed for the per-publish latency; 0 = skip")
     ap.add_argument("--conc-threads", type=int, default=64,
@@ -445,6 +448,7 @@ def main():
         steady = steady_state(idx, tb, to, n, dev, args) if world == 1 and not shard_of and args.steady_steps else None
         gproxy = gather_proxy(idx, tb, to, n, dev, args, shard_of[1]) if world == 1 and shard_of else None
         lat = latency(idx, w, args) if args.latency_topics and world == 1 else None
+        ident = identifiers_leg(idx, tb, to, n, dev, args) if args.ident_steps and world == 1 else None
         if not args.no_cpu_baseline:
             if world == 1:
                 cpu, stats = cpu_baseline(w, args)
@@ -507,6 +511,7 @@ def main():
                             "with_every_delivery_read": host["legs"]["iterate"]["value"]} if host else None),
             "steady_state": steady,
             "single_topic_latency": lat,
+            "identifiers": ident,
         }
         print(json.dumps(out), flush=True)
     for c in pipe.get("ctxs", []):
@@ -514,6 +519,43 @@ def main():
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def identifiers_leg(idx, tb, to, n, dev, args):
+    """The drop-in's real configuration: the Go shim creates its index with
+    MQM_CFG_IDENTIFIERS, because Subscription.Merge always
+    builds the Identifiers map (packets.go:250-259).  --ident-steps blocking
+    batches of the same 10M topics, each mqm_match_device followed by
+    mqm_identifiers_device (k_ident over the walk's records), against the same
+    number of blocking batches without it; inputs resident in HBM."""
+    import torch
+
+    stream = torch.cuda.current_stream(dev)
+
+    def timed(with_ids):
+        idx.match_device(tb.data_ptr(), to.data_ptr(), n, stream.cuda_stream)  # warm
+        if with_ids:
+            idx.identifiers_device(stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        t_ids, nid = 0.0, 0
+        t0 = time.perf_counter()
+        for _ in range(args.ident_steps):
+            idx.match_device(tb.data_ptr(), to.data_ptr(), n, stream.cuda_stream)
+            if with_ids:
+                t1 = time.perf_counter()
+                d = idx.identifiers_device(stream.cuda_stream)  # (synchronises: it reads the total back)
+                t_ids += time.perf_counter() - t1
+                nid = int(d.n_idents)
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) / args.ident_steps, t_ids / args.ident_steps, nid
+
+    plain, _, _ = timed(False)
+    both, ids, nid = timed(True)
+    return {"value": n / both, "unit": "topics/s", "ms_per_step": both * 1e3, "match_only_ms_per_step": plain * 1e3,
+            "identifiers_pass_ms": ids * 1e3, "identifiers_share_of_step": ids / both,
+            "listed_sids_per_topic": nid / n,
+            "what": "blocking mqm_match_device + mqm_identifiers_device per 10M-topic batch (the shim's "
+                    "MQM_CFG_IDENTIFIERS configuration), vs blocking mqm_match_device alone"}
 
 
 def steady_state(idx, tb, to, n, dev, args):

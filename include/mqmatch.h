@@ -285,6 +285,8 @@ int mqm_batching_policy(mqm_index *h, uint32_t max_batch, uint32_t linger_us);
  * statistics: calls served in the ring, calls that took the batch path, server
  * launches.  MQM_EINVAL on a host-only index (or for stats while off). */
 int mqm_serve_policy(mqm_index *h, uint32_t grid, uint32_t idle_us);
+/* (grid is capped at half the device's CUs: a server under steady traffic
+ * never idles out, and batch-path calls need the rest of the device) */
 int mqm_serve_stats(mqm_index *h, uint64_t *served, uint64_t *fallbacks, uint64_t *launches);
 /* mean device time per served call (us[4]): claim to published result, then
  * its phases: topic staged + level keys, trie walk, emission + publish */
@@ -329,11 +331,15 @@ int mqm_match_ctx_stats(mqm_match_ctx *ctx, uint64_t *requeued);
  * first.Identifier} (kept even when 0) plus {n.Filter: n.Identifier} for
  * every other subscription n of the client gathered for the topic with
  * n.Identifier > 0 (server.go:805-810 turns it into the PUBLISH's
- * subscription identifiers).  This pass returns, per topic, the sids of the
- * gathered non-shared subscriptions with Identifier > 0 (a subscription
- * gathered twice — a '#' node reached by the parent probe and by '#' — may
- * repeat); the map of delivery (topic, client) is {filter(first): ident(first)}
- * plus {filter(s): ident(s)} for the listed s whose client is that client
+ * subscription identifiers).  This pass returns, per topic, sids of gathered
+ * non-shared subscriptions with Identifier > 0: at least every such
+ * subscription of a client with more than one subscription in the topic's
+ * gather (a subscription gathered twice — a '#' node reached by the parent
+ * probe and by '#' — may repeat).  A client with one gathered subscription
+ * gets the map {filter(first): ident(first)} alone, so its sid adds nothing
+ * and the batch pipeline does not list it (the per-publish paths may).  The
+ * map of delivery (topic, client) is {filter(first): ident(first)} plus
+ * {filter(s): ident(s)} for the listed s whose client is that client
  * (resolve with mqm_result_sub_info).  Device form: for the last
  * mqm_match_device call on the index, whose topic buffers must still hold the
  * batch, against the snapshot that call read; MQM_EINVAL if there was none. */
@@ -432,6 +438,12 @@ int mqm_messages_device(mqm_index *h, const uint8_t *d_filter_bytes, const uint6
 
 /* ---- result accessors --------------------------------------------------- */
 uint32_t mqm_result_num_topics(const mqm_result *r);
+/* the store version (mqm_commit_state.store_version) of the snapshot the
+ * result was matched on: every mutation counted up to that version is in the
+ * result, none after it.  The reference matches its live trie
+ * (topics.go:484-518); a drop-in caller that needs to know which mutations a
+ * result reflects reads this.  0 for NULL. */
+uint64_t mqm_result_snapshot_version(const mqm_result *r);
 const uint64_t *mqm_result_offsets(const mqm_result *r);          /* n + 1          */
 const mqm_delivery *mqm_result_deliveries(const mqm_result *r); /* NULL for a packed result */
 const uint32_t *mqm_result_packed(const mqm_result *r);         /* packed words (mqm_match_batch_packed;

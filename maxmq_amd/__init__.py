@@ -99,6 +99,8 @@ class BatchResult:
         self._h = handle
         n = L.mqm_result_num_topics(handle)
         self.n = n
+        # the store version of the snapshot it was matched on (mqm_result_snapshot_version)
+        self.snapshot_version = int(L.mqm_result_snapshot_version(handle))
 
         def arr(ptr, count, dtype):
             if count == 0 or not ptr:

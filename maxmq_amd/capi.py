@@ -50,6 +50,7 @@ EXPORTED = [
     "mqm_match_device_async", "mqm_match_ctx_wait", "mqm_match_ctx_stats", "mqm_match_batch_packed",
     "mqm_result_packed", "mqm_match_batch_runs", "mqm_result_runs", "mqm_result_expand",
     "mqm_serve_policy", "mqm_serve_stats", "mqm_serve_device_us", "mqm_serve_host_us",
+    "mqm_result_snapshot_version",
 ]
 
 
@@ -162,6 +163,7 @@ def lib():
         "mqm_batching_stats": ([vp, C.POINTER(u64), C.POINTER(u64)], C.c_int),
         "mqm_match_device": ([vp, vp, vp, u32, vp, C.POINTER(DeviceResult)], C.c_int),
         "mqm_result_num_topics": ([vp], u32),
+        "mqm_result_snapshot_version": ([vp], u64),
         "mqm_result_offsets": ([vp], vp),
         "mqm_result_deliveries": ([vp], vp),
         "mqm_result_shared_offsets": ([vp], vp),

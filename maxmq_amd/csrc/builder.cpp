@@ -135,6 +135,7 @@ bool Builder::take(BuiltSnapshot *out) {
   *out = std::move(ready_);
   ready_ = BuiltSnapshot();
   has_ready_ = false;
+  ready_flag_.store(false, std::memory_order_release);
   return true;
 }
 
@@ -194,6 +195,7 @@ void Builder::run() {
         log.replay(shadow_);
         replayed = true;
         auto hs = std::make_shared<HostSnapshot>();
+        hs->version = version;
         rc = fault == 2 ? MQM_ENOMEM : flatten(shadow_, hs.get());
         if (rc == MQM_OK && device_ >= 0 && !stream_) rc = MQM_EHIP;
         if (rc == MQM_OK) rc = fault == 3 ? MQM_ENOMEM : upload(std::move(hs), device_, stream_, &b.snap);
@@ -212,6 +214,7 @@ void Builder::run() {
       if (rc == MQM_OK) {
         ready_ = std::move(b);  // replaces an unpublished older build
         has_ready_ = true;
+        ready_flag_.store(true, std::memory_order_release);
         dirty_ = false;
         shadow_bad_ = false;
       } else {

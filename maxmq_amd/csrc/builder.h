@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <cstdint>
 #include <memory>
@@ -92,6 +93,8 @@ class Builder {
   void inject_fault(int stage, int count);
   // the newest finished snapshot, if any (older unpublished ones are dropped)
   bool take(BuiltSnapshot *out);
+  // take() would return a snapshot (no lock: the per-publish path checks it per call)
+  bool has_ready() const { return ready_flag_.load(std::memory_order_acquire); }
   // block until every submitted log is built; returns the first build error
   int wait_idle();
   bool busy();
@@ -109,6 +112,7 @@ class Builder {
   bool has_queued_ = false, working_ = false, stop_ = false;
   bool dirty_ = false, shadow_bad_ = false;
   bool has_ready_ = false;
+  std::atomic<bool> ready_flag_{false};  // has_ready_, readable without mu_
   BuiltSnapshot ready_;
   int err_ = 0;
   int fault_stage_ = 0, fault_count_ = 0;

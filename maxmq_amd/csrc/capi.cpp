@@ -133,6 +133,8 @@ struct mqm_index {
   // that turns them into the back buffer (builder.h)
   DeltaLog journal;
   std::unique_ptr<Builder> builder;
+  std::atomic<Builder *> builder_pub{nullptr};  // builder.get(), readable without mu (front_fast)
+  std::atomic<int64_t> submit_due_ns{0};        // policy_ms: when the logged mutations are due (0: none)
   uint64_t policy_ops = 0;               // auto-submit after this many logged mutations (0 = off)
   uint32_t policy_ms = 0;                // ... or when the oldest one is this old (0 = off)
   std::chrono::steady_clock::time_point journal_t0;
@@ -232,18 +234,33 @@ int install(mqm_index *h, std::shared_ptr<GpuSnapshot> g, uint64_t version) {
   return MQM_OK;
 }
 
+int64_t steady_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+// the index's builder, created on first use (mu held)
+Builder *builder_locked(mqm_index *h) {
+  if (!h->builder) {
+    h->builder = std::make_unique<Builder>(h->cfg.device);
+    h->builder_pub.store(h->builder.get(), std::memory_order_release);
+  }
+  return h->builder.get();
+}
+
 // hand the journal to the builder (MQM_CFG_ASYNC_COMMIT); after a replay that
 // failed part-way the builder gets a full copy of the store instead
 void submit_locked(mqm_index *h) {
   // the builder starts empty: the journal of an async index holds every
   // mutation since mqm_create
-  if (!h->builder) h->builder = std::make_unique<Builder>(h->cfg.device);
+  builder_locked(h);
   if (h->builder->shadow_bad())
     h->builder->submit_full(h->store, h->store.version());
   else
     h->builder->submit(std::move(h->journal), h->store.version());
   h->journal.clear();
   h->journal_t0 = std::chrono::steady_clock::now();
+  h->submit_due_ns.store(0, std::memory_order_relaxed);
 }
 
 // publish the builder's newest finished snapshot, if any
@@ -263,8 +280,13 @@ int publish_locked(mqm_index *h, int *published) {
 void maybe_submit(mqm_index *h) {
   if (!h->async() || h->journal.empty()) return;
   if (h->policy_ops && h->journal.size() >= h->policy_ops) return submit_locked(h);
-  if (h->policy_ms && std::chrono::steady_clock::now() - h->journal_t0 >= std::chrono::milliseconds(h->policy_ms))
-    submit_locked(h);
+  if (h->policy_ms) {
+    const auto due = h->journal_t0 + std::chrono::milliseconds(h->policy_ms);
+    if (std::chrono::steady_clock::now() >= due) return submit_locked(h);
+    // (front_fast submits when this passes without another mutation)
+    h->submit_due_ns.store(std::chrono::duration_cast<std::chrono::nanoseconds>(due.time_since_epoch()).count(),
+                           std::memory_order_relaxed);
+  }
 }
 
 int commit_locked(mqm_index *h) {
@@ -283,6 +305,7 @@ int commit_locked(mqm_index *h) {
     return h->snap && h->snap_version == h->store.version() ? MQM_OK : MQM_EINVAL;
   }
   auto hs = std::make_shared<HostSnapshot>();
+  hs->version = h->store.version();
   int rc = flatten(h->store, hs.get());
   if (rc != MQM_OK) return rc;
   std::unique_ptr<GpuSnapshot> g;
@@ -310,15 +333,29 @@ int front(mqm_index *h, std::shared_ptr<GpuSnapshot> *out) {
   return MQM_OK;
 }
 
-// front() without the index lock, when nothing is to commit or publish: an
-// index without MQM_CFG_ASYNC_COMMIT whose front buffer exists and (with
-// MQM_CFG_AUTOCOMMIT) reflects the store's current version.  false: take
-// front().  (The per-publish server's callers: 64 of them on mu queue up.)
+// front() without waiting for the index lock (the per-publish server's
+// callers: 64 of them on mu queue up behind every mutation).  The front buffer
+// is returned when it exists and, with MQM_CFG_AUTOCOMMIT, reflects the
+// store's current version; false: take front() (it commits first).  With
+// MQM_CFG_ASYNC_COMMIT and no autocommit a finished build is published (or a
+// due policy submit made) by whichever caller gets the lock without waiting;
+// the others match the current front buffer meanwhile.
 bool front_fast(mqm_index *h, std::shared_ptr<GpuSnapshot> *out) {
-  if (h->async()) return false;
+  const bool autoc = (h->cfg.flags & MQM_CFG_AUTOCOMMIT) != 0;
+  if (h->async() && !autoc) {
+    const Builder *b = h->builder_pub.load(std::memory_order_acquire);
+    const int64_t due = h->submit_due_ns.load(std::memory_order_relaxed);
+    if ((b && b->has_ready()) || (due && steady_ns() >= due)) {
+      std::unique_lock<std::mutex> g(h->mu, std::try_to_lock);
+      if (g.owns_lock()) {
+        maybe_submit(h);
+        (void)publish_locked(h, nullptr);
+      }
+    }
+  }
   std::shared_lock<std::shared_mutex> r(h->snap_rw);
   if (!h->snap) return false;
-  if ((h->cfg.flags & MQM_CFG_AUTOCOMMIT) && h->snap_version != h->store.version()) return false;
+  if (autoc && h->snap_version != h->store.version()) return false;
   *out = h->snap;
   return true;
 }
@@ -554,6 +591,7 @@ int mqm_destroy(mqm_index *h) {
   if (h->live_ctxs.load(std::memory_order_acquire) != 0) return MQM_EINVAL;
   h->stop_server();     // first: its kernel reads the snapshot
   h->stop_collector();  // its thread matches (and may commit) through this index
+  h->builder_pub.store(nullptr, std::memory_order_release);
   h->builder.reset();    // finishes a running build and joins the worker
   if (h->cfg.device != MQM_DEVICE_NONE) {
     (void)hipSetDevice(h->cfg.device);
@@ -567,8 +605,7 @@ int mqm_debug_fault(mqm_index *h, int stage, int count) {
   if (!h || stage < 1 || stage > 3 || count < 0) return MQM_EINVAL;
   std::lock_guard<std::mutex> g(h->mu);
   if (!h->async()) return MQM_EINVAL;
-  if (!h->builder) h->builder = std::make_unique<Builder>(h->cfg.device);
-  h->builder->inject_fault(stage, count);
+  builder_locked(h)->inject_fault(stage, count);
   return MQM_OK;
 }
 
@@ -1396,27 +1433,45 @@ struct Collector {
 };
 
 // MQM_CFG_SERVE: the persistent per-publish server (fast.hip k_serve).
+//
+// Snapshots: every launch serves one snapshot and writes its version into
+// each slot it answers; the caller decodes the result's sids with the host
+// snapshot of that version (the last kHist launches' are kept), never with a
+// snapshot it merely read before posting.  The server only ever moves to a
+// newer snapshot (a caller holding an older front buffer does not relaunch
+// it), and a caller posts only once the running launch's snapshot is at least
+// as new as its own front buffer, so a result never predates the caller's
+// view of the store (MQM_CFG_AUTOCOMMIT: read-your-writes).
 struct Server {
   mqm_index *h;
-  ServeQueue *q = nullptr;                // pinned, coherent, device-mapped
-  unsigned long long *claimed = nullptr;  // device: the next request number a workgroup takes
-  unsigned long long claim_from = 0;      // (mu) its value at the last launch
+  ServeQueue *q = nullptr;            // pinned, coherent, device-mapped
+  unsigned long long *ctr = nullptr;  // device: [0] the next request number a workgroup takes, [1] exited workgroups
   hipStream_t st = nullptr;
-  std::mutex mu;                          // launches / snapshot switches
-  std::shared_ptr<GpuSnapshot> snap;      // what the running kernel reads
-  bool launched = false;                  // (mu) a launch may still run
+  std::mutex mu;                      // launches / snapshot switches
+  std::shared_ptr<GpuSnapshot> snap;  // (mu) what the running launch reads
+  bool launched = false;              // (mu) a launch may still run
+  uint64_t gen = 0;                   // (mu) launches so far = the running launch's generation
   uint32_t grid = 32, idle_us = 20000;
+  uint32_t max_grid = 128;            // half the device's CUs (init): batch-path kernels keep the rest
   const bool want_ids;
+  // the running launch, readable without mu: generation, snapshot version + 1 (0: none)
+  std::atomic<uint64_t> run_gen{0}, run_ver{0};
+  // host snapshots of the last kHist launches (decoding a result whose launch
+  // served a snapshot other than the caller's front buffer)
+  static constexpr uint32_t kHist = 8;
+  std::mutex hist_mu;
+  std::shared_ptr<const HostSnapshot> hist[kHist];
+  uint32_t hist_next = 0;
   std::atomic<uint64_t> ticket{0};
-  std::unique_ptr<std::atomic<uint64_t>[]> free_seq;  // slot i takes request k once free_seq[i] == k
-  std::atomic<uint64_t> served{0}, fallbacks{0}, launches{0};
+  std::unique_ptr<std::atomic<uint64_t>[]> free_seq;   // slot i takes request k once free_seq[i] == k
+  std::unique_ptr<std::atomic<uint64_t>[]> abandoned;  // slot i: k + 1 of a posted request whose caller gave up
+  std::atomic<uint64_t> served{0}, fallbacks{0}, launches{0}, stale{0};
   std::atomic<uint64_t> device_ticks{0};  // claim -> publish on the device, summed (100 MHz ticks)
   std::atomic<uint64_t> phase_ticks[3] = {};  // stage + keys, walk, emission + publish
   std::atomic<uint64_t> timed{0};
   // host-side time per call (ns, summed; mqm_serve_host_us reads and resets):
   // entry -> posted, posted -> result seen, result seen -> returned; calls that slept
   std::atomic<uint64_t> host_ns[3] = {}, host_calls{0}, host_slept{0};
-  std::atomic<bool> live{false};                   // launched (may have exited idle since)
   // completion pollers: callers that stopped spinning sleep on waitw[slot];
   // poller p watches the done words of the sleepers on slots i = p mod
   // n_pollers and wakes them (one thread's FUTEX_WAKE calls cap the wake rate
@@ -1459,28 +1514,32 @@ struct Server {
       __builtin_ia32_pause();
     }
   }
-  std::atomic<const GpuSnapshot *> running_on{nullptr};
 
   explicit Server(mqm_index *idx) : h(idx), want_ids((idx->cfg.flags & MQM_CFG_IDENTIFIERS) != 0) {
     free_seq.reset(new std::atomic<uint64_t>[kServeSlots]);
+    abandoned.reset(new std::atomic<uint64_t>[kServeSlots]);
     waiting.reset(new std::atomic<uint64_t>[kServeSlots]);
     waitw.reset(new std::atomic<uint32_t>[kServeSlots]);
     for (uint32_t i = 0; i < kServeSlots; i++) {
       free_seq[i].store(i);
+      abandoned[i].store(0);
       waiting[i].store(0);
       waitw[i].store(0);
     }
   }
   int init() {
     if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->cfg.device) == hipSuccess && cus > 1)
+      max_grid = (uint32_t)cus / 2;
     void *p = nullptr;
     if (hipHostMalloc(&p, sizeof(ServeQueue), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
       return MQM_ENOMEM;
     q = static_cast<ServeQueue *>(p);
     memset((void *)q, 0, sizeof(ServeQueue));
-    if (hipMalloc(&claimed, sizeof(unsigned long long)) != hipSuccess) return MQM_ENOMEM;
+    if (hipMalloc(&ctr, 2 * sizeof(unsigned long long)) != hipSuccess) return MQM_ENOMEM;
     if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return MQM_EHIP;
-    if (hipMemsetAsync(claimed, 0, sizeof(unsigned long long), st) != hipSuccess ||
+    if (hipMemsetAsync(ctr, 0, 2 * sizeof(unsigned long long), st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
       return MQM_EHIP;
     for (uint32_t p = 0; p < n_pollers; p++) pollers[p].th = std::thread([this, p] { poll_loop(p); });
@@ -1488,12 +1547,12 @@ struct Server {
   }
   // (mu held) stop a running kernel and wait for it
   void halt() {
+    run_ver.store(0, std::memory_order_release);
     if (!launched) return;
     __atomic_store_n(&q->stop, 1ull, __ATOMIC_SEQ_CST);
     (void)hipStreamSynchronize(st);
     __atomic_store_n(&q->stop, 0ull, __ATOMIC_SEQ_CST);
     launched = false;
-    live.store(false, std::memory_order_release);
   }
   ~Server() {
     poller_quit.store(true, std::memory_order_release);
@@ -1507,33 +1566,78 @@ struct Server {
       halt();
     }
     if (st) (void)hipStreamDestroy(st);
-    if (claimed) (void)hipFree(claimed);
+    if (ctr) (void)hipFree(ctr);
     if (q) (void)hipHostFree(q);
   }
-  // the kernel runs on `cur` (mu held): relaunch when it has exited (idle) or
-  // the snapshot it reads is not the current one
+  // the running launch's last workgroup has exited (idle): a posted request
+  // waits for a relaunch
+  bool exited() const {
+    return __atomic_load_n(&q->exited, __ATOMIC_ACQUIRE) == run_gen.load(std::memory_order_acquire);
+  }
+  // (mu held) a launch runs on a snapshot at least as new as `cur`: relaunch
+  // when the server has exited or reads an older one.  Never moves back to an
+  // older snapshot than the one it has run (a caller may hold a stale front
+  // buffer: it then gets the newer snapshot's result, and decodes with it).
   int ensure(const std::shared_ptr<GpuSnapshot> &cur) {
-    if (launched && snap == cur && hipStreamQuery(st) == hipErrorNotReady) return MQM_OK;
+    std::shared_ptr<GpuSnapshot> want = snap && snap->host->version >= cur->host->version ? snap : cur;
+    if (launched && want == snap && !exited() && hipStreamQuery(st) == hipErrorNotReady) return MQM_OK;
     halt();
-    snap = cur;
+    snap = std::move(want);
     if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
     // (no kernel runs now) the device counter restarts at the first request
     // not yet served: a stopped kernel may have taken numbers past it
     const uint64_t T = ticket.load(std::memory_order_acquire);
-    claim_from = T;
+    unsigned long long c[2] = {T, 0};
     for (uint64_t k = T > kServeSlots ? T - kServeSlots : 0; k < T; k++)
       if (__atomic_load_n(&q->done[k % kServeSlots], __ATOMIC_ACQUIRE) < k + 1) {
-        claim_from = k;
+        c[0] = k;
         break;
       }
-    if (hipMemcpyAsync(claimed, &claim_from, sizeof(claim_from), hipMemcpyHostToDevice, st) != hipSuccess)
-      return MQM_EHIP;
-    if (serve_launch(snap->dev, q, claimed, grid, idle_us, want_ids, st) != 0) return MQM_EHIP;
+    if (hipMemcpyAsync(ctr, c, sizeof(c), hipMemcpyHostToDevice, st) != hipSuccess) return MQM_EHIP;
+    const uint64_t ver = snap->host->version;
+    if (serve_launch(snap->dev, q, ctr, grid, idle_us, want_ids, ver, gen + 1, st) != 0) return MQM_EHIP;
+    gen++;
     launched = true;
     launches++;
-    running_on.store(snap.get(), std::memory_order_release);
-    live.store(true, std::memory_order_release);
+    {
+      std::lock_guard<std::mutex> g(hist_mu);
+      const uint32_t last = (hist_next + kHist - 1) % kHist;
+      if (!hist[last] || hist[last]->version != ver) {
+        hist[hist_next] = snap->host;
+        hist_next = (hist_next + 1) % kHist;
+      }
+    }
+    run_gen.store(gen, std::memory_order_release);
+    run_ver.store(ver + 1, std::memory_order_release);
     return MQM_OK;
+  }
+  // the host snapshot a launch of version `ver` served (nullptr: no longer kept)
+  std::shared_ptr<const HostSnapshot> host_of(uint64_t ver, const std::shared_ptr<GpuSnapshot> &cur) {
+    if (cur->host->version == ver) return cur->host;
+    std::lock_guard<std::mutex> g(hist_mu);
+    for (const auto &x : hist)
+      if (x && x->version == ver) return x;
+    return nullptr;
+  }
+  // a caller that posted request k gives up on it: the slot goes to its next
+  // owner once the late result has arrived (wait_slot)
+  void abandon(uint32_t i, uint64_t k) { abandoned[i].store(k + 1, std::memory_order_release); }
+  // wait until slot i may take request k (its previous request's caller has
+  // read the result, or gave up on it and the result has arrived)
+  bool wait_slot(uint32_t i, uint64_t k) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0;; spin++) {
+      const uint64_t f = free_seq[i].load(std::memory_order_acquire);
+      if (f == k) return true;
+      if (k >= kServeSlots && f == k - kServeSlots && abandoned[i].load(std::memory_order_acquire) == f + 1 &&
+          __atomic_load_n(&q->done[i], __ATOMIC_ACQUIRE) == f + 1) {
+        abandoned[i].store(0, std::memory_order_relaxed);
+        free_seq[i].store(k, std::memory_order_release);
+        return true;
+      }
+      if ((spin & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) return false;
+      std::this_thread::yield();
+    }
   }
 
   int submit(const char *topic, size_t len, mqm_result **out) {
@@ -1546,9 +1650,21 @@ struct Server {
     std::shared_ptr<GpuSnapshot> cur;
     int rc = front_fast(h, &cur) ? MQM_OK : front(h, &cur);  // (commits first with MQM_CFG_AUTOCOMMIT)
     if (rc != MQM_OK) return rc;
+    // before posting: the running launch serves a snapshot at least as new as
+    // the caller's (any later launch is newer still)
+    const uint64_t rv = run_ver.load(std::memory_order_acquire);
+    if (rv == 0 || rv - 1 < cur->host->version || exited()) {
+      std::lock_guard<std::mutex> g(mu);
+      if ((rc = ensure(cur)) != MQM_OK) return rc;
+    }
     const uint64_t k = ticket.fetch_add(1, std::memory_order_relaxed);
     const uint32_t i = (uint32_t)(k % kServeSlots);
-    while (free_seq[i].load(std::memory_order_acquire) != k) std::this_thread::yield();  // the slot's previous caller is done
+    if (!wait_slot(i, k)) {
+      // (the slot's previous request never completed: the device is gone.
+      // Request k is never posted, so its slot stays taken as well)
+      fprintf(stderr, "mqmatch: per-publish server: ring slot %u not free after 10 s\n", i);
+      return MQM_EHIP;
+    }
     ServeSlot &sl = q->slot[i];
     memcpy(sl.topic, topic, len);
     sl.len = (uint32_t)len;
@@ -1560,12 +1676,12 @@ struct Server {
     memcpy(head, sl.topic, kServeHead);
     sl.chk = serve_check(seqw, head);
     __atomic_store_n(&sl.seq, seqw, __ATOMIC_RELEASE);
-    // (no HIP call on the common path: the kernel's liveness is checked only
-    // when a result is late, below)
-    if (!live.load(std::memory_order_acquire) || running_on.load(std::memory_order_acquire) != cur.get()) {
+    // the server exited (idle) since the check above: relaunch now rather
+    // than at the liveness check below (no HIP call on the common path)
+    if (exited() || run_ver.load(std::memory_order_acquire) == 0) {
       std::lock_guard<std::mutex> g(mu);
       if ((rc = ensure(cur)) != MQM_OK) {
-        free_seq[i].store(k + kServeSlots, std::memory_order_release);
+        abandon(i, k);
         return rc;
       }
     }
@@ -1591,6 +1707,13 @@ struct Server {
       waiting[i].store(k + 1, std::memory_order_release);
       Poller &pl = pollers[i % n_pollers];
       if (pl.sleepers.fetch_add(1, std::memory_order_acq_rel) == 0) poke_poller(pl);
+      auto give_up = [&](int code) {
+        waiting[i].store(0, std::memory_order_release);
+        pl.sleepers.fetch_sub(1, std::memory_order_acq_rel);
+        inflight.fetch_sub(1, std::memory_order_acq_rel);
+        abandon(i, k);
+        return code;
+      };
       while (__atomic_load_n(&q->done[i], __ATOMIC_ACQUIRE) != k + 1) {
         const struct timespec ts = {0, 500000};  // 500 us (a late result: the liveness check below)
         syscall(SYS_futex, reinterpret_cast<uint32_t *>(&waitw[i]), FUTEX_WAIT_PRIVATE, 0, &ts, nullptr, 0);
@@ -1602,10 +1725,7 @@ struct Server {
         const auto now = clk::now();
         if (now - t0 > std::chrono::seconds(10)) {
           fprintf(stderr, "mqmatch: per-publish server: no result for 10 s\n");
-          waiting[i].store(0, std::memory_order_release);
-          pl.sleepers.fetch_sub(1, std::memory_order_acq_rel);
-          inflight.fetch_sub(1, std::memory_order_acq_rel);
-          return MQM_EHIP;  // (the slot stays taken: its late result is never read)
+          return give_up(MQM_EHIP);
         }
         // one liveness check per 200 us across all late callers (each is a
         // HIP call under mu; 64 callers checking at once cost more CPU than
@@ -1615,12 +1735,7 @@ struct Server {
         if (now - t0 > std::chrono::microseconds(200) && now_ns - last > 200000 &&
             last_check_ns.compare_exchange_strong(last, now_ns, std::memory_order_acq_rel)) {
           std::lock_guard<std::mutex> g(mu);
-          if ((rc = ensure(snap ? snap : cur)) != MQM_OK) {
-            waiting[i].store(0, std::memory_order_release);
-            pl.sleepers.fetch_sub(1, std::memory_order_acq_rel);
-            inflight.fetch_sub(1, std::memory_order_acq_rel);
-            return rc;
-          }
+          if ((rc = ensure(cur)) != MQM_OK) return give_up(rc);
         }
       }
       waiting[i].store(0, std::memory_order_release);
@@ -1629,7 +1744,7 @@ struct Server {
     }
     const auto t_seen = clk::now();
     inflight.fetch_sub(1, std::memory_order_acq_rel);
-    const uint32_t status = sl.status;
+    uint32_t status = sl.status;
     if (sl.t_done > sl.t_claim && sl.t_phase[0] >= sl.t_claim && sl.t_phase[1] >= sl.t_phase[0] &&
         sl.t_done >= sl.t_phase[1]) {
       device_ticks += sl.t_done - sl.t_claim;
@@ -1639,13 +1754,20 @@ struct Server {
       timed++;
     }
     if (status == kServeOk) {
-      try {
-        rc = Collector::single(cur->host, sl.dout, sl.dcount, sl.hout, sl.hcount, want_ids ? sl.iout : nullptr,
-                               want_ids ? sl.icount : 0, want_ids, out);
-      } catch (const std::bad_alloc &) {
-        rc = MQM_ENOMEM;
+      // the sids are positions in the snapshot the launch served
+      std::shared_ptr<const HostSnapshot> hs = host_of(sl.ver, cur);
+      if (!hs) {
+        stale++;
+        status = kServeFallback;
+      } else {
+        try {
+          rc = Collector::single(std::move(hs), sl.dout, sl.dcount, sl.hout, sl.hcount, want_ids ? sl.iout : nullptr,
+                                 want_ids ? sl.icount : 0, want_ids, out);
+        } catch (const std::bad_alloc &) {
+          rc = MQM_ENOMEM;
+        }
+        served++;
       }
-      served++;
     }
     free_seq[i].store(k + kServeSlots, std::memory_order_release);
     host_ns[0] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t0 - t_in).count();
@@ -1739,7 +1861,9 @@ int mqm_serve_policy(mqm_index *h, uint32_t grid, uint32_t idle_us) {
   if (rc != MQM_OK) return rc;
   Server *sv = h->server.load(std::memory_order_acquire);
   std::lock_guard<std::mutex> g(sv->mu);
-  sv->grid = grid ? std::min<uint32_t>(grid, 1024) : 32;
+  // (capped at half the CUs: a persistent grid that never idles out would
+  // otherwise starve the batch-path kernels of fallback calls)
+  sv->grid = std::min<uint32_t>(grid ? grid : 32, sv->max_grid);
   sv->idle_us = idle_us ? idle_us : 20000;
   sv->halt();  // the next call launches with these
   return MQM_OK;
@@ -1787,6 +1911,7 @@ int mqm_batching_stats(mqm_index *h, uint64_t *batches, uint64_t *topics) {
 }
 
 uint32_t mqm_result_num_topics(const mqm_result *r) { return r ? r->n : 0; }
+uint64_t mqm_result_snapshot_version(const mqm_result *r) { return r && r->snap ? r->snap->version : 0; }
 const uint64_t *mqm_result_offsets(const mqm_result *r) { return r ? r->offsets : nullptr; }
 const mqm_delivery *mqm_result_deliveries(const mqm_result *r) { return r ? r->deliveries : nullptr; }
 const uint32_t *mqm_result_packed(const mqm_result *r) { return r ? r->packed : nullptr; }

@@ -494,6 +494,7 @@ struct ServeSink {
   uint32_t *hout;
   uint32_t *iout;
   unsigned long long k;
+  unsigned long long ver;  // the launch's snapshot version, reported with every result
   __device__ bool reserve(FastLds &L, unsigned long long need, uint32_t H) {
     L.dbase = L.hbase = L.ibase = 0;
     if (need > kServeD || H > kServeH || (iout && need > kServeI)) {  // too big for a slot: the pipeline
@@ -507,6 +508,7 @@ struct ServeSink {
     slot->dcount = d;
     slot->hcount = h;
     slot->icount = i;
+    slot->ver = ver;
     slot->t_done = __builtin_amdgcn_s_memrealtime();
     __threadfence_system();  // the result reaches host memory before done
     __hip_atomic_store(done_word, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -516,8 +518,10 @@ struct ServeSink {
   __device__ void done(FastLds &L, uint32_t d, uint32_t h) { publish(kServeOk, d, h, L.nid); }
 };
 
-__global__ __launch_bounds__(kFT) void k_serve(DeviceSnapshot s, ServeQueue *q, unsigned long long *claimed,
-                                               uint64_t idle_ticks, int want_ids) {
+__global__ __launch_bounds__(kFT) void k_serve(DeviceSnapshot s, ServeQueue *q, unsigned long long *ctr,
+                                               uint64_t idle_ticks, int want_ids, unsigned long long ver,
+                                               unsigned long long gen) {
+  unsigned long long *claimed = ctr;  // ctr[1]: workgroups of this launch that have exited
   __shared__ FastLds L;
   __shared__ unsigned long long job;
   __shared__ uint32_t job_len;
@@ -583,10 +587,20 @@ __global__ __launch_bounds__(kFT) void k_serve(DeviceSnapshot s, ServeQueue *q, 
       if (lane == 0) quit = got ? 0 : 1;
     }
     __syncthreads();
-    if (quit) break;
+    if (quit) {
+      // the launch's last workgroup out tells the host (q->exited = gen): a
+      // caller that posts after it relaunches at once instead of waiting for
+      // its liveness check
+      if (tid == 0 && atomicAdd(ctr + 1, 1ull) == (unsigned long long)gridDim.x - 1) {
+        __threadfence_system();
+        __hip_atomic_store(&q->exited, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      break;
+    }
     ServeSlot *slot = &q->slot[job % kServeSlots];
     if (tid == 0) slot->t_claim = __builtin_amdgcn_s_memrealtime();
-    ServeSink sink{slot, &q->done[job % kServeSlots], slot->dout, slot->hout, want_ids ? slot->iout : nullptr, job};
+    ServeSink sink{slot, &q->done[job % kServeSlots], slot->dout, slot->hout, want_ids ? slot->iout : nullptr, job,
+                   ver};
     fast_topic(s, L, reinterpret_cast<const uint8_t *>(slot->topic), min(job_len, kServeTopic + 1), sink, kServeHead);
     __syncthreads();
   }
@@ -628,11 +642,11 @@ FastArena::~FastArena() {
   if (ctl) (void)hipFree(ctl);
 }
 
-int serve_launch(const DeviceSnapshot &s, ServeQueue *q, unsigned long long *claimed, uint32_t grid, uint32_t idle_us,
-                 bool want_ids, hipStream_t st) {
+int serve_launch(const DeviceSnapshot &s, ServeQueue *q, unsigned long long *ctr, uint32_t grid, uint32_t idle_us,
+                 bool want_ids, uint64_t ver, uint64_t gen, hipStream_t st) {
   const uint64_t idle_ticks = (uint64_t)idle_us * 100;  // s_memrealtime: 100 MHz
-  hipLaunchKernelGGL(k_serve, dim3(std::max<uint32_t>(1, grid)), dim3(kFT), 0, st, s, q, claimed, idle_ticks,
-                     want_ids ? 1 : 0);
+  hipLaunchKernelGGL(k_serve, dim3(std::max<uint32_t>(1, grid)), dim3(kFT), 0, st, s, q, ctr, idle_ticks,
+                     want_ids ? 1 : 0, (unsigned long long)ver, (unsigned long long)gen);
   HIP_TRY(hipGetLastError());
   return 0;
 }

@@ -63,6 +63,9 @@ struct HostSnapshot {
   std::vector<RevGroup> rgroups;     // DeviceRetained::groups (empty: no index)
   uint32_t sys_child = kNone;
   bool has_empty = false;
+  // the store version this snapshot reflects (set by the committer before
+  // flatten; equal versions mean equal snapshots: flatten is deterministic)
+  uint64_t version = 0;
 };
 
 // Build the snapshot; returns MQM_OK or MQM_ELIMIT.

@@ -202,6 +202,7 @@ struct alignas(64) ServeSlot {
   char topic[kServeTopic];  // topic bytes (0 .. kServeHead - 1 in line 0)
   uint32_t len, status;     // topic length; kServe* (fallback: the caller runs the batch pipeline)
   uint32_t dcount, hcount, icount, pad;
+  unsigned long long ver;              // the snapshot version the result was matched on (HostSnapshot::version)
   unsigned long long t_claim, t_done;  // device clock (s_memrealtime, 100 MHz): claimed, published
   unsigned long long t_phase[2];       // ... topic staged and keys built, trie walked
   uint64_t dout[kServeD];   // {client, packed} deliveries
@@ -220,18 +221,22 @@ MQM_HD uint32_t serve_check(unsigned long long seq, const unsigned long long *he
   return (uint32_t)(x >> 29);
 }
 struct ServeQueue {
-  unsigned long long stop;  // host: 1 = every workgroup exits
-  unsigned long long pad[7];
+  unsigned long long stop;    // host: 1 = every workgroup exits
+  unsigned long long exited;  // device: the launch generation whose last workgroup has exited
+  unsigned long long pad[6];
   // device: done[i] = k + 1 once request k's result (slot i = k % kServeSlots)
   // is complete — one contiguous 2-KB array, so the host's completion poller
   // scans 32 cache lines rather than a line (and a page) per slot
   unsigned long long done[kServeSlots];
   ServeSlot slot[kServeSlots];
 };
-// launch the server on `st` (q: host-mapped; claimed: the device counter, set
-// by the host before every launch to the first request not yet served)
-int serve_launch(const DeviceSnapshot &s, ServeQueue *q, unsigned long long *claimed, uint32_t grid, uint32_t idle_us,
-                 bool want_ids, hipStream_t st);
+// launch the server on `st` (q: host-mapped; ctr: two device counters, set by
+// the host before every launch: ctr[0] the first request not yet served, ctr[1]
+// = 0 the workgroups that have exited).  `ver` is written into every slot the
+// launch serves (the snapshot's version), `gen` into q->exited by the launch's
+// last workgroup to exit.
+int serve_launch(const DeviceSnapshot &s, ServeQueue *q, unsigned long long *ctr, uint32_t grid, uint32_t idle_us,
+                 bool want_ids, uint64_t ver, uint64_t gen, hipStream_t st);
 
 // Identifiers support for the last match_device call on `ws` (its topic
 // buffers must still hold the batch): per topic, the sids of the gathered

@@ -1604,11 +1604,16 @@ __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *
 
 // ---------------------------------------------------------------------------
 // k_ident<P>: Subscription.Identifiers support (packets.go:250-259).  For every
-// bounded topic, the sids of the gathered non-shared entries whose Identifier
-// is > 0 (kMetaIdent), hit by hit from the walk's record (P0 counts, P1
-// writes at istart).  A node gathered twice repeats its sids; the map the
-// host builds keeps one key per filter, as the reference's does.  DFS topics
-// are handled by k_dfs<3|4>.
+// bounded topic, the sids of the gathered *multi* entries whose Identifier is
+// > 0 (kMetaIdent), part by part from the walk's record (P0 counts, P1 writes
+// at istart).  A solo entry is its client's only subscription in any topic's
+// gather (that is what solo means, flatten.cpp), so its delivery's map is its
+// first pair {Filter: Identifier} alone, which the host already has from the
+// delivery's first sid: listing it would add nothing.  So only the multi
+// parts are read — C3 gathers 233 entries per topic, almost all solo, and
+// reading each one's word cost ~2 KB per topic.  A node gathered twice
+// repeats its sids; the map the host builds keeps one key per filter, as the
+// reference's does.  DFS topics are handled by k_dfs<3|4> (every entry).
 // ---------------------------------------------------------------------------
 template <int kPhase>
 __global__ __launch_bounds__(256) void k_ident(DeviceSnapshot s, Outputs o, uint32_t n) {
@@ -1618,26 +1623,15 @@ __global__ __launch_bounds__(256) void k_ident(DeviceSnapshot s, Outputs o, uint
     const uint8_t cls = o.cls[t];
     if (cls == kClsDfs) continue;
     uint32_t nid = 0;
-    if (cls != kClsDone) {
-      // every gathered range: the solo parts, then the multi parts
-      const uint32_t *rec = o.recs + (uint64_t)t * kRecStrideAlloc;
+    // (the walk writes the record header, which counts the multi parts, for
+    // every topic with multi entries)
+    if (cls != kClsDone && o.mcount[t]) {
       const uint4 *gt = rec_tail(o.recs, t);
-      // (the walk writes the header only for topics with multi parts or
-      // shared hits, or in the runs form, where nsolo is 0)
-      const bool hdr = o.runs || o.mcount[t] || o.hcount[t];
-      const uint4 hd = hdr ? gt[0] : make_uint4(0, 0, 0, o.nsolo[t]);
-      const uint32_t nm = hd.x & 0xFFu, nq = hd.w;
+      const uint32_t nm = gt[0].x & 0xFFu;
       const uint64_t ib = kPhase == 1 ? o.istart[t] : 0;
-      for (uint32_t h = 0; h < nq + nm; h++) {
-        uint32_t off, cnt;
-        if (h < nq) {
-          off = rec[2 * h];
-          cnt = rec[2 * h + 1];
-        } else {
-          const uint4 u = gt[-(int)(1 + h - nq)];
-          off = u.x;
-          cnt = u.y;
-        }
+      for (uint32_t h = 0; h < nm; h++) {  // the multi parts (solo parts: see above)
+        const uint4 u = gt[-(int)(1 + h)];
+        const uint32_t off = u.x, cnt = u.y;
         for (uint32_t b0 = 0; b0 < cnt; b0 += kWave) {
           const uint32_t j = b0 + lane;
           const bool has = j < cnt && (s.subs[off + j].word & kWordIdent);
@@ -1967,6 +1961,73 @@ static uint32_t resident_blocks(Workspace &ws, int, K kern) {
   return slot_v;
 }
 
+// ---------------------------------------------------------------------------
+// Launch guard (host side, before every launch that takes an Outputs): every
+// array the kernel reads or writes is set, and the workspace buffer behind it
+// holds what the kernel indexes for n topics.  A miss returns -1 (MQM_EINVAL)
+// and names the kernel and the array — never a launch with a null or short
+// array (round 4's r04x fault: k_ident read record headers through a null
+// nsolo / mcount / hcount that its launch site had not set).
+// ---------------------------------------------------------------------------
+enum : uint32_t {
+  kOHCount = 1u << 0, kODCount = 1u << 1, kOMCount = 1u << 2, kOSCount = 1u << 3, kONSolo = 1u << 4,
+  kODStart = 1u << 5, kOHStart = 1u << 6, kOCls = 1u << 7, kODfsList = 1u << 8, kORecs = 1u << 9,
+  kOCtr = 1u << 10, kODOut = 1u << 11, kOHOut = 1u << 12, kOICount = 1u << 13, kOIStart = 1u << 14,
+  kOIOut = 1u << 15,
+};
+// what each kernel family touches (match.hip bodies and the helpers they call)
+constexpr uint32_t kNeedWalk = kOHCount | kODCount | kOMCount | kOSCount | kONSolo | kOCls | kODfsList | kORecs | kOCtr;
+constexpr uint32_t kNeedMerge = kODCount | kOMCount | kODStart | kORecs | kOCtr | kODOut;
+constexpr uint32_t kNeedDesc = kODCount | kOMCount | kOSCount | kONSolo | kODStart | kOCls | kORecs | kOCtr;
+constexpr uint32_t kNeedShared = kOHCount | kOHStart | kORecs | kOCtr | kOHOut;
+constexpr uint32_t kNeedDfs = kOHCount | kODCount | kODStart | kOHStart | kODfsList | kOCtr | kODOut | kOHOut;
+constexpr uint32_t kNeedRuns = kOCls | kORecs | kOCtr;
+constexpr uint32_t kNeedIdentIn = kOMCount | kOCls | kORecs | kOCtr | kODfsList;
+constexpr uint32_t kNeedIdent = kNeedIdentIn | kOICount | kOIStart;
+
+static int guard_outputs(const Workspace &ws, const Outputs &o, uint32_t need, uint32_t n, const char *kernel) {
+  const uint64_t n1 = (uint64_t)n + 1;
+  struct F {
+    uint32_t bit;
+    const void *p;
+    uint64_t bytes;
+    const char *name;
+  } f[] = {{kOHCount, o.hcount, 4 * (uint64_t)n, "hcount"},
+           {kODCount, o.dcount, 4 * (uint64_t)n, "dcount"},
+           {kOMCount, o.mcount, 4 * (uint64_t)n, "mcount"},
+           {kOSCount, o.scount, 4 * (uint64_t)n, "scount"},
+           {kONSolo, o.nsolo, 4 * (uint64_t)n, "nsolo"},
+           {kODStart, o.dstart, 8 * n1, "dstart"},
+           {kOHStart, o.hstart, 8 * n1, "hstart"},
+           {kOCls, o.cls, (uint64_t)n, "cls"},
+           {kODfsList, o.dfs_list, 4 * (uint64_t)std::min<uint64_t>(o.dfs_cap, n1), "dfs_list"},  // (k_dfs reads min(n_dfs, dfs_cap))
+           {kORecs, o.recs, 4 * (uint64_t)kRecStrideAlloc * n, "recs"},
+           {kOCtr, o.ctr, sizeof(Counters), "ctr"},
+           {kODOut, o.dout, 4 * o.dcap, "dout"},
+           {kOHOut, o.hout, 4 * o.hcap, "hout"},
+           {kOICount, o.icount, 4 * (uint64_t)n, "icount"},
+           {kOIStart, o.istart, 8 * n1, "istart"},
+           {kOIOut, o.iout, 0, "iout"}};
+  for (const F &x : f) {
+    if (!(need & x.bit)) continue;
+    if (!x.p) {
+      fprintf(stderr, "mqmatch: %s not launched: Outputs::%s is not set\n", kernel, x.name);
+      return -1;
+    }
+    for (const auto &b : ws.bufs)  // an array the workspace owns must hold what the kernel indexes
+      if (b.p == x.p && b.cap < x.bytes) {
+        fprintf(stderr, "mqmatch: %s not launched: Outputs::%s holds %zu B, the launch indexes %llu B\n", kernel,
+                x.name, b.cap, (unsigned long long)x.bytes);
+        return -1;
+      }
+  }
+  return 0;
+}
+#define GUARD(o, need, n, kernel)                                   \
+  do {                                                              \
+    if (guard_outputs(ws, (o), (need), (n), (kernel)) != 0) return -1; \
+  } while (0)
+
 // counts (n) -> exclusive offsets (u64, n + 1).  u32 counts are widened on
 // the fly: hipCUB accumulates in the input type, and a batch's raw entries can
 // pass 2^32 (config 4 shards gather ~6.8G per 10M topics)
@@ -2045,6 +2106,8 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
   auto *desc_start = (uint64_t *)ws.ptr(W::kDescStart);
   HIP_TRY(hipMemsetAsync(o.ctr, 0, sizeof(Counters), st));
   mark(ws, 0, st);
+  o.dfs_cap = n + 1;  // (the walk lists DFS topics in dfs_list, one per topic at most)
+  GUARD(o, kNeedWalk, n, "k_walk");
   if (n > 0) {
     constexpr uint32_t per_block = kWalkWaves * (kWave / kWalkG);
     const uint32_t blocks = std::max<uint32_t>(
@@ -2141,6 +2204,13 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
   o.hout = (uint32_t *)ws.ptr(W::kHOut);
   o.dcap = dcap;
   o.hcap = hcap;
+  // every emission kernel below (merges, solo copy, shared candidates, DFS)
+  GUARD(o, kNeedMerge | kNeedDesc | kNeedShared, n, "the emission kernels");
+  if (dfs) {
+    Outputs od = o;
+    od.dfs_cap = dfs_cap;
+    GUARD(od, kNeedDfs, n, "k_dfs");
+  }
   auto *desc = (uint4 *)ws.ptr(W::kDesc);
   auto *win = (uint32_t *)ws.ptr(W::kWin);
   GEnt *tab = nullptr;
@@ -2377,6 +2447,8 @@ int runs_device(Workspace &ws, hipStream_t st, const MatchOutput &m, RunsOutput 
   auto *nrun = (uint32_t *)ws.ptr(W::kRunCount);
   auto *roff = (uint64_t *)ws.ptr(W::kRunOffs);
   auto *runs = (uint2 *)ws.ptr(W::kRuns);
+  GUARD(o, kNeedRuns, n, "k_run_count / k_run_copy");
+  if (!nrun || !roff || !runs) return -1;
   if (n > 0) {
     hipLaunchKernelGGL(k_run_count, dim3(std::min<uint32_t>((n + 255) / 256, 8192)), dim3(256), 0, st, o, n, nrun);
     HIP_TRY(hipGetLastError());
@@ -2400,21 +2472,19 @@ int identifiers_device(const DeviceSnapshot &s, Workspace &ws, hipStream_t st, I
   using W = Workspace;
   const uint32_t n = ws.last_n;
   if (!ws.last_valid) return -1;
-  if (ws.get(W::kICount, sizeof(uint32_t) * (n + 1)) || ws.get(W::kIStart, sizeof(uint64_t) * (n + 1))) return -2;
   Outputs o{};
   o.cls = (uint8_t *)ws.ptr(W::kCls);
   o.recs = (uint32_t *)ws.ptr(W::kRecs);
   o.dfs_list = (uint32_t *)ws.ptr(W::kDfsList);
   o.dfs_cap = ws.last_n_dfs;  // the whole list (phases 3 / 4 keep no per-topic arrays)
   o.ctr = (Counters *)ws.ptr(W::kCounters);
+  o.mcount = (uint32_t *)ws.ptr(W::kMCount);  // (k_ident: the topics with multi parts, k_walk)
+  o.runs = ws.last_runs ? 1u : 0u;
+  GUARD(o, kNeedIdentIn, n, "k_ident");  // the last match's arrays, before anything is allocated
+  if (ws.get(W::kICount, sizeof(uint32_t) * (n + 1)) || ws.get(W::kIStart, sizeof(uint64_t) * (n + 1))) return -2;
   o.icount = (uint32_t *)ws.ptr(W::kICount);
   o.istart = (uint64_t *)ws.ptr(W::kIStart);
-  // (k_ident: a record header exists only where these say so, k_walk)
-  o.nsolo = (uint32_t *)ws.ptr(W::kNSolo);
-  o.mcount = (uint32_t *)ws.ptr(W::kMCount);
-  o.hcount = (uint32_t *)ws.ptr(W::kHCount);
-  o.runs = ws.last_runs ? 1u : 0u;
-  if (!o.nsolo || !o.mcount || !o.hcount) return -1;
+  GUARD(o, kNeedIdent, n, "k_ident");
   const uint32_t max_levels = s.height + 1;
   const size_t fb_lds = sizeof(uint32_t) * (((max_levels + 1) & ~1u) + 4 * (2 * max_levels + 8)) +
                         sizeof(uint64_t) * 2 * max_levels;
@@ -2437,6 +2507,7 @@ int identifiers_device(const DeviceSnapshot &s, Workspace &ws, hipStream_t st, I
   const uint64_t total = hp[0];
   if (ws.get(W::kIOut, sizeof(uint32_t) * (total + 1))) return -2;
   o.iout = (uint32_t *)ws.ptr(W::kIOut);
+  GUARD(o, kNeedIdent | kOIOut, n, "k_ident<1>");
   if (n > 0 && total > 0) {
     hipLaunchKernelGGL(k_ident<1>, dim3(blocks), dim3(256), 0, st, s, o, n);
     HIP_TRY(hipGetLastError());

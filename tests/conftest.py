@@ -26,6 +26,8 @@ _make("oracle", "oracle/_build/libmochi_ref.so")
 _make("tools", "tools/_build/libmqgen.so")
 _make("maxmq_amd/csrc", "maxmq_amd/_lib/libmqmatch.so")
 _make("tests/harness", "tests/harness/_build/shim_harness")
+_make("tests/harness", "tests/harness/_build/churn_harness")
+_make("tests/harness", "tests/harness/_build/guard_test")
 
 
 @pytest.fixture(scope="session")

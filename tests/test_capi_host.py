@@ -113,3 +113,19 @@ def test_subscribe_rejects_out_of_range_options():
     with pytest.raises(maxmq_amd.MqmError):
         idx.subscribe_many(Strings.from_list(["x", "y"]), Strings.from_list(["p", "q"]), np.array([1, 3], np.uint8))
     assert idx.subscribe("x", maxmq_amd.Subscription("p"))  # the bulk call applied nothing
+
+
+def test_launch_guard_refuses_missing_or_short_arrays():
+    """match.hip guard_outputs: identifiers_device on a workspace whose last
+    match left an array unset (round 4's r04x fault: k_ident read record
+    headers through null nsolo / mcount / hcount) or too short for its topics
+    returns -1 (MQM_EINVAL) before any allocation or launch
+    (tests/harness/guard_test.cpp, CPU only)."""
+    import subprocess
+
+    exe = os.path.join(ROOT, "tests", "harness", "_build", "guard_test")
+    if not os.path.exists(exe):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "tests", "harness")])
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.strip().endswith("OK") and r.stdout.count("-> -1") == 7, r.stdout

@@ -331,10 +331,13 @@ def test_identifiers_vs_oracle(config, overrides):
     assert_same(g, r, "identifiers")
 
 
-def test_identifiers_dfs_topics_and_device_form():
+def test_identifiers_dfs_topics_and_device_form(monkeypatch):
     """Hubs of identified subscriptions (9000 multi entries per topic: the
     partitioned workgroup merge) and topics deeper than the walk's 16 cached
-    levels (the unbounded DFS path), with identifiers."""
+    levels (the unbounded DFS path), with identifiers.  The host call runs the
+    batch pipeline too (MQM_NO_FAST=1), so its listed sids and the device
+    form's come from the same pass (k_ident lists multi entries only: a solo
+    delivery's map is its first pair)."""
     filters, clients, subs = [], [], []
     for i in range(3000):  # 3 compatible filters per client: 9000 multi entries on hub/x
         filters += ["hub/#", "hub/x", "+/x"]
@@ -349,7 +352,9 @@ def test_identifiers_dfs_topics_and_device_form():
         clients += [f"p{i}"] * 3
         subs += [(i % 3, 0, 0, 0, i + 1), (1, 1, 0, 0, 0), (2, 0, 1, 2, 5)]
     topics = ["hub/x", "hub", "a/b", "a/b/c", "zz/x", "$SYS/x", deep, deep + "/e"]
+    monkeypatch.setenv("MQM_NO_FAST", "1")
     idx = maxmq_amd.TopicsIndex(0, identifiers=True)
+    monkeypatch.delenv("MQM_NO_FAST")
     ora = OracleIndex()
     for f, c, (q, nl, rap, rh, ident) in zip(filters, clients, subs):
         idx.subscribe(c, maxmq_amd.Subscription(f, q, ident, bool(nl), bool(rap), rh))
