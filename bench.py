@@ -101,6 +101,10 @@ def parse():
                     help="forward: Subscribers (headline); reverse: Messages over retained topics (config 5); "
                          "churn: Subscribe/Unsubscribe at rate with background snapshot rebuilds")
     ap.add_argument("--churn-ops", type=int, default=1000000, help="churn: mutations per round (half unsubscribes)")
+    ap.add_argument("--serve-churn-s", type=float, default=20.0,
+                    help="churn: seconds of per-publish calls (64 native callers through MQM_CFG_SERVE) while "
+                         "--churn-rate Subscribe/Unsubscribe per second run (0 = skip)")
+    ap.add_argument("--churn-rate", type=float, default=100000.0, help="churn: mutations/s during the served leg")
     ap.add_argument("--retained", type=int, default=50000000, help="reverse: retained topics")
     ap.add_argument("--sweep", default="",
                     help="tuning sweep before the measurement: ';'-separated variants of "
@@ -826,7 +830,9 @@ def latency(idx, w, args):
            "topics_per_s": one["topics_per_s"], "driver": "native threads (tools/conc_driver.cpp)"}
     T, per = args.conc_threads, args.conc_calls
     run(T, 20)  # warm: every caller's context (stream, workspace, pinned blocks) exists before timing
+    idx.direct_host_us()  # (reset)
     conc = {"threads": T, "calls_per_thread": per, "direct": run(T, per)}
+    conc["direct"]["phases_us"] = idx.direct_host_us()
     idx.batching_policy(0, 0)  # MQM_CFG_BATCHING on from here
     run(T, 20)
     b0, t0_ = idx.batching_stats()
@@ -977,8 +983,108 @@ def run_churn(args, dist, rank, world, local, dev):
         "match_steps_during_rebuild": len(during),
         "commit_state": st,
     }
+    if args.serve_churn_s > 0:
+        out["served_under_churn"] = serve_churn(idx, w, args)
     if rank == 0:
         print(json.dumps(out), flush=True)
+
+
+def serve_churn(idx, w, args):
+    """Per-publish Subscribers(topic) calls through the persistent server
+    (MQM_CFG_SERVE) on the async index while --churn-rate Subscribe /
+    Unsubscribe per second run on another thread (the reference takes both
+    concurrently: server.go:1013 / topics.go:303-321 beside server.go:776).
+    Native threads (tools/conc_driver.cpp mqd_serve_churn): --conc-threads
+    callers for --serve-churn-s seconds, first with no mutations (baseline),
+    then with them.  The index rebuilds in the background
+    (mqm_commit_policy: submit 50 ms after the first unsubmitted mutation;
+    logs coalesce while a build runs), and callers match the newest published
+    snapshot without taking the index lock.  Visibility lag of a mutation = the
+    first return of a call whose result's snapshot version includes it, minus
+    the mutation's time."""
+    import ctypes as C
+
+    from maxmq_amd import capi
+    from tools.mqgen import Strings
+
+    L = capi.lib()
+    D = C.CDLL(os.path.join(ROOT, "tools", "_build", "libmqdrive.so"))
+
+    class Api(C.Structure):
+        _fields_ = [(x, C.c_void_p) for x in ("subscribers", "offsets", "result_free", "version", "subscribe",
+                                              "unsubscribe", "state")]
+
+    class Out(C.Structure):
+        _fields_ = [(x, C.c_uint64) for x in ("calls", "deliveries", "mutations", "failed_mutations")]
+
+    api = Api(*[C.cast(getattr(L, f), C.c_void_p) for f in (
+        "mqm_subscribers", "mqm_result_offsets", "mqm_result_free", "mqm_result_snapshot_version", "mqm_subscribe",
+        "mqm_unsubscribe", "mqm_commit_state_get")])
+    vp = C.c_void_p
+    D.mqd_serve_churn.argtypes = [C.POINTER(Api), vp, vp, vp, C.c_uint32, C.c_int, C.c_double, C.c_uint32,
+                                  C.c_uint32, vp, vp, vp, vp, C.c_uint32, C.c_double, vp, vp, vp, vp, C.c_uint64, vp,
+                                  vp, C.POINTER(Out)]
+    D.mqd_serve_churn.restype = C.c_int64
+    n = min(len(w.topics), 1 << 20)
+    data = np.ascontiguousarray(w.topics.data[: int(w.topics.offs[n])])
+    offs = np.ascontiguousarray(w.topics.offs[: n + 1].astype(np.uint64))
+    m = 200000
+    rng = np.random.default_rng(0x5EC4)
+    sel = rng.choice(len(w.filters), size=m, replace=False)
+    fl = Strings.from_list([w.filters[int(i)] for i in sel])
+    cl = Strings.from_list([f"churner-{j}" for j in range(m)])
+    T = args.conc_threads
+    idx.commit_policy(0, 50)
+    idx.serve_policy(T, 20000)
+    p = lambda a: a.ctypes.data_as(vp)  # noqa: E731
+
+    def run(seconds, rate):
+        cap = int(seconds * 40000) + 1000  # calls per thread (>= 40k/s per caller)
+        sample = 16
+        lat = np.zeros(T * cap, np.uint32)
+        done = np.zeros(T, np.uint32)
+        per_s = cap // sample + 1
+        s_t = np.zeros(T * per_s, np.uint32)
+        s_v = np.zeros(T * per_s, np.uint64)
+        mcap = int(seconds * rate * 1.2) + 1000 if rate > 0 else 1
+        m_t = np.zeros(mcap, np.uint32)
+        m_v = np.zeros(mcap, np.uint64)
+        o = Out()
+        st0 = idx.commit_state()
+        ns = D.mqd_serve_churn(C.byref(api), idx._h, p(data), p(offs), n, T, seconds, cap, sample, p(cl.data),
+                               p(cl.offs), p(fl.data), p(fl.offs), m, rate, p(lat), p(done), p(s_t), p(s_v), mcap,
+                               p(m_t), p(m_v), C.byref(o))
+        if ns < 0:
+            raise RuntimeError("mqm_subscribers failed in the churn driver")
+        st1 = idx.commit_state()
+        us = np.concatenate([lat[k * cap: k * cap + int(done[k])] for k in range(T)]).astype(np.float64) / 1e3
+        r = {"seconds": ns * 1e-9, "calls": int(o.calls), "topics_per_s": o.calls / (ns * 1e-9),
+             "p50_us": float(np.median(us)), "p99_us": float(np.percentile(us, 99)),
+             "p999_us": float(np.percentile(us, 99.9)), "max_us": float(us.max()),
+             "deliveries_per_topic": o.deliveries / max(1, o.calls),
+             "snapshots_published": st1["builds"] - st0["builds"], "last_build_ms": st1["last_build_ms"]}
+        if rate > 0:
+            nm = int(o.mutations)
+            r.update({"mutations": nm, "mutations_per_s": nm / (ns * 1e-9), "failed_mutations": int(o.failed_mutations)})
+            # visibility: sampled calls in return order, the newest version seen so far
+            keep = np.concatenate([np.arange(k * per_s, k * per_s + (int(done[k]) + sample - 1) // sample)
+                                   for k in range(T)])
+            order = np.argsort(s_t[keep], kind="stable")
+            tr, vr = s_t[keep][order].astype(np.float64), np.maximum.accumulate(s_v[keep][order])
+            pos = np.searchsorted(vr, m_v[:nm], side="left")  # first call whose result includes mutation k
+            seen = pos < len(vr)
+            lag = (tr[np.minimum(pos, len(vr) - 1)] - m_t[:nm].astype(np.float64))[seen] / 1e3
+            r["visibility_lag_ms"] = ({"p50": float(np.median(lag)), "p99": float(np.percentile(lag, 99)),
+                                       "max": float(lag.max())} if len(lag) else None)
+            r["mutations_seen_by_a_call"] = float(seen.mean()) if nm else None
+        return r
+
+    run(2.0, 0)  # warm: the server, every caller's path
+    base = run(min(args.serve_churn_s, 10.0), 0)
+    churn = run(args.serve_churn_s, args.churn_rate)
+    return {"threads": T, "driver": "native threads (tools/conc_driver.cpp mqd_serve_churn)",
+            "index": "MQM_CFG_ASYNC_COMMIT | MQM_CFG_SERVE, commit_policy(0 ops, 50 ms)",
+            "baseline_no_mutations": base, "under_churn": churn, "target_rate": args.churn_rate}
 
 
 def run_reverse(args, dist, rank, world, local, dev):

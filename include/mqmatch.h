@@ -298,6 +298,12 @@ int mqm_serve_device_us(mqm_index *h, double *us);
  * calls that slept on the completion poller instead of spinning */
 int mqm_serve_host_us(mqm_index *h, double *us);
 int mqm_batching_stats(mqm_index *h, uint64_t *batches, uint64_t *topics);
+/* single-topic calls on the direct path (no collector, no server: the
+ * small-batch kernel per call) since the previous call of this function
+ * (us[9]; reads and resets): mean time per phase — front buffer (commit check),
+ * context from the pool, launch + wait for the kernel, result block — then the
+ * maximum of each phase, then the number of calls */
+int mqm_direct_host_us(mqm_index *h, double *us);
 /* Device in / device out on `hip_stream` (hipStream_t, NULL = default stream). */
 int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t *d_topic_offsets,
                      uint32_t n_topics, void *hip_stream, mqm_device_result *out);

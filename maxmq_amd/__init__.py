@@ -267,6 +267,14 @@ class TopicsIndex:
         check("mqm_serve_host_us", lib().mqm_serve_host_us(self._h, v))
         return {"post": v[0], "wait": v[1], "collect": v[2], "slept_share": v[3]}
 
+    def direct_host_us(self):
+        """single-topic calls on the direct path since the previous read (us):
+        mean and max per phase (front buffer, context, launch + wait, result)"""
+        v = (C.c_double * 9)()
+        check("mqm_direct_host_us", lib().mqm_direct_host_us(self._h, v))
+        names = ("front", "context", "kernel", "result")
+        return {"mean": dict(zip(names, v[0:4])), "max": dict(zip(names, v[4:8])), "calls": int(v[8])}
+
     def batching_stats(self):
         """(batches run, topics they carried) of the MQM_CFG_BATCHING collector"""
         b, t = C.c_uint64(), C.c_uint64()

@@ -50,7 +50,7 @@ EXPORTED = [
     "mqm_match_device_async", "mqm_match_ctx_wait", "mqm_match_ctx_stats", "mqm_match_batch_packed",
     "mqm_result_packed", "mqm_match_batch_runs", "mqm_result_runs", "mqm_result_expand",
     "mqm_serve_policy", "mqm_serve_stats", "mqm_serve_device_us", "mqm_serve_host_us",
-    "mqm_result_snapshot_version",
+    "mqm_result_snapshot_version", "mqm_direct_host_us",
 ]
 
 
@@ -164,6 +164,7 @@ def lib():
         "mqm_match_device": ([vp, vp, vp, u32, vp, C.POINTER(DeviceResult)], C.c_int),
         "mqm_result_num_topics": ([vp], u32),
         "mqm_result_snapshot_version": ([vp], u64),
+        "mqm_direct_host_us": ([vp, C.POINTER(C.c_double)], C.c_int),
         "mqm_result_offsets": ([vp], vp),
         "mqm_result_deliveries": ([vp], vp),
         "mqm_result_shared_offsets": ([vp], vp),
@@ -218,7 +219,9 @@ def lib():
         "mqm_serve_host_us": ([vp, vp], C.c_int),
     }
     for name, (args, res) in sigs.items():
-        f = getattr(L, name)
+        f = getattr(L, name, None)
+        if f is None:  # (a library older than this file: tests/test_capi_host.py checks every export)
+            continue
         f.argtypes = args
         f.restype = res
     _LIB = L

@@ -160,6 +160,9 @@ struct mqm_index {
   void stop_server();
   std::atomic<Collector *> collector{nullptr};
   std::atomic<uint32_t> live_ctxs{0};  // mqm_match_ctx objects of this index (mqm_destroy refuses while any live)
+  // single-topic calls on the direct small-batch path (mqm_direct_host_us):
+  // per phase (front buffer, context, launch + wait, result), summed and max ns
+  std::atomic<uint64_t> direct_ns[4] = {}, direct_max_ns[4] = {}, direct_calls{0};
   void stop_collector();
   ~mqm_index();
 };
@@ -794,11 +797,16 @@ static int match_batch_impl(mqm_index *h, const char *topic_bytes, const uint64_
   return guarded([&] {
     if (h->cfg.device == MQM_DEVICE_NONE) return MQM_ENODEV;
     if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
+    using clk = std::chrono::steady_clock;
+    clk::time_point ts[5];
+    ts[0] = clk::now();
     std::shared_ptr<GpuSnapshot> snap;
-    int rc = front(h, &snap);
+    int rc = front_fast(h, &snap) ? MQM_OK : front(h, &snap);  // (commits first with MQM_CFG_AUTOCOMMIT)
     if (rc != MQM_OK) return rc;
+    ts[1] = clk::now();
     auto c = ctx_acquire(h, &rc);
     if (rc != MQM_OK) return rc;
+    ts[2] = clk::now();
     auto r = std::make_unique<mqm_result>();
     const bool want_ids = (h->cfg.flags & MQM_CFG_IDENTIFIERS) != 0;
     // small batches (the per-publish call shape): the one-launch path, unless
@@ -813,10 +821,22 @@ static int match_batch_impl(mqm_index *h, const char *topic_bytes, const uint64_
         return e < 0 ? hip_rc(e) : MQM_EHIP;
       }
       if (e == 0) {
+        ts[3] = clk::now();
         rc = fast_result(h, snap, fo, packed, r.get());
         ctx_release(h, std::move(c));
         if (rc != MQM_OK) return rc;
         *out = r.release();
+        if (n_topics == 1) {  // the direct per-publish call: its phases (mqm_direct_host_us)
+          ts[4] = clk::now();
+          for (int i = 0; i < 4; i++) {
+            const uint64_t d = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(ts[i + 1] - ts[i]).count();
+            h->direct_ns[i].fetch_add(d, std::memory_order_relaxed);
+            uint64_t m = h->direct_max_ns[i].load(std::memory_order_relaxed);
+            while (d > m && !h->direct_max_ns[i].compare_exchange_weak(m, d, std::memory_order_relaxed)) {
+            }
+          }
+          h->direct_calls.fetch_add(1, std::memory_order_relaxed);
+        }
         return MQM_OK;
       }
     }
@@ -1898,6 +1918,18 @@ int mqm_serve_host_us(mqm_index *h, double *us) {
   }
   const uint64_t sl = sv->host_slept.exchange(0);
   us[3] = n ? (double)sl / (double)n : 0.0;
+  return MQM_OK;
+}
+
+int mqm_direct_host_us(mqm_index *h, double *us) {
+  if (!h || !us) return MQM_EINVAL;
+  const uint64_t n = h->direct_calls.exchange(0);
+  for (int i = 0; i < 4; i++) {
+    const uint64_t t = h->direct_ns[i].exchange(0), m = h->direct_max_ns[i].exchange(0);
+    us[i] = n ? (double)t / 1e3 / (double)n : 0.0;
+    us[4 + i] = (double)m / 1e3;
+  }
+  us[8] = (double)n;
   return MQM_OK;
 }
 

@@ -118,4 +118,61 @@ __device__ __forceinline__ uint32_t walk_step(const DeviceSnapshot &s, bool do_p
   return c;
 }
 
+// walk_step over the paired node slots (snapshot.h DeviceSnapshot::slots):
+// a wildcard child's step loads its whole 64-B slot — one sector, as its
+// 32-B descriptor was — and hands the child's own '+' child's descriptor to
+// `carry` as well.  Probes as in walk_step.
+template <class Carry>
+__device__ __forceinline__ uint32_t walk_step_slot(const DeviceSnapshot &s, bool do_probe, bool do_desc,
+                                                   uint32_t parent, uint32_t wc, uint64_t k0, uint64_t k1,
+                                                   const uint8_t *tok, uint32_t tok_len, NodeDesc *desc,
+                                                   Carry &&carry) {
+  const Key key{k0, k1};
+  const uint64_t nslots = s.n_buckets * kEdgesPerBucket;
+  const uint64_t h = do_probe ? edge_hash(parent, key) : 0;
+  uint64_t slot = do_probe ? bucket_of(h, s.n_buckets) * kEdgesPerBucket : 0;
+  const uint4 *q = do_probe ? reinterpret_cast<const uint4 *>(s.edges + slot)
+                            : reinterpret_cast<const uint4 *>(s.slots + 2 * (uint64_t)(do_desc ? wc : 0));
+  uint4 x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3];
+  uint32_t c = kNone;
+  bool more = false;
+  // carry(do_desc, the node's descriptor halves, its '+' child's halves): called
+  // by every lane (it may use wave ops) before the probe loop, so the '+'
+  // child's descriptor is consumed at once and holds no registers past here
+  carry(do_desc, x0, x1, x2, x3);
+  if (do_desc) {
+    c = wc;
+    *desc = NodeDesc{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+  }
+  for (;;) {
+    if (do_probe && x1.x != kNone) {
+      const bool hit = x1.x == parent && (((uint64_t)x0.y << 32) | x0.x) == k0 &&
+                       (((uint64_t)x0.w << 32) | x0.z) == k1;
+      bool ok = hit;
+      if (hit && key_is_long(key)) {  // hashed long token: verify the bytes
+        ok = x1.w == tok_len;
+        for (uint32_t i = 0; ok && i < tok_len; i++) ok = s.tok_pool[x1.z + i] == tok[i];
+      }
+      if (ok) {
+        c = x1.y;
+        *desc = NodeDesc{x2.x, x2.y, x2.z, x2.w, x3.x, x3.y, x3.z, x3.w};
+      }
+      more = !ok;
+    } else {
+      more = false;
+    }
+    if (!__any(more)) break;  // wave-uniform
+    if (more) {
+      slot = slot + 1 == nslots ? 0 : slot + 1;
+      const uint4 *e = reinterpret_cast<const uint4 *>(s.edges + slot);
+      x0 = e[0];
+      x1 = e[1];
+      x2 = e[2];
+      x3 = e[3];
+    }
+    do_probe = more;
+  }
+  return c;
+}
+
 }  // namespace mqm

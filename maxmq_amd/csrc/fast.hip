@@ -635,7 +635,13 @@ int pinned_grow(void **p, size_t *cap, size_t need, bool coherent = false) {
 
 }  // namespace
 
+static bool spin_sync() {
+  static const bool v = getenv("MQM_SPIN_SYNC") && atoi(getenv("MQM_SPIN_SYNC")) != 0;
+  return v;
+}
+
 FastArena::~FastArena() {
+  if (done_ev) (void)hipEventDestroy(done_ev);
   for (void *p : {(void *)in_bytes, (void *)in_offs, (void *)recs, (void *)dout, (void *)hout, (void *)iout,
                   (void *)status})
     if (p) (void)hipHostFree(p);
@@ -689,7 +695,13 @@ int match_small(const DeviceSnapshot &s, Workspace &ws, const char *bytes, const
                        a.recs, a.dout, a.dout_cap / sizeof(uint64_t), a.hout, a.hout_cap / sizeof(uint32_t),
                        want_ids ? a.iout : nullptr, a.iout_cap / sizeof(uint32_t), a.status);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipStreamSynchronize(st));
+    if (spin_sync()) {
+      HIP_TRY(hipStreamSynchronize(st));
+    } else {
+      if (!a.done_ev) HIP_TRY(hipEventCreateWithFlags(&a.done_ev, hipEventBlockingSync | hipEventDisableTiming));
+      HIP_TRY(hipEventRecord(a.done_ev, st));
+      HIP_TRY(hipEventSynchronize(a.done_ev));
+    }
     FastStatus stt;
     memcpy(&stt, (const void *)a.status, sizeof(stt));  // after the stream synchronisation
     if (!stt.done) {

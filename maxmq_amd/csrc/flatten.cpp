@@ -720,6 +720,7 @@ GpuSnapshot::~GpuSnapshot() {
   for (void *b : buffers)
     if (b) (void)hipFree(b);
   if (words) (void)hipFree(words);
+  if (slots) (void)hipFree(slots);
   if (nflags) (void)hipFree(nflags);
   if (bloom) (void)hipFree(bloom);
   if (pinfo) (void)hipFree(pinfo);
@@ -765,6 +766,12 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
     g->device_bytes += bb;
   }
   g->device_bytes += n_sub_ents * 4;
+  {  // paired node slots (snapshot.h DeviceSnapshot::slots)
+    const uint64_t nn = hs->nodes.size();
+    if (hipMalloc(&g->slots, nn * 2 * sizeof(NodeDesc) + 64) != hipSuccess) return MQM_ENOMEM;
+    if (derive_slots((const NodeDesc *)g->buffers[0], (NodeDesc *)g->slots, nn, stream)) return MQM_EHIP;
+    g->device_bytes += nn * 2 * sizeof(NodeDesc);
+  }
   {  // partners of the multi entries (merge by resolution)
     const size_t pb = hs->pinfo.size() * sizeof(uint2), qb = hs->partners.size() * 4;
     if (hipMalloc(&g->pinfo, pb + 64) != hipSuccess || hipMalloc(&g->partners, qb + 64) != hipSuccess)
@@ -804,6 +811,7 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
     g->ret.has_empty = hs->has_empty ? 1u : 0u;
   }
   g->dev.nodes = (const NodeDesc *)g->buffers[0];
+  g->dev.slots = (const NodeDesc *)g->slots;
   g->dev.edges = (const EdgeEntry *)g->buffers[1];
   g->dev.subs = (const SubEnt *)g->buffers[2];
   g->dev.words = (const uint32_t *)g->words;

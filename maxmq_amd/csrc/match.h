@@ -39,6 +39,11 @@ struct FastArena {
   size_t in_cap = 0, offs_cap = 0, rec_cap = 0, dout_cap = 0, hout_cap = 0, iout_cap = 0, status_cap = 0;
   FastCtl *ctl = nullptr;  // device
   uint32_t grid = 0;       // resident k_fast workgroups
+  // the call's completion: a blocking-sync event (the waiting caller sleeps in
+  // the driver instead of spinning: 64 direct callers spinning in
+  // hipStreamSynchronize on a 16-CPU quota starve the ones whose results are
+  // ready — MQM_SPIN_SYNC=1 keeps the stream synchronisation, for A/B)
+  hipEvent_t done_ev = nullptr;
   ~FastArena();
 };
 struct FastOutput {
@@ -58,7 +63,9 @@ struct Workspace {
     kInBytes, kInOffs, kListS, kICount, kIStart, kIOut, kNSolo, kDescStart, kDesc, kWin, kMCount, kRunCount, kRunOffs, kRuns, kListW, kListT1, kListT2, kListT3, kListP, kListH, kListRS, kListR,
     // reverse match (retained.hip)
     kROffs, kRNLev, kRWild, kRLOff, kRFCount, kRFCur, kRLevels, kRNCount, kRNOff, kRItemF0, kRItemN0, kRItemF1,
-    kRItemN1, kRChild, kRECount, kREOff, kREmit, kRPos, kRChunks, kRCOff, kROut, kRInBytes, kRInOffs, kNumSlots
+    kRItemN1, kRChild, kRECount, kREOff, kREmit, kRPos, kRChunks, kRCOff, kROut, kRInBytes, kRInOffs,
+    kLDesc,  // the long solo parts (k_longcopy)
+    kNumSlots
   };
   struct Buf {
     void *p = nullptr;
@@ -150,6 +157,8 @@ struct MatchOutput {
   bool exact = false;                     // sized by its own read-back (the first call of a workspace, or a re-run)
 };
 
+// slots[2i] = nodes[i], slots[2i + 1] = nodes[nodes[i].plus] or zeros (snapshot upload, on `st`)
+int derive_slots(const NodeDesc *nodes, NodeDesc *slots, uint64_t n, hipStream_t st);
 // words[i] = subs[i].word & kPackedMask for i < n (snapshot upload, on `st`)
 int derive_words(const SubEnt *subs, uint32_t *words, uint64_t n, hipStream_t st);
 // nflags[i] = nodes[i].sh_cnt_flags >> 24 for i < n (snapshot upload, on `st`)

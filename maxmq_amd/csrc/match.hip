@@ -109,7 +109,12 @@ static_assert(kLMax % kWalkG == 0, "levels per lane");
 // a load item of the walk: the literal-child probe of a frontier node (pushed
 // only when the edge filter says the next level's key may be a child of it),
 // or the descriptor load of its '+' / '#' child
-enum : uint32_t { kItemLit = 0, kItemPlus = 1, kItemHash = 2 };
+enum : uint32_t { kItemLit = 0, kItemPlus = 1, kItemHash = 2, kItemPlusKnown = 3 };
+// kItemPlusKnown: a '+' child whose descriptor came with its parent's node
+// slot (DeviceSnapshot::slots) — no load; the descriptor waits in the topic's
+// LDS (TopicLds::pdesc, kPK per level, by rank among the level's such items;
+// a parent past kPK pushes a plain kItemPlus)
+constexpr int kPK = 2;
 
 // topic class (cls): Done = no entries and no shared candidates; Bounded (+
 // FewHits when nh <= kSmallHits, for k_route) = emitted from its record; Dfs
@@ -144,6 +149,7 @@ struct Counters {              // zeroed before every batch
   unsigned long long n_solo;                    // solo entries the walk copied
   unsigned long long tab_total, dfs_raw, dfs_h; // DFS: dedupe table, raw entries, shared candidates
   unsigned long long d_sum, h_sum;              // deliveries, shared candidates (after dedupe)
+  unsigned long long n_long;                    // k_desc: solo parts long enough for k_longcopy
 #if MQM_WALK_STATS
   unsigned long long st_probe, st_miss, st_desc;
 #endif
@@ -175,11 +181,12 @@ struct Outputs {
   uint32_t runs;
 };
 
-constexpr int kTopicWords = (2 * kLMax + 8 * kICap + kStage) / 4;
+constexpr int kTopicWords = (2 * kLMax + 8 * kICap + kStage) / 4 + 2 * kPK * 8;
 struct TopicLds {              // k_walk context of one topic (one lane group)
   uint16_t sep[kLMax];         // position of the '/' ending level k (topics > 64 KiB: DFS path)
   uint32_t item[2][kICap];     // the level's load items: node id << 2 | kind (kItem*)
   uint8_t stage[kStage];       // the topic's first kStage bytes
+  uint32_t pdesc[2][kPK][8];   // kItemPlusKnown descriptors: [level parity][rank among the level's such items]
   uint32_t pad[kTopicWords % 2 ? 2 : 1];  // odd dword stride: the groups of a wave reading the
                                //   same field hit different banks (a 128-dword stride put all
                                //   16 groups on one bank: SQ_LDS_BANK_CONFLICT 3x the LDS cycles)
@@ -336,8 +343,8 @@ __device__ __forceinline__ const uint4 *rec_tail(const uint32_t *recs, uint32_t 
 }
 
 
-template <int kG, int kChunk = 0>
-__global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, const uint8_t *__restrict__ tbytes,
+template <int kG, int kChunk = 0, bool kSlots = true>
+__global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_eu(4))) void k_walk(DeviceSnapshot s, const uint8_t *__restrict__ tbytes,
                                                            const uint64_t *__restrict__ toffs, uint32_t n,
                                                            Outputs o) {
   constexpr int kGroups = kWave / kG;
@@ -351,6 +358,12 @@ __global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, co
   const uint32_t gmask_lt = (1u << gl) - 1u;
   const uint64_t stride = (uint64_t)gridDim.x * kWalkWaves * kGroups;
   const NodeDesc root = load_desc(s.nodes);
+  // the root's '+' child (every topic visits it at level 0): its descriptor is
+  // the second half of the root's slot, kept in LDS for the block (copied
+  // into each topic's pdesc at its start; not a register across the loop)
+  __shared__ uint32_t root_plus[8];
+  if (kSlots && threadIdx.x < 8) root_plus[threadIdx.x] = reinterpret_cast<const uint32_t *>(s.slots + 1)[threadIdx.x];
+  __syncthreads();
   uint32_t n_parts = 0; // solo parts of this lane's topics (Counters::n_desc; group leaders)
   uint32_t n_solo = 0;  // solo entries of this lane's topics (Counters::n_solo; group leaders, flushed before 2^32)
 
@@ -431,12 +444,17 @@ __global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, co
         my_k1[j] = k.k1;
       }
     }
-    // level 0's items: the root's literal probe, '+' and '#' children
+    // level 0's items: the root's literal probe, '+' (its descriptor known:
+    // the root's slot) and '#' children
     if (gl == 0) {
       uint32_t k = 0;
       if ((root.sh_cnt_flags >> 24) & kFlagHasLiteral) L.item[0][k++] = (0u << 2) | kItemLit;
-      if (root.plus != kNone) L.item[0][k++] = (root.plus << 2) | kItemPlus;
+      if (root.plus != kNone) L.item[0][k++] = (root.plus << 2) | (kSlots ? kItemPlusKnown : kItemPlus);
       if (root.hash != kNone) L.item[0][k++] = (root.hash << 2) | kItemHash;
+    }
+    if (kSlots && root.plus != kNone) {  // (lanes gl copy words gl, gl + kG, ...)
+#pragma unroll
+      for (int w = 0; w < 8; w += kG) L.pdesc[0][0][w + gl] = root_plus[w + gl];
     }
     const uint32_t root_items = (((root.sh_cnt_flags >> 24) & kFlagHasLiteral) ? 1u : 0u) +
                                 (root.plus != kNone ? 1u : 0u) + (root.hash != kNone ? 1u : 0u);
@@ -480,21 +498,52 @@ __global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, co
       const uint32_t tst = d == 0 ? 0 : L.sep[d - 1] + 1;
       const uint32_t tln = ((d < nsep) ? L.sep[d] : len) - tst;
       uint32_t nnext = 0;
+      uint32_t k3r = 0, k3w = 0;  // kItemPlusKnown items read at this level / carried to the next (group-uniform)
       for (uint32_t base = 0; base < ni; base += kG) {
         const uint32_t it = base + gl;
         const bool live = it < ni;
         const uint32_t iw = L.item[cur][live ? it : 0];
         const uint32_t kind = iw & 3u, id = iw >> 2;
         const bool lit = kind == kItemLit;
+        const bool known = live && kind == kItemPlusKnown;
+        const uint32_t m3 = (uint32_t)(__ballot(known) >> gbase) & kGMask;
+        const uint32_t r3 = k3r + __popc(m3 & gmask_lt);
+        k3r += __popc(m3);
+        // a node loaded from its slot brings its '+' child's descriptor: when
+        // that child is pushed, the descriptor goes to the next level in LDS
+        // (the first kPK such per level) right at the load (the walk is at its
+        // VGPR budget)
+        const bool slot_load = live && !lit && !known;
+        bool pk = false;
         NodeDesc dc;
-        const uint32_t c = walk_step(s, live && lit && !lit_is_wild, live && !lit, id, id, k0, k1, tp + tst, tln, &dc);
+        uint32_t c = !kSlots ? walk_step(s, live && lit && !lit_is_wild, slot_load, id, id, k0, k1, tp + tst, tln, &dc)
+                             : walk_step_slot(s, live && lit && !lit_is_wild, slot_load, id, id, k0, k1, tp + tst, tln, &dc,
+                                    [&](bool ld, const uint4 &a0, const uint4 &a1, const uint4 &p0, const uint4 &p1) {
+                                      // (pushed: has_next and children; x.plus = a0.x, flags = a1.w >> 24)
+                                      const bool want3 = ld && has_next && ((a1.w >> 24) & kFlagHasChildren) &&
+                                                         a0.x != kNone;
+                                      const uint32_t mw = (uint32_t)(__ballot(want3) >> gbase) & kGMask;
+                                      const uint32_t w3 = k3w + __popc(mw & gmask_lt);
+                                      pk = want3 && w3 < (uint32_t)kPK;
+                                      k3w += __popc(mw);
+                                      if (pk) {
+                                        uint32_t *q = L.pdesc[(d + 1) & 1][w3];
+                                        q[0] = p0.x, q[1] = p0.y, q[2] = p0.z, q[3] = p0.w;
+                                        q[4] = p1.x, q[5] = p1.y, q[6] = p1.z, q[7] = p1.w;
+                                      }
+                                    });
+        if (known) {
+          const uint32_t *q = L.pdesc[d & 1][r3];
+          dc = NodeDesc{q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7]};
+          c = id;
+        }
         const bool found = c != kNone;
 #if MQM_WALK_STATS
         {
           const bool pr = live && lit && !lit_is_wild;
           const uint32_t mp = (uint32_t)(__ballot(pr) >> gbase) & kGMask;
           const uint32_t mm = (uint32_t)(__ballot(pr && !found) >> gbase) & kGMask;
-          const uint32_t md = (uint32_t)(__ballot(live && !lit) >> gbase) & kGMask;
+          const uint32_t md = (uint32_t)(__ballot(slot_load) >> gbase) & kGMask;
           if (gl == 0) {
             atomicAdd(&o.ctr->st_probe, (unsigned long long)__popc(mp));
             atomicAdd(&o.ctr->st_miss, (unsigned long long)__popc(mm));
@@ -591,7 +640,7 @@ __global__ __launch_bounds__(kWave *kWalkWaves) void k_walk(DeviceSnapshot s, co
           uint32_t *nx = &L.item[cur ^ 1][nnext + __popc(m_i0 & gmask_lt) + 2 * __popc(m_i1 & gmask_lt)];
           uint32_t k = 0;
           if (lit_next) nx[k++] = (c << 2) | kItemLit;
-          if (dc.plus != kNone) nx[k++] = (dc.plus << 2) | kItemPlus;
+          if (dc.plus != kNone) nx[k++] = (dc.plus << 2) | (pk ? kItemPlusKnown : kItemPlus);
           if (dc.hash != kNone && !leaf) nx[k++] = (dc.hash << 2) | kItemHash;
         }
         nh += n_own + n_par + n_hl;
@@ -690,7 +739,8 @@ struct alignas(8) DescLds {
 };
 
 __global__ __launch_bounds__(256) void k_desc(Outputs o, uint32_t n, const uint64_t *__restrict__ desc_start,
-                                              uint4 *__restrict__ desc, uint64_t desc_cap) {
+                                              uint4 *__restrict__ desc, uint64_t desc_cap, uint4 *__restrict__ ldesc,
+                                              uint32_t long_min) {
   __shared__ DescLds lds_all[4];
   const int lane = threadIdx.x & (kWave - 1);
   DescLds &L = lds_all[threadIdx.x / kWave];
@@ -738,9 +788,21 @@ __global__ __launch_bounds__(256) void k_desc(Outputs o, uint32_t n, const uint6
       }
       const uint64_t at = valid ? L.run[j] + (si - part.y) : 0;
       const bool seg_end = __shfl_down(seg, 1, kWave) != seg || lane == kWave - 1;
+      // a long part goes to k_longcopy's list (any order: each is copied on
+      // its own); its place in the window copy's list keeps its output
+      // position with no entries (a gap the window copy skips)
+      const bool lng = valid && part.y >= long_min;
+      const uint64_t lm = __ballot(lng);
+      uint64_t lbase = 0;
+      if (lm) {
+        if (lane == 0) lbase = atomicAdd(&o.ctr->n_long, (unsigned long long)__popcll(lm));
+        lbase = shfl64(lbase, 0);
+      }
       wave_lds_sync();
       if (valid) {
-        put_checked(desc, pb + k, desc_cap, make_uint4(part.x, part.y, (uint32_t)at, (uint32_t)(at >> 32)), &o.ctr->oob);
+        const uint4 dv = make_uint4(part.x, part.y, (uint32_t)at, (uint32_t)(at >> 32));
+        put_checked(desc, pb + k, desc_cap, lng ? make_uint4(part.x, 0u, dv.z, dv.w) : dv, &o.ctr->oob);
+        if (lng) put_checked(ldesc, lbase + __popcll(lm & lanemask_lt(lane)), desc_cap, dv, &o.ctr->oob);
         if (seg_end) L.run[j] += si;
       }
       wave_lds_sync();
@@ -823,6 +885,7 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
       L.en[lane] = (uint32_t)(b - g0);
       L.src[lane] = d.x + (uint32_t)(a - dst);
       wave_lds_sync();
+      uint64_t nem;  // blocks of 64 positions some descriptor of this batch covers (others: gaps)
       {  // block lane (positions lane * 64 ..): the last descriptor starting at or before its start
         static_assert(kWin / kWave == kWave, "one block per lane");
         const uint32_t q = (uint32_t)lane * kWave;
@@ -830,14 +893,29 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
 #pragma unroll
         for (uint32_t step = 32; step > 0; step >>= 1) k = L.st[k + step] <= q ? k + step : k;
         L.blk[lane] = k;
+        // covered: that descriptor runs past the block start, or the next one
+        // starts inside the block (the long parts k_longcopy takes are gaps
+        // here: a step over them does no search, load or store)
+        nem = __ballot(L.en[k] > q || (k + 1 < (uint32_t)kWave && L.st[k + 1] < q + kWave && L.st[k + 1] < L.en[k + 1]));
       }
       wave_lds_sync();
       const uint32_t q0 = (uint32_t)(pos - g0), q1 = (uint32_t)(bend - g0);
       for (uint32_t base = q0; base < q1; base += kWave * kCU) {
         uint32_t sa[kCU];
         bool in[kCU];
+        uint32_t rows = 0;  // rows u (positions base + u * 64 + lane) that touch a covered block
 #pragma unroll
         for (int u = 0; u < kCU; u++) {
+          const uint32_t r0 = base + u * kWave, b1 = min(r0, (uint32_t)kWin - 1) / kWave,
+                         b2 = min(r0 + kWave - 1, (uint32_t)kWin - 1) / kWave;
+          if (r0 < q1 && (((nem >> b1) | (nem >> b2)) & 1ull)) rows |= 1u << u;
+        }
+        if (!rows) continue;  // a gap step (wave-uniform)
+#pragma unroll
+        for (int u = 0; u < kCU; u++) {
+          in[u] = false;
+          sa[u] = 0;
+          if (!((rows >> u) & 1u)) continue;  // (wave-uniform)
           const uint32_t q = base + u * kWave + lane;
           // the last descriptor starting at or before q: within [blk[b], blk[b + 1]]
           const uint32_t bq = min(q, (uint32_t)kWin - 1) / kWave;
@@ -856,7 +934,8 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
         }
         uint32_t v[kCU];
 #pragma unroll
-        for (int u = 0; u < kCU; u++) v[u] = __builtin_amdgcn_raw_buffer_load_b32(words, (int)(sa[u] * 4u), 0, 0);
+        for (int u = 0; u < kCU; u++)
+          v[u] = ((rows >> u) & 1u) ? __builtin_amdgcn_raw_buffer_load_b32(words, (int)(sa[u] * 4u), 0, 0) : 0u;
 #pragma unroll
         for (int u = 0; u < kCU; u++) {
           if (!in[u]) continue;
@@ -870,6 +949,65 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
       wave_lds_sync();
       pos = bend;
       j += kWave;
+    }
+  }
+}
+
+// ---- k_longcopy: the long solo parts, a wavefront per part ------------------
+// A solo part is a run of `words` copied as it stands (its entries are their
+// clients' deliveries).  The window copy above pays a descriptor search and a
+// 4-B load and store per entry; a part of >= long_min entries (C3: 0.16 parts
+// of >= 256 entries per topic hold 61 % of the solo entries, tools/walk_census)
+// is instead moved by one wavefront with 16-B stores aligned on the output
+// (the 4-word units inside the part) and 16-B loads at the matching source
+// offset (dword-aligned: `words` and `dout` shift by different amounts), its
+// first and last partial units word by word.  4 units per lane in flight.
+__global__ __launch_bounds__(kWave *kEmitWaves) void k_longcopy(DeviceSnapshot s, const uint4 *__restrict__ ldesc,
+                                                              const unsigned long long *__restrict__ nl_ptr,
+                                                              uint64_t lcap, uint32_t *__restrict__ out, uint64_t cap,
+                                                              unsigned int *oob) {
+  const uint64_t nl = min((uint64_t)*nl_ptr, lcap);
+  const int lane = threadIdx.x & (kWave - 1);
+  const __amdgpu_buffer_rsrc_t words =
+      __builtin_amdgcn_make_buffer_rsrc((void *)s.words, (short)0, (int)(s.n_subs * 4u + 64u), 0x00020000);
+  const uint64_t nw = (uint64_t)gridDim.x * kEmitWaves;
+  constexpr int kU = 4;
+  for (uint64_t i = (uint64_t)blockIdx.x * kEmitWaves + threadIdx.x / kWave; i < nl; i += nw) {
+    const uint4 d = ldesc[i];
+    const uint64_t dst = d.z | ((uint64_t)d.w << 32), e = dst + d.y, a = dst & ~3ull;
+    const uint64_t units = (e - a + 3) >> 2;
+    const uint32_t src = d.x;
+    for (uint64_t u0 = 0; u0 < units; u0 += (uint64_t)kWave * kU) {
+      uint4 v[kU];
+      bool full[kU];
+#pragma unroll
+      for (int k = 0; k < kU; k++) {
+        const uint64_t unit = u0 + (uint64_t)k * kWave + lane, w0 = a + 4 * unit;
+        full[k] = unit < units && w0 >= dst && w0 + 4 <= e;
+        if (full[k]) {
+          const auto x = __builtin_amdgcn_raw_buffer_load_b128(words, (int)(4u * (src + (uint32_t)(w0 - dst))), 0, 0);
+          v[k] = make_uint4(x[0], x[1], x[2], x[3]);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kU; k++) {
+        const uint64_t unit = u0 + (uint64_t)k * kWave + lane, w0 = a + 4 * unit;
+        if (unit >= units) continue;
+        if (full[k]) {
+          if (w0 + 4 <= cap)
+            *reinterpret_cast<uint4 *>(out + w0) = v[k];
+          else
+            atomicOr(oob, kOobStore);
+        } else {  // the part's first or last unit: the words inside it
+#pragma unroll
+          for (int z = 0; z < 4; z++) {
+            const uint64_t p = w0 + z;
+            if (p < dst || p >= e) continue;
+            const uint32_t x = __builtin_amdgcn_raw_buffer_load_b32(words, (int)(4u * (src + (uint32_t)(p - dst))), 0, 0);
+            put_checked(out, p, cap, x, oob);
+          }
+        }
+      }
     }
   }
 }
@@ -900,6 +1038,18 @@ __global__ __launch_bounds__(256) void k_nflags(const NodeDesc *__restrict__ nod
                                                 uint64_t n) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     f[i] = (uint8_t)(nodes[i].sh_cnt_flags >> 24);
+}
+
+// slot i = {node i, its '+' child (zeros without one)} (snapshot.h DeviceSnapshot::slots)
+__global__ __launch_bounds__(256) void k_slots(const NodeDesc *__restrict__ nodes, NodeDesc *__restrict__ slots,
+                                               uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const NodeDesc d = load_desc(nodes + i);
+    NodeDesc p{kNone, kNone, 0, 0, 0, 0, 0, 0};
+    if (d.plus != kNone && d.plus < n) p = load_desc(nodes + d.plus);
+    slots[2 * i] = d;
+    slots[2 * i + 1] = p;
+  }
 }
 
 __global__ __launch_bounds__(256) void k_words(const SubEnt *__restrict__ subs, uint32_t *__restrict__ words,
@@ -1257,6 +1407,20 @@ __global__ __launch_bounds__(kBigThreads) void k_multi_part(DeviceSnapshot s, Ou
 // ms against a threshold of 769).  Read at every batch (a test compares modes in one process):
 // MQM_RESOLVE=1 every light topic, MQM_RESOLVE=0 none,
 // MQM_RESOLVE_MIN=m the threshold.
+static bool walk_slots() {
+  static const bool v = !(getenv("MQM_NO_SLOTS") && atoi(getenv("MQM_NO_SLOTS")) != 0);
+  return v;
+}
+// solo parts of at least this many entries take k_longcopy (MQM_LONG_PART:
+// A/B; 0 = none)
+constexpr uint32_t kLongPartDefault = 256;
+static uint32_t long_part_min() {
+  if (const char *v = getenv("MQM_LONG_PART")) {
+    const long x = atol(v);
+    return x <= 0 ? 0xFFFFFFFFu : (uint32_t)x;
+  }
+  return kLongPartDefault;
+}
 constexpr uint32_t kResolveMinDefault = 193;
 static uint32_t resolve_min() {
   if (const char *v = getenv("MQM_RESOLVE")) return atoi(v) != 0 ? 1u : 0xFFFFFFFFu;
@@ -2116,10 +2280,14 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
     // C3 walk 5.76 -> 5.19 ms, C4 shard 6.22 -> 5.57 (r04an, r04ao; 16 at a
     // time 5.37, 1 at a time 7.53: the counter's atomics serialise); the fixed
     // stride for batches whose counter could pass 2^32
-    if (n < (1u << 31))
+    // (MQM_NO_SLOTS=1: the round-4 walk, 32-B descriptor loads from `nodes`, for A/B)
+    if (n >= (1u << 31))
+      hipLaunchKernelGGL(k_walk<kWalkG>, dim3(blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o);
+    else if (walk_slots())
       hipLaunchKernelGGL((k_walk<kWalkG, 4>), dim3(blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o);
     else
-      hipLaunchKernelGGL(k_walk<kWalkG>, dim3(blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o);
+      hipLaunchKernelGGL((k_walk<kWalkG, 4, false>), dim3(blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs,
+                         n, o);
   }
   HIP_TRY(hipGetLastError());
   mark(ws, 1, st);
@@ -2198,7 +2366,8 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
     tab_cap = std::max<uint64_t>(cap_of(W::kTable, sizeof(GEnt)), 1u << 16);
   }
   if (ws.get(W::kDOut, sizeof(uint32_t) * (dcap + 1)) || ws.get(W::kHOut, sizeof(uint32_t) * (hcap + 1)) ||
-      ws.get(W::kDesc, sizeof(uint4) * (desc_cap + 1)) || ws.get(W::kWin, sizeof(uint32_t) * (win_cap + 1)))
+      ws.get(W::kDesc, sizeof(uint4) * (desc_cap + 1)) || ws.get(W::kWin, sizeof(uint32_t) * (win_cap + 1)) ||
+      (!ws.runs && ws.get(W::kLDesc, sizeof(uint4) * (desc_cap + 1))))
     return -2;
   o.dout = (uint32_t *)ws.ptr(W::kDOut);
   o.hout = (uint32_t *)ws.ptr(W::kHOut);
@@ -2301,8 +2470,14 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
     }
     // the solo copy (none in the runs form: the solo parts stay runs)
     if (!ws.runs) {
+      auto *ldesc = (uint4 *)ws.ptr(W::kLDesc);
+      if (!ldesc) return -1;
       hipLaunchKernelGGL(k_desc, dim3(std::min<uint32_t>((n + 255) / 256, 8192)), dim3(256), 0, st, o, n, desc_start,
-                         desc, desc_cap);  // a wavefront per 64 topics
+                         desc, desc_cap, ldesc, long_part_min());  // a wavefront per 64 topics
+      HIP_TRY(hipGetLastError());
+      // the long parts (their own list, 16-B moves) before the window copy of the rest
+      hipLaunchKernelGGL(k_longcopy, grid(k_longcopy), dim3(kWave * kEmitWaves), 0, st, s, ldesc, &o.ctr->n_long,
+                         desc_cap, o.dout, o.dcap, &o.ctr->oob);
       HIP_TRY(hipGetLastError());
       if (!exact || hc->n_desc > 0) {
         const uint64_t nd_grid = exact ? hc->n_desc : desc_cap;
@@ -2528,6 +2703,13 @@ int derive_node_flags(const NodeDesc *nodes, uint8_t *nflags, uint64_t n, hipStr
   if (n)
     hipLaunchKernelGGL(k_nflags, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 16384)), dim3(256), 0, st, nodes,
                        nflags, n);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+int derive_slots(const NodeDesc *nodes, NodeDesc *slots, uint64_t n, hipStream_t st) {
+  if (n)
+    hipLaunchKernelGGL(k_slots, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 16384)), dim3(256), 0, st, nodes,
+                       slots, n);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

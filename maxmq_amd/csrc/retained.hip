@@ -76,6 +76,10 @@ struct RevCtr {
   unsigned int pad;
   unsigned long long items[1];    // [levels + 1]
 };
+// MQM_REV_STATS=1: per level d < kStatLevels, the mix of its items (after the
+// counters in the same buffer) — live items, literal probes, children listed
+// by wildcard expansions, edges of the literal-edge index's ranges, emissions
+constexpr uint32_t kStatLevels = 16, kStatKinds = 5;
 
 __device__ __forceinline__ uint32_t level_type(const Level &l) {
   if (l.k1 != (1ull << 56)) return kTypeLiteral;
@@ -218,6 +222,7 @@ struct LevelArgs {
   Emit *emit;
   uint64_t emit_cap;
   RevCtr *ctr;
+  unsigned long long *st;           // MQM_REV_STATS: the levels' item mix [kStatLevels][kStatKinds], else null
 };
 
 // a thread per item of level d; the loop is grid-stride over the level's
@@ -306,6 +311,16 @@ __global__ __launch_bounds__(kThreads) void k_level(LevelArgs a) {
           e0 = Emit{f, 0, r.cum[p + 1], r.cum[end]};
           ne = e0.hi > e0.lo;
         }
+      }
+    }
+    if (a.st && a.d < kStatLevels) {  // the level's item mix (MQM_REV_STATS)
+      const bool is_lit = p != kNone && ch_hi == ch_lo && rg_hi == rg_lo && (nx_one != kNone || ne <= 1) &&
+                          (a.wild[f] == 0 || level_type(a.lv[a.loff[f] + a.d]) == kTypeLiteral);
+      const uint64_t v[5] = {p != kNone ? 1u : 0u, is_lit ? 1u : 0u, ch_hi - ch_lo, rg_hi - rg_lo, ne};
+      for (int k = 0; k < 5; k++) {
+        uint64_t tot;
+        (void)wave_excl(v[k], &tot);
+        if (lane == 0 && tot) atomicAdd(&a.st[a.d * kStatKinds + k], (unsigned long long)tot);
       }
     }
     // next-level items: one per literal hit, the child list of a wildcard
@@ -634,9 +649,11 @@ int messages_device(const DeviceSnapshot &s, const DeviceRetained *r, Workspace 
       return -2;
     // levels 0 .. height: an item of level d sits on a node of depth d
     const uint32_t max_levels = s.height + 1;
-    if (ws.get(W::kRNCount, ctr_bytes(max_levels + 1))) return -2;
+    const size_t st_at = (ctr_bytes(max_levels + 1) + 15) & ~size_t(15);
+    const size_t st_bytes = sizeof(unsigned long long) * kStatLevels * kStatKinds;
+    if (ws.get(W::kRNCount, st_at + st_bytes)) return -2;
     auto *ctr = (RevCtr *)ws.ptr(W::kRNCount);
-    HIP_TRY(hipMemsetAsync(ctr, 0, ctr_bytes(max_levels + 1), st));
+    HIP_TRY(hipMemsetAsync(ctr, 0, st_at + st_bytes, st));
     HIP_TRY(hipMemsetAsync(ws.ptr(W::kRFCount), 0, sizeof(uint64_t) * (n + 1), st));
     HIP_TRY(hipMemsetAsync(ws.ptr(W::kRFCur), 0, sizeof(uint64_t) * (n + 1), st));
     LevelArgs a{};
@@ -653,6 +670,8 @@ int messages_device(const DeviceSnapshot &s, const DeviceRetained *r, Workspace 
     a.emit = (Emit *)ws.ptr(W::kREmit);
     a.emit_cap = emit_cap;
     a.ctr = ctr;
+    static const bool rev_stats = getenv("MQM_REV_STATS") && atoi(getenv("MQM_REV_STATS")) != 0;
+    a.st = rev_stats ? reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(ctr) + st_at) : nullptr;
     // level L's list lives in buffer pair L % 3 (a level appends to the next
     // two: wildcard + literal through the edge index jumps one level)
     const W::Slot lf[3] = {W::kRItemF0, W::kRItemF1, W::kRChild}, ln[3] = {W::kRItemN0, W::kRItemN1, W::kRECount};
@@ -698,6 +717,14 @@ int messages_device(const DeviceSnapshot &s, const DeviceRetained *r, Workspace 
     const uint64_t n_refs = hp[15];
     const unsigned ovf = hc->ovf;
     const uint64_t n_emit = hc->n_emit, n_tasks = hc->n_tasks, need_items = hc->need_items;
+    if (ovf == 0 && a.st) {
+      unsigned long long sv[kStatLevels * kStatKinds];
+      HIP_TRY(hipMemcpy(sv, a.st, sizeof(sv), hipMemcpyDeviceToHost));
+      fprintf(stderr, "[rev-stats] level live literal expand_children index_edges emissions\n");
+      for (uint32_t d = 0; d < std::min<uint32_t>(max_levels, kStatLevels); d++)
+        fprintf(stderr, "[rev-stats] %u %llu %llu %llu %llu %llu\n", d, sv[d * kStatKinds], sv[d * kStatKinds + 1],
+                sv[d * kStatKinds + 2], sv[d * kStatKinds + 3], sv[d * kStatKinds + 4]);
+    }
     if (ovf == 0) {
       out->n_refs = n_refs;
       out->refs = refs_out;

@@ -127,6 +127,14 @@ constexpr uint32_t kMaxPartners = 15;
 
 struct DeviceSnapshot {
   const NodeDesc *nodes;
+  // paired node slots, 64 B per node (derived on the device at upload):
+  // slots[i] = {nodes[i], nodes[nodes[i].plus] (zeros without a '+' child)}.
+  // The batch walk loads a '+' / '#' child's slot instead of its descriptor —
+  // the same one 64-B sector, so the same one DRAM request — and gets that
+  // child's own '+' child's descriptor with it: the next level's '+' item
+  // then costs no load (C3: 2.1 of the 4.9 '+' loads per topic, and the
+  // root's '+' child for every topic; tools/walk_census CENSUS_SLOTS=1)
+  const NodeDesc *slots;
   const EdgeEntry *edges;
   const SubEnt *subs;
   const uint32_t *words;  // n_subs: subs[i].word & kPackedMask (the entry's own delivery)

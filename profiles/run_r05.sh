@@ -3,6 +3,10 @@
 # time limit, chained so that the first failure ends the call.
 #   tests   : every -m gpu test                          -> gpurun_out/TAG/pytest_gpu.log
 #   serve   : the per-publish server tests (incl. served calls under Subscribe/Unsubscribe churn)
+#   ab / c4ab: `fast` (C3) / the C4 shard bench with the round-5 walk (paired node slots) and long-part
+#             copy, then each switched off (MQM_NO_SLOTS=1, MQM_LONG_PART=0)
+#   revstats: the C5 reverse bench with the per-level item mix (MQM_REV_STATS=1)
+#   churnserve: the churn workload with the served-calls-under-churn leg
 #   c4test  : the C4 shard 0/8 full-batch test            -> gpurun_out/TAG/pytest_c4.log
 #   ret     : the retained (reverse-match) tests           -> gpurun_out/TAG/pytest_ret.log
 #   nobloom : the edge-case / random-op parity tests with the edge filter off (MQM_NO_BLOOM=1)
@@ -42,6 +46,19 @@ for step in "$@"; do
     tests) timeout -k 10 1000 $PYT tests -m gpu --timeout 600 --durations=15 > $OUT/pytest_gpu.log 2>&1 ;;
     serve) timeout -k 10 600 $PYT tests/test_gpu_serve.py tests/test_gpu_serve_churn.py tests/test_gpu_shim.py -m gpu \
              --timeout 300 > $OUT/pytest_serve.log 2>&1 ;;
+    ab) for V in base:X=0 noslots:MQM_NO_SLOTS=1 nolong:MQM_LONG_PART=0; do
+          N=${V%%:*}; E=${V#*:}
+          env $E timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_$N.json 2> $OUT/bench_fast_$N.log || exit 1
+        done ;;
+    c4ab) for V in base:X=0 noslots:MQM_NO_SLOTS=1 nolong:MQM_LONG_PART=0; do
+          N=${V%%:*}; E=${V#*:}
+          env $E timeout -k 10 600 python3 -u bench.py --config 4 --shard 0/8 $FAST > $OUT/bench_c4_$N.json \
+            2> $OUT/bench_c4_$N.log || exit 1
+        done ;;
+    revstats) MQM_REV_STATS=1 timeout -k 10 600 python3 -u bench.py --workload reverse --steps 2 --warmup 1 \
+             --no-cpu-baseline > $OUT/bench_rev_stats.json 2> $OUT/bench_rev_stats.log ;;
+    churnserve) timeout -k 10 900 python3 -u bench.py --workload churn --steps 3 --warmup 1 --serve-churn-s 20 \
+             > $OUT/bench_churn.json 2> $OUT/bench_churn.log ;;
     c4test) timeout -k 10 600 $PYT tests/test_gpu_c4_shard.py -m gpu --timeout 500 > $OUT/pytest_c4.log 2>&1 ;;
     ret) timeout -k 10 600 $PYT tests/test_gpu_retained.py -m gpu --timeout 300 > $OUT/pytest_ret.log 2>&1 ;;
     nobloom) MQM_NO_BLOOM=1 timeout -k 10 400 $PYT tests/test_gpu_parity.py -m gpu --timeout 200 \

@@ -17,13 +17,17 @@ from tools import mqgen
 
 
 def _rows(res):
-    """per topic: sorted deliveries, sorted shared candidates, sorted idents"""
+    """per topic: sorted deliveries, sorted shared candidates, and every
+    delivery's Identifiers map (packets.go:250-259) — the maps, not the listed
+    sids: the batch pipeline lists only the identified entries of clients with
+    several gathered subscriptions (a solo delivery's map is its first pair),
+    the per-publish paths list every identified entry (include/mqmatch.h)"""
     out = []
     for i in range(res.n):
         d = res.deliveries[int(res.offsets[i]):int(res.offsets[i + 1])]
         s = res.shared[int(res.shared_offsets[i]):int(res.shared_offsets[i + 1])]
         ids = () if res.idents is None else tuple(sorted(
-            int(x) for x in res.idents[int(res.ident_offsets[i]):int(res.ident_offsets[i + 1])]))
+            (c, tuple(sorted(m.items()))) for c, m in res.identifiers(i).items()))
         out.append((tuple(sorted((int(c), int(p)) for c, p in zip(d["client"], d["packed"]))),
                     tuple(sorted(int(x) for x in s)), ids))
     return out

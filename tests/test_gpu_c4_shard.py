@@ -6,7 +6,7 @@ per-GPU unit of a node step: shard 0 of the 8-way client-range split
 
 C4 is the config that drove the widest merges before '#' subscriptions after a
 literal parent became solo (kFlagParentLit, snapshot.h): with the old marking
-(MQM_HASH_MULTI=1, a second index of the same shard) hub topics carry
+(MQM_HASH_MULTI=1, the same store flattened again) hub topics carry
 thousands of multi entries (the k_multi<4096> tier); the test
 asserts the k_multi<4096> tier ran there and that both markings give the same
 result for every topic (per-topic counts, and checksums over (client, first
@@ -148,16 +148,20 @@ def test_config4_shard0of8_full_batch():
     assert len(g) > 1_000_000
     assert_same(g, ref, "C4 shard 0/8 deliveries (sample)")
     assert_same(gs, rs, "C4 shard 0/8 shared (sample)")
-    idx.close()
-    del idx
     # the old marking ('#' subscriptions after a literal parent multi): the wide
-    # merge tiers and the DFS path under load, and the same result per topic
+    # merge tiers and the DFS path under load, and the same result per topic.
+    # The same store is flattened again with MQM_HASH_MULTI=1 (read at
+    # flatten time): a Subscribe + Unsubscribe of a path no topic reaches moves
+    # the store version (a commit at an unchanged version is a no-op) and
+    # leaves the trie as it was (its names intern after every existing id), so
+    # no second 12.5M-filter store is built
     import os
 
+    idx_h = idx
+    assert idx_h.subscribe("zz-marking-probe", maxmq_amd.Subscription("zz/marking/probe", 0))
+    assert idx_h.unsubscribe("zz/marking/probe", "zz-marking-probe")
     os.environ["MQM_HASH_MULTI"] = "1"
     try:
-        idx_h = maxmq_amd.TopicsIndex(0, autocommit=False)
-        idx_h.subscribe_workload(w)
         idx_h.commit()
     finally:
         del os.environ["MQM_HASH_MULTI"]

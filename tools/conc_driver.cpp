@@ -154,3 +154,119 @@ int64_t mqd_host_path(const mqd_host_api *api, void *h, const char *bytes, const
   return failed.load() ? -1 : ns;
 }
 }
+
+// ---- per-publish calls while subscriptions change (bench.py serve_churn) --
+// `threads` native callers make mqm_subscribers calls for `seconds` while one
+// mutator thread runs Subscribe / Unsubscribe at `rate` per second (the
+// reference takes both concurrently: Subscribe under the trie's root mutex,
+// server.go:1013 / topics.go:303-321, beside one Subscribers goroutine per
+// connection, server.go:776).  Mutation k: even k subscribes pair k/2 mod m,
+// odd k unsubscribes pair (k/2 + m/2) mod m (about half the pairs present at
+// any time).  Recorded: every call's latency (ns, saturated to u32), and per
+// sampled call (every `sample`-th) its return time (us since the start) and
+// result snapshot version; per mutation its time (us) and the store version
+// after it.  -> wall ns, or -1 if a call failed.
+extern "C" {
+typedef uint64_t (*version_fn)(const void *r);
+typedef int (*subscribe_fn)(void *h, const char *c, size_t cl, const char *f, size_t fl, const void *sub, int *is_new);
+typedef int (*unsubscribe_fn)(void *h, const char *f, size_t fl, const char *c, size_t cl, int *existed);
+typedef int (*state_fn)(void *h, void *state);
+struct mqd_churn_api {
+  subscribers_fn subscribers;
+  offsets_fn offsets;
+  free_fn result_free;
+  version_fn version;
+  subscribe_fn subscribe;
+  unsubscribe_fn unsubscribe;
+  state_fn state;
+};
+struct mqd_churn_out {
+  uint64_t calls, deliveries, mutations, failed_mutations;
+};
+
+int64_t mqd_serve_churn(const mqd_churn_api *api, void *h, const char *bytes, const uint64_t *offs, uint32_t n,
+                        int threads, double seconds, uint32_t cap_per_thread, uint32_t sample, const char *cbytes,
+                        const uint64_t *coffs, const char *fbytes, const uint64_t *foffs, uint32_t m, double rate,
+                        uint32_t *lat_ns, uint32_t *calls_done, uint32_t *s_t_us, uint64_t *s_ver,
+                        uint64_t mut_cap, uint32_t *m_t_us, uint64_t *m_ver, mqd_churn_out *out) {
+  std::atomic<int> ready{0}, failed{0};
+  std::atomic<bool> go{false}, stop{false};
+  std::atomic<uint64_t> dsum{0}, nmut{0}, mfail{0};
+  std::vector<std::thread> ths;
+  using clk = std::chrono::steady_clock;
+  clk::time_point t0;
+  const uint32_t per_s = cap_per_thread / (sample ? sample : 1) + 1;
+  for (int k = 0; k < threads; k++) {
+    ths.emplace_back([&, k] {
+      ready++;
+      while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
+      uint64_t d = 0;
+      uint32_t j = 0;
+      for (; j < cap_per_thread && !stop.load(std::memory_order_relaxed); j++) {
+        const uint32_t t = (uint32_t)(((uint64_t)k * 7919u + (uint64_t)j * 104729u) % n);
+        void *res = nullptr;
+        const auto a = clk::now();
+        if (api->subscribers(h, bytes + offs[t], offs[t + 1] - offs[t], &res) != 0) {
+          failed++;
+          break;
+        }
+        const auto b = clk::now();
+        d += api->offsets(res)[1];
+        const uint64_t ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
+        lat_ns[(uint64_t)k * cap_per_thread + j] = ns > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)ns;
+        if (sample && j % sample == 0) {
+          const uint64_t si = (uint64_t)k * per_s + j / sample;
+          s_t_us[si] = (uint32_t)std::chrono::duration_cast<std::chrono::microseconds>(b - t0).count();
+          s_ver[si] = api->version(res);
+        }
+        api->result_free(res);
+      }
+      calls_done[k] = j;
+      dsum += d;
+    });
+  }
+  std::thread mut([&] {
+    while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
+    if (rate <= 0 || m == 0) return;
+    const uint8_t sub[8] = {1, 0, 0, 0, 0, 0, 0, 0};  // mqm_subscription: QoS 1, Identifier 0
+    struct {
+      uint64_t store_version, snapshot_version, pending_ops, builds, last_build_ops;
+      double last_build_ms;
+      int32_t has_snapshot, building;
+    } st;
+    for (uint64_t k = 0; k < mut_cap && !stop.load(std::memory_order_relaxed); k++) {
+      if ((k & 63) == 0) {  // pace: mutation k is due at t0 + k / rate
+        const auto due = t0 + std::chrono::nanoseconds((int64_t)((double)k * 1e9 / rate));
+        while (clk::now() < due && !stop.load(std::memory_order_relaxed))
+          std::this_thread::sleep_for(std::chrono::microseconds(50));
+      }
+      const uint32_t p = (k & 1) ? (uint32_t)((k / 2 + m / 2) % m) : (uint32_t)((k / 2) % m);
+      int x = 0;
+      const int rc = (k & 1) ? api->unsubscribe(h, fbytes + foffs[p], foffs[p + 1] - foffs[p], cbytes + coffs[p],
+                                                coffs[p + 1] - coffs[p], &x)
+                             : api->subscribe(h, cbytes + coffs[p], coffs[p + 1] - coffs[p], fbytes + foffs[p],
+                                              foffs[p + 1] - foffs[p], sub, &x);
+      if (rc != 0) mfail++;
+      api->state(h, &st);
+      m_t_us[k] = (uint32_t)std::chrono::duration_cast<std::chrono::microseconds>(clk::now() - t0).count();
+      m_ver[k] = st.store_version;
+      nmut++;
+    }
+  });
+  while (ready.load() < threads) std::this_thread::yield();
+  t0 = clk::now();
+  go.store(true, std::memory_order_release);
+  std::this_thread::sleep_for(std::chrono::duration<double>(seconds));
+  stop.store(true, std::memory_order_release);
+  for (auto &t : ths) t.join();
+  mut.join();
+  const int64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - t0).count();
+  uint64_t calls = 0;
+  for (int k = 0; k < threads; k++) calls += calls_done[k];
+  out->calls = calls;
+  out->deliveries = dsum.load();
+  out->mutations = nmut.load();
+  out->failed_mutations = mfail.load();
+  return failed.load() ? -1 : ns;
+}
+}

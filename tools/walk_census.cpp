@@ -13,6 +13,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -63,6 +64,10 @@ int main(int argc, char **argv) {
   if (flatten(st, &hs) != 0) return 2;
   uint64_t n_lit = 0, n_plus = 0, n_plus_leaf = 0, n_plus_leaf_empty = 0, n_hash = 0, n_topics = 0;
   uint64_t n_lit_filtered = 0;
+  uint64_t part_hist[8] = {}, entry_hist[8] = {};  // solo parts by length: count, entries
+  uint64_t n_plus_after_wild = 0, n_plus_after_root = 0;  // '+' items pushed by a node reached through '+' / '#'
+  uint64_t n_plus_free = 0;  // paired slots: '+' items whose descriptor came with the parent's slot
+  const bool slots = getenv("CENSUS_SLOTS") != nullptr;
   std::vector<uint32_t> cur, nxt;  // item: id << 2 | kind (0 literal probe of id, 1 '+' node id, 2 '#' node id)
   for (uint64_t t = 0; t < w.topics.n; t++) {
     const char *tb = w.topics.bytes + w.topics.offs[t];
@@ -95,6 +100,7 @@ int main(int argc, char **argv) {
           c = e->child;
           dc = e->desc;
         } else {
+          if (kind == 3) n_plus_free++;
           if (kind == 1) {
             n_plus++;
             const NodeDesc &pd = hs.nodes[id];
@@ -111,6 +117,26 @@ int main(int argc, char **argv) {
           dc = hs.nodes[id];
         }
         const uint32_t fl = dc.sh_cnt_flags >> 24;
+        {  // the solo part this visit gathers (approximate: the '#' double-gather rules aside)
+          const uint32_t solo = dc.sub_cnt - std::min<uint32_t>(dc.sub_cnt, dc.multi & 0xFFFFu);
+          if (solo && !(kind == 2 && (fl & kFlagParentLit))) {
+            int b = 0;
+            while (b < 7 && solo >= (16u << (2 * b))) b++;  // <16, <64, <256, <1K, <4K, <16K, <64K, more
+            part_hist[b]++;
+            entry_hist[b] += solo;
+          }
+          // the '#' child's range: the next level's '#' probe when the topic
+          // continues, else the parent-'#' probe after a literal (topics.go:503-509)
+          if (dc.hash != kNone && (has_next || kind == 0)) {
+            const uint32_t hs_solo = dc.hsub_cnt - std::min<uint32_t>(dc.hsub_cnt, dc.multi >> 16);
+            if (hs_solo) {
+              int b = 0;
+              while (b < 7 && hs_solo >= (16u << (2 * b))) b++;
+              part_hist[b]++;
+              entry_hist[b] += hs_solo;
+            }
+          }
+        }
         if (!(has_next && (fl & kFlagHasChildren))) continue;
         if ((fl & kFlagHasLiteral) && d + 1 < 16) {
           if (bloom_pass(hs, c, keys[d + 1]))
@@ -118,7 +144,14 @@ int main(int argc, char **argv) {
           else
             n_lit_filtered++;
         }
-        if (dc.plus != kNone) nxt.push_back(dc.plus << 2 | 1);
+        if (dc.plus != kNone) {
+          // paired node slots: a node LOADED from the node array (kind 1 or 2)
+          // brings its '+' child's descriptor in the same 64-B slot -> kind 3 (free)
+          const bool free_plus = slots && (kind == 1 || kind == 2);
+          nxt.push_back(dc.plus << 2 | (free_plus ? 3u : 1u));
+          if (kind != 0) n_plus_after_wild++;  // parent's descriptor came from a node load, not an edge probe
+          else if (it == (0u << 2 | 0) && d == 0) n_plus_after_root++;
+        }
         if (dc.hash != kNone && !(fl & kFlagHashLeaf)) nxt.push_back(dc.hash << 2 | 2);
       }
       std::swap(cur, nxt);
@@ -130,6 +163,15 @@ int main(int argc, char **argv) {
          "\"hash_loads\": %.3f}}\n",
          config, (unsigned long long)p.n_filters, (unsigned long long)n_topics, hs.nodes.size(), n_lit / n,
          n_lit_filtered / n, n_plus / n, n_plus_leaf / n, n_plus_leaf_empty / n, n_hash / n);
+  printf("'+' items pushed by a node whose descriptor came from a '+'/'#' node load: %.3f per topic\n",
+         n_plus_after_wild / n);
+  if (slots) printf("paired slots: '+' loads %.3f + free '+' items %.3f per topic\n", n_plus / n, n_plus_free / n);
+  const char *bn[8] = {"<16", "<64", "<256", "<1K", "<4K", "<16K", "<64K", ">=64K"};
+  uint64_t te = 0;
+  for (int b = 0; b < 8; b++) te += entry_hist[b];
+  printf("solo parts by length (per topic: parts, entries, share of entries)\n");
+  for (int b = 0; b < 8; b++)
+    printf("  %-6s %8.3f %10.2f %6.3f\n", bn[b], part_hist[b] / n, entry_hist[b] / n, te ? (double)entry_hist[b] / te : 0.0);
   mqgen_free(&w);
   return 0;
 }
