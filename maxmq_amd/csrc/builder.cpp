@@ -195,8 +195,8 @@ void Builder::run() {
         log.replay(shadow_);
         replayed = true;
         auto hs = std::make_shared<HostSnapshot>();
-        hs->version = version;
         rc = fault == 2 ? MQM_ENOMEM : flatten(shadow_, hs.get());
+        hs->version = version;  // (after flatten, which starts from an empty snapshot)
         if (rc == MQM_OK && device_ >= 0 && !stream_) rc = MQM_EHIP;
         if (rc == MQM_OK) rc = fault == 3 ? MQM_ENOMEM : upload(std::move(hs), device_, stream_, &b.snap);
       } catch (const std::bad_alloc &) {

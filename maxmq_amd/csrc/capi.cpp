@@ -308,9 +308,9 @@ int commit_locked(mqm_index *h) {
     return h->snap && h->snap_version == h->store.version() ? MQM_OK : MQM_EINVAL;
   }
   auto hs = std::make_shared<HostSnapshot>();
-  hs->version = h->store.version();
   int rc = flatten(h->store, hs.get());
   if (rc != MQM_OK) return rc;
+  hs->version = h->store.version();  // (after flatten, which starts from an empty snapshot; mu held)
   std::unique_ptr<GpuSnapshot> g;
   rc = upload(std::move(hs), h->cfg.device, h->dev.stream, &g);
   if (rc != MQM_OK) return rc;

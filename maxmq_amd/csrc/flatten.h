@@ -63,7 +63,7 @@ struct HostSnapshot {
   std::vector<RevGroup> rgroups;     // DeviceRetained::groups (empty: no index)
   uint32_t sys_child = kNone;
   bool has_empty = false;
-  // the store version this snapshot reflects (set by the committer before
+  // the store version this snapshot reflects (set by the committer after
   // flatten; equal versions mean equal snapshots: flatten is deterministic)
   uint64_t version = 0;
 };

@@ -76,7 +76,7 @@ struct Workspace {
   uint32_t max_blocks = 2048;  // walk-kernel grid cap (grid-stride beyond)
   // reverse match (retained.hip): list capacities carried from call to call
   // (grown when a call's device counters report an overflow)
-  uint64_t rev_item_cap = 0, rev_emit_cap = 0, rev_task_cap = 0, rev_out_cap = 0;
+  uint64_t rev_item_cap = 0, rev_emit_cap = 0, rev_task_cap = 0, rev_out_cap = 0, rev_ltask_cap = 0;
   std::unordered_map<const void *, uint32_t> resident;  // kernel -> resident blocks on the device
   // why the last batch's DFS topics left the bounded path:
   // frontier, hits, cached levels, shared hits, raw entries

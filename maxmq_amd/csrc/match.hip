@@ -12,7 +12,10 @@
 //                   checked against the edge filter when pushed / '+' child /
 //                   '#' child), so a level costs one dependent memory round
 //                   trip (the literal child's descriptor is inline in its
-//                   edge entry).  Hits are compacted with ballot + popcount
+//                   edge entry; a wildcard child's 64-B node slot carries its
+//                   own '+' child's descriptor, which waits in LDS for the
+//                   next level: that '+' item costs no load).  Hits are
+//                   compacted with ballot + popcount
 //                   and written to the topic's record: solo parts (off,
 //                   count), multi parts (off, count, rank = 2 * node + slot,
 //                   the reference's emission order, snapshot.h), shared
@@ -20,10 +23,12 @@
 //   scans     S and H -> each topic's segment start (S bounds its
 //             deliveries, so every later kernel writes final positions).
 //   solo copy k_desc turns the records' solo parts into copy descriptors in
-//             topic order; k_winmap / k_wincopy copy the solo entries (~90 %
-//             of the deliveries: an entry whose client meets no other of its
-//             subscriptions in the topic is its client's merged delivery as
-//             it stands) in fixed windows of the output space.  (Round 4
+//             topic order; k_longcopy moves the long parts (>= 256 entries)
+//             a wavefront each with 16-B stores, k_winmap / k_wincopy copy the
+//             other solo entries (~90 % of the deliveries are solo: an entry
+//             whose client meets no other of its subscriptions in the topic is
+//             its client's merged delivery as it stands) in fixed windows of
+//             the output space, skipping the long parts' gaps.  (Round 4
 //             measured the copy fused into k_walk from LDS-held parts: 15.2
 //             / 17.5 ms per C3 batch at 4 / 3 waves per SIMD against 14.4 ms
 //             this way — the walk's register budget leaves too few loads in
@@ -1412,12 +1417,14 @@ static bool walk_slots() {
   return v;
 }
 // solo parts of at least this many entries take k_longcopy (MQM_LONG_PART:
-// A/B; 0 = none)
+// A/B; 0 = none).  At least 64: k_wincopy's gap test looks at the first
+// descriptor starting inside a 64-position block only, so the part after a
+// long part's (empty) place must start at least a block later
 constexpr uint32_t kLongPartDefault = 256;
 static uint32_t long_part_min() {
   if (const char *v = getenv("MQM_LONG_PART")) {
     const long x = atol(v);
-    return x <= 0 ? 0xFFFFFFFFu : (uint32_t)x;
+    return x <= 0 ? 0xFFFFFFFFu : (uint32_t)std::max(64L, x);
   }
   return kLongPartDefault;
 }

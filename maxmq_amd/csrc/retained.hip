@@ -63,7 +63,19 @@ struct Level {         // one level of one filter
 
 enum : uint32_t { kTypeLiteral = 0, kTypePlus = 1, kTypeHash = 2 };
 
-enum : uint32_t { kOvfItems = 1, kOvfEmit = 2, kOvfTasks = 4, kOvfOut = 8 };
+enum : uint32_t { kOvfItems = 1, kOvfEmit = 2, kOvfTasks = 4, kOvfOut = 8, kOvfLTasks = 16 };
+
+// level tasks (MQM_REV_TASKS=1): the long child lists and the literal-edge
+// index ranges of a level are cut into chunks of at most kTaskEdges and
+// spread over every wavefront of a second launch (k_level_tasks), instead of
+// being worked through by the wavefront that found them, lane after lane
+constexpr uint32_t kTaskEdges = 1024;
+enum : uint32_t { kLTChildren = 0, kLTIndexItems = 1, kLTIndexEmit = 2 };
+struct LTask {
+  uint32_t f, lo, n, need;  // filter, first child / edge, count, node flags the next level needs
+  uint64_t at;              // children: their slots in the next level's list
+  uint32_t kind, root;      // kLT*; the level is the root's ("$SYS" dropped)
+};
 
 // device-side counters of one call (zeroed at its start); items[d] = items
 // appended to level d (d >= 1), the append cursor of that level's list
@@ -74,6 +86,8 @@ struct RevCtr {
   unsigned long long skipped;     // items the reference visits that the edge index jumps over
   unsigned int ovf;               // kOvf* bits
   unsigned int pad;
+  unsigned long long n_ltasks;    // level tasks of the current level (reset before each level)
+  unsigned long long need_ltasks; // most level tasks any level appended (also past the capacity)
   unsigned long long items[1];    // [levels + 1]
 };
 // MQM_REV_STATS=1: per level d < kStatLevels, the mix of its items (after the
@@ -223,6 +237,8 @@ struct LevelArgs {
   uint64_t emit_cap;
   RevCtr *ctr;
   unsigned long long *st;           // MQM_REV_STATS: the levels' item mix [kStatLevels][kStatKinds], else null
+  LTask *ltasks;                    // MQM_REV_TASKS: this level's tasks (nullptr: the wavefront works its own)
+  uint64_t ltask_cap;
 };
 
 // a thread per item of level d; the loop is grid-stride over the level's
@@ -347,6 +363,17 @@ __global__ __launch_bounds__(kThreads) void k_level(LevelArgs a) {
         }
       }
       uint64_t big = __ballot(nx_one == kNone && nn > kCoopItems);
+      if (a.ltasks && big) {  // long child lists: chunks for k_level_tasks
+        const bool mine = nx_one == kNone && nn > kCoopItems;
+        const uint32_t nch = mine ? (nn + kTaskEdges - 1) / kTaskEdges : 0;
+        const uint64_t t0 = wave_reserve(&a.ctr->n_ltasks, nch);
+        if (lane == 63) atomicMax(&a.ctr->need_ltasks, (unsigned long long)(t0 + nch));
+        if (t0 + nch > a.ltask_cap) atomicOr(&a.ctr->ovf, (unsigned)kOvfLTasks);
+        for (uint32_t k = 0; k < nch && t0 + k < a.ltask_cap; k++)
+          a.ltasks[t0 + k] = LTask{f, ch_lo + k * kTaskEdges, min(kTaskEdges, nn - k * kTaskEdges), need,
+                                   at + (uint64_t)k * kTaskEdges, kLTChildren, a.d == 0 ? 1u : 0u};
+        big = 0;
+      }
       while (big) {  // long child lists: the whole wavefront writes each
         const int src = __builtin_ctzll(big);
         big &= big - 1;
@@ -374,6 +401,17 @@ __global__ __launch_bounds__(kThreads) void k_level(LevelArgs a) {
     }
     // index ranges, a wavefront each, 64 edges per step, outputs compacted
     uint64_t rt = __ballot(rg_hi > rg_lo);
+    if (a.ltasks && rt) {  // ... or chunks for k_level_tasks
+      const uint32_t rn = rg_hi - rg_lo;
+      const uint32_t nch = (rn + kTaskEdges - 1) / kTaskEdges;
+      const uint64_t t0 = wave_reserve(&a.ctr->n_ltasks, nch);
+      if (lane == 63) atomicMax(&a.ctr->need_ltasks, (unsigned long long)(t0 + nch));
+      if (t0 + nch > a.ltask_cap) atomicOr(&a.ctr->ovf, (unsigned)kOvfLTasks);
+      for (uint32_t k = 0; k < nch && t0 + k < a.ltask_cap; k++)
+        a.ltasks[t0 + k] = LTask{f, rg_lo + k * kTaskEdges, min(kTaskEdges, rn - k * kTaskEdges), need2, 0,
+                                 rg_emit ? kLTIndexEmit : kLTIndexItems, a.d == 0 ? 1u : 0u};
+      rt = 0;
+    }
     while (rt) {
       const int src = __builtin_ctzll(rt);
       rt &= rt - 1;
@@ -420,6 +458,70 @@ __global__ __launch_bounds__(kThreads) void k_level(LevelArgs a) {
             a.skip_f[pos] = sf;
             a.skip_n[pos] = c;
           }
+        }
+      }
+    }
+  }
+}
+
+// k_level_tasks: a wavefront per task of the level (grid-stride), 64
+// children / edges per step — the same writes k_level's wavefront loops make
+__global__ __launch_bounds__(kThreads) void k_level_tasks(LevelArgs a) {
+  const DeviceRetained &r = a.r;
+  const int lane = threadIdx.x & 63;
+  const uint64_t nt = min((uint64_t)a.ctr->n_ltasks, a.ltask_cap);
+  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / 64);
+  for (uint64_t t = (uint64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; t < nt; t += nw) {
+    const LTask k = a.ltasks[t];
+    if (k.kind == kLTChildren) {
+      const uint32_t skip = k.root ? r.sys_child : kNone;
+      for (uint32_t j = lane; j < k.n; j += 64) {
+        if (k.at + j >= a.item_cap) break;
+        const uint32_t c = r.child_ids[k.lo + j];
+        a.next_f[k.at + j] = k.f;
+        a.next_n[k.at + j] = c == skip || !(r.nflags[c] & k.need) ? kNone : c;
+      }
+      continue;
+    }
+    const bool semit = k.kind == kLTIndexEmit;
+    for (uint32_t j0 = 0; j0 < k.n; j0 += 64) {
+      const uint32_t j = k.lo + j0 + lane;
+      bool valid = j0 + lane < k.n;
+      uint32_t c = 0;
+      Emit em{k.f, 0, 0, 0};
+      if (valid) {
+        const uint2 ed = r.inv[j];
+        c = ed.y;
+        valid = !(k.root && ed.x == r.sys_child);
+        if (valid && !semit) {
+          valid = (r.nflags[c] & k.need) != 0;
+        } else if (valid) {  // the literal is last: c's message, else Retained.Get("") (:474)
+          if (retained_node(r, c))
+            em = Emit{k.f, 0, r.cum[c], r.cum[c] + 1};
+          else if (r.has_empty)
+            em = Emit{k.f, 0, (uint32_t)r.n_ret, (uint32_t)r.n_ret + 1};
+          else
+            valid = false;
+        }
+      }
+      const uint64_t m = __ballot(valid);
+      if (!m) continue;
+      const uint32_t cnt = (uint32_t)__popcll(m);
+      unsigned long long base = 0;
+      if (lane == 0) base = atomicAdd(semit ? &a.ctr->n_emit : &a.ctr->items[a.d + 2], (unsigned long long)cnt);
+      base = bcast64(base, 0);
+      const uint64_t pos = base + __popcll(m & ((1ull << lane) - 1ull));
+      if (semit) {
+        if (lane == 0 && base + cnt > a.emit_cap) atomicOr(&a.ctr->ovf, (unsigned)kOvfEmit);
+        if (valid && pos < a.emit_cap) a.emit[pos] = em;
+      } else {
+        if (lane == 0) {
+          atomicMax(&a.ctr->need_items, base + cnt);
+          if (base + cnt > a.item_cap) atomicOr(&a.ctr->ovf, (unsigned)kOvfItems);
+        }
+        if (valid && pos < a.item_cap) {
+          a.skip_f[pos] = k.f;
+          a.skip_n[pos] = c;
         }
       }
     }
@@ -626,17 +728,19 @@ int messages_device(const DeviceSnapshot &s, const DeviceRetained *r, Workspace 
 
   // every list starts at its size from the previous call (grown on overflow)
   uint64_t &item_cap = ws.rev_item_cap, &emit_cap = ws.rev_emit_cap, &task_cap = ws.rev_task_cap,
-           &out_cap = ws.rev_out_cap;
+           &out_cap = ws.rev_out_cap, &ltask_cap = ws.rev_ltask_cap;
+  static const bool use_ltasks = getenv("MQM_REV_TASKS") && atoi(getenv("MQM_REV_TASKS")) != 0;
   // MQM_REV_CAP0=k (tests): a fresh workspace starts every list at k entries,
   // so the first calls overflow and re-queue at every level
   const char *cap0_env = getenv("MQM_REV_CAP0");
   const uint64_t cap0 = cap0_env ? strtoull(cap0_env, nullptr, 10) : 0;
   if (cap0) {
-    if (!item_cap) item_cap = emit_cap = task_cap = out_cap = cap0;
+    if (!item_cap) item_cap = emit_cap = task_cap = out_cap = ltask_cap = cap0;
   } else {
     item_cap = std::max<uint64_t>(item_cap, std::max<uint64_t>(4ull * n, 1u << 16));
     emit_cap = std::max<uint64_t>(emit_cap, std::max<uint64_t>(2ull * n, 1u << 16));
     task_cap = std::max<uint64_t>(task_cap, 1u << 12);
+    ltask_cap = std::max<uint64_t>(ltask_cap, std::max<uint64_t>(n, 1u << 16));
     out_cap = std::max<uint64_t>(out_cap, std::max<uint64_t>(4ull * n, 1u << 16));
   }
   const uint32_t grid = resident_grid();
@@ -645,7 +749,8 @@ int messages_device(const DeviceSnapshot &s, const DeviceRetained *r, Workspace 
         ws.get(W::kRItemF1, sizeof(uint32_t) * item_cap) || ws.get(W::kRItemN1, sizeof(uint32_t) * item_cap) ||
         ws.get(W::kRChild, sizeof(uint32_t) * item_cap) || ws.get(W::kRECount, sizeof(uint32_t) * item_cap) ||
         ws.get(W::kREmit, sizeof(Emit) * emit_cap) || ws.get(W::kRChunks, sizeof(Task) * task_cap) ||
-        ws.get(W::kROut, sizeof(uint64_t) * out_cap))
+        ws.get(W::kROut, sizeof(uint64_t) * out_cap) ||
+        (use_ltasks && ws.get(W::kRPos, sizeof(LTask) * ltask_cap)))
       return -2;
     // levels 0 .. height: an item of level d sits on a node of depth d
     const uint32_t max_levels = s.height + 1;
@@ -672,6 +777,8 @@ int messages_device(const DeviceSnapshot &s, const DeviceRetained *r, Workspace 
     a.ctr = ctr;
     static const bool rev_stats = getenv("MQM_REV_STATS") && atoi(getenv("MQM_REV_STATS")) != 0;
     a.st = rev_stats ? reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(ctr) + st_at) : nullptr;
+    a.ltasks = use_ltasks ? (LTask *)ws.ptr(W::kRPos) : nullptr;
+    a.ltask_cap = use_ltasks ? ltask_cap : 0;
     // level L's list lives in buffer pair L % 3 (a level appends to the next
     // two: wildcard + literal through the edge index jumps one level)
     const W::Slot lf[3] = {W::kRItemF0, W::kRItemF1, W::kRChild}, ln[3] = {W::kRItemN0, W::kRItemN1, W::kRECount};
@@ -684,8 +791,13 @@ int messages_device(const DeviceSnapshot &s, const DeviceRetained *r, Workspace 
       a.skip_f = (uint32_t *)ws.ptr(lf[(d + 2) % 3]);
       a.skip_n = (uint32_t *)ws.ptr(ln[(d + 2) % 3]);
       const uint32_t g = d == 0 ? std::min<uint32_t>(grid, blocks_for(n)) : grid;
+      if (a.ltasks) HIP_TRY(hipMemsetAsync(&ctr->n_ltasks, 0, sizeof(unsigned long long), st));
       hipLaunchKernelGGL(k_level, dim3(g), dim3(kThreads), 0, st, a);
       HIP_TRY(hipGetLastError());
+      if (a.ltasks) {
+        hipLaunchKernelGGL(k_level_tasks, dim3(grid), dim3(kThreads), 0, st, a);
+        HIP_TRY(hipGetLastError());
+      }
       // every kLevelBatch levels, stop early once the next two levels are empty
       if ((d + 1) % kLevelBatch == 0 && d + 1 < max_levels) {
         HIP_TRY(hipMemcpyAsync(hp, &ctr->items[d + 1], 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
@@ -716,7 +828,8 @@ int messages_device(const DeviceSnapshot &s, const DeviceRetained *r, Workspace 
     HIP_TRY(hipStreamSynchronize(st));
     const uint64_t n_refs = hp[15];
     const unsigned ovf = hc->ovf;
-    const uint64_t n_emit = hc->n_emit, n_tasks = hc->n_tasks, need_items = hc->need_items;
+    const uint64_t n_emit = hc->n_emit, n_tasks = hc->n_tasks, need_items = hc->need_items,
+                   need_ltasks = hc->need_ltasks;
     if (ovf == 0 && a.st) {
       unsigned long long sv[kStatLevels * kStatKinds];
       HIP_TRY(hipMemcpy(sv, a.st, sizeof(sv), hipMemcpyDeviceToHost));
@@ -740,6 +853,7 @@ int messages_device(const DeviceSnapshot &s, const DeviceRetained *r, Workspace 
     if (ovf & kOvfEmit) emit_cap = std::max(emit_cap, n_emit + n_emit / 4);
     if (ovf & kOvfTasks) task_cap = std::max(task_cap, n_tasks + n_tasks / 4);
     if (ovf & kOvfOut) out_cap = std::max(out_cap, n_refs + n_refs / 4);
+    if (ovf & kOvfLTasks) ltask_cap = std::max(ltask_cap, need_ltasks + need_ltasks / 4);
   }
 }
 

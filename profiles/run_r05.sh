@@ -6,6 +6,8 @@
 #   ab / c4ab: `fast` (C3) / the C4 shard bench with the round-5 walk (paired node slots) and long-part
 #             copy, then each switched off (MQM_NO_SLOTS=1, MQM_LONG_PART=0)
 #   revstats: the C5 reverse bench with the per-level item mix (MQM_REV_STATS=1)
+#   revab   : the C5 reverse bench without and with level tasks (MQM_REV_TASKS=1)
+#   node    : the sharded node step with two rank processes and the HIP matcher (tests/test_gpu_node_step.py)
 #   churnserve: the churn workload with the served-calls-under-churn leg
 #   c4test  : the C4 shard 0/8 full-batch test            -> gpurun_out/TAG/pytest_c4.log
 #   ret     : the retained (reverse-match) tests           -> gpurun_out/TAG/pytest_ret.log
@@ -57,6 +59,12 @@ for step in "$@"; do
         done ;;
     revstats) MQM_REV_STATS=1 timeout -k 10 600 python3 -u bench.py --workload reverse --steps 2 --warmup 1 \
              --no-cpu-baseline > $OUT/bench_rev_stats.json 2> $OUT/bench_rev_stats.log ;;
+    node) timeout -k 10 400 $PYT tests/test_gpu_node_step.py -m gpu --timeout 300 > $OUT/pytest_node.log 2>&1 ;;
+    revab) for V in base:X=0 tasks:MQM_REV_TASKS=1; do
+          N=${V%%:*}; E=${V#*:}
+          env $E timeout -k 10 600 python3 -u bench.py --workload reverse --steps 3 --warmup 1 --no-cpu-baseline \
+            > $OUT/bench_rev_$N.json 2> $OUT/bench_rev_$N.log || exit 1
+        done ;;
     churnserve) timeout -k 10 900 python3 -u bench.py --workload churn --steps 3 --warmup 1 --serve-churn-s 20 \
              > $OUT/bench_churn.json 2> $OUT/bench_churn.log ;;
     c4test) timeout -k 10 600 $PYT tests/test_gpu_c4_shard.py -m gpu --timeout 500 > $OUT/pytest_c4.log 2>&1 ;;
