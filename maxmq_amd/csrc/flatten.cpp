@@ -766,7 +766,7 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
     g->device_bytes += bb;
   }
   g->device_bytes += n_sub_ents * 4;
-  {  // paired node slots (snapshot.h DeviceSnapshot::slots)
+  if (slots_enabled()) {  // paired node slots (snapshot.h DeviceSnapshot::slots; MQM_SLOTS=1)
     const uint64_t nn = hs->nodes.size();
     if (hipMalloc(&g->slots, nn * 2 * sizeof(NodeDesc) + 64) != hipSuccess) return MQM_ENOMEM;
     if (derive_slots((const NodeDesc *)g->buffers[0], (NodeDesc *)g->slots, nn, stream)) return MQM_EHIP;

@@ -63,9 +63,7 @@ struct Workspace {
     kInBytes, kInOffs, kListS, kICount, kIStart, kIOut, kNSolo, kDescStart, kDesc, kWin, kMCount, kRunCount, kRunOffs, kRuns, kListW, kListT1, kListT2, kListT3, kListP, kListH, kListRS, kListR,
     // reverse match (retained.hip)
     kROffs, kRNLev, kRWild, kRLOff, kRFCount, kRFCur, kRLevels, kRNCount, kRNOff, kRItemF0, kRItemN0, kRItemF1,
-    kRItemN1, kRChild, kRECount, kREOff, kREmit, kRPos, kRChunks, kRCOff, kROut, kRInBytes, kRInOffs,
-    kLDesc,  // the long solo parts (k_longcopy)
-    kNumSlots
+    kRItemN1, kRChild, kRECount, kREOff, kREmit, kRPos, kRChunks, kRCOff, kROut, kRInBytes, kRInOffs, kNumSlots
   };
   struct Buf {
     void *p = nullptr;
@@ -157,6 +155,9 @@ struct MatchOutput {
   bool exact = false;                     // sized by its own read-back (the first call of a workspace, or a re-run)
 };
 
+// MQM_SLOTS=1: the snapshot carries DeviceSnapshot::slots and the batch walk
+// uses them (off by default: measured slower)
+bool slots_enabled();
 // slots[2i] = nodes[i], slots[2i + 1] = nodes[nodes[i].plus] or zeros (snapshot upload, on `st`)
 int derive_slots(const NodeDesc *nodes, NodeDesc *slots, uint64_t n, hipStream_t st);
 // words[i] = subs[i].word & kPackedMask for i < n (snapshot upload, on `st`)

@@ -154,7 +154,6 @@ struct Counters {              // zeroed before every batch
   unsigned long long n_solo;                    // solo entries the walk copied
   unsigned long long tab_total, dfs_raw, dfs_h; // DFS: dedupe table, raw entries, shared candidates
   unsigned long long d_sum, h_sum;              // deliveries, shared candidates (after dedupe)
-  unsigned long long n_long;                    // k_desc: solo parts long enough for k_longcopy
 #if MQM_WALK_STATS
   unsigned long long st_probe, st_miss, st_desc;
 #endif
@@ -743,9 +742,12 @@ struct alignas(8) DescLds {
   uint32_t pre[kWave + 1];        // exclusive prefix of the topics' solo-part counts
 };
 
+// a long solo part's descriptor keeps its length with this flag: the window
+// copy reads it as empty (a gap), k_longcopy finds it by the flag
+constexpr uint32_t kDescLong = 0x80000000u;
+
 __global__ __launch_bounds__(256) void k_desc(Outputs o, uint32_t n, const uint64_t *__restrict__ desc_start,
-                                              uint4 *__restrict__ desc, uint64_t desc_cap, uint4 *__restrict__ ldesc,
-                                              uint32_t long_min) {
+                                              uint4 *__restrict__ desc, uint64_t desc_cap, uint32_t long_min) {
   __shared__ DescLds lds_all[4];
   const int lane = threadIdx.x & (kWave - 1);
   DescLds &L = lds_all[threadIdx.x / kWave];
@@ -793,21 +795,14 @@ __global__ __launch_bounds__(256) void k_desc(Outputs o, uint32_t n, const uint6
       }
       const uint64_t at = valid ? L.run[j] + (si - part.y) : 0;
       const bool seg_end = __shfl_down(seg, 1, kWave) != seg || lane == kWave - 1;
-      // a long part goes to k_longcopy's list (any order: each is copied on
-      // its own); its place in the window copy's list keeps its output
-      // position with no entries (a gap the window copy skips)
+      // a long part is flagged (kDescLong): k_longcopy moves it, the window
+      // copy sees a gap at its place (parts are < 2^24 entries, kSMax)
       const bool lng = valid && part.y >= long_min;
-      const uint64_t lm = __ballot(lng);
-      uint64_t lbase = 0;
-      if (lm) {
-        if (lane == 0) lbase = atomicAdd(&o.ctr->n_long, (unsigned long long)__popcll(lm));
-        lbase = shfl64(lbase, 0);
-      }
       wave_lds_sync();
       if (valid) {
-        const uint4 dv = make_uint4(part.x, part.y, (uint32_t)at, (uint32_t)(at >> 32));
-        put_checked(desc, pb + k, desc_cap, lng ? make_uint4(part.x, 0u, dv.z, dv.w) : dv, &o.ctr->oob);
-        if (lng) put_checked(ldesc, lbase + __popcll(lm & lanemask_lt(lane)), desc_cap, dv, &o.ctr->oob);
+        put_checked(desc, pb + k, desc_cap,
+                    make_uint4(part.x, part.y | (lng ? kDescLong : 0u), (uint32_t)at, (uint32_t)(at >> 32)),
+                    &o.ctr->oob);
         if (seg_end) L.run[j] += si;
       }
       wave_lds_sync();
@@ -879,7 +874,7 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
       uint4 d = make_uint4(0, 0, 0xFFFFFFFFu, 0xFFFFFFFFu);
       if (jj < nd) d = desc[jj];
       const uint64_t dst = d.z | ((uint64_t)d.w << 32);
-      const uint64_t dend = jj < nd ? dst + d.y : ~0ull;
+      const uint64_t dend = jj < nd ? dst + ((d.y & kDescLong) ? 0u : d.y) : ~0ull;
       uint64_t a = dst > pos ? dst : pos, b = dend < g1 ? dend : g1;
       if (b < a) b = a;
       if (a > g1) a = b = g1;
@@ -937,10 +932,9 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
           in[u] = q < q1 && q >= L.st[k] && q < L.en[k];
           sa[u] = in[u] ? L.src[k] + (q - L.st[k]) : 0u;
         }
-        uint32_t v[kCU];
+        uint32_t v[kCU];  // (unconditional: all kCU loads in flight together; a gap row loads words[0])
 #pragma unroll
-        for (int u = 0; u < kCU; u++)
-          v[u] = ((rows >> u) & 1u) ? __builtin_amdgcn_raw_buffer_load_b32(words, (int)(sa[u] * 4u), 0, 0) : 0u;
+        for (int u = 0; u < kCU; u++) v[u] = __builtin_amdgcn_raw_buffer_load_b32(words, (int)(sa[u] * 4u), 0, 0);
 #pragma unroll
         for (int u = 0; u < kCU; u++) {
           if (!in[u]) continue;
@@ -967,18 +961,27 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
 // (the 4-word units inside the part) and 16-B loads at the matching source
 // offset (dword-aligned: `words` and `dout` shift by different amounts), its
 // first and last partial units word by word.  4 units per lane in flight.
-__global__ __launch_bounds__(kWave *kEmitWaves) void k_longcopy(DeviceSnapshot s, const uint4 *__restrict__ ldesc,
-                                                              const unsigned long long *__restrict__ nl_ptr,
-                                                              uint64_t lcap, uint32_t *__restrict__ out, uint64_t cap,
+__global__ __launch_bounds__(kWave *kEmitWaves) void k_longcopy(DeviceSnapshot s, const uint4 *__restrict__ desc,
+                                                              const uint64_t *__restrict__ nd_ptr, uint64_t desc_cap,
+                                                              uint32_t *__restrict__ out, uint64_t cap,
                                                               unsigned int *oob) {
-  const uint64_t nl = min((uint64_t)*nl_ptr, lcap);
+  const uint64_t nd = min(*nd_ptr, desc_cap);
   const int lane = threadIdx.x & (kWave - 1);
   const __amdgpu_buffer_rsrc_t words =
       __builtin_amdgcn_make_buffer_rsrc((void *)s.words, (short)0, (int)(s.n_subs * 4u + 64u), 0x00020000);
   const uint64_t nw = (uint64_t)gridDim.x * kEmitWaves;
   constexpr int kU = 4;
-  for (uint64_t i = (uint64_t)blockIdx.x * kEmitWaves + threadIdx.x / kWave; i < nl; i += nw) {
-    const uint4 d = ldesc[i];
+  // 64 descriptors per wave step (one coalesced load), then the flagged ones,
+  // each by the whole wavefront
+  for (uint64_t j0 = ((uint64_t)blockIdx.x * kEmitWaves + threadIdx.x / kWave) * kWave; j0 < nd; j0 += nw * kWave) {
+    uint4 mine = make_uint4(0, 0, 0, 0);
+    if (j0 + lane < nd) mine = desc[j0 + lane];
+    uint64_t lm = __ballot((mine.y & kDescLong) != 0);
+   while (lm) {
+    const int src_lane = __builtin_ctzll(lm);
+    lm &= lm - 1;
+    const uint4 d = make_uint4(__shfl(mine.x, src_lane, 64), __shfl(mine.y, src_lane, 64) & ~kDescLong,
+                               __shfl(mine.z, src_lane, 64), __shfl(mine.w, src_lane, 64));
     const uint64_t dst = d.z | ((uint64_t)d.w << 32), e = dst + d.y, a = dst & ~3ull;
     const uint64_t units = (e - a + 3) >> 2;
     const uint32_t src = d.x;
@@ -1014,6 +1017,7 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_longcopy(DeviceSnapshot s
         }
       }
     }
+   }
   }
 }
 
@@ -1412,10 +1416,7 @@ __global__ __launch_bounds__(kBigThreads) void k_multi_part(DeviceSnapshot s, Ou
 // ms against a threshold of 769).  Read at every batch (a test compares modes in one process):
 // MQM_RESOLVE=1 every light topic, MQM_RESOLVE=0 none,
 // MQM_RESOLVE_MIN=m the threshold.
-static bool walk_slots() {
-  static const bool v = !(getenv("MQM_NO_SLOTS") && atoi(getenv("MQM_NO_SLOTS")) != 0);
-  return v;
-}
+static bool walk_slots() { return slots_enabled(); }
 // solo parts of at least this many entries take k_longcopy (MQM_LONG_PART:
 // A/B; 0 = none).  At least 64: k_wincopy's gap test looks at the first
 // descriptor starting inside a 64-position block only, so the part after a
@@ -1788,9 +1789,14 @@ __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *
 // ---------------------------------------------------------------------------
 template <int kPhase>
 __global__ __launch_bounds__(256) void k_ident(DeviceSnapshot s, Outputs o, uint32_t n) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const uint32_t waves = gridDim.x * (blockDim.x / kWave);
-  for (uint32_t t = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave; t < n; t += waves) {
+  // an 8-lane group per topic: most topics have a few short multi parts, and
+  // a wavefront per topic left 56 lanes idle through each topic's dependent
+  // loads (C3: 5.5 ms for the two phases, r05d)
+  constexpr int kL = 8;
+  const int lane = threadIdx.x & (kWave - 1), gl = lane % kL, gbase = lane - gl;
+  const uint64_t glt = (1ull << gl) - 1ull;
+  const uint32_t groups = gridDim.x * (blockDim.x / kL);
+  for (uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) / kL; t < n; t += groups) {
     const uint8_t cls = o.cls[t];
     if (cls == kClsDfs) continue;
     uint32_t nid = 0;
@@ -1803,16 +1809,16 @@ __global__ __launch_bounds__(256) void k_ident(DeviceSnapshot s, Outputs o, uint
       for (uint32_t h = 0; h < nm; h++) {  // the multi parts (solo parts: see above)
         const uint4 u = gt[-(int)(1 + h)];
         const uint32_t off = u.x, cnt = u.y;
-        for (uint32_t b0 = 0; b0 < cnt; b0 += kWave) {
-          const uint32_t j = b0 + lane;
+        for (uint32_t b0 = 0; b0 < cnt; b0 += kL) {
+          const uint32_t j = b0 + gl;
           const bool has = j < cnt && (s.subs[off + j].word & kWordIdent);
-          const uint64_t m = __ballot(has);
-          if (kPhase == 1 && has) o.iout[ib + nid + __popcll(m & lanemask_lt(lane))] = off + j;
+          const uint64_t m = (__ballot(has) >> gbase) & ((1ull << kL) - 1ull);
+          if (kPhase == 1 && has) o.iout[ib + nid + __popcll(m & glt)] = off + j;
           nid += (uint32_t)__popcll(m);
         }
       }
     }
-    if (kPhase == 0 && lane == 0) o.icount[t] = nid;
+    if (kPhase == 0 && gl == 0) o.icount[t] = nid;
   }
 }
 
@@ -2287,10 +2293,10 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
     // C3 walk 5.76 -> 5.19 ms, C4 shard 6.22 -> 5.57 (r04an, r04ao; 16 at a
     // time 5.37, 1 at a time 7.53: the counter's atomics serialise); the fixed
     // stride for batches whose counter could pass 2^32
-    // (MQM_NO_SLOTS=1: the round-4 walk, 32-B descriptor loads from `nodes`, for A/B)
+    // (MQM_SLOTS=1: the walk over paired node slots; measured slower, r05d: see DESIGN §3)
     if (n >= (1u << 31))
       hipLaunchKernelGGL(k_walk<kWalkG>, dim3(blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o);
-    else if (walk_slots())
+    else if (walk_slots() && s.slots)
       hipLaunchKernelGGL((k_walk<kWalkG, 4>), dim3(blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o);
     else
       hipLaunchKernelGGL((k_walk<kWalkG, 4, false>), dim3(blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs,
@@ -2373,8 +2379,7 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
     tab_cap = std::max<uint64_t>(cap_of(W::kTable, sizeof(GEnt)), 1u << 16);
   }
   if (ws.get(W::kDOut, sizeof(uint32_t) * (dcap + 1)) || ws.get(W::kHOut, sizeof(uint32_t) * (hcap + 1)) ||
-      ws.get(W::kDesc, sizeof(uint4) * (desc_cap + 1)) || ws.get(W::kWin, sizeof(uint32_t) * (win_cap + 1)) ||
-      (!ws.runs && ws.get(W::kLDesc, sizeof(uint4) * (desc_cap + 1))))
+      ws.get(W::kDesc, sizeof(uint4) * (desc_cap + 1)) || ws.get(W::kWin, sizeof(uint32_t) * (win_cap + 1)))
     return -2;
   o.dout = (uint32_t *)ws.ptr(W::kDOut);
   o.hout = (uint32_t *)ws.ptr(W::kHOut);
@@ -2477,15 +2482,16 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
     }
     // the solo copy (none in the runs form: the solo parts stay runs)
     if (!ws.runs) {
-      auto *ldesc = (uint4 *)ws.ptr(W::kLDesc);
-      if (!ldesc) return -1;
+      const uint32_t long_min = long_part_min();
       hipLaunchKernelGGL(k_desc, dim3(std::min<uint32_t>((n + 255) / 256, 8192)), dim3(256), 0, st, o, n, desc_start,
-                         desc, desc_cap, ldesc, long_part_min());  // a wavefront per 64 topics
+                         desc, desc_cap, long_min);  // a wavefront per 64 topics
       HIP_TRY(hipGetLastError());
-      // the long parts (their own list, 16-B moves) before the window copy of the rest
-      hipLaunchKernelGGL(k_longcopy, grid(k_longcopy), dim3(kWave * kEmitWaves), 0, st, s, ldesc, &o.ctr->n_long,
-                         desc_cap, o.dout, o.dcap, &o.ctr->oob);
-      HIP_TRY(hipGetLastError());
+      // the long parts (flagged descriptors, 16-B moves) before the window copy of the rest
+      if (long_min != 0xFFFFFFFFu) {
+        hipLaunchKernelGGL(k_longcopy, grid(k_longcopy), dim3(kWave * kEmitWaves), 0, st, s, desc, desc_start + n,
+                           desc_cap, o.dout, o.dcap, &o.ctr->oob);
+        HIP_TRY(hipGetLastError());
+      }
       if (!exact || hc->n_desc > 0) {
         const uint64_t nd_grid = exact ? hc->n_desc : desc_cap;
         hipLaunchKernelGGL(k_winmap,
@@ -2671,7 +2677,7 @@ int identifiers_device(const DeviceSnapshot &s, Workspace &ws, hipStream_t st, I
   const size_t fb_lds = sizeof(uint32_t) * (((max_levels + 1) & ~1u) + 4 * (2 * max_levels + 8)) +
                         sizeof(uint64_t) * 2 * max_levels;
   const uint32_t fb_blocks = std::max<uint32_t>(1, std::min<uint32_t>(ws.last_n_dfs, 4096));
-  const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + 3) / 4, 8192));
+  const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + 31) / 32, 8192));  // 32 topics per block
   if (n > 0) {
     hipLaunchKernelGGL(k_ident<0>, dim3(blocks), dim3(256), 0, st, s, o, n);
     HIP_TRY(hipGetLastError());
@@ -2711,6 +2717,11 @@ int derive_node_flags(const NodeDesc *nodes, uint8_t *nflags, uint64_t n, hipStr
     hipLaunchKernelGGL(k_nflags, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 16384)), dim3(256), 0, st, nodes,
                        nflags, n);
   return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+bool slots_enabled() {
+  static const bool v = getenv("MQM_SLOTS") && atoi(getenv("MQM_SLOTS")) != 0;
+  return v;
 }
 
 int derive_slots(const NodeDesc *nodes, NodeDesc *slots, uint64_t n, hipStream_t st) {

@@ -4,7 +4,7 @@
 #   tests   : every -m gpu test                          -> gpurun_out/TAG/pytest_gpu.log
 #   serve   : the per-publish server tests (incl. served calls under Subscribe/Unsubscribe churn)
 #   ab / c4ab: `fast` (C3) / the C4 shard bench with the round-5 walk (paired node slots) and long-part
-#             copy, then each switched off (MQM_NO_SLOTS=1, MQM_LONG_PART=0)
+#             copy, then each switched off (MQM_SLOTS=1 switches the slot walk on, MQM_LONG_PART=0 the long copy off)
 #   revstats: the C5 reverse bench with the per-level item mix (MQM_REV_STATS=1)
 #   revab   : the C5 reverse bench without and with level tasks (MQM_REV_TASKS=1)
 #   node    : the sharded node step with two rank processes and the HIP matcher (tests/test_gpu_node_step.py)
@@ -48,11 +48,11 @@ for step in "$@"; do
     tests) timeout -k 10 1000 $PYT tests -m gpu --timeout 600 --durations=15 > $OUT/pytest_gpu.log 2>&1 ;;
     serve) timeout -k 10 600 $PYT tests/test_gpu_serve.py tests/test_gpu_serve_churn.py tests/test_gpu_shim.py -m gpu \
              --timeout 300 > $OUT/pytest_serve.log 2>&1 ;;
-    ab) for V in base:X=0 noslots:MQM_NO_SLOTS=1 nolong:MQM_LONG_PART=0; do
+    ab) for V in base:X=0 slots:MQM_SLOTS=1 nolong:MQM_LONG_PART=0; do
           N=${V%%:*}; E=${V#*:}
           env $E timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_$N.json 2> $OUT/bench_fast_$N.log || exit 1
         done ;;
-    c4ab) for V in base:X=0 noslots:MQM_NO_SLOTS=1 nolong:MQM_LONG_PART=0; do
+    c4ab) for V in base:X=0 nolong:MQM_LONG_PART=0; do
           N=${V%%:*}; E=${V#*:}
           env $E timeout -k 10 600 python3 -u bench.py --config 4 --shard 0/8 $FAST > $OUT/bench_c4_$N.json \
             2> $OUT/bench_c4_$N.log || exit 1
