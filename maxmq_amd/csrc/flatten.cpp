@@ -721,6 +721,7 @@ GpuSnapshot::~GpuSnapshot() {
     if (b) (void)hipFree(b);
   if (words) (void)hipFree(words);
   if (slots) (void)hipFree(slots);
+  if (ident_bits) (void)hipFree(ident_bits);
   if (nflags) (void)hipFree(nflags);
   if (bloom) (void)hipFree(bloom);
   if (pinfo) (void)hipFree(pinfo);
@@ -766,6 +767,13 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
     g->device_bytes += bb;
   }
   g->device_bytes += n_sub_ents * 4;
+  {  // Identifier > 0, one bit per entry (DeviceSnapshot::ident_bits)
+    const uint64_t nw = (n_sub_ents + 31) / 32;
+    if (hipMalloc(&g->ident_bits, nw * 4 + 64) != hipSuccess) return MQM_ENOMEM;
+    if (derive_ident_bits((const SubEnt *)g->buffers[2], (uint32_t *)g->ident_bits, n_sub_ents, stream))
+      return MQM_EHIP;
+    g->device_bytes += nw * 4;
+  }
   if (slots_enabled()) {  // paired node slots (snapshot.h DeviceSnapshot::slots; MQM_SLOTS=1)
     const uint64_t nn = hs->nodes.size();
     if (hipMalloc(&g->slots, nn * 2 * sizeof(NodeDesc) + 64) != hipSuccess) return MQM_ENOMEM;
@@ -815,6 +823,7 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
   g->dev.edges = (const EdgeEntry *)g->buffers[1];
   g->dev.subs = (const SubEnt *)g->buffers[2];
   g->dev.words = (const uint32_t *)g->words;
+  g->dev.ident_bits = (const uint32_t *)g->ident_bits;
   g->dev.pinfo = (const uint2 *)g->pinfo;
   g->dev.partners = (const uint32_t *)g->partners;
   g->dev.bloom = (const uint64_t *)g->bloom;

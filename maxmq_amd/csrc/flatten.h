@@ -80,6 +80,7 @@ struct GpuSnapshot {
   void *buffers[kNumBuffers] = {};
   void *words = nullptr;  // DeviceSnapshot::words (derived on the device at upload)
   void *slots = nullptr;  // DeviceSnapshot::slots (derived on the device at upload)
+  void *ident_bits = nullptr;  // DeviceSnapshot::ident_bits (derived on the device at upload)
   void *nflags = nullptr; // DeviceRetained::nflags (derived on the device at upload)
   void *bloom = nullptr;  // DeviceSnapshot::bloom
   void *pinfo = nullptr, *partners = nullptr;  // DeviceSnapshot::pinfo / partners

@@ -160,6 +160,8 @@ struct MatchOutput {
 bool slots_enabled();
 // slots[2i] = nodes[i], slots[2i + 1] = nodes[nodes[i].plus] or zeros (snapshot upload, on `st`)
 int derive_slots(const NodeDesc *nodes, NodeDesc *slots, uint64_t n, hipStream_t st);
+// bits[i / 32] bit i % 32 = subs[i].word & kWordIdent (snapshot upload, on `st`)
+int derive_ident_bits(const SubEnt *subs, uint32_t *bits, uint64_t n, hipStream_t st);
 // words[i] = subs[i].word & kPackedMask for i < n (snapshot upload, on `st`)
 int derive_words(const SubEnt *subs, uint32_t *words, uint64_t n, hipStream_t st);
 // nflags[i] = nodes[i].sh_cnt_flags >> 24 for i < n (snapshot upload, on `st`)

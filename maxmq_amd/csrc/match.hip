@@ -402,34 +402,60 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
     uint32_t why = kNoWhy;
 
     // ---- 1. tokenize ------------------------------------------------------
-    // each lane issues kStage/kG independent byte loads per chunk (one round
-    // trip); the first chunk is kept in LDS for the key build below
+    // lane gl takes the chunk's bytes [16 gl, 16 gl + 16) as 5 aligned dword
+    // loads (clamped into the topic's last dword), one round trip; 16 byte
+    // loads per lane cost the address unit 16 instructions per chunk (TA busy
+    // 0.69 in the walk, r04ay).  Separators: counted per lane, placed in order
+    // through the group's prefix.  The first chunk is kept in LDS for the key
+    // build below.
+    static_assert(kStage == 16 * kG, "16 bytes per lane per chunk");
     uint32_t nsep = 0;
     bool dollar = false;
     for (uint32_t base = 0; base < len && nsep < (uint32_t)kLMax; base += kStage) {
-      uint8_t b[kStage / kG];
+      const uint32_t p0 = base + 16 * gl;
+      const uint64_t first = reinterpret_cast<uint64_t>(len ? tp + p0 : o.cls);
+      const uint64_t lastw = reinterpret_cast<uint64_t>(len ? tp + len - 1 : o.cls) & ~3ull;
+      const uint64_t a0 = first & ~3ull;
+      const uint32_t r = (uint32_t)(first & 3u);
+      uint32_t w[5];
 #pragma unroll
-      for (int j = 0; j < kStage / kG; j++) {  // unconditional: clamped into the topic (or a dummy byte)
-        const uint32_t p = base + j * kG + gl;
-        const uint8_t v = *(len ? tp + (p < len ? p : len - 1) : o.cls);
-        b[j] = p < len ? v : 0;
+      for (int k = 0; k < 5; k++) w[k] = *reinterpret_cast<const uint32_t *>(min(a0 + 4 * k, lastw));
+      uint32_t b4[4];  // the lane's 16 bytes, little-endian words, shifted by r
+#pragma unroll
+      for (int k = 0; k < 4; k++) b4[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], r);
+      // bytes at or past len read as 0 (never a separator)
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t pk = p0 + 4 * k;
+        if (pk >= len) b4[k] = 0;
+        else if (pk + 4 > len) b4[k] &= 0xFFFFFFFFu >> (8 * (pk + 4 - len));
       }
       if (base == 0) {
 #pragma unroll
-        for (int j = 0; j < kStage / kG; j++) L.stage[j * kG + gl] = b[j];
-        dollar = __shfl(b[0], gbase, 64) == '$';
+        for (int k = 0; k < 4; k++) reinterpret_cast<uint32_t *>(L.stage)[4 * gl + k] = b4[k];
+        dollar = (__shfl(b4[0], gbase, 64) & 0xFFu) == '$';
       }
+      // '/' bytes: a 16-bit mask of the lane's bytes
+      uint32_t sm = 0;
 #pragma unroll
-      for (int j = 0; j < kStage / kG; j++) {
-        const uint32_t p = base + j * kG + gl;
-        const bool sep = p < len && b[j] == '/';
-        const uint32_t m = (uint32_t)(__ballot(sep) >> gbase) & kGMask;
-        if (sep) {
-          const uint32_t idx = nsep + __popc(m & gmask_lt);
-          if (idx < (uint32_t)kLMax) L.sep[idx] = (uint16_t)p;
-        }
-        nsep += __popc(m);
+      for (int k = 0; k < 4; k++) {
+        const uint32_t x = b4[k] ^ 0x2F2F2F2Fu;  // zero byte where '/'
+        // high bit set per non-zero byte, exactly (no carry crosses a byte: 0x7F + 0x7F < 0x100)
+        const uint32_t y = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+        const uint32_t z = ~y & 0x80808080u;  // where '/'
+        sm |= (((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u)) << (4 * k);
       }
+      const uint32_t cnt = __popc(sm);
+      uint32_t pre = cnt;  // inclusive prefix over the group's lanes
+#pragma unroll
+      for (int d = 1; d < kG; d <<= 1) {
+        const uint32_t v = __shfl_up(pre, d, kG);
+        if (gl >= d) pre += v;
+      }
+      uint32_t idx = nsep + pre - cnt;
+      for (uint32_t m = sm; m; m &= m - 1, idx++)
+        if (idx < (uint32_t)kLMax) L.sep[idx] = (uint16_t)(p0 + __builtin_ctz(m));
+      nsep += __shfl(pre, gbase + kG - 1, 64);
     }
     // levels known: 0 .. nlev-1, with nlev capped at kLMax + 1
     const uint32_t nlev = len == 0 ? 0 : (nsep >= (uint32_t)kLMax ? kLMax + 1 : nsep + 1);
@@ -874,7 +900,7 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
       uint4 d = make_uint4(0, 0, 0xFFFFFFFFu, 0xFFFFFFFFu);
       if (jj < nd) d = desc[jj];
       const uint64_t dst = d.z | ((uint64_t)d.w << 32);
-      const uint64_t dend = jj < nd ? dst + ((d.y & kDescLong) ? 0u : d.y) : ~0ull;
+      const uint64_t dend = jj < nd ? dst + ((d.y & kDescLong) ? 0u : d.y) : ~0ull;  // (a long part: a gap)
       uint64_t a = dst > pos ? dst : pos, b = dend < g1 ? dend : g1;
       if (b < a) b = a;
       if (a > g1) a = b = g1;
@@ -885,7 +911,6 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
       L.en[lane] = (uint32_t)(b - g0);
       L.src[lane] = d.x + (uint32_t)(a - dst);
       wave_lds_sync();
-      uint64_t nem;  // blocks of 64 positions some descriptor of this batch covers (others: gaps)
       {  // block lane (positions lane * 64 ..): the last descriptor starting at or before its start
         static_assert(kWin / kWave == kWave, "one block per lane");
         const uint32_t q = (uint32_t)lane * kWave;
@@ -893,29 +918,14 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
 #pragma unroll
         for (uint32_t step = 32; step > 0; step >>= 1) k = L.st[k + step] <= q ? k + step : k;
         L.blk[lane] = k;
-        // covered: that descriptor runs past the block start, or the next one
-        // starts inside the block (the long parts k_longcopy takes are gaps
-        // here: a step over them does no search, load or store)
-        nem = __ballot(L.en[k] > q || (k + 1 < (uint32_t)kWave && L.st[k + 1] < q + kWave && L.st[k + 1] < L.en[k + 1]));
       }
       wave_lds_sync();
       const uint32_t q0 = (uint32_t)(pos - g0), q1 = (uint32_t)(bend - g0);
       for (uint32_t base = q0; base < q1; base += kWave * kCU) {
         uint32_t sa[kCU];
         bool in[kCU];
-        uint32_t rows = 0;  // rows u (positions base + u * 64 + lane) that touch a covered block
 #pragma unroll
         for (int u = 0; u < kCU; u++) {
-          const uint32_t r0 = base + u * kWave, b1 = min(r0, (uint32_t)kWin - 1) / kWave,
-                         b2 = min(r0 + kWave - 1, (uint32_t)kWin - 1) / kWave;
-          if (r0 < q1 && (((nem >> b1) | (nem >> b2)) & 1ull)) rows |= 1u << u;
-        }
-        if (!rows) continue;  // a gap step (wave-uniform)
-#pragma unroll
-        for (int u = 0; u < kCU; u++) {
-          in[u] = false;
-          sa[u] = 0;
-          if (!((rows >> u) & 1u)) continue;  // (wave-uniform)
           const uint32_t q = base + u * kWave + lane;
           // the last descriptor starting at or before q: within [blk[b], blk[b + 1]]
           const uint32_t bq = min(q, (uint32_t)kWin - 1) / kWave;
@@ -932,7 +942,7 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
           in[u] = q < q1 && q >= L.st[k] && q < L.en[k];
           sa[u] = in[u] ? L.src[k] + (q - L.st[k]) : 0u;
         }
-        uint32_t v[kCU];  // (unconditional: all kCU loads in flight together; a gap row loads words[0])
+        uint32_t v[kCU];
 #pragma unroll
         for (int u = 0; u < kCU; u++) v[u] = __builtin_amdgcn_raw_buffer_load_b32(words, (int)(sa[u] * 4u), 0, 0);
 #pragma unroll
@@ -1047,6 +1057,17 @@ __global__ __launch_bounds__(256) void k_nflags(const NodeDesc *__restrict__ nod
                                                 uint64_t n) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     f[i] = (uint8_t)(nodes[i].sh_cnt_flags >> 24);
+}
+
+// word w of DeviceSnapshot::ident_bits: entries 32w .. 32w + 31
+__global__ __launch_bounds__(256) void k_ident_bits(const SubEnt *__restrict__ subs, uint32_t *__restrict__ bits,
+                                                    uint64_t n) {
+  const uint64_t nw = (n + 31) / 32;
+  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t b = 0;
+    for (uint32_t k = 0; k < 32 && w * 32 + k < n; k++) b |= ((subs[w * 32 + k].word & kWordIdent) ? 1u : 0u) << k;
+    bits[w] = b;
+  }
 }
 
 // slot i = {node i, its '+' child (zeros without one)} (snapshot.h DeviceSnapshot::slots)
@@ -1417,17 +1438,14 @@ __global__ __launch_bounds__(kBigThreads) void k_multi_part(DeviceSnapshot s, Ou
 // MQM_RESOLVE=1 every light topic, MQM_RESOLVE=0 none,
 // MQM_RESOLVE_MIN=m the threshold.
 static bool walk_slots() { return slots_enabled(); }
-// solo parts of at least this many entries take k_longcopy (MQM_LONG_PART:
-// A/B; 0 = none).  At least 64: k_wincopy's gap test looks at the first
-// descriptor starting inside a 64-position block only, so the part after a
-// long part's (empty) place must start at least a block later
-constexpr uint32_t kLongPartDefault = 256;
+// MQM_LONG_PART=m: solo parts of at least m entries take k_longcopy (A/B; off
+// by default: measured slower than the window copy alone, r05e — DESIGN §3)
 static uint32_t long_part_min() {
   if (const char *v = getenv("MQM_LONG_PART")) {
     const long x = atol(v);
-    return x <= 0 ? 0xFFFFFFFFu : (uint32_t)std::max(64L, x);
+    return x <= 0 ? 0xFFFFFFFFu : (uint32_t)x;
   }
-  return kLongPartDefault;
+  return 0xFFFFFFFFu;
 }
 constexpr uint32_t kResolveMinDefault = 193;
 static uint32_t resolve_min() {
@@ -1811,7 +1829,8 @@ __global__ __launch_bounds__(256) void k_ident(DeviceSnapshot s, Outputs o, uint
         const uint32_t off = u.x, cnt = u.y;
         for (uint32_t b0 = 0; b0 < cnt; b0 += kL) {
           const uint32_t j = b0 + gl;
-          const bool has = j < cnt && (s.subs[off + j].word & kWordIdent);
+          const uint32_t q = off + j;
+          const bool has = j < cnt && ((s.ident_bits[q >> 5] >> (q & 31)) & 1u);
           const uint64_t m = (__ballot(has) >> gbase) & ((1ull << kL) - 1ull);
           if (kPhase == 1 && has) o.iout[ib + nid + __popcll(m & glt)] = off + j;
           nid += (uint32_t)__popcll(m);
@@ -2728,6 +2747,14 @@ int derive_slots(const NodeDesc *nodes, NodeDesc *slots, uint64_t n, hipStream_t
   if (n)
     hipLaunchKernelGGL(k_slots, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 16384)), dim3(256), 0, st, nodes,
                        slots, n);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+int derive_ident_bits(const SubEnt *subs, uint32_t *bits, uint64_t n, hipStream_t st) {
+  const uint64_t nw = (n + 31) / 32;
+  if (nw)
+    hipLaunchKernelGGL(k_ident_bits, dim3((uint32_t)std::min<uint64_t>((nw + 255) / 256, 16384)), dim3(256), 0, st,
+                       subs, bits, n);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

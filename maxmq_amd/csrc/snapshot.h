@@ -138,6 +138,10 @@ struct DeviceSnapshot {
   const EdgeEntry *edges;
   const SubEnt *subs;
   const uint32_t *words;  // n_subs: subs[i].word & kPackedMask (the entry's own delivery)
+  // bit i = subs[i].word & kWordIdent (Identifier > 0), 1 bit per entry
+  // (1.25 MB at C3: stays in L2; the identifiers pass reads it instead of
+  // the 8-B entries)
+  const uint32_t *ident_bits;
   const uint8_t *tok_pool;
   uint64_t n_buckets;     // edge buckets (kEdgesPerBucket entries each; any count)
   // literal-edge existence filter, >= 16 bits per edge (64 MB at 10M filters:
