@@ -772,8 +772,13 @@ struct alignas(8) DescLds {
 // copy reads it as empty (a gap), k_longcopy finds it by the flag
 constexpr uint32_t kDescLong = 0x80000000u;
 
-__global__ __launch_bounds__(256) void k_desc(Outputs o, uint32_t n, const uint64_t *__restrict__ desc_start,
-                                              uint4 *__restrict__ desc, uint64_t desc_cap, uint32_t long_min) {
+// kCopy (MQM_DESC_COPY=1, A/B): no descriptors — the wave copies the step's
+// 64 parts itself, 4 parts at a time, each by the whole wavefront (lanes over
+// its entries: no position -> descriptor search, no k_winmap / k_wincopy)
+template <bool kCopy = false>
+__global__ __launch_bounds__(256) void k_desc(DeviceSnapshot s, Outputs o, uint32_t n,
+                                              const uint64_t *__restrict__ desc_start, uint4 *__restrict__ desc,
+                                              uint64_t desc_cap, uint32_t long_min) {
   __shared__ DescLds lds_all[4];
   const int lane = threadIdx.x & (kWave - 1);
   DescLds &L = lds_all[threadIdx.x / kWave];
@@ -826,10 +831,40 @@ __global__ __launch_bounds__(256) void k_desc(Outputs o, uint32_t n, const uint6
       const bool lng = valid && part.y >= long_min;
       wave_lds_sync();
       if (valid) {
-        put_checked(desc, pb + k, desc_cap,
-                    make_uint4(part.x, part.y | (lng ? kDescLong : 0u), (uint32_t)at, (uint32_t)(at >> 32)),
-                    &o.ctr->oob);
+        if (!kCopy)
+          put_checked(desc, pb + k, desc_cap,
+                      make_uint4(part.x, part.y | (lng ? kDescLong : 0u), (uint32_t)at, (uint32_t)(at >> 32)),
+                      &o.ctr->oob);
         if (seg_end) L.run[j] += si;
+      }
+      if (kCopy) {
+        uint64_t vm = __ballot(valid && part.y > 0);
+        while (vm) {  // (wave-uniform)
+          uint32_t src[4], len[4];
+          uint64_t dst[4];
+          uint32_t mx = 0;
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            len[i] = 0, src[i] = 0, dst[i] = 0;
+            if (vm) {
+              const int l = __builtin_ctzll(vm);
+              vm &= vm - 1;
+              src[i] = __shfl(part.x, l, 64);
+              len[i] = __shfl(part.y, l, 64);
+              dst[i] = shfl64(at, l);
+              mx = max(mx, len[i]);
+            }
+          }
+          for (uint32_t r0 = 0; r0 < mx; r0 += kWave) {
+            const uint32_t jj = r0 + lane;
+            uint32_t v[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) v[i] = jj < len[i] ? s.words[src[i] + jj] : 0u;
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+              if (jj < len[i]) put_checked(o.dout, dst[i] + jj, o.dcap, v[i], &o.ctr->oob);
+          }
+        }
       }
       wave_lds_sync();
     }
@@ -1438,6 +1473,10 @@ __global__ __launch_bounds__(kBigThreads) void k_multi_part(DeviceSnapshot s, Ou
 // MQM_RESOLVE=1 every light topic, MQM_RESOLVE=0 none,
 // MQM_RESOLVE_MIN=m the threshold.
 static bool walk_slots() { return slots_enabled(); }
+static bool desc_copy_on() {
+  static const bool v = getenv("MQM_DESC_COPY") && atoi(getenv("MQM_DESC_COPY")) != 0;
+  return v;
+}
 // MQM_LONG_PART=m: solo parts of at least m entries take k_longcopy (A/B; off
 // by default: measured slower than the window copy alone, r05e — DESIGN §3)
 static uint32_t long_part_min() {
@@ -2502,16 +2541,21 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
     // the solo copy (none in the runs form: the solo parts stay runs)
     if (!ws.runs) {
       const uint32_t long_min = long_part_min();
-      hipLaunchKernelGGL(k_desc, dim3(std::min<uint32_t>((n + 255) / 256, 8192)), dim3(256), 0, st, o, n, desc_start,
-                         desc, desc_cap, long_min);  // a wavefront per 64 topics
+      const bool desc_copy = desc_copy_on();
+      if (desc_copy)  // (A/B: the parts copied by k_desc itself; no window copy below)
+        hipLaunchKernelGGL(k_desc<true>, dim3(std::min<uint32_t>((n + 255) / 256, 8192)), dim3(256), 0, st, s, o, n,
+                           desc_start, desc, desc_cap, 0xFFFFFFFFu);
+      else
+        hipLaunchKernelGGL(k_desc<false>, dim3(std::min<uint32_t>((n + 255) / 256, 8192)), dim3(256), 0, st, s, o, n,
+                           desc_start, desc, desc_cap, long_min);  // a wavefront per 64 topics
       HIP_TRY(hipGetLastError());
       // the long parts (flagged descriptors, 16-B moves) before the window copy of the rest
-      if (long_min != 0xFFFFFFFFu) {
+      if (!desc_copy && long_min != 0xFFFFFFFFu) {
         hipLaunchKernelGGL(k_longcopy, grid(k_longcopy), dim3(kWave * kEmitWaves), 0, st, s, desc, desc_start + n,
                            desc_cap, o.dout, o.dcap, &o.ctr->oob);
         HIP_TRY(hipGetLastError());
       }
-      if (!exact || hc->n_desc > 0) {
+      if (!desc_copy && (!exact || hc->n_desc > 0)) {
         const uint64_t nd_grid = exact ? hc->n_desc : desc_cap;
         hipLaunchKernelGGL(k_winmap,
                            dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nd_grid + 255) / 256, 8192))),

@@ -48,11 +48,11 @@ for step in "$@"; do
     tests) timeout -k 10 1000 $PYT tests -m gpu --timeout 600 --durations=15 > $OUT/pytest_gpu.log 2>&1 ;;
     serve) timeout -k 10 600 $PYT tests/test_gpu_serve.py tests/test_gpu_serve_churn.py tests/test_gpu_shim.py -m gpu \
              --timeout 300 > $OUT/pytest_serve.log 2>&1 ;;
-    ab) for V in base:X=0 long:MQM_LONG_PART=256; do
+    ab) for V in base:X=0 long:MQM_LONG_PART=256 desccopy:MQM_DESC_COPY=1; do
           N=${V%%:*}; E=${V#*:}
           env $E timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_$N.json 2> $OUT/bench_fast_$N.log || exit 1
         done ;;
-    c4ab) for V in base:X=0 nolong:MQM_LONG_PART=0; do
+    c4ab) for V in base:X=0 long:MQM_LONG_PART=256; do
           N=${V%%:*}; E=${V#*:}
           env $E timeout -k 10 600 python3 -u bench.py --config 4 --shard 0/8 $FAST > $OUT/bench_c4_$N.json \
             2> $OUT/bench_c4_$N.log || exit 1
