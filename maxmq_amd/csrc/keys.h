@@ -108,4 +108,31 @@ MQM_HD uint64_t bloom_bits(uint64_t h) {
   return (1ull << ((h >> 34) & 63)) | (1ull << ((h >> 40) & 63)) | (1ull << ((h >> 46) & 63));
 }
 
+// The walk's tokenizer (match.hip k_walk): a lane holds 16 topic bytes as 4
+// little-endian words, bytes at or past the topic's end zeroed.  -> a 16-bit
+// mask of the '/' bytes (bit i = byte i).  Per byte exactly: the high bit of
+// ((x & 0x7F..) + 0x7F..) | x is set for every non-zero byte of x and no carry
+// crosses a byte, so no borrow from a '/' can flag its neighbour (the usual
+// (x - 0x01..) & ~x trick flags a '.' after a '/').  tests/harness/tok_test.cpp
+// checks it against a byte scan.
+MQM_HD uint32_t slash_mask16(const uint32_t (&b4)[4]) {
+  uint32_t sm = 0;
+  for (int k = 0; k < 4; k++) {
+    const uint32_t x = b4[k] ^ 0x2F2F2F2Fu;  // zero byte where '/'
+    const uint32_t y = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+    const uint32_t z = ~y & 0x80808080u;
+    sm |= (((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u)) << (4 * k);
+  }
+  return sm;
+}
+// bytes [r, r + 4) of the 8-byte little-endian pair (lo, hi), r in 0..3
+// (v_alignbyte_b32 on the device)
+MQM_HD uint32_t align_byte(uint32_t hi, uint32_t lo, uint32_t r) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_alignbyte(hi, lo, r);
+#else
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * r));
+#endif
+}
+
 }  // namespace mqm

@@ -422,7 +422,7 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
       for (int k = 0; k < 5; k++) w[k] = *reinterpret_cast<const uint32_t *>(min(a0 + 4 * k, lastw));
       uint32_t b4[4];  // the lane's 16 bytes, little-endian words, shifted by r
 #pragma unroll
-      for (int k = 0; k < 4; k++) b4[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], r);
+      for (int k = 0; k < 4; k++) b4[k] = align_byte(w[k + 1], w[k], r);
       // bytes at or past len read as 0 (never a separator)
 #pragma unroll
       for (int k = 0; k < 4; k++) {
@@ -435,16 +435,7 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
         for (int k = 0; k < 4; k++) reinterpret_cast<uint32_t *>(L.stage)[4 * gl + k] = b4[k];
         dollar = (__shfl(b4[0], gbase, 64) & 0xFFu) == '$';
       }
-      // '/' bytes: a 16-bit mask of the lane's bytes
-      uint32_t sm = 0;
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const uint32_t x = b4[k] ^ 0x2F2F2F2Fu;  // zero byte where '/'
-        // high bit set per non-zero byte, exactly (no carry crosses a byte: 0x7F + 0x7F < 0x100)
-        const uint32_t y = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
-        const uint32_t z = ~y & 0x80808080u;  // where '/'
-        sm |= (((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u)) << (4 * k);
-      }
+      const uint32_t sm = slash_mask16(b4);  // the lane's '/' bytes (keys.h)
       const uint32_t cnt = __popc(sm);
       uint32_t pre = cnt;  // inclusive prefix over the group's lanes
 #pragma unroll

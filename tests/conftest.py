@@ -28,6 +28,7 @@ _make("maxmq_amd/csrc", "maxmq_amd/_lib/libmqmatch.so")
 _make("tests/harness", "tests/harness/_build/shim_harness")
 _make("tests/harness", "tests/harness/_build/churn_harness")
 _make("tests/harness", "tests/harness/_build/guard_test")
+_make("tests/harness", "tests/harness/_build/tok_test")
 
 
 @pytest.fixture(scope="session")

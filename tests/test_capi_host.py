@@ -129,3 +129,16 @@ def test_launch_guard_refuses_missing_or_short_arrays():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.strip().endswith("OK") and r.stdout.count("-> -1") == 7, r.stdout
+
+
+def test_walk_tokenizer_masks_match_a_byte_scan():
+    """keys.h slash_mask16 / align_byte — the word-level separator search of
+    match.hip k_walk's tokenizer — against a byte scan on random topics at
+    every alignment (tests/harness/tok_test.cpp, CPU)."""
+    import subprocess
+
+    exe = os.path.join(ROOT, "tests", "harness", "_build", "tok_test")
+    if not os.path.exists(exe):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "tests", "harness")])
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr
