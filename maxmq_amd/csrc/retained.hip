@@ -86,6 +86,7 @@ struct RevCtr {
   unsigned long long skipped;     // items the reference visits that the edge index jumps over
   unsigned int ovf;               // kOvf* bits
   unsigned int pad;
+  unsigned long long appended;    // items appended to the lists over all levels (chunk padding excluded)
   unsigned long long n_ltasks;    // level tasks of the current level (reset before each level)
   unsigned long long need_ltasks; // most level tasks any level appended (also past the capacity)
   unsigned long long items[1];    // [levels + 1]
@@ -166,6 +167,45 @@ __device__ __forceinline__ uint64_t wave_reserve(unsigned long long *ctr, uint64
   return (((uint64_t)hi << 32) | lo) + ex;
 }
 
+// A wavefront's private chunk of a list: slots [base, base + size) reserved
+// with one global atomic and filled in order (wave-uniform state).  One
+// atomic per 64 appends on one counter serialised the level kernels: one
+// address takes ~88 returning atomics per microsecond (MI355X_MICROARCH,
+// dequeue), and C5's levels appended ~2.8M times (r05f rev-stats).  The
+// unused tail of a chunk is padded with dead entries (items: node kNone;
+// emissions: filter kNone, empty) when the wave takes a new chunk or leaves.
+struct WaveChunk {
+  uint64_t base = 0, fill = 0, size = 0;
+};
+constexpr uint64_t kChunkMin = 256, kChunkMax = 2048;
+
+// -> this lane's first slot for its v appends (every lane of the wave calls it)
+template <class Pad>
+__device__ __forceinline__ uint64_t chunk_take(WaveChunk &c, unsigned long long *ctr, uint64_t v, Pad &&pad,
+                                               unsigned long long *need, uint64_t cap, unsigned int *ovf,
+                                               unsigned int ovf_bit) {
+  uint64_t total;
+  const uint64_t ex = wave_excl(v, &total);
+  if (total == 0) return 0;
+  if (c.fill + total > c.size) {
+    if (c.size > c.fill) pad(c.base + c.fill, c.size - c.fill);
+    const uint64_t want = max(total, min(kChunkMax, max(kChunkMin, 8 * total)));
+    unsigned long long b = 0;
+    if ((threadIdx.x & 63) == 0) {
+      b = atomicAdd(ctr, (unsigned long long)want);
+      if (need) atomicMax(need, b + want);
+      if (b + want > cap) atomicOr(ovf, ovf_bit);
+    }
+    const uint32_t lo = __shfl((uint32_t)b, 0, 64), hi = __shfl((uint32_t)(b >> 32), 0, 64);
+    c.base = ((uint64_t)hi << 32) | lo;
+    c.fill = 0;
+    c.size = want;
+  }
+  const uint64_t at = c.base + c.fill + ex;
+  c.fill += total;
+  return at;
+}
+
 __device__ __forceinline__ uint64_t bcast64(uint64_t v, int src) {
   const uint32_t lo = __shfl((uint32_t)v, src, 64), hi = __shfl((uint32_t)(v >> 32), src, 64);
   return ((uint64_t)hi << 32) | lo;
@@ -241,6 +281,33 @@ struct LevelArgs {
   uint64_t ltask_cap;
 };
 
+// edge j of a wildcard + literal index range, written at slot `pos` of the
+// emissions (the literal is last: c's message, else Retained.Get("") through
+// an empty retainPath, topics.go:474) or of level d + 2's list (c, when it can
+// continue); anything else writes an empty emission / a dead item
+__device__ __forceinline__ void rev_index_edge(const DeviceRetained &r, const LevelArgs &a, bool root, bool emit,
+                                               uint32_t f, uint32_t need, uint32_t j, uint64_t pos) {
+  const uint2 ed = r.inv[j];
+  const uint32_t c = ed.y;
+  bool valid = !(root && ed.x == r.sys_child);
+  if (emit) {
+    Emit em{kNone, 0, 0, 0};
+    if (valid) {
+      if (retained_node(r, c))
+        em = Emit{f, 0, r.cum[c], r.cum[c] + 1};
+      else if (r.has_empty)
+        em = Emit{f, 0, (uint32_t)r.n_ret, (uint32_t)r.n_ret + 1};
+    }
+    if (pos < a.emit_cap) a.emit[pos] = em;
+  } else {
+    valid = valid && (r.nflags[c] & need) != 0;
+    if (pos < a.item_cap) {
+      a.skip_f[pos] = f;
+      a.skip_n[pos] = valid ? c : kNone;
+    }
+  }
+}
+
 // a thread per item of level d; the loop is grid-stride over the level's
 // count as the previous launch left it in ctr->items[d]
 __global__ __launch_bounds__(kThreads) void k_level(LevelArgs a) {
@@ -248,6 +315,25 @@ __global__ __launch_bounds__(kThreads) void k_level(LevelArgs a) {
   const int lane = threadIdx.x & 63;
   const uint64_t cnt = a.d == 0 ? a.n : min((uint64_t)a.ctr->items[a.d], a.item_cap);
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  // the wave's chunks of the next level's list, the level after (edge-index
+  // jumps) and the emissions; dead-entry padding for their unused tails
+  WaveChunk cnext, cskip, cemit;
+  uint64_t app = 0, skipped_sum = 0;  // (lane 0 / every lane: flushed once at the end)
+  auto pad_items = [&](uint32_t *lf, uint32_t *ln) {
+    return [&a, lf, ln, lane](uint64_t pos, uint64_t len) {
+      for (uint64_t k = lane; k < len; k += 64)
+        if (pos + k < a.item_cap) {
+          lf[pos + k] = 0;
+          ln[pos + k] = kNone;
+        }
+    };
+  };
+  auto pad_next = pad_items(a.next_f, a.next_n);
+  auto pad_skip = pad_items(a.skip_f, a.skip_n);
+  auto pad_emit = [&](uint64_t pos, uint64_t len) {
+    for (uint64_t k = lane; k < len; k += 64)
+      if (pos + k < a.emit_cap) a.emit[pos + k] = Emit{kNone, 0, 0, 0};
+  };
   // whole wavefronts iterate together (the appends below are wave-collective)
   for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < cnt; base += stride) {
     const uint64_t i = base + lane;
@@ -342,9 +428,9 @@ __global__ __launch_bounds__(kThreads) void k_level(LevelArgs a) {
     // next-level items: one per literal hit, the child list of a wildcard
     const uint32_t nn = nx_one != kNone ? 1u : ch_hi - ch_lo;
     if (__any(nn != 0)) {
-      const uint64_t at = wave_reserve(&a.ctr->items[a.d + 1], nn);
-      if (lane == 63) atomicMax(&a.ctr->need_items, (unsigned long long)(at + nn));
-      if (at + nn > a.item_cap) atomicOr(&a.ctr->ovf, (unsigned)kOvfItems);
+      const uint64_t at = chunk_take(cnext, &a.ctr->items[a.d + 1], nn, pad_next, &a.ctr->need_items, a.item_cap,
+                                     &a.ctr->ovf, kOvfItems);
+      app += nn;
       // "$SYS" at the root, and every child that cannot continue (node flags),
       // become dead items (kNone): the next level skips them without a read
       const uint32_t skip = a.d == 0 ? r.sys_child : kNone;
@@ -389,79 +475,55 @@ __global__ __launch_bounds__(kThreads) void k_level(LevelArgs a) {
       }
     }
     if (__any(ne != 0)) {
-      const uint64_t at = wave_reserve(&a.ctr->n_emit, ne);
-      if (at + ne > a.emit_cap) atomicOr(&a.ctr->ovf, (unsigned)kOvfEmit);
+      const uint64_t at = chunk_take(cemit, &a.ctr->n_emit, ne, pad_emit, nullptr, a.emit_cap, &a.ctr->ovf,
+                                     kOvfEmit);
       if (ne > 0 && at < a.emit_cap) a.emit[at] = e0;
       if (ne > 1 && at + 1 < a.emit_cap) a.emit[at + 1] = e1;
     }
-    if (__any(skipped != 0)) {  // statistics: the reference's level d + 1 items
-      uint64_t tot;
-      (void)wave_excl(skipped, &tot);
-      if (lane == 0) atomicAdd(&a.ctr->skipped, (unsigned long long)tot);
-    }
-    // index ranges, a wavefront each, 64 edges per step, outputs compacted
+    skipped_sum += skipped;  // statistics: the reference's level d + 1 items
+    // index ranges: every edge gets its slot up front (one reservation per
+    // lane's range), a wavefront writes each range, 64 edges per step; an
+    // edge that yields nothing writes a dead item / an empty emission
     uint64_t rt = __ballot(rg_hi > rg_lo);
-    if (a.ltasks && rt) {  // ... or chunks for k_level_tasks
+    if (rt) {
       const uint32_t rn = rg_hi - rg_lo;
-      const uint32_t nch = (rn + kTaskEdges - 1) / kTaskEdges;
-      const uint64_t t0 = wave_reserve(&a.ctr->n_ltasks, nch);
-      if (lane == 63) atomicMax(&a.ctr->need_ltasks, (unsigned long long)(t0 + nch));
-      if (t0 + nch > a.ltask_cap) atomicOr(&a.ctr->ovf, (unsigned)kOvfLTasks);
-      for (uint32_t k = 0; k < nch && t0 + k < a.ltask_cap; k++)
-        a.ltasks[t0 + k] = LTask{f, rg_lo + k * kTaskEdges, min(kTaskEdges, rn - k * kTaskEdges), need2, 0,
-                                 rg_emit ? kLTIndexEmit : kLTIndexItems, a.d == 0 ? 1u : 0u};
-      rt = 0;
-    }
-    while (rt) {
-      const int src = __builtin_ctzll(rt);
-      rt &= rt - 1;
-      const uint32_t sf = __shfl(f, src, 64), slo = __shfl(rg_lo, src, 64), shi = __shfl(rg_hi, src, 64);
-      const uint32_t sneed = __shfl(need2, src, 64);
-      const bool semit = __shfl((uint32_t)rg_emit, src, 64) != 0;
-      const bool sroot = a.d == 0;
-      for (uint32_t j0 = slo; j0 < shi; j0 += 64) {
-        const uint32_t j = j0 + lane;
-        bool valid = j < shi;
-        uint32_t c = 0;
-        Emit em{sf, 0, 0, 0};
-        if (valid) {
-          const uint2 ed = r.inv[j];
-          c = ed.y;
-          valid = !(sroot && ed.x == r.sys_child);
-          if (valid && !semit) {
-            valid = (r.nflags[c] & sneed) != 0;
-          } else if (valid) {  // the literal is last: c's message, else Retained.Get("") (:474)
-            if (retained_node(r, c))
-              em = Emit{sf, 0, r.cum[c], r.cum[c] + 1};
-            else if (r.has_empty)
-              em = Emit{sf, 0, (uint32_t)r.n_ret, (uint32_t)r.n_ret + 1};
-            else
-              valid = false;
-          }
-        }
-        const uint64_t m = __ballot(valid);
-        if (!m) continue;
-        const uint32_t k = (uint32_t)__popcll(m);
-        unsigned long long base = 0;
-        if (lane == 0) base = atomicAdd(semit ? &a.ctr->n_emit : &a.ctr->items[a.d + 2], (unsigned long long)k);
-        base = bcast64(base, 0);
-        const uint64_t pos = base + __popcll(m & ((1ull << lane) - 1ull));
-        if (semit) {
-          if (lane == 0 && base + k > a.emit_cap) atomicOr(&a.ctr->ovf, (unsigned)kOvfEmit);
-          if (valid && pos < a.emit_cap) a.emit[pos] = em;
-        } else {
-          if (lane == 0) {
-            atomicMax(&a.ctr->need_items, base + k);
-            if (base + k > a.item_cap) atomicOr(&a.ctr->ovf, (unsigned)kOvfItems);
-          }
-          if (valid && pos < a.item_cap) {
-            a.skip_f[pos] = sf;
-            a.skip_n[pos] = c;
-          }
-        }
+      const uint64_t ra_e = chunk_take(cemit, &a.ctr->n_emit, rg_emit ? rn : 0u, pad_emit, nullptr, a.emit_cap,
+                                       &a.ctr->ovf, kOvfEmit);
+      const uint64_t ra_s = chunk_take(cskip, &a.ctr->items[a.d + 2], rg_emit ? 0u : rn, pad_skip,
+                                       &a.ctr->need_items, a.item_cap, &a.ctr->ovf, kOvfItems);
+      app += rg_emit ? 0u : rn;
+      const uint64_t ra = rg_emit ? ra_e : ra_s;
+      if (a.ltasks) {  // ... or chunks for k_level_tasks
+        const uint32_t nch = (rn + kTaskEdges - 1) / kTaskEdges;
+        const uint64_t t0 = wave_reserve(&a.ctr->n_ltasks, nch);
+        if (lane == 63) atomicMax(&a.ctr->need_ltasks, (unsigned long long)(t0 + nch));
+        if (t0 + nch > a.ltask_cap) atomicOr(&a.ctr->ovf, (unsigned)kOvfLTasks);
+        for (uint32_t k = 0; k < nch && t0 + k < a.ltask_cap; k++)
+          a.ltasks[t0 + k] = LTask{f, rg_lo + k * kTaskEdges, min(kTaskEdges, rn - k * kTaskEdges), need2,
+                                   ra + (uint64_t)k * kTaskEdges, rg_emit ? kLTIndexEmit : kLTIndexItems,
+                                   a.d == 0 ? 1u : 0u};
+        rt = 0;
+      }
+      while (rt) {
+        const int src = __builtin_ctzll(rt);
+        rt &= rt - 1;
+        const uint32_t sf = __shfl(f, src, 64), slo = __shfl(rg_lo, src, 64), shi = __shfl(rg_hi, src, 64);
+        const uint32_t sneed = __shfl(need2, src, 64);
+        const bool semit = __shfl((uint32_t)rg_emit, src, 64) != 0;
+        const uint64_t sra = bcast64(ra, src);
+        for (uint32_t j = slo + lane; j < shi; j += 64)
+          rev_index_edge(r, a, a.d == 0, semit, sf, sneed, j, sra + (j - slo));
       }
     }
   }
+  if (cnext.size > cnext.fill) pad_next(cnext.base + cnext.fill, cnext.size - cnext.fill);
+  if (cskip.size > cskip.fill) pad_skip(cskip.base + cskip.fill, cskip.size - cskip.fill);
+  if (cemit.size > cemit.fill) pad_emit(cemit.base + cemit.fill, cemit.size - cemit.fill);
+  uint64_t tot;
+  (void)wave_excl(skipped_sum, &tot);
+  if (lane == 0 && tot) atomicAdd(&a.ctr->skipped, (unsigned long long)tot);
+  (void)wave_excl(app, &tot);
+  if (lane == 0 && tot) atomicAdd(&a.ctr->appended, (unsigned long long)tot);
 }
 
 // k_level_tasks: a wavefront per task of the level (grid-stride), 64
@@ -484,47 +546,7 @@ __global__ __launch_bounds__(kThreads) void k_level_tasks(LevelArgs a) {
       continue;
     }
     const bool semit = k.kind == kLTIndexEmit;
-    for (uint32_t j0 = 0; j0 < k.n; j0 += 64) {
-      const uint32_t j = k.lo + j0 + lane;
-      bool valid = j0 + lane < k.n;
-      uint32_t c = 0;
-      Emit em{k.f, 0, 0, 0};
-      if (valid) {
-        const uint2 ed = r.inv[j];
-        c = ed.y;
-        valid = !(k.root && ed.x == r.sys_child);
-        if (valid && !semit) {
-          valid = (r.nflags[c] & k.need) != 0;
-        } else if (valid) {  // the literal is last: c's message, else Retained.Get("") (:474)
-          if (retained_node(r, c))
-            em = Emit{k.f, 0, r.cum[c], r.cum[c] + 1};
-          else if (r.has_empty)
-            em = Emit{k.f, 0, (uint32_t)r.n_ret, (uint32_t)r.n_ret + 1};
-          else
-            valid = false;
-        }
-      }
-      const uint64_t m = __ballot(valid);
-      if (!m) continue;
-      const uint32_t cnt = (uint32_t)__popcll(m);
-      unsigned long long base = 0;
-      if (lane == 0) base = atomicAdd(semit ? &a.ctr->n_emit : &a.ctr->items[a.d + 2], (unsigned long long)cnt);
-      base = bcast64(base, 0);
-      const uint64_t pos = base + __popcll(m & ((1ull << lane) - 1ull));
-      if (semit) {
-        if (lane == 0 && base + cnt > a.emit_cap) atomicOr(&a.ctr->ovf, (unsigned)kOvfEmit);
-        if (valid && pos < a.emit_cap) a.emit[pos] = em;
-      } else {
-        if (lane == 0) {
-          atomicMax(&a.ctr->need_items, base + cnt);
-          if (base + cnt > a.item_cap) atomicOr(&a.ctr->ovf, (unsigned)kOvfItems);
-        }
-        if (valid && pos < a.item_cap) {
-          a.skip_f[pos] = k.f;
-          a.skip_n[pos] = c;
-        }
-      }
-    }
+    for (uint32_t j = lane; j < k.n; j += 64) rev_index_edge(r, a, k.root != 0, semit, k.f, k.need, k.lo + j, k.at + j);
   }
 }
 
@@ -560,11 +582,9 @@ __device__ __forceinline__ Run fold_runs(uint32_t f, uint64_t cnt) {
 // grid-stride over the emissions the level kernels appended
 __global__ __launch_bounds__(kThreads) void k_emit_count(const Emit *__restrict__ e, uint64_t cap, RevCtr *ctr,
                                                         unsigned long long *__restrict__ fcount, uint32_t levels) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) {  // the level kernels are done: total their lists
-    unsigned long long t = 0;
-    for (uint32_t d = 1; d <= levels; d++) t += ctr->items[d];
-    ctr->items_total = t + ctr->skipped;
-  }
+  if (blockIdx.x == 0 && threadIdx.x == 0)  // the level kernels are done: the items appended (no padding)
+    ctr->items_total = ctr->appended + ctr->skipped;
+  (void)levels;
   const uint64_t ne = min((uint64_t)ctr->n_emit, cap);
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < ne; base += stride) {
@@ -573,7 +593,7 @@ __global__ __launch_bounds__(kThreads) void k_emit_count(const Emit *__restrict_
     const uint32_t f = ok ? e[i].f : 0xFFFFFFFFu;
     const uint64_t cnt = ok ? e[i].hi - e[i].lo : 0;
     const Run r = fold_runs(f, cnt);
-    if (ok && r.last) atomicAdd(&fcount[f], (unsigned long long)r.inc);
+    if (ok && r.last && f != kNone) atomicAdd(&fcount[f], (unsigned long long)r.inc);  // (kNone: chunk padding)
   }
 }
 
@@ -601,7 +621,7 @@ __global__ __launch_bounds__(kThreads) void k_emit_place(const Emit *__restrict_
     const uint64_t cnt = it.hi - it.lo;
     const Run r = fold_runs(it.f, cnt);
     unsigned long long rb = 0;
-    if (ok && r.last) rb = foff[it.f] + atomicAdd(&fcur[it.f], (unsigned long long)r.inc);
+    if (ok && r.last && it.f != kNone) rb = foff[it.f] + atomicAdd(&fcur[it.f], (unsigned long long)r.inc);
     const uint64_t pos = bcast64(rb, r.last_lane) + (r.inc - cnt);  // run base + the run's entries before this lane
     if (!ok || cnt == 0) continue;
     if (pos + cnt > out_cap) {
