@@ -101,10 +101,13 @@ def parse():
                     help="forward: Subscribers (headline); reverse: Messages over retained topics (config 5); "
                          "churn: Subscribe/Unsubscribe at rate with background snapshot rebuilds")
     ap.add_argument("--churn-ops", type=int, default=1000000, help="churn: mutations per round (half unsubscribes)")
-    ap.add_argument("--serve-churn-s", type=float, default=20.0,
+    ap.add_argument("--serve-churn-s", type=float, default=30.0,
                     help="churn: seconds of per-publish calls (64 native callers through MQM_CFG_SERVE) while "
                          "--churn-rate Subscribe/Unsubscribe per second run (0 = skip)")
     ap.add_argument("--churn-rate", type=float, default=100000.0, help="churn: mutations/s during the served leg")
+    ap.add_argument("--churn-build-threads", default="16,4",
+                    help="churn: comma-separated host thread counts for the background rebuild "
+                         "(mqm_build_threads), one served-under-churn leg each")
     ap.add_argument("--retained", type=int, default=50000000, help="reverse: retained topics")
     ap.add_argument("--sweep", default="",
                     help="tuning sweep before the measurement: ';'-separated variants of "
@@ -1077,14 +1080,25 @@ def serve_churn(idx, w, args):
             r["visibility_lag_ms"] = ({"p50": float(np.median(lag)), "p99": float(np.percentile(lag, 99)),
                                        "max": float(lag.max())} if len(lag) else None)
             r["mutations_seen_by_a_call"] = float(seen.mean()) if nm else None
+            ph = (C.c_double * 4)()
+            capi.check("mqm_build_phases_ms", L.mqm_build_phases_ms(idx._h, ph))
+            r["last_build_phases_ms"] = {"replay": ph[0], "flatten": ph[1], "upload": ph[2],
+                                         "build_threads": int(ph[3])}
+        r["host_phase_max"] = idx.serve_host_max_us()
         return r
 
     run(2.0, 0)  # warm: the server, every caller's path
     base = run(min(args.serve_churn_s, 10.0), 0)
-    churn = run(args.serve_churn_s, args.churn_rate)
+    legs = {}
+    for bt in [int(x) for x in str(args.churn_build_threads).split(",") if x.strip()]:
+        capi.check("mqm_build_threads", L.mqm_build_threads(bt))
+        idx.commit_poll(wait=True)  # (the previous leg's mutations built and published)
+        legs[f"build_threads_{bt}"] = run(args.serve_churn_s, args.churn_rate)
+        log(f"[serve churn] build threads {bt}: {legs[f'build_threads_{bt}']}")
+    capi.check("mqm_build_threads", L.mqm_build_threads(0))
     return {"threads": T, "driver": "native threads (tools/conc_driver.cpp mqd_serve_churn)",
             "index": "MQM_CFG_ASYNC_COMMIT | MQM_CFG_SERVE, commit_policy(0 ops, 50 ms)",
-            "baseline_no_mutations": base, "under_churn": churn, "target_rate": args.churn_rate}
+            "baseline_no_mutations": base, "under_churn": legs, "target_rate": args.churn_rate}
 
 
 def run_reverse(args, dist, rank, world, local, dev):

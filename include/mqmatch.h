@@ -229,6 +229,13 @@ typedef struct {
   int32_t has_snapshot, building;
 } mqm_commit_state;
 int mqm_commit_state_get(mqm_index *h, mqm_commit_state *out);
+/* the last published build's phases (ms[4]): delta-log replay, flatten,
+ * upload (ms), then the host threads a flatten runs on */
+int mqm_build_phases_ms(mqm_index *h, double *ms);
+/* host threads for every flatten of this process (0: MQM_BUILD_THREADS, else
+ * min(16, hardware threads)); a background build under served traffic shares
+ * the CPUs with the callers */
+int mqm_build_threads(uint32_t n);
 /* 64-bit digest of the published snapshot's arrays: replicas and rebuilds of
  * the same store state have equal digests */
 int mqm_snapshot_digest(mqm_index *h, uint64_t *out);
@@ -297,6 +304,11 @@ int mqm_serve_device_us(mqm_index *h, double *us);
  * wake-up), result seen to return (result block built); then the share of
  * calls that slept on the completion poller instead of spinning */
 int mqm_serve_host_us(mqm_index *h, double *us);
+/* the longest served call per host phase since the previous call of this
+ * function (us[8]; reads and resets): front buffer, server check / relaunch,
+ * slot wait + post, result wait, result block, batch-path fallback; then the
+ * number of calls over 10 ms, then 0 */
+int mqm_serve_host_max_us(mqm_index *h, double *us);
 int mqm_batching_stats(mqm_index *h, uint64_t *batches, uint64_t *topics);
 /* single-topic calls on the direct path (no collector, no server: the
  * small-batch kernel per call) since the previous call of this function

@@ -267,6 +267,14 @@ class TopicsIndex:
         check("mqm_serve_host_us", lib().mqm_serve_host_us(self._h, v))
         return {"post": v[0], "wait": v[1], "collect": v[2], "slept_share": v[3]}
 
+    def serve_host_max_us(self):
+        """the longest served call per host phase since the previous read (us),
+        and the number of calls over 10 ms"""
+        v = (C.c_double * 8)()
+        check("mqm_serve_host_max_us", lib().mqm_serve_host_max_us(self._h, v))
+        names = ("front", "server_check", "slot_post", "result_wait", "result_block", "fallback")
+        return {"max": dict(zip(names, v[0:6])), "calls_over_10ms": int(v[6])}
+
     def direct_host_us(self):
         """single-topic calls on the direct path since the previous read (us):
         mean and max per phase (front buffer, context, launch + wait, result)"""

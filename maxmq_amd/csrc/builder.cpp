@@ -8,6 +8,10 @@
 #include <new>
 #include <thread>
 
+#include <sys/resource.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include "../../include/mqmatch.h"
 
 namespace mqm {
@@ -153,6 +157,9 @@ bool Builder::busy() {
 }
 
 void Builder::run() {
+  // a background rebuild yields the CPU to the callers it publishes for (its
+  // flatten threads inherit the nice value)
+  (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), 5);
   if (device_ >= 0) {
     if (hipSetDevice(device_) != hipSuccess ||
         hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) {
@@ -192,13 +199,19 @@ void Builder::run() {
           log.replay(shadow_, log.size() / 2);
           throw std::bad_alloc();
         }
+        using ms = std::chrono::duration<double, std::milli>;
         log.replay(shadow_);
         replayed = true;
+        const auto t1 = std::chrono::steady_clock::now();
         auto hs = std::make_shared<HostSnapshot>();
         rc = fault == 2 ? MQM_ENOMEM : flatten(shadow_, hs.get());
         hs->version = version;  // (after flatten, which starts from an empty snapshot)
+        const auto t2 = std::chrono::steady_clock::now();
         if (rc == MQM_OK && device_ >= 0 && !stream_) rc = MQM_EHIP;
         if (rc == MQM_OK) rc = fault == 3 ? MQM_ENOMEM : upload(std::move(hs), device_, stream_, &b.snap);
+        b.phase_ms[0] = ms(t1 - t0).count();
+        b.phase_ms[1] = ms(t2 - t1).count();
+        b.phase_ms[2] = ms(std::chrono::steady_clock::now() - t2).count();
       } catch (const std::bad_alloc &) {
         rc = MQM_ENOMEM;
       } catch (...) {
@@ -260,7 +273,7 @@ uint64_t edges_digest_of(const HostSnapshot &hs) {
   const uint64_t n = hs.edges.size();
   std::vector<uint64_t> part(kChunks, 0);
   std::vector<std::thread> th;
-  const uint32_t nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const uint32_t nt = build_threads();
   for (uint32_t w = 0; w < nt; w++)
     th.emplace_back([&, w] {
       for (uint64_t c = w; c < kChunks; c += nt) {

@@ -67,6 +67,7 @@ struct BuiltSnapshot {
   std::unique_ptr<GpuSnapshot> snap;
   uint64_t version = 0;
   double build_ms = 0;  // replay + flatten + upload
+  double phase_ms[3] = {0, 0, 0};  // replay, flatten, upload
   uint64_t n_ops = 0;   // delta-log entries folded in
 };
 

@@ -137,9 +137,10 @@ struct mqm_index {
   std::atomic<int64_t> submit_due_ns{0};        // policy_ms: when the logged mutations are due (0: none)
   uint64_t policy_ops = 0;               // auto-submit after this many logged mutations (0 = off)
   uint32_t policy_ms = 0;                // ... or when the oldest one is this old (0 = off)
-  std::chrono::steady_clock::time_point journal_t0;
+  std::chrono::steady_clock::time_point journal_t0;  // when the oldest unsubmitted mutation was logged
+  bool journal_dated = false;                          // (journal_t0 is set for the current journal)
   uint64_t builds = 0, last_build_ops = 0;
-  double last_build_ms = 0;
+  double last_build_ms = 0, last_build_phase_ms[3] = {0, 0, 0};
   bool fast_path = true;  // MQM_NO_FAST=1: small batches also take the batch pipeline (A/B, tests)
   bool async() const { return (cfg.flags & MQM_CFG_ASYNC_COMMIT) != 0; }
   // the device-result API's context (mqm_match_device & follow-ups)
@@ -262,7 +263,7 @@ void submit_locked(mqm_index *h) {
   else
     h->builder->submit(std::move(h->journal), h->store.version());
   h->journal.clear();
-  h->journal_t0 = std::chrono::steady_clock::now();
+  h->journal_dated = false;
   h->submit_due_ns.store(0, std::memory_order_relaxed);
 }
 
@@ -275,6 +276,7 @@ int publish_locked(mqm_index *h, int *published) {
   h->builds++;
   h->last_build_ms = b.build_ms;
   h->last_build_ops = b.n_ops;
+  for (int i = 0; i < 3; i++) h->last_build_phase_ms[i] = b.phase_ms[i];
   if (published) *published = 1;
   return install(h, std::shared_ptr<GpuSnapshot>(std::move(b.snap)), b.version);
 }
@@ -283,6 +285,10 @@ int publish_locked(mqm_index *h, int *published) {
 void maybe_submit(mqm_index *h) {
   if (!h->async() || h->journal.empty()) return;
   if (h->policy_ops && h->journal.size() >= h->policy_ops) return submit_locked(h);
+  if (!h->journal_dated) {  // the first mutation since the last submit
+    h->journal_t0 = std::chrono::steady_clock::now();
+    h->journal_dated = true;
+  }
   if (h->policy_ms) {
     const auto due = h->journal_t0 + std::chrono::milliseconds(h->policy_ms);
     if (std::chrono::steady_clock::now() >= due) return submit_locked(h);
@@ -1492,6 +1498,15 @@ struct Server {
   // host-side time per call (ns, summed; mqm_serve_host_us reads and resets):
   // entry -> posted, posted -> result seen, result seen -> returned; calls that slept
   std::atomic<uint64_t> host_ns[3] = {}, host_calls{0}, host_slept{0};
+  // the longest call per host phase (ns; mqm_serve_host_max_us reads and
+  // resets): front buffer, server check / relaunch, slot wait + post, result
+  // wait, result block; then the longest batch-path fallback, calls > 10 ms
+  std::atomic<uint64_t> host_max_ns[6] = {}, host_slow{0};
+  static void note_max(std::atomic<uint64_t> &m, uint64_t v) {
+    uint64_t c = m.load(std::memory_order_relaxed);
+    while (v > c && !m.compare_exchange_weak(c, v, std::memory_order_relaxed)) {
+    }
+  }
   // completion pollers: callers that stopped spinning sleep on waitw[slot];
   // poller p watches the done words of the sleepers on slots i = p mod
   // n_pollers and wakes them (one thread's FUTEX_WAKE calls cap the wake rate
@@ -1670,6 +1685,7 @@ struct Server {
     std::shared_ptr<GpuSnapshot> cur;
     int rc = front_fast(h, &cur) ? MQM_OK : front(h, &cur);  // (commits first with MQM_CFG_AUTOCOMMIT)
     if (rc != MQM_OK) return rc;
+    const auto t_front = clk::now();
     // before posting: the running launch serves a snapshot at least as new as
     // the caller's (any later launch is newer still)
     const uint64_t rv = run_ver.load(std::memory_order_acquire);
@@ -1677,6 +1693,7 @@ struct Server {
       std::lock_guard<std::mutex> g(mu);
       if ((rc = ensure(cur)) != MQM_OK) return rc;
     }
+    const auto t_ens = clk::now();
     const uint64_t k = ticket.fetch_add(1, std::memory_order_relaxed);
     const uint32_t i = (uint32_t)(k % kServeSlots);
     if (!wait_slot(i, k)) {
@@ -1790,13 +1807,26 @@ struct Server {
       }
     }
     free_seq[i].store(k + kServeSlots, std::memory_order_release);
-    host_ns[0] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t0 - t_in).count();
-    host_ns[1] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t_seen - t0).count();
-    host_ns[2] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - t_seen).count();
+    const auto t_end = clk::now();
+    auto ns = [](clk::duration d) { return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(d).count(); };
+    host_ns[0] += ns(t0 - t_in);
+    host_ns[1] += ns(t_seen - t0);
+    host_ns[2] += ns(t_end - t_seen);
     host_calls++;
-    if (status == kServeOk) return rc;
+    note_max(host_max_ns[0], ns(t_front - t_in));
+    note_max(host_max_ns[1], ns(t_ens - t_front));
+    note_max(host_max_ns[2], ns(t0 - t_ens));
+    note_max(host_max_ns[3], ns(t_seen - t0));
+    note_max(host_max_ns[4], ns(t_end - t_seen));
+    if (status == kServeOk) {
+      if (t_end - t_in > std::chrono::milliseconds(10)) host_slow++;
+      return rc;
+    }
     fallbacks++;
-    return direct(topic, len, out);
+    rc = direct(topic, len, out);
+    note_max(host_max_ns[5], ns(clk::now() - t_end));
+    if (clk::now() - t_in > std::chrono::milliseconds(10)) host_slow++;
+    return rc;
   }
   int direct(const char *topic, size_t len, mqm_result **out) {
     uint64_t offs[2] = {0, len};
@@ -1905,6 +1935,15 @@ int mqm_serve_device_us(mqm_index *h, double *us) {
   // s_memrealtime: 100 MHz; us[0] claim -> published, us[1..3] its phases
   us[0] = n ? (double)sv->device_ticks.load() / 100.0 / (double)n : 0.0;
   for (int i = 0; i < 3; i++) us[1 + i] = n ? (double)sv->phase_ticks[i].load() / 100.0 / (double)n : 0.0;
+  return MQM_OK;
+}
+
+int mqm_serve_host_max_us(mqm_index *h, double *us) {
+  Server *sv = h ? h->server.load(std::memory_order_acquire) : nullptr;
+  if (!sv || !us) return MQM_EINVAL;
+  for (int i = 0; i < 6; i++) us[i] = (double)sv->host_max_ns[i].exchange(0) / 1e3;
+  us[6] = (double)sv->host_slow.exchange(0);
+  us[7] = 0.0;
   return MQM_OK;
 }
 
@@ -2088,6 +2127,20 @@ int mqm_commit_state_get(mqm_index *h, mqm_commit_state *out) {
   out->builds = h->builds;
   out->last_build_ops = h->last_build_ops;
   out->last_build_ms = h->last_build_ms;
+  return MQM_OK;
+}
+
+int mqm_build_threads(uint32_t n) {
+  if (n > 256) return MQM_EINVAL;
+  set_build_threads(n);
+  return MQM_OK;
+}
+
+int mqm_build_phases_ms(mqm_index *h, double *ms) {
+  if (!h || !ms) return MQM_EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  for (int i = 0; i < 3; i++) ms[i] = h->last_build_phase_ms[i];
+  ms[3] = (double)build_threads();
   return MQM_OK;
 }
 

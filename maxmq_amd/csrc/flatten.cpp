@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -23,11 +24,28 @@
 namespace mqm {
 
 namespace {
-// run f(t) for t in [0, n) on up to 16 host threads (the box's CPU share)
+std::atomic<uint32_t> g_build_threads{0};  // mqm_build_threads (0: the default)
+}  // namespace
+
+uint32_t build_threads() {
+  const uint32_t set = g_build_threads.load(std::memory_order_relaxed);
+  if (set) return set;
+  static const uint32_t dflt = [] {
+    const char *e = getenv("MQM_BUILD_THREADS");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? (uint32_t)v : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  }();
+  return dflt;
+}
+
+void set_build_threads(uint32_t n) { g_build_threads.store(n, std::memory_order_relaxed); }
+
+namespace {
+// run f(t) for t in [0, n) on up to build_threads() host threads (default 16,
+// the box's CPU share)
 template <class F>
 void parallel_for(uint32_t n, F &&f) {
-  const uint32_t hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  const uint32_t nt = std::min(hw, n);
+  const uint32_t nt = std::min(build_threads(), n);
   if (nt <= 1) {
     for (uint32_t t = 0; t < n; t++) f(t);
     return;

@@ -70,6 +70,10 @@ struct HostSnapshot {
 
 // Build the snapshot; returns MQM_OK or MQM_ELIMIT.
 int flatten(const Store &st, HostSnapshot *out);
+// host threads a flatten (and the snapshot digest) runs on: mqm_build_threads,
+// else MQM_BUILD_THREADS, else min(16, hardware threads)
+uint32_t build_threads();
+void set_build_threads(uint32_t n);  // 0: back to the default
 
 // Device copy of a HostSnapshot.  Host side tables stay shared with results
 // (shared_ptr) so a result can outlive the next commit.
