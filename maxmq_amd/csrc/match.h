@@ -61,6 +61,7 @@ struct Workspace {
     kSCount, kHCount, kDCount, kDStart, kHStart, kCls, kDfsList, kRecs, kCounters, kDOut, kHOut,
     kDense, kDenseShared, kDenseOffs, kDenseHOffs, kScanTmp, kRawCnt, kTabOff, kTabSize, kTable,
     kInBytes, kInOffs, kListS, kICount, kIStart, kIOut, kNSolo, kDescStart, kDesc, kWin, kMCount, kRunCount, kRunOffs, kRuns, kListW, kListT1, kListT2, kListT3, kListP, kListH, kListRS, kListR,
+    kIMStart, kIScratch,
     // reverse match (retained.hip)
     kROffs, kRNLev, kRWild, kRLOff, kRFCount, kRFCur, kRLevels, kRNCount, kRNOff, kRItemF0, kRItemN0, kRItemF1,
     kRItemN1, kRChild, kRECount, kREOff, kREmit, kRPos, kRChunks, kRCOff, kROut, kRInBytes, kRInOffs, kNumSlots

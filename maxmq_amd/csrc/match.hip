@@ -1823,20 +1823,23 @@ __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *
 }
 
 // ---------------------------------------------------------------------------
-// k_ident<P>: Subscription.Identifiers support (packets.go:250-259).  For every
+// k_ident: Subscription.Identifiers support (packets.go:250-259).  For every
 // bounded topic, the sids of the gathered *multi* entries whose Identifier is
-// > 0 (kMetaIdent), part by part from the walk's record (P0 counts, P1 writes
-// at istart).  A solo entry is its client's only subscription in any topic's
-// gather (that is what solo means, flatten.cpp), so its delivery's map is its
-// first pair {Filter: Identifier} alone, which the host already has from the
-// delivery's first sid: listing it would add nothing.  So only the multi
-// parts are read — C3 gathers 233 entries per topic, almost all solo, and
-// reading each one's word cost ~2 KB per topic.  A node gathered twice
-// repeats its sids; the map the host builds keeps one key per filter, as the
-// reference's does.  DFS topics are handled by k_dfs<3|4> (every entry).
+// > 0 (kMetaIdent), part by part from the walk's record, written once into the
+// topic's Ms-bounded scratch area (mstart = the scan of mcount) with their
+// count; k_ident_pack then moves them to iout at the scan of the counts.  (One
+// pass over the records: round 5's count-then-write pair read every record
+// and identifier word twice, 3.1 + 3.5 ms on C3.)  A solo entry is its
+// client's only subscription in any topic's gather (that is what solo means,
+// flatten.cpp), so its delivery's map is its first pair {Filter: Identifier}
+// alone, which the host already has from the delivery's first sid: listing it
+// would add nothing.  So only the multi parts are read — C3 gathers 233
+// entries per topic, almost all solo.  A node gathered twice repeats its
+// sids; the map the host builds keeps one key per filter, as the reference's
+// does.  DFS topics are handled by k_dfs<3|4> (every entry).
 // ---------------------------------------------------------------------------
-template <int kPhase>
-__global__ __launch_bounds__(256) void k_ident(DeviceSnapshot s, Outputs o, uint32_t n) {
+__global__ __launch_bounds__(256) void k_ident(DeviceSnapshot s, Outputs o, uint32_t n,
+                                               const uint64_t *__restrict__ mstart, uint32_t *__restrict__ scratch) {
   // an 8-lane group per topic: most topics have a few short multi parts, and
   // a wavefront per topic left 56 lanes idle through each topic's dependent
   // loads (C3: 5.5 ms for the two phases, r05d)
@@ -1850,10 +1853,11 @@ __global__ __launch_bounds__(256) void k_ident(DeviceSnapshot s, Outputs o, uint
     uint32_t nid = 0;
     // (the walk writes the record header, which counts the multi parts, for
     // every topic with multi entries)
-    if (cls != kClsDone && o.mcount[t]) {
+    const uint32_t ms = cls != kClsDone ? o.mcount[t] : 0u;
+    if (ms) {
       const uint4 *gt = rec_tail(o.recs, t);
       const uint32_t nm = gt[0].x & 0xFFu;
-      const uint64_t ib = kPhase == 1 ? o.istart[t] : 0;
+      const uint64_t ib = mstart[t];
       for (uint32_t h = 0; h < nm; h++) {  // the multi parts (solo parts: see above)
         const uint4 u = gt[-(int)(1 + h)];
         const uint32_t off = u.x, cnt = u.y;
@@ -1862,12 +1866,29 @@ __global__ __launch_bounds__(256) void k_ident(DeviceSnapshot s, Outputs o, uint
           const uint32_t q = off + j;
           const bool has = j < cnt && ((s.ident_bits[q >> 5] >> (q & 31)) & 1u);
           const uint64_t m = (__ballot(has) >> gbase) & ((1ull << kL) - 1ull);
-          if (kPhase == 1 && has) o.iout[ib + nid + __popcll(m & glt)] = off + j;
+          const uint32_t at = nid + (uint32_t)__popcll(m & glt);
+          if (has && at < ms) scratch[ib + at] = q;  // (at < Ms: the multi entries bound the listed ones)
           nid += (uint32_t)__popcll(m);
         }
       }
+      nid = min(nid, ms);
     }
-    if (kPhase == 0 && gl == 0) o.icount[t] = nid;
+    if (gl == 0) o.icount[t] = nid;
+  }
+}
+
+// 8 lanes per topic: its listed sids from the scratch area to iout[istart[t] ..)
+// (DFS topics: k_dfs<4> writes theirs)
+__global__ __launch_bounds__(256) void k_ident_pack(Outputs o, uint32_t n, const uint64_t *__restrict__ mstart,
+                                                    const uint32_t *__restrict__ scratch, uint64_t cap) {
+  constexpr int kL = 8;
+  const uint32_t gl = threadIdx.x % kL, ng = gridDim.x * (blockDim.x / kL);
+  for (uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) / kL; t < n; t += ng) {
+    if (o.cls[t] == kClsDfs) continue;
+    const uint32_t c = o.icount[t];
+    if (!c) continue;
+    const uint64_t a = o.istart[t], m = mstart[t];
+    for (uint32_t j = gl; j < c; j += kL) put_checked(o.iout, a + j, cap, scratch[m + j], &o.ctr->oob);
   }
 }
 
@@ -2732,8 +2753,19 @@ int identifiers_device(const DeviceSnapshot &s, Workspace &ws, hipStream_t st, I
                         sizeof(uint64_t) * 2 * max_levels;
   const uint32_t fb_blocks = std::max<uint32_t>(1, std::min<uint32_t>(ws.last_n_dfs, 4096));
   const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + 31) / 32, 8192));  // 32 topics per block
+  // the topics' scratch areas: the scan of their multi-entry counts
+  if (ws.get(W::kIMStart, sizeof(uint64_t) * (n + 1))) return -2;
+  uint64_t *mstart = (uint64_t *)ws.ptr(W::kIMStart);
+  if (scan_offsets(ws, o.mcount, mstart, n, st)) return -3;
+  uint64_t *hp = ws.pinned_u64();
+  if (!hp) return -2;
+  HIP_TRY(hipMemcpyAsync(hp, mstart + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  const uint64_t n_multi = hp[0];
+  if (ws.get(W::kIScratch, sizeof(uint32_t) * (n_multi + 1))) return -2;
+  uint32_t *scratch = (uint32_t *)ws.ptr(W::kIScratch);
   if (n > 0) {
-    hipLaunchKernelGGL(k_ident<0>, dim3(blocks), dim3(256), 0, st, s, o, n);
+    hipLaunchKernelGGL(k_ident, dim3(blocks), dim3(256), 0, st, s, o, n, mstart, scratch);
     HIP_TRY(hipGetLastError());
     if (ws.last_n_dfs) {
       hipLaunchKernelGGL(k_dfs<3>, dim3(fb_blocks), dim3(kWave), fb_lds, st, s, ws.last_bytes, ws.last_offs, o,
@@ -2742,16 +2774,14 @@ int identifiers_device(const DeviceSnapshot &s, Workspace &ws, hipStream_t st, I
     }
   }
   if (scan_offsets(ws, o.icount, o.istart, n, st)) return -3;
-  uint64_t *hp = ws.pinned_u64();
-  if (!hp) return -2;
   HIP_TRY(hipMemcpyAsync(hp, o.istart + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   const uint64_t total = hp[0];
   if (ws.get(W::kIOut, sizeof(uint32_t) * (total + 1))) return -2;
   o.iout = (uint32_t *)ws.ptr(W::kIOut);
-  GUARD(o, kNeedIdent | kOIOut, n, "k_ident<1>");
+  GUARD(o, kNeedIdent | kOIOut, n, "k_ident_pack");
   if (n > 0 && total > 0) {
-    hipLaunchKernelGGL(k_ident<1>, dim3(blocks), dim3(256), 0, st, s, o, n);
+    hipLaunchKernelGGL(k_ident_pack, dim3(blocks), dim3(256), 0, st, o, n, mstart, scratch, total);
     HIP_TRY(hipGetLastError());
     if (ws.last_n_dfs) {
       hipLaunchKernelGGL(k_dfs<4>, dim3(fb_blocks), dim3(kWave), fb_lds, st, s, ws.last_bytes, ws.last_offs, o,

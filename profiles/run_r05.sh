@@ -8,7 +8,8 @@
 #   revstats: the C5 reverse bench with the per-level item mix (MQM_REV_STATS=1)
 #   revab   : the C5 reverse bench without and with level tasks (MQM_REV_TASKS=1)
 #   node    : the sharded node step with two rank processes and the HIP matcher (tests/test_gpu_node_step.py)
-#   churnserve: the churn workload with the served-calls-under-churn leg
+#   churnserve: the churn workload with the served-calls-under-churn legs (one per rebuild thread count)
+#   ident   : the Identifiers parity tests (batch, DFS, runs, batching collector)
 #   c4test  : the C4 shard 0/8 full-batch test            -> gpurun_out/TAG/pytest_c4.log
 #   ret     : the retained (reverse-match) tests           -> gpurun_out/TAG/pytest_ret.log
 #   nobloom : the edge-case / random-op parity tests with the edge filter off (MQM_NO_BLOOM=1)
@@ -65,8 +66,10 @@ for step in "$@"; do
           env $E timeout -k 10 600 python3 -u bench.py --workload reverse --steps 3 --warmup 1 --no-cpu-baseline \
             > $OUT/bench_rev_$N.json 2> $OUT/bench_rev_$N.log || exit 1
         done ;;
-    churnserve) timeout -k 10 900 python3 -u bench.py --workload churn --steps 3 --warmup 1 --serve-churn-s 20 \
+    churnserve) timeout -k 10 1100 python3 -u bench.py --workload churn --steps 3 --warmup 1 --serve-churn-s 30 \
              > $OUT/bench_churn.json 2> $OUT/bench_churn.log ;;
+    ident) timeout -k 10 500 $PYT tests/test_gpu_parity.py tests/test_gpu_runs.py tests/test_gpu_batching.py -m gpu \
+             --timeout 200 -k "ident or batched" > $OUT/pytest_ident.log 2>&1 ;;
     c4test) timeout -k 10 600 $PYT tests/test_gpu_c4_shard.py -m gpu --timeout 500 > $OUT/pytest_c4.log 2>&1 ;;
     ret) timeout -k 10 600 $PYT tests/test_gpu_retained.py -m gpu --timeout 300 > $OUT/pytest_ret.log 2>&1 ;;
     nobloom) MQM_NO_BLOOM=1 timeout -k 10 400 $PYT tests/test_gpu_parity.py -m gpu --timeout 200 \
