@@ -204,7 +204,7 @@ void Builder::run() {
         replayed = true;
         const auto t1 = std::chrono::steady_clock::now();
         auto hs = std::make_shared<HostSnapshot>();
-        rc = fault == 2 ? MQM_ENOMEM : flatten(shadow_, hs.get());
+        rc = fault == 2 ? MQM_ENOMEM : flatten(shadow_, hs.get(), device_ < 0);
         hs->version = version;  // (after flatten, which starts from an empty snapshot)
         const auto t2 = std::chrono::steady_clock::now();
         if (rc == MQM_OK && device_ >= 0 && !stream_) rc = MQM_EHIP;
@@ -268,9 +268,8 @@ struct Digest {
 };
 }  // namespace
 
-uint64_t edges_digest_of(const HostSnapshot &hs) {
+uint64_t edges_digest_sum(const EdgeEntry *edges, uint64_t n) {
   constexpr uint64_t kChunks = 64;
-  const uint64_t n = hs.edges.size();
   std::vector<uint64_t> part(kChunks, 0);
   std::vector<std::thread> th;
   const uint32_t nt = build_threads();
@@ -278,16 +277,26 @@ uint64_t edges_digest_of(const HostSnapshot &hs) {
     th.emplace_back([&, w] {
       for (uint64_t c = w; c < kChunks; c += nt) {
         const uint64_t lo = n * c / kChunks, hi = n * (c + 1) / kChunks;
-        Digest d;
-        d.add(hs.edges.data() + lo, (hi - lo) * sizeof(EdgeEntry));
-        part[c] = d.h;
+        uint64_t sum = 0;
+        for (uint64_t s = lo; s < hi; s++) sum += edge_slot_mix(s, edges[s]);
+        part[c] = sum;
       }
     });
   for (auto &x : th) x.join();
+  uint64_t sum = 0;
+  for (uint64_t v : part) sum += v;
+  return sum;
+}
+
+uint64_t edges_digest_final(uint64_t sum, uint64_t n) {
   Digest d;
-  for (uint64_t v : part) d.mix(v);
+  d.mix(sum);
   d.mix(n);
   return d.h;
+}
+
+uint64_t edges_digest_of(const HostSnapshot &hs) {
+  return edges_digest_final(edges_digest_sum(hs.edges.data(), hs.edges.size()), hs.edges.size());
 }
 
 uint64_t snapshot_digest(const HostSnapshot &hs) {

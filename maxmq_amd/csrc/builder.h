@@ -122,8 +122,13 @@ class Builder {
 
 // 64-bit digest of a snapshot's arrays (replicas / shards compare it)
 uint64_t snapshot_digest(const HostSnapshot &hs);
-// digest of the edge table (64 fixed chunks hashed in parallel, combined in
-// order); snapshot_digest uses the kept value once the host copy is released
+// digest of the edge table (a sum of per-slot terms, so the host's chunks and
+// the device's reduction agree); snapshot_digest uses the kept value once the
+// host copy is released or when the device built the table
 uint64_t edges_digest_of(const HostSnapshot &hs);
+// its parts: the sum of edge_slot_mix over the slots (snapshot.h; the device
+// computes the same sum), then the final mix with the slot count
+uint64_t edges_digest_sum(const EdgeEntry *edges, uint64_t n);
+uint64_t edges_digest_final(uint64_t sum, uint64_t n);
 
 }  // namespace mqm

@@ -295,7 +295,68 @@ static void build_reverse_index(const Store &st, const std::vector<uint32_t> &or
     }
 }
 
-int flatten(const Store &st, HostSnapshot *out) {
+void insert_edges_host(HostSnapshot &hs, const EdgeVec &staged) {
+  // (b) stable partition by home slot into kEdgeParts contiguous slot ranges;
+  // (c) linear-probing insertion per partition in edge order, in parallel;
+  // (d) edges whose probe runs past their partition's end, serially in
+  // partition order (snapshot.h: the layout edges.hip reproduces)
+  constexpr uint32_t kChunks = 64, P = kEdgeParts;
+  const uint64_t ne = staged.size(), n_slots = hs.n_buckets * kEdgesPerBucket;
+  std::vector<uint64_t, NoInitAlloc<uint64_t>> home(ne);
+  std::vector<uint64_t> cnt((uint64_t)kChunks * P, 0);  // [chunk][part]
+  parallel_for(kChunks, [&](uint32_t c) {
+    const uint64_t lo = ne * c / kChunks, hi = ne * (c + 1) / kChunks;
+    for (uint64_t e = lo; e < hi; e++) {
+      home[e] = edge_home(staged[e], hs.n_buckets);
+      cnt[(uint64_t)c * P + edge_part_of(home[e], n_slots)]++;
+    }
+  });
+  std::vector<uint64_t> pstart(P + 1, 0);
+  {
+    uint64_t run = 0;
+    for (uint32_t p = 0; p < P; p++) {
+      pstart[p] = run;
+      for (uint32_t c = 0; c < kChunks; c++) {
+        const uint64_t v = cnt[(uint64_t)c * P + p];
+        cnt[(uint64_t)c * P + p] = run;
+        run += v;
+      }
+    }
+    pstart[P] = run;
+  }
+  std::vector<uint32_t, NoInitAlloc<uint32_t>> by_part(ne);
+  parallel_for(kChunks, [&](uint32_t c) {
+    const uint64_t lo = ne * c / kChunks, hi = ne * (c + 1) / kChunks;
+    for (uint64_t e = lo; e < hi; e++) by_part[cnt[(uint64_t)c * P + edge_part_of(home[e], n_slots)]++] = (uint32_t)e;
+  });
+  EdgeEntry empty;
+  memset(&empty, 0, sizeof(empty));
+  empty.parent = kNone;
+  empty.child = kNone;
+  hs.edges.resize(n_slots);
+  std::vector<std::vector<uint32_t>> spill(P);
+  parallel_for(P, [&](uint32_t p) {
+    const uint64_t lo = edge_part_lo(p, n_slots), hi = edge_part_lo(p + 1, n_slots);
+    std::fill(hs.edges.begin() + lo, hs.edges.begin() + hi, empty);
+    for (uint64_t j = pstart[p]; j < pstart[p + 1]; j++) {
+      const uint32_t e = by_part[j];
+      uint64_t slot = home[e];
+      while (slot < hi && hs.edges[slot].parent != kNone) slot++;
+      if (slot == hi)
+        spill[p].push_back(e);
+      else
+        hs.edges[slot] = staged[e];
+    }
+  });
+  for (uint32_t p = 0; p < P; p++)
+    for (uint32_t e : spill[p]) {
+      uint64_t slot = home[e];
+      while (hs.edges[slot].parent != kNone) slot = slot + 1 == n_slots ? 0 : slot + 1;
+      hs.edges[slot] = staged[e];
+    }
+}
+
+int flatten(const Store &st, HostSnapshot *out, bool host_edges) {
   PhaseTimer pt;
   const auto &nodes = st.nodes();
   const uint32_t plus_tok = st.plus_token(), hash_tok = st.hash_token();
@@ -394,6 +455,11 @@ int flatten(const Store &st, HostSnapshot *out) {
     }
   });
   const uint64_t nn = order.size();
+  if (pt.on) {
+    uint64_t mx = 0;
+    for (auto &x : seq) mx = std::max(mx, x.size);
+    fprintf(stderr, "[flatten] nodes %zu items %u largest subtree %zu\n", (size_t)nn, n_items, (size_t)mx);
+  }
   pt.mark("preorder");
 
   // 2. descriptors, subscription ranges, flags — in parallel over preorder
@@ -606,8 +672,7 @@ int flatten(const Store &st, HostSnapshot *out) {
       std::max<uint64_t>(1, (uint64_t)((double)n_literal_edges / (load * kEdgesPerBucket)) + 1);
   hs.n_buckets = buckets;
   hs.n_edges = n_literal_edges;
-  const uint64_t n_slots = buckets * kEdgesPerBucket;
-  if (n_literal_edges >= kNone) return MQM_ELIMIT;
+  if (n_literal_edges >= kNone || buckets * kEdgesPerBucket >= (1ull << 50)) return MQM_ELIMIT;
   // long tokens (> kInlineMax bytes) go to the pool in token-id order
   const Interner &toks = st.tokens();
   std::vector<uint32_t> pool_off(toks.size(), kNone);
@@ -619,16 +684,14 @@ int flatten(const Store &st, HostSnapshot *out) {
     hs.tok_pool.insert(hs.tok_pool.end(), tok.begin(), tok.end());
   }
   // (a) every literal edge in (parent preorder, child list) order, in parallel
-  //     over node ranges; (b) stable partition by home slot into kParts
-  //     contiguous slot ranges; (c) linear-probing insertion per partition in
-  //     edge order, in parallel; (d) edges whose probe runs past their
-  //     partition's end, serially in partition order.  The layout depends on
-  //     kParts only, not on the thread count, so digests are reproducible.
-  constexpr uint32_t kParts = 256, kChunks = 64;
+  //     over node ranges; the table is then built from this list on the host
+  //     (insert_edges_host) or on the device at upload (edges.hip, the same
+  //     bytes: the layout depends on kEdgeParts only, not on the thread count,
+  //     so digests are reproducible)
+  constexpr uint32_t kChunks = 64;
   std::vector<uint64_t> eoff(nn + 1, 0);
   for (uint64_t i = 0; i < nn; i++) eoff[i + 1] = eoff[i] + nlit[i];
-  std::vector<EdgeEntry, NoInitAlloc<EdgeEntry>> staged(n_literal_edges);
-  std::vector<uint64_t, NoInitAlloc<uint64_t>> home(n_literal_edges);
+  EdgeVec staged(n_literal_edges);
   parallel_for(kChunks, [&](uint32_t c) {
     const uint64_t lo = nn * c / kChunks, hi = nn * (c + 1) / kChunks;
     for (uint64_t i = lo; i < hi; i++) {
@@ -647,7 +710,6 @@ int flatten(const Store &st, HostSnapshot *out) {
         e.tok_off = key_is_long(k) ? pool_off[nodes[c2].key] : 0;
         e.tok_len = (uint32_t)tok.size();
         e.desc = hs.nodes[cn];
-        home[e_i] = bucket_of(edge_hash((uint32_t)i, k), hs.n_buckets) * kEdgesPerBucket;
         e_i++;
       }
     }
@@ -670,64 +732,16 @@ int flatten(const Store &st, HostSnapshot *out) {
       }
     });
   }
-  auto part_of = [&](uint64_t slot) { return (uint32_t)((unsigned __int128)slot * kParts / n_slots); };
-  auto part_lo = [&](uint32_t p) { return (uint64_t)(((unsigned __int128)n_slots * p + kParts - 1) / kParts); };
   pt.mark("e:stage");
-  std::vector<uint64_t> cnt((uint64_t)kChunks * kParts, 0);  // [chunk][part]
-  parallel_for(kChunks, [&](uint32_t c) {
-    const uint64_t lo = n_literal_edges * c / kChunks, hi = n_literal_edges * (c + 1) / kChunks;
-    for (uint64_t e = lo; e < hi; e++) cnt[(uint64_t)c * kParts + part_of(home[e])]++;
-  });
-  std::vector<uint64_t> pstart(kParts + 1, 0);
-  {
-    uint64_t run = 0;
-    for (uint32_t p = 0; p < kParts; p++) {
-      pstart[p] = run;
-      for (uint32_t c = 0; c < kChunks; c++) {
-        const uint64_t v = cnt[(uint64_t)c * kParts + p];
-        cnt[(uint64_t)c * kParts + p] = run;
-        run += v;
-      }
-    }
-    pstart[kParts] = run;
-  }
-  std::vector<uint32_t, NoInitAlloc<uint32_t>> by_part(n_literal_edges);
-  parallel_for(kChunks, [&](uint32_t c) {
-    const uint64_t lo = n_literal_edges * c / kChunks, hi = n_literal_edges * (c + 1) / kChunks;
-    for (uint64_t e = lo; e < hi; e++) by_part[cnt[(uint64_t)c * kParts + part_of(home[e])]++] = (uint32_t)e;
-  });
-  pt.mark("e:part");
-  EdgeEntry empty;
-  memset(&empty, 0, sizeof(empty));
-  empty.parent = kNone;
-  empty.child = kNone;
-  hs.edges.resize(n_slots);
-  pt.mark("e:alloc");
-  std::vector<std::vector<uint32_t>> spill(kParts);
-  parallel_for(kParts, [&](uint32_t p) {
-    const uint64_t lo = part_lo(p), hi = part_lo(p + 1);
-    std::fill(hs.edges.begin() + lo, hs.edges.begin() + hi, empty);
-    for (uint64_t j = pstart[p]; j < pstart[p + 1]; j++) {
-      const uint32_t e = by_part[j];
-      uint64_t slot = home[e];
-      while (slot < hi && hs.edges[slot].parent != kNone) slot++;
-      if (slot == hi)
-        spill[p].push_back(e);
-      else
-        hs.edges[slot] = staged[e];
-    }
-  });
-  pt.mark("e:insert");
-  for (uint32_t p = 0; p < kParts; p++)
-    for (uint32_t e : spill[p]) {
-      uint64_t slot = home[e];
-      while (hs.edges[slot].parent != kNone) slot = slot + 1 == n_slots ? 0 : slot + 1;
-      hs.edges[slot] = staged[e];
-    }
-  pt.mark("edges");
   if (st.retained_len() > 0) {
     build_reverse_index(st, order, staged, hs);
     pt.mark("rev-index");
+  }
+  if (host_edges) {
+    insert_edges_host(hs, staged);
+    pt.mark("e:insert");
+  } else {
+    hs.staged = std::move(staged);
   }
   if (hs.tok_pool.empty()) hs.tok_pool.push_back(0);
   if (hs.subs.empty()) hs.subs.push_back(SubEnt{0, 0});
@@ -760,8 +774,13 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
                                                hs->child_ids.data(), hs->cum.data(),       hs->refs.data(),
                                                hs->rch_off.data(),   hs->rch_refs.data(),  hs->rinv.data(),
                                                hs->rgroups.data()};
+  // the table is built on the device from the staged edges (flatten's
+  // host_edges = false) unless the host built it
+  const bool dev_edges = hs->edges.empty();
+  const uint64_t n_slots = hs->n_buckets * kEdgesPerBucket;
+  if (dev_edges && hs->staged.size() != hs->n_edges) return MQM_EINVAL;
   const size_t sz[GpuSnapshot::kNumBuffers] = {
-      hs->nodes.size() * sizeof(NodeDesc), hs->edges.size() * sizeof(EdgeEntry), hs->subs.size() * sizeof(SubEnt),
+      hs->nodes.size() * sizeof(NodeDesc), n_slots * sizeof(EdgeEntry), hs->subs.size() * sizeof(SubEnt),
       hs->tok_pool.size(),                 hs->subtree.size() * 4,                hs->child_off.size() * 4,
       hs->child_ids.size() * 4,            hs->cum.size() * 4,                    hs->refs.size() * 8,
       hs->rch_off.size() * 4,              hs->rch_refs.size() * 8,               hs->rinv.size() * 8,
@@ -770,9 +789,30 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
     if (i >= 4 && !ret) break;
     // +64 B: walk_step reads 64 B at any node descriptor (the last one included)
     if (hipMalloc(&g->buffers[i], (sz[i] ? sz[i] : 16) + 64) != hipSuccess) return MQM_ENOMEM;
-    if (sz[i] && hipMemcpyAsync(g->buffers[i], src[i], sz[i], hipMemcpyHostToDevice, stream) != hipSuccess)
+    if (sz[i] && !(i == 1 && dev_edges) &&
+        hipMemcpyAsync(g->buffers[i], src[i], sz[i], hipMemcpyHostToDevice, stream) != hipSuccess)
       return MQM_EHIP;
     g->device_bytes += sz[i];
+  }
+  if (dev_edges) {  // edges.hip; a run-past overflow (never seen) falls back to the host build
+    const uint64_t ne = hs->staged.size();
+    void *d_staged = nullptr;
+    if (hipMallocAsync(&d_staged, ne * sizeof(EdgeEntry) + 64, stream) != hipSuccess) return MQM_ENOMEM;
+    if (ne && hipMemcpyAsync(d_staged, hs->staged.data(), ne * sizeof(EdgeEntry), hipMemcpyHostToDevice, stream) !=
+                  hipSuccess)
+      return MQM_EHIP;
+    uint64_t sum = 0;
+    const int rc = build_edges_device((const EdgeEntry *)d_staged, ne, hs->n_buckets, (EdgeEntry *)g->buffers[1],
+                                      stream, &sum);
+    if (hipFreeAsync(d_staged, stream) != hipSuccess || rc < 0) return MQM_EHIP;
+    if (rc == 1) {
+      insert_edges_host(*hs, hs->staged);
+      if (hipMemcpyAsync(g->buffers[1], hs->edges.data(), sz[1], hipMemcpyHostToDevice, stream) != hipSuccess)
+        return MQM_EHIP;
+    } else {
+      hs->edges_digest = edges_digest_final(sum, n_slots);
+    }
+    decltype(hs->staged)().swap(hs->staged);
   }
   // the packed delivery of every subscription entry (snapshot.h: words)
   const uint64_t n_sub_ents = hs->subs.size();
@@ -816,8 +856,10 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
   }
   if (hipStreamSynchronize(stream) != hipSuccess) return MQM_EHIP;
   // the device holds the edge table now: keep its digest, release the host copy
-  hs->edges_digest = edges_digest_of(*hs);
-  decltype(hs->edges)().swap(hs->edges);
+  if (!hs->edges.empty()) {
+    hs->edges_digest = edges_digest_of(*hs);
+    decltype(hs->edges)().swap(hs->edges);
+  }
   if (ret) {
     g->has_retained = true;
     g->ret.nflags = (const uint8_t *)g->nflags;

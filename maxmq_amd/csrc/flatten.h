@@ -40,9 +40,12 @@ struct SubInfo {
   uint8_t qos, no_local, rap, rh;
 };
 
+using EdgeVec = std::vector<EdgeEntry, NoInitAlloc<EdgeEntry>>;
+
 struct HostSnapshot {
   std::vector<NodeDesc> nodes;
-  std::vector<EdgeEntry, NoInitAlloc<EdgeEntry>> edges;  // n_buckets * kEdgesPerBucket (empty after upload)
+  EdgeVec edges;   // n_buckets * kEdgesPerBucket (empty after upload, and when built on the device)
+  EdgeVec staged;  // the literal edges in (parent preorder, child list) order, while the device builds the table
   uint64_t edges_digest = 0;  // edges_digest_of(edges), kept when the host copy is released
   std::vector<SubEnt> subs;
   std::vector<uint32_t> words;       // subs[i].word & kPackedMask (mqm_result_runs: a run's deliveries)
@@ -68,8 +71,21 @@ struct HostSnapshot {
   uint64_t version = 0;
 };
 
-// Build the snapshot; returns MQM_OK or MQM_ELIMIT.
-int flatten(const Store &st, HostSnapshot *out);
+// Build the snapshot; returns MQM_OK or MQM_ELIMIT.  host_edges = false: the
+// edge table is left to upload(), which builds it on the device from
+// `staged` (the host fill of the table and its transfer were most of a
+// rebuild: 18.5 GB at config 3 against 2.2 GB of staged edges).
+int flatten(const Store &st, HostSnapshot *out, bool host_edges = true);
+// the edge table from the staged edges, on the host (snapshot.h layout)
+void insert_edges_host(HostSnapshot &hs, const EdgeVec &staged);
+// the same table built on the device into `table` (n_buckets * kEdgesPerBucket
+// slots) from the staged edges already on the device, and its digest (the
+// sum of edge_slot_mix over the slots); 1: a partition's run-past list
+// overflowed its buffer (the caller builds the table on the host instead)
+int build_edges_device(const EdgeEntry *d_staged, uint64_t n_edges, uint64_t n_buckets, EdgeEntry *table,
+                       hipStream_t stream, uint64_t *digest_sum);
+// digest sum of a device table (build_edges_device's, for a table copied in)
+int digest_edges_device(const EdgeEntry *table, uint64_t n_slots, hipStream_t stream, uint64_t *digest_sum);
 // host threads a flatten (and the snapshot digest) runs on: mqm_build_threads,
 // else MQM_BUILD_THREADS, else min(16, hardware threads)
 uint32_t build_threads();

@@ -63,6 +63,35 @@ static_assert(sizeof(EdgeEntry) == 64, "EdgeEntry layout");
 
 constexpr uint32_t kEdgesPerBucket = 2;
 
+// Edge-table layout (flatten.cpp builds it on the host, edges.hip on the
+// device — the same bytes): the slots fall into kEdgeParts contiguous
+// partitions; each partition takes the edges whose home slot is inside it, in
+// edge order, by linear probing that stops at the partition's end; the edges
+// that ran past it are then placed in partition order by probing with
+// wrap-around.  A slot is in partition edge_part_of(slot) and partition p
+// starts at edge_part_lo(p) (slot * kEdgeParts < 2^64: n_slots < 2^50).
+constexpr uint32_t kEdgeParts = 16384;
+MQM_HD uint32_t edge_part_of(uint64_t slot, uint64_t n_slots) { return (uint32_t)(slot * kEdgeParts / n_slots); }
+MQM_HD uint64_t edge_part_lo(uint32_t p, uint64_t n_slots) {
+  return (n_slots * p + kEdgeParts - 1) / kEdgeParts;
+}
+// home slot of an edge among nb buckets
+MQM_HD uint64_t edge_home(const EdgeEntry &e, uint64_t nb) {
+  return bucket_of(edge_hash(e.parent, Key{e.k0, e.k1}), nb) * kEdgesPerBucket;
+}
+// one slot's term of the edge-table digest (the digest sums them over the
+// slots, so host and device reductions in any order agree)
+MQM_HD uint64_t edge_slot_mix(uint64_t slot, const EdgeEntry &e) {
+  const uint64_t *w = reinterpret_cast<const uint64_t *>(&e);
+  uint64_t h = slot * 0x9E3779B97F4A7C15ull ^ 0x6D716D2D65646765ull;
+  for (int i = 0; i < 8; i++) {
+    h ^= w[i];
+    h *= 0xFF51AFD7ED558CCDull;
+    h ^= h >> 32;
+  }
+  return h;
+}
+
 // non-shared subscription entry as the device reads it; sid = its index.  A
 // node's range holds its solo entries first, then its multi entries, and the
 // range of a node's '#' child follows it directly.

@@ -9,6 +9,7 @@
 #   revab   : the C5 reverse bench without and with level tasks (MQM_REV_TASKS=1)
 #   node    : the sharded node step with two rank processes and the HIP matcher (tests/test_gpu_node_step.py)
 #   churnserve: the churn workload with the served-calls-under-churn legs (one per rebuild thread count)
+#   edges   : the device-built edge table equals the host's (digests), async commits on the GPU
 #   ident   : the Identifiers parity tests (batch, DFS, runs, batching collector)
 #   c4test  : the C4 shard 0/8 full-batch test            -> gpurun_out/TAG/pytest_c4.log
 #   ret     : the retained (reverse-match) tests           -> gpurun_out/TAG/pytest_ret.log
@@ -68,6 +69,8 @@ for step in "$@"; do
         done ;;
     churnserve) timeout -k 10 1100 python3 -u bench.py --workload churn --steps 3 --warmup 1 --serve-churn-s 30 \
              > $OUT/bench_churn.json 2> $OUT/bench_churn.log ;;
+    edges) timeout -k 10 400 $PYT tests/test_gpu_edges.py tests/test_commit.py -m gpu --timeout 200 \
+             > $OUT/pytest_edges.log 2>&1 ;;
     ident) timeout -k 10 500 $PYT tests/test_gpu_parity.py tests/test_gpu_runs.py tests/test_gpu_batching.py -m gpu \
              --timeout 200 -k "ident or batched" > $OUT/pytest_ident.log 2>&1 ;;
     c4test) timeout -k 10 600 $PYT tests/test_gpu_c4_shard.py -m gpu --timeout 500 > $OUT/pytest_c4.log 2>&1 ;;
