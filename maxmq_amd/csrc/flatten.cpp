@@ -408,23 +408,10 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges) {
       push_children(stack, pc, hc, lits);
     }
   }
-  // subtree sizes
+  // subtree sizes: the store keeps them (HNode::subtree)
   const uint32_t n_items = (uint32_t)seq.size();
-  parallel_for(64, [&](uint32_t w) {
-    std::vector<uint32_t> stack, lits;
-    for (uint32_t j = w; j < n_items; j += 64) {
-      if (!seq[j].task) continue;
-      uint64_t cnt = 0;
-      stack.assign(1, seq[j].node);
-      while (!stack.empty()) {
-        const uint32_t n = stack.back();
-        stack.pop_back();
-        cnt++;
-        for (uint32_t c = nodes[n].first_child; c != kNone; c = nodes[c].next_sibling) stack.push_back(c);
-      }
-      seq[j].size = cnt;
-    }
-  });
+  for (uint32_t j = 0; j < n_items; j++)
+    if (seq[j].task) seq[j].size = nodes[seq[j].node].subtree;
   std::vector<uint64_t> base(n_items);
   uint64_t total = 0;
   for (uint32_t j = 0; j < n_items; j++) {
@@ -433,6 +420,7 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges) {
   }
   if (total >= (1ull << 30)) return MQM_ELIMIT;  // k_walk packs node id << 2 | item kind
   std::vector<uint32_t> order(total), pc_of(total), hc_of(total), nlit(total);
+  std::atomic<bool> size_bad{false};
   // number every item: a top node itself, a subtree by DFS from its base
   parallel_for(64, [&](uint32_t w) {
     std::vector<uint32_t> stack, lits;
@@ -442,6 +430,7 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges) {
       while (!stack.empty()) {
         const uint32_t n = stack.back();
         stack.pop_back();
+        if (id >= base[j] + seq[j].size) break;  // (flagged below: no write past the item's range)
         new_id[n] = (uint32_t)id;
         order[id] = n;
         uint32_t pc, hc;
@@ -452,8 +441,10 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges) {
         id++;
         if (seq[j].task) push_children(stack, pc, hc, lits);
       }
+      if (id != base[j] + seq[j].size || !stack.empty()) size_bad.store(true, std::memory_order_relaxed);
     }
   });
+  if (size_bad.load()) return MQM_EINVAL;  // (the store's subtree counts are off: never seen)
   const uint64_t nn = order.size();
   if (pt.on) {
     uint64_t mx = 0;

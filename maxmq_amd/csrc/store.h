@@ -35,6 +35,7 @@ struct HNode {        // particle (topics.go:627-635)
   uint32_t first_child = 0xFFFFFFFFu, next_sibling = 0xFFFFFFFFu, prev_sibling = 0xFFFFFFFFu;
   uint32_t n_children = 0;
   uint32_t depth = 0;
+  uint32_t subtree = 1;          // nodes in the subtree rooted here (itself included; flatten's preorder bases)
   bool retain_path = false;      // retainPath != ""
   uint64_t ret_ref = 0;          // caller's message ref of the retained packet (retain_path)
   bool live = false;
