@@ -105,9 +105,9 @@ def parse():
                     help="churn: seconds of per-publish calls (64 native callers through MQM_CFG_SERVE) while "
                          "--churn-rate Subscribe/Unsubscribe per second run (0 = skip)")
     ap.add_argument("--churn-rate", type=float, default=100000.0, help="churn: mutations/s during the served leg")
-    ap.add_argument("--churn-build-threads", default="16,4",
+    ap.add_argument("--churn-build-threads", default="16,4,2,-1",
                     help="churn: comma-separated host thread counts for the background rebuild "
-                         "(mqm_build_threads), one served-under-churn leg each")
+                         "(mqm_build_threads), one served-under-churn leg each (-1: no rebuild during the leg)")
     ap.add_argument("--retained", type=int, default=50000000, help="reverse: retained topics")
     ap.add_argument("--sweep", default="",
                     help="tuning sweep before the measurement: ';'-separated variants of "
@@ -1018,7 +1018,9 @@ def serve_churn(idx, w, args):
                                               "unsubscribe", "state")]
 
     class Out(C.Structure):
-        _fields_ = [(x, C.c_uint64) for x in ("calls", "deliveries", "mutations", "failed_mutations")]
+        _fields_ = [(x, C.c_uint64) for x in ("calls", "deliveries", "mutations", "failed_mutations")] + [
+            ("slow_ns", C.c_uint64 * 256), ("slow_t_us", C.c_uint64 * 256), ("n_pub", C.c_uint64),
+            ("pub_t_us", C.c_uint64 * 256), ("pub_builds", C.c_uint64 * 256)]
 
     api = Api(*[C.cast(getattr(L, f), C.c_void_p) for f in (
         "mqm_subscribers", "mqm_result_offsets", "mqm_result_free", "mqm_result_snapshot_version", "mqm_subscribe",
@@ -1065,6 +1067,11 @@ def serve_churn(idx, w, args):
              "p50_us": float(np.median(us)), "p99_us": float(np.percentile(us, 99)),
              "p999_us": float(np.percentile(us, 99.9)), "max_us": float(us.max()),
              "deliveries_per_topic": o.deliveries / max(1, o.calls),
+             "p9999_us": float(np.percentile(us, 99.99)),
+             "calls_over_ms": {str(t): int((us > t * 1e3).sum()) for t in (1, 10, 100, 1000)},
+             "slowest_calls": sorted(([round(o.slow_ns[k] / 1e6, 3), round(o.slow_t_us[k] / 1e6, 3)]
+                                      for k in range(min(T, 256))), reverse=True)[:8],
+             "publishes_at_s": [round(o.pub_t_us[i] / 1e6, 3) for i in range(int(o.n_pub))],
              "snapshots_published": st1["builds"] - st0["builds"], "last_build_ms": st1["last_build_ms"]}
         if rate > 0:
             nm = int(o.mutations)
@@ -1091,11 +1098,15 @@ def serve_churn(idx, w, args):
     base = run(min(args.serve_churn_s, 10.0), 0)
     legs = {}
     for bt in [int(x) for x in str(args.churn_build_threads).split(",") if x.strip()]:
-        capi.check("mqm_build_threads", L.mqm_build_threads(bt))
+        # bt < 0: no background rebuild during the leg (the mutations' own cost)
+        capi.check("mqm_build_threads", L.mqm_build_threads(max(bt, 0)))
         idx.commit_poll(wait=True)  # (the previous leg's mutations built and published)
-        legs[f"build_threads_{bt}"] = run(args.serve_churn_s, args.churn_rate)
-        log(f"[serve churn] build threads {bt}: {legs[f'build_threads_{bt}']}")
+        idx.commit_policy(0, 50 if bt >= 0 else 0)
+        name = f"build_threads_{bt}" if bt >= 0 else "no_rebuild"
+        legs[name] = run(args.serve_churn_s, args.churn_rate)
+        log(f"[serve churn] {name}: {legs[name]}")
     capi.check("mqm_build_threads", L.mqm_build_threads(0))
+    idx.commit_policy(0, 50)
     return {"threads": T, "driver": "native threads (tools/conc_driver.cpp mqd_serve_churn)",
             "index": "MQM_CFG_ASYNC_COMMIT | MQM_CFG_SERVE, commit_policy(0 ops, 50 ms)",
             "baseline_no_mutations": base, "under_churn": legs, "target_rate": args.churn_rate}

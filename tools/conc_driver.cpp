@@ -182,6 +182,10 @@ struct mqd_churn_api {
 };
 struct mqd_churn_out {
   uint64_t calls, deliveries, mutations, failed_mutations;
+  // the slowest call of each thread: its latency (ns) and return time (us since the start)
+  uint64_t slow_ns[256], slow_t_us[256];
+  // snapshot publishes the mutator saw (mqm_commit_state builds moving): time (us), builds
+  uint64_t n_pub, pub_t_us[256], pub_builds[256];
 };
 
 int64_t mqd_serve_churn(const mqd_churn_api *api, void *h, const char *bytes, const uint64_t *offs, uint32_t n,
@@ -200,7 +204,7 @@ int64_t mqd_serve_churn(const mqd_churn_api *api, void *h, const char *bytes, co
     ths.emplace_back([&, k] {
       ready++;
       while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
-      uint64_t d = 0;
+      uint64_t d = 0, slow = 0, slow_t = 0;
       uint32_t j = 0;
       for (; j < cap_per_thread && !stop.load(std::memory_order_relaxed); j++) {
         const uint32_t t = (uint32_t)(((uint64_t)k * 7919u + (uint64_t)j * 104729u) % n);
@@ -214,6 +218,10 @@ int64_t mqd_serve_churn(const mqd_churn_api *api, void *h, const char *bytes, co
         d += api->offsets(res)[1];
         const uint64_t ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
         lat_ns[(uint64_t)k * cap_per_thread + j] = ns > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)ns;
+        if (ns > slow) {
+          slow = ns;
+          slow_t = (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(b - t0).count();
+        }
         if (sample && j % sample == 0) {
           const uint64_t si = (uint64_t)k * per_s + j / sample;
           s_t_us[si] = (uint32_t)std::chrono::duration_cast<std::chrono::microseconds>(b - t0).count();
@@ -223,8 +231,13 @@ int64_t mqd_serve_churn(const mqd_churn_api *api, void *h, const char *bytes, co
       }
       calls_done[k] = j;
       dsum += d;
+      if (k < 256) {
+        out->slow_ns[k] = slow;
+        out->slow_t_us[k] = slow_t;
+      }
     });
   }
+  out->n_pub = 0;
   std::thread mut([&] {
     while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
     if (rate <= 0 || m == 0) return;
@@ -247,9 +260,14 @@ int64_t mqd_serve_churn(const mqd_churn_api *api, void *h, const char *bytes, co
                              : api->subscribe(h, cbytes + coffs[p], coffs[p + 1] - coffs[p], fbytes + foffs[p],
                                               foffs[p + 1] - foffs[p], sub, &x);
       if (rc != 0) mfail++;
+      const uint64_t b0 = k ? st.builds : 0;
       api->state(h, &st);
       m_t_us[k] = (uint32_t)std::chrono::duration_cast<std::chrono::microseconds>(clk::now() - t0).count();
       m_ver[k] = st.store_version;
+      if (k && st.builds != b0 && out->n_pub < 256) {
+        out->pub_t_us[out->n_pub] = m_t_us[k];
+        out->pub_builds[out->n_pub++] = st.builds;
+      }
       nmut++;
     }
   });
