@@ -243,6 +243,24 @@ int64_t steady_ns() {
       .count();
 }
 
+// MQM_SERVE_TRACE=1: the served path's slow steps (publish, server relaunch)
+// to stderr with their durations
+bool serve_trace() {
+  static const bool v = getenv("MQM_SERVE_TRACE") && atoi(getenv("MQM_SERVE_TRACE")) != 0;
+  return v;
+}
+struct TraceSpan {
+  const char *what;
+  int64_t t0 = serve_trace() ? steady_ns() : 0;
+  explicit TraceSpan(const char *w) : what(w) {}
+  void mark(const char *step) {
+    if (!t0) return;
+    const int64_t t = steady_ns();
+    if (t - t0 > 5000000) fprintf(stderr, "[serve-trace] %.6f %s: %s after %.1f ms\n", t * 1e-9, what, step, (t - t0) / 1e6);
+    t0 = t;
+  }
+};
+
 // the index's builder, created on first use (mu held)
 Builder *builder_locked(mqm_index *h) {
   if (!h->builder) {
@@ -357,8 +375,11 @@ bool front_fast(mqm_index *h, std::shared_ptr<GpuSnapshot> *out) {
     if ((b && b->has_ready()) || (due && steady_ns() >= due)) {
       std::unique_lock<std::mutex> g(h->mu, std::try_to_lock);
       if (g.owns_lock()) {
+        TraceSpan ts("front_fast");
         maybe_submit(h);
+        ts.mark("submit");
         (void)publish_locked(h, nullptr);
+        ts.mark("publish");
       }
     }
   }
@@ -1585,7 +1606,10 @@ struct Server {
     run_ver.store(0, std::memory_order_release);
     if (!launched) return;
     __atomic_store_n(&q->stop, 1ull, __ATOMIC_SEQ_CST);
+    const auto t0 = std::chrono::steady_clock::now();
     (void)hipStreamSynchronize(st);
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (ms > 50.0) fprintf(stderr, "mqmatch: per-publish server: stopping the kernel took %.1f ms\n", ms);
     __atomic_store_n(&q->stop, 0ull, __ATOMIC_SEQ_CST);
     launched = false;
   }
@@ -1616,8 +1640,11 @@ struct Server {
   int ensure(const std::shared_ptr<GpuSnapshot> &cur) {
     std::shared_ptr<GpuSnapshot> want = snap && snap->host->version >= cur->host->version ? snap : cur;
     if (launched && want == snap && !exited() && hipStreamQuery(st) == hipErrorNotReady) return MQM_OK;
+    TraceSpan ts("ensure");
     halt();
+    ts.mark("halt");
     snap = std::move(want);
+    ts.mark("snapshot switch");
     if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
     // (no kernel runs now) the device counter restarts at the first request
     // not yet served: a stopped kernel may have taken numbers past it
@@ -1644,6 +1671,7 @@ struct Server {
     }
     run_gen.store(gen, std::memory_order_release);
     run_ver.store(ver + 1, std::memory_order_release);
+    ts.mark("relaunch");
     return MQM_OK;
   }
   // the host snapshot a launch of version `ver` served (nullptr: no longer kept)
@@ -1699,7 +1727,13 @@ struct Server {
     if (!wait_slot(i, k)) {
       // (the slot's previous request never completed: the device is gone.
       // Request k is never posted, so its slot stays taken as well)
-      fprintf(stderr, "mqmatch: per-publish server: ring slot %u not free after 10 s\n", i);
+      fprintf(stderr,
+              "mqmatch: per-publish server: ring slot %u not free after 10 s (request %llu; slot owner %llu, "
+              "abandoned %llu, done %llu; ticket %llu, run_gen %llu, exited %llu, run_ver %llu)\n",
+              i, (unsigned long long)k, (unsigned long long)free_seq[i].load(),
+              (unsigned long long)abandoned[i].load(), (unsigned long long)__atomic_load_n(&q->done[i], __ATOMIC_ACQUIRE),
+              (unsigned long long)ticket.load(), (unsigned long long)run_gen.load(),
+              (unsigned long long)__atomic_load_n(&q->exited, __ATOMIC_ACQUIRE), (unsigned long long)run_ver.load());
       return MQM_EHIP;
     }
     ServeSlot &sl = q->slot[i];

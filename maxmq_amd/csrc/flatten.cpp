@@ -740,6 +740,7 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges) {
 }
 
 GpuSnapshot::~GpuSnapshot() {
+  const auto t0 = std::chrono::steady_clock::now();
   for (void *b : buffers)
     if (b) (void)hipFree(b);
   if (words) (void)hipFree(words);
@@ -749,6 +750,8 @@ GpuSnapshot::~GpuSnapshot() {
   if (bloom) (void)hipFree(bloom);
   if (pinfo) (void)hipFree(pinfo);
   if (partners) (void)hipFree(partners);
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (ms > 50.0) fprintf(stderr, "mqmatch: freeing a snapshot's device buffers took %.1f ms\n", ms);
 }
 
 int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std::unique_ptr<GpuSnapshot> *out) {

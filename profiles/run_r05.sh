@@ -18,6 +18,7 @@
 #   quick   : every -m gpu test except the full-size ones
 #   lat     : C3 bench with the per-publish legs (single topic, 64 native callers direct / batched)
 #   c4pmc / pmc: FETCH_SIZE / WRITE_SIZE passes (C4 shard / C3) -> traffic_c4.json / traffic.json
+#   freeprobe: tools/_build/free_probe (does hipFree wait for a running kernel?) -> free_probe.txt
 #   calib   : tools/_build/calib_fetch (random-gather / cooperative-gather rates) -> calib_kernels.txt
 #   c4fast  : the C4 shard bench without CPU baseline
 #   pipe    : `fast` with pipelined steps on 2 and 3 contexts -> bench_fast_pipe{2,3}.json
@@ -71,6 +72,8 @@ for step in "$@"; do
              > $OUT/bench_churn.json 2> $OUT/bench_churn.log ;;
     edges) timeout -k 10 400 $PYT tests/test_gpu_edges.py tests/test_commit.py -m gpu --timeout 200 \
              > $OUT/pytest_edges.log 2>&1 ;;
+    churndiag) timeout -k 10 520 python3 -u bench.py --workload churn --steps 2 --warmup 1 --serve-churn-s 12 \
+             --churn-build-threads 16,4,-1 > $OUT/bench_churn.json 2> $OUT/bench_churn.log ;;
     ident) timeout -k 10 500 $PYT tests/test_gpu_parity.py tests/test_gpu_runs.py tests/test_gpu_batching.py -m gpu \
              --timeout 200 -k "ident or batched" > $OUT/pytest_ident.log 2>&1 ;;
     c4test) timeout -k 10 600 $PYT tests/test_gpu_c4_shard.py -m gpu --timeout 500 > $OUT/pytest_c4.log 2>&1 ;;
@@ -98,6 +101,7 @@ for step in "$@"; do
              2> $OUT/bench_fast_pipe$P.log || exit 1; done ;;
     par) timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_gpu_queued.py -m gpu --timeout 300 \
              > $OUT/pytest_par.log 2>&1 ;;
+    freeprobe) timeout -k 10 60 tools/_build/free_probe > $OUT/free_probe.txt 2>&1 ;;
     calib) timeout -k 10 120 tools/_build/calib_fetch > $OUT/calib_kernels.txt 2>&1 ;;
     smoke) timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 ;;
     bench) timeout -k 10 600 python3 -u bench.py > $OUT/bench.json 2> $OUT/bench.log ;;
