@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <thread>
 
 #include "../../include/mqmatch.h"
@@ -739,23 +740,70 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges) {
   return MQM_OK;
 }
 
+namespace {
+// Snapshot buffers come from the device's stream-ordered pool and go back with
+// hipFreeAsync on a stream of their own: hipFree (and hipFreeAsync of
+// hipMalloc'd memory) waits until every kernel on the device has finished —
+// including the per-publish server, which runs as long as calls arrive
+// (tools/free_probe.hip on the box: 1000 ms, the spinner's whole run, against
+// 0.0 ms for a pool free).  The pool keeps what is freed (release threshold:
+// max), so a rebuild reuses the previous snapshot's memory without mapping it
+// again.
+struct Reclaim {
+  std::mutex mu;
+  hipStream_t st[64] = {};
+};
+Reclaim &reclaim() {
+  static Reclaim r;
+  return r;
+}
+hipStream_t reclaim_stream(int device) {
+  if (device < 0 || device >= 64) return nullptr;
+  Reclaim &r = reclaim();
+  std::lock_guard<std::mutex> g(r.mu);
+  if (!r.st[device]) {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(device);
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess) {
+      r.st[device] = s;
+      hipMemPool_t pool;
+      if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+        uint64_t keep = ~0ull;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+      }
+    }
+    (void)hipSetDevice(cur);
+  }
+  return r.st[device];
+}
+}  // namespace
+
+static void buffers_free(void *b, hipStream_t rs) {
+  if (b) (void)hipFreeAsync(b, rs);
+}
+
 GpuSnapshot::~GpuSnapshot() {
   const auto t0 = std::chrono::steady_clock::now();
-  for (void *b : buffers)
-    if (b) (void)hipFree(b);
-  if (words) (void)hipFree(words);
-  if (slots) (void)hipFree(slots);
-  if (ident_bits) (void)hipFree(ident_bits);
-  if (nflags) (void)hipFree(nflags);
-  if (bloom) (void)hipFree(bloom);
-  if (pinfo) (void)hipFree(pinfo);
-  if (partners) (void)hipFree(partners);
+  // (every reader holds this snapshot until its work is done: the server
+  // until it is halted, a batch until its stream is synchronised, a queued
+  // context until its next call — so nothing on the device reads these now)
+  const hipStream_t rs = reclaim_stream(device);
+  for (void *b : {words, slots, ident_bits, nflags, bloom, pinfo, partners}) buffers_free(b, rs);
+  for (void *b : buffers) buffers_free(b, rs);
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (ms > 50.0) fprintf(stderr, "mqmatch: freeing a snapshot's device buffers took %.1f ms\n", ms);
 }
 
+
 int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std::unique_ptr<GpuSnapshot> *out) {
   auto g = std::make_unique<GpuSnapshot>();
+  if (device >= 0) {
+    g->device = device;
+    (void)reclaim_stream(device);  // (creates it, sets the pool's release threshold)
+  }
+  auto dalloc = [&](void **p, size_t n) { return hipMallocAsync(p, n, stream); };
   if (device < 0) {  // host-only index: no device copy
     g->host = std::move(hs);
     *out = std::move(g);
@@ -782,7 +830,7 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
   for (int i = 0; i < GpuSnapshot::kNumBuffers; i++) {
     if (i >= 4 && !ret) break;
     // +64 B: walk_step reads 64 B at any node descriptor (the last one included)
-    if (hipMalloc(&g->buffers[i], (sz[i] ? sz[i] : 16) + 64) != hipSuccess) return MQM_ENOMEM;
+    if (dalloc(&g->buffers[i], (sz[i] ? sz[i] : 16) + 64) != hipSuccess) return MQM_ENOMEM;
     if (sz[i] && !(i == 1 && dev_edges) &&
         hipMemcpyAsync(g->buffers[i], src[i], sz[i], hipMemcpyHostToDevice, stream) != hipSuccess)
       return MQM_EHIP;
@@ -810,31 +858,31 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
   }
   // the packed delivery of every subscription entry (snapshot.h: words)
   const uint64_t n_sub_ents = hs->subs.size();
-  if (hipMalloc(&g->words, n_sub_ents * 4 + 64) != hipSuccess) return MQM_ENOMEM;
+  if (dalloc(&g->words, n_sub_ents * 4 + 64) != hipSuccess) return MQM_ENOMEM;
   if (derive_words((const SubEnt *)g->buffers[2], (uint32_t *)g->words, n_sub_ents, stream)) return MQM_EHIP;
   if (!hs->bloom.empty()) {
     const size_t bb = hs->bloom.size() * 8;
-    if (hipMalloc(&g->bloom, bb) != hipSuccess) return MQM_ENOMEM;
+    if (dalloc(&g->bloom, bb) != hipSuccess) return MQM_ENOMEM;
     if (hipMemcpyAsync(g->bloom, hs->bloom.data(), bb, hipMemcpyHostToDevice, stream) != hipSuccess) return MQM_EHIP;
     g->device_bytes += bb;
   }
   g->device_bytes += n_sub_ents * 4;
   {  // Identifier > 0, one bit per entry (DeviceSnapshot::ident_bits)
     const uint64_t nw = (n_sub_ents + 31) / 32;
-    if (hipMalloc(&g->ident_bits, nw * 4 + 64) != hipSuccess) return MQM_ENOMEM;
+    if (dalloc(&g->ident_bits, nw * 4 + 64) != hipSuccess) return MQM_ENOMEM;
     if (derive_ident_bits((const SubEnt *)g->buffers[2], (uint32_t *)g->ident_bits, n_sub_ents, stream))
       return MQM_EHIP;
     g->device_bytes += nw * 4;
   }
   if (slots_enabled()) {  // paired node slots (snapshot.h DeviceSnapshot::slots; MQM_SLOTS=1)
     const uint64_t nn = hs->nodes.size();
-    if (hipMalloc(&g->slots, nn * 2 * sizeof(NodeDesc) + 64) != hipSuccess) return MQM_ENOMEM;
+    if (dalloc(&g->slots, nn * 2 * sizeof(NodeDesc) + 64) != hipSuccess) return MQM_ENOMEM;
     if (derive_slots((const NodeDesc *)g->buffers[0], (NodeDesc *)g->slots, nn, stream)) return MQM_EHIP;
     g->device_bytes += nn * 2 * sizeof(NodeDesc);
   }
   {  // partners of the multi entries (merge by resolution)
     const size_t pb = hs->pinfo.size() * sizeof(uint2), qb = hs->partners.size() * 4;
-    if (hipMalloc(&g->pinfo, pb + 64) != hipSuccess || hipMalloc(&g->partners, qb + 64) != hipSuccess)
+    if (dalloc(&g->pinfo, pb + 64) != hipSuccess || dalloc(&g->partners, qb + 64) != hipSuccess)
       return MQM_ENOMEM;
     if (pb && hipMemcpyAsync(g->pinfo, hs->pinfo.data(), pb, hipMemcpyHostToDevice, stream) != hipSuccess)
       return MQM_EHIP;
@@ -844,7 +892,7 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
   }
   if (ret) {  // node flags, one byte per node, for the reverse walk
     const uint64_t nn = hs->nodes.size();
-    if (hipMalloc(&g->nflags, nn + 64) != hipSuccess) return MQM_ENOMEM;
+    if (dalloc(&g->nflags, nn + 64) != hipSuccess) return MQM_ENOMEM;
     if (derive_node_flags((const NodeDesc *)g->buffers[0], (uint8_t *)g->nflags, nn, stream)) return MQM_EHIP;
     g->device_bytes += nn;
   }

@@ -106,6 +106,7 @@ struct GpuSnapshot {
   void *pinfo = nullptr, *partners = nullptr;  // DeviceSnapshot::pinfo / partners
   DeviceRetained ret{};
   bool has_retained = false;
+  int device = -1;  // the buffers' device (from its stream-ordered pool; freed with hipFreeAsync)
   uint64_t device_bytes = 0;
   ~GpuSnapshot();
 };
