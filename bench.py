@@ -1087,10 +1087,10 @@ def serve_churn(idx, w, args):
             r["visibility_lag_ms"] = ({"p50": float(np.median(lag)), "p99": float(np.percentile(lag, 99)),
                                        "max": float(lag.max())} if len(lag) else None)
             r["mutations_seen_by_a_call"] = float(seen.mean()) if nm else None
-            ph = (C.c_double * 4)()
+            ph = (C.c_double * 5)()
             capi.check("mqm_build_phases_ms", L.mqm_build_phases_ms(idx._h, ph))
             r["last_build_phases_ms"] = {"replay": ph[0], "flatten": ph[1], "upload": ph[2],
-                                         "build_threads": int(ph[3])}
+                                         "build_threads": int(ph[3]), "kept_shape": bool(ph[4])}
         r["host_phase_max"] = idx.serve_host_max_us()
         return r
 

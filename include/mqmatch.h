@@ -229,8 +229,10 @@ typedef struct {
   int32_t has_snapshot, building;
 } mqm_commit_state;
 int mqm_commit_state_get(mqm_index *h, mqm_commit_state *out);
-/* the last published build's phases (ms[4]): delta-log replay, flatten,
- * upload (ms), then the host threads a flatten runs on */
+/* the last published build's phases (ms[5]): delta-log replay, flatten,
+ * upload (ms), then the host threads a flatten runs on, then 1 if the build
+ * kept the previous build's trie shape (preorder and edge list: no node was
+ * created or removed since) */
 int mqm_build_phases_ms(mqm_index *h, double *ms);
 /* host threads for every flatten of this process (0: MQM_BUILD_THREADS, else
  * min(16, hardware threads)); a background build under served traffic shares

@@ -194,7 +194,10 @@ void Builder::run() {
       rc = MQM_EINVAL;  // a log on top of a half-replayed shadow would build a wrong trie
     } else {
       try {
-        if (full) shadow_ = std::move(*full);
+        if (full) {
+          shadow_ = std::move(*full);
+          shape_.valid = false;  // (another store instance)
+        }
         if (fault == 1) {  // stop half-way, as a bad_alloc while interning would
           log.replay(shadow_, log.size() / 2);
           throw std::bad_alloc();
@@ -204,7 +207,9 @@ void Builder::run() {
         replayed = true;
         const auto t1 = std::chrono::steady_clock::now();
         auto hs = std::make_shared<HostSnapshot>();
-        rc = fault == 2 ? MQM_ENOMEM : flatten(shadow_, hs.get(), device_ < 0);
+        const uint64_t reuses = shape_.reuses;
+        rc = fault == 2 ? MQM_ENOMEM : flatten(shadow_, hs.get(), device_ < 0, &shape_);
+        b.kept_shape = shape_.reuses != reuses;
         hs->version = version;  // (after flatten, which starts from an empty snapshot)
         const auto t2 = std::chrono::steady_clock::now();
         if (rc == MQM_OK && device_ >= 0 && !stream_) rc = MQM_EHIP;
@@ -233,6 +238,7 @@ void Builder::run() {
       } else {
         if (!err_) err_ = rc;
         dirty_ = true;
+        shape_.valid = false;
         if (!stale && !replayed) shadow_bad_ = true;  // the replay stopped part-way
       }
     }

@@ -68,6 +68,7 @@ struct BuiltSnapshot {
   uint64_t version = 0;
   double build_ms = 0;  // replay + flatten + upload
   double phase_ms[3] = {0, 0, 0};  // replay, flatten, upload
+  bool kept_shape = false;         // the flatten reused the previous build's preorder and edges (FlattenCache)
   uint64_t n_ops = 0;   // delta-log entries folded in
 };
 
@@ -104,6 +105,7 @@ class Builder {
   void run();
   const int device_;
   Store shadow_;  // touched only by the worker thread
+  FlattenCache shape_;  // the last build's preorder and edge list (worker thread)
   hipStream_t stream_ = nullptr;
   std::mutex mu_;
   std::condition_variable cv_;

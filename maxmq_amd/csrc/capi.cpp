@@ -141,6 +141,7 @@ struct mqm_index {
   bool journal_dated = false;                          // (journal_t0 is set for the current journal)
   uint64_t builds = 0, last_build_ops = 0;
   double last_build_ms = 0, last_build_phase_ms[3] = {0, 0, 0};
+  bool last_build_kept_shape = false;
   bool fast_path = true;  // MQM_NO_FAST=1: small batches also take the batch pipeline (A/B, tests)
   bool async() const { return (cfg.flags & MQM_CFG_ASYNC_COMMIT) != 0; }
   // the device-result API's context (mqm_match_device & follow-ups)
@@ -295,6 +296,7 @@ int publish_locked(mqm_index *h, int *published) {
   h->last_build_ms = b.build_ms;
   h->last_build_ops = b.n_ops;
   for (int i = 0; i < 3; i++) h->last_build_phase_ms[i] = b.phase_ms[i];
+  h->last_build_kept_shape = b.kept_shape;
   if (published) *published = 1;
   return install(h, std::shared_ptr<GpuSnapshot>(std::move(b.snap)), b.version);
 }
@@ -2175,6 +2177,7 @@ int mqm_build_phases_ms(mqm_index *h, double *ms) {
   std::lock_guard<std::mutex> g(h->mu);
   for (int i = 0; i < 3; i++) ms[i] = h->last_build_phase_ms[i];
   ms[3] = (double)build_threads();
+  ms[4] = h->last_build_kept_shape ? 1.0 : 0.0;
   return MQM_OK;
 }
 

@@ -357,19 +357,28 @@ void insert_edges_host(HostSnapshot &hs, const EdgeVec &staged) {
     }
 }
 
-int flatten(const Store &st, HostSnapshot *out, bool host_edges) {
+int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *cache) {
   PhaseTimer pt;
   const auto &nodes = st.nodes();
   const uint32_t plus_tok = st.plus_token(), hash_tok = st.hash_token();
   HostSnapshot &hs = *out;
   hs = HostSnapshot();
-
+  // the trie's shape as the cache saw it: its preorder and edge list stand
+  const bool reuse = cache && cache->valid && cache->structure == st.structure_version() &&
+                     cache->n_tokens == st.tokens().size() && cache->host_edges == host_edges &&
+                     st.retained_len() == 0 && cache->new_id.size() == nodes.size();
+  FlattenCache local;
+  FlattenCache &pre = reuse ? *cache : local;
+  if (cache && !reuse) cache->valid = false;
+  std::vector<uint32_t> &new_id = pre.new_id, &order = pre.order, &pc_of = pre.pc_of, &hc_of = pre.hc_of,
+                        &nlit = pre.nlit;
+  if (!reuse) {
   // 1. preorder ids.  Visiting order at a node: literal children in child-list
   //    order, then '+', then '#'.  Nodes above depth kTop are numbered
   //    serially; the subtrees rooted at depth kTop are counted, then numbered
   //    at their preorder base, in parallel.
   constexpr uint32_t kTop = 2;
-  std::vector<uint32_t> new_id(nodes.size(), kNone);
+  new_id.assign(nodes.size(), kNone);
   // '+' / '#' children (store ids) and literal-child counts by preorder id
   auto scan_children = [&](uint32_t n, uint32_t *pc, uint32_t *hc, std::vector<uint32_t> &lits) {
     *pc = *hc = kNone;
@@ -420,7 +429,10 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges) {
     total += seq[j].size;
   }
   if (total >= (1ull << 30)) return MQM_ELIMIT;  // k_walk packs node id << 2 | item kind
-  std::vector<uint32_t> order(total), pc_of(total), hc_of(total), nlit(total);
+  order.assign(total, 0);
+  pc_of.assign(total, 0);
+  hc_of.assign(total, 0);
+  nlit.assign(total, 0);
   std::atomic<bool> size_bad{false};
   // number every item: a top node itself, a subtree by DFS from its base
   parallel_for(64, [&](uint32_t w) {
@@ -446,13 +458,14 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges) {
     }
   });
   if (size_bad.load()) return MQM_EINVAL;  // (the store's subtree counts are off: never seen)
-  const uint64_t nn = order.size();
   if (pt.on) {
     uint64_t mx = 0;
     for (auto &x : seq) mx = std::max(mx, x.size);
-    fprintf(stderr, "[flatten] nodes %zu items %u largest subtree %zu\n", (size_t)nn, n_items, (size_t)mx);
+    fprintf(stderr, "[flatten] nodes %zu items %u largest subtree %zu\n", order.size(), n_items, (size_t)mx);
   }
-  pt.mark("preorder");
+  }  // (!reuse)
+  const uint64_t nn = order.size();
+  pt.mark(reuse ? "preorder (kept)" : "preorder");
 
   // 2. descriptors, subscription ranges, flags — in parallel over preorder
   //    chunks: (A) counts, child ids and own flags per node, (prefix sums over
@@ -681,59 +694,90 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges) {
   //     bytes: the layout depends on kEdgeParts only, not on the thread count,
   //     so digests are reproducible)
   constexpr uint32_t kChunks = 64;
-  std::vector<uint64_t> eoff(nn + 1, 0);
-  for (uint64_t i = 0; i < nn; i++) eoff[i + 1] = eoff[i] + nlit[i];
-  EdgeVec staged(n_literal_edges);
-  parallel_for(kChunks, [&](uint32_t c) {
-    const uint64_t lo = nn * c / kChunks, hi = nn * (c + 1) / kChunks;
-    for (uint64_t i = lo; i < hi; i++) {
-      uint64_t e_i = eoff[i];
-      const uint32_t pc = pc_of[i], hc = hc_of[i];
-      for (uint32_t c2 = nodes[order[i]].first_child; c2 != kNone; c2 = nodes[c2].next_sibling) {
-        if (c2 == pc || c2 == hc) continue;
-        const uint32_t cn = new_id[c2];
-        const std::string_view tok = toks.name(nodes[c2].key);
-        Key k = make_key([&](uint32_t j) { return (uint8_t)tok[j]; }, (uint32_t)tok.size());
-        EdgeEntry &e = staged[e_i];
-        e.k0 = k.k0;
-        e.k1 = k.k1;
-        e.parent = (uint32_t)i;
-        e.child = cn;
-        e.tok_off = key_is_long(k) ? pool_off[nodes[c2].key] : 0;
-        e.tok_len = (uint32_t)tok.size();
-        e.desc = hs.nodes[cn];
-        e_i++;
-      }
+  if (reuse) {
+    // the same edges in the same order: only the inline child descriptors change
+    if (!pre.staged || pre.staged->size() != n_literal_edges) {
+      cache->valid = false;
+      return MQM_EINVAL;  // (the shape moved without its version: never seen)
     }
-  });
-  // the edge-existence filter: >= 16 bits per edge, a power of two of words
-  // (env MQM_NO_BLOOM=1: none, for A/B runs); OR is order-free, so the
-  // parallel fill is deterministic
-  hs.bloom.clear();
-  if (n_literal_edges && !getenv("MQM_NO_BLOOM")) {
-    uint64_t bits = 4096;
-    while (bits < 16 * n_literal_edges) bits <<= 1;
-    hs.bloom.assign(bits / 64, 0);
-    const uint64_t mask = bits / 64 - 1;
+    EdgeVec &staged = *pre.staged;
     parallel_for(kChunks, [&](uint32_t c) {
       const uint64_t lo = n_literal_edges * c / kChunks, hi = n_literal_edges * (c + 1) / kChunks;
-      for (uint64_t e = lo; e < hi; e++) {
-        const EdgeEntry &x = staged[e];
-        const uint64_t h = edge_hash(x.parent, Key{x.k0, x.k1});
-        __atomic_fetch_or(&hs.bloom[bloom_word(h, mask)], bloom_bits(h), __ATOMIC_RELAXED);
+      for (uint64_t e = lo; e < hi; e++) staged[e].desc = hs.nodes[staged[e].child];
+    });
+    hs.bloom = pre.bloom;
+    cache->reuses++;
+  } else {
+    constexpr uint32_t kChunks = 64;
+    std::vector<uint64_t> eoff(nn + 1, 0);
+    for (uint64_t i = 0; i < nn; i++) eoff[i + 1] = eoff[i] + nlit[i];
+    pre.staged = std::make_shared<EdgeVec>(n_literal_edges);
+    EdgeVec &staged = *pre.staged;
+    parallel_for(kChunks, [&](uint32_t c) {
+      const uint64_t lo = nn * c / kChunks, hi = nn * (c + 1) / kChunks;
+      for (uint64_t i = lo; i < hi; i++) {
+        uint64_t e_i = eoff[i];
+        const uint32_t pc = pc_of[i], hc = hc_of[i];
+        for (uint32_t c2 = nodes[order[i]].first_child; c2 != kNone; c2 = nodes[c2].next_sibling) {
+          if (c2 == pc || c2 == hc) continue;
+          const uint32_t cn = new_id[c2];
+          const std::string_view tok = toks.name(nodes[c2].key);
+          Key k = make_key([&](uint32_t j) { return (uint8_t)tok[j]; }, (uint32_t)tok.size());
+          EdgeEntry &e = staged[e_i];
+          e.k0 = k.k0;
+          e.k1 = k.k1;
+          e.parent = (uint32_t)i;
+          e.child = cn;
+          e.tok_off = key_is_long(k) ? pool_off[nodes[c2].key] : 0;
+          e.tok_len = (uint32_t)tok.size();
+          e.desc = hs.nodes[cn];
+          e_i++;
+        }
       }
     });
+    // the edge-existence filter: >= 16 bits per edge, a power of two of words
+    // (env MQM_NO_BLOOM=1: none, for A/B runs); OR is order-free, so the
+    // parallel fill is deterministic
+    hs.bloom.clear();
+    if (n_literal_edges && !getenv("MQM_NO_BLOOM")) {
+      uint64_t bits = 4096;
+      while (bits < 16 * n_literal_edges) bits <<= 1;
+      hs.bloom.assign(bits / 64, 0);
+      const uint64_t mask = bits / 64 - 1;
+      parallel_for(kChunks, [&](uint32_t c) {
+        const uint64_t lo = n_literal_edges * c / kChunks, hi = n_literal_edges * (c + 1) / kChunks;
+        for (uint64_t e = lo; e < hi; e++) {
+          const EdgeEntry &x = staged[e];
+          const uint64_t h = edge_hash(x.parent, Key{x.k0, x.k1});
+          __atomic_fetch_or(&hs.bloom[bloom_word(h, mask)], bloom_bits(h), __ATOMIC_RELAXED);
+        }
+      });
+    }
+
   }
   pt.mark("e:stage");
   if (st.retained_len() > 0) {
-    build_reverse_index(st, order, staged, hs);
+    build_reverse_index(st, order, *pre.staged, hs);
     pt.mark("rev-index");
   }
   if (host_edges) {
-    insert_edges_host(hs, staged);
+    insert_edges_host(hs, *pre.staged);
     pt.mark("e:insert");
   } else {
-    hs.staged = std::move(staged);
+    hs.staged = pre.staged;
+  }
+  if (cache && !reuse) {  // keep this build's shape for the next one
+    cache->order = std::move(order);
+    cache->new_id = std::move(new_id);
+    cache->pc_of = std::move(pc_of);
+    cache->hc_of = std::move(hc_of);
+    cache->nlit = std::move(nlit);
+    cache->staged = pre.staged;
+    cache->bloom = hs.bloom;
+    cache->structure = st.structure_version();
+    cache->n_tokens = st.tokens().size();
+    cache->host_edges = host_edges;
+    cache->valid = st.retained_len() == 0;
   }
   if (hs.tok_pool.empty()) hs.tok_pool.push_back(0);
   if (hs.subs.empty()) hs.subs.push_back(SubEnt{0, 0});
@@ -820,7 +864,7 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
   // host_edges = false) unless the host built it
   const bool dev_edges = hs->edges.empty();
   const uint64_t n_slots = hs->n_buckets * kEdgesPerBucket;
-  if (dev_edges && hs->staged.size() != hs->n_edges) return MQM_EINVAL;
+  if (dev_edges && (!hs->staged || hs->staged->size() != hs->n_edges)) return MQM_EINVAL;
   const size_t sz[GpuSnapshot::kNumBuffers] = {
       hs->nodes.size() * sizeof(NodeDesc), n_slots * sizeof(EdgeEntry), hs->subs.size() * sizeof(SubEnt),
       hs->tok_pool.size(),                 hs->subtree.size() * 4,                hs->child_off.size() * 4,
@@ -837,10 +881,10 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
     g->device_bytes += sz[i];
   }
   if (dev_edges) {  // edges.hip; a run-past overflow (never seen) falls back to the host build
-    const uint64_t ne = hs->staged.size();
+    const uint64_t ne = hs->staged->size();
     void *d_staged = nullptr;
     if (hipMallocAsync(&d_staged, ne * sizeof(EdgeEntry) + 64, stream) != hipSuccess) return MQM_ENOMEM;
-    if (ne && hipMemcpyAsync(d_staged, hs->staged.data(), ne * sizeof(EdgeEntry), hipMemcpyHostToDevice, stream) !=
+    if (ne && hipMemcpyAsync(d_staged, hs->staged->data(), ne * sizeof(EdgeEntry), hipMemcpyHostToDevice, stream) !=
                   hipSuccess)
       return MQM_EHIP;
     uint64_t sum = 0;
@@ -848,13 +892,13 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
                                       stream, &sum);
     if (hipFreeAsync(d_staged, stream) != hipSuccess || rc < 0) return MQM_EHIP;
     if (rc == 1) {
-      insert_edges_host(*hs, hs->staged);
+      insert_edges_host(*hs, *hs->staged);
       if (hipMemcpyAsync(g->buffers[1], hs->edges.data(), sz[1], hipMemcpyHostToDevice, stream) != hipSuccess)
         return MQM_EHIP;
     } else {
       hs->edges_digest = edges_digest_final(sum, n_slots);
     }
-    decltype(hs->staged)().swap(hs->staged);
+    hs->staged.reset();  // (the builder's FlattenCache may keep it for the next build)
   }
   // the packed delivery of every subscription entry (snapshot.h: words)
   const uint64_t n_sub_ents = hs->subs.size();

@@ -45,7 +45,9 @@ using EdgeVec = std::vector<EdgeEntry, NoInitAlloc<EdgeEntry>>;
 struct HostSnapshot {
   std::vector<NodeDesc> nodes;
   EdgeVec edges;   // n_buckets * kEdgesPerBucket (empty after upload, and when built on the device)
-  EdgeVec staged;  // the literal edges in (parent preorder, child list) order, while the device builds the table
+  // the literal edges in (parent preorder, child list) order, while the
+  // device builds the table (shared with the builder's FlattenCache)
+  std::shared_ptr<EdgeVec> staged;
   uint64_t edges_digest = 0;  // edges_digest_of(edges), kept when the host copy is released
   std::vector<SubEnt> subs;
   std::vector<uint32_t> words;       // subs[i].word & kPackedMask (mqm_result_runs: a run's deliveries)
@@ -71,11 +73,27 @@ struct HostSnapshot {
   uint64_t version = 0;
 };
 
+// What a rebuild of the same trie shape can reuse (the background builder
+// keeps one): the preorder numbering, the staged edge list (its inline child
+// descriptors refreshed) and the edge filter.  Valid while the store's
+// structure_version and token count are those it was built at, no message is
+// retained and the table is built where it was.  Subscribe / Unsubscribe of
+// filters that exist (and keep other subscribers) leave the shape alone.
+struct FlattenCache {
+  bool valid = false;
+  uint64_t structure = 0, n_tokens = 0;
+  bool host_edges = false;
+  std::vector<uint32_t> order, new_id, pc_of, hc_of, nlit;
+  std::shared_ptr<EdgeVec> staged;
+  std::vector<uint64_t> bloom;
+  uint64_t reuses = 0;  // builds that took the cache (statistics)
+};
+
 // Build the snapshot; returns MQM_OK or MQM_ELIMIT.  host_edges = false: the
 // edge table is left to upload(), which builds it on the device from
 // `staged` (the host fill of the table and its transfer were most of a
 // rebuild: 18.5 GB at config 3 against 2.2 GB of staged edges).
-int flatten(const Store &st, HostSnapshot *out, bool host_edges = true);
+int flatten(const Store &st, HostSnapshot *out, bool host_edges = true, FlattenCache *cache = nullptr);
 // the edge table from the staged edges, on the host (snapshot.h layout)
 void insert_edges_host(HostSnapshot &hs, const EdgeVec &staged);
 // the same table built on the device into `table` (n_buckets * kEdgesPerBucket

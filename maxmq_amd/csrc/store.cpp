@@ -228,6 +228,7 @@ uint32_t Store::new_node(uint32_t parent, uint32_t tok) {
   p.first_child = id;
   p.n_children++;
   for (uint32_t a = parent; a != kNone; a = nodes_[a].parent) nodes_[a].subtree++;
+  structure_version_++;
   children_.insert(edge_id(parent, tok), id);
   return id;
 }
@@ -242,6 +243,7 @@ void Store::unlink(uint32_t id) {
   if (n.next_sibling != kNone) nodes_[n.next_sibling].prev_sibling = n.prev_sibling;
   p.n_children--;
   for (uint32_t a = n.parent; a != kNone; a = nodes_[a].parent) nodes_[a].subtree -= n.subtree;  // (a leaf: 1)
+  structure_version_++;
   children_.erase(edge_id(n.parent, n.key));
   n = HNode();
   free_.push_back(id);

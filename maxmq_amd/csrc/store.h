@@ -107,6 +107,9 @@ class Store {
   const Interner &filters() const { return filters_; }
   const std::vector<HNode> &nodes() const { return nodes_; }
   uint32_t root() const { return 0; }
+  // moves whenever a node is created or removed (the trie's shape, which
+  // flatten's preorder and edge list depend on; subscriptions do not move it)
+  uint64_t structure_version() const { return structure_version_; }
   uint32_t plus_token() const { return plus_tok_; }
   uint32_t hash_token() const { return hash_tok_; }
   uint32_t child(uint32_t parent, uint32_t tok) const;
@@ -121,6 +124,7 @@ class Store {
   void unlink(uint32_t n);
 
   std::vector<HNode> nodes_;
+  uint64_t structure_version_ = 0;
   std::vector<uint32_t> free_;
   EdgeMap children_;
   Interner tokens_, clients_, filters_;

@@ -296,3 +296,50 @@ def test_solo_marking_of_hash_nodes():
     idx.subscribe("c3", maxmq_amd.Subscription("x/#"))
     idx.commit()
     assert idx.snapshot_stats()["solo_subs"] == 2
+
+
+def _kept_shape(idx):
+    import ctypes as C
+    ms = (C.c_double * 5)()
+    capi.check("mqm_build_phases_ms", capi.lib().mqm_build_phases_ms(idx._h, ms))
+    return bool(ms[4])
+
+
+def test_rebuild_keeps_the_trie_shape_when_no_node_moves():
+    """FlattenCache (flatten.h): a background build after Subscribe /
+    Unsubscribe calls that create or remove no node reuses the previous
+    build's preorder and edge list (refreshing the edges' inline child
+    descriptors) — and must still equal a full flatten of the store, byte
+    for byte; a call that creates a node (a new filter) or removes one (the
+    last subscriber of a leaf) forces the full path."""
+    from tools import mqgen
+
+    w = mqgen.generate(1, n_filters=4000, n_topics=10)
+    rng = random.Random(11)
+    sync = maxmq_amd.TopicsIndex(device=None, autocommit=False)
+    asy = maxmq_amd.TopicsIndex(device=None, autocommit=False, async_commit=True)
+    for idx in (sync, asy):
+        idx.subscribe_workload(w)
+        idx.commit()
+    filters = [w.filters[i] for i in range(len(w.filters))]
+    kept = []
+    for rnd in range(6):
+        for k in range(200):  # existing filters, new clients (and some of them leaving again)
+            f = rng.choice(filters)
+            c = f"churn-{rnd}-{k % 50}"
+            for idx in (sync, asy):
+                if k % 3 == 2:
+                    idx.unsubscribe(f, c)
+                else:
+                    idx.subscribe(c, maxmq_amd.Subscription(f, qos=k % 3, identifier=k % 4))
+        if rnd == 3:  # a new filter: new nodes
+            for idx in (sync, asy):
+                idx.subscribe("newcomer", maxmq_amd.Subscription(f"zz/{rnd}/+/leaf"))
+        if rnd == 4:  # its only subscriber leaves: the nodes go again
+            for idx in (sync, asy):
+                idx.unsubscribe(f"zz/3/+/leaf", "newcomer")
+        sync.commit()
+        asy.commit()
+        assert asy.snapshot_digest() == sync.snapshot_digest(), rnd
+        kept.append(_kept_shape(asy))
+    assert kept == [True, True, True, False, False, True], kept
