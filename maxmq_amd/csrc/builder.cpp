@@ -75,7 +75,9 @@ void DeltaLog::append(DeltaLog &&o) {
   }
   const uint64_t shift = bytes_.size();
   bytes_.insert(bytes_.end(), o.bytes_.begin(), o.bytes_.end());
-  ops_.reserve(ops_.size() + o.ops_.size());
+  // (no exact reserve: logs coalesce 20 times a second while a build runs,
+  // and an exact reserve copied the whole queue each time — up to 44 ms under
+  // the index lock at 100k mutations/s, r05k)
   for (Op op : o.ops_) {
     op.a_off += shift;
     ops_.push_back(op);

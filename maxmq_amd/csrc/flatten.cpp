@@ -785,6 +785,22 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
 }
 
 namespace {
+// host -> device in pieces of kUploadChunk: one long DMA of gigabytes held the
+// per-publish server's polls of its ring (reads of host memory, whose data
+// crosses PCIe in the same direction) for up to 230 ms (r05k); between pieces
+// they get through
+constexpr size_t kUploadChunk = 32ull << 20;
+hipError_t upload_copy(void *dst, const void *src, size_t n, hipStream_t st) {
+  for (size_t o = 0; o < n; o += kUploadChunk) {
+    const hipError_t e = hipMemcpyAsync((char *)dst + o, (const char *)src + o, std::min(kUploadChunk, n - o),
+                                        hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+}  // namespace
+
+namespace {
 // Snapshot buffers come from the device's stream-ordered pool and go back with
 // hipFreeAsync on a stream of their own: hipFree (and hipFreeAsync of
 // hipMalloc'd memory) waits until every kernel on the device has finished —
@@ -876,7 +892,7 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
     // +64 B: walk_step reads 64 B at any node descriptor (the last one included)
     if (dalloc(&g->buffers[i], (sz[i] ? sz[i] : 16) + 64) != hipSuccess) return MQM_ENOMEM;
     if (sz[i] && !(i == 1 && dev_edges) &&
-        hipMemcpyAsync(g->buffers[i], src[i], sz[i], hipMemcpyHostToDevice, stream) != hipSuccess)
+        upload_copy(g->buffers[i], src[i], sz[i], stream) != hipSuccess)
       return MQM_EHIP;
     g->device_bytes += sz[i];
   }
@@ -884,7 +900,7 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
     const uint64_t ne = hs->staged->size();
     void *d_staged = nullptr;
     if (hipMallocAsync(&d_staged, ne * sizeof(EdgeEntry) + 64, stream) != hipSuccess) return MQM_ENOMEM;
-    if (ne && hipMemcpyAsync(d_staged, hs->staged->data(), ne * sizeof(EdgeEntry), hipMemcpyHostToDevice, stream) !=
+    if (ne && upload_copy(d_staged, hs->staged->data(), ne * sizeof(EdgeEntry), stream) !=
                   hipSuccess)
       return MQM_EHIP;
     uint64_t sum = 0;
@@ -893,7 +909,7 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
     if (hipFreeAsync(d_staged, stream) != hipSuccess || rc < 0) return MQM_EHIP;
     if (rc == 1) {
       insert_edges_host(*hs, *hs->staged);
-      if (hipMemcpyAsync(g->buffers[1], hs->edges.data(), sz[1], hipMemcpyHostToDevice, stream) != hipSuccess)
+      if (upload_copy(g->buffers[1], hs->edges.data(), sz[1], stream) != hipSuccess)
         return MQM_EHIP;
     } else {
       hs->edges_digest = edges_digest_final(sum, n_slots);
@@ -907,7 +923,7 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
   if (!hs->bloom.empty()) {
     const size_t bb = hs->bloom.size() * 8;
     if (dalloc(&g->bloom, bb) != hipSuccess) return MQM_ENOMEM;
-    if (hipMemcpyAsync(g->bloom, hs->bloom.data(), bb, hipMemcpyHostToDevice, stream) != hipSuccess) return MQM_EHIP;
+    if (upload_copy(g->bloom, hs->bloom.data(), bb, stream) != hipSuccess) return MQM_EHIP;
     g->device_bytes += bb;
   }
   g->device_bytes += n_sub_ents * 4;
@@ -928,9 +944,9 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
     const size_t pb = hs->pinfo.size() * sizeof(uint2), qb = hs->partners.size() * 4;
     if (dalloc(&g->pinfo, pb + 64) != hipSuccess || dalloc(&g->partners, qb + 64) != hipSuccess)
       return MQM_ENOMEM;
-    if (pb && hipMemcpyAsync(g->pinfo, hs->pinfo.data(), pb, hipMemcpyHostToDevice, stream) != hipSuccess)
+    if (pb && upload_copy(g->pinfo, hs->pinfo.data(), pb, stream) != hipSuccess)
       return MQM_EHIP;
-    if (qb && hipMemcpyAsync(g->partners, hs->partners.data(), qb, hipMemcpyHostToDevice, stream) != hipSuccess)
+    if (qb && upload_copy(g->partners, hs->partners.data(), qb, stream) != hipSuccess)
       return MQM_EHIP;
     g->device_bytes += pb + qb;
   }
