@@ -232,6 +232,47 @@ std::string_view sv(const char *p, size_t n) { return std::string_view(p ? p : "
 int hip_rc(int rc) { return rc == -2 ? MQM_ENOMEM : rc == -1 ? MQM_EINVAL : rc < 0 ? MQM_EHIP : rc; }
 
 // make g the front buffer; readers that hold the old one keep it alive
+// Retired snapshots are destroyed on a thread of their own: freeing a
+// snapshot's device buffers can take hundreds of milliseconds while the
+// per-publish server runs (r05l: 299 ms once, even with stream-ordered
+// frees), and the last reference to a snapshot is often dropped by a caller
+// thread holding the server's or the index's lock.  (Never destroyed itself:
+// snapshots still queued at process exit are left to the OS.)
+struct Reaper {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<GpuSnapshot *> q;
+  Reaper() {
+    std::thread([this] {
+      for (;;) {
+        std::vector<GpuSnapshot *> batch;
+        {
+          std::unique_lock<std::mutex> g(mu);
+          cv.wait(g, [this] { return !q.empty(); });
+          batch.swap(q);
+        }
+        for (GpuSnapshot *s : batch) delete s;
+      }
+    }).detach();
+  }
+  void retire(GpuSnapshot *s) {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      q.push_back(s);
+    }
+    cv.notify_one();
+  }
+};
+Reaper &reaper() {
+  static Reaper *r = new Reaper;
+  return *r;
+}
+std::shared_ptr<GpuSnapshot> share_snapshot(std::unique_ptr<GpuSnapshot> g) {
+  return std::shared_ptr<GpuSnapshot>(g.release(), [](GpuSnapshot *s) {
+    if (s) reaper().retire(s);
+  });
+}
+
 int install(mqm_index *h, std::shared_ptr<GpuSnapshot> g, uint64_t version) {
   std::unique_lock<std::shared_mutex> w(h->snap_rw);
   h->snap = std::move(g);
@@ -298,7 +339,7 @@ int publish_locked(mqm_index *h, int *published) {
   for (int i = 0; i < 3; i++) h->last_build_phase_ms[i] = b.phase_ms[i];
   h->last_build_kept_shape = b.kept_shape;
   if (published) *published = 1;
-  return install(h, std::shared_ptr<GpuSnapshot>(std::move(b.snap)), b.version);
+  return install(h, share_snapshot(std::move(b.snap)), b.version);
 }
 
 // after a logged mutation: the periodic-rebuild policy (mqm_commit_policy)
@@ -340,7 +381,7 @@ int commit_locked(mqm_index *h) {
   std::unique_ptr<GpuSnapshot> g;
   rc = upload(std::move(hs), h->cfg.device, h->dev.stream, &g);
   if (rc != MQM_OK) return rc;
-  return install(h, std::shared_ptr<GpuSnapshot>(std::move(g)), h->store.version());
+  return install(h, share_snapshot(std::move(g)), h->store.version());
 }
 
 int ensure_snapshot_locked(mqm_index *h) {
