@@ -1590,6 +1590,7 @@ struct Server {
   std::atomic<uint32_t> inflight{0};
   std::atomic<int64_t> last_check_ns{0};  // the last liveness check of a late caller (steady clock)
   std::atomic<bool> poller_quit{false};
+  bool counted = false;  // (serve_count: the rebuild's default thread count while a server lives)
   void poke_poller(Poller &pl) {
     pl.word.fetch_add(1, std::memory_order_acq_rel);
     syscall(SYS_futex, reinterpret_cast<uint32_t *>(&pl.word), FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
@@ -1642,6 +1643,8 @@ struct Server {
         hipStreamSynchronize(st) != hipSuccess)
       return MQM_EHIP;
     for (uint32_t p = 0; p < n_pollers; p++) pollers[p].th = std::thread([this, p] { poll_loop(p); });
+    serve_count(+1);
+    counted = true;
     return MQM_OK;
   }
   // (mu held) stop a running kernel and wait for it
@@ -1657,6 +1660,7 @@ struct Server {
     launched = false;
   }
   ~Server() {
+    if (counted) serve_count(-1);
     poller_quit.store(true, std::memory_order_release);
     for (uint32_t p = 0; p < n_pollers; p++)
       if (pollers[p].th.joinable()) {

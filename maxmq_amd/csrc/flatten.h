@@ -108,6 +108,7 @@ int digest_edges_device(const EdgeEntry *table, uint64_t n_slots, hipStream_t st
 // else MQM_BUILD_THREADS, else min(16, hardware threads)
 uint32_t build_threads();
 void set_build_threads(uint32_t n);  // 0: back to the default
+void serve_count(int delta);         // a per-publish server started (+1) / stopped (-1): the default drops to 4
 
 // Device copy of a HostSnapshot.  Host side tables stay shared with results
 // (shared_ptr) so a result can outlive the next commit.

@@ -73,7 +73,7 @@ for step in "$@"; do
     edges) timeout -k 10 400 $PYT tests/test_gpu_edges.py tests/test_commit.py -m gpu --timeout 200 \
              > $OUT/pytest_edges.log 2>&1 ;;
     churndiag) timeout -k 10 520 python3 -u bench.py --workload churn --steps 2 --warmup 1 --serve-churn-s 12 \
-             --churn-build-threads 16,4,-1 > $OUT/bench_churn.json 2> $OUT/bench_churn.log ;;
+             --churn-build-threads 4,16,-1 > $OUT/bench_churn.json 2> $OUT/bench_churn.log ;;
     ident) timeout -k 10 500 $PYT tests/test_gpu_parity.py tests/test_gpu_runs.py tests/test_gpu_batching.py -m gpu \
              --timeout 200 -k "ident or batched" > $OUT/pytest_ident.log 2>&1 ;;
     c4test) timeout -k 10 600 $PYT tests/test_gpu_c4_shard.py -m gpu --timeout 500 > $OUT/pytest_c4.log 2>&1 ;;
