@@ -28,6 +28,11 @@ __global__ void poller(const int *flag, unsigned long long *out, unsigned long l
   out[1] = polls;
 }
 
+__global__ __launch_bounds__(256) void fill(uint4 *p, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    p[i] = make_uint4((uint32_t)i, 0u, 0u, 1u);
+}
+
 #define CK(x)                                                  \
   do {                                                         \
     hipError_t e = (x);                                        \
@@ -53,14 +58,28 @@ int main() {
   CK(hipStreamCreateWithFlags(&b, hipStreamNonBlocking));
   const char *what[] = {"no copy", "pageable, one 4 GB copy", "pageable, 32 MB pieces queued",
                         "pageable, 32 MB pieces, sync + 200 us between", "pinned, one 4 GB copy",
-                        "pinned, 32 MB pieces, sync + 200 us between"};
-  for (int mode = 0; mode < 6; mode++) {
+                        "pinned, 32 MB pieces, sync + 200 us between", "hipMalloc 20 GB + memset",
+                        "hipMallocAsync 20 GB + memset (+ free async)", "fill kernel over 16 GB (16384 x 256)",
+                        "hipMallocAsync 20 GB again (pool warm)"};
+  const size_t big = 20ull << 30;
+  void *extra = nullptr;
+  for (int mode = 0; mode < 10; mode++) {
     __atomic_store_n(flag, 0, __ATOMIC_SEQ_CST);
     hipLaunchKernelGGL(poller, dim3(1), dim3(64), 0, a, flag, d_out, 400000000ull);
     std::this_thread::sleep_for(std::chrono::milliseconds(50));
     const auto t = std::chrono::steady_clock::now();
     const char *src = mode >= 4 ? (const char *)pinned : pageable.data();
-    if (mode == 1 || mode == 4) {
+    if (mode == 6) {
+      CK(hipMalloc(&extra, big));
+      CK(hipMemsetAsync(extra, 0, big, b));
+    } else if (mode == 7 || mode == 9) {
+      void *x = nullptr;
+      CK(hipMallocAsync(&x, big, b));
+      CK(hipMemsetAsync(x, 0, big, b));
+      CK(hipFreeAsync(x, b));
+    } else if (mode == 8) {
+      hipLaunchKernelGGL(fill, dim3(16384), dim3(256), 0, b, (uint4 *)extra, (uint64_t)(16ull << 30) / 16);
+    } else if (mode == 1 || mode == 4) {
       CK(hipMemcpyAsync(dst, src, total, hipMemcpyHostToDevice, b));
     } else if (mode > 0) {
       for (size_t o = 0; o < total; o += chunk) {
@@ -80,6 +99,7 @@ int main() {
     printf("%-48s copy %8.1f ms; longest gap between polls %8.3f ms (%llu polls)\n", what[mode], ms,
            h_out[0] / 1e5, h_out[1]);
   }
+  if (extra) CK(hipFree(extra));
   printf("OK\n");
   return 0;
 }
