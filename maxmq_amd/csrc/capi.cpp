@@ -232,47 +232,6 @@ std::string_view sv(const char *p, size_t n) { return std::string_view(p ? p : "
 int hip_rc(int rc) { return rc == -2 ? MQM_ENOMEM : rc == -1 ? MQM_EINVAL : rc < 0 ? MQM_EHIP : rc; }
 
 // make g the front buffer; readers that hold the old one keep it alive
-// Retired snapshots are destroyed on a thread of their own: freeing a
-// snapshot's device buffers can take hundreds of milliseconds while the
-// per-publish server runs (r05l: 299 ms once, even with stream-ordered
-// frees), and the last reference to a snapshot is often dropped by a caller
-// thread holding the server's or the index's lock.  (Never destroyed itself:
-// snapshots still queued at process exit are left to the OS.)
-struct Reaper {
-  std::mutex mu;
-  std::condition_variable cv;
-  std::vector<GpuSnapshot *> q;
-  Reaper() {
-    std::thread([this] {
-      for (;;) {
-        std::vector<GpuSnapshot *> batch;
-        {
-          std::unique_lock<std::mutex> g(mu);
-          cv.wait(g, [this] { return !q.empty(); });
-          batch.swap(q);
-        }
-        for (GpuSnapshot *s : batch) delete s;
-      }
-    }).detach();
-  }
-  void retire(GpuSnapshot *s) {
-    {
-      std::lock_guard<std::mutex> g(mu);
-      q.push_back(s);
-    }
-    cv.notify_one();
-  }
-};
-Reaper &reaper() {
-  static Reaper *r = new Reaper;
-  return *r;
-}
-std::shared_ptr<GpuSnapshot> share_snapshot(std::unique_ptr<GpuSnapshot> g) {
-  return std::shared_ptr<GpuSnapshot>(g.release(), [](GpuSnapshot *s) {
-    if (s) reaper().retire(s);
-  });
-}
-
 int install(mqm_index *h, std::shared_ptr<GpuSnapshot> g, uint64_t version) {
   std::unique_lock<std::shared_mutex> w(h->snap_rw);
   h->snap = std::move(g);
@@ -339,7 +298,7 @@ int publish_locked(mqm_index *h, int *published) {
   for (int i = 0; i < 3; i++) h->last_build_phase_ms[i] = b.phase_ms[i];
   h->last_build_kept_shape = b.kept_shape;
   if (published) *published = 1;
-  return install(h, share_snapshot(std::move(b.snap)), b.version);
+  return install(h, std::shared_ptr<GpuSnapshot>(std::move(b.snap)), b.version);
 }
 
 // after a logged mutation: the periodic-rebuild policy (mqm_commit_policy)
@@ -381,7 +340,7 @@ int commit_locked(mqm_index *h) {
   std::unique_ptr<GpuSnapshot> g;
   rc = upload(std::move(hs), h->cfg.device, h->dev.stream, &g);
   if (rc != MQM_OK) return rc;
-  return install(h, share_snapshot(std::move(g)), h->store.version());
+  return install(h, std::shared_ptr<GpuSnapshot>(std::move(g)), h->store.version());
 }
 
 int ensure_snapshot_locked(mqm_index *h) {
@@ -1532,6 +1491,9 @@ struct Collector {
 // it), and a caller posts only once the running launch's snapshot is at least
 // as new as its own front buffer, so a result never predates the caller's
 // view of the store (MQM_CFG_AUTOCOMMIT: read-your-writes).
+void server_register(Server *s);
+void server_unregister(Server *s);
+
 struct Server {
   mqm_index *h;
   ServeQueue *q = nullptr;            // pinned, coherent, device-mapped
@@ -1645,6 +1607,7 @@ struct Server {
     for (uint32_t p = 0; p < n_pollers; p++) pollers[p].th = std::thread([this, p] { poll_loop(p); });
     serve_count(+1);
     counted = true;
+    server_register(this);
     return MQM_OK;
   }
   // (mu held) stop a running kernel and wait for it
@@ -1660,7 +1623,10 @@ struct Server {
     launched = false;
   }
   ~Server() {
-    if (counted) serve_count(-1);
+    if (counted) {
+      server_unregister(this);  // (waits for a reaper pass that holds this server stopped)
+      serve_count(-1);
+    }
     poller_quit.store(true, std::memory_order_release);
     for (uint32_t p = 0; p < n_pollers; p++)
       if (pollers[p].th.joinable()) {
@@ -1915,7 +1881,88 @@ struct Server {
   }
 };
 
+// Live servers, for the reaper to stop while it frees.
+struct ServerRegistry {
+  std::mutex mu;
+  std::vector<Server *> list;
+};
+ServerRegistry &server_registry() {
+  static auto *r = new ServerRegistry;  // (never destroyed: the reaper thread outlives static destruction)
+  return *r;
+}
+void server_register(Server *s) {
+  ServerRegistry &r = server_registry();
+  std::lock_guard<std::mutex> g(r.mu);
+  r.list.push_back(s);
+}
+void server_unregister(Server *s) {
+  ServerRegistry &r = server_registry();
+  std::lock_guard<std::mutex> g(r.mu);
+  r.list.erase(std::remove(r.list.begin(), r.list.end(), s), r.list.end());
+}
+
+// The device buffers of destroyed snapshots, freed on a thread of their own
+// (flatten.h retire_device_buffers).  hipFree waits until every kernel on
+// the device has finished (tools/free_probe.hip: it waited out a 1 s spinner),
+// and a per-publish server runs for as long as calls arrive: a caller, the
+// builder or the committing thread that dropped a snapshot's last reference
+// used to block there — until the load stopped, or for good once a ring slot
+// had been abandoned (r05i).  The reaper stops every live server (its lock
+// held, so no caller relaunches it meanwhile), frees, and lets the next call
+// relaunch.
+struct BufReaper {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<std::pair<int, std::vector<void *>>> q;
+  BufReaper() {
+    std::thread([this] { run(); }).detach();
+  }
+  void run() {
+    for (;;) {
+      std::vector<std::pair<int, std::vector<void *>>> batch;
+      {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [this] { return !q.empty(); });
+        batch.swap(q);
+      }
+      const int64_t t0 = steady_ns();
+      ServerRegistry &r = server_registry();
+      std::lock_guard<std::mutex> rg(r.mu);
+      std::vector<std::unique_lock<std::mutex>> held;
+      held.reserve(r.list.size());
+      for (Server *sv : r.list) {
+        held.emplace_back(sv->mu);
+        sv->halt();
+      }
+      for (auto &x : batch) {
+        if (x.first >= 0) (void)hipSetDevice(x.first);
+        for (void *p : x.second) (void)hipFree(p);
+      }
+      const int64_t t1 = steady_ns();
+      if (serve_trace() && t1 - t0 > 5000000)
+        fprintf(stderr, "[serve-trace] %.6f reaper: %zu snapshot(s) freed with %zu server(s) stopped in %.1f ms\n",
+                t1 * 1e-9, batch.size(), held.size(), (t1 - t0) / 1e6);
+    }
+  }
+  void push(int device, std::vector<void *> bufs) {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      q.emplace_back(device, std::move(bufs));
+    }
+    cv.notify_one();
+  }
+};
+
 }  // namespace
+
+}  // extern "C" (a C++ function for flatten.cpp)
+namespace mqm {
+void retire_device_buffers(int device, std::vector<void *> bufs) {
+  static auto *r = new BufReaper;  // (never destroyed, like its thread)
+  r->push(device, std::move(bufs));
+}
+}  // namespace mqm
+extern "C" {
 
 void mqm_index::stop_server() {
   server.store(nullptr, std::memory_order_release);

@@ -848,8 +848,17 @@ hipStream_t reclaim_stream(int device) {
 }
 }  // namespace
 
-static void buffers_free(void *b, hipStream_t rs) {
-  if (b) (void)hipFreeAsync(b, rs);
+// MQM_SNAP_POOL=1 (A/B, unsafe): snapshot buffers from the stream-ordered
+// pool, freed with hipFreeAsync.  Measured wrong on the box: served results
+// under churn missed the newest subscriptions (tests/test_gpu_serve_churn.py,
+// r05o-r05r), and tools/reuse_probe.hip saw a kernel on another stream read
+// pool memory that a synchronised host -> device copy had refilled without the
+// new data (r05s).  The default is hipMalloc / hipFree, the frees handed to
+// the index layer's reaper (retire_device_buffers), which stops the
+// per-publish servers first: hipFree waits for every running kernel.
+static bool snap_pool() {
+  static const bool v = getenv("MQM_SNAP_POOL") && atoi(getenv("MQM_SNAP_POOL")) != 0;
+  return v;
 }
 
 GpuSnapshot::~GpuSnapshot() {
@@ -857,9 +866,17 @@ GpuSnapshot::~GpuSnapshot() {
   // (every reader holds this snapshot until its work is done: the server
   // until it is halted, a batch until its stream is synchronised, a queued
   // context until its next call — so nothing on the device reads these now)
-  const hipStream_t rs = reclaim_stream(device);
-  for (void *b : {words, slots, ident_bits, nflags, bloom, pinfo, partners}) buffers_free(b, rs);
-  for (void *b : buffers) buffers_free(b, rs);
+  std::vector<void *> bufs;
+  for (void *b : {words, slots, ident_bits, nflags, bloom, pinfo, partners})
+    if (b) bufs.push_back(b);
+  for (void *b : buffers)
+    if (b) bufs.push_back(b);
+  if (snap_pool()) {
+    const hipStream_t rs = reclaim_stream(device);
+    for (void *b : bufs) (void)hipFreeAsync(b, rs);
+  } else if (!bufs.empty()) {
+    retire_device_buffers(device, std::move(bufs));
+  }
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (ms > 50.0) fprintf(stderr, "mqmatch: freeing a snapshot's device buffers took %.1f ms\n", ms);
 }
@@ -869,9 +886,9 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
   auto g = std::make_unique<GpuSnapshot>();
   if (device >= 0) {
     g->device = device;
-    (void)reclaim_stream(device);  // (creates it, sets the pool's release threshold)
+    if (snap_pool()) (void)reclaim_stream(device);  // (creates it, sets the pool's release threshold)
   }
-  auto dalloc = [&](void **p, size_t n) { return hipMallocAsync(p, n, stream); };
+  auto dalloc = [&](void **p, size_t n) { return snap_pool() ? hipMallocAsync(p, n, stream) : hipMalloc(p, n); };
   if (device < 0) {  // host-only index: no device copy
     g->host = std::move(hs);
     *out = std::move(g);

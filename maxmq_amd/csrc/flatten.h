@@ -130,6 +130,12 @@ struct GpuSnapshot {
   ~GpuSnapshot();
 };
 
+// Device buffers of a destroyed snapshot, freed later by the index layer
+// (capi.cpp): hipFree waits for every kernel on the device, the per-publish
+// server included, so the frees run on a thread of their own with the
+// servers stopped.
+void retire_device_buffers(int device, std::vector<void *> bufs);
+
 // Copies on `stream` and waits for them (nullptr: the null stream).  device < 0
 // (MQM_DEVICE_NONE) wraps the host snapshot without device buffers, so a
 // host-only index still has stats and a digest.

@@ -49,6 +49,7 @@ for step in "$@"; do
   echo "[run_r05] $step $(date +%T)"
   case $step in
     tests) timeout -k 10 1000 $PYT tests -m gpu --timeout 600 --durations=15 > $OUT/pytest_gpu.log 2>&1 ;;
+    churnt) timeout -k 10 500 $PYT tests/test_gpu_serve_churn.py -m gpu --timeout 300 > $OUT/pytest_churn.log 2>&1 ;;
     serve) timeout -k 10 600 $PYT tests/test_gpu_serve.py tests/test_gpu_serve_churn.py tests/test_gpu_shim.py -m gpu \
              --timeout 300 > $OUT/pytest_serve.log 2>&1 ;;
     ab) for V in base:X=0 long:MQM_LONG_PART=256 desccopy:MQM_DESC_COPY=1; do
@@ -101,6 +102,7 @@ for step in "$@"; do
              2> $OUT/bench_fast_pipe$P.log || exit 1; done ;;
     par) timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_gpu_queued.py -m gpu --timeout 300 \
              > $OUT/pytest_par.log 2>&1 ;;
+    reuseprobe) timeout -k 10 120 tools/_build/reuse_probe > $OUT/reuse_probe.txt 2>&1 ;;
     pollprobe) timeout -k 10 120 tools/_build/poll_probe > $OUT/poll_probe.txt 2>&1 ;;
     freeprobe) timeout -k 10 60 tools/_build/free_probe > $OUT/free_probe.txt 2>&1 ;;
     calib) timeout -k 10 120 tools/_build/calib_fetch > $OUT/calib_kernels.txt 2>&1 ;;

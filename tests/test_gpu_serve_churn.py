@@ -172,5 +172,21 @@ def test_served_calls_under_churn_equal_oracle_at_their_version(tmp_path, mode, 
             if sorted(lines) != want[t]:
                 bad.append((k, v, t))
     ora.close()
-    assert not bad, f"{len(bad)} of {len(calls_out)} results differ from the oracle at their version, first {bad[0]}"
+    if bad:  # what differs in the first few (rows only in the result / only in the oracle's)
+        detail = []
+        for k, v, t in bad[:3]:
+            got = set(calls_out[k][2])
+            ora2 = OracleIndex()
+            for c, f, q, nl, rap, rh, ident in base:
+                ora2.subscribe(c, f, q, bool(nl), bool(rap), rh, ident)
+            for op in ops[:prefix[v]]:
+                if op[0] == "S":
+                    ora2.subscribe(op[1], op[2], op[3], bool(op[4]), bool(op[5]), op[6], op[7])
+                else:
+                    ora2.unsubscribe(op[1], op[2])
+            w = set(_render_oracle(ora2, [t], topics)[t])
+            ora2.close()
+            detail.append((k, v, t, topics[t], sorted(got - w)[:4], sorted(w - got)[:4]))
+        raise AssertionError(f"{len(bad)} of {len(calls_out)} results differ from the oracle at their version; "
+                             f"(call, version, topic, name, only in result, only in oracle): {detail}")
     assert launches >= 2, launches
