@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <thread>
 
@@ -861,24 +862,82 @@ static bool snap_pool() {
   return v;
 }
 
+// Snapshot buffers are recycled, not freed: a destroyed snapshot's buffers go
+// to a per-device free list and the next upload takes the smallest one that
+// fits (a rebuild's arrays are within a few percent of the last one's).
+// Refilling a kept hipMalloc buffer in place is read correctly by kernels on
+// other streams (tools/reuse_probe.hip, r05u), unlike a pool reallocation;
+// and no hipFree — which waits for the per-publish server — runs at all while
+// the free list stays under kRecycleCap.  Above it, the largest spare buffers
+// go to the index layer's reaper (retire_device_buffers), which stops the
+// servers before freeing.
+namespace {
+constexpr size_t kRecycleCap = 96ull << 30;  // spare bytes kept per device
+struct Recycler {
+  std::mutex mu;
+  std::multimap<size_t, void *> spare[64];  // capacity -> buffer
+  size_t bytes[64] = {};
+};
+Recycler &recycler() {
+  static auto *r = new Recycler;  // (never destroyed: snapshots may die during static destruction)
+  return *r;
+}
+// a buffer of at least n bytes: a spare one of capacity in [n, 1.25 n], else a
+// new one with 1/16 headroom (the next rebuild's array may be a little larger)
+hipError_t recycled_alloc(int device, void **p, size_t n, size_t *cap) {
+  if (device >= 0 && device < 64) {
+    Recycler &r = recycler();
+    std::lock_guard<std::mutex> g(r.mu);
+    auto it = r.spare[device].lower_bound(n);
+    if (it != r.spare[device].end() && it->first <= n + n / 4) {
+      *p = it->second;
+      *cap = it->first;
+      r.bytes[device] -= it->first;
+      r.spare[device].erase(it);
+      return hipSuccess;
+    }
+  }
+  const size_t want = n + n / 16;
+  *cap = want;
+  return hipMalloc(p, want);
+}
+void recycled_free(int device, std::vector<std::pair<void *, size_t>> &held) {
+  if (held.empty()) return;
+  if (device < 0 || device >= 64) {
+    std::vector<void *> v;
+    for (auto &x : held) v.push_back(x.first);
+    retire_device_buffers(device, std::move(v));
+    return;
+  }
+  std::vector<void *> excess;
+  {
+    Recycler &r = recycler();
+    std::lock_guard<std::mutex> g(r.mu);
+    for (auto &x : held) {
+      r.spare[device].emplace(x.second, x.first);
+      r.bytes[device] += x.second;
+    }
+    while (r.bytes[device] > kRecycleCap && !r.spare[device].empty()) {
+      auto it = std::prev(r.spare[device].end());
+      excess.push_back(it->second);
+      r.bytes[device] -= it->first;
+      r.spare[device].erase(it);
+    }
+  }
+  if (!excess.empty()) retire_device_buffers(device, std::move(excess));
+}
+}  // namespace
+
 GpuSnapshot::~GpuSnapshot() {
-  const auto t0 = std::chrono::steady_clock::now();
   // (every reader holds this snapshot until its work is done: the server
   // until it is halted, a batch until its stream is synchronised, a queued
   // context until its next call — so nothing on the device reads these now)
-  std::vector<void *> bufs;
-  for (void *b : {words, slots, ident_bits, nflags, bloom, pinfo, partners})
-    if (b) bufs.push_back(b);
-  for (void *b : buffers)
-    if (b) bufs.push_back(b);
   if (snap_pool()) {
     const hipStream_t rs = reclaim_stream(device);
-    for (void *b : bufs) (void)hipFreeAsync(b, rs);
-  } else if (!bufs.empty()) {
-    retire_device_buffers(device, std::move(bufs));
+    for (auto &x : held) (void)hipFreeAsync(x.first, rs);
+  } else {
+    recycled_free(device, held);
   }
-  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  if (ms > 50.0) fprintf(stderr, "mqmatch: freeing a snapshot's device buffers took %.1f ms\n", ms);
 }
 
 
@@ -888,7 +947,12 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
     g->device = device;
     if (snap_pool()) (void)reclaim_stream(device);  // (creates it, sets the pool's release threshold)
   }
-  auto dalloc = [&](void **p, size_t n) { return snap_pool() ? hipMallocAsync(p, n, stream) : hipMalloc(p, n); };
+  auto dalloc = [&](void **p, size_t n) {
+    size_t cap = n;
+    const hipError_t e = snap_pool() ? hipMallocAsync(p, n, stream) : recycled_alloc(device, p, n, &cap);
+    if (e == hipSuccess) g->held.emplace_back(*p, cap);
+    return e;
+  };
   if (device < 0) {  // host-only index: no device copy
     g->host = std::move(hs);
     *out = std::move(g);

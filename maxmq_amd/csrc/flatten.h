@@ -125,7 +125,8 @@ struct GpuSnapshot {
   void *pinfo = nullptr, *partners = nullptr;  // DeviceSnapshot::pinfo / partners
   DeviceRetained ret{};
   bool has_retained = false;
-  int device = -1;  // the buffers' device (from its stream-ordered pool; freed with hipFreeAsync)
+  int device = -1;  // the buffers' device
+  std::vector<std::pair<void *, size_t>> held;  // every device buffer above, with its capacity (recycled)
   uint64_t device_bytes = 0;
   ~GpuSnapshot();
 };

@@ -40,13 +40,17 @@ int main() {
   std::vector<unsigned> a(n, 0xAAAAAAAAu), b(n, 0xBBBBBBBBu);
   unsigned long long *cnt = nullptr, h = 0;
   CK(hipMalloc((void **)&cnt, 8));
-  for (int mode = 0; mode < 4; mode++) {
+  void *keep_buf = nullptr;  // mode 4: one hipMalloc'd buffer refilled in place (no free)
+  for (int mode = 0; mode < 6; mode++) {
     // mode 0: pool, copy on U; 1: pool, copy on S (the reading stream);
     // 2: pool, D2D through a fresh staging buffer; 3: hipMalloc / hipFree
     void *m = nullptr;
-    if (mode == 3)
+    if (mode == 3 || mode == 5)
       CK(hipMalloc(&m, bytes));
-    else
+    else if (mode == 4) {
+      if (!keep_buf) CK(hipMalloc(&keep_buf, bytes));
+      m = keep_buf;
+    } else
       CK(hipMallocAsync(&m, bytes, u));
     CK(hipMemcpyAsync(m, a.data(), bytes, hipMemcpyHostToDevice, u));
     CK(hipStreamSynchronize(u));
@@ -56,7 +60,9 @@ int main() {
     CK(hipMemcpy(&h, cnt, 8, hipMemcpyDeviceToHost));
     const unsigned long long first = h;
     void *m2 = nullptr;
-    if (mode == 3) {
+    if (mode == 4 || mode == 5) {
+      m2 = m;  // refilled in place
+    } else if (mode == 3) {
       CK(hipFree(m));
       CK(hipMalloc(&m2, bytes));
     } else {
@@ -84,15 +90,17 @@ int main() {
     CK(hipStreamSynchronize(s));
     CK(hipMemcpy(&h, cnt, 8, hipMemcpyDeviceToHost));
     const char *what[] = {"pool, refill H2D on another stream", "pool, refill H2D on the reading stream",
-                          "pool, refill D2D from a fresh buffer", "hipMalloc / hipFree"};
+                          "pool, refill D2D from a fresh buffer", "hipMalloc / hipFree",
+                          "one hipMalloc buffer refilled (kept)", "fresh hipMalloc buffer refilled"};
     printf("%-42s same address %d; A words before %llu / %zu, stale A words after refill %llu\n", what[mode],
            m2 == m, first, n, h);
-    if (mode == 3)
+    if (mode == 3 || mode == 5)
       CK(hipFree(m2));
-    else
+    else if (mode != 4)
       CK(hipFreeAsync(m2, u));
     CK(hipStreamSynchronize(u));
   }
+  if (keep_buf) CK(hipFree(keep_buf));
   printf("OK\n");
   return 0;
 }
