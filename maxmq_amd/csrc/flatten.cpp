@@ -873,11 +873,28 @@ static bool snap_pool() {
 // servers before freeing.
 namespace {
 constexpr size_t kRecycleCap = 96ull << 30;  // spare bytes kept per device
+struct Spare {
+  void *p;
+  int64_t since_ns;  // retired at (a spare is taken only after kQuarantineNs)
+};
 struct Recycler {
   std::mutex mu;
-  std::multimap<size_t, void *> spare[64];  // capacity -> buffer
+  std::multimap<size_t, Spare> spare[64];  // capacity -> buffer
   size_t bytes[64] = {};
 };
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+const int64_t kQuarantineNs = [] {
+  const char *e = getenv("MQM_RECYCLE_QUARANTINE_MS");
+  return (int64_t)(e ? atoi(e) : 2000) * 1000000;
+}();
+// MQM_SNAP_RECYCLE=1 (A/B): recycle snapshot buffers (default: hipFree on the reaper)
+bool snap_recycle() {
+  static const bool v = getenv("MQM_SNAP_RECYCLE") && atoi(getenv("MQM_SNAP_RECYCLE")) != 0;
+  return v;
+}
 Recycler &recycler() {
   static auto *r = new Recycler;  // (never destroyed: snapshots may die during static destruction)
   return *r;
@@ -888,9 +905,10 @@ hipError_t recycled_alloc(int device, void **p, size_t n, size_t *cap) {
   if (device >= 0 && device < 64) {
     Recycler &r = recycler();
     std::lock_guard<std::mutex> g(r.mu);
-    auto it = r.spare[device].lower_bound(n);
-    if (it != r.spare[device].end() && it->first <= n + n / 4) {
-      *p = it->second;
+    const int64_t now = now_ns();
+    for (auto it = r.spare[device].lower_bound(n); it != r.spare[device].end() && it->first <= n + n / 4; ++it) {
+      if (now - it->second.since_ns < kQuarantineNs) continue;
+      *p = it->second.p;
       *cap = it->first;
       r.bytes[device] -= it->first;
       r.spare[device].erase(it);
@@ -913,13 +931,14 @@ void recycled_free(int device, std::vector<std::pair<void *, size_t>> &held) {
   {
     Recycler &r = recycler();
     std::lock_guard<std::mutex> g(r.mu);
+    const int64_t now = now_ns();
     for (auto &x : held) {
-      r.spare[device].emplace(x.second, x.first);
+      r.spare[device].emplace(x.second, Spare{x.first, now});
       r.bytes[device] += x.second;
     }
     while (r.bytes[device] > kRecycleCap && !r.spare[device].empty()) {
       auto it = std::prev(r.spare[device].end());
-      excess.push_back(it->second);
+      excess.push_back(it->second.p);
       r.bytes[device] -= it->first;
       r.spare[device].erase(it);
     }
@@ -935,8 +954,12 @@ GpuSnapshot::~GpuSnapshot() {
   if (snap_pool()) {
     const hipStream_t rs = reclaim_stream(device);
     for (auto &x : held) (void)hipFreeAsync(x.first, rs);
-  } else {
+  } else if (snap_recycle()) {
     recycled_free(device, held);
+  } else if (!held.empty()) {
+    std::vector<void *> v;
+    for (auto &x : held) v.push_back(x.first);
+    retire_device_buffers(device, std::move(v));
   }
 }
 
@@ -949,7 +972,9 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
   }
   auto dalloc = [&](void **p, size_t n) {
     size_t cap = n;
-    const hipError_t e = snap_pool() ? hipMallocAsync(p, n, stream) : recycled_alloc(device, p, n, &cap);
+    const hipError_t e = snap_pool()      ? hipMallocAsync(p, n, stream)
+                         : snap_recycle() ? recycled_alloc(device, p, n, &cap)
+                                          : hipMalloc(p, n);
     if (e == hipSuccess) g->held.emplace_back(*p, cap);
     return e;
   };
