@@ -483,7 +483,8 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
   //    layout equals that of one serial pass.
   hs.nodes.resize(nn);
   std::vector<uint8_t> flags(nn, 0);
-  std::vector<uint32_t> par_new(nn, kNone);
+  std::vector<uint32_t, NoInitAlloc<uint32_t>> par_new(nn);  // (set for every node below; kNone at the root)
+  par_new[0] = kNone;
   constexpr uint32_t kNChunks = 256;
   std::vector<uint64_t> sub_base(kNChunks + 1, 0), sh_base(kNChunks + 1, 0), lit_c(kNChunks, 0);
   std::vector<uint32_t> height_c(kNChunks, 0);
@@ -583,12 +584,20 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
   if (st.retained_len() > 0) build_retained(st, order, new_id, hs);
   pt.mark("retained");
   // every range: solo entries first, then multi (stable); count the multi ones
+  // (nodes are independent: in parallel over preorder chunks)
+  constexpr uint32_t kRChunks = 256;
+  auto rchunk = [&](uint32_t c, uint64_t *lo, uint64_t *hi) {
+    *lo = nn * c / kRChunks;
+    *hi = nn * (c + 1) / kRChunks;
+  };
   std::vector<uint32_t> own_multi(nn, 0);
   std::vector<uint32_t> new_sid(hs.subs.size());
-  {
+  parallel_for(kRChunks, [&](uint32_t c) {
+    uint64_t lo, hi;
+    rchunk(c, &lo, &hi);
     std::vector<SubEnt> se;
     std::vector<SubInfo> si;
-    for (uint64_t i = 0; i < nn; i++) {
+    for (uint64_t i = lo; i < hi; i++) {
       const uint32_t off = hs.nodes[i].sub_off, cnt = hs.nodes[i].sub_cnt;
       se.clear();
       si.clear();
@@ -603,7 +612,7 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
       std::copy(se.begin(), se.end(), hs.subs.begin() + off);
       std::copy(si.begin(), si.end(), hs.sub_info.begin() + off);
     }
-  }
+  });
   // the multi subscriptions' partner lists in final sids (snapshot.h: pinfo)
   {
     const uint64_t nsub = hs.subs.size();
@@ -613,53 +622,97 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
     // a partner is known by the multi-tail start of its node's range (where
     // the walk's multi part of that range starts, whichever probe gathered it)
     std::vector<uint32_t> tail_of(nsub, 0);
-    for (uint64_t i = 0; i < nn; i++) {
-      const uint32_t off = hs.nodes[i].sub_off, cnt = hs.nodes[i].sub_cnt;
-      for (uint32_t j = off + cnt - own_multi[i]; j < off + cnt; j++) tail_of[j] = off + cnt - own_multi[i];
-    }
+    parallel_for(kRChunks, [&](uint32_t c) {
+      uint64_t lo, hi;
+      rchunk(c, &lo, &hi);
+      for (uint64_t i = lo; i < hi; i++) {
+        const uint32_t off = hs.nodes[i].sub_off, cnt = hs.nodes[i].sub_cnt;
+        for (uint32_t j = off + cnt - own_multi[i]; j < off + cnt; j++) tail_of[j] = off + cnt - own_multi[i];
+      }
+    });
     auto pkey = [&](uint32_t old) {
       const uint32_t p = new_sid[old], m = hs.subs[p].word;  // build-time meta (snapshot.h): qos[1:0], nl[2]
       return tail_of[p] | (m & 3u) << 28 | ((m >> 2) & 1u) << 30;
     };
-    for (uint64_t x = 0; x < nsub; x++) {
-      const uint16_t c = partners.cnt[x];
-      if (c == 0) continue;
-      const uint32_t nx = new_sid[x];
-      if (c == kPHeavy) {
-        hs.pinfo[nx] = make_uint2(kNone, kPInfoHeavy);
-        heavy_at[nx] = 1;
-      } else if (c <= 2) {  // inline: the partner's key | QoS << 28 | NoLocal << 30
-        const uint64_t o = partners.off[x];
-        hs.pinfo[nx] = make_uint2(pkey(partners.part[o]), c == 2 ? pkey(partners.part[o + 1]) : kNone);
-      } else {
-        hs.pinfo[nx] = make_uint2((uint32_t)hs.partners.size(), kPInfoList | c);
-        for (uint64_t o = partners.off[x]; o < partners.off[x + 1]; o++) hs.partners.push_back(pkey(partners.part[o]));
+    // lists of more than two partners, at offsets in entry order (counted,
+    // prefix-summed, filled in parallel: the layout of one serial pass)
+    constexpr uint32_t kPChunks = 256;
+    std::vector<uint64_t> list_base(kPChunks + 1, 0);
+    auto pchunk = [&](uint32_t c, uint64_t *lo, uint64_t *hi) {
+      *lo = nsub * c / kPChunks;
+      *hi = nsub * (c + 1) / kPChunks;
+    };
+    parallel_for(kPChunks, [&](uint32_t c) {
+      uint64_t lo, hi, t = 0;
+      pchunk(c, &lo, &hi);
+      for (uint64_t x = lo; x < hi; x++) {
+        const uint16_t k = partners.cnt[x];
+        if (k > 2 && k != kPHeavy) t += k;
       }
-    }
-    // a node whose range (multi tail) holds a heavy entry: its topics merge by hash table
-    for (uint64_t i = 0; i < nn; i++) {
-      const uint32_t off = hs.nodes[i].sub_off, cnt = hs.nodes[i].sub_cnt;
-      for (uint32_t j = off + cnt - own_multi[i]; j < off + cnt; j++)
-        if (heavy_at[j]) {
-          flags[i] |= kFlagHeavyOwn;
-          break;
+      list_base[c + 1] = t;
+    });
+    for (uint32_t c = 0; c < kPChunks; c++) list_base[c + 1] += list_base[c];
+    hs.partners.resize(list_base[kPChunks]);
+    parallel_for(kPChunks, [&](uint32_t c) {
+      uint64_t lo, hi;
+      pchunk(c, &lo, &hi);
+      uint64_t w = list_base[c];
+      for (uint64_t x = lo; x < hi; x++) {
+        const uint16_t k = partners.cnt[x];
+        if (k == 0) continue;
+        const uint32_t nx = new_sid[x];
+        if (k == kPHeavy) {
+          hs.pinfo[nx] = make_uint2(kNone, kPInfoHeavy);
+          heavy_at[nx] = 1;
+        } else if (k <= 2) {  // inline: the partner's key | QoS << 28 | NoLocal << 30
+          const uint64_t o = partners.off[x];
+          hs.pinfo[nx] = make_uint2(pkey(partners.part[o]), k == 2 ? pkey(partners.part[o + 1]) : kNone);
+        } else {
+          hs.pinfo[nx] = make_uint2((uint32_t)w, kPInfoList | k);
+          for (uint64_t o = partners.off[x]; o < partners.off[x + 1]; o++) hs.partners[w++] = pkey(partners.part[o]);
         }
-    }
+      }
+    });
+    // a node whose range (multi tail) holds a heavy entry: its topics merge by hash table
+    parallel_for(kRChunks, [&](uint32_t c) {
+      uint64_t lo, hi;
+      rchunk(c, &lo, &hi);
+      for (uint64_t i = lo; i < hi; i++) {
+        const uint32_t off = hs.nodes[i].sub_off, cnt = hs.nodes[i].sub_cnt;
+        for (uint32_t j = off + cnt - own_multi[i]; j < off + cnt; j++)
+          if (heavy_at[j]) {
+            flags[i] |= kFlagHeavyOwn;
+            break;
+          }
+      }
+    });
   }
-  for (uint64_t i = 0; i < nn; i++) {
-    NodeDesc &d = hs.nodes[i];
-    const uint32_t hm = d.hash != kNone ? own_multi[d.hash] : 0;
-    d.hsub_cnt = d.hash != kNone ? hs.nodes[d.hash].sub_cnt : 0;
-    d.multi = std::min<uint32_t>(own_multi[i], 0xFFFF) | (std::min<uint32_t>(hm, 0xFFFF) << 16);
-    if (own_multi[i] >= 0xFFFF || hm >= 0xFFFF) d.sh_cnt_flags |= (uint32_t)kFlagMultiSat << 24;
-    d.sh_cnt_flags |= (uint32_t)(flags[i] & kFlagHeavyOwn) << 24;
-    if (d.hash != kNone && (flags[d.hash] & kFlagHeavyOwn)) d.sh_cnt_flags |= (uint32_t)kFlagHeavyHash << 24;
-    if (i > 0 && d.hash != kNone) {  // root: its '#' child is dollar-wild, unlike the root itself
-      const NodeDesc &h = hs.nodes[d.hash];
-      if (!((h.sh_cnt_flags >> 24) & kFlagHasChildren) && (h.sh_cnt_flags & kShCntMask) == 0)
+  // a '#' child that is a leaf without shared subscriptions, read before the
+  // pass below adds flag bits (kFlagHashLeaf)
+  std::vector<uint8_t> hash_leaf(nn, 0);
+  parallel_for(kRChunks, [&](uint32_t c) {
+    uint64_t lo, hi;
+    rchunk(c, &lo, &hi);
+    for (uint64_t i = lo; i < hi; i++) {
+      const NodeDesc &h = hs.nodes[i];
+      hash_leaf[i] = !((h.sh_cnt_flags >> 24) & kFlagHasChildren) && (h.sh_cnt_flags & kShCntMask) == 0;
+    }
+  });
+  parallel_for(kRChunks, [&](uint32_t c) {
+    uint64_t lo, hi;
+    rchunk(c, &lo, &hi);
+    for (uint64_t i = lo; i < hi; i++) {
+      NodeDesc &d = hs.nodes[i];
+      const uint32_t hm = d.hash != kNone ? own_multi[d.hash] : 0;
+      d.hsub_cnt = d.hash != kNone ? hs.nodes[d.hash].sub_cnt : 0;
+      d.multi = std::min<uint32_t>(own_multi[i], 0xFFFF) | (std::min<uint32_t>(hm, 0xFFFF) << 16);
+      if (own_multi[i] >= 0xFFFF || hm >= 0xFFFF) d.sh_cnt_flags |= (uint32_t)kFlagMultiSat << 24;
+      d.sh_cnt_flags |= (uint32_t)(flags[i] & kFlagHeavyOwn) << 24;
+      if (d.hash != kNone && (flags[d.hash] & kFlagHeavyOwn)) d.sh_cnt_flags |= (uint32_t)kFlagHeavyHash << 24;
+      if (i > 0 && d.hash != kNone && hash_leaf[d.hash])  // root: its '#' child is dollar-wild, unlike the root itself
         d.sh_cnt_flags |= (uint32_t)kFlagHashLeaf << 24;
     }
-  }
+  });
 
   // the device word (snapshot.h): the entry's own delivery, ident flag on top
   // (and the host copy of DeviceSnapshot::words: the runs form's deliveries)

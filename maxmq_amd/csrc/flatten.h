@@ -43,7 +43,7 @@ struct SubInfo {
 using EdgeVec = std::vector<EdgeEntry, NoInitAlloc<EdgeEntry>>;
 
 struct HostSnapshot {
-  std::vector<NodeDesc> nodes;
+  std::vector<NodeDesc, NoInitAlloc<NodeDesc>> nodes;  // (every field is written by flatten)
   EdgeVec edges;   // n_buckets * kEdgesPerBucket (empty after upload, and when built on the device)
   // the literal edges in (parent preorder, child list) order, while the
   // device builds the table (shared with the builder's FlattenCache)
