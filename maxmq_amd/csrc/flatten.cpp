@@ -104,9 +104,12 @@ static void mark_multi(const Store &st, const std::vector<uint32_t> &order, Host
   const auto &nodes = st.nodes();
   const uint32_t plus_tok = st.plus_token(), hash_tok = st.hash_token();
   const uint64_t nsub = hs.sub_info.size();
-  std::vector<uint32_t> sub_node(nsub);
-  for (uint64_t i = 0; i < hs.nodes.size(); i++)
-    for (uint32_t j = 0; j < hs.nodes[i].sub_cnt; j++) sub_node[hs.nodes[i].sub_off + j] = order[i];
+  std::vector<uint32_t, NoInitAlloc<uint32_t>> sub_node(nsub);  // (every range is written: ranges tile the subs)
+  const uint64_t nn = hs.nodes.size();
+  parallel_for(256, [&](uint32_t c) {
+    for (uint64_t i = nn * c / 256; i < nn * (c + 1) / 256; i++)
+      for (uint32_t j = 0; j < hs.nodes[i].sub_cnt; j++) sub_node[hs.nodes[i].sub_off + j] = order[i];
+  });
   const uint32_t nc = st.clients().size();
   std::vector<uint32_t> cstart(nc + 2, 0), by_client(nsub);
   for (uint64_t s = 0; s < nsub; s++) cstart[hs.subs[s].client + 2]++;
