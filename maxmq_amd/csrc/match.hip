@@ -1877,18 +1877,49 @@ __global__ __launch_bounds__(256) void k_ident(DeviceSnapshot s, Outputs o, uint
   }
 }
 
-// 8 lanes per topic: its listed sids from the scratch area to iout[istart[t] ..)
-// (DFS topics: k_dfs<4> writes theirs)
+// a wavefront per 64 topics: their listed sids from the scratch areas to
+// iout[istart[t] ..).  The lanes scan the 64 counts, then copy the wave's
+// entries 64 at a time (entry -> topic by a 6-step search over the prefix in
+// LDS), so loads and stores stay lane-consecutive across topic boundaries
+// (8 lanes per topic moved 19 sids per topic at 0.86 TB/s, 1.81 ms on C3,
+// r05y).  DFS topics: k_dfs<4> writes theirs.
 __global__ __launch_bounds__(256) void k_ident_pack(Outputs o, uint32_t n, const uint64_t *__restrict__ mstart,
                                                     const uint32_t *__restrict__ scratch, uint64_t cap) {
-  constexpr int kL = 8;
-  const uint32_t gl = threadIdx.x % kL, ng = gridDim.x * (blockDim.x / kL);
-  for (uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) / kL; t < n; t += ng) {
-    if (o.cls[t] == kClsDfs) continue;
-    const uint32_t c = o.icount[t];
-    if (!c) continue;
-    const uint64_t a = o.istart[t], m = mstart[t];
-    for (uint32_t j = gl; j < c; j += kL) put_checked(o.iout, a + j, cap, scratch[m + j], &o.ctr->oob);
+  __shared__ uint32_t pre_all[4][kWave + 1];
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  uint32_t *pre = pre_all[wid];
+  const uint32_t nw = gridDim.x * (blockDim.x / kWave);
+  for (uint32_t w = blockIdx.x * (blockDim.x / kWave) + wid; (uint64_t)w * kWave < n; w += nw) {
+    const uint32_t t = w * kWave + lane;
+    uint32_t c = 0;
+    uint64_t src = 0, dst = 0;
+    if (t < n && o.cls[t] != kClsDfs) {
+      c = o.icount[t];
+      src = mstart[t];
+      dst = o.istart[t];
+    }
+    uint32_t inc = c;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const uint32_t v = __shfl_up(inc, d, kWave);
+      if (lane >= d) inc += v;
+    }
+    const uint32_t total = __shfl(inc, kWave - 1, kWave);
+    if (total == 0) continue;  // (wave-uniform)
+    pre[lane] = inc - c;
+    if (lane == 0) pre[kWave] = total;
+    wave_lds_sync();
+    for (uint32_t b = 0; b < total; b += kWave) {  // (every lane runs every step: the shuffles)
+      const uint32_t e = b + lane;
+      const bool ok = e < total;
+      uint32_t k = 0;  // the topic holding entry e: the largest k with pre[k] <= e
+#pragma unroll
+      for (uint32_t step = 32; step > 0; step >>= 1) k = pre[k + step] <= e ? k + step : k;
+      const uint32_t j = e - pre[k];
+      const uint64_t s0 = shfl64(src, (int)k), d0 = shfl64(dst, (int)k);
+      if (ok) put_checked(o.iout, d0 + j, cap, scratch[s0 + j], &o.ctr->oob);
+    }
+    wave_lds_sync();
   }
 }
 
@@ -2781,7 +2812,8 @@ int identifiers_device(const DeviceSnapshot &s, Workspace &ws, hipStream_t st, I
   o.iout = (uint32_t *)ws.ptr(W::kIOut);
   GUARD(o, kNeedIdent | kOIOut, n, "k_ident_pack");
   if (n > 0 && total > 0) {
-    hipLaunchKernelGGL(k_ident_pack, dim3(blocks), dim3(256), 0, st, o, n, mstart, scratch, total);
+    hipLaunchKernelGGL(k_ident_pack, dim3(std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, 16384))), dim3(256),
+                       0, st, o, n, mstart, scratch, total);
     HIP_TRY(hipGetLastError());
     if (ws.last_n_dfs) {
       hipLaunchKernelGGL(k_dfs<4>, dim3(fb_blocks), dim3(kWave), fb_lds, st, s, ws.last_bytes, ws.last_offs, o,
