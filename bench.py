@@ -557,12 +557,21 @@ def identifiers_leg(idx, tb, to, n, dev, args):
         return (time.perf_counter() - t0) / args.ident_steps, t_ids / args.ident_steps, nid
 
     plain, _, _ = timed(False)
-    both, ids, nid = timed(True)
+    after, ids_after, nid = timed(True)  # the pass after the match
+    idx.identifiers_early(True)  # the pass beside the match's merges (mqm_identifiers_early)
+    try:
+        both, ids, nid_e = timed(True)
+    finally:
+        idx.identifiers_early(False)
+    assert nid_e == nid, (nid_e, nid)
     return {"value": n / both, "unit": "topics/s", "ms_per_step": both * 1e3, "match_only_ms_per_step": plain * 1e3,
-            "identifiers_pass_ms": ids * 1e3, "identifiers_share_of_step": ids / both,
+            "identifiers_extra_ms": (both - plain) * 1e3, "identifiers_share_of_step": (both - plain) / both,
+            "collect_ms": ids * 1e3,
+            "after_the_match": {"value": n / after, "ms_per_step": after * 1e3, "identifiers_pass_ms": ids_after * 1e3},
             "listed_sids_per_topic": nid / n,
             "what": "blocking mqm_match_device + mqm_identifiers_device per 10M-topic batch (the shim's "
-                    "MQM_CFG_IDENTIFIERS configuration), vs blocking mqm_match_device alone"}
+                    "MQM_CFG_IDENTIFIERS configuration), the pass beside the merges (mqm_identifiers_early; "
+                    "after_the_match: run after it), vs blocking mqm_match_device alone"}
 
 
 def steady_state(idx, tb, to, n, dev, args):

@@ -320,6 +320,12 @@ int mqm_batching_stats(mqm_index *h, uint64_t *batches, uint64_t *topics);
  * maximum of each phase, then the number of calls */
 int mqm_direct_host_us(mqm_index *h, double *us);
 /* Device in / device out on `hip_stream` (hipStream_t, NULL = default stream). */
+/* on != 0: every device match (mqm_match_device, queued contexts) computes
+ * the Identifiers lists beside its merges (a second stream forked after the
+ * walk), so a following mqm_identifiers_device only collects them; for a
+ * caller that wants them after every batch.  Host-path matches of an
+ * MQM_CFG_IDENTIFIERS index always do. */
+int mqm_identifiers_early(mqm_index *h, int on);
 int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t *d_topic_offsets,
                      uint32_t n_topics, void *hip_stream, mqm_device_result *out);
 

@@ -267,6 +267,11 @@ class TopicsIndex:
         check("mqm_serve_host_us", lib().mqm_serve_host_us(self._h, v))
         return {"post": v[0], "wait": v[1], "collect": v[2], "slept_share": v[3]}
 
+    def identifiers_early(self, on: bool = True):
+        """device matches compute the Identifiers lists beside their merges
+        (mqm_identifiers_early); identifiers_device then only collects"""
+        check("mqm_identifiers_early", lib().mqm_identifiers_early(self._h, 1 if on else 0))
+
     def serve_host_max_us(self):
         """the longest served call per host phase since the previous read (us),
         and the number of calls over 10 ms"""

@@ -50,7 +50,7 @@ EXPORTED = [
     "mqm_match_device_async", "mqm_match_ctx_wait", "mqm_match_ctx_stats", "mqm_match_batch_packed",
     "mqm_result_packed", "mqm_match_batch_runs", "mqm_result_runs", "mqm_result_expand",
     "mqm_serve_policy", "mqm_serve_stats", "mqm_serve_device_us", "mqm_serve_host_us", "mqm_serve_host_max_us",
-    "mqm_build_phases_ms", "mqm_build_threads",
+    "mqm_build_phases_ms", "mqm_build_threads", "mqm_identifiers_early",
     "mqm_result_snapshot_version", "mqm_direct_host_us",
 ]
 
@@ -221,6 +221,7 @@ def lib():
         "mqm_serve_host_max_us": ([vp, vp], C.c_int),
         "mqm_build_phases_ms": ([vp, vp], C.c_int),
         "mqm_build_threads": ([C.c_uint32], C.c_int),
+        "mqm_identifiers_early": ([vp, C.c_int], C.c_int),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name, None)

@@ -133,6 +133,7 @@ struct mqm_index {
   // that turns them into the back buffer (builder.h)
   DeltaLog journal;
   std::unique_ptr<Builder> builder;
+  std::atomic<bool> ident_early{false};         // mqm_identifiers_early: device matches compute Identifiers beside
   std::atomic<Builder *> builder_pub{nullptr};  // builder.get(), readable without mu (front_fast)
   std::atomic<int64_t> submit_due_ns{0};        // policy_ms: when the logged mutations are due (0: none)
   uint64_t policy_ops = 0;               // auto-submit after this many logged mutations (0 = off)
@@ -800,6 +801,7 @@ int mqm_match_device(mqm_index *h, const uint8_t *d_topic_bytes, const uint64_t 
     c.has_mo = false;
     c.snap = snap;
     c.ws.begin(st);
+    c.ws.ident_early = h->ident_early.load(std::memory_order_relaxed);
     MatchOutput mo;
     rc = match_device(snap->dev, c.ws, d_topic_bytes, d_topic_offsets, n_topics, st, &mo);
     if (c.ws.end(st)) rc = rc ? rc : -3;
@@ -880,6 +882,7 @@ static int match_batch_impl(mqm_index *h, const char *topic_bytes, const uint64_
       if (e != MQM_OK) return e;
       MatchOutput mo;
       ws.runs = runs;
+      ws.ident_early = want_ids;  // (its identifiers pass runs beside the merges)
       e = match_device(snap->dev, ws, d_bytes, d_offs, n_topics, st, &mo);
       ws.runs = false;
       if (e != 0) return hip_rc(e);
@@ -1019,6 +1022,7 @@ int mqm_match_device_async(mqm_match_ctx *x, const uint8_t *d_topic_bytes, const
     x->c.snap = snap;  // held until the next call on this context
     x->c.has_mo = false;
     x->c.ws.begin(st);
+    x->c.ws.ident_early = h->ident_early.load(std::memory_order_relaxed);
     rc = match_enqueue(snap->dev, x->c.ws, d_topic_bytes, d_topic_offsets, n_topics, st, false);
     if (x->c.ws.end(st)) rc = rc ? rc : -3;
     if (rc != 0) return hip_rc(rc);
@@ -2255,6 +2259,12 @@ int mqm_commit_state_get(mqm_index *h, mqm_commit_state *out) {
   out->builds = h->builds;
   out->last_build_ops = h->last_build_ops;
   out->last_build_ms = h->last_build_ms;
+  return MQM_OK;
+}
+
+int mqm_identifiers_early(mqm_index *h, int on) {
+  if (!h || h->cfg.device == MQM_DEVICE_NONE) return MQM_EINVAL;
+  h->ident_early.store(on != 0, std::memory_order_relaxed);
   return MQM_OK;
 }
 

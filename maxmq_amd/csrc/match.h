@@ -61,7 +61,7 @@ struct Workspace {
     kSCount, kHCount, kDCount, kDStart, kHStart, kCls, kDfsList, kRecs, kCounters, kDOut, kHOut,
     kDense, kDenseShared, kDenseOffs, kDenseHOffs, kScanTmp, kRawCnt, kTabOff, kTabSize, kTable,
     kInBytes, kInOffs, kListS, kICount, kIStart, kIOut, kNSolo, kDescStart, kDesc, kWin, kMCount, kRunCount, kRunOffs, kRuns, kListW, kListT1, kListT2, kListT3, kListP, kListH, kListRS, kListR,
-    kIMStart, kIScratch,
+    kIMStart, kIScratch, kScanTmp2,
     // reverse match (retained.hip)
     kROffs, kRNLev, kRWild, kRLOff, kRFCount, kRFCur, kRLevels, kRNCount, kRNOff, kRItemF0, kRItemN0, kRItemF1,
     kRItemN1, kRChild, kRECount, kREOff, kREmit, kRPos, kRChunks, kRCOff, kROut, kRInBytes, kRInOffs, kNumSlots
@@ -100,6 +100,16 @@ struct Workspace {
   bool runs = false, last_runs = false;
   const uint8_t *last_bytes = nullptr;
   const uint64_t *last_offs = nullptr;
+  // Identifiers computed beside the match (mqm_identifiers_early, and every
+  // host-path call of an MQM_CFG_IDENTIFIERS index): after the walk, k_ident
+  // and its scans run on `side` while the merges and the solo copy run on the
+  // call's stream, joined before the call's read-back; identifiers_device then
+  // only collects.  ident_cap: the scratch / iout capacity (grown from the
+  // multi entries a call reported)
+  bool ident_early = false, ident_ready = false;
+  uint64_t ident_cap = 0;
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 
   // the small-batch path's pinned blocks (fast.hip)
   FastArena fast;

@@ -1838,8 +1838,12 @@ __global__ __launch_bounds__(kWave) void k_dfs(DeviceSnapshot s, const uint8_t *
 // sids; the map the host builds keeps one key per filter, as the reference's
 // does.  DFS topics are handled by k_dfs<3|4> (every entry).
 // ---------------------------------------------------------------------------
+// (early: beside the match, ident_launch — DFS topics get a count of 0 and a
+// scratch area past `cap` raises *ovf instead of writing; the call then runs
+// the pass again after the match)
 __global__ __launch_bounds__(256) void k_ident(DeviceSnapshot s, Outputs o, uint32_t n,
-                                               const uint64_t *__restrict__ mstart, uint32_t *__restrict__ scratch) {
+                                               const uint64_t *__restrict__ mstart, uint32_t *__restrict__ scratch,
+                                               uint64_t cap, unsigned long long *ovf) {
   // an 8-lane group per topic: most topics have a few short multi parts, and
   // a wavefront per topic left 56 lanes idle through each topic's dependent
   // loads (C3: 5.5 ms for the two phases, r05d)
@@ -1849,15 +1853,22 @@ __global__ __launch_bounds__(256) void k_ident(DeviceSnapshot s, Outputs o, uint
   const uint32_t groups = gridDim.x * (blockDim.x / kL);
   for (uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) / kL; t < n; t += groups) {
     const uint8_t cls = o.cls[t];
-    if (cls == kClsDfs) continue;
+    if (cls == kClsDfs) {
+      if (ovf && gl == 0) o.icount[t] = 0;
+      continue;
+    }
     uint32_t nid = 0;
     // (the walk writes the record header, which counts the multi parts, for
     // every topic with multi entries)
-    const uint32_t ms = cls != kClsDone ? o.mcount[t] : 0u;
+    uint32_t ms = cls != kClsDone ? o.mcount[t] : 0u;
+    const uint64_t ib = ms ? mstart[t] : 0;
+    if (ms && ib + ms > cap) {
+      if (gl == 0) atomicOr(ovf, 1ull);
+      ms = 0;
+    }
     if (ms) {
       const uint4 *gt = rec_tail(o.recs, t);
       const uint32_t nm = gt[0].x & 0xFFu;
-      const uint64_t ib = mstart[t];
       for (uint32_t h = 0; h < nm; h++) {  // the multi parts (solo parts: see above)
         const uint4 u = gt[-(int)(1 + h)];
         const uint32_t off = u.x, cnt = u.y;
@@ -1884,7 +1895,8 @@ __global__ __launch_bounds__(256) void k_ident(DeviceSnapshot s, Outputs o, uint
 // (8 lanes per topic moved 19 sids per topic at 0.86 TB/s, 1.81 ms on C3,
 // r05y).  DFS topics: k_dfs<4> writes theirs.
 __global__ __launch_bounds__(256) void k_ident_pack(Outputs o, uint32_t n, const uint64_t *__restrict__ mstart,
-                                                    const uint32_t *__restrict__ scratch, uint64_t cap) {
+                                                    const uint32_t *__restrict__ scratch, uint64_t cap,
+                                                    unsigned long long *ovf) {
   __shared__ uint32_t pre_all[4][kWave + 1];
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
   uint32_t *pre = pre_all[wid];
@@ -1917,7 +1929,14 @@ __global__ __launch_bounds__(256) void k_ident_pack(Outputs o, uint32_t n, const
       for (uint32_t step = 32; step > 0; step >>= 1) k = pre[k + step] <= e ? k + step : k;
       const uint32_t j = e - pre[k];
       const uint64_t s0 = shfl64(src, (int)k), d0 = shfl64(dst, (int)k);
-      if (ok) put_checked(o.iout, d0 + j, cap, scratch[s0 + j], &o.ctr->oob);
+      if (ok) {
+        if (!ovf)
+          put_checked(o.iout, d0 + j, cap, scratch[s0 + j], &o.ctr->oob);
+        else if (d0 + j < cap)
+          o.iout[d0 + j] = scratch[s0 + j];
+        else
+          atomicOr(ovf, 2ull);
+      }
     }
     wave_lds_sync();
   }
@@ -2207,6 +2226,9 @@ Workspace::~Workspace() {
   if (host_pinned) (void)hipHostFree(host_pinned);
   for (auto &e : ev)
     if (e) (void)hipEventDestroy(e);
+  if (ev_fork) (void)hipEventDestroy(ev_fork);
+  if (ev_join) (void)hipEventDestroy(ev_join);
+  if (side) (void)hipStreamDestroy(side);
 }
 
 static void mark(Workspace &ws, int i, hipStream_t st) {
@@ -2313,20 +2335,23 @@ struct Widen {
   __host__ __device__ uint64_t operator()(uint32_t c) const { return c; }
 };
 template <class T>
-static int scan_offsets_it(Workspace &ws, T counts, uint64_t *offs, uint32_t n, hipStream_t st);
-static int scan_offsets(Workspace &ws, const uint32_t *counts, uint64_t *offs, uint32_t n, hipStream_t st) {
+static int scan_offsets_it(Workspace &ws, T counts, uint64_t *offs, uint32_t n, hipStream_t st,
+                           Workspace::Slot tmp_slot = Workspace::kScanTmp);
+static int scan_offsets(Workspace &ws, const uint32_t *counts, uint64_t *offs, uint32_t n, hipStream_t st,
+                        Workspace::Slot tmp_slot = Workspace::kScanTmp) {
   return scan_offsets_it(ws, hipcub::TransformInputIterator<uint64_t, Widen, const uint32_t *>(counts, Widen{}), offs,
-                         n, st);
+                         n, st, tmp_slot);
 }
 template <class T>
-static int scan_offsets_it(Workspace &ws, T counts, uint64_t *offs, uint32_t n, hipStream_t st) {
+static int scan_offsets_it(Workspace &ws, T counts, uint64_t *offs, uint32_t n, hipStream_t st,
+                           Workspace::Slot tmp_slot) {
   static_assert(sizeof(typename std::iterator_traits<T>::value_type) == 8, "64-bit accumulation");
   HIP_TRY(hipMemsetAsync(offs, 0, sizeof(uint64_t), st));
   if (n == 0) return 0;
   size_t tmp = 0;
   HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, tmp, counts, offs + 1, n, st));
-  if (ws.get(Workspace::kScanTmp, tmp)) return -2;
-  HIP_TRY(hipcub::DeviceScan::InclusiveSum(ws.ptr(Workspace::kScanTmp), tmp, counts, offs + 1, n, st));
+  if (ws.get(tmp_slot, tmp)) return -2;
+  HIP_TRY(hipcub::DeviceScan::InclusiveSum(ws.ptr(tmp_slot), tmp, counts, offs + 1, n, st));
   return 0;
 }
 
@@ -2350,6 +2375,68 @@ static Counters *pinned_counters(Workspace &ws) {
   if (!ws.pinned_u64()) return nullptr;
   static_assert(sizeof(Counters) <= kPinnedU64, "pinned layout");
   return reinterpret_cast<Counters *>(ws.host_pinned);
+}
+
+// The identifiers pass beside the match (Workspace::ident_early): forked
+// from `st` after the walk onto ws.side — the walk's records, classes and
+// multi counts are final then, and the merges and the solo copy only read
+// them — and joined back before the call's read-back (match_enqueue).  Sized
+// from the last call's multi entries; a scratch area or list past that
+// capacity sets the flag the collect reads, and identifiers_device runs the
+// pass again after the match.  Pinned read-backs: total listed, overflow
+// flag, total multi entries (hp[8..10]).
+static int ident_launch(const DeviceSnapshot &s, Workspace &ws, Outputs o, uint32_t n, hipStream_t st) {
+  using W = Workspace;
+  if (!ws.side) {
+    if (hipStreamCreateWithFlags(&ws.side, hipStreamNonBlocking) != hipSuccess) {
+      ws.side = nullptr;
+      return -3;
+    }
+    if (hipEventCreateWithFlags(&ws.ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ws.ev_join, hipEventDisableTiming) != hipSuccess)
+      return -3;
+  }
+  uint64_t *hp = ws.pinned_u64();
+  if (!hp) return -2;
+  const uint64_t cap = std::max<uint64_t>(ws.ident_cap, 4ull * n + 4096);
+  size_t tmp = 0;
+  {
+    hipcub::TransformInputIterator<uint64_t, Widen, const uint32_t *> it(o.mcount, Widen{});
+    HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, tmp, it, (uint64_t *)nullptr, (int)std::max<uint32_t>(n, 1), st));
+  }
+  // (every buffer sized on the host before the fork: a growth waits for this
+  // workspace's queued work, which must not include the side stream's)
+  if (ws.get(W::kIMStart, sizeof(uint64_t) * (n + 1)) || ws.get(W::kICount, sizeof(uint32_t) * (n + 1)) ||
+      ws.get(W::kIStart, sizeof(uint64_t) * (n + 2)) || ws.get(W::kIScratch, sizeof(uint32_t) * (cap + 1)) ||
+      ws.get(W::kIOut, sizeof(uint32_t) * (cap + 1)) || ws.get(W::kScanTmp2, tmp + 16))
+    return -2;
+  uint64_t *mstart = (uint64_t *)ws.ptr(W::kIMStart);
+  uint32_t *scratch = (uint32_t *)ws.ptr(W::kIScratch);
+  o.icount = (uint32_t *)ws.ptr(W::kICount);
+  o.istart = (uint64_t *)ws.ptr(W::kIStart);
+  o.iout = (uint32_t *)ws.ptr(W::kIOut);
+  GUARD(o, kNeedIdent | kOIOut, n, "k_ident (early)");
+  unsigned long long *ovf = (unsigned long long *)(o.istart + n + 1);
+  HIP_TRY(hipEventRecord(ws.ev_fork, st));
+  HIP_TRY(hipStreamWaitEvent(ws.side, ws.ev_fork, 0));
+  hipStream_t sd = ws.side;
+  HIP_TRY(hipMemsetAsync(ovf, 0, sizeof(uint64_t), sd));
+  if (scan_offsets(ws, o.mcount, mstart, n, sd, W::kScanTmp2)) return -3;
+  const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + 31) / 32, 8192));
+  if (n > 0) {
+    hipLaunchKernelGGL(k_ident, dim3(blocks), dim3(256), 0, sd, s, o, n, mstart, scratch, cap, ovf);
+    HIP_TRY(hipGetLastError());
+  }
+  if (scan_offsets(ws, o.icount, o.istart, n, sd, W::kScanTmp2)) return -3;
+  if (n > 0) {
+    hipLaunchKernelGGL(k_ident_pack, dim3(std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, 16384))), dim3(256),
+                       0, sd, o, n, mstart, scratch, cap, ovf);
+    HIP_TRY(hipGetLastError());
+  }
+  HIP_TRY(hipMemcpyAsync(hp + 8, o.istart + n, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, sd));
+  HIP_TRY(hipMemcpyAsync(hp + 10, mstart + n, sizeof(uint64_t), hipMemcpyDeviceToHost, sd));
+  HIP_TRY(hipEventRecord(ws.ev_join, sd));
+  return 0;
 }
 
 int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes, const uint64_t *d_offs, uint32_t n,
@@ -2405,6 +2492,8 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
   }
   HIP_TRY(hipGetLastError());
   mark(ws, 1, st);
+  ws.ident_ready = false;
+  if (ws.ident_early && !ws.runs && ident_launch(s, ws, o, n, st) == 0) ws.ident_ready = true;
   // segment starts: exclusive scans of S (raw entries, an upper bound of a
   // topic's deliveries) and H (shared candidates); the solo descriptors'
   // positions: exclusive scan of the solo-part counts
@@ -2625,6 +2714,9 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
     HIP_TRY(hipGetLastError());
   }
   mark(ws, 3, st);
+  // the identifiers pass beside the match: joined here, so the read-back's
+  // synchronisation covers it (and the next call's buffers wait for it)
+  if (ws.ident_ready) HIP_TRY(hipStreamWaitEvent(st, ws.ev_join, 0));
   // totals for the caller: sums of the counts, then the one read-back
   {
     size_t tmp = 0;
@@ -2766,6 +2858,20 @@ int identifiers_device(const DeviceSnapshot &s, Workspace &ws, hipStream_t st, I
   using W = Workspace;
   const uint32_t n = ws.last_n;
   if (!ws.last_valid) return -1;
+  if (ws.ident_ready) {  // computed beside the match (ident_launch; the collect synchronised the join)
+    ws.ident_ready = false;
+    const uint64_t *hp = ws.pinned_u64();
+    const uint64_t total = hp[8], ovf = hp[9], n_multi = hp[10];
+    ws.ident_cap = std::max<uint64_t>(ws.ident_cap, n_multi + n_multi / 4 + 1024);
+    if (!ovf && ws.last_n_dfs == 0 && !ws.last_runs) {
+      out->n_topics = n;
+      out->n_idents = total;
+      out->offsets = (const uint64_t *)ws.ptr(W::kIStart);
+      out->sids = (const uint32_t *)ws.ptr(W::kIOut);
+      return 0;
+    }
+    // (a capacity passed, or DFS topics, whose sids k_dfs<3|4> list: the pass again, below)
+  }
   Outputs o{};
   o.cls = (uint8_t *)ws.ptr(W::kCls);
   o.recs = (uint32_t *)ws.ptr(W::kRecs);
@@ -2796,7 +2902,8 @@ int identifiers_device(const DeviceSnapshot &s, Workspace &ws, hipStream_t st, I
   if (ws.get(W::kIScratch, sizeof(uint32_t) * (n_multi + 1))) return -2;
   uint32_t *scratch = (uint32_t *)ws.ptr(W::kIScratch);
   if (n > 0) {
-    hipLaunchKernelGGL(k_ident, dim3(blocks), dim3(256), 0, st, s, o, n, mstart, scratch);
+    hipLaunchKernelGGL(k_ident, dim3(blocks), dim3(256), 0, st, s, o, n, mstart, scratch, ~0ull,
+                       (unsigned long long *)nullptr);
     HIP_TRY(hipGetLastError());
     if (ws.last_n_dfs) {
       hipLaunchKernelGGL(k_dfs<3>, dim3(fb_blocks), dim3(kWave), fb_lds, st, s, ws.last_bytes, ws.last_offs, o,
@@ -2813,7 +2920,7 @@ int identifiers_device(const DeviceSnapshot &s, Workspace &ws, hipStream_t st, I
   GUARD(o, kNeedIdent | kOIOut, n, "k_ident_pack");
   if (n > 0 && total > 0) {
     hipLaunchKernelGGL(k_ident_pack, dim3(std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, 16384))), dim3(256),
-                       0, st, o, n, mstart, scratch, total);
+                       0, st, o, n, mstart, scratch, total, (unsigned long long *)nullptr);
     HIP_TRY(hipGetLastError());
     if (ws.last_n_dfs) {
       hipLaunchKernelGGL(k_dfs<4>, dim3(fb_blocks), dim3(kWave), fb_lds, st, s, ws.last_bytes, ws.last_offs, o,

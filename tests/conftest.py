@@ -17,8 +17,11 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
 
 
-def _make(subdir, target):
-    if not os.path.exists(os.path.join(ROOT, target)):
+def _make(subdir, target, always=False):
+    # (always: small harnesses compiled against the library's headers — make
+    # rebuilds them when a header they include changed, e.g. the Workspace
+    # layout guard_test fills in)
+    if always or not os.path.exists(os.path.join(ROOT, target)):
         subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, subdir)])
 
 
@@ -27,7 +30,7 @@ _make("tools", "tools/_build/libmqgen.so")
 _make("maxmq_amd/csrc", "maxmq_amd/_lib/libmqmatch.so")
 _make("tests/harness", "tests/harness/_build/shim_harness")
 _make("tests/harness", "tests/harness/_build/churn_harness")
-_make("tests/harness", "tests/harness/_build/guard_test")
+_make("tests/harness", "tests/harness/_build/guard_test", always=True)
 _make("tests/harness", "tests/harness/_build/tok_test")
 
 
