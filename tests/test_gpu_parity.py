@@ -373,6 +373,52 @@ def test_identifiers_dfs_topics_and_device_form(monkeypatch):
     assert d.n_topics == len(topics) and d.n_idents == int(res.ident_offsets[-1])
 
 
+@pytest.mark.parametrize("config,overrides", [(3, dict(n_filters=40000, n_topics=30000)),
+                                              (4, dict(n_filters=30000, n_topics=20000))])
+def test_identifiers_beside_the_match_equal_after(config, overrides):
+    """mqm_identifiers_early: the identifiers pass forked onto a side stream
+    after the walk (overlapping the merges) lists exactly what the pass run
+    after the match lists — offsets and sids, byte for byte — over several
+    batches (the capacity it sizes from the last call grows in between), and
+    the host path of an MQM_CFG_IDENTIFIERS index (which always runs it
+    beside the match) still equals the oracle's maps."""
+    import torch
+
+    from maxmq_amd.devbuf import dev_view_copy
+
+    w = mqgen.generate(config, **overrides)
+    idx = maxmq_amd.TopicsIndex(0, identifiers=True)
+    idx.subscribe_workload(w)
+    idx.commit()
+    dev = torch.device("cuda", 0)
+    s = w.topics
+    tb = torch.from_numpy(s.data).to(dev)
+    to = torch.from_numpy(s.offs.view(np.int64)).to(dev)
+    n = len(s)
+
+    def run(early):
+        idx.identifiers_early(early)
+        idx.match_device(tb.data_ptr(), to.data_ptr(), n)
+        d = idx.identifiers_device()
+        offs = dev_view_copy(d.offsets, n + 1, torch.int64, dev).cpu().numpy()
+        sids = dev_view_copy(d.sids, max(int(d.n_idents), 1), torch.int32, dev).cpu().numpy()[:int(d.n_idents)]
+        torch.cuda.synchronize()
+        return int(d.n_idents), offs, sids
+
+    late = run(False)
+    for _ in range(3):
+        early = run(True)
+        assert early[0] == late[0] and np.array_equal(early[1], late[1]) and np.array_equal(early[2], late[2])
+    idx.identifiers_early(False)
+    assert late[0] > 0
+    ora = OracleIndex()
+    ora.subscribe_workload(w)
+    k = min(n, 4000)
+    res = idx.match_batch(s.data[: int(s.offs[k])], s.offs[: k + 1])
+    assert_same(canon_gpu_idents(res), canon_oracle_idents(*ora.identifiers(s.data[: int(s.offs[k])], s.offs[: k + 1])),
+                "identifiers")
+
+
 # ---- subscriber-sharded node result (SURVEY §8e): mqm_dense_device + mqm_gather_shards ----------
 
 @pytest.mark.parametrize("n_shards", [1, 3, 4])
