@@ -904,6 +904,12 @@ struct alignas(16) WinLds {
   uint32_t blk[kWin / kWave];
 };
 
+// kVec (MQM_WINCOPY_VEC=1, A/B): each lane moves 4 consecutive positions at
+// a time — one 16-B load and one 16-B store when one descriptor covers all
+// four (a quarter of the memory instructions), position by position at part
+// boundaries
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+template <bool kVec = false>
 __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_eu(8))) void k_wincopy(
     DeviceSnapshot s, const uint4 *__restrict__ desc, const uint64_t *__restrict__ nd_ptr, uint64_t desc_cap,
     const uint32_t *__restrict__ win, uint64_t win_cap, const uint64_t *__restrict__ total_ptr,
@@ -947,7 +953,63 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
       }
       wave_lds_sync();
       const uint32_t q0 = (uint32_t)(pos - g0), q1 = (uint32_t)(bend - g0);
-      for (uint32_t base = q0; base < q1; base += kWave * kCU) {
+      auto desc_of = [&](uint32_t q) {  // the last descriptor starting at or before q (q < kWin)
+        const uint32_t bq = q / kWave;
+        uint32_t k = L.blk[bq], left = (bq + 1 < kWin / kWave ? L.blk[bq + 1] : kWave - 1) - k;
+        while (left > 0) {
+          const uint32_t half = (left + 1) / 2;
+          if (L.st[k + half] <= q) {
+            k += half;
+            left -= half;
+          } else {
+            left = half - 1;
+          }
+        }
+        return k;
+      };
+      if (kVec) {
+        constexpr int kU = 4;  // units of 4 positions per lane per step
+        for (uint32_t base = q0 & ~3u; base < q1; base += kWave * 4 * kU) {
+          uint32_t qa[kU], sa[kU];
+          bool full[kU];
+#pragma unroll
+          for (int u = 0; u < kU; u++) {
+            const uint32_t q = base + (u * kWave + lane) * 4;
+            const uint32_t k = desc_of(min(q, (uint32_t)kWin - 1));
+            full[u] = q >= q0 && q + 4 <= q1 && q >= L.st[k] && q + 4 <= L.en[k];
+            qa[u] = q;
+            sa[u] = full[u] ? L.src[k] + (q - L.st[k]) : 0u;
+          }
+          u32x4 vv[kU];
+#pragma unroll
+          for (int u = 0; u < kU; u++) vv[u] = __builtin_amdgcn_raw_buffer_load_b128(words, (int)(sa[u] * 4u), 0, 0);
+#pragma unroll
+          for (int u = 0; u < kU; u++) {
+            const uint32_t q = qa[u];
+            if (full[u]) {
+              const uint64_t p = g0 + q;
+              if (p + 4 <= cap)
+                *reinterpret_cast<uint4 *>(out + p) = make_uint4(vv[u].x, vv[u].y, vv[u].z, vv[u].w);
+              else
+                atomicOr(oob, kOobStore);
+              continue;
+            }
+            for (uint32_t r = 0; r < 4; r++) {  // a part boundary or the batch's ends inside the unit
+              const uint32_t qr = q + r;
+              if (qr < q0 || qr >= q1) continue;
+              const uint32_t k = desc_of(qr);
+              if (qr < L.st[k] || qr >= L.en[k]) continue;
+              const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(words, (int)((L.src[k] + (qr - L.st[k])) * 4u), 0, 0);
+              const uint64_t p = g0 + qr;
+              if (p < cap)
+                out[p] = v;
+              else
+                atomicOr(oob, kOobStore);
+            }
+          }
+        }
+      }
+      for (uint32_t base = q0; !kVec && base < q1; base += kWave * kCU) {
         uint32_t sa[kCU];
         bool in[kCU];
 #pragma unroll
@@ -1466,6 +1528,11 @@ __global__ __launch_bounds__(kBigThreads) void k_multi_part(DeviceSnapshot s, Ou
 static bool walk_slots() { return slots_enabled(); }
 static bool desc_copy_on() {
   static const bool v = getenv("MQM_DESC_COPY") && atoi(getenv("MQM_DESC_COPY")) != 0;
+  return v;
+}
+// MQM_WINCOPY_VEC=1: the window copy moves 4 positions per lane at a time (A/B)
+static bool wincopy_vec() {
+  static const bool v = getenv("MQM_WINCOPY_VEC") && atoi(getenv("MQM_WINCOPY_VEC")) != 0;
   return v;
 }
 // MQM_LONG_PART=m: solo parts of at least m entries take k_longcopy (A/B; off
@@ -2693,8 +2760,12 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
                            dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nd_grid + 255) / 256, 8192))),
                            dim3(256), 0, st, desc, desc_start + n, desc_cap, o.dstart + n, win, win_cap, &o.ctr->oob);
         HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(k_wincopy, grid(k_wincopy), dim3(kWave * kEmitWaves), 0, st, s, desc, desc_start + n,
-                           desc_cap, win, win_cap, o.dstart + n, o.dout, o.dcap, &o.ctr->oob);
+        if (wincopy_vec())
+          hipLaunchKernelGGL(k_wincopy<true>, grid(k_wincopy<true>), dim3(kWave * kEmitWaves), 0, st, s, desc,
+                             desc_start + n, desc_cap, win, win_cap, o.dstart + n, o.dout, o.dcap, &o.ctr->oob);
+        else
+          hipLaunchKernelGGL(k_wincopy<false>, grid(k_wincopy<false>), dim3(kWave * kEmitWaves), 0, st, s, desc,
+                             desc_start + n, desc_cap, win, win_cap, o.dstart + n, o.dout, o.dcap, &o.ctr->oob);
         HIP_TRY(hipGetLastError());
       }
     }

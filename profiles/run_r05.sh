@@ -10,6 +10,7 @@
 #   node    : the sharded node step with two rank processes and the HIP matcher (tests/test_gpu_node_step.py)
 #   churnserve: the churn workload with the served-calls-under-churn legs (one per rebuild thread count)
 #   edges   : the device-built edge table equals the host's (digests), async commits on the GPU
+#   vecab   : the 4-positions-per-lane window copy (MQM_WINCOPY_VEC=1): parity subset, then C3 / C4 shard A/B
 #   ident   : the Identifiers parity tests (batch, DFS, runs, batching collector)
 #   c4test  : the C4 shard 0/8 full-batch test            -> gpurun_out/TAG/pytest_c4.log
 #   ret     : the retained (reverse-match) tests           -> gpurun_out/TAG/pytest_ret.log
@@ -75,6 +76,14 @@ for step in "$@"; do
              > $OUT/pytest_edges.log 2>&1 ;;
     churndiag) timeout -k 10 520 python3 -u bench.py --workload churn --steps 2 --warmup 1 --serve-churn-s 12 \
              --churn-build-threads 4,16,-1 > $OUT/bench_churn.json 2> $OUT/bench_churn.log ;;
+    vecab) MQM_WINCOPY_VEC=1 timeout -k 10 500 $PYT tests/test_gpu_parity.py tests/test_gpu_fast.py -m gpu --timeout 300 \
+             -k "config_vs_oracle or edge_cases or full_size_c3 or kat" > $OUT/pytest_vec.log 2>&1 &&
+           for V in base:X=0 vec:MQM_WINCOPY_VEC=1; do
+             N=${V%%:*}; E=${V#*:}
+             env $E timeout -k 10 400 python3 -u bench.py $FAST --ident-steps 0 > $OUT/bench_fast_$N.json 2> $OUT/bench_fast_$N.log || exit 1
+             env $E timeout -k 10 600 python3 -u bench.py --config 4 --shard 0/8 $FAST --ident-steps 0 > $OUT/bench_c4_$N.json \
+               2> $OUT/bench_c4_$N.log || exit 1
+           done ;;
     ident) timeout -k 10 500 $PYT tests/test_gpu_parity.py tests/test_gpu_runs.py tests/test_gpu_batching.py -m gpu \
              --timeout 200 -k "ident or batched" > $OUT/pytest_ident.log 2>&1 ;;
     c4test) timeout -k 10 600 $PYT tests/test_gpu_c4_shard.py -m gpu --timeout 500 > $OUT/pytest_c4.log 2>&1 ;;
