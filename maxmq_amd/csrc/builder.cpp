@@ -29,16 +29,22 @@ DeltaLog::Op &DeltaLog::push(Kind k, std::string_view a, std::string_view b) {
 }
 
 void DeltaLog::subscribe(std::string_view client, std::string_view filter, uint8_t qos, uint8_t no_local,
-                         uint8_t rap, uint8_t rh, int32_t ident) {
+                         uint8_t rap, uint8_t rh, int32_t ident, const Store::Footprint *fp) {
   Op &op = push(kSub, client, filter);
   op.qos = qos;
   op.no_local = no_local;
   op.rap = rap;
   op.rh = rh;
   op.ident = ident;
+  if (fp) op.fp = *fp;
+  fast_ += !op.fp.structural;
 }
 
-void DeltaLog::unsubscribe(std::string_view filter, std::string_view client) { push(kUnsub, filter, client); }
+void DeltaLog::unsubscribe(std::string_view filter, std::string_view client, const Store::Footprint *fp) {
+  Op &op = push(kUnsub, filter, client);
+  if (fp) op.fp = *fp;
+  fast_ += !op.fp.structural;
+}
 
 void DeltaLog::retain(std::string_view topic, uint64_t msg_ref, uint32_t payload_len, bool retain_flag) {
   Op &op = push(kRetain, topic, std::string_view());
@@ -54,10 +60,16 @@ void DeltaLog::replay(Store &st, size_t limit) const {
     const std::string_view a(base + op.a_off, op.a_len), b(base + op.a_off + op.a_len, op.b_len);
     switch (op.kind) {
       case kSub:
-        st.subscribe(a, b, op.qos, op.no_local, op.rap, op.rh, op.ident);
+        if (!op.fp.structural)
+          st.subscribe_at(op.fp, op.qos, op.no_local, op.rap, op.rh, op.ident);
+        else
+          st.subscribe(a, b, op.qos, op.no_local, op.rap, op.rh, op.ident);
         break;
       case kUnsub:
-        st.unsubscribe(a, b);
+        if (!op.fp.structural)
+          st.unsubscribe_at(op.fp);
+        else
+          st.unsubscribe(a, b);
         break;
       default:
         st.retain_message(a, op.msg_ref, op.payload_len, op.retain_flag != 0);
@@ -70,6 +82,7 @@ void DeltaLog::append(DeltaLog &&o) {
   if (ops_.empty()) {
     ops_.swap(o.ops_);
     bytes_.swap(o.bytes_);
+    fast_ = o.fast_;
     o.clear();
     return;
   }
@@ -82,6 +95,7 @@ void DeltaLog::append(DeltaLog &&o) {
     op.a_off += shift;
     ops_.push_back(op);
   }
+  fast_ += o.fast_;
   o.clear();
 }
 

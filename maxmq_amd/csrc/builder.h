@@ -32,9 +32,13 @@ namespace mqm {
 // Store mutations in call order; strings packed into one arena.
 class DeltaLog {
  public:
+  // fp: the authoritative store's footprint of the call just made
+  // (Store::last_footprint); a call that was not structural is replayed on its
+  // node directly (no path walk, no interning)
   void subscribe(std::string_view client, std::string_view filter, uint8_t qos, uint8_t no_local, uint8_t rap,
-                 uint8_t rh, int32_t ident);
-  void unsubscribe(std::string_view filter, std::string_view client);
+                 uint8_t rh, int32_t ident, const Store::Footprint *fp = nullptr);
+  void unsubscribe(std::string_view filter, std::string_view client, const Store::Footprint *fp = nullptr);
+  uint64_t fast_ops() const { return fast_; }  // calls recorded with a usable footprint (statistics)
   void retain(std::string_view topic, uint64_t msg_ref, uint32_t payload_len, bool retain_flag);
   // re-run the first `limit` recorded calls on st, in order
   void replay(Store &st, size_t limit = SIZE_MAX) const;
@@ -44,6 +48,7 @@ class DeltaLog {
   void clear() {
     ops_.clear();
     bytes_.clear();
+    fast_ = 0;
   }
 
  private:
@@ -55,10 +60,12 @@ class DeltaLog {
     uint32_t a_len, b_len;  // strings at bytes_[a_off ..), then b
     uint64_t a_off;
     uint64_t msg_ref;
+    Store::Footprint fp;    // fp.structural: replay by the strings
   };
   Op &push(Kind k, std::string_view a, std::string_view b);
   std::vector<Op> ops_;
   std::vector<char> bytes_;
+  uint64_t fast_ = 0;
 };
 
 // A snapshot ready to be published: device copy (or host-only when the index

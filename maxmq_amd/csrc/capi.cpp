@@ -651,7 +651,8 @@ int mqm_subscribe(mqm_index *h, const char *client, size_t client_len, const cha
                                 sub->retain_as_published, sub->retain_handling, sub->identifier);
     if (h->async()) {
       h->journal.subscribe(sv(client, client_len), sv(filter, filter_len), sub->qos, sub->no_local,
-                           sub->retain_as_published, sub->retain_handling, sub->identifier);
+                           sub->retain_as_published, sub->retain_handling, sub->identifier,
+                           &h->store.last_footprint());
       maybe_submit(h);
     }
     if (is_new) *is_new = n ? 1 : 0;
@@ -672,7 +673,9 @@ int mqm_subscribe_many(mqm_index *h, size_t n, const char *client_bytes, const u
       const auto c = sv(client_bytes + client_offs[i], client_offs[i + 1] - client_offs[i]);
       const auto f = sv(filter_bytes + filter_offs[i], filter_offs[i + 1] - filter_offs[i]);
       bool r = h->store.subscribe(c, f, s.qos, s.no_local, s.retain_as_published, s.retain_handling, s.identifier);
-      if (h->async()) h->journal.subscribe(c, f, s.qos, s.no_local, s.retain_as_published, s.retain_handling, s.identifier);
+      if (h->async())
+        h->journal.subscribe(c, f, s.qos, s.no_local, s.retain_as_published, s.retain_handling, s.identifier,
+                             &h->store.last_footprint());
       if (is_new) is_new[i] = r ? 1 : 0;
     }
     maybe_submit(h);
@@ -687,7 +690,7 @@ int mqm_unsubscribe(mqm_index *h, const char *filter, size_t filter_len, const c
     std::lock_guard<std::mutex> g(h->mu);
     bool r = h->store.unsubscribe(sv(filter, filter_len), sv(client, client_len));
     if (r && h->async()) {  // false: no node, nothing changed (topics.go:334-336)
-      h->journal.unsubscribe(sv(filter, filter_len), sv(client, client_len));
+      h->journal.unsubscribe(sv(filter, filter_len), sv(client, client_len), &h->store.last_footprint());
       maybe_submit(h);
     }
     if (existed) *existed = r ? 1 : 0;
@@ -726,7 +729,7 @@ int mqm_unsubscribe_many(mqm_index *h, size_t n, const char *filter_bytes, const
       const auto f = sv(filter_bytes + filter_offs[i], filter_offs[i + 1] - filter_offs[i]);
       const auto c = sv(client_bytes + client_offs[i], client_offs[i + 1] - client_offs[i]);
       bool r = h->store.unsubscribe(f, c);
-      if (r && h->async()) h->journal.unsubscribe(f, c);
+      if (r && h->async()) h->journal.unsubscribe(f, c, &h->store.last_footprint());
       if (existed) existed[i] = r ? 1 : 0;
     }
     maybe_submit(h);

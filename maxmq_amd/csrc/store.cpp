@@ -290,6 +290,8 @@ void Store::trim(uint32_t id) {
 
 bool Store::subscribe(std::string_view client, std::string_view filter, uint8_t qos, uint8_t no_local, uint8_t rap,
                       uint8_t rh, int32_t ident) {
+  const uint64_t mark0 = shape_mark();
+  last_ = Footprint();
   SubRec rec;
   rec.client = clients_.intern(client);
   rec.filter = filters_.intern(filter);
@@ -306,6 +308,7 @@ bool Store::subscribe(std::string_view client, std::string_view filter, uint8_t 
     isolate_particle(filter, 1, &group);
     uint32_t gtok = tokens_.intern(group);
     uint32_t n = set_path(filter, 2);
+    last_ = Footprint{n, rec.client, rec.filter, gtok, true, shape_mark() != mark0};
     for (auto &s : nodes_[n].shared)
       if (s.group == gtok && s.sub.client == rec.client) {
         s.sub = rec;
@@ -315,6 +318,7 @@ bool Store::subscribe(std::string_view client, std::string_view filter, uint8_t 
     return true;
   }
   uint32_t n = set_path(filter, 0);
+  last_ = Footprint{n, rec.client, rec.filter, 0xFFFFFFFFu, false, shape_mark() != mark0};
   auto &subs = nodes_[n].subs;
   // hub nodes can hold many subscribers: keep them sorted by client
   auto it = std::lower_bound(subs.begin(), subs.end(), rec.client,
@@ -329,19 +333,35 @@ bool Store::subscribe(std::string_view client, std::string_view filter, uint8_t 
 
 bool Store::unsubscribe(std::string_view filter, std::string_view client) {
   int d = filter.substr(0, 6) == "$SHARE" ? 2 : 0;  // strings.HasPrefix: case-sensitive (topics.go:330)
+  last_ = Footprint();
   uint32_t n = seek_path(filter, d);
   if (n == kNone) return false;
+  const uint64_t mark0 = shape_mark();
   version_.v.fetch_add(1, std::memory_order_release);
   uint32_t cid = clients_.find(client);
   std::string_view prefix;
   isolate_particle(filter, 0, &prefix);
+  Footprint fp{n, cid, kNone, kNone, false, false};
   if (equal_fold_share(prefix)) {
     std::string_view group;
     isolate_particle(filter, 1, &group);
-    uint32_t gtok = tokens_.find(group);
+    fp.shared = true;
+    fp.group = tokens_.find(group);
+  }
+  drop_sub(fp);
+  trim(n);
+  fp.structural = shape_mark() != mark0;
+  last_ = fp;
+  return true;  // true whenever the node exists (topics.go:347-348)
+}
+
+// the list change of an unsubscribe at its node (unsubscribe, unsubscribe_at)
+void Store::drop_sub(const Footprint &fp) {
+  const uint32_t n = fp.node, cid = fp.client;
+  if (fp.shared) {
     auto &sh = nodes_[n].shared;
     for (size_t i = 0; i < sh.size(); i++)
-      if (sh[i].group == gtok && sh[i].sub.client == cid) {
+      if (sh[i].group == fp.group && sh[i].sub.client == cid) {
         sh.erase(sh.begin() + (std::ptrdiff_t)i);
         break;
       }
@@ -351,8 +371,46 @@ bool Store::unsubscribe(std::string_view filter, std::string_view client) {
                                [](const SubRec &a, uint32_t c) { return a.client < c; });
     if (it != subs.end() && it->client == cid) subs.erase(it);
   }
-  trim(n);
-  return true;  // true whenever the node exists (topics.go:347-348)
+}
+
+bool Store::subscribe_at(const Footprint &fp, uint8_t qos, uint8_t no_local, uint8_t rap, uint8_t rh,
+                         int32_t ident) {
+  SubRec rec;
+  rec.client = fp.client;
+  rec.filter = fp.filter;
+  rec.ident = ident;
+  rec.qos = qos;
+  rec.no_local = no_local;
+  rec.rap = rap;
+  rec.rh = rh;
+  version_.v.fetch_add(1, std::memory_order_release);
+  last_ = fp;
+  const uint32_t n = fp.node;
+  if (fp.shared) {
+    for (auto &s : nodes_[n].shared)
+      if (s.group == fp.group && s.sub.client == rec.client) {
+        s.sub = rec;
+        return false;
+      }
+    nodes_[n].shared.push_back(SharedRec{fp.group, rec});
+    return true;
+  }
+  auto &subs = nodes_[n].subs;
+  auto it = std::lower_bound(subs.begin(), subs.end(), rec.client,
+                             [](const SubRec &a, uint32_t c) { return a.client < c; });
+  if (it != subs.end() && it->client == rec.client) {
+    *it = rec;
+    return false;
+  }
+  subs.insert(it, rec);
+  return true;
+}
+
+void Store::unsubscribe_at(const Footprint &fp) {
+  version_.v.fetch_add(1, std::memory_order_release);
+  last_ = fp;
+  drop_sub(fp);
+  trim(fp.node);  // (removes nothing: the call was not structural)
 }
 
 int64_t Store::retain_message(std::string_view topic, uint64_t msg_ref, uint32_t payload_len, bool retain_flag) {

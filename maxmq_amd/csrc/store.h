@@ -98,6 +98,20 @@ class Store {
   bool subscribe(std::string_view client, std::string_view filter, uint8_t qos, uint8_t no_local, uint8_t rap,
                  uint8_t rh, int32_t ident);                                   // topics.go:303-321
   bool unsubscribe(std::string_view filter, std::string_view client);         // topics.go:325-349
+  // What the last subscribe / unsubscribe touched: its node, the client's,
+  // filter's and share group's interned ids, whether it was a shared
+  // subscription, and whether it changed anything but that node's lists (a
+  // node created or removed, a string interned for the first time).  A store
+  // replaying the same calls in the same order (the builder's shadow) holds
+  // the same ids, so a call that was not `structural` can be replayed on the
+  // node directly (subscribe_at / unsubscribe_at) instead of walking the path.
+  struct Footprint {
+    uint32_t node = 0xFFFFFFFFu, client = 0xFFFFFFFFu, filter = 0xFFFFFFFFu, group = 0xFFFFFFFFu;
+    bool shared = false, structural = true;
+  };
+  const Footprint &last_footprint() const { return last_; }
+  bool subscribe_at(const Footprint &fp, uint8_t qos, uint8_t no_local, uint8_t rap, uint8_t rh, int32_t ident);
+  void unsubscribe_at(const Footprint &fp);
   int64_t retain_message(std::string_view topic, uint64_t msg_ref, uint32_t payload_len,
                          bool retain_flag);                                    // topics.go:354-377
   uint64_t retained_len() const { return retained_.size(); }
@@ -120,11 +134,17 @@ class Store {
   uint32_t set_path(std::string_view s, int d);          // set  (topics.go:380-397)
   uint32_t seek_path(std::string_view s, int d) const;   // seek (topics.go:400-414)
   void trim(uint32_t n);                                 // trim (topics.go:417-423)
+  void drop_sub(const Footprint &fp);
   uint32_t new_node(uint32_t parent, uint32_t tok);
   void unlink(uint32_t n);
 
   std::vector<HNode> nodes_;
   uint64_t structure_version_ = 0;
+  Footprint last_;
+  // sizes that a structural call moves (Footprint::structural)
+  uint64_t shape_mark() const {
+    return structure_version_ + tokens_.size() + clients_.size() + filters_.size();
+  }
   std::vector<uint32_t> free_;
   EdgeMap children_;
   Interner tokens_, clients_, filters_;
