@@ -233,10 +233,50 @@ std::string_view sv(const char *p, size_t n) { return std::string_view(p ? p : "
 int hip_rc(int rc) { return rc == -2 ? MQM_ENOMEM : rc == -1 ? MQM_EINVAL : rc < 0 ? MQM_EHIP : rc; }
 
 // make g the front buffer; readers that hold the old one keep it alive
+// Snapshot references dropped on a latency path (a publish, a server
+// relaunch, a served result freed) are handed to this thread, so the last one
+// — which frees gigabytes of host arrays (HostSnapshot) and retires the device
+// buffers — is never dropped by a caller, let alone under the index's or the
+// server's lock (r05: served calls paused ~0.2 s around each publish).
+struct Releaser {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<std::shared_ptr<const void>> q;
+  Releaser() {
+    std::thread([this] {
+      for (;;) {
+        std::vector<std::shared_ptr<const void>> batch;
+        {
+          std::unique_lock<std::mutex> g(mu);
+          cv.wait(g, [this] { return !q.empty(); });
+          batch.swap(q);
+        }
+        batch.clear();  // (the last references: the destructors run here)
+      }
+    }).detach();
+  }
+};
+void defer_release(std::shared_ptr<const void> p) {
+  // (only a reference that looks like the last one goes to the thread: a
+  // served call's own reference to a live snapshot is dropped here, no lock)
+  if (!p || p.use_count() > 1) return;
+  static auto *r = new Releaser;  // (never destroyed, like its thread)
+  {
+    std::lock_guard<std::mutex> g(r->mu);
+    r->q.push_back(std::move(p));
+  }
+  r->cv.notify_one();
+}
+
 int install(mqm_index *h, std::shared_ptr<GpuSnapshot> g, uint64_t version) {
-  std::unique_lock<std::shared_mutex> w(h->snap_rw);
-  h->snap = std::move(g);
-  h->snap_version = version;
+  std::shared_ptr<GpuSnapshot> old;
+  {
+    std::unique_lock<std::shared_mutex> w(h->snap_rw);
+    old = std::move(h->snap);
+    h->snap = std::move(g);
+    h->snap_version = version;
+  }
+  defer_release(std::move(old));
   return MQM_OK;
 }
 
@@ -1663,6 +1703,7 @@ struct Server {
     TraceSpan ts("ensure");
     halt();
     ts.mark("halt");
+    defer_release(std::move(snap));  // (the launch that read it has stopped)
     snap = std::move(want);
     ts.mark("snapshot switch");
     if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
@@ -1685,6 +1726,7 @@ struct Server {
       std::lock_guard<std::mutex> g(hist_mu);
       const uint32_t last = (hist_next + kHist - 1) % kHist;
       if (!hist[last] || hist[last]->version != ver) {
+        defer_release(std::move(hist[hist_next]));  // (the evicted host snapshot, if this was its last holder)
         hist[hist_next] = snap->host;
         hist_next = (hist_next + 1) % kHist;
       }
@@ -1731,6 +1773,10 @@ struct Server {
     using clk = std::chrono::steady_clock;
     const auto t_in = clk::now();
     std::shared_ptr<GpuSnapshot> cur;
+    struct DeferCur {  // the caller's reference is dropped on the releaser thread
+      std::shared_ptr<GpuSnapshot> &p;
+      ~DeferCur() { defer_release(std::move(p)); }
+    } defer_cur{cur};
     int rc = front_fast(h, &cur) ? MQM_OK : front(h, &cur);  // (commits first with MQM_CFG_AUTOCOMMIT)
     if (rc != MQM_OK) return rc;
     const auto t_front = clk::now();
@@ -2177,7 +2223,11 @@ int mqm_result_sub_infos(const mqm_result *r, int shared, const uint32_t *subs, 
   return MQM_OK;
 }
 
-void mqm_result_free(mqm_result *r) { delete r; }
+void mqm_result_free(mqm_result *r) {
+  if (!r) return;
+  defer_release(std::move(r->snap));  // (a served result may hold the last reference to its host snapshot)
+  delete r;
+}
 
 static int copy_name(std::string_view s, char *buf, size_t cap, size_t *len) {
   if (len) *len = s.size();
