@@ -31,6 +31,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <shared_mutex>
 #include <new>
 #include <string_view>
@@ -1562,9 +1563,11 @@ struct Server {
   std::shared_ptr<const HostSnapshot> hist[kHist];
   uint32_t hist_next = 0;
   std::atomic<uint64_t> ticket{0};
+  std::mutex np_mu;
+  std::set<uint64_t> never_posted;  // (np_mu) tickets whose caller gave up before posting (ensure skips them)
   std::unique_ptr<std::atomic<uint64_t>[]> free_seq;   // slot i takes request k once free_seq[i] == k
   std::unique_ptr<std::atomic<uint64_t>[]> abandoned;  // slot i: k + 1 of a posted request whose caller gave up
-  std::atomic<uint64_t> served{0}, fallbacks{0}, launches{0}, stale{0};
+  std::atomic<uint64_t> served{0}, fallbacks{0}, launches{0}, stale{0}, forced{0};
   std::atomic<uint64_t> device_ticks{0};  // claim -> publish on the device, summed (100 MHz ticks)
   std::atomic<uint64_t> phase_ticks[3] = {};  // stage + keys, walk, emission + publish
   std::atomic<uint64_t> timed{0};
@@ -1708,14 +1711,31 @@ struct Server {
     ts.mark("snapshot switch");
     if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
     // (no kernel runs now) the device counter restarts at the first request
-    // not yet served: a stopped kernel may have taken numbers past it
+    // not yet served: a stopped kernel may have taken numbers past it.  That
+    // is the oldest of (a) requests posted and not served, in any slot (also
+    // older than the last kServeSlots tickets: callers that gave up on a
+    // request while their slot stayed taken push the ticket counter on), and
+    // (b) the last kServeSlots tickets taken and not yet posted — except those
+    // whose caller gave up before posting (never_posted): a workgroup would
+    // wait on such a number until the next stop
     const uint64_t T = ticket.load(std::memory_order_acquire);
     unsigned long long c[2] = {T, 0};
-    for (uint64_t k = T > kServeSlots ? T - kServeSlots : 0; k < T; k++)
-      if (__atomic_load_n(&q->done[k % kServeSlots], __ATOMIC_ACQUIRE) < k + 1) {
-        c[0] = k;
-        break;
+    for (uint32_t i = 0; i < kServeSlots; i++) {
+      const unsigned long long p = __atomic_load_n(&q->slot[i].seq, __ATOMIC_ACQUIRE) & kServeSeqMask;
+      if (p && __atomic_load_n(&q->done[i], __ATOMIC_ACQUIRE) < p) c[0] = std::min<unsigned long long>(c[0], p - 1);
+    }
+    {
+      std::lock_guard<std::mutex> g(np_mu);
+      for (uint64_t k = T > kServeSlots ? T - kServeSlots : 0; k < T && k < c[0]; k++) {
+        const uint32_t i = (uint32_t)(k % kServeSlots);
+        const bool posted = (__atomic_load_n(&q->slot[i].seq, __ATOMIC_ACQUIRE) & kServeSeqMask) == k + 1;
+        if (!posted && __atomic_load_n(&q->done[i], __ATOMIC_ACQUIRE) < k + 1 && !never_posted.count(k)) {
+          c[0] = k;
+          break;
+        }
       }
+      while (!never_posted.empty() && *never_posted.begin() + 4 * kServeSlots < T) never_posted.erase(never_posted.begin());
+    }
     if (hipMemcpyAsync(ctr, c, sizeof(c), hipMemcpyHostToDevice, st) != hipSuccess) return MQM_EHIP;
     const uint64_t ver = snap->host->version;
     if (serve_launch(snap->dev, q, ctr, grid, idle_us, want_ids, ver, gen + 1, st) != 0) return MQM_EHIP;
@@ -1792,7 +1812,12 @@ struct Server {
     const uint32_t i = (uint32_t)(k % kServeSlots);
     if (!wait_slot(i, k)) {
       // (the slot's previous request never completed: the device is gone.
-      // Request k is never posted, so its slot stays taken as well)
+      // Request k is never posted, so its slot stays taken as well; the next
+      // relaunch skips its number)
+      {
+        std::lock_guard<std::mutex> g(np_mu);
+        never_posted.insert(k);
+      }
       fprintf(stderr,
               "mqmatch: per-publish server: ring slot %u not free after 10 s (request %llu; slot owner %llu, "
               "abandoned %llu, done %llu; ticket %llu, run_gen %llu, exited %llu, run_ver %llu)\n",
@@ -1872,6 +1897,15 @@ struct Server {
         if (now - t0 > std::chrono::microseconds(200) && now_ns - last > 200000 &&
             last_check_ns.compare_exchange_strong(last, now_ns, std::memory_order_acq_rel)) {
           std::lock_guard<std::mutex> g(mu);
+          // a request unserved for a second while the launch runs: its number
+          // was skipped or a workgroup waits on one never posted — stop and
+          // relaunch (the counter restarts at the oldest unserved request)
+          if (now - t0 > std::chrono::seconds(1) && launched && run_gen.load() == gen) {
+            forced++;
+            fprintf(stderr, "mqmatch: per-publish server: request %llu unserved for %.1f s, relaunching\n",
+                    (unsigned long long)k, std::chrono::duration<double>(now - t0).count());
+            halt();
+          }
           if ((rc = ensure(cur)) != MQM_OK) return give_up(rc);
         }
       }
