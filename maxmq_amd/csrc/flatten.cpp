@@ -100,7 +100,7 @@ struct Partners {
   std::vector<uint32_t> part;  // partner old sids
 };
 
-static void mark_multi(const Store &st, const std::vector<uint32_t> &order, HostSnapshot &hs, Partners &pt) {
+static void mark_multi(const Store &st, const U32Vec &order, HostSnapshot &hs, Partners &pt) {
   const auto &nodes = st.nodes();
   const uint32_t plus_tok = st.plus_token(), hash_tok = st.hash_token();
   const uint64_t nsub = hs.sub_info.size();
@@ -111,7 +111,8 @@ static void mark_multi(const Store &st, const std::vector<uint32_t> &order, Host
       for (uint32_t j = 0; j < hs.nodes[i].sub_cnt; j++) sub_node[hs.nodes[i].sub_off + j] = order[i];
   });
   const uint32_t nc = st.clients().size();
-  std::vector<uint32_t> cstart(nc + 2, 0), by_client(nsub);
+  std::vector<uint32_t> cstart(nc + 2, 0);
+  U32Vec by_client(nsub);
   for (uint64_t s = 0; s < nsub; s++) cstart[hs.subs[s].client + 2]++;
   for (uint32_t c = 0; c < nc; c++) cstart[c + 2] += cstart[c + 1];
   for (uint64_t s = 0; s < nsub; s++) by_client[cstart[hs.subs[s].client + 1]++] = (uint32_t)s;
@@ -178,7 +179,7 @@ static void mark_multi(const Store &st, const std::vector<uint32_t> &order, Host
 }
 
 // DeviceRetained arrays (snapshot.h) over the preorder ids
-static void build_retained(const Store &st, const std::vector<uint32_t> &order, const std::vector<uint32_t> &new_id,
+static void build_retained(const Store &st, const U32Vec &order, const U32Vec &new_id,
                            HostSnapshot &hs) {
   const auto &nodes = st.nodes();
   const uint64_t nn = order.size();
@@ -229,7 +230,7 @@ static void build_retained(const Store &st, const std::vector<uint32_t> &order, 
 // fixed depth, preorder orders children like their parents), then one table
 // slot per group.  Depends on nothing but the store: digests are reproducible.
 template <class Staged>
-static void build_reverse_index(const Store &st, const std::vector<uint32_t> &order, const Staged &staged,
+static void build_reverse_index(const Store &st, const U32Vec &order, const Staged &staged,
                                 HostSnapshot &hs) {
   const auto &nodes = st.nodes();
   const uint64_t ne = staged.size();
@@ -262,21 +263,22 @@ static void build_reverse_index(const Store &st, const std::vector<uint32_t> &or
   }
   struct GE {
     uint64_t g;
-    uint32_t e;
+    uint32_t e, parent;  // a group's edges by parent preorder (retained.hip inv_lower)
   };
   std::vector<GE, NoInitAlloc<GE>> tmp(ne);
   parallel_for(kC, [&](uint32_t c) {
     const uint64_t lo = ne * c / kC, hi = ne * (c + 1) / kC;
     for (uint64_t e = lo; e < hi; e++) {
       const uint64_t g = gkey(e);
-      tmp[cnt[(uint64_t)c * kB + bucket(g)]++] = GE{g, (uint32_t)e};
+      tmp[cnt[(uint64_t)c * kB + bucket(g)]++] = GE{g, (uint32_t)e, staged[e].parent};
     }
   });
   hs.rinv.resize(ne);
   std::vector<std::vector<RevGroup>> bg(kB);
   parallel_for(kB, [&](uint32_t b) {
-    std::stable_sort(tmp.begin() + bstart[b], tmp.begin() + bstart[b + 1],
-                     [](const GE &x, const GE &y) { return x.g < y.g; });
+    // (a parent has one child per key: (g, parent) is unique)
+    std::sort(tmp.begin() + bstart[b], tmp.begin() + bstart[b + 1],
+              [](const GE &x, const GE &y) { return x.g != y.g ? x.g < y.g : x.parent < y.parent; });
     for (uint64_t j = bstart[b]; j < bstart[b + 1]; j++) {
       const auto &ed = staged[tmp[j].e];
       hs.rinv[j] = uint2{ed.parent, ed.child};
@@ -382,32 +384,77 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
   FlattenCache local;
   FlattenCache &pre = reuse ? *cache : local;
   if (cache && !reuse) cache->valid = false;
-  std::vector<uint32_t> &new_id = pre.new_id, &order = pre.order, &pc_of = pre.pc_of, &hc_of = pre.hc_of,
+  U32Vec &new_id = pre.new_id, &order = pre.order, &pc_of = pre.pc_of, &hc_of = pre.hc_of,
                         &nlit = pre.nlit;
+  // literal children by parent (store ids), as offsets + list, in store-id
+  // order; set below when the shape is not kept, read by the preorder and the
+  // edge staging
+  U32Vec loff, lch, kch;  // (kch: lch's token ids)
   if (!reuse) {
-  // 1. preorder ids.  Visiting order at a node: literal children in child-list
-  //    order, then '+', then '#'.  Nodes above depth kTop are numbered
-  //    serially; the subtrees rooted at depth kTop are counted, then numbered
-  //    at their preorder base, in parallel.
-  constexpr uint32_t kTop = 2;
-  new_id.assign(nodes.size(), kNone);
-  // '+' / '#' children (store ids) and literal-child counts by preorder id
-  auto scan_children = [&](uint32_t n, uint32_t *pc, uint32_t *hc, std::vector<uint32_t> &lits) {
-    *pc = *hc = kNone;
-    lits.clear();
-    for (uint32_t c = nodes[n].first_child; c != kNone; c = nodes[c].next_sibling) {
-      if (nodes[c].key == plus_tok)
-        *pc = c;
-      else if (nodes[c].key == hash_tok)
-        *hc = c;
-      else
-        lits.push_back(c);
-    }
+  // 0. every node's children from one pass over the node array (the store's
+  //    sibling links cost a dependent cache miss per child: the preorder's
+  //    chase took 6.5 s on 4 threads at C3).  A node's '+' / '#' child goes to
+  //    pcs / hcs, its literal children to its range of lch, sorted by id (the
+  //    placement is by atomic counter, so each range is sorted after).
+  const uint32_t n_store = (uint32_t)nodes.size();
+  U32Vec pcs(n_store, kNone), hcs(n_store, kNone);
+  loff.assign((size_t)n_store + 1, 0);
+  constexpr uint32_t kSChunks = 256;
+  auto schunk = [&](uint32_t c, uint32_t *lo, uint32_t *hi) {
+    *lo = (uint32_t)((uint64_t)n_store * c / kSChunks);
+    *hi = (uint32_t)((uint64_t)n_store * (c + 1) / kSChunks);
   };
-  auto push_children = [](std::vector<uint32_t> &stack, uint32_t pc, uint32_t hc, const std::vector<uint32_t> &lits) {
-    if (hc != kNone) stack.push_back(hc);  // LIFO: '#' visited last
-    if (pc != kNone) stack.push_back(pc);
-    for (auto it = lits.rbegin(); it != lits.rend(); ++it) stack.push_back(*it);
+  parallel_for(kSChunks, [&](uint32_t c) {
+    uint32_t lo, hi;
+    schunk(c, &lo, &hi);
+    for (uint32_t n = lo; n < hi; n++) {
+      const HNode &h = nodes[n];
+      if (h.parent == kNone) continue;  // the root, a free slot
+      if (h.key == plus_tok)
+        pcs[h.parent] = n;
+      else if (h.key == hash_tok)
+        hcs[h.parent] = n;
+      else
+        __atomic_fetch_add(&loff[h.parent + 1], 1u, __ATOMIC_RELAXED);
+    }
+  });
+  pt.mark("c:count");
+  for (uint32_t n = 0; n < n_store; n++) loff[n + 1] += loff[n];
+  pt.mark("c:prefix");
+  lch.resize(loff[n_store]);
+  kch.resize(loff[n_store]);
+  {
+    U32Vec fill(loff.begin(), loff.end() - 1);
+    parallel_for(kSChunks, [&](uint32_t c) {
+      uint32_t lo, hi;
+      schunk(c, &lo, &hi);
+      for (uint32_t n = lo; n < hi; n++) {
+        const HNode &h = nodes[n];
+        if (h.parent == kNone || h.key == plus_tok || h.key == hash_tok) continue;
+        lch[__atomic_fetch_add(&fill[h.parent], 1u, __ATOMIC_RELAXED)] = n;
+      }
+    });
+    pt.mark("c:place");
+    parallel_for(kSChunks, [&](uint32_t c) {
+      uint32_t lo, hi;
+      schunk(c, &lo, &hi);
+      for (uint32_t n = lo; n < hi; n++)
+        if (loff[n + 1] - loff[n] > 1) std::sort(lch.begin() + loff[n], lch.begin() + loff[n + 1]);
+      // the children's tokens, beside them (the edge staging reads them in order)
+      for (uint64_t k = loff[lo]; k < loff[hi]; k++) kch[k] = nodes[lch[k]].key;
+    });
+  }
+  pt.mark("p:children");
+  // 1. preorder ids.  Visiting order at a node: literal children by store id,
+  //    then '+', then '#'.  The root and its children are numbered serially;
+  //    the subtrees rooted at depth 2 are counted (HNode::subtree), then
+  //    numbered at their preorder base, in parallel.
+  new_id.assign(nodes.size(), kNone);
+  // children of n in visiting order, pushed for a LIFO visit
+  auto push_children = [&](std::vector<uint32_t> &stack, uint32_t n) {
+    if (hcs[n] != kNone) stack.push_back(hcs[n]);  // LIFO: '#' visited last
+    if (pcs[n] != kNone) stack.push_back(pcs[n]);
+    for (uint32_t k = loff[n + 1]; k > loff[n]; k--) stack.push_back(lch[k - 1]);
   };
   struct Item {
     uint32_t node;
@@ -416,24 +463,25 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
   };
   std::vector<Item> seq;  // the top levels in preorder, subtrees as placeholders
   {
-    std::vector<uint32_t> stack{st.root()}, lits;
-    while (!stack.empty()) {
-      const uint32_t n = stack.back();
-      stack.pop_back();
-      if (nodes[n].depth >= kTop) {
-        seq.push_back(Item{n, true, 0});
-        continue;
-      }
-      seq.push_back(Item{n, false, 1});
-      uint32_t pc, hc;
-      scan_children(n, &pc, &hc, lits);
-      push_children(stack, pc, hc, lits);
+    std::vector<uint32_t> top;
+    push_children(top, st.root());
+    std::reverse(top.begin(), top.end());  // visit order
+    seq.push_back(Item{st.root(), false, 1});
+    std::vector<uint32_t> kids;
+    for (uint32_t r : top) {
+      seq.push_back(Item{r, false, 1});
+      kids.clear();
+      push_children(kids, r);
+      for (auto it = kids.rbegin(); it != kids.rend(); ++it) seq.push_back(Item{*it, true, 0});
     }
   }
+  pt.mark("p:top");
   // subtree sizes: the store keeps them (HNode::subtree)
   const uint32_t n_items = (uint32_t)seq.size();
-  for (uint32_t j = 0; j < n_items; j++)
-    if (seq[j].task) seq[j].size = nodes[seq[j].node].subtree;
+  parallel_for(64, [&](uint32_t w) {
+    for (uint32_t j = w; j < n_items; j += 64)
+      if (seq[j].task) seq[j].size = nodes[seq[j].node].subtree;
+  });
   std::vector<uint64_t> base(n_items);
   uint64_t total = 0;
   for (uint32_t j = 0; j < n_items; j++) {
@@ -448,7 +496,7 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
   std::atomic<bool> size_bad{false};
   // number every item: a top node itself, a subtree by DFS from its base
   parallel_for(64, [&](uint32_t w) {
-    std::vector<uint32_t> stack, lits;
+    std::vector<uint32_t> stack;
     for (uint32_t j = w; j < n_items; j += 64) {
       uint64_t id = base[j];
       stack.assign(1, seq[j].node);
@@ -458,13 +506,11 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
         if (id >= base[j] + seq[j].size) break;  // (flagged below: no write past the item's range)
         new_id[n] = (uint32_t)id;
         order[id] = n;
-        uint32_t pc, hc;
-        scan_children(n, &pc, &hc, lits);
-        pc_of[id] = pc;
-        hc_of[id] = hc;
-        nlit[id] = (uint32_t)lits.size();
+        pc_of[id] = pcs[n];
+        hc_of[id] = hcs[n];
+        nlit[id] = loff[n + 1] - loff[n];
         id++;
-        if (seq[j].task) push_children(stack, pc, hc, lits);
+        if (seq[j].task) push_children(stack, n);
       }
       if (id != base[j] + seq[j].size || !stack.empty()) size_bad.store(true, std::memory_order_relaxed);
     }
@@ -593,8 +639,8 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
     *lo = nn * c / kRChunks;
     *hi = nn * (c + 1) / kRChunks;
   };
-  std::vector<uint32_t> own_multi(nn, 0);
-  std::vector<uint32_t> new_sid(hs.subs.size());
+  U32Vec own_multi(nn, 0);
+  U32Vec new_sid(hs.subs.size());
   parallel_for(kRChunks, [&](uint32_t c) {
     uint64_t lo, hi;
     rchunk(c, &lo, &hi);
@@ -624,7 +670,7 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
     std::vector<uint8_t> heavy_at(nsub, 0);
     // a partner is known by the multi-tail start of its node's range (where
     // the walk's multi part of that range starts, whichever probe gathered it)
-    std::vector<uint32_t> tail_of(nsub, 0);
+    U32Vec tail_of(nsub, 0);
     parallel_for(kRChunks, [&](uint32_t c) {
       uint64_t lo, hi;
       rchunk(c, &lo, &hi);
@@ -753,7 +799,7 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
     pool_off[t] = (uint32_t)hs.tok_pool.size();
     hs.tok_pool.insert(hs.tok_pool.end(), tok.begin(), tok.end());
   }
-  // (a) every literal edge in (parent preorder, child list) order, in parallel
+  // (a) every literal edge in (parent store id, child store id) order, in parallel
   //     over node ranges; the table is then built from this list on the host
   //     (insert_edges_host) or on the device at upload (edges.hip, the same
   //     bytes: the layout depends on kEdgeParts only, not on the thread count,
@@ -773,33 +819,35 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
     hs.bloom = pre.bloom;
     cache->reuses++;
   } else {
-    constexpr uint32_t kChunks = 64;
-    std::vector<uint64_t> eoff(nn + 1, 0);
-    for (uint64_t i = 0; i < nn; i++) eoff[i + 1] = eoff[i] + nlit[i];
+    // by parent store id, then child store id (the children lists): the
+    // position of an edge is its place in lch
+    if (lch.size() != n_literal_edges) return MQM_EINVAL;  // (every live node is reached: never seen)
     pre.staged = std::make_shared<EdgeVec>(n_literal_edges);
     EdgeVec &staged = *pre.staged;
-    parallel_for(kChunks, [&](uint32_t c) {
-      const uint64_t lo = nn * c / kChunks, hi = nn * (c + 1) / kChunks;
-      for (uint64_t i = lo; i < hi; i++) {
-        uint64_t e_i = eoff[i];
-        const uint32_t pc = pc_of[i], hc = hc_of[i];
-        for (uint32_t c2 = nodes[order[i]].first_child; c2 != kNone; c2 = nodes[c2].next_sibling) {
-          if (c2 == pc || c2 == hc) continue;
-          const uint32_t cn = new_id[c2];
-          const std::string_view tok = toks.name(nodes[c2].key);
+    const uint32_t n_store = (uint32_t)nodes.size();
+    constexpr uint32_t kPChunks = 256;
+    parallel_for(kPChunks, [&](uint32_t c) {
+      const uint32_t lo = (uint32_t)((uint64_t)n_store * c / kPChunks),
+                     hi = (uint32_t)((uint64_t)n_store * (c + 1) / kPChunks);
+      for (uint32_t p = lo; p < hi; p++) {
+        if (loff[p] == loff[p + 1]) continue;
+        const uint32_t pi = new_id[p];
+        for (uint32_t q = loff[p]; q < loff[p + 1]; q++) {
+          const uint32_t cn = new_id[lch[q]];
+          const std::string_view tok = toks.name(kch[q]);
           Key k = make_key([&](uint32_t j) { return (uint8_t)tok[j]; }, (uint32_t)tok.size());
-          EdgeEntry &e = staged[e_i];
+          EdgeEntry &e = staged[q];
           e.k0 = k.k0;
           e.k1 = k.k1;
-          e.parent = (uint32_t)i;
+          e.parent = pi;
           e.child = cn;
-          e.tok_off = key_is_long(k) ? pool_off[nodes[c2].key] : 0;
+          e.tok_off = key_is_long(k) ? pool_off[kch[q]] : 0;
           e.tok_len = (uint32_t)tok.size();
           e.desc = hs.nodes[cn];
-          e_i++;
         }
       }
     });
+    pt.mark("e:list");
     // the edge-existence filter: >= 16 bits per edge, a power of two of words
     // (env MQM_NO_BLOOM=1: none, for A/B runs); OR is order-free, so the
     // parallel fill is deterministic

@@ -12,10 +12,10 @@
 
 namespace mqm {
 
-// std::allocator that default-initialises (no zero fill): the big snapshot
-// arrays are first touched by the threads that fill them
+// an allocator that default-initialises (no zero fill): the big snapshot
+// arrays are first touched by the threads that fill them (huge pages: HugeAlloc)
 template <class T>
-struct NoInitAlloc : std::allocator<T> {
+struct NoInitAlloc : HugeAlloc<T> {
   template <class U>
   struct rebind {
     using other = NoInitAlloc<U>;
@@ -45,7 +45,7 @@ using EdgeVec = std::vector<EdgeEntry, NoInitAlloc<EdgeEntry>>;
 struct HostSnapshot {
   std::vector<NodeDesc, NoInitAlloc<NodeDesc>> nodes;  // (every field is written by flatten)
   EdgeVec edges;   // n_buckets * kEdgesPerBucket (empty after upload, and when built on the device)
-  // the literal edges in (parent preorder, child list) order, while the
+  // the literal edges in (parent store id, child store id) order, while the
   // device builds the table (shared with the builder's FlattenCache)
   std::shared_ptr<EdgeVec> staged;
   uint64_t edges_digest = 0;  // edges_digest_of(edges), kept when the host copy is released
@@ -83,7 +83,7 @@ struct FlattenCache {
   bool valid = false;
   uint64_t structure = 0, n_tokens = 0;
   bool host_edges = false;
-  std::vector<uint32_t> order, new_id, pc_of, hc_of, nlit;
+  U32Vec order, new_id, pc_of, hc_of, nlit;
   std::shared_ptr<EdgeVec> staged;
   std::vector<uint64_t> bloom;
   uint64_t reuses = 0;  // builds that took the cache (statistics)

@@ -9,6 +9,10 @@
 #pragma once
 #include <atomic>
 #include <stdint.h>
+#include <sys/mman.h>
+
+#include <memory>
+#include <new>
 
 #include <string>
 #include <string_view>
@@ -16,6 +20,45 @@
 #include <vector>
 
 namespace mqm {
+
+// std::allocator whose large blocks (>= 4 MB) are 2-MB aligned anonymous
+// mappings marked MADV_HUGEPAGE: the flatten reads the node array (3.7 GB at
+// C3) and its own per-node arrays in store-id or preorder order, i.e. at
+// random in the other, and with 4-KB pages nearly every such read also
+// missed the TLB
+template <class T>
+struct HugeAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = HugeAlloc<U>;
+  };
+  static constexpr size_t kHuge = 2ull << 20, kMin = 4ull << 20;
+  HugeAlloc() = default;
+  template <class U>
+  HugeAlloc(const HugeAlloc<U> &) {}
+  static size_t span(size_t n) { return (n * sizeof(T) + kHuge - 1) & ~(kHuge - 1); }
+  T *allocate(size_t n) {
+    if (n * sizeof(T) < kMin) return std::allocator<T>::allocate(n);
+    const size_t len = span(n);
+    char *base = (char *)mmap(nullptr, len + kHuge, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (base == MAP_FAILED) throw std::bad_alloc();
+    char *p = (char *)(((uintptr_t)base + kHuge - 1) & ~(uintptr_t)(kHuge - 1));
+    if (p > base) munmap(base, (size_t)(p - base));  // trim to the aligned span
+    if (base + len + kHuge > p + len) munmap(p + len, (size_t)(base + len + kHuge - (p + len)));
+    (void)madvise(p, len, MADV_HUGEPAGE);
+    return (T *)p;
+  }
+  void deallocate(T *p, size_t n) {
+    if (n * sizeof(T) < kMin) return std::allocator<T>::deallocate(p, n);
+    munmap((void *)p, span(n));
+  }
+};
+template <class T, class U>
+bool operator==(const HugeAlloc<T> &, const HugeAlloc<U> &) { return true; }
+template <class T, class U>
+bool operator!=(const HugeAlloc<T> &, const HugeAlloc<U> &) { return false; }
+
+using U32Vec = std::vector<uint32_t, HugeAlloc<uint32_t>>;
 
 struct SubRec {       // packets.Subscription (packets.go:168-178), interned
   uint32_t client;
@@ -119,7 +162,7 @@ class Store {
   const Interner &tokens() const { return tokens_; }
   const Interner &clients() const { return clients_; }
   const Interner &filters() const { return filters_; }
-  const std::vector<HNode> &nodes() const { return nodes_; }
+  const std::vector<HNode, HugeAlloc<HNode>> &nodes() const { return nodes_; }
   uint32_t root() const { return 0; }
   // moves whenever a node is created or removed (the trie's shape, which
   // flatten's preorder and edge list depend on; subscriptions do not move it)
@@ -138,7 +181,7 @@ class Store {
   uint32_t new_node(uint32_t parent, uint32_t tok);
   void unlink(uint32_t n);
 
-  std::vector<HNode> nodes_;
+  std::vector<HNode, HugeAlloc<HNode>> nodes_;
   uint64_t structure_version_ = 0;
   Footprint last_;
   // sizes that a structural call moves (Footprint::structural)

@@ -72,6 +72,11 @@ for step in "$@"; do
         done ;;
     churnserve) timeout -k 10 1100 python3 -u bench.py --workload churn --steps 3 --warmup 1 --serve-churn-s 30 \
              > $OUT/bench_churn.json 2> $OUT/bench_churn.log ;;
+    flat) timeout -k 10 700 $PYT tests/test_gpu_retained.py tests/test_gpu_edges.py tests/test_commit.py \
+             tests/test_gpu_serve_churn.py tests/test_gpu_parity.py -m gpu --timeout 300 --durations=10 \
+             > $OUT/pytest_flat.log 2>&1 ;;
+    churnfast) MQM_FAST_REPLAY=1 timeout -k 10 700 python3 -u bench.py --workload churn --steps 2 --warmup 1 \
+             --serve-churn-s 30 --churn-build-threads 4,2 > $OUT/bench_churnfast.json 2> $OUT/bench_churnfast.log ;;
     edges) timeout -k 10 400 $PYT tests/test_gpu_edges.py tests/test_commit.py -m gpu --timeout 200 \
              > $OUT/pytest_edges.log 2>&1 ;;
     churndiag) timeout -k 10 520 python3 -u bench.py --workload churn --steps 2 --warmup 1 --serve-churn-s 12 \
