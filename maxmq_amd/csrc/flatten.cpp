@@ -389,61 +389,98 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
   // literal children by parent (store ids), as offsets + list, in store-id
   // order; set below when the shape is not kept, read by the preorder and the
   // edge staging
-  U32Vec loff, lch, kch;  // (kch: lch's token ids)
+  struct Kids {
+    uint32_t off, cnt;  // literal children: lch[off, off + cnt)
+    uint32_t pc, hc;    // '+' / '#' child (kNone: none)
+  };
+  std::vector<Kids, NoInitAlloc<Kids>> kid;  // by store id (one 16-B read per node for the preorder)
+  std::vector<uint32_t, NoInitAlloc<uint32_t>> lch, kch;  // (kch: lch's token ids)
   if (!reuse) {
   // 0. every node's children from one pass over the node array (the store's
   //    sibling links cost a dependent cache miss per child: the preorder's
   //    chase took 6.5 s on 4 threads at C3).  A node's '+' / '#' child goes to
-  //    pcs / hcs, its literal children to its range of lch, sorted by id (the
-  //    placement is by atomic counter, so each range is sorted after).
+  //    kid[].pc / .hc, its literal children to its range of lch in store-id order:
+  //    a counting sort of the (parent, child) pairs — by parent range into
+  //    kPBins bins (per-chunk counts, no atomics: an atomic per child cost a
+  //    second at C3), then each bin by parent with the bin's counters in cache;
+  //    the pairs of a bin stay in child order, so no range needs sorting.
   const uint32_t n_store = (uint32_t)nodes.size();
-  U32Vec pcs(n_store, kNone), hcs(n_store, kNone);
-  loff.assign((size_t)n_store + 1, 0);
-  constexpr uint32_t kSChunks = 256;
+  kid.resize(n_store);
+  constexpr uint32_t kSChunks = 256, kPBins = 256;
+  const uint32_t bin_w = n_store / kPBins + 1;  // parents per bin
   auto schunk = [&](uint32_t c, uint32_t *lo, uint32_t *hi) {
     *lo = (uint32_t)((uint64_t)n_store * c / kSChunks);
     *hi = (uint32_t)((uint64_t)n_store * (c + 1) / kSChunks);
   };
+  std::vector<uint32_t, NoInitAlloc<uint32_t>> lpar(n_store), ktok(n_store);  // a literal child's parent (else kNone), every node's token
+  std::vector<uint64_t> bcnt((size_t)kSChunks * kPBins, 0);  // [chunk][bin]
   parallel_for(kSChunks, [&](uint32_t c) {
     uint32_t lo, hi;
     schunk(c, &lo, &hi);
+    for (uint32_t n = lo; n < hi; n++) kid[n] = Kids{0, 0, kNone, kNone};
+  });
+  parallel_for(kSChunks, [&](uint32_t c) {
+    uint32_t lo, hi;
+    schunk(c, &lo, &hi);
+    uint64_t *cnt = &bcnt[(size_t)c * kPBins];
     for (uint32_t n = lo; n < hi; n++) {
       const HNode &h = nodes[n];
+      ktok[n] = h.key;
+      lpar[n] = kNone;
       if (h.parent == kNone) continue;  // the root, a free slot
       if (h.key == plus_tok)
-        pcs[h.parent] = n;
+        kid[h.parent].pc = n;
       else if (h.key == hash_tok)
-        hcs[h.parent] = n;
-      else
-        __atomic_fetch_add(&loff[h.parent + 1], 1u, __ATOMIC_RELAXED);
+        kid[h.parent].hc = n;
+      else {
+        lpar[n] = h.parent;
+        cnt[h.parent / bin_w]++;
+      }
     }
   });
   pt.mark("c:count");
-  for (uint32_t n = 0; n < n_store; n++) loff[n + 1] += loff[n];
-  pt.mark("c:prefix");
-  lch.resize(loff[n_store]);
-  kch.resize(loff[n_store]);
+  std::vector<uint64_t> bin_lo(kPBins + 1, 0);
   {
-    U32Vec fill(loff.begin(), loff.end() - 1);
-    parallel_for(kSChunks, [&](uint32_t c) {
-      uint32_t lo, hi;
-      schunk(c, &lo, &hi);
-      for (uint32_t n = lo; n < hi; n++) {
-        const HNode &h = nodes[n];
-        if (h.parent == kNone || h.key == plus_tok || h.key == hash_tok) continue;
-        lch[__atomic_fetch_add(&fill[h.parent], 1u, __ATOMIC_RELAXED)] = n;
+    uint64_t run = 0;
+    for (uint32_t b = 0; b < kPBins; b++) {
+      bin_lo[b] = run;
+      for (uint32_t c = 0; c < kSChunks; c++) {
+        const uint64_t v = bcnt[(size_t)c * kPBins + b];
+        bcnt[(size_t)c * kPBins + b] = run;
+        run += v;
       }
-    });
-    pt.mark("c:place");
-    parallel_for(kSChunks, [&](uint32_t c) {
-      uint32_t lo, hi;
-      schunk(c, &lo, &hi);
-      for (uint32_t n = lo; n < hi; n++)
-        if (loff[n + 1] - loff[n] > 1) std::sort(lch.begin() + loff[n], lch.begin() + loff[n + 1]);
-      // the children's tokens, beside them (the edge staging reads them in order)
-      for (uint64_t k = loff[lo]; k < loff[hi]; k++) kch[k] = nodes[lch[k]].key;
-    });
+    }
+    bin_lo[kPBins] = run;
   }
+  const uint64_t n_lit = bin_lo[kPBins];
+  std::vector<uint2, NoInitAlloc<uint2>> pairs(n_lit);  // (parent, child), by bin, child order within
+  parallel_for(kSChunks, [&](uint32_t c) {
+    uint32_t lo, hi;
+    schunk(c, &lo, &hi);
+    uint64_t *off = &bcnt[(size_t)c * kPBins];
+    for (uint32_t n = lo; n < hi; n++)
+      if (lpar[n] != kNone) pairs[off[lpar[n] / bin_w]++] = make_uint2(lpar[n], n);
+  });
+  pt.mark("c:place");
+  lch.resize(n_lit);
+  kch.resize(n_lit);
+  parallel_for(kPBins, [&](uint32_t b) {
+    const uint32_t plo = std::min<uint64_t>((uint64_t)b * bin_w, n_store),
+                   phi = std::min<uint64_t>((uint64_t)(b + 1) * bin_w, n_store);
+    for (uint64_t k = bin_lo[b]; k < bin_lo[b + 1]; k++) kid[pairs[k].x].cnt++;
+    uint64_t run = bin_lo[b];
+    for (uint32_t p = plo; p < phi; p++) {
+      kid[p].off = (uint32_t)run;
+      run += kid[p].cnt;
+      kid[p].cnt = 0;  // (counts again as the cursor below)
+    }
+    for (uint64_t k = bin_lo[b]; k < bin_lo[b + 1]; k++) {
+      Kids &d = kid[pairs[k].x];
+      const uint32_t q = d.off + d.cnt++;
+      lch[q] = pairs[k].y;
+      kch[q] = ktok[pairs[k].y];
+    }
+  });
   pt.mark("p:children");
   // 1. preorder ids.  Visiting order at a node: literal children by store id,
   //    then '+', then '#'.  The root and its children are numbered serially;
@@ -452,9 +489,10 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
   new_id.assign(nodes.size(), kNone);
   // children of n in visiting order, pushed for a LIFO visit
   auto push_children = [&](std::vector<uint32_t> &stack, uint32_t n) {
-    if (hcs[n] != kNone) stack.push_back(hcs[n]);  // LIFO: '#' visited last
-    if (pcs[n] != kNone) stack.push_back(pcs[n]);
-    for (uint32_t k = loff[n + 1]; k > loff[n]; k--) stack.push_back(lch[k - 1]);
+    const Kids d = kid[n];
+    if (d.hc != kNone) stack.push_back(d.hc);  // LIFO: '#' visited last
+    if (d.pc != kNone) stack.push_back(d.pc);
+    for (uint32_t k = d.off + d.cnt; k > d.off; k--) stack.push_back(lch[k - 1]);
   };
   struct Item {
     uint32_t node;
@@ -506,9 +544,10 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
         if (id >= base[j] + seq[j].size) break;  // (flagged below: no write past the item's range)
         new_id[n] = (uint32_t)id;
         order[id] = n;
-        pc_of[id] = pcs[n];
-        hc_of[id] = hcs[n];
-        nlit[id] = loff[n + 1] - loff[n];
+        const Kids d = kid[n];
+        pc_of[id] = d.pc;
+        hc_of[id] = d.hc;
+        nlit[id] = d.cnt;
         id++;
         if (seq[j].task) push_children(stack, n);
       }
@@ -830,9 +869,10 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
       const uint32_t lo = (uint32_t)((uint64_t)n_store * c / kPChunks),
                      hi = (uint32_t)((uint64_t)n_store * (c + 1) / kPChunks);
       for (uint32_t p = lo; p < hi; p++) {
-        if (loff[p] == loff[p + 1]) continue;
+        const Kids d = kid[p];
+        if (d.cnt == 0) continue;
         const uint32_t pi = new_id[p];
-        for (uint32_t q = loff[p]; q < loff[p + 1]; q++) {
+        for (uint32_t q = d.off; q < d.off + d.cnt; q++) {
           const uint32_t cn = new_id[lch[q]];
           const std::string_view tok = toks.name(kch[q]);
           Key k = make_key([&](uint32_t j) { return (uint8_t)tok[j]; }, (uint32_t)tok.size());
