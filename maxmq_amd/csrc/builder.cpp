@@ -54,10 +54,14 @@ void DeltaLog::retain(std::string_view topic, uint64_t msg_ref, uint32_t payload
   op.retain_flag = retain_flag ? 1 : 0;
 }
 
-// MQM_FAST_REPLAY=1: non-structural calls replayed on their node (opt-in
-// while a served-churn hang seen with it on, r05ac, is unexplained)
+// non-structural calls replayed on their node (the footprint the
+// authoritative store recorded; the shadow store has the same node ids);
+// MQM_FAST_REPLAY=0: every call replayed through the path (A/B).  It was
+// opt-in after the served-churn stall of r05ac; with the served path's
+// counter restart and forced relaunch since (capi.cpp Server) the runs with
+// it on are clean (r05ae churnfast, r05af)
 static bool fast_replay() {
-  static const bool v = getenv("MQM_FAST_REPLAY") && atoi(getenv("MQM_FAST_REPLAY")) != 0;
+  static const bool v = !getenv("MQM_FAST_REPLAY") || atoi(getenv("MQM_FAST_REPLAY")) != 0;
   return v;
 }
 

@@ -68,6 +68,15 @@ void parallel_for(uint32_t n, F &&f) {
   for (auto &x : th) x.join();
 }
 
+// the flatten's loops walk one array in order and read another at the
+// positions it holds (store ids <-> preorder ids): prefetching a few
+// iterations ahead keeps several of those misses in flight per thread
+constexpr uint64_t kAhead = 8;
+inline void prefetch_node(const HNode *h) {
+  __builtin_prefetch(h);
+  __builtin_prefetch(reinterpret_cast<const char *>(h) + 64);  // (96 B: may span two lines)
+}
+
 // MQM_FLATTEN_TRACE=1: per-phase wall time to stderr
 struct PhaseTimer {
   bool on = getenv("MQM_FLATTEN_TRACE") != nullptr;
@@ -102,6 +111,7 @@ struct Partners {
 
 static void mark_multi(const Store &st, const U32Vec &order, HostSnapshot &hs, Partners &pt) {
   const auto &nodes = st.nodes();
+  PhaseTimer ph;
   const uint32_t plus_tok = st.plus_token(), hash_tok = st.hash_token();
   const uint64_t nsub = hs.sub_info.size();
   std::vector<uint32_t, NoInitAlloc<uint32_t>> sub_node(nsub);  // (every range is written: ranges tile the subs)
@@ -110,12 +120,14 @@ static void mark_multi(const Store &st, const U32Vec &order, HostSnapshot &hs, P
     for (uint64_t i = nn * c / 256; i < nn * (c + 1) / 256; i++)
       for (uint32_t j = 0; j < hs.nodes[i].sub_cnt; j++) sub_node[hs.nodes[i].sub_off + j] = order[i];
   });
+  ph.mark("m:subnode");
   const uint32_t nc = st.clients().size();
   std::vector<uint32_t> cstart(nc + 2, 0);
   U32Vec by_client(nsub);
   for (uint64_t s = 0; s < nsub; s++) cstart[hs.subs[s].client + 2]++;
   for (uint32_t c = 0; c < nc; c++) cstart[c + 2] += cstart[c + 1];
   for (uint64_t s = 0; s < nsub; s++) by_client[cstart[hs.subs[s].client + 1]++] = (uint32_t)s;
+  ph.mark("m:byclient");
   auto wild = [&](uint32_t tok) { return tok == plus_tok || tok == hash_tok; };
   // (read at every flatten: a test compares both markings in one process)
   const bool hash_multi = getenv("MQM_HASH_MULTI") && atoi(getenv("MQM_HASH_MULTI")) != 0;
@@ -159,6 +171,7 @@ static void mark_multi(const Store &st, const U32Vec &order, HostSnapshot &hs, P
     }
   });
   for (uint64_t v : solo) hs.n_solo += v;
+  ph.mark("m:mark");
   pt.off.assign(nsub + 1, 0);
   for (uint64_t sx = 0; sx < nsub; sx++) pt.off[sx + 1] = pt.off[sx] + (pt.cnt[sx] == kPHeavy ? 0 : pt.cnt[sx]);
   pt.part.resize(pt.off[nsub]);
@@ -583,7 +596,9 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
   parallel_for(kNChunks, [&](uint32_t c) {
     uint64_t subs_n = 0, sh_n = 0, lit = 0;
     uint32_t height = 0;
-    for (uint64_t i = chunk_lo(c); i < chunk_lo(c + 1); i++) {
+    const uint64_t i_end = chunk_lo(c + 1);
+    for (uint64_t i = chunk_lo(c); i < i_end; i++) {
+      if (i + kAhead < i_end) prefetch_node(&nodes[order[i + kAhead]]);
       const HNode &h = nodes[order[i]];
       NodeDesc &d = hs.nodes[i];
       const uint32_t pc = pc_of[i], hc = hc_of[i];
@@ -638,7 +653,10 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
   pt.mark("n:alloc");
   parallel_for(kNChunks, [&](uint32_t c) {
     uint64_t so = sub_base[c], ho = sh_base[c];
-    for (uint64_t i = chunk_lo(c); i < chunk_lo(c + 1); i++) {
+    const uint64_t i_end = chunk_lo(c + 1);
+    for (uint64_t i = chunk_lo(c); i < i_end; i++) {
+      if (i + 2 * kAhead < i_end) prefetch_node(&nodes[order[i + 2 * kAhead]]);
+      if (i + kAhead < i_end) __builtin_prefetch(nodes[order[i + kAhead]].subs.data());
       if (chain_start(i))
         for (uint32_t k = (uint32_t)i, sn = order[i];;) {
           const auto &subs = nodes[sn].subs;
@@ -868,11 +886,14 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
     parallel_for(kPChunks, [&](uint32_t c) {
       const uint32_t lo = (uint32_t)((uint64_t)n_store * c / kPChunks),
                      hi = (uint32_t)((uint64_t)n_store * (c + 1) / kPChunks);
+      const uint64_t q_end = hi < n_store ? kid[hi].off : lch.size();
       for (uint32_t p = lo; p < hi; p++) {
         const Kids d = kid[p];
         if (d.cnt == 0) continue;
         const uint32_t pi = new_id[p];
         for (uint32_t q = d.off; q < d.off + d.cnt; q++) {
+          if (q + 2 * kAhead < q_end) __builtin_prefetch(&new_id[lch[q + 2 * kAhead]]);
+          if (q + kAhead < q_end) __builtin_prefetch(&hs.nodes[new_id[lch[q + kAhead]]]);
           const uint32_t cn = new_id[lch[q]];
           const std::string_view tok = toks.name(kch[q]);
           Key k = make_key([&](uint32_t j) { return (uint8_t)tok[j]; }, (uint32_t)tok.size());

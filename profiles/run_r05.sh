@@ -77,6 +77,8 @@ for step in "$@"; do
              > $OUT/pytest_flat.log 2>&1 ;;
     churnfast) MQM_FAST_REPLAY=1 timeout -k 10 700 python3 -u bench.py --workload churn --steps 2 --warmup 1 \
              --serve-churn-s 30 --churn-build-threads 4,2 > $OUT/bench_churnfast.json 2> $OUT/bench_churnfast.log ;;
+    churnslow) MQM_FAST_REPLAY=0 timeout -k 10 700 python3 -u bench.py --workload churn --steps 2 --warmup 1 \
+             --serve-churn-s 30 --churn-build-threads 4,2 > $OUT/bench_churnslow.json 2> $OUT/bench_churnslow.log ;;
     edges) timeout -k 10 400 $PYT tests/test_gpu_edges.py tests/test_commit.py -m gpu --timeout 200 \
              > $OUT/pytest_edges.log 2>&1 ;;
     churndiag) timeout -k 10 520 python3 -u bench.py --workload churn --steps 2 --warmup 1 --serve-churn-s 12 \
