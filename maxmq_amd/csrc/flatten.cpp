@@ -109,8 +109,13 @@ struct Partners {
   std::vector<uint32_t> part;  // partner old sids
 };
 
-static void mark_multi(const Store &st, const U32Vec &order, HostSnapshot &hs, Partners &pt) {
-  const auto &nodes = st.nodes();
+// (par / kd: every node's parent, and its token and depth, by preorder id —
+// the pairwise level checks climb these: a parent sits just before its
+// subtree, so a climb mostly stays in lines already read, where the node
+// array by store id was a miss per level)
+template <class ParVec>
+static void mark_multi(const Store &st, HostSnapshot &hs, Partners &pt, const ParVec &par,
+                       const std::vector<uint2, NoInitAlloc<uint2>> &kd) {
   PhaseTimer ph;
   const uint32_t plus_tok = st.plus_token(), hash_tok = st.hash_token();
   const uint64_t nsub = hs.sub_info.size();
@@ -118,7 +123,7 @@ static void mark_multi(const Store &st, const U32Vec &order, HostSnapshot &hs, P
   const uint64_t nn = hs.nodes.size();
   parallel_for(256, [&](uint32_t c) {
     for (uint64_t i = nn * c / 256; i < nn * (c + 1) / 256; i++)
-      for (uint32_t j = 0; j < hs.nodes[i].sub_cnt; j++) sub_node[hs.nodes[i].sub_off + j] = order[i];
+      for (uint32_t j = 0; j < hs.nodes[i].sub_cnt; j++) sub_node[hs.nodes[i].sub_off + j] = (uint32_t)i;
   });
   ph.mark("m:subnode");
   const uint32_t nc = st.clients().size();
@@ -132,10 +137,10 @@ static void mark_multi(const Store &st, const U32Vec &order, HostSnapshot &hs, P
   // (read at every flatten: a test compares both markings in one process)
   const bool hash_multi = getenv("MQM_HASH_MULTI") && atoi(getenv("MQM_HASH_MULTI")) != 0;
   auto compatible = [&](uint32_t a, uint32_t b) {
-    while (nodes[a].depth > nodes[b].depth) a = nodes[a].parent;
-    while (nodes[b].depth > nodes[a].depth) b = nodes[b].parent;
-    for (; a != b; a = nodes[a].parent, b = nodes[b].parent) {  // common ancestor: same levels above
-      const uint32_t ka = nodes[a].key, kb = nodes[b].key;
+    while (kd[a].y > kd[b].y) a = par[a];
+    while (kd[b].y > kd[a].y) b = par[b];
+    for (; a != b; a = par[a], b = par[b]) {  // common ancestor: same levels above
+      const uint32_t ka = kd[a].x, kb = kd[b].x;
       if (ka != kb && !wild(ka) && !wild(kb)) return false;
     }
     return true;
@@ -154,12 +159,12 @@ static void mark_multi(const Store &st, const U32Vec &order, HostSnapshot &hs, P
     for (uint32_t c = c_lo; c < c_hi; c++) {
       const uint32_t lo = cstart[c], hi = cstart[c + 1];
       for (uint32_t x = lo; x < hi; x++) {
-        const uint32_t sx = by_client[x], nx = sub_node[sx], px = nodes[nx].parent;
+        const uint32_t sx = by_client[x], nx = sub_node[sx], px = par[nx];
         // the parent probe emits a '#' node's subscriptions after a literal hit on its
         // parent; the walks skip the own visit of such a node (kFlagParentLit), so
         // it is emitted once per topic.  MQM_HASH_MULTI=1 (A/B): treat them as multi.
         const bool heavy = hi - lo > kMaxPairwise ||
-                           (hash_multi && nodes[nx].key == hash_tok && px != st.root() && !wild(nodes[px].key));
+                           (hash_multi && kd[nx].x == hash_tok && px != 0 && !wild(kd[px].x));
         uint32_t pc = 0;
         if (!heavy)
           for (uint32_t y = lo; y < hi; y++) pc += y != x && compatible(nx, sub_node[by_client[y]]);
@@ -586,6 +591,7 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
   std::vector<uint8_t> flags(nn, 0);
   std::vector<uint32_t, NoInitAlloc<uint32_t>> par_new(nn);  // (set for every node below; kNone at the root)
   par_new[0] = kNone;
+  std::vector<uint2, NoInitAlloc<uint2>> kd_pre(nn);  // token, depth by preorder id (mark_multi)
   constexpr uint32_t kNChunks = 256;
   std::vector<uint64_t> sub_base(kNChunks + 1, 0), sh_base(kNChunks + 1, 0), lit_c(kNChunks, 0);
   std::vector<uint32_t> height_c(kNChunks, 0);
@@ -601,6 +607,7 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
       if (i + kAhead < i_end) prefetch_node(&nodes[order[i + kAhead]]);
       const HNode &h = nodes[order[i]];
       NodeDesc &d = hs.nodes[i];
+      kd_pre[i] = make_uint2(h.key, h.depth);
       const uint32_t pc = pc_of[i], hc = hc_of[i];
       d.plus = pc == kNone ? kNone : new_id[pc];
       d.hash = hc == kNone ? kNone : new_id[hc];
@@ -685,7 +692,7 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
   for (uint64_t i = 0; i < nn; i++) hs.nodes[i].sh_cnt_flags |= (uint32_t)flags[i] << 24;
   pt.mark("nodes");
   Partners partners;
-  mark_multi(st, order, hs, partners);
+  mark_multi(st, hs, partners, par_new, kd_pre);
   pt.mark("multi");
   if (st.retained_len() > 0) build_retained(st, order, new_id, hs);
   pt.mark("retained");
