@@ -1551,6 +1551,7 @@ struct Server {
   std::shared_ptr<GpuSnapshot> snap;  // (mu) what the running launch reads
   bool launched = false;              // (mu) a launch may still run
   uint64_t gen = 0;                   // (mu) launches so far = the running launch's generation
+  uint64_t seen = 0;                  // (mu) request numbers handed out by the launches so far
   uint32_t grid = 32, idle_us = 20000;
   uint32_t max_grid = 128;            // half the device's CUs (init): batch-path kernels keep the rest
   const bool want_ids;
@@ -1710,35 +1711,42 @@ struct Server {
     snap = std::move(want);
     ts.mark("snapshot switch");
     if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
-    // (no kernel runs now) the device counter restarts at the first request
-    // not yet served: a stopped kernel may have taken numbers past it.  That
-    // is the oldest of (a) requests posted and not served, in any slot (also
-    // older than the last kServeSlots tickets: callers that gave up on a
-    // request while their slot stayed taken push the ticket counter on), and
-    // (b) the last kServeSlots tickets taken and not yet posted — except those
-    // whose caller gave up before posting (never_posted): a workgroup would
-    // wait on such a number until the next stop
+    // (no kernel runs now) the device counter restarts at the oldest request
+    // not yet served.  Slot i's tickets take it in turn (i, i + kServeSlots,
+    // ...): free_seq[i] = f is its current or next owner, so its oldest
+    // unserved ticket is f, or f + kServeSlots once f's result is in (done) —
+    // if that ticket has been taken (< T) and its caller did not give up
+    // before posting (never_posted: a workgroup would wait on it until the
+    // next stop).  A caller may move on meanwhile: the minimum can only come
+    // out low, and the launch skips served numbers below `seen` (k_serve)
+    // instead of serving them again.  (Round 5 scanned the posted slots plus
+    // the last kServeSlots tickets: a ticket older than that whose caller had
+    // not posted yet — a thread descheduled between taking it and posting —
+    // was skipped, and its request waited for the forced relaunch, r05af.)
+    {
+      unsigned long long c0 = 0;
+      if (hipMemcpyAsync(&c0, ctr, sizeof(c0), hipMemcpyDeviceToHost, st) != hipSuccess ||
+          hipStreamSynchronize(st) != hipSuccess)
+        return MQM_EHIP;
+      seen = std::max<uint64_t>(seen, c0);
+    }
     const uint64_t T = ticket.load(std::memory_order_acquire);
     unsigned long long c[2] = {T, 0};
-    for (uint32_t i = 0; i < kServeSlots; i++) {
-      const unsigned long long p = __atomic_load_n(&q->slot[i].seq, __ATOMIC_ACQUIRE) & kServeSeqMask;
-      if (p && __atomic_load_n(&q->done[i], __ATOMIC_ACQUIRE) < p) c[0] = std::min<unsigned long long>(c[0], p - 1);
-    }
     {
       std::lock_guard<std::mutex> g(np_mu);
-      for (uint64_t k = T > kServeSlots ? T - kServeSlots : 0; k < T && k < c[0]; k++) {
-        const uint32_t i = (uint32_t)(k % kServeSlots);
-        const bool posted = (__atomic_load_n(&q->slot[i].seq, __ATOMIC_ACQUIRE) & kServeSeqMask) == k + 1;
-        if (!posted && __atomic_load_n(&q->done[i], __ATOMIC_ACQUIRE) < k + 1 && !never_posted.count(k)) {
-          c[0] = k;
-          break;
-        }
+      for (uint32_t i = 0; i < kServeSlots; i++) {
+        const uint64_t f = free_seq[i].load(std::memory_order_acquire);
+        if (f >= T) continue;  // no ticket for this slot yet
+        const uint64_t d = __atomic_load_n(&q->done[i], __ATOMIC_ACQUIRE);
+        const uint64_t u = d >= f + 1 ? f + kServeSlots : f;
+        if (u < T && !never_posted.count(u)) c[0] = std::min<unsigned long long>(c[0], u);
       }
       while (!never_posted.empty() && *never_posted.begin() + 4 * kServeSlots < T) never_posted.erase(never_posted.begin());
     }
     if (hipMemcpyAsync(ctr, c, sizeof(c), hipMemcpyHostToDevice, st) != hipSuccess) return MQM_EHIP;
     const uint64_t ver = snap->host->version;
-    if (serve_launch(snap->dev, q, ctr, grid, idle_us, want_ids, ver, gen + 1, st) != 0) return MQM_EHIP;
+    if (serve_launch(snap->dev, q, ctr, grid, idle_us, want_ids, ver, gen + 1, std::max<uint64_t>(seen, T), st) != 0)
+      return MQM_EHIP;
     gen++;
     launched = true;
     launches++;

@@ -520,7 +520,7 @@ struct ServeSink {
 
 __global__ __launch_bounds__(kFT) void k_serve(DeviceSnapshot s, ServeQueue *q, unsigned long long *ctr,
                                                uint64_t idle_ticks, int want_ids, unsigned long long ver,
-                                               unsigned long long gen) {
+                                               unsigned long long gen, unsigned long long seen) {
   unsigned long long *claimed = ctr;  // ctr[1]: workgroups of this launch that have exited
   __shared__ FastLds L;
   __shared__ unsigned long long job;
@@ -532,12 +532,22 @@ __global__ __launch_bounds__(kFT) void k_serve(DeviceSnapshot s, ServeQueue *q, 
       // take the next request number first (a device atomic: workgroups wait
       // on distinct requests in parallel, instead of queueing behind one PCIe
       // poll per claim), then wait for its topic
-      unsigned int clo = 0, chi = 0;
-      if (lane == 0) {
-        const unsigned long long c0 = atomicAdd(claimed, 1ull);
-        clo = (unsigned int)c0, chi = (unsigned int)(c0 >> 32);
+      // (a number below `seen` was handed out by an earlier launch, which may
+      // have served it: the counter restarts at the oldest unserved request,
+      // and the requests after it that are done are skipped, not served twice
+      // into a slot whose caller may be reading it)
+      unsigned long long c;
+      for (;;) {
+        unsigned int clo = 0, chi = 0, served = 0;
+        if (lane == 0) {
+          const unsigned long long c0 = atomicAdd(claimed, 1ull);
+          clo = (unsigned int)c0, chi = (unsigned int)(c0 >> 32);
+          if (c0 < seen)
+            served = __hip_atomic_load(&q->done[c0 % kServeSlots], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= c0 + 1;
+        }
+        c = ((unsigned long long)__shfl(chi, 0, 64) << 32) | __shfl(clo, 0, 64);
+        if (!__shfl(served, 0, 64)) break;
       }
-      const unsigned long long c = ((unsigned long long)__shfl(chi, 0, 64) << 32) | __shfl(clo, 0, 64);
       const unsigned long long *line = reinterpret_cast<const unsigned long long *>(&q->slot[c % kServeSlots]);
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       uint32_t nap = 1;
@@ -649,10 +659,10 @@ FastArena::~FastArena() {
 }
 
 int serve_launch(const DeviceSnapshot &s, ServeQueue *q, unsigned long long *ctr, uint32_t grid, uint32_t idle_us,
-                 bool want_ids, uint64_t ver, uint64_t gen, hipStream_t st) {
+                 bool want_ids, uint64_t ver, uint64_t gen, uint64_t seen, hipStream_t st) {
   const uint64_t idle_ticks = (uint64_t)idle_us * 100;  // s_memrealtime: 100 MHz
   hipLaunchKernelGGL(k_serve, dim3(std::max<uint32_t>(1, grid)), dim3(kFT), 0, st, s, q, ctr, idle_ticks,
-                     want_ids ? 1 : 0, (unsigned long long)ver, (unsigned long long)gen);
+                     want_ids ? 1 : 0, (unsigned long long)ver, (unsigned long long)gen, (unsigned long long)seen);
   HIP_TRY(hipGetLastError());
   return 0;
 }

@@ -254,12 +254,14 @@ struct ServeQueue {
   ServeSlot slot[kServeSlots];
 };
 // launch the server on `st` (q: host-mapped; ctr: two device counters, set by
-// the host before every launch: ctr[0] the first request not yet served, ctr[1]
+// the host before every launch: ctr[0] the oldest request not yet served, ctr[1]
 // = 0 the workgroups that have exited).  `ver` is written into every slot the
 // launch serves (the snapshot's version), `gen` into q->exited by the launch's
-// last workgroup to exit.
+// last workgroup to exit; request numbers below `seen` (the highest number an
+// earlier launch handed out) are skipped when their slot's done word shows
+// them served.
 int serve_launch(const DeviceSnapshot &s, ServeQueue *q, unsigned long long *ctr, uint32_t grid, uint32_t idle_us,
-                 bool want_ids, uint64_t ver, uint64_t gen, hipStream_t st);
+                 bool want_ids, uint64_t ver, uint64_t gen, uint64_t seen, hipStream_t st);
 
 // Identifiers support for the last match_device call on `ws` (its topic
 // buffers must still hold the batch): per topic, the sids of the gathered
