@@ -927,10 +927,19 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
       const uint64_t mask = bits / 64 - 1;
       parallel_for(kChunks, [&](uint32_t c) {
         const uint64_t lo = n_literal_edges * c / kChunks, hi = n_literal_edges * (c + 1) / kChunks;
-        for (uint64_t e = lo; e < hi; e++) {
-          const EdgeEntry &x = staged[e];
-          const uint64_t h = edge_hash(x.parent, Key{x.k0, x.k1});
-          __atomic_fetch_or(&hs.bloom[bloom_word(h, mask)], bloom_bits(h), __ATOMIC_RELAXED);
+        // 64 edges at a time: their words are prefetched for writing first, so
+        // the atomics (each drains the store buffer) find their lines in cache
+        for (uint64_t e0 = lo; e0 < hi; e0 += 64) {
+          const uint32_t m = (uint32_t)std::min<uint64_t>(64, hi - e0);
+          uint64_t w[64], bb[64];
+          for (uint32_t j = 0; j < m; j++) {
+            const EdgeEntry &x = staged[e0 + j];
+            const uint64_t h = edge_hash(x.parent, Key{x.k0, x.k1});
+            w[j] = bloom_word(h, mask);
+            bb[j] = bloom_bits(h);
+            __builtin_prefetch(&hs.bloom[w[j]], 1);
+          }
+          for (uint32_t j = 0; j < m; j++) __atomic_fetch_or(&hs.bloom[w[j]], bb[j], __ATOMIC_RELAXED);
         }
       });
     }
