@@ -400,19 +400,16 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
                      cache->n_tokens == st.tokens().size() && cache->host_edges == host_edges &&
                      st.retained_len() == 0 && cache->new_id.size() == nodes.size();
   FlattenCache local;
-  FlattenCache &pre = reuse ? *cache : local;
+  FlattenCache &pre = cache ? *cache : local;  // (its arrays are rewritten when the shape is not kept)
   if (cache && !reuse) cache->valid = false;
   U32Vec &new_id = pre.new_id, &order = pre.order, &pc_of = pre.pc_of, &hc_of = pre.hc_of,
                         &nlit = pre.nlit;
   // literal children by parent (store ids), as offsets + list, in store-id
   // order; set below when the shape is not kept, read by the preorder and the
   // edge staging
-  struct Kids {
-    uint32_t off, cnt;  // literal children: lch[off, off + cnt)
-    uint32_t pc, hc;    // '+' / '#' child (kNone: none)
-  };
-  std::vector<Kids, NoInitAlloc<Kids>> kid;  // by store id (one 16-B read per node for the preorder)
-  std::vector<uint32_t, NoInitAlloc<uint32_t>> lch, kch;  // (kch: lch's token ids)
+  using Kids = FlatKids;
+  auto &kid = pre.kid;            // by store id (one 16-B read per node for the preorder)
+  auto &lch = pre.lch, &kch = pre.kch;  // (kch: lch's token ids)
   if (!reuse) {
   // 0. every node's children from one pass over the node array (the store's
   //    sibling links cost a dependent cache miss per child: the preorder's
@@ -430,13 +427,16 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
     *lo = (uint32_t)((uint64_t)n_store * c / kSChunks);
     *hi = (uint32_t)((uint64_t)n_store * (c + 1) / kSChunks);
   };
-  std::vector<uint32_t, NoInitAlloc<uint32_t>> lpar(n_store), ktok(n_store);  // a literal child's parent (else kNone), every node's token
+  auto &lpar = pre.lpar, &ktok = pre.ktok;  // a literal child's parent (else kNone), every node's token
+  lpar.resize(n_store);
+  ktok.resize(n_store);
   std::vector<uint64_t> bcnt((size_t)kSChunks * kPBins, 0);  // [chunk][bin]
   parallel_for(kSChunks, [&](uint32_t c) {
     uint32_t lo, hi;
     schunk(c, &lo, &hi);
     for (uint32_t n = lo; n < hi; n++) kid[n] = Kids{0, 0, kNone, kNone};
   });
+  pt.mark("c:init");
   parallel_for(kSChunks, [&](uint32_t c) {
     uint32_t lo, hi;
     schunk(c, &lo, &hi);
@@ -886,7 +886,11 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
     // by parent store id, then child store id (the children lists): the
     // position of an edge is its place in lch
     if (lch.size() != n_literal_edges) return MQM_EINVAL;  // (every live node is reached: never seen)
-    pre.staged = std::make_shared<EdgeVec>(n_literal_edges);
+    // (the previous build's list, once no snapshot holds it: upload drops it)
+    if (pre.staged && pre.staged.use_count() == 1)
+      pre.staged->resize(n_literal_edges);
+    else
+      pre.staged = std::make_shared<EdgeVec>(n_literal_edges);
     EdgeVec &staged = *pre.staged;
     const uint32_t n_store = (uint32_t)nodes.size();
     constexpr uint32_t kPChunks = 256;
@@ -957,12 +961,7 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
     hs.staged = pre.staged;
   }
   if (cache && !reuse) {  // keep this build's shape for the next one
-    cache->order = std::move(order);
-    cache->new_id = std::move(new_id);
-    cache->pc_of = std::move(pc_of);
-    cache->hc_of = std::move(hc_of);
-    cache->nlit = std::move(nlit);
-    cache->staged = pre.staged;
+    // (order, new_id, pc_of, hc_of, nlit and staged were built in place)
     cache->bloom = hs.bloom;
     cache->structure = st.structure_version();
     cache->n_tokens = st.tokens().size();

@@ -79,6 +79,13 @@ struct HostSnapshot {
 // structure_version and token count are those it was built at, no message is
 // retained and the table is built where it was.  Subscribe / Unsubscribe of
 // filters that exist (and keep other subscribers) leave the shape alone.
+// a node's children (flatten.cpp): literal ones at lch[off, off + cnt)
+struct FlatKids {
+  uint32_t off, cnt;
+  uint32_t pc, hc;  // '+' / '#' child (kNone: none)
+};
+using ScratchU32 = std::vector<uint32_t, NoInitAlloc<uint32_t>>;
+
 struct FlattenCache {
   bool valid = false;
   uint64_t structure = 0, n_tokens = 0;
@@ -87,6 +94,10 @@ struct FlattenCache {
   std::shared_ptr<EdgeVec> staged;
   std::vector<uint64_t> bloom;
   uint64_t reuses = 0;  // builds that took the cache (statistics)
+  // working arrays kept from build to build (their pages stay mapped: a fresh
+  // 2-MB page costs its zeroing and, when memory is fragmented, compaction)
+  std::vector<FlatKids, NoInitAlloc<FlatKids>> kid;
+  ScratchU32 lpar, ktok, lch, kch;
 };
 
 // Build the snapshot; returns MQM_OK or MQM_ELIMIT.  host_edges = false: the
