@@ -504,13 +504,23 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
   //    then '+', then '#'.  The root and its children are numbered serially;
   //    the subtrees rooted at depth 2 are counted (HNode::subtree), then
   //    numbered at their preorder base, in parallel.
-  new_id.assign(nodes.size(), kNone);
+  new_id.resize(nodes.size());  // (kNone everywhere first: free slots keep it)
+  parallel_for(64, [&](uint32_t c) {
+    std::fill(new_id.begin() + nodes.size() * c / 64, new_id.begin() + nodes.size() * (c + 1) / 64, kNone);
+  });
   // children of n in visiting order, pushed for a LIFO visit
+  // (each child's record and id slot are prefetched as it is pushed: the
+  // DFS pops it soon after)
   auto push_children = [&](std::vector<uint32_t> &stack, uint32_t n) {
     const Kids d = kid[n];
-    if (d.hc != kNone) stack.push_back(d.hc);  // LIFO: '#' visited last
-    if (d.pc != kNone) stack.push_back(d.pc);
-    for (uint32_t k = d.off + d.cnt; k > d.off; k--) stack.push_back(lch[k - 1]);
+    auto push = [&](uint32_t c) {
+      __builtin_prefetch(&kid[c]);
+      __builtin_prefetch(&new_id[c], 1);
+      stack.push_back(c);
+    };
+    if (d.hc != kNone) push(d.hc);  // LIFO: '#' visited last
+    if (d.pc != kNone) push(d.pc);
+    for (uint32_t k = d.off + d.cnt; k > d.off; k--) push(lch[k - 1]);
   };
   struct Item {
     uint32_t node;
@@ -522,13 +532,16 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
     std::vector<uint32_t> top;
     push_children(top, st.root());
     std::reverse(top.begin(), top.end());  // visit order
+    size_t n_seq = 1 + top.size();
+    for (uint32_t r : top) n_seq += kid[r].cnt + (kid[r].pc != kNone) + (kid[r].hc != kNone);
+    seq.reserve(n_seq);
     seq.push_back(Item{st.root(), false, 1});
-    std::vector<uint32_t> kids;
     for (uint32_t r : top) {
       seq.push_back(Item{r, false, 1});
-      kids.clear();
-      push_children(kids, r);
-      for (auto it = kids.rbegin(); it != kids.rend(); ++it) seq.push_back(Item{*it, true, 0});
+      const Kids d = kid[r];  // visit order: literals, '+', '#'
+      for (uint32_t k = d.off; k < d.off + d.cnt; k++) seq.push_back(Item{lch[k], true, 0});
+      if (d.pc != kNone) seq.push_back(Item{d.pc, true, 0});
+      if (d.hc != kNone) seq.push_back(Item{d.hc, true, 0});
     }
   }
   pt.mark("p:top");
@@ -545,10 +558,11 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
     total += seq[j].size;
   }
   if (total >= (1ull << 30)) return MQM_ELIMIT;  // k_walk packs node id << 2 | item kind
-  order.assign(total, 0);
-  pc_of.assign(total, 0);
-  hc_of.assign(total, 0);
-  nlit.assign(total, 0);
+  // (every entry is written by the numbering below)
+  order.resize(total);
+  pc_of.resize(total);
+  hc_of.resize(total);
+  nlit.resize(total);
   std::atomic<bool> size_bad{false};
   // number every item: a top node itself, a subtree by DFS from its base
   parallel_for(64, [&](uint32_t w) {
