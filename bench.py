@@ -105,7 +105,7 @@ def parse():
                     help="churn: seconds of per-publish calls (64 native callers through MQM_CFG_SERVE) while "
                          "--churn-rate Subscribe/Unsubscribe per second run (0 = skip)")
     ap.add_argument("--churn-rate", type=float, default=100000.0, help="churn: mutations/s during the served leg")
-    ap.add_argument("--churn-build-threads", default="4,2,16,-1",
+    ap.add_argument("--churn-build-threads", default="2,4,16,-1",
                     help="churn: comma-separated host thread counts for the background rebuild "
                          "(mqm_build_threads), one served-under-churn leg each (-1: no rebuild during the leg)")
     ap.add_argument("--retained", type=int, default=50000000, help="reverse: retained topics")

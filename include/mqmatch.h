@@ -235,7 +235,7 @@ int mqm_commit_state_get(mqm_index *h, mqm_commit_state *out);
  * created or removed since) */
 int mqm_build_phases_ms(mqm_index *h, double *ms);
 /* host threads for every flatten of this process (0: MQM_BUILD_THREADS, else
- * min(16, hardware threads), and at most 4 while a per-publish server
+ * min(16, hardware threads), and at most 2 while a per-publish server
  * (MQM_CFG_SERVE) lives: a background build shares the CPUs with its callers,
  * DESIGN §9) */
 int mqm_build_threads(uint32_t n);

@@ -40,10 +40,12 @@ uint32_t build_threads() {
   }();
   if (env > 0) return (uint32_t)env;
   const uint32_t hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  // a per-publish server's callers share the CPUs with the rebuild: 16 flatten
-  // threads cut served calls under churn to 0.62M/s at p99 339 us, 4 threads
-  // kept 0.86M/s at p99 86 us (r05l, 64 callers, 100k mutations/s)
-  return g_servers.load(std::memory_order_relaxed) > 0 ? std::min(hw, 4u) : hw;
+  // a per-publish server's callers share the CPUs with the rebuild, which runs
+  // back to back under churn (its CPU share is its thread count): 16 / 4 / 2
+  // flatten threads give 0.79-0.82 / 0.85-1.00 / 0.93-1.10M served calls/s
+  // at a visibility lag of 4-5 / 7-8 / 11-13 s (r05af-r05ai, 64 callers,
+  // 100k mutations/s, C3)
+  return g_servers.load(std::memory_order_relaxed) > 0 ? std::min(hw, 2u) : hw;
 }
 
 void serve_count(int delta) { g_servers.fetch_add(delta, std::memory_order_relaxed); }
