@@ -129,11 +129,53 @@ static void mark_multi(const Store &st, HostSnapshot &hs, Partners &pt, const Pa
   });
   ph.mark("m:subnode");
   const uint32_t nc = st.clients().size();
+  // the subscriptions by client, each client's in sid order (cstart[c] ..
+  // cstart[c + 1]): a counting sort by client-range bin with per-chunk counts,
+  // then each bin by client (the serial pass took 0.3 s at C3)
   std::vector<uint32_t> cstart(nc + 2, 0);
   U32Vec by_client(nsub);
-  for (uint64_t s = 0; s < nsub; s++) cstart[hs.subs[s].client + 2]++;
-  for (uint32_t c = 0; c < nc; c++) cstart[c + 2] += cstart[c + 1];
-  for (uint64_t s = 0; s < nsub; s++) by_client[cstart[hs.subs[s].client + 1]++] = (uint32_t)s;
+  {
+    constexpr uint32_t kB = 256, kS = 256;
+    const uint32_t bw = nc / kB + 1;
+    std::vector<uint64_t> cnt((size_t)kS * kB, 0), blo(kB + 1, 0);
+    auto srange = [&](uint32_t c, uint64_t *lo, uint64_t *hi) {
+      *lo = nsub * c / kS;
+      *hi = nsub * (c + 1) / kS;
+    };
+    parallel_for(kS, [&](uint32_t c) {
+      uint64_t lo, hi;
+      srange(c, &lo, &hi);
+      for (uint64_t x = lo; x < hi; x++) cnt[(size_t)c * kB + hs.subs[x].client / bw]++;
+    });
+    uint64_t run = 0;
+    for (uint32_t b = 0; b < kB; b++) {
+      blo[b] = run;
+      for (uint32_t c = 0; c < kS; c++) {
+        const uint64_t v = cnt[(size_t)c * kB + b];
+        cnt[(size_t)c * kB + b] = run;
+        run += v;
+      }
+    }
+    blo[kB] = run;
+    U32Vec tmp(nsub);  // sids by bin, sid order within
+    parallel_for(kS, [&](uint32_t c) {
+      uint64_t lo, hi;
+      srange(c, &lo, &hi);
+      for (uint64_t x = lo; x < hi; x++) tmp[cnt[(size_t)c * kB + hs.subs[x].client / bw]++] = (uint32_t)x;
+    });
+    parallel_for(kB, [&](uint32_t b) {
+      const uint32_t clo = std::min<uint64_t>((uint64_t)b * bw, nc), chi = std::min<uint64_t>((uint64_t)(b + 1) * bw, nc);
+      for (uint64_t j = blo[b]; j < blo[b + 1]; j++) cstart[hs.subs[tmp[j]].client + 1]++;
+      uint64_t r = blo[b];
+      for (uint32_t c = clo; c < chi; c++) {
+        const uint32_t v = cstart[c + 1];
+        cstart[c + 1] = (uint32_t)r;  // (a cursor first, then client c's end)
+        r += v;
+      }
+      for (uint64_t j = blo[b]; j < blo[b + 1]; j++) by_client[cstart[hs.subs[tmp[j]].client + 1]++] = tmp[j];
+    });
+    // cstart[c + 1] is now client c's end = client c + 1's start
+  }
   ph.mark("m:byclient");
   auto wild = [&](uint32_t tok) { return tok == plus_tok || tok == hash_tok; };
   // (read at every flatten: a test compares both markings in one process)
