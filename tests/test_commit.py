@@ -343,3 +343,35 @@ def test_rebuild_keeps_the_trie_shape_when_no_node_moves():
         assert asy.snapshot_digest() == sync.snapshot_digest(), rnd
         kept.append(_kept_shape(asy))
     assert kept == [True, True, True, False, False, True], kept
+
+
+def test_flatten_layout_independent_of_thread_count():
+    """The flatten's children lists (a binned counting sort over the node
+    array), preorder, edge staging and client grouping are laid out by store
+    ids and fixed chunk counts, never by thread timing: the same store state
+    flattened on 1, 3 and 8 host threads gives one digest.  The op sequence
+    removes nodes and re-creates others, so store ids are reused from the free
+    list and are not in creation order; retained messages add the reverse
+    index (its groups sorted by parent)."""
+    rng = random.Random(7)
+    ops = []
+    for step in range(3000):
+        f = "/".join(rng.choice(LEVELS[:5] + ["m", "n", "o"]) for _ in range(rng.randint(1, 5)))
+        ops.append((rng.random(), f, f"c{rng.randint(0, 40)}", step))
+    digests = []
+    try:
+        for threads in (1, 3, 8):
+            capi.check("mqm_build_threads", capi.lib().mqm_build_threads(threads))
+            idx = maxmq_amd.TopicsIndex(device=None, autocommit=False)
+            for r, f, c, step in ops:
+                if r < 0.6:
+                    idx.subscribe(c, maxmq_amd.Subscription(f, qos=step % 3, identifier=step % 4))
+                elif r < 0.9:
+                    idx.unsubscribe(f, c)
+                else:
+                    idx.retain_message(f.replace("+", "p").replace("#", "h"), step, 3)
+            idx.commit()
+            digests.append(idx.snapshot_digest())
+    finally:
+        capi.lib().mqm_build_threads(0)
+    assert digests[0] == digests[1] == digests[2]
