@@ -909,7 +909,9 @@ struct alignas(16) WinLds {
 // four (a quarter of the memory instructions), position by position at part
 // boundaries
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-template <bool kVec = false>
+// kNT (MQM_NT_STORE=1, A/B): the scalar path's stores non-temporal, so the
+// result stream does not evict the hub ranges the copy re-reads from L2
+template <bool kVec = false, bool kNT = false>
 __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_eu(8))) void k_wincopy(
     DeviceSnapshot s, const uint4 *__restrict__ desc, const uint64_t *__restrict__ nd_ptr, uint64_t desc_cap,
     const uint32_t *__restrict__ win, uint64_t win_cap, const uint64_t *__restrict__ total_ptr,
@@ -1037,10 +1039,14 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
         for (int u = 0; u < kCU; u++) {
           if (!in[u]) continue;
           const uint64_t p = g0 + base + u * kWave + lane;
-          if (p < cap)
-            out[p] = v[u];
-          else
+          if (p < cap) {
+            if (kNT)
+              __builtin_nontemporal_store(v[u], out + p);
+            else
+              out[p] = v[u];
+          } else {
             atomicOr(oob, kOobStore);
+          }
         }
       }
       wave_lds_sync();
@@ -1533,6 +1539,11 @@ static bool desc_copy_on() {
 // MQM_WINCOPY_VEC=1: the window copy moves 4 positions per lane at a time (A/B)
 static bool wincopy_vec() {
   static const bool v = getenv("MQM_WINCOPY_VEC") && atoi(getenv("MQM_WINCOPY_VEC")) != 0;
+  return v;
+}
+// MQM_NT_STORE=1: the window copy's stores non-temporal (A/B)
+static bool nt_store() {
+  static const bool v = getenv("MQM_NT_STORE") && atoi(getenv("MQM_NT_STORE")) != 0;
   return v;
 }
 // MQM_LONG_PART=m: solo parts of at least m entries take k_longcopy (A/B; off
@@ -2763,6 +2774,10 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
         if (wincopy_vec())
           hipLaunchKernelGGL(k_wincopy<true>, grid(k_wincopy<true>), dim3(kWave * kEmitWaves), 0, st, s, desc,
                              desc_start + n, desc_cap, win, win_cap, o.dstart + n, o.dout, o.dcap, &o.ctr->oob);
+        else if (nt_store())
+          hipLaunchKernelGGL((k_wincopy<false, true>), grid(k_wincopy<false, true>), dim3(kWave * kEmitWaves), 0, st,
+                             s, desc, desc_start + n, desc_cap, win, win_cap, o.dstart + n, o.dout, o.dcap,
+                             &o.ctr->oob);
         else
           hipLaunchKernelGGL(k_wincopy<false>, grid(k_wincopy<false>), dim3(kWave * kEmitWaves), 0, st, s, desc,
                              desc_start + n, desc_cap, win, win_cap, o.dstart + n, o.dout, o.dcap, &o.ctr->oob);

@@ -62,6 +62,17 @@ for step in "$@"; do
           env $E timeout -k 10 600 python3 -u bench.py --config 4 --shard 0/8 $FAST > $OUT/bench_c4_$N.json \
             2> $OUT/bench_c4_$N.log || exit 1
         done ;;
+    ntab) for V in base:X=0 nt:MQM_NT_STORE=1 base2:X=0 nt2:MQM_NT_STORE=1; do
+          N=${V%%:*}; E=${V#*:}
+          env $E timeout -k 10 400 python3 -u bench.py $FAST --ident-steps 0 > $OUT/bench_fast_$N.json 2> $OUT/bench_fast_$N.log || exit 1
+        done ;;
+    c4ntab) for V in base:X=0 nt:MQM_NT_STORE=1; do
+          N=${V%%:*}; E=${V#*:}
+          env $E timeout -k 10 600 python3 -u bench.py --config 4 --shard 0/8 $FAST --ident-steps 0 > $OUT/bench_c4_$N.json \
+            2> $OUT/bench_c4_$N.log || exit 1
+        done ;;
+    ntpar) MQM_NT_STORE=1 timeout -k 10 500 $PYT tests/test_gpu_parity.py -m gpu --timeout 300 \
+             -k "config_vs_oracle or edge_cases or kat" > $OUT/pytest_nt.log 2>&1 ;;
     revstats) MQM_REV_STATS=1 timeout -k 10 600 python3 -u bench.py --workload reverse --steps 2 --warmup 1 \
              --no-cpu-baseline > $OUT/bench_rev_stats.json 2> $OUT/bench_rev_stats.log ;;
     node) timeout -k 10 400 $PYT tests/test_gpu_node_step.py -m gpu --timeout 300 > $OUT/pytest_node.log 2>&1 ;;
