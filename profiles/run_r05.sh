@@ -62,11 +62,11 @@ for step in "$@"; do
           env $E timeout -k 10 600 python3 -u bench.py --config 4 --shard 0/8 $FAST > $OUT/bench_c4_$N.json \
             2> $OUT/bench_c4_$N.log || exit 1
         done ;;
-    ntab) for V in base:X=0 nt:MQM_NT_STORE=1 base2:X=0 nt2:MQM_NT_STORE=1; do
+    ntab) for V in base:MQM_NT_STORE=0 nt:X=0 base2:MQM_NT_STORE=0 nt2:X=0; do
           N=${V%%:*}; E=${V#*:}
           env $E timeout -k 10 400 python3 -u bench.py $FAST --ident-steps 0 > $OUT/bench_fast_$N.json 2> $OUT/bench_fast_$N.log || exit 1
         done ;;
-    c4ntab) for V in base:X=0 nt:MQM_NT_STORE=1; do
+    c4ntab) for V in base:MQM_NT_STORE=0 nt:X=0; do
           N=${V%%:*}; E=${V#*:}
           env $E timeout -k 10 600 python3 -u bench.py --config 4 --shard 0/8 $FAST --ident-steps 0 > $OUT/bench_c4_$N.json \
             2> $OUT/bench_c4_$N.log || exit 1
