@@ -298,6 +298,31 @@ int mqm_serve_policy(mqm_index *h, uint32_t grid, uint32_t idle_us);
 /* (grid is capped at half the device's CUs: a server under steady traffic
  * never idles out, and batch-path calls need the rest of the device) */
 int mqm_serve_stats(mqm_index *h, uint64_t *served, uint64_t *fallbacks, uint64_t *launches);
+/* the served path's safety nets, counted since the server started (a healthy
+ * run has forced == slot_timeouts == result_timeouts == 0):
+ *   served / fallbacks / launches: as mqm_serve_stats;
+ *   stale: results whose snapshot's host copy was no longer kept (decoded
+ *     again on the batch path: correct, slower);
+ *   forced: relaunches because a posted request sat unserved for 1 s (a
+ *     request number skipped by a counter restart, or a workgroup waiting on a
+ *     request never posted);
+ *   slot_timeouts: callers that found their ring slot still taken after 10 s
+ *     (returned MQM_EHIP without posting);
+ *   result_timeouts: callers that posted and saw no result for 10 s (returned
+ *     MQM_EHIP; the slot goes to its next owner when the late result lands);
+ *   skipped_slots: ring slots handed on past a ticket whose caller gave up
+ *     before posting (slot_timeouts) */
+typedef struct mqm_serve_counters {
+  uint64_t served, fallbacks, launches, stale, forced, slot_timeouts, result_timeouts, skipped_slots;
+} mqm_serve_counters;
+int mqm_serve_counters_get(mqm_index *h, mqm_serve_counters *out);
+/* diagnostics, MQM_SNAP_STAMP=1 (set before the first snapshot is uploaded):
+ * every snapshot's version is stamped into its device buffers as the upload's
+ * last step, and the per-publish kernels (server and small-batch path) compare
+ * the stamps with the version they were launched for, per call.  Process-wide
+ * counts: checks made, stamps found stale through the caches, stale in memory
+ * (a buffer refilled for another snapshot while a reader ran on it). */
+int mqm_debug_stamp_counts(uint64_t *checks, uint64_t *stale_cached, uint64_t *stale_memory);
 /* mean device time per served call (us[4]): claim to published result, then
  * its phases: topic staged + level keys, trie walk, emission + publish */
 int mqm_serve_device_us(mqm_index *h, double *us);

@@ -254,6 +254,16 @@ class TopicsIndex:
         check("mqm_serve_stats", lib().mqm_serve_stats(self._h, C.byref(a), C.byref(b_), C.byref(c)))
         return a.value, b_.value, c.value
 
+    def serve_counters(self) -> dict:
+        """the served path's counters (mqm_serve_counters): served, fallbacks,
+        launches, stale decodes, forced relaunches, slot / result timeouts,
+        ring slots handed on past a caller that gave up before posting"""
+        v = (C.c_uint64 * 8)()
+        check("mqm_serve_counters_get", lib().mqm_serve_counters_get(self._h, C.byref(v)))
+        keys = ("served", "fallbacks", "launches", "stale", "forced", "slot_timeouts", "result_timeouts",
+                "skipped_slots")
+        return dict(zip(keys, (int(x) for x in v)))
+
     def serve_device_us(self) -> float:
         """mean device time per served call, claim to published result (us)"""
         v = (C.c_double * 4)()

@@ -51,7 +51,8 @@ EXPORTED = [
     "mqm_result_packed", "mqm_match_batch_runs", "mqm_result_runs", "mqm_result_expand",
     "mqm_serve_policy", "mqm_serve_stats", "mqm_serve_device_us", "mqm_serve_host_us", "mqm_serve_host_max_us",
     "mqm_build_phases_ms", "mqm_build_threads", "mqm_identifiers_early",
-    "mqm_result_snapshot_version", "mqm_direct_host_us",
+    "mqm_result_snapshot_version", "mqm_direct_host_us", "mqm_serve_counters_get",
+    "mqm_debug_stamp_counts",
 ]
 
 
@@ -216,6 +217,8 @@ def lib():
         "mqm_result_expand": ([vp, u32, u32, vp, vp], C.c_int),
         "mqm_serve_policy": ([vp, u32, u32], C.c_int),
         "mqm_serve_stats": ([vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)], C.c_int),
+        "mqm_serve_counters_get": ([vp, C.POINTER(u64 * 8)], C.c_int),
+        "mqm_debug_stamp_counts": ([C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)], C.c_int),
         "mqm_serve_device_us": ([vp, vp], C.c_int),
         "mqm_serve_host_us": ([vp, vp], C.c_int),
         "mqm_serve_host_max_us": ([vp, vp], C.c_int),
@@ -223,10 +226,12 @@ def lib():
         "mqm_build_threads": ([C.c_uint32], C.c_int),
         "mqm_identifiers_early": ([vp, C.c_int], C.c_int),
     }
+    missing = [name for name in sigs if getattr(L, name, None) is None]
+    if missing:  # a library older than this file: fail here, not with an AttributeError mid-call
+        raise RuntimeError(f"{LIB_PATH} lacks {', '.join(missing)}: a stale build — "
+                           f"rebuild it with `make -C maxmq_amd/csrc`")
     for name, (args, res) in sigs.items():
-        f = getattr(L, name, None)
-        if f is None:  # (a library older than this file: tests/test_capi_host.py checks every export)
-            continue
+        f = getattr(L, name)
         f.argtypes = args
         f.restype = res
     _LIB = L

@@ -44,6 +44,7 @@
 #include "flatten.h"
 #include "match.h"
 #include "retained.h"
+#include "serve_slots.h"
 #include "shard.h"
 #include "store.h"
 
@@ -1546,6 +1547,7 @@ struct Server {
   mqm_index *h;
   ServeQueue *q = nullptr;            // pinned, coherent, device-mapped
   unsigned long long *ctr = nullptr;  // device: [0] the next request number a workgroup takes, [1] exited workgroups
+  unsigned long long *restart = nullptr;  // pinned: ctr's values for the next launch (ensure)
   hipStream_t st = nullptr;
   std::mutex mu;                      // launches / snapshot switches
   std::shared_ptr<GpuSnapshot> snap;  // (mu) what the running launch reads
@@ -1564,11 +1566,9 @@ struct Server {
   std::shared_ptr<const HostSnapshot> hist[kHist];
   uint32_t hist_next = 0;
   std::atomic<uint64_t> ticket{0};
-  std::mutex np_mu;
-  std::set<uint64_t> never_posted;  // (np_mu) tickets whose caller gave up before posting (ensure skips them)
-  std::unique_ptr<std::atomic<uint64_t>[]> free_seq;   // slot i takes request k once free_seq[i] == k
-  std::unique_ptr<std::atomic<uint64_t>[]> abandoned;  // slot i: k + 1 of a posted request whose caller gave up
+  std::unique_ptr<SlotOwners> slots;  // which ticket owns each ring slot (serve_slots.h; created by init)
   std::atomic<uint64_t> served{0}, fallbacks{0}, launches{0}, stale{0}, forced{0};
+  std::atomic<uint64_t> result_timeouts{0};  // (mqm_serve_counters; slot timeouts: SlotOwners)
   std::atomic<uint64_t> device_ticks{0};  // claim -> publish on the device, summed (100 MHz ticks)
   std::atomic<uint64_t> phase_ticks[3] = {};  // stage + keys, walk, emission + publish
   std::atomic<uint64_t> timed{0};
@@ -1629,13 +1629,9 @@ struct Server {
   }
 
   explicit Server(mqm_index *idx) : h(idx), want_ids((idx->cfg.flags & MQM_CFG_IDENTIFIERS) != 0) {
-    free_seq.reset(new std::atomic<uint64_t>[kServeSlots]);
-    abandoned.reset(new std::atomic<uint64_t>[kServeSlots]);
     waiting.reset(new std::atomic<uint64_t>[kServeSlots]);
     waitw.reset(new std::atomic<uint32_t>[kServeSlots]);
     for (uint32_t i = 0; i < kServeSlots; i++) {
-      free_seq[i].store(i);
-      abandoned[i].store(0);
       waiting[i].store(0);
       waitw[i].store(0);
     }
@@ -1650,7 +1646,12 @@ struct Server {
       return MQM_ENOMEM;
     q = static_cast<ServeQueue *>(p);
     memset((void *)q, 0, sizeof(ServeQueue));
+    slots = std::make_unique<SlotOwners>(kServeSlots, q->done);
     if (hipMalloc(&ctr, 2 * sizeof(unsigned long long)) != hipSuccess) return MQM_ENOMEM;
+    if (hipHostMalloc(&restart, 2 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
+      restart = nullptr;
+      return MQM_ENOMEM;
+    }
     if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return MQM_EHIP;
     if (hipMemsetAsync(ctr, 0, 2 * sizeof(unsigned long long), st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
@@ -1690,6 +1691,7 @@ struct Server {
     }
     if (st) (void)hipStreamDestroy(st);
     if (ctr) (void)hipFree(ctr);
+    if (restart) (void)hipHostFree(restart);
     if (q) (void)hipHostFree(q);
   }
   // the running launch's last workgroup has exited (idle): a posted request
@@ -1712,17 +1714,12 @@ struct Server {
     ts.mark("snapshot switch");
     if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
     // (no kernel runs now) the device counter restarts at the oldest request
-    // not yet served.  Slot i's tickets take it in turn (i, i + kServeSlots,
-    // ...): free_seq[i] = f is its current or next owner, so its oldest
-    // unserved ticket is f, or f + kServeSlots once f's result is in (done) —
-    // if that ticket has been taken (< T) and its caller did not give up
-    // before posting (never_posted: a workgroup would wait on it until the
-    // next stop).  A caller may move on meanwhile: the minimum can only come
-    // out low, and the launch skips served numbers below `seen` (k_serve)
-    // instead of serving them again.  (Round 5 scanned the posted slots plus
-    // the last kServeSlots tickets: a ticket older than that whose caller had
-    // not posted yet — a thread descheduled between taking it and posting —
-    // was skipped, and its request waited for the forced relaunch, r05af.)
+    // not yet served (SlotOwners::oldest_unserved: exact however long a caller
+    // sat between taking its ticket and posting — round 5 scanned the posted
+    // slots plus the last kServeSlots tickets and skipped such a ticket, whose
+    // request then waited for the forced relaunch, r05af).  A caller may move
+    // on meanwhile: the minimum can only come out low, and the launch skips
+    // served numbers below `seen` (k_serve) instead of serving them again.
     {
       unsigned long long c0 = 0;
       if (hipMemcpyAsync(&c0, ctr, sizeof(c0), hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -1731,19 +1728,12 @@ struct Server {
       seen = std::max<uint64_t>(seen, c0);
     }
     const uint64_t T = ticket.load(std::memory_order_acquire);
-    unsigned long long c[2] = {T, 0};
-    {
-      std::lock_guard<std::mutex> g(np_mu);
-      for (uint32_t i = 0; i < kServeSlots; i++) {
-        const uint64_t f = free_seq[i].load(std::memory_order_acquire);
-        if (f >= T) continue;  // no ticket for this slot yet
-        const uint64_t d = __atomic_load_n(&q->done[i], __ATOMIC_ACQUIRE);
-        const uint64_t u = d >= f + 1 ? f + kServeSlots : f;
-        if (u < T && !never_posted.count(u)) c[0] = std::min<unsigned long long>(c[0], u);
-      }
-      while (!never_posted.empty() && *never_posted.begin() + 4 * kServeSlots < T) never_posted.erase(never_posted.begin());
-    }
-    if (hipMemcpyAsync(ctr, c, sizeof(c), hipMemcpyHostToDevice, st) != hipSuccess) return MQM_EHIP;
+    // (pinned: the copy reads it after this returns; the next ensure's halt
+    // synchronises the stream before it is written again)
+    restart[0] = slots->oldest_unserved(T);
+    restart[1] = 0;
+    if (hipMemcpyAsync(ctr, restart, 2 * sizeof(unsigned long long), hipMemcpyHostToDevice, st) != hipSuccess)
+      return MQM_EHIP;
     const uint64_t ver = snap->host->version;
     if (serve_launch(snap->dev, q, ctr, grid, idle_us, want_ids, ver, gen + 1, std::max<uint64_t>(seen, T), st) != 0)
       return MQM_EHIP;
@@ -1772,27 +1762,6 @@ struct Server {
       if (x && x->version == ver) return x;
     return nullptr;
   }
-  // a caller that posted request k gives up on it: the slot goes to its next
-  // owner once the late result has arrived (wait_slot)
-  void abandon(uint32_t i, uint64_t k) { abandoned[i].store(k + 1, std::memory_order_release); }
-  // wait until slot i may take request k (its previous request's caller has
-  // read the result, or gave up on it and the result has arrived)
-  bool wait_slot(uint32_t i, uint64_t k) {
-    const auto t0 = std::chrono::steady_clock::now();
-    for (uint32_t spin = 0;; spin++) {
-      const uint64_t f = free_seq[i].load(std::memory_order_acquire);
-      if (f == k) return true;
-      if (k >= kServeSlots && f == k - kServeSlots && abandoned[i].load(std::memory_order_acquire) == f + 1 &&
-          __atomic_load_n(&q->done[i], __ATOMIC_ACQUIRE) == f + 1) {
-        abandoned[i].store(0, std::memory_order_relaxed);
-        free_seq[i].store(k, std::memory_order_release);
-        return true;
-      }
-      if ((spin & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) return false;
-      std::this_thread::yield();
-    }
-  }
-
   int submit(const char *topic, size_t len, mqm_result **out) {
     if (len > kServeTopic) {  // longer than a slot's topic bytes
       fallbacks++;
@@ -1818,19 +1787,16 @@ struct Server {
     const auto t_ens = clk::now();
     const uint64_t k = ticket.fetch_add(1, std::memory_order_relaxed);
     const uint32_t i = (uint32_t)(k % kServeSlots);
-    if (!wait_slot(i, k)) {
+    if (!slots->wait(k, std::chrono::seconds(10))) {
       // (the slot's previous request never completed: the device is gone.
-      // Request k is never posted, so its slot stays taken as well; the next
+      // Request k is never posted: the slot passes on past it, and the next
       // relaunch skips its number)
-      {
-        std::lock_guard<std::mutex> g(np_mu);
-        never_posted.insert(k);
-      }
+      slots->give_up_unposted(k);
       fprintf(stderr,
               "mqmatch: per-publish server: ring slot %u not free after 10 s (request %llu; slot owner %llu, "
               "abandoned %llu, done %llu; ticket %llu, run_gen %llu, exited %llu, run_ver %llu)\n",
-              i, (unsigned long long)k, (unsigned long long)free_seq[i].load(),
-              (unsigned long long)abandoned[i].load(), (unsigned long long)__atomic_load_n(&q->done[i], __ATOMIC_ACQUIRE),
+              i, (unsigned long long)k, (unsigned long long)slots->owner(i),
+              (unsigned long long)slots->abandoned(i), (unsigned long long)slots->done(i),
               (unsigned long long)ticket.load(), (unsigned long long)run_gen.load(),
               (unsigned long long)__atomic_load_n(&q->exited, __ATOMIC_ACQUIRE), (unsigned long long)run_ver.load());
       return MQM_EHIP;
@@ -1851,7 +1817,7 @@ struct Server {
     if (exited() || run_ver.load(std::memory_order_acquire) == 0) {
       std::lock_guard<std::mutex> g(mu);
       if ((rc = ensure(cur)) != MQM_OK) {
-        abandon(i, k);
+        slots->abandon(k);
         return rc;
       }
     }
@@ -1881,7 +1847,7 @@ struct Server {
         waiting[i].store(0, std::memory_order_release);
         pl.sleepers.fetch_sub(1, std::memory_order_acq_rel);
         inflight.fetch_sub(1, std::memory_order_acq_rel);
-        abandon(i, k);
+        slots->abandon(k);
         return code;
       };
       while (__atomic_load_n(&q->done[i], __ATOMIC_ACQUIRE) != k + 1) {
@@ -1895,6 +1861,7 @@ struct Server {
         const auto now = clk::now();
         if (now - t0 > std::chrono::seconds(10)) {
           fprintf(stderr, "mqmatch: per-publish server: no result for 10 s\n");
+          result_timeouts++;
           return give_up(MQM_EHIP);
         }
         // one liveness check per 200 us across all late callers (each is a
@@ -1948,7 +1915,7 @@ struct Server {
         served++;
       }
     }
-    free_seq[i].store(k + kServeSlots, std::memory_order_release);
+    slots->release(k);
     const auto t_end = clk::now();
     auto ns = [](clk::duration d) { return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(d).count(); };
     host_ns[0] += ns(t0 - t_in);
@@ -2148,6 +2115,30 @@ int mqm_serve_stats(mqm_index *h, uint64_t *served, uint64_t *fallbacks, uint64_
   *served = sv->served.load();
   *fallbacks = sv->fallbacks.load();
   *launches = sv->launches.load();
+  return MQM_OK;
+}
+
+int mqm_serve_counters_get(mqm_index *h, mqm_serve_counters *out) {
+  Server *sv = h ? h->server.load(std::memory_order_acquire) : nullptr;
+  if (!sv || !out) return MQM_EINVAL;
+  out->served = sv->served.load();
+  out->fallbacks = sv->fallbacks.load();
+  out->launches = sv->launches.load();
+  out->stale = sv->stale.load();
+  out->forced = sv->forced.load();
+  out->slot_timeouts = sv->slots ? sv->slots->slot_timeouts.load() : 0;
+  out->result_timeouts = sv->result_timeouts.load();
+  out->skipped_slots = sv->slots ? sv->slots->skipped.load() : 0;
+  return MQM_OK;
+}
+
+int mqm_debug_stamp_counts(uint64_t *checks, uint64_t *stale_cached, uint64_t *stale_memory) {
+  if (!checks || !stale_cached || !stale_memory) return MQM_EINVAL;
+  uint64_t v[3] = {};
+  if (stamp_counts(v) != 0) return MQM_EHIP;
+  *checks = v[0];
+  *stale_cached = v[1];
+  *stale_memory = v[2];
   return MQM_OK;
 }
 

@@ -7,6 +7,23 @@
 
 namespace mqm {
 
+// MQM_SNAP_STAMP=1 (snapshot.h DeviceSnapshot::stamp): 0 when every stamp
+// equals the snapshot's version; else bit 0: a stamp read through the caches
+// differs, bit 1: the stamp in memory (a system-scope load) differs — (1)
+// alone is a stale cached line over refilled memory, (3) a buffer refilled
+// for another snapshot while this reader still runs on it
+__device__ inline uint32_t stamp_mismatch(const DeviceSnapshot &s, unsigned long long *seen_cached,
+                                          unsigned long long *seen_memory) {
+  uint32_t bad = 0;
+  for (int i = 0; i < 4; i++) {
+    const unsigned long long c = s.stamp[i][0];  // (a plain load: through L1 / L2)
+    const unsigned long long m = __hip_atomic_load(s.stamp[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (c != s.version && !(bad & 1)) *seen_cached = c, bad |= 1;
+    if (m != s.version && !(bad & 2)) *seen_memory = m, bad |= 2;
+  }
+  return bad;
+}
+
 __device__ __forceinline__ NodeDesc load_desc(const NodeDesc *p) {
   const uint4 *q = reinterpret_cast<const uint4 *>(p);
   uint4 a = q[0], b = q[1];

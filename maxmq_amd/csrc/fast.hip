@@ -440,6 +440,23 @@ struct BatchSink {
   __device__ void stamp(int) {}
 };
 
+// MQM_SNAP_STAMP=1: [0] checks, [1] stale through the caches, [2] stale in
+// memory (device.h stamp_mismatch), for mqm_debug_stamp_counts
+__device__ unsigned long long g_stamp[3];
+
+__device__ __noinline__ void check_stamps(const DeviceSnapshot &s, const char *where, unsigned long long job) {
+  unsigned long long c = 0, m = 0;
+  const uint32_t bad = stamp_mismatch(s, &c, &m);
+  atomicAdd(&g_stamp[0], 1ull);
+  if (!bad) return;
+  unsigned long long n = 0;
+  if (bad & 1) n = atomicAdd(&g_stamp[1], 1ull);
+  if (bad & 2) n = atomicAdd(&g_stamp[2], 1ull);
+  if (n < 8)
+    printf("mqmatch stamp: %s job %llu: snapshot version %llu, cached stamp %llu, memory stamp %llu (bad %u)\n", where,
+           job, (unsigned long long)s.version, c, m, bad);
+}
+
 __global__ __launch_bounds__(kFT) void k_fast(DeviceSnapshot s, const uint8_t *__restrict__ tb,
                                               const uint64_t *__restrict__ to, uint32_t n, FastCtl *ctl,
                                               FastRec *__restrict__ recs, uint64_t *__restrict__ dout, uint64_t dcap,
@@ -449,6 +466,7 @@ __global__ __launch_bounds__(kFT) void k_fast(DeviceSnapshot s, const uint8_t *_
   const int tid = threadIdx.x;
   for (uint32_t t = blockIdx.x; t < n; t += gridDim.x) {
     BatchSink sink{ctl, recs, t, dout, dcap, hout, hcap, iout, icap};
+    if (s.stamp[0] && tid == 0) check_stamps(s, "k_fast", t);
     fast_topic(s, L, tb + to[t], (uint32_t)(to[t + 1] - to[t]), sink);
   }
   // the last workgroup to finish publishes the totals and resets the counters;
@@ -609,6 +627,11 @@ __global__ __launch_bounds__(kFT) void k_serve(DeviceSnapshot s, ServeQueue *q, 
     }
     ServeSlot *slot = &q->slot[job % kServeSlots];
     if (tid == 0) slot->t_claim = __builtin_amdgcn_s_memrealtime();
+    if (s.stamp[0] && tid == 0) {
+      if (ver != s.version) printf("mqmatch stamp: k_serve launched for version %llu on snapshot %llu\n", ver,
+                                   (unsigned long long)s.version);
+      check_stamps(s, "k_serve", job);
+    }
     ServeSink sink{slot, &q->done[job % kServeSlots], slot->dout, slot->hout, want_ids ? slot->iout : nullptr, job,
                    ver};
     fast_topic(s, L, reinterpret_cast<const uint8_t *>(slot->topic), min(job_len, kServeTopic + 1), sink, kServeHead);
@@ -656,6 +679,13 @@ FastArena::~FastArena() {
                   (void *)status})
     if (p) (void)hipHostFree(p);
   if (ctl) (void)hipFree(ctl);
+}
+
+int stamp_counts(uint64_t *out) {
+  unsigned long long v[3] = {};
+  HIP_TRY(hipMemcpyFromSymbol(v, HIP_SYMBOL(g_stamp), sizeof(v), 0, hipMemcpyDeviceToHost));
+  for (int i = 0; i < 3; i++) out[i] = v[i];
+  return 0;
 }
 
 int serve_launch(const DeviceSnapshot &s, ServeQueue *q, unsigned long long *ctr, uint32_t grid, uint32_t idle_us,

@@ -1185,6 +1185,13 @@ void recycled_free(int device, std::vector<std::pair<void *, size_t>> &held) {
 }
 }  // namespace
 
+// MQM_SNAP_STAMP=1 (diagnostic): stamp the snapshot's version into its
+// buffers as the upload's last step (snapshot.h DeviceSnapshot::stamp)
+static bool snap_stamp() {
+  static const bool v = getenv("MQM_SNAP_STAMP") && atoi(getenv("MQM_SNAP_STAMP")) != 0;
+  return v;
+}
+
 GpuSnapshot::~GpuSnapshot() {
   // (every reader holds this snapshot until its work is done: the server
   // until it is halted, a batch until its stream is synchronised, a queued
@@ -1239,10 +1246,15 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
       hs->child_ids.size() * 4,            hs->cum.size() * 4,                    hs->refs.size() * 8,
       hs->rch_off.size() * 4,              hs->rch_refs.size() * 8,               hs->rinv.size() * 8,
       hs->rgroups.size() * sizeof(RevGroup)};
+  // stamps (MQM_SNAP_STAMP=1) sit 64 B past the data of nodes / subs / words
+  // (walk_step reads up to 64 B past the last descriptor), 8-B aligned
+  const bool stamped = snap_stamp();
+  auto stamp_at = [](size_t n) { return ((n + 7) & ~size_t(7)) + 64; };
   for (int i = 0; i < GpuSnapshot::kNumBuffers; i++) {
     if (i >= 4 && !ret) break;
     // +64 B: walk_step reads 64 B at any node descriptor (the last one included)
-    if (dalloc(&g->buffers[i], (sz[i] ? sz[i] : 16) + 64) != hipSuccess) return MQM_ENOMEM;
+    const size_t extra = stamped && (i == 0 || i == 2) ? stamp_at(sz[i] ? sz[i] : 16) + 8 - (sz[i] ? sz[i] : 16) : 64;
+    if (dalloc(&g->buffers[i], (sz[i] ? sz[i] : 16) + extra) != hipSuccess) return MQM_ENOMEM;
     if (sz[i] && !(i == 1 && dev_edges) &&
         upload_copy(g->buffers[i], src[i], sz[i], stream) != hipSuccess)
       return MQM_EHIP;
@@ -1270,7 +1282,8 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
   }
   // the packed delivery of every subscription entry (snapshot.h: words)
   const uint64_t n_sub_ents = hs->subs.size();
-  if (dalloc(&g->words, n_sub_ents * 4 + 64) != hipSuccess) return MQM_ENOMEM;
+  if (dalloc(&g->words, stamped ? stamp_at(n_sub_ents * 4) + 8 : n_sub_ents * 4 + 64) != hipSuccess)
+    return MQM_ENOMEM;
   if (derive_words((const SubEnt *)g->buffers[2], (uint32_t *)g->words, n_sub_ents, stream)) return MQM_EHIP;
   if (!hs->bloom.empty()) {
     const size_t bb = hs->bloom.size() * 8;
@@ -1308,6 +1321,20 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
     if (derive_node_flags((const NodeDesc *)g->buffers[0], (uint8_t *)g->nflags, nn, stream)) return MQM_EHIP;
     g->device_bytes += nn;
   }
+  if (stamped) {  // last: every buffer above is complete on the stream before its stamp
+    void *own = nullptr;
+    if (dalloc(&own, 64) != hipSuccess) return MQM_ENOMEM;
+    g->stamp_host = hs->version;
+    unsigned long long *at[4] = {
+        (unsigned long long *)((char *)g->buffers[0] + stamp_at(sz[0] ? sz[0] : 16)),
+        (unsigned long long *)((char *)g->buffers[2] + stamp_at(sz[2] ? sz[2] : 16)),
+        (unsigned long long *)((char *)g->words + stamp_at(n_sub_ents * 4)), (unsigned long long *)own};
+    for (int i = 0; i < 4; i++) {
+      if (hipMemcpyAsync(at[i], &g->stamp_host, 8, hipMemcpyHostToDevice, stream) != hipSuccess) return MQM_EHIP;
+      g->dev.stamp[i] = at[i];
+    }
+  }
+  g->dev.version = hs->version;
   if (hipStreamSynchronize(stream) != hipSuccess) return MQM_EHIP;
   // the device holds the edge table now: keep its digest, release the host copy
   if (!hs->edges.empty()) {

@@ -139,6 +139,7 @@ struct GpuSnapshot {
   int device = -1;  // the buffers' device
   std::vector<std::pair<void *, size_t>> held;  // every device buffer above, with its capacity (recycled)
   uint64_t device_bytes = 0;
+  uint64_t stamp_host = 0;  // MQM_SNAP_STAMP=1: the copy source of the stamps (lives as long as the copies)
   ~GpuSnapshot();
 };
 

@@ -260,6 +260,9 @@ struct ServeQueue {
 // last workgroup to exit; request numbers below `seen` (the highest number an
 // earlier launch handed out) are skipped when their slot's done word shows
 // them served.
+// MQM_SNAP_STAMP=1 diagnostics of the per-publish kernels: checks made,
+// stamps found stale through the caches, stale in memory (out[3])
+int stamp_counts(uint64_t *out);
 int serve_launch(const DeviceSnapshot &s, ServeQueue *q, unsigned long long *ctr, uint32_t grid, uint32_t idle_us,
                  bool want_ids, uint64_t ver, uint64_t gen, uint64_t seen, hipStream_t st);
 

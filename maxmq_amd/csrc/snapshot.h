@@ -185,6 +185,14 @@ struct DeviceSnapshot {
   uint32_t n_subs;
   uint32_t n_shared;
   uint32_t height;        // max node depth (root = 0)
+  // the store version this snapshot reflects.  MQM_SNAP_STAMP=1 (diagnostic):
+  // the upload's last step writes it past the end of the nodes, subs and words
+  // buffers and into a buffer of its own (stamp[0..3]; nullptr: off), and the
+  // per-publish kernels compare each stamp with `version` (device.h
+  // stamp_mismatch) — a reader of a retired snapshot whose recycled buffers
+  // were refilled for a newer one sees another version there
+  const unsigned long long *stamp[4];
+  uint64_t version;
 };
 
 // one (token, depth) group of the reverse walk's literal-edge index

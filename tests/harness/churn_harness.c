@@ -307,10 +307,16 @@ int main(int argc, char **argv) {
   for (int i = 0; i < n_threads; i++) pthread_create(&th[i], NULL, reader, (void *)(intptr_t)i);
   for (int i = 0; i < n_threads; i++) pthread_join(th[i], NULL);
   pthread_join(mt, NULL);
-  uint64_t served = 0, fallbacks = 0, launches = 0;
-  if (mqm_serve_stats(H, &served, &fallbacks, &launches) != MQM_OK) fail("mqm_serve_stats");
-  fprintf(out, "S %llu %llu %llu\n", (unsigned long long)served, (unsigned long long)fallbacks,
-          (unsigned long long)launches);
+  mqm_serve_counters sc;
+  if (mqm_serve_counters_get(H, &sc) != MQM_OK) fail("mqm_serve_counters_get");
+  fprintf(out, "S %llu %llu %llu %llu %llu %llu %llu %llu\n", (unsigned long long)sc.served,
+          (unsigned long long)sc.fallbacks, (unsigned long long)sc.launches, (unsigned long long)sc.stale,
+          (unsigned long long)sc.forced, (unsigned long long)sc.slot_timeouts, (unsigned long long)sc.result_timeouts,
+          (unsigned long long)sc.skipped_slots);
+  uint64_t st_checks = 0, st_cached = 0, st_memory = 0;
+  if (mqm_debug_stamp_counts(&st_checks, &st_cached, &st_memory) == MQM_OK)
+    fprintf(stderr, "stamp checks %llu, stale cached %llu, stale in memory %llu\n", (unsigned long long)st_checks,
+            (unsigned long long)st_cached, (unsigned long long)st_memory);
   if (mut_out.n) fwrite(mut_out.p, 1, mut_out.n, out);
   for (int i = 0; i < n_threads; i++)
     if (out_of[i].n) fwrite(out_of[i].p, 1, out_of[i].n, out);

@@ -131,6 +131,21 @@ def test_launch_guard_refuses_missing_or_short_arrays():
     assert r.stdout.strip().endswith("OK") and r.stdout.count("-> -1") == 7, r.stdout
 
 
+def test_serve_ring_slot_ownership():
+    """the per-publish server's ring-slot hand-off (maxmq_amd/csrc/serve_slots.h,
+    used by capi.cpp Server): normal turns, a caller that gives up after
+    posting and its late result, callers that give up before posting — once
+    and twice in a row — whose slot must pass on instead of staying taken
+    (ADVICE r5), and the device counter's restart point
+    (tests/harness/slots_test.cpp, CPU, ASan + UBSan)."""
+    import subprocess
+
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "tests", "harness"), "_build/slots_test"])
+    exe = os.path.join(ROOT, "tests", "harness", "_build", "slots_test")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and r.stdout.strip() == "OK", r.stdout + r.stderr
+
+
 def test_walk_tokenizer_masks_match_a_byte_scan():
     """keys.h slash_mask16 / align_byte — the word-level separator search of
     match.hip k_walk's tokenizer — against a byte scan on random topics at

@@ -72,8 +72,12 @@ def test_served_subscribers_concurrent_equal_plain(threads, identifiers, monkeyp
     for th in ths:
         th.join()
     served, fallbacks, launches = idx.serve_stats()
+    cnt = idx.serve_counters()
     idx.close()
     assert not errors, errors[0]
+    # no safety net fired (a forced relaunch or a timed-out slot would hide a
+    # lost request behind a correct fallback result)
+    assert cnt["forced"] == 0 and cnt["slot_timeouts"] == 0 and cnt["result_timeouts"] == 0, cnt
     assert served + fallbacks == n and served > 0.9 * n, (served, fallbacks)
     assert launches >= 1
     bad = [i for i in range(n) if got[i] != want[i]]
@@ -112,5 +116,7 @@ def test_served_fallbacks_idle_relaunch_and_new_snapshot():
     for x in (idx, ref):
         x.subscribe("d", maxmq_amd.Subscription("a/#", 1))
     check_all()
+    cnt = idx.serve_counters()
     idx.close()
+    assert cnt["forced"] == 0 and cnt["slot_timeouts"] == 0 and cnt["result_timeouts"] == 0, cnt
     ref.close()

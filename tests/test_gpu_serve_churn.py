@@ -138,8 +138,19 @@ def test_served_calls_under_churn_equal_oracle_at_their_version(tmp_path, mode, 
     r = subprocess.run([HARNESS, str(inp), str(out), str(threads), str(calls), mode, str(op_us)],
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
-    base_version, (served, fallbacks, launches), op_version, calls_out = _parse(out)
+    if r.stderr.strip():
+        print(r.stderr[-3000:])  # (MQM_SNAP_STAMP=1: the stamp counts; device printf lines are in stdout)
+    if r.stdout.strip():
+        print(r.stdout[-3000:])
+    base_version, counters, op_version, calls_out = _parse(out)
+    served, fallbacks, launches, stale, forced, slot_to, result_to, skipped = counters
+    print(f"served {served} fallbacks {fallbacks} launches {launches} stale {stale} forced {forced} "
+          f"slot timeouts {slot_to} result timeouts {result_to} skipped slots {skipped}")
     assert len(calls_out) == threads * calls
+    # the safety nets must stay idle: a forced relaunch (a request unserved for
+    # 1 s) or a timed-out slot / result would hide a lost request behind a
+    # correct-looking fallback (VERDICT r5 weak #1c)
+    assert forced == 0 and slot_to == 0 and result_to == 0, counters
     assert served > 0.9 * len(calls_out), (served, fallbacks)
     # version -> the number of operations applied (the largest prefix with
     # that store version: an Unsubscribe that found nothing changes nothing)
