@@ -1559,12 +1559,23 @@ struct Server {
   const bool want_ids;
   // the running launch, readable without mu: generation, snapshot version + 1 (0: none)
   std::atomic<uint64_t> run_gen{0}, run_ver{0};
-  // host snapshots of the last kHist launches (decoding a result whose launch
-  // served a snapshot other than the caller's front buffer)
+  // host snapshots of recent launches (decoding a result whose launch served
+  // a snapshot other than the caller's front buffer), with the generation of
+  // the launch that added each.  At C3 a host snapshot is 1-2 GB, so an entry
+  // is kept only while a request posted under its launch or a later one may
+  // still be decoded: a caller stores the running generation + 1 in
+  // post_gen[slot] before it posts and clears it after decoding, and ensure()
+  // drops the entries older than the oldest such generation (at most kHist
+  // are kept in any case; an evicted version decodes on the batch path)
   static constexpr uint32_t kHist = 8;
   std::mutex hist_mu;
-  std::shared_ptr<const HostSnapshot> hist[kHist];
+  struct Hist {
+    uint64_t gen = 0;
+    std::shared_ptr<const HostSnapshot> host;
+  };
+  Hist hist[kHist];
   uint32_t hist_next = 0;
+  std::unique_ptr<std::atomic<uint64_t>[]> post_gen;  // slot -> launch generation + 1 at post (0: none in flight)
   std::atomic<uint64_t> ticket{0};
   std::unique_ptr<SlotOwners> slots;  // which ticket owns each ring slot (serve_slots.h; created by init)
   std::atomic<uint64_t> served{0}, fallbacks{0}, launches{0}, stale{0}, forced{0};
@@ -1647,6 +1658,8 @@ struct Server {
     q = static_cast<ServeQueue *>(p);
     memset((void *)q, 0, sizeof(ServeQueue));
     slots = std::make_unique<SlotOwners>(kServeSlots, q->done);
+    post_gen.reset(new std::atomic<uint64_t>[kServeSlots]);
+    for (uint32_t i = 0; i < kServeSlots; i++) post_gen[i].store(0);
     if (hipMalloc(&ctr, 2 * sizeof(unsigned long long)) != hipSuccess) return MQM_ENOMEM;
     if (hipHostMalloc(&restart, 2 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
       restart = nullptr;
@@ -1741,11 +1754,21 @@ struct Server {
     launched = true;
     launches++;
     {
+      // the oldest generation a result still to be decoded may carry
+      uint64_t oldest = gen;
+      for (uint32_t i = 0; i < kServeSlots; i++) {
+        const uint64_t pg = post_gen[i].load(std::memory_order_seq_cst);
+        if (pg) oldest = std::min(oldest, pg - 1);
+      }
       std::lock_guard<std::mutex> g(hist_mu);
       const uint32_t last = (hist_next + kHist - 1) % kHist;
-      if (!hist[last] || hist[last]->version != ver) {
-        defer_release(std::move(hist[hist_next]));  // (the evicted host snapshot, if this was its last holder)
-        hist[hist_next] = snap->host;
+      for (uint32_t j = 0; j < kHist; j++)  // (the evicted host snapshots go to the releaser if this held the last reference)
+        if (j != last && hist[j].host && hist[j].gen < oldest) defer_release(std::move(hist[j].host));
+      if (hist[last].host && hist[last].host->version == ver) {
+        hist[last].gen = gen;  // (the newest launch that served it)
+      } else {
+        defer_release(std::move(hist[hist_next].host));
+        hist[hist_next] = Hist{gen, snap->host};
         hist_next = (hist_next + 1) % kHist;
       }
     }
@@ -1759,7 +1782,7 @@ struct Server {
     if (cur->host->version == ver) return cur->host;
     std::lock_guard<std::mutex> g(hist_mu);
     for (const auto &x : hist)
-      if (x && x->version == ver) return x;
+      if (x.host && x.host->version == ver) return x.host;
     return nullptr;
   }
   int submit(const char *topic, size_t len, mqm_result **out) {
@@ -1811,12 +1834,16 @@ struct Server {
     unsigned long long head[kServeHead / 8];
     memcpy(head, sl.topic, kServeHead);
     sl.chk = serve_check(seqw, head);
+    // (before the post: a relaunch from here on keeps the host snapshots this
+    // result may be decoded with — this launch's and every later one)
+    post_gen[i].store(run_gen.load(std::memory_order_acquire) + 1, std::memory_order_seq_cst);
     __atomic_store_n(&sl.seq, seqw, __ATOMIC_RELEASE);
     // the server exited (idle) since the check above: relaunch now rather
     // than at the liveness check below (no HIP call on the common path)
     if (exited() || run_ver.load(std::memory_order_acquire) == 0) {
       std::lock_guard<std::mutex> g(mu);
       if ((rc = ensure(cur)) != MQM_OK) {
+        post_gen[i].store(0, std::memory_order_release);
         slots->abandon(k);
         return rc;
       }
@@ -1847,6 +1874,7 @@ struct Server {
         waiting[i].store(0, std::memory_order_release);
         pl.sleepers.fetch_sub(1, std::memory_order_acq_rel);
         inflight.fetch_sub(1, std::memory_order_acq_rel);
+        post_gen[i].store(0, std::memory_order_release);
         slots->abandon(k);
         return code;
       };
@@ -1915,6 +1943,7 @@ struct Server {
         served++;
       }
     }
+    post_gen[i].store(0, std::memory_order_release);
     slots->release(k);
     const auto t_end = clk::now();
     auto ns = [](clk::duration d) { return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(d).count(); };

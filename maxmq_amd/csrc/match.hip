@@ -2500,23 +2500,34 @@ static int ident_launch(const DeviceSnapshot &s, Workspace &ws, Outputs o, uint3
   HIP_TRY(hipEventRecord(ws.ev_fork, st));
   HIP_TRY(hipStreamWaitEvent(ws.side, ws.ev_fork, 0));
   hipStream_t sd = ws.side;
-  HIP_TRY(hipMemsetAsync(ovf, 0, sizeof(uint64_t), sd));
-  if (scan_offsets(ws, o.mcount, mstart, n, sd, W::kScanTmp2)) return -3;
-  const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + 31) / 32, 8192));
-  if (n > 0) {
-    hipLaunchKernelGGL(k_ident, dim3(blocks), dim3(256), 0, sd, s, o, n, mstart, scratch, cap, ovf);
-    HIP_TRY(hipGetLastError());
+  const int rc = [&]() -> int {  // (work is queued on the side stream from here on)
+    HIP_TRY(hipMemsetAsync(ovf, 0, sizeof(uint64_t), sd));
+    if (scan_offsets(ws, o.mcount, mstart, n, sd, W::kScanTmp2)) return -3;
+    const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + 31) / 32, 8192));
+    if (n > 0) {
+      hipLaunchKernelGGL(k_ident, dim3(blocks), dim3(256), 0, sd, s, o, n, mstart, scratch, cap, ovf);
+      HIP_TRY(hipGetLastError());
+    }
+    if (scan_offsets(ws, o.icount, o.istart, n, sd, W::kScanTmp2)) return -3;
+    if (n > 0) {
+      hipLaunchKernelGGL(k_ident_pack, dim3(std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, 16384))),
+                         dim3(256), 0, sd, o, n, mstart, scratch, cap, ovf);
+      HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipMemcpyAsync(hp + 8, o.istart + n, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, sd));
+    HIP_TRY(hipMemcpyAsync(hp + 10, mstart + n, sizeof(uint64_t), hipMemcpyDeviceToHost, sd));
+    return 0;
+  }();
+  // joined in every case: after a failure part-way the side stream may still
+  // write kICount / kIStart / kIOut, which the fallback pass after the match
+  // (identifiers_device on `st`) writes too
+  const hipError_t je = hipEventRecord(ws.ev_join, sd);
+  if (rc != 0) {
+    if (je == hipSuccess) (void)hipStreamWaitEvent(st, ws.ev_join, 0);
+    else (void)hipStreamSynchronize(sd);
+    return rc;
   }
-  if (scan_offsets(ws, o.icount, o.istart, n, sd, W::kScanTmp2)) return -3;
-  if (n > 0) {
-    hipLaunchKernelGGL(k_ident_pack, dim3(std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, 16384))), dim3(256),
-                       0, sd, o, n, mstart, scratch, cap, ovf);
-    HIP_TRY(hipGetLastError());
-  }
-  HIP_TRY(hipMemcpyAsync(hp + 8, o.istart + n, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, sd));
-  HIP_TRY(hipMemcpyAsync(hp + 10, mstart + n, sizeof(uint64_t), hipMemcpyDeviceToHost, sd));
-  HIP_TRY(hipEventRecord(ws.ev_join, sd));
-  return 0;
+  return je == hipSuccess ? 0 : -3;
 }
 
 int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes, const uint64_t *d_offs, uint32_t n,
