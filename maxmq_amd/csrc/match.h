@@ -107,6 +107,10 @@ struct Workspace {
   // only collects.  ident_cap: the scratch / iout capacity (grown from the
   // multi entries a call reported)
   bool ident_early = false, ident_ready = false;
+  // ident_fused: the last enqueued call listed Identifiers in its merges
+  // (match.hip ident_base; the default form of ident_early, MQM_IDENT_FUSED=0
+  // for the side-stream pass); its totals come back with the call's counters
+  bool ident_fused = false;
   uint64_t ident_cap = 0;
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;

@@ -154,6 +154,10 @@ struct Counters {              // zeroed before every batch
   unsigned long long n_solo;                    // solo entries the walk copied
   unsigned long long tab_total, dfs_raw, dfs_h; // DFS: dedupe table, raw entries, shared candidates
   unsigned long long d_sum, h_sum;              // deliveries, shared candidates (after dedupe)
+  // Identifiers listed by the merges (Outputs::iscratch): total listed, total
+  // multi entries (the scratch areas' extent), a scratch area or the packed
+  // list past its capacity (then identifiers_device runs its own pass)
+  unsigned long long i_total, i_multi, i_ovf;
 #if MQM_WALK_STATS
   unsigned long long st_probe, st_miss, st_desc;
 #endif
@@ -175,6 +179,13 @@ struct Outputs {
   uint32_t *icount;
   uint64_t *istart;
   uint32_t *iout;
+  // Identifiers listed by the merges themselves (nullptr: not listed): each
+  // merge writes the sids of a topic's multi entries with Identifier > 0 to
+  // iscratch[imstart[t] ..) (imstart: the scan of mcount, so a topic's area
+  // holds all its multi entries) and their count to icount[t]; capacity icap
+  uint64_t *imstart;
+  uint32_t *iscratch;
+  uint64_t icap;
   // capacities of dout / hout in entries: every store is checked against them
   // (a wrong offset becomes a reported error, never an out-of-bounds write)
   uint64_t dcap, hcap;
@@ -344,6 +355,33 @@ __device__ __forceinline__ void rec_prefix(uint32_t *rec, uint32_t nh, int gl) {
 // 1 + h = multi part h)
 __device__ __forceinline__ const uint4 *rec_tail(const uint32_t *recs, uint32_t t) {
   return reinterpret_cast<const uint4 *>(recs + ((uint64_t)t + 1) * kRecStrideAlloc) - 1;
+}
+
+// ---- Identifiers listed by the merges (Outputs::iscratch; packets.go:257-259)
+// A merge reads every multi entry of its topic anyway, so it lists the ones
+// whose Identifier is > 0 as it goes, in entry order (the order k_ident used:
+// part by part), instead of a pass of its own over the records (k_ident: 3.6
+// ms on C3, r05z).  A solo entry is its client's only one in the topic, so its
+// map is its first pair, which its delivery already names (see k_ident).
+// The topic's scratch base, or ~0 when listing is off or its area would pass
+// the capacity (flagged: identifiers_device then runs the separate pass).
+__device__ __forceinline__ uint64_t ident_base(const Outputs &o, uint32_t t, uint32_t M, bool leader) {
+  if (!o.iscratch) return ~0ull;
+  const uint64_t ib = o.imstart[t];
+  if (ib + M > o.icap) {
+    if (leader) atomicOr(&o.ctr->i_ovf, 1ull);
+    return ~0ull;
+  }
+  return ib;
+}
+// a kE-lane group lists the entries with `has` set at ib + nid .. in lane order
+template <int kE>
+__device__ __forceinline__ void ident_put(const Outputs &o, uint64_t ib, bool has, uint32_t sid, int gbase,
+                                          uint64_t glt, uint32_t &nid) {
+  constexpr uint64_t kGMask = kE == 64 ? ~0ull : (1ull << kE) - 1ull;
+  const uint64_t m = (__ballot(has) >> gbase) & kGMask;
+  if (has) o.iscratch[ib + nid + __popcll(m & glt)] = sid;
+  nid += (uint32_t)__popcll(m);
 }
 
 
@@ -1266,14 +1304,16 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
     t_nn = i + 2 * ngroups < nl ? list[i + 2 * ngroups] : 0;
     wave_lds_sync();
     const uint32_t nh = L.rec[0] & 0xFFu, Ss = L.rec[1], M = L.rec[2];
+    const uint64_t ib = ident_base(o, t, M, gl == 0);
     rec_prefix<kSE, kSmallHits>(L.rec, nh, gl);
     wave_lds_sync();
-    uint32_t mcl[kMPer], mw[kMPer], mrk[kMPer];
+    uint32_t mcl[kMPer], mw[kMPer], mrk[kMPer], msid[kMPer];
 #pragma unroll
     for (int k = 0; k < kMPer; k++) {
       const uint32_t q = gl + k * kSE;
       uint32_t h;
       const uint32_t sid = multi_sid(L.rec, nh, q < M ? q : 0, &h);
+      msid[k] = sid;
       mrk[k] = rec_at(L.rec, h, kFieldRank);
       const SubEnt e = load_sub(s, sid);
       mcl[k] = e.client;
@@ -1282,6 +1322,14 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
     const uint32_t D = merge_multi<kSE, kMPer>(MergeTable{L.tkb, L.tfirst}, kSmallTab, mcl, mw, mrk, M, gl,
                                                gbase, o.dout, db, Ss, o.dcap, &o.ctr->oob);
     if (gl == 0) o.dcount[t] = D;
+    if (o.iscratch) {  // (wave-uniform: every group runs the ballots)
+      uint32_t nid = 0;
+      const uint64_t glt = (1ull << gl) - 1ull;
+#pragma unroll
+      for (int k = 0; k < kMPer; k++)
+        ident_put<kSE>(o, ib, ib != ~0ull && gl + k * kSE < M && (mw[k] & kWordIdent), msid[k], gbase, glt, nid);
+      if (gl == 0 && ib != ~0ull) o.icount[t] = nid;
+    }
     wave_lds_sync();
   }
 }
@@ -1319,17 +1367,19 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_merge(DeviceSnapshot s, O
     if (i + nw < nl) fetch(i + nw);
     wave_lds_sync();
     const uint32_t nh = L.rec[0] & 0xFFu, Ss = L.rec[1], M = L.rec[2];
+    const uint64_t ib = ident_base(o, t, M, lane == 0);
     const uint4 *gt = rec_tail(o.recs, t);
     for (uint32_t u = 16 + lane; u < 1 + nh; u += kWave) rec4[u] = gt[-(int)u];
     wave_lds_sync();
     rec_prefix<kWave>(L.rec, nh, lane);
     wave_lds_sync();
-    uint32_t mcl[kMPer], mw[kMPer], mrk[kMPer];
+    uint32_t mcl[kMPer], mw[kMPer], mrk[kMPer], msid[kMPer];
 #pragma unroll
     for (int k = 0; k < kMPer; k++) {
       const uint32_t q = lane + k * kWave;
       uint32_t h;
       const uint32_t sid = multi_sid(L.rec, nh, q < M ? q : 0, &h);
+      msid[k] = sid;
       mrk[k] = rec_at(L.rec, h, kFieldRank);
       const SubEnt e = load_sub(s, sid);
       mcl[k] = e.client;
@@ -1339,6 +1389,13 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_merge(DeviceSnapshot s, O
         merge_multi<kWave, kMPer>(MergeTable{L.tkb, L.tfirst}, kSmallSlots, mcl, mw, mrk, M, lane, 0,
                                   o.dout, db, Ss, o.dcap, &o.ctr->oob);
     if (lane == 0) o.dcount[t] = D;
+    if (ib != ~0ull) {  // (wave-uniform)
+      uint32_t nid = 0;
+#pragma unroll
+      for (int k = 0; k < kMPer; k++)
+        ident_put<kWave>(o, ib, lane + k * kWave < M && (mw[k] & kWordIdent), msid[k], 0, lanemask_lt(lane), nid);
+      if (lane == 0) o.icount[t] = nid;
+    }
     wave_lds_sync();
   }
 }
@@ -1419,6 +1476,39 @@ __device__ __forceinline__ uint32_t block_winners(MergeTable tb, uint32_t nslots
   return total;
 }
 
+// the workgroup merges' Identifiers listing (Outputs::iscratch): a pass over
+// the topic's multi entries after its merge, 256 at a time, placed in entry
+// order by a block prefix of the waves' ballots (wsum: the winners' scratch)
+__device__ __forceinline__ void block_ident(const DeviceSnapshot &s, Outputs o, uint32_t t, uint32_t nh, uint32_t M,
+                                            const uint32_t *rec, uint32_t *wsum) {
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+  constexpr int kW = kBigThreads / kWave;
+  const uint64_t ib = ident_base(o, t, M, tid == 0);
+  if (ib == ~0ull) return;  // (block-uniform)
+  uint32_t nid = 0;
+  for (uint32_t q0 = 0; q0 < M; q0 += kBigThreads) {
+    const uint32_t q = q0 + tid;
+    uint32_t h, sid = 0;
+    bool has = false;
+    if (q < M) {
+      sid = multi_sid(rec, nh, q, &h);
+      has = (s.ident_bits[sid >> 5] >> (sid & 31)) & 1u;
+    }
+    const uint64_t m = __ballot(has);
+    if (lane == 0) wsum[wid] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t w = nid, tot = 0;
+    for (int k = 0; k < kW; k++) {
+      if (k < wid) w += wsum[k];
+      tot += wsum[k];
+    }
+    if (has) o.iscratch[ib + w + __popcll(m & lanemask_lt(lane))] = sid;
+    nid += tot;
+    __syncthreads();
+  }
+  if (tid == 0) o.icount[t] = nid;
+}
+
 template <int kSlots>
 __global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs o, const uint32_t *__restrict__ list,
                                                       const unsigned int *__restrict__ count) {
@@ -1450,6 +1540,7 @@ __global__ __launch_bounds__(kBigThreads) void k_multi(DeviceSnapshot s, Outputs
     __syncthreads();
     const uint32_t D = block_winners(tb, mask + 1, L.wsum, o, db, Ss);
     if (tid == 0) o.dcount[t] = D;
+    if (o.iscratch) block_ident(s, o, t, nh, M, L.rec, L.wsum);
   }
 }
 
@@ -1502,6 +1593,7 @@ __global__ __launch_bounds__(kBigThreads) void k_multi_part(DeviceSnapshot s, Ou
       D = block_winners(tb, kSlots, L.wsum, o, db, D);
     }
     if (tid == 0) o.dcount[t] = D;
+    if (o.iscratch) block_ident(s, o, t, nh, M, L.rec, L.wsum);
   }
 }
 
@@ -1626,6 +1718,8 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_resolve(DeviceSnapshot s,
     if (i_next < nl) fetch(i_next);
     wave_lds_sync();
     const uint32_t nh = L.rec[0] & 0xFFu, Ss = L.rec[1], M = L.rec[2];
+    const uint64_t ib = ident_base(o, t, M, gl == 0);
+    uint32_t nid = 0;
     // the gathered multi parts by their range's multi-tail start (a node's
     // range is gathered at most once per topic: distinct keys)
     for (uint32_t h = gl; h < nh; h += kE) {
@@ -1639,7 +1733,7 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_resolve(DeviceSnapshot s,
     wave_lds_sync();
     uint32_t D = 0;
     for (uint32_t q0 = 0; q0 < M; q0 += kE * kPer) {
-      uint32_t sid[kPer], rk[kPer], wd[kPer];
+      uint32_t sid[kPer], rk[kPer], wd[kPer], iw[kPer];
       uint2 pi[kPer];
 #pragma unroll
       for (int k = 0; k < kPer; k++) {  // every entry's loads in flight together
@@ -1649,6 +1743,14 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_resolve(DeviceSnapshot s,
         rk[k] = rec_at(L.rec, h, kFieldRank);
         wd[k] = s.words[sid[k]];
         pi[k] = s.pinfo[sid[k]];
+        iw[k] = o.iscratch ? s.ident_bits[sid[k] >> 5] : 0u;  // (1.25 MB at C3: L2)
+      }
+      if (o.iscratch) {  // (wave-uniform)
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+          const uint32_t q = q0 + k * kE + gl;
+          ident_put<kE>(o, ib, ib != ~0ull && q < M && ((iw[k] >> (sid[k] & 31)) & 1u), sid[k], gbase, glt, nid);
+        }
       }
 #pragma unroll
       for (int k = 0; k < kPer; k++) {
@@ -1685,6 +1787,7 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_resolve(DeviceSnapshot s,
       }
     }
     if (gl == 0) o.dcount[t] = Ss + D;
+    if (gl == 0 && ib != ~0ull) o.icount[t] = nid;
     wave_lds_sync();
   }
 }
@@ -2530,6 +2633,13 @@ static int ident_launch(const DeviceSnapshot &s, Workspace &ws, Outputs o, uint3
   return je == hipSuccess ? 0 : -3;
 }
 
+// MQM_IDENT_FUSED=0: Identifiers by the separate pass beside the match
+// (ident_launch, round 5) instead of listed by the merges
+static bool ident_fused_on() {
+  static const bool v = !getenv("MQM_IDENT_FUSED") || atoi(getenv("MQM_IDENT_FUSED")) != 0;
+  return v;
+}
+
 int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes, const uint64_t *d_offs, uint32_t n,
                   hipStream_t st, bool exact) {
   using W = Workspace;
@@ -2584,7 +2694,23 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
   HIP_TRY(hipGetLastError());
   mark(ws, 1, st);
   ws.ident_ready = false;
-  if (ws.ident_early && !ws.runs && ident_launch(s, ws, o, n, st) == 0) ws.ident_ready = true;
+  ws.ident_fused = false;
+  const bool fuse_ids = ws.ident_early && !ws.runs && ident_fused_on();
+  if (fuse_ids) {
+    // Identifiers listed by the merges: every count starts at 0 (topics
+    // without multi entries, DFS topics), each topic's scratch area at the
+    // scan of the multi counts; its extent comes back with the exact
+    // read-back below and sizes the scratch
+    if (ws.get(W::kIMStart, sizeof(uint64_t) * (n + 1)) || ws.get(W::kICount, sizeof(uint32_t) * (n + 1)))
+      return -2;
+    o.imstart = (uint64_t *)ws.ptr(W::kIMStart);
+    o.icount = (uint32_t *)ws.ptr(W::kICount);
+    HIP_TRY(hipMemsetAsync(o.icount, 0, sizeof(uint32_t) * (n + 1), st));
+    if (scan_offsets(ws, o.mcount, o.imstart, n, st)) return -3;
+    HIP_TRY(hipMemcpyAsync(&o.ctr->i_multi, o.imstart + n, sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
+  } else if (ws.ident_early && !ws.runs && ident_launch(s, ws, o, n, st) == 0) {
+    ws.ident_ready = true;
+  }
   // segment starts: exclusive scans of S (raw entries, an upper bound of a
   // topic's deliveries) and H (shared candidates); the solo descriptors'
   // positions: exclusive scan of the solo-part counts
@@ -2662,6 +2788,16 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
   if (ws.get(W::kDOut, sizeof(uint32_t) * (dcap + 1)) || ws.get(W::kHOut, sizeof(uint32_t) * (hcap + 1)) ||
       ws.get(W::kDesc, sizeof(uint4) * (desc_cap + 1)) || ws.get(W::kWin, sizeof(uint32_t) * (win_cap + 1)))
     return -2;
+  if (fuse_ids) {  // the scratch and the packed list: at most one sid per multi entry
+    const uint64_t icap = exact ? hc->i_multi : std::max<uint64_t>(ws.ident_cap, 4ull * n + 4096);
+    if (ws.get(W::kIScratch, sizeof(uint32_t) * (icap + 1)) || ws.get(W::kIOut, sizeof(uint32_t) * (icap + 1)) ||
+        ws.get(W::kIStart, sizeof(uint64_t) * (n + 2)))
+      return -2;
+    o.iscratch = (uint32_t *)ws.ptr(W::kIScratch);
+    o.iout = (uint32_t *)ws.ptr(W::kIOut);
+    o.istart = (uint64_t *)ws.ptr(W::kIStart);
+    o.icap = icap;
+  }
   o.dout = (uint32_t *)ws.ptr(W::kDOut);
   o.hout = (uint32_t *)ws.ptr(W::kHOut);
   o.dcap = dcap;
@@ -2812,6 +2948,16 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
                        tab_off, tab, max_levels);
     HIP_TRY(hipGetLastError());
   }
+  if (fuse_ids) {  // the merges' lists, packed in topic order (DFS topics: identifiers_device)
+    if (scan_offsets(ws, o.icount, o.istart, n, st)) return -3;
+    if (n > 0) {
+      hipLaunchKernelGGL(k_ident_pack, dim3(std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, 16384))),
+                         dim3(256), 0, st, o, n, o.imstart, o.iscratch, o.icap, &o.ctr->i_ovf);
+      HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipMemcpyAsync(&o.ctr->i_total, o.istart + n, sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
+    ws.ident_fused = true;
+  }
   mark(ws, 3, st);
   // the identifiers pass beside the match: joined here, so the read-back's
   // synchronisation covers it (and the next call's buffers wait for it)
@@ -2957,6 +3103,20 @@ int identifiers_device(const DeviceSnapshot &s, Workspace &ws, hipStream_t st, I
   using W = Workspace;
   const uint32_t n = ws.last_n;
   if (!ws.last_valid) return -1;
+  if (ws.ident_fused) {  // listed by the merges (the collect synchronised the call)
+    ws.ident_fused = false;
+    const Counters *hc = pinned_counters(ws);
+    if (!hc) return -2;
+    ws.ident_cap = std::max<uint64_t>(ws.ident_cap, hc->i_multi + hc->i_multi / 4 + 1024);
+    if (!hc->i_ovf && ws.last_n_dfs == 0 && !ws.last_runs) {
+      out->n_topics = n;
+      out->n_idents = hc->i_total;
+      out->offsets = (const uint64_t *)ws.ptr(W::kIStart);
+      out->sids = (const uint32_t *)ws.ptr(W::kIOut);
+      return 0;
+    }
+    // (a capacity passed, or DFS topics, whose sids k_dfs<3|4> list: the pass below)
+  }
   if (ws.ident_ready) {  // computed beside the match (ident_launch; the collect synchronised the join)
     ws.ident_ready = false;
     const uint64_t *hp = ws.pinned_u64();
