@@ -650,9 +650,14 @@ def host_path(idx, w, args, form="runs"):
     L.mqm_result_free(res)
     out_per_batch = 8 * n_runs + 4 * win + 4 * sh + (24 if form == "runs" else 16) * per
     legs = {}
+    ph = (C.c_double * 6)()
     for consume, name in ((0, "to_host"), (1, "iterate"), (2, "expand")):
+        L.mqm_batch_host_us(idx._h, ph)  # (reset)
         dt, nd = run(nb, consume)
         legs[name] = {"value": nb * per / dt, "deliveries_per_s": nd / dt, "ms_per_call": dt * 1e3 * args.host_threads / nb}
+        if L.mqm_batch_host_us(idx._h, ph) == 0:  # where a call's time goes (mean us per phase)
+            legs[name]["phases_us"] = dict(zip(("front_ctx", "h2d", "match", "runs_densify", "d2h_sync"),
+                                               (round(ph[i], 1) for i in range(5))))
     # link rates: 1 GiB pinned <-> device, each direction alone
     dev = torch.device("cuda", torch.cuda.current_device())
     g = torch.empty(1 << 30, dtype=torch.uint8, device=dev)

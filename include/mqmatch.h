@@ -344,6 +344,13 @@ int mqm_batching_stats(mqm_index *h, uint64_t *batches, uint64_t *topics);
  * context from the pool, launch + wait for the kernel, result block — then the
  * maximum of each phase, then the number of calls */
 int mqm_direct_host_us(mqm_index *h, double *us);
+/* host-path calls through the batch pipeline (mqm_match_batch / _packed /
+ * _runs, the SURVEY §8(d) end-to-end form) since the previous call of this
+ * function (us[6]; reads and resets): mean time per phase — front buffer and
+ * context, topics H2D (after the context's previous work), match (walk to
+ * merges, collected), runs / identifiers / densify, result D2H + stream
+ * synchronisation — then the number of calls */
+int mqm_batch_host_us(mqm_index *h, double *us);
 /* Device in / device out on `hip_stream` (hipStream_t, NULL = default stream). */
 /* on != 0: every device match (mqm_match_device, queued contexts) computes
  * the Identifiers lists beside its merges (a second stream forked after the

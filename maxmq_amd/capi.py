@@ -52,7 +52,7 @@ EXPORTED = [
     "mqm_serve_policy", "mqm_serve_stats", "mqm_serve_device_us", "mqm_serve_host_us", "mqm_serve_host_max_us",
     "mqm_build_phases_ms", "mqm_build_threads", "mqm_identifiers_early",
     "mqm_result_snapshot_version", "mqm_direct_host_us", "mqm_serve_counters_get",
-    "mqm_debug_stamp_counts",
+    "mqm_debug_stamp_counts", "mqm_batch_host_us",
 ]
 
 
@@ -219,6 +219,7 @@ def lib():
         "mqm_serve_stats": ([vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)], C.c_int),
         "mqm_serve_counters_get": ([vp, C.POINTER(u64 * 8)], C.c_int),
         "mqm_debug_stamp_counts": ([C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)], C.c_int),
+        "mqm_batch_host_us": ([vp, C.POINTER(C.c_double)], C.c_int),
         "mqm_serve_device_us": ([vp, vp], C.c_int),
         "mqm_serve_host_us": ([vp, vp], C.c_int),
         "mqm_serve_host_max_us": ([vp, vp], C.c_int),

@@ -168,6 +168,10 @@ struct mqm_index {
   // single-topic calls on the direct small-batch path (mqm_direct_host_us):
   // per phase (front buffer, context, launch + wait, result), summed and max ns
   std::atomic<uint64_t> direct_ns[4] = {}, direct_max_ns[4] = {}, direct_calls{0};
+  // batch-pipeline host-path calls (mqm_batch_host_us): per phase ns, summed
+  // — front buffer + context, topics H2D, match (walk .. merges, collected),
+  // runs / identifiers / densify, result D2H + synchronisation
+  std::atomic<uint64_t> batch_ns[5] = {}, batch_calls{0};
   void stop_collector();
   ~mqm_index();
 };
@@ -916,6 +920,8 @@ static int match_batch_impl(mqm_index *h, const char *topic_bytes, const uint64_
         return MQM_OK;
       }
     }
+    clk::time_point tb[5];
+    tb[0] = clk::now();
     rc = [&]() -> int {
       Workspace &ws = c->ws;
       const hipStream_t st = c->stream;
@@ -925,18 +931,21 @@ static int match_batch_impl(mqm_index *h, const char *topic_bytes, const uint64_
       int e = upload_batch(c.get(), Workspace::kInBytes, Workspace::kInOffs, topic_bytes, topic_offsets, n_topics,
                            &d_bytes, &d_offs);
       if (e != MQM_OK) return e;
+      tb[1] = clk::now();
       MatchOutput mo;
       ws.runs = runs;
-      ws.ident_early = want_ids;  // (its identifiers pass runs beside the merges)
+      ws.ident_early = want_ids;  // (listed by the merges, or a pass beside them)
       e = match_device(snap->dev, ws, d_bytes, d_offs, n_topics, st, &mo);
       ws.runs = false;
       if (e != 0) return hip_rc(e);
+      tb[2] = clk::now();
       RunsOutput ro;
       if (runs && (e = runs_device(ws, st, mo, &ro)) != 0) return hip_rc(e);
       IdentOutput io;
       if (want_ids && (e = identifiers_device(snap->dev, ws, st, &io)) != 0) return hip_rc(e);
       DenseOutput dn;
       if ((e = densify(snap->dev, ws, mo, st, &dn, packed)) != 0) return hip_rc(e);
+      tb[3] = clk::now();
       // one pinned block: three offset arrays, then the entries (16-B aligned parts)
       const uint64_t n1 = (uint64_t)n_topics + 1, ni = want_ids ? io.n_idents : 0;
       auto up = [](uint64_t b) { return (b + 15) & ~15ull; };
@@ -984,6 +993,11 @@ static int match_batch_impl(mqm_index *h, const char *topic_bytes, const uint64_
         if (ni && hipMemcpyAsync(B + o_i, io.sids, 4 * ni, hipMemcpyDeviceToHost, st) != hipSuccess) return MQM_EHIP;
       }
       if (ws.end(st) || hipStreamSynchronize(st) != hipSuccess) return MQM_EHIP;
+      tb[4] = clk::now();
+      auto ns = [](clk::duration x) { return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(x).count(); };
+      h->batch_ns[0].fetch_add(ns(tb[0] - ts[0]), std::memory_order_relaxed);
+      for (int i = 1; i < 5; i++) h->batch_ns[i].fetch_add(ns(tb[i] - tb[i - 1]), std::memory_order_relaxed);
+      h->batch_calls.fetch_add(1, std::memory_order_relaxed);
       if (runs && r->run_offsets[n_topics] != ro.n_runs) {  // the records' part counts vs the walk's tally
         fprintf(stderr, "mqmatch: runs form: %llu runs listed, %llu counted by the walk\n",
                 (unsigned long long)r->run_offsets[n_topics], (unsigned long long)ro.n_runs);
@@ -2212,6 +2226,17 @@ int mqm_direct_host_us(mqm_index *h, double *us) {
     us[4 + i] = (double)m / 1e3;
   }
   us[8] = (double)n;
+  return MQM_OK;
+}
+
+int mqm_batch_host_us(mqm_index *h, double *us) {
+  if (!h || !us) return MQM_EINVAL;
+  const uint64_t n = h->batch_calls.exchange(0);
+  for (int i = 0; i < 5; i++) {
+    const uint64_t v = h->batch_ns[i].exchange(0);
+    us[i] = n ? (double)v / 1e3 / (double)n : 0.0;
+  }
+  us[5] = (double)n;
   return MQM_OK;
 }
 

@@ -939,6 +939,7 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
       for (uint64_t e = lo; e < hi; e++) staged[e].desc = hs.nodes[staged[e].child];
     });
     hs.bloom = pre.bloom;
+    hs.bloom_words = pre.bloom_words;
     cache->reuses++;
   } else {
     // by parent store id, then child store id (the children lists): the
@@ -982,11 +983,16 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
     // (env MQM_NO_BLOOM=1: none, for A/B runs); OR is order-free, so the
     // parallel fill is deterministic
     hs.bloom.clear();
+    hs.bloom_words = 0;
     if (n_literal_edges && !getenv("MQM_NO_BLOOM")) {
       uint64_t bits = 4096;
       while (bits < 16 * n_literal_edges) bits <<= 1;
-      hs.bloom.assign(bits / 64, 0);
-      const uint64_t mask = bits / 64 - 1;
+      const uint64_t words = bits / 64, mask = words - 1;
+      hs.bloom_words = words;
+      hs.bloom.assign(2 * words, 0);  // the edge filter, then the path filter (snapshot.h bloom2)
+      uint64_t *path = hs.bloom.data() + words;
+      // the hash of each literal child's own edge (0: reached by '+' / '#', or the root)
+      std::vector<uint64_t> in_h(hs.nodes.size(), 0);
       parallel_for(kChunks, [&](uint32_t c) {
         const uint64_t lo = n_literal_edges * c / kChunks, hi = n_literal_edges * (c + 1) / kChunks;
         // 64 edges at a time: their words are prefetched for writing first, so
@@ -999,9 +1005,32 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
             const uint64_t h = edge_hash(x.parent, Key{x.k0, x.k1});
             w[j] = bloom_word(h, mask);
             bb[j] = bloom_bits(h);
+            in_h[x.child] = h | 1;  // (never 0 for a literal child)
             __builtin_prefetch(&hs.bloom[w[j]], 1);
           }
           for (uint32_t j = 0; j < m; j++) __atomic_fetch_or(&hs.bloom[w[j]], bb[j], __ATOMIC_RELAXED);
+        }
+      });
+      // every two-level literal path p -k1-> c -k2-> g: c's own edge hash
+      // (edge_hash(p, k1), low bit forced) and g's key (keys.h path_hash; the
+      // walk hashes edge_hash(p, k1) | 1 the same way)
+      parallel_for(kChunks, [&](uint32_t c) {
+        const uint64_t lo = n_literal_edges * c / kChunks, hi = n_literal_edges * (c + 1) / kChunks;
+        for (uint64_t e0 = lo; e0 < hi; e0 += 64) {
+          const uint32_t m = (uint32_t)std::min<uint64_t>(64, hi - e0);
+          uint64_t w[64], bb[64];
+          uint32_t k = 0;
+          for (uint32_t j = 0; j < m; j++) {
+            const EdgeEntry &x = staged[e0 + j];
+            const uint64_t h1 = in_h[x.parent];
+            if (!h1) continue;
+            const uint64_t h = path_hash(h1, Key{x.k0, x.k1});
+            w[k] = bloom_word(h, mask);
+            bb[k] = bloom_bits(h);
+            __builtin_prefetch(&path[w[k]], 1);
+            k++;
+          }
+          for (uint32_t j = 0; j < k; j++) __atomic_fetch_or(&path[w[j]], bb[j], __ATOMIC_RELAXED);
         }
       });
     }
@@ -1021,6 +1050,7 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
   if (cache && !reuse) {  // keep this build's shape for the next one
     // (order, new_id, pc_of, hc_of, nlit and staged were built in place)
     cache->bloom = hs.bloom;
+    cache->bloom_words = hs.bloom_words;
     cache->structure = st.structure_version();
     cache->n_tokens = st.tokens().size();
     cache->host_edges = host_edges;
@@ -1184,6 +1214,13 @@ void recycled_free(int device, std::vector<std::pair<void *, size_t>> &held) {
   if (!excess.empty()) retire_device_buffers(device, std::move(excess));
 }
 }  // namespace
+
+// MQM_PATH_FILTER=0: the walk checks the edge filter after each probe (A/B;
+// the path filter is built either way)
+static bool path_filter_on() {
+  static const bool v = !getenv("MQM_PATH_FILTER") || atoi(getenv("MQM_PATH_FILTER")) != 0;
+  return v;
+}
 
 // MQM_SNAP_STAMP=1 (diagnostic): stamp the snapshot's version into its
 // buffers as the upload's last step (snapshot.h DeviceSnapshot::stamp)
@@ -1368,7 +1405,10 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
   g->dev.pinfo = (const uint2 *)g->pinfo;
   g->dev.partners = (const uint32_t *)g->partners;
   g->dev.bloom = (const uint64_t *)g->bloom;
-  g->dev.bloom_mask = g->bloom ? hs->bloom.size() - 1 : 0;
+  g->dev.bloom_mask = g->bloom ? hs->bloom_words - 1 : 0;
+  g->dev.bloom2 = g->bloom && hs->bloom.size() == 2 * hs->bloom_words && path_filter_on()
+                      ? (const uint64_t *)g->bloom + hs->bloom_words
+                      : nullptr;
   g->dev.tok_pool = (const uint8_t *)g->buffers[3];
   g->dev.n_buckets = hs->n_buckets;
   g->dev.n_nodes = (uint32_t)hs->nodes.size();

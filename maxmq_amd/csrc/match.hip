@@ -385,7 +385,8 @@ __device__ __forceinline__ void ident_put(const Outputs &o, uint64_t ib, bool ha
 }
 
 
-template <int kG, int kChunk = 0, bool kSlots = true>
+// kPath: the path filter's words are loaded with the items (DeviceSnapshot::bloom2)
+template <int kG, int kChunk = 0, bool kSlots = true, bool kPath = false>
 __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_eu(4))) void k_walk(DeviceSnapshot s, const uint8_t *__restrict__ tbytes,
                                                            const uint64_t *__restrict__ toffs, uint32_t n,
                                                            Outputs o) {
@@ -573,6 +574,15 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
         // (the first kPK such per level) right at the load (the walk is at its
         // VGPR budget)
         const bool slot_load = live && !lit && !known;
+        // the filter word for the literal probe this item's node would push
+        // at the next level, issued before the item's own loads (s.bloom2: the
+        // path filter answers for a literal item's child before the probe does)
+        // so a level costs one round trip; without it, loaded after the probe
+        const bool pre = kPath && live && has_next && d + 1 < (uint32_t)kLMax && !next_wild && !(lit && lit_is_wild);
+        const uint64_t ph = !pre ? 0 : lit ? path_hash(edge_hash(id, Key{k0, k1}) | 1, Key{nk0, nk1})
+                                           : edge_hash(id, Key{nk0, nk1});
+        const uint64_t pw = pre ? (lit ? s.bloom2 : s.bloom)[bloom_word(ph, s.bloom_mask)] : 0;
+        const uint64_t pb = bloom_bits(ph);
         bool pk = false;
         NodeDesc dc;
         uint32_t c = !kSlots ? walk_step(s, live && lit && !lit_is_wild, slot_load, id, id, k0, k1, tp + tst, tln, &dc)
@@ -625,9 +635,9 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
         // overlaps this level's record writes, and a negative (or a '+' / '#'
         // next level, whose literal probe is the wildcard's) drops the item
         const bool chk = push && (fl & kFlagHasLiteral) && s.bloom && d + 1 < (uint32_t)kLMax && !next_wild;
-        const uint64_t nh2 = chk ? edge_hash(c, Key{nk0, nk1}) : 0;
-        const uint64_t bw = chk ? s.bloom[bloom_word(nh2, s.bloom_mask)] : 0;
-        const uint64_t bb = bloom_bits(nh2);
+        const uint64_t nh2 = chk && !kPath ? edge_hash(c, Key{nk0, nk1}) : 0;
+        const uint64_t bw = !chk ? 0 : kPath ? pw : s.bloom[bloom_word(nh2, s.bloom_mask)];
+        const uint64_t bb = kPath ? pb : bloom_bits(nh2);
         const uint32_t m_own = (uint32_t)(__ballot(c_own > 0) >> gbase) & kGMask;
         const uint32_t m_par = (uint32_t)(__ballot(c_par > 0) >> gbase) & kGMask;
         const uint32_t m_hl = (uint32_t)(__ballot(c_hl > 0) >> gbase) & kGMask;
@@ -2687,6 +2697,9 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
       hipLaunchKernelGGL(k_walk<kWalkG>, dim3(blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o);
     else if (walk_slots() && s.slots)
       hipLaunchKernelGGL((k_walk<kWalkG, 4>), dim3(blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o);
+    else if (s.bloom2)  // (the path filter: one round trip per level)
+      hipLaunchKernelGGL((k_walk<kWalkG, 4, false, true>), dim3(blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes,
+                         d_offs, n, o);
     else
       hipLaunchKernelGGL((k_walk<kWalkG, 4, false>), dim3(blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs,
                          n, o);

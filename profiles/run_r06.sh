@@ -3,6 +3,7 @@
 # time limit, chained so that the first failure ends the call.
 #   stampt  : served churn test with recycled snapshot buffers (no quarantine) and version stamps checked
 #   recyclet: served + churn tests with recycled snapshot buffers, no quarantine
+#   pathab  : `fast` with the walk's path filter, without it (MQM_PATH_FILTER=0), with it again
 #   tests   : every -m gpu test                          -> gpurun_out/TAG/pytest_gpu.log
 #   serve   : the per-publish server tests (incl. served calls under Subscribe/Unsubscribe churn)
 #   ab / c4ab: `fast` (C3) / the C4 shard bench with the round-5 walk (paired node slots) and long-part
@@ -56,6 +57,10 @@ for step in "$@"; do
              tests/test_gpu_serve_churn.py -m gpu --timeout 300 > $OUT/pytest_stamp.log 2>&1 ;;
     recyclet) MQM_SNAP_RECYCLE=1 MQM_RECYCLE_QUARANTINE_MS=0 timeout -k 10 500 $PYT -s \
              tests/test_gpu_serve_churn.py tests/test_gpu_serve.py -m gpu --timeout 300 > $OUT/pytest_recycle.log 2>&1 ;;
+    pathab) for V in path:X=0 nopath:MQM_PATH_FILTER=0 path2:X=0; do
+          N=${V%%:*}; E=${V#*:}
+          env $E timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_$N.json 2> $OUT/bench_fast_$N.log || exit 1
+        done ;;
     churnt) timeout -k 10 500 $PYT tests/test_gpu_serve_churn.py -m gpu --timeout 300 > $OUT/pytest_churn.log 2>&1 ;;
     serve) timeout -k 10 600 $PYT tests/test_gpu_serve.py tests/test_gpu_serve_churn.py tests/test_gpu_shim.py -m gpu \
              --timeout 300 > $OUT/pytest_serve.log 2>&1 ;;
