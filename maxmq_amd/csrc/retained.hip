@@ -602,8 +602,16 @@ struct Task {            // copy list[lo, lo + len) to out[dst ..)
   uint32_t lo, len_list; // len | list << 31
 };
 
-// each emission's place in its filter's segment: small ones copied here,
+// each emission's place in its filter's segment: small ones copied here by
+// the whole wavefront (lanes over the concatenated small emissions of the 64:
+// consecutive refs on consecutive lanes — adjacent emissions of one filter are
+// adjacent in its segment too; round 5 copied each one on its own lane, 8-B
+// accesses strided across the wave: k_emit_place 3.5 ms of 22.1, r05aa),
 // large ones cut into kTaskRefs copy tasks
+struct EmitLds {
+  uint32_t pre[65];           // exclusive prefix of the small emissions' counts
+  uint64_t pos[64], src[64];  // output position, source index | list << 63
+};
 __global__ __launch_bounds__(kThreads) void k_emit_place(const Emit *__restrict__ e, uint64_t cap, RevCtr *ctr,
                                                         const uint64_t *__restrict__ foff,
                                                         unsigned long long *__restrict__ fcur,
@@ -611,6 +619,8 @@ __global__ __launch_bounds__(kThreads) void k_emit_place(const Emit *__restrict_
                                                         const uint64_t *__restrict__ rch_refs,
                                                         uint64_t *__restrict__ out, uint64_t out_cap,
                                                         Task *__restrict__ tasks, uint64_t task_cap) {
+  __shared__ EmitLds lds_all[kThreads / 64];
+  EmitLds &L = lds_all[threadIdx.x / 64];
   const uint64_t ne = min((uint64_t)ctr->n_emit, cap);
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   const int lane = threadIdx.x & 63;
@@ -623,16 +633,38 @@ __global__ __launch_bounds__(kThreads) void k_emit_place(const Emit *__restrict_
     unsigned long long rb = 0;
     if (ok && r.last && it.f != kNone) rb = foff[it.f] + atomicAdd(&fcur[it.f], (unsigned long long)r.inc);
     const uint64_t pos = bcast64(rb, r.last_lane) + (r.inc - cnt);  // run base + the run's entries before this lane
-    if (!ok || cnt == 0) continue;
-    if (pos + cnt > out_cap) {
-      atomicOr(&ctr->ovf, (unsigned)kOvfOut);
-      continue;
+    const bool fits = ok && cnt > 0 && pos + cnt <= out_cap;
+    if (ok && cnt > 0 && !fits) atomicOr(&ctr->ovf, (unsigned)kOvfOut);
+    // the small ones, together (every lane takes part: wave-uniform loop)
+    const uint32_t cs = fits && cnt <= kSmallEmit ? (uint32_t)cnt : 0u;
+    uint32_t inc = cs;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t v = __shfl_up(inc, d, 64);
+      if (lane >= d) inc += v;
     }
-    const uint64_t *src = (it.list ? rch_refs : refs) + it.lo;
-    if (cnt <= kSmallEmit) {
-      for (uint32_t j = 0; j < (uint32_t)cnt; j++) out[pos + j] = src[j];
-      continue;
+    const uint32_t total = __shfl(inc, 63, 64);
+    if (total) {
+      L.pre[lane] = inc - cs;
+      if (lane == 0) L.pre[64] = total;
+      L.pos[lane] = pos;
+      L.src[lane] = it.lo | ((uint64_t)it.list << 63);
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      for (uint32_t q = lane; q < total + 63 - (total + 63) % 64; q += 64) {  // (whole-wave steps)
+        if (q < total) {
+          uint32_t j = 0;  // the emission holding ref q: the largest j with pre[j] <= q
+#pragma unroll
+          for (uint32_t step = 32; step > 0; step >>= 1) j = L.pre[j + step] <= q ? j + step : j;
+          const uint32_t o = q - L.pre[j];
+          const uint64_t sw = L.src[j];
+          out[L.pos[j] + o] = ((sw >> 63) ? rch_refs : refs)[(sw & ~(1ull << 63)) + o];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
+    if (!fits || cnt <= kSmallEmit) continue;
     const uint32_t nt = (uint32_t)((cnt + kTaskRefs - 1) / kTaskRefs);
     const unsigned long long t0 = atomicAdd(&ctr->n_tasks, (unsigned long long)nt);
     if (t0 + nt > task_cap) atomicOr(&ctr->ovf, (unsigned)kOvfTasks);
@@ -658,7 +690,12 @@ __global__ __launch_bounds__(kThreads) void k_task_copy(const Task *__restrict__
     const uint32_t len = k.len_list & 0x7FFFFFFFu;
     const uint64_t *src = ((k.len_list >> 31) ? rch_refs : refs) + k.lo;
     uint64_t *dst = out + k.dst;
-    for (uint32_t j = lane; j < len; j += 64) dst[j] = src[j];
+    uint32_t j = lane;
+    for (; j + 192 < len; j += 256) {  // 4 loads in flight per lane
+      const uint64_t a = src[j], b = src[j + 64], c = src[j + 128], d = src[j + 192];
+      dst[j] = a, dst[j + 64] = b, dst[j + 128] = c, dst[j + 192] = d;
+    }
+    for (; j < len; j += 64) dst[j] = src[j];
   }
 }
 
