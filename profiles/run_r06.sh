@@ -148,6 +148,7 @@ for step in "$@"; do
              2> $OUT/bench_fast_pipe$P.log || exit 1; done ;;
     par) timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_gpu_queued.py -m gpu --timeout 300 \
              > $OUT/pytest_par.log 2>&1 ;;
+    l2probe) timeout -k 10 120 tools/_build/l2_probe > $OUT/l2_probe.txt 2>&1 ;;
     reuseprobe) timeout -k 10 120 tools/_build/reuse_probe > $OUT/reuse_probe.txt 2>&1 ;;
     pollprobe) timeout -k 10 120 tools/_build/poll_probe > $OUT/poll_probe.txt 2>&1 ;;
     freeprobe) timeout -k 10 60 tools/_build/free_probe > $OUT/free_probe.txt 2>&1 ;;
