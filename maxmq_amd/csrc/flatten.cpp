@@ -939,7 +939,6 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
       for (uint64_t e = lo; e < hi; e++) staged[e].desc = hs.nodes[staged[e].child];
     });
     hs.bloom = pre.bloom;
-    hs.bloom_words = pre.bloom_words;
     cache->reuses++;
   } else {
     // by parent store id, then child store id (the children lists): the
@@ -983,16 +982,11 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
     // (env MQM_NO_BLOOM=1: none, for A/B runs); OR is order-free, so the
     // parallel fill is deterministic
     hs.bloom.clear();
-    hs.bloom_words = 0;
     if (n_literal_edges && !getenv("MQM_NO_BLOOM")) {
       uint64_t bits = 4096;
       while (bits < 16 * n_literal_edges) bits <<= 1;
-      const uint64_t words = bits / 64, mask = words - 1;
-      hs.bloom_words = words;
-      hs.bloom.assign(2 * words, 0);  // the edge filter, then the path filter (snapshot.h bloom2)
-      uint64_t *path = hs.bloom.data() + words;
-      // the hash of each literal child's own edge (0: reached by '+' / '#', or the root)
-      std::vector<uint64_t> in_h(hs.nodes.size(), 0);
+      hs.bloom.assign(bits / 64, 0);
+      const uint64_t mask = bits / 64 - 1;
       parallel_for(kChunks, [&](uint32_t c) {
         const uint64_t lo = n_literal_edges * c / kChunks, hi = n_literal_edges * (c + 1) / kChunks;
         // 64 edges at a time: their words are prefetched for writing first, so
@@ -1005,32 +999,9 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
             const uint64_t h = edge_hash(x.parent, Key{x.k0, x.k1});
             w[j] = bloom_word(h, mask);
             bb[j] = bloom_bits(h);
-            in_h[x.child] = h | 1;  // (never 0 for a literal child)
             __builtin_prefetch(&hs.bloom[w[j]], 1);
           }
           for (uint32_t j = 0; j < m; j++) __atomic_fetch_or(&hs.bloom[w[j]], bb[j], __ATOMIC_RELAXED);
-        }
-      });
-      // every two-level literal path p -k1-> c -k2-> g: c's own edge hash
-      // (edge_hash(p, k1), low bit forced) and g's key (keys.h path_hash; the
-      // walk hashes edge_hash(p, k1) | 1 the same way)
-      parallel_for(kChunks, [&](uint32_t c) {
-        const uint64_t lo = n_literal_edges * c / kChunks, hi = n_literal_edges * (c + 1) / kChunks;
-        for (uint64_t e0 = lo; e0 < hi; e0 += 64) {
-          const uint32_t m = (uint32_t)std::min<uint64_t>(64, hi - e0);
-          uint64_t w[64], bb[64];
-          uint32_t k = 0;
-          for (uint32_t j = 0; j < m; j++) {
-            const EdgeEntry &x = staged[e0 + j];
-            const uint64_t h1 = in_h[x.parent];
-            if (!h1) continue;
-            const uint64_t h = path_hash(h1, Key{x.k0, x.k1});
-            w[k] = bloom_word(h, mask);
-            bb[k] = bloom_bits(h);
-            __builtin_prefetch(&path[w[k]], 1);
-            k++;
-          }
-          for (uint32_t j = 0; j < k; j++) __atomic_fetch_or(&path[w[j]], bb[j], __ATOMIC_RELAXED);
         }
       });
     }
@@ -1050,7 +1021,6 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
   if (cache && !reuse) {  // keep this build's shape for the next one
     // (order, new_id, pc_of, hc_of, nlit and staged were built in place)
     cache->bloom = hs.bloom;
-    cache->bloom_words = hs.bloom_words;
     cache->structure = st.structure_version();
     cache->n_tokens = st.tokens().size();
     cache->host_edges = host_edges;
@@ -1215,10 +1185,11 @@ void recycled_free(int device, std::vector<std::pair<void *, size_t>> &held) {
 }
 }  // namespace
 
-// MQM_PATH_FILTER=0: the walk checks the edge filter after each probe (A/B;
-// the path filter is built either way)
-static bool path_filter_on() {
-  static const bool v = !getenv("MQM_PATH_FILTER") || atoi(getenv("MQM_PATH_FILTER")) != 0;
+// MQM_SNAP_VERIFY=1 (diagnostic): after an upload, read the device arrays
+// back and compare them with the host arrays (the edge table: a host build of
+// the same staged edges, by digest); mismatches go to stderr
+static bool snap_verify() {
+  static const bool v = getenv("MQM_SNAP_VERIFY") && atoi(getenv("MQM_SNAP_VERIFY")) != 0;
   return v;
 }
 
@@ -1314,6 +1285,24 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
         return MQM_EHIP;
     } else {
       hs->edges_digest = edges_digest_final(sum, n_slots);
+      if (snap_verify()) {  // the same table built on the host, compared slot by slot
+        HostSnapshot tmp;
+        tmp.n_buckets = hs->n_buckets;
+        insert_edges_host(tmp, *hs->staged);
+        std::vector<EdgeEntry> dev(n_slots);
+        if (hipMemcpyAsync(dev.data(), g->buffers[1], n_slots * sizeof(EdgeEntry), hipMemcpyDeviceToHost, stream) !=
+                hipSuccess ||
+            hipStreamSynchronize(stream) != hipSuccess)
+          return MQM_EHIP;
+        uint64_t bad = 0, first = ~0ull;
+        for (uint64_t i = 0; i < n_slots; i++)
+          if (memcmp(&dev[i], &tmp.edges[i], sizeof(EdgeEntry)) != 0 && bad++ == 0) first = i;
+        const uint64_t dg = edges_digest_of(tmp);
+        if (bad || dg != hs->edges_digest)
+          fprintf(stderr, "mqmatch verify: version %llu edge table: %llu of %llu slots differ from the host build "
+                  "(first %llu), digest %s\n", (unsigned long long)hs->version, (unsigned long long)bad,
+                  (unsigned long long)n_slots, (unsigned long long)first, dg == hs->edges_digest ? "equal" : "differs");
+      }
     }
     hs->staged.reset();  // (the builder's FlattenCache may keep it for the next build)
   }
@@ -1357,6 +1346,31 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
     if (dalloc(&g->nflags, nn + 64) != hipSuccess) return MQM_ENOMEM;
     if (derive_node_flags((const NodeDesc *)g->buffers[0], (uint8_t *)g->nflags, nn, stream)) return MQM_EHIP;
     g->device_bytes += nn;
+  }
+  if (snap_verify()) {  // the uploaded and derived arrays, read back
+    if (hipStreamSynchronize(stream) != hipSuccess) return MQM_EHIP;
+    auto check = [&](const char *what, const void *dptr, const void *host, size_t n) {
+      if (!n) return;
+      std::vector<uint8_t> b(n);
+      if (hipMemcpy(b.data(), dptr, n, hipMemcpyDeviceToHost) != hipSuccess) return;
+      if (memcmp(b.data(), host, n) != 0) {
+        size_t k = 0;
+        while (k < n && b[k] == ((const uint8_t *)host)[k]) k++;
+        fprintf(stderr, "mqmatch verify: version %llu %s differs from the host array at byte %zu of %zu\n",
+                (unsigned long long)hs->version, what, k, n);
+      }
+    };
+    check("nodes", g->buffers[0], hs->nodes.data(), hs->nodes.size() * sizeof(NodeDesc));
+    check("subs", g->buffers[2], hs->subs.data(), hs->subs.size() * sizeof(SubEnt));
+    check("tok_pool", g->buffers[3], hs->tok_pool.data(), hs->tok_pool.size());
+    if (!hs->bloom.empty()) check("bloom", g->bloom, hs->bloom.data(), hs->bloom.size() * 8);
+    check("pinfo", g->pinfo, hs->pinfo.data(), hs->pinfo.size() * sizeof(uint2));
+    check("partners", g->partners, hs->partners.data(), hs->partners.size() * 4);
+    {
+      std::vector<uint32_t> w(n_sub_ents);
+      for (uint64_t i = 0; i < n_sub_ents; i++) w[i] = hs->subs[i].word & kPackedMask;
+      check("words", g->words, w.data(), n_sub_ents * 4);
+    }
   }
   if (stamped) {  // last: every buffer above is complete on the stream before its stamp
     void *own = nullptr;
@@ -1405,10 +1419,7 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
   g->dev.pinfo = (const uint2 *)g->pinfo;
   g->dev.partners = (const uint32_t *)g->partners;
   g->dev.bloom = (const uint64_t *)g->bloom;
-  g->dev.bloom_mask = g->bloom ? hs->bloom_words - 1 : 0;
-  g->dev.bloom2 = g->bloom && hs->bloom.size() == 2 * hs->bloom_words && path_filter_on()
-                      ? (const uint64_t *)g->bloom + hs->bloom_words
-                      : nullptr;
+  g->dev.bloom_mask = g->bloom ? hs->bloom.size() - 1 : 0;
   g->dev.tok_pool = (const uint8_t *)g->buffers[3];
   g->dev.n_buckets = hs->n_buckets;
   g->dev.n_nodes = (uint32_t)hs->nodes.size();

@@ -54,8 +54,7 @@ struct HostSnapshot {
   std::vector<SubInfo> sub_info;     // by non-shared sid
   std::vector<SubInfo> shared_info;  // by shared sid
   std::vector<uint8_t> tok_pool;
-  std::vector<uint64_t> bloom;       // DeviceSnapshot::bloom, then bloom2 (empty: none)
-  uint64_t bloom_words = 0;          // words of each filter (bloom.size() = 2 * bloom_words)
+  std::vector<uint64_t> bloom;       // DeviceSnapshot::bloom (empty: none)
   std::vector<uint2> pinfo;          // DeviceSnapshot::pinfo (by final sid)
   std::vector<uint32_t> partners;    // DeviceSnapshot::partners
   uint64_t n_buckets = 0;
@@ -94,7 +93,6 @@ struct FlattenCache {
   U32Vec order, new_id, pc_of, hc_of, nlit;
   std::shared_ptr<EdgeVec> staged;
   std::vector<uint64_t> bloom;
-  uint64_t bloom_words = 0;
   uint64_t reuses = 0;  // builds that took the cache (statistics)
   // working arrays kept from build to build (their pages stay mapped: a fresh
   // 2-MB page costs its zeroing and, when memory is fragmented, compaction)

@@ -108,17 +108,6 @@ MQM_HD uint64_t bloom_bits(uint64_t h) {
   return (1ull << ((h >> 34) & 63)) | (1ull << ((h >> 40) & 63)) | (1ull << ((h >> 46) & 63));
 }
 
-// path filter (DeviceSnapshot::bloom2): the hash of a two-level literal path
-// p -k1-> c -k2-> g from h1 = edge_hash(p, k1), so the walk can ask "does the
-// child it is probing for have a literal child k2?" in the same round trip as
-// the probe itself (a plain edge filter needs the child's id, i.e. the probe's
-// answer: one dependent round trip more per level)
-MQM_HD uint64_t path_hash(uint64_t h1, const Key &k2) {
-  const uint64_t x = h1 ^ (k2.k0 * 0xC2B2AE3D27D4EB4Full) ^ rotl64(k2.k1, 17);
-  uint64_t h = (x ^ (x >> 29)) * 0x94D049BB133111EBull;
-  return h ^ (h >> 32);
-}
-
 // The walk's tokenizer (match.hip k_walk): a lane holds 16 topic bytes as 4
 // little-endian words, bytes at or past the topic's end zeroed.  -> a 16-bit
 // mask of the '/' bytes (bit i = byte i).  Per byte exactly: the high bit of

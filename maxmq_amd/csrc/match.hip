@@ -385,8 +385,7 @@ __device__ __forceinline__ void ident_put(const Outputs &o, uint64_t ib, bool ha
 }
 
 
-// kPath: the path filter's words are loaded with the items (DeviceSnapshot::bloom2)
-template <int kG, int kChunk = 0, bool kSlots = true, bool kPath = false>
+template <int kG, int kChunk = 0, bool kSlots = true>
 __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_eu(4))) void k_walk(DeviceSnapshot s, const uint8_t *__restrict__ tbytes,
                                                            const uint64_t *__restrict__ toffs, uint32_t n,
                                                            Outputs o) {
@@ -574,15 +573,6 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
         // (the first kPK such per level) right at the load (the walk is at its
         // VGPR budget)
         const bool slot_load = live && !lit && !known;
-        // the filter word for the literal probe this item's node would push
-        // at the next level, issued before the item's own loads (s.bloom2: the
-        // path filter answers for a literal item's child before the probe does)
-        // so a level costs one round trip; without it, loaded after the probe
-        const bool pre = kPath && live && has_next && d + 1 < (uint32_t)kLMax && !next_wild && !(lit && lit_is_wild);
-        const uint64_t ph = !pre ? 0 : lit ? path_hash(edge_hash(id, Key{k0, k1}) | 1, Key{nk0, nk1})
-                                           : edge_hash(id, Key{nk0, nk1});
-        const uint64_t pw = pre ? (lit ? s.bloom2 : s.bloom)[bloom_word(ph, s.bloom_mask)] : 0;
-        const uint64_t pb = bloom_bits(ph);
         bool pk = false;
         NodeDesc dc;
         uint32_t c = !kSlots ? walk_step(s, live && lit && !lit_is_wild, slot_load, id, id, k0, k1, tp + tst, tln, &dc)
@@ -635,9 +625,9 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
         // overlaps this level's record writes, and a negative (or a '+' / '#'
         // next level, whose literal probe is the wildcard's) drops the item
         const bool chk = push && (fl & kFlagHasLiteral) && s.bloom && d + 1 < (uint32_t)kLMax && !next_wild;
-        const uint64_t nh2 = chk && !kPath ? edge_hash(c, Key{nk0, nk1}) : 0;
-        const uint64_t bw = !chk ? 0 : kPath ? pw : s.bloom[bloom_word(nh2, s.bloom_mask)];
-        const uint64_t bb = kPath ? pb : bloom_bits(nh2);
+        const uint64_t nh2 = chk ? edge_hash(c, Key{nk0, nk1}) : 0;
+        const uint64_t bw = chk ? s.bloom[bloom_word(nh2, s.bloom_mask)] : 0;
+        const uint64_t bb = bloom_bits(nh2);
         const uint32_t m_own = (uint32_t)(__ballot(c_own > 0) >> gbase) & kGMask;
         const uint32_t m_par = (uint32_t)(__ballot(c_par > 0) >> gbase) & kGMask;
         const uint32_t m_hl = (uint32_t)(__ballot(c_hl > 0) >> gbase) & kGMask;
@@ -959,11 +949,7 @@ struct alignas(16) WinLds {
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 // kNT (default; MQM_NT_STORE=0 off): the scalar path's stores non-temporal, so the
 // result stream does not evict the hub ranges the copy re-reads from L2
-// kPair (MQM_WINCOPY_PAIR=1, A/B): each lane moves 2 consecutive positions
-// per unit — one descriptor search (the second position is the same part or,
-// at a boundary, the next one), two 4-B loads, one 8-B store: half the store
-// instructions and searches of the scalar path, no serialised fallback
-template <bool kVec = false, bool kNT = false, bool kPair = false>
+template <bool kVec = false, bool kNT = false>
 __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_eu(8))) void k_wincopy(
     DeviceSnapshot s, const uint4 *__restrict__ desc, const uint64_t *__restrict__ nd_ptr, uint64_t desc_cap,
     const uint32_t *__restrict__ win, uint64_t win_cap, const uint64_t *__restrict__ total_ptr,
@@ -1063,48 +1049,7 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
           }
         }
       }
-      constexpr int kPU = kCU / 4;  // pairs per lane per step (8: VGPR spills at 8 waves per SIMD)
-      for (uint32_t base = q0 & ~1u; kPair && base < q1; base += kWave * 2 * kPU) {
-        uint32_t sa0[kPU], sa1[kPU];  // source word | 1 << 31 when the position is copied (sids < 2^28)
-#pragma unroll
-        for (int u = 0; u < kPU; u++) {
-          const uint32_t q = base + 2 * (u * kWave + lane);
-          const uint32_t k = desc_of(min(q, (uint32_t)kWin - 1));
-          const bool in0 = q >= q0 && q < q1 && q >= L.st[k] && q < L.en[k];
-          // q + 1: the same part, or the first one starting at or before it
-          uint32_t k1 = k;
-          if (q + 1 < (uint32_t)kWin && !(q + 1 < L.en[k])) k1 = desc_of(q + 1);
-          const bool in1 = q + 1 >= q0 && q + 1 < q1 && q + 1 >= L.st[k1] && q + 1 < L.en[k1];
-          sa0[u] = in0 ? (L.src[k] + (q - L.st[k])) | 0x80000000u : 0u;
-          sa1[u] = in1 ? (L.src[k1] + (q + 1 - L.st[k1])) | 0x80000000u : 0u;
-        }
-        uint32_t v0[kPU], v1[kPU];
-#pragma unroll
-        for (int u = 0; u < kPU; u++) {
-          v0[u] = __builtin_amdgcn_raw_buffer_load_b32(words, (int)((sa0[u] & 0x7FFFFFFFu) * 4u), 0, 0);
-          v1[u] = __builtin_amdgcn_raw_buffer_load_b32(words, (int)((sa1[u] & 0x7FFFFFFFu) * 4u), 0, 0);
-        }
-#pragma unroll
-        for (int u = 0; u < kPU; u++) {
-          const uint32_t inm = (sa0[u] >> 31) | ((sa1[u] >> 31) << 1);
-          if (!inm) continue;
-          const uint64_t p = g0 + base + 2 * (u * kWave + lane);
-          if (p + 1 >= cap) {
-            atomicOr(oob, kOobStore);
-          } else if (inm == 3u) {
-            const uint64_t v = ((uint64_t)v1[u] << 32) | v0[u];
-            if (kNT)
-              __builtin_nontemporal_store(v, reinterpret_cast<uint64_t *>(out + p));
-            else
-              *reinterpret_cast<uint64_t *>(out + p) = v;
-          } else if (inm == 1u) {
-            out[p] = v0[u];
-          } else {
-            out[p + 1] = v1[u];
-          }
-        }
-      }
-      for (uint32_t base = q0; !kVec && !kPair && base < q1; base += kWave * kCU) {
+      for (uint32_t base = q0; !kVec && base < q1; base += kWave * kCU) {
         uint32_t sa[kCU];
         bool in[kCU];
 #pragma unroll
@@ -1686,11 +1631,6 @@ static bool desc_copy_on() {
 // MQM_WINCOPY_VEC=1: the window copy moves 4 positions per lane at a time (A/B)
 static bool wincopy_vec() {
   static const bool v = getenv("MQM_WINCOPY_VEC") && atoi(getenv("MQM_WINCOPY_VEC")) != 0;
-  return v;
-}
-// MQM_WINCOPY_PAIR=1: the window copy moves 2 positions per lane per unit (A/B)
-static bool wincopy_pair() {
-  static const bool v = getenv("MQM_WINCOPY_PAIR") && atoi(getenv("MQM_WINCOPY_PAIR")) != 0;
   return v;
 }
 // the window copy's stores non-temporal, on by default (C3 773-782M vs
@@ -2747,9 +2687,6 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
       hipLaunchKernelGGL(k_walk<kWalkG>, dim3(blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o);
     else if (walk_slots() && s.slots)
       hipLaunchKernelGGL((k_walk<kWalkG, 4>), dim3(blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o);
-    else if (s.bloom2)  // (the path filter: one round trip per level)
-      hipLaunchKernelGGL((k_walk<kWalkG, 4, false, true>), dim3(blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes,
-                         d_offs, n, o);
     else
       hipLaunchKernelGGL((k_walk<kWalkG, 4, false>), dim3(blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs,
                          n, o);
@@ -2986,10 +2923,6 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
         if (wincopy_vec())
           hipLaunchKernelGGL(k_wincopy<true>, grid(k_wincopy<true>), dim3(kWave * kEmitWaves), 0, st, s, desc,
                              desc_start + n, desc_cap, win, win_cap, o.dstart + n, o.dout, o.dcap, &o.ctr->oob);
-        else if (wincopy_pair())
-          hipLaunchKernelGGL((k_wincopy<false, true, true>), grid(k_wincopy<false, true, true>),
-                             dim3(kWave * kEmitWaves), 0, st, s, desc, desc_start + n, desc_cap, win, win_cap,
-                             o.dstart + n, o.dout, o.dcap, &o.ctr->oob);
         else if (nt_store())
           hipLaunchKernelGGL((k_wincopy<false, true>), grid(k_wincopy<false, true>), dim3(kWave * kEmitWaves), 0, st,
                              s, desc, desc_start + n, desc_cap, win, win_cap, o.dstart + n, o.dout, o.dcap,

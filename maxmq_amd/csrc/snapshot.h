@@ -181,12 +181,6 @@ struct DeviceSnapshot {
   const uint32_t *partners;
   const uint64_t *bloom;  // nullptr: no filter
   uint64_t bloom_mask;    // words - 1 (a power of two)
-  // the path filter (keys.h path_hash), same size and word mapping, right
-  // after the edge filter: every two-level literal path p -k1-> c -k2-> g.  A
-  // literal probe of (p, k1) checks it for the next level's key k2 while the
-  // probe is in flight, so a level costs one round trip (nullptr: the walk
-  // checks the edge filter after the probe, MQM_PATH_FILTER=0)
-  const uint64_t *bloom2;
   uint32_t n_nodes;
   uint32_t n_subs;
   uint32_t n_shared;

@@ -57,6 +57,8 @@ for step in "$@"; do
     tests) timeout -k 10 1000 $PYT tests -m gpu --timeout 600 --durations=15 > $OUT/pytest_gpu.log 2>&1 ;;
     stampt) MQM_SNAP_RECYCLE=1 MQM_RECYCLE_QUARANTINE_MS=0 MQM_SNAP_STAMP=1 timeout -k 10 500 $PYT -s \
              tests/test_gpu_serve_churn.py -m gpu --timeout 300 > $OUT/pytest_stamp.log 2>&1 ;;
+    verifyt) MQM_SNAP_RECYCLE=1 MQM_RECYCLE_QUARANTINE_MS=0 MQM_SNAP_VERIFY=1 timeout -k 10 500 $PYT -s \
+             tests/test_gpu_serve_churn.py -m gpu --timeout 300 > $OUT/pytest_verify.log 2>&1 ;;
     recyclet) MQM_SNAP_RECYCLE=1 MQM_RECYCLE_QUARANTINE_MS=0 timeout -k 10 500 $PYT -s \
              tests/test_gpu_serve_churn.py tests/test_gpu_serve.py -m gpu --timeout 300 > $OUT/pytest_recycle.log 2>&1 ;;
     pathab) for V in path:X=0 nopath:MQM_PATH_FILTER=0 path2:X=0; do
