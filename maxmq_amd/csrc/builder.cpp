@@ -237,7 +237,7 @@ void Builder::run() {
         const auto t1 = std::chrono::steady_clock::now();
         auto hs = std::make_shared<HostSnapshot>();
         const uint64_t reuses = shape_.reuses;
-        rc = fault == 2 ? MQM_ENOMEM : flatten(shadow_, hs.get(), device_ < 0, &shape_);
+        rc = fault == 2 ? MQM_ENOMEM : flatten(shadow_, hs.get(), device_ < 0 || host_edges_forced(), &shape_);
         b.kept_shape = shape_.reuses != reuses;
         hs->version = version;  // (after flatten, which starts from an empty snapshot)
         const auto t2 = std::chrono::steady_clock::now();

@@ -381,7 +381,7 @@ int commit_locked(mqm_index *h) {
     return h->snap && h->snap_version == h->store.version() ? MQM_OK : MQM_EINVAL;
   }
   auto hs = std::make_shared<HostSnapshot>();
-  int rc = flatten(h->store, hs.get(), h->cfg.device < 0);  // (a device builds the edge table itself)
+  int rc = flatten(h->store, hs.get(), h->cfg.device < 0 || host_edges_forced());  // (a device builds the edge table itself)
   if (rc != MQM_OK) return rc;
   hs->version = h->store.version();  // (after flatten, which starts from an empty snapshot; mu held)
   std::unique_ptr<GpuSnapshot> g;

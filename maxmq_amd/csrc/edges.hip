@@ -22,6 +22,8 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include <mutex>
+
 #include "flatten.h"
 
 namespace mqm {
@@ -149,60 +151,121 @@ int digest_edges_device(const EdgeEntry *table, uint64_t n_slots, hipStream_t st
   return 0;
 }
 
-int build_edges_device(const EdgeEntry *d_staged, uint64_t ne, uint64_t nb, EdgeEntry *table, hipStream_t st,
+// The build's device memory: the staged edges and every temporary, carved
+// from one region per device that is kept from build to build (grown, never
+// shrunk; a grown-out region is freed by the index layer's reaper, which
+// stops the per-publish servers first: hipFree waits for every kernel).
+// Round 5 took them from the stream-ordered pool (hipMallocAsync /
+// hipFreeAsync on the upload stream), whose reuse of freed memory was seen to
+// serve stale contents to kernels (tools/reuse_probe.hip, r05s/r05u); with
+// snapshot buffers recycled in place — no hipFree between builds — served
+// results then missed the newest subscriptions of one snapshot now and then
+// (r06a/r06b, tests/test_gpu_serve_churn.py).  MQM_EDGE_POOL=1: the pool.
+struct EdgeScratch {
+  std::mutex mu;
+  char *p = nullptr;
+  size_t cap = 0;
+};
+EdgeScratch &edge_scratch(int dev) {
+  static auto *s = new EdgeScratch[64];  // (never destroyed: uploads may run during static destruction)
+  return s[dev & 63];
+}
+bool edge_pool() {
+  static const bool v = getenv("MQM_EDGE_POOL") && atoi(getenv("MQM_EDGE_POOL")) != 0;
+  return v;
+}
+
+int build_edges_device(const EdgeEntry *h_staged, uint64_t ne, uint64_t nb, EdgeEntry *table, hipStream_t st,
                        uint64_t *digest_sum) {
   constexpr uint32_t P = kEdgeParts;
   const uint64_t n_slots = nb * kEdgesPerBucket;
   if (ne >= kNone || n_slots >= (1ull << 50)) return -1;
-  hipLaunchKernelGGL(k_edge_empty, dim3(grid_for(n_slots * 4)), dim3(256), 0, st, (uint4 *)table, n_slots);
-  EDGE_TRY(hipGetLastError());
-  int rc = 0;
-  if (ne) {
-    const uint64_t n1 = ne;
-    uint32_t *part = nullptr, *idx = nullptr, *part2 = nullptr, *idx2 = nullptr, *spill_cnt = nullptr, *spill = nullptr;
-    unsigned int *cnt = nullptr, *ovf = nullptr;
-    uint64_t *pstart = nullptr;
-    void *tmp = nullptr;
-    size_t tsort = 0, tscan = 0;
-    hipcub::TransformInputIterator<uint64_t, Widen32, const unsigned int *> cnt64(cnt, Widen32{});
-    EDGE_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tsort, part, part2, idx, idx2, (int)n1, 0, 14, st));
-    EDGE_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tscan, cnt64, pstart, (int)P + 1, st));
-    EDGE_TRY(hipMallocAsync((void **)&part, 4 * n1, st));
-    EDGE_TRY(hipMallocAsync((void **)&idx, 4 * n1, st));
-    EDGE_TRY(hipMallocAsync((void **)&part2, 4 * n1, st));
-    EDGE_TRY(hipMallocAsync((void **)&idx2, 4 * n1, st));
-    EDGE_TRY(hipMallocAsync((void **)&cnt, 4 * (P + 1) + 4, st));  // [P]: 0 (the scan's total); ovf after it
-    EDGE_TRY(hipMallocAsync((void **)&pstart, 8 * (P + 1), st));
-    EDGE_TRY(hipMallocAsync((void **)&spill_cnt, 4 * P, st));
-    EDGE_TRY(hipMallocAsync((void **)&spill, 4 * (uint64_t)P * kSpillCap, st));
-    EDGE_TRY(hipMallocAsync(&tmp, std::max(tsort, tscan) + 16, st));
-    ovf = cnt + P + 1;
-    EDGE_TRY(hipMemsetAsync(cnt, 0, 4 * (P + 1) + 4, st));
-    hipLaunchKernelGGL(k_edge_keys, dim3(grid_for(ne)), dim3(256), 0, st, d_staged, ne, nb, part, idx, cnt);
+  int dev = 0;
+  EDGE_TRY(hipGetDevice(&dev));
+  // sizes of the carved parts (256-B aligned)
+  const uint64_t n1 = ne ? ne : 1;
+  size_t tsort = 0, tscan = 0;
+  {
+    uint32_t *np = nullptr;
+    uint64_t *pp = nullptr;
+    hipcub::TransformInputIterator<uint64_t, Widen32, const unsigned int *> c0((const unsigned int *)np, Widen32{});
+    EDGE_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tsort, np, np, np, np, (int)n1, 0, 14, st));
+    EDGE_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tscan, c0, pp, (int)P + 1, st));
+  }
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  const size_t z_staged = al(ne * sizeof(EdgeEntry) + 64), z4 = al(4 * n1), z_cnt = al(4 * (P + 1) + 4),
+               z_pstart = al(8 * (P + 1)), z_spc = al(4 * P), z_spill = al(4 * (uint64_t)P * kSpillCap),
+               z_tmp = al(std::max(tsort, tscan) + 16), z_sum = al(8);
+  const size_t total = z_staged + 4 * z4 + z_cnt + z_pstart + z_spc + z_spill + z_tmp + z_sum;
+  EdgeScratch &sc = edge_scratch(dev);
+  std::unique_lock<std::mutex> lk(sc.mu, std::defer_lock);
+  char *base = nullptr;
+  if (edge_pool()) {
+    EDGE_TRY(hipMallocAsync((void **)&base, total, st));
+  } else {
+    lk.lock();  // (held until the build has synchronised its stream: the region is reused by the next build)
+    if (sc.cap < total) {
+      if (sc.p) retire_device_buffers(dev, {sc.p});
+      sc.p = nullptr;
+      sc.cap = 0;
+      const size_t want = total + total / 4;
+      EDGE_TRY(hipMalloc((void **)&sc.p, want));
+      sc.cap = want;
+    }
+    base = sc.p;
+  }
+  size_t off = 0;
+  auto carve = [&](size_t z) {
+    char *q = base + off;
+    off += z;
+    return q;
+  };
+  EdgeEntry *d_staged = (EdgeEntry *)carve(z_staged);
+  uint32_t *part = (uint32_t *)carve(z4), *idx = (uint32_t *)carve(z4), *part2 = (uint32_t *)carve(z4),
+           *idx2 = (uint32_t *)carve(z4);
+  unsigned int *cnt = (unsigned int *)carve(z_cnt);  // [P]: 0 (the scan's total); ovf after it
+  uint64_t *pstart = (uint64_t *)carve(z_pstart);
+  uint32_t *spill_cnt = (uint32_t *)carve(z_spc), *spill = (uint32_t *)carve(z_spill);
+  void *tmp = carve(z_tmp);
+  unsigned long long *sum = (unsigned long long *)carve(z_sum);
+  const int rc = [&]() -> int {
+    if (ne) EDGE_TRY(hipMemcpyAsync(d_staged, h_staged, ne * sizeof(EdgeEntry), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_edge_empty, dim3(grid_for(n_slots * 4)), dim3(256), 0, st, (uint4 *)table, n_slots);
     EDGE_TRY(hipGetLastError());
-    size_t t1 = tsort;
-    EDGE_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, t1, part, part2, idx, idx2, (int)n1, 0, 14, st));
-    hipcub::TransformInputIterator<uint64_t, Widen32, const unsigned int *> c64(cnt, Widen32{});
-    size_t t2 = tscan;
-    EDGE_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, t2, c64, pstart, (int)P + 1, st));
-    hipLaunchKernelGGL(k_edge_insert, dim3(P / 256), dim3(256), 0, st, d_staged, idx2, pstart, nb, table, spill_cnt,
-                       spill, ovf);
-    EDGE_TRY(hipGetLastError());
-    unsigned int h_ovf = 0;
-    EDGE_TRY(hipMemcpyAsync(&h_ovf, ovf, sizeof(h_ovf), hipMemcpyDeviceToHost, st));
-    EDGE_TRY(hipStreamSynchronize(st));
-    if (h_ovf) {
-      rc = 1;
-    } else {
+    if (ne) {
+      unsigned int *ovf = cnt + P + 1;
+      EDGE_TRY(hipMemsetAsync(cnt, 0, 4 * (P + 1) + 4, st));
+      hipLaunchKernelGGL(k_edge_keys, dim3(grid_for(ne)), dim3(256), 0, st, d_staged, ne, nb, part, idx, cnt);
+      EDGE_TRY(hipGetLastError());
+      size_t t1 = tsort;
+      EDGE_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, t1, part, part2, idx, idx2, (int)n1, 0, 14, st));
+      hipcub::TransformInputIterator<uint64_t, Widen32, const unsigned int *> c64(cnt, Widen32{});
+      size_t t2 = tscan;
+      EDGE_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, t2, c64, pstart, (int)P + 1, st));
+      hipLaunchKernelGGL(k_edge_insert, dim3(P / 256), dim3(256), 0, st, d_staged, idx2, pstart, nb, table, spill_cnt,
+                         spill, ovf);
+      EDGE_TRY(hipGetLastError());
+      unsigned int h_ovf = 0;
+      EDGE_TRY(hipMemcpyAsync(&h_ovf, ovf, sizeof(h_ovf), hipMemcpyDeviceToHost, st));
+      EDGE_TRY(hipStreamSynchronize(st));
+      if (h_ovf) return 1;
       hipLaunchKernelGGL(k_edge_spill, dim3(1), dim3(64), 0, st, d_staged, spill_cnt, spill, nb, table);
       EDGE_TRY(hipGetLastError());
     }
-    for (void *p : {(void *)part, (void *)idx, (void *)part2, (void *)idx2, (void *)cnt, (void *)pstart,
-                    (void *)spill_cnt, (void *)spill, tmp})
-      EDGE_TRY(hipFreeAsync(p, st));
-  }
-  if (rc) return rc;
-  return digest_edges_device(table, n_slots, st, digest_sum);
+    // the digest's sum of per-slot terms
+    EDGE_TRY(hipMemsetAsync(sum, 0, sizeof(unsigned long long), st));
+    hipLaunchKernelGGL(k_edge_digest, dim3(grid_for(n_slots)), dim3(256), 0, st, table, n_slots, sum);
+    EDGE_TRY(hipGetLastError());
+    unsigned long long h = 0;
+    EDGE_TRY(hipMemcpyAsync(&h, sum, sizeof(h), hipMemcpyDeviceToHost, st));
+    EDGE_TRY(hipStreamSynchronize(st));
+    *digest_sum = h;
+    return 0;
+  }();
+  if (edge_pool()) (void)hipFreeAsync(base, st);
+  // (an error part-way may leave work queued on the region: wait for it before the next build reuses it)
+  if (rc < 0) (void)hipStreamSynchronize(st);
+  return rc;
 }
 
 }  // namespace mqm

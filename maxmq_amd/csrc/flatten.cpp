@@ -1185,6 +1185,11 @@ void recycled_free(int device, std::vector<std::pair<void *, size_t>> &held) {
 }
 }  // namespace
 
+bool host_edges_forced() {
+  static const bool v = getenv("MQM_HOST_EDGES") && atoi(getenv("MQM_HOST_EDGES")) != 0;
+  return v;
+}
+
 // MQM_SNAP_VERIFY=1 (diagnostic): after an upload, read the device arrays
 // back and compare them with the host arrays (the edge table: a host build of
 // the same staged edges, by digest); mismatches go to stderr
@@ -1270,15 +1275,9 @@ int upload(std::shared_ptr<HostSnapshot> hs, int device, hipStream_t stream, std
   }
   if (dev_edges) {  // edges.hip; a run-past overflow (never seen) falls back to the host build
     const uint64_t ne = hs->staged->size();
-    void *d_staged = nullptr;
-    if (hipMallocAsync(&d_staged, ne * sizeof(EdgeEntry) + 64, stream) != hipSuccess) return MQM_ENOMEM;
-    if (ne && upload_copy(d_staged, hs->staged->data(), ne * sizeof(EdgeEntry), stream) !=
-                  hipSuccess)
-      return MQM_EHIP;
     uint64_t sum = 0;
-    const int rc = build_edges_device((const EdgeEntry *)d_staged, ne, hs->n_buckets, (EdgeEntry *)g->buffers[1],
-                                      stream, &sum);
-    if (hipFreeAsync(d_staged, stream) != hipSuccess || rc < 0) return MQM_EHIP;
+    const int rc = build_edges_device(hs->staged->data(), ne, hs->n_buckets, (EdgeEntry *)g->buffers[1], stream, &sum);
+    if (rc < 0) return MQM_EHIP;
     if (rc == 1) {
       insert_edges_host(*hs, *hs->staged);
       if (upload_copy(g->buffers[1], hs->edges.data(), sz[1], stream) != hipSuccess)

@@ -105,13 +105,19 @@ struct FlattenCache {
 // `staged` (the host fill of the table and its transfer were most of a
 // rebuild: 18.5 GB at config 3 against 2.2 GB of staged edges).
 int flatten(const Store &st, HostSnapshot *out, bool host_edges = true, FlattenCache *cache = nullptr);
+// MQM_HOST_EDGES=1 (A/B, diagnostics): the edge table is built on the host
+// and copied, never on the device (edges.hip)
+bool host_edges_forced();
 // the edge table from the staged edges, on the host (snapshot.h layout)
 void insert_edges_host(HostSnapshot &hs, const EdgeVec &staged);
 // the same table built on the device into `table` (n_buckets * kEdgesPerBucket
-// slots) from the staged edges already on the device, and its digest (the
-// sum of edge_slot_mix over the slots); 1: a partition's run-past list
-// overflowed its buffer (the caller builds the table on the host instead)
-int build_edges_device(const EdgeEntry *d_staged, uint64_t n_edges, uint64_t n_buckets, EdgeEntry *table,
+// slots) from the staged edges (host memory: copied in first), and its digest
+// (the sum of edge_slot_mix over the slots); 1: a partition's run-past list
+// overflowed its buffer (the caller builds the table on the host instead).
+// The staged copy and every temporary live in a per-device scratch region
+// that is kept from build to build (edges.hip; MQM_EDGE_POOL=1: the
+// stream-ordered pool instead, round 5's form)
+int build_edges_device(const EdgeEntry *h_staged, uint64_t n_edges, uint64_t n_buckets, EdgeEntry *table,
                        hipStream_t stream, uint64_t *digest_sum);
 // digest sum of a device table (build_edges_device's, for a table copied in)
 int digest_edges_device(const EdgeEntry *table, uint64_t n_slots, hipStream_t stream, uint64_t *digest_sum);

@@ -59,6 +59,15 @@ for step in "$@"; do
              tests/test_gpu_serve_churn.py -m gpu --timeout 300 > $OUT/pytest_stamp.log 2>&1 ;;
     verifyt) MQM_SNAP_RECYCLE=1 MQM_RECYCLE_QUARANTINE_MS=0 MQM_SNAP_VERIFY=1 timeout -k 10 500 $PYT -s \
              tests/test_gpu_serve_churn.py -m gpu --timeout 300 > $OUT/pytest_verify.log 2>&1 ;;
+    recyclematrix)  # served churn tests with recycled snapshot buffers (no quarantine), per edge-build memory; each variant 3x
+          for V in scratch:X=0 pool:MQM_EDGE_POOL=1 hostedges:MQM_HOST_EDGES=1; do
+            N=${V%%:*}; E=${V#*:}
+            for k in 1 2 3; do
+              env $E MQM_SNAP_RECYCLE=1 MQM_RECYCLE_QUARANTINE_MS=0 timeout -k 10 300 $PYT -s tests/test_gpu_serve_churn.py \
+                -m gpu --timeout 200 > $OUT/pytest_recycle_${N}_$k.log 2>&1 && echo "$N $k passed" >> $OUT/matrix.txt \
+                || echo "$N $k FAILED: $(grep -o '[0-9]* of [0-9]* results differ' $OUT/pytest_recycle_${N}_$k.log | head -2 | tr '\n' ' ')" >> $OUT/matrix.txt
+            done
+          done ;;
     recyclet) MQM_SNAP_RECYCLE=1 MQM_RECYCLE_QUARANTINE_MS=0 timeout -k 10 500 $PYT -s \
              tests/test_gpu_serve_churn.py tests/test_gpu_serve.py -m gpu --timeout 300 > $OUT/pytest_recycle.log 2>&1 ;;
     pathab) for V in path:X=0 nopath:MQM_PATH_FILTER=0 path2:X=0; do
