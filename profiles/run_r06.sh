@@ -6,6 +6,8 @@
 #   pathab  : `fast` with the walk's path filter, without it (MQM_PATH_FILTER=0), with it again
 #   pairab  : `fast` with the paired-position window copy (MQM_WINCOPY_PAIR=1), then without
 #   pairpar : parity subset with the paired window copy
+#   cooppar : parity + queued tests with the cooperative walk loads (MQM_WALK_COOP=1)
+#   coopab  : `fast` with / without / with the cooperative walk loads
 #   tests   : every -m gpu test                          -> gpurun_out/TAG/pytest_gpu.log
 #   serve   : the per-publish server tests (incl. served calls under Subscribe/Unsubscribe churn)
 #   ab / c4ab: `fast` (C3) / the C4 shard bench with the round-5 walk (paired node slots) and long-part
@@ -80,6 +82,12 @@ for step in "$@"; do
         done ;;
     pairpar) MQM_WINCOPY_PAIR=1 timeout -k 10 500 $PYT tests/test_gpu_parity.py -m gpu --timeout 300 \
              -k "config_vs_oracle or edge_cases or kat or full_size" > $OUT/pytest_pair.log 2>&1 ;;
+    cooppar) MQM_WALK_COOP=1 timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_gpu_queued.py -m gpu --timeout 300 \
+             > $OUT/pytest_coop.log 2>&1 ;;
+    coopab) for V in coop:MQM_WALK_COOP=1 base:X=0 coop2:MQM_WALK_COOP=1; do
+          N=${V%%:*}; E=${V#*:}
+          env $E timeout -k 10 400 python3 -u bench.py $FAST --ident-steps 0 > $OUT/bench_fast_$N.json 2> $OUT/bench_fast_$N.log || exit 1
+        done ;;
     churnt) timeout -k 10 500 $PYT tests/test_gpu_serve_churn.py -m gpu --timeout 300 > $OUT/pytest_churn.log 2>&1 ;;
     serve) timeout -k 10 600 $PYT tests/test_gpu_serve.py tests/test_gpu_serve_churn.py tests/test_gpu_shim.py -m gpu \
              --timeout 300 > $OUT/pytest_serve.log 2>&1 ;;
