@@ -137,20 +137,6 @@ uint32_t grid_for(uint64_t n) { return (uint32_t)std::max<uint64_t>(1, std::min<
 
 }  // namespace
 
-int digest_edges_device(const EdgeEntry *table, uint64_t n_slots, hipStream_t st, uint64_t *digest_sum) {
-  unsigned long long *sum = nullptr;
-  EDGE_TRY(hipMallocAsync((void **)&sum, sizeof(unsigned long long), st));
-  EDGE_TRY(hipMemsetAsync(sum, 0, sizeof(unsigned long long), st));
-  hipLaunchKernelGGL(k_edge_digest, dim3(grid_for(n_slots)), dim3(256), 0, st, table, n_slots, sum);
-  EDGE_TRY(hipGetLastError());
-  unsigned long long h = 0;
-  EDGE_TRY(hipMemcpyAsync(&h, sum, sizeof(h), hipMemcpyDeviceToHost, st));
-  EDGE_TRY(hipFreeAsync(sum, st));
-  EDGE_TRY(hipStreamSynchronize(st));
-  *digest_sum = h;
-  return 0;
-}
-
 // The build's device memory: the staged edges and every temporary, carved
 // from one region per device that is kept from build to build (grown, never
 // shrunk; a grown-out region is freed by the index layer's reaper, which

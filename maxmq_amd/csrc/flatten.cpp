@@ -1092,23 +1092,30 @@ hipStream_t reclaim_stream(int device) {
 // under churn missed the newest subscriptions (tests/test_gpu_serve_churn.py,
 // r05o-r05r), and tools/reuse_probe.hip saw a kernel on another stream read
 // pool memory that a synchronised host -> device copy had refilled without the
-// new data (r05s).  The default is hipMalloc / hipFree, the frees handed to
-// the index layer's reaper (retire_device_buffers), which stops the
-// per-publish servers first: hipFree waits for every running kernel.
+// new data (r05s).  Snapshot buffers are hipMalloc'd and recycled in place
+// (below); nothing in the library takes pool memory any more.
 static bool snap_pool() {
   static const bool v = getenv("MQM_SNAP_POOL") && atoi(getenv("MQM_SNAP_POOL")) != 0;
   return v;
 }
 
-// Snapshot buffers are recycled, not freed: a destroyed snapshot's buffers go
-// to a per-device free list and the next upload takes the smallest one that
-// fits (a rebuild's arrays are within a few percent of the last one's).
-// Refilling a kept hipMalloc buffer in place is read correctly by kernels on
-// other streams (tools/reuse_probe.hip, r05u), unlike a pool reallocation;
-// and no hipFree — which waits for the per-publish server — runs at all while
-// the free list stays under kRecycleCap.  Above it, the largest spare buffers
-// go to the index layer's reaper (retire_device_buffers), which stops the
-// servers before freeing.
+// Snapshot buffers are recycled, not freed (the default since round 6): a
+// destroyed snapshot's buffers go to a per-device free list and the next
+// upload takes the smallest one that fits (a rebuild's arrays are within a
+// few percent of the last one's).  Refilling a kept hipMalloc buffer in place
+// is read correctly by kernels on other streams (tools/reuse_probe.hip r05u,
+// tools/l2_probe.hip r06b); and no hipFree — which waits for the per-publish
+// server — runs at all while the free list stays under kRecycleCap.  Above
+// it, the largest spare buffers go to the index layer's reaper
+// (retire_device_buffers), which stops the servers before freeing.  (Round 5
+// found recycling correct only with a 2-s reuse quarantine; the cause was not
+// the recycled buffers but the device edge build's temporaries from the
+// stream-ordered pool, which served the build a previous build's staged edges
+// now and then — the reaper's hipFree between builds had hidden it.  With the
+// temporaries in a kept scratch region, edges.hip, served churn results equal
+// the oracle at every version with no quarantine: r06d, 3 of 3 runs, against
+// 3 of 3 failing with the pool temporaries.)  MQM_SNAP_RECYCLE=0: hipMalloc /
+// hipFree per snapshot through the reaper (round 5's default).
 namespace {
 constexpr size_t kRecycleCap = 96ull << 30;  // spare bytes kept per device
 struct Spare {
@@ -1124,13 +1131,15 @@ int64_t now_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
       .count();
 }
+// MQM_RECYCLE_QUARANTINE_MS: a retired buffer is reused only after this long
+// (default 0; round 5's workaround was 2000)
 const int64_t kQuarantineNs = [] {
   const char *e = getenv("MQM_RECYCLE_QUARANTINE_MS");
-  return (int64_t)(e ? atoi(e) : 2000) * 1000000;
+  return (int64_t)(e ? atoi(e) : 0) * 1000000;
 }();
-// MQM_SNAP_RECYCLE=1 (A/B): recycle snapshot buffers (default: hipFree on the reaper)
+// MQM_SNAP_RECYCLE=0: hipFree each snapshot on the reaper instead of recycling
 bool snap_recycle() {
-  static const bool v = getenv("MQM_SNAP_RECYCLE") && atoi(getenv("MQM_SNAP_RECYCLE")) != 0;
+  static const bool v = !getenv("MQM_SNAP_RECYCLE") || atoi(getenv("MQM_SNAP_RECYCLE")) != 0;
   return v;
 }
 Recycler &recycler() {

@@ -119,8 +119,6 @@ void insert_edges_host(HostSnapshot &hs, const EdgeVec &staged);
 // stream-ordered pool instead, round 5's form)
 int build_edges_device(const EdgeEntry *h_staged, uint64_t n_edges, uint64_t n_buckets, EdgeEntry *table,
                        hipStream_t stream, uint64_t *digest_sum);
-// digest sum of a device table (build_edges_device's, for a table copied in)
-int digest_edges_device(const EdgeEntry *table, uint64_t n_slots, hipStream_t stream, uint64_t *digest_sum);
 // host threads a flatten (and the snapshot digest) runs on: mqm_build_threads,
 // else MQM_BUILD_THREADS, else min(16, hardware threads)
 uint32_t build_threads();

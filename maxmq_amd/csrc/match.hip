@@ -53,6 +53,7 @@
 #include <vector>
 
 #include "device.h"
+#include "flatten.h"
 #include "match.h"
 
 // MQM_WALK_STATS=1: count the walk's literal probes, the ones that found no
@@ -2489,19 +2490,33 @@ int Workspace::drain() {
   return 0;
 }
 
+// Workspace memory comes from hipMalloc, and a grown-out buffer goes to the
+// index layer's reaper (flatten.h retire_device_buffers: it stops the
+// per-publish servers, then hipFree — which waits for every kernel on the
+// device).  Round 5 used the stream-ordered pool (hipMallocAsync /
+// hipFreeAsync), whose reuse of freed memory served kernels stale contents
+// (tools/reuse_probe.hip r05s/r05u; the device edge build's pool temporaries
+// made recycled snapshots miss their newest edges, r06d): no pool memory
+// anywhere in the library now.
+static void retire(void *p) {
+  if (!p) return;
+  int dev = -1;
+  (void)hipGetDevice(&dev);
+  retire_device_buffers(dev, {p});
+}
+
 int Workspace::reserve(void **p, size_t *cap, size_t need) {
   if (*cap >= need && *p) return 0;
   if (*p) {
     // queued kernels of this call (cur) or of earlier calls (last_use) may
-    // still read the old buffer; hipFree would also wait for every other
-    // stream on the device, hipFreeAsync does not
+    // still read the old buffer
     if (drain()) return -3;
-    (void)hipFreeAsync(*p, cur);
+    retire(*p);
   }
   *p = nullptr;
   size_t n = std::max<size_t>(need, 256);
   n = n + n / 4;
-  if (hipMallocAsync(p, n, cur) != hipSuccess || hipStreamSynchronize(cur) != hipSuccess) {
+  if (hipMalloc(p, n) != hipSuccess) {
     *p = nullptr;
     *cap = 0;
     return -2;
@@ -2519,10 +2534,10 @@ int Workspace::grow_keep(Slot s, size_t used_bytes, size_t need, hipStream_t st)
   if (reserve(&p, &cap, need)) return -2;
   if (used_bytes && (hipMemcpyAsync(p, b.p, used_bytes, hipMemcpyDeviceToDevice, st) != hipSuccess ||
                      hipStreamSynchronize(st) != hipSuccess)) {
-    (void)hipFreeAsync(p, cur);
+    retire(p);
     return -3;
   }
-  if (b.p) (void)hipFreeAsync(b.p, cur);
+  retire(b.p);
   b.p = p;
   b.cap = cap;
   return 0;
@@ -2538,8 +2553,7 @@ uint64_t *Workspace::pinned_u64() {
 Workspace::~Workspace() {
   // `cur` may name a caller's stream that no longer exists: wait on our event
   if (used && last_use) (void)hipEventSynchronize(last_use);
-  for (auto &b : bufs)
-    if (b.p) (void)hipFree(b.p);
+  for (auto &b : bufs) retire(b.p);  // (hipFree would wait for a running per-publish server)
   if (last_use) (void)hipEventDestroy(last_use);
   if (host_pinned) (void)hipHostFree(host_pinned);
   for (auto &e : ev)
