@@ -1070,6 +1070,7 @@ def serve_churn(idx, w, args):
         m_v = np.zeros(mcap, np.uint64)
         o = Out()
         st0 = idx.commit_state()
+        c0 = idx.serve_counters()
         ns = D.mqd_serve_churn(C.byref(api), idx._h, p(data), p(offs), n, T, seconds, cap, sample, p(cl.data),
                                p(cl.offs), p(fl.data), p(fl.offs), m, rate, p(lat), p(done), p(s_t), p(s_v), mcap,
                                p(m_t), p(m_v), C.byref(o))
@@ -1106,6 +1107,11 @@ def serve_churn(idx, w, args):
             r["last_build_phases_ms"] = {"replay": ph[0], "flatten": ph[1], "upload": ph[2],
                                          "build_threads": int(ph[3]), "kept_shape": bool(ph[4])}
         r["host_phase_max"] = idx.serve_host_max_us()
+        # the served path's safety nets during the leg (all 0 in a healthy run:
+        # forced relaunches, slot / result timeouts; stale = decoded again on
+        # the batch path because the result's host snapshot was gone)
+        c1 = idx.serve_counters()
+        r["serve_counters"] = {k: c1[k] - c0[k] for k in c1}
         return r
 
     run(2.0, 0)  # warm: the server, every caller's path

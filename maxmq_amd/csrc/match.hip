@@ -49,7 +49,6 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
-#include <type_traits>
 #include <vector>
 
 #include "device.h"
@@ -210,31 +209,6 @@ struct TopicLds {              // k_walk context of one topic (one lane group)
 };
 static_assert(kStage % 16 == 0 && kICap >= 3, "walk context");
 static_assert((sizeof(TopicLds) / 4) % 2 == 1, "bank-skewed topic contexts");
-
-// k_walk<.., kCoop = true>: the group's item loads are cooperative — the 4
-// lanes of a topic's group load the 4 16-B parts of ONE item's 64-B entry in
-// one instruction (global_load_lds_dwordx4 straight into LDS), the item's
-// owner lane reads them back.  A per-lane 64-B entry costs 4 instructions
-// that each touch 64 different lines; the cooperative form touches 16 lines
-// per instruction: tools/calib_fetch, 2.2x the random-entry rate (r03a).  The
-// staging takes 4 KB of LDS per wavefront (one 1-KB block per item slot of
-// the groups); it also holds the topics' first bytes while their keys are
-// built (block 0), and the frontier lists shrink to kICapCoop items a level,
-// so a block still fits four to a CU
-constexpr int kICapCoop = 40;
-struct TopicLdsCoop {
-  uint16_t sep[kLMax];
-  uint32_t item[2][kICapCoop];
-  uint32_t pad[1];  // odd dword stride (as TopicLds)
-};
-static_assert((sizeof(TopicLdsCoop) / 4) % 2 == 1, "bank-skewed topic contexts");
-typedef __attribute__((address_space(3))) void lds_void;
-
-// lane gl of a 4-lane quad gets lane q's v (DPP quad_perm [q, q, q, q])
-template <int q>
-__device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, q * 0x55, 0xF, 0xF, false);
-}
 
 __device__ __forceinline__ void wave_lds_sync() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -412,88 +386,7 @@ __device__ __forceinline__ void ident_put(const Outputs &o, uint64_t ib, bool ha
 }
 
 
-// walk_step (device.h) with the item loads cooperative inside each 4-lane
-// group (k_walk<.., kCoop>): lane gl of a group owns the group's item gl;
-// item slot p's loads are issued by all 4 lanes of every group that has an
-// item p — part gl of its entry, 16 B, straight into the staging block p —
-// and the owners read their entries back.  Every lane of the wavefront calls
-// it (the loads and the DPP broadcasts are wave-wide).  Probes that run on
-// past their first slot (linear probing, load 0.12: rare) load per lane.
-__device__ __forceinline__ uint32_t walk_step_coop(const DeviceSnapshot &s, bool do_probe, bool do_desc, uint32_t id,
-                                                   uint64_t k0, uint64_t k1, const uint8_t *tok, uint32_t tok_len,
-                                                   NodeDesc *desc, uint4 *coop, int lane) {
-  const int gl = lane & 3;
-  const Key key{k0, k1};
-  const uint64_t nslots = s.n_buckets * kEdgesPerBucket;
-  uint64_t slot = do_probe ? bucket_of(edge_hash(id, key), s.n_buckets) * kEdgesPerBucket : 0;
-  const uint64_t addr = do_probe ? reinterpret_cast<uint64_t>(s.edges + slot)
-                                 : do_desc ? reinterpret_cast<uint64_t>(s.nodes + id) : 0ull;
-  const uint32_t np = do_probe ? 4u : do_desc ? 2u : 0u;  // 16-B parts: an edge entry, a descriptor
-  const uint64_t used = __ballot(np != 0);
-  constexpr uint64_t kQ = 0x1111111111111111ull;  // the lanes gl == 0 of every group
-#define MQM_COOP_SLOT(p)                                                                                  \
-  if (used & (kQ << (p))) {                                                                               \
-    const uint32_t alo = quad_bcast<p>((uint32_t)addr), ahi = quad_bcast<p>((uint32_t)(addr >> 32));      \
-    if ((uint32_t)gl < quad_bcast<p>(np))                                                                 \
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4 *>(((uint64_t)ahi << 32) | alo) + gl, \
-                                       (lds_void *)(coop + (p) * kWave), 16, 0, 0);                       \
-  }
-  MQM_COOP_SLOT(0)
-  MQM_COOP_SLOT(1)
-  MQM_COOP_SLOT(2)
-  MQM_COOP_SLOT(3)
-#undef MQM_COOP_SLOT
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-  uint4 x0 = make_uint4(0, 0, 0, 0), x1 = x0, x2 = x0, x3 = x0;
-  const uint4 *own = coop + gl * kWave + (lane & ~3);  // item slot gl's block, this group's 4 parts
-  if (np) {
-    x0 = own[0];
-    x1 = own[1];
-  }
-  if (np == 4u) {
-    x2 = own[2];
-    x3 = own[3];
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (read before the next step's loads land)
-  __builtin_amdgcn_wave_barrier();
-  uint32_t c = kNone;
-  bool more = false;
-  if (do_desc) {
-    c = id;
-    *desc = NodeDesc{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-  }
-  for (;;) {
-    if (do_probe && x1.x != kNone) {
-      const bool hit = x1.x == id && (((uint64_t)x0.y << 32) | x0.x) == k0 && (((uint64_t)x0.w << 32) | x0.z) == k1;
-      bool ok = hit;
-      if (hit && key_is_long(key)) {  // hashed long token: verify the bytes
-        ok = x1.w == tok_len;
-        for (uint32_t i = 0; ok && i < tok_len; i++) ok = s.tok_pool[x1.z + i] == tok[i];
-      }
-      if (ok) {
-        c = x1.y;
-        *desc = NodeDesc{x2.x, x2.y, x2.z, x2.w, x3.x, x3.y, x3.z, x3.w};
-      }
-      more = !ok;
-    } else {
-      more = false;
-    }
-    if (!__any(more)) break;  // wave-uniform
-    if (more) {
-      slot = slot + 1 == nslots ? 0 : slot + 1;
-      const uint4 *e = reinterpret_cast<const uint4 *>(s.edges + slot);
-      x0 = e[0];
-      x1 = e[1];
-      x2 = e[2];
-      x3 = e[3];
-    }
-    do_probe = more;
-  }
-  return c;
-}
-
-template <int kG, int kChunk = 0, bool kSlots = true, bool kCoop = false>
+template <int kG, int kChunk = 0, bool kSlots = true>
 __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_eu(4))) void k_walk(DeviceSnapshot s, const uint8_t *__restrict__ tbytes,
                                                            const uint64_t *__restrict__ toffs, uint32_t n,
                                                            Outputs o) {
@@ -501,24 +394,10 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
   constexpr int kLPer = (kLMax + kG - 1) / kG;  // level keys held per lane
   constexpr uint32_t kGMask = (1u << kG) - 1u;
   static_assert(kLMax % kG == 0 || kG > kLMax, "levels per lane");
-  static_assert(!kCoop || (kG == 4 && !kSlots), "the cooperative loads: quads of lanes, no paired slots");
-  using TL = std::conditional_t<kCoop, TopicLdsCoop, TopicLds>;
-  constexpr uint32_t kIC = kCoop ? kICapCoop : kICap;
-  __shared__ TL lds_all[kWalkWaves * kGroups];
-  // (kCoop) the item staging, [wave][item slot][lane] 16 B: slot p's block
-  // holds item p of every group, its 4 parts at lanes 4g .. 4g + 3
-  __shared__ uint4 coop_all[kCoop ? kWalkWaves * 4 * kWave : 1];
+  __shared__ TopicLds lds_all[kWalkWaves * kGroups];
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / kG, gl = lane & (kG - 1), gbase = g * kG;
-  TL &L = lds_all[(threadIdx.x / kWave) * kGroups + g];
-  uint4 *coop = coop_all + (kCoop ? (threadIdx.x / kWave) * 4 * kWave : 0);
-  // the topic's first kStage bytes: its own array, or (kCoop) block 0 of the staging
-  uint8_t *stage = [&]() -> uint8_t * {
-    if constexpr (kCoop)
-      return reinterpret_cast<uint8_t *>(coop + 4 * g);
-    else
-      return L.stage;
-  }();
+  TopicLds &L = lds_all[(threadIdx.x / kWave) * kGroups + g];
   const uint32_t gmask_lt = (1u << gl) - 1u;
   const uint64_t stride = (uint64_t)gridDim.x * kWalkWaves * kGroups;
   const NodeDesc root = load_desc(s.nodes);
@@ -592,7 +471,7 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
       }
       if (base == 0) {
 #pragma unroll
-        for (int k = 0; k < 4; k++) reinterpret_cast<uint32_t *>(stage)[4 * gl + k] = b4[k];
+        for (int k = 0; k < 4; k++) reinterpret_cast<uint32_t *>(L.stage)[4 * gl + k] = b4[k];
         dollar = (__shfl(b4[0], gbase, 64) & 0xFFu) == '$';
       }
       const uint32_t sm = slash_mask16(b4);  // the lane's '/' bytes (keys.h)
@@ -619,7 +498,7 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
       if (lv < nlev && lv < (uint32_t)kLMax) {
         const uint32_t st = lv == 0 ? 0 : L.sep[lv - 1] + 1;
         const uint32_t en = (lv < nsep) ? L.sep[lv] : len;
-        Key k = en <= (uint32_t)kStage ? make_key([&](uint32_t i) { return stage[st + i]; }, en - st)
+        Key k = en <= (uint32_t)kStage ? make_key([&](uint32_t i) { return L.stage[st + i]; }, en - st)
                                        : make_key([&](uint32_t i) { return tp[st + i]; }, en - st);
         my_k0[j] = k.k0;
         my_k1[j] = k.k1;
@@ -633,11 +512,9 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
       if (root.plus != kNone) L.item[0][k++] = (root.plus << 2) | (kSlots ? kItemPlusKnown : kItemPlus);
       if (root.hash != kNone) L.item[0][k++] = (root.hash << 2) | kItemHash;
     }
-    if constexpr (kSlots) {
-      if (root.plus != kNone) {  // (lanes gl copy words gl, gl + kG, ...)
+    if (kSlots && root.plus != kNone) {  // (lanes gl copy words gl, gl + kG, ...)
 #pragma unroll
-        for (int w = 0; w < 8; w += kG) L.pdesc[0][0][w + gl] = root_plus[w + gl];
-      }
+      for (int w = 0; w < 8; w += kG) L.pdesc[0][0][w + gl] = root_plus[w + gl];
     }
     const uint32_t root_items = (((root.sh_cnt_flags >> 24) & kFlagHasLiteral) ? 1u : 0u) +
                                 (root.plus != kNone ? 1u : 0u) + (root.hash != kNone ? 1u : 0u);
@@ -699,32 +576,26 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
         const bool slot_load = live && !lit && !known;
         bool pk = false;
         NodeDesc dc;
-        uint32_t c;
-        if constexpr (kCoop) {
-          c = walk_step_coop(s, live && lit && !lit_is_wild, slot_load, id, k0, k1, tp + tst, tln, &dc, coop, lane);
-        } else if constexpr (!kSlots) {
-          c = walk_step(s, live && lit && !lit_is_wild, slot_load, id, id, k0, k1, tp + tst, tln, &dc);
-        } else {
-          c = walk_step_slot(s, live && lit && !lit_is_wild, slot_load, id, id, k0, k1, tp + tst, tln, &dc,
-                             [&](bool ld, const uint4 &a0, const uint4 &a1, const uint4 &p0, const uint4 &p1) {
-                               // (pushed: has_next and children; x.plus = a0.x, flags = a1.w >> 24)
-                               const bool want3 =
-                                   ld && has_next && ((a1.w >> 24) & kFlagHasChildren) && a0.x != kNone;
-                               const uint32_t mw = (uint32_t)(__ballot(want3) >> gbase) & kGMask;
-                               const uint32_t w3 = k3w + __popc(mw & gmask_lt);
-                               pk = want3 && w3 < (uint32_t)kPK;
-                               k3w += __popc(mw);
-                               if (pk) {
-                                 uint32_t *q = L.pdesc[(d + 1) & 1][w3];
-                                 q[0] = p0.x, q[1] = p0.y, q[2] = p0.z, q[3] = p0.w;
-                                 q[4] = p1.x, q[5] = p1.y, q[6] = p1.z, q[7] = p1.w;
-                               }
-                             });
-          if (known) {
-            const uint32_t *q = L.pdesc[d & 1][r3];
-            dc = NodeDesc{q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7]};
-            c = id;
-          }
+        uint32_t c = !kSlots ? walk_step(s, live && lit && !lit_is_wild, slot_load, id, id, k0, k1, tp + tst, tln, &dc)
+                             : walk_step_slot(s, live && lit && !lit_is_wild, slot_load, id, id, k0, k1, tp + tst, tln, &dc,
+                                    [&](bool ld, const uint4 &a0, const uint4 &a1, const uint4 &p0, const uint4 &p1) {
+                                      // (pushed: has_next and children; x.plus = a0.x, flags = a1.w >> 24)
+                                      const bool want3 = ld && has_next && ((a1.w >> 24) & kFlagHasChildren) &&
+                                                         a0.x != kNone;
+                                      const uint32_t mw = (uint32_t)(__ballot(want3) >> gbase) & kGMask;
+                                      const uint32_t w3 = k3w + __popc(mw & gmask_lt);
+                                      pk = want3 && w3 < (uint32_t)kPK;
+                                      k3w += __popc(mw);
+                                      if (pk) {
+                                        uint32_t *q = L.pdesc[(d + 1) & 1][w3];
+                                        q[0] = p0.x, q[1] = p0.y, q[2] = p0.z, q[3] = p0.w;
+                                        q[4] = p1.x, q[5] = p1.y, q[6] = p1.z, q[7] = p1.w;
+                                      }
+                                    });
+        if (known) {
+          const uint32_t *q = L.pdesc[d & 1][r3];
+          dc = NodeDesc{q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7]};
+          c = id;
         }
         const bool found = c != kNone;
 #if MQM_WALK_STATS
@@ -821,7 +692,7 @@ __global__ __launch_bounds__(kWave *kWalkWaves) __attribute__((amdgpu_waves_per_
         const uint32_t m_i0 = (uint32_t)(__ballot(n_items & 1u) >> gbase) & kGMask;
         const uint32_t m_i1 = (uint32_t)(__ballot(n_items & 2u) >> gbase) & kGMask;
         const uint32_t t_items = __popc(m_i0) + 2 * __popc(m_i1);
-        if (nnext + t_items > kIC) {
+        if (nnext + t_items > (uint32_t)kICap) {
           why = kWhyFrontier;
           break;
         }
@@ -1754,12 +1625,6 @@ __global__ __launch_bounds__(kBigThreads) void k_multi_part(DeviceSnapshot s, Ou
 // MQM_RESOLVE=1 every light topic, MQM_RESOLVE=0 none,
 // MQM_RESOLVE_MIN=m the threshold.
 static bool walk_slots() { return slots_enabled(); }
-// MQM_WALK_COOP=1: the walk's item loads cooperative inside each topic's lane
-// group (k_walk<.., kCoop>, walk_step_coop)
-static bool walk_coop() {
-  static const bool v = getenv("MQM_WALK_COOP") && atoi(getenv("MQM_WALK_COOP")) != 0;
-  return v;
-}
 static bool desc_copy_on() {
   static const bool v = getenv("MQM_DESC_COPY") && atoi(getenv("MQM_DESC_COPY")) != 0;
   return v;
@@ -2836,9 +2701,6 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
       hipLaunchKernelGGL(k_walk<kWalkG>, dim3(blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o);
     else if (walk_slots() && s.slots)
       hipLaunchKernelGGL((k_walk<kWalkG, 4>), dim3(blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs, n, o);
-    else if (walk_coop())
-      hipLaunchKernelGGL((k_walk<kWalkG, 4, false, true>), dim3(blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes,
-                         d_offs, n, o);
     else
       hipLaunchKernelGGL((k_walk<kWalkG, 4, false>), dim3(blocks), dim3(kWave * kWalkWaves), 0, st, s, d_bytes, d_offs,
                          n, o);
