@@ -90,8 +90,11 @@ struct mqd_host_api {
   free_fn result_free;
 };
 
+// (n_batches calls over the n_distinct batches in the topic buffer, cycling:
+// many calls amortise the threads' start and the last calls' tail)
 int64_t mqd_host_path(const mqd_host_api *api, void *h, const char *bytes, const uint64_t *offs, uint32_t per,
-                      uint32_t n_batches, int threads, int consume, uint64_t *deliveries, uint64_t *checksum) {
+                      uint32_t n_batches, uint32_t n_distinct, int threads, int consume, uint64_t *deliveries,
+                      uint64_t *checksum) {
   std::atomic<uint32_t> next{0};
   std::atomic<int> failed{0};
   std::atomic<uint64_t> dsum{0}, csum{0};
@@ -107,7 +110,7 @@ int64_t mqd_host_path(const mqd_host_api *api, void *h, const char *bytes, const
         const uint32_t b = next.fetch_add(1);
         if (b >= n_batches) break;
         void *res = nullptr;
-        if (api->batch(h, bytes, offs + (uint64_t)b * per, per, &res) != 0) {
+        if (api->batch(h, bytes, offs + (uint64_t)(b % n_distinct) * per, per, &res) != 0) {
           failed++;
           break;
         }
