@@ -369,8 +369,9 @@ __device__ __forceinline__ const uint4 *rec_tail(const uint32_t *recs, uint32_t 
 __device__ __forceinline__ uint64_t ident_base(const Outputs &o, uint32_t t, uint32_t M, bool leader) {
   if (!o.iscratch) return ~0ull;
   const uint64_t ib = o.imstart[t];
-  if (ib + M > o.icap) {
-    if (leader) atomicOr(&o.ctr->i_ovf, 1ull);
+  if (ib + M > o.icap) {  // (one atomic once the flag is up, not one per topic)
+    if (leader && !__hip_atomic_load(&o.ctr->i_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      atomicOr(&o.ctr->i_ovf, 1ull);
     return ~0ull;
   }
   return ib;
@@ -1270,7 +1271,10 @@ struct alignas(8) SmallLds {
 };
 static_assert(sizeof(SmallLds) % 256 == 8, "bank-skewed group contexts");
 
-template <int kOcc>
+// kIdent: the merges list Identifiers (Outputs::iscratch); a variant of its
+// own, so the plain merges keep their registers (k_merge 72 VGPRs, 7 waves /
+// SIMD; with the listing compiled in: 82, 5 — r06f, 1.08 -> 1.26 ms on C3)
+template <int kOcc, bool kIdent = false>
 __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_eu(kOcc))) void k_merge_small(
     DeviceSnapshot s, Outputs o, const uint32_t *__restrict__ list, const unsigned int *__restrict__ count) {
   constexpr int kMPer = kSmallMultiS / kSE, kRecPer = kSRecPer;
@@ -1305,30 +1309,38 @@ __global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_
     t_nn = i + 2 * ngroups < nl ? list[i + 2 * ngroups] : 0;
     wave_lds_sync();
     const uint32_t nh = L.rec[0] & 0xFFu, Ss = L.rec[1], M = L.rec[2];
-    const uint64_t ib = ident_base(o, t, M, gl == 0);
+    const uint64_t ib = kIdent ? ident_base(o, t, M, gl == 0) : ~0ull;
     rec_prefix<kSE, kSmallHits>(L.rec, nh, gl);
     wave_lds_sync();
-    uint32_t mcl[kMPer], mw[kMPer], mrk[kMPer], msid[kMPer];
+    uint32_t mcl[kMPer], mw[kMPer], mrk[kMPer];
 #pragma unroll
     for (int k = 0; k < kMPer; k++) {
       const uint32_t q = gl + k * kSE;
       uint32_t h;
       const uint32_t sid = multi_sid(L.rec, nh, q < M ? q : 0, &h);
-      msid[k] = sid;
       mrk[k] = rec_at(L.rec, h, kFieldRank);
       const SubEnt e = load_sub(s, sid);
       mcl[k] = e.client;
       mw[k] = e.word;
     }
+    uint32_t im = 0;  // (kIdent) bit k: entry k's Identifier is > 0 — one register across the merge
+    if constexpr (kIdent) {
+#pragma unroll
+      for (int k = 0; k < kMPer; k++) im |= (mw[k] & kWordIdent) ? 1u << k : 0u;
+    }
     const uint32_t D = merge_multi<kSE, kMPer>(MergeTable{L.tkb, L.tfirst}, kSmallTab, mcl, mw, mrk, M, gl,
                                                gbase, o.dout, db, Ss, o.dcap, &o.ctr->oob);
     if (gl == 0) o.dcount[t] = D;
-    if (o.iscratch) {  // (wave-uniform: every group runs the ballots)
+    if constexpr (kIdent) {  // (wave-uniform: every group runs the ballots; sids again from the record in LDS)
       uint32_t nid = 0;
       const uint64_t glt = (1ull << gl) - 1ull;
 #pragma unroll
-      for (int k = 0; k < kMPer; k++)
-        ident_put<kSE>(o, ib, ib != ~0ull && gl + k * kSE < M && (mw[k] & kWordIdent), msid[k], gbase, glt, nid);
+      for (int k = 0; k < kMPer; k++) {
+        const uint32_t q = gl + k * kSE;
+        uint32_t h;
+        const uint32_t sid = multi_sid(L.rec, nh, q < M ? q : 0, &h);
+        ident_put<kSE>(o, ib, ib != ~0ull && q < M && ((im >> k) & 1u), sid, gbase, glt, nid);
+      }
       if (gl == 0 && ib != ~0ull) o.icount[t] = nid;
     }
     wave_lds_sync();
@@ -1342,6 +1354,7 @@ struct alignas(16) MergeLds {
   uint32_t rec[kRecLds];
 };
 
+template <bool kIdent = false>
 __global__ __launch_bounds__(kWave *kEmitWaves) void k_merge(DeviceSnapshot s, Outputs o,
                                                             const uint32_t *__restrict__ list,
                                                             const unsigned int *__restrict__ count) {
@@ -1368,34 +1381,44 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_merge(DeviceSnapshot s, O
     if (i + nw < nl) fetch(i + nw);
     wave_lds_sync();
     const uint32_t nh = L.rec[0] & 0xFFu, Ss = L.rec[1], M = L.rec[2];
-    const uint64_t ib = ident_base(o, t, M, lane == 0);
+    const uint64_t ib = kIdent ? ident_base(o, t, M, lane == 0) : ~0ull;
     const uint4 *gt = rec_tail(o.recs, t);
     for (uint32_t u = 16 + lane; u < 1 + nh; u += kWave) rec4[u] = gt[-(int)u];
     wave_lds_sync();
     rec_prefix<kWave>(L.rec, nh, lane);
     wave_lds_sync();
-    uint32_t mcl[kMPer], mw[kMPer], mrk[kMPer], msid[kMPer];
+    uint32_t mcl[kMPer], mw[kMPer], mrk[kMPer];
 #pragma unroll
     for (int k = 0; k < kMPer; k++) {
       const uint32_t q = lane + k * kWave;
       uint32_t h;
       const uint32_t sid = multi_sid(L.rec, nh, q < M ? q : 0, &h);
-      msid[k] = sid;
       mrk[k] = rec_at(L.rec, h, kFieldRank);
       const SubEnt e = load_sub(s, sid);
       mcl[k] = e.client;
       mw[k] = e.word;
     }
+    uint32_t im = 0;  // (kIdent) bit k: entry k's Identifier is > 0
+    if constexpr (kIdent) {
+#pragma unroll
+      for (int k = 0; k < kMPer; k++) im |= (mw[k] & kWordIdent) ? 1u << k : 0u;
+    }
     const uint32_t D =
         merge_multi<kWave, kMPer>(MergeTable{L.tkb, L.tfirst}, kSmallSlots, mcl, mw, mrk, M, lane, 0,
                                   o.dout, db, Ss, o.dcap, &o.ctr->oob);
     if (lane == 0) o.dcount[t] = D;
-    if (ib != ~0ull) {  // (wave-uniform)
-      uint32_t nid = 0;
+    if constexpr (kIdent) {
+      if (ib != ~0ull) {  // (wave-uniform)
+        uint32_t nid = 0;
 #pragma unroll
-      for (int k = 0; k < kMPer; k++)
-        ident_put<kWave>(o, ib, lane + k * kWave < M && (mw[k] & kWordIdent), msid[k], 0, lanemask_lt(lane), nid);
-      if (lane == 0) o.icount[t] = nid;
+        for (int k = 0; k < kMPer; k++) {
+          const uint32_t q = lane + k * kWave;
+          uint32_t h;
+          const uint32_t sid = multi_sid(L.rec, nh, q < M ? q : 0, &h);
+          ident_put<kWave>(o, ib, q < M && ((im >> k) & 1u), sid, 0, lanemask_lt(lane), nid);
+        }
+        if (lane == 0) o.icount[t] = nid;
+      }
     }
     wave_lds_sync();
   }
@@ -1663,8 +1686,8 @@ struct alignas(16) ResolveLds {
   uint32_t key[2 * kH], rank[2 * kH];  // gathered multi parts by multi-tail start + 1 (0: empty) -> hit rank
 };
 
-template <int kE, int kH, int kPer, int kChunk = 0>
-__global__ __launch_bounds__(kWave *kEmitWaves) void k_resolve(DeviceSnapshot s, Outputs o,
+template <int kE, int kH, int kPer, int kChunk = 0, bool kIdent = false>
+__global__ __launch_bounds__(kWave *kEmitWaves) __attribute__((amdgpu_waves_per_eu(6))) void k_resolve(DeviceSnapshot s, Outputs o,
                                                                const uint32_t *__restrict__ list,
                                                                const unsigned int *__restrict__ count) {
   constexpr int kGroups = kWave / kE;
@@ -1719,7 +1742,7 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_resolve(DeviceSnapshot s,
     if (i_next < nl) fetch(i_next);
     wave_lds_sync();
     const uint32_t nh = L.rec[0] & 0xFFu, Ss = L.rec[1], M = L.rec[2];
-    const uint64_t ib = ident_base(o, t, M, gl == 0);
+    const uint64_t ib = kIdent ? ident_base(o, t, M, gl == 0) : ~0ull;
     uint32_t nid = 0;
     // the gathered multi parts by their range's multi-tail start (a node's
     // range is gathered at most once per topic: distinct keys)
@@ -1734,7 +1757,8 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_resolve(DeviceSnapshot s,
     wave_lds_sync();
     uint32_t D = 0;
     for (uint32_t q0 = 0; q0 < M; q0 += kE * kPer) {
-      uint32_t sid[kPer], rk[kPer], wd[kPer], iw[kPer];
+      uint32_t sid[kPer], rk[kPer], wd[kPer], iw[kIdent ? kPer : 1];
+      uint32_t im = 0;  // (kIdent) bit k: entry k's Identifier is > 0
       uint2 pi[kPer];
 #pragma unroll
       for (int k = 0; k < kPer; k++) {  // every entry's loads in flight together
@@ -1744,14 +1768,11 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_resolve(DeviceSnapshot s,
         rk[k] = rec_at(L.rec, h, kFieldRank);
         wd[k] = s.words[sid[k]];
         pi[k] = s.pinfo[sid[k]];
-        iw[k] = o.iscratch ? s.ident_bits[sid[k] >> 5] : 0u;  // (1.25 MB at C3: L2)
+        if constexpr (kIdent) iw[k] = s.ident_bits[sid[k] >> 5];  // (1.25 MB at C3: L2)
       }
-      if (o.iscratch) {  // (wave-uniform)
+      if constexpr (kIdent) {
 #pragma unroll
-        for (int k = 0; k < kPer; k++) {
-          const uint32_t q = q0 + k * kE + gl;
-          ident_put<kE>(o, ib, ib != ~0ull && q < M && ((iw[k] >> (sid[k] & 31)) & 1u), sid[k], gbase, glt, nid);
-        }
+        for (int k = 0; k < kPer; k++) im |= ((iw[k] >> (sid[k] & 31)) & 1u) << k;
       }
 #pragma unroll
       for (int k = 0; k < kPer; k++) {
@@ -1786,9 +1807,16 @@ __global__ __launch_bounds__(kWave *kEmitWaves) void k_resolve(DeviceSnapshot s,
                       pack_delivery(sid[k], 31u - __builtin_clz(qb & 7u), (qb >> 3) & 1u), &o.ctr->oob);
         D += __popcll(m);
       }
+      if constexpr (kIdent) {  // (wave-uniform) the identified entries, in entry order
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+          const uint32_t q = q0 + k * kE + gl;
+          ident_put<kE>(o, ib, ib != ~0ull && q < M && ((im >> k) & 1u), sid[k], gbase, glt, nid);
+        }
+      }
     }
     if (gl == 0) o.dcount[t] = Ss + D;
-    if (gl == 0 && ib != ~0ull) o.icount[t] = nid;
+    if (kIdent && gl == 0 && ib != ~0ull) o.icount[t] = nid;
     wave_lds_sync();
   }
 }
@@ -2658,8 +2686,10 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
                   hipStream_t st, bool exact) {
   using W = Workspace;
   if (ws.pending) return -1;  // one call in flight per workspace (collect it first)
-  // queued calls need every output buffer sized by an earlier call
-  exact = exact || !ws.caps_known;
+  const bool fuse_ids = ws.ident_early && !ws.runs && ident_fused_on();
+  // queued calls need every output buffer sized by an earlier call (the
+  // Identifiers scratch included: its first call reads the multi-entry total back)
+  exact = exact || !ws.caps_known || (fuse_ids && ws.ident_cap == 0);
   if (ws.get(W::kSCount, sizeof(uint32_t) * (n + 1)) || ws.get(W::kHCount, sizeof(uint32_t) * (n + 1)) ||
       ws.get(W::kDCount, sizeof(uint32_t) * (n + 1)) || ws.get(W::kDStart, sizeof(uint64_t) * (n + 1)) ||
       ws.get(W::kHStart, sizeof(uint64_t) * (n + 1)) || ws.get(W::kCls, n + 1) ||
@@ -2709,7 +2739,6 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
   mark(ws, 1, st);
   ws.ident_ready = false;
   ws.ident_fused = false;
-  const bool fuse_ids = ws.ident_early && !ws.runs && ident_fused_on();
   if (fuse_ids) {
     // Identifiers listed by the merges: every count starts at 0 (topics
     // without multi entries, DFS topics), each topic's scratch area at the
@@ -2854,6 +2883,7 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
       if (l) launched |= 1u << list;
       return l;
     };
+    const bool ids = o.iscratch != nullptr;  // (the merges list Identifiers: their kIdent variants)
     const bool l_small = has_list(hc->n_small, kLSmall), l_wave = has_list(hc->n_wmerge, kLWave),
                l_t1 = has_list(hc->n_t1, kLT1), l_t2 = has_list(hc->n_t2, kLT2), l_t3 = has_list(hc->n_t3, kLT3),
                l_part = has_list(hc->n_part, kLPart), l_sh = has_list(hc->n_shlist, kLShared),
@@ -2868,10 +2898,16 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
       // (4, 64 VGPRs) and 21.07 (8, 86 VGPRs, 5 waves/SIMD) — r04z;
       // topics handed out 4 at a time from a device counter: C4 shard emission
       // 19.03 ms against 20.22 with a fixed stride and 19.15 with 16 (r04ae)
-      if (n < (1u << 31))
+      if (n < (1u << 31) && ids)
+        hipLaunchKernelGGL((k_resolve<kWave, kHCap, 6, 4, true>), grid((k_resolve<kWave, kHCap, 6, 4, true>)),
+                           dim3(kWave * kEmitWaves), 0, st, s, o, lists.l[kLRes], lcount + kLRes);
+      else if (n < (1u << 31))
         hipLaunchKernelGGL((k_resolve<kWave, kHCap, 6, 4>), grid((k_resolve<kWave, kHCap, 6, 4>)),
                            dim3(kWave * kEmitWaves), 0, st, s, o, lists.l[kLRes], lcount + kLRes);
-      else  // (the counter could pass 2^32)
+      else if (ids)  // (the counter could pass 2^32)
+        hipLaunchKernelGGL((k_resolve<kWave, kHCap, 6, 0, true>), grid((k_resolve<kWave, kHCap, 6, 0, true>)),
+                           dim3(kWave * kEmitWaves), 0, st, s, o, lists.l[kLRes], lcount + kLRes);
+      else
         hipLaunchKernelGGL((k_resolve<kWave, kHCap, 6>), grid((k_resolve<kWave, kHCap, 6>)),
                            dim3(kWave * kEmitWaves), 0, st, s, o, lists.l[kLRes], lcount + kLRes);
       HIP_TRY(hipGetLastError());
@@ -2897,18 +2933,30 @@ int match_enqueue(const DeviceSnapshot &s, Workspace &ws, const uint8_t *d_bytes
       HIP_TRY(hipGetLastError());
     }
     if (l_rs) {
-      hipLaunchKernelGGL((k_resolve<kSmallLanes, 16, 3>), grid((k_resolve<kSmallLanes, 16, 3>)),
-                         dim3(kWave * kEmitWaves), 0, st, s, o, lists.l[kLResSmall], lcount + kLResSmall);
+      if (ids)
+        hipLaunchKernelGGL((k_resolve<kSmallLanes, 16, 3, 0, true>), grid((k_resolve<kSmallLanes, 16, 3, 0, true>)),
+                           dim3(kWave * kEmitWaves), 0, st, s, o, lists.l[kLResSmall], lcount + kLResSmall);
+      else
+        hipLaunchKernelGGL((k_resolve<kSmallLanes, 16, 3>), grid((k_resolve<kSmallLanes, 16, 3>)),
+                           dim3(kWave * kEmitWaves), 0, st, s, o, lists.l[kLResSmall], lcount + kLResSmall);
       HIP_TRY(hipGetLastError());
     }
     if (l_small) {
-      hipLaunchKernelGGL((k_merge_small<6>), grid(k_merge_small<6>), dim3(kWave * kEmitWaves), 0, st, s, o,
-                         lists.l[kLSmall], lcount + kLSmall);
+      if (ids)
+        hipLaunchKernelGGL((k_merge_small<6, true>), grid(k_merge_small<6, true>), dim3(kWave * kEmitWaves), 0, st, s,
+                           o, lists.l[kLSmall], lcount + kLSmall);
+      else
+        hipLaunchKernelGGL((k_merge_small<6>), grid(k_merge_small<6>), dim3(kWave * kEmitWaves), 0, st, s, o,
+                           lists.l[kLSmall], lcount + kLSmall);
       HIP_TRY(hipGetLastError());
     }
     if (l_wave) {
-      hipLaunchKernelGGL(k_merge, grid(k_merge), dim3(kWave * kEmitWaves), 0, st, s, o, lists.l[kLWave],
-                         lcount + kLWave);
+      if (ids)
+        hipLaunchKernelGGL(k_merge<true>, grid(k_merge<true>), dim3(kWave * kEmitWaves), 0, st, s, o, lists.l[kLWave],
+                           lcount + kLWave);
+      else
+        hipLaunchKernelGGL(k_merge<false>, grid(k_merge<false>), dim3(kWave * kEmitWaves), 0, st, s, o,
+                           lists.l[kLWave], lcount + kLWave);
       HIP_TRY(hipGetLastError());
     }
     // the solo copy (none in the runs form: the solo parts stay runs)
@@ -3030,6 +3078,8 @@ int match_collect(Workspace &ws, hipStream_t st, MatchOutput *out) {
   ws.caps_known = true;
   ws.last_valid = true;
   ws.last_n_dfs = hc->n_dfs;
+  if (ws.ident_fused)  // (the next queued call's Identifiers scratch: this one's multi entries, with room)
+    ws.ident_cap = std::max<uint64_t>(ws.ident_cap, hc->i_multi + hc->i_multi / 4 + 1024);
   for (int i = 0; i < 5; i++) ws.why[i] = hc->why[i];
 #if MQM_WALK_STATS
   fprintf(stderr, "[walk-stats] topics %u literal probes %llu missed %llu wildcard-child loads %llu\n", n,
