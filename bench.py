@@ -80,8 +80,10 @@ def parse():
                     help="PCIe-inclusive host path (mqm_match_batch): topics per call, outside the timed region; 0 = skip")
     ap.add_argument("--host-passes", type=int, default=8,
                     help="host-path legs: passes over the batch in the to_host leg (many calls: no start / tail effect)")
-    ap.add_argument("--host-threads", type=int, default=8,
-                    help="host path: concurrent callers (each its own stream), batches overlapped across them")
+    ap.add_argument("--host-threads", type=int, default=4,
+                    help="host path: concurrent callers (each its own stream), batches overlapped across them "
+                         "(4: the best of 4 / 8 / 12 / 16 measured, r06i / r06j — more callers queue more copies "
+                         "behind each other's and their kernels behind them)")
     ap.add_argument("--pipeline", type=int, default=2,
                     help="timed steps through the queued device API on this many contexts / streams (a step "
                          "submits its batch and waits for the one submitted that many steps earlier; every "

@@ -470,6 +470,14 @@ void ctx_release(mqm_index *h, std::unique_ptr<MatchCtx> c) {
   h->pool.push_back(std::move(c));
 }
 
+// MQM_D2H_KERNEL=1: a host-path call's result parts go to its pinned block by
+// one copy kernel (match.hip k_copy_out) instead of a DMA copy each (read per
+// call: tests switch it)
+bool d2h_kernel() {
+  const char *e = getenv("MQM_D2H_KERNEL");
+  return e && atoi(e) != 0;
+}
+
 // pinned staging for n + 1 rebased offsets
 uint64_t *ctx_staging(MatchCtx *c, size_t bytes) {
   if (c->staging_cap < bytes) {
@@ -969,28 +977,51 @@ static int match_batch_impl(mqm_index *h, const char *topic_bytes, const uint64_
         r->deliveries = reinterpret_cast<const mqm_delivery *>(B + o_d);
       r->shared = reinterpret_cast<const uint32_t *>(B + o_s);
       r->snap = snap->host;
-      if (hipMemcpyAsync(B + o_off, dn.offsets, 8 * n1, hipMemcpyDeviceToHost, st) != hipSuccess ||
-          hipMemcpyAsync(B + o_sh, dn.shared_offsets, 8 * n1, hipMemcpyDeviceToHost, st) != hipSuccess)
-        return MQM_EHIP;
-      if (mo.n_deliveries &&
-          hipMemcpyAsync(B + o_d, dn.deliveries, dsz * mo.n_deliveries, hipMemcpyDeviceToHost, st) != hipSuccess)
-        return MQM_EHIP;
-      if (mo.n_shared && hipMemcpyAsync(B + o_s, dn.shared, 4 * mo.n_shared, hipMemcpyDeviceToHost, st) != hipSuccess)
-        return MQM_EHIP;
+      // the parts: DMA copies, or (MQM_D2H_KERNEL=1) one kernel storing into
+      // the block's device view (tools/duplex_probe)
+      CopyOut co;
+      char *dB = nullptr;
+      if (d2h_kernel()) {
+        void *v = nullptr;
+        if (hipHostGetDevicePointer(&v, B, 0) == hipSuccess) dB = static_cast<char *>(v);
+      }
+      auto part = [&](uint64_t off, const void *src, uint64_t bytes) -> bool {
+        if (!bytes) return true;
+        if (dB && co.n < CopyOut::kMax) {
+          co.src[co.n] = src;
+          co.dst[co.n] = dB + off;
+          co.bytes[co.n++] = bytes;
+          return true;
+        }
+        return hipMemcpyAsync(B + off, src, bytes, hipMemcpyDeviceToHost, st) == hipSuccess;
+      };
+      if (!part(o_off, dn.offsets, 8 * n1) || !part(o_sh, dn.shared_offsets, 8 * n1)) return MQM_EHIP;
+      if (mo.n_deliveries && !part(o_d, dn.deliveries, dsz * mo.n_deliveries)) return MQM_EHIP;
+      if (mo.n_shared && !part(o_s, dn.shared, 4 * mo.n_shared)) return MQM_EHIP;
       if (runs) {
         r->run_offsets = reinterpret_cast<const uint64_t *>(B + o_ro);
         r->runs = reinterpret_cast<const mqm_run *>(B + o_r);
         r->n_solo = mo.n_solo;
-        if (hipMemcpyAsync(B + o_ro, ro.offsets, 8 * n1, hipMemcpyDeviceToHost, st) != hipSuccess) return MQM_EHIP;
-        if (ro.n_runs && hipMemcpyAsync(B + o_r, ro.runs, 8 * ro.n_runs, hipMemcpyDeviceToHost, st) != hipSuccess)
-          return MQM_EHIP;
+        if (!part(o_ro, ro.offsets, 8 * n1)) return MQM_EHIP;
+        if (ro.n_runs && !part(o_r, ro.runs, 8 * ro.n_runs)) return MQM_EHIP;
       }
       if (want_ids) {
         r->has_idents = true;
         r->ident_offsets = reinterpret_cast<const uint64_t *>(B + o_io);
         r->idents = reinterpret_cast<const uint32_t *>(B + o_i);
-        if (hipMemcpyAsync(B + o_io, io.offsets, 8 * n1, hipMemcpyDeviceToHost, st) != hipSuccess) return MQM_EHIP;
-        if (ni && hipMemcpyAsync(B + o_i, io.sids, 4 * ni, hipMemcpyDeviceToHost, st) != hipSuccess) return MQM_EHIP;
+        if (!part(o_io, io.offsets, 8 * n1)) return MQM_EHIP;
+        if (ni && !part(o_i, io.sids, 4 * ni)) return MQM_EHIP;
+      }
+      if (co.n) {
+        const int ce = copy_out_device(co, st);
+        if (ce == -4) {  // (a part off the kernel's alignment: the DMA copies)
+          for (int k = 0; k < co.n; k++)
+            if (hipMemcpyAsync(B + (static_cast<char *>(co.dst[k]) - dB), co.src[k], co.bytes[k],
+                               hipMemcpyDeviceToHost, st) != hipSuccess)
+              return MQM_EHIP;
+        } else if (ce != 0) {
+          return hip_rc(ce);
+        }
       }
       if (ws.end(st) || hipStreamSynchronize(st) != hipSuccess) return MQM_EHIP;
       tb[4] = clk::now();

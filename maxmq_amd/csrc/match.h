@@ -304,4 +304,16 @@ struct DenseOutput {
 int densify(const DeviceSnapshot &s, Workspace &ws, const MatchOutput &m, hipStream_t st, DenseOutput *out,
             bool packed = false);
 
+// A host-path call's result parts from device buffers into its pinned host
+// block (device views), by one kernel on `st` instead of a DMA copy per part
+// (MQM_D2H_KERNEL, capi.cpp).  Parts: 4-B multiples, 16-B aligned ends.
+struct CopyOut {
+  static constexpr int kMax = 8;
+  const void *src[kMax];
+  void *dst[kMax];
+  uint64_t bytes[kMax];
+  int n = 0;
+};
+int copy_out_device(const CopyOut &c, hipStream_t st);
+
 }  // namespace mqm

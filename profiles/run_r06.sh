@@ -29,6 +29,9 @@
 #   freeprobe: tools/_build/free_probe (does hipFree wait for a running kernel?) -> free_probe.txt
 #   calib   : tools/_build/calib_fetch (random-gather / cooperative-gather rates) -> calib_kernels.txt
 #   duplex  : tools/_build/duplex_probe (H2D / D2H alone and at once, DMA and kernel copies) -> duplex_probe.txt
+#   hostab  : the host-path legs with DMA / kernel result copies (MQM_D2H_KERNEL=1), 4 / 8 HW queues
+#   hostthreads: the host-path legs on 4 / 12 / 16 caller threads
+#   kcopyt  : the runs-form tests, kernel copy-out parity included
 #   c2      : the C2 bench line (1M filters, 10M topics) with roofline and CPU baseline -> bench_c2.json
 #   c4fast  : the C4 shard bench without CPU baseline
 #   pipe    : `fast` with pipelined steps on 2 and 3 contexts -> bench_fast_pipe{2,3}.json
@@ -154,6 +157,16 @@ for step in "$@"; do
              > $OUT/pytest_quick.log 2>&1 ;;
     lat) timeout -k 10 600 python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --host-topics 0 \
              > $OUT/bench_lat.json 2> $OUT/bench_lat.log ;;
+    hostab) for V in dma:X=0 kern:MQM_D2H_KERNEL=1 hwq8:GPU_MAX_HW_QUEUES=8 kernhwq8:MQM_D2H_KERNEL=1:GPU_MAX_HW_QUEUES=8; do
+          N=${V%%:*}; E=$(echo ${V#*:} | tr ':' ' ')
+          env $E timeout -k 10 500 python3 -u bench.py --steps 1 --warmup 1 --no-cpu-baseline --latency-topics 0 \
+            --steady-steps 0 --ident-steps 0 > $OUT/bench_host_$N.json 2> $OUT/bench_host_$N.log || exit 1
+        done ;;
+    hostthreads) for T in ${HOST_THREADS:-4 12 16}; do
+          timeout -k 10 500 python3 -u bench.py --steps 1 --warmup 1 --no-cpu-baseline --latency-topics 0 \
+            --steady-steps 0 --ident-steps 0 --host-threads $T > $OUT/bench_host_t$T.json 2> $OUT/bench_host_t$T.log || exit 1
+        done ;;
+    kcopyt) timeout -k 10 400 $PYT tests/test_gpu_runs.py -m gpu --timeout 200 > $OUT/pytest_kcopy.log 2>&1 ;;
     c2) timeout -k 10 600 python3 -u bench.py --config 2 --steps 10 --warmup 3 --host-topics 0 --latency-topics 0 \
              --steady-steps 0 --cpu-seconds 10 > $OUT/bench_c2.json 2> $OUT/bench_c2.log ;;
     c4fast) timeout -k 10 600 python3 -u bench.py --config 4 --shard 0/8 $FAST > $OUT/bench_c4_fast.json 2> $OUT/bench_c4_fast.log ;;
@@ -171,8 +184,8 @@ for step in "$@"; do
              2> $OUT/bench_fast_pipe$P.log || exit 1; done ;;
     par) timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_gpu_queued.py -m gpu --timeout 300 \
              > $OUT/pytest_par.log 2>&1 ;;
-    duplex) (timeout -k 10 120 tools/_build/duplex_probe 128 16 && timeout -k 10 120 tools/_build/duplex_probe 32 64 \
-             && timeout -k 10 120 tools/_build/duplex_probe 128 16 2048) > $OUT/duplex_probe.txt 2>&1 ;;
+    duplex) (timeout -k 10 200 tools/_build/duplex_probe 128 16 && timeout -k 10 200 tools/_build/duplex_probe 32 64 \
+             && timeout -k 10 200 tools/_build/duplex_probe 128 16 2048) > $OUT/duplex_probe.txt 2>&1 ;;
     l2probe) timeout -k 10 120 tools/_build/l2_probe > $OUT/l2_probe.txt 2>&1 ;;
     reuseprobe) timeout -k 10 120 tools/_build/reuse_probe > $OUT/reuse_probe.txt 2>&1 ;;
     pollprobe) timeout -k 10 120 tools/_build/poll_probe > $OUT/poll_probe.txt 2>&1 ;;

@@ -102,3 +102,30 @@ def test_runs_form_identifiers():
     assert_same(g, r, "runs form (identifiers index) vs oracle")
     assert_same(canon_gpu_idents(res), canon_oracle_idents(*ora.identifiers(s.data, s.offs, nthreads=8)),
                 "runs form identifiers")
+
+
+@pytest.mark.parametrize("form", ["runs", "packed", "plain"])
+def test_kernel_copy_out_matches_dma(form, monkeypatch):
+    """MQM_D2H_KERNEL=1 (the result parts stored into the pinned block by one
+    kernel, match.hip k_copy_out) returns what the DMA copies return, and the
+    oracle's sets — shared subscriptions and Identifiers included."""
+    w = mqgen.generate(1, n_filters=20000, n_topics=30000, p_shared=0.05)
+    idx = maxmq_amd.TopicsIndex(0, identifiers=True)
+    idx.subscribe_workload(w)
+    s = w.topics
+    call = {"runs": idx.match_batch_runs, "packed": idx.match_batch_packed, "plain": idx.match_batch}[form]
+    got = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("MQM_D2H_KERNEL", mode)
+        res = call(s.data, s.offs)
+        got[mode] = (canon_gpu(res), canon_gpu_idents(res))
+    (g0, gs0), i0 = got["0"]
+    (g1, gs1), i1 = got["1"]
+    assert_same(g1, g0, f"{form}: kernel copy-out vs DMA")
+    assert_same(gs1, gs0, f"{form}: kernel copy-out vs DMA (shared)")
+    assert_same(i1, i0, f"{form}: kernel copy-out vs DMA (identifiers)")
+    ora = OracleIndex()
+    ora.subscribe_workload(w)
+    r, rs = canon_oracle(*ora.match(s.data, s.offs, nthreads=8)[:4])
+    assert_same(g1, r, f"{form}: kernel copy-out vs oracle")
+    assert_same(gs1, rs, f"{form}: kernel copy-out vs oracle (shared)")
