@@ -677,11 +677,30 @@ def host_path(idx, w, args, form="runs"):
             dst.copy_(src, non_blocking=True)
         torch.cuda.synchronize()
         rates[name] = 3 * (1 << 30) / (time.perf_counter() - t1)
-    del g, h
+    # both directions at once (two streams; tools/duplex_probe: each direction
+    # slows to ~48 of ~57 GB/s while the other runs)
+    g2 = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
+    h2 = torch.empty(1 << 30, dtype=torch.uint8).pin_memory()
+    sa, sb = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(3):
+        with torch.cuda.stream(sa):
+            g.copy_(h, non_blocking=True)
+        with torch.cuda.stream(sb):
+            h2.copy_(g2, non_blocking=True)
+    torch.cuda.synchronize()
+    rates["both"] = 3 * (1 << 30) / (time.perf_counter() - t1)  # per direction
+    del g, h, g2, h2
     n = nb * per
     in_b = int(w.topics.offs[n]) + 8 * n
     out_b = out_per_batch * nb
     bound_s = max(in_b / rates["h2d"], out_b / rates["d2h"])
+    # the same bytes when the smaller direction overlaps the larger one at the
+    # concurrent rate, the rest of the larger at its own rate
+    ov = min(in_b, out_b) / rates["both"]
+    rest = (max(in_b, out_b) - min(in_b, out_b)) / (rates["d2h"] if out_b >= in_b else rates["h2d"])
+    duplex_s = max(bound_s, ov + rest)
     # SURVEY §8(d)'s end-to-end definition: topics in pinned host memory ->
     # the CSR result in pinned host memory ("to_host"; the runs form's CSR is
     # runs + winners); "iterate" adds the consumer reading every delivery
@@ -691,11 +710,14 @@ def host_path(idx, w, args, form="runs"):
             "d2h_bytes_per_topic": out_b / n, "runs_per_topic": n_runs / per, "winners_per_topic": win / per,
             "h2d_GBps": rates["h2d"] / 1e9, "d2h_GBps": rates["d2h"] / 1e9,
             "pcie_bound_topics_per_s": n / bound_s, "frac_of_pcie_bound": best["value"] / (n / bound_s),
+            "both_directions_GBps": rates["both"] / 1e9, "pcie_duplex_bound_topics_per_s": n / duplex_s,
+            "frac_of_duplex_bound": best["value"] / (n / duplex_s),
             "note": "pinned topics in -> match -> result into pinned blocks -> consumed on the calling thread (" +
                     ("mqm_match_batch_runs: 8-B solo runs of the host word table + 4-B merged winners"
                      if form == "runs" else "mqm_match_batch_packed: 4-B packed words") +
                     "); native caller threads (tools/conc_driver.cpp); pcie_bound = max(H2D bytes / H2D rate, "
-                    "D2H bytes / D2H rate)"}
+                    "D2H bytes / D2H rate), each rate alone; duplex bound: the smaller direction overlapped at "
+                    "the both-at-once rate"}
 
 
 def gather_proxy(idx, tb, to, n, dev, args, shards=8):
