@@ -112,6 +112,9 @@ def parse():
     ap.add_argument("--churn-build-threads", default="2,4,16,-1",
                     help="churn: comma-separated host thread counts for the background rebuild "
                          "(mqm_build_threads), one served-under-churn leg each (-1: no rebuild during the leg)")
+    ap.add_argument("--churn-fresh-legs", default="2",
+                    help="churn: build thread counts of the served-under-churn legs with MQM_CFG_FRESH corrections "
+                         "on (mqm_fresh_policy; the legs above run with them off: the snapshot's view)")
     ap.add_argument("--retained", type=int, default=50000000, help="reverse: retained topics")
     ap.add_argument("--sweep", default="",
                     help="tuning sweep before the measurement: ';'-separated variants of "
@@ -958,7 +961,10 @@ def run_churn(args, dist, rank, world, local, dev):
     w = mqgen.generate(args.config, **overrides)
     n = len(w.topics)
     t0 = time.time()
-    idx = maxmq_amd.TopicsIndex(device=local, autocommit=False, async_commit=True)
+    # (MQM_CFG_FRESH: the overlay is kept from the start; the served legs switch
+    # its corrections on or off with mqm_fresh_policy)
+    idx = maxmq_amd.TopicsIndex(device=local, autocommit=False, async_commit=True,
+                                fresh=bool(args.churn_fresh_legs.strip()))
     idx.subscribe_workload(w)
     idx.commit()
     build_s = time.time() - t0
@@ -1145,18 +1151,30 @@ def serve_churn(idx, w, args):
     run(2.0, 0)  # warm: the server, every caller's path
     base = run(min(args.serve_churn_s, 10.0), 0)
     legs = {}
-    for bt in [int(x) for x in str(args.churn_build_threads).split(",") if x.strip()]:
+    fresh_on = idx.fresh
+    plan = [(int(x), False) for x in str(args.churn_build_threads).split(",") if x.strip()]
+    if fresh_on:
+        plan += [(int(x), True) for x in str(args.churn_fresh_legs).split(",") if x.strip()]
+    for bt, fresh in plan:
         # bt < 0: no background rebuild during the leg (the mutations' own cost)
         capi.check("mqm_build_threads", L.mqm_build_threads(max(bt, 0)))
+        if fresh_on:
+            idx.fresh_policy(fresh)
         idx.commit_poll(wait=True)  # (the previous leg's mutations built and published)
         idx.commit_policy(0, 50 if bt >= 0 else 0)
-        name = f"build_threads_{bt}" if bt >= 0 else "no_rebuild"
+        name = ("fresh_" if fresh else "") + (f"build_threads_{bt}" if bt >= 0 else "no_rebuild")
         legs[name] = run(args.serve_churn_s, args.churn_rate)
+        if fresh:
+            legs[name]["fresh_clients_held"] = idx.fresh_clients()
         log(f"[serve churn] {name}: {legs[name]}")
+    if fresh_on:
+        idx.fresh_policy(False)
     capi.check("mqm_build_threads", L.mqm_build_threads(0))
     idx.commit_policy(0, 50)
     return {"threads": T, "driver": "native threads (tools/conc_driver.cpp mqd_serve_churn)",
-            "index": "MQM_CFG_ASYNC_COMMIT | MQM_CFG_SERVE, commit_policy(0 ops, 50 ms)",
+            "index": "MQM_CFG_ASYNC_COMMIT | MQM_CFG_SERVE" + (" | MQM_CFG_FRESH" if idx.fresh else "") +
+                     ", commit_policy(0 ops, 50 ms); fresh_* legs: the calls corrected for every mutation so far "
+                     "(include/mqmatch.h MQM_CFG_FRESH), the other legs: the published snapshot's view",
             "baseline_no_mutations": base, "under_churn": legs, "target_rate": args.churn_rate}
 
 

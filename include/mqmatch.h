@@ -78,6 +78,20 @@ extern "C" {
  * results past a slot's capacities take the batch path.  Results are
  * identical.  Takes precedence over MQM_CFG_BATCHING. */
 #define MQM_CFG_SERVE 16u
+/* MQM_CFG_FRESH (with MQM_CFG_ASYNC_COMMIT): mqm_subscribers returns the
+ * store's current subscriptions, as the reference's live trie does
+ * (topics.go:303-321, 484-518), without waiting for a rebuild: a result
+ * matched on the published snapshot is corrected on the host for the clients
+ * a mutation touched since that snapshot (their rows dropped, then recomputed
+ * from their current subscriptions by the reference's scan and merge), and
+ * mqm_result_snapshot_version reports the store version the result reflects.
+ * Corrected results carry subscription ids past the snapshot's; resolve them
+ * with mqm_result_sub_info / mqm_result_shared_info as usual.  Batch calls
+ * (mqm_match_batch*, mqm_match_device) keep the snapshot's view.  Costs: each
+ * publish builds a by-client index of the snapshot; each mutation updates the
+ * overlay under the index mutex; a call on a stale snapshot adds a host scan
+ * of the touched clients' subscriptions. */
+#define MQM_CFG_FRESH 32u
 /* device value for a host-only index: the store and its mutation API work,
  * mqm_commit / mqm_match_* return MQM_ENODEV (there is no CPU match path). */
 #define MQM_DEVICE_NONE (-1)
@@ -295,6 +309,12 @@ int mqm_batching_policy(mqm_index *h, uint32_t max_batch, uint32_t linger_us);
  * statistics: calls served in the ring, calls that took the batch path, server
  * launches.  MQM_EINVAL on a host-only index (or for stats while off). */
 int mqm_serve_policy(mqm_index *h, uint32_t grid, uint32_t idle_us);
+/* MQM_CFG_FRESH indexes: correct_calls = 0 makes mqm_subscribers return the
+ * snapshot's view again (the overlay is still kept up to date; A/B and
+ * measurement), 1 turns the correction back on; statistics: the clients the
+ * overlay holds.  MQM_EINVAL on an index created without the flag. */
+int mqm_fresh_policy(mqm_index *h, int correct_calls);
+int mqm_fresh_stats(mqm_index *h, uint64_t *held_clients);
 /* (grid is capped at half the device's CUs: a server under steady traffic
  * never idles out, and batch-path calls need the rest of the device) */
 int mqm_serve_stats(mqm_index *h, uint64_t *served, uint64_t *fallbacks, uint64_t *launches);
@@ -502,7 +522,7 @@ uint32_t mqm_result_num_topics(const mqm_result *r);
  * result, none after it.  The reference matches its live trie
  * (topics.go:484-518); a drop-in caller that needs to know which mutations a
  * result reflects reads this.  0 for NULL. */
-uint64_t mqm_result_snapshot_version(const mqm_result *r);
+uint64_t mqm_result_snapshot_version(const mqm_result *r); /* (MQM_CFG_FRESH: the store version it reflects) */
 const uint64_t *mqm_result_offsets(const mqm_result *r);          /* n + 1          */
 const mqm_delivery *mqm_result_deliveries(const mqm_result *r); /* NULL for a packed result */
 const uint32_t *mqm_result_packed(const mqm_result *r);         /* packed words (mqm_match_batch_packed;

@@ -220,7 +220,7 @@ class TopicsIndex:
     """TopicsIndex (topics.go:285) backed by the MI355X matcher."""
 
     def __init__(self, device: int | None = 0, autocommit: bool = True, identifiers: bool = False,
-                 async_commit: bool = False, batching: bool = False, serve: bool = False):
+                 async_commit: bool = False, batching: bool = False, serve: bool = False, fresh: bool = False):
         """identifiers=True: match_batch / subscribers also return the full
         Subscription.Identifiers maps (an extra GPU pass per batch).
         async_commit=True: mutations are logged and snapshots are rebuilt by a
@@ -228,19 +228,39 @@ class TopicsIndex:
         batching=True: concurrent subscribers() calls are gathered into GPU
         batches by a collector thread (MQM_CFG_BATCHING).
         serve=True: subscribers() calls go to a persistent GPU server through
-        a ring of pinned slots (MQM_CFG_SERVE; no launch per call)."""
+        a ring of pinned slots (MQM_CFG_SERVE; no launch per call).
+        fresh=True (with async_commit): subscribers() returns the store's
+        current subscriptions without waiting for a rebuild (MQM_CFG_FRESH)."""
         L = lib()
         cfg = capi.Config(capi.MQM_DEVICE_NONE if device is None else device,
                           (capi.MQM_CFG_AUTOCOMMIT if autocommit else 0) |
                           (capi.MQM_CFG_IDENTIFIERS if identifiers else 0) |
                           (capi.MQM_CFG_ASYNC_COMMIT if async_commit else 0) |
                           (capi.MQM_CFG_BATCHING if batching else 0) |
-                          (capi.MQM_CFG_SERVE if serve else 0))
+                          (capi.MQM_CFG_SERVE if serve else 0) |
+                          (capi.MQM_CFG_FRESH if fresh else 0))
         h = C.c_void_p()
         check("mqm_create", L.mqm_create(C.byref(cfg), C.byref(h)))
         self._h = h
         self.device = device
+        self._fresh = bool(fresh)
         self._ctxs = weakref.WeakSet()  # live MatchContexts (destroyed before the index)
+
+    @property
+    def fresh(self) -> bool:
+        """created with fresh=True (MQM_CFG_FRESH)"""
+        return self._fresh
+
+    def fresh_policy(self, correct_calls: bool):
+        """MQM_CFG_FRESH: subscribers() corrected for every mutation (True,
+        the default) or the published snapshot's view (False)"""
+        check("mqm_fresh_policy", lib().mqm_fresh_policy(self._h, int(bool(correct_calls))))
+
+    def fresh_clients(self) -> int:
+        """clients the fresh overlay holds (touched since the previous snapshot)"""
+        v = C.c_uint64()
+        check("mqm_fresh_stats", lib().mqm_fresh_stats(self._h, C.byref(v)))
+        return v.value
 
     def batching_policy(self, max_batch: int = 0, linger_us: int = 0):
         check("mqm_batching_policy", lib().mqm_batching_policy(self._h, max_batch, linger_us))
@@ -484,6 +504,13 @@ class TopicsIndex:
         check("mqm_match_batch_runs", lib().mqm_match_batch_runs(
             self._h, data.ctypes.data_as(C.c_void_p), offs.ctypes.data_as(C.c_void_p), len(offs) - 1,
             C.byref(h)))
+        return BatchResult(self, h)
+
+    def subscribers_result(self, topic: str) -> BatchResult:
+        """mqm_subscribers' raw single-topic result (ids, not names)"""
+        t = b(topic)
+        h = C.c_void_p()
+        check("mqm_subscribers", lib().mqm_subscribers(self._h, t, len(t), C.byref(h)))
         return BatchResult(self, h)
 
     def subscribers(self, topic: str) -> Subscribers:

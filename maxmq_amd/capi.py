@@ -28,6 +28,7 @@ MQM_CFG_IDENTIFIERS = 2
 MQM_CFG_ASYNC_COMMIT = 4
 MQM_CFG_BATCHING = 8
 MQM_CFG_SERVE = 16
+MQM_CFG_FRESH = 32
 MQM_DEVICE_NONE = -1
 
 ERRORS = {MQM_EINVAL: "EINVAL", MQM_ENOMEM: "ENOMEM", MQM_EHIP: "EHIP", MQM_ELIMIT: "ELIMIT",
@@ -51,7 +52,8 @@ EXPORTED = [
     "mqm_result_packed", "mqm_match_batch_runs", "mqm_result_runs", "mqm_result_expand",
     "mqm_serve_policy", "mqm_serve_stats", "mqm_serve_device_us", "mqm_serve_host_us", "mqm_serve_host_max_us",
     "mqm_build_phases_ms", "mqm_build_threads", "mqm_identifiers_early",
-    "mqm_result_snapshot_version", "mqm_direct_host_us", "mqm_serve_counters_get",
+    "mqm_result_snapshot_version", "mqm_direct_host_us", "mqm_serve_counters_get", "mqm_fresh_policy",
+    "mqm_fresh_stats",
     "mqm_debug_stamp_counts", "mqm_batch_host_us",
 ]
 
@@ -218,6 +220,8 @@ def lib():
         "mqm_serve_policy": ([vp, u32, u32], C.c_int),
         "mqm_serve_stats": ([vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)], C.c_int),
         "mqm_serve_counters_get": ([vp, C.POINTER(u64 * 8)], C.c_int),
+        "mqm_fresh_policy": ([vp, C.c_int], C.c_int),
+        "mqm_fresh_stats": ([vp, C.POINTER(C.c_uint64)], C.c_int),
         "mqm_debug_stamp_counts": ([C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)], C.c_int),
         "mqm_batch_host_us": ([vp, C.POINTER(C.c_double)], C.c_int),
         "mqm_serve_device_us": ([vp, vp], C.c_int),

@@ -239,6 +239,7 @@ void Builder::run() {
         const uint64_t reuses = shape_.reuses;
         rc = fault == 2 ? MQM_ENOMEM : flatten(shadow_, hs.get(), device_ < 0 || host_edges_forced(), &shape_);
         b.kept_shape = shape_.reuses != reuses;
+        if (rc == MQM_OK && client_index_.load(std::memory_order_relaxed)) build_client_index(*hs);
         hs->version = version;  // (after flatten, which starts from an empty snapshot)
         const auto t2 = std::chrono::steady_clock::now();
         if (rc == MQM_OK && device_ >= 0 && !stream_) rc = MQM_EHIP;

@@ -107,6 +107,8 @@ class Builder {
   // block until every submitted log is built; returns the first build error
   int wait_idle();
   bool busy();
+  // builds also index their subscriptions by client (MQM_CFG_FRESH: fresh.h)
+  void set_client_index(bool on) { client_index_.store(on, std::memory_order_relaxed); }
 
  private:
   void run();
@@ -123,6 +125,7 @@ class Builder {
   bool dirty_ = false, shadow_bad_ = false;
   bool has_ready_ = false;
   std::atomic<bool> ready_flag_{false};  // has_ready_, readable without mu_
+  std::atomic<bool> client_index_{false};
   BuiltSnapshot ready_;
   int err_ = 0;
   int fault_stage_ = 0, fault_count_ = 0;

@@ -42,6 +42,7 @@
 #include "builder.h"
 #include "bulkload.h"
 #include "flatten.h"
+#include "fresh.h"
 #include "match.h"
 #include "retained.h"
 #include "serve_slots.h"
@@ -146,6 +147,10 @@ struct mqm_index {
   double last_build_ms = 0, last_build_phase_ms[3] = {0, 0, 0};
   bool last_build_kept_shape = false;
   bool fast_path = true;  // MQM_NO_FAST=1: small batches also take the batch pipeline (A/B, tests)
+  // MQM_CFG_FRESH: the touched clients' current subscriptions (fresh.h), written
+  // under mu with every mutation and publish, read by mqm_subscribers
+  std::unique_ptr<FreshOverlay> fresh;
+  std::atomic<bool> fresh_reads{true};  // mqm_fresh_policy: calls corrected (the overlay is kept either way)
   bool async() const { return (cfg.flags & MQM_CFG_ASYNC_COMMIT) != 0; }
   // the device-result API's context (mqm_match_device & follow-ups)
   std::mutex dev_mu;
@@ -198,6 +203,11 @@ struct mqm_result {
   const mqm_run *runs = nullptr;
   uint64_t n_solo = 0;
   std::shared_ptr<const HostSnapshot> snap;
+  // MQM_CFG_FRESH (freshen): subscriptions past the snapshot's sids (sid
+  // snap->sub_info.size() + k is extra[k]; shared likewise), and the store
+  // version the corrected result reflects (0: the snapshot's)
+  std::vector<SubInfo> extra, extra_shared;
+  uint64_t version = 0;
   bool heap = false;  // blk from malloc (results filled by host copies, no DMA into them)
   ~mqm_result() {
     if (heap)
@@ -276,14 +286,24 @@ void defer_release(std::shared_ptr<const void> p) {
 
 int install(mqm_index *h, std::shared_ptr<GpuSnapshot> g, uint64_t version) {
   std::shared_ptr<GpuSnapshot> old;
+  std::shared_ptr<const HostSnapshot> host = g ? g->host : nullptr;
   {
     std::unique_lock<std::shared_mutex> w(h->snap_rw);
     old = std::move(h->snap);
     h->snap = std::move(g);
     h->snap_version = version;
   }
+  if (h->fresh) h->fresh->on_install(std::move(host), h->store);
   defer_release(std::move(old));
   return MQM_OK;
+}
+
+// after a Store::subscribe (mu held): the overlay takes the record
+void fresh_subscribe(mqm_index *h, std::string_view filter, uint8_t qos, uint8_t no_local, uint8_t rap, uint8_t rh,
+                     int32_t ident) {
+  if (!h->fresh) return;
+  const Store::Footprint &fp = h->store.last_footprint();
+  h->fresh->on_subscribe(h->store, filter, SubRec{fp.client, fp.filter, ident, qos, no_local, rap, rh});
 }
 
 int64_t steady_ns() {
@@ -313,6 +333,7 @@ struct TraceSpan {
 Builder *builder_locked(mqm_index *h) {
   if (!h->builder) {
     h->builder = std::make_unique<Builder>(h->cfg.device);
+    if (h->fresh) h->builder->set_client_index(true);
     h->builder_pub.store(h->builder.get(), std::memory_order_release);
   }
   return h->builder.get();
@@ -383,6 +404,7 @@ int commit_locked(mqm_index *h) {
   auto hs = std::make_shared<HostSnapshot>();
   int rc = flatten(h->store, hs.get(), h->cfg.device < 0 || host_edges_forced());  // (a device builds the edge table itself)
   if (rc != MQM_OK) return rc;
+  if (h->fresh) build_client_index(*hs);
   hs->version = h->store.version();  // (after flatten, which starts from an empty snapshot; mu held)
   std::unique_ptr<GpuSnapshot> g;
   rc = upload(std::move(hs), h->cfg.device, h->dev.stream, &g);
@@ -661,6 +683,7 @@ int mqm_create(const mqm_config *cfg, mqm_index **out) {
     if (h->cfg.device < 0 || h->cfg.device >= ndev) return MQM_EINVAL;
     if (hipSetDevice(h->cfg.device) != hipSuccess) return MQM_EHIP;
     if (const char *e = getenv("MQM_NO_FAST")) h->fast_path = atoi(e) == 0;
+    if (h->cfg.flags & MQM_CFG_FRESH) h->fresh = std::make_unique<FreshOverlay>();
     if (ctx_init(h.get(), &h->dev) != MQM_OK) return MQM_EHIP;
     if ((h->cfg.flags & MQM_CFG_SERVE) && mqm_serve_policy(h.get(), 0, 0) != MQM_OK) return MQM_EHIP;
     if (h->cfg.flags & MQM_CFG_BATCHING) {
@@ -703,6 +726,8 @@ int mqm_subscribe(mqm_index *h, const char *client, size_t client_len, const cha
     std::lock_guard<std::mutex> g(h->mu);
     bool n = h->store.subscribe(sv(client, client_len), sv(filter, filter_len), sub->qos, sub->no_local,
                                 sub->retain_as_published, sub->retain_handling, sub->identifier);
+    fresh_subscribe(h, sv(filter, filter_len), sub->qos, sub->no_local, sub->retain_as_published,
+                    sub->retain_handling, sub->identifier);
     if (h->async()) {
       h->journal.subscribe(sv(client, client_len), sv(filter, filter_len), sub->qos, sub->no_local,
                            sub->retain_as_published, sub->retain_handling, sub->identifier,
@@ -727,6 +752,7 @@ int mqm_subscribe_many(mqm_index *h, size_t n, const char *client_bytes, const u
       const auto c = sv(client_bytes + client_offs[i], client_offs[i + 1] - client_offs[i]);
       const auto f = sv(filter_bytes + filter_offs[i], filter_offs[i + 1] - filter_offs[i]);
       bool r = h->store.subscribe(c, f, s.qos, s.no_local, s.retain_as_published, s.retain_handling, s.identifier);
+      fresh_subscribe(h, f, s.qos, s.no_local, s.retain_as_published, s.retain_handling, s.identifier);
       if (h->async())
         h->journal.subscribe(c, f, s.qos, s.no_local, s.retain_as_published, s.retain_handling, s.identifier,
                              &h->store.last_footprint());
@@ -743,6 +769,7 @@ int mqm_unsubscribe(mqm_index *h, const char *filter, size_t filter_len, const c
   return guarded([&] {
     std::lock_guard<std::mutex> g(h->mu);
     bool r = h->store.unsubscribe(sv(filter, filter_len), sv(client, client_len));
+    if (r && h->fresh) h->fresh->on_unsubscribe(h->store, sv(filter, filter_len));
     if (r && h->async()) {  // false: no node, nothing changed (topics.go:334-336)
       h->journal.unsubscribe(sv(filter, filter_len), sv(client, client_len), &h->store.last_footprint());
       maybe_submit(h);
@@ -764,6 +791,7 @@ int mqm_load_subscriptions_json(mqm_index *h, const char *json, size_t len, uint
       if (r.qos > 2 || r.retain_handling > 3 || r.identifier < INT32_MIN || r.identifier > INT32_MAX) return false;
       const uint8_t nl = r.no_local ? 1 : 0, rap = r.retain_as_published ? 1 : 0;
       if (h->store.subscribe(client, filter, r.qos, nl, rap, r.retain_handling, (int32_t)r.identifier)) fresh++;
+      fresh_subscribe(h, filter, r.qos, nl, rap, r.retain_handling, (int32_t)r.identifier);
       if (h->async()) h->journal.subscribe(client, filter, r.qos, nl, rap, r.retain_handling, (int32_t)r.identifier);
       return true;
     };
@@ -783,6 +811,7 @@ int mqm_unsubscribe_many(mqm_index *h, size_t n, const char *filter_bytes, const
       const auto f = sv(filter_bytes + filter_offs[i], filter_offs[i + 1] - filter_offs[i]);
       const auto c = sv(client_bytes + client_offs[i], client_offs[i + 1] - client_offs[i]);
       bool r = h->store.unsubscribe(f, c);
+      if (r && h->fresh) h->fresh->on_unsubscribe(h->store, f);
       if (r && h->async()) h->journal.unsubscribe(f, c, &h->store.last_footprint());
       if (existed) existed[i] = r ? 1 : 0;
     }
@@ -797,6 +826,7 @@ int mqm_retain_message(mqm_index *h, const char *topic, size_t topic_len, uint64
   return guarded([&] {
     std::lock_guard<std::mutex> g(h->mu);
     int64_t r = h->store.retain_message(sv(topic, topic_len), message_ref, payload_len, retain_flag != 0);
+    if (h->fresh) h->fresh->on_version(h->store);
     if (h->async()) {
       h->journal.retain(sv(topic, topic_len), message_ref, payload_len, retain_flag != 0);
       maybe_submit(h);
@@ -816,6 +846,7 @@ int mqm_retain_many(mqm_index *h, size_t n, const char *topic_bytes, const uint6
       const auto t = sv(topic_bytes + topic_offs[i], topic_offs[i + 1] - topic_offs[i]);
       const bool flag = retain_flags ? retain_flags[i] != 0 : true;
       int64_t r = h->store.retain_message(t, message_refs[i], payload_lens[i], flag);
+      if (h->fresh) h->fresh->on_version(h->store);
       if (h->async()) h->journal.retain(t, message_refs[i], payload_lens[i], flag);
       if (results) results[i] = r;
     }
@@ -2116,8 +2147,89 @@ mqm_index::~mqm_index() {
   pool.clear();
 }
 
-int mqm_subscribers(mqm_index *h, const char *topic, size_t topic_len, mqm_result **out) {
-  if (!h || !out) return MQM_EINVAL;
+// MQM_CFG_FRESH: a single-topic result brought to the store's current
+// subscriptions (fresh.h).  Returns MQM_OK (the result replaced when a client
+// in it, or one that now matches, was touched after its snapshot), 1 when the
+// result's snapshot is older than the overlay covers (match again), or an error.
+static int freshen(mqm_index *h, std::string_view topic, mqm_result **res) {
+  mqm_result *r = *res;
+  if (!r || r->n != 1 || !r->snap) return MQM_OK;
+  const uint64_t vs = r->snap->version;
+  FreshOverlay::Reader rd(*h->fresh);
+  const int st = rd.status(vs);
+  if (st <= 0) return st < 0 ? 1 : MQM_OK;
+  FreshOverlay::Match m;
+  rd.match(topic, vs, &m);
+  const HostSnapshot &hs = *r->snap;
+  const uint64_t base = hs.sub_info.size(), sbase = hs.shared_info.size();
+  if (base + m.subs.size() > MQM_DELIVERY_SUB(~0u) + 1ull || sbase + m.shared.size() > MQM_DELIVERY_SUB(~0u) + 1ull)
+    return MQM_ELIMIT;
+  const bool packed = r->deliveries == nullptr;
+  // the snapshot's rows of clients nobody touched since it, then the touched
+  // clients' rows from the overlay
+  std::vector<mqm_delivery> dl;
+  dl.reserve(r->offsets[1] - r->offsets[0] + m.rows.size());
+  for (uint64_t j = r->offsets[0]; j < r->offsets[1]; j++) {
+    const uint32_t pk = packed ? r->packed[j] : r->deliveries[j].packed;
+    const uint32_t client = packed ? hs.sub_info[MQM_DELIVERY_SUB(pk)].client : r->deliveries[j].client;
+    if (!rd.touched(client, vs)) dl.push_back(mqm_delivery{client, pk});
+  }
+  for (const auto &row : m.rows)
+    dl.push_back(mqm_delivery{row.client, (uint32_t)(base + row.first) | (uint32_t)(row.qos & 3u) << 28 |
+                                              (uint32_t)(row.no_local & 1u) << 30});
+  std::vector<uint32_t> sh;
+  for (uint64_t j = r->shared_offsets[0]; j < r->shared_offsets[1]; j++)
+    if (!rd.touched(hs.shared_info[r->shared[j]].client, vs)) sh.push_back(r->shared[j]);
+  for (size_t k = 0; k < m.shared.size(); k++) sh.push_back((uint32_t)(sbase + k));
+  std::vector<uint32_t> ids;
+  if (r->has_idents) {
+    for (uint64_t j = r->ident_offsets[0]; j < r->ident_offsets[1]; j++)
+      if (!rd.touched(hs.sub_info[r->idents[j]].client, vs)) ids.push_back(r->idents[j]);
+    for (size_t g = 0; g < m.subs.size(); g++)  // (packets.go:257-259: Identifiers > 0)
+      if (m.subs[g].info.ident > 0) ids.push_back((uint32_t)(base + g));
+  }
+  auto r2 = std::make_unique<mqm_result>();
+  const ResultLayout lay(2, dl.size(), sh.size(), packed ? 4 : 8, ids.size(), r->has_idents);
+  if (!r2->alloc(h->pinned, lay.total, false)) return MQM_ENOMEM;
+  char *B = static_cast<char *>(r2->blk);
+  auto *off = reinterpret_cast<uint64_t *>(B), *soff = reinterpret_cast<uint64_t *>(B + lay.o_sh);
+  off[0] = 0;
+  off[1] = dl.size();
+  soff[0] = 0;
+  soff[1] = sh.size();
+  if (packed) {
+    auto *p4 = reinterpret_cast<uint32_t *>(B + lay.o_d);
+    for (size_t j = 0; j < dl.size(); j++) p4[j] = dl[j].packed;
+    r2->packed = p4;
+  } else {
+    if (!dl.empty()) memcpy(B + lay.o_d, dl.data(), sizeof(mqm_delivery) * dl.size());
+    r2->deliveries = reinterpret_cast<const mqm_delivery *>(B + lay.o_d);
+  }
+  if (!sh.empty()) memcpy(B + lay.o_s, sh.data(), 4 * sh.size());
+  if (r->has_idents) {
+    auto *ioff = reinterpret_cast<uint64_t *>(B + lay.o_io);
+    ioff[0] = 0;
+    ioff[1] = ids.size();
+    if (!ids.empty()) memcpy(B + lay.o_i, ids.data(), 4 * ids.size());
+    r2->has_idents = true;
+    r2->ident_offsets = ioff;
+    r2->idents = reinterpret_cast<const uint32_t *>(B + lay.o_i);
+  }
+  r2->n = 1;
+  r2->offsets = off;
+  r2->shared_offsets = soff;
+  r2->shared = reinterpret_cast<const uint32_t *>(B + lay.o_s);
+  r2->snap = r->snap;
+  r2->version = m.version;
+  r2->extra.reserve(m.subs.size());
+  for (const auto &g : m.subs) r2->extra.push_back(g.info);
+  r2->extra_shared = std::move(m.shared);
+  mqm_result_free(r);
+  *res = r2.release();
+  return MQM_OK;
+}
+
+static int subscribers_once(mqm_index *h, const char *topic, size_t topic_len, mqm_result **out) {
   if (Server *sv = h->server.load(std::memory_order_acquire)) {
     *out = nullptr;
     return guarded([&] { return sv->submit(topic ? topic : "", topic_len, out); });
@@ -2128,6 +2240,35 @@ int mqm_subscribers(mqm_index *h, const char *topic, size_t topic_len, mqm_resul
   }
   uint64_t offs[2] = {0, topic_len};
   return mqm_match_batch(h, topic ? topic : "", offs, 1, out);
+}
+
+int mqm_subscribers(mqm_index *h, const char *topic, size_t topic_len, mqm_result **out) {
+  if (!h || !out) return MQM_EINVAL;
+  if (!h->fresh || !h->fresh_reads.load(std::memory_order_relaxed)) return subscribers_once(h, topic, topic_len, out);
+  // (a result on a snapshot two publishes old: the newest one is at most one
+  // publish behind the overlay, so the second attempt corrects)
+  for (int attempt = 0; attempt < 8; attempt++) {
+    int rc = subscribers_once(h, topic, topic_len, out);
+    if (rc != MQM_OK) return rc;
+    rc = guarded([&] { return freshen(h, std::string_view(topic ? topic : "", topic_len), out); });
+    if (rc != 1) return rc;
+    mqm_result_free(*out);
+    *out = nullptr;
+  }
+  return MQM_EHIP;
+}
+
+int mqm_fresh_policy(mqm_index *h, int correct_calls) {
+  if (!h || !h->fresh) return MQM_EINVAL;
+  h->fresh_reads.store(correct_calls != 0, std::memory_order_relaxed);
+  return MQM_OK;
+}
+
+int mqm_fresh_stats(mqm_index *h, uint64_t *held_clients) {
+  if (!h || !h->fresh || !held_clients) return MQM_EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  *held_clients = h->fresh->clients();
+  return MQM_OK;
 }
 
 int mqm_batching_policy(mqm_index *h, uint32_t max_batch, uint32_t linger_us) {
@@ -2281,7 +2422,9 @@ int mqm_batching_stats(mqm_index *h, uint64_t *batches, uint64_t *topics) {
 }
 
 uint32_t mqm_result_num_topics(const mqm_result *r) { return r ? r->n : 0; }
-uint64_t mqm_result_snapshot_version(const mqm_result *r) { return r && r->snap ? r->snap->version : 0; }
+uint64_t mqm_result_snapshot_version(const mqm_result *r) {
+  return !r ? 0 : r->version ? r->version : r->snap ? r->snap->version : 0;
+}
 const uint64_t *mqm_result_offsets(const mqm_result *r) { return r ? r->offsets : nullptr; }
 const mqm_delivery *mqm_result_deliveries(const mqm_result *r) { return r ? r->deliveries : nullptr; }
 const uint32_t *mqm_result_packed(const mqm_result *r) { return r ? r->packed : nullptr; }
@@ -2321,22 +2464,33 @@ int mqm_result_expand(const mqm_result *r, uint32_t t0, uint32_t t1, uint64_t *o
 const uint64_t *mqm_result_shared_offsets(const mqm_result *r) { return r ? r->shared_offsets : nullptr; }
 const uint32_t *mqm_result_shared(const mqm_result *r) { return r ? r->shared : nullptr; }
 
+// a result's subscription record: the snapshot's, or past its sids a fresh
+// result's own (freshen)
+static const SubInfo *result_info(const mqm_result *r, uint32_t sub, bool shared) {
+  const auto &tab = shared ? r->snap->shared_info : r->snap->sub_info;
+  if (sub < tab.size()) return &tab[sub];
+  const auto &ext = shared ? r->extra_shared : r->extra;
+  return sub - tab.size() < ext.size() ? &ext[sub - tab.size()] : nullptr;
+}
+
 int mqm_result_sub_info(const mqm_result *r, uint32_t sub, mqm_sub_info *out) {
-  if (!r || !out || !r->snap || sub >= r->snap->sub_info.size()) return MQM_EINVAL;
-  return fill_info(r->snap->sub_info[sub], out);
+  if (!r || !out || !r->snap) return MQM_EINVAL;
+  const SubInfo *x = result_info(r, sub, false);
+  return x ? fill_info(*x, out) : MQM_EINVAL;
 }
 
 int mqm_result_shared_info(const mqm_result *r, uint32_t shared_sub, mqm_sub_info *out) {
-  if (!r || !out || !r->snap || shared_sub >= r->snap->shared_info.size()) return MQM_EINVAL;
-  return fill_info(r->snap->shared_info[shared_sub], out);
+  if (!r || !out || !r->snap) return MQM_EINVAL;
+  const SubInfo *x = result_info(r, shared_sub, true);
+  return x ? fill_info(*x, out) : MQM_EINVAL;
 }
 
 int mqm_result_sub_infos(const mqm_result *r, int shared, const uint32_t *subs, size_t n, mqm_sub_info *out) {
   if (!r || !r->snap || (n && (!subs || !out))) return MQM_EINVAL;
-  const auto &tab = shared ? r->snap->shared_info : r->snap->sub_info;
   for (size_t i = 0; i < n; i++) {
-    if (subs[i] >= tab.size()) return MQM_EINVAL;
-    fill_info(tab[subs[i]], &out[i]);
+    const SubInfo *x = result_info(r, subs[i], shared != 0);
+    if (!x) return MQM_EINVAL;
+    fill_info(*x, &out[i]);
   }
   return MQM_OK;
 }

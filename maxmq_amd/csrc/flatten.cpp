@@ -1031,6 +1031,22 @@ int flatten(const Store &st, HostSnapshot *out, bool host_edges, FlattenCache *c
   return MQM_OK;
 }
 
+// counting sorts of the sids by client (sids ascending within a client)
+void build_client_index(HostSnapshot &hs) {
+  auto by_client = [](const std::vector<SubInfo> &info, std::vector<uint32_t> &off, std::vector<uint32_t> &ids) {
+    uint32_t nc = 0;
+    for (const SubInfo &x : info) nc = std::max(nc, x.client + 1);
+    off.assign((size_t)nc + 1, 0);
+    for (const SubInfo &x : info) off[x.client + 1]++;
+    for (uint32_t c = 0; c < nc; c++) off[c + 1] += off[c];
+    ids.resize(info.size());
+    std::vector<uint32_t> cur(off.begin(), off.end() - 1);
+    for (uint32_t sid = 0; sid < (uint32_t)info.size(); sid++) ids[cur[info[sid].client]++] = sid;
+  };
+  by_client(hs.sub_info, hs.client_off, hs.client_subs);
+  by_client(hs.shared_info, hs.client_shoff, hs.client_shared);
+}
+
 namespace {
 // host -> device in pieces of kUploadChunk: one long DMA of gigabytes held the
 // per-publish server's polls of its ring (reads of host memory, whose data

@@ -71,6 +71,10 @@ struct HostSnapshot {
   // the store version this snapshot reflects (set by the committer after
   // flatten; equal versions mean equal snapshots: flatten is deterministic)
   uint64_t version = 0;
+  // MQM_CFG_FRESH (fresh.h): the subscriptions by client, built after flatten
+  // (build_client_index) — client c's sids at client_subs[client_off[c] ..
+  // client_off[c + 1]), its shared sids likewise; empty when not built
+  std::vector<uint32_t> client_off, client_subs, client_shoff, client_shared;
 };
 
 // What a rebuild of the same trie shape can reuse (the background builder
@@ -105,6 +109,9 @@ struct FlattenCache {
 // `staged` (the host fill of the table and its transfer were most of a
 // rebuild: 18.5 GB at config 3 against 2.2 GB of staged edges).
 int flatten(const Store &st, HostSnapshot *out, bool host_edges = true, FlattenCache *cache = nullptr);
+// the snapshot's subscriptions by client (HostSnapshot::client_off ..), for
+// the fresh overlay's first look at a client (fresh.h)
+void build_client_index(HostSnapshot &hs);
 // MQM_HOST_EDGES=1 (A/B, diagnostics): the edge table is built on the host
 // and copied, never on the device (edges.hip)
 bool host_edges_forced();

@@ -32,6 +32,7 @@
 #   hostab  : the host-path legs with DMA / kernel result copies (MQM_D2H_KERNEL=1), 4 / 8 HW queues
 #   hostthreads: the host-path legs on 4 / 12 / 16 caller threads
 #   kcopyt  : the runs-form tests, kernel copy-out parity included
+#   freshtest: the MQM_CFG_FRESH tests (every mutation visible at once) + the served / churn tests
 #   c2      : the C2 bench line (1M filters, 10M topics) with roofline and CPU baseline -> bench_c2.json
 #   c4fast  : the C4 shard bench without CPU baseline
 #   pipe    : `fast` with pipelined steps on 2 and 3 contexts -> bench_fast_pipe{2,3}.json
@@ -167,6 +168,8 @@ for step in "$@"; do
             --steady-steps 0 --ident-steps 0 --host-threads $T > $OUT/bench_host_t$T.json 2> $OUT/bench_host_t$T.log || exit 1
         done ;;
     kcopyt) timeout -k 10 400 $PYT tests/test_gpu_runs.py -m gpu --timeout 200 > $OUT/pytest_kcopy.log 2>&1 ;;
+    freshtest) timeout -k 10 600 $PYT -s tests/test_gpu_fresh.py tests/test_gpu_serve_churn.py tests/test_gpu_serve.py -m gpu \
+             --timeout 300 > $OUT/pytest_fresh.log 2>&1 ;;
     c2) timeout -k 10 600 python3 -u bench.py --config 2 --steps 10 --warmup 3 --host-topics 0 --latency-topics 0 \
              --steady-steps 0 --cpu-seconds 10 > $OUT/bench_c2.json 2> $OUT/bench_c2.log ;;
     c4fast) timeout -k 10 600 python3 -u bench.py --config 4 --shard 0/8 $FAST > $OUT/bench_c4_fast.json 2> $OUT/bench_c4_fast.log ;;

@@ -21,14 +21,15 @@
  *         the mutations before it, read-your-writes) or "async"
  *         (ASYNC_COMMIT | IDENTIFIERS | SERVE, rebuilt in the background by
  *         mqm_commit_policy(64 ops, 2 ms): calls match the newest published
- *         snapshot)
+ *         snapshot) or "fresh" (async + MQM_CFG_FRESH: calls return the
+ *         store's current subscriptions, read-your-writes checked)
  *   OP_US: microseconds the mutator sleeps between operations
  *   OUT : "B version" (after the base subscriptions), "V j version" after
  *         operation j, then per call "C thread call topic version" followed by
  *         that result's rendered lines (shim_harness.c's format:
  *         "D t client qos nl filter ident rap rh f1=i1,..." / "H t filter client")
  * Reader thread r makes CALLS calls on topics (r * 7919 + c * 104729) mod
- * n_topics.  A reader in "autocommit" mode also checks read-your-writes: the
+ * n_topics.  A reader in "autocommit" or "fresh" mode also checks read-your-writes: the
  * version of a result is at least the store version it read before the call.
  * Exit status 0 when every call returned MQM_OK and every check held.
  */
@@ -74,7 +75,7 @@ static mqm_index *H;
 static char **topics;
 static size_t *topic_len;
 static uint32_t n_topics, n_calls;
-static int n_threads, autocommit;
+static int n_threads, autocommit, fresh;
 static volatile int failed;
 static Buf *out_of;  /* per reader thread */
 
@@ -175,7 +176,7 @@ static void *reader(void *arg) {
   Buf *b = &out_of[id];
   for (uint32_t c = 0; c < n_calls; c++) {
     const uint32_t t = (uint32_t)(((uint64_t)id * 7919u + (uint64_t)c * 104729u) % n_topics);
-    const uint64_t before = autocommit ? store_version() : 0;
+    const uint64_t before = autocommit || fresh ? store_version() : 0;
     mqm_result *r = NULL;
     if (mqm_subscribers(H, topics[t], topic_len[t], &r) != MQM_OK || mqm_result_num_topics(r) != 1) {
       fail("mqm_subscribers");
@@ -183,7 +184,7 @@ static void *reader(void *arg) {
       continue;
     }
     const uint64_t v = mqm_result_snapshot_version(r);
-    if (autocommit && v < before) {
+    if ((autocommit || fresh) && v < before) {
       char msg[128];
       snprintf(msg, sizeof msg, "read-your-writes: result version %llu < store version %llu before the call",
                (unsigned long long)v, (unsigned long long)before);
@@ -251,15 +252,16 @@ int main(int argc, char **argv) {
   n_threads = atoi(argv[3]);
   n_calls = (uint32_t)atoi(argv[4]);
   autocommit = strcmp(argv[5], "autocommit") == 0;
+  fresh = strcmp(argv[5], "fresh") == 0;
   op_us = (unsigned)atoi(argv[6]);
-  if (n_threads < 1 || n_threads > 128 || (!autocommit && strcmp(argv[5], "async") != 0)) return 2;
+  if (n_threads < 1 || n_threads > 128 || (!autocommit && !fresh && strcmp(argv[5], "async") != 0)) return 2;
   FILE *in = fopen(argv[1], "rb");
   FILE *out = fopen(argv[2], "wb");
   if (!in || !out) return 2;
   unsigned long nb = 0, no = 0, nt = 0;
   if (fscanf(in, "%lu %lu %lu\n", &nb, &no, &nt) != 3 || nt == 0) return 2;
   mqm_config cfg = {0, MQM_CFG_IDENTIFIERS | MQM_CFG_SERVE |
-                           (autocommit ? MQM_CFG_AUTOCOMMIT : MQM_CFG_ASYNC_COMMIT)};
+                           (autocommit ? MQM_CFG_AUTOCOMMIT : MQM_CFG_ASYNC_COMMIT) | (fresh ? MQM_CFG_FRESH : 0u)};
   if (mqm_create(&cfg, &H) != MQM_OK) {
     fprintf(stderr, "mqm_create failed\n");
     return 3;

@@ -10,8 +10,9 @@ on (mqm_result_snapshot_version).  Each result must equal the oracle
 (oracle/mochi_ref.c, topics.go:484-555 + packets.go:250-270) replayed up to
 exactly that version — the full rendered `*Subscribers` value: client, QoS,
 NoLocal, first filter, its Identifier, RAP, RH, the Identifiers map, and the
-shared (filter, client) pairs.  With MQM_CFG_AUTOCOMMIT the harness also
-checks read-your-writes (a result's version is at least the store version the
+shared (filter, client) pairs.  With MQM_CFG_AUTOCOMMIT, and with
+MQM_CFG_FRESH (results corrected on the host for the clients touched since
+their snapshot, no commit per call), the harness also checks read-your-writes (a result's version is at least the store version the
 caller read before the call).  A result decoded with another snapshot than the
 one the server matched it on (the round-4 race: sids are snapshot positions)
 shows up here as a wrong first filter / identifier or a mismatched set."""
@@ -128,11 +129,12 @@ def _render_oracle(ora, topic_ids, topics):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode,threads,calls,op_us", [("autocommit", 32, 120, 3000), ("async", 64, 150, 200)])
+@pytest.mark.parametrize("mode,threads,calls,op_us", [("autocommit", 32, 120, 3000), ("async", 64, 150, 200),
+                                                     ("fresh", 64, 150, 200)])
 def test_served_calls_under_churn_equal_oracle_at_their_version(tmp_path, mode, threads, calls, op_us):
     _harness()
-    base, ops, topics = _plan(n_base=6000, n_extra=1500, n_topics=800, n_ops=1200 if mode == "async" else 300,
-                              seed=0xC4A2 + (mode == "async"))
+    base, ops, topics = _plan(n_base=6000, n_extra=1500, n_topics=800, n_ops=300 if mode == "autocommit" else 1200,
+                              seed=0xC4A2 + (mode != "autocommit"))
     inp, out = tmp_path / "in.txt", tmp_path / "out.txt"
     _write(inp, base, ops, topics)
     r = subprocess.run([HARNESS, str(inp), str(out), str(threads), str(calls), mode, str(op_us)],
