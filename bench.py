@@ -967,6 +967,8 @@ def run_churn(args, dist, rank, world, local, dev):
                                 fresh=bool(args.churn_fresh_legs.strip()))
     idx.subscribe_workload(w)
     idx.commit()
+    if idx.fresh:
+        idx.fresh_policy(False)  # (on for the fresh_* served legs only)
     build_s = time.time() - t0
     log(f"[rank {rank}] async index built in {build_s:.1f}s: {idx.commit_state()}")
     tb = torch.from_numpy(w.topics.data).to(dev)
@@ -1162,10 +1164,14 @@ def serve_churn(idx, w, args):
             idx.fresh_policy(fresh)
         idx.commit_poll(wait=True)  # (the previous leg's mutations built and published)
         idx.commit_policy(0, 50 if bt >= 0 else 0)
+        f0 = idx.fresh_stats() if fresh else None
         name = ("fresh_" if fresh else "") + (f"build_threads_{bt}" if bt >= 0 else "no_rebuild")
         legs[name] = run(args.serve_churn_s, args.churn_rate)
         if fresh:
-            legs[name]["fresh_clients_held"] = idx.fresh_clients()
+            f1 = idx.fresh_stats()
+            fs = {k: f1[k] - f0[k] if k != "held_clients" else f1[k] for k in f1}
+            fs["read_us_per_corrected_call"] = fs["read_ns"] / max(1, fs["calls_corrected"]) / 1e3
+            legs[name]["fresh"] = fs
         log(f"[serve churn] {name}: {legs[name]}")
     if fresh_on:
         idx.fresh_policy(False)

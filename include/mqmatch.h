@@ -310,11 +310,13 @@ int mqm_batching_policy(mqm_index *h, uint32_t max_batch, uint32_t linger_us);
  * launches.  MQM_EINVAL on a host-only index (or for stats while off). */
 int mqm_serve_policy(mqm_index *h, uint32_t grid, uint32_t idle_us);
 /* MQM_CFG_FRESH indexes: correct_calls = 0 makes mqm_subscribers return the
- * snapshot's view again (the overlay is still kept up to date; A/B and
- * measurement), 1 turns the correction back on; statistics: the clients the
- * overlay holds.  MQM_EINVAL on an index created without the flag. */
+ * snapshot's view again and drops the overlay (mutations cost nothing extra;
+ * A/B and measurement), 1 starts it again from the published snapshot.
+ * Statistics (out[5]): clients held, overlay operations applied (per copy), applier rounds,
+ * calls corrected, nanoseconds spent in the corrections' read sections.
+ * MQM_EINVAL on an index created without the flag. */
 int mqm_fresh_policy(mqm_index *h, int correct_calls);
-int mqm_fresh_stats(mqm_index *h, uint64_t *held_clients);
+int mqm_fresh_stats(mqm_index *h, uint64_t *out);
 /* (grid is capped at half the device's CUs: a server under steady traffic
  * never idles out, and batch-path calls need the rest of the device) */
 int mqm_serve_stats(mqm_index *h, uint64_t *served, uint64_t *fallbacks, uint64_t *launches);

@@ -256,11 +256,14 @@ class TopicsIndex:
         the default) or the published snapshot's view (False)"""
         check("mqm_fresh_policy", lib().mqm_fresh_policy(self._h, int(bool(correct_calls))))
 
-    def fresh_clients(self) -> int:
-        """clients the fresh overlay holds (touched since the previous snapshot)"""
-        v = C.c_uint64()
+    def fresh_stats(self) -> dict:
+        """the fresh overlay: clients held (touched since the previous
+        snapshot), mutations applied per copy, flushes, calls corrected and
+        the time in their read sections"""
+        v = (C.c_uint64 * 5)()
         check("mqm_fresh_stats", lib().mqm_fresh_stats(self._h, C.byref(v)))
-        return v.value
+        return {"held_clients": v[0], "ops_applied": v[1], "rounds": v[2], "calls_corrected": v[3],
+                "read_ns": v[4]}
 
     def batching_policy(self, max_batch: int = 0, linger_us: int = 0):
         check("mqm_batching_policy", lib().mqm_batching_policy(self._h, max_batch, linger_us))

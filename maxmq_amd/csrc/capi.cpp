@@ -2154,40 +2154,48 @@ mqm_index::~mqm_index() {
 static int freshen(mqm_index *h, std::string_view topic, mqm_result **res) {
   mqm_result *r = *res;
   if (!r || r->n != 1 || !r->snap) return MQM_OK;
+  h->fresh->await_own_writes();  // (this thread's mutations still queued: applied first)
+  const int64_t t_read = steady_ns();
   const uint64_t vs = r->snap->version;
-  FreshOverlay::Reader rd(*h->fresh);
-  const int st = rd.status(vs);
-  if (st <= 0) return st < 0 ? 1 : MQM_OK;
-  FreshOverlay::Match m;
-  rd.match(topic, vs, &m);
   const HostSnapshot &hs = *r->snap;
   const uint64_t base = hs.sub_info.size(), sbase = hs.shared_info.size();
-  if (base + m.subs.size() > MQM_DELIVERY_SUB(~0u) + 1ull || sbase + m.shared.size() > MQM_DELIVERY_SUB(~0u) + 1ull)
-    return MQM_ELIMIT;
   const bool packed = r->deliveries == nullptr;
-  // the snapshot's rows of clients nobody touched since it, then the touched
-  // clients' rows from the overlay
-  std::vector<mqm_delivery> dl;
-  dl.reserve(r->offsets[1] - r->offsets[0] + m.rows.size());
-  for (uint64_t j = r->offsets[0]; j < r->offsets[1]; j++) {
-    const uint32_t pk = packed ? r->packed[j] : r->deliveries[j].packed;
-    const uint32_t client = packed ? hs.sub_info[MQM_DELIVERY_SUB(pk)].client : r->deliveries[j].client;
-    if (!rd.touched(client, vs)) dl.push_back(mqm_delivery{client, pk});
+  // (per-thread scratch: their capacity kept from call to call)
+  thread_local FreshOverlay::Match m;
+  thread_local std::vector<mqm_delivery> dl;
+  thread_local std::vector<uint32_t> sh, ids;
+  dl.clear();
+  sh.clear();
+  ids.clear();
+  {
+    FreshOverlay::Reader rd(*h->fresh);
+    const int st = rd.status(vs);
+    if (st <= 0) return st < 0 ? 1 : MQM_OK;
+    rd.match(topic, vs, &m);
+    if (base + m.subs.size() > MQM_DELIVERY_SUB(~0u) + 1ull || sbase + m.shared.size() > MQM_DELIVERY_SUB(~0u) + 1ull)
+      return MQM_ELIMIT;
+    // the snapshot's rows of clients nobody touched since it, then the touched
+    // clients' rows from the overlay
+    dl.reserve(r->offsets[1] - r->offsets[0] + m.rows.size());
+    for (uint64_t j = r->offsets[0]; j < r->offsets[1]; j++) {
+      const uint32_t pk = packed ? r->packed[j] : r->deliveries[j].packed;
+      const uint32_t client = packed ? hs.sub_info[MQM_DELIVERY_SUB(pk)].client : r->deliveries[j].client;
+      if (!rd.touched(client, vs)) dl.push_back(mqm_delivery{client, pk});
+    }
+    for (uint64_t j = r->shared_offsets[0]; j < r->shared_offsets[1]; j++)
+      if (!rd.touched(hs.shared_info[r->shared[j]].client, vs)) sh.push_back(r->shared[j]);
+    if (r->has_idents)
+      for (uint64_t j = r->ident_offsets[0]; j < r->ident_offsets[1]; j++)
+        if (!rd.touched(hs.sub_info[r->idents[j]].client, vs)) ids.push_back(r->idents[j]);
   }
+  h->fresh->count_read((uint64_t)(steady_ns() - t_read));
   for (const auto &row : m.rows)
     dl.push_back(mqm_delivery{row.client, (uint32_t)(base + row.first) | (uint32_t)(row.qos & 3u) << 28 |
                                               (uint32_t)(row.no_local & 1u) << 30});
-  std::vector<uint32_t> sh;
-  for (uint64_t j = r->shared_offsets[0]; j < r->shared_offsets[1]; j++)
-    if (!rd.touched(hs.shared_info[r->shared[j]].client, vs)) sh.push_back(r->shared[j]);
   for (size_t k = 0; k < m.shared.size(); k++) sh.push_back((uint32_t)(sbase + k));
-  std::vector<uint32_t> ids;
-  if (r->has_idents) {
-    for (uint64_t j = r->ident_offsets[0]; j < r->ident_offsets[1]; j++)
-      if (!rd.touched(hs.sub_info[r->idents[j]].client, vs)) ids.push_back(r->idents[j]);
+  if (r->has_idents)
     for (size_t g = 0; g < m.subs.size(); g++)  // (packets.go:257-259: Identifiers > 0)
       if (m.subs[g].info.ident > 0) ids.push_back((uint32_t)(base + g));
-  }
   auto r2 = std::make_unique<mqm_result>();
   const ResultLayout lay(2, dl.size(), sh.size(), packed ? 4 : 8, ids.size(), r->has_idents);
   if (!r2->alloc(h->pinned, lay.total, false)) return MQM_ENOMEM;
@@ -2223,7 +2231,7 @@ static int freshen(mqm_index *h, std::string_view topic, mqm_result **res) {
   r2->version = m.version;
   r2->extra.reserve(m.subs.size());
   for (const auto &g : m.subs) r2->extra.push_back(g.info);
-  r2->extra_shared = std::move(m.shared);
+  r2->extra_shared.assign(m.shared.begin(), m.shared.end());
   mqm_result_free(r);
   *res = r2.release();
   return MQM_OK;
@@ -2260,14 +2268,22 @@ int mqm_subscribers(mqm_index *h, const char *topic, size_t topic_len, mqm_resul
 
 int mqm_fresh_policy(mqm_index *h, int correct_calls) {
   if (!h || !h->fresh) return MQM_EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  // (off: the overlay is dropped and mutations cost nothing more; on: it
+  // starts again from the published snapshot)
   h->fresh_reads.store(correct_calls != 0, std::memory_order_relaxed);
+  h->fresh->set_enabled(correct_calls != 0, h->snap ? h->snap->host : nullptr, h->store);
   return MQM_OK;
 }
 
-int mqm_fresh_stats(mqm_index *h, uint64_t *held_clients) {
-  if (!h || !h->fresh || !held_clients) return MQM_EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
-  *held_clients = h->fresh->clients();
+int mqm_fresh_stats(mqm_index *h, uint64_t *out) {
+  if (!h || !h->fresh || !out) return MQM_EINVAL;
+  const FreshOverlay::Stats s = h->fresh->stats();
+  out[0] = s.held;
+  out[1] = s.ops;
+  out[2] = s.rounds;
+  out[3] = s.corrected;
+  out[4] = s.read_ns;
   return MQM_OK;
 }
 

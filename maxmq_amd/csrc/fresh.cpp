@@ -2,7 +2,7 @@
 #include "fresh.h"
 
 #include <algorithm>
-#include <mutex>
+#include <chrono>
 
 namespace mqm {
 
@@ -14,15 +14,287 @@ uint64_t fnv(std::string_view s) {
 }
 // gatherSubscriptions' "$" rule (topics.go:527) tests the filter's first byte
 uint8_t dollar_skip(std::string_view f) { return !f.empty() && (f[0] == '+' || f[0] == '#'); }
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+// the calling thread's newest queued mutation per overlay (a few overlays:
+// the thread's own writes its next call on that index must see)
+struct LastWrite {
+  const void *owner = nullptr;
+  uint64_t version = 0;
+};
+thread_local LastWrite tl_writes[4];
+void note_write(const void *o, uint64_t v) {
+  for (auto &w : tl_writes)
+    if (w.owner == o) {
+      w.version = v;
+      return;
+    }
+  for (int i = 3; i > 0; i--) tl_writes[i] = tl_writes[i - 1];
+  tl_writes[0] = LastWrite{o, v};
+}
+uint64_t last_write(const void *o) {
+  for (const auto &w : tl_writes)
+    if (w.owner == o) return w.version;
+  return 0;
+}
 }  // namespace
 
-uint32_t FreshOverlay::token(std::string_view s, bool create) {
-  const uint64_t h = fnv(s);
-  auto it = tok_head_.find(h);
+// ---- lifecycle, the applier ------------------------------------------------
+
+FreshOverlay::FreshOverlay() { th_ = std::thread([this] { run(); }); }
+
+FreshOverlay::~FreshOverlay() {
+  {
+    std::lock_guard<std::mutex> g(qmu_);
+    stop_ = true;
+  }
+  qcv_.notify_all();
+  done_cv_.notify_all();
+  th_.join();
+}
+
+void FreshOverlay::run() {
+  std::unique_lock<std::mutex> lk(qmu_);
+  for (;;) {
+    qcv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+    if (stop_) return;
+    // let a batch gather for up to kApplyNs after its first operation
+    const auto due = std::chrono::steady_clock::time_point(std::chrono::nanoseconds(oldest_ns_ + kApplyNs));
+    qcv_.wait_until(lk, due, [&] { return stop_ || urgent_ || q_.size() >= kBatch; });
+    if (stop_) return;
+    std::vector<Op> batch;
+    batch.swap(q_);
+    urgent_ = false;
+    oldest_ns_ = 0;
+    lk.unlock();
+    round(batch);
+    lk.lock();
+    done_cv_.notify_all();
+  }
+}
+
+// one left-right round: the batch (and the previous one) into the copy no call
+// reads, then that copy becomes the current one
+void FreshOverlay::round(std::vector<Op> &batch) {
+  if (batch.empty()) return;
+  const int c = cur_.load(std::memory_order_seq_cst), o = 1 - c;
+  // the calls that entered the other copy before it stopped being current (a
+  // caller preempted inside it: yield rather than spin a timeslice away)
+  for (uint32_t spin = 0; readers_[o].n.load(std::memory_order_seq_cst) != 0; spin++) {
+    if (spin < 2048)
+      __builtin_ia32_pause();
+    else
+      std::this_thread::yield();
+  }
+  State &x = s_[o];
+  for (const Op &op : lag_) x.apply(op);
+  for (const Op &op : batch) x.apply(op);
+  cur_.store(o, std::memory_order_seq_cst);
+  applied_.store(batch.back().version, std::memory_order_release);
+  ops_.fetch_add(lag_.size() + batch.size(), std::memory_order_relaxed);
+  rounds_.fetch_add(1, std::memory_order_relaxed);
+  lag_.swap(batch);
+}
+
+void FreshOverlay::await_own_writes() {
+  const uint64_t w = last_write(this);
+  if (w == 0 || applied_.load(std::memory_order_acquire) >= w) return;
+  std::unique_lock<std::mutex> lk(qmu_);
+  urgent_ = true;
+  qcv_.notify_one();
+  // (bounded: a result that misses the write still reports its version)
+  done_cv_.wait_for(lk, std::chrono::milliseconds(200),
+                    [&] { return stop_ || applied_.load(std::memory_order_acquire) >= w; });
+}
+
+// ---- the mutating side (index mutex held) ----------------------------------
+
+void FreshOverlay::enqueue(Op &&op) {
+  note_write(this, op.version);
+  bool wake = false;
+  {
+    std::lock_guard<std::mutex> g(qmu_);
+    if (q_.empty()) {
+      oldest_ns_ = now_ns();
+      wake = true;
+    }
+    q_.push_back(std::move(op));
+    wake |= q_.size() >= kBatch;
+  }
+  if (wake) qcv_.notify_one();
+}
+
+// a client's first touch since the overlay last held it: its subscriptions as
+// the published snapshot has them (it had no mutation since: it would be held)
+void FreshOverlay::hold(const Store &st, uint32_t c, uint64_t v) {
+  auto it = mirror_.find(c);
+  if (it != mirror_.end()) {
+    it->second = v;
+    return;
+  }
+  Op op;
+  op.kind = Op::kLoad;
+  op.client = c;
+  op.version = v;
+  const HostSnapshot &hs = *mbase_;
+  if ((size_t)c + 1 < hs.client_off.size())
+    for (uint32_t k = hs.client_off[c]; k < hs.client_off[c + 1]; k++) {
+      const SubInfo &si = hs.sub_info[hs.client_subs[k]];
+      op.loads.push_back(Load{std::string(st.filters().name(si.filter)), 0, si});
+    }
+  if ((size_t)c + 1 < hs.client_shoff.size())
+    for (uint32_t k = hs.client_shoff[c]; k < hs.client_shoff[c + 1]; k++) {
+      const SubInfo &si = hs.shared_info[hs.client_shared[k]];
+      op.loads.push_back(Load{std::string(st.filters().name(si.filter)), 1, si});
+    }
+  enqueue(std::move(op));
+  mirror_.emplace(c, v);
+  held_n_.fetch_add(1, std::memory_order_relaxed);
+}
+
+// a few clients at a time: a publish under churn passes the floor over
+// hundreds of thousands at once (their entries are ignored by every result the
+// overlay still corrects until then: last mutation <= floor)
+void FreshOverlay::emit_prunes(size_t n) {
+  const uint64_t v = applied_.load(std::memory_order_relaxed);
+  for (; n > 0 && !mprune_.empty(); n--) {
+    const uint32_t c = mprune_.back();
+    mprune_.pop_back();
+    auto it = mirror_.find(c);
+    if (it == mirror_.end() || it->second > mfloor_) continue;  // (touched again since)
+    mirror_.erase(it);
+    held_n_.fetch_sub(1, std::memory_order_relaxed);
+    Op op;
+    op.kind = Op::kPrune;
+    op.client = c;
+    op.version = std::max(v, queued_version_);
+    enqueue(std::move(op));
+  }
+}
+
+void FreshOverlay::on_subscribe(const Store &st, std::string_view filter, const SubRec &rec) {
+  if (!enabled_) return;
+  Op op;
+  op.version = queued_version_ = st.version();
+  if (!mactive_) {
+    op.kind = Op::kVersion;
+    return enqueue(std::move(op));
+  }
+  hold(st, rec.client, op.version);
+  op.kind = Op::kPut;
+  op.client = rec.client;
+  op.filter = std::string(filter);
+  op.shared = st.last_footprint().shared;
+  op.info = SubInfo{rec.filter, rec.client, rec.ident, rec.qos, rec.no_local, rec.rap, rec.rh};
+  enqueue(std::move(op));
+  emit_prunes(2);
+}
+
+void FreshOverlay::on_unsubscribe(const Store &st, std::string_view filter) {
+  if (!enabled_) return;
+  const Store::Footprint &fp = st.last_footprint();
+  Op op;
+  op.version = queued_version_ = st.version();
+  if (!mactive_ || fp.client == kNone) {  // (a client never seen: nothing of it changes)
+    op.kind = Op::kVersion;
+    return enqueue(std::move(op));
+  }
+  hold(st, fp.client, op.version);
+  op.kind = Op::kDrop;
+  op.client = fp.client;
+  op.filter = std::string(filter);
+  op.shared = fp.shared;
+  enqueue(std::move(op));
+  emit_prunes(2);
+}
+
+void FreshOverlay::on_version(const Store &st) {
+  if (!enabled_) return;
+  Op op;
+  op.kind = Op::kVersion;
+  op.version = queued_version_ = st.version();
+  enqueue(std::move(op));
+}
+
+void FreshOverlay::on_install(std::shared_ptr<const HostSnapshot> hs, const Store &st) {
+  if (!enabled_) return;
+  Op op;
+  op.version = queued_version_ = st.version();
+  if (!hs || (hs->client_off.empty() && !hs->sub_info.empty()) ||
+      (hs->client_shoff.empty() && !hs->shared_info.empty())) {  // (no client index: nothing to start from)
+    mactive_ = false;
+    mirror_.clear();
+    mprune_.clear();
+    held_n_.store(0, std::memory_order_relaxed);
+    op.kind = Op::kReset;
+    return enqueue(std::move(op));
+  }
+  // results on the snapshot published before this one are still corrected;
+  // the clients only older results would need are dropped
+  mfloor_ = mactive_ && mbase_ ? mbase_->version : hs->version;
+  mprune_.clear();
+  for (const auto &kv : mirror_)
+    if (kv.second <= mfloor_) mprune_.push_back(kv.first);
+  mbase_ = std::move(hs);
+  mactive_ = true;
+  op.kind = Op::kInstall;
+  op.floor = mfloor_;
+  enqueue(std::move(op));
+}
+
+void FreshOverlay::set_enabled(bool on, std::shared_ptr<const HostSnapshot> published, const Store &st) {
+  if (on == enabled_) return;
+  if (!on) {
+    Op op;
+    op.kind = Op::kReset;
+    op.version = queued_version_ = st.version();
+    enqueue(std::move(op));
+    enabled_ = mactive_ = false;
+    mirror_.clear();
+    mprune_.clear();
+    mbase_.reset();
+    held_n_.store(0, std::memory_order_relaxed);
+    return;
+  }
+  enabled_ = true;
+  on_install(std::move(published), st);
+}
+
+// ---- one copy (the applier) ------------------------------------------------
+
+void FreshOverlay::State::Kids::insert(uint64_t k, uint32_t v) {
+  if (2 * (n + 1) > key.size()) {  // load <= 0.5
+    std::vector<uint64_t> ok(key.size() * 2, ~0ull);
+    std::vector<uint32_t> ov(key.size() * 2, 0);
+    ok.swap(key);
+    ov.swap(val);
+    n = 0;
+    for (size_t i = 0; i < ok.size(); i++)
+      if (ok[i] != ~0ull) insert(ok[i], ov[i]);
+  }
+  const uint64_t m = key.size() - 1;
+  uint64_t i = mix(k) & m;
+  while (key[i] != ~0ull) i = (i + 1) & m;
+  key[i] = k;
+  val[i] = v;
+  n++;
+}
+
+uint32_t FreshOverlay::State::find_token(std::string_view s) const {
+  auto it = tok_head_.find(fnv(s));
   if (it != tok_head_.end())
     for (uint32_t id = it->second; id != kNone; id = tok_next_[id])
       if (tok_str_[id] == s) return id;
-  if (!create) return kNone;
+  return kNone;
+}
+
+uint32_t FreshOverlay::State::token(std::string_view s, bool create) {
+  const uint32_t found = find_token(s);
+  if (found != kNone || !create) return found;
+  const uint64_t h = fnv(s);
+  auto it = tok_head_.find(h);
   const uint32_t id = (uint32_t)tok_str_.size();
   tok_str_.emplace_back(s);
   tok_next_.push_back(it != tok_head_.end() ? it->second : kNone);
@@ -32,14 +304,9 @@ uint32_t FreshOverlay::token(std::string_view s, bool create) {
   return id;
 }
 
-uint32_t FreshOverlay::child(uint32_t parent, uint32_t tok) const {
-  auto it = kids_.find((uint64_t)parent << 32 | tok);
-  return it == kids_.end() ? kNone : it->second;
-}
-
 // the node a filter's subscription is stored at: levels from d, as the store's
 // set_path / seek_path walk them (topics.go:380-414)
-uint32_t FreshOverlay::path(std::string_view filter, int d, bool create) {
+uint32_t FreshOverlay::State::path(std::string_view filter, int d, bool create) {
   uint32_t n = 0;
   for (bool has_next = true; has_next; d++) {
     std::string_view key;
@@ -51,14 +318,14 @@ uint32_t FreshOverlay::path(std::string_view filter, int d, bool create) {
       if (!create) return kNone;
       c = (uint32_t)nodes_.size();
       nodes_.emplace_back();
-      kids_[(uint64_t)n << 32 | tok] = c;
+      kids_.insert((uint64_t)n << 32 | tok, c);
     }
     n = c;
   }
   return n;
 }
 
-void FreshOverlay::put(uint32_t node, const Ent &e) {
+void FreshOverlay::State::put(uint32_t node, const Ent &e) {
   for (Ent &x : nodes_[node].ents)
     if (x.client == e.client && x.shared == e.shared && x.group == e.group) {
       x = e;  // (a re-subscription replaces the record: topics.go:390-396)
@@ -69,7 +336,19 @@ void FreshOverlay::put(uint32_t node, const Ent &e) {
   if (v.empty() || v.back() != node) v.push_back(node);
 }
 
-void FreshOverlay::drop(uint32_t node, uint32_t client, uint8_t shared, uint32_t group) {
+// a subscription as Subscribe stores it: shared ones (level 0 EqualFolds
+// "$SHARE") at levels >= 2 under group = level 1 (topics.go:306-318)
+void FreshOverlay::State::put_sub(uint32_t c, std::string_view filter, uint8_t shared, const SubInfo &si) {
+  if (shared) {
+    std::string_view g;
+    isolate_particle(filter, 1, &g);
+    put(path(filter, 2, true), Ent{c, token(g, true), 1, 0, si});
+  } else {
+    put(path(filter, 0, true), Ent{c, kNone, 0, dollar_skip(filter), si});
+  }
+}
+
+void FreshOverlay::State::drop(uint32_t node, uint32_t client, uint8_t shared, uint32_t group) {
   auto &es = nodes_[node].ents;
   for (size_t i = 0; i < es.size(); i++)
     if (es[i].client == client && es[i].shared == shared && es[i].group == group) {
@@ -78,133 +357,79 @@ void FreshOverlay::drop(uint32_t node, uint32_t client, uint8_t shared, uint32_t
     }
 }
 
-// a client's first mutation since the overlay last held it: its subscriptions
-// as the published snapshot has them (no mutation of it since: it would be held)
-void FreshOverlay::touch(const Store &st, uint32_t c) {
-  if (c >= last_mut_.size()) last_mut_.resize((size_t)c + 1 + last_mut_.size() / 2, 0);
-  if (last_mut_[c] != 0) return;
-  n_clients_++;
-  held_[c];  // (held from now on, even with no subscription)
-  const HostSnapshot &hs = *base_;
-  if ((size_t)c + 1 < hs.client_off.size())
-    for (uint32_t k = hs.client_off[c]; k < hs.client_off[c + 1]; k++) {
-      const SubInfo &si = hs.sub_info[hs.client_subs[k]];
-      const std::string_view f = st.filters().name(si.filter);
-      put(path(f, 0, true), Ent{c, kNone, 0, dollar_skip(f), si});
-    }
-  if ((size_t)c + 1 < hs.client_shoff.size())
-    for (uint32_t k = hs.client_shoff[c]; k < hs.client_shoff[c + 1]; k++) {
-      const SubInfo &si = hs.shared_info[hs.client_shared[k]];
-      const std::string_view f = st.filters().name(si.filter);
-      std::string_view g;
-      isolate_particle(f, 1, &g);
-      put(path(f, 2, true), Ent{c, token(g, true), 1, 0, si});
-    }
+void FreshOverlay::State::stamp(uint32_t c, uint64_t v) {
+  if (c >= last_mut_.size()) {
+    last_mut_.resize((size_t)c + 1 + last_mut_.size() / 2, 0);
+    held_bits_.resize((last_mut_.size() + 63) / 64, 0);
+  }
+  last_mut_[c] = v;
+  if (v)
+    held_bits_[c >> 6] |= 1ull << (c & 63);
+  else
+    held_bits_[c >> 6] &= ~(1ull << (c & 63));
 }
 
-void FreshOverlay::on_subscribe(const Store &st, std::string_view filter, const SubRec &rec) {
-  std::unique_lock<std::shared_mutex> w(rw_);
-  version_ = st.version();
-  if (!active_) return;
-  const Store::Footprint &fp = st.last_footprint();
-  touch(st, rec.client);
-  const SubInfo si{rec.filter, rec.client, rec.ident, rec.qos, rec.no_local, rec.rap, rec.rh};
-  if (fp.shared) {  // stored at levels >= 2 under group = level 1 (topics.go:306-318)
-    std::string_view g;
-    isolate_particle(filter, 1, &g);
-    put(path(filter, 2, true), Ent{rec.client, token(g, true), 1, 0, si});
-  } else {
-    put(path(filter, 0, true), Ent{rec.client, kNone, 0, dollar_skip(filter), si});
-  }
-  last_mut_[rec.client] = version_;
-}
-
-void FreshOverlay::on_unsubscribe(const Store &st, std::string_view filter) {
-  std::unique_lock<std::shared_mutex> w(rw_);
-  version_ = st.version();
-  if (!active_) return;
-  const Store::Footprint &fp = st.last_footprint();
-  if (fp.client == kNone) return;  // a client never seen: nothing of it changes
-  touch(st, fp.client);
-  // the node the store looked at: levels from 2 only for a case-sensitive
-  // "$SHARE" prefix (topics.go:330); the shared record dropped when level 0
-  // EqualFolds "$SHARE" (:337-341)
-  const int d = filter.substr(0, 6) == "$SHARE" ? 2 : 0;
-  const uint32_t n = path(filter, d, false);
-  if (n != kNone) {
-    if (fp.shared) {
-      std::string_view g;
-      isolate_particle(filter, 1, &g);
-      const uint32_t gt = token(g, false);
-      if (gt != kNone) drop(n, fp.client, 1, gt);
-    } else {
-      drop(n, fp.client, 0, kNone);
+void FreshOverlay::State::apply(const Op &op) {
+  version_ = op.version;
+  switch (op.kind) {
+    case Op::kReset:
+      *this = State();
+      version_ = op.version;
+      return;
+    case Op::kInstall:
+      floor_ = op.floor;
+      active_ = true;
+      return;
+    case Op::kVersion:
+      return;
+    case Op::kLoad:
+      held_[op.client];  // (held from now on, even with no subscription)
+      for (const Load &l : op.loads) put_sub(op.client, l.filter, l.shared, l.info);
+      stamp(op.client, op.version);
+      return;
+    case Op::kPut:
+      put_sub(op.client, op.filter, op.shared, op.info);
+      stamp(op.client, op.version);
+      return;
+    case Op::kDrop: {
+      // the node the store looked at: levels from 2 only for a case-sensitive
+      // "$SHARE" prefix (topics.go:330); the shared record dropped when level
+      // 0 EqualFolds "$SHARE" (:337-341)
+      const int d = std::string_view(op.filter).substr(0, 6) == "$SHARE" ? 2 : 0;
+      const uint32_t n = path(op.filter, d, false);
+      if (n != kNone) {
+        if (op.shared) {
+          std::string_view g;
+          isolate_particle(op.filter, 1, &g);
+          const uint32_t gt = find_token(g);
+          if (gt != kNone) drop(n, op.client, 1, gt);
+        } else {
+          drop(n, op.client, 0, kNone);
+        }
+      }
+      stamp(op.client, op.version);
+      return;
     }
-  }
-  last_mut_[fp.client] = version_;
-}
-
-void FreshOverlay::on_version(const Store &st) {
-  std::unique_lock<std::shared_mutex> w(rw_);
-  version_ = st.version();
-}
-
-void FreshOverlay::on_install(std::shared_ptr<const HostSnapshot> hs, const Store &st) {
-  std::unique_lock<std::shared_mutex> w(rw_);
-  version_ = st.version();
-  if (!hs || (hs->client_off.empty() && !hs->sub_info.empty()) ||
-      (hs->client_shoff.empty() && !hs->shared_info.empty())) {  // (no client index: nothing to start from)
-    active_ = false;
-    return;
-  }
-  // results on the snapshot published before this one are still corrected;
-  // the clients only older results would need are dropped
-  floor_ = active_ && base_ ? base_->version : hs->version;
-  for (auto it = held_.begin(); it != held_.end();) {
-    const uint32_t c = it->first;
-    if (last_mut_[c] > floor_) {
-      ++it;
-      continue;
-    }
-    for (uint32_t node : it->second) {
-      auto &es = nodes_[node].ents;
-      es.erase(std::remove_if(es.begin(), es.end(), [c](const Ent &e) { return e.client == c; }), es.end());
-    }
-    last_mut_[c] = 0;
-    n_clients_--;
-    it = held_.erase(it);
-  }
-  // the trie keeps every path it ever held: start over once it is mostly empty
-  size_t live = 0;
-  for (const auto &kv : held_) live += kv.second.size();
-  if (nodes_.size() > 4096 && nodes_.size() > 16 * (live + 64)) {
-    std::vector<Ent> keep;
-    for (const auto &kv : held_)
-      for (uint32_t node : kv.second)
-        for (const Ent &e : nodes_[node].ents)
-          if (e.client == kv.first) keep.push_back(e);
-    nodes_.assign(1, Node());
-    kids_.clear();
-    for (auto &kv : held_) kv.second.clear();
-    for (const Ent &e : keep) {
-      const std::string_view f = st.filters().name(e.info.filter);
-      put(e.shared ? path(f, 2, true) : path(f, 0, true), e);
+    case Op::kPrune: {
+      const uint32_t c = op.client;
+      auto it = held_.find(c);
+      if (it != held_.end()) {
+        for (uint32_t node : it->second) {
+          auto &es = nodes_[node].ents;
+          es.erase(std::remove_if(es.begin(), es.end(), [c](const Ent &e) { return e.client == c; }), es.end());
+        }
+        held_.erase(it);
+      }
+      stamp(c, 0);
+      return;
     }
   }
-  base_ = std::move(hs);
-  active_ = true;
 }
 
-int FreshOverlay::Reader::status(uint64_t vs) const {
-  if (!o_.active_) return 0;
-  if (vs < o_.floor_) return -1;
-  return o_.version_ > vs ? 1 : 0;
-}
-
-void FreshOverlay::gather(uint32_t node, std::string_view topic, uint64_t vs, bool with_shared, Match *m,
-                          std::unordered_map<uint32_t, uint32_t> *row_of) const {
+void FreshOverlay::State::gather(uint32_t node, std::string_view topic, uint64_t vs, bool with_shared, Match *m,
+                                 std::unordered_map<uint32_t, uint32_t> *row_of) const {
   for (const Ent &e : nodes_[node].ents) {
-    if (!(e.client < last_mut_.size() && last_mut_[e.client] > vs)) continue;  // its snapshot rows stand
+    if (!touched(e.client, vs)) continue;  // its snapshot rows stand
     if (e.shared) {  // gatherSharedSubscriptions (topics.go:541-555): no "$" rule
       if (with_shared) m->shared.push_back(e.info);
       continue;
@@ -224,42 +449,44 @@ void FreshOverlay::gather(uint32_t node, std::string_view topic, uint64_t vs, bo
 }
 
 // scanSubscribers (topics.go:493-518), restated: the slice {key, "+", "#"} per
-// level, gather at every visited node, the parent-"#" probe after a literal
-void FreshOverlay::scan(std::string_view topic, int d, uint32_t node, uint64_t vs, Match *m,
-                        std::unordered_map<uint32_t, uint32_t> *row_of) const {
-  std::string_view key;
-  const bool has_next = isolate_particle(topic, d, &key);
-  const std::string_view keys[3] = {key, "+", "#"};
+// level, gather at every visited node, the parent-"#" probe after a literal.
+// lt[d]: level d's token (kNone: no overlay filter has it)
+void FreshOverlay::State::scan(std::string_view topic, const uint32_t *lt, int nl, int d, uint32_t node, uint64_t vs,
+                               Match *m, std::unordered_map<uint32_t, uint32_t> *row_of) const {
+  const bool has_next = d + 1 < nl;
+  const uint32_t keys[3] = {lt[d], plus_tok_ >= 0 ? (uint32_t)plus_tok_ : kNone,
+                            hash_tok_ >= 0 ? (uint32_t)hash_tok_ : kNone};
   for (int k = 0; k < 3; k++) {
-    uint32_t tok = kNone;
-    const uint64_t h = fnv(keys[k]);
-    auto it = tok_head_.find(h);
-    if (it != tok_head_.end())
-      for (uint32_t id = it->second; id != kNone; id = tok_next_[id])
-        if (tok_str_[id] == keys[k]) {
-          tok = id;
-          break;
-        }
-    if (tok == kNone) continue;
-    const uint32_t p = child(node, tok);
+    if (keys[k] == kNone) continue;
+    const uint32_t p = child(node, keys[k]);
     if (p == kNone) continue;
     gather(p, topic, vs, true, m, row_of);
-    if (keys[k] != "#" && keys[k] != "+" && hash_tok_ >= 0) {
+    const bool literal = keys[k] != (uint32_t)plus_tok_ && keys[k] != (uint32_t)hash_tok_;
+    if (literal && hash_tok_ >= 0) {
       const uint32_t wc = child(p, (uint32_t)hash_tok_);
       if (wc != kNone) gather(wc, topic, vs, false, m, row_of);
     }
-    if (has_next) scan(topic, d + 1, p, vs, m, row_of);
+    if (has_next) scan(topic, lt, nl, d + 1, p, vs, m, row_of);
   }
 }
 
-void FreshOverlay::Reader::match(std::string_view topic, uint64_t vs, Match *out) const {
-  out->version = o_.version_;
+void FreshOverlay::State::match(std::string_view topic, uint64_t vs, Match *out) const {
+  out->version = version_;
   out->rows.clear();
   out->subs.clear();
   out->shared.clear();
   if (topic.empty()) return;  // (topics.go:498)
-  std::unordered_map<uint32_t, uint32_t> row_of;
-  o_.scan(topic, 0, 0, vs, out, &row_of);
+  // the topic's levels as overlay tokens, once (isolateParticle, topics.go:558-577)
+  thread_local std::vector<uint32_t> lt;
+  lt.clear();
+  for (bool has_next = true; has_next;) {
+    std::string_view key;
+    has_next = isolate_particle(topic, (int)lt.size(), &key);
+    lt.push_back(find_token(key));
+  }
+  thread_local std::unordered_map<uint32_t, uint32_t> row_of;  // (its buckets kept from call to call)
+  row_of.clear();
+  scan(topic, lt.data(), (int)lt.size(), 0, 0, vs, out, &row_of);
 }
 
 }  // namespace mqm

@@ -22,14 +22,17 @@
  *         (ASYNC_COMMIT | IDENTIFIERS | SERVE, rebuilt in the background by
  *         mqm_commit_policy(64 ops, 2 ms): calls match the newest published
  *         snapshot) or "fresh" (async + MQM_CFG_FRESH: calls return the
- *         store's current subscriptions, read-your-writes checked)
+ *         store's current subscriptions less at most the last millisecond of
+ *         mutations under load; the test checks that bound from the times)
  *   OP_US: microseconds the mutator sleeps between operations
- *   OUT : "B version" (after the base subscriptions), "V j version" after
- *         operation j, then per call "C thread call topic version" followed by
+ *   OUT : "B version" (after the base subscriptions), "V j version us" after
+ *         operation j (us: microseconds since the start, after the call
+ *         returned), then per call "C thread call topic version us" (us: when
+ *         the call started) followed by
  *         that result's rendered lines (shim_harness.c's format:
  *         "D t client qos nl filter ident rap rh f1=i1,..." / "H t filter client")
  * Reader thread r makes CALLS calls on topics (r * 7919 + c * 104729) mod
- * n_topics.  A reader in "autocommit" or "fresh" mode also checks read-your-writes: the
+ * n_topics.  A reader in "autocommit" mode also checks read-your-writes: the
  * version of a result is at least the store version it read before the call.
  * Exit status 0 when every call returned MQM_OK and every check held.
  */
@@ -165,6 +168,13 @@ static void render(Buf *b, mqm_result *r, uint32_t t) {
   }
 }
 
+static struct timespec t_start;
+static uint64_t now_us(void) {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (uint64_t)(t.tv_sec - t_start.tv_sec) * 1000000u + (uint64_t)((t.tv_nsec - t_start.tv_nsec) / 1000);
+}
+
 static uint64_t store_version(void) {
   mqm_commit_state st;
   if (mqm_commit_state_get(H, &st) != MQM_OK) fail("mqm_commit_state_get");
@@ -176,7 +186,8 @@ static void *reader(void *arg) {
   Buf *b = &out_of[id];
   for (uint32_t c = 0; c < n_calls; c++) {
     const uint32_t t = (uint32_t)(((uint64_t)id * 7919u + (uint64_t)c * 104729u) % n_topics);
-    const uint64_t before = autocommit || fresh ? store_version() : 0;
+    const uint64_t t_call = now_us();
+    const uint64_t before = autocommit ? store_version() : 0;
     mqm_result *r = NULL;
     if (mqm_subscribers(H, topics[t], topic_len[t], &r) != MQM_OK || mqm_result_num_topics(r) != 1) {
       fail("mqm_subscribers");
@@ -184,13 +195,13 @@ static void *reader(void *arg) {
       continue;
     }
     const uint64_t v = mqm_result_snapshot_version(r);
-    if ((autocommit || fresh) && v < before) {
+    if (autocommit && v < before) {
       char msg[128];
       snprintf(msg, sizeof msg, "read-your-writes: result version %llu < store version %llu before the call",
                (unsigned long long)v, (unsigned long long)before);
       fail(msg);
     }
-    buf_fmt(b, "C %d %u %u %llu\n", id, c, t, (unsigned long long)v);
+    buf_fmt(b, "C %d %u %u %llu %llu\n", id, c, t, (unsigned long long)v, (unsigned long long)t_call);
     render(b, r, t);
     mqm_result_free(r);
   }
@@ -216,7 +227,7 @@ static void *mutator(void *arg) {
                  ? mqm_subscribe(H, ops[j].a, strlen(ops[j].a), ops[j].b, strlen(ops[j].b), &ops[j].sub, &x)
                  : mqm_unsubscribe(H, ops[j].a, strlen(ops[j].a), ops[j].b, strlen(ops[j].b), &x);
     if (rc != MQM_OK) fail("mutation");
-    buf_fmt(&mut_out, "V %u %llu\n", j, (unsigned long long)store_version());
+    buf_fmt(&mut_out, "V %u %llu %llu\n", j, (unsigned long long)store_version(), (unsigned long long)now_us());
     if (op_us) {
       struct timespec ts = {op_us / 1000000u, (long)(op_us % 1000000u) * 1000L};
       nanosleep(&ts, NULL);
@@ -304,6 +315,7 @@ int main(int argc, char **argv) {
   }
   free(line);
   out_of = calloc((size_t)n_threads, sizeof(Buf));
+  clock_gettime(CLOCK_MONOTONIC, &t_start);
   pthread_t th[128], mt;
   pthread_create(&mt, NULL, mutator, NULL);
   for (int i = 0; i < n_threads; i++) pthread_create(&th[i], NULL, reader, (void *)(intptr_t)i);

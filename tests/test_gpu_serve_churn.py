@@ -92,12 +92,12 @@ def _parse(path):
             elif tag == "S":
                 served = tuple(int(x) for x in ln.split()[1:])
             elif tag == "V":
-                _, j, v = ln.split()
-                op_version[int(j)] = int(v)
+                _, j, v, us = ln.split()
+                op_version[int(j)] = (int(v), int(us))
             elif tag == "C":
-                _, th, c, t, v = ln.split()
+                _, th, c, t, v, us = ln.split()
                 cur = (int(th), int(c))
-                calls[cur] = (int(t), int(v), [])
+                calls[cur] = (int(t), int(v), [], int(us))
             else:
                 calls[cur][2].append(ln)
     return base_version, served, op_version, calls
@@ -158,9 +158,25 @@ def test_served_calls_under_churn_equal_oracle_at_their_version(tmp_path, mode, 
     # that store version: an Unsubscribe that found nothing changes nothing)
     prefix = {base_version: 0}
     for j in sorted(op_version):
-        prefix[op_version[j]] = j + 1
+        prefix[op_version[j][0]] = j + 1
+    if mode == "fresh":
+        # every mutation that returned 2 ms (the overlay's 1-ms batching bound +
+        # slack) before a call started is in its result
+        import bisect
+        times = [op_version[j][1] for j in sorted(op_version)]
+        vers = [op_version[j][0] for j in sorted(op_version)]
+        late, exact = [], 0
+        for key, (t, v, lines, us) in calls_out.items():
+            k = bisect.bisect_right(times, us - 2000)
+            need = max(vers[:k], default=base_version)
+            if v < need:
+                late.append((key, v, need))
+            k2 = bisect.bisect_right(times, us)
+            exact += v >= max(vers[:k2], default=base_version)
+        print(f"fresh: {exact} of {len(calls_out)} results held every mutation returned before the call")
+        assert not late, late[:5]
     by_version = defaultdict(list)
-    for key, (t, v, lines) in calls_out.items():
+    for key, (t, v, lines, _) in calls_out.items():
         assert v in prefix, f"result version {v} is no state the mutator produced"
         by_version[v].append(key)
     versions = sorted(by_version)
@@ -181,7 +197,7 @@ def test_served_calls_under_churn_equal_oracle_at_their_version(tmp_path, mode, 
         keys = by_version[v]
         want = _render_oracle(ora, sorted({calls_out[k][0] for k in keys}), topics)
         for k in keys:
-            t, _, lines = calls_out[k]
+            t, _, lines, _ = calls_out[k]
             if sorted(lines) != want[t]:
                 bad.append((k, v, t))
     ora.close()
