@@ -43,6 +43,12 @@ uint64_t last_write(const void *o) {
 
 // ---- lifecycle, the applier ------------------------------------------------
 
+int FreshOverlay::slot() {
+  static std::atomic<int> next{0};
+  thread_local const int k = next.fetch_add(1, std::memory_order_relaxed) % kSlots;
+  return k;
+}
+
 FreshOverlay::FreshOverlay() { th_ = std::thread([this] { run(); }); }
 
 FreshOverlay::~FreshOverlay() {
@@ -82,7 +88,7 @@ void FreshOverlay::round(std::vector<Op> &batch) {
   const int c = cur_.load(std::memory_order_seq_cst), o = 1 - c;
   // the calls that entered the other copy before it stopped being current (a
   // caller preempted inside it: yield rather than spin a timeslice away)
-  for (uint32_t spin = 0; readers_[o].n.load(std::memory_order_seq_cst) != 0; spin++) {
+  for (uint32_t spin = 0; !drained(o); spin++) {
     if (spin < 2048)
       __builtin_ia32_pause();
     else
@@ -319,6 +325,8 @@ uint32_t FreshOverlay::State::path(std::string_view filter, int d, bool create) 
       c = (uint32_t)nodes_.size();
       nodes_.emplace_back();
       kids_.insert((uint64_t)n << 32 | tok, c);
+      if ((int32_t)tok == plus_tok_) nodes_[n].plus = c;
+      if ((int32_t)tok == hash_tok_) nodes_[n].hash = c;
     }
     n = c;
   }
@@ -454,18 +462,22 @@ void FreshOverlay::State::gather(uint32_t node, std::string_view topic, uint64_t
 void FreshOverlay::State::scan(std::string_view topic, const uint32_t *lt, int nl, int d, uint32_t node, uint64_t vs,
                                Match *m, std::unordered_map<uint32_t, uint32_t> *row_of) const {
   const bool has_next = d + 1 < nl;
-  const uint32_t keys[3] = {lt[d], plus_tok_ >= 0 ? (uint32_t)plus_tok_ : kNone,
-                            hash_tok_ >= 0 ? (uint32_t)hash_tok_ : kNone};
+  const Node &nd = nodes_[node];
+  // the key's child by the table (a key that is "+" or "#" itself: the
+  // node's wildcard child, as the reference's map lookup would find), then
+  // the '+' and '#' children from the node
+  const uint32_t key = lt[d];
+  const uint32_t kids[3] = {key == kNone ? kNone
+                            : (int32_t)key == plus_tok_ ? nd.plus
+                            : (int32_t)key == hash_tok_ ? nd.hash
+                                                        : child(node, key),
+                            nd.plus, nd.hash};
   for (int k = 0; k < 3; k++) {
-    if (keys[k] == kNone) continue;
-    const uint32_t p = child(node, keys[k]);
+    const uint32_t p = kids[k];
     if (p == kNone) continue;
     gather(p, topic, vs, true, m, row_of);
-    const bool literal = keys[k] != (uint32_t)plus_tok_ && keys[k] != (uint32_t)hash_tok_;
-    if (literal && hash_tok_ >= 0) {
-      const uint32_t wc = child(p, (uint32_t)hash_tok_);
-      if (wc != kNone) gather(wc, topic, vs, false, m, row_of);
-    }
+    const bool literal = k == 0 && (int32_t)key != plus_tok_ && (int32_t)key != hash_tok_;
+    if (literal && nodes_[p].hash != kNone) gather(nodes_[p].hash, topic, vs, false, m, row_of);
     if (has_next) scan(topic, lt, nl, d + 1, p, vs, m, row_of);
   }
 }

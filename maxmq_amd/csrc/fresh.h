@@ -160,6 +160,7 @@ class FreshOverlay {
     };
     struct Node {
       std::vector<Ent> ents;
+      uint32_t plus = kNone, hash = kNone;  // the '+' / '#' child (no table probe for them)
     };
     // (parent << 32 | token) -> child: open addressing, insert-only
     struct Kids {
@@ -231,10 +232,19 @@ class FreshOverlay {
   // the two copies
   State s_[2];
   std::atomic<int> cur_{0};
+  // calls inside each copy, counted in per-thread slots (64 callers on one
+  // counter made its cache line the hot spot)
+  static constexpr int kSlots = 16;
   struct alignas(64) Count {
     std::atomic<int> n{0};
   };
-  mutable Count readers_[2];
+  mutable Count readers_[2][kSlots];
+  static int slot();
+  bool drained(int copy) const {
+    for (int k = 0; k < kSlots; k++)
+      if (readers_[copy][k].n.load(std::memory_order_seq_cst) != 0) return false;
+    return true;
+  }
   std::atomic<uint64_t> ops_{0}, rounds_{0};
   mutable std::atomic<uint64_t> corrected_{0}, read_ns_{0};
   std::thread th_;
@@ -242,15 +252,15 @@ class FreshOverlay {
  public:
   class Reader {
    public:
-    explicit Reader(const FreshOverlay &o) : o_(o) {
+    explicit Reader(const FreshOverlay &o) : o_(o), k_(slot()) {
       for (;;) {  // (left-right: enter the current copy, then check it still is)
         i_ = o.cur_.load(std::memory_order_seq_cst);
-        o.readers_[i_].n.fetch_add(1, std::memory_order_seq_cst);
+        o.readers_[i_][k_].n.fetch_add(1, std::memory_order_seq_cst);
         if (o.cur_.load(std::memory_order_seq_cst) == i_) break;
-        o.readers_[i_].n.fetch_sub(1, std::memory_order_seq_cst);
+        o.readers_[i_][k_].n.fetch_sub(1, std::memory_order_seq_cst);
       }
     }
-    ~Reader() { o_.readers_[i_].n.fetch_sub(1, std::memory_order_release); }
+    ~Reader() { o_.readers_[i_][k_].n.fetch_sub(1, std::memory_order_release); }
     Reader(const Reader &) = delete;
     Reader &operator=(const Reader &) = delete;
     // 0: nothing newer than vs (or no overlay), 1: correct the result, -1: vs
@@ -261,7 +271,7 @@ class FreshOverlay {
 
    private:
     const FreshOverlay &o_;
-    int i_ = 0;
+    int k_, i_ = 0;
   };
 };
 
