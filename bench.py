@@ -84,6 +84,9 @@ def parse():
                     help="host path: concurrent callers (each its own stream), batches overlapped across them "
                          "(4: the best of 4 / 8 / 12 / 16 measured, r06i / r06j — more callers queue more copies "
                          "behind each other's and their kernels behind them)")
+    ap.add_argument("--sort-topics", action="store_true",
+                    help="(diagnostic, not a bench line) the device batch reordered by its first 8 bytes: how much "
+                         "of the walk is prefix locality (with MQM_WALK_XCD=1: one XCD per eighth of the batch)")
     ap.add_argument("--pipeline", type=int, default=2,
                     help="timed steps through the queued device API on this many contexts / streams (a step "
                          "submits its batch and waits for the one submitted that many steps earlier; every "
@@ -270,8 +273,14 @@ def main():
     snap = idx.snapshot_stats()
     log(f"[rank {rank}] index built in {time.time() - t0:.1f}s: {snap}")
 
-    tb = torch.from_numpy(w.topics.data).to(dev)
-    to = torch.from_numpy(w.topics.offs.view(np.int64)).to(dev)
+    if args.sort_topics:
+        sdata, soffs = _sorted_by_prefix(w.topics.data, w.topics.offs)
+        tb = torch.from_numpy(sdata).to(dev)
+        to = torch.from_numpy(soffs.view(np.int64)).to(dev)
+        log(f"[rank {rank}] device batch sorted by its first 8 bytes (diagnostic)")
+    else:
+        tb = torch.from_numpy(w.topics.data).to(dev)
+        to = torch.from_numpy(w.topics.offs.view(np.int64)).to(dev)
     stream = torch.cuda.current_stream(dev)
     chunk = n
     if sharded and args.gather == "host":
@@ -616,6 +625,25 @@ def steady_state(idx, tb, to, n, dev, args):
             "requeued_batches": requeued,
             "note": "mqm_match_device_async on 2 contexts / 2 streams, host waits only for the batch queued two "
                     "steps earlier; no read-back inside a batch (outputs sized by the contexts' first batch)"}
+
+
+def _sorted_by_prefix(data, offs):
+    """(--sort-topics) the batch reordered by the big-endian key of each
+    topic's first 8 bytes (zero past its end), stable"""
+    o = offs.astype(np.int64)
+    lens = np.diff(o)
+    pad = np.concatenate([data, np.zeros(8, np.uint8)])
+    key = np.zeros(len(lens), np.uint64)
+    for k in range(8):
+        b = pad[o[:-1] + k].astype(np.uint64)
+        b[lens <= k] = 0
+        key |= b << np.uint64(56 - 8 * k)
+    perm = np.argsort(key, kind="stable")
+    lp = lens[perm]
+    no = np.zeros(len(lens) + 1, np.int64)
+    np.cumsum(lp, out=no[1:])
+    src = np.repeat(o[:-1][perm] - no[:-1], lp) + np.arange(no[-1], dtype=np.int64)
+    return np.ascontiguousarray(data[src]), no.astype(np.uint64)
 
 
 def host_path(idx, w, args, form="runs"):

@@ -33,6 +33,9 @@
 #   hostthreads: the host-path legs on 4 / 12 / 16 caller threads
 #   kcopyt  : the runs-form tests, kernel copy-out parity included
 #   freshtest: the MQM_CFG_FRESH tests (every mutation visible at once) + the served / churn tests
+#   xcdab   : `fast` with / without the XCD-affine walk parts (MQM_WALK_XCD=1), on the batch as generated and sorted
+#   xcdpar  : parity + queued tests with the XCD-affine walk
+#   sortab  : `fast` with the walk in prefix order (default), in batch order (MQM_WALK_SORT=0), in prefix order again
 #   c2      : the C2 bench line (1M filters, 10M topics) with roofline and CPU baseline -> bench_c2.json
 #   c4fast  : the C4 shard bench without CPU baseline
 #   pipe    : `fast` with pipelined steps on 2 and 3 contexts -> bench_fast_pipe{2,3}.json
@@ -170,6 +173,18 @@ for step in "$@"; do
     kcopyt) timeout -k 10 400 $PYT tests/test_gpu_runs.py -m gpu --timeout 200 > $OUT/pytest_kcopy.log 2>&1 ;;
     freshtest) timeout -k 10 600 $PYT -s tests/test_gpu_fresh.py tests/test_gpu_serve_churn.py tests/test_gpu_serve.py -m gpu \
              --timeout 300 > $OUT/pytest_fresh.log 2>&1 ;;
+    xcdab) for V in base:X=0 xcd:MQM_WALK_XCD=1; do
+          N=${V%%:*}; E=${V#*:}
+          env $E timeout -k 10 400 python3 -u bench.py $FAST --ident-steps 0 > $OUT/bench_fast_$N.json 2> $OUT/bench_fast_$N.log || exit 1
+          env $E timeout -k 10 400 python3 -u bench.py $FAST --ident-steps 0 --sort-topics > $OUT/bench_fast_sorted_$N.json \
+            2> $OUT/bench_fast_sorted_$N.log || exit 1
+        done ;;
+    xcdpar) MQM_WALK_XCD=1 timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_gpu_queued.py -m gpu --timeout 300 \
+             > $OUT/pytest_xcd.log 2>&1 ;;
+    sortab) for V in sorted:X=0 batch:MQM_WALK_SORT=0 sorted2:X=0; do
+          N=${V%%:*}; E=${V#*:}
+          env $E timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_$N.json 2> $OUT/bench_fast_$N.log || exit 1
+        done ;;
     c2) timeout -k 10 600 python3 -u bench.py --config 2 --steps 10 --warmup 3 --host-topics 0 --latency-topics 0 \
              --steady-steps 0 --cpu-seconds 10 > $OUT/bench_c2.json 2> $OUT/bench_c2.log ;;
     c4fast) timeout -k 10 600 python3 -u bench.py --config 4 --shard 0/8 $FAST > $OUT/bench_c4_fast.json 2> $OUT/bench_c4_fast.log ;;
