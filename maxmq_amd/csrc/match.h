@@ -128,10 +128,11 @@ struct Workspace {
     prof_walk_ms = prof_dedupe_ms = prof_total_ms = 0;
   }
 
-  // Buffers are stream-ordered allocations (hipMallocAsync / hipFreeAsync on
-  // `cur`), so growing one never waits for other streams (a background
-  // snapshot upload, another index's matches): only for this workspace's own
-  // queued work (`cur`) and its previous calls (`last_use`).
+  // Buffers are hipMalloc'd and grown by replacement: the old one is retired
+  // through the reaper (retire_device_buffers) after this workspace's own
+  // queued work (`cur`) and its previous calls (`last_use`) — never freed
+  // under a running kernel, and no stream-ordered pool memory (its reuse
+  // served stale data: DESIGN §9, round 6).
   hipStream_t cur = nullptr;     // stream of the call in progress (begin())
   hipEvent_t last_use = nullptr; // recorded by end() after every call's work
   bool used = false;
