@@ -1197,8 +1197,10 @@ def serve_churn(idx, w, args):
         legs[name] = run(args.serve_churn_s, args.churn_rate)
         if fresh:
             f1 = idx.fresh_stats()
-            fs = {k: f1[k] - f0[k] if k != "held_clients" else f1[k] for k in f1}
+            fs = {k: f1[k] - f0[k] if k not in ("held_clients", "max_batch_age_ns", "max_round_ns",
+                                                 "max_copy_wait_ns") else f1[k] for k in f1}
             fs["read_us_per_corrected_call"] = fs["read_ns"] / max(1, fs["calls_corrected"]) / 1e3
+            fs["scan_us_per_corrected_call"] = fs["scan_ns"] / max(1, fs["calls_corrected"]) / 1e3
             legs[name]["fresh"] = fs
         log(f"[serve churn] {name}: {legs[name]}")
     if fresh_on:

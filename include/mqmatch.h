@@ -312,8 +312,11 @@ int mqm_serve_policy(mqm_index *h, uint32_t grid, uint32_t idle_us);
 /* MQM_CFG_FRESH indexes: correct_calls = 0 makes mqm_subscribers return the
  * snapshot's view again and drops the overlay (mutations cost nothing extra;
  * A/B and measurement), 1 starts it again from the published snapshot.
- * Statistics (out[5]): clients held, overlay operations applied (per copy), applier rounds,
- * calls corrected, nanoseconds spent in the corrections' read sections.
+ * Statistics (out[9]): clients held, overlay operations applied, applier
+ * rounds, calls corrected, nanoseconds spent in the corrections' read
+ * sections, the part of them in the overlay's scan, then the largest age of a
+ * batch when the applier took it, the longest round and the longest wait for
+ * a copy no call was in (ns).
  * MQM_EINVAL on an index created without the flag. */
 int mqm_fresh_policy(mqm_index *h, int correct_calls);
 int mqm_fresh_stats(mqm_index *h, uint64_t *out);

@@ -260,10 +260,11 @@ class TopicsIndex:
         """the fresh overlay: clients held (touched since the previous
         snapshot), mutations applied per copy, flushes, calls corrected and
         the time in their read sections"""
-        v = (C.c_uint64 * 5)()
+        v = (C.c_uint64 * 9)()
         check("mqm_fresh_stats", lib().mqm_fresh_stats(self._h, C.byref(v)))
         return {"held_clients": v[0], "ops_applied": v[1], "rounds": v[2], "calls_corrected": v[3],
-                "read_ns": v[4]}
+                "read_ns": v[4], "scan_ns": v[5], "max_batch_age_ns": v[6], "max_round_ns": v[7],
+                "max_copy_wait_ns": v[8]}
 
     def batching_policy(self, max_batch: int = 0, linger_us: int = 0):
         check("mqm_batching_policy", lib().mqm_batching_policy(self._h, max_batch, linger_us))

@@ -221,7 +221,7 @@ def lib():
         "mqm_serve_stats": ([vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)], C.c_int),
         "mqm_serve_counters_get": ([vp, C.POINTER(u64 * 8)], C.c_int),
         "mqm_fresh_policy": ([vp, C.c_int], C.c_int),
-        "mqm_fresh_stats": ([vp, C.POINTER(C.c_uint64 * 5)], C.c_int),
+        "mqm_fresh_stats": ([vp, C.POINTER(C.c_uint64 * 9)], C.c_int),
         "mqm_debug_stamp_counts": ([C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)], C.c_int),
         "mqm_batch_host_us": ([vp, C.POINTER(C.c_double)], C.c_int),
         "mqm_serve_device_us": ([vp, vp], C.c_int),

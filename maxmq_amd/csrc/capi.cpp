@@ -2172,6 +2172,7 @@ static int freshen(mqm_index *h, std::string_view topic, mqm_result **res) {
     const int st = rd.status(vs);
     if (st <= 0) return st < 0 ? 1 : MQM_OK;
     rd.match(topic, vs, &m);
+    h->fresh->count_match((uint64_t)(steady_ns() - t_read));
     if (base + m.subs.size() > MQM_DELIVERY_SUB(~0u) + 1ull || sbase + m.shared.size() > MQM_DELIVERY_SUB(~0u) + 1ull)
       return MQM_ELIMIT;
     // the snapshot's rows of clients nobody touched since it, then the touched
@@ -2284,6 +2285,10 @@ int mqm_fresh_stats(mqm_index *h, uint64_t *out) {
   out[2] = s.rounds;
   out[3] = s.corrected;
   out[4] = s.read_ns;
+  out[5] = s.match_ns;
+  out[6] = s.max_age_ns;
+  out[7] = s.max_round_ns;
+  out[8] = s.max_wait_ns;
   return MQM_OK;
 }
 

@@ -67,41 +67,70 @@ void FreshOverlay::run() {
     qcv_.wait(lk, [&] { return stop_ || !q_.empty(); });
     if (stop_) return;
     // let a batch gather for up to kApplyNs after its first operation
-    const auto due = std::chrono::steady_clock::time_point(std::chrono::nanoseconds(oldest_ns_ + kApplyNs));
+    const int64_t t0 = oldest_ns_.load(std::memory_order_relaxed);
+    const auto due = std::chrono::steady_clock::time_point(std::chrono::nanoseconds((t0 ? t0 : now_ns()) + kApplyNs));
     qcv_.wait_until(lk, due, [&] { return stop_ || urgent_ || q_.size() >= kBatch; });
     if (stop_) return;
-    std::vector<Op> batch;
-    batch.swap(q_);
-    urgent_ = false;
-    oldest_ns_ = 0;
     lk.unlock();
-    round(batch);
+    {
+      std::lock_guard<std::mutex> r(round_mu_);
+      std::vector<Op> batch;
+      int64_t age = 0;
+      {
+        std::lock_guard<std::mutex> g(qmu_);
+        batch.swap(q_);
+        urgent_ = false;
+        const int64_t t = oldest_ns_.exchange(0, std::memory_order_acq_rel);
+        age = t ? now_ns() - t : 0;
+      }
+      if ((uint64_t)age > max_age_ns_.load(std::memory_order_relaxed)) max_age_ns_.store(age, std::memory_order_relaxed);
+      const int64_t r0 = now_ns();
+      round(batch);
+      const uint64_t rd = (uint64_t)(now_ns() - r0);
+      if (rd > max_round_ns_.load(std::memory_order_relaxed)) max_round_ns_.store(rd, std::memory_order_relaxed);
+    }
     lk.lock();
     done_cv_.notify_all();
   }
 }
 
-// one left-right round: the batch (and the previous one) into the copy no call
-// reads, then that copy becomes the current one
+// one round: the batch appended to the log; the least up-to-date copy no call
+// is in (not the current one: the copies take turns, so the log stays short)
+// brought up to the log's end and made current; the log trimmed to the least
+// up-to-date copy
 void FreshOverlay::round(std::vector<Op> &batch) {
   if (batch.empty()) return;
-  const int c = cur_.load(std::memory_order_seq_cst), o = 1 - c;
-  // the calls that entered the other copy before it stopped being current (a
-  // caller preempted inside it: yield rather than spin a timeslice away)
-  for (uint32_t spin = 0; !drained(o); spin++) {
+  for (Op &op : batch) log_.push_back(std::move(op));
+  const uint64_t end = log_base_ + log_.size();
+  const int c = cur_.load(std::memory_order_seq_cst);
+  int t = -1;
+  const int64_t w0 = now_ns();
+  // (a caller preempted inside a copy: take another; all busy, yield)
+  for (uint32_t spin = 0; t < 0; spin++) {
+    for (int k = 0; k < kCopies; k++)
+      if (k != c && drained(k) && (t < 0 || pos_[k] < pos_[t])) t = k;
+    if (t >= 0) break;
     if (spin < 2048)
       __builtin_ia32_pause();
     else
       std::this_thread::yield();
   }
-  State &x = s_[o];
-  for (const Op &op : lag_) x.apply(op);
-  for (const Op &op : batch) x.apply(op);
-  cur_.store(o, std::memory_order_seq_cst);
-  applied_.store(batch.back().version, std::memory_order_release);
-  ops_.fetch_add(lag_.size() + batch.size(), std::memory_order_relaxed);
+  const uint64_t wt = (uint64_t)(now_ns() - w0);
+  if (wt > max_wait_ns_.load(std::memory_order_relaxed)) max_wait_ns_.store(wt, std::memory_order_relaxed);
+  State &x = s_[t];
+  for (uint64_t i = pos_[t]; i < end; i++) x.apply(log_[i - log_base_]);
+  ops_.fetch_add(end - pos_[t], std::memory_order_relaxed);
+  pos_[t] = end;
+  cur_.store(t, std::memory_order_seq_cst);
+  applied_.store(log_.back().version, std::memory_order_release);
   rounds_.fetch_add(1, std::memory_order_relaxed);
-  lag_.swap(batch);
+  uint64_t lo = end;
+  for (int k = 0; k < kCopies; k++) lo = std::min(lo, pos_[k]);
+  if (lo > log_base_) {
+    log_.erase(log_.begin(), log_.begin() + (std::ptrdiff_t)(lo - log_base_));
+    log_base_ = lo;
+  }
+  batch.clear();
 }
 
 void FreshOverlay::await_own_writes() {
@@ -123,7 +152,7 @@ void FreshOverlay::enqueue(Op &&op) {
   {
     std::lock_guard<std::mutex> g(qmu_);
     if (q_.empty()) {
-      oldest_ns_ = now_ns();
+      oldest_ns_.store(now_ns(), std::memory_order_release);
       wake = true;
     }
     q_.push_back(std::move(op));
@@ -243,6 +272,12 @@ void FreshOverlay::on_install(std::shared_ptr<const HostSnapshot> hs, const Stor
   mprune_.clear();
   for (const auto &kv : mirror_)
     if (kv.second <= mfloor_) mprune_.push_back(kv.first);
+  // (the copies' per-client arrays sized for the snapshot's clients and a
+  // quarter more: grown inside a round they cost that round its zeroing and
+  // copy — a 306-ms round, r06af)
+  const uint64_t nc = std::max<uint64_t>(hs->client_off.size(), hs->client_shoff.size());
+  op.client = (uint32_t)std::min<uint64_t>(nc + nc / 4 + 1024, 0xFFFFFFF0u);
+  op.nodes_hint = hs->nodes.size();
   mbase_ = std::move(hs);
   mactive_ = true;
   op.kind = Op::kInstall;
@@ -269,6 +304,19 @@ void FreshOverlay::set_enabled(bool on, std::shared_ptr<const HostSnapshot> publ
 }
 
 // ---- one copy (the applier) ------------------------------------------------
+
+void FreshOverlay::State::Kids::reserve(uint64_t slots) {
+  if (slots <= key.size()) return;
+  uint64_t sz = key.size();
+  while (sz < slots) sz *= 2;
+  std::vector<uint64_t> ok(sz, ~0ull);
+  std::vector<uint32_t> ov(sz, 0);
+  ok.swap(key);
+  ov.swap(val);
+  n = 0;
+  for (size_t i = 0; i < ok.size(); i++)
+    if (ok[i] != ~0ull) insert(ok[i], ov[i]);
+}
 
 void FreshOverlay::State::Kids::insert(uint64_t k, uint32_t v) {
   if (2 * (n + 1) > key.size()) {  // load <= 0.5
@@ -366,8 +414,8 @@ void FreshOverlay::State::drop(uint32_t node, uint32_t client, uint8_t shared, u
 }
 
 void FreshOverlay::State::stamp(uint32_t c, uint64_t v) {
-  if (c >= last_mut_.size()) {
-    last_mut_.resize((size_t)c + 1 + last_mut_.size() / 2, 0);
+  if (c >= last_mut_.size()) {  // (clients new since the snapshot: doubled, so rarely)
+    last_mut_.resize(std::max<size_t>((size_t)c + 1, 2 * last_mut_.size()), 0);
     held_bits_.resize((last_mut_.size() + 63) / 64, 0);
   }
   last_mut_[c] = v;
@@ -387,6 +435,19 @@ void FreshOverlay::State::apply(const Op &op) {
     case Op::kInstall:
       floor_ = op.floor;
       active_ = true;
+      if (op.client != kNone && last_mut_.size() < op.client) {
+        last_mut_.resize(op.client, 0);
+        held_bits_.resize((last_mut_.size() + 63) / 64, 0);
+      }
+      {  // room for an eighth of the snapshot's trie (at most 2M paths), once
+        const uint64_t want = std::min<uint64_t>(op.nodes_hint / 8, 1u << 21);
+        if (nodes_.capacity() < want) {
+          kids_.reserve(2 * want);
+          nodes_.reserve(want);
+          held_.reserve(want / 2);
+          tok_head_.reserve(want / 2);
+        }
+      }
       return;
     case Op::kVersion:
       return;

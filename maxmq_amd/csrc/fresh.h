@@ -32,10 +32,11 @@
 // snapshot subscriptions, names resolved — and queues them; it decides which
 // clients are held and dropped, so the overlay copies never read the store.
 // An applier thread applies the queue every kApplyNs (or at kBatch queued).
-// Calls never wait for it: the overlay is kept twice (left-right), calls read
-// the current copy, the applier writes the other one (after the calls still in
-// it have left), makes it current, and brings the first up to date in its next
-// round.  A call whose own thread made a mutation still queued waits for the
+// Calls never wait for it: the overlay is kept in kCopies copies
+// (left-right), calls read the current copy, the applier brings a copy no
+// call is in up to date from its log of operations and makes it current.
+// (A third copy, so that a caller preempted inside a copy never holds the
+// applier up, tripled the applier's work and lost: r06ad, r06ag.)  A call whose own thread made a mutation still queued waits for the
 // applier (read-your-writes); other threads' mutations reach calls within
 // about kApplyNs; every result reports the version it reflects.  (One
 // reader-writer-locked overlay updated at every mutation, with 64 callers
@@ -105,13 +106,17 @@ class FreshOverlay {
   // statistics: operations applied (per copy), applier rounds, calls
   // corrected, ns in their read sections (sum), clients held
   struct Stats {
-    uint64_t ops, rounds, corrected, read_ns, held;
+    uint64_t ops, rounds, corrected, read_ns, held, match_ns;
+    uint64_t max_age_ns, max_round_ns, max_wait_ns;  // oldest batch taken, longest round, longest wait for a free copy
   };
   Stats stats() const {
-    return Stats{ops_.load(std::memory_order_relaxed), rounds_.load(std::memory_order_relaxed),
-                 corrected_.load(std::memory_order_relaxed), read_ns_.load(std::memory_order_relaxed),
-                 held_n_.load(std::memory_order_relaxed)};
+    return Stats{ops_.load(std::memory_order_relaxed),         rounds_.load(std::memory_order_relaxed),
+                 corrected_.load(std::memory_order_relaxed),   read_ns_.load(std::memory_order_relaxed),
+                 held_n_.load(std::memory_order_relaxed),      match_ns_.load(std::memory_order_relaxed),
+                 max_age_ns_.load(std::memory_order_relaxed),  max_round_ns_.load(std::memory_order_relaxed),
+                 max_wait_ns_.load(std::memory_order_relaxed)};
   }
+  void count_match(uint64_t ns) const { match_ns_.fetch_add(ns, std::memory_order_relaxed); }
   void count_read(uint64_t ns) const {
     corrected_.fetch_add(1, std::memory_order_relaxed);
     read_ns_.fetch_add(ns, std::memory_order_relaxed);
@@ -131,7 +136,8 @@ class FreshOverlay {
     uint64_t version = 0;
     std::string filter;          // kPut / kDrop: the filter as called (path and group derived)
     SubInfo info{};              // kPut
-    uint64_t floor = 0;          // kInstall
+    uint64_t floor = 0;          // kInstall (and the snapshot's node count: the copies' tables sized from it)
+    uint64_t nodes_hint = 0;
     std::vector<Load> loads;     // kLoad
   };
   // one copy of the overlay (written by the applier only)
@@ -180,6 +186,7 @@ class FreshOverlay {
         }
       }
       void insert(uint64_t k, uint32_t v);
+      void reserve(uint64_t slots);  // (a rehash inside a round delays every call's view)
     };
     uint32_t token(std::string_view s, bool create);
     uint32_t find_token(std::string_view s) const;
@@ -223,30 +230,34 @@ class FreshOverlay {
   std::mutex qmu_;
   std::condition_variable qcv_, done_cv_;
   std::vector<Op> q_;
-  int64_t oldest_ns_ = 0;
+  std::atomic<int64_t> oldest_ns_{0};
+  std::mutex round_mu_;  // one round at a time (the applier, or a call helping)
   bool urgent_ = false, stop_ = false;
   std::atomic<uint64_t> applied_{0};    // the newest version the current copy holds
-  std::vector<Op> lag_;                 // (applier) applied to the current copy, not yet to the other
   void run();
   void round(std::vector<Op> &batch);
-  // the two copies
-  State s_[2];
+  // the copies, the operations since the least up-to-date one (applier)
+  static constexpr int kCopies = 2;
+  State s_[kCopies];
   std::atomic<int> cur_{0};
+  std::vector<Op> log_;       // operations log_base_ .. log_base_ + log_.size()
+  uint64_t log_base_ = 0;
+  uint64_t pos_[kCopies] = {};  // operations each copy holds (absolute)
   // calls inside each copy, counted in per-thread slots (64 callers on one
   // counter made its cache line the hot spot)
   static constexpr int kSlots = 16;
   struct alignas(64) Count {
     std::atomic<int> n{0};
   };
-  mutable Count readers_[2][kSlots];
+  mutable Count readers_[kCopies][kSlots];
   static int slot();
   bool drained(int copy) const {
     for (int k = 0; k < kSlots; k++)
       if (readers_[copy][k].n.load(std::memory_order_seq_cst) != 0) return false;
     return true;
   }
-  std::atomic<uint64_t> ops_{0}, rounds_{0};
-  mutable std::atomic<uint64_t> corrected_{0}, read_ns_{0};
+  std::atomic<uint64_t> ops_{0}, rounds_{0}, max_age_ns_{0}, max_round_ns_{0}, max_wait_ns_{0};
+  mutable std::atomic<uint64_t> corrected_{0}, read_ns_{0}, match_ns_{0};
   std::thread th_;
 
  public:

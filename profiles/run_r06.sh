@@ -36,6 +36,7 @@
 #   xcdab   : `fast` with / without the XCD-affine walk parts (MQM_WALK_XCD=1), on the batch as generated and sorted
 #   xcdpar  : parity + queued tests with the XCD-affine walk
 #   sortab  : `fast` with the walk in prefix order (default), in batch order (MQM_WALK_SORT=0), in prefix order again
+#   freshleg: the churn workload with one plain and one MQM_CFG_FRESH served leg (2 build threads, 20 s each)
 #   c2      : the C2 bench line (1M filters, 10M topics) with roofline and CPU baseline -> bench_c2.json
 #   c4fast  : the C4 shard bench without CPU baseline
 #   pipe    : `fast` with pipelined steps on 2 and 3 contexts -> bench_fast_pipe{2,3}.json
@@ -185,6 +186,8 @@ for step in "$@"; do
           N=${V%%:*}; E=${V#*:}
           env $E timeout -k 10 400 python3 -u bench.py $FAST > $OUT/bench_fast_$N.json 2> $OUT/bench_fast_$N.log || exit 1
         done ;;
+    freshleg) timeout -k 10 900 python3 -u bench.py --workload churn --steps 2 --warmup 1 --serve-churn-s 20 \
+             --churn-build-threads 2 > $OUT/bench_churn.json 2> $OUT/bench_churn.log ;;
     c2) timeout -k 10 600 python3 -u bench.py --config 2 --steps 10 --warmup 3 --host-topics 0 --latency-topics 0 \
              --steady-steps 0 --cpu-seconds 10 > $OUT/bench_c2.json 2> $OUT/bench_c2.log ;;
     c4fast) timeout -k 10 600 python3 -u bench.py --config 4 --shard 0/8 $FAST > $OUT/bench_c4_fast.json 2> $OUT/bench_c4_fast.log ;;
