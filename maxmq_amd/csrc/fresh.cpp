@@ -309,8 +309,8 @@ void FreshOverlay::State::Kids::reserve(uint64_t slots) {
   if (slots <= key.size()) return;
   uint64_t sz = key.size();
   while (sz < slots) sz *= 2;
-  std::vector<uint64_t> ok(sz, ~0ull);
-  std::vector<uint32_t> ov(sz, 0);
+  HVec<uint64_t> ok(sz, ~0ull);
+  HVec<uint32_t> ov(sz, 0);
   ok.swap(key);
   ov.swap(val);
   n = 0;
@@ -320,8 +320,8 @@ void FreshOverlay::State::Kids::reserve(uint64_t slots) {
 
 void FreshOverlay::State::Kids::insert(uint64_t k, uint32_t v) {
   if (2 * (n + 1) > key.size()) {  // load <= 0.5
-    std::vector<uint64_t> ok(key.size() * 2, ~0ull);
-    std::vector<uint32_t> ov(key.size() * 2, 0);
+    HVec<uint64_t> ok(key.size() * 2, ~0ull);
+    HVec<uint32_t> ov(key.size() * 2, 0);
     ok.swap(key);
     ov.swap(val);
     n = 0;

@@ -169,9 +169,13 @@ class FreshOverlay {
       uint32_t plus = kNone, hash = kNone;  // the '+' / '#' child (no table probe for them)
     };
     // (parent << 32 | token) -> child: open addressing, insert-only
+    // (the big arrays on 2-MB pages: a call's scan and checks are random reads
+    // into tens of MB, a TLB miss each on 4-KB pages)
+    template <class T>
+    using HVec = std::vector<T, HugeAlloc<T>>;
     struct Kids {
-      std::vector<uint64_t> key = std::vector<uint64_t>(1024, ~0ull);
-      std::vector<uint32_t> val = std::vector<uint32_t>(1024, 0);
+      HVec<uint64_t> key = HVec<uint64_t>(1024, ~0ull);
+      HVec<uint32_t> val = HVec<uint32_t>(1024, 0);
       uint64_t n = 0;
       static uint64_t mix(uint64_t k) {
         k ^= k >> 31;
@@ -204,11 +208,11 @@ class FreshOverlay {
     bool active_ = false;
     uint64_t floor_ = 0;    // results on snapshots older than this are retried
     uint64_t version_ = 0;  // the store version the overlay reflects
-    std::vector<uint64_t> last_mut_;  // by client: the version after its last mutation (0: not held)
-    std::vector<uint64_t> held_bits_; // by client: held (last_mut_ != 0)
+    HVec<uint64_t> last_mut_;   // by client: the version after its last mutation (0: not held)
+    HVec<uint64_t> held_bits_;  // by client: held (last_mut_ != 0)
     std::unordered_map<uint32_t, std::vector<uint32_t>> held_;  // client -> nodes holding its entries
     // the trie: nodes, (parent, token) -> child, tokens by hash (chained)
-    std::vector<Node> nodes_{Node()};
+    HVec<Node> nodes_{Node()};
     Kids kids_;
     std::vector<std::string> tok_str_;
     std::vector<uint32_t> tok_next_;
