@@ -18,17 +18,17 @@ int64_t now_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
       .count();
 }
-// the calling thread's newest queued mutation per overlay (a few overlays:
+// the calling thread's newest queued operation per overlay (a few overlays:
 // the thread's own writes its next call on that index must see)
 struct LastWrite {
   const void *owner = nullptr;
-  uint64_t version = 0;
+  uint64_t seq = 0;
 };
 thread_local LastWrite tl_writes[4];
 void note_write(const void *o, uint64_t v) {
   for (auto &w : tl_writes)
     if (w.owner == o) {
-      w.version = v;
+      w.seq = v;
       return;
     }
   for (int i = 3; i > 0; i--) tl_writes[i] = tl_writes[i - 1];
@@ -36,7 +36,7 @@ void note_write(const void *o, uint64_t v) {
 }
 uint64_t last_write(const void *o) {
   for (const auto &w : tl_writes)
-    if (w.owner == o) return w.version;
+    if (w.owner == o) return w.seq;
   return 0;
 }
 }  // namespace
@@ -123,6 +123,7 @@ void FreshOverlay::round(std::vector<Op> &batch) {
   pos_[t] = end;
   cur_.store(t, std::memory_order_seq_cst);
   applied_.store(log_.back().version, std::memory_order_release);
+  applied_seq_.store(log_.back().seq, std::memory_order_release);
   rounds_.fetch_add(1, std::memory_order_relaxed);
   uint64_t lo = end;
   for (int k = 0; k < kCopies; k++) lo = std::min(lo, pos_[k]);
@@ -133,21 +134,27 @@ void FreshOverlay::round(std::vector<Op> &batch) {
   batch.clear();
 }
 
-void FreshOverlay::await_own_writes() {
-  const uint64_t w = last_write(this);
-  if (w == 0 || applied_.load(std::memory_order_acquire) >= w) return;
+bool FreshOverlay::await_seq(uint64_t w, int64_t ms) {
+  if (w == 0 || applied_seq_.load(std::memory_order_acquire) >= w) return true;
   std::unique_lock<std::mutex> lk(qmu_);
   urgent_ = true;
   qcv_.notify_one();
-  // (bounded: a result that misses the write still reports its version)
-  done_cv_.wait_for(lk, std::chrono::milliseconds(200),
-                    [&] { return stop_ || applied_.load(std::memory_order_acquire) >= w; });
+  return done_cv_.wait_for(lk, std::chrono::milliseconds(ms),
+                           [&] { return stop_ || applied_seq_.load(std::memory_order_acquire) >= w; });
 }
+
+// (bounded: a result that misses the write still reports its version)
+void FreshOverlay::await_own_writes() { await_seq(last_write(this), 200); }
+
+bool FreshOverlay::await_all(int64_t ms) { return await_seq(seq_.load(std::memory_order_acquire), ms); }
 
 // ---- the mutating side (index mutex held) ----------------------------------
 
 void FreshOverlay::enqueue(Op &&op) {
-  note_write(this, op.version);
+  // (by operation, not version: a publish or a policy change queues one at
+  // the version of the mutation before it, and the thread's next call sees it)
+  op.seq = seq_.fetch_add(1, std::memory_order_relaxed) + 1;
+  note_write(this, op.seq);
   bool wake = false;
   {
     std::lock_guard<std::mutex> g(qmu_);
@@ -214,6 +221,7 @@ void FreshOverlay::on_subscribe(const Store &st, std::string_view filter, const 
   Op op;
   op.version = queued_version_ = st.version();
   if (!mactive_) {
+    mdirty_[rec.client] = op.version;
     op.kind = Op::kVersion;
     return enqueue(std::move(op));
   }
@@ -233,6 +241,7 @@ void FreshOverlay::on_unsubscribe(const Store &st, std::string_view filter) {
   Op op;
   op.version = queued_version_ = st.version();
   if (!mactive_ || fp.client == kNone) {  // (a client never seen: nothing of it changes)
+    if (!mactive_ && fp.client != kNone) mdirty_[fp.client] = op.version;
     op.kind = Op::kVersion;
     return enqueue(std::move(op));
   }
@@ -259,13 +268,24 @@ void FreshOverlay::on_install(std::shared_ptr<const HostSnapshot> hs, const Stor
   op.version = queued_version_ = st.version();
   if (!hs || (hs->client_off.empty() && !hs->sub_info.empty()) ||
       (hs->client_shoff.empty() && !hs->shared_info.empty())) {  // (no client index: nothing to start from)
+    // (the held clients are the ones mutated since the floor: remembered, so
+    // that a later snapshot can start the overlay again)
+    for (const auto &kv : mirror_) mdirty_[kv.first] = std::max(mdirty_[kv.first], kv.second);
     mactive_ = false;
+    mbase_.reset();
     mirror_.clear();
     mprune_.clear();
     held_n_.store(0, std::memory_order_relaxed);
     op.kind = Op::kReset;
     return enqueue(std::move(op));
   }
+  // (not holding clients yet, and mutations from before mwait_ were not
+  // followed: only a snapshot that has them can start the overlay)
+  if (!mactive_ && hs->version < mwait_) {
+    op.kind = Op::kVersion;
+    return enqueue(std::move(op));
+  }
+  const bool first = !mactive_;
   // results on the snapshot published before this one are still corrected;
   // the clients only older results would need are dropped
   mfloor_ = mactive_ && mbase_ ? mbase_->version : hs->version;
@@ -283,6 +303,49 @@ void FreshOverlay::on_install(std::shared_ptr<const HostSnapshot> hs, const Stor
   op.kind = Op::kInstall;
   op.floor = mfloor_;
   enqueue(std::move(op));
+  if (first) load_dirty(st);
+}
+
+// The overlay starts (first install, or on again) from a snapshot that may be
+// older than the store: the clients mutated since it was built are held from
+// the start, with their subscriptions as the store has them now — one pass
+// over the store's nodes under the index mutex, at a start only (a first
+// publish under churn, mqm_fresh_policy on).  Every other client's first
+// touch loads from the snapshot, which is then its state.
+void FreshOverlay::load_dirty(const Store &st) {
+  const uint64_t base = mbase_->version, now = st.version();
+  std::vector<Op> ops;
+  std::vector<uint32_t> at(st.clients().size(), kNone);  // client -> its op
+  for (const auto &kv : mdirty_)
+    if (kv.second > base && kv.first < at.size() && !mirror_.count(kv.first)) {
+      at[kv.first] = (uint32_t)ops.size();
+      Op op;
+      op.kind = Op::kLoad;
+      op.client = kv.first;
+      op.version = now;       // (the overlay's version only moves forward)
+      op.last = kv.second;    // the client's last mutation
+      ops.push_back(std::move(op));
+    }
+  mdirty_.clear();
+  if (ops.empty()) return;
+  for (const HNode &n : st.nodes()) {
+    if (!n.live) continue;
+    for (const SubRec &r : n.subs)
+      if (r.client < at.size() && at[r.client] != kNone)
+        ops[at[r.client]].loads.push_back(Load{std::string(st.filters().name(r.filter)), 0,
+                                               SubInfo{r.filter, r.client, r.ident, r.qos, r.no_local, r.rap, r.rh}});
+    for (const SharedRec &x : n.shared) {
+      const SubRec &r = x.sub;
+      if (r.client < at.size() && at[r.client] != kNone)
+        ops[at[r.client]].loads.push_back(Load{std::string(st.filters().name(r.filter)), 1,
+                                               SubInfo{r.filter, r.client, r.ident, r.qos, r.no_local, r.rap, r.rh}});
+    }
+  }
+  for (Op &op : ops) {
+    mirror_.emplace(op.client, op.last);
+    held_n_.fetch_add(1, std::memory_order_relaxed);
+    enqueue(std::move(op));
+  }
 }
 
 void FreshOverlay::set_enabled(bool on, std::shared_ptr<const HostSnapshot> published, const Store &st) {
@@ -295,11 +358,15 @@ void FreshOverlay::set_enabled(bool on, std::shared_ptr<const HostSnapshot> publ
     enabled_ = mactive_ = false;
     mirror_.clear();
     mprune_.clear();
+    mdirty_.clear();
     mbase_.reset();
     held_n_.store(0, std::memory_order_relaxed);
     return;
   }
   enabled_ = true;
+  // (the mutations while off were not followed: a snapshot that has them all
+  // starts the overlay — the published one when nothing changed since)
+  mwait_ = st.version();
   on_install(std::move(published), st);
 }
 
@@ -454,7 +521,7 @@ void FreshOverlay::State::apply(const Op &op) {
     case Op::kLoad:
       held_[op.client];  // (held from now on, even with no subscription)
       for (const Load &l : op.loads) put_sub(op.client, l.filter, l.shared, l.info);
-      stamp(op.client, op.version);
+      stamp(op.client, op.last ? op.last : op.version);
       return;
     case Op::kPut:
       put_sub(op.client, op.filter, op.shared, op.info);

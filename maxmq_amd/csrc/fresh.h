@@ -21,7 +21,10 @@
 // Clients nobody touched since Vs keep their snapshot rows, which are current.
 // The first time a mutation touches a client, its subscriptions are read from
 // the published snapshot (HostSnapshot::client_off, built for fresh indexes)
-// and the mutation is applied on top; later mutations update the set.  At each
+// and the mutation is applied on top; later mutations update the set.  The
+// overlay starts at the first publish (switched on again: at the first publish
+// that has every mutation made while it was off); the clients mutated since
+// that snapshot was built are read from the store then (load_dirty).  At each
 // publish the clients whose last mutation is no newer than the previous
 // snapshot are dropped, a few at each mutation: a result on the published or
 // the previous snapshot still finds every client it needs; one on an older
@@ -85,6 +88,8 @@ class FreshOverlay {
   // ---- calls ----
   // a mutation of the calling thread is still queued: wait until it is applied
   void await_own_writes();
+  // every operation queued so far applied (false: not within ms)
+  bool await_all(int64_t ms);
 
   struct Gathered {
     uint32_t client;
@@ -139,6 +144,8 @@ class FreshOverlay {
     uint64_t floor = 0;          // kInstall (and the snapshot's node count: the copies' tables sized from it)
     uint64_t nodes_hint = 0;
     std::vector<Load> loads;     // kLoad
+    uint64_t last = 0;           // kLoad at a start: the client's last mutation (else op.version)
+    uint64_t seq = 0;            // queue order (await_own_writes)
   };
   // one copy of the overlay (written by the applier only)
   class State {
@@ -224,11 +231,16 @@ class FreshOverlay {
   void enqueue(Op &&op);
   void emit_prunes(size_t n);
   void hold(const Store &st, uint32_t c, uint64_t v);  // a Load op at a client's first touch
+  void load_dirty(const Store &st);                    // at a start: the clients mutated since its snapshot
   bool enabled_ = true, mactive_ = false;
   std::shared_ptr<const HostSnapshot> mbase_;
   uint64_t mfloor_ = 0, queued_version_ = 0;
   std::unordered_map<uint32_t, uint64_t> mirror_;  // held clients -> their last mutation's version
   std::vector<uint32_t> mprune_;                   // candidates to drop (last mutation <= floor at a publish)
+  // not holding clients yet (no snapshot, or on again): the clients mutated
+  // meanwhile, and the version a snapshot must have to start from (0: any)
+  std::unordered_map<uint32_t, uint64_t> mdirty_;
+  uint64_t mwait_ = 0;
   std::atomic<uint64_t> held_n_{0};
   // the queue (qmu_) and the applier
   std::mutex qmu_;
@@ -238,8 +250,10 @@ class FreshOverlay {
   std::mutex round_mu_;  // one round at a time (the applier, or a call helping)
   bool urgent_ = false, stop_ = false;
   std::atomic<uint64_t> applied_{0};    // the newest version the current copy holds
+  std::atomic<uint64_t> seq_{0}, applied_seq_{0};  // operations queued / in the current copy
   void run();
   void round(std::vector<Op> &batch);
+  bool await_seq(uint64_t w, int64_t ms);
   // the copies, the operations since the least up-to-date one (applier)
   static constexpr int kCopies = 2;
   State s_[kCopies];

@@ -730,7 +730,7 @@ static void subscribers_one(const oref *x, const char *topic, uint32_t tlen, scr
   s->st.topics++;
   s->st.topic_bytes += tlen;
   scan_subscribers(x, topic, tlen, 0, x->root, s);
-  qsort(s->touched, s->ntouched, sizeof(uint32_t), cmp_u32);
+  if (s->ntouched > 1) qsort(s->touched, s->ntouched, sizeof(uint32_t), cmp_u32);
   if (s->nsh > 1) {
     qsort(s->sh, s->nsh, sizeof(oref_shared), cmp_shared);
     uint32_t w = 1;

@@ -157,3 +157,23 @@ def test_walk_tokenizer_masks_match_a_byte_scan():
         subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "tests", "harness")])
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("build", ["asan", "tsan"])
+def test_fresh_overlay_against_the_oracle_under_sanitizers(build):
+    """The fresh overlay (maxmq_amd/csrc/fresh.h, MQM_CFG_FRESH) driven as
+    capi.cpp drives it — mutation hooks, snapshots published late, the policy
+    switched off and on, a first snapshot older than the store — with every
+    call's status, touched clients and corrected rows / shared candidates
+    checked against the C oracle (topics.go:493-538, packets.go:250-270); then
+    4 reader threads against the mutating thread and the applier, and the
+    quiescent overlay checked again (tests/harness/fresh_test.cpp, CPU, ASan +
+    UBSan and TSan builds)."""
+    import subprocess
+
+    target = f"_build/fresh_test_{build}"
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "tests", "harness"), target])
+    r = subprocess.run([os.path.join(ROOT, "tests", "harness", target), "3000"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and r.stdout.strip().endswith("fresh_test ok"), r.stdout + r.stderr[-4000:]
+    assert "WARNING" not in r.stderr and "ERROR" not in r.stderr, r.stderr[-4000:]
