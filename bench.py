@@ -1190,7 +1190,8 @@ def serve_churn(idx, w, args):
         capi.check("mqm_build_threads", L.mqm_build_threads(max(bt, 0)))
         if fresh_on:
             idx.fresh_policy(fresh)
-        idx.commit_poll(wait=True)  # (the previous leg's mutations built and published)
+        idx.commit_async()  # (the previous leg's mutations built and published: a fresh
+        idx.commit_poll(wait=True)  # leg's overlay starts from that snapshot)
         idx.commit_policy(0, 50 if bt >= 0 else 0)
         f0 = idx.fresh_stats() if fresh else None
         name = ("fresh_" if fresh else "") + (f"build_threads_{bt}" if bt >= 0 else "no_rebuild")

@@ -90,7 +90,9 @@ extern "C" {
  * (mqm_match_batch*, mqm_match_device) keep the snapshot's view.  Costs: each
  * publish builds a by-client index of the snapshot; each mutation updates the
  * overlay under the index mutex; a call on a stale snapshot adds a host scan
- * of the touched clients' subscriptions. */
+ * of the touched clients' subscriptions.  Corrections start with the first
+ * publish; the clients mutated after that snapshot was built are then read
+ * from the store once (one pass over its nodes, under the index mutex). */
 #define MQM_CFG_FRESH 32u
 /* device value for a host-only index: the store and its mutation API work,
  * mqm_commit / mqm_match_* return MQM_ENODEV (there is no CPU match path). */
@@ -311,7 +313,10 @@ int mqm_batching_policy(mqm_index *h, uint32_t max_batch, uint32_t linger_us);
 int mqm_serve_policy(mqm_index *h, uint32_t grid, uint32_t idle_us);
 /* MQM_CFG_FRESH indexes: correct_calls = 0 makes mqm_subscribers return the
  * snapshot's view again and drops the overlay (mutations cost nothing extra;
- * A/B and measurement), 1 starts it again from the published snapshot.
+ * A/B and measurement), 1 starts it again: at once when the published
+ * snapshot holds every mutation, else at the first publish that does
+ * (mqm_commit_async then mqm_commit_poll(wait) gives one); until then calls
+ * return the snapshot's view, reporting its version.
  * Statistics (out[9]): clients held, overlay operations applied, applier
  * rounds, calls corrected, nanoseconds spent in the corrections' read
  * sections, the part of them in the overlay's scan, then the largest age of a
