@@ -15,8 +15,8 @@
 //   * touched(c, vs) == "c's last mutation is newer than vs" for every client;
 //   * the corrected rows: for every touched client, the oracle's current
 //     delivery (client, QoS max, NoLocal or, first-merged filter, Identifier,
-//     RetainAsPublished, RetainHandling: topics.go:493-538, packets.go:250-270)
-//     and its shared candidates; nothing for any other client.
+//     RetainAsPublished, RetainHandling: topics.go:493-538, packets.go:250-270),
+//     its Identifiers and its shared candidates; nothing for any other client.
 // Phase 1 checks every call single-threaded.  Phase 2 runs 4 reader threads
 // (Reader, status, match, touched) against the mutating thread and the
 // applier, then checks the quiescent overlay as phase 1 does — the left-right
@@ -287,6 +287,39 @@ struct World {
       for (const Cand &c : keep) fprintf(stderr, "  want %s %s %d\n", std::get<0>(c).c_str(), std::get<1>(c).c_str(), std::get<2>(c));
       for (const Cand &c : got_c) fprintf(stderr, "  got  %s %s %d\n", std::get<0>(c).c_str(), std::get<1>(c).c_str(), std::get<2>(c));
     }
+    // Subscription.Identifiers of the touched clients' deliveries
+    // (packets.go:250-258): {first.Filter: first.Identifier} and every other
+    // gathered subscription with an Identifier > 0 — capi.cpp freshen lists
+    // the gathered entries with one, the first comes with its row
+    using Ident = std::tuple<std::string, std::string, int>;  // client, filter, ident
+    std::vector<Ident> want_i, got_i;
+    {
+      uint64_t offs[2] = {0, t.size()};
+      uint32_t ic = 0;
+      oref_match_ident_counts(orc, t.data(), offs, 1, 1, &ic);
+      std::vector<oref_ident> iv(ic + 1);
+      uint64_t ioff[2] = {0, ic};
+      oref_match_ident_fill(orc, t.data(), offs, 1, 1, ioff, iv.data());
+      char a[512], b[512];
+      for (uint32_t i = 0; i < ic; i++) {
+        const std::string cn(a, oref_client_name(orc, iv[i].client, a, sizeof a));
+        const uint32_t id = st.clients().find(cn);
+        if (id == 0xFFFFFFFFu || id >= touched.size() || !touched[id]) continue;
+        want_i.push_back(Ident{cn, std::string(b, oref_filter_name(orc, iv[i].filter, b, sizeof b)), iv[i].ident});
+      }
+    }
+    auto ident_of = [&](const FreshOverlay::Gathered &g) {
+      return Ident{std::string(st.clients().name(g.client)), std::string(st.filters().name(g.info.filter)), g.info.ident};
+    };
+    for (const auto &r : m.rows)
+      if (r.first < m.subs.size()) got_i.push_back(ident_of(m.subs[r.first]));
+    for (const auto &g : m.subs)
+      if (g.info.ident > 0) got_i.push_back(ident_of(g));
+    std::sort(want_i.begin(), want_i.end());
+    std::sort(got_i.begin(), got_i.end());
+    got_i.erase(std::unique(got_i.begin(), got_i.end()), got_i.end());
+    CHECK(want_i == got_i, "topic '%s' vs %llu: identifiers %zu, want %zu", t.c_str(), (unsigned long long)vs,
+          got_i.size(), want_i.size());
   }
   void check_round() {
     for (int k = 0; k < 3; k++) {
