@@ -608,10 +608,21 @@ struct Task {            // copy list[lo, lo + len) to out[dst ..)
 // adjacent in its segment too; round 5 copied each one on its own lane, 8-B
 // accesses strided across the wave: k_emit_place 3.5 ms of 22.1, r05aa),
 // large ones cut into kTaskRefs copy tasks
+// an output ref: non-temporal (MQM_REV_NT, default on) — the call writes its
+// refs once (2,196 per filter at C5: 17.6 GB) and reads none of them back
+template <bool kNT>
+__device__ __forceinline__ void put_ref(uint64_t *p, uint64_t v) {
+  if constexpr (kNT)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
+
 struct EmitLds {
   uint32_t pre[65];           // exclusive prefix of the small emissions' counts
   uint64_t pos[64], src[64];  // output position, source index | list << 63
 };
+template <bool kNT>
 __global__ __launch_bounds__(kThreads) void k_emit_place(const Emit *__restrict__ e, uint64_t cap, RevCtr *ctr,
                                                         const uint64_t *__restrict__ foff,
                                                         unsigned long long *__restrict__ fcur,
@@ -658,7 +669,7 @@ __global__ __launch_bounds__(kThreads) void k_emit_place(const Emit *__restrict_
           for (uint32_t step = 32; step > 0; step >>= 1) j = L.pre[j + step] <= q ? j + step : j;
           const uint32_t o = q - L.pre[j];
           const uint64_t sw = L.src[j];
-          out[L.pos[j] + o] = ((sw >> 63) ? rch_refs : refs)[(sw & ~(1ull << 63)) + o];
+          put_ref<kNT>(out + L.pos[j] + o, ((sw >> 63) ? rch_refs : refs)[(sw & ~(1ull << 63)) + o]);
         }
       }
       __builtin_amdgcn_wave_barrier();
@@ -677,6 +688,7 @@ __global__ __launch_bounds__(kThreads) void k_emit_place(const Emit *__restrict_
 }
 
 // a wavefront per copy task, grid-stride over the tasks k_emit_place queued
+template <bool kNT>
 __global__ __launch_bounds__(kThreads) void k_task_copy(const Task *__restrict__ tasks, uint64_t cap,
                                                        const RevCtr *ctr, const uint64_t *__restrict__ refs,
                                                        const uint64_t *__restrict__ rch_refs,
@@ -693,9 +705,12 @@ __global__ __launch_bounds__(kThreads) void k_task_copy(const Task *__restrict__
     uint32_t j = lane;
     for (; j + 192 < len; j += 256) {  // 4 loads in flight per lane
       const uint64_t a = src[j], b = src[j + 64], c = src[j + 128], d = src[j + 192];
-      dst[j] = a, dst[j + 64] = b, dst[j + 128] = c, dst[j + 192] = d;
+      put_ref<kNT>(dst + j, a);
+      put_ref<kNT>(dst + j + 64, b);
+      put_ref<kNT>(dst + j + 128, c);
+      put_ref<kNT>(dst + j + 192, d);
     }
-    for (; j < len; j += 64) dst[j] = src[j];
+    for (; j < len; j += 64) put_ref<kNT>(dst + j, src[j]);
   }
 }
 
@@ -870,12 +885,13 @@ int messages_device(const DeviceSnapshot &s, const DeviceRetained *r, Workspace 
     if (scan_u64(ws, (const uint64_t *)fcount, foff, n, st)) return -3;
     auto *refs_out = (uint64_t *)ws.ptr(W::kROut);
     auto *tasks = (Task *)ws.ptr(W::kRChunks);
-    hipLaunchKernelGGL(k_emit_place, dim3(grid), dim3(kThreads), 0, st, a.emit, emit_cap, ctr, foff,
-                       (unsigned long long *)ws.ptr(W::kRFCur), r->refs, r->rch_refs, refs_out, out_cap, tasks,
-                       task_cap);
+    static const bool nt_refs = !getenv("MQM_REV_NT") || atoi(getenv("MQM_REV_NT")) != 0;
+    hipLaunchKernelGGL(nt_refs ? k_emit_place<true> : k_emit_place<false>, dim3(grid), dim3(kThreads), 0, st, a.emit,
+                       emit_cap, ctr, foff, (unsigned long long *)ws.ptr(W::kRFCur), r->refs, r->rch_refs, refs_out,
+                       out_cap, tasks, task_cap);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_task_copy, dim3(grid), dim3(kThreads), 0, st, tasks, task_cap, ctr, r->refs, r->rch_refs,
-                       refs_out);
+    hipLaunchKernelGGL(nt_refs ? k_task_copy<true> : k_task_copy<false>, dim3(grid), dim3(kThreads), 0, st, tasks,
+                       task_cap, ctr, r->refs, r->rch_refs, refs_out);
     HIP_TRY(hipGetLastError());
     // the one read-back: sizes and overflow flags
     RevCtr *hc = reinterpret_cast<RevCtr *>(hp);

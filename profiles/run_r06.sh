@@ -227,6 +227,11 @@ for step in "$@"; do
              --latency-topics 0 --steady-steps 0 > $OUT/bench_c4_host.json 2> $OUT/bench_c4_host.log ;;
     rev) timeout -k 10 900 python3 -u bench.py --workload reverse --steps 5 --warmup 1 --cpu-seconds 10 \
              > $OUT/bench_reverse.json 2> $OUT/bench_reverse.log ;;
+    revnt) for V in nt:X=0 plain:MQM_REV_NT=0; do
+          N=${V%%:*}; E=${V#*:}
+          env $E timeout -k 10 600 python3 -u bench.py --workload reverse --steps 5 --warmup 1 --no-cpu-baseline \
+            > $OUT/bench_reverse_$N.json 2> $OUT/bench_reverse_$N.log || exit 1
+        done ;;
     revpmc) (cd /tmp && export TMPDIR=/tmp && for C in FETCH_SIZE WRITE_SIZE; do
              timeout -s KILL 500 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/revpmc/pmc_$C -o pmc \
              -- python3 $ROOT/bench.py --workload reverse --steps 1 --warmup 1 --no-cpu-baseline \
