@@ -253,13 +253,16 @@ class TopicsIndex:
 
     def fresh_policy(self, correct_calls: bool):
         """MQM_CFG_FRESH: subscribers() corrected for every mutation (True,
-        the default) or the published snapshot's view (False)"""
+        the default) or the published snapshot's view (False).  Switched on
+        again, the corrections start with a published snapshot that holds
+        every mutation made while off (at once when the published one does;
+        commit_async() then commit_poll(wait=True) publishes one)."""
         check("mqm_fresh_policy", lib().mqm_fresh_policy(self._h, int(bool(correct_calls))))
 
     def fresh_stats(self) -> dict:
         """the fresh overlay: clients held (touched since the previous
-        snapshot), mutations applied per copy, flushes, calls corrected and
-        the time in their read sections"""
+        snapshot), operations applied per copy, applier rounds, calls
+        corrected and the time in their read sections"""
         v = (C.c_uint64 * 9)()
         check("mqm_fresh_stats", lib().mqm_fresh_stats(self._h, C.byref(v)))
         return {"held_clients": v[0], "ops_applied": v[1], "rounds": v[2], "calls_corrected": v[3],
