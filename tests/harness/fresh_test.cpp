@@ -6,7 +6,8 @@
 //
 // The overlay is driven exactly as capi.cpp drives it (mutation hooks under
 // one mutating thread, snapshots published late as the background builder
-// does, mqm_fresh_policy off and on), with snapshots built here from the
+// does, mqm_fresh_policy off and on, now and then a snapshot without the
+// by-client index), with snapshots built here from the
 // store's own lists (HostSnapshot's sub_info / shared_info and the by-client
 // index; no device, no flatten).  Checked, for every call:
 //   * status: -1 below the floor (the snapshot before the published one), 0
@@ -151,7 +152,12 @@ struct World {
   // the background builder: a snapshot taken now, published a few mutations
   // later (capi.cpp install -> FreshOverlay::on_install)
   void publish_step() {
-    if (!pending && pick(12) == 0) pending = snapshot_of(st);
+    if (!pending && pick(12) == 0) {
+      pending = snapshot_of(st);
+      // (now and then one without the by-client index: the overlay stops, and
+      // starts again at the next snapshot that has one)
+      if (pick(15) == 0 && !pending->sub_info.empty()) pending->client_off.clear();
+    }
     if (pending && pick(6) == 0) {
       previous = published;
       published = std::move(pending);
@@ -164,6 +170,11 @@ struct World {
   // what on_install(hs) must do: start the overlay (floor = hs), move the
   // floor to the snapshot it took before, or nothing (hs older than wait)
   void offer(const std::shared_ptr<HostSnapshot> &hs) {
+    if (hs->client_off.empty() && !hs->sub_info.empty()) {
+      active = false;
+      base = nullptr;
+      return;
+    }
     if (!active) {
       if (hs->version < wait) return;
       active = true;
